@@ -1,0 +1,141 @@
+// pybind11 bindings of the kmls native runtime (module `_native`).
+//
+// All heavy calls release the GIL.  GPU entry points take raw device pointers / stream
+// handles (ints) so Python can hand in torch-allocated HBM buffers and torch's current HIP
+// stream; the native code never links libtorch.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "kmls/gpu.hpp"
+#include "kmls/host.hpp"
+
+namespace py = pybind11;
+using namespace kmls;
+
+template <typename T>
+static py::array_t<T> to_array(std::vector<T>&& v) {
+  auto* heap = new std::vector<T>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete reinterpret_cast<std::vector<T>*>(p); });
+  return py::array_t<T>({(py::ssize_t)heap->size()}, {(py::ssize_t)sizeof(T)}, heap->data(), owner);
+}
+
+static py::dict trie_to_dict(ItemsetTrie&& t) {
+  py::dict d;
+  d["parent"] = to_array(std::move(t.parent));
+  d["item"] = to_array(std::move(t.item));
+  d["count"] = to_array(std::move(t.count));
+  d["depth"] = to_array(std::move(t.depth));
+  return d;
+}
+
+using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+using F64 = py::array_t<double, py::array::c_style | py::array::forcecast>;
+using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "kmls native runtime: CSV ingest, CPU/HIP FP-Growth miners, rule-index matchers";
+
+  // ---------------- ingest ----------------
+  m.def("read_csv_encoded", [](const std::string& path, const std::vector<std::string>& cols) {
+    EncodedTable t;
+    {
+      py::gil_scoped_release nogil;
+      t = read_csv_encoded(path, cols);
+    }
+    py::dict out;
+    out["n_rows"] = t.n_rows;
+    out["header"] = t.header;
+    py::dict cd;
+    for (size_t w = 0; w < t.columns.size(); ++w) {
+      py::list u;
+      for (auto& s : t.uniques[w]) u.append(py::str(s));
+      cd[py::str(t.columns[w])] = py::make_tuple(to_array(std::move(t.codes[w])), u);
+    }
+    out["columns"] = cd;
+    return out;
+  }, py::arg("path"), py::arg("columns"));
+
+  m.def("group_to_csr", [](I32 keys, I32 vals, int32_t n_keys, bool dedup, bool sort_rows) {
+    KMLS_CHECK(keys.size() == vals.size(), "keys/vals size mismatch");
+    CSR g;
+    {
+      py::gil_scoped_release nogil;
+      g = group_to_csr(keys.data(), vals.data(), keys.size(), n_keys, dedup, sort_rows);
+    }
+    return py::make_tuple(to_array(std::move(g.ptr)), to_array(std::move(g.idx)));
+  }, py::arg("keys"), py::arg("vals"), py::arg("n_keys"), py::arg("dedup") = true,
+     py::arg("sort_rows") = true);
+
+  // ---------------- thresholds ----------------
+  m.def("level1_threshold", &level1_threshold);
+  m.def("level2_threshold", &level2_threshold);
+
+  // ---------------- CPU miner ----------------
+  m.def("mine_cpu", [](I64 tx_ptr, I32 items, int64_t n_items, double min_support, int max_len,
+                       int threads, bool pairs_only) {
+    KMLS_CHECK(tx_ptr.size() >= 1, "tx_ptr must have T+1 entries");
+    MineConfig cfg;
+    cfg.min_support = min_support; cfg.max_len = max_len; cfg.threads = threads;
+    cfg.pairs_only = pairs_only;
+    MineStats st;
+    ItemsetTrie t;
+    {
+      py::gil_scoped_release nogil;
+      t = mine_cpu(tx_ptr.data(), items.data(), tx_ptr.size() - 1, n_items, cfg, &st);
+    }
+    py::dict d = trie_to_dict(std::move(t));
+    py::dict s;
+    s["n_frequent_items"] = st.n_frequent_items; s["n_itemsets"] = st.n_itemsets;
+    s["n_candidates"] = st.n_candidates; s["max_depth"] = st.max_depth; s["seconds"] = st.seconds;
+    d["stats"] = s;
+    return d;
+  }, py::arg("tx_ptr"), py::arg("items"), py::arg("n_items"), py::arg("min_support"),
+     py::arg("max_len") = 0, py::arg("threads") = 0, py::arg("pairs_only") = false);
+
+  // ---------------- CPU matcher ----------------
+  py::class_<RuleIndex, std::shared_ptr<RuleIndex>>(m, "RuleIndex")
+      .def(py::init([](int64_t n_items, I64 row_ptr, I32 cons, F64 score, U8 is_key) {
+        return std::make_shared<RuleIndex>(
+            n_items, std::vector<int64_t>(row_ptr.data(), row_ptr.data() + row_ptr.size()),
+            std::vector<int32_t>(cons.data(), cons.data() + cons.size()),
+            std::vector<double>(score.data(), score.data() + score.size()),
+            std::vector<uint8_t>(is_key.data(), is_key.data() + is_key.size()));
+      }))
+      .def_property_readonly("n_items", &RuleIndex::n_items)
+      .def_property_readonly("nnz", &RuleIndex::nnz)
+      .def("query", [](const RuleIndex& ix, I32 seeds, int k) -> py::object {
+        std::vector<int32_t> ids((size_t)std::max(k, 0));
+        int n;
+        {
+          py::gil_scoped_release nogil;
+          n = ix.query(seeds.data(), (int)seeds.size(), k, ids.data(), nullptr);
+        }
+        if (n < 0) return py::none();
+        ids.resize((size_t)n);
+        return to_array(std::move(ids));
+      })
+      .def("query_batch", [](const RuleIndex& ix, I64 q_ptr, I32 seeds, int k) {
+        // returns (ids int32[B,k], n int32[B]) ; n = -1 means "no seed known"
+        const int64_t B = q_ptr.size() - 1;
+        py::array_t<int32_t> ids({(py::ssize_t)B, (py::ssize_t)k});
+        py::array_t<int32_t> ns({(py::ssize_t)B});
+        int32_t* po = ids.mutable_data();
+        int32_t* pn = ns.mutable_data();
+        const int64_t* qp = q_ptr.data();
+        const int32_t* sd = seeds.data();
+        {
+          py::gil_scoped_release nogil;
+          std::fill(po, po + B * k, -1);
+          for (int64_t b = 0; b < B; ++b)
+            pn[b] = ix.query(sd + qp[b], (int)(qp[b + 1] - qp[b]), k, po + b * k, nullptr);
+        }
+        return py::make_tuple(ids, ns);
+      });
+
+  // ---------------- HIP runtime ----------------
+  register_gpu_bindings(m);
+}

@@ -1,0 +1,140 @@
+// pybind11 bindings of the HIP runtime objects (GpuMiner, GpuRuleIndex).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "kmls/gpu.hpp"
+
+namespace py = pybind11;
+
+namespace kmls {
+
+namespace {
+template <typename T>
+py::array_t<T> to_array(std::vector<T>&& v) {
+  auto* heap = new std::vector<T>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete reinterpret_cast<std::vector<T>*>(p); });
+  return py::array_t<T>({(py::ssize_t)heap->size()}, {(py::ssize_t)sizeof(T)}, heap->data(), owner);
+}
+
+py::dict result_to_dict(gpu::GpuMineResult&& r) {
+  py::dict d;
+  d["parent"] = to_array(std::move(r.trie.parent));
+  d["item"] = to_array(std::move(r.trie.item));
+  d["count"] = to_array(std::move(r.trie.count));
+  d["depth"] = to_array(std::move(r.trie.depth));
+  py::dict s;
+  s["n_frequent_items"] = r.stats.n_frequent_items;
+  s["n_itemsets"] = r.stats.n_itemsets;
+  s["n_candidates"] = r.stats.n_candidates;
+  s["max_depth"] = r.stats.max_depth;
+  s["seconds"] = r.stats.seconds;
+  s["arena_high_water"] = r.arena_high_water;
+  py::dict ph;
+  for (auto& p : r.phases) ph[py::str(p.name)] = p.ms;
+  s["phases_ms"] = ph;
+  d["stats"] = s;
+  return d;
+}
+
+MineConfig make_cfg(double ms, int max_len, bool pairs_only, bool gram, bool mfma) {
+  MineConfig c;
+  c.min_support = ms;
+  c.max_len = max_len;
+  c.pairs_only = pairs_only;
+  c.level2_gram = gram;
+  c.level2_mfma = mfma;
+  return c;
+}
+
+using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+using U32 = py::array_t<uint32_t, py::array::c_style | py::array::forcecast>;
+using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+}  // namespace
+
+void register_gpu_bindings(py::module_& m) {
+  m.def("gpu_available", &gpu::available);
+  m.def("gpu_device_count", &gpu::device_count);
+  m.def("gpu_device_name", &gpu::device_name);
+
+  py::class_<gpu::GpuMiner>(m, "GpuMiner")
+      .def(py::init<int, size_t, uintptr_t>(), py::arg("device") = 0, py::arg("arena_bytes") = 0,
+           py::arg("stream") = 0)
+      .def("load_csr", [](gpu::GpuMiner& g, I64 tx_ptr, I32 items, int64_t n_items) {
+        KMLS_CHECK(tx_ptr.size() >= 1, "tx_ptr must have T+1 entries");
+        py::gil_scoped_release nogil;
+        g.load_csr(tx_ptr.data(), items.data(), tx_ptr.size() - 1, n_items);
+      })
+      .def_property_readonly("n_tx", &gpu::GpuMiner::n_tx)
+      .def_property_readonly("n_items", &gpu::GpuMiner::n_items)
+      .def_property_readonly("stream", &gpu::GpuMiner::stream)
+      .def_property_readonly("arena_capacity", &gpu::GpuMiner::arena_capacity)
+      .def("item_support", &gpu::GpuMiner::item_support, py::call_guard<py::gil_scoped_release>())
+      .def("select", [](gpu::GpuMiner& g, U32 counts, int64_t n_tx, double ms) {
+        KMLS_CHECK(counts.size() == g.n_items(), "counts size != n_items");
+        py::gil_scoped_release nogil;
+        return g.select(counts.data(), n_tx, ms);
+      })
+      .def("frequent", [](const gpu::GpuMiner& g) {
+        auto& f = g.frequent();
+        return py::make_tuple(to_array(std::vector<int32_t>(f.ids)),
+                              to_array(std::vector<uint32_t>(f.counts)), f.minsup2);
+      })
+      .def("words_local", &gpu::GpuMiner::words_local)
+      .def("encode_bitmaps", &gpu::GpuMiner::encode_bitmaps, py::call_guard<py::gil_scoped_release>())
+      .def("pair_counts", &gpu::GpuMiner::pair_counts, py::call_guard<py::gil_scoped_release>())
+      .def("mine_bitmaps", [](gpu::GpuMiner& g, uintptr_t bm, int64_t Wp, double ms, int max_len,
+                              bool pairs_only, py::object owned, bool emit_level1, bool download,
+                              bool gram, bool mfma) {
+        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma);
+        std::vector<uint8_t> own;
+        const uint8_t* po = nullptr;
+        if (!owned.is_none()) {
+          U8 o = owned.cast<U8>();
+          own.assign(o.data(), o.data() + o.size());
+          KMLS_CHECK((int64_t)own.size() == (int64_t)g.frequent().ids.size(), "owned mask size != F");
+          po = own.data();
+        }
+        gpu::GpuMineResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = g.mine_bitmaps(bm, Wp, c, po, emit_level1, download);
+        }
+        return result_to_dict(std::move(r));
+      }, py::arg("bm"), py::arg("Wp"), py::arg("min_support"), py::arg("max_len") = 0,
+         py::arg("pairs_only") = false, py::arg("owned") = py::none(), py::arg("emit_level1") = true,
+         py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false)
+      .def("mine", [](gpu::GpuMiner& g, double ms, int max_len, bool pairs_only, bool download,
+                      bool gram, bool mfma) {
+        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma);
+        gpu::GpuMineResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = g.mine(c, download);
+        }
+        return result_to_dict(std::move(r));
+      }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("pairs_only") = false,
+         py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false)
+      .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<gpu::GpuRuleIndex>(m, "GpuRuleIndex")
+      .def(py::init<int, const RuleIndex&, uintptr_t>(), py::arg("device"), py::arg("index"),
+           py::arg("stream") = 0)
+      .def_property_readonly("nnz", &gpu::GpuRuleIndex::nnz)
+      .def_property_readonly("max_row", &gpu::GpuRuleIndex::max_row)
+      .def("query_batch", [](gpu::GpuRuleIndex& ix, I64 q_ptr, I32 seeds, int k) {
+        const int64_t B = q_ptr.size() - 1;
+        py::array_t<int32_t> ids({(py::ssize_t)B, (py::ssize_t)k});
+        py::array_t<int32_t> ns({(py::ssize_t)B});
+        int32_t* po = ids.mutable_data();
+        int32_t* pn = ns.mutable_data();
+        {
+          py::gil_scoped_release nogil;
+          ix.query_batch(q_ptr.data(), B, seeds.data(), k, po, pn);
+        }
+        return py::make_tuple(ids, ns);
+      });
+}
+
+}  // namespace kmls

@@ -1,0 +1,193 @@
+// CPU bitmap-Eclat miner: the native CPU path (MINER=cpu) and the fast oracle for the HIP miner.
+//
+// Produces exactly the itemset set of mlxtend.fpgrowth (machine-learning/main.py:272; semantics
+// in SURVEY Appendix A): level 1 uses `count/T >= ms`, deeper levels `count >= ceil(ms*T)`.
+// The reference's pure-Python FP-tree recursion is replaced by vertical tid-bitmaps:
+// support(P ∪ {b}) = popcount(bits(P) & bits(b)).  Work is split over threads by top-level
+// equivalence class (dynamic scheduling); output order is deterministic (class order).
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "kmls/common.hpp"
+#include "kmls/host.hpp"
+
+namespace kmls {
+
+uint32_t level2_threshold(uint64_t n_tx, double min_support) {
+  return (uint32_t)std::ceil(min_support * (double)n_tx);
+}
+
+uint32_t level1_threshold(uint64_t n_tx, double min_support) {
+  double guess = std::floor(min_support * (double)n_tx);
+  int64_t c = std::max<int64_t>(0, (int64_t)guess - 2);
+  while (!level1_frequent((uint64_t)c, n_tx, min_support)) ++c;
+  while (c > 0 && level1_frequent((uint64_t)(c - 1), n_tx, min_support)) --c;
+  return (uint32_t)c;
+}
+
+FrequentItems select_frequent(const uint32_t* cnt, int64_t n_items, uint64_t n_tx,
+                              double min_support) {
+  FrequentItems f;
+  f.rank_of.assign((size_t)n_items, -1);
+  for (int64_t i = 0; i < n_items; ++i)
+    if (n_tx > 0 && level1_frequent(cnt[i], n_tx, min_support)) f.ids.push_back((int32_t)i);
+  std::stable_sort(f.ids.begin(), f.ids.end(),
+                   [&](int32_t a, int32_t b) { return cnt[a] < cnt[b]; });
+  f.counts.resize(f.ids.size());
+  for (size_t r = 0; r < f.ids.size(); ++r) {
+    f.rank_of[f.ids[r]] = (int32_t)r;
+    f.counts[r] = cnt[f.ids[r]];
+  }
+  f.minsup2 = level2_threshold(n_tx, min_support);
+  return f;
+}
+
+void count_items(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, int64_t n_items,
+                 uint32_t* out) {
+  std::fill(out, out + n_items, 0u);
+  for (int64_t i = tx_ptr[0]; i < tx_ptr[n_tx]; ++i) out[items[i]]++;
+}
+
+namespace {
+
+// A class member: `off` >= 0 is an offset into the thread's arena, < 0 encodes the
+// top-level bitmap of Eclat rank (-1 - off).  Offsets (not pointers) because the arena grows.
+struct Member {
+  int32_t rank;
+  uint32_t cnt;
+  int64_t off;
+  int64_t node;  // task-local node id (>=0) or -1-global for level-1 nodes
+};
+
+struct Task {
+  std::vector<int64_t> parent;  // >=0 local, <0 : -1-global
+  std::vector<int32_t> item;
+  std::vector<uint32_t> count;
+  std::vector<uint8_t> depth;
+  int64_t candidates = 0;
+  int max_depth = 0;
+};
+
+struct Ctx {
+  const FrequentItems* fi;
+  const uint64_t* top_bm;  // [F][W]
+  int64_t W;
+  uint32_t minsup;
+  int max_len;
+};
+
+inline const uint64_t* resolve(const Ctx& cx, const std::vector<uint64_t>& arena, int64_t off) {
+  return off >= 0 ? arena.data() + off : cx.top_bm + (-1 - off) * cx.W;
+}
+
+// Expand member i of class `cls` (itemset size `depth`): intersect it with every later member,
+// emit the frequent ones, then recurse into the child class.  Child bitmaps are bump-allocated
+// at `top` in the per-thread arena.
+void expand_member(const Ctx& cx, const std::vector<Member>& cls, size_t i, int depth,
+                   std::vector<uint64_t>& arena, size_t top, Task& task) {
+  const int64_t W = cx.W;
+  const size_t need = top + (cls.size() - i - 1) * (size_t)W;
+  if (arena.size() < need) arena.resize(need + (need >> 1) + 1024);
+  const Member a = cls[i];
+  const uint64_t* x = resolve(cx, arena, a.off);
+  std::vector<Member> child;
+  size_t cur = top;
+  for (size_t j = i + 1; j < cls.size(); ++j) {
+    const uint64_t* y = resolve(cx, arena, cls[j].off);
+    uint64_t* o = arena.data() + cur;
+    uint32_t c = 0;
+    for (int64_t w = 0; w < W; ++w) {
+      uint64_t v = x[w] & y[w];
+      o[w] = v;
+      c += (uint32_t)__builtin_popcountll(v);
+    }
+    ++task.candidates;
+    if (c >= cx.minsup) {
+      int64_t id = (int64_t)task.item.size();
+      task.parent.push_back(a.node);
+      task.item.push_back(cx.fi->ids[cls[j].rank]);
+      task.count.push_back(c);
+      task.depth.push_back((uint8_t)(depth + 1));
+      child.push_back(Member{cls[j].rank, c, (int64_t)cur, id});
+      cur += (size_t)W;
+    }
+  }
+  if (!child.empty() && depth + 1 > task.max_depth) task.max_depth = depth + 1;
+  if (child.size() >= 2 && (cx.max_len == 0 || depth + 1 < cx.max_len)) {
+    for (size_t k = 0; k + 1 < child.size(); ++k) expand_member(cx, child, k, depth + 1, arena, cur, task);
+  }
+}
+
+}  // namespace
+
+ItemsetTrie mine_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, int64_t n_items,
+                     const MineConfig& cfg, MineStats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint32_t> cnt((size_t)n_items);
+  count_items(tx_ptr, items, n_tx, n_items, cnt.data());
+  FrequentItems fi = select_frequent(cnt.data(), n_items, (uint64_t)n_tx, cfg.min_support);
+  const int64_t F = (int64_t)fi.ids.size();
+  const int64_t W = (n_tx + 63) / 64;
+  // item-major bitmaps of frequent items
+  std::vector<uint64_t> bm((size_t)(F * W), 0);
+  for (int64_t t = 0; t < n_tx; ++t) {
+    for (int64_t p = tx_ptr[t]; p < tx_ptr[t + 1]; ++p) {
+      int32_t r = fi.rank_of[items[p]];
+      if (r >= 0) bm[(size_t)r * W + (t >> 6)] |= (1ull << (t & 63));
+    }
+  }
+  ItemsetTrie out;
+  for (int64_t r = 0; r < F; ++r) out.push(-1, fi.ids[r], fi.counts[r], 1);
+  const int max_len = cfg.pairs_only ? 2 : cfg.max_len;
+  std::vector<Task> tasks((size_t)std::max<int64_t>(F, 0));
+  if (F >= 2 && max_len != 1) {
+    Ctx cx{&fi, bm.data(), W, fi.minsup2, max_len};
+    int nth = cfg.threads > 0 ? cfg.threads : (int)std::thread::hardware_concurrency();
+    nth = std::max(1, std::min<int>(nth, (int)F));
+    std::atomic<int64_t> next{0};
+    std::vector<Member> root((size_t)F);
+    for (int64_t j = 0; j < F; ++j) root[(size_t)j] = Member{(int32_t)j, fi.counts[j], -1 - j, -1 - j};
+    auto worker = [&]() {
+      std::vector<uint64_t> arena;
+      while (true) {
+        int64_t i = next.fetch_add(1);
+        if (i >= F - 1) break;
+        expand_member(cx, root, (size_t)i, 1, arena, 0, tasks[(size_t)i]);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nth; ++t) pool.emplace_back(worker);
+    for (auto& th : pool) th.join();
+  }
+  int64_t total = F, cands = 0;
+  int maxd = F > 0 ? 1 : 0;
+  for (auto& t : tasks) {
+    total += (int64_t)t.item.size();
+    cands += t.candidates;
+    maxd = std::max(maxd, t.max_depth);
+  }
+  out.reserve((size_t)total);
+  for (auto& t : tasks) {
+    const int64_t off = out.size();
+    for (size_t k = 0; k < t.item.size(); ++k) {
+      int64_t p = t.parent[k];
+      out.push(p >= 0 ? off + p : (-1 - p), t.item[k], t.count[k], t.depth[k]);
+    }
+    std::vector<int64_t>().swap(t.parent);
+  }
+  if (stats) {
+    stats->n_frequent_items = F;
+    stats->n_itemsets = out.size();
+    stats->n_candidates = cands;
+    stats->max_depth = maxd;
+    stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return out;
+}
+
+}  // namespace kmls

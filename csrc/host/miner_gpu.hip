@@ -1,0 +1,482 @@
+// Host driver of the GPU FP-Growth miner (HIP runtime; kernels in csrc/kernels/mine.hip).
+//
+// Search order is "DFS over batches": each level of the equivalence-class tree is expanded in
+// candidate chunks (BFS-wide inside a chunk, so a launch has millions of teams to fill 256
+// CUs), and each chunk's survivors are recursed into before the next chunk, so HBM use is
+// bounded by one chunk per depth (LIFO device arena) instead of a whole level.
+// Replaces mlxtend's recursive conditional-FP-tree generator (machine-learning/main.py:272,
+// SURVEY §3.1 "HOT LOOP 3").
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../kernels/kernels.hpp"
+#include "kmls/gpu.hpp"
+
+#define KMLS_HIP(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +      \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__));     \
+  } while (0)
+
+namespace kmls {
+namespace gpu {
+
+bool available() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return n > 0;
+}
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+std::string device_name(int dev) {
+  hipDeviceProp_t p;
+  KMLS_HIP(hipGetDeviceProperties(&p, dev));
+  return std::string(p.name) + " (" + p.gcnArchName + ")";
+}
+
+// ------------------------------------------------------------------------------------------
+DeviceArena::DeviceArena(size_t bytes) : cap_(bytes) {
+  KMLS_HIP(hipMalloc((void**)&base_, bytes));
+}
+DeviceArena::~DeviceArena() {
+  if (base_) (void)hipFree(base_);
+}
+void* DeviceArena::push(size_t bytes) {
+  size_t off = (top_ + 255) & ~(size_t)255;
+  if (off + bytes > cap_)
+    throw std::runtime_error("kmls: device arena exhausted (" + std::to_string(off + bytes) +
+                             " > " + std::to_string(cap_) + " bytes); raise KMLS_ARENA_GB");
+  top_ = off + bytes;
+  hw_ = std::max(hw_, top_);
+  return base_ + off;
+}
+
+namespace {
+
+template <typename T>
+struct DevVec {  // growable device array (output trie)
+  T* p = nullptr;
+  int64_t cap = 0;
+  void reserve(int64_t n, hipStream_t s) {
+    if (n <= cap) return;
+    int64_t nc = std::max<int64_t>(n, cap * 2);
+    T* q = nullptr;
+    KMLS_HIP(hipMalloc((void**)&q, (size_t)nc * sizeof(T)));
+    if (p) {
+      KMLS_HIP(hipMemcpyAsync(q, p, (size_t)cap * sizeof(T), hipMemcpyDeviceToDevice, s));
+      KMLS_HIP(hipStreamSynchronize(s));
+      KMLS_HIP(hipFree(p));
+    }
+    p = q;
+    cap = nc;
+  }
+  ~DevVec() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+struct Level {
+  int64_t n = 0;
+  const uint64_t* bm = nullptr;
+  const int32_t* rank = nullptr;
+  const int64_t* gid = nullptr;
+  const int32_t* row_end = nullptr;
+};
+
+struct Event {
+  hipEvent_t e;
+  Event() { KMLS_HIP(hipEventCreate(&e)); }
+  ~Event() { (void)hipEventDestroy(e); }
+};
+
+constexpr int64_t kCandCap = 32ll << 20;  // candidates per chunk
+
+struct MineRun {
+  hipStream_t s;
+  DeviceArena* arena;
+  int64_t Wp;
+  uint32_t minsup;
+  int max_len;
+  const int32_t* d_ids;
+  const uint32_t* gram = nullptr;  // root-level pair counts (dense F x F) if computed
+  int64_t F = 0;
+  DevVec<int64_t> out_parent;
+  DevVec<int32_t> out_item;
+  DevVec<uint32_t> out_count;
+  DevVec<uint8_t> out_depth;
+  int64_t out_size = 0;
+  int64_t n_candidates = 0;
+  int max_depth = 1;
+  int64_t* h_scalar = nullptr;  // pinned
+
+  int64_t read_scalar(const int64_t* dptr) {
+    KMLS_HIP(hipMemcpyAsync(h_scalar, dptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+    return *h_scalar;
+  }
+
+  void ensure_out(int64_t n) {
+    out_parent.reserve(n, s);
+    out_item.reserve(n, s);
+    out_count.reserve(n, s);
+    out_depth.reserve(n, s);
+  }
+
+  // Expand every row of level L (itemsets of size `depth`).  `root_len` (host) overrides the
+  // per-row candidate counts at the root (ownership mask for item-sharded multi-GPU).
+  void process(const Level& L, int depth, const std::vector<int64_t>* root_len) {
+    if (L.n < 2 || (max_len && depth >= max_len)) return;
+    const size_t mark0 = arena->mark();
+    int64_t* len = (int64_t*)arena->push((size_t)L.n * sizeof(int64_t));
+    if (root_len) {
+      KMLS_HIP(hipMemcpyAsync(len, root_len->data(), (size_t)L.n * sizeof(int64_t),
+                              hipMemcpyHostToDevice, s));
+    } else {
+      kern::row_lengths(L.row_end, L.n, len, s);
+    }
+    int64_t* cand_off = (int64_t*)arena->push((size_t)(L.n + 1) * sizeof(int64_t));
+    const size_t tb = kern::scan_temp_bytes(L.n);
+    void* tmp = arena->push(tb);
+    kern::exclusive_scan_i64(len, cand_off, L.n, tmp, tb, s);
+    const int64_t total = read_scalar(cand_off + L.n);
+    if (total == 0) {
+      arena->pop_to(mark0);
+      return;
+    }
+    // chunk boundaries at row granularity
+    std::vector<std::pair<int64_t, int64_t>> chunks;  // candidate ranges
+    if (total <= kCandCap) {
+      chunks.push_back({0, total});
+    } else {
+      std::vector<int64_t> off((size_t)L.n + 1);
+      KMLS_HIP(hipMemcpyAsync(off.data(), cand_off, off.size() * sizeof(int64_t),
+                              hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipStreamSynchronize(s));
+      int64_t c0 = 0;
+      for (int64_t a = 0; a < L.n; ++a) {
+        if (off[a + 1] - c0 > kCandCap && off[a] > c0) {
+          chunks.push_back({c0, off[a]});
+          c0 = off[a];
+        }
+      }
+      chunks.push_back({c0, total});
+    }
+    for (auto [c0, c1] : chunks) {
+      const size_t mark = arena->mark();
+      const int64_t nc = c1 - c0;
+      uint32_t* cnt = (uint32_t*)arena->push((size_t)nc * sizeof(uint32_t));
+      if (gram && depth == 1)
+        kern::gram_to_cand(gram, F, cand_off, c0, c1, cnt, s);
+      else
+        kern::extend_count(L.bm, Wp, cand_off, L.n, c0, c1, cnt, s);
+      int64_t* pos = (int64_t*)arena->push((size_t)(nc + 1) * sizeof(int64_t));
+      const size_t fb = kern::flag_scan_temp_bytes(nc);
+      void* ftmp = arena->push(fb);
+      kern::flag_scan(cnt, minsup, nc, pos, ftmp, fb, s);
+      n_candidates += nc;
+      const int64_t S = read_scalar(pos + nc);
+      if (S == 0) {
+        arena->pop_to(mark);
+        continue;
+      }
+      ensure_out(out_size + S);
+      Level C;
+      C.n = S;
+      uint64_t* cbm = (uint64_t*)arena->push((size_t)S * Wp * sizeof(uint64_t));
+      int32_t* crank = (int32_t*)arena->push((size_t)S * sizeof(int32_t));
+      int64_t* cgid = (int64_t*)arena->push((size_t)S * sizeof(int64_t));
+      int32_t* cend = (int32_t*)arena->push((size_t)S * sizeof(int32_t));
+      kern::LevelOut o{cbm, crank, cgid, cend, out_parent.p, out_item.p, out_count.p,
+                       out_depth.p, out_size, (uint8_t)(depth + 1)};
+      kern::extend_materialize(L.bm, Wp, cand_off, L.n, L.rank, L.gid, d_ids, c0, c1, cnt, minsup,
+                               pos, o, s);
+      out_size += S;
+      max_depth = std::max(max_depth, depth + 1);
+      C.bm = cbm;
+      C.rank = crank;
+      C.gid = cgid;
+      C.row_end = cend;
+      process(C, depth + 1, nullptr);
+      arena->pop_to(mark);
+    }
+    arena->pop_to(mark0);
+  }
+};
+
+size_t default_arena_bytes() {
+  size_t free_b = 0, total_b = 0;
+  KMLS_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (const char* e = std::getenv("KMLS_ARENA_GB")) {
+    const double gb = std::atof(e);
+    if (gb > 0) return std::min(free_b - (free_b >> 4), (size_t)(gb * (1ull << 30)));
+  }
+  // half of free HBM by default (the other half stays with torch / RCCL buffers)
+  return free_b / 2;
+}
+
+float elapsed(const Event& a, const Event& b) {
+  float ms = 0.f;
+  KMLS_HIP(hipEventElapsedTime(&ms, a.e, b.e));
+  return ms;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(device) {
+  KMLS_HIP(hipSetDevice(device));
+  if (stream) {
+    stream_ = (void*)stream;
+  } else {
+    hipStream_t s;
+    KMLS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    stream_ = (void*)s;
+    own_stream_ = true;
+  }
+  arena_ = std::make_unique<DeviceArena>(arena_bytes ? arena_bytes : default_arena_bytes());
+}
+
+GpuMiner::~GpuMiner() {
+  (void)hipSetDevice(device_);
+  if (d_tx_ptr_) (void)hipFree(d_tx_ptr_);
+  if (d_items_) (void)hipFree(d_items_);
+  if (d_rank_of_) (void)hipFree(d_rank_of_);
+  if (d_ids_) (void)hipFree(d_ids_);
+  if (d_own_bm_) (void)hipFree(d_own_bm_);
+  arena_.reset();
+  if (own_stream_) (void)hipStreamDestroy((hipStream_t)stream_);
+}
+
+size_t GpuMiner::arena_capacity() const { return arena_->capacity(); }
+
+void GpuMiner::synchronize() { KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_)); }
+
+void GpuMiner::load_csr(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
+                        int64_t n_items) {
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  if (d_tx_ptr_) KMLS_HIP(hipFree(d_tx_ptr_));
+  if (d_items_) KMLS_HIP(hipFree(d_items_));
+  d_tx_ptr_ = nullptr;
+  d_items_ = nullptr;
+  n_tx_ = n_tx;
+  n_items_ = n_items;
+  const int64_t base = tx_ptr[0];
+  nnz_ = tx_ptr[n_tx] - base;
+  std::vector<int64_t> rebased((size_t)n_tx + 1);
+  for (int64_t t = 0; t <= n_tx; ++t) rebased[t] = tx_ptr[t] - base;
+  for (int64_t p = 0; p < nnz_; ++p) {
+    const int32_t it = items[base + p];
+    KMLS_CHECK(it >= 0 && it < n_items, "item id out of range in CSR");
+  }
+  KMLS_HIP(hipMalloc((void**)&d_tx_ptr_, rebased.size() * sizeof(int64_t)));
+  KMLS_HIP(hipMalloc((void**)&d_items_, (size_t)std::max<int64_t>(nnz_, 4) * sizeof(int32_t)));
+  KMLS_HIP(hipMemcpyAsync(d_tx_ptr_, rebased.data(), rebased.size() * sizeof(int64_t),
+                          hipMemcpyHostToDevice, s));
+  if (nnz_)
+    KMLS_HIP(hipMemcpyAsync(d_items_, items + base, (size_t)nnz_ * sizeof(int32_t),
+                            hipMemcpyHostToDevice, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+}
+
+void GpuMiner::item_support(uintptr_t counts_dev) {
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  KMLS_HIP(hipMemsetAsync((void*)counts_dev, 0, (size_t)n_items_ * sizeof(uint32_t), s));
+  kern::item_support(d_items_, nnz_, (int32_t)n_items_, (uint32_t*)counts_dev, s);
+}
+
+int64_t GpuMiner::select(const uint32_t* global_counts, int64_t global_n_tx, double min_support) {
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  global_n_tx_ = global_n_tx;
+  fi_ = select_frequent(global_counts, n_items_, (uint64_t)global_n_tx, min_support);
+  if (d_rank_of_) KMLS_HIP(hipFree(d_rank_of_));
+  if (d_ids_) KMLS_HIP(hipFree(d_ids_));
+  KMLS_HIP(hipMalloc((void**)&d_rank_of_, (size_t)std::max<int64_t>(n_items_, 1) * sizeof(int32_t)));
+  KMLS_HIP(hipMalloc((void**)&d_ids_, std::max<size_t>(fi_.ids.size(), 1) * sizeof(int32_t)));
+  KMLS_HIP(hipMemcpyAsync(d_rank_of_, fi_.rank_of.data(), (size_t)n_items_ * sizeof(int32_t),
+                          hipMemcpyHostToDevice, s));
+  if (!fi_.ids.empty())
+    KMLS_HIP(hipMemcpyAsync(d_ids_, fi_.ids.data(), fi_.ids.size() * sizeof(int32_t),
+                            hipMemcpyHostToDevice, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  return (int64_t)fi_.ids.size();
+}
+
+int64_t GpuMiner::words_local() const {
+  const int64_t w = (n_tx_ + 63) / 64;
+  return (w + 3) & ~(int64_t)3;  // 32-byte rows: 16-B team loads and the MFMA 4-word stride
+}
+
+void GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_off) {
+  KMLS_HIP(hipSetDevice(device_));
+  kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev, Wp_total,
+                      word_off, (hipStream_t)stream_);
+}
+
+void GpuMiner::pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev, bool use_mfma) {
+  KMLS_HIP(hipSetDevice(device_));
+  const int64_t F = (int64_t)fi_.ids.size();
+  hipStream_t s = (hipStream_t)stream_;
+  KMLS_HIP(hipMemsetAsync((void*)out_dev, 0, (size_t)F * F * sizeof(uint32_t), s));
+  if (use_mfma)
+    kern::pair_gram_mfma_i8((const uint64_t*)bm_dev, Wp_total, F, (uint32_t*)out_dev, s);
+  else
+    kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp_total, F, (uint32_t*)out_dev, s);
+}
+
+GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineConfig& cfg,
+                                     const uint8_t* owned_mask, bool emit_level1,
+                                     bool download) {
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  GpuMineResult res;
+  const int64_t F = (int64_t)fi_.ids.size();
+  MineRun run;
+  run.s = s;
+  run.arena = arena_.get();
+  run.Wp = Wp;
+  run.minsup = fi_.minsup2;
+  run.max_len = cfg.pairs_only ? 2 : cfg.max_len;
+  run.d_ids = d_ids_;
+  run.F = F;
+  KMLS_HIP(hipHostMalloc((void**)&run.h_scalar, 64));
+  Event e0, e1, e2, e3;
+  KMLS_HIP(hipEventRecord(e0.e, s));
+  const size_t mark = arena_->mark();
+  // level-1 nodes: gid = Eclat rank
+  run.ensure_out(std::max<int64_t>(F * 8, 1 << 16));
+  {
+    std::vector<int64_t> par((size_t)F, -1);
+    std::vector<uint8_t> dep((size_t)F, 1);
+    if (F) {
+      KMLS_HIP(hipMemcpyAsync(run.out_parent.p, par.data(), F * sizeof(int64_t), hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(run.out_item.p, fi_.ids.data(), F * sizeof(int32_t), hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(run.out_count.p, fi_.counts.data(), F * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(run.out_depth.p, dep.data(), F * sizeof(uint8_t), hipMemcpyHostToDevice, s));
+    }
+    run.out_size = F;
+  }
+  if (F >= 2 && run.max_len != 1) {
+    // root level: one class of all F frequent items
+    std::vector<int32_t> rank((size_t)F), row_end((size_t)F, (int32_t)F);
+    std::vector<int64_t> gid((size_t)F), root_len((size_t)F);
+    for (int64_t a = 0; a < F; ++a) {
+      rank[a] = (int32_t)a;
+      gid[a] = a;
+      const bool own = owned_mask == nullptr || owned_mask[a];
+      root_len[a] = own ? (F - a - 1) : 0;
+    }
+    int32_t* d_rank = (int32_t*)arena_->push(F * sizeof(int32_t));
+    int64_t* d_gid = (int64_t*)arena_->push(F * sizeof(int64_t));
+    int32_t* d_end = (int32_t*)arena_->push(F * sizeof(int32_t));
+    KMLS_HIP(hipMemcpyAsync(d_rank, rank.data(), F * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    KMLS_HIP(hipMemcpyAsync(d_gid, gid.data(), F * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    KMLS_HIP(hipMemcpyAsync(d_end, row_end.data(), F * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    // level 2 through the bit-GEMM (LDS-tiled, 64x64 tiles) when the dense F x F fits
+    if (F <= 32768 && cfg.level2_gram) {
+      uint32_t* gram = (uint32_t*)arena_->push((size_t)F * F * sizeof(uint32_t));
+      KMLS_HIP(hipMemsetAsync(gram, 0, (size_t)F * F * sizeof(uint32_t), s));
+      if (cfg.level2_mfma)
+        kern::pair_gram_mfma_i8((const uint64_t*)bm_dev, Wp, F, gram, s);
+      else
+        kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);
+      run.gram = gram;
+    }
+    KMLS_HIP(hipEventRecord(e1.e, s));
+    Level root;
+    root.n = F;
+    root.bm = (const uint64_t*)bm_dev;
+    root.rank = d_rank;
+    root.gid = d_gid;
+    root.row_end = d_end;
+    run.process(root, 1, &root_len);
+  } else {
+    KMLS_HIP(hipEventRecord(e1.e, s));
+  }
+  KMLS_HIP(hipEventRecord(e2.e, s));
+  const int64_t N = run.out_size;
+  if (download) {
+    res.trie.parent.resize((size_t)N);
+    res.trie.item.resize((size_t)N);
+    res.trie.count.resize((size_t)N);
+    res.trie.depth.resize((size_t)N);
+    if (N) {
+      KMLS_HIP(hipMemcpyAsync(res.trie.parent.data(), run.out_parent.p, N * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.trie.item.data(), run.out_item.p, N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.trie.count.data(), run.out_count.p, N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.trie.depth.data(), run.out_depth.p, N * sizeof(uint8_t), hipMemcpyDeviceToHost, s));
+    }
+  }
+  KMLS_HIP(hipEventRecord(e3.e, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  res.phases.push_back({"level2_gram", elapsed(e0, e1)});
+  res.phases.push_back({"levels_3plus", elapsed(e1, e2)});
+  res.phases.push_back({"download", elapsed(e2, e3)});
+  res.stats.n_frequent_items = F;
+  res.stats.n_itemsets = emit_level1 ? N : N - F;
+  res.stats.n_candidates = run.n_candidates;
+  res.stats.max_depth = F ? run.max_depth : 0;
+  res.arena_high_water = (int64_t)arena_->high_water();
+  arena_->pop_to(mark);
+  (void)hipHostFree(run.h_scalar);
+  return res;
+}
+
+GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download) {
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  auto t0 = std::chrono::steady_clock::now();
+  Event e0, e1, e2;
+  KMLS_HIP(hipEventRecord(e0.e, s));
+  const size_t mark = arena_->mark();
+  uint32_t* d_cnt = (uint32_t*)arena_->push((size_t)std::max<int64_t>(n_items_, 1) * sizeof(uint32_t));
+  item_support((uintptr_t)d_cnt);
+  std::vector<uint32_t> cnt((size_t)n_items_);
+  KMLS_HIP(hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  arena_->pop_to(mark);
+  const int64_t F = select(cnt.data(), n_tx_, cfg.min_support);
+  KMLS_HIP(hipEventRecord(e1.e, s));
+  const int64_t Wp = words_local();
+  const size_t need = (size_t)std::max<int64_t>(F, 1) * Wp * sizeof(uint64_t);
+  if (need > own_bm_bytes_) {
+    if (d_own_bm_) KMLS_HIP(hipFree(d_own_bm_));
+    KMLS_HIP(hipMalloc((void**)&d_own_bm_, need));
+    own_bm_bytes_ = need;
+  }
+  KMLS_HIP(hipMemsetAsync(d_own_bm_, 0, need, s));
+  encode_bitmaps((uintptr_t)d_own_bm_, Wp, 0);
+  KMLS_HIP(hipEventRecord(e2.e, s));
+  GpuMineResult r = mine_bitmaps((uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
+  std::vector<Phase> ph;
+  ph.push_back({"support+select", elapsed(e0, e1)});
+  ph.push_back({"encode_bitmap", elapsed(e1, e2)});
+  for (auto& p : r.phases) ph.push_back(p);
+  r.phases = ph;
+  r.stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return r;
+}
+
+}  // namespace gpu
+}  // namespace kmls

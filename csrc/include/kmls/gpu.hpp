@@ -1,0 +1,146 @@
+// HIP (gfx950) runtime API of kmls: the GPU FP-Growth miner and the HBM-resident rule index.
+//
+// Host code talks to the device only through this header; kernels live in csrc/kernels/*.hip.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "kmls/common.hpp"
+#include "kmls/host.hpp"
+
+namespace pybind11 { class module_; }
+
+namespace kmls {
+
+void register_gpu_bindings(pybind11::module_& m);
+
+namespace gpu {
+
+bool available();
+int device_count();
+std::string device_name(int dev);
+
+// Bump/stack allocator over one big hipMalloc (DFS-of-batches needs strictly LIFO buffers).
+class DeviceArena {
+ public:
+  explicit DeviceArena(size_t bytes);
+  ~DeviceArena();
+  void* push(size_t bytes);   // 256-byte aligned
+  size_t mark() const { return top_; }
+  void pop_to(size_t mark) { top_ = mark; }
+  size_t capacity() const { return cap_; }
+  size_t high_water() const { return hw_; }
+  size_t used() const { return top_; }
+ private:
+  char* base_ = nullptr;
+  size_t cap_ = 0, top_ = 0, hw_ = 0;
+};
+
+struct Phase {
+  std::string name;
+  double ms;
+};
+
+struct GpuMineResult {
+  ItemsetTrie trie;           // empty if download == false
+  MineStats stats;
+  std::vector<Phase> phases;  // hipEvent-timed phases
+  int64_t arena_high_water = 0;
+};
+
+// Resident-data GPU miner.  Typical use: load() once (CSR → HBM), mine() many times.
+// Multi-GPU: every rank calls the same sequence; collectives are done by the Python layer
+// (torch.distributed / RCCL) on the buffers exposed through the *_dev accessors.
+class GpuMiner {
+ public:
+  GpuMiner(int device, size_t arena_bytes, uintptr_t stream);
+  ~GpuMiner();
+
+  // Transaction CSR (rows duplicate-free) → HBM.  tx ids are local to this shard.
+  void load_csr(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, int64_t n_items);
+  int64_t n_tx() const { return n_tx_; }
+  int64_t n_items() const { return n_items_; }
+
+  // Phase A: per-item supports of the resident shard into `counts_dev` (uint32[n_items]).
+  void item_support(uintptr_t counts_dev);
+  // Phase B: frequent-item selection from GLOBAL supports (host array) + global T.
+  // Returns F.  `owned` (optional, size F): which top-level classes this rank mines.
+  int64_t select(const uint32_t* global_counts, int64_t global_n_tx, double min_support);
+  // Phase C: tid-bitmaps of frequent items for the resident shard, into an external buffer
+  // (uint64[F][Wp]) at word offset `word_off` of rows of stride `Wp_total` words.
+  int64_t words_local() const;  // padded words for the local shard
+  void encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_off);
+  // Phase D: full mining over replicated bitmaps (uint64[F][Wp_total]) covering `n_tx_total`.
+  //   owned_mask: optional uint8[F] (top-level classes to expand; level-1 nodes always emitted
+  //   by rank 0 only when emit_level1).
+  GpuMineResult mine_bitmaps(uintptr_t bm_dev, int64_t Wp_total, const MineConfig& cfg,
+                             const uint8_t* owned_mask, bool emit_level1, bool download);
+  // Convenience single-GPU path: A + B + C + D.
+  GpuMineResult mine(const MineConfig& cfg, bool download);
+
+  // Frequent items of the last select(): ids (ascending support) and counts.
+  const FrequentItems& frequent() const { return fi_; }
+  // Pair supports (level-2) between frequent items as a dense upper-triangular matrix
+  // count[F][F] (row-major, only i<j valid) via the bit-GEMM kernels. Used by the rule-map
+  // fast path and by the multi-GPU pair all-reduce.
+  void pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev, bool use_mfma);
+
+  uintptr_t stream() const { return (uintptr_t)stream_; }
+  void synchronize();
+  size_t arena_capacity() const;
+
+ private:
+  int device_;
+  void* stream_ = nullptr;
+  bool own_stream_ = false;
+  std::unique_ptr<DeviceArena> arena_;
+  int64_t n_tx_ = 0, n_items_ = 0, nnz_ = 0;
+  int64_t* d_tx_ptr_ = nullptr;
+  int32_t* d_items_ = nullptr;
+  FrequentItems fi_;
+  int64_t global_n_tx_ = 0;
+  int32_t* d_rank_of_ = nullptr;
+  int32_t* d_ids_ = nullptr;
+  uint64_t* d_own_bm_ = nullptr;  // single-GPU bitmap buffer
+  size_t own_bm_bytes_ = 0;
+};
+
+// HBM-resident rule index + batched matcher kernel (serve_match_topk).
+class GpuRuleIndex {
+ public:
+  GpuRuleIndex(int device, const RuleIndex& host, uintptr_t stream);
+  ~GpuRuleIndex();
+  // q_ptr: int64[B+1], seeds: int32[nnz] (host).  Output host arrays ids[B*k], n[B]
+  // with n = -1 when no seed is a key.  Exact reference ordering (score desc, then
+  // first-insertion order).
+  void query_batch(const int64_t* q_ptr, int64_t B, const int32_t* seeds, int k, int32_t* out_ids,
+                   int32_t* out_n);
+  int64_t nnz() const { return nnz_; }
+  int64_t n_items() const { return n_items_; }
+  int max_row() const { return max_row_; }
+
+ private:
+  int device_;
+  void* stream_ = nullptr;
+  bool own_stream_ = false;
+  int64_t n_items_ = 0, nnz_ = 0;
+  int max_row_ = 0;
+  int64_t* d_row_ptr_ = nullptr;
+  int32_t* d_cons_ = nullptr;
+  uint32_t* d_score_ = nullptr;  // dense rank of the score (exact order key), see serve.hip
+  uint8_t* d_is_key_ = nullptr;
+  // staging buffers (grown on demand)
+  int64_t cap_q_ = 0, cap_s_ = 0, cap_o_ = 0;
+  int64_t* d_q_ptr_ = nullptr;
+  int32_t* d_seeds_ = nullptr;
+  int32_t* d_out_ = nullptr;
+  int32_t* h_pinned_ = nullptr;
+  int64_t cap_pinned_ = 0;
+};
+
+}  // namespace gpu
+}  // namespace kmls

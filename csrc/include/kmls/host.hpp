@@ -1,0 +1,79 @@
+// Host-side (CPU) native runtime API: CSV ingest, CSR build, CPU miner, CPU matcher.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kmls/common.hpp"
+
+namespace kmls {
+
+// ---- ingest -------------------------------------------------------------------------------
+struct EncodedTable {
+  int64_t n_rows = 0;
+  std::vector<std::string> header;
+  std::vector<std::string> columns;                  // requested columns
+  std::vector<std::vector<int32_t>> codes;           // per column, per row: dictionary code
+  std::vector<std::vector<std::string>> uniques;     // per column: code -> string
+};
+EncodedTable read_csv_encoded(const std::string& path, const std::vector<std::string>& wanted);
+
+struct CSR {
+  std::vector<int64_t> ptr;
+  std::vector<int32_t> idx;
+};
+// Group `vals` by `keys` (codes in [0, n_keys)), preserving row order inside a group unless
+// sort_rows/dedup are requested.
+CSR group_to_csr(const int32_t* keys, const int32_t* vals, int64_t n, int32_t n_keys, bool dedup,
+                 bool sort_rows);
+
+// ---- CPU miner (bitmap Eclat, std::thread) -------------------------------------------------
+// CSR rows must be duplicate-free.  Produces the complete FP-Growth itemset set.
+struct MineStats {
+  int64_t n_frequent_items = 0;
+  int64_t n_itemsets = 0;
+  int64_t n_candidates = 0;
+  int max_depth = 0;
+  double seconds = 0.0;
+};
+ItemsetTrie mine_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, int64_t n_items,
+                     const MineConfig& cfg, MineStats* stats);
+
+// Pair supports among frequent items (rule-map fast path).
+struct PairTable {
+  std::vector<int32_t> a, b;     // item ids, a has lower Eclat rank than b
+  std::vector<uint32_t> count;
+};
+void count_items(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, int64_t n_items,
+                 uint32_t* out_counts);
+
+// ---- CPU matcher ---------------------------------------------------------------------------
+// Rule index: for each key item, an ordered row of (consequent, score).  Rows may be empty
+// (frequent songs without pairs are keys with `{}`; rest_api/app/main.py:235 distinguishes
+// "key with empty row" from "not a key").
+class RuleIndex {
+ public:
+  RuleIndex(int64_t n_items, std::vector<int64_t> row_ptr, std::vector<int32_t> cons,
+            std::vector<double> score, std::vector<uint8_t> is_key);
+  int64_t n_items() const { return n_items_; }
+  int64_t nnz() const { return (int64_t)cons_.size(); }
+  // Reference matcher semantics (rest_api/app/main.py:235-254): present seeds in request
+  // order; max-merge; stable sort by score desc (ties: first-insertion order); top-k.
+  // Returns -1 when no seed is a key (caller falls back), else the number of results.
+  int query(const int32_t* seeds, int n_seeds, int k, int32_t* out_ids, double* out_scores) const;
+  const std::vector<int64_t>& row_ptr() const { return row_ptr_; }
+  const std::vector<int32_t>& cons() const { return cons_; }
+  const std::vector<double>& score() const { return score_; }
+  const std::vector<uint8_t>& is_key() const { return is_key_; }
+
+ private:
+  int64_t n_items_;
+  std::vector<int64_t> row_ptr_;
+  std::vector<int32_t> cons_;
+  std::vector<double> score_;
+  std::vector<uint8_t> is_key_;
+};
+
+}  // namespace kmls

@@ -1,0 +1,134 @@
+// Level-2 co-occurrence GEMM on the matrix cores: G = A·Aᵀ over the transaction axis, with A
+// the 0/1 one-hot matrix of frequent items stored as packed tid-bitmaps (SURVEY §2.C O8,
+// BASELINE north star "MFMA int8 one-hot×one-hot co-occurrence GEMM for the first pass").
+//
+// v_mfma_i32_32x32x32_i8 (gfx950): lane l (r = l&31, h = l>>5) supplies A[row r][k = 16h + j]
+// and B[k = 16h + j][col r], j = 0..15, as 16 int8 in 4 VGPRs; C/D (16 i32 / lane):
+// col = l&31, row = (reg&3) + 8*(reg>>2) + 4*h.  Bits are unpacked to int8 in registers
+// (4 bits → one dword: ((n * 0x00204081) & 0x01010101)), so HBM/L2 traffic stays at 1 bit per
+// (item, transaction) — 8x fewer bytes than an int8 one-hot operand.
+//
+// Tiling: 256-thread block = 4 waves (2x2) → 128x128 output tile; each wave 64x64 = 2x2 MFMA
+// tiles (4 accumulators, 64 AGPRs) so every unpacked fragment feeds 2 MFMAs.  Row words are
+// read 32 B at a time per lane (4 words = 256 transactions = 8 K-steps of 32).  Only upper-
+// triangular block tiles are launched (G is symmetric); blocks are remapped XCD-aware so the
+// tiles of one tile-row share an XCD L2.
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels.hpp"
+
+namespace kmls {
+namespace kern {
+
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint32_t nib(uint32_t x) { return (x * 0x00204081u) & 0x01010101u; }
+
+// 16 bits → 16 int8 {0,1} (k order = bit order)
+__device__ __forceinline__ v4i unpack16(uint32_t bits) {
+  v4i r;
+  r.x = (int)nib(bits & 0xF);
+  r.y = (int)nib((bits >> 4) & 0xF);
+  r.z = (int)nib((bits >> 8) & 0xF);
+  r.w = (int)nib((bits >> 12) & 0xF);
+  return r;
+}
+
+constexpr int kTile = 128;
+
+__global__ __launch_bounds__(256) void k_pair_gram_mfma(const unsigned long long* __restrict__ bm,
+                                                         int64_t Wp, int64_t F, int64_t n_tiles,
+                                                         int64_t n_blocks,
+                                                         uint32_t* __restrict__ out) {
+  // XCD-aware bijective remap (cdna_hip_programming.md §5): consecutive logical tiles go to
+  // the same XCD (blockIdx % 8 labels an XCD group).
+  const int64_t orig = blockIdx.x;
+  const int64_t q = n_blocks / 8, rr = n_blocks % 8, xcd = orig % 8;
+  int64_t idx = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  int64_t ti = 0;
+  while (idx >= n_tiles - ti) { idx -= n_tiles - ti; ++ti; }
+  const int64_t tj = ti + idx;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t a0 = ti * kTile + wr * 64 + r, a1 = a0 + 32;
+  const int64_t b0 = tj * kTile + wc * 64 + r, b1 = b0 + 32;
+  const bool va0 = a0 < F, va1 = a1 < F, vb0 = b0 < F, vb1 = b1 < F;
+  const ulonglong2* pa0 = reinterpret_cast<const ulonglong2*>(bm + (va0 ? a0 : 0) * Wp);
+  const ulonglong2* pa1 = reinterpret_cast<const ulonglong2*>(bm + (va1 ? a1 : 0) * Wp);
+  const ulonglong2* pb0 = reinterpret_cast<const ulonglong2*>(bm + (vb0 ? b0 : 0) * Wp);
+  const ulonglong2* pb1 = reinterpret_cast<const ulonglong2*>(bm + (vb1 ? b1 : 0) * Wp);
+
+  v16i acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
+  const int shift = 16 * h;
+  const int64_t n2 = Wp >> 1;  // 16-byte chunks per row (Wp is a multiple of 4 words)
+  for (int64_t w2 = 0; w2 < n2; w2 += 2) {
+    ulonglong2 A0[2], A1[2], B0[2], B1[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      A0[u] = va0 ? pa0[w2 + u] : make_ulonglong2(0, 0);
+      A1[u] = va1 ? pa1[w2 + u] : make_ulonglong2(0, 0);
+      B0[u] = vb0 ? pb0[w2 + u] : make_ulonglong2(0, 0);
+      B1[u] = vb1 ? pb1[w2 + u] : make_ulonglong2(0, 0);
+    }
+#pragma unroll
+    for (int wd = 0; wd < 4; ++wd) {
+      const unsigned long long xa0 = (wd & 1) ? A0[wd >> 1].y : A0[wd >> 1].x;
+      const unsigned long long xa1 = (wd & 1) ? A1[wd >> 1].y : A1[wd >> 1].x;
+      const unsigned long long xb0 = (wd & 1) ? B0[wd >> 1].y : B0[wd >> 1].x;
+      const unsigned long long xb1 = (wd & 1) ? B1[wd >> 1].y : B1[wd >> 1].x;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {  // 32 transactions per MFMA K-step
+        const int sh = 32 * half + shift;
+        const v4i fa0 = unpack16((uint32_t)(xa0 >> sh) & 0xFFFFu);
+        const v4i fa1 = unpack16((uint32_t)(xa1 >> sh) & 0xFFFFu);
+        const v4i fb0 = unpack16((uint32_t)(xb0 >> sh) & 0xFFFFu);
+        const v4i fb1 = unpack16((uint32_t)(xb1 >> sh) & 0xFFFFu);
+        acc00 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb0, acc00, 0, 0, 0);
+        acc01 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb1, acc01, 0, 0, 0);
+        acc10 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb0, acc10, 0, 0, 0);
+        acc11 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb1, acc11, 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: row = (reg&3) + 8*(reg>>2) + 4h (within the 32-row MFMA tile), col = lane&31
+  const int64_t rowb0 = ti * kTile + wr * 64, colb0 = tj * kTile + wc * 64;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    const int64_t rA = rowb0 + row, rB = rowb0 + 32 + row;
+    const int64_t cA = colb0 + r, cB = colb0 + 32 + r;
+    if (rA < F) {
+      if (cA < F && cA > rA) out[rA * F + cA] = (uint32_t)acc00[reg];
+      if (cB < F && cB > rA) out[rA * F + cB] = (uint32_t)acc01[reg];
+    }
+    if (rB < F) {
+      if (cA < F && cA > rB) out[rB * F + cA] = (uint32_t)acc10[reg];
+      if (cB < F && cB > rB) out[rB * F + cB] = (uint32_t)acc11[reg];
+    }
+  }
+}
+
+}  // namespace
+
+void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s) {
+  if (F < 2) return;
+  if (Wp % 4 != 0) throw std::runtime_error("kmls: pair_gram_mfma_i8 needs Wp % 4 == 0");
+  const int64_t nt = (F + kTile - 1) / kTile;
+  const int64_t blocks = nt * (nt + 1) / 2;
+  hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)blocks), dim3(256), 0, s,
+                     (const unsigned long long*)bm, Wp, F, nt, blocks, out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e));
+}
+
+}  // namespace kern
+}  // namespace kmls

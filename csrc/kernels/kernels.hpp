@@ -1,0 +1,61 @@
+// Launch wrappers of the CDNA4 kernels (implemented in csrc/kernels/*.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace kmls {
+namespace kern {
+
+// ---- mining (mine.hip) ----
+void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* counts,
+                  hipStream_t s);
+void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
+                   const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
+                   hipStream_t s);
+// per-row candidate count len[a] = row_end[a] - a - 1  → out_len (int64[n])
+void row_lengths(const int32_t* row_end, int64_t n, int64_t* out_len, hipStream_t s);
+// exclusive prefix sum over int64[n] into out[n+1] (out[n] = total); temp from arena
+size_t scan_temp_bytes(int64_t n);
+void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* temp, size_t temp_bytes,
+                        hipStream_t s);
+// flags (count >= minsup) exclusive scan over int32 counts → pos[n+1]
+size_t flag_scan_temp_bytes(int64_t n);
+void flag_scan(const uint32_t* cnt, uint32_t minsup, int64_t n, int64_t* pos, void* temp,
+               size_t temp_bytes, hipStream_t s);
+// candidate support counting, candidates [c0, c1) of a level (cand_off has n_rows+1 entries,
+// absolute); writes cnt[c - c0]
+void extend_count(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
+                  int64_t c0, int64_t c1, uint32_t* cnt, hipStream_t s);
+// materialise the survivors of candidates [c0, c1)
+struct LevelOut {
+  uint64_t* bm;        // child bitmaps [S][Wp]
+  int32_t* rank;       // child last-item Eclat rank
+  int64_t* gid;        // child global node id
+  int32_t* row_end;    // child class end (child-local index)
+  int64_t* out_parent; // global trie arrays (indexed by out_base + s)
+  int32_t* out_item;
+  uint32_t* out_count;
+  uint8_t* out_depth;
+  int64_t out_base;
+  uint8_t depth;
+};
+void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
+                        const int32_t* rank, const int64_t* gid, const int32_t* ids,
+                        int64_t c0, int64_t c1, const uint32_t* cnt, uint32_t minsup,
+                        const int64_t* pos, const LevelOut& o, hipStream_t s);
+// dense upper-triangular pair counts over a single class of F rows (level 2 bit-GEMM)
+void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
+void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
+// dense Gram (F x F, i<j valid) → per-candidate counts in (a, b) row-major candidate order
+void gram_to_cand(const uint32_t* gram, int64_t F, const int64_t* cand_off, int64_t c0, int64_t c1,
+                  uint32_t* cnt, hipStream_t s);
+
+// ---- serving (serve.hip) ----
+void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,
+                      const uint8_t* is_key, int64_t n_items, const int64_t* q_ptr,
+                      const int32_t* seeds, int64_t B, int k, int32_t* out, hipStream_t s);
+
+}  // namespace kern
+}  // namespace kmls

@@ -1,0 +1,392 @@
+// CDNA4 (gfx950) kernels of the GPU FP-Growth miner.
+//
+// Replaces the reference's mining hot path (mlxtend TransactionEncoder + fpgrowth + the rule
+// loop, machine-learning/main.py:262-296) with vertical tid-bitmaps:
+//   item_support      O5  per-item supports (LDS-privatised histogram)
+//   encode_bitmap     O4  CSR → item-major bit-packed tid bitmaps (uint64 words, HBM resident)
+//   pair_gram_*       O8  level-2 co-occurrence "GEMM" over the transaction axis
+//   extend_count      O8  |S|>=3 candidate supports: wave64 teams AND + popcount
+//   extend_materialize    survivors' bitmaps + itemset-trie append (ordered compaction)
+//
+// All kernels are wave64-native: teams are power-of-two lane groups inside a 64-lane wave,
+// reductions use __shfl_xor within the team, block sizes are multiples of 64.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels.hpp"
+
+#define KMLS_HIP(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +      \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__));     \
+  } while (0)
+
+namespace kmls {
+namespace kern {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline int grid_for(int64_t work, int per_block, int cap = 4096) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// ----------------------------------------------------------------------------------------
+// O5 item supports
+// ----------------------------------------------------------------------------------------
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void k_item_support(const int32_t* __restrict__ items,
+                                                         int64_t nnz, int32_t n_items,
+                                                         uint32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+  if constexpr (kLds) {
+    for (int i = threadIdx.x; i < n_items; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+  }
+  uint32_t* dst = kLds ? hist : counts;
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  // 16-byte vector loads over the aligned body (items comes from hipMalloc)
+  const int64_t n4 = nnz >> 2;
+  const int4* v = reinterpret_cast<const int4*>(items);
+  for (int64_t i = gtid; i < n4; i += nthr) {
+    const int4 q = v[i];
+    atomicAdd(&dst[q.x], 1u);
+    atomicAdd(&dst[q.y], 1u);
+    atomicAdd(&dst[q.z], 1u);
+    atomicAdd(&dst[q.w], 1u);
+  }
+  for (int64_t i = (n4 << 2) + gtid; i < nnz; i += nthr) atomicAdd(&dst[items[i]], 1u);
+  if constexpr (kLds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < n_items; i += blockDim.x) {
+      const uint32_t h = hist[i];
+      if (h) atomicAdd(&counts[i], h);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// O4 bitmap encode: bit t of row rank_of[item] for every (t, item) of the CSR shard
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restrict__ tx_ptr,
+                                                          const int32_t* __restrict__ items,
+                                                          int64_t n_tx,
+                                                          const int32_t* __restrict__ rank_of,
+                                                          unsigned long long* __restrict__ bm,
+                                                          int64_t Wp, int64_t word_off) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_tx; t += nthr) {
+    const unsigned long long bit = 1ull << (t & 63);
+    const int64_t w = word_off + (t >> 6);
+    const int64_t p1 = tx_ptr[t + 1];
+    for (int64_t p = tx_ptr[t]; p < p1; ++p) {
+      const int32_t r = rank_of[items[p]];
+      if (r >= 0) atomicOr(&bm[(int64_t)r * Wp + w], bit);
+    }
+  }
+}
+
+__global__ void k_row_lengths(const int32_t* __restrict__ row_end, int64_t n,
+                              int64_t* __restrict__ len) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; a < n; a += nthr)
+    len[a] = (int64_t)row_end[a] - a - 1;
+}
+
+__global__ void k_scan_tail(const int64_t* __restrict__ in, int64_t* __restrict__ out, int64_t n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) out[n] = n ? out[n - 1] + in[n - 1] : 0;
+}
+
+struct FlagOp {
+  uint32_t minsup;
+  __host__ __device__ int64_t operator()(uint32_t c) const { return c >= minsup ? 1 : 0; }
+};
+
+__global__ void k_flag_tail(const uint32_t* __restrict__ cnt, uint32_t minsup,
+                            int64_t* __restrict__ pos, int64_t n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0)
+    pos[n] = n ? pos[n - 1] + (cnt[n - 1] >= minsup ? 1 : 0) : 0;
+}
+
+// ----------------------------------------------------------------------------------------
+// candidate → (row a, sibling b) decode: largest a with cand_off[a] <= c
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t find_row(const int64_t* __restrict__ cand_off, int64_t n_rows,
+                                            int64_t c) {
+  int64_t lo = 0, hi = n_rows;
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (cand_off[mid] <= c) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// ----------------------------------------------------------------------------------------
+// O8 |S|>=3: team-per-candidate AND + popcount (TS lanes of a wave64 per candidate)
+// ----------------------------------------------------------------------------------------
+template <int TS>
+__global__ __launch_bounds__(kBlock) void k_extend_count(const unsigned long long* __restrict__ bm,
+                                                         int64_t Wp,
+                                                         const int64_t* __restrict__ cand_off,
+                                                         int64_t n_rows, int64_t c0, int64_t c1,
+                                                         uint32_t* __restrict__ cnt) {
+  const int tl = threadIdx.x & (TS - 1);
+  const int64_t team = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / TS;
+  const int64_t nteams = ((int64_t)gridDim.x * blockDim.x) / TS;
+  for (int64_t c = c0 + team; c < c1; c += nteams) {
+    const int64_t a = find_row(cand_off, n_rows, c);
+    const int64_t b = a + 1 + (c - cand_off[a]);
+    const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
+    const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
+    uint32_t s = 0;
+    const int64_t n2 = Wp >> 1;
+    for (int64_t w = tl; w < n2; w += TS) {
+      const ulonglong2 u = x[w], v = y[w];
+      s += (uint32_t)__popcll(u.x & v.x) + (uint32_t)__popcll(u.y & v.y);
+    }
+#pragma unroll
+    for (int off = TS >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, TS);
+    if (tl == 0) cnt[c - c0] = s;
+  }
+}
+
+template <int TS>
+__global__ __launch_bounds__(kBlock) void k_extend_materialize(
+    const unsigned long long* __restrict__ bm, int64_t Wp, const int64_t* __restrict__ cand_off,
+    int64_t n_rows, const int32_t* __restrict__ rank, const int64_t* __restrict__ gid,
+    const int32_t* __restrict__ ids, int64_t c0, int64_t c1, const uint32_t* __restrict__ cnt,
+    uint32_t minsup, const int64_t* __restrict__ pos, LevelOut o) {
+  const int tl = threadIdx.x & (TS - 1);
+  const int64_t team = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / TS;
+  const int64_t nteams = ((int64_t)gridDim.x * blockDim.x) / TS;
+  for (int64_t c = c0 + team; c < c1; c += nteams) {
+    const uint32_t k = cnt[c - c0];
+    if (k < minsup) continue;  // team-uniform
+    const int64_t a = find_row(cand_off, n_rows, c);
+    const int64_t b = a + 1 + (c - cand_off[a]);
+    const int64_t s = pos[c - c0];
+    const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
+    const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
+    ulonglong2* z = reinterpret_cast<ulonglong2*>(o.bm + s * Wp);
+    const int64_t n2 = Wp >> 1;
+    for (int64_t w = tl; w < n2; w += TS) {
+      const ulonglong2 u = x[w], v = y[w];
+      z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
+    }
+    if (tl == 0) {
+      const int32_t rb = rank[b];
+      o.rank[s] = rb;
+      o.gid[s] = o.out_base + s;
+      o.row_end[s] = (int32_t)pos[cand_off[a + 1] - c0];
+      o.out_parent[o.out_base + s] = gid[a];
+      o.out_item[o.out_base + s] = ids[rb];
+      o.out_count[o.out_base + s] = k;
+      o.out_depth[o.out_base + s] = o.depth;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// O8 level 2: tiled bit-GEMM  G[i][j] = popcount(row_i & row_j), 64x64 output tile / block,
+// K staged through LDS in transposed [k][row] layout (16 words per stage).
+// ----------------------------------------------------------------------------------------
+constexpr int kGT = 64;   // tile rows/cols
+constexpr int kGK = 16;   // words per K stage
+
+__global__ __launch_bounds__(kBlock) void k_pair_gram_popcount(
+    const unsigned long long* __restrict__ bm, int64_t Wp, int64_t F, int64_t n_tiles,
+    uint32_t* __restrict__ out) {
+  __shared__ unsigned long long As[kGK][kGT + 2];
+  __shared__ unsigned long long Bs[kGK][kGT + 2];
+  // upper-triangular tile decode: blockIdx.x → (ti <= tj)
+  int64_t idx = blockIdx.x, ti = 0;
+  while (idx >= n_tiles - ti) { idx -= n_tiles - ti; ++ti; }
+  const int64_t tj = ti + idx;
+  const int64_t r0 = ti * kGT, q0 = tj * kGT;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  uint32_t acc[4][4] = {};
+  // staging map: thread → (row = tid>>2, words (tid&3)*4 .. +3)
+  const int lr = threadIdx.x >> 2, lk = (threadIdx.x & 3) * 4;
+  for (int64_t k0 = 0; k0 < Wp; k0 += kGK) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t kk = k0 + lk + i;
+      const int64_t ra = r0 + lr, rb = q0 + lr;
+      As[lk + i][lr] = (ra < F && kk < Wp) ? bm[ra * Wp + kk] : 0ull;
+      Bs[lk + i][lr] = (rb < F && kk < Wp) ? bm[rb * Wp + kk] : 0ull;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < kGK; ++k) {
+      unsigned long long a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { a[i] = As[k][ty * 4 + i]; b[i] = Bs[k][tx * 4 + i]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += (uint32_t)__popcll(a[i] & b[j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t r = r0 + ty * 4 + i;
+    if (r >= F) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t q = q0 + tx * 4 + j;
+      if (q < F && q > r) out[r * F + q] = acc[i][j];
+    }
+  }
+}
+
+// gram (dense F x F, i<j valid) → per-candidate counts in (a, b) row-major candidate order
+__global__ void k_gram_to_cand(const uint32_t* __restrict__ gram, int64_t F,
+                               const int64_t* __restrict__ cand_off, int64_t c0, int64_t c1,
+                               uint32_t* __restrict__ cnt) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t c = c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < c1; c += nthr) {
+    const int64_t a = find_row(cand_off, F, c);
+    const int64_t b = a + 1 + (c - cand_off[a]);
+    cnt[c - c0] = gram[a * F + b];
+  }
+}
+
+int team_size(int64_t Wp) {
+  const int64_t chunks = Wp >> 1;  // 16-byte chunks per row
+  if (chunks >= 128) return 64;
+  if (chunks >= 64) return 32;
+  if (chunks >= 32) return 16;
+  if (chunks >= 12) return 8;
+  return 4;
+}
+
+}  // namespace
+
+void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* counts,
+                  hipStream_t s) {
+  if (nnz <= 0) return;
+  const size_t lds = (size_t)n_items * sizeof(uint32_t);
+  if (lds <= 64 * 1024) {
+    const int g = grid_for(nnz, kBlock * 64, 1024);
+    hipLaunchKernelGGL(k_item_support<true>, dim3(g), dim3(kBlock), lds, s, items, nnz, n_items,
+                       counts);
+  } else {
+    const int g = grid_for(nnz, kBlock * 4, 8192);
+    hipLaunchKernelGGL(k_item_support<false>, dim3(g), dim3(kBlock), 0, s, items, nnz, n_items,
+                       counts);
+  }
+  KMLS_HIP(hipGetLastError());
+}
+
+void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
+                   const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
+                   hipStream_t s) {
+  if (n_tx <= 0) return;
+  hipLaunchKernelGGL(k_encode_bitmap, dim3(grid_for(n_tx, kBlock, 8192)), dim3(kBlock), 0, s,
+                     tx_ptr, items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off);
+  KMLS_HIP(hipGetLastError());
+}
+
+void row_lengths(const int32_t* row_end, int64_t n, int64_t* out_len, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_row_lengths, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, row_end, n,
+                     out_len);
+  KMLS_HIP(hipGetLastError());
+}
+
+size_t scan_temp_bytes(int64_t n) {
+  size_t bytes = 0;
+  KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int64_t*)nullptr,
+                                            (int64_t*)nullptr, (int)std::max<int64_t>(n, 1)));
+  return bytes;
+}
+
+void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* temp, size_t temp_bytes,
+                        hipStream_t s) {
+  if (n > 0) KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s));
+  hipLaunchKernelGGL(k_scan_tail, dim3(1), dim3(64), 0, s, in, out, n);
+  KMLS_HIP(hipGetLastError());
+}
+
+size_t flag_scan_temp_bytes(int64_t n) {
+  size_t bytes = 0;
+  hipcub::TransformInputIterator<int64_t, FlagOp, const uint32_t*> it(nullptr, FlagOp{0});
+  KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (int64_t*)nullptr,
+                                            (int)std::max<int64_t>(n, 1)));
+  return bytes;
+}
+
+void flag_scan(const uint32_t* cnt, uint32_t minsup, int64_t n, int64_t* pos, void* temp,
+               size_t temp_bytes, hipStream_t s) {
+  if (n > 0) {
+    hipcub::TransformInputIterator<int64_t, FlagOp, const uint32_t*> it(cnt, FlagOp{minsup});
+    KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, it, pos, (int)n, s));
+  }
+  hipLaunchKernelGGL(k_flag_tail, dim3(1), dim3(64), 0, s, cnt, minsup, pos, n);
+  KMLS_HIP(hipGetLastError());
+}
+
+#define KMLS_TEAM_DISPATCH(TS_VAR, KERNEL, ...)                                              \
+  switch (TS_VAR) {                                                                          \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                               \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                               \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                             \
+    case 32: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                             \
+    default: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                             \
+  }
+
+void extend_count(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
+                  int64_t c0, int64_t c1, uint32_t* cnt, hipStream_t s) {
+  if (c1 <= c0) return;
+  const int ts = team_size(Wp);
+  const int64_t teams_per_block = kBlock / ts;
+  const int g = grid_for(c1 - c0, (int)teams_per_block, 256 * 32);
+  KMLS_TEAM_DISPATCH(ts, k_extend_count, dim3(g), dim3(kBlock), 0, s,
+                     (const unsigned long long*)bm, Wp, cand_off, n_rows, c0, c1, cnt);
+  KMLS_HIP(hipGetLastError());
+}
+
+void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
+                        const int32_t* rank, const int64_t* gid, const int32_t* ids, int64_t c0,
+                        int64_t c1, const uint32_t* cnt, uint32_t minsup, const int64_t* pos,
+                        const LevelOut& o, hipStream_t s) {
+  if (c1 <= c0) return;
+  const int ts = team_size(Wp);
+  const int64_t teams_per_block = kBlock / ts;
+  const int g = grid_for(c1 - c0, (int)teams_per_block, 256 * 32);
+  KMLS_TEAM_DISPATCH(ts, k_extend_materialize, dim3(g), dim3(kBlock), 0, s,
+                     (const unsigned long long*)bm, Wp, cand_off, n_rows, rank, gid, ids, c0, c1,
+                     cnt, minsup, pos, o);
+  KMLS_HIP(hipGetLastError());
+}
+
+void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s) {
+  if (F < 2) return;
+  const int64_t nt = (F + kGT - 1) / kGT;
+  const int64_t blocks = nt * (nt + 1) / 2;
+  hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks), dim3(kBlock), 0, s,
+                     (const unsigned long long*)bm, Wp, F, nt, out);
+  KMLS_HIP(hipGetLastError());
+}
+
+void gram_to_cand(const uint32_t* gram, int64_t F, const int64_t* cand_off, int64_t c0, int64_t c1,
+                  uint32_t* cnt, hipStream_t s) {
+  if (c1 <= c0) return;
+  hipLaunchKernelGGL(k_gram_to_cand, dim3(grid_for(c1 - c0, kBlock, 8192)), dim3(kBlock), 0, s,
+                     gram, F, cand_off, c0, c1, cnt);
+  KMLS_HIP(hipGetLastError());
+}
+
+}  // namespace kern
+}  // namespace kmls
