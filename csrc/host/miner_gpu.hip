@@ -374,6 +374,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       KMLS_HIP(hipMemcpyAsync(run.out_item.p, fi_.ids.data(), F * sizeof(int32_t), hipMemcpyHostToDevice, s));
       KMLS_HIP(hipMemcpyAsync(run.out_count.p, fi_.counts.data(), F * sizeof(uint32_t), hipMemcpyHostToDevice, s));
       KMLS_HIP(hipMemcpyAsync(run.out_depth.p, dep.data(), F * sizeof(uint8_t), hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipStreamSynchronize(s));  // par/dep are pageable and die at scope end
     }
     run.out_size = F;
   }
