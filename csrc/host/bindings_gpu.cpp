@@ -17,12 +17,20 @@ py::array_t<T> to_array(std::vector<T>&& v) {
   return py::array_t<T>({(py::ssize_t)heap->size()}, {(py::ssize_t)sizeof(T)}, heap->data(), owner);
 }
 
+template <typename T>
+py::array_t<T> pinned_array(const std::shared_ptr<void>& buf, int64_t n) {
+  if (!buf) return py::array_t<T>(0);
+  auto* keep = new std::shared_ptr<void>(buf);
+  py::capsule owner(keep, [](void* p) { delete reinterpret_cast<std::shared_ptr<void>*>(p); });
+  return py::array_t<T>({(py::ssize_t)n}, {(py::ssize_t)sizeof(T)}, (T*)buf.get(), owner);
+}
+
 py::dict result_to_dict(gpu::GpuMineResult&& r) {
   py::dict d;
-  d["parent"] = to_array(std::move(r.trie.parent));
-  d["item"] = to_array(std::move(r.trie.item));
-  d["count"] = to_array(std::move(r.trie.count));
-  d["depth"] = to_array(std::move(r.trie.depth));
+  d["parent"] = pinned_array<int64_t>(r.h_parent, r.n_nodes);
+  d["item"] = pinned_array<int32_t>(r.h_item, r.n_nodes);
+  d["count"] = pinned_array<uint32_t>(r.h_count, r.n_nodes);
+  d["depth"] = pinned_array<uint8_t>(r.h_depth, r.n_nodes);
   py::dict s;
   s["n_frequent_items"] = r.stats.n_frequent_items;
   s["n_itemsets"] = r.stats.n_itemsets;

@@ -70,6 +70,41 @@ void* DeviceArena::push(size_t bytes) {
   return base_ + off;
 }
 
+PinnedPool::~PinnedPool() {
+  for (auto& b : bufs_) (void)hipHostFree(b.p);
+  delete (std::mutex*)mu_;
+}
+
+std::shared_ptr<PinnedPool> make_pinned_pool() {
+  auto p = std::shared_ptr<PinnedPool>(new PinnedPool());
+  p->mu_ = new std::mutex();
+  return p;
+}
+
+std::shared_ptr<void> PinnedPool::get(size_t bytes) {
+  bytes = std::max<size_t>(bytes, 64);
+  std::lock_guard<std::mutex> lk(*(std::mutex*)mu_);
+  int best = -1;
+  for (int i = 0; i < (int)bufs_.size(); ++i)
+    if (!bufs_[i].busy && bufs_[i].bytes >= bytes && (best < 0 || bufs_[i].bytes < bufs_[best].bytes))
+      best = i;
+  if (best < 0) {
+    void* p = nullptr;
+    const size_t cap = bytes + (bytes >> 2);
+    KMLS_HIP(hipHostMalloc(&p, cap));
+    bufs_.push_back({p, cap, false});
+    best = (int)bufs_.size() - 1;
+  }
+  bufs_[best].busy = true;
+  void* ptr = bufs_[best].p;
+  auto self = shared_from_this();
+  return std::shared_ptr<void>(ptr, [self, ptr](void*) {
+    std::lock_guard<std::mutex> lk(*(std::mutex*)self->mu_);
+    for (auto& b : self->bufs_)
+      if (b.p == ptr) b.busy = false;
+  });
+}
+
 namespace {
 
 template <typename T>
@@ -126,12 +161,15 @@ struct MineRun {
   int64_t out_size = 0;
   int64_t n_candidates = 0;
   int max_depth = 1;
-  int64_t* h_scalar = nullptr;  // pinned
+  int64_t* h_scalar = nullptr;  // pinned [2]
 
-  int64_t read_scalar(const int64_t* dptr) {
-    KMLS_HIP(hipMemcpyAsync(h_scalar, dptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  uint64_t* d_pair = nullptr;   // device [survivors, next-level candidates]
+
+  void read_pair(int64_t& S, int64_t& next_total) {
+    KMLS_HIP(hipMemcpyAsync(h_scalar, d_pair, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     KMLS_HIP(hipStreamSynchronize(s));
-    return *h_scalar;
+    S = h_scalar[0];
+    next_total = h_scalar[1];
   }
 
   void ensure_out(int64_t n) {
@@ -141,48 +179,39 @@ struct MineRun {
     out_depth.reserve(n, s);
   }
 
-  // Expand every row of level L (itemsets of size `depth`).  `root_len` (host) overrides the
-  // per-row candidate counts at the root (ownership mask for item-sharded multi-GPU).
-  void process(const Level& L, int depth, const std::vector<int64_t>* root_len) {
-    if (L.n < 2 || (max_len && depth >= max_len)) return;
+  // Expand every row of level L (itemsets of size `depth`).  `len` (device, L.n+1 entries,
+  // len[L.n] == 0) holds each row's candidate count and `total` their sum — both produced by
+  // the parent chunk (or the host at the root), so a chunk costs ONE host readback: the
+  // survivor count and the child level's candidate total, read together.
+  void process(const Level& L, int depth, const int64_t* len, int64_t total) {
+    if (L.n < 2 || total == 0 || (max_len && depth >= max_len)) return;
     const size_t mark0 = arena->mark();
-    int64_t* len = (int64_t*)arena->push((size_t)L.n * sizeof(int64_t));
-    if (root_len) {
-      KMLS_HIP(hipMemcpyAsync(len, root_len->data(), (size_t)L.n * sizeof(int64_t),
-                              hipMemcpyHostToDevice, s));
-    } else {
-      kern::row_lengths(L.row_end, L.n, len, s);
-    }
     int64_t* cand_off = (int64_t*)arena->push((size_t)(L.n + 1) * sizeof(int64_t));
     const size_t tb = kern::scan_temp_bytes(L.n);
     void* tmp = arena->push(tb);
     kern::exclusive_scan_i64(len, cand_off, L.n, tmp, tb, s);
-    const int64_t total = read_scalar(cand_off + L.n);
-    if (total == 0) {
-      arena->pop_to(mark0);
-      return;
-    }
-    // chunk boundaries at row granularity
-    std::vector<std::pair<int64_t, int64_t>> chunks;  // candidate ranges
+    struct Chunk { int64_t a0, a1, c0, c1; };
+    std::vector<Chunk> chunks;
     if (total <= kCandCap) {
-      chunks.push_back({0, total});
-    } else {
+      chunks.push_back({0, L.n, 0, total});
+    } else {  // split at row boundaries
       std::vector<int64_t> off((size_t)L.n + 1);
       KMLS_HIP(hipMemcpyAsync(off.data(), cand_off, off.size() * sizeof(int64_t),
                               hipMemcpyDeviceToHost, s));
       KMLS_HIP(hipStreamSynchronize(s));
-      int64_t c0 = 0;
+      int64_t a0 = 0;
       for (int64_t a = 0; a < L.n; ++a) {
-        if (off[a + 1] - c0 > kCandCap && off[a] > c0) {
-          chunks.push_back({c0, off[a]});
-          c0 = off[a];
+        if (off[a + 1] - off[a0] > kCandCap && a > a0) {
+          chunks.push_back({a0, a, off[a0], off[a]});
+          a0 = a;
         }
       }
-      chunks.push_back({c0, total});
+      chunks.push_back({a0, L.n, off[a0], off[L.n]});
     }
-    for (auto [c0, c1] : chunks) {
+    for (const Chunk& ch : chunks) {
+      const int64_t c0 = ch.c0, c1 = ch.c1, nc = c1 - c0;
+      if (nc == 0) continue;
       const size_t mark = arena->mark();
-      const int64_t nc = c1 - c0;
       uint32_t* cnt = (uint32_t*)arena->push((size_t)nc * sizeof(uint32_t));
       if (gram && depth == 1)
         kern::gram_to_cand(gram, F, cand_off, c0, c1, cnt, s);
@@ -192,8 +221,10 @@ struct MineRun {
       const size_t fb = kern::flag_scan_temp_bytes(nc);
       void* ftmp = arena->push(fb);
       kern::flag_scan(cnt, minsup, nc, pos, ftmp, fb, s);
+      kern::child_totals(cand_off, ch.a0, ch.a1, c0, pos, nc, d_pair, s);
       n_candidates += nc;
-      const int64_t S = read_scalar(pos + nc);
+      int64_t S = 0, next_total = 0;
+      read_pair(S, next_total);
       if (S == 0) {
         arena->pop_to(mark);
         continue;
@@ -205,7 +236,9 @@ struct MineRun {
       int32_t* crank = (int32_t*)arena->push((size_t)S * sizeof(int32_t));
       int64_t* cgid = (int64_t*)arena->push((size_t)S * sizeof(int64_t));
       int32_t* cend = (int32_t*)arena->push((size_t)S * sizeof(int32_t));
-      kern::LevelOut o{cbm, crank, cgid, cend, out_parent.p, out_item.p, out_count.p,
+      int64_t* clen = (int64_t*)arena->push((size_t)(S + 1) * sizeof(int64_t));
+      KMLS_HIP(hipMemsetAsync(clen + S, 0, sizeof(int64_t), s));
+      kern::LevelOut o{cbm, crank, cgid, cend, clen, out_parent.p, out_item.p, out_count.p,
                        out_depth.p, out_size, (uint8_t)(depth + 1)};
       kern::extend_materialize(L.bm, Wp, cand_off, L.n, L.rank, L.gid, d_ids, c0, c1, cnt, minsup,
                                pos, o, s);
@@ -215,7 +248,7 @@ struct MineRun {
       C.rank = crank;
       C.gid = cgid;
       C.row_end = cend;
-      process(C, depth + 1, nullptr);
+      process(C, depth + 1, clen, next_total);
       arena->pop_to(mark);
     }
     arena->pop_to(mark0);
@@ -253,6 +286,7 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
     own_stream_ = true;
   }
   arena_ = std::make_unique<DeviceArena>(arena_bytes ? arena_bytes : default_arena_bytes());
+  pinned_ = make_pinned_pool();
 }
 
 GpuMiner::~GpuMiner() {
@@ -361,6 +395,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   run.d_ids = d_ids_;
   run.F = F;
   KMLS_HIP(hipHostMalloc((void**)&run.h_scalar, 64));
+  KMLS_HIP(hipMalloc((void**)&run.d_pair, 2 * sizeof(uint64_t)));
   Event e0, e1, e2, e3;
   KMLS_HIP(hipEventRecord(e0.e, s));
   const size_t mark = arena_->mark();
@@ -381,12 +416,14 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   if (F >= 2 && run.max_len != 1) {
     // root level: one class of all F frequent items
     std::vector<int32_t> rank((size_t)F), row_end((size_t)F, (int32_t)F);
-    std::vector<int64_t> gid((size_t)F), root_len((size_t)F);
+    std::vector<int64_t> gid((size_t)F), root_len((size_t)F + 1, 0);
+    int64_t root_total = 0;
     for (int64_t a = 0; a < F; ++a) {
       rank[a] = (int32_t)a;
       gid[a] = a;
       const bool own = owned_mask == nullptr || owned_mask[a];
       root_len[a] = own ? (F - a - 1) : 0;
+      root_total += root_len[a];
     }
     int32_t* d_rank = (int32_t*)arena_->push(F * sizeof(int32_t));
     int64_t* d_gid = (int64_t*)arena_->push(F * sizeof(int64_t));
@@ -394,6 +431,8 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     KMLS_HIP(hipMemcpyAsync(d_rank, rank.data(), F * sizeof(int32_t), hipMemcpyHostToDevice, s));
     KMLS_HIP(hipMemcpyAsync(d_gid, gid.data(), F * sizeof(int64_t), hipMemcpyHostToDevice, s));
     KMLS_HIP(hipMemcpyAsync(d_end, row_end.data(), F * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    int64_t* d_len = (int64_t*)arena_->push((F + 1) * sizeof(int64_t));
+    KMLS_HIP(hipMemcpyAsync(d_len, root_len.data(), (F + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
     // level 2 through the bit-GEMM (LDS-tiled, 64x64 tiles) when the dense F x F fits
     if (F <= 32768 && cfg.level2_gram) {
       uint32_t* gram = (uint32_t*)arena_->push((size_t)F * F * sizeof(uint32_t));
@@ -411,22 +450,24 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     root.rank = d_rank;
     root.gid = d_gid;
     root.row_end = d_end;
-    run.process(root, 1, &root_len);
+    run.process(root, 1, d_len, root_total);
+    KMLS_HIP(hipStreamSynchronize(s));  // host staging vectors die at scope end
   } else {
     KMLS_HIP(hipEventRecord(e1.e, s));
   }
   KMLS_HIP(hipEventRecord(e2.e, s));
   const int64_t N = run.out_size;
+  res.n_nodes = N;
   if (download) {
-    res.trie.parent.resize((size_t)N);
-    res.trie.item.resize((size_t)N);
-    res.trie.count.resize((size_t)N);
-    res.trie.depth.resize((size_t)N);
+    res.h_parent = pinned_->get((size_t)N * sizeof(int64_t));
+    res.h_item = pinned_->get((size_t)N * sizeof(int32_t));
+    res.h_count = pinned_->get((size_t)N * sizeof(uint32_t));
+    res.h_depth = pinned_->get((size_t)N * sizeof(uint8_t));
     if (N) {
-      KMLS_HIP(hipMemcpyAsync(res.trie.parent.data(), run.out_parent.p, N * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-      KMLS_HIP(hipMemcpyAsync(res.trie.item.data(), run.out_item.p, N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-      KMLS_HIP(hipMemcpyAsync(res.trie.count.data(), run.out_count.p, N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-      KMLS_HIP(hipMemcpyAsync(res.trie.depth.data(), run.out_depth.p, N * sizeof(uint8_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.h_parent.get(), run.out_parent.p, N * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.h_item.get(), run.out_item.p, N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.h_count.get(), run.out_count.p, N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.h_depth.get(), run.out_depth.p, N * sizeof(uint8_t), hipMemcpyDeviceToHost, s));
     }
   }
   KMLS_HIP(hipEventRecord(e3.e, s));
@@ -441,6 +482,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   res.arena_high_water = (int64_t)arena_->high_water();
   arena_->pop_to(mark);
   (void)hipHostFree(run.h_scalar);
+  (void)hipFree(run.d_pair);
   return res;
 }
 

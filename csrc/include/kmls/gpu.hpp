@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -45,8 +46,25 @@ struct Phase {
   double ms;
 };
 
+// Recycling pool of pinned host buffers (hipHostMalloc): results are handed to Python as numpy
+// arrays that alias a buffer; the buffer returns to the pool when the last array dies, so the
+// steady-state download costs no allocation and runs at pinned-DMA speed.
+class PinnedPool : public std::enable_shared_from_this<PinnedPool> {
+ public:
+  ~PinnedPool();
+  std::shared_ptr<void> get(size_t bytes);
+ private:
+  struct Buf { void* p; size_t bytes; bool busy; };
+  std::vector<Buf> bufs_;
+  void* mu_ = nullptr;  // std::mutex (kept out of the header)
+  friend std::shared_ptr<PinnedPool> make_pinned_pool();
+};
+std::shared_ptr<PinnedPool> make_pinned_pool();
+
 struct GpuMineResult {
-  ItemsetTrie trie;           // empty if download == false
+  ItemsetTrie trie;           // host vectors (unused when the pinned arrays below are set)
+  int64_t n_nodes = 0;
+  std::shared_ptr<void> h_parent, h_item, h_count, h_depth;  // pinned, n_nodes entries
   MineStats stats;
   std::vector<Phase> phases;  // hipEvent-timed phases
   int64_t arena_high_water = 0;
@@ -107,6 +125,7 @@ class GpuMiner {
   int32_t* d_ids_ = nullptr;
   uint64_t* d_own_bm_ = nullptr;  // single-GPU bitmap buffer
   size_t own_bm_bytes_ = 0;
+  std::shared_ptr<PinnedPool> pinned_;
 };
 
 // HBM-resident rule index + batched matcher kernel (serve_match_topk).

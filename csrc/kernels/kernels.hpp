@@ -14,13 +14,11 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
 void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                    const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
                    hipStream_t s);
-// per-row candidate count len[a] = row_end[a] - a - 1  → out_len (int64[n])
-void row_lengths(const int32_t* row_end, int64_t n, int64_t* out_len, hipStream_t s);
-// exclusive prefix sum over int64[n] into out[n+1] (out[n] = total); temp from arena
+// exclusive prefix sum over int64[n+1] (in[n] == 0) into out[n+1] (out[n] = total)
 size_t scan_temp_bytes(int64_t n);
 void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* temp, size_t temp_bytes,
                         hipStream_t s);
-// flags (count >= minsup) exclusive scan over int32 counts → pos[n+1]
+// flags (count >= minsup) exclusive scan over n+1 flags → pos[n+1] (pos[n] = survivors)
 size_t flag_scan_temp_bytes(int64_t n);
 void flag_scan(const uint32_t* cnt, uint32_t minsup, int64_t n, int64_t* pos, void* temp,
                size_t temp_bytes, hipStream_t s);
@@ -28,12 +26,16 @@ void flag_scan(const uint32_t* cnt, uint32_t minsup, int64_t n, int64_t* pos, vo
 // absolute); writes cnt[c - c0]
 void extend_count(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
                   int64_t c0, int64_t c1, uint32_t* cnt, hipStream_t s);
+// out2[0] = survivors of chunk, out2[1] = next level's candidate total (one readback)
+void child_totals(const int64_t* cand_off, int64_t a0, int64_t a1, int64_t c0, const int64_t* pos,
+                  int64_t nc, uint64_t* out2, hipStream_t s);
 // materialise the survivors of candidates [c0, c1)
 struct LevelOut {
   uint64_t* bm;        // child bitmaps [S][Wp]
   int32_t* rank;       // child last-item Eclat rank
   int64_t* gid;        // child global node id
   int32_t* row_end;    // child class end (child-local index)
+  int64_t* len;        // child candidate-row lengths (row_end - s - 1), S+1 entries
   int64_t* out_parent; // global trie arrays (indexed by out_base + s)
   int32_t* out_item;
   uint32_t* out_count;

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -76,7 +77,9 @@ __global__ __launch_bounds__(kBlock) void k_item_support(const int32_t* __restri
 }
 
 // ----------------------------------------------------------------------------------------
-// O4 bitmap encode: bit t of row rank_of[item] for every (t, item) of the CSR shard
+// O4 bitmap encode: bit t of row rank_of[item] for every (t, item) of the CSR shard.
+// One wave64 per transaction (lanes stride its items), so a 2k-transaction shard already
+// spreads over ~560 workgroups; 64 transactions share a word column, hence atomicOr.
 // ----------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restrict__ tx_ptr,
                                                           const int32_t* __restrict__ items,
@@ -84,39 +87,28 @@ __global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restr
                                                           const int32_t* __restrict__ rank_of,
                                                           unsigned long long* __restrict__ bm,
                                                           int64_t Wp, int64_t word_off) {
-  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_tx; t += nthr) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < n_tx; t += nwaves) {
     const unsigned long long bit = 1ull << (t & 63);
     const int64_t w = word_off + (t >> 6);
     const int64_t p1 = tx_ptr[t + 1];
-    for (int64_t p = tx_ptr[t]; p < p1; ++p) {
+    for (int64_t p = tx_ptr[t] + lane; p < p1; p += 64) {
       const int32_t r = rank_of[items[p]];
       if (r >= 0) atomicOr(&bm[(int64_t)r * Wp + w], bit);
     }
   }
 }
 
-__global__ void k_row_lengths(const int32_t* __restrict__ row_end, int64_t n,
-                              int64_t* __restrict__ len) {
-  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; a < n; a += nthr)
-    len[a] = (int64_t)row_end[a] - a - 1;
-}
-
-__global__ void k_scan_tail(const int64_t* __restrict__ in, int64_t* __restrict__ out, int64_t n) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) out[n] = n ? out[n - 1] + in[n - 1] : 0;
-}
-
+// flag(i) = (i < n && cnt[i] >= minsup); scanning n+1 flags gives pos[n] = #survivors directly
 struct FlagOp {
+  const uint32_t* cnt;
+  int64_t n;
   uint32_t minsup;
-  __host__ __device__ int64_t operator()(uint32_t c) const { return c >= minsup ? 1 : 0; }
+  __host__ __device__ int64_t operator()(int64_t i) const {
+    return (i < n && cnt[i] >= minsup) ? 1 : 0;
+  }
 };
-
-__global__ void k_flag_tail(const uint32_t* __restrict__ cnt, uint32_t minsup,
-                            int64_t* __restrict__ pos, int64_t n) {
-  if (threadIdx.x == 0 && blockIdx.x == 0)
-    pos[n] = n ? pos[n - 1] + (cnt[n - 1] >= minsup ? 1 : 0) : 0;
-}
 
 // ----------------------------------------------------------------------------------------
 // candidate → (row a, sibling b) decode: largest a with cand_off[a] <= c
@@ -187,7 +179,9 @@ __global__ __launch_bounds__(kBlock) void k_extend_materialize(
       const int32_t rb = rank[b];
       o.rank[s] = rb;
       o.gid[s] = o.out_base + s;
-      o.row_end[s] = (int32_t)pos[cand_off[a + 1] - c0];
+      const int64_t re = pos[cand_off[a + 1] - c0];
+      o.row_end[s] = (int32_t)re;
+      o.len[s] = re - s - 1;
       o.out_parent[o.out_base + s] = gid[a];
       o.out_item[o.out_base + s] = ids[rb];
       o.out_count[o.out_base + s] = k;
@@ -293,47 +287,63 @@ void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                    const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
                    hipStream_t s) {
   if (n_tx <= 0) return;
-  hipLaunchKernelGGL(k_encode_bitmap, dim3(grid_for(n_tx, kBlock, 8192)), dim3(kBlock), 0, s,
+  hipLaunchKernelGGL(k_encode_bitmap, dim3(grid_for(n_tx, kBlock / 64, 8192)), dim3(kBlock), 0, s,
                      tx_ptr, items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off);
-  KMLS_HIP(hipGetLastError());
-}
-
-void row_lengths(const int32_t* row_end, int64_t n, int64_t* out_len, hipStream_t s) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_row_lengths, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, row_end, n,
-                     out_len);
   KMLS_HIP(hipGetLastError());
 }
 
 size_t scan_temp_bytes(int64_t n) {
   size_t bytes = 0;
   KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int64_t*)nullptr,
-                                            (int64_t*)nullptr, (int)std::max<int64_t>(n, 1)));
+                                            (int64_t*)nullptr, (int)(n + 1)));
   return bytes;
 }
 
+// in has n+1 entries with in[n] == 0, so out[n] is the total
 void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* temp, size_t temp_bytes,
                         hipStream_t s) {
-  if (n > 0) KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s));
-  hipLaunchKernelGGL(k_scan_tail, dim3(1), dim3(64), 0, s, in, out, n);
-  KMLS_HIP(hipGetLastError());
+  KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)(n + 1), s));
 }
+
+using FlagIt = hipcub::TransformInputIterator<int64_t, FlagOp, hipcub::CountingInputIterator<int64_t>>;
 
 size_t flag_scan_temp_bytes(int64_t n) {
   size_t bytes = 0;
-  hipcub::TransformInputIterator<int64_t, FlagOp, const uint32_t*> it(nullptr, FlagOp{0});
-  KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (int64_t*)nullptr,
-                                            (int)std::max<int64_t>(n, 1)));
+  FlagIt it(hipcub::CountingInputIterator<int64_t>(0), FlagOp{nullptr, n, 0});
+  KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (int64_t*)nullptr, (int)(n + 1)));
   return bytes;
 }
 
 void flag_scan(const uint32_t* cnt, uint32_t minsup, int64_t n, int64_t* pos, void* temp,
                size_t temp_bytes, hipStream_t s) {
-  if (n > 0) {
-    hipcub::TransformInputIterator<int64_t, FlagOp, const uint32_t*> it(cnt, FlagOp{minsup});
-    KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, it, pos, (int)n, s));
+  FlagIt it(hipcub::CountingInputIterator<int64_t>(0), FlagOp{cnt, n, minsup});
+  KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, it, pos, (int)(n + 1), s));
+}
+
+// After the flag scan of chunk [c0, c1) over rows [a0, a1): child class of row a has
+// size k_a = pos[cand_off[a+1]-c0] - pos[cand_off[a]-c0]; the next level's candidate total is
+// Σ k_a (k_a - 1) / 2.  Written to out[1] (out[0] = #survivors) so ONE readback serves both.
+__global__ void k_child_totals(const int64_t* __restrict__ cand_off, int64_t a0, int64_t a1,
+                               int64_t c0, const int64_t* __restrict__ pos, int64_t nc,
+                               unsigned long long* __restrict__ out) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long acc = 0;
+  for (int64_t a = a0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; a < a1; a += nthr) {
+    const int64_t k = pos[cand_off[a + 1] - c0] - pos[cand_off[a] - c0];
+    acc += (unsigned long long)(k * (k - 1) / 2);
   }
-  hipLaunchKernelGGL(k_flag_tail, dim3(1), dim3(64), 0, s, cnt, minsup, pos, n);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(&out[1], acc);
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&out[0], (unsigned long long)pos[nc]);
+}
+
+void child_totals(const int64_t* cand_off, int64_t a0, int64_t a1, int64_t c0, const int64_t* pos,
+                  int64_t nc, uint64_t* out2, hipStream_t s) {
+  KMLS_HIP(hipMemsetAsync(out2, 0, 2 * sizeof(uint64_t), s));
+  hipLaunchKernelGGL(k_child_totals, dim3(grid_for(std::max<int64_t>(a1 - a0, 1), kBlock, 1024)),
+                     dim3(kBlock), 0, s, cand_off, a0, a1, c0, pos, nc,
+                     (unsigned long long*)out2);
   KMLS_HIP(hipGetLastError());
 }
 

@@ -19,6 +19,23 @@ class NativeUnavailable(RuntimeError):
     pass
 
 
+def _bind_torch_runtime() -> None:
+    """Import torch (if installed) BEFORE the extension.
+
+    The ROCm torch wheel ships its own ``libamdhip64.so`` with the same SONAME
+    (``libamdhip64.so.7``) as /opt/rocm's.  Loading torch first makes the extension's
+    ``NEEDED libamdhip64.so.7`` resolve to the already-loaded runtime, so the process has ONE
+    HIP runtime and torch tensors / RCCL collectives and our kernels share devices and streams.
+    Loading ours first would leave torch with a second runtime that sees no GPU.
+    """
+    if os.environ.get("KMLS_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def load(build_if_missing: bool = True) -> ModuleType:
     global _mod
     if _mod is not None:
@@ -26,6 +43,7 @@ def load(build_if_missing: bool = True) -> ModuleType:
     with _lock:
         if _mod is not None:
             return _mod
+        _bind_torch_runtime()
         try:
             _mod = importlib.import_module("kubernetes_machine_learning_server_amd._native")
             return _mod
