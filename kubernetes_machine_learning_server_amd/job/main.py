@@ -1,0 +1,194 @@
+"""The ML job: one run = pick the next dataset, mine it, publish artifacts.
+
+Reference driver: ``machine-learning/main.py:421-484``.  Same sequence, same artifacts, same
+print lines, same exit code; the mining itself runs on the HIP miner (``MINER=gpu``), the
+native CPU miner (``cpu``) or the mlxtend-faithful oracle (``oracle``):
+
+  get_dataset_list → get_next_run_index → read_tracks/clean → total_songs →
+  artistsMapping.pickle (validate) → trackNameToRepeatedUris.pickle (if any) →
+  trackIdsToInfo.pickle → best_tracks.pickle → transactions → [experiment sweep] →
+  FP-Growth + rule map → recommendations.pickle (+ rules.idx, frequent_itemsets.npz) →
+  dataset_history.csv + last_execution.txt (marker LAST) → exit 0
+
+Multi-GPU: ``torchrun --nproc-per-node N -m kubernetes_machine_learning_server_amd.job`` with
+``NUM_GPUS=N`` mines with ``parallel.dist_miner`` (RCCL); rank 0 writes every artifact.
+Run: ``python -m kubernetes_machine_learning_server_amd.job``.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ..config import JobSettings
+from ..models.fpgrowth import ItemsetTrie, default_backend, mine_csr
+from ..serve.index import RuleIndexData, build_index_from_trie
+from ..utils.atomic_io import atomic_pickle, atomic_write_bytes
+from ..utils.timeutil import current_time_str, format_timedelta
+from . import preprocess as pp
+from . import rotation as rot
+
+PICKLE_ARTISTS_FILE = "artistsMapping.pickle"
+PICKLE_TRACK_ID_TO_TRACK_INFO = "trackIdsToInfo.pickle"
+PICKLE_DUPLICATED_TRACKS = "trackNameToRepeatedUris.pickle"
+RULES_INDEX_FILE = "rules.idx"
+ITEMSETS_FILE = "frequent_itemsets.npz"
+EXPERIMENT_CSV = "fp_growth_experiment_results.csv"
+
+
+def save_pickle(cfg: JobSettings, name: str, data) -> None:
+    full = cfg.pickles_folder / name
+    print("\tSaving pickle to", full)
+    atomic_pickle(full, data)
+
+
+def _fault(point: str) -> None:
+    """Fault injection for tests: KMLS_FAULT=<point> raises at that point."""
+    if os.environ.get("KMLS_FAULT") == point:
+        raise RuntimeError(f"injected fault at {point}")
+
+
+def mine_rules(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float,
+               total_songs: int, backend: Optional[str] = None, verbose: bool = True
+               ) -> Tuple[RuleIndexData, ItemsetTrie, str, Tuple[int, float]]:
+    """``calculate_and_save_fp_growth_fast`` (main.py:262-313): mine + rule map + timing."""
+    t0 = time.perf_counter()
+    backend = backend or (default_backend() if cfg.miner == "auto" else cfg.miner)
+    trie = mine_csr(tx.tx_ptr, tx.items, len(tx.names), min_support, backend=backend,
+                    pairs_only=(cfg.rules_mode == "pairs"), columns=tx.names)
+    idx = build_index_from_trie(trie.parent, trie.item, trie.count, trie.depth, tx.n_tx,
+                                len(tx.names), tx.names)
+    missing = total_songs - idx.n_keys
+    dur = time.perf_counter() - t0
+    if verbose:
+        print("Songs without recommendations:", missing)
+        print(f"Time elapsed in rule generation: {format_timedelta(dur)}")
+    info = f"min_support: {min_support} \tmissing songs: {missing} \ttime: {format_timedelta(dur)}"
+    return idx, trie, info, (missing, dur)
+
+
+def mine_rules_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float,
+                           total_songs: int) -> Optional[Tuple[RuleIndexData, ItemsetTrie, str, Tuple[int, float]]]:
+    """Multi-GPU mining (torchrun); returns the result on rank 0, None elsewhere."""
+    import torch.distributed as dist
+    from ..parallel.dist_miner import DistMiner, gather_trie
+    t0 = time.perf_counter()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dm = DistMiner(tx.tx_ptr, tx.items, len(tx.names), min_support, device=local,
+                   max_len=2 if cfg.rules_mode == "pairs" else 0)
+    r = dm.step(download=True)
+    F = int(r["stats"].get("n_frequent_items", 0))
+    merged = gather_trie(r["trie"], rank, world, F)
+    if rank != 0:
+        return None
+    trie = ItemsetTrie(merged["parent"], merged["item"], merged["count"], merged["depth"],
+                       tx.n_tx, min_support, dict(r["stats"]), tx.names)
+    idx = build_index_from_trie(trie.parent, trie.item, trie.count, trie.depth, tx.n_tx,
+                                len(tx.names), tx.names)
+    missing = total_songs - idx.n_keys
+    dur = time.perf_counter() - t0
+    print("Songs without recommendations:", missing)
+    print(f"Time elapsed in rule generation: {format_timedelta(dur)}")
+    info = f"min_support: {min_support} \tmissing songs: {missing} \ttime: {format_timedelta(dur)}"
+    return idx, trie, info, (missing, dur)
+
+
+def run_support_sweep(cfg: JobSettings, tx: pp.PlaylistTransactions, total_songs: int,
+                      supports: Optional[List[float]] = None, out_csv: str = EXPERIMENT_CSV):
+    """J14: the min_support sweep (main.py:450-473), written to ``fp_growth_experiment_results.csv``."""
+    import pandas as pd
+    supports = supports if supports is not None else np.arange(0.03, 0.2, 0.0025).tolist()
+    rows = []
+    for ms in supports:
+        ms = round(ms, 3)
+        print(f"Calculating for min_support: {ms}")
+        _, trie, _, (missing, dur) = mine_rules(cfg, tx, ms, total_songs)
+        rows.append({"min_support": ms, "songs_without_recommendations": missing,
+                     "duration": dur, "n_itemsets": len(trie)})
+        pd.DataFrame(rows).to_csv(out_csv, index=False)
+    return rows
+
+
+def save_itemsets(cfg: JobSettings, trie: ItemsetTrie) -> None:
+    import io
+    buf = io.BytesIO()
+    np.savez(buf, parent=trie.parent, item=trie.item, count=trie.count, depth=trie.depth,
+             n_tx=np.int64(trie.n_tx), min_support=np.float64(trie.min_support))
+    atomic_write_bytes(cfg.pickles_folder / ITEMSETS_FILE, buf.getvalue())
+
+
+def run(cfg: Optional[JobSettings] = None) -> Dict:
+    cfg = cfg or JobSettings.from_env()
+    distributed = cfg.num_gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) > 1
+    rank = 0
+    if distributed:
+        import torch
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        rank = dist.get_rank()
+    say = print if rank == 0 else (lambda *a, **k: None)
+    say("=== Starting execution on ", current_time_str(), " ===")
+    datasets = rot.get_dataset_list(cfg) if rank == 0 else None
+    if distributed:
+        import torch.distributed as dist
+        box = [datasets]
+        dist.broadcast_object_list(box, src=0)
+        datasets = box[0]
+    new_index = rot.get_next_run_index(cfg, datasets)
+    selected = datasets[new_index - 1]
+    say(f"Selected dataset: {selected}")
+    t = pp.clean_df(pp.read_tracks(selected, cfg.sample_ratio, verbose=rank == 0))
+    total_songs = t.n_unique("track_uri")
+    if rank == 0:
+        save_pickle(cfg, PICKLE_ARTISTS_FILE, pp.validate_and_map_artists_names_to_ids(t))
+        dups = pp.extract_repeated_track_names(t)
+        if dups:
+            print(f"\tFound {len(dups)} duplicate songs, saving to {PICKLE_DUPLICATED_TRACKS}")
+            save_pickle(cfg, PICKLE_DUPLICATED_TRACKS, dups)
+        save_pickle(cfg, PICKLE_TRACK_ID_TO_TRACK_INFO, pp.map_song_ids_to_song_info(t))
+        best = pp.filter_best_tracks(pp.get_most_frequent_tracks(t), cfg.top_tracks_save_percentile)
+        save_pickle(cfg, cfg.best_tracks_file, best)
+    else:
+        pp.validate_and_map_artists_names_to_ids(t)  # every rank fails the same way
+    _fault("after_best_tracks")
+    tx = pp.group_tracks_by_playlist(t)
+    if cfg.experiment_supports and rank == 0:
+        run_support_sweep(cfg, tx, total_songs)
+    if distributed:
+        res = mine_rules_distributed(cfg, tx, cfg.min_support, total_songs)
+    else:
+        res = mine_rules(cfg, tx, cfg.min_support, total_songs)
+    summary: Dict = {}
+    if rank == 0:
+        idx, trie, info, (missing, dur) = res
+        _fault("before_recommendations")
+        save_pickle(cfg, cfg.recommendations_file, idx.to_rec_dict())
+        idx.save(cfg.pickles_folder / RULES_INDEX_FILE)
+        if cfg.rules_mode == "full":
+            save_itemsets(cfg, trie)
+        _fault("before_marker")
+        ts = rot.append_dataset_history(cfg, new_index, selected)
+        summary = {"dataset_index": new_index, "dataset": selected, "marker": ts,
+                   "n_keys": idx.n_keys, "songs_without_recommendations": missing,
+                   "n_itemsets": len(trie), "rule_seconds": dur, "backend": trie.stats.get("backend")}
+        print("=== Run complete. Exiting, current time is ", current_time_str(), " ===")
+    if distributed:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+    return summary
+
+
+def main() -> int:
+    run()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

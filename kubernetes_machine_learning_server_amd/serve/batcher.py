@@ -1,0 +1,102 @@
+"""Async request micro-batcher feeding the HIP matcher (SURVEY §2.E "intra-process concurrency").
+
+Requests arriving within ``BATCH_WAIT_US`` (or until ``BATCH_MAX``) are concatenated into one
+CSR query batch; one ``serve_match_topk`` launch answers all of them (one workgroup per query)
+and the futures are resolved on the event loop.  Batches smaller than ``GPU_MIN_BATCH`` go to
+the C++ CPU matcher instead: for a handful of queries the ~20-40 µs H2D+launch+D2H round trip
+costs more than the CPU merge.  The device work runs in a worker thread (the native call
+releases the GIL), so the event loop keeps accepting requests while a batch is in flight.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+
+class MicroBatcher:
+    def __init__(self, max_batch: int = 256, max_wait_us: int = 200, gpu_min_batch: int = 16):
+        self.max_batch = max(1, int(max_batch))
+        self.max_wait = max(0, int(max_wait_us)) / 1e6
+        self.gpu_min_batch = int(gpu_min_batch)
+        self._q: Optional[asyncio.Queue] = None
+        self._task: Optional[asyncio.Task] = None
+        self.batches = 0
+        self.gpu_batches = 0
+        self.queries = 0
+        self.last_batch = 0
+
+    def start(self) -> None:
+        if self._task is None:
+            self._q = asyncio.Queue()
+            self._task = asyncio.get_running_loop().create_task(self._run())
+
+    async def stop(self) -> None:
+        if self._task is not None:
+            self._task.cancel()
+            try:
+                await self._task
+            except (asyncio.CancelledError, Exception):
+                pass
+            self._task = None
+
+    async def submit(self, snap, ids: np.ndarray, k: int) -> Tuple[np.ndarray, int]:
+        """Returns (ids[k], n) for one query; n == -1 → no seed is a key."""
+        fut = asyncio.get_running_loop().create_future()
+        await self._q.put((snap, ids, k, fut))
+        return await fut
+
+    async def _run(self) -> None:
+        loop = asyncio.get_running_loop()
+        while True:
+            first = await self._q.get()
+            items = [first]
+            deadline = time.perf_counter() + self.max_wait
+            while len(items) < self.max_batch:
+                try:
+                    items.append(self._q.get_nowait())
+                    continue
+                except asyncio.QueueEmpty:
+                    pass
+                rem = deadline - time.perf_counter()
+                if rem <= 0:
+                    break
+                try:
+                    items.append(await asyncio.wait_for(self._q.get(), rem))
+                except asyncio.TimeoutError:
+                    break
+            # group by (snapshot, k): a reload between requests must not mix indices
+            groups = {}
+            for it in items:
+                groups.setdefault((id(it[0]), it[2]), []).append(it)
+            for (_, k), grp in groups.items():
+                snap = grp[0][0]
+                try:
+                    ids, n = await loop.run_in_executor(None, self._run_batch, snap, grp, k)
+                    for j, it in enumerate(grp):
+                        if not it[3].done():
+                            it[3].set_result((ids[j], int(n[j])))
+                except Exception as e:  # pragma: no cover - surfaced to the requests
+                    for it in grp:
+                        if not it[3].done():
+                            it[3].set_exception(e)
+
+    def _run_batch(self, snap, grp: List, k: int):
+        lens = [len(it[1]) for it in grp]
+        q_ptr = np.zeros(len(grp) + 1, np.int64)
+        np.cumsum(lens, out=q_ptr[1:])
+        seeds = np.concatenate([it[1] for it in grp]) if grp else np.zeros(0, np.int32)
+        self.batches += 1
+        self.queries += len(grp)
+        self.last_batch = len(grp)
+        if snap.gpu_index is not None and len(grp) >= self.gpu_min_batch:
+            self.gpu_batches += 1
+            ids, n = snap.gpu_index.query_batch(q_ptr, seeds.astype(np.int32), k)
+            if (n == -2).any():  # kernel table overflow: answer those on the CPU
+                cids, cn = snap.index.native().query_batch(q_ptr, seeds.astype(np.int32), k)
+                m = n == -2
+                ids[m], n[m] = cids[m], cn[m]
+            return ids, n
+        return snap.index.native().query_batch(q_ptr, seeds.astype(np.int32), k)

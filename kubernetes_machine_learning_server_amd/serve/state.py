@@ -1,0 +1,150 @@
+"""Model state and hot reload (reference ``rest_api/app/main.py:52-122``).
+
+Protocol kept: poll the marker ``last_execution.txt`` every ``POLLING_WAIT_IN_MINUTES``;
+reload when it changed or when nothing is loaded yet; ``model_date`` = marker contents; the
+same log lines (they are the reference's reload test oracle, ``relatorio.pdf`` p.7).
+
+Fixes: the loaded model is ONE immutable snapshot object
+swapped by a single reference assignment (no torn best_tracks/recommendations pair), the marker
+value is committed only after a successful load (a failed reload is retried on the next tick
+instead of being forgotten), and a missing artifact at boot does not crash the process — the
+server stays up, reports not-ready, and keeps polling.
+"""
+from __future__ import annotations
+
+import dataclasses
+import logging
+import pathlib
+import pickle
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from ..config import ApiSettings
+from .index import RuleIndexData
+
+logger = logging.getLogger("kmls.api")
+
+RULES_INDEX_FILE = "rules.idx"
+
+
+@dataclasses.dataclass(frozen=True)
+class ModelSnapshot:
+    best_tracks: List[Dict[str, Any]]
+    index: RuleIndexData
+    marker: Optional[str]
+    loaded_at: float
+    n_recommendations: int
+    source: str  # "rules.idx" | "pickle"
+    gpu_index: Any = None  # _native.GpuRuleIndex when SERVE_BACKEND uses the GPU
+
+    @property
+    def best_track_names(self) -> List[str]:
+        return [t["track_name"] for t in self.best_tracks]
+
+
+def read_pickle_dict(cfg: ApiSettings, prefer_index: bool = True):
+    """Load best tracks + recommendations (``read_pickle_dict``, main.py:52-80).
+
+    ``best_tracks.pickle`` is required (``ValueError`` otherwise, as the reference).  The rules
+    come from ``rules.idx`` (binary CSR written by our job, no unpickling) when it is at least as
+    new as ``recommendations.pickle``; otherwise from the pickle (any reference-format dict,
+    e.g. one written by the reference job), indexed preserving its inner order.
+    """
+    cfg.base_dir.mkdir(parents=True, exist_ok=True)
+    cfg.pickles_folder.mkdir(parents=True, exist_ok=True)
+    best_path = cfg.pickles_folder / cfg.best_tracks_file
+    if not best_path.exists():
+        logger.error(f"Best tracks file not found at {best_path}")
+        raise ValueError(f"Best tracks file not found at {best_path}")
+    with open(best_path, "rb") as f:
+        best_tracks = pickle.load(f)
+    logger.info(f"Best tracks loaded: {len(best_tracks)}")
+    rec_path = cfg.pickles_folder / cfg.recommendations_file
+    idx_path = cfg.pickles_folder / RULES_INDEX_FILE
+    use_idx = (prefer_index and idx_path.exists() and
+               (not rec_path.exists() or idx_path.stat().st_mtime >= rec_path.stat().st_mtime))
+    if use_idx:
+        index = RuleIndexData.load(idx_path)
+        source = "rules.idx"
+    else:
+        with open(rec_path, "rb") as f:
+            rec = pickle.load(f)
+        index = RuleIndexData.from_rec_dict(rec)
+        source = "pickle"
+    logger.info(f"Recommendations loaded: {index.n_keys}")
+    return best_tracks, index, source
+
+
+class ReloadManager:
+    """Owns the current snapshot; thread-safe reload with single-assignment swap."""
+
+    def __init__(self, cfg: ApiSettings, gpu_factory=None):
+        self.cfg = cfg
+        self.snapshot: Optional[ModelSnapshot] = None
+        self.reload_counter = 0
+        self.failed_reloads = 0
+        self.last_error: Optional[str] = None
+        self._lock = threading.Lock()
+        self._gpu_factory = gpu_factory
+        self.last_reload_seconds = 0.0
+
+    # -- reference-compatible accessors -------------------------------------------------
+    @property
+    def finished_loading(self) -> bool:
+        return self.snapshot is not None
+
+    @property
+    def cache_value(self) -> Optional[str]:
+        s = self.snapshot
+        return s.marker if s is not None else None
+
+    def read_marker(self) -> Optional[str]:
+        p = self.cfg.cache_file
+        if not p.exists():
+            return None
+        with open(p, "r") as f:
+            return f.read()
+
+    def is_data_stale(self) -> bool:
+        marker = self.read_marker()
+        if marker is None:
+            logger.info("Cache file does not exist")
+            return True
+        current = self.cache_value
+        if current != marker:
+            logger.info(f"Data is stale, current value is {current} and last value was {marker}")
+            return True
+        return False
+
+    def reload_data_if_required(self) -> bool:
+        with self._lock:
+            if not self.is_data_stale() and self.finished_loading:
+                logger.info("data is not stale, no need to reload")
+                return False
+            return self._perform_reload()
+
+    def _perform_reload(self) -> bool:
+        logger.info("Reloading data!")
+        t0 = time.perf_counter()
+        marker = self.read_marker()
+        try:
+            best, index, source = read_pickle_dict(self.cfg)
+            gpu_index = self._gpu_factory(index) if self._gpu_factory else None
+        except Exception as e:  # keep serving the previous snapshot; retry next tick
+            self.failed_reloads += 1
+            self.last_error = f"{type(e).__name__}: {e}"
+            logger.error(f"Reload failed ({self.last_error}); keeping the previous model")
+            return False
+        # the marker may have moved while we were reading: re-read, and only commit the value
+        # we read BEFORE loading (a later change triggers another reload next tick)
+        snap = ModelSnapshot(best, index, marker, time.time(), index.n_keys, source, gpu_index)
+        self.snapshot = snap  # single reference assignment = atomic swap
+        self.reload_counter += 1
+        self.last_error = None
+        self.last_reload_seconds = time.perf_counter() - t0
+        logger.info("Finished reloading, should reflect changes. "
+                    f"Data was reloaded {self.reload_counter} times")
+        return True

@@ -30,7 +30,9 @@ def _fsync_dir(d: pathlib.Path) -> None:
         os.close(fd)
 
 
-def atomic_write_bytes(path: PathLike, data: bytes) -> None:
+def atomic_write_bytes(path: PathLike, data: bytes, mode: int = 0o644) -> None:
+    """Write-to-temp + fsync + rename.  ``mode`` is applied before the rename (mkstemp creates
+    0600 files, which other pods' UIDs could not read on a shared RWX volume)."""
     p = pathlib.Path(path)
     p.parent.mkdir(parents=True, exist_ok=True)
     fd, tmp = tempfile.mkstemp(prefix=f".{p.name}.", suffix=".tmp", dir=str(p.parent))
@@ -39,6 +41,7 @@ def atomic_write_bytes(path: PathLike, data: bytes) -> None:
             f.write(data)
             f.flush()
             os.fsync(f.fileno())
+        os.chmod(tmp, mode)
         os.replace(tmp, p)
     except BaseException:
         try:

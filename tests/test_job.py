@@ -1,0 +1,176 @@
+"""Job pipeline tests (SURVEY §7.6 unit + artifact contract §2.F, failure handling §5.3)."""
+import pickle
+
+import numpy as np
+import pytest
+
+from kubernetes_machine_learning_server_amd.job import main as job
+from kubernetes_machine_learning_server_amd.job import preprocess as pp
+from kubernetes_machine_learning_server_amd.job import rotation as rot
+from kubernetes_machine_learning_server_amd.models import oracle
+from kubernetes_machine_learning_server_amd.serve.index import RuleIndexData
+from tests.helpers import job_settings, make_datasets
+
+
+@pytest.fixture()
+def pvc(tmp_path):
+    make_datasets(tmp_path)
+    return tmp_path
+
+
+def load(p):
+    with open(p, "rb") as f:
+        return pickle.load(f)
+
+
+def test_job_artifacts_and_rotation(pvc, capsys):
+    cfg = job_settings(pvc)
+    s1 = job.run(cfg)
+    assert s1["dataset_index"] == 1
+    pk = cfg.pickles_folder
+    rec = load(pk / "recommendations.pickle")
+    best = load(pk / "best_tracks.pickle")
+    artists = load(pk / "artistsMapping.pickle")
+    info = load(pk / "trackIdsToInfo.pickle")
+    assert isinstance(rec, dict) and all(isinstance(v, dict) for v in rec.values())
+    assert all(isinstance(x, float) for row in rec.values() for x in row.values())
+    assert isinstance(best, list) and set(best[0]) == {"track_name", "count"}
+    assert [b["count"] for b in best] == sorted([b["count"] for b in best], reverse=True)
+    assert all(isinstance(v, str) for v in artists.values())
+    assert set(next(iter(info.values()))) == {"track_name", "artist_name", "album_name"}
+    marker = (cfg.base_dir / "last_execution.txt").read_text()
+    assert len(marker) == 19 and marker[4] == "-" and marker[13] == ":"
+    hist = (cfg.base_dir / "dataset_history.csv").read_text().splitlines()
+    assert hist[0] == "time,dataset_index,dataset_file" and hist[1].split(",")[1] == "1"
+    lst = (cfg.base_dir / "datasets_list.txt").read_text().splitlines()
+    assert lst == sorted(lst) and len(lst) == 2
+    # second run → dataset 2, third wraps to 1
+    assert job.run(cfg)["dataset_index"] == 2
+    assert job.run(cfg)["dataset_index"] == 1
+    out = capsys.readouterr().out
+    assert "Songs without recommendations:" in out and "Time elapsed in rule generation:" in out
+
+
+def test_rule_map_matches_oracle(pvc):
+    """recommendations.pickle == the reference rule loop over mlxtend-faithful itemsets."""
+    cfg = job_settings(pvc, min_support=0.05)
+    job.run(cfg)
+    rec = load(cfg.pickles_folder / "recommendations.pickle")
+    t = pp.clean_df(pp.read_tracks(str(pvc / "datasets" / "2023_spotify_ds1.csv"), verbose=False))
+    txl = pp.group_tracks_by_playlist(t).as_lists()
+    X, cols = oracle.transaction_encode(txl)
+    ref = oracle.rule_map_from_itemsets(oracle.fpgrowth_oracle(X, 0.05, cols))
+    assert set(rec) == set(ref)
+    for k in ref:
+        assert rec[k] == ref[k]
+    # rules.idx round-trips to the same dict
+    idx = RuleIndexData.load(cfg.pickles_folder / "rules.idx")
+    assert idx.to_rec_dict() == rec
+
+
+@pytest.mark.parametrize("mode", ["pairs", "full"])
+def test_rules_modes_identical(pvc, mode):
+    cfg = job_settings(pvc, rules_mode=mode)
+    job.run(cfg)
+    rec = load(cfg.pickles_folder / "recommendations.pickle")
+    cfg2 = job_settings(pvc, miner="oracle")
+    cfg2.base_dir = pvc / "api-oracle"
+    cfg2.pickles_folder = cfg2.base_dir / "pickles"
+    job.run(cfg2)
+    assert rec == load(cfg2.pickles_folder / "recommendations.pickle")
+
+
+def test_history_malformed_and_wrap(pvc):
+    cfg = job_settings(pvc)
+    cfg.base_dir.mkdir(parents=True)
+    ds = ["a.csv", "b.csv", "c.csv"]
+    assert rot.get_next_run_index(cfg, ds) == 1
+    cfg.dataset_history_file.write_text("time,dataset_index,dataset_file\n2025,3,c.csv\n")
+    assert rot.get_next_run_index(cfg, ds) == 1  # wrap
+    cfg.dataset_history_file.write_text("time,dataset_index,dataset_file\n2025,2,b.csv\n")
+    assert rot.get_next_run_index(cfg, ds) == 3
+    cfg.dataset_history_file.write_text("time,dataset_index,dataset_file\ngarbage\n")
+    assert rot.get_next_run_index(cfg, ds) == 1
+
+
+def test_no_datasets_raises(tmp_path):
+    cfg = job_settings(tmp_path)
+    with pytest.raises(FileNotFoundError):
+        rot.get_dataset_list(cfg)
+
+
+def test_artist_validation_raises(tmp_path):
+    ds = tmp_path / "datasets"
+    ds.mkdir()
+    (ds / "2023_spotify_ds1.csv").write_text(
+        "pid,track_uri,track_name,artist_name,artist_uri,album_name,album_uri,duration_ms\n"
+        "0,u1,Song A,Artist X,ax1,Al,al,1\n0,u2,Song B,Artist X,ax2,Al,al,1\n")
+    cfg = job_settings(tmp_path)
+    with pytest.raises(ValueError, match="duplicate artists"):
+        job.run(cfg)
+
+
+def test_duplicates_pickle_only_when_present(tmp_path):
+    ds = tmp_path / "datasets"
+    ds.mkdir()
+    (ds / "2023_spotify_ds1.csv").write_text(
+        "pid,track_uri,track_name,artist_name,artist_uri,album_name,album_uri,duration_ms\n"
+        "0,u1,Song A,X,x,Al,al,1\n0,u2,Song B,X,x,Al,al,1\n1,u1,Song A,X,x,Al,al,1\n"
+        "1,u2,Song B,X,x,Al,al,1\n")
+    cfg = job_settings(tmp_path, pct=1.0, min_support=0.5)
+    job.run(cfg)
+    assert not (cfg.pickles_folder / "trackNameToRepeatedUris.pickle").exists()
+    rec = load(cfg.pickles_folder / "recommendations.pickle")
+    assert rec == {"Song A": {"Song B": 1.0}, "Song B": {"Song A": 1.0}}
+    # a name with two URIs (the encoder collapses them inside a playlist)
+    (ds / "2023_spotify_ds1.csv").write_text(
+        "pid,track_uri,track_name,artist_name,artist_uri,album_name,album_uri,duration_ms\n"
+        "0,u1,Song A,X,x,Al,al,1\n0,u3,Song A,X,x,Al,al,1\n0,u2,Song B,X,x,Al,al,1\n")
+    cfg2 = job_settings(tmp_path, pct=1.0, min_support=0.5)
+    cfg2.base_dir = tmp_path / "api2"
+    cfg2.pickles_folder = cfg2.base_dir / "pickles"
+    job.run(cfg2)
+    dups = load(cfg2.pickles_folder / "trackNameToRepeatedUris.pickle")
+    assert dups == {"Song A": ["u1", "u3"]}
+
+
+def test_marker_written_last_under_fault(pvc, monkeypatch):
+    cfg = job_settings(pvc)
+    job.run(cfg)
+    marker = (cfg.base_dir / "last_execution.txt").read_text()
+    rec_before = (cfg.pickles_folder / "recommendations.pickle").read_bytes()
+    monkeypatch.setenv("KMLS_FAULT", "before_recommendations")
+    with pytest.raises(RuntimeError):
+        job.run(cfg)
+    # no marker change, old artifacts intact (atomic writes)
+    assert (cfg.base_dir / "last_execution.txt").read_text() == marker
+    assert (cfg.pickles_folder / "recommendations.pickle").read_bytes() == rec_before
+    monkeypatch.setenv("KMLS_FAULT", "before_marker")
+    with pytest.raises(RuntimeError):
+        job.run(cfg)
+    assert (cfg.base_dir / "last_execution.txt").read_text() == marker
+
+
+def test_support_sweep(pvc, tmp_path):
+    cfg = job_settings(pvc)
+    t = pp.clean_df(pp.read_tracks(str(pvc / "datasets" / "2023_spotify_ds1.csv"), verbose=False))
+    tx = pp.group_tracks_by_playlist(t)
+    out = tmp_path / "sweep.csv"
+    rows = job.run_support_sweep(cfg, tx, t.n_unique("track_uri"), [0.2, 0.1, 0.05], str(out))
+    missing = [r["songs_without_recommendations"] for r in rows]
+    assert missing == sorted(missing, reverse=True)  # lower support → more keys
+    import pandas as pd
+    df = pd.read_csv(out)
+    assert list(df.columns[:3]) == ["min_support", "songs_without_recommendations", "duration"]
+
+
+def test_csv_reader_quotes(tmp_path):
+    p = tmp_path / "q.csv"
+    p.write_text('pid,track_uri,track_name,artist_name,artist_uri,album_name,album_uri,duration_ms\r\n'
+                 '7,"u,1","City Of Stars - From ""La La Land""","A, B",a,"Al",x,3\r\n'
+                 '7,u2,Plain,"A, B",a,Al,x,4\r\n')
+    t = pp.read_tracks(str(p), verbose=False)
+    assert t.n_rows == 2 and t.width == 8
+    assert t.uniques["track_name"] == ['City Of Stars - From "La La Land"', "Plain"]
+    assert t.uniques["track_uri"] == ["u,1", "u2"]
+    assert t.uniques["artist_name"] == ["A, B"]
