@@ -80,7 +80,7 @@ def main() -> int:
             st = dm.step(download=True)["stats"]
             return st
 
-        sync = dm.g.synchronize
+        sync = dm.synchronize
         dtype = "uint64-bitmap/int32-count"
 
     st = None

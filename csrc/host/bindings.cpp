@@ -96,6 +96,52 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("tx_ptr"), py::arg("items"), py::arg("n_items"), py::arg("min_support"),
      py::arg("max_len") = 0, py::arg("threads") = 0, py::arg("pairs_only") = false);
 
+  m.def("select_frequent", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> counts,
+                              int64_t n_tx, double ms) {
+    FrequentItems f = select_frequent(counts.data(), counts.size(), (uint64_t)n_tx, ms);
+    return py::make_tuple(to_array(std::move(f.ids)), to_array(std::move(f.counts)),
+                          to_array(std::move(f.rank_of)), f.minsup2);
+  });
+  m.def("encode_bitmaps_cpu", [](I64 tx_ptr, I32 items, I32 rank_of, int64_t F, int64_t W) {
+    py::array_t<uint64_t> bm({(py::ssize_t)F, (py::ssize_t)W});
+    uint64_t* p = bm.mutable_data();
+    {
+      py::gil_scoped_release nogil;
+      std::fill(p, p + F * W, 0ull);
+      encode_bitmaps_cpu(tx_ptr.data(), items.data(), tx_ptr.size() - 1, rank_of.data(), p, W);
+    }
+    return bm;
+  });
+  m.def("mine_cpu_bitmaps", [](py::array_t<uint64_t, py::array::c_style | py::array::forcecast> bm,
+                               I32 ids, py::array_t<uint32_t, py::array::c_style | py::array::forcecast> counts,
+                               uint32_t minsup, int max_len, py::object owned, int threads) {
+    KMLS_CHECK(bm.ndim() == 2 && bm.shape(0) == ids.size(), "bm must be [F][W]");
+    FrequentItems fi;
+    fi.ids.assign(ids.data(), ids.data() + ids.size());
+    fi.counts.assign(counts.data(), counts.data() + counts.size());
+    fi.minsup2 = minsup;
+    std::vector<uint8_t> own;
+    if (!owned.is_none()) {
+      U8 o = owned.cast<U8>();
+      own.assign(o.data(), o.data() + o.size());
+      KMLS_CHECK(own.size() == fi.ids.size(), "owned mask size != F");
+    }
+    MineStats st;
+    ItemsetTrie t;
+    {
+      py::gil_scoped_release nogil;
+      t = mine_cpu_bitmaps(bm.data(), bm.shape(0), bm.shape(1), fi, max_len, threads,
+                           own.empty() ? nullptr : own.data(), &st);
+    }
+    py::dict d = trie_to_dict(std::move(t));
+    py::dict s;
+    s["n_frequent_items"] = st.n_frequent_items; s["n_itemsets"] = st.n_itemsets;
+    s["n_candidates"] = st.n_candidates; s["max_depth"] = st.max_depth; s["seconds"] = st.seconds;
+    d["stats"] = s;
+    return d;
+  }, py::arg("bm"), py::arg("ids"), py::arg("counts"), py::arg("minsup"), py::arg("max_len") = 0,
+     py::arg("owned") = py::none(), py::arg("threads") = 0);
+
   // ---------------- CPU matcher ----------------
   py::class_<RuleIndex, std::shared_ptr<RuleIndex>>(m, "RuleIndex")
       .def(py::init([](int64_t n_items, I64 row_ptr, I32 cons, F64 score, U8 is_key) {

@@ -125,29 +125,15 @@ void expand_member(const Ctx& cx, const std::vector<Member>& cls, size_t i, int 
 
 }  // namespace
 
-ItemsetTrie mine_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, int64_t n_items,
-                     const MineConfig& cfg, MineStats* stats) {
+ItemsetTrie mine_cpu_bitmaps(const uint64_t* bm, int64_t F, int64_t W, const FrequentItems& fi,
+                             int max_len, int threads, const uint8_t* owned, MineStats* stats) {
   auto t0 = std::chrono::steady_clock::now();
-  std::vector<uint32_t> cnt((size_t)n_items);
-  count_items(tx_ptr, items, n_tx, n_items, cnt.data());
-  FrequentItems fi = select_frequent(cnt.data(), n_items, (uint64_t)n_tx, cfg.min_support);
-  const int64_t F = (int64_t)fi.ids.size();
-  const int64_t W = (n_tx + 63) / 64;
-  // item-major bitmaps of frequent items
-  std::vector<uint64_t> bm((size_t)(F * W), 0);
-  for (int64_t t = 0; t < n_tx; ++t) {
-    for (int64_t p = tx_ptr[t]; p < tx_ptr[t + 1]; ++p) {
-      int32_t r = fi.rank_of[items[p]];
-      if (r >= 0) bm[(size_t)r * W + (t >> 6)] |= (1ull << (t & 63));
-    }
-  }
   ItemsetTrie out;
   for (int64_t r = 0; r < F; ++r) out.push(-1, fi.ids[r], fi.counts[r], 1);
-  const int max_len = cfg.pairs_only ? 2 : cfg.max_len;
   std::vector<Task> tasks((size_t)std::max<int64_t>(F, 0));
   if (F >= 2 && max_len != 1) {
-    Ctx cx{&fi, bm.data(), W, fi.minsup2, max_len};
-    int nth = cfg.threads > 0 ? cfg.threads : (int)std::thread::hardware_concurrency();
+    Ctx cx{&fi, bm, W, fi.minsup2, max_len};
+    int nth = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
     nth = std::max(1, std::min<int>(nth, (int)F));
     std::atomic<int64_t> next{0};
     std::vector<Member> root((size_t)F);
@@ -157,6 +143,7 @@ ItemsetTrie mine_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, 
       while (true) {
         int64_t i = next.fetch_add(1);
         if (i >= F - 1) break;
+        if (owned && !owned[i]) continue;  // item-sharded: another rank expands this class
         expand_member(cx, root, (size_t)i, 1, arena, 0, tasks[(size_t)i]);
       }
     };
@@ -187,6 +174,32 @@ ItemsetTrie mine_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, 
     stats->max_depth = maxd;
     stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
+  return out;
+}
+
+void encode_bitmaps_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
+                        const int32_t* rank_of, uint64_t* bm, int64_t W) {
+  for (int64_t t = 0; t < n_tx; ++t)
+    for (int64_t p = tx_ptr[t]; p < tx_ptr[t + 1]; ++p) {
+      const int32_t r = rank_of[items[p]];
+      if (r >= 0) bm[(size_t)r * W + (t >> 6)] |= (1ull << (t & 63));
+    }
+}
+
+ItemsetTrie mine_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, int64_t n_items,
+                     const MineConfig& cfg, MineStats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint32_t> cnt((size_t)n_items);
+  count_items(tx_ptr, items, n_tx, n_items, cnt.data());
+  FrequentItems fi = select_frequent(cnt.data(), n_items, (uint64_t)n_tx, cfg.min_support);
+  const int64_t F = (int64_t)fi.ids.size();
+  const int64_t W = (n_tx + 63) / 64;
+  std::vector<uint64_t> bm((size_t)(F * W), 0);
+  encode_bitmaps_cpu(tx_ptr, items, n_tx, fi.rank_of.data(), bm.data(), W);
+  const int max_len = cfg.pairs_only ? 2 : cfg.max_len;
+  ItemsetTrie out = mine_cpu_bitmaps(bm.data(), F, W, fi, max_len, cfg.threads, nullptr, stats);
+  if (stats)
+    stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return out;
 }
 

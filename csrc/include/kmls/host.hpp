@@ -41,6 +41,13 @@ struct MineStats {
 ItemsetTrie mine_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, int64_t n_items,
                      const MineConfig& cfg, MineStats* stats);
 
+// Same search from prebuilt item-major bitmaps [F][W] (the multi-rank protocol's replicated
+// bitmaps); `owned` (size F, optional) restricts the root classes expanded by this rank.
+ItemsetTrie mine_cpu_bitmaps(const uint64_t* bm, int64_t F, int64_t W, const FrequentItems& fi,
+                             int max_len, int threads, const uint8_t* owned, MineStats* stats);
+void encode_bitmaps_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
+                        const int32_t* rank_of, uint64_t* bm, int64_t W);
+
 // Pair supports among frequent items (rule-map fast path).
 struct PairTable {
   std::vector<int32_t> a, b;     // item ids, a has lower Eclat rank than b

@@ -49,34 +49,150 @@ def shard_bounds(n_tx: int, world: int, rank: int, align: int = 256) -> Tuple[in
 
 
 def lpt_partition(cost: np.ndarray, world: int) -> np.ndarray:
-    """Longest-processing-time-first assignment of root classes to ranks (deterministic)."""
-    owner = np.zeros(len(cost), dtype=np.int32)
-    if world <= 1:
+    """Balanced, deterministic assignment of root classes to ranks.
+
+    Classes are sorted by estimated cost (desc) and dealt in snake order (0..N-1, N-1..0, ...):
+    an O(F log F) vectorised stand-in for LPT that keeps the per-step host cost in the tens of
+    microseconds (an interpreted LPT loop costs ~1 ms at F≈800).  Identical on every rank.
+    """
+    F = len(cost)
+    owner = np.zeros(F, dtype=np.int32)
+    if world <= 1 or F == 0:
         return owner
-    order = np.argsort(-cost, kind="stable")
-    load = np.zeros(world, dtype=np.float64)
-    for a in order:
-        r = int(np.argmin(load))
-        owner[a] = r
-        load[r] += float(cost[a])
+    order = np.argsort(-np.asarray(cost, dtype=np.float64), kind="stable")
+    k = np.arange(F)
+    rnd, pos = k // world, k % world
+    owner[order] = np.where(rnd % 2 == 0, pos, world - 1 - pos).astype(np.int32)
     return owner
 
 
-def root_costs(gram: np.ndarray, minsup: int) -> np.ndarray:
-    """Estimated subtree cost of each root class from level-2 counts: n_a^2 + 1 where n_a is the
-    number of frequent extensions of item a (its level-3 candidate count ~ n_a^2 / 2)."""
-    F = gram.shape[0]
-    upper = np.triu(gram >= minsup, k=1)
+def root_costs(gram, minsup: int) -> np.ndarray:
+    """Estimated subtree cost of each root class from level-2 counts: n_a^2 + 1, n_a = number
+    of frequent extensions of item a (its level-3 candidates ~ n_a^2 / 2).  Accepts a torch
+    tensor (reduced on its device; only F values cross to the host) or a numpy array."""
+    if torch is not None and isinstance(gram, torch.Tensor):
+        F = gram.shape[0]
+        m = (gram.to(torch.int64) & 0xFFFFFFFF) >= minsup
+        n = torch.triu(m, diagonal=1).sum(dim=1).to(torch.float64)
+        return (n * n + 1.0).cpu().numpy()
+    upper = np.triu(np.asarray(gram) >= minsup, k=1)
     n = upper.sum(axis=1).astype(np.float64)
     return n * n + 1.0
 
 
+class _GpuOps:
+    """Device ops of the protocol on one MI355X (HIP kernels; tensors in HBM; RCCL)."""
+
+    def __init__(self, dm: "DistMiner", tx_ptr, items, arena_bytes: int):
+        N = native.require_gpu()
+        self.dev = torch.device("cuda", dm.device)
+        if dm.world > 1:
+            torch.cuda.set_device(dm.device)
+            self.stream = torch.cuda.Stream(device=dm.device)
+            self.g = N.GpuMiner(dm.device, arena_bytes, self.stream.cuda_stream)
+        else:
+            self.stream = None
+            self.g = N.GpuMiner(dm.device, arena_bytes, 0)
+        self.g.load_csr(tx_ptr, items, dm.n_items)
+        self.n_items = dm.n_items
+
+    def ctx(self):
+        return torch.cuda.stream(self.stream)
+
+    def supports(self):
+        c = torch.empty(self.n_items, dtype=torch.int32, device=self.dev)
+        self.g.item_support(c.data_ptr())
+        return c
+
+    def select(self, host_counts: np.ndarray, n_tx: int, ms: float):
+        F = self.g.select(host_counts, n_tx, ms)
+        ids, counts, minsup = self.g.frequent()
+        return F, ids, counts, int(minsup)
+
+    def encode(self, F: int, ws: int):
+        local = torch.zeros((F, ws), dtype=torch.int64, device=self.dev)
+        self.g.encode_bitmaps(local.data_ptr(), ws, 0)
+        return local
+
+    def all_gather(self, local, world: int):
+        out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, local)
+        return out
+
+    def gram(self, bm, wp: int, mfma: bool):
+        F = bm.shape[0]
+        gram = torch.empty((F, F), dtype=torch.int32, device=self.dev)
+        self.g.pair_counts(bm.data_ptr(), wp, gram.data_ptr(), mfma)
+        return gram  # stays in HBM; root_costs reduces it on the device
+
+    def mine(self, bm, wp, dm: "DistMiner", owned, emit_level1: bool, download: bool):
+        if self.stream is not None:
+            self.stream.synchronize()
+        return self.g.mine_bitmaps(bm.data_ptr(), wp, dm.min_support, dm.max_len, False, owned,
+                                   emit_level1, download, True, dm.mfma)
+
+    def synchronize(self):
+        self.g.synchronize()
+
+
+class _CpuOps:
+    """The same protocol on the host (C++ kernels; gloo collectives) — CPU multi-rank tests."""
+
+    def __init__(self, dm: "DistMiner", tx_ptr, items, arena_bytes: int):
+        self.N = native.load()
+        self.tx_ptr, self.items = tx_ptr, items
+        self.n_items = dm.n_items
+        self.rank_of = None
+
+    def ctx(self):
+        import contextlib
+        return contextlib.nullcontext()
+
+    def supports(self):
+        c = np.bincount(self.items, minlength=self.n_items).astype(np.int32)
+        return torch.from_numpy(c)
+
+    def select(self, host_counts, n_tx, ms):
+        ids, counts, rank_of, minsup = self.N.select_frequent(host_counts, n_tx, ms)
+        self.rank_of = rank_of
+        return len(ids), ids, counts, int(minsup)
+
+    def encode(self, F, ws):
+        bm = self.N.encode_bitmaps_cpu(self.tx_ptr, self.items, self.rank_of, F, ws)
+        return torch.from_numpy(bm.view(np.int64))
+
+    def all_gather(self, local, world):
+        parts = [torch.empty_like(local) for _ in range(world)]
+        dist.all_gather(parts, local)
+        return torch.stack(parts)
+
+    def gram(self, bm, wp, mfma):
+        x = bm.numpy().view(np.uint64)
+        bits = np.unpackbits(x.view(np.uint8), axis=1, bitorder="little").astype(np.float32)
+        return (bits @ bits.T).astype(np.uint32)
+
+    def mine(self, bm, wp, dm, owned, emit_level1, download):
+        ids, counts, minsup = self.sel
+        r = self.N.mine_cpu_bitmaps(np.ascontiguousarray(bm.numpy()).view(np.uint64), ids,
+                                    counts, minsup, dm.max_len, owned)
+        F = len(ids)
+        if not emit_level1:
+            r["stats"]["n_itemsets"] = int(r["stats"]["n_itemsets"]) - F
+        return r
+
+    def synchronize(self):
+        pass
+
+
 class DistMiner:
-    """Mine one resident dataset repeatedly (the bench step / the job's mining call)."""
+    """Mine one resident dataset repeatedly (the bench step / the job's mining call).
+
+    ``backend="gpu"``: HIP kernels + RCCL (one process per MI355X).  ``backend="cpu"``: the same
+    protocol with the C++ CPU kernels + gloo (used by the multi-process CPU tests)."""
 
     def __init__(self, tx_ptr: np.ndarray, items: np.ndarray, n_items: int, min_support: float,
                  device: int = 0, max_len: int = 0, mfma: bool = False,
-                 arena_bytes: int = 0):
+                 arena_bytes: int = 0, backend: str = "gpu", force_protocol: bool = False):
         self.world = dist.get_world_size() if (dist is not None and dist.is_initialized()) else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
         self.n_tx = len(tx_ptr) - 1
@@ -85,69 +201,75 @@ class DistMiner:
         self.max_len = int(max_len)
         self.mfma = bool(mfma)
         self.device = device
-        N = native.require_gpu()
-        if self.world > 1:
-            torch.cuda.set_device(device)
-            self.stream = torch.cuda.Stream(device=device)
-            self.g = N.GpuMiner(device, arena_bytes, self.stream.cuda_stream)
-        else:
-            self.stream = None
-            self.g = N.GpuMiner(device, arena_bytes, 0)
+        self.backend = backend
+        self.force_protocol = force_protocol
         lo, hi, ts = shard_bounds(self.n_tx, self.world, self.rank)
         self.lo, self.hi, self.ts = lo, hi, ts
-        sp = tx_ptr[lo:hi + 1]
-        self.g.load_csr(np.ascontiguousarray(sp - sp[0], dtype=np.int64),
-                        np.ascontiguousarray(items[sp[0]:sp[-1]], dtype=np.int32), self.n_items)
+        sp = np.asarray(tx_ptr[lo:hi + 1])
+        sptr = np.ascontiguousarray(sp - sp[0], dtype=np.int64)
+        sitems = np.ascontiguousarray(items[sp[0]:sp[-1]], dtype=np.int32)
+        ops_cls = _GpuOps if backend == "gpu" else _CpuOps
+        self.ops = ops_cls(self, sptr, sitems, arena_bytes)
+        self.g = getattr(self.ops, "g", None)
         self.last: Dict = {}
+
+    def synchronize(self):
+        self.ops.synchronize()
 
     # ------------------------------------------------------------------------------------
     def step(self, download: bool = True) -> Dict:
-        if self.world == 1:
+        if self.world == 1 and self.backend == "gpu" and not self.force_protocol:
             r = self.g.mine(self.min_support, self.max_len, False, download, True, self.mfma)
             st = dict(r["stats"])
             st["global_itemsets"] = int(st["n_itemsets"])
             self.last = r
             return {"stats": st, "trie": r}
-        return self._step_dist(download)
+        return self._step_protocol(download)
 
-    def _step_dist(self, download: bool) -> Dict:
-        g = self.g
-        dev = torch.device("cuda", self.device)
+    def _step_protocol(self, download: bool) -> Dict:
+        ops = self.ops
         t0 = time.perf_counter()
         ph: Dict[str, float] = {}
-        with torch.cuda.stream(self.stream):
-            counts = torch.empty(self.n_items, dtype=torch.int32, device=dev)
-            g.item_support(counts.data_ptr())
-            dist.all_reduce(counts, op=dist.ReduceOp.SUM)  # RCCL over xGMI
+        with ops.ctx():
+            # 1. transaction-DP supports + all-reduce
+            counts = ops.supports()
+            if self.world > 1:
+                dist.all_reduce(counts, op=dist.ReduceOp.SUM)
             host_counts = counts.cpu().numpy().view(np.uint32)
-            F = g.select(host_counts, self.n_tx, self.min_support)
+            F, ids, fcounts, minsup = ops.select(host_counts, self.n_tx, self.min_support)
+            ops.sel = (ids, fcounts, minsup)
             ph["supports_allreduce"] = time.perf_counter() - t0
+            if F == 0:
+                st = {"n_itemsets": 0, "global_itemsets": 0, "n_frequent_items": 0, "max_depth": 0}
+                return {"stats": st, "trie": {"parent": np.zeros(0, np.int64),
+                                              "item": np.zeros(0, np.int32),
+                                              "count": np.zeros(0, np.uint32),
+                                              "depth": np.zeros(0, np.uint8), "stats": st}}
+            # 2. bitmaps of the local shard, all-gather re-shard to replicated [F][N*Ws]
             ws = self.ts // 64
             wp = ws * self.world
-            if F == 0:
-                return {"stats": {"n_itemsets": 0, "global_itemsets": 0, "n_frequent_items": 0}}
-            local = torch.zeros((F, ws), dtype=torch.int64, device=dev)
-            g.encode_bitmaps(local.data_ptr(), ws, 0)
-            gathered = torch.empty((self.world, F, ws), dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(gathered, local)
-            bm = gathered.permute(1, 0, 2).reshape(F, wp).contiguous()
-            del gathered, local
+            local = ops.encode(F, ws)
+            if self.world > 1:
+                gathered = ops.all_gather(local, self.world)
+                bm = gathered.permute(1, 0, 2).reshape(F, wp).contiguous()
+                del gathered
+            else:
+                bm = local
+            del local
             ph["bitmap_allgather"] = time.perf_counter() - t0
-            # ownership from level-2 counts (identical on every rank)
-            gram = torch.empty((F, F), dtype=torch.int32, device=dev)
-            g.pair_counts(bm.data_ptr(), wp, gram.data_ptr(), self.mfma)
-            _, _, minsup = g.frequent()
-            gh = gram.cpu().numpy().view(np.uint32)
-            owner = lpt_partition(root_costs(gh, int(minsup)), self.world)
-            owned = (owner == self.rank).astype(np.uint8)
-            del gram
+            # 3. ownership of root classes (identical on every rank, no collective)
+            if self.world > 1 or self.force_protocol:
+                owner = lpt_partition(root_costs(ops.gram(bm, wp, self.mfma), minsup), self.world)
+                owned = (owner == self.rank).astype(np.uint8)
+            else:
+                owned = None
             ph["partition"] = time.perf_counter() - t0
-            self.stream.synchronize()
-            r = g.mine_bitmaps(bm.data_ptr(), wp, self.min_support, self.max_len, False, owned,
-                               self.rank == 0, download, True, self.mfma)
+            r = ops.mine(bm, wp, self, owned, self.rank == 0, download)
             ph["mine"] = time.perf_counter() - t0
-            tot = torch.tensor([int(r["stats"]["n_itemsets"])], dtype=torch.int64, device=dev)
-            dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+            tot = torch.tensor([int(r["stats"]["n_itemsets"])], dtype=torch.int64,
+                               device=getattr(ops, "dev", "cpu"))
+            if self.world > 1:
+                dist.all_reduce(tot, op=dist.ReduceOp.SUM)
             st = dict(r["stats"])
             st["global_itemsets"] = int(tot.item())
             st["host_phases_s"] = ph

@@ -1,0 +1,86 @@
+"""Multi-process tests of the distributed mining protocol on CPU (gloo), SURVEY §7.6.
+
+Same code path as the RCCL run (``parallel/dist_miner.py``) with the CPU device-ops backend:
+tx-sharded supports + all_reduce, bitmap all_gather re-shard, LPT item-sharded DFS, sub-trie
+gather.  The merged result must equal the single-process miner exactly.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, shape, ms, max_len, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), OMP_NUM_THREADS="1")
+    import torch.distributed as dist
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner, gather_trie
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tx = generate(shape, seed=3)
+        dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, ms, max_len=max_len, backend="cpu")
+        r = dm.step()
+        merged = gather_trie(r["trie"], rank, world, int(r["stats"]["n_frequent_items"]))
+        if rank == 0:
+            out_q.put({"merged": merged, "global": r["stats"]["global_itemsets"],
+                       "lo_hi": (dm.lo, dm.hi)})
+    finally:
+        dist.destroy_process_group()
+
+
+def _sets(par, it, cnt):
+    memo, out = [], {}
+    for n in range(len(it)):
+        s = (memo[par[n]] if par[n] >= 0 else frozenset()) | {int(it[n])}
+        memo.append(s)
+        out[s] = int(cnt[n])
+    return out
+
+
+@pytest.mark.parametrize("world,shape,ms,max_len", [(2, "ds2_weak", 0.03, 0), (4, "tiny", 0.02, 0),
+                                                     (3, "ds2_weak", 0.05, 2)])
+def test_dist_protocol_equals_single_process(world, shape, ms, max_len):
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.ops import native
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shape, ms, max_len, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    tx = generate(shape, seed=3)
+    ref = native.load().mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, max_len=max_len)
+    m = res["merged"]
+    assert res["global"] == ref["stats"]["n_itemsets"] == len(m["item"])
+    assert _sets(m["parent"], m["item"], m["count"]) == _sets(ref["parent"], ref["item"], ref["count"])
+
+
+def test_shard_bounds_and_lpt():
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import lpt_partition, shard_bounds
+    T = 2246
+    for world in (1, 2, 4, 8):
+        spans = [shard_bounds(T, world, r) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == T
+        assert all(s[2] % 256 == 0 for s in spans)
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+    cost = np.array([10, 1, 1, 1, 9, 2, 2, 5], dtype=float)
+    own = lpt_partition(cost, 3)
+    loads = [cost[own == r].sum() for r in range(3)]
+    assert max(loads) - min(loads) <= 2
+    assert (lpt_partition(cost, 3) == own).all()  # deterministic across ranks

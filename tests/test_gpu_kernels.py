@@ -136,3 +136,16 @@ def test_dist_miner_world1(gpu_mod):
     st = dm.step()["stats"]
     c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.03)
     assert st["global_itemsets"] == c["stats"]["n_itemsets"]
+
+
+def test_dist_protocol_path_on_gpu(gpu_mod):
+    """The multi-GPU protocol code path (torch HBM buffers, gram-based partition, owned-mask
+    DFS) at world size 1 on the real device."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+    tx = generate("ds2", seed=2)
+    for mfma in (False, True):
+        dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, 0.05, mfma=mfma, force_protocol=True)
+        st = dm.step()["stats"]
+        c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.05)
+        assert st["global_itemsets"] == c["stats"]["n_itemsets"]
