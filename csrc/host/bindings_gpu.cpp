@@ -45,8 +45,10 @@ py::dict result_to_dict(gpu::GpuMineResult&& r) {
   return d;
 }
 
-MineConfig make_cfg(double ms, int max_len, bool pairs_only, bool gram, bool mfma) {
+MineConfig make_cfg(double ms, int max_len, bool pairs_only, bool gram, bool mfma,
+                    bool persistent = true) {
   MineConfig c;
+  c.persistent = persistent;
   c.min_support = ms;
   c.max_len = max_len;
   c.pairs_only = pairs_only;
@@ -94,8 +96,8 @@ void register_gpu_bindings(py::module_& m) {
       .def("pair_counts", &gpu::GpuMiner::pair_counts, py::call_guard<py::gil_scoped_release>())
       .def("mine_bitmaps", [](gpu::GpuMiner& g, uintptr_t bm, int64_t Wp, double ms, int max_len,
                               bool pairs_only, py::object owned, bool emit_level1, bool download,
-                              bool gram, bool mfma) {
-        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma);
+                              bool gram, bool mfma, bool persistent) {
+        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma, persistent);
         std::vector<uint8_t> own;
         const uint8_t* po = nullptr;
         if (!owned.is_none()) {
@@ -112,10 +114,11 @@ void register_gpu_bindings(py::module_& m) {
         return result_to_dict(std::move(r));
       }, py::arg("bm"), py::arg("Wp"), py::arg("min_support"), py::arg("max_len") = 0,
          py::arg("pairs_only") = false, py::arg("owned") = py::none(), py::arg("emit_level1") = true,
-         py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false)
+         py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
+         py::arg("persistent") = true)
       .def("mine", [](gpu::GpuMiner& g, double ms, int max_len, bool pairs_only, bool download,
-                      bool gram, bool mfma) {
-        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma);
+                      bool gram, bool mfma, bool persistent) {
+        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma, persistent);
         gpu::GpuMineResult r;
         {
           py::gil_scoped_release nogil;
@@ -123,7 +126,8 @@ void register_gpu_bindings(py::module_& m) {
         }
         return result_to_dict(std::move(r));
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("pairs_only") = false,
-         py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false)
+         py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
+         py::arg("persistent") = true)
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
   py::class_<gpu::GpuRuleIndex>(m, "GpuRuleIndex")

@@ -162,6 +162,10 @@ struct MineRun {
   int64_t n_candidates = 0;
   int max_depth = 1;
   int64_t* h_scalar = nullptr;  // pinned [2]
+  bool persistent = true;       // levels >= 3 through the persistent DFS kernel
+  int64_t rows_hint = 0;        // persistent pool capacity (rows = trie nodes)
+  int n_cus = 256;
+  bool overflowed = false;
 
   uint64_t* d_pair = nullptr;   // device [survivors, next-level candidates]
 
@@ -183,8 +187,62 @@ struct MineRun {
   // len[L.n] == 0) holds each row's candidate count and `total` their sum — both produced by
   // the parent chunk (or the host at the root), so a chunk costs ONE host readback: the
   // survivor count and the child level's candidate total, read together.
+  // Levels >= 3 in one persistent launch (dfs_persistent.hip): seed = every class of L.
+  void run_persistent(const Level& L, int depth) {
+    const size_t mark = arena->mark();
+    const int64_t row_cap = std::max<int64_t>(rows_hint, 1 << 20);
+    const int64_t task_cap = row_cap / 2 + L.n + 1024;
+    ensure_out(out_size + row_cap);
+    kern::DfsArgs a{};
+    a.seed_bm = L.bm;
+    a.seed_rank = L.rank;
+    a.seed_gid = L.gid;
+    a.seed_row_end = L.row_end;
+    a.seed_rows = L.n;
+    a.seed_depth = depth;
+    a.tasks = (kern::DfsTask*)arena->push((size_t)task_cap * sizeof(kern::DfsTask));
+    a.ready = (unsigned int*)arena->push((size_t)task_cap * sizeof(unsigned int));
+    a.task_cap = task_cap;
+    a.ctl = (kern::DfsCtl*)arena->push(sizeof(kern::DfsCtl));
+    a.pool_bm = (uint64_t*)arena->push((size_t)row_cap * Wp * sizeof(uint64_t));
+    a.pool_rank = (int32_t*)arena->push((size_t)row_cap * sizeof(int32_t));
+    a.pool_gid = (int64_t*)arena->push((size_t)row_cap * sizeof(int64_t));
+    a.row_cap = row_cap;
+    a.out_parent = out_parent.p;
+    a.out_item = out_item.p;
+    a.out_count = out_count.p;
+    a.out_depth = out_depth.p;
+    a.out_base = out_size;
+    a.ids = d_ids;
+    a.Wp = Wp;
+    a.minsup = minsup;
+    a.max_len = max_len;
+    a.n_cus = n_cus;
+    KMLS_HIP(hipMemsetAsync(a.ready, 0, (size_t)task_cap * sizeof(unsigned int), s));
+    KMLS_HIP(hipMemsetAsync(a.ctl, 0, sizeof(kern::DfsCtl), s));
+    kern::dfs_persistent(a, s);
+    kern::DfsCtl h;
+    KMLS_HIP(hipMemcpyAsync(&h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+    if (h.timeout) throw std::runtime_error("kmls: persistent DFS kernel timed out");
+    if (h.overflow) {
+      overflowed = true;
+      rows_hint = std::max<int64_t>(row_cap * 4, (int64_t)h.row_top * 2);
+    } else {
+      out_size += (int64_t)h.row_top;
+      n_candidates += (int64_t)h.candidates;
+      max_depth = std::max<int>(max_depth, (int)h.max_depth);
+      rows_hint = std::max<int64_t>(rows_hint, (int64_t)h.row_top + (int64_t)(h.row_top >> 2));
+    }
+    arena->pop_to(mark);
+  }
+
   void process(const Level& L, int depth, const int64_t* len, int64_t total) {
     if (L.n < 2 || total == 0 || (max_len && depth >= max_len)) return;
+    if (persistent && depth >= 2) {
+      run_persistent(L, depth);
+      return;
+    }
     const size_t mark0 = arena->mark();
     int64_t* cand_off = (int64_t*)arena->push((size_t)(L.n + 1) * sizeof(int64_t));
     const size_t tb = kern::scan_temp_bytes(L.n);
@@ -287,6 +345,9 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
   }
   arena_ = std::make_unique<DeviceArena>(arena_bytes ? arena_bytes : default_arena_bytes());
   pinned_ = make_pinned_pool();
+  hipDeviceProp_t prop;
+  KMLS_HIP(hipGetDeviceProperties(&prop, device));
+  n_cus_ = std::max(1, prop.multiProcessorCount);
 }
 
 GpuMiner::~GpuMiner() {
@@ -386,7 +447,16 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   hipStream_t s = (hipStream_t)stream_;
   GpuMineResult res;
   const int64_t F = (int64_t)fi_.ids.size();
-  MineRun run;
+  Event e0, e1, e2, e3;
+  const size_t mark = arena_->mark();
+  KMLS_HIP(hipEventRecord(e0.e, s));
+  std::unique_ptr<MineRun> runp;
+  for (int attempt = 0;; ++attempt) {
+  runp = std::make_unique<MineRun>();
+  MineRun& run = *runp;
+  run.persistent = cfg.persistent;
+  run.rows_hint = rows_hint_;
+  run.n_cus = n_cus_;
   run.s = s;
   run.arena = arena_.get();
   run.Wp = Wp;
@@ -396,9 +466,6 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   run.F = F;
   KMLS_HIP(hipHostMalloc((void**)&run.h_scalar, 64));
   KMLS_HIP(hipMalloc((void**)&run.d_pair, 2 * sizeof(uint64_t)));
-  Event e0, e1, e2, e3;
-  KMLS_HIP(hipEventRecord(e0.e, s));
-  const size_t mark = arena_->mark();
   // level-1 nodes: gid = Eclat rank
   run.ensure_out(std::max<int64_t>(F * 8, 1 << 16));
   {
@@ -455,6 +522,18 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   } else {
     KMLS_HIP(hipEventRecord(e1.e, s));
   }
+  rows_hint_ = run.rows_hint;
+  if (!run.overflowed || attempt >= 6) {
+    if (run.overflowed) throw std::runtime_error("kmls: persistent DFS capacity overflow");
+    break;
+  }
+  arena_->pop_to(mark);
+  (void)hipHostFree(run.h_scalar);
+  run.h_scalar = nullptr;
+  (void)hipFree(run.d_pair);
+  run.d_pair = nullptr;
+  }
+  MineRun& run = *runp;
   KMLS_HIP(hipEventRecord(e2.e, s));
   const int64_t N = run.out_size;
   res.n_nodes = N;

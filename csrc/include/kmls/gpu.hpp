@@ -126,6 +126,8 @@ class GpuMiner {
   uint64_t* d_own_bm_ = nullptr;  // single-GPU bitmap buffer
   size_t own_bm_bytes_ = 0;
   std::shared_ptr<PinnedPool> pinned_;
+  int64_t rows_hint_ = 0;  // learned persistent-DFS pool capacity
+  int n_cus_ = 256;
 };
 
 // HBM-resident rule index + batched matcher kernel (serve_match_topk).

@@ -54,6 +54,48 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
 void gram_to_cand(const uint32_t* gram, int64_t F, const int64_t* cand_off, int64_t c0, int64_t c1,
                   uint32_t* cnt, hipStream_t s);
 
+// ---- persistent DFS (dfs_persistent.hip) ----
+struct DfsTask {
+  const unsigned long long* bm;  // class members' bitmaps [n][Wp]
+  const int32_t* rank;           // members' last-item Eclat rank
+  const int64_t* gid;            // members' global trie node ids
+  int32_t n, depth, a0, a1;      // class size, members' itemset size, rows [a0, a1) to expand
+};
+struct DfsCtl {  // zeroed before every launch
+  unsigned long long q_head, q_tail, pending, row_top, candidates;
+  unsigned int overflow, timeout, max_depth, pad;
+};
+struct DfsArgs {
+  // seed level (classes = runs of equal row_end)
+  const uint64_t* seed_bm;
+  const int32_t* seed_rank;
+  const int64_t* seed_gid;
+  const int32_t* seed_row_end;
+  int64_t seed_rows;
+  int seed_depth;
+  // queue + pool
+  DfsTask* tasks;
+  unsigned int* ready;
+  int64_t task_cap;
+  DfsCtl* ctl;
+  uint64_t* pool_bm;
+  int32_t* pool_rank;
+  int64_t* pool_gid;
+  int64_t row_cap;
+  // output trie (node id = out_base + pool row)
+  int64_t* out_parent;
+  int32_t* out_item;
+  uint32_t* out_count;
+  uint8_t* out_depth;
+  int64_t out_base;
+  const int32_t* ids;
+  int64_t Wp;
+  uint32_t minsup;
+  int max_len;
+  int n_cus;
+};
+void dfs_persistent(const DfsArgs& a, hipStream_t s);
+
 // ---- serving (serve.hip) ----
 void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,
                       const uint8_t* is_key, int64_t n_items, const int64_t* q_ptr,

@@ -129,7 +129,7 @@ class _GpuOps:
         if self.stream is not None:
             self.stream.synchronize()
         return self.g.mine_bitmaps(bm.data_ptr(), wp, dm.min_support, dm.max_len, False, owned,
-                                   emit_level1, download, True, dm.mfma)
+                                   emit_level1, download, True, dm.mfma, dm.persistent)
 
     def synchronize(self):
         self.g.synchronize()
@@ -192,7 +192,8 @@ class DistMiner:
 
     def __init__(self, tx_ptr: np.ndarray, items: np.ndarray, n_items: int, min_support: float,
                  device: int = 0, max_len: int = 0, mfma: bool = False,
-                 arena_bytes: int = 0, backend: str = "gpu", force_protocol: bool = False):
+                 arena_bytes: int = 0, backend: str = "gpu", force_protocol: bool = False,
+                 persistent: bool = True):
         self.world = dist.get_world_size() if (dist is not None and dist.is_initialized()) else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
         self.n_tx = len(tx_ptr) - 1
@@ -203,6 +204,7 @@ class DistMiner:
         self.device = device
         self.backend = backend
         self.force_protocol = force_protocol
+        self.persistent = bool(persistent)
         lo, hi, ts = shard_bounds(self.n_tx, self.world, self.rank)
         self.lo, self.hi, self.ts = lo, hi, ts
         sp = np.asarray(tx_ptr[lo:hi + 1])
@@ -219,7 +221,8 @@ class DistMiner:
     # ------------------------------------------------------------------------------------
     def step(self, download: bool = True) -> Dict:
         if self.world == 1 and self.backend == "gpu" and not self.force_protocol:
-            r = self.g.mine(self.min_support, self.max_len, False, download, True, self.mfma)
+            r = self.g.mine(self.min_support, self.max_len, False, download, True, self.mfma,
+                            self.persistent)
             st = dict(r["stats"])
             st["global_itemsets"] = int(st["n_itemsets"])
             self.last = r

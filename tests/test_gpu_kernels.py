@@ -149,3 +149,26 @@ def test_dist_protocol_path_on_gpu(gpu_mod):
         st = dm.step()["stats"]
         c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.05)
         assert st["global_itemsets"] == c["stats"]["n_itemsets"]
+
+
+@pytest.mark.parametrize("shape,ms", [("ds2", 0.05), ("ds2_weak", 0.03), ("tiny", 0.02),
+                                      ("ds2", 0.06)])
+def test_persistent_dfs_equals_level_wise(gpu_mod, shape, ms):
+    """Persistent work-queue DFS == level-wise path == CPU miner (first call also exercises the
+    capacity-overflow re-run: the initial pool holds 1M rows)."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    tx = generate(shape, seed=21)
+    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
+    g = gpu_mod.GpuMiner(0, 4 << 30, 0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    for _ in range(2):
+        p = g.mine(ms, persistent=True)
+        assert p["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
+        assert p["stats"]["max_depth"] == c["stats"]["max_depth"]
+        assert np.array_equal(np.sort(p["count"]), np.sort(c["count"]))
+        # parents precede children (trie order used by every consumer)
+        assert (p["parent"] < np.arange(len(p["parent"]))).all()
+    lw = g.mine(ms, persistent=False)
+    assert lw["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
+    if c["stats"]["n_itemsets"] < 300_000:
+        assert _trie_dict(p) == _trie_dict(c)
