@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -218,12 +220,23 @@ struct MineRun {
     a.minsup = minsup;
     a.max_len = max_len;
     a.n_cus = n_cus;
+    {
+      const char* e = std::getenv("KMLS_DFS_TIMEOUT_MS");
+      const double ms = e ? std::atof(e) : 20000.0;
+      a.timeout_ticks = (unsigned long long)(ms * 1e5);  // 100 MHz
+    }
     KMLS_HIP(hipMemsetAsync(a.ready, 0, (size_t)task_cap * sizeof(unsigned int), s));
     KMLS_HIP(hipMemsetAsync(a.ctl, 0, sizeof(kern::DfsCtl), s));
     kern::dfs_persistent(a, s);
     kern::DfsCtl h;
     KMLS_HIP(hipMemcpyAsync(&h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
     KMLS_HIP(hipStreamSynchronize(s));
+    if (std::getenv("KMLS_DFS_DEBUG"))
+      fprintf(stderr,
+              "[dfs] seed_rows=%lld depth=%d row_cap=%lld task_cap=%lld | q_head=%llu q_tail=%llu "
+              "pending=%llu row_top=%llu cands=%llu overflow=%u timeout=%u max_depth=%u\n",
+              (long long)L.n, depth, (long long)row_cap, (long long)task_cap, h.q_head, h.q_tail,
+              h.pending, h.row_top, h.candidates, h.overflow, h.timeout, h.max_depth);
     if (h.timeout) throw std::runtime_error("kmls: persistent DFS kernel timed out");
     if (h.overflow) {
       overflowed = true;

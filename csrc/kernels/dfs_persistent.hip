@@ -36,7 +36,6 @@ namespace {
 
 constexpr int kWaves = 4;             // waves per workgroup
 constexpr int kTaskCands = 4096;      // max candidates per task (row-range split)
-constexpr unsigned long long kTimeoutTicks = 100000000ull * 20;  // 20 s at 100 MHz wall clock
 
 __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -63,6 +62,7 @@ struct Ctx {
   int64_t task_cap;
   uint32_t minsup;
   int max_len;
+  unsigned long long timeout_ticks;
 };
 
 // Split a class into row-range tasks and publish them.  Called by ONE wave; lane 0 does the
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
           st = 1;
         } else if (ld_relaxed(&cx.ctl->pending) == 0ull) {
           st = (idx < (unsigned long long)cx.task_cap && ld_relaxed(&cx.ready[idx]) != 0u) ? 1 : 2;
-        } else if (wall_clock64() - t_start > kTimeoutTicks) {
+        } else if (wall_clock64() - t_start > cx.timeout_ticks) {
           atomicOr(&cx.ctl->timeout, 1u);
           st = 2;
         }
@@ -289,7 +289,7 @@ int team_size_for(int64_t Wp) {
 void dfs_persistent(const DfsArgs& a, hipStream_t s) {
   Ctx cx{a.tasks, a.ready, a.ctl, (unsigned long long*)a.pool_bm, a.pool_rank, a.pool_gid,
          a.out_parent, a.out_item, a.out_count, a.out_depth, a.ids, a.out_base, a.Wp, a.row_cap,
-         a.task_cap, a.minsup, a.max_len};
+         a.task_cap, a.minsup, a.max_len, a.timeout_ticks};
   // seed
   const int64_t nr = a.seed_rows;
   const int sg = (int)std::min<int64_t>(std::max<int64_t>((nr + 255) / 256, 1), 4096);

@@ -93,6 +93,7 @@ struct DfsArgs {
   uint32_t minsup;
   int max_len;
   int n_cus;
+  unsigned long long timeout_ticks;  // 100 MHz wall-clock ticks
 };
 void dfs_persistent(const DfsArgs& a, hipStream_t s);
 

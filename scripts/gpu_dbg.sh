@@ -1,0 +1,4 @@
+#!/usr/bin/env bash
+source "$(dirname "$0")/gpu_round.sh"
+export PYTHONUNBUFFERED=1
+step dfs_debug 240 python -u scripts/dfs_debug.py
