@@ -15,6 +15,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../kernels/kernels.hpp"
@@ -168,6 +169,8 @@ struct MineRun {
   int64_t rows_hint = 0;        // persistent pool capacity (rows = trie nodes)
   int n_cus = 256;
   bool overflowed = false;
+  unsigned int* abort_host = nullptr;  // mapped pinned watchdog flag
+  const unsigned int* abort_dev = nullptr;
 
   uint64_t* d_pair = nullptr;   // device [survivors, next-level candidates]
 
@@ -225,12 +228,54 @@ struct MineRun {
       const double ms = e ? std::atof(e) : 20000.0;
       a.timeout_ticks = (unsigned long long)(ms * 1e5);  // 100 MHz
     }
+    const int n_waves = n_cus * 2 * 4;
+    a.wave_state = (unsigned int*)arena->push((size_t)n_waves * 4 * sizeof(unsigned int));
+    a.abort_flag = abort_dev;
+    *abort_host = 0u;
     KMLS_HIP(hipMemsetAsync(a.ready, 0, (size_t)task_cap * sizeof(unsigned int), s));
     KMLS_HIP(hipMemsetAsync(a.ctl, 0, sizeof(kern::DfsCtl), s));
+    KMLS_HIP(hipMemsetAsync(a.wave_state, 0, (size_t)n_waves * 4 * sizeof(unsigned int), s));
     kern::dfs_persistent(a, s);
+    // host watchdog: poll completion; past the deadline raise the mapped abort flag so every
+    // wave leaves its loops, then report the queue state
+    {
+      const double limit_ms = (double)a.timeout_ticks / 1e5 + 2000.0;
+      const auto tw = std::chrono::steady_clock::now();
+      bool aborted = false;
+      while (true) {
+        hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) KMLS_HIP(q);
+        const double el = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
+        if (!aborted && el > limit_ms) {
+          __atomic_store_n(abort_host, 1u, __ATOMIC_SEQ_CST);
+          aborted = true;
+          fprintf(stderr, "[dfs] watchdog: kernel exceeded %.0f ms, abort raised\n", limit_ms);
+        }
+        if (aborted && el > limit_ms + 10000.0) {
+          fprintf(stderr, "[dfs] watchdog: kernel did not honour abort; giving up\n");
+          throw std::runtime_error("kmls: persistent DFS kernel hung (abort not honoured)");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(aborted ? 1000 : 20));
+      }
+    }
     kern::DfsCtl h;
     KMLS_HIP(hipMemcpyAsync(&h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
     KMLS_HIP(hipStreamSynchronize(s));
+    if (h.timeout || h.aborted || h.bad_task || std::getenv("KMLS_DFS_DEBUG")) {
+      std::vector<unsigned int> ws((size_t)n_waves * 4);
+      KMLS_HIP(hipMemcpy(ws.data(), a.wave_state, ws.size() * sizeof(unsigned int), hipMemcpyDeviceToHost));
+      int hist[10] = {0};
+      for (int w = 0; w < n_waves; ++w) hist[std::min(9u, ws[4 * w])]++;
+      fprintf(stderr, "[dfs] waves: state0=%d polling=%d expanding=%d retiring=%d exited=%d | exited_ctr=%u aborted=%u bad_task=%u\n",
+              hist[0], hist[1], hist[2], hist[3], hist[9], h.exited, h.aborted, h.bad_task);
+      int shown = 0;
+      for (int w = 0; w < n_waves && shown < 8; ++w)
+        if (ws[4 * w] == 2 || ws[4 * w] == 3) {
+          fprintf(stderr, "[dfs]   wave %d state=%u idx=%u n=%u a1=%u\n", w, ws[4 * w], ws[4 * w + 1], ws[4 * w + 2], ws[4 * w + 3]);
+          ++shown;
+        }
+    }
     if (std::getenv("KMLS_DFS_DEBUG"))
       fprintf(stderr,
               "[dfs] seed_rows=%lld depth=%d row_cap=%lld task_cap=%lld | q_head=%llu q_tail=%llu "
@@ -358,6 +403,9 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
   }
   arena_ = std::make_unique<DeviceArena>(arena_bytes ? arena_bytes : default_arena_bytes());
   pinned_ = make_pinned_pool();
+  KMLS_HIP(hipHostMalloc((void**)&abort_host_, 64, hipHostMallocMapped));
+  *abort_host_ = 0u;
+  KMLS_HIP(hipHostGetDevicePointer((void**)&abort_dev_, abort_host_, 0));
   hipDeviceProp_t prop;
   KMLS_HIP(hipGetDeviceProperties(&prop, device));
   n_cus_ = std::max(1, prop.multiProcessorCount);
@@ -370,6 +418,7 @@ GpuMiner::~GpuMiner() {
   if (d_rank_of_) (void)hipFree(d_rank_of_);
   if (d_ids_) (void)hipFree(d_ids_);
   if (d_own_bm_) (void)hipFree(d_own_bm_);
+  if (abort_host_) (void)hipHostFree(abort_host_);
   arena_.reset();
   if (own_stream_) (void)hipStreamDestroy((hipStream_t)stream_);
 }
@@ -470,6 +519,8 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   run.persistent = cfg.persistent;
   run.rows_hint = rows_hint_;
   run.n_cus = n_cus_;
+  run.abort_host = abort_host_;
+  run.abort_dev = abort_dev_;
   run.s = s;
   run.arena = arena_.get();
   run.Wp = Wp;

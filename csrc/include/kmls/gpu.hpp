@@ -127,6 +127,8 @@ class GpuMiner {
   size_t own_bm_bytes_ = 0;
   std::shared_ptr<PinnedPool> pinned_;
   int64_t rows_hint_ = 0;  // learned persistent-DFS pool capacity
+  unsigned int* abort_host_ = nullptr;       // watchdog flag (pinned, device-mapped)
+  const unsigned int* abort_dev_ = nullptr;
   int n_cus_ = 256;
 };
 

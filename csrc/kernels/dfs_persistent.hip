@@ -63,7 +63,23 @@ struct Ctx {
   uint32_t minsup;
   int max_len;
   unsigned long long timeout_ticks;
+  const unsigned int* abort_flag;
+  unsigned int* wave_state;
 };
+
+__device__ __forceinline__ bool host_abort(const Ctx& cx) {
+  return __hip_atomic_load(cx.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+}
+
+__device__ __forceinline__ void crumb(const Ctx& cx, int gw, int lane, unsigned st, unsigned a,
+                                      unsigned b, unsigned c) {
+  if (lane == 0 && cx.wave_state) {
+    __hip_atomic_store(&cx.wave_state[4 * gw + 0], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cx.wave_state[4 * gw + 1], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cx.wave_state[4 * gw + 2], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cx.wave_state[4 * gw + 3], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 // Split a class into row-range tasks and publish them.  Called by ONE wave; lane 0 does the
 // bookkeeping (classes larger than a task are rare).  Payload (child bitmaps, ranks, gids) was
@@ -137,6 +153,9 @@ __device__ void expand_task(const Ctx& cx, const DfsTask& tk, int lane) {
   const int n = tk.n;
   unsigned long long cands = 0;
   for (int a = tk.a0; a < tk.a1; ++a) {
+    int ab = 0;
+    if (lane == 0) ab = host_abort(cx) ? 1 : 0;
+    if (__shfl(ab, 0)) break;
     const ulonglong2* xa = reinterpret_cast<const ulonglong2*>(tk.bm + (int64_t)a * Wp);
     // pass 1: survivor count
     uint32_t S = 0;
@@ -198,21 +217,28 @@ __device__ void expand_task(const Ctx& cx, const DfsTask& tk, int lane) {
 template <int TS>
 __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
   const int lane = threadIdx.x & 63;
+  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const unsigned long long t_start = wall_clock64();
+  unsigned long long polls = 0;
   while (true) {
     unsigned long long idx = 0;
     if (lane == 0) idx = atomicAdd(&cx.ctl->q_head, 1ull);
     idx = __shfl(idx, 0);
+    crumb(cx, gw, lane, 1u, (unsigned)idx, 0u, 0u);
     // wait until slot idx is published, or until no task can ever be published again
     bool got = false;
     while (true) {
       int st = 0;  // 1 = ready, 2 = terminate
       if (lane == 0) {
+        ++polls;
         if (idx < (unsigned long long)cx.task_cap && ld_relaxed(&cx.ready[idx]) != 0u) {
           st = 1;
         } else if (ld_relaxed(&cx.ctl->pending) == 0ull) {
           st = (idx < (unsigned long long)cx.task_cap && ld_relaxed(&cx.ready[idx]) != 0u) ? 1 : 2;
-        } else if (wall_clock64() - t_start > cx.timeout_ticks) {
+        } else if (host_abort(cx)) {
+          atomicOr(&cx.ctl->aborted, 1u);
+          st = 2;
+        } else if (wall_clock64() - t_start > cx.timeout_ticks || polls > (1ull << 26)) {
           atomicOr(&cx.ctl->timeout, 1u);
           st = 2;
         }
@@ -222,10 +248,21 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
       if (st == 2) break;
       __builtin_amdgcn_s_sleep(2);
     }
-    if (!got) return;
+    if (!got) {
+      crumb(cx, gw, lane, 9u, (unsigned)idx, 0u, 0u);
+      if (lane == 0) atomicAdd(&cx.ctl->exited, 1u);
+      return;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const DfsTask tk = cx.tasks[idx];
-    expand_task<TS>(cx, tk, lane);
+    crumb(cx, gw, lane, 2u, (unsigned)idx, (unsigned)tk.n, (unsigned)tk.a1);
+    if (tk.n < 2 || tk.n > (1 << 24) || tk.a0 < 0 || tk.a1 > tk.n - 1 || tk.a0 > tk.a1 ||
+        tk.bm == nullptr) {
+      if (lane == 0) atomicOr(&cx.ctl->bad_task, 1u);
+    } else {
+      expand_task<TS>(cx, tk, lane);
+    }
+    crumb(cx, gw, lane, 3u, (unsigned)idx, 0u, 0u);
     // retire: children (if any) were added to pending inside expand_task
     if (lane == 0) atomicAdd(&cx.ctl->pending, (unsigned long long)(-1ll));
   }
@@ -289,7 +326,7 @@ int team_size_for(int64_t Wp) {
 void dfs_persistent(const DfsArgs& a, hipStream_t s) {
   Ctx cx{a.tasks, a.ready, a.ctl, (unsigned long long*)a.pool_bm, a.pool_rank, a.pool_gid,
          a.out_parent, a.out_item, a.out_count, a.out_depth, a.ids, a.out_base, a.Wp, a.row_cap,
-         a.task_cap, a.minsup, a.max_len, a.timeout_ticks};
+         a.task_cap, a.minsup, a.max_len, a.timeout_ticks, a.abort_flag, a.wave_state};
   // seed
   const int64_t nr = a.seed_rows;
   const int sg = (int)std::min<int64_t>(std::max<int64_t>((nr + 255) / 256, 1), 4096);

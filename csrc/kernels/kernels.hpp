@@ -63,7 +63,7 @@ struct DfsTask {
 };
 struct DfsCtl {  // zeroed before every launch
   unsigned long long q_head, q_tail, pending, row_top, candidates;
-  unsigned int overflow, timeout, max_depth, pad;
+  unsigned int overflow, timeout, max_depth, bad_task, aborted, exited, pad0, pad1;
 };
 struct DfsArgs {
   // seed level (classes = runs of equal row_end)
@@ -94,6 +94,8 @@ struct DfsArgs {
   int max_len;
   int n_cus;
   unsigned long long timeout_ticks;  // 100 MHz wall-clock ticks
+  const unsigned int* abort_flag;    // host-mapped pinned word; host watchdog sets it to 1
+  unsigned int* wave_state;          // per-wave breadcrumbs (debug): [state, idx_lo, a, n]
 };
 void dfs_persistent(const DfsArgs& a, hipStream_t s);
 

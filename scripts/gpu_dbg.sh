@@ -1,4 +1,5 @@
 #!/usr/bin/env bash
 source "$(dirname "$0")/gpu_round.sh"
 export PYTHONUNBUFFERED=1
+export PYTHONPATH="$PWD:${PYTHONPATH:-}"
 step dfs_debug 240 python -u scripts/dfs_debug.py

@@ -5,6 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
+export PYTHONPATH="$PWD:${PYTHONPATH:-}"
 export TMPDIR=/tmp
 step() {  # step <name> <timeout-seconds> <cmd...>
   local name=$1 t=$2; shift 2
