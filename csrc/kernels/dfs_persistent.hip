@@ -226,27 +226,37 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
     idx = __shfl(idx, 0);
     crumb(cx, gw, lane, 1u, (unsigned)idx, 0u, 0u);
     // wait until slot idx is published, or until no task can ever be published again
+    // Back-off polling: 2k waves re-reading the hot `ready`/`pending` lines (which producers
+    // update with atomics) at full rate starve the producers' atomics; the first version of
+    // this loop made no progress at all.  Poll the slot every iteration with a growing sleep,
+    // check termination every 8th and the host abort flag / clock every 256th poll.
     bool got = false;
+    unsigned it = 0;
     while (true) {
       int st = 0;  // 1 = ready, 2 = terminate
       if (lane == 0) {
         ++polls;
         if (idx < (unsigned long long)cx.task_cap && ld_relaxed(&cx.ready[idx]) != 0u) {
           st = 1;
-        } else if (ld_relaxed(&cx.ctl->pending) == 0ull) {
+        } else if ((it & 7u) == 7u && ld_relaxed(&cx.ctl->pending) == 0ull) {
           st = (idx < (unsigned long long)cx.task_cap && ld_relaxed(&cx.ready[idx]) != 0u) ? 1 : 2;
-        } else if (host_abort(cx)) {
-          atomicOr(&cx.ctl->aborted, 1u);
-          st = 2;
-        } else if (wall_clock64() - t_start > cx.timeout_ticks || polls > (1ull << 26)) {
-          atomicOr(&cx.ctl->timeout, 1u);
-          st = 2;
+        } else if ((it & 255u) == 255u) {
+          if (host_abort(cx)) {
+            atomicOr(&cx.ctl->aborted, 1u);
+            st = 2;
+          } else if (wall_clock64() - t_start > cx.timeout_ticks || polls > (1ull << 26)) {
+            atomicOr(&cx.ctl->timeout, 1u);
+            st = 2;
+          }
         }
       }
       st = __shfl(st, 0);
       if (st == 1) { got = true; break; }
       if (st == 2) break;
-      __builtin_amdgcn_s_sleep(2);
+      if (it < 16) __builtin_amdgcn_s_sleep(1);
+      else if (it < 256) __builtin_amdgcn_s_sleep(8);
+      else __builtin_amdgcn_s_sleep(32);
+      ++it;
     }
     if (!got) {
       crumb(cx, gw, lane, 9u, (unsigned)idx, 0u, 0u);
