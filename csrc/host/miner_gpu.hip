@@ -193,10 +193,20 @@ struct MineRun {
   // the parent chunk (or the host at the root), so a chunk costs ONE host readback: the
   // survivor count and the child level's candidate total, read together.
   // Levels >= 3 in one persistent launch (dfs_persistent.hip): seed = every class of L.
-  void run_persistent(const Level& L, int depth) {
+  // Returns false (nothing emitted) when the pool/queue capacity was exceeded: the caller then
+  // runs the exact level-wise path for L, and the next call starts with a larger pool.
+  bool run_persistent(const Level& L, int depth) {
     const size_t mark = arena->mark();
-    const int64_t row_cap = std::max<int64_t>(rows_hint, 1 << 20);
-    const int64_t task_cap = row_cap / 2 + L.n + 1024;
+    const int64_t task_cap_min = L.n + 4096;
+    // bytes per pool row: bitmap + rank + gid + compaction (pos + 4 staged outputs)
+    const int64_t per_row = Wp * 8 + 4 + 8 + 8 + 17;
+    const int64_t avail = (int64_t)(arena->capacity() - arena->used()) - (64ll << 20) -
+                          task_cap_min * (int64_t)(sizeof(kern::DfsTask) + 4);
+    int64_t row_cap = std::max<int64_t>(rows_hint, 1 << 20);
+    if (avail <= 0) return false;
+    row_cap = std::min<int64_t>(row_cap, avail / (per_row + (int64_t)(sizeof(kern::DfsTask) + 4) / 2));
+    if (row_cap < 4096) return false;
+    const int64_t task_cap = row_cap / 2 + task_cap_min;
     ensure_out(out_size + row_cap);
     kern::DfsArgs a{};
     a.seed_bm = L.bm;
@@ -228,79 +238,100 @@ struct MineRun {
       const double ms = e ? std::atof(e) : 20000.0;
       a.timeout_ticks = (unsigned long long)(ms * 1e5);  // 100 MHz
     }
+    const bool debug = std::getenv("KMLS_DFS_DEBUG") != nullptr;
     const int n_waves = n_cus * 2 * 4;
-    a.wave_state = (unsigned int*)arena->push((size_t)n_waves * 4 * sizeof(unsigned int));
+    unsigned int* crumbs = (unsigned int*)arena->push((size_t)n_waves * 4 * sizeof(unsigned int));
+    a.wave_state = debug ? crumbs : nullptr;
     a.abort_flag = abort_dev;
     *abort_host = 0u;
     KMLS_HIP(hipMemsetAsync(a.ready, 0, (size_t)task_cap * sizeof(unsigned int), s));
     KMLS_HIP(hipMemsetAsync(a.ctl, 0, sizeof(kern::DfsCtl), s));
-    KMLS_HIP(hipMemsetAsync(a.wave_state, 0, (size_t)n_waves * 4 * sizeof(unsigned int), s));
+    KMLS_HIP(hipMemsetAsync(out_depth.p + out_size, 0, (size_t)row_cap, s));  // holes = depth 0
+    if (debug) KMLS_HIP(hipMemsetAsync(crumbs, 0, (size_t)n_waves * 4 * sizeof(unsigned int), s));
+    const auto t_launch = std::chrono::steady_clock::now();
     kern::dfs_persistent(a, s);
     // host watchdog: poll completion; past the deadline raise the mapped abort flag so every
-    // wave leaves its loops, then report the queue state
+    // wave leaves its loops, then report
     {
       const double limit_ms = (double)a.timeout_ticks / 1e5 + 2000.0;
-      const auto tw = std::chrono::steady_clock::now();
       bool aborted = false;
       while (true) {
         hipError_t q = hipStreamQuery(s);
         if (q == hipSuccess) break;
         if (q != hipErrorNotReady) KMLS_HIP(q);
-        const double el = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
+        const double el = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_launch).count();
         if (!aborted && el > limit_ms) {
           __atomic_store_n(abort_host, 1u, __ATOMIC_SEQ_CST);
           aborted = true;
           fprintf(stderr, "[dfs] watchdog: kernel exceeded %.0f ms, abort raised\n", limit_ms);
         }
-        if (aborted && el > limit_ms + 10000.0) {
-          fprintf(stderr, "[dfs] watchdog: kernel did not honour abort; giving up\n");
+        if (aborted && el > limit_ms + 10000.0)
           throw std::runtime_error("kmls: persistent DFS kernel hung (abort not honoured)");
-        }
-        std::this_thread::sleep_for(std::chrono::microseconds(aborted ? 1000 : 20));
+        if (el > 2.0) std::this_thread::sleep_for(std::chrono::microseconds(aborted ? 1000 : 10));
       }
     }
     kern::DfsCtl h;
     KMLS_HIP(hipMemcpyAsync(&h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
     KMLS_HIP(hipStreamSynchronize(s));
-    if (h.timeout || h.aborted || h.bad_task || std::getenv("KMLS_DFS_DEBUG")) {
-      std::vector<unsigned int> ws((size_t)n_waves * 4);
-      KMLS_HIP(hipMemcpy(ws.data(), a.wave_state, ws.size() * sizeof(unsigned int), hipMemcpyDeviceToHost));
-      int hist[10] = {0};
-      for (int w = 0; w < n_waves; ++w) hist[std::min(9u, ws[4 * w])]++;
-      fprintf(stderr, "[dfs] waves: state0=%d polling=%d expanding=%d retiring=%d exited=%d | exited_ctr=%u aborted=%u bad_task=%u\n",
-              hist[0], hist[1], hist[2], hist[3], hist[9], h.exited, h.aborted, h.bad_task);
-      int shown = 0;
-      for (int w = 0; w < n_waves && shown < 8; ++w)
-        if (ws[4 * w] == 2 || ws[4 * w] == 3) {
-          fprintf(stderr, "[dfs]   wave %d state=%u idx=%u n=%u a1=%u\n", w, ws[4 * w], ws[4 * w + 1], ws[4 * w + 2], ws[4 * w + 3]);
-          ++shown;
-        }
-    }
-    if (std::getenv("KMLS_DFS_DEBUG"))
+    if (debug || h.timeout || h.aborted || h.bad_task) {
       fprintf(stderr,
               "[dfs] seed_rows=%lld depth=%d row_cap=%lld task_cap=%lld | q_head=%llu q_tail=%llu "
-              "pending=%llu row_top=%llu cands=%llu overflow=%u timeout=%u max_depth=%u\n",
+              "pending=%llu row_top=%llu cands=%llu overflow=%u timeout=%u aborted=%u bad=%u "
+              "exited=%u max_depth=%u\n",
               (long long)L.n, depth, (long long)row_cap, (long long)task_cap, h.q_head, h.q_tail,
-              h.pending, h.row_top, h.candidates, h.overflow, h.timeout, h.max_depth);
-    if (h.timeout) throw std::runtime_error("kmls: persistent DFS kernel timed out");
-    if (h.overflow) {
-      overflowed = true;
-      rows_hint = std::max<int64_t>(row_cap * 4, (int64_t)h.row_top * 2);
-    } else {
-      out_size += (int64_t)h.row_top;
-      n_candidates += (int64_t)h.candidates;
-      max_depth = std::max<int>(max_depth, (int)h.max_depth);
-      rows_hint = std::max<int64_t>(rows_hint, (int64_t)h.row_top + (int64_t)(h.row_top >> 2));
+              h.pending, h.row_top, h.candidates, h.overflow, h.timeout, h.aborted, h.bad_task,
+              h.exited, h.max_depth);
+      if (debug) {
+        std::vector<unsigned int> ws((size_t)n_waves * 4);
+        KMLS_HIP(hipMemcpy(ws.data(), crumbs, ws.size() * sizeof(unsigned int), hipMemcpyDeviceToHost));
+        int hist[10] = {0};
+        for (int w = 0; w < n_waves; ++w) hist[std::min(9u, ws[4 * w])]++;
+        fprintf(stderr, "[dfs] waves: polling=%d expanding=%d retiring=%d exited=%d\n", hist[1],
+                hist[2], hist[3], hist[9]);
+      }
     }
+    if (h.timeout || h.aborted) throw std::runtime_error("kmls: persistent DFS kernel timed out");
+    if (h.bad_task) throw std::runtime_error("kmls: persistent DFS kernel read a corrupt task");
+    if (h.overflow) {
+      rows_hint = std::max<int64_t>(row_cap * 4, (int64_t)h.row_top * 2);
+      arena->pop_to(mark);
+      return false;
+    }
+    // compact the holes left by per-wave row chunks
+    const int64_t rows = (int64_t)h.row_top;
+    if (rows > 0) {
+      int64_t* pos = (int64_t*)arena->push((size_t)(rows + 1) * sizeof(int64_t));
+      const size_t tb = kern::dfs_compact_temp_bytes(rows);
+      void* tmp = arena->push(tb);
+      int64_t* par2 = (int64_t*)arena->push((size_t)rows * sizeof(int64_t));
+      int32_t* item2 = (int32_t*)arena->push((size_t)rows * sizeof(int32_t));
+      uint32_t* cnt2 = (uint32_t*)arena->push((size_t)rows * sizeof(uint32_t));
+      uint8_t* dep2 = (uint8_t*)arena->push((size_t)rows);
+      kern::dfs_compact(rows, out_size, out_parent.p, out_item.p, out_count.p, out_depth.p, pos,
+                        tmp, tb, par2, item2, cnt2, dep2, s);
+      const int64_t V = read_i64(pos + rows);
+      KMLS_HIP(hipMemcpyAsync(out_parent.p + out_size, par2, V * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(out_item.p + out_size, item2, V * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(out_count.p + out_size, cnt2, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(out_depth.p + out_size, dep2, V * sizeof(uint8_t), hipMemcpyDeviceToDevice, s));
+      out_size += V;
+    }
+    n_candidates += (int64_t)h.candidates;
+    max_depth = std::max<int>(max_depth, (int)h.max_depth);
+    rows_hint = std::max<int64_t>(rows_hint, rows + (rows >> 2));
     arena->pop_to(mark);
+    return true;
+  }
+
+  int64_t read_i64(const int64_t* dptr) {
+    KMLS_HIP(hipMemcpyAsync(h_scalar, dptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+    return h_scalar[0];
   }
 
   void process(const Level& L, int depth, const int64_t* len, int64_t total) {
     if (L.n < 2 || total == 0 || (max_len && depth >= max_len)) return;
-    if (persistent && depth >= 2) {
-      run_persistent(L, depth);
-      return;
-    }
+    if (persistent && depth >= 2 && run_persistent(L, depth)) return;
     const size_t mark0 = arena->mark();
     int64_t* cand_off = (int64_t*)arena->push((size_t)(L.n + 1) * sizeof(int64_t));
     const size_t tb = kern::scan_temp_bytes(L.n);

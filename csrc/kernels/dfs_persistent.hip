@@ -1,29 +1,35 @@
-// Persistent device-driven DFS over equivalence classes (levels >= 3 in ONE launch).
+// Persistent device-driven DFS over equivalence classes (all levels >= 3 in ONE launch).
 //
 // The level-wise driver (miner_gpu.hip) pays a host readback + ~7 launches per level chunk; on
-// the reference's ds2-shaped data the tree is 14 levels deep with ~1M tiny classes, so that
-// path is latency-bound (SURVEY §7.7 hard part 3).  Here every wave64 of a resident grid runs
-// a loop: pop a task from a device work queue, expand it, push the child classes.
+// the reference's ds2-shaped data the class tree is 14 levels deep with ~10^5-10^6 tiny
+// classes, so that path is latency-bound (SURVEY §7.7 hard part 3).  Here each wave64 of a
+// resident grid runs its own depth-first search:
 //
-//   task      = (class members' bitmaps/ranks/gids, class size n, itemset size, row range
-//               [a0,a1) of members to expand); big classes are split into row ranges so that a
-//               task holds <= kTaskCands candidates.
-//   expand a  = for b in (a, n): cnt = popcount(bits(a) & bits(b)) by TS-lane teams;
-//               pass 1 counts survivors (ballot), one atomicAdd reserves S rows (= S trie
-//               nodes), pass 2 recomputes and writes child bitmaps + node records, the child
-//               class of a (S >= 2) is pushed as new task(s).
-//   publish   = producer wave: plain stores of payload → s_waitcnt vmcnt(0) → agent-scope
-//               release fence → vmcnt(0) → relaxed agent atomic store of the slot's ready flag
+//   frame     = class members' bitmaps/ranks/gids + class size n + itemset size + next row a
+//               (+ row limit a1), kept on a per-wave LDS stack (kStack frames).
+//   expand a  = for b in (a, n): popcount(bits(a) & bits(b)) by TS-lane teams; pass 1 counts
+//               survivors (ballot), S rows are carved from the wave's private row chunk, pass 2
+//               recomputes and writes child bitmaps + trie-node records.  The child class of a
+//               (S >= 2) is pushed on the LOCAL stack (depth-first, no global traffic) ...
+//   share     = ... unless another wave is idle (`idle` counter, sampled every 16 rows) or the
+//               local stack is full: then it is published to the global queue, split into row
+//               ranges of <= kTaskCands candidates.  Publish: plain payload stores →
+//               s_waitcnt vmcnt(0) → agent-scope release → relaxed agent store of the slot flag;
+//               consume: lane 0 polls the flag (back-off), whole wave does an agent acquire
 //               (cdna_hip_programming.md §6 Guideline 16, recipe R1).
-//   consume   = lane 0 polls the flag relaxed (s_sleep back-off); whole wave executes an
-//               agent-scope acquire fence; then plain loads.
-//   terminate = `pending` counts published-but-unfinished tasks (children are added before the
-//               parent is retired), so pending == 0 ⇔ no task can ever appear again.  Every spin
-//               is bounded by a wall-clock timeout that sets an error flag.
-//   overflow  = row or task capacity exceeded → flag; the host re-runs with 4x capacity (the
-//               result is recomputed from scratch, so it stays exact).
+//   rows      = each wave reserves 256-row chunks from one counter (1 atomic per chunk, not per
+//               class); unused chunk tails leave holes (depth 0) that a scan + scatter pass
+//               removes afterwards, remapping parent ids (dfs_compact).
+//   terminate = `pending` counts published-but-unretired tasks; a task is retired only when the
+//               wave's local stack for it is empty, and shared children are counted before they
+//               are published, so pending == 0 ⇔ no work can ever appear again.  Every spin is
+//               bounded (clock + poll count) and a host watchdog can raise a mapped abort flag.
+//   overflow  = row/task capacity exhausted → flag; the host falls back to the level-wise path
+//               (exact), so capacity only affects speed.
+// Hot counters live on separate 128-byte lines; per-wave statistics are reduced in registers.
 #include <hip/hip_runtime.h>
 
+#include <hipcub/hipcub.hpp>
 #include <stdexcept>
 #include <string>
 
@@ -34,8 +40,10 @@ namespace kern {
 
 namespace {
 
-constexpr int kWaves = 4;             // waves per workgroup
-constexpr int kTaskCands = 4096;      // max candidates per task (row-range split)
+constexpr int kWaves = 4;          // waves per workgroup
+constexpr int kStack = 24;         // local DFS frames per wave
+constexpr int kTaskCands = 4096;   // max candidates per shared task (row-range split)
+constexpr unsigned kRowChunk = 256;
 
 __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -73,7 +81,7 @@ __device__ __forceinline__ bool host_abort(const Ctx& cx) {
 
 __device__ __forceinline__ void crumb(const Ctx& cx, int gw, int lane, unsigned st, unsigned a,
                                       unsigned b, unsigned c) {
-  if (lane == 0 && cx.wave_state) {
+  if (cx.wave_state != nullptr && lane == 0) {
     __hip_atomic_store(&cx.wave_state[4 * gw + 0], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&cx.wave_state[4 * gw + 1], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&cx.wave_state[4 * gw + 2], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -81,31 +89,29 @@ __device__ __forceinline__ void crumb(const Ctx& cx, int gw, int lane, unsigned 
   }
 }
 
-// Split a class into row-range tasks and publish them.  Called by ONE wave; lane 0 does the
-// bookkeeping (classes larger than a task are rare).  Payload (child bitmaps, ranks, gids) was
-// written by this same wave before the call.
-__device__ void push_class(const Ctx& cx, const unsigned long long* bm, const int32_t* rank,
-                           const int64_t* gid, int n, int depth, int lane) {
-  if (lane != 0) return;
-  // count tasks
+__device__ __forceinline__ int count_tasks(int n) {
   int n_tasks = 0;
-  {
-    long long acc = 0;
-    for (int a = 0; a < n - 1; ++a) {
-      const long long m = n - a - 1;
-      if (acc > 0 && acc + m > kTaskCands) { ++n_tasks; acc = 0; }
-      acc += m;
-    }
-    if (acc > 0) ++n_tasks;
+  long long acc = 0;
+  for (int a = 0; a < n - 1; ++a) {
+    const long long m = n - a - 1;
+    if (acc > 0 && acc + m > kTaskCands) { ++n_tasks; acc = 0; }
+    acc += m;
   }
-  if (n_tasks == 0) return;
+  return n_tasks + (acc > 0 ? 1 : 0);
+}
+
+// Publish a class to the global queue as row-range tasks.  Lane 0 only; the payload (child
+// bitmaps, ranks, gids) was written by this wave before the call.  Returns false on overflow.
+__device__ bool share_class(const Ctx& cx, const unsigned long long* bm, const int32_t* rank,
+                            const int64_t* gid, int n, int depth) {
+  const int n_tasks = count_tasks(n);
+  if (n_tasks == 0) return true;
   atomicAdd(&cx.ctl->pending, (unsigned long long)n_tasks);
   const unsigned long long base = atomicAdd(&cx.ctl->q_tail, (unsigned long long)n_tasks);
   if (base + n_tasks > (unsigned long long)cx.task_cap) {
     atomicOr(&cx.ctl->overflow, 2u);
     atomicAdd(&cx.ctl->pending, (unsigned long long)(-(long long)n_tasks));
-    // slots beyond capacity are never published; waiters exit through pending == 0
-    return;
+    return false;
   }
   int t = 0, a0 = 0;
   long long acc = 0;
@@ -118,12 +124,12 @@ __device__ void push_class(const Ctx& cx, const unsigned long long* bm, const in
     acc += m;
   }
   cx.tasks[base + t] = DfsTask{bm, rank, gid, n, depth, a0, n - 1};
-  // publish: drain this wave's stores (payload + records), release at agent scope, then flags
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int i = 0; i < n_tasks; ++i)
     __hip_atomic_store(&cx.ready[base + i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
 }
 
 template <int TS>
@@ -139,97 +145,110 @@ __device__ __forceinline__ uint32_t team_and_popcount(const ulonglong2* x, const
   return s;
 }
 
+struct WaveState {  // per-wave registers (uniform)
+  unsigned long long row_next, row_end;  // private row chunk [row_next, row_end)
+  unsigned long long cands;
+  unsigned max_depth;
+  unsigned rows_since_probe;
+  bool share_hint;
+  bool dead;                             // overflow: stop producing
+};
+
+// Expand row a of frame f.  Returns (row0, S) of the child class (S = 0: none).
 template <int TS>
-__device__ void expand_task(const Ctx& cx, const DfsTask& tk, int lane) {
-  constexpr int TPW = 64 / TS;  // teams per wave
-  const int tl = lane & (TS - 1);
-  const int team = lane / TS;
-  const unsigned long long leader_mask = [] {
+__device__ void expand_row(const Ctx& cx, const DfsTask& f, int a, int lane, WaveState& ws,
+                           unsigned long long& row0_out, unsigned& S_out) {
+  constexpr int TPW = 64 / TS;
+  constexpr unsigned long long kLeaders = [] {
     unsigned long long m = 0;
     for (int i = 0; i < 64; i += TS) m |= 1ull << i;
     return m;
   }();
+  const int tl = lane & (TS - 1);
+  const int team = lane / TS;
   const int64_t Wp = cx.Wp, n2 = Wp >> 1;
-  const int n = tk.n;
-  unsigned long long cands = 0;
-  for (int a = tk.a0; a < tk.a1; ++a) {
-    int ab = 0;
-    if (lane == 0) ab = host_abort(cx) ? 1 : 0;
-    if (__shfl(ab, 0)) break;
-    const ulonglong2* xa = reinterpret_cast<const ulonglong2*>(tk.bm + (int64_t)a * Wp);
-    // pass 1: survivor count
-    uint32_t S = 0;
-    for (int g = a + 1; g < n; g += TPW) {
-      const int b = g + team;
-      uint32_t c = 0;
-      if (b < n) c = team_and_popcount<TS>(xa, reinterpret_cast<const ulonglong2*>(tk.bm + (int64_t)b * Wp), n2, tl);
-      const bool pass = (b < n) && c >= cx.minsup;
-      S += (uint32_t)__popcll(__ballot(pass) & leader_mask);
-    }
-    cands += (unsigned long long)(n - a - 1);
-    if (S == 0) continue;
-    unsigned long long row0 = 0;
-    if (lane == 0) row0 = atomicAdd(&cx.ctl->row_top, (unsigned long long)S);
-    row0 = __shfl(row0, 0);
-    if (row0 + S > (unsigned long long)cx.row_cap) {
-      if (lane == 0) atomicOr(&cx.ctl->overflow, 1u);
-      continue;
-    }
-    // pass 2: recompute, compact by ballot prefix, write child rows + trie nodes
-    uint32_t j0 = 0;
-    const int64_t gid_a = tk.gid[a];
-    for (int g = a + 1; g < n; g += TPW) {
-      const int b = g + team;
-      uint32_t c = 0;
-      if (b < n) c = team_and_popcount<TS>(xa, reinterpret_cast<const ulonglong2*>(tk.bm + (int64_t)b * Wp), n2, tl);
-      const bool pass = (b < n) && c >= cx.minsup;
-      const unsigned long long bal = __ballot(pass) & leader_mask;
-      const int leader = lane - tl;
-      const uint32_t j = j0 + (uint32_t)__popcll(bal & ((1ull << leader) - 1ull));
-      if (pass) {
-        const int64_t row = (int64_t)row0 + j;
-        const ulonglong2* yb = reinterpret_cast<const ulonglong2*>(tk.bm + (int64_t)b * Wp);
-        ulonglong2* z = reinterpret_cast<ulonglong2*>(cx.pool_bm + row * Wp);
-        for (int64_t w = tl; w < n2; w += TS) {
-          const ulonglong2 u = xa[w], v = yb[w];
-          z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
-        }
-        if (tl == 0) {
-          const int32_t rb = tk.rank[b];
-          cx.pool_rank[row] = rb;
-          cx.pool_gid[row] = cx.out_base + row;
-          cx.out_parent[cx.out_base + row] = gid_a;
-          cx.out_item[cx.out_base + row] = cx.ids[rb];
-          cx.out_count[cx.out_base + row] = c;
-          cx.out_depth[cx.out_base + row] = (uint8_t)(tk.depth + 1);
-        }
-      }
-      j0 += (uint32_t)__popcll(bal);
-    }
-    if (lane == 0) atomicMax(&cx.ctl->max_depth, (unsigned int)(tk.depth + 1));
-    if (S >= 2 && (cx.max_len == 0 || tk.depth + 1 < cx.max_len))
-      push_class(cx, cx.pool_bm + (int64_t)row0 * Wp, cx.pool_rank + row0, cx.pool_gid + row0,
-                 (int)S, tk.depth + 1, lane);
+  const int n = f.n;
+  const ulonglong2* xa = reinterpret_cast<const ulonglong2*>(f.bm + (int64_t)a * Wp);
+  unsigned S = 0;
+  for (int g = a + 1; g < n; g += TPW) {  // pass 1
+    const int b = g + team;
+    uint32_t c = 0;
+    if (b < n) c = team_and_popcount<TS>(xa, reinterpret_cast<const ulonglong2*>(f.bm + (int64_t)b * Wp), n2, tl);
+    S += (unsigned)__popcll(__ballot((b < n) && c >= cx.minsup) & kLeaders);
   }
-  if (lane == 0) atomicAdd(&cx.ctl->candidates, cands);
+  ws.cands += (unsigned long long)(n - a - 1);
+  S_out = 0;
+  if (S == 0 || ws.dead) return;
+  // carve S contiguous rows from the private chunk (refill: 1 atomic per chunk)
+  if (ws.row_next + S > ws.row_end) {
+    const unsigned take = S > kRowChunk ? S : kRowChunk;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&cx.ctl->row_top, (unsigned long long)take);
+    base = __shfl(base, 0);
+    if (base + take > (unsigned long long)cx.row_cap) {
+      if (lane == 0) atomicOr(&cx.ctl->overflow, 1u);
+      ws.dead = true;
+      return;
+    }
+    ws.row_next = base;
+    ws.row_end = base + take;
+  }
+  const unsigned long long row0 = ws.row_next;
+  ws.row_next += S;
+  unsigned j0 = 0;
+  const int64_t gid_a = f.gid[a];
+  const uint8_t dchild = (uint8_t)(f.depth + 1);
+  for (int g = a + 1; g < n; g += TPW) {  // pass 2
+    const int b = g + team;
+    uint32_t c = 0;
+    const ulonglong2* yb = reinterpret_cast<const ulonglong2*>(f.bm + (int64_t)b * Wp);
+    if (b < n) c = team_and_popcount<TS>(xa, yb, n2, tl);
+    const bool pass = (b < n) && c >= cx.minsup;
+    const unsigned long long bal = __ballot(pass) & kLeaders;
+    if (pass) {
+      const int leader = lane - tl;
+      const int64_t row = (int64_t)row0 + j0 + (unsigned)__popcll(bal & ((1ull << leader) - 1ull));
+      ulonglong2* z = reinterpret_cast<ulonglong2*>(cx.pool_bm + row * Wp);
+      for (int64_t w = tl; w < n2; w += TS) {
+        const ulonglong2 u = xa[w], v = yb[w];
+        z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
+      }
+      if (tl == 0) {
+        const int32_t rb = f.rank[b];
+        cx.pool_rank[row] = rb;
+        cx.pool_gid[row] = cx.out_base + row;
+        cx.out_parent[cx.out_base + row] = gid_a;
+        cx.out_item[cx.out_base + row] = cx.ids[rb];
+        cx.out_count[cx.out_base + row] = c;
+        cx.out_depth[cx.out_base + row] = dchild;
+      }
+    }
+    j0 += (unsigned)__popcll(bal);
+  }
+  if (dchild > ws.max_depth) ws.max_depth = dchild;
+  row0_out = row0;
+  S_out = S;
 }
 
 template <int TS>
 __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
+  __shared__ DfsTask stack_all[kWaves][kStack];
   const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
   const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  DfsTask* stack = stack_all[wid];
   const unsigned long long t_start = wall_clock64();
   unsigned long long polls = 0;
+  WaveState ws{0, 0, 0, 0, 0, false, false};
   while (true) {
+    // ---- get a task from the global queue -------------------------------------------------
     unsigned long long idx = 0;
-    if (lane == 0) idx = atomicAdd(&cx.ctl->q_head, 1ull);
+    if (lane == 0) {
+      idx = atomicAdd(&cx.ctl->q_head, 1ull);
+      atomicAdd(&cx.ctl->idle, 1u);
+    }
     idx = __shfl(idx, 0);
     crumb(cx, gw, lane, 1u, (unsigned)idx, 0u, 0u);
-    // wait until slot idx is published, or until no task can ever be published again
-    // Back-off polling: 2k waves re-reading the hot `ready`/`pending` lines (which producers
-    // update with atomics) at full rate starve the producers' atomics; the first version of
-    // this loop made no progress at all.  Poll the slot every iteration with a growing sleep,
-    // check termination every 8th and the host abort flag / clock every 256th poll.
     bool got = false;
     unsigned it = 0;
     while (true) {
@@ -258,23 +277,72 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
       else __builtin_amdgcn_s_sleep(32);
       ++it;
     }
-    if (!got) {
-      crumb(cx, gw, lane, 9u, (unsigned)idx, 0u, 0u);
-      if (lane == 0) atomicAdd(&cx.ctl->exited, 1u);
-      return;
-    }
+    if (lane == 0) atomicSub(&cx.ctl->idle, 1u);
+    if (!got) break;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const DfsTask tk = cx.tasks[idx];
-    crumb(cx, gw, lane, 2u, (unsigned)idx, (unsigned)tk.n, (unsigned)tk.a1);
-    if (tk.n < 2 || tk.n > (1 << 24) || tk.a0 < 0 || tk.a1 > tk.n - 1 || tk.a0 > tk.a1 ||
-        tk.bm == nullptr) {
+    const DfsTask root = cx.tasks[idx];
+    crumb(cx, gw, lane, 2u, (unsigned)idx, (unsigned)root.n, (unsigned)root.a1);
+    if (root.n < 2 || root.n > (1 << 24) || root.a0 < 0 || root.a1 > root.n - 1 ||
+        root.a0 > root.a1 || root.bm == nullptr) {
       if (lane == 0) atomicOr(&cx.ctl->bad_task, 1u);
     } else {
-      expand_task<TS>(cx, tk, lane);
+      // ---- local depth-first search rooted at the task ----------------------------------
+      // The stack is wave-private LDS: lane 0 writes a frame, every lane reads it after the
+      // wave barrier (LDS ops of one wave complete in order, the barrier orders the compiler).
+      if (lane == 0) stack[0] = root;
+      int top = 1;
+      bool aborted = false;
+      while (top > 0 && !aborted) {
+        __builtin_amdgcn_wave_barrier();
+        const DfsTask f = stack[top - 1];
+        __builtin_amdgcn_wave_barrier();
+        if (f.a0 >= f.a1) { --top; continue; }
+        const int a = f.a0;
+        if (lane == 0) stack[top - 1].a0 = a + 1;
+        if (++ws.rows_since_probe >= 16) {
+          ws.rows_since_probe = 0;
+          int probe = 0;
+          if (lane == 0) {
+            probe = ld_relaxed(&cx.ctl->idle) > 0u ? 1 : 0;
+            if (host_abort(cx)) probe = 2;
+          }
+          probe = __shfl(probe, 0);
+          if (probe == 2) {
+            aborted = true;
+            if (lane == 0) atomicOr(&cx.ctl->aborted, 1u);
+            break;
+          }
+          ws.share_hint = probe == 1;
+        }
+        unsigned long long row0 = 0;
+        unsigned S = 0;
+        expand_row<TS>(cx, f, a, lane, ws, row0, S);
+        if (S >= 2 && (cx.max_len == 0 || f.depth + 1 < cx.max_len)) {
+          const unsigned long long* cbm = cx.pool_bm + row0 * cx.Wp;
+          const int32_t* crk = cx.pool_rank + row0;
+          const int64_t* cgd = cx.pool_gid + row0;
+          if (ws.share_hint || top >= kStack) {
+            int ok = 1;
+            if (lane == 0) ok = share_class(cx, cbm, crk, cgd, (int)S, f.depth + 1) ? 1 : 0;
+            ok = __shfl(ok, 0);
+            if (!ok) ws.dead = true;
+            ws.share_hint = false;  // re-probe before sharing again
+          } else {
+            // child rows were written by this wave: its own later loads see them in order
+            if (lane == 0) stack[top] = DfsTask{cbm, crk, cgd, (int)S, f.depth + 1, 0, (int)S - 1};
+            ++top;
+          }
+        }
+      }
     }
     crumb(cx, gw, lane, 3u, (unsigned)idx, 0u, 0u);
-    // retire: children (if any) were added to pending inside expand_task
     if (lane == 0) atomicAdd(&cx.ctl->pending, (unsigned long long)(-1ll));
+  }
+  crumb(cx, gw, lane, 9u, 0u, 0u, 0u);
+  if (lane == 0) {
+    atomicAdd(&cx.ctl->candidates, ws.cands);
+    atomicMax(&cx.ctl->max_depth, ws.max_depth);
+    atomicAdd(&cx.ctl->exited, 1u);
   }
 }
 
@@ -290,14 +358,7 @@ __global__ void k_dfs_seed(const unsigned long long* __restrict__ bm, const int3
     if (s > 0 && row_end[s - 1] != s) continue;  // not a class start
     const int n = (int)(row_end[s] - s);
     if (n < 2) continue;
-    int n_tasks = 0;
-    long long acc = 0;
-    for (int a = 0; a < n - 1; ++a) {
-      const long long m = n - a - 1;
-      if (acc > 0 && acc + m > kTaskCands) { ++n_tasks; acc = 0; }
-      acc += m;
-    }
-    if (acc > 0) ++n_tasks;
+    const int n_tasks = count_tasks(n);
     atomicAdd(&ctl->pending, (unsigned long long)n_tasks);
     const unsigned long long base = atomicAdd(&ctl->q_tail, (unsigned long long)n_tasks);
     if (base + n_tasks > (unsigned long long)task_cap) {
@@ -307,7 +368,7 @@ __global__ void k_dfs_seed(const unsigned long long* __restrict__ bm, const int3
     }
     const unsigned long long* cbm = bm + s * Wp;
     int t = 0, a0 = 0;
-    acc = 0;
+    long long acc = 0;
     for (int a = 0; a < n - 1; ++a) {
       const long long m = n - a - 1;
       if (acc > 0 && acc + m > kTaskCands) {
@@ -322,6 +383,33 @@ __global__ void k_dfs_seed(const unsigned long long* __restrict__ bm, const int3
   }
 }
 
+// ---- hole compaction ---------------------------------------------------------------------
+struct ValidOp {
+  const uint8_t* depth;
+  int64_t n;
+  __host__ __device__ int64_t operator()(int64_t i) const { return (i < n && depth[i] != 0) ? 1 : 0; }
+};
+using ValidIt = hipcub::TransformInputIterator<int64_t, ValidOp, hipcub::CountingInputIterator<int64_t>>;
+
+__global__ void k_dfs_scatter(const int64_t* __restrict__ pos, int64_t rows, int64_t out_base,
+                              const int64_t* __restrict__ par, const int32_t* __restrict__ item,
+                              const uint32_t* __restrict__ cnt, const uint8_t* __restrict__ dep,
+                              int64_t* __restrict__ par2, int32_t* __restrict__ item2,
+                              uint32_t* __restrict__ cnt2, uint8_t* __restrict__ dep2) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += nthr) {
+    const uint8_t d = dep[r];
+    if (d == 0) continue;
+    const int64_t k = pos[r];
+    int64_t p = par[r];
+    if (p >= out_base) p = out_base + pos[p - out_base];  // parent inside the DFS region
+    par2[k] = p;
+    item2[k] = item[r];
+    cnt2[k] = cnt[r];
+    dep2[k] = d;
+  }
+}
+
 int team_size_for(int64_t Wp) {
   const int64_t chunks = Wp >> 1;
   if (chunks >= 128) return 64;
@@ -331,13 +419,16 @@ int team_size_for(int64_t Wp) {
   return 4;
 }
 
+void check(hipError_t e) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e));
+}
+
 }  // namespace
 
 void dfs_persistent(const DfsArgs& a, hipStream_t s) {
   Ctx cx{a.tasks, a.ready, a.ctl, (unsigned long long*)a.pool_bm, a.pool_rank, a.pool_gid,
          a.out_parent, a.out_item, a.out_count, a.out_depth, a.ids, a.out_base, a.Wp, a.row_cap,
          a.task_cap, a.minsup, a.max_len, a.timeout_ticks, a.abort_flag, a.wave_state};
-  // seed
   const int64_t nr = a.seed_rows;
   const int sg = (int)std::min<int64_t>(std::max<int64_t>((nr + 255) / 256, 1), 4096);
   hipLaunchKernelGGL(k_dfs_seed, dim3(sg), dim3(256), 0, s, (const unsigned long long*)a.seed_bm,
@@ -352,8 +443,27 @@ void dfs_persistent(const DfsArgs& a, hipStream_t s) {
     case 32: hipLaunchKernelGGL(k_dfs_persistent<32>, grid, block, 0, s, cx); break;
     default: hipLaunchKernelGGL(k_dfs_persistent<64>, grid, block, 0, s, cx); break;
   }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e));
+  check(hipGetLastError());
+}
+
+size_t dfs_compact_temp_bytes(int64_t rows) {
+  size_t bytes = 0;
+  ValidIt it(hipcub::CountingInputIterator<int64_t>(0), ValidOp{nullptr, rows});
+  check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (int64_t*)nullptr, (int)(rows + 1)));
+  return bytes;
+}
+
+void dfs_compact(int64_t rows, int64_t out_base, int64_t* par, int32_t* item, uint32_t* cnt,
+                 uint8_t* dep, int64_t* pos, void* temp, size_t temp_bytes, int64_t* par2,
+                 int32_t* item2, uint32_t* cnt2, uint8_t* dep2, hipStream_t s) {
+  // pos has rows+1 entries; pos[rows] = number of valid nodes
+  ValidIt it(hipcub::CountingInputIterator<int64_t>(0), ValidOp{dep + out_base, rows});
+  check(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, it, pos, (int)(rows + 1), s));
+  const int g = (int)std::min<int64_t>(std::max<int64_t>((rows + 255) / 256, 1), 8192);
+  hipLaunchKernelGGL(k_dfs_scatter, dim3(g), dim3(256), 0, s, pos, rows, out_base,
+                     par + out_base, item + out_base, cnt + out_base, dep + out_base, par2, item2,
+                     cnt2, dep2);
+  check(hipGetLastError());
 }
 
 }  // namespace kern

@@ -61,9 +61,14 @@ struct DfsTask {
   const int64_t* gid;            // members' global trie node ids
   int32_t n, depth, a0, a1;      // class size, members' itemset size, rows [a0, a1) to expand
 };
-struct DfsCtl {  // zeroed before every launch
-  unsigned long long q_head, q_tail, pending, row_top, candidates;
-  unsigned int overflow, timeout, max_depth, bad_task, aborted, exited, pad0, pad1;
+struct DfsCtl {  // zeroed before every launch; hot counters on separate 128-byte lines
+  unsigned long long q_head;     char pad0[120];
+  unsigned long long q_tail;     char pad1[120];
+  unsigned long long pending;    char pad2[120];
+  unsigned long long row_top;    char pad3[120];
+  unsigned int idle;             char pad4[124];
+  unsigned long long candidates;
+  unsigned int overflow, timeout, max_depth, bad_task, aborted, exited;
 };
 struct DfsArgs {
   // seed level (classes = runs of equal row_end)
@@ -98,6 +103,12 @@ struct DfsArgs {
   unsigned int* wave_state;          // per-wave breadcrumbs (debug): [state, idx_lo, a, n]
 };
 void dfs_persistent(const DfsArgs& a, hipStream_t s);
+// remove unused-row holes of the DFS region [out_base, out_base+rows): pos[rows+1] scan,
+// compacted copies into par2/item2/cnt2/dep2 (parents inside the region remapped)
+size_t dfs_compact_temp_bytes(int64_t rows);
+void dfs_compact(int64_t rows, int64_t out_base, int64_t* par, int32_t* item, uint32_t* cnt,
+                 uint8_t* dep, int64_t* pos, void* temp, size_t temp_bytes, int64_t* par2,
+                 int32_t* item2, uint32_t* cnt2, uint8_t* dep2, hipStream_t s);
 
 // ---- serving (serve.hip) ----
 void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,
