@@ -199,7 +199,7 @@ struct MineRun {
     const size_t mark = arena->mark();
     const int64_t task_cap_min = L.n + 4096;
     // bytes per pool row: bitmap + rank + gid + compaction (pos + 4 staged outputs)
-    const int64_t per_row = Wp * 8 + 4 + 8 + 8 + 17;
+    const int64_t per_row = Wp * 8 + 4 + 8 + 17 + 25 + 16;  // pool + staged outputs + sort
     const int64_t avail = (int64_t)(arena->capacity() - arena->used()) - (64ll << 20) -
                           task_cap_min * (int64_t)(sizeof(kern::DfsTask) + 4);
     int64_t row_cap = std::max<int64_t>(rows_hint, 1 << 20);
@@ -300,16 +300,15 @@ struct MineRun {
     // compact the holes left by per-wave row chunks
     const int64_t rows = (int64_t)h.row_top;
     if (rows > 0) {
-      int64_t* pos = (int64_t*)arena->push((size_t)(rows + 1) * sizeof(int64_t));
       const size_t tb = kern::dfs_compact_temp_bytes(rows);
       void* tmp = arena->push(tb);
       int64_t* par2 = (int64_t*)arena->push((size_t)rows * sizeof(int64_t));
       int32_t* item2 = (int32_t*)arena->push((size_t)rows * sizeof(int32_t));
       uint32_t* cnt2 = (uint32_t*)arena->push((size_t)rows * sizeof(uint32_t));
       uint8_t* dep2 = (uint8_t*)arena->push((size_t)rows);
-      kern::dfs_compact(rows, out_size, out_parent.p, out_item.p, out_count.p, out_depth.p, pos,
-                        tmp, tb, par2, item2, cnt2, dep2, s);
-      const int64_t V = read_i64(pos + rows);
+      const int64_t V = kern::dfs_compact(rows, out_size, out_parent.p, out_item.p, out_count.p,
+                                          out_depth.p, tmp, tb, par2, item2, cnt2, dep2,
+                                          (unsigned long long*)h_scalar, s);
       KMLS_HIP(hipMemcpyAsync(out_parent.p + out_size, par2, V * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
       KMLS_HIP(hipMemcpyAsync(out_item.p + out_size, item2, V * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
       KMLS_HIP(hipMemcpyAsync(out_count.p + out_size, cnt2, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));

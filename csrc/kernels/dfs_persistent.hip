@@ -13,10 +13,16 @@
 //               (S >= 2) is pushed on the LOCAL stack (depth-first, no global traffic) ...
 //   share     = ... unless another wave is idle (`idle` counter, sampled every 16 rows) or the
 //               local stack is full: then it is published to the global queue, split into row
-//               ranges of <= kTaskCands candidates.  Publish: plain payload stores →
-//               s_waitcnt vmcnt(0) → agent-scope release → relaxed agent store of the slot flag;
-//               consume: lane 0 polls the flag (back-off), whole wave does an agent acquire
-//               (cdna_hip_programming.md §6 Guideline 16, recipe R1).
+//               ranges of <= kTaskCands candidates.
+//   coherence = FENCE-FREE (cdna_hip_programming.md §6 G16, the sc1 form of recipe R1): every
+//               pool write (child bitmaps, ranks, gids, task records) is a write-through sc1
+//               store; a wave drains them (s_waitcnt vmcnt(0)) before raising a slot flag (sc1
+//               store); a consumer polls the flag with sc1 loads and reads a POPPED class with
+//               sc1 loads only.  Classes a wave produced itself are read with plain 16-B loads
+//               (same wave, same XCD L2).  Agent-scope fences would write back / invalidate the
+//               whole XCD L2 per task — the first version of this kernel spent 97% of its time
+//               there.  Row chunks are 16-row aligned so no 128-B line holds rows of two
+//               writers.
 //   rows      = each wave reserves 256-row chunks from one counter (1 atomic per chunk, not per
 //               class); unused chunk tails leave holes (depth 0) that a scan + scatter pass
 //               removes afterwards, remapping parent ids (dfs_compact).
@@ -50,6 +56,39 @@ __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long lon
 }
 __device__ __forceinline__ unsigned int ld_relaxed(const unsigned int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(unsigned int* p, unsigned int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Task records as 5 x 8-byte words (sc1 stores / loads).
+__device__ __forceinline__ void store_task(DfsTask* t, const DfsTask& v) {
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(t);
+  st_sc1(w + 0, (unsigned long long)v.bm);
+  st_sc1(w + 1, (unsigned long long)v.rank);
+  st_sc1(w + 2, (unsigned long long)v.gid);
+  st_sc1(w + 3, (unsigned long long)(unsigned)v.n | ((unsigned long long)(unsigned)v.depth << 32));
+  st_sc1(w + 4, (unsigned long long)(unsigned)v.a0 | ((unsigned long long)(unsigned)v.a1 << 32));
+}
+__device__ __forceinline__ DfsTask load_task(const DfsTask* t) {
+  const unsigned long long* w = reinterpret_cast<const unsigned long long*>(t);
+  DfsTask v;
+  v.bm = (const unsigned long long*)ld_sc1(w + 0);
+  v.rank = (const int32_t*)ld_sc1(w + 1);
+  v.gid = (const int64_t*)ld_sc1(w + 2);
+  const unsigned long long nd = ld_sc1(w + 3), aa = ld_sc1(w + 4);
+  v.n = (int32_t)(unsigned)(nd & 0xFFFFFFFFu);
+  v.depth = (int32_t)(unsigned)(nd >> 32);
+  v.a0 = (int32_t)(unsigned)(aa & 0xFFFFFFFFu);
+  v.a1 = (int32_t)(unsigned)(aa >> 32);
+  return v;
 }
 
 struct Ctx {
@@ -118,17 +157,16 @@ __device__ bool share_class(const Ctx& cx, const unsigned long long* bm, const i
   for (int a = 0; a < n - 1; ++a) {
     const long long m = n - a - 1;
     if (acc > 0 && acc + m > kTaskCands) {
-      cx.tasks[base + t] = DfsTask{bm, rank, gid, n, depth, a0, a};
+      store_task(&cx.tasks[base + t], DfsTask{bm, rank, gid, n, depth, a0, a});
       ++t; a0 = a; acc = 0;
     }
     acc += m;
   }
-  cx.tasks[base + t] = DfsTask{bm, rank, gid, n, depth, a0, n - 1};
+  store_task(&cx.tasks[base + t], DfsTask{bm, rank, gid, n, depth, a0, n - 1});
+  // payload (written through by the whole wave before this call) + records are performed
+  // once this wave's vmcnt drains; then the flags
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (int i = 0; i < n_tasks; ++i)
-    __hip_atomic_store(&cx.ready[base + i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = 0; i < n_tasks; ++i) st_sc1(&cx.ready[base + i], 1u);
   return true;
 }
 
@@ -145,6 +183,17 @@ __device__ __forceinline__ uint32_t team_and_popcount(const ulonglong2* x, const
   return s;
 }
 
+template <int TS>
+__device__ __forceinline__ uint32_t team_and_popcount_sc1(const unsigned long long* x,
+                                                          const unsigned long long* y,
+                                                          int64_t Wp, int tl) {
+  uint32_t s = 0;
+  for (int64_t w = tl; w < Wp; w += TS) s += (uint32_t)__popcll(ld_sc1(x + w) & ld_sc1(y + w));
+#pragma unroll
+  for (int off = TS >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, TS);
+  return s;
+}
+
 struct WaveState {  // per-wave registers (uniform)
   unsigned long long row_next, row_end;  // private row chunk [row_next, row_end)
   unsigned long long cands;
@@ -154,8 +203,9 @@ struct WaveState {  // per-wave registers (uniform)
   bool dead;                             // overflow: stop producing
 };
 
-// Expand row a of frame f.  Returns (row0, S) of the child class (S = 0: none).
-template <int TS>
+// Expand row a of frame f.  Returns (row0, S) of the child class (S = 0: none).  REMOTE frames
+// (popped from the queue) read their class through sc1 loads; local frames with plain loads.
+template <int TS, bool REMOTE>
 __device__ void expand_row(const Ctx& cx, const DfsTask& f, int a, int lane, WaveState& ws,
                            unsigned long long& row0_out, unsigned& S_out) {
   constexpr int TPW = 64 / TS;
@@ -168,20 +218,28 @@ __device__ void expand_row(const Ctx& cx, const DfsTask& f, int a, int lane, Wav
   const int team = lane / TS;
   const int64_t Wp = cx.Wp, n2 = Wp >> 1;
   const int n = f.n;
-  const ulonglong2* xa = reinterpret_cast<const ulonglong2*>(f.bm + (int64_t)a * Wp);
+  const unsigned long long* xa8 = f.bm + (int64_t)a * Wp;
+  const ulonglong2* xa = reinterpret_cast<const ulonglong2*>(xa8);
+  auto pc = [&](int b) -> uint32_t {
+    const unsigned long long* y8 = f.bm + (int64_t)b * Wp;
+    if constexpr (REMOTE) return team_and_popcount_sc1<TS>(xa8, y8, Wp, tl);
+    else return team_and_popcount<TS>(xa, reinterpret_cast<const ulonglong2*>(y8), n2, tl);
+  };
   unsigned S = 0;
   for (int g = a + 1; g < n; g += TPW) {  // pass 1
     const int b = g + team;
     uint32_t c = 0;
-    if (b < n) c = team_and_popcount<TS>(xa, reinterpret_cast<const ulonglong2*>(f.bm + (int64_t)b * Wp), n2, tl);
+    if (b < n) c = pc(b);
     S += (unsigned)__popcll(__ballot((b < n) && c >= cx.minsup) & kLeaders);
   }
   ws.cands += (unsigned long long)(n - a - 1);
   S_out = 0;
   if (S == 0 || ws.dead) return;
-  // carve S contiguous rows from the private chunk (refill: 1 atomic per chunk)
+  // carve S contiguous rows from the private chunk (refill: 1 atomic per chunk; chunks are
+  // multiples of 16 rows so chunk boundaries are 128-byte aligned in every pool array)
   if (ws.row_next + S > ws.row_end) {
-    const unsigned take = S > kRowChunk ? S : kRowChunk;
+    unsigned take = S > kRowChunk ? S : kRowChunk;
+    take = (take + 31u) & ~31u;
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(&cx.ctl->row_top, (unsigned long long)take);
     base = __shfl(base, 0);
@@ -196,27 +254,35 @@ __device__ void expand_row(const Ctx& cx, const DfsTask& f, int a, int lane, Wav
   const unsigned long long row0 = ws.row_next;
   ws.row_next += S;
   unsigned j0 = 0;
-  const int64_t gid_a = f.gid[a];
+  int64_t gid_a;
+  if constexpr (REMOTE) gid_a = (int64_t)ld_sc1(reinterpret_cast<const unsigned long long*>(f.gid + a));
+  else gid_a = f.gid[a];
   const uint8_t dchild = (uint8_t)(f.depth + 1);
   for (int g = a + 1; g < n; g += TPW) {  // pass 2
     const int b = g + team;
     uint32_t c = 0;
-    const ulonglong2* yb = reinterpret_cast<const ulonglong2*>(f.bm + (int64_t)b * Wp);
-    if (b < n) c = team_and_popcount<TS>(xa, yb, n2, tl);
+    if (b < n) c = pc(b);
     const bool pass = (b < n) && c >= cx.minsup;
     const unsigned long long bal = __ballot(pass) & kLeaders;
     if (pass) {
       const int leader = lane - tl;
       const int64_t row = (int64_t)row0 + j0 + (unsigned)__popcll(bal & ((1ull << leader) - 1ull));
-      ulonglong2* z = reinterpret_cast<ulonglong2*>(cx.pool_bm + row * Wp);
-      for (int64_t w = tl; w < n2; w += TS) {
-        const ulonglong2 u = xa[w], v = yb[w];
-        z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
+      const unsigned long long* y8 = f.bm + (int64_t)b * Wp;
+      unsigned long long* z = cx.pool_bm + row * Wp;
+      for (int64_t w = tl; w < Wp; w += TS) {  // write-through child bitmap
+        unsigned long long u, v;
+        if constexpr (REMOTE) { u = ld_sc1(xa8 + w); v = ld_sc1(y8 + w); }
+        else { u = xa8[w]; v = y8[w]; }
+        st_sc1(z + w, u & v);
       }
       if (tl == 0) {
-        const int32_t rb = f.rank[b];
-        cx.pool_rank[row] = rb;
-        cx.pool_gid[row] = cx.out_base + row;
+        int32_t rb;
+        if constexpr (REMOTE)
+          rb = (int32_t)__hip_atomic_load(f.rank + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else rb = f.rank[b];
+        st_sc1(reinterpret_cast<unsigned int*>(cx.pool_rank + row), (unsigned)rb);
+        st_sc1(reinterpret_cast<unsigned long long*>(cx.pool_gid + row),
+               (unsigned long long)(cx.out_base + row));
         cx.out_parent[cx.out_base + row] = gid_a;
         cx.out_item[cx.out_base + row] = cx.ids[rb];
         cx.out_count[cx.out_base + row] = c;
@@ -279,8 +345,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
     }
     if (lane == 0) atomicSub(&cx.ctl->idle, 1u);
     if (!got) break;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const DfsTask root = cx.tasks[idx];
+    const DfsTask root = load_task(&cx.tasks[idx]);
     crumb(cx, gw, lane, 2u, (unsigned)idx, (unsigned)root.n, (unsigned)root.a1);
     if (root.n < 2 || root.n > (1 << 24) || root.a0 < 0 || root.a1 > root.n - 1 ||
         root.a0 > root.a1 || root.bm == nullptr) {
@@ -290,7 +355,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
       // The stack is wave-private LDS: lane 0 writes a frame, every lane reads it after the
       // wave barrier (LDS ops of one wave complete in order, the barrier orders the compiler).
       if (lane == 0) stack[0] = root;
-      int top = 1;
+      int top = 1;  // stack[0] is the popped (remote) class, deeper frames are local
       bool aborted = false;
       while (top > 0 && !aborted) {
         __builtin_amdgcn_wave_barrier();
@@ -316,7 +381,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
         }
         unsigned long long row0 = 0;
         unsigned S = 0;
-        expand_row<TS>(cx, f, a, lane, ws, row0, S);
+        if (top == 1) expand_row<TS, true>(cx, f, a, lane, ws, row0, S);
+        else expand_row<TS, false>(cx, f, a, lane, ws, row0, S);
         if (S >= 2 && (cx.max_len == 0 || f.depth + 1 < cx.max_len)) {
           const unsigned long long* cbm = cx.pool_bm + row0 * cx.Wp;
           const int32_t* crk = cx.pool_rank + row0;
@@ -328,7 +394,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
             if (!ok) ws.dead = true;
             ws.share_hint = false;  // re-probe before sharing again
           } else {
-            // child rows were written by this wave: its own later loads see them in order
+            // child rows were written by this wave (cross-lane): drain before reading them back
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) stack[top] = DfsTask{cbm, crk, cgd, (int)S, f.depth + 1, 0, (int)S - 1};
             ++top;
           }
@@ -383,30 +450,51 @@ __global__ void k_dfs_seed(const unsigned long long* __restrict__ bm, const int3
   }
 }
 
-// ---- hole compaction ---------------------------------------------------------------------
-struct ValidOp {
-  const uint8_t* depth;
-  int64_t n;
-  __host__ __device__ int64_t operator()(int64_t i) const { return (i < n && depth[i] != 0) ? 1 : 0; }
-};
-using ValidIt = hipcub::TransformInputIterator<int64_t, ValidOp, hipcub::CountingInputIterator<int64_t>>;
+// ---- hole compaction + topological order ---------------------------------------------------
+// Rows come from per-wave chunks, so a child row may precede its parent row.  Sorting the DFS
+// region stably by depth (holes = depth 0 sort first) restores "parents before children" (the
+// trie invariant every consumer relies on); rows are then scattered with parents remapped.
+__global__ void k_iota(int64_t* __restrict__ v, int64_t n) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr) v[i] = i;
+}
 
-__global__ void k_dfs_scatter(const int64_t* __restrict__ pos, int64_t rows, int64_t out_base,
+__global__ void k_count_zero(const uint8_t* __restrict__ keys, int64_t n,
+                             unsigned long long* __restrict__ out) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr)
+    c += keys[i] == 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+__global__ void k_inverse(const int64_t* __restrict__ sorted_rows, int64_t n,
+                          const unsigned long long* __restrict__ holes, int64_t* __restrict__ inv) {
+  const int64_t H = (int64_t)*holes;
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = H + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr)
+    inv[sorted_rows[i]] = i - H;
+}
+
+__global__ void k_dfs_scatter(const int64_t* __restrict__ sorted_rows, int64_t n,
+                              const unsigned long long* __restrict__ holes,
+                              const int64_t* __restrict__ inv, int64_t out_base,
                               const int64_t* __restrict__ par, const int32_t* __restrict__ item,
                               const uint32_t* __restrict__ cnt, const uint8_t* __restrict__ dep,
                               int64_t* __restrict__ par2, int32_t* __restrict__ item2,
                               uint32_t* __restrict__ cnt2, uint8_t* __restrict__ dep2) {
+  const int64_t H = (int64_t)*holes;
   const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += nthr) {
-    const uint8_t d = dep[r];
-    if (d == 0) continue;
-    const int64_t k = pos[r];
+  for (int64_t i = H + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr) {
+    const int64_t r = sorted_rows[i], k = i - H;
     int64_t p = par[r];
-    if (p >= out_base) p = out_base + pos[p - out_base];  // parent inside the DFS region
+    if (p >= out_base) p = out_base + inv[p - out_base];  // parent inside the DFS region
     par2[k] = p;
     item2[k] = item[r];
     cnt2[k] = cnt[r];
-    dep2[k] = d;
+    dep2[k] = dep[r];
   }
 }
 
@@ -448,22 +536,43 @@ void dfs_persistent(const DfsArgs& a, hipStream_t s) {
 
 size_t dfs_compact_temp_bytes(int64_t rows) {
   size_t bytes = 0;
-  ValidIt it(hipcub::CountingInputIterator<int64_t>(0), ValidOp{nullptr, rows});
-  check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (int64_t*)nullptr, (int)(rows + 1)));
-  return bytes;
+  check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint8_t*)nullptr,
+                                           (uint8_t*)nullptr, (const int64_t*)nullptr,
+                                           (int64_t*)nullptr, (int)std::max<int64_t>(rows, 1), 0, 8));
+  // + keys_out (rows) + vals_in/vals_out/inv (3 * rows * 8) + holes counter, 256-B aligned parts
+  return bytes + 256 + ((size_t)rows + 256) + 3 * ((size_t)rows * 8 + 256) + 256;
 }
 
-void dfs_compact(int64_t rows, int64_t out_base, int64_t* par, int32_t* item, uint32_t* cnt,
-                 uint8_t* dep, int64_t* pos, void* temp, size_t temp_bytes, int64_t* par2,
-                 int32_t* item2, uint32_t* cnt2, uint8_t* dep2, hipStream_t s) {
-  // pos has rows+1 entries; pos[rows] = number of valid nodes
-  ValidIt it(hipcub::CountingInputIterator<int64_t>(0), ValidOp{dep + out_base, rows});
-  check(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, it, pos, (int)(rows + 1), s));
+int64_t dfs_compact(int64_t rows, int64_t out_base, int64_t* par, int32_t* item, uint32_t* cnt,
+                    uint8_t* dep, void* temp, size_t temp_bytes, int64_t* par2, int32_t* item2,
+                    uint32_t* cnt2, uint8_t* dep2, unsigned long long* h_holes, hipStream_t s) {
+  size_t sort_bytes = 0;
+  check(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint8_t*)nullptr,
+                                           (uint8_t*)nullptr, (const int64_t*)nullptr,
+                                           (int64_t*)nullptr, (int)rows, 0, 8));
+  char* p = (char*)temp;
+  auto carve = [&](size_t n) { char* q = p; p += (n + 255) & ~(size_t)255; return q; };
+  void* sort_tmp = carve(sort_bytes);
+  uint8_t* keys_out = (uint8_t*)carve((size_t)rows);
+  int64_t* vals_in = (int64_t*)carve((size_t)rows * 8);
+  int64_t* vals_out = (int64_t*)carve((size_t)rows * 8);
+  int64_t* inv = (int64_t*)carve((size_t)rows * 8);
+  unsigned long long* holes = (unsigned long long*)carve(8);
+  if ((size_t)(p - (char*)temp) > temp_bytes) throw std::runtime_error("kmls: dfs_compact temp");
   const int g = (int)std::min<int64_t>(std::max<int64_t>((rows + 255) / 256, 1), 8192);
-  hipLaunchKernelGGL(k_dfs_scatter, dim3(g), dim3(256), 0, s, pos, rows, out_base,
-                     par + out_base, item + out_base, cnt + out_base, dep + out_base, par2, item2,
-                     cnt2, dep2);
+  hipLaunchKernelGGL(k_iota, dim3(g), dim3(256), 0, s, vals_in, rows);
+  check(hipcub::DeviceRadixSort::SortPairs(sort_tmp, sort_bytes, dep + out_base, keys_out, vals_in,
+                                           vals_out, (int)rows, 0, 8, s));
+  check(hipMemsetAsync(holes, 0, 8, s));
+  hipLaunchKernelGGL(k_count_zero, dim3(std::min(g, 1024)), dim3(256), 0, s, keys_out, rows, holes);
+  hipLaunchKernelGGL(k_inverse, dim3(g), dim3(256), 0, s, vals_out, rows, holes, inv);
+  hipLaunchKernelGGL(k_dfs_scatter, dim3(g), dim3(256), 0, s, vals_out, rows, holes, inv,
+                     out_base, par + out_base, item + out_base, cnt + out_base, dep + out_base,
+                     par2, item2, cnt2, dep2);
   check(hipGetLastError());
+  check(hipMemcpyAsync(h_holes, holes, 8, hipMemcpyDeviceToHost, s));
+  check(hipStreamSynchronize(s));
+  return rows - (int64_t)*h_holes;
 }
 
 }  // namespace kern

@@ -103,12 +103,13 @@ struct DfsArgs {
   unsigned int* wave_state;          // per-wave breadcrumbs (debug): [state, idx_lo, a, n]
 };
 void dfs_persistent(const DfsArgs& a, hipStream_t s);
-// remove unused-row holes of the DFS region [out_base, out_base+rows): pos[rows+1] scan,
-// compacted copies into par2/item2/cnt2/dep2 (parents inside the region remapped)
+// DFS region [out_base, out_base+rows): drop holes (depth 0), order rows by depth (stable:
+// parents before children) into par2/item2/cnt2/dep2 with in-region parents remapped.
+// Returns the number of valid nodes (synchronises the stream).
 size_t dfs_compact_temp_bytes(int64_t rows);
-void dfs_compact(int64_t rows, int64_t out_base, int64_t* par, int32_t* item, uint32_t* cnt,
-                 uint8_t* dep, int64_t* pos, void* temp, size_t temp_bytes, int64_t* par2,
-                 int32_t* item2, uint32_t* cnt2, uint8_t* dep2, hipStream_t s);
+int64_t dfs_compact(int64_t rows, int64_t out_base, int64_t* par, int32_t* item, uint32_t* cnt,
+                    uint8_t* dep, void* temp, size_t temp_bytes, int64_t* par2, int32_t* item2,
+                    uint32_t* cnt2, uint8_t* dep2, unsigned long long* h_holes, hipStream_t s);
 
 // ---- serving (serve.hip) ----
 void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,
