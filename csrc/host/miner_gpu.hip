@@ -215,6 +215,7 @@ struct MineRun {
     a.seed_row_end = L.row_end;
     a.seed_rows = L.n;
     a.seed_depth = depth;
+    a.seed_items = (int32_t*)arena->push((size_t)std::max<int64_t>(L.n, 1) * sizeof(int32_t));
     a.tasks = (kern::DfsTask*)arena->push((size_t)task_cap * sizeof(kern::DfsTask));
     a.ready = (unsigned int*)arena->push((size_t)task_cap * sizeof(unsigned int));
     a.task_cap = task_cap;

@@ -276,15 +276,16 @@ __device__ void expand_row(const Ctx& cx, const DfsTask& f, int a, int lane, Wav
         st_sc1(z + w, u & v);
       }
       if (tl == 0) {
-        int32_t rb;
+        // frames carry ORIGINAL item ids (seeds are converted once by k_seed_items)
+        int32_t ib;
         if constexpr (REMOTE)
-          rb = (int32_t)__hip_atomic_load(f.rank + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else rb = f.rank[b];
-        st_sc1(reinterpret_cast<unsigned int*>(cx.pool_rank + row), (unsigned)rb);
+          ib = (int32_t)__hip_atomic_load(f.rank + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else ib = f.rank[b];
+        st_sc1(reinterpret_cast<unsigned int*>(cx.pool_rank + row), (unsigned)ib);
         st_sc1(reinterpret_cast<unsigned long long*>(cx.pool_gid + row),
                (unsigned long long)(cx.out_base + row));
         cx.out_parent[cx.out_base + row] = gid_a;
-        cx.out_item[cx.out_base + row] = cx.ids[rb];
+        cx.out_item[cx.out_base + row] = ib;
         cx.out_count[cx.out_base + row] = c;
         cx.out_depth[cx.out_base + row] = dchild;
       }
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
         if (f.a0 >= f.a1) { --top; continue; }
         const int a = f.a0;
         if (lane == 0) stack[top - 1].a0 = a + 1;
-        if (++ws.rows_since_probe >= 16) {
+        if (++ws.rows_since_probe >= 4) {
           ws.rows_since_probe = 0;
           int probe = 0;
           if (lane == 0) {
@@ -377,7 +378,40 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
             if (lane == 0) atomicOr(&cx.ctl->aborted, 1u);
             break;
           }
-          ws.share_hint = probe == 1;
+          if (probe == 1 && lane == 0) {
+            // work splitting: give away the upper half (by candidates) of the remaining rows of
+            // the OLDEST frame that still has >= 2 rows — the largest pending subtrees.  Its
+            // class data is already performed in memory (written through + drained before the
+            // frame was pushed, or published by another wave).
+            for (int i = 0; i < top; ++i) {
+              const DfsTask& bf = stack[i];
+              const int lo = (i == top - 1) ? a + 1 : bf.a0;
+              if (bf.a1 - lo < 2) continue;
+              long long total = 0;
+              for (int r = lo; r < bf.a1; ++r) total += bf.n - 1 - r;
+              long long acc = 0;
+              int mid = lo;
+              while (mid < bf.a1 - 1 && 2 * (acc + (bf.n - 1 - mid)) <= total) {
+                acc += bf.n - 1 - mid;
+                ++mid;
+              }
+              if (mid <= lo) mid = lo + 1;
+              const unsigned long long slot = [&] {
+                atomicAdd(&cx.ctl->pending, 1ull);
+                return atomicAdd(&cx.ctl->q_tail, 1ull);
+              }();
+              if (slot >= (unsigned long long)cx.task_cap) {
+                atomicOr(&cx.ctl->overflow, 2u);
+                atomicAdd(&cx.ctl->pending, (unsigned long long)(-1ll));
+                break;
+              }
+              store_task(&cx.tasks[slot], DfsTask{bf.bm, bf.rank, bf.gid, bf.n, bf.depth, mid, bf.a1});
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              st_sc1(&cx.ready[slot], 1u);
+              stack[i].a1 = mid;
+              break;
+            }
+          }
         }
         unsigned long long row0 = 0;
         unsigned S = 0;
@@ -387,15 +421,15 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfs_persistent(Ctx cx) {
           const unsigned long long* cbm = cx.pool_bm + row0 * cx.Wp;
           const int32_t* crk = cx.pool_rank + row0;
           const int64_t* cgd = cx.pool_gid + row0;
-          if (ws.share_hint || top >= kStack) {
+          // child rows were written through by this wave (cross-lane): drain before they are
+          // read back locally or handed to another wave
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (top >= kStack) {
             int ok = 1;
             if (lane == 0) ok = share_class(cx, cbm, crk, cgd, (int)S, f.depth + 1) ? 1 : 0;
             ok = __shfl(ok, 0);
             if (!ok) ws.dead = true;
-            ws.share_hint = false;  // re-probe before sharing again
           } else {
-            // child rows were written by this wave (cross-lane): drain before reading them back
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) stack[top] = DfsTask{cbm, crk, cgd, (int)S, f.depth + 1, 0, (int)S - 1};
             ++top;
           }
@@ -448,6 +482,13 @@ __global__ void k_dfs_seed(const unsigned long long* __restrict__ bm, const int3
     tasks[base + t] = DfsTask{cbm, rank + s, gid + s, n, depth, a0, n - 1};
     ready[base + t] = 1u;
   }
+}
+
+// frames carry original item ids: convert the seed level's Eclat ranks once
+__global__ void k_seed_items(const int32_t* __restrict__ rank, const int32_t* __restrict__ ids,
+                             int64_t n, int32_t* __restrict__ out) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr) out[i] = ids[rank[i]];
 }
 
 // ---- hole compaction + topological order ---------------------------------------------------
@@ -519,8 +560,9 @@ void dfs_persistent(const DfsArgs& a, hipStream_t s) {
          a.task_cap, a.minsup, a.max_len, a.timeout_ticks, a.abort_flag, a.wave_state};
   const int64_t nr = a.seed_rows;
   const int sg = (int)std::min<int64_t>(std::max<int64_t>((nr + 255) / 256, 1), 4096);
+  hipLaunchKernelGGL(k_seed_items, dim3(sg), dim3(256), 0, s, a.seed_rank, a.ids, nr, a.seed_items);
   hipLaunchKernelGGL(k_dfs_seed, dim3(sg), dim3(256), 0, s, (const unsigned long long*)a.seed_bm,
-                     a.seed_rank, a.seed_gid, a.seed_row_end, nr, a.Wp, a.seed_depth, a.tasks,
+                     a.seed_items, a.seed_gid, a.seed_row_end, nr, a.Wp, a.seed_depth, a.tasks,
                      a.ready, a.ctl, a.task_cap);
   // persistent grid: 2 workgroups of 4 waves per CU (resident; no grid barrier is needed)
   const dim3 grid(a.n_cus * 2), block(64 * kWaves);

@@ -57,7 +57,7 @@ void gram_to_cand(const uint32_t* gram, int64_t F, const int64_t* cand_off, int6
 // ---- persistent DFS (dfs_persistent.hip) ----
 struct DfsTask {
   const unsigned long long* bm;  // class members' bitmaps [n][Wp]
-  const int32_t* rank;           // members' last-item Eclat rank
+  const int32_t* rank;           // members' last item (original item id inside the DFS kernel)
   const int64_t* gid;            // members' global trie node ids
   int32_t n, depth, a0, a1;      // class size, members' itemset size, rows [a0, a1) to expand
 };
@@ -76,6 +76,7 @@ struct DfsArgs {
   const int32_t* seed_rank;
   const int64_t* seed_gid;
   const int32_t* seed_row_end;
+  int32_t* seed_items;  // scratch [seed_rows]: original item ids of the seed rows
   int64_t seed_rows;
   int seed_depth;
   // queue + pool

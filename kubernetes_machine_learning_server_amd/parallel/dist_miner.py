@@ -86,18 +86,21 @@ class _GpuOps:
     def __init__(self, dm: "DistMiner", tx_ptr, items, arena_bytes: int):
         N = native.require_gpu()
         self.dev = torch.device("cuda", dm.device)
-        if dm.world > 1:
+        if dm.world > 1 or dm.force_protocol:
+            # every torch op of the protocol (allocations, fills, collectives) and every native
+            # kernel run on ONE stream, so they are ordered without extra synchronisation
             torch.cuda.set_device(dm.device)
             self.stream = torch.cuda.Stream(device=dm.device)
             self.g = N.GpuMiner(dm.device, arena_bytes, self.stream.cuda_stream)
         else:
-            self.stream = None
+            self.stream = None  # native-only single-GPU path: the miner owns its stream
             self.g = N.GpuMiner(dm.device, arena_bytes, 0)
         self.g.load_csr(tx_ptr, items, dm.n_items)
         self.n_items = dm.n_items
 
     def ctx(self):
-        return torch.cuda.stream(self.stream)
+        import contextlib
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
 
     def supports(self):
         c = torch.empty(self.n_items, dtype=torch.int32, device=self.dev)

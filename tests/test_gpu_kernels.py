@@ -35,9 +35,11 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma):
     import torch
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     tx = generate(shape, seed=11, n_tx=n_tx)
-    g = gpu_mod.GpuMiner(0, 1 << 28, 0)
+    # run the miner on torch's current stream so torch allocations/fills are ordered with it
+    g = gpu_mod.GpuMiner(0, 1 << 28, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     cnt = torch.zeros(tx.n_items, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
     g.item_support(cnt.data_ptr())
     g.synchronize()
     host = cnt.cpu().numpy().view(np.uint32)
@@ -47,8 +49,9 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma):
     ids, counts, minsup = g.frequent()
     Wp = g.words_local()
     bm = torch.zeros((max(F, 1), Wp), dtype=torch.int64, device="cuda")
-    g.encode_bitmaps(bm.data_ptr(), Wp, 0)
     gram = torch.zeros((F, F), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the fills ran on torch's stream
+    g.encode_bitmaps(bm.data_ptr(), Wp, 0)
     g.pair_counts(bm.data_ptr(), Wp, gram.data_ptr(), use_mfma)
     g.synchronize()
     got = np.triu(gram.cpu().numpy().astype(np.int64), 1)
