@@ -39,8 +39,8 @@ def main() -> int:
     ap.add_argument("--mfma", action="store_true", help="level-2 on the i8 matrix cores")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="native CPU miner (no GPU)")
-    ap.add_argument("--level-wise", action="store_true",
-                    help="levels >= 3 level-by-level instead of the persistent DFS kernel")
+    ap.add_argument("--persistent", action="store_true",
+                    help="levels >= 3 in the persistent work-queue DFS kernel (A/B option)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -76,7 +76,7 @@ def main() -> int:
     else:
         from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
         dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, args.min_support, device=local_rank,
-                       mfma=args.mfma, persistent=not args.level_wise)
+                       mfma=args.mfma, persistent=args.persistent)
 
         def step():
             st = dm.step(download=True)["stats"]
@@ -135,7 +135,7 @@ def main() -> int:
             "n_frequent_items": int(st.get("n_frequent_items", 0)),
             "max_depth": int(st.get("max_depth", 0)),
             "level2": "mfma-i8" if args.mfma else "popcount-bitgemm",
-            "levels3plus": "level-wise" if args.level_wise else "persistent-dfs",
+            "levels3plus": "persistent-dfs" if args.persistent else "level-wise",
         },
         "verified_vs_cpu_miner": verified,
         "reference_seconds_ds2_0.05": REF_SECONDS_DS2_005,

@@ -46,7 +46,7 @@ py::dict result_to_dict(gpu::GpuMineResult&& r) {
 }
 
 MineConfig make_cfg(double ms, int max_len, bool pairs_only, bool gram, bool mfma,
-                    bool persistent = true) {
+                    bool persistent = false) {
   MineConfig c;
   c.persistent = persistent;
   c.min_support = ms;
@@ -115,7 +115,7 @@ void register_gpu_bindings(py::module_& m) {
       }, py::arg("bm"), py::arg("Wp"), py::arg("min_support"), py::arg("max_len") = 0,
          py::arg("pairs_only") = false, py::arg("owned") = py::none(), py::arg("emit_level1") = true,
          py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
-         py::arg("persistent") = true)
+         py::arg("persistent") = false)
       .def("mine", [](gpu::GpuMiner& g, double ms, int max_len, bool pairs_only, bool download,
                       bool gram, bool mfma, bool persistent) {
         MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma, persistent);
@@ -127,7 +127,7 @@ void register_gpu_bindings(py::module_& m) {
         return result_to_dict(std::move(r));
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("pairs_only") = false,
          py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
-         py::arg("persistent") = true)
+         py::arg("persistent") = false)
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
   py::class_<gpu::GpuRuleIndex>(m, "GpuRuleIndex")

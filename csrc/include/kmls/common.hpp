@@ -40,7 +40,8 @@ struct MineConfig {
   bool pairs_only = false;  // stop after 2-itemsets (rule-map fast path)
   bool level2_gram = true;  // GPU: level 2 through the tiled bit-GEMM
   bool level2_mfma = false; // GPU: ... on the i8 matrix cores instead of VALU popcount
-  bool persistent = true;   // GPU: levels >= 3 in one persistent work-queue launch
+  bool persistent = false;  // GPU: levels >= 3 in one persistent work-queue launch (A/B option;
+                            // level-wise wins on many-tiny-class trees, profiles/r1_dfs_ab.md)
 };
 
 // Frequent-item selection shared by all miners: ids ordered by ascending support

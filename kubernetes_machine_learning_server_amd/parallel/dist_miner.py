@@ -196,7 +196,7 @@ class DistMiner:
     def __init__(self, tx_ptr: np.ndarray, items: np.ndarray, n_items: int, min_support: float,
                  device: int = 0, max_len: int = 0, mfma: bool = False,
                  arena_bytes: int = 0, backend: str = "gpu", force_protocol: bool = False,
-                 persistent: bool = True):
+                 persistent: bool = False):
         self.world = dist.get_world_size() if (dist is not None and dist.is_initialized()) else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
         self.n_tx = len(tx_ptr) - 1

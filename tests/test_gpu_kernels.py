@@ -171,7 +171,7 @@ def test_persistent_dfs_equals_level_wise(gpu_mod, shape, ms):
         assert np.array_equal(np.sort(p["count"]), np.sort(c["count"]))
         # parents precede children (trie order used by every consumer)
         assert (p["parent"] < np.arange(len(p["parent"]))).all()
-    lw = g.mine(ms, persistent=False)
+    lw = g.mine(ms, persistent=False)  # default path
     assert lw["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
     if c["stats"]["n_itemsets"] < 300_000:
         assert _trie_dict(p) == _trie_dict(c)
