@@ -1,0 +1,247 @@
+"""Serving benchmark: p50/p99 latency of POST /api/recommend/ at fixed offered QPS.
+
+BASELINE.json's second metric.  Open-loop load (requests are issued on a fixed schedule, not
+when the previous one returns, so queueing shows up as latency): ``--clients`` processes each
+run an asyncio/aiohttp loop at QPS/clients.  The server is the real uvicorn app (``--workers``
+processes) over a PVC directory populated by the real job on ds1-shaped synthetic data.
+Backends: ``hip`` (HBM index + micro-batched HIP matcher), ``cpu`` (C++ matcher), ``python``
+(the reference's own dict/defaultdict/sorted matcher, rest_api/app/main.py:224-254) — all in
+the same harness.  Also ``--matcher-only``: in-process matcher throughput without HTTP.
+
+  python -m kubernetes_machine_learning_server_amd.bench.bench_serve --backend cpu --qps 1000,5000
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import multiprocessing as mp
+import os
+import pathlib
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+from typing import List
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[2]
+
+
+def prepare_pvc(root: pathlib.Path, shape: str = "ds1", ms: float = 0.05, miner: str = "auto"):
+    from ..config import JobSettings
+    from ..data.synthetic import generate, to_reference_csv
+    from ..job import main as job
+    ds = root / "datasets"
+    ds.mkdir(parents=True, exist_ok=True)
+    tx = generate(shape, seed=0)
+    to_reference_csv(tx, ds / "2023_spotify_ds1.csv", seed=0)
+    base = root / "api-data"
+    cfg = JobSettings(min_support=ms, base_dir=base, datasets_dir=ds, pickles_folder=base / "pickles",
+                      recommendations_file="recommendations.pickle", best_tracks_file="best_tracks.pickle",
+                      data_invalidation_file="last_execution.txt", regex_filename="2023_spotify_ds*.csv",
+                      top_tracks_save_percentile=0.03, miner=miner, rules_mode="pairs")
+    return job.run(cfg), base
+
+
+def make_queries(base: pathlib.Path, n: int, seed: int = 0) -> List[List[str]]:
+    from ..serve.index import RuleIndexData
+    idx = RuleIndexData.load(base / "pickles" / "rules.idx")
+    keys = [idx.names[i] for i in np.nonzero(idx.is_key)[0]]
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        k = int(rng.integers(1, 6))
+        q = [keys[int(i)] for i in rng.integers(0, len(keys), k)]
+        if rng.random() < 0.2:
+            q = [f"unknown song {int(rng.integers(1e9))}"]
+        out.append(q)
+    return out
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def start_server(base: pathlib.Path, backend: str, workers: int, port: int):
+    env = dict(os.environ)
+    env.update(BASE_DIR=str(base) + "/", PICKLE_DIR="pickles/", SERVE_BACKEND=backend,
+               KMLS_LOG_LEVEL="ERROR", POLLING_WAIT_IN_MINUTES="60",
+               PYTHONPATH=str(ROOT) + os.pathsep + env.get("PYTHONPATH", ""))
+    cmd = [sys.executable, "-m", "kubernetes_machine_learning_server_amd.serve", "--host",
+           "127.0.0.1", "--port", str(port), "--workers", str(workers), "--log-level", "error"]
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                            start_new_session=True)
+    import urllib.request
+    t0 = time.time()
+    while time.time() - t0 < 240:
+        if proc.poll() is not None:
+            raise RuntimeError("server died: " + proc.stderr.read().decode()[-2000:])
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}/readyz", timeout=2) as r:
+                if r.status == 200:
+                    return proc
+        except Exception:
+            time.sleep(0.5)
+    stop_server(proc)
+    raise RuntimeError("server not ready after 240 s")
+
+
+def stop_server(proc):
+    try:
+        os.killpg(proc.pid, signal.SIGTERM)
+        proc.wait(timeout=20)
+    except Exception:
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except Exception:
+            pass
+
+
+def _client(port: int, qps: float, duration: float, queries, t_start: float, out_q):
+    import aiohttp
+
+    async def run():
+        lat, errs = [], 0
+        conn = aiohttp.TCPConnector(limit=0, force_close=False)
+        timeout = aiohttp.ClientTimeout(total=30)
+        async with aiohttp.ClientSession(connector=conn, timeout=timeout) as sess:
+            url = f"http://127.0.0.1:{port}/api/recommend/"
+            n = int(qps * duration)
+            tasks = []
+
+            async def one(i, when):
+                nonlocal errs
+                await asyncio.sleep(max(0.0, when - time.perf_counter()))
+                t = time.perf_counter()
+                try:
+                    async with sess.post(url, json={"songs": queries[i % len(queries)]}) as r:
+                        await r.read()
+                        if r.status != 200:
+                            errs += 1
+                            return
+                except Exception:
+                    errs += 1
+                    return
+                lat.append((time.perf_counter() - t, t - when))
+            base = time.perf_counter() + max(0.0, t_start - time.time())
+            for i in range(n):
+                tasks.append(asyncio.ensure_future(one(i, base + i / qps)))
+            await asyncio.gather(*tasks)
+        return lat, errs
+    lat, errs = asyncio.run(run())
+    out_q.put((lat, errs))
+
+
+def measure(port: int, qps: float, duration: float, clients: int, queries) -> dict:
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    t_start = time.time() + 1.0
+    procs = [ctx.Process(target=_client, args=(port, qps / clients, duration,
+                                                queries[c::clients], t_start, q))
+             for c in range(clients)]
+    for p in procs:
+        p.start()
+    lat, errs = [], 0
+    for _ in procs:
+        l, e = q.get(timeout=duration + 120)
+        lat.extend(l)
+        errs += e
+    for p in procs:
+        p.join(timeout=30)
+    a = np.array([x[0] for x in lat]) * 1e3 if lat else np.zeros(1)
+    lag = np.array([x[1] for x in lat]) * 1e3 if lat else np.zeros(1)
+    return {"offered_qps": qps, "completed": len(lat), "errors": errs,
+            "achieved_qps": round(len(lat) / duration, 1),
+            "p50_ms": round(float(np.percentile(a, 50)), 3), "p90_ms": round(float(np.percentile(a, 90)), 3),
+            "p99_ms": round(float(np.percentile(a, 99)), 3), "mean_ms": round(float(a.mean()), 3),
+            "client_send_lag_p99_ms": round(float(np.percentile(lag, 99)), 3)}
+
+
+def matcher_bench(base: pathlib.Path, n_queries: int = 20000) -> dict:
+    """In-process matcher throughput (no HTTP): python reference vs C++ vs HIP batched."""
+    from ..models.oracle import recommend_oracle
+    from ..ops import native
+    from ..serve.index import RuleIndexData
+    idx = RuleIndexData.load(base / "pickles" / "rules.idx")
+    rec = idx.to_rec_dict()
+    qs = make_queries(base, n_queries, seed=1)
+    n2i = idx.name_to_id
+    ids = [np.array([n2i.get(s, -1) for s in q], np.int32) for q in qs]
+    q_ptr = np.zeros(len(ids) + 1, np.int64)
+    np.cumsum([len(x) for x in ids], out=q_ptr[1:])
+    seeds = np.concatenate(ids)
+    out = {"n_queries": n_queries, "index_keys": idx.n_keys, "index_nnz": idx.nnz}
+    t = time.perf_counter()
+    for q in qs[:5000]:
+        recommend_oracle(rec, q, 10)
+    out["python_ref_us_per_query"] = round((time.perf_counter() - t) / 5000 * 1e6, 2)
+    host = idx.native()
+    t = time.perf_counter()
+    for x in ids:
+        host.query(x, 10)
+    out["cpp_single_us_per_query"] = round((time.perf_counter() - t) / len(ids) * 1e6, 3)
+    t = time.perf_counter()
+    host.query_batch(q_ptr, seeds, 10)
+    out["cpp_batch_us_per_query"] = round((time.perf_counter() - t) / len(ids) * 1e6, 3)
+    if native.gpu_available():
+        N = native.load()
+        g = N.GpuRuleIndex(0, host)
+        for B in (1, 16, 256, 4096, n_queries):
+            qp = q_ptr[:B + 1]
+            sd = seeds[:qp[-1]]
+            g.query_batch(qp, sd, 10)  # warm
+            reps = max(3, 2000 // B)
+            t = time.perf_counter()
+            for _ in range(reps):
+                r_ids, r_n = g.query_batch(qp, sd, 10)
+            dt = (time.perf_counter() - t) / reps
+            c_ids, c_n = host.query_batch(qp, sd, 10)
+            out[f"hip_batch{B}_us_per_batch"] = round(dt * 1e6, 2)
+            out[f"hip_batch{B}_us_per_query"] = round(dt / B * 1e6, 3)
+            out[f"hip_batch{B}_exact"] = bool((r_ids == c_ids).all() and (r_n == c_n).all())
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--backend", default="cpu", help="hip | cpu | python | auto")
+    ap.add_argument("--qps", default="1000,5000,10000")
+    ap.add_argument("--duration", type=float, default=10.0)
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--clients", type=int, default=4)
+    ap.add_argument("--matcher-only", action="store_true")
+    ap.add_argument("--pvc", default=None, help="reuse a populated PVC dir")
+    a = ap.parse_args(argv)
+    tmp = tempfile.mkdtemp(prefix="kmls_serve_") if a.pvc is None else a.pvc
+    root = pathlib.Path(tmp)
+    if not (root / "api-data" / "pickles" / "rules.idx").exists():
+        summary, base = prepare_pvc(root)
+    base = root / "api-data"
+    if a.matcher_only:
+        print(json.dumps({"bench": "matcher", **matcher_bench(base)}), flush=True)
+        return 0
+    queries = make_queries(base, 50000)
+    port = _free_port()
+    proc = start_server(base, a.backend, a.workers, port)
+    try:
+        measure(port, 200, 2.0, 1, queries)  # warm-up
+        for qps in [float(x) for x in a.qps.split(",")]:
+            r = measure(port, qps, a.duration, a.clients, queries)
+            r.update(bench="serve", backend=a.backend, workers=a.workers, clients=a.clients,
+                     duration_s=a.duration)
+            print(json.dumps(r), flush=True)
+    finally:
+        stop_server(proc)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

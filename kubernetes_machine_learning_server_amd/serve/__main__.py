@@ -1,6 +1,8 @@
-"""``python -m kubernetes_machine_learning_server_amd.serve [--port 80] [--host 0.0.0.0]``."""
+"""``python -m kubernetes_machine_learning_server_amd.serve [--port 80] [--workers N]``."""
 import argparse
 import sys
+
+from .runner import run
 
 
 def main() -> int:
@@ -8,11 +10,9 @@ def main() -> int:
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=80)
     ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--log-level", default="info")
     a = ap.parse_args()
-    import uvicorn
-    uvicorn.run("kubernetes_machine_learning_server_amd.serve.app:app", host=a.host, port=a.port,
-                workers=a.workers, log_level="info")
-    return 0
+    return run(a.host, a.port, a.workers, a.log_level)
 
 
 sys.exit(main())

@@ -38,7 +38,7 @@ logger = logging.getLogger("kmls.api")
 def _setup_logging() -> None:
     if getattr(_setup_logging, "_done", False):
         return
-    logger.setLevel(logging.DEBUG)
+    logger.setLevel(os.environ.get("KMLS_LOG_LEVEL", "DEBUG").upper())
     h = logging.StreamHandler(sys.stdout)
     h.setFormatter(logging.Formatter(fmt="%(asctime)s - %(levelname)s - %(message)s"))
     logger.addHandler(h)
@@ -69,9 +69,18 @@ OPENAPI_EXAMPLES = {
 TAGS_METADATA = [{"name": "recommend", "description": "Song recommendation service"}]
 
 
+def _python_match(snap, seeds, k):
+    rec = getattr(snap, "_py_rec", None)
+    if rec is None:
+        rec = snap.index.to_rec_dict()
+        object.__setattr__(snap, "_py_rec", rec)
+    from ..models.oracle import recommend_oracle
+    return recommend_oracle(rec, seeds, k)
+
+
 def _gpu_factory(cfg: ApiSettings):
     """HBM index builder for SERVE_BACKEND=hip|auto (None → CPU matcher only)."""
-    if cfg.serve_backend == "cpu":
+    if cfg.serve_backend in ("cpu", "python"):
         return None
     from ..ops import native
     if not native.gpu_available():
@@ -158,7 +167,10 @@ def create_app(cfg: Optional[ApiSettings] = None) -> FastAPI:
             metrics.requests.labels("not_loaded").inc()
             return [M.NO_RECOMMENDATIONS]
         k = cfg.k_best_tracks
-        if snap.gpu_index is not None:
+        if cfg.serve_backend == "python":
+            # the reference's own matcher (dict-of-dicts + defaultdict + sorted), for A/B benches
+            res = _python_match(snap, seeds, k)
+        elif snap.gpu_index is not None:
             ids, n = await batcher.submit(snap, M.seed_ids(snap, seeds), k)
             res = None if n < 0 else [snap.index.names[i] for i in ids[:n]]
             metrics.batch.set(batcher.last_batch)

@@ -31,7 +31,7 @@ RULES_INDEX_FILE = "rules.idx"
 
 
 @dataclasses.dataclass(frozen=True)
-class ModelSnapshot:
+class ModelSnapshot:  # immutable; _py_rec (python backend cache) is set once via object.__setattr__
     best_tracks: List[Dict[str, Any]]
     index: RuleIndexData
     marker: Optional[str]
