@@ -142,6 +142,29 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("bm"), py::arg("ids"), py::arg("counts"), py::arg("minsup"), py::arg("max_len") = 0,
      py::arg("owned") = py::none(), py::arg("threads") = 0);
 
+  // ---------------- association rules ----------------
+  m.def("association_rules", [](I64 parent, I32 item, py::array_t<uint32_t, py::array::c_style | py::array::forcecast> count,
+                                U8 depth, int64_t n_tx, int metric, double min_threshold,
+                                int max_antecedent, int threads) {
+    const int64_t n = item.size();
+    KMLS_CHECK(parent.size() == n && count.size() == n && depth.size() == n, "trie arrays differ in size");
+    RuleSet r;
+    {
+      py::gil_scoped_release nogil;
+      r = association_rules_cpu(parent.data(), item.data(), count.data(), depth.data(), n, n_tx,
+                                (RuleMetric)metric, min_threshold, max_antecedent, threads);
+    }
+    py::dict d;
+    d["itemset"] = to_array(std::move(r.itemset));
+    d["antecedent"] = to_array(std::move(r.antecedent));
+    d["consequent"] = to_array(std::move(r.consequent));
+    d["confidence"] = to_array(std::move(r.confidence));
+    d["lift"] = to_array(std::move(r.lift));
+    return d;
+  }, py::arg("parent"), py::arg("item"), py::arg("count"), py::arg("depth"), py::arg("n_tx"),
+     py::arg("metric") = 0, py::arg("min_threshold") = 0.8, py::arg("max_antecedent") = 0,
+     py::arg("threads") = 0);
+
   // ---------------- CPU matcher ----------------
   py::class_<RuleIndex, std::shared_ptr<RuleIndex>>(m, "RuleIndex")
       .def(py::init([](int64_t n_items, I64 row_ptr, I32 cons, F64 score, U8 is_key) {

@@ -56,6 +56,23 @@ struct PairTable {
 void count_items(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, int64_t n_items,
                  uint32_t* out_counts);
 
+// ---- association rules (rules_cpu.cpp) ------------------------------------------------------
+enum class RuleMetric { Confidence = 0, Lift = 1, Leverage = 2, Support = 3, Conviction = 4,
+                        ConfidenceStrict = 5 /* fpgrowth_py: conf > minConf */ };
+struct RuleSet {  // rule r: antecedent node -> consequent node (trie ids), from itemset node
+  std::vector<int64_t> itemset, antecedent, consequent;
+  std::vector<double> confidence, lift;
+  void reserve(size_t n) {
+    itemset.reserve(n); antecedent.reserve(n); consequent.reserve(n);
+    confidence.reserve(n); lift.reserve(n);
+  }
+  size_t size() const { return itemset.size(); }
+};
+RuleSet association_rules_cpu(const int64_t* parent, const int32_t* item, const uint32_t* count,
+                              const uint8_t* depth, int64_t n_nodes, int64_t n_tx,
+                              RuleMetric metric, double min_threshold, int max_antecedent,
+                              int threads);
+
 // ---- CPU matcher ---------------------------------------------------------------------------
 // Rule index: for each key item, an ordered row of (consequent, score).  Rows may be empty
 // (frequent songs without pairs are keys with `{}`; rest_api/app/main.py:235 distinguishes
