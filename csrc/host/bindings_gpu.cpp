@@ -38,6 +38,7 @@ py::dict result_to_dict(gpu::GpuMineResult&& r) {
   s["max_depth"] = r.stats.max_depth;
   s["seconds"] = r.stats.seconds;
   s["arena_high_water"] = r.arena_high_water;
+  s["levels_path"] = r.levels_path;
   py::dict ph;
   for (auto& p : r.phases) ph[py::str(p.name)] = p.ms;
   s["phases_ms"] = ph;

@@ -108,8 +108,6 @@ std::shared_ptr<void> PinnedPool::get(size_t bytes) {
   });
 }
 
-namespace {
-
 template <typename T>
 struct DevVec {  // growable device array (output trie)
   T* p = nullptr;
@@ -131,6 +129,44 @@ struct DevVec {  // growable device array (output trie)
     if (p) (void)hipFree(p);
   }
 };
+
+// Output trie (parent, item, count, depth) — owned by the GpuMiner so that steady-state mining
+// allocates nothing; plus the side stream that streams finished levels to pinned host memory
+// while deeper levels are still being mined.
+struct OutBufs {
+  DevVec<int64_t> parent;
+  DevVec<int32_t> item;
+  DevVec<uint32_t> count;
+  DevVec<uint8_t> depth;
+  hipStream_t copy_s = nullptr;
+  hipEvent_t ev = nullptr;
+  // fused level path (levels.hip): look-back status words (epoch-tagged, zeroed once)
+  unsigned long long* status = nullptr;
+  int64_t status_cap = 1 << 20;  // tiles per launch (256M candidates / 2G rows)
+  unsigned epoch = 0;
+  int depth_hint = 6;            // levels enqueued before the first completion check
+  OutBufs() {
+    KMLS_HIP(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
+    KMLS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    KMLS_HIP(hipMalloc((void**)&status, (size_t)status_cap * sizeof(unsigned long long)));
+    KMLS_HIP(hipMemset(status, 0, (size_t)status_cap * sizeof(unsigned long long)));
+  }
+  unsigned next_epoch(hipStream_t s) {
+    if (++epoch >= (1u << 24) - 1) {  // 24-bit tag wraps: forget every old word
+      KMLS_HIP(hipMemsetAsync(status, 0, (size_t)status_cap * sizeof(unsigned long long), s));
+      epoch = 1;
+    }
+    return epoch;
+  }
+  ~OutBufs() {
+    if (copy_s) (void)hipStreamSynchronize(copy_s);
+    if (status) (void)hipFree(status);
+    if (ev) (void)hipEventDestroy(ev);
+    if (copy_s) (void)hipStreamDestroy(copy_s);
+  }
+};
+
+namespace {
 
 struct Level {
   int64_t n = 0;
@@ -157,11 +193,22 @@ struct MineRun {
   const int32_t* d_ids;
   const uint32_t* gram = nullptr;  // root-level pair counts (dense F x F) if computed
   int64_t F = 0;
-  DevVec<int64_t> out_parent;
-  DevVec<int32_t> out_item;
-  DevVec<uint32_t> out_count;
-  DevVec<uint8_t> out_depth;
+  OutBufs* ob = nullptr;
+  DevVec<int64_t>& out_parent;
+  DevVec<int32_t>& out_item;
+  DevVec<uint32_t>& out_count;
+  DevVec<uint8_t>& out_depth;
   int64_t out_size = 0;
+  // streamed download: [0, streamed) already queued to the pinned host arrays on ob->copy_s
+  bool stream_dl = false;
+  int64_t host_cap = 0, streamed = 0;
+  int64_t* h_parent = nullptr;
+  int32_t* h_item = nullptr;
+  uint32_t* h_count = nullptr;
+  uint8_t* h_depth = nullptr;
+
+  explicit MineRun(OutBufs* o)
+      : ob(o), out_parent(o->parent), out_item(o->item), out_count(o->count), out_depth(o->depth) {}
   int64_t n_candidates = 0;
   int max_depth = 1;
   int64_t* h_scalar = nullptr;  // pinned [2]
@@ -181,7 +228,26 @@ struct MineRun {
     next_total = h_scalar[1];
   }
 
+  // queue the D2H copy of the nodes finished since the last call (ordered after them on s)
+  void stream_out() {
+    if (!stream_dl || out_size <= streamed) return;
+    if (out_size > host_cap) {  // pinned arrays too small: the final download does it all
+      stream_dl = false;
+      return;
+    }
+    const int64_t a = streamed, n = out_size - streamed;
+    KMLS_HIP(hipEventRecord(ob->ev, s));
+    KMLS_HIP(hipStreamWaitEvent(ob->copy_s, ob->ev, 0));
+    KMLS_HIP(hipMemcpyAsync(h_parent + a, out_parent.p + a, n * sizeof(int64_t), hipMemcpyDeviceToHost, ob->copy_s));
+    KMLS_HIP(hipMemcpyAsync(h_item + a, out_item.p + a, n * sizeof(int32_t), hipMemcpyDeviceToHost, ob->copy_s));
+    KMLS_HIP(hipMemcpyAsync(h_count + a, out_count.p + a, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ob->copy_s));
+    KMLS_HIP(hipMemcpyAsync(h_depth + a, out_depth.p + a, n * sizeof(uint8_t), hipMemcpyDeviceToHost, ob->copy_s));
+    streamed = out_size;
+  }
+
   void ensure_out(int64_t n) {
+    if (n > out_parent.cap || n > out_item.cap || n > out_count.cap || n > out_depth.cap)
+      KMLS_HIP(hipStreamSynchronize(ob->copy_s));  // in-flight copies read the old arrays
     out_parent.reserve(n, s);
     out_item.reserve(n, s);
     out_count.reserve(n, s);
@@ -315,6 +381,7 @@ struct MineRun {
       KMLS_HIP(hipMemcpyAsync(out_count.p + out_size, cnt2, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
       KMLS_HIP(hipMemcpyAsync(out_depth.p + out_size, dep2, V * sizeof(uint8_t), hipMemcpyDeviceToDevice, s));
       out_size += V;
+      stream_out();
     }
     n_candidates += (int64_t)h.candidates;
     max_depth = std::max<int>(max_depth, (int)h.max_depth);
@@ -322,6 +389,130 @@ struct MineRun {
     arena->pop_to(mark);
     return true;
   }
+
+
+  // ---- fused, host-sync-free level expansion (levels.hip) -----------------------------------
+  // All levels are enqueued back to back (2 kernels per level, sizes stay on the device); the
+  // host synchronises once per batch of levels.  Returns false with nothing committed when a
+  // device-side capacity check fails — the caller then runs the chunked path (process()).
+  std::shared_ptr<PinnedPool> pinned;
+  bool run_fast(const Level& root, const std::vector<int64_t>& root_off, int64_t root_total) {
+    constexpr int kMaxLv = 64;
+    const int64_t Fr = root.n;
+    const size_t mark = arena->mark();
+    const int64_t row_bytes = Wp * 8 + 4 + 8 + 4 + 8;  // child bitmap + rank + gid + prow + pos
+    const size_t root_need = (size_t)(root_total + 1) * (size_t)row_bytes + (size_t)(Fr + 1) * 8 +
+                             kMaxLv * sizeof(kern::FLevel) + 4096;
+    const size_t free_b = arena->capacity() - arena->used();
+    if (root_need + (256ull << 20) > free_b) return false;
+    {
+      const int64_t want = std::max<int64_t>(out_size + root_total + 1, fast_hint);
+      ensure_out(want);
+    }
+    const int64_t out_cap = std::min<int64_t>({out_parent.cap, out_item.cap, out_count.cap, out_depth.cap});
+    if (out_size + root_total > out_cap) return false;
+    kern::FLevel* d_desc = (kern::FLevel*)arena->push(kMaxLv * sizeof(kern::FLevel));
+    kern::FCtl* d_ctl = (kern::FCtl*)arena->push(sizeof(kern::FCtl));
+    int64_t* d_off = (int64_t*)arena->push((size_t)(Fr + 1) * 8);
+    int64_t* d_pos = (int64_t*)arena->push((size_t)(root_total + 1) * 8);
+    uint64_t* c_bm = (uint64_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * Wp * 8);
+    int32_t* c_rank = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
+    int64_t* c_gid = (int64_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 8);
+    int32_t* c_prow = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
+    const size_t rem = arena->capacity() - arena->used();
+    const size_t bump_bytes = rem > (320ull << 20) ? rem - (64ull << 20) : 0;
+    if (bump_bytes < (256ull << 20)) {
+      arena->pop_to(mark);
+      return false;
+    }
+    char* bump_base = (char*)arena->push(bump_bytes);
+    // host-side descriptors → device (pinned staging, alive until the first sync below)
+    const size_t stage_bytes = kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl) + (size_t)(Fr + 1) * 8;
+    std::shared_ptr<void> stage = pinned->get(stage_bytes);
+    kern::FLevel* h_desc = (kern::FLevel*)stage.get();
+    std::memset(h_desc, 0, kMaxLv * sizeof(kern::FLevel));
+    kern::FCtl* h_ctl = (kern::FCtl*)(h_desc + kMaxLv);
+    std::memset(h_ctl, 0, sizeof(kern::FCtl));
+    int64_t* h_off = (int64_t*)(h_ctl + 1);
+    std::memcpy(h_off, root_off.data(), (size_t)(Fr + 1) * 8);
+    kern::FLevel& r = h_desc[1];
+    r.n_rows = Fr;
+    r.bm = root.bm;
+    r.rank = root.rank;
+    r.gid = root.gid;
+    r.cand_off = d_off;
+    r.n_cand = root_total;
+    r.pos = d_pos;
+    r.child_base = out_size;
+    h_desc[2].bm = c_bm;
+    h_desc[2].rank = c_rank;
+    h_desc[2].gid = c_gid;
+    h_desc[2].prow = c_prow;
+    h_ctl->bump_base = bump_base;
+    h_ctl->bump_cap = bump_bytes;
+    h_ctl->status_cap = (unsigned long long)ob->status_cap;
+    KMLS_HIP(hipMemcpyAsync(d_desc, h_desc, stage_bytes - (size_t)(Fr + 1) * 8, hipMemcpyHostToDevice, s));
+    KMLS_HIP(hipMemcpyAsync(d_off, h_off, (size_t)(Fr + 1) * 8, hipMemcpyHostToDevice, s));
+    const int grid = kern::level_grid(n_cus);
+    kern::CopyOutArgs co{out_parent.p, out_item.p, out_count.p, out_depth.p,
+                         h_parent, h_item, h_count, h_depth, stream_dl ? host_cap : 0};
+    auto count_level = [&](int L) {
+      kern::LevelCountArgs a{Wp, minsup, L == 1 ? gram : nullptr, F, d_ids, out_parent.p,
+                             out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1)};
+      kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a, grid, s);
+      if (stream_dl) {
+        KMLS_HIP(hipEventRecord(ob->ev, s));
+        KMLS_HIP(hipStreamWaitEvent(ob->copy_s, ob->ev, 0));
+        kern::level_copyout(&d_desc[L], &d_desc[L + 1], d_ctl, co, ob->copy_s);
+      }
+    };
+    const int L_allowed = std::min(kMaxLv - 2, max_len ? max_len - 1 : kMaxLv - 2);
+    count_level(1);
+    int last = 1;
+    int target = std::min(L_allowed, std::max(ob->depth_hint, 2));
+    std::shared_ptr<void> back = pinned->get(kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
+    kern::FLevel* b_desc = (kern::FLevel*)back.get();
+    kern::FCtl* b_ctl = (kern::FCtl*)(b_desc + kMaxLv);
+    bool ok = true;
+    while (true) {
+      for (int L = last + 1; L <= target; ++L) {
+        kern::level_scan(&d_desc[L - 1], &d_desc[L], &d_desc[L + 1], d_ctl, ob->status,
+                         ob->next_epoch(s), Wp, out_cap, grid, s);
+        count_level(L);
+        last = L;
+      }
+      KMLS_HIP(hipMemcpyAsync(b_desc, d_desc, kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl),
+                              hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipStreamSynchronize(s));
+      if (b_ctl->overflow) {
+        ok = false;
+        break;
+      }
+      if (last < L_allowed && b_desc[last + 1].n_rows >= 2) {
+        target = std::min(L_allowed, last + 4);
+        continue;
+      }
+      break;
+    }
+    KMLS_HIP(hipStreamSynchronize(ob->copy_s));
+    if (!ok) {
+      arena->pop_to(mark);
+      return false;
+    }
+    const int64_t new_size = b_desc[last + 1].child_base;
+    for (int L = 1; L <= last; ++L)
+      if (b_desc[L + 1].n_rows > 0) max_depth = std::max(max_depth, L + 1);
+    n_candidates += (int64_t)b_ctl->candidates;
+    out_size = new_size;
+    if (stream_dl) {
+      if (b_ctl->dl_overflow) stream_dl = false;  // final full copy
+      else streamed = out_size;
+    }
+    ob->depth_hint = std::max(2, max_depth);
+    arena->pop_to(mark);
+    return true;
+  }
+  int64_t fast_hint = 0;
 
   int64_t read_i64(const int64_t* dptr) {
     KMLS_HIP(hipMemcpyAsync(h_scalar, dptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -390,6 +581,7 @@ struct MineRun {
       kern::extend_materialize(L.bm, Wp, cand_off, L.n, L.rank, L.gid, d_ids, c0, c1, cnt, minsup,
                                pos, o, s);
       out_size += S;
+      stream_out();
       max_depth = std::max(max_depth, depth + 1);
       C.bm = cbm;
       C.rank = crank;
@@ -401,6 +593,11 @@ struct MineRun {
     arena->pop_to(mark0);
   }
 };
+
+bool fused_levels_enabled() {
+  const char* e = std::getenv("KMLS_FUSED_LEVELS");
+  return !(e && e[0] == '0');
+}
 
 size_t default_arena_bytes() {
   size_t free_b = 0, total_b = 0;
@@ -450,6 +647,7 @@ GpuMiner::~GpuMiner() {
   if (d_ids_) (void)hipFree(d_ids_);
   if (d_own_bm_) (void)hipFree(d_own_bm_);
   if (abort_host_) (void)hipHostFree(abort_host_);
+  out_.reset();
   arena_.reset();
   if (own_stream_) (void)hipStreamDestroy((hipStream_t)stream_);
 }
@@ -545,7 +743,8 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   KMLS_HIP(hipEventRecord(e0.e, s));
   std::unique_ptr<MineRun> runp;
   for (int attempt = 0;; ++attempt) {
-  runp = std::make_unique<MineRun>();
+  if (!out_) out_ = std::make_unique<OutBufs>();
+  runp = std::make_unique<MineRun>(out_.get());
   MineRun& run = *runp;
   run.persistent = cfg.persistent;
   run.rows_hint = rows_hint_;
@@ -562,7 +761,19 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   KMLS_HIP(hipHostMalloc((void**)&run.h_scalar, 64));
   KMLS_HIP(hipMalloc((void**)&run.d_pair, 2 * sizeof(uint64_t)));
   // level-1 nodes: gid = Eclat rank
-  run.ensure_out(std::max<int64_t>(F * 8, 1 << 16));
+  run.ensure_out(std::max<int64_t>({F * 8, (int64_t)1 << 16, last_nodes_ + (last_nodes_ >> 3)}));
+  if (download) {  // pinned host arrays sized from the previous trie; levels stream into them
+    run.host_cap = std::max<int64_t>({F * 8, (int64_t)1 << 16, last_nodes_ + (last_nodes_ >> 3)});
+    res.h_parent = pinned_->get((size_t)run.host_cap * sizeof(int64_t));
+    res.h_item = pinned_->get((size_t)run.host_cap * sizeof(int32_t));
+    res.h_count = pinned_->get((size_t)run.host_cap * sizeof(uint32_t));
+    res.h_depth = pinned_->get((size_t)run.host_cap * sizeof(uint8_t));
+    run.h_parent = (int64_t*)res.h_parent.get();
+    run.h_item = (int32_t*)res.h_item.get();
+    run.h_count = (uint32_t*)res.h_count.get();
+    run.h_depth = (uint8_t*)res.h_depth.get();
+    run.stream_dl = true;
+  }
   {
     std::vector<int64_t> par((size_t)F, -1);
     std::vector<uint8_t> dep((size_t)F, 1);
@@ -574,6 +785,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       KMLS_HIP(hipStreamSynchronize(s));  // par/dep are pageable and die at scope end
     }
     run.out_size = F;
+    run.stream_out();
   }
   if (F >= 2 && run.max_len != 1) {
     // root level: one class of all F frequent items
@@ -612,7 +824,16 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     root.rank = d_rank;
     root.gid = d_gid;
     root.row_end = d_end;
-    run.process(root, 1, d_len, root_total);
+    bool done = false;
+    if (!cfg.persistent && fused_levels_enabled()) {
+      std::vector<int64_t> off((size_t)F + 1, 0);
+      for (int64_t a = 0; a < F; ++a) off[a + 1] = off[a] + root_len[a];
+      run.pinned = pinned_;
+      run.fast_hint = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 4ll << 20);
+      done = run.run_fast(root, off, root_total);
+    }
+    if (!done) run.process(root, 1, d_len, root_total);
+    res.levels_path = done ? "fused" : (cfg.persistent ? "persistent" : "chunked");
     KMLS_HIP(hipStreamSynchronize(s));  // host staging vectors die at scope end
   } else {
     KMLS_HIP(hipEventRecord(e1.e, s));
@@ -623,16 +844,25 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     break;
   }
   arena_->pop_to(mark);
+  KMLS_HIP(hipStreamSynchronize(out_->copy_s));
   (void)hipHostFree(run.h_scalar);
   run.h_scalar = nullptr;
   (void)hipFree(run.d_pair);
   run.d_pair = nullptr;
+  res.h_parent.reset();
+  res.h_item.reset();
+  res.h_count.reset();
+  res.h_depth.reset();
   }
   MineRun& run = *runp;
   KMLS_HIP(hipEventRecord(e2.e, s));
   const int64_t N = run.out_size;
   res.n_nodes = N;
-  if (download) {
+  last_nodes_ = N;
+  if (download && run.stream_dl) {
+    run.stream_out();  // tail (normally empty: every chunk streamed itself)
+  } else if (download) {  // the trie outgrew the pinned arrays: one full copy
+    KMLS_HIP(hipStreamSynchronize(out_->copy_s));
     res.h_parent = pinned_->get((size_t)N * sizeof(int64_t));
     res.h_item = pinned_->get((size_t)N * sizeof(int32_t));
     res.h_count = pinned_->get((size_t)N * sizeof(uint32_t));
@@ -646,6 +876,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   }
   KMLS_HIP(hipEventRecord(e3.e, s));
   KMLS_HIP(hipStreamSynchronize(s));
+  KMLS_HIP(hipStreamSynchronize(out_->copy_s));
   res.phases.push_back({"level2_gram", elapsed(e0, e1)});
   res.phases.push_back({"levels_3plus", elapsed(e1, e2)});
   res.phases.push_back({"download", elapsed(e2, e3)});

@@ -68,7 +68,10 @@ struct GpuMineResult {
   MineStats stats;
   std::vector<Phase> phases;  // hipEvent-timed phases
   int64_t arena_high_water = 0;
+  std::string levels_path = "none";  // "fused" | "chunked" | "persistent" | "none"
 };
+
+struct OutBufs;  // persistent device trie buffers + download stream (miner_gpu.hip)
 
 // Resident-data GPU miner.  Typical use: load() once (CSR → HBM), mine() many times.
 // Multi-GPU: every rank calls the same sequence; collectives are done by the Python layer
@@ -130,6 +133,8 @@ class GpuMiner {
   unsigned int* abort_host_ = nullptr;       // watchdog flag (pinned, device-mapped)
   const unsigned int* abort_dev_ = nullptr;
   int n_cus_ = 256;
+  std::unique_ptr<OutBufs> out_;  // output trie kept allocated across mine() calls
+  int64_t last_nodes_ = 0;        // size of the previous trie (pinned download sizing)
 };
 
 // HBM-resident rule index + batched matcher kernel (serve_match_topk).

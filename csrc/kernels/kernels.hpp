@@ -54,6 +54,61 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
 void gram_to_cand(const uint32_t* gram, int64_t F, const int64_t* cand_off, int64_t c0, int64_t c1,
                   uint32_t* cnt, hipStream_t s);
 
+// ---- fused host-sync-free levels (levels.hip) ----
+struct FLevel {  // device-resident descriptor of one level (rows = itemsets of one size)
+  int64_t n_rows;
+  const uint64_t* bm;      // [n_rows][Wp]
+  const int32_t* rank;     // last item's Eclat rank
+  const int64_t* gid;      // trie node id
+  const int32_t* prow;     // row in the parent level
+  int64_t* cand_off;       // [n_rows + 1]
+  int64_t n_cand;
+  int64_t* pos;            // [n_cand + 1] survivor index of each candidate
+  int64_t child_base;      // trie id of this level's first child
+  unsigned int scan_ticket, count_ticket;
+  char pad[40];
+};
+struct FCtl {
+  char* bump_base;
+  unsigned long long bump_cap, bump_top;
+  unsigned long long status_cap;   // look-back tiles available
+  unsigned long long candidates;   // Σ n_cand over the counted levels
+  unsigned int overflow;           // 1 bump, 2 spin, 3/4 capacity → host falls back
+  unsigned int dl_overflow;        // pinned host arrays too small → host copies at the end
+};
+struct LevelCountArgs {
+  int64_t Wp;
+  uint32_t minsup;
+  const uint32_t* gram;    // root level: dense F x F pair counts (else nullptr)
+  int64_t F;
+  const int32_t* ids;      // Eclat rank → original item id
+  int64_t* out_parent;
+  int32_t* out_item;
+  uint32_t* out_count;
+  uint8_t* out_depth;
+  uint8_t child_depth;
+};
+struct CopyOutArgs {
+  const int64_t* d_parent;
+  const int32_t* d_item;
+  const uint32_t* d_count;
+  const uint8_t* d_depth;
+  int64_t* h_parent;
+  int32_t* h_item;
+  uint32_t* h_count;
+  uint8_t* h_depth;
+  int64_t host_cap;
+};
+int level_grid(int n_cus);
+int64_t level_tile();
+int64_t level_scan_tile();
+void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status,
+                unsigned epoch, int64_t Wp, int64_t out_cap, int grid, hipStream_t s);
+void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
+                 const LevelCountArgs& a, int grid, hipStream_t s);
+void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const CopyOutArgs& a,
+                   hipStream_t s);
+
 // ---- persistent DFS (dfs_persistent.hip) ----
 struct DfsTask {
   const unsigned long long* bm;  // class members' bitmaps [n][Wp]

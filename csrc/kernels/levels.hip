@@ -1,0 +1,438 @@
+// Fused, host-sync-free level expansion for the GPU FP-Growth miner (levels >= 2).
+//
+// The chunked driver (mine.hip + miner_gpu.hip "process") needs the host between every step of a
+// level: survivor counts size the child buffers, candidate totals size the next launch.  Here
+// every size lives in a device-resident descriptor (FLevel) and every launch is a fixed grid of
+// persistent blocks that pull tiles from a ticket counter, so the host enqueues all levels back
+// to back and synchronises ONCE per mining call.  Two kernels per level:
+//
+//   k_level_scan  (level L >= 2): len[s] = #siblings after s in its class (from the parent
+//                 level's survivor positions), single-pass decoupled-look-back exclusive scan →
+//                 cand_off, n_cand; the last tile bump-allocates the level's outputs.
+//   k_level_count (every level): per 256-candidate tile — decode (a, b) against an LDS window of
+//                 cand_off, wave64-team AND+popcount (or a gram lookup at the root), block scan
+//                 of the survivor flags + decoupled look-back → global survivor index, then
+//                 materialise survivors (child bitmap, rank, gid, parent row, trie append) in
+//                 the same kernel.  This fuses the chunked path's count, flag scan (2 rocprim
+//                 kernels), child_totals and materialise launches, and reads each parent row
+//                 pair once into L1/L2 for both phases.
+//   k_level_copyout: streams a finished level of the trie to pinned host memory (side stream).
+//
+// Look-back status words pack (epoch:24 | flag:2 | value:38) in one 64-bit word, so publishing
+// needs no fence, and the per-call epoch makes re-zeroing the status array unnecessary.
+// Every spin is bounded: a bug sets FCtl::overflow and the host falls back to the chunked path
+// instead of hanging the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+#include "kernels.hpp"
+
+#define KMLS_HIP(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +      \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__));     \
+  } while (0)
+
+namespace kmls {
+namespace kern {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kTile = 256;              // candidates per count tile
+constexpr int kScanItems = 8;           // rows per thread in the scan
+constexpr int kScanTile = kBlock * kScanItems;
+constexpr int kWin = 1024;              // LDS cand_off window (rows) per count tile
+constexpr unsigned long long kValMask = (1ull << 38) - 1;
+constexpr long long kSpinLimit = 1ll << 26;
+
+__device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long pack(unsigned epoch, unsigned flag,
+                                                   unsigned long long v) {
+  return ((unsigned long long)(epoch & 0xFFFFFFu) << 40) | ((unsigned long long)flag << 38) |
+         (v & kValMask);
+}
+
+// Single-thread decoupled look-back for tile t; returns the exclusive prefix of the tile.
+__device__ int64_t lookback(unsigned long long* st, int64_t t, unsigned epoch, int64_t agg,
+                            FCtl* ctl) {
+  const unsigned e = epoch & 0xFFFFFFu;
+  if (t == 0) {
+    st_relaxed(&st[0], pack(e, 2, (unsigned long long)agg));
+    return 0;
+  }
+  st_relaxed(&st[t], pack(e, 1, (unsigned long long)agg));
+  int64_t excl = 0;
+  int64_t j = t - 1;
+  long long spins = 0;
+  while (j >= 0) {
+    const unsigned long long w = ld_relaxed(&st[j]);
+    const unsigned we = (unsigned)(w >> 40), wf = (unsigned)(w >> 38) & 3u;
+    if (we != e || wf == 0) {
+      if (++spins > kSpinLimit) {  // never expected: predecessors always make progress
+        atomicExch(&ctl->overflow, 2u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    excl += (int64_t)(w & kValMask);
+    if (wf == 2) break;
+    --j;
+  }
+  st_relaxed(&st[t], pack(e, 2, (unsigned long long)(excl + agg)));
+  return excl;
+}
+
+// Bump allocation from the device region (256-byte aligned); nullptr + overflow flag if full.
+__device__ void* bump(FCtl* ctl, unsigned long long bytes) {
+  bytes = (bytes + 255ull) & ~255ull;
+  const unsigned long long off = atomicAdd(&ctl->bump_top, bytes);
+  if (off + bytes > ctl->bump_cap) {
+    atomicExch(&ctl->overflow, 1u);
+    return nullptr;
+  }
+  return ctl->bump_base + off;
+}
+
+// Block-wide exclusive scan of one int64 per thread (256 threads = 4 waves); returns the
+// thread's exclusive prefix, *total = block sum.
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* s_w, int64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  int64_t wbase = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kBlock / 64; ++i) {
+    if (i < w) wbase += s_w[i];
+    tot += s_w[i];
+  }
+  *total = tot;
+  return wbase + x - v;
+}
+
+__device__ __forceinline__ int64_t find_row_g(const int64_t* __restrict__ off, int64_t lo,
+                                              int64_t hi, int64_t c) {
+  // largest a in [lo, hi) with off[a] <= c
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (off[mid] <= c) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
+                                                       FLevel* __restrict__ lv,
+                                                       FLevel* __restrict__ nx, FCtl* ctl,
+                                                       unsigned long long* __restrict__ status,
+                                                       unsigned epoch, int64_t Wp,
+                                                       int64_t out_cap) {
+  __shared__ int64_t s_w[kBlock / 64];
+  __shared__ int64_t s_base;
+  __shared__ int64_t s_ticket;
+  if (ctl->overflow) return;
+  const int64_t n = lv->n_rows;
+  const int64_t n_tiles = (n + kScanTile - 1) / kScanTile;
+  if (n_tiles > (int64_t)ctl->status_cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&ctl->overflow, 3u);
+    return;
+  }
+  if (n == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      lv->n_cand = 0;
+      nx->n_rows = 0;
+      nx->child_base = lv->child_base;
+    }
+    return;
+  }
+  const int32_t* __restrict__ prow = lv->prow;
+  const int64_t* __restrict__ pco = pv->cand_off;
+  const int64_t* __restrict__ ppos = pv->pos;
+  int64_t* __restrict__ co = lv->cand_off;
+  while (true) {
+    if (threadIdx.x == 0) s_ticket = (int64_t)atomicAdd(&lv->scan_ticket, 1u);
+    __syncthreads();
+    const int64_t t = s_ticket;
+    if (t >= n_tiles) return;
+    const int64_t s0 = t * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    int64_t len[kScanItems];
+    int64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+      const int64_t s = s0 + i;
+      int64_t l = 0;
+      if (s < n) {
+        const int64_t a = prow[s];
+        l = ppos[pco[a + 1]] - s - 1;  // siblings after s in its class
+      }
+      len[i] = l;
+      sum += l;
+    }
+    int64_t tile_total;
+    const int64_t excl = block_excl_scan(sum, s_w, &tile_total);
+    if (threadIdx.x == 0) s_base = lookback(status, t, epoch, tile_total, ctl);
+    __syncthreads();
+    int64_t run = s_base + excl;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+      const int64_t s = s0 + i;
+      if (s < n) co[s] = run;
+      run += len[i];
+    }
+    if (t == n_tiles - 1 && threadIdx.x == 0) {
+      const int64_t total = s_base + tile_total;
+      co[n] = total;
+      lv->n_cand = total;
+      const int64_t tiles = (total + kTile - 1) / kTile;
+      if (lv->child_base + total > out_cap || tiles > (int64_t)ctl->status_cap) {
+        atomicExch(&ctl->overflow, 4u);
+      } else if (total > 0) {
+        lv->pos = (int64_t*)bump(ctl, (unsigned long long)(total + 1) * 8ull);
+        nx->bm = (const uint64_t*)bump(ctl, (unsigned long long)total * (unsigned long long)Wp * 8ull);
+        nx->rank = (const int32_t*)bump(ctl, (unsigned long long)total * 4ull);
+        nx->gid = (const int64_t*)bump(ctl, (unsigned long long)total * 8ull);
+        nx->prow = (const int32_t*)bump(ctl, (unsigned long long)total * 4ull);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int TS>
+__global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
+                                                        FLevel* __restrict__ nx, FCtl* ctl,
+                                                        unsigned long long* __restrict__ status,
+                                                        unsigned epoch, LevelCountArgs A) {
+  __shared__ int64_t s_off[kWin + 1];
+  __shared__ uint32_t s_cnt[kTile];
+  __shared__ int32_t s_lpos[kTile];
+  __shared__ int64_t s_w[kBlock / 64];
+  __shared__ int64_t s_rr[2];
+  __shared__ int64_t s_base;
+  __shared__ int64_t s_ticket;
+  if (ctl->overflow) return;
+  const int64_t n_cand = lv->n_cand;
+  const int64_t n_rows = lv->n_rows;
+  const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
+  const int64_t child_base = lv->child_base;
+  if (n_tiles == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      nx->n_rows = 0;
+      nx->child_base = child_base;
+      nx->cand_off = (int64_t*)bump(ctl, 8ull);
+      if (nx->cand_off) nx->cand_off[0] = 0;
+    }
+    return;
+  }
+  const int64_t* __restrict__ co = lv->cand_off;
+  const unsigned long long* __restrict__ bm = (const unsigned long long*)lv->bm;
+  const int32_t* __restrict__ rank = lv->rank;
+  const int64_t* __restrict__ gid = lv->gid;
+  int64_t* __restrict__ pos = lv->pos;
+  unsigned long long* __restrict__ cbm = (unsigned long long*)nx->bm;
+  int32_t* __restrict__ crank = (int32_t*)nx->rank;
+  int64_t* __restrict__ cgid = (int64_t*)nx->gid;
+  int32_t* __restrict__ cprow = (int32_t*)nx->prow;
+  const int64_t Wp = A.Wp;
+  const int64_t n2 = Wp >> 1;
+  const int tl = threadIdx.x & (TS - 1);
+  const int team = threadIdx.x / TS;
+  constexpr int kTeams = kBlock / TS;
+  constexpr int kPer = kTile / kTeams;
+  while (true) {
+    if (threadIdx.x == 0) s_ticket = (int64_t)atomicAdd(&lv->count_ticket, 1u);
+    __syncthreads();
+    const int64_t t = s_ticket;
+    if (t >= n_tiles) return;
+    const int64_t c0 = t * kTile;
+    const int cn = (int)min((int64_t)kTile, n_cand - c0);
+    if (threadIdx.x < 2)
+      s_rr[threadIdx.x] = find_row_g(co, 0, n_rows, c0 + (threadIdx.x ? cn - 1 : 0));
+    __syncthreads();
+    const int64_t r0 = s_rr[0], r1 = s_rr[1];
+    const int64_t nr = r1 - r0 + 1;
+    const bool win = nr + 1 <= kWin;
+    if (win)
+      for (int64_t i = threadIdx.x; i <= nr; i += kBlock) s_off[i] = co[r0 + i];
+    __syncthreads();
+    // ---- phase 1: supports ----
+    for (int j = 0; j < kPer; ++j) {
+      const int i = team * kPer + j;
+      if (i >= cn) break;  // team-uniform
+      const int64_t c = c0 + i;
+      int64_t a, oa;
+      if (win) {
+        int64_t lo = 0, hi = nr;  // largest k in [0, nr) with s_off[k] <= c
+        while (hi - lo > 1) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (s_off[mid] <= c) lo = mid; else hi = mid;
+        }
+        a = r0 + lo;
+        oa = s_off[lo];
+      } else {
+        a = find_row_g(co, r0, r1 + 1, c);
+        oa = co[a];
+      }
+      const int64_t b = a + 1 + (c - oa);
+      uint32_t k;
+      if (A.gram) {
+        k = A.gram[a * A.F + b];
+      } else {
+        const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
+        const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
+        uint32_t sacc = 0;
+        for (int64_t w = tl; w < n2; w += TS) {
+          const ulonglong2 u = x[w], v = y[w];
+          sacc += (uint32_t)__popcll(u.x & v.x) + (uint32_t)__popcll(u.y & v.y);
+        }
+#pragma unroll
+        for (int off = TS >> 1; off > 0; off >>= 1) sacc += __shfl_xor(sacc, off, TS);
+        k = sacc;
+      }
+      if (tl == 0) s_cnt[i] = k;
+    }
+    __syncthreads();
+    // ---- phase 2: survivor positions (block scan + look-back) ----
+    const int flag = ((int)threadIdx.x < cn && s_cnt[threadIdx.x] >= A.minsup) ? 1 : 0;
+    int64_t tile_total;
+    const int64_t lx = block_excl_scan(flag, s_w, &tile_total);
+    s_lpos[threadIdx.x] = (int32_t)lx;
+    if (threadIdx.x == 0) s_base = lookback(status, t, epoch, tile_total, ctl);
+    __syncthreads();
+    const int64_t base = s_base;
+    if ((int)threadIdx.x < cn) pos[c0 + threadIdx.x] = base + lx;
+    // ---- phase 3: materialise survivors ----
+    for (int j = 0; j < kPer; ++j) {
+      const int i = team * kPer + j;
+      if (i >= cn) break;
+      const uint32_t k = s_cnt[i];
+      if (k < A.minsup) continue;  // team-uniform
+      const int64_t c = c0 + i;
+      int64_t a, oa;
+      if (win) {
+        int64_t lo = 0, hi = nr;
+        while (hi - lo > 1) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (s_off[mid] <= c) lo = mid; else hi = mid;
+        }
+        a = r0 + lo;
+        oa = s_off[lo];
+      } else {
+        a = find_row_g(co, r0, r1 + 1, c);
+        oa = co[a];
+      }
+      const int64_t b = a + 1 + (c - oa);
+      const int64_t s = base + s_lpos[i];
+      const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
+      const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
+      ulonglong2* z = reinterpret_cast<ulonglong2*>(cbm + s * Wp);
+      for (int64_t w = tl; w < n2; w += TS) {
+        const ulonglong2 u = x[w], v = y[w];
+        z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
+      }
+      if (tl == 0) {
+        const int32_t rb = rank[b];
+        const int64_t node = child_base + s;
+        crank[s] = rb;
+        cgid[s] = node;
+        cprow[s] = (int32_t)a;
+        A.out_parent[node] = gid[a];
+        A.out_item[node] = A.ids[rb];
+        A.out_count[node] = k;
+        A.out_depth[node] = A.child_depth;
+      }
+    }
+    if (t == n_tiles - 1 && threadIdx.x == 0) {
+      const int64_t S = base + tile_total;
+      pos[n_cand] = S;
+      nx->n_rows = S;
+      nx->child_base = child_base + S;
+      nx->cand_off = (int64_t*)bump(ctl, (unsigned long long)(S + 1) * 8ull);
+      atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_level_copyout(const FLevel* __restrict__ lv,
+                                                          const FLevel* __restrict__ nx,
+                                                          FCtl* ctl, CopyOutArgs A) {
+  if (ctl->overflow) return;
+  const int64_t base = lv->child_base;
+  const int64_t S = nx->n_rows;
+  if (S <= 0) return;
+  if (base + S > A.host_cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&ctl->dl_overflow, 1u);
+    return;
+  }
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < base + S; i += nthr) {
+    A.h_parent[i] = A.d_parent[i];
+    A.h_item[i] = A.d_item[i];
+    A.h_count[i] = A.d_count[i];
+    A.h_depth[i] = A.d_depth[i];
+  }
+}
+
+int team_size_for(int64_t Wp) {
+  const int64_t chunks = Wp >> 1;  // 16-byte chunks per row
+  if (chunks >= 128) return 64;
+  if (chunks >= 64) return 32;
+  if (chunks >= 32) return 16;
+  if (chunks >= 12) return 8;
+  return 4;
+}
+
+}  // namespace
+
+int level_grid(int n_cus) { return std::max(64, n_cus * 4); }
+
+void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status,
+                unsigned epoch, int64_t Wp, int64_t out_cap, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_level_scan, dim3(grid), dim3(kBlock), 0, s, pv, lv, nx, ctl, status, epoch,
+                     Wp, out_cap);
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
+                 const LevelCountArgs& a, int grid, hipStream_t s) {
+  switch (team_size_for(a.Wp)) {
+    case 4: hipLaunchKernelGGL(k_level_count<4>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
+    case 8: hipLaunchKernelGGL(k_level_count<8>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
+    case 16: hipLaunchKernelGGL(k_level_count<16>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
+    case 32: hipLaunchKernelGGL(k_level_count<32>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
+    default: hipLaunchKernelGGL(k_level_count<64>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
+  }
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const CopyOutArgs& a,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(k_level_copyout, dim3(256), dim3(kBlock), 0, s, lv, nx, ctl, a);
+  KMLS_HIP(hipGetLastError());
+}
+
+int64_t level_tile() { return kTile; }
+int64_t level_scan_tile() { return kScanTile; }
+
+}  // namespace kern
+}  // namespace kmls

@@ -323,9 +323,11 @@ void flag_scan(const uint32_t* cnt, uint32_t minsup, int64_t n, int64_t* pos, vo
 // After the flag scan of chunk [c0, c1) over rows [a0, a1): child class of row a has
 // size k_a = pos[cand_off[a+1]-c0] - pos[cand_off[a]-c0]; the next level's candidate total is
 // Σ k_a (k_a - 1) / 2.  Written to out[1] (out[0] = #survivors) so ONE readback serves both.
-__global__ void k_child_totals(const int64_t* __restrict__ cand_off, int64_t a0, int64_t a1,
-                               int64_t c0, const int64_t* __restrict__ pos, int64_t nc,
-                               unsigned long long* __restrict__ out) {
+__global__ __launch_bounds__(kBlock) void k_child_totals(const int64_t* __restrict__ cand_off,
+                                                        int64_t a0, int64_t a1, int64_t c0,
+                                                        const int64_t* __restrict__ pos, int64_t nc,
+                                                        unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long part[kBlock / 64];
   const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
   unsigned long long acc = 0;
   for (int64_t a = a0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; a < a1; a += nthr) {
@@ -334,14 +336,22 @@ __global__ void k_child_totals(const int64_t* __restrict__ cand_off, int64_t a0,
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(&out[1], acc);
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&out[0], (unsigned long long)pos[nc]);
+  // one same-address atomic per block, not per wave: they serialise in L2
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+    if (t) atomicAdd(&out[1], t);
+    if (blockIdx.x == 0) atomicAdd(&out[0], (unsigned long long)pos[nc]);
+  }
 }
 
 void child_totals(const int64_t* cand_off, int64_t a0, int64_t a1, int64_t c0, const int64_t* pos,
                   int64_t nc, uint64_t* out2, hipStream_t s) {
   KMLS_HIP(hipMemsetAsync(out2, 0, 2 * sizeof(uint64_t), s));
-  hipLaunchKernelGGL(k_child_totals, dim3(grid_for(std::max<int64_t>(a1 - a0, 1), kBlock, 1024)),
+  hipLaunchKernelGGL(k_child_totals, dim3(grid_for(std::max<int64_t>(a1 - a0, 1), kBlock, 256)),
                      dim3(kBlock), 0, s, cand_off, a0, a1, c0, pos, nc,
                      (unsigned long long*)out2);
   KMLS_HIP(hipGetLastError());

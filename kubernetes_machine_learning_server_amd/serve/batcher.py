@@ -1,11 +1,13 @@
 """Async request micro-batcher feeding the HIP matcher (SURVEY §2.E "intra-process concurrency").
 
-Requests arriving within ``BATCH_WAIT_US`` (or until ``BATCH_MAX``) are concatenated into one
-CSR query batch; one ``serve_match_topk`` launch answers all of them (one workgroup per query)
-and the futures are resolved on the event loop.  Batches smaller than ``GPU_MIN_BATCH`` go to
-the C++ CPU matcher instead: for a handful of queries the ~20-40 µs H2D+launch+D2H round trip
-costs more than the CPU merge.  The device work runs in a worker thread (the native call
-releases the GIL), so the event loop keeps accepting requests while a batch is in flight.
+Requests already queued when the batcher wakes are concatenated into one CSR query batch; one
+``serve_match_topk`` launch answers all of them (one workgroup per query) and the futures are
+resolved on the event loop.  The batcher only WAITS (up to ``BATCH_WAIT_US``, until
+``BATCH_MAX``) when recent load shows that waiting fills a GPU-sized batch — at low QPS a
+timer would only add latency.  Batches smaller than ``GPU_MIN_BATCH`` are answered inline by
+the C++ CPU matcher (~1 µs/query; an executor hop alone costs ~50 µs); GPU batches run in a
+worker thread (the native call releases the GIL), so the event loop keeps accepting requests
+while a batch is in flight.
 """
 from __future__ import annotations
 
@@ -27,6 +29,7 @@ class MicroBatcher:
         self.gpu_batches = 0
         self.queries = 0
         self.last_batch = 0
+        self._load = 0.0  # EWMA of the immediately-available batch size
 
     def start(self) -> None:
         if self._task is None:
@@ -53,20 +56,24 @@ class MicroBatcher:
         while True:
             first = await self._q.get()
             items = [first]
-            deadline = time.perf_counter() + self.max_wait
-            while len(items) < self.max_batch:
+            while len(items) < self.max_batch:  # drain what is already queued
                 try:
                     items.append(self._q.get_nowait())
-                    continue
                 except asyncio.QueueEmpty:
-                    pass
-                rem = deadline - time.perf_counter()
-                if rem <= 0:
                     break
-                try:
-                    items.append(await asyncio.wait_for(self._q.get(), rem))
-                except asyncio.TimeoutError:
-                    break
+            self._load = 0.8 * self._load + 0.2 * len(items)
+            gpu = first[0].gpu_index is not None
+            if (gpu and self.max_wait > 0 and len(items) < self.gpu_min_batch
+                    and self._load * 4 >= self.gpu_min_batch):
+                deadline = time.perf_counter() + self.max_wait
+                while len(items) < self.max_batch:
+                    rem = deadline - time.perf_counter()
+                    if rem <= 0:
+                        break
+                    try:
+                        items.append(await asyncio.wait_for(self._q.get(), rem))
+                    except asyncio.TimeoutError:
+                        break
             # group by (snapshot, k): a reload between requests must not mix indices
             groups = {}
             for it in items:
@@ -74,7 +81,10 @@ class MicroBatcher:
             for (_, k), grp in groups.items():
                 snap = grp[0][0]
                 try:
-                    ids, n = await loop.run_in_executor(None, self._run_batch, snap, grp, k)
+                    if snap.gpu_index is not None and len(grp) >= self.gpu_min_batch:
+                        ids, n = await loop.run_in_executor(None, self._run_batch, snap, grp, k)
+                    else:
+                        ids, n = self._run_batch(snap, grp, k)
                     for j, it in enumerate(grp):
                         if not it[3].done():
                             it[3].set_result((ids[j], int(n[j])))

@@ -63,15 +63,18 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma):
     np.testing.assert_array_equal(pc.reshape(max(F, 1), Wp).sum(1)[:F], counts)
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("use_mfma", [False, True])
 @pytest.mark.parametrize("shape,ms", [("tiny", 0.05), ("tiny", 0.02), ("ds2_weak", 0.05),
                                       ("ds2_weak", 0.03), ("ds2", 0.07), ("ds2", 0.05)])
-def test_gpu_miner_matches_cpu(gpu_mod, shape, ms, use_mfma):
+def test_gpu_miner_matches_cpu(gpu_mod, shape, ms, use_mfma, fused, monkeypatch):
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    monkeypatch.setenv("KMLS_FUSED_LEVELS", fused)
     tx = generate(shape, seed=5)
     g = gpu_mod.GpuMiner(0, 1 << 31, 0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     r = g.mine(ms, mfma=use_mfma)
+    assert r["stats"]["levels_path"] == ("fused" if fused == "1" else "chunked")
     c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
     assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
     assert r["stats"]["max_depth"] == c["stats"]["max_depth"]
@@ -98,6 +101,7 @@ def test_gpu_miner_max_len_and_pairs(gpu_mod):
 def test_gpu_miner_chunked_levels(gpu_mod, monkeypatch):
     """Force many candidates per level (multi-chunk path) on a larger synthetic set."""
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    monkeypatch.setenv("KMLS_FUSED_LEVELS", "0")
     tx = generate("ds2", seed=9)
     g = gpu_mod.GpuMiner(0, 8 << 30, 0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
@@ -105,6 +109,30 @@ def test_gpu_miner_chunked_levels(gpu_mod, monkeypatch):
     c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.045)
     assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
     assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
+
+
+def test_fused_levels_repeat_and_small_arena(gpu_mod):
+    """Repeated calls (epoch-tagged look-back state, persistent output buffers, streamed
+    download sized from the previous call) and the fallback when the arena is too small."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    tx = generate("ds2", seed=3)
+    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.05)
+    g = gpu_mod.GpuMiner(0, 4 << 30, 0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    keep = []
+    for i in range(4):
+        r = g.mine(0.05)
+        assert r["stats"]["levels_path"] == "fused"
+        assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
+        assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
+        keep.append(r)  # results stay valid while later calls run (pinned buffers not reused)
+    for r in keep:
+        assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
+    small = gpu_mod.GpuMiner(0, 1 << 28, 0)
+    small.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    r = small.mine(0.05)
+    assert r["stats"]["levels_path"] == "chunked"
+    assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
 
 
 def test_gpu_serve_matches_cpu(gpu_mod):
