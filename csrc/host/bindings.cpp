@@ -96,6 +96,21 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("tx_ptr"), py::arg("items"), py::arg("n_items"), py::arg("min_support"),
      py::arg("max_len") = 0, py::arg("threads") = 0, py::arg("pairs_only") = false);
 
+  m.def("synth_transactions", [](int64_t n_tx, int64_t n_items, double mean_len, int n_genres,
+                                 double affinity, double zipf_s, uint64_t seed, int threads,
+                                 int64_t tx_begin, int64_t tx_end) {
+    std::vector<int64_t> ptr;
+    std::vector<int32_t> items;
+    {
+      py::gil_scoped_release nogil;
+      synth_transactions(n_tx, n_items, mean_len, n_genres, affinity, zipf_s, seed, threads, ptr,
+                         items, tx_begin, tx_end);
+    }
+    return py::make_tuple(to_array(std::move(ptr)), to_array(std::move(items)));
+  }, py::arg("n_tx"), py::arg("n_items"), py::arg("mean_len"), py::arg("n_genres"),
+     py::arg("affinity"), py::arg("zipf_s") = 0.85, py::arg("seed") = 0, py::arg("threads") = 0,
+     py::arg("tx_begin") = 0, py::arg("tx_end") = -1);
+
   m.def("select_frequent", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> counts,
                               int64_t n_tx, double ms) {
     FrequentItems f = select_frequent(counts.data(), counts.size(), (uint64_t)n_tx, ms);

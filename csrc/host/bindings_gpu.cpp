@@ -69,6 +69,45 @@ void register_gpu_bindings(py::module_& m) {
   m.def("gpu_device_count", &gpu::device_count);
   m.def("gpu_device_name", &gpu::device_name);
 
+  m.def("association_rules_gpu", [](I64 parent, I32 item, U32 count, U8 depth, int64_t n_tx,
+                                    int metric, double min_threshold, int max_antecedent,
+                                    int device) {
+    const int64_t n = item.size();
+    KMLS_CHECK(parent.size() == n && count.size() == n && depth.size() == n, "trie arrays differ in size");
+    RuleSet r;
+    double ms = 0;
+    {
+      py::gil_scoped_release nogil;
+      r = gpu::association_rules_gpu(device, parent.data(), item.data(), count.data(), depth.data(),
+                                     n, n_tx, (RuleMetric)metric, min_threshold, max_antecedent, &ms);
+    }
+    py::dict d;
+    d["itemset"] = to_array(std::move(r.itemset));
+    d["antecedent"] = to_array(std::move(r.antecedent));
+    d["consequent"] = to_array(std::move(r.consequent));
+    d["confidence"] = to_array(std::move(r.confidence));
+    d["lift"] = to_array(std::move(r.lift));
+    d["kernel_ms"] = ms;
+    return d;
+  }, py::arg("parent"), py::arg("item"), py::arg("count"), py::arg("depth"), py::arg("n_tx"),
+     py::arg("metric") = 0, py::arg("min_threshold") = 0.8, py::arg("max_antecedent") = 0,
+     py::arg("device") = 0);
+
+  m.def("comm_unique_id", []() { return py::bytes(gpu::comm_unique_id()); });
+  py::class_<gpu::Comm>(m, "Comm")
+      .def(py::init([](int rank, int world, py::bytes uid, int device) {
+             std::string u = uid;
+             py::gil_scoped_release nogil;
+             return new gpu::Comm(rank, world, u, device);
+           }), py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"))
+      .def_property_readonly("rank", &gpu::Comm::rank)
+      .def_property_readonly("world", &gpu::Comm::world)
+      .def("all_reduce_u32", [](gpu::Comm& c, uintptr_t buf, size_t n, uintptr_t stream) {
+        py::gil_scoped_release nogil;
+        c.all_reduce((void*)buf, (void*)buf, n, gpu::CommDtype::U32, false, (void*)stream);
+      })
+      .def("abort", &gpu::Comm::abort);
+
   py::class_<gpu::GpuMiner>(m, "GpuMiner")
       .def(py::init<int, size_t, uintptr_t>(), py::arg("device") = 0, py::arg("arena_bytes") = 0,
            py::arg("stream") = 0)
@@ -129,6 +168,17 @@ void register_gpu_bindings(py::module_& m) {
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("pairs_only") = false,
          py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
          py::arg("persistent") = false)
+      .def("mine_txdp", [](gpu::GpuMiner& g, gpu::Comm* comm, int64_t global_n_tx, double ms,
+                           int max_len, bool download, bool mfma, int support_tiles) {
+        gpu::GpuMineResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = g.mine_txdp(comm, global_n_tx, make_cfg(ms, max_len, false, true, mfma), download,
+                          support_tiles);
+        }
+        return result_to_dict(std::move(r));
+      }, py::arg("comm"), py::arg("global_n_tx"), py::arg("min_support"), py::arg("max_len") = 0,
+         py::arg("download") = true, py::arg("mfma") = false, py::arg("support_tiles") = 4)
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
   py::class_<gpu::GpuRuleIndex>(m, "GpuRuleIndex")

@@ -220,6 +220,7 @@ struct MineRun {
   const unsigned int* abort_dev = nullptr;
 
   uint64_t* d_pair = nullptr;   // device [survivors, next-level candidates]
+  Comm* comm = nullptr;         // tx-DP: candidate counts are shard-partial → all-reduce
 
   void read_pair(int64_t& S, int64_t& next_total) {
     KMLS_HIP(hipMemcpyAsync(h_scalar, d_pair, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -404,13 +405,19 @@ struct MineRun {
     const size_t root_need = (size_t)(root_total + 1) * (size_t)row_bytes + (size_t)(Fr + 1) * 8 +
                              kMaxLv * sizeof(kern::FLevel) + 4096;
     const size_t free_b = arena->capacity() - arena->used();
-    if (root_need + (256ull << 20) > free_b) return false;
+    if (root_need + (256ull << 20) > free_b) {
+      fallback_reason = "arena too small for the root level";
+      return false;
+    }
     {
       const int64_t want = std::max<int64_t>(out_size + root_total + 1, fast_hint);
       ensure_out(want);
     }
     const int64_t out_cap = std::min<int64_t>({out_parent.cap, out_item.cap, out_count.cap, out_depth.cap});
-    if (out_size + root_total > out_cap) return false;
+    if (out_size + root_total > out_cap) {
+      fallback_reason = "output capacity";
+      return false;
+    }
     kern::FLevel* d_desc = (kern::FLevel*)arena->push(kMaxLv * sizeof(kern::FLevel));
     kern::FCtl* d_ctl = (kern::FCtl*)arena->push(sizeof(kern::FCtl));
     int64_t* d_off = (int64_t*)arena->push((size_t)(Fr + 1) * 8);
@@ -423,6 +430,7 @@ struct MineRun {
     const size_t bump_bytes = rem > (320ull << 20) ? rem - (64ull << 20) : 0;
     if (bump_bytes < (256ull << 20)) {
       arena->pop_to(mark);
+      fallback_reason = "arena too small for the bump region";
       return false;
     }
     char* bump_base = (char*)arena->push(bump_bytes);
@@ -453,6 +461,19 @@ struct MineRun {
     h_ctl->status_cap = (unsigned long long)ob->status_cap;
     KMLS_HIP(hipMemcpyAsync(d_desc, h_desc, stage_bytes - (size_t)(Fr + 1) * 8, hipMemcpyHostToDevice, s));
     KMLS_HIP(hipMemcpyAsync(d_off, h_off, (size_t)(Fr + 1) * 8, hipMemcpyHostToDevice, s));
+    if (!levels_loop(d_desc, d_ctl, out_cap, false)) {
+      arena->pop_to(mark);
+      return false;
+    }
+    arena->pop_to(mark);
+    return true;
+  }
+
+  // The level loop shared by the host- and device-prepared fused paths: count level 1 (root),
+  // then scan+count per level, one host sync per batch of levels.  copy_level0: also stream the
+  // level-1 trie nodes (written on the device by the resident prologue).
+  bool levels_loop(kern::FLevel* d_desc, kern::FCtl* d_ctl, int64_t out_cap, bool copy_level0) {
+    constexpr int kMaxLv = 64;
     const int grid = kern::level_grid(n_cus);
     kern::CopyOutArgs co{out_parent.p, out_item.p, out_count.p, out_depth.p,
                          h_parent, h_item, h_count, h_depth, stream_dl ? host_cap : 0};
@@ -467,6 +488,11 @@ struct MineRun {
       }
     };
     const int L_allowed = std::min(kMaxLv - 2, max_len ? max_len - 1 : kMaxLv - 2);
+    if (copy_level0 && stream_dl) {
+      KMLS_HIP(hipEventRecord(ob->ev, s));
+      KMLS_HIP(hipStreamWaitEvent(ob->copy_s, ob->ev, 0));
+      kern::level_copyout(&d_desc[0], &d_desc[1], d_ctl, co, ob->copy_s);
+    }
     count_level(1);
     int last = 1;
     int target = std::min(L_allowed, std::max(ob->depth_hint, 2));
@@ -486,6 +512,10 @@ struct MineRun {
       KMLS_HIP(hipStreamSynchronize(s));
       if (b_ctl->overflow) {
         ok = false;
+        fallback_reason = "device overflow code " + std::to_string(b_ctl->overflow) +
+                          " at level " + std::to_string(last) + " (bump " +
+                          std::to_string(b_ctl->bump_top >> 20) + "/" +
+                          std::to_string(b_ctl->bump_cap >> 20) + " MiB)";
         break;
       }
       if (last < L_allowed && b_desc[last + 1].n_rows >= 2) {
@@ -495,10 +525,8 @@ struct MineRun {
       break;
     }
     KMLS_HIP(hipStreamSynchronize(ob->copy_s));
-    if (!ok) {
-      arena->pop_to(mark);
-      return false;
-    }
+    if (!ok) return false;
+    last_desc.assign(b_desc, b_desc + kMaxLv);
     const int64_t new_size = b_desc[last + 1].child_base;
     for (int L = 1; L <= last; ++L)
       if (b_desc[L + 1].n_rows > 0) max_depth = std::max(max_depth, L + 1);
@@ -509,10 +537,12 @@ struct MineRun {
       else streamed = out_size;
     }
     ob->depth_hint = std::max(2, max_depth);
-    arena->pop_to(mark);
     return true;
   }
+  std::vector<kern::FLevel> last_desc;  // host copy of the descriptors after levels_loop
+
   int64_t fast_hint = 0;
+  std::string fallback_reason;
 
   int64_t read_i64(const int64_t* dptr) {
     KMLS_HIP(hipMemcpyAsync(h_scalar, dptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -551,10 +581,12 @@ struct MineRun {
       if (nc == 0) continue;
       const size_t mark = arena->mark();
       uint32_t* cnt = (uint32_t*)arena->push((size_t)nc * sizeof(uint32_t));
-      if (gram && depth == 1)
-        kern::gram_to_cand(gram, F, cand_off, c0, c1, cnt, s);
-      else
+      if (gram && depth == 1) {
+        kern::gram_to_cand(gram, F, cand_off, c0, c1, cnt, s);  // gram already global
+      } else {
         kern::extend_count(L.bm, Wp, cand_off, L.n, c0, c1, cnt, s);
+        if (comm) comm->all_reduce(cnt, cnt, (size_t)nc, CommDtype::U32, false, s);
+      }
       int64_t* pos = (int64_t*)arena->push((size_t)(nc + 1) * sizeof(int64_t));
       const size_t fb = kern::flag_scan_temp_bytes(nc);
       void* ftmp = arena->push(fb);
@@ -670,6 +702,12 @@ void GpuMiner::load_csr(const int64_t* tx_ptr, const int32_t* items, int64_t n_t
   nnz_ = tx_ptr[n_tx] - base;
   std::vector<int64_t> rebased((size_t)n_tx + 1);
   for (int64_t t = 0; t <= n_tx; ++t) rebased[t] = tx_ptr[t] - base;
+  tile_tx_.assign(65, 0);
+  tile_nnz_.assign(65, 0);
+  for (int k = 0; k <= 64; ++k) {
+    tile_tx_[k] = n_tx * k / 64;
+    tile_nnz_[k] = rebased[tile_tx_[k]];
+  }
   for (int64_t p = 0; p < nnz_; ++p) {
     const int32_t it = items[base + p];
     KMLS_CHECK(it >= 0 && it < n_items, "item id out of range in CSR");
@@ -746,7 +784,8 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   if (!out_) out_ = std::make_unique<OutBufs>();
   runp = std::make_unique<MineRun>(out_.get());
   MineRun& run = *runp;
-  run.persistent = cfg.persistent;
+  run.persistent = cfg.persistent && comm_ == nullptr;
+  run.comm = comm_;
   run.rows_hint = rows_hint_;
   run.n_cus = n_cus_;
   run.abort_host = abort_host_;
@@ -815,6 +854,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
         kern::pair_gram_mfma_i8((const uint64_t*)bm_dev, Wp, F, gram, s);
       else
         kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);
+      if (comm_) comm_->all_reduce(gram, gram, (size_t)F * F, CommDtype::U32, false, s);
       run.gram = gram;
     }
     KMLS_HIP(hipEventRecord(e1.e, s));
@@ -825,15 +865,16 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     root.gid = d_gid;
     root.row_end = d_end;
     bool done = false;
-    if (!cfg.persistent && fused_levels_enabled()) {
+    if (!run.persistent && comm_ == nullptr && fused_levels_enabled()) {
       std::vector<int64_t> off((size_t)F + 1, 0);
       for (int64_t a = 0; a < F; ++a) off[a + 1] = off[a] + root_len[a];
       run.pinned = pinned_;
-      run.fast_hint = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 4ll << 20);
+      run.fast_hint = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 16ll << 20);
       done = run.run_fast(root, off, root_total);
     }
     if (!done) run.process(root, 1, d_len, root_total);
-    res.levels_path = done ? "fused" : (cfg.persistent ? "persistent" : "chunked");
+    res.levels_path = done ? "fused" : (run.persistent ? "persistent" : (comm_ ? "chunked-txdp" : "chunked"));
+    if (!done && !run.fallback_reason.empty()) res.levels_path += " (fused fallback: " + run.fallback_reason + ")";
     KMLS_HIP(hipStreamSynchronize(s));  // host staging vectors die at scope end
   } else {
     KMLS_HIP(hipEventRecord(e1.e, s));
@@ -891,9 +932,161 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   return res;
 }
 
+
+// Single-GPU mining with a device-resident prologue: supports, frequent-item selection, bitmap
+// encode, level-2 gram and the root descriptor are all produced on the device, so together with
+// the fused level loop one mining call has no host round trip before the final one.  Returns
+// false (nothing committed) when the fused loop overflowed; mine() then runs the host path.
+bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res) {
+  hipStream_t s = (hipStream_t)stream_;
+  auto t0 = std::chrono::steady_clock::now();
+  const int64_t I = n_items_;
+  const int64_t Wp = words_local();
+  constexpr int kMaxLv = 64;
+  Event e0, e1, e2;
+  KMLS_HIP(hipEventRecord(e0.e, s));
+  const size_t mark = arena_->mark();
+  uint32_t* d_cnt = (uint32_t*)arena_->push((size_t)I * 4);
+  int32_t* d_rank_of = (int32_t*)arena_->push((size_t)I * 4);
+  int32_t* d_ids = (int32_t*)arena_->push((size_t)I * 4);
+  uint32_t* d_fcnt = (uint32_t*)arena_->push((size_t)I * 4);
+  uint32_t* d_gram = (uint32_t*)arena_->push((size_t)I * I * 4);
+  int32_t* d_rrank = (int32_t*)arena_->push((size_t)I * 4);
+  int64_t* d_rgid = (int64_t*)arena_->push((size_t)I * 8);
+  int64_t* d_roff = (int64_t*)arena_->push((size_t)(I + 1) * 8);
+  kern::FLevel* d_desc = (kern::FLevel*)arena_->push(kMaxLv * sizeof(kern::FLevel));
+  kern::FCtl* d_ctl = (kern::FCtl*)arena_->push(sizeof(kern::FCtl));
+  const size_t need = (size_t)std::max<int64_t>(I, 1) * Wp * sizeof(uint64_t);
+  if (need > own_bm_bytes_) {
+    if (d_own_bm_) KMLS_HIP(hipFree(d_own_bm_));
+    KMLS_HIP(hipMalloc((void**)&d_own_bm_, need));
+    own_bm_bytes_ = need;
+  }
+  if (!out_) out_ = std::make_unique<OutBufs>();
+  MineRun run(out_.get());
+  run.s = s;
+  run.arena = arena_.get();
+  run.Wp = Wp;
+  run.minsup = level2_threshold((uint64_t)n_tx_, cfg.min_support);
+  run.max_len = cfg.max_len;
+  run.d_ids = d_ids;
+  run.F = I;  // gram row stride
+  run.gram = d_gram;
+  run.pinned = pinned_;
+  run.n_cus = n_cus_;
+  run.persistent = false;
+  KMLS_HIP(hipHostMalloc((void**)&run.h_scalar, 64));
+  struct ScalarGuard { int64_t*& p; ~ScalarGuard() { if (p) (void)hipHostFree(p); p = nullptr; } } sgd{run.h_scalar};
+  const int64_t cap_nodes = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 16ll << 20);
+  run.ensure_out(cap_nodes);
+  const int64_t out_cap = std::min<int64_t>({run.out_parent.cap, run.out_item.cap, run.out_count.cap, run.out_depth.cap});
+  if (download) {
+    run.host_cap = std::max<int64_t>({I * 8, (int64_t)1 << 16, last_nodes_ + (last_nodes_ >> 3)});
+    res.h_parent = pinned_->get((size_t)run.host_cap * sizeof(int64_t));
+    res.h_item = pinned_->get((size_t)run.host_cap * sizeof(int32_t));
+    res.h_count = pinned_->get((size_t)run.host_cap * sizeof(uint32_t));
+    res.h_depth = pinned_->get((size_t)run.host_cap * sizeof(uint8_t));
+    run.h_parent = (int64_t*)res.h_parent.get();
+    run.h_item = (int32_t*)res.h_item.get();
+    run.h_count = (uint32_t*)res.h_count.get();
+    run.h_depth = (uint8_t*)res.h_depth.get();
+    run.stream_dl = true;
+  }
+  const size_t rem = arena_->capacity() - arena_->used();
+  if (rem < (512ull << 20)) {
+    arena_->pop_to(mark);
+    res = GpuMineResult();
+    return false;
+  }
+  const size_t bump_bytes = rem - (64ull << 20);
+  char* bump_base = (char*)arena_->push(bump_bytes);
+  std::shared_ptr<void> stage = pinned_->get(kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
+  std::memset(stage.get(), 0, kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
+  kern::FCtl* h_ctl = (kern::FCtl*)((kern::FLevel*)stage.get() + kMaxLv);
+  h_ctl->bump_base = bump_base;
+  h_ctl->bump_cap = bump_bytes;
+  h_ctl->status_cap = (unsigned long long)out_->status_cap;
+  KMLS_HIP(hipMemcpyAsync(d_desc, stage.get(), kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl),
+                          hipMemcpyHostToDevice, s));
+  // prologue, all on the device
+  KMLS_HIP(hipMemsetAsync(d_cnt, 0, (size_t)I * 4, s));
+  kern::item_support(d_items_, nnz_, (int32_t)I, d_cnt, s);
+  kern::level_select(d_cnt, I, level1_threshold((uint64_t)n_tx_, cfg.min_support), d_ids, d_fcnt,
+                     d_rank_of, d_desc, s);
+  KMLS_HIP(hipMemsetAsync(d_own_bm_, 0, need, s));
+  kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of, d_own_bm_, Wp, 0, s);
+  KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));
+  kern::pair_gram_popcount_dev(d_own_bm_, Wp, &d_desc[1].n_rows, I, d_gram, s);
+  kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
+                         run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap};
+  kern::level_root_setup(d_desc, d_ctl, ra, s);
+  // frequent-item tables for the frequent() API: staged to pinned memory while levels run
+  std::shared_ptr<void> fstage = pinned_->get((size_t)I * 12);
+  KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)I * 4, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipMemcpyAsync((char*)fstage.get() + I * 4, d_fcnt, (size_t)I * 4, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipMemcpyAsync((char*)fstage.get() + I * 8, d_rank_of, (size_t)I * 4, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipEventRecord(e1.e, s));
+  const bool ok = run.levels_loop(d_desc, d_ctl, out_cap, true);
+  if (!ok) {
+    fused_fallback_ = run.fallback_reason;
+    arena_->pop_to(mark);
+    res = GpuMineResult();
+    return false;
+  }
+  const int64_t F = run.last_desc[1].n_rows;
+  // frequent items to the host (frequent() API); small
+  {
+    const int32_t* hs = (const int32_t*)fstage.get();
+    fi_.ids.assign(hs, hs + F);
+    fi_.counts.assign((const uint32_t*)(hs + I), (const uint32_t*)(hs + I) + F);
+    fi_.rank_of.assign(hs + 2 * I, hs + 3 * I);
+  }
+  fi_.minsup2 = run.minsup;
+  global_n_tx_ = n_tx_;
+  KMLS_HIP(hipEventRecord(e2.e, s));
+  const int64_t N = run.out_size;
+  res.n_nodes = N;
+  last_nodes_ = N;
+  if (download && !run.stream_dl) {
+    KMLS_HIP(hipStreamSynchronize(out_->copy_s));
+    res.h_parent = pinned_->get((size_t)N * sizeof(int64_t));
+    res.h_item = pinned_->get((size_t)N * sizeof(int32_t));
+    res.h_count = pinned_->get((size_t)N * sizeof(uint32_t));
+    res.h_depth = pinned_->get((size_t)N * sizeof(uint8_t));
+    if (N) {
+      KMLS_HIP(hipMemcpyAsync(res.h_parent.get(), run.out_parent.p, N * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.h_item.get(), run.out_item.p, N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.h_count.get(), run.out_count.p, N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(res.h_depth.get(), run.out_depth.p, N * sizeof(uint8_t), hipMemcpyDeviceToHost, s));
+    }
+  } else if (!download) {
+    res.h_parent.reset();
+  }
+  KMLS_HIP(hipStreamSynchronize(s));
+  KMLS_HIP(hipStreamSynchronize(out_->copy_s));
+  res.phases.push_back({"prologue(support+select+encode+gram)", elapsed(e0, e1)});
+  res.phases.push_back({"levels", elapsed(e1, e2)});
+  res.stats.n_frequent_items = F;
+  res.stats.n_itemsets = N;
+  res.stats.n_candidates = run.n_candidates;
+  res.stats.max_depth = F ? run.max_depth : 0;
+  res.stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  res.arena_high_water = (int64_t)arena_->high_water();
+  res.levels_path = "fused-resident";
+  arena_->pop_to(mark);
+  return true;
+}
+
 GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download) {
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
+  fused_fallback_.clear();
+  if (fused_levels_enabled() && !cfg.persistent && cfg.level2_gram && !cfg.level2_mfma &&
+      !cfg.pairs_only && cfg.max_len != 1 && n_items_ >= 2 && n_items_ <= kern::kSelectMaxItems &&
+      (size_t)n_items_ * words_local() * 8 <= (1ull << 30) && n_tx_ > 0) {
+    GpuMineResult r;
+    if (mine_resident(cfg, download, r)) return r;
+  }
   auto t0 = std::chrono::steady_clock::now();
   Event e0, e1, e2;
   KMLS_HIP(hipEventRecord(e0.e, s));
@@ -917,8 +1110,82 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download) {
   encode_bitmaps((uintptr_t)d_own_bm_, Wp, 0);
   KMLS_HIP(hipEventRecord(e2.e, s));
   GpuMineResult r = mine_bitmaps((uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
+  if (!fused_fallback_.empty() && r.levels_path.find("fallback") == std::string::npos)
+    r.levels_path += " (resident fallback: " + fused_fallback_ + ")";
   std::vector<Phase> ph;
   ph.push_back({"support+select", elapsed(e0, e1)});
+  ph.push_back({"encode_bitmap", elapsed(e1, e2)});
+  for (auto& p : r.phases) ph.push_back(p);
+  r.phases = ph;
+  r.stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return r;
+}
+
+
+GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineConfig& cfg,
+                                  bool download, int support_tiles) {
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  auto t0 = std::chrono::steady_clock::now();
+  Event e0, e1, e2;
+  KMLS_HIP(hipEventRecord(e0.e, s));
+  const size_t mark = arena_->mark();
+  // 1. supports in K tiles; tile k's all-reduce (comm stream) overlaps tile k+1's histogram
+  const int K = std::max(1, std::min(64, support_tiles));
+  const size_t vec = (size_t)std::max<int64_t>(n_items_, 1) * sizeof(uint32_t);
+  uint32_t* d_part = (uint32_t*)arena_->push(vec * K);
+  KMLS_HIP(hipMemsetAsync(d_part, 0, vec * K, s));
+  hipStream_t cs = nullptr;
+  KMLS_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  std::vector<hipEvent_t> evs((size_t)K);
+  for (auto& e : evs) KMLS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (int k = 0; k < K; ++k) {
+    const int64_t a = tile_nnz_[(size_t)(64 * k / K)], b = tile_nnz_[(size_t)(64 * (k + 1) / K)];
+    uint32_t* part = d_part + (size_t)k * (size_t)std::max<int64_t>(n_items_, 1);
+    kern::item_support(d_items_ + a, b - a, (int32_t)n_items_, part, s);
+    KMLS_HIP(hipEventRecord(evs[(size_t)k], s));
+    KMLS_HIP(hipStreamWaitEvent(cs, evs[(size_t)k], 0));
+    if (comm) comm->all_reduce(part, part, (size_t)n_items_, CommDtype::U32, false, cs);
+  }
+  hipEvent_t done;
+  KMLS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+  KMLS_HIP(hipEventRecord(done, cs));
+  KMLS_HIP(hipStreamWaitEvent(s, done, 0));
+  for (int k = 1; k < K; ++k)
+    kern::add_u32(d_part, d_part + (size_t)k * (size_t)std::max<int64_t>(n_items_, 1), n_items_, s);
+  std::vector<uint32_t> cnt((size_t)n_items_);
+  KMLS_HIP(hipMemcpyAsync(cnt.data(), d_part, cnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  for (auto& e : evs) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(done);
+  (void)hipStreamDestroy(cs);
+  arena_->pop_to(mark);
+  // 2. selection from global supports (identical on every rank)
+  const int64_t F = select(cnt.data(), global_n_tx, cfg.min_support);
+  KMLS_HIP(hipEventRecord(e1.e, s));
+  // 3. shard-local bitmaps
+  const int64_t Wp = words_local();
+  const size_t need = (size_t)std::max<int64_t>(F, 1) * Wp * sizeof(uint64_t);
+  if (need > own_bm_bytes_) {
+    if (d_own_bm_) KMLS_HIP(hipFree(d_own_bm_));
+    KMLS_HIP(hipMalloc((void**)&d_own_bm_, need));
+    own_bm_bytes_ = need;
+  }
+  KMLS_HIP(hipMemsetAsync(d_own_bm_, 0, need, s));
+  encode_bitmaps((uintptr_t)d_own_bm_, Wp, 0);
+  KMLS_HIP(hipEventRecord(e2.e, s));
+  // 4. level loop with all-reduced candidate counts
+  comm_ = comm;
+  GpuMineResult r;
+  try {
+    r = mine_bitmaps((uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
+  } catch (...) {
+    comm_ = nullptr;
+    throw;
+  }
+  comm_ = nullptr;
+  std::vector<Phase> ph;
+  ph.push_back({"support_tiles+allreduce+select", elapsed(e0, e1)});
   ph.push_back({"encode_bitmap", elapsed(e1, e2)});
   for (auto& p : r.phases) ph.push_back(p);
   r.phases = ph;

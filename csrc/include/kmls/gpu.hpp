@@ -71,6 +71,28 @@ struct GpuMineResult {
   std::string levels_path = "none";  // "fused" | "chunked" | "persistent" | "none"
 };
 
+// Native RCCL communicator (comm_rccl.cpp) over the librccl torch already loaded.
+enum class CommDtype { U32, I64, U64, F64 };
+size_t comm_dtype_bytes(CommDtype t);
+std::string comm_unique_id();  // 128 opaque bytes, broadcast by the caller (torch.distributed)
+class Comm {
+ public:
+  Comm(int rank, int world, const std::string& uid, int device);
+  ~Comm();
+  Comm(const Comm&) = delete;
+  Comm& operator=(const Comm&) = delete;
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  // stream-ordered collectives on `stream` (a hipStream_t); in place when send == recv
+  void all_reduce(const void* send, void* recv, size_t count, CommDtype t, bool max_op,
+                  void* stream);
+  void all_gather(const void* send, void* recv, size_t count, CommDtype t, void* stream);
+  void abort();
+ private:
+  int rank_ = 0, world_ = 1;
+  void* comm_ = nullptr;
+};
+
 struct OutBufs;  // persistent device trie buffers + download stream (miner_gpu.hip)
 
 // Resident-data GPU miner.  Typical use: load() once (CSR → HBM), mine() many times.
@@ -102,6 +124,13 @@ class GpuMiner {
                              const uint8_t* owned_mask, bool emit_level1, bool download);
   // Convenience single-GPU path: A + B + C + D.
   GpuMineResult mine(const MineConfig& cfg, bool download);
+  // Transaction-data-parallel mining (large T): this rank holds a transaction shard; supports
+  // are counted in `support_tiles` tiles whose all-reduces overlap the next tile's histogram
+  // (comm stream); bitmaps stay shard-local ([F][Ws] words), and every level's candidate
+  // counts are all-reduced in the loop, so all ranks build the identical global trie without
+  // ever replicating bitmaps.  comm == nullptr behaves as world size 1.
+  GpuMineResult mine_txdp(Comm* comm, int64_t global_n_tx, const MineConfig& cfg, bool download,
+                          int support_tiles);
 
   // Frequent items of the last select(): ids (ascending support) and counts.
   const FrequentItems& frequent() const { return fi_; }
@@ -133,9 +162,21 @@ class GpuMiner {
   unsigned int* abort_host_ = nullptr;       // watchdog flag (pinned, device-mapped)
   const unsigned int* abort_dev_ = nullptr;
   int n_cus_ = 256;
+  bool mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res);
+  std::string fused_fallback_;
   std::unique_ptr<OutBufs> out_;  // output trie kept allocated across mine() calls
+  Comm* comm_ = nullptr;          // set during mine_txdp: level counts are all-reduced
+  std::vector<int64_t> tile_tx_;  // 65 evenly spaced transaction boundaries of the shard
+  std::vector<int64_t> tile_nnz_; // and their item offsets
   int64_t last_nodes_ = 0;        // size of the previous trie (pinned download sizing)
 };
+
+// Association rules on the GPU (rules_gpu.hip / kernels/rules.hip): same output and order as
+// association_rules_cpu.  kernel_ms (optional) = hash build + both rule passes.
+RuleSet association_rules_gpu(int device, const int64_t* parent, const int32_t* item,
+                              const uint32_t* count, const uint8_t* depth, int64_t n, int64_t n_tx,
+                              RuleMetric metric, double min_threshold, int max_antecedent,
+                              double* kernel_ms);
 
 // HBM-resident rule index + batched matcher kernel (serve_match_topk).
 class GpuRuleIndex {

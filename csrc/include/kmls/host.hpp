@@ -100,4 +100,10 @@ class RuleIndex {
   std::vector<uint8_t> is_key_;
 };
 
+// Multi-threaded synthetic transactions (csrc/host/synth.cpp): CSR with sorted, unique items.
+void synth_transactions(int64_t n_tx, int64_t n_items, double mean_len, int n_genres,
+                        double affinity, double zipf_s, uint64_t seed, int threads,
+                        std::vector<int64_t>& tx_ptr, std::vector<int32_t>& items,
+                        int64_t tx_begin = 0, int64_t tx_end = -1);
+
 }  // namespace kmls

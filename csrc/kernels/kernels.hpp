@@ -14,6 +14,8 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
 void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                    const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
                    hipStream_t s);
+// dst[i] += src[i]
+void add_u32(uint32_t* dst, const uint32_t* src, int64_t n, hipStream_t s);
 // exclusive prefix sum over int64[n+1] (in[n] == 0) into out[n+1] (out[n] = total)
 size_t scan_temp_bytes(int64_t n);
 void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* temp, size_t temp_bytes,
@@ -50,6 +52,9 @@ void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off,
 // dense upper-triangular pair counts over a single class of F rows (level 2 bit-GEMM)
 void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
 void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
+// same with F read from the device (grid and row stride sized for F_max)
+void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, int64_t F_max,
+                            uint32_t* out, hipStream_t s);
 // dense Gram (F x F, i<j valid) → per-candidate counts in (a, b) row-major candidate order
 void gram_to_cand(const uint32_t* gram, int64_t F, const int64_t* cand_off, int64_t c0, int64_t c1,
                   uint32_t* cnt, hipStream_t s);
@@ -99,6 +104,28 @@ struct CopyOutArgs {
   uint8_t* h_depth;
   int64_t host_cap;
 };
+// device-resident prologue (single GPU, small vocabularies): selection + root descriptor
+// without a host round trip.  select: items with cnt >= c1, ranked by (count asc, id asc)
+// (= select_frequent), F → desc[1].n_rows.  root_setup: level-1 trie nodes, root cand_off
+// (closed form), iota rank/gid, root children buffers from the bump region.
+constexpr int64_t kSelectMaxItems = 16384;
+void level_select(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* ids,
+                  uint32_t* fcounts, int32_t* rank_of, FLevel* desc, hipStream_t s);
+struct RootSetupArgs {
+  const uint64_t* bm;
+  int32_t* rank;       // [n_items]
+  int64_t* gid;        // [n_items]
+  int64_t* cand_off;   // [n_items + 1]
+  const int32_t* ids;
+  const uint32_t* fcounts;
+  int64_t* out_parent;
+  int32_t* out_item;
+  uint32_t* out_count;
+  uint8_t* out_depth;
+  int64_t Wp;
+  int64_t out_cap;
+};
+void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s);
 int level_grid(int n_cus);
 int64_t level_tile();
 int64_t level_scan_tile();
@@ -166,6 +193,42 @@ size_t dfs_compact_temp_bytes(int64_t rows);
 int64_t dfs_compact(int64_t rows, int64_t out_base, int64_t* par, int32_t* item, uint32_t* cnt,
                     uint8_t* dep, void* temp, size_t temp_bytes, int64_t* par2, int32_t* item2,
                     uint32_t* cnt2, uint8_t* dep2, unsigned long long* h_holes, hipStream_t s);
+
+// ---- association rules (rules.hip) ----
+struct RuleArgs {
+  const int64_t* parent;
+  const int32_t* item;
+  const uint32_t* count;
+  const uint8_t* depth;
+  int64_t n;
+  double T;
+  int metric;              // RuleMetric
+  double thr;
+  int max_ante;
+  const unsigned long long* keys;  // (parent+1, item) → node hash
+  const int32_t* vals;
+  unsigned long long mask;
+  int32_t* scratch;        // per-wave global subset tables (k in (12, scratch_bits]) or null
+  int scratch_bits;
+  unsigned long long* ticket;
+  unsigned int* error;     // 1 = subset missing from the trie, 2 = itemset longer than 30
+  int pass;                // 0 = count, 1 = write
+  int64_t* nrules;         // pass 0: [n+1]
+  const int64_t* off;      // pass 1: exclusive scan of nrules
+  int64_t* o_itemset;
+  int64_t* o_ante;
+  int64_t* o_cons;
+  double* o_conf;
+  double* o_lift;
+};
+void rules_hash_build(const int64_t* parent, const int32_t* item, int64_t n,
+                      unsigned long long* keys, int32_t* vals, unsigned long long mask,
+                      hipStream_t s);
+int rules_grid(int n_cus);
+int rules_waves_per_block();
+void rules_pass(const RuleArgs& a, int grid, hipStream_t s);
+size_t rules_scan_temp_bytes(int64_t n);
+void rules_scan(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tb, hipStream_t s);
 
 // ---- serving (serve.hip) ----
 void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,

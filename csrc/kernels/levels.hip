@@ -63,34 +63,48 @@ __device__ __forceinline__ unsigned long long pack(unsigned epoch, unsigned flag
          (v & kValMask);
 }
 
-// Single-thread decoupled look-back for tile t; returns the exclusive prefix of the tile.
+// Wave-parallel decoupled look-back for tile t (called by all 64 lanes of wave 0): each round
+// inspects 64 predecessors at once (lane 0 = nearest), sums their aggregates up to the nearest
+// inclusive prefix, and only spins while one of those is unpublished.  A one-thread walk costs
+// one memory latency per predecessor — O(tiles) per tile, which made the first version of this
+// kernel latency-bound.  Returns the tile's exclusive prefix (same value in every lane).
 __device__ int64_t lookback(unsigned long long* st, int64_t t, unsigned epoch, int64_t agg,
                             FCtl* ctl) {
   const unsigned e = epoch & 0xFFFFFFu;
+  const int lane = threadIdx.x & 63;
   if (t == 0) {
-    st_relaxed(&st[0], pack(e, 2, (unsigned long long)agg));
+    if (lane == 0) st_relaxed(&st[0], pack(e, 2, (unsigned long long)agg));
     return 0;
   }
-  st_relaxed(&st[t], pack(e, 1, (unsigned long long)agg));
+  if (lane == 0) st_relaxed(&st[t], pack(e, 1, (unsigned long long)agg));
   int64_t excl = 0;
-  int64_t j = t - 1;
+  int64_t end = t;  // window = predecessors [end-64, end)
   long long spins = 0;
-  while (j >= 0) {
-    const unsigned long long w = ld_relaxed(&st[j]);
+  while (true) {
+    const int64_t j = end - 1 - lane;
+    unsigned long long w = j >= 0 ? ld_relaxed(&st[j]) : pack(e, 2, 0);  // virtual P(0) before tile 0
     const unsigned we = (unsigned)(w >> 40), wf = (unsigned)(w >> 38) & 3u;
-    if (we != e || wf == 0) {
+    const bool valid = we == e && wf != 0;
+    const unsigned long long pmask = __ballot(valid && wf == 2);
+    const unsigned long long imask = __ballot(!valid);
+    const int first_p = pmask ? __builtin_ctzll(pmask) : 64;
+    const unsigned long long need = first_p >= 63 ? ~0ull : ((1ull << (first_p + 1)) - 1ull);
+    if (imask & need) {
       if (++spins > kSpinLimit) {  // never expected: predecessors always make progress
-        atomicExch(&ctl->overflow, 2u);
+        if (lane == 0) atomicExch(&ctl->overflow, 2u);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    excl += (int64_t)(w & kValMask);
-    if (wf == 2) break;
-    --j;
+    int64_t v = lane <= first_p ? (int64_t)(w & kValMask) : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    excl += v;
+    if (first_p < 64) break;
+    end -= 64;
   }
-  st_relaxed(&st[t], pack(e, 2, (unsigned long long)(excl + agg)));
+  if (lane == 0) st_relaxed(&st[t], pack(e, 2, (unsigned long long)(excl + agg)));
   return excl;
 }
 
@@ -162,6 +176,9 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
     }
     return;
   }
+  // Idle blocks leave before touching the ticket: same-address device atomics serialise, and
+  // 2048 of them per launch cost more than a small level's whole scan.
+  if ((int64_t)blockIdx.x >= n_tiles) return;
   const int32_t* __restrict__ prow = lv->prow;
   const int64_t* __restrict__ pco = pv->cand_off;
   const int64_t* __restrict__ ppos = pv->pos;
@@ -187,7 +204,10 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
     }
     int64_t tile_total;
     const int64_t excl = block_excl_scan(sum, s_w, &tile_total);
-    if (threadIdx.x == 0) s_base = lookback(status, t, epoch, tile_total, ctl);
+    if (threadIdx.x < 64) {
+      const int64_t b = lookback(status, t, epoch, tile_total, ctl);
+      if (threadIdx.x == 0) s_base = b;
+    }
     __syncthreads();
     int64_t run = s_base + excl;
 #pragma unroll
@@ -221,11 +241,13 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
                                                         FLevel* __restrict__ nx, FCtl* ctl,
                                                         unsigned long long* __restrict__ status,
                                                         unsigned epoch, LevelCountArgs A) {
-  __shared__ int64_t s_off[kWin + 1];
+  __shared__ int64_t s_off[kWin];
   __shared__ uint32_t s_cnt[kTile];
   __shared__ int32_t s_lpos[kTile];
+  __shared__ int64_t s_a[kTile];   // candidate → parent row a
+  __shared__ int64_t s_b[kTile];   // candidate → sibling row b
   __shared__ int64_t s_w[kBlock / 64];
-  __shared__ int64_t s_rr[2];
+  __shared__ int64_t s_r0;
   __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
   if (ctl->overflow) return;
@@ -242,6 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
     }
     return;
   }
+  if ((int64_t)blockIdx.x >= n_tiles) return;  // idle blocks: no ticket atomic (see scan)
   const int64_t* __restrict__ co = lv->cand_off;
   const unsigned long long* __restrict__ bm = (const unsigned long long*)lv->bm;
   const int32_t* __restrict__ rank = lv->rank;
@@ -264,23 +287,35 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
     if (t >= n_tiles) return;
     const int64_t c0 = t * kTile;
     const int cn = (int)min((int64_t)kTile, n_cand - c0);
-    if (threadIdx.x < 2)
-      s_rr[threadIdx.x] = find_row_g(co, 0, n_rows, c0 + (threadIdx.x ? cn - 1 : 0));
+    if (threadIdx.x < 64) {  // row of the tile's first candidate: 64-ary search by wave 0
+      const int64_t c = c0;
+      int64_t lo = 0, hi = n_rows;  // invariant: co[lo] <= c < co[hi]
+      while (hi - lo > 64) {
+        const int64_t step = (hi - lo + 63) / 64;
+        const int64_t p = lo + (int64_t)threadIdx.x * step;
+        const unsigned long long bal = __ballot(p < hi && co[p] <= c);
+        const int last = 63 - __builtin_clzll(bal);  // lane 0 always true (p = lo)
+        const int64_t nlo = lo + (int64_t)last * step;
+        hi = min(hi, nlo + step);
+        lo = nlo;
+      }
+      const int64_t p = lo + threadIdx.x;
+      const unsigned long long bal = __ballot(p < hi && co[p] <= c);
+      if (threadIdx.x == 0) s_r0 = lo + (63 - __builtin_clzll(bal));
+    }
     __syncthreads();
-    const int64_t r0 = s_rr[0], r1 = s_rr[1];
-    const int64_t nr = r1 - r0 + 1;
-    const bool win = nr + 1 <= kWin;
-    if (win)
-      for (int64_t i = threadIdx.x; i <= nr; i += kBlock) s_off[i] = co[r0 + i];
+    // window co[r0 .. r0 + nw) in LDS; a candidate past the window searches HBM (rare: only
+    // when the tile spans more than kWin rows, i.e. many empty class tails)
+    const int64_t r0 = s_r0;
+    const int64_t nw = min((int64_t)kWin, n_rows + 1 - r0);
+    for (int64_t i = threadIdx.x; i < nw; i += kBlock) s_off[i] = co[r0 + i];
     __syncthreads();
-    // ---- phase 1: supports ----
-    for (int j = 0; j < kPer; ++j) {
-      const int i = team * kPer + j;
-      if (i >= cn) break;  // team-uniform
-      const int64_t c = c0 + i;
+    // one decode per candidate, shared by the count and materialise phases
+    if ((int)threadIdx.x < cn) {
+      const int64_t c = c0 + threadIdx.x;
       int64_t a, oa;
-      if (win) {
-        int64_t lo = 0, hi = nr;  // largest k in [0, nr) with s_off[k] <= c
+      if (nw >= 2 && s_off[nw - 1] > c) {  // row in window: largest k < nw-1 with s_off[k] <= c
+        int64_t lo = 0, hi = nw - 1;
         while (hi - lo > 1) {
           const int64_t mid = (lo + hi) >> 1;
           if (s_off[mid] <= c) lo = mid; else hi = mid;
@@ -288,26 +323,44 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
         a = r0 + lo;
         oa = s_off[lo];
       } else {
-        a = find_row_g(co, r0, r1 + 1, c);
+        a = find_row_g(co, r0, n_rows, c);
         oa = co[a];
       }
-      const int64_t b = a + 1 + (c - oa);
-      uint32_t k;
+      s_a[threadIdx.x] = a;
+      s_b[threadIdx.x] = a + 1 + (c - oa);
+    }
+    __syncthreads();
+    // ---- phase 1: supports (team per candidate, 2 candidates in flight) ----
+    for (int j = 0; j < kPer; j += 2) {
+      const int i0 = team * kPer + j, i1 = i0 + 1;
+      if (i0 >= cn) break;  // team-uniform
+      const bool two = i1 < cn;
       if (A.gram) {
-        k = A.gram[a * A.F + b];
-      } else {
-        const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
-        const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
-        uint32_t sacc = 0;
-        for (int64_t w = tl; w < n2; w += TS) {
-          const ulonglong2 u = x[w], v = y[w];
-          sacc += (uint32_t)__popcll(u.x & v.x) + (uint32_t)__popcll(u.y & v.y);
+        if (tl == 0) {
+          s_cnt[i0] = A.gram[s_a[i0] * A.F + s_b[i0]];
+          if (two) s_cnt[i1] = A.gram[s_a[i1] * A.F + s_b[i1]];
         }
-#pragma unroll
-        for (int off = TS >> 1; off > 0; off >>= 1) sacc += __shfl_xor(sacc, off, TS);
-        k = sacc;
+        continue;
       }
-      if (tl == 0) s_cnt[i] = k;
+      const ulonglong2* x0 = reinterpret_cast<const ulonglong2*>(bm + s_a[i0] * Wp);
+      const ulonglong2* y0 = reinterpret_cast<const ulonglong2*>(bm + s_b[i0] * Wp);
+      const ulonglong2* x1 = reinterpret_cast<const ulonglong2*>(bm + s_a[two ? i1 : i0] * Wp);
+      const ulonglong2* y1 = reinterpret_cast<const ulonglong2*>(bm + s_b[two ? i1 : i0] * Wp);
+      uint32_t k0 = 0, k1 = 0;
+      for (int64_t w = tl; w < n2; w += TS) {
+        const ulonglong2 u0 = x0[w], v0 = y0[w], u1 = x1[w], v1 = y1[w];
+        k0 += (uint32_t)__popcll(u0.x & v0.x) + (uint32_t)__popcll(u0.y & v0.y);
+        k1 += (uint32_t)__popcll(u1.x & v1.x) + (uint32_t)__popcll(u1.y & v1.y);
+      }
+#pragma unroll
+      for (int off = TS >> 1; off > 0; off >>= 1) {
+        k0 += __shfl_xor(k0, off, TS);
+        k1 += __shfl_xor(k1, off, TS);
+      }
+      if (tl == 0) {
+        s_cnt[i0] = k0;
+        if (two) s_cnt[i1] = k1;
+      }
     }
     __syncthreads();
     // ---- phase 2: survivor positions (block scan + look-back) ----
@@ -315,40 +368,17 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
     int64_t tile_total;
     const int64_t lx = block_excl_scan(flag, s_w, &tile_total);
     s_lpos[threadIdx.x] = (int32_t)lx;
-    if (threadIdx.x == 0) s_base = lookback(status, t, epoch, tile_total, ctl);
+    if (threadIdx.x < 64) {
+      const int64_t b = lookback(status, t, epoch, tile_total, ctl);
+      if (threadIdx.x == 0) s_base = b;
+    }
     __syncthreads();
     const int64_t base = s_base;
-    if ((int)threadIdx.x < cn) pos[c0 + threadIdx.x] = base + lx;
-    // ---- phase 3: materialise survivors ----
-    for (int j = 0; j < kPer; ++j) {
-      const int i = team * kPer + j;
-      if (i >= cn) break;
-      const uint32_t k = s_cnt[i];
-      if (k < A.minsup) continue;  // team-uniform
-      const int64_t c = c0 + i;
-      int64_t a, oa;
-      if (win) {
-        int64_t lo = 0, hi = nr;
-        while (hi - lo > 1) {
-          const int64_t mid = (lo + hi) >> 1;
-          if (s_off[mid] <= c) lo = mid; else hi = mid;
-        }
-        a = r0 + lo;
-        oa = s_off[lo];
-      } else {
-        a = find_row_g(co, r0, r1 + 1, c);
-        oa = co[a];
-      }
-      const int64_t b = a + 1 + (c - oa);
-      const int64_t s = base + s_lpos[i];
-      const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
-      const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
-      ulonglong2* z = reinterpret_cast<ulonglong2*>(cbm + s * Wp);
-      for (int64_t w = tl; w < n2; w += TS) {
-        const ulonglong2 u = x[w], v = y[w];
-        z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
-      }
-      if (tl == 0) {
+    if ((int)threadIdx.x < cn) {
+      pos[c0 + threadIdx.x] = base + lx;
+      if (flag) {  // per-survivor scalars: one thread each
+        const int64_t a = s_a[threadIdx.x], b = s_b[threadIdx.x];
+        const int64_t s = base + lx;
         const int32_t rb = rank[b];
         const int64_t node = child_base + s;
         crank[s] = rb;
@@ -356,8 +386,22 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
         cprow[s] = (int32_t)a;
         A.out_parent[node] = gid[a];
         A.out_item[node] = A.ids[rb];
-        A.out_count[node] = k;
+        A.out_count[node] = s_cnt[threadIdx.x];
         A.out_depth[node] = A.child_depth;
+      }
+    }
+    // ---- phase 3: survivors' bitmaps (team per survivor) ----
+    for (int j = 0; j < kPer; ++j) {
+      const int i = team * kPer + j;
+      if (i >= cn) break;
+      if (s_cnt[i] < A.minsup) continue;  // team-uniform
+      const int64_t s = base + s_lpos[i];
+      const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + s_a[i] * Wp);
+      const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + s_b[i] * Wp);
+      ulonglong2* z = reinterpret_cast<ulonglong2*>(cbm + s * Wp);
+      for (int64_t w = tl; w < n2; w += TS) {
+        const ulonglong2 u = x[w], v = y[w];
+        z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
       }
     }
     if (t == n_tiles - 1 && threadIdx.x == 0) {
@@ -393,18 +437,96 @@ __global__ __launch_bounds__(kBlock) void k_level_copyout(const FLevel* __restri
   }
 }
 
-int team_size_for(int64_t Wp) {
+// ---------------------------------------------------------------------------------------------
+// device-resident prologue
+// one thread per item, every block holds all counts in LDS: rank = #frequent items ordered
+// before it by (count, id); F accumulates into desc[1].n_rows (zeroed by the host upload)
+__global__ __launch_bounds__(256) void k_level_select(const uint32_t* __restrict__ cnt,
+                                                      int64_t n_items, uint32_t c1,
+                                                      int32_t* __restrict__ ids,
+                                                      uint32_t* __restrict__ fcounts,
+                                                      int32_t* __restrict__ rank_of,
+                                                      FLevel* desc) {
+  __shared__ uint32_t s_cnt[kSelectMaxItems];
+  __shared__ unsigned int s_F;
+  if (threadIdx.x == 0) s_F = 0;
+  for (int64_t i = threadIdx.x; i < n_items; i += blockDim.x) s_cnt[i] = cnt[i];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_items) {
+    const uint32_t ci = s_cnt[i];
+    if (ci < c1) {
+      rank_of[i] = -1;
+    } else {
+      int32_t r = 0;
+      for (int64_t j = 0; j < n_items; ++j) {
+        const uint32_t cj = s_cnt[j];
+        r += (cj >= c1 && (cj < ci || (cj == ci && j < i))) ? 1 : 0;
+      }
+      rank_of[i] = r;
+      ids[r] = (int32_t)i;
+      fcounts[r] = ci;
+      atomicAdd(&s_F, 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_F) atomicAdd((unsigned long long*)&desc[1].n_rows, (unsigned long long)s_F);
+}
+
+__global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* ctl,
+                                                           RootSetupArgs a) {
+  __shared__ int ok;
+  const int64_t F = desc[1].n_rows;
+  const int64_t n_cand = F * (F - 1) / 2;
+  if (threadIdx.x == 0) {
+    FLevel& r = desc[1];
+    r.bm = a.bm;
+    r.rank = a.rank;
+    r.gid = a.gid;
+    r.cand_off = a.cand_off;
+    r.n_cand = n_cand;
+    r.child_base = F;
+    desc[0].child_base = 0;  // level-1 trie nodes [0, F) for the copy-out of "level 0"
+    ok = 1;
+    if (F + n_cand > a.out_cap || (n_cand + kTile - 1) / kTile > (int64_t)ctl->status_cap) {
+      atomicExch(&ctl->overflow, 4u);
+      ok = 0;
+    } else if (n_cand > 0) {
+      r.pos = (int64_t*)bump(ctl, (unsigned long long)(n_cand + 1) * 8ull);
+      desc[2].bm = (const uint64_t*)bump(ctl, (unsigned long long)n_cand * (unsigned long long)a.Wp * 8ull);
+      desc[2].rank = (const int32_t*)bump(ctl, (unsigned long long)n_cand * 4ull);
+      desc[2].gid = (const int64_t*)bump(ctl, (unsigned long long)n_cand * 8ull);
+      desc[2].prow = (const int32_t*)bump(ctl, (unsigned long long)n_cand * 4ull);
+      if (ctl->overflow) ok = 0;
+    }
+  }
+  __syncthreads();
+  if (!ok) return;
+  for (int64_t i = threadIdx.x; i <= F; i += blockDim.x) {
+    a.cand_off[i] = i * (2 * F - i - 1) / 2;  // Σ_{a < i} (F - a - 1)
+    if (i < F) {
+      a.rank[i] = (int32_t)i;
+      a.gid[i] = i;
+      a.out_parent[i] = -1;
+      a.out_item[i] = a.ids[i];
+      a.out_count[i] = a.fcounts[i];
+      a.out_depth[i] = 1;
+    }
+  }
+}
+
+int team_size_for(int64_t Wp) {  // lanes per candidate: ~4-8 16-byte chunks per lane
   const int64_t chunks = Wp >> 1;  // 16-byte chunks per row
-  if (chunks >= 128) return 64;
-  if (chunks >= 64) return 32;
-  if (chunks >= 32) return 16;
-  if (chunks >= 12) return 8;
+  if (chunks >= 256) return 64;
+  if (chunks >= 128) return 32;
+  if (chunks >= 64) return 16;
+  if (chunks >= 32) return 8;
   return 4;
 }
 
 }  // namespace
 
-int level_grid(int n_cus) { return std::max(64, n_cus * 4); }
+int level_grid(int n_cus) { return std::max(64, n_cus * 8); }  // 8 x 256-thread blocks per CU
 
 void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status,
                 unsigned epoch, int64_t Wp, int64_t out_cap, int grid, hipStream_t s) {
@@ -427,7 +549,20 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
 
 void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const CopyOutArgs& a,
                    hipStream_t s) {
-  hipLaunchKernelGGL(k_level_copyout, dim3(256), dim3(kBlock), 0, s, lv, nx, ctl, a);
+  hipLaunchKernelGGL(k_level_copyout, dim3(64), dim3(kBlock), 0, s, lv, nx, ctl, a);
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_select(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* ids,
+                  uint32_t* fcounts, int32_t* rank_of, FLevel* desc, hipStream_t s) {
+  if (n_items > kSelectMaxItems) throw std::runtime_error("level_select: vocabulary too large");
+  hipLaunchKernelGGL(k_level_select, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, s, cnt,
+                     n_items, c1, ids, fcounts, rank_of, desc);
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_level_root_setup, dim3(1), dim3(1024), 0, s, desc, ctl, a);
   KMLS_HIP(hipGetLastError());
 }
 

@@ -198,15 +198,18 @@ constexpr int kGT = 64;   // tile rows/cols
 constexpr int kGK = 16;   // words per K stage
 
 __global__ __launch_bounds__(kBlock) void k_pair_gram_popcount(
-    const unsigned long long* __restrict__ bm, int64_t Wp, int64_t F, int64_t n_tiles,
-    uint32_t* __restrict__ out) {
+    const unsigned long long* __restrict__ bm, int64_t Wp, int64_t F_host, int64_t n_tiles,
+    uint32_t* __restrict__ out, int64_t ld, const int64_t* __restrict__ dF) {
   __shared__ unsigned long long As[kGK][kGT + 2];
   __shared__ unsigned long long Bs[kGK][kGT + 2];
+  // F from the device when the selection ran there (grid sized for an upper bound)
+  const int64_t F = dF ? *dF : F_host;
   // upper-triangular tile decode: blockIdx.x → (ti <= tj)
   int64_t idx = blockIdx.x, ti = 0;
   while (idx >= n_tiles - ti) { idx -= n_tiles - ti; ++ti; }
   const int64_t tj = ti + idx;
   const int64_t r0 = ti * kGT, q0 = tj * kGT;
+  if (q0 >= F) return;  // block-uniform
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   uint32_t acc[4][4] = {};
   // staging map: thread → (row = tid>>2, words (tid&3)*4 .. +3)
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(kBlock) void k_pair_gram_popcount(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t q = q0 + tx * 4 + j;
-      if (q < F && q > r) out[r * F + q] = acc[i][j];
+      if (q < F && q > r) out[r * ld + q] = acc[i][j];
     }
   }
 }
@@ -289,6 +292,17 @@ void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
   if (n_tx <= 0) return;
   hipLaunchKernelGGL(k_encode_bitmap, dim3(grid_for(n_tx, kBlock / 64, 8192)), dim3(kBlock), 0, s,
                      tx_ptr, items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off);
+  KMLS_HIP(hipGetLastError());
+}
+
+__global__ void k_add_u32(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, int64_t n) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr) dst[i] += src[i];
+}
+
+void add_u32(uint32_t* dst, const uint32_t* src, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_add_u32, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, s, dst, src, n);
   KMLS_HIP(hipGetLastError());
 }
 
@@ -396,7 +410,17 @@ void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out
   const int64_t nt = (F + kGT - 1) / kGT;
   const int64_t blocks = nt * (nt + 1) / 2;
   hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks), dim3(kBlock), 0, s,
-                     (const unsigned long long*)bm, Wp, F, nt, out);
+                     (const unsigned long long*)bm, Wp, F, nt, out, F, (const int64_t*)nullptr);
+  KMLS_HIP(hipGetLastError());
+}
+
+void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, int64_t F_max,
+                            uint32_t* out, hipStream_t s) {
+  if (F_max < 2) return;
+  const int64_t nt = (F_max + kGT - 1) / kGT;
+  const int64_t blocks = nt * (nt + 1) / 2;
+  hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks), dim3(kBlock), 0, s,
+                     (const unsigned long long*)bm, Wp, F_max, nt, out, F_max, dF);
   KMLS_HIP(hipGetLastError());
 }
 

@@ -82,7 +82,10 @@ def mine_rules_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_su
                    max_len=2 if cfg.rules_mode == "pairs" else 0)
     r = dm.step(download=True)
     F = int(r["stats"].get("n_frequent_items", 0))
-    merged = gather_trie(r["trie"], rank, world, F)
+    if dm.mode == "tx":  # every rank holds the identical global trie; rank 0 downloaded it
+        merged = r["trie"] if rank == 0 else None
+    else:
+        merged = gather_trie(r["trie"], rank, world, F)
     if rank != 0:
         return None
     trie = ItemsetTrie(merged["parent"], merged["item"], merged["count"], merged["depth"],

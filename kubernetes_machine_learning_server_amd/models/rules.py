@@ -84,14 +84,25 @@ class Rules:
 
 
 def rules_from_trie(trie: ItemsetTrie, metric: str = "confidence", min_threshold: float = 0.8,
-                    max_antecedent: int = 0, strict: bool = False) -> Rules:
+                    max_antecedent: int = 0, strict: bool = False, backend: str = "auto",
+                    device: int = 0) -> Rules:
+    """``backend``: "gpu" (HIP rule_score kernels, csrc/kernels/rules.hip), "cpu" (threaded
+    C++), "auto" (GPU when one is visible and the trie is large enough to amortise the upload).
+    Both produce identical rules in identical order."""
     if metric not in _METRICS:
         raise ValueError(f"unknown metric {metric!r}; choose from {sorted(_METRICS)}")
     m = 5 if (strict and metric == "confidence") else _METRICS[metric]
-    raw = native.load().association_rules(
-        np.ascontiguousarray(trie.parent, np.int64), np.ascontiguousarray(trie.item, np.int32),
-        np.ascontiguousarray(trie.count, np.uint32), np.ascontiguousarray(trie.depth, np.uint8),
-        int(trie.n_tx), m, float(min_threshold), int(max_antecedent))
+    args = (np.ascontiguousarray(trie.parent, np.int64), np.ascontiguousarray(trie.item, np.int32),
+            np.ascontiguousarray(trie.count, np.uint32), np.ascontiguousarray(trie.depth, np.uint8),
+            int(trie.n_tx), m, float(min_threshold), int(max_antecedent))
+    if backend == "auto":
+        backend = "gpu" if (len(trie) >= 50_000 and native.gpu_available()) else "cpu"
+    if backend == "gpu":
+        raw = native.require_gpu().association_rules_gpu(*args, device)
+    elif backend == "cpu":
+        raw = native.load().association_rules(*args)
+    else:
+        raise ValueError(f"unknown backend {backend!r}")
     return Rules(trie, raw)
 
 

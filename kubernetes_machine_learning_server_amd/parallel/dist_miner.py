@@ -20,6 +20,15 @@ no parallelism).  Here the mining step is split across the N GPUs of a node:
    ``gather_trie`` concatenates sub-tries on rank 0 when the caller needs them (the job).
 
 With N == 1 every collective is skipped and the native single-GPU ``mine`` path runs.
+
+**Transaction-DP mode** (``mode="tx"``, the default for T >= 4M — BASELINE configs 3 and 5):
+replicating [F][T/64] bitmaps stops paying when T is large (100M transactions x 756 frequent
+items = 9.4 GB per GPU), so each rank keeps only its own shard's bitmap words and the C++
+level loop all-reduces every level's candidate counts through a native RCCL communicator
+(``csrc/host/comm_rccl.cpp``) on the miner's stream — no Python round trip per level.  The
+per-item supports are counted in tiles whose all-reduces run on a side stream while the next
+tile's histogram runs (the overlap the north star asks for).  Every rank ends with the same
+global trie; rank 0 downloads it.
 """
 from __future__ import annotations
 
@@ -86,7 +95,16 @@ class _GpuOps:
     def __init__(self, dm: "DistMiner", tx_ptr, items, arena_bytes: int):
         N = native.require_gpu()
         self.dev = torch.device("cuda", dm.device)
-        if dm.world > 1 or dm.force_protocol:
+        self.comm = None
+        if dm.mode == "tx":
+            torch.cuda.set_device(dm.device)
+            uid = [N.comm_unique_id() if dm.rank == 0 and dm.world > 1 else b"\0" * 128]
+            if dm.world > 1:
+                dist.broadcast_object_list(uid, src=0)
+            self.comm = N.Comm(dm.rank, dm.world, uid[0], dm.device)
+            self.stream = None
+            self.g = N.GpuMiner(dm.device, arena_bytes, 0)
+        elif dm.world > 1 or dm.force_protocol:
             # every torch op of the protocol (allocations, fills, collectives) and every native
             # kernel run on ONE stream, so they are ordered without extra synchronisation
             torch.cuda.set_device(dm.device)
@@ -101,6 +119,10 @@ class _GpuOps:
     def ctx(self):
         import contextlib
         return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
+    def mine_txdp(self, dm: "DistMiner", download: bool):
+        return self.g.mine_txdp(self.comm, dm.n_tx, dm.min_support, dm.max_len, download,
+                                dm.mfma, dm.support_tiles)
 
     def supports(self):
         c = torch.empty(self.n_items, dtype=torch.int32, device=self.dev)
@@ -196,10 +218,22 @@ class DistMiner:
     def __init__(self, tx_ptr: np.ndarray, items: np.ndarray, n_items: int, min_support: float,
                  device: int = 0, max_len: int = 0, mfma: bool = False,
                  arena_bytes: int = 0, backend: str = "gpu", force_protocol: bool = False,
-                 persistent: bool = False):
+                 persistent: bool = False, mode: str = "auto",
+                 global_n_tx: Optional[int] = None, support_tiles: int = 4):
+        """``global_n_tx`` given ⇒ (tx_ptr, items) already hold only this rank's shard (tx mode;
+        large datasets are generated/loaded per shard).  ``mode``: "item" (replicated bitmaps,
+        item-sharded DFS), "tx" (transaction-DP, see module doc) or "auto"."""
         self.world = dist.get_world_size() if (dist is not None and dist.is_initialized()) else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
-        self.n_tx = len(tx_ptr) - 1
+        self.n_tx = int(global_n_tx) if global_n_tx is not None else len(tx_ptr) - 1
+        if mode == "auto":
+            mode = "tx" if (global_n_tx is not None or self.n_tx >= (4 << 20)) else "item"
+        if mode == "tx" and backend != "gpu":
+            raise ValueError("mode='tx' needs the GPU backend (native RCCL communicator)")
+        if global_n_tx is not None and mode != "tx":
+            raise ValueError("pre-sharded input (global_n_tx) requires mode='tx'")
+        self.mode = mode
+        self.support_tiles = int(support_tiles)
         self.n_items = int(n_items)
         self.min_support = float(min_support)
         self.max_len = int(max_len)
@@ -210,9 +244,13 @@ class DistMiner:
         self.persistent = bool(persistent)
         lo, hi, ts = shard_bounds(self.n_tx, self.world, self.rank)
         self.lo, self.hi, self.ts = lo, hi, ts
-        sp = np.asarray(tx_ptr[lo:hi + 1])
-        sptr = np.ascontiguousarray(sp - sp[0], dtype=np.int64)
-        sitems = np.ascontiguousarray(items[sp[0]:sp[-1]], dtype=np.int32)
+        if global_n_tx is not None:  # already this rank's shard
+            sptr = np.ascontiguousarray(np.asarray(tx_ptr) - tx_ptr[0], dtype=np.int64)
+            sitems = np.ascontiguousarray(items[tx_ptr[0]:tx_ptr[-1]], dtype=np.int32)
+        else:
+            sp = np.asarray(tx_ptr[lo:hi + 1])
+            sptr = np.ascontiguousarray(sp - sp[0], dtype=np.int64)
+            sitems = np.ascontiguousarray(items[sp[0]:sp[-1]], dtype=np.int32)
         ops_cls = _GpuOps if backend == "gpu" else _CpuOps
         self.ops = ops_cls(self, sptr, sitems, arena_bytes)
         self.g = getattr(self.ops, "g", None)
@@ -223,6 +261,12 @@ class DistMiner:
 
     # ------------------------------------------------------------------------------------
     def step(self, download: bool = True) -> Dict:
+        if self.mode == "tx":
+            r = self.ops.mine_txdp(self, download and self.rank == 0)
+            st = dict(r["stats"])
+            st["global_itemsets"] = int(st["n_itemsets"])  # identical trie on every rank
+            self.last = r
+            return {"stats": st, "trie": r}
         if self.world == 1 and self.backend == "gpu" and not self.force_protocol:
             r = self.g.mine(self.min_support, self.max_len, False, download, True, self.mfma,
                             self.persistent)

@@ -1,0 +1,7 @@
+#!/usr/bin/env bash
+source "$(dirname "$0")/gpu_round.sh"
+export PYTHONUNBUFFERED=1
+step pytest_gpu 700 python -u -m pytest tests/test_gpu_kernels.py -q -x --timeout 200
+step bench 240 python -u bench.py --steps 30 --warmup 5
+step bench_chunked 240 env KMLS_FUSED_LEVELS=0 python -u bench.py --steps 30 --warmup 5
+step rocprof 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof9 -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3

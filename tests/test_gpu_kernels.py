@@ -74,7 +74,8 @@ def test_gpu_miner_matches_cpu(gpu_mod, shape, ms, use_mfma, fused, monkeypatch)
     g = gpu_mod.GpuMiner(0, 1 << 31, 0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     r = g.mine(ms, mfma=use_mfma)
-    assert r["stats"]["levels_path"] == ("fused" if fused == "1" else "chunked")
+    path = r["stats"]["levels_path"]
+    assert path.startswith("fused") if fused == "1" else path == "chunked", r["stats"]
     c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
     assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
     assert r["stats"]["max_depth"] == c["stats"]["max_depth"]
@@ -122,16 +123,16 @@ def test_fused_levels_repeat_and_small_arena(gpu_mod):
     keep = []
     for i in range(4):
         r = g.mine(0.05)
-        assert r["stats"]["levels_path"] == "fused"
+        assert r["stats"]["levels_path"] == "fused-resident", r["stats"]
         assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
         assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
         keep.append(r)  # results stay valid while later calls run (pinned buffers not reused)
     for r in keep:
         assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
-    small = gpu_mod.GpuMiner(0, 1 << 28, 0)
+    small = gpu_mod.GpuMiner(0, 360 << 20, 0)
     small.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     r = small.mine(0.05)
-    assert r["stats"]["levels_path"] == "chunked"
+    assert r["stats"]["levels_path"].startswith("chunked (fused fallback")
     assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
 
 
@@ -203,3 +204,73 @@ def test_persistent_dfs_equals_level_wise(gpu_mod, shape, ms):
     assert lw["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
     if c["stats"]["n_itemsets"] < 300_000:
         assert _trie_dict(p) == _trie_dict(c)
+
+
+@pytest.mark.parametrize("tiles", [1, 4])
+def test_txdp_mode_world1(gpu_mod, tiles):
+    """Transaction-DP path (tiled supports, shard-local bitmaps, per-level count all-reduce
+    through the native communicator — a copy at world size 1) equals the CPU miner."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+    tx = generate("ds2_weak", seed=4)
+    dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, 0.03, mode="tx", support_tiles=tiles)
+    r = dm.step(download=True)
+    assert r["stats"]["levels_path"] == "chunked-txdp"
+    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.03)
+    assert _trie_dict(r["trie"]) == _trie_dict(c)
+
+
+def test_txdp_presharded_large(gpu_mod):
+    """Pre-sharded input (global_n_tx) on a 2M-transaction slice of the 10M x 1M shape."""
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+    T = 2_000_000
+    ptr, items = gpu_mod.synth_transactions(T, 1_000_000, 40.0, 2000, 0.85, 0.85, 1)
+    dm = DistMiner(ptr, items, 1_000_000, 0.002, mode="tx", global_n_tx=T)
+    r = dm.step(download=True)
+    c = gpu_mod.mine_cpu(ptr, items, 1_000_000, 0.002)
+    assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
+    assert _trie_dict(r["trie"]) == _trie_dict(c)
+
+
+@pytest.mark.parametrize("metric,thr,strict,max_ante", [("confidence", 0.6, False, 0),
+                                                        ("confidence", 0.5, True, 0),
+                                                        ("lift", 1.2, False, 2),
+                                                        ("leverage", 0.0, False, 0)])
+def test_gpu_rules_equal_cpu(gpu_mod, metric, thr, strict, max_ante):
+    """HIP rule_score (hash + subset DP + ballot compaction) is bit-identical to the CPU engine,
+    including deep itemsets (k > 12 → per-wave global subset tables)."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.models.fpgrowth import mine_csr
+    from kubernetes_machine_learning_server_amd.models.rules import rules_from_trie
+    tx = generate("ds2", seed=1)
+    trie = mine_csr(tx.tx_ptr, tx.items, tx.n_items, 0.06, backend="cpu")
+    assert int(trie.depth.max()) >= 10
+    g = rules_from_trie(trie, metric, thr, max_antecedent=max_ante, strict=strict, backend="gpu")
+    c = rules_from_trie(trie, metric, thr, max_antecedent=max_ante, strict=strict, backend="cpu")
+    assert len(g) == len(c) and len(c) > 0
+    for f in ("itemset", "antecedent", "consequent", "confidence", "lift"):
+        np.testing.assert_array_equal(getattr(g, f), getattr(c, f))
+
+
+@pytest.mark.parametrize("scratch_bits", ["18", "14"])
+def test_gpu_rules_deep_itemsets(gpu_mod, monkeypatch, scratch_bits):
+    """16-item cliques: itemsets up to size 16 exercise the per-wave global subset tables
+    (13 <= k <= scratch_bits) and the hash-walk path (k > scratch_bits)."""
+    from kubernetes_machine_learning_server_amd.models.fpgrowth import mine_csr
+    from kubernetes_machine_learning_server_amd.models.rules import rules_from_trie
+    monkeypatch.setenv("KMLS_RULES_SCRATCH_BITS", scratch_bits)
+    rng = np.random.default_rng(0)
+    rows = []
+    for t in range(40):
+        core = list(range(16)) if t < 24 else list(rng.choice(16, size=12, replace=False))
+        rows.append(sorted(set(core) | set(rng.choice(np.arange(16, 60), size=5).tolist())))
+    ptr = np.zeros(len(rows) + 1, np.int64)
+    ptr[1:] = np.cumsum([len(r) for r in rows])
+    items = np.concatenate([np.array(r, np.int32) for r in rows])
+    trie = mine_csr(ptr, items, 60, 0.5, backend="cpu")
+    assert int(trie.depth.max()) == 16
+    g = rules_from_trie(trie, "confidence", 0.95, backend="gpu")
+    c = rules_from_trie(trie, "confidence", 0.95, backend="cpu")
+    assert len(g) == len(c) and len(c) > 0
+    for f in ("itemset", "antecedent", "consequent", "confidence", "lift"):
+        np.testing.assert_array_equal(getattr(g, f), getattr(c, f))
