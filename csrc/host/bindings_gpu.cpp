@@ -93,6 +93,17 @@ void register_gpu_bindings(py::module_& m) {
      py::arg("metric") = 0, py::arg("min_threshold") = 0.8, py::arg("max_antecedent") = 0,
      py::arg("device") = 0);
 
+  m.def("group_to_csr_gpu", [](I32 keys, I32 vals, int32_t n_keys, bool dedup, int device) {
+    KMLS_CHECK(keys.size() == vals.size(), "keys/vals differ in size");
+    CSR g;
+    {
+      py::gil_scoped_release nogil;
+      g = gpu::group_to_csr_gpu(device, keys.data(), vals.data(), keys.size(), n_keys, dedup);
+    }
+    return py::make_tuple(to_array(std::move(g.ptr)), to_array(std::move(g.idx)));
+  }, py::arg("keys"), py::arg("vals"), py::arg("n_keys"), py::arg("dedup") = true,
+     py::arg("device") = 0);
+
   m.def("comm_unique_id", []() { return py::bytes(gpu::comm_unique_id()); });
   py::class_<gpu::Comm>(m, "Comm")
       .def(py::init([](int rank, int world, py::bytes uid, int device) {

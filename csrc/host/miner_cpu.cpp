@@ -13,10 +13,20 @@
 #include <thread>
 #include <vector>
 
+#include <cstdlib>
+
 #include "kmls/common.hpp"
 #include "kmls/host.hpp"
 
 namespace kmls {
+
+int default_threads() {
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const int n = std::atoi(e);
+    if (n > 0) return n;
+  }
+  return std::max(1, (int)std::thread::hardware_concurrency());
+}
 
 uint32_t level2_threshold(uint64_t n_tx, double min_support) {
   return (uint32_t)std::ceil(min_support * (double)n_tx);
@@ -133,7 +143,7 @@ ItemsetTrie mine_cpu_bitmaps(const uint64_t* bm, int64_t F, int64_t W, const Fre
   std::vector<Task> tasks((size_t)std::max<int64_t>(F, 0));
   if (F >= 2 && max_len != 1) {
     Ctx cx{&fi, bm, W, fi.minsup2, max_len};
-    int nth = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+    int nth = threads > 0 ? threads : default_threads();
     nth = std::max(1, std::min<int>(nth, (int)F));
     std::atomic<int64_t> next{0};
     std::vector<Member> root((size_t)F);

@@ -183,6 +183,7 @@ struct Event {
 };
 
 constexpr int64_t kCandCap = 32ll << 20;  // candidates per chunk
+size_t fused_bump_cap(size_t bytes);
 
 struct MineRun {
   hipStream_t s;
@@ -427,8 +428,8 @@ struct MineRun {
     int64_t* c_gid = (int64_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 8);
     int32_t* c_prow = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
     const size_t rem = arena->capacity() - arena->used();
-    const size_t bump_bytes = rem > (320ull << 20) ? rem - (64ull << 20) : 0;
-    if (bump_bytes < (256ull << 20)) {
+    const size_t bump_bytes = fused_bump_cap(rem > (320ull << 20) ? rem - (64ull << 20) : 0);
+    if (bump_bytes < (16ull << 20)) {
       arena->pop_to(mark);
       fallback_reason = "arena too small for the bump region";
       return false;
@@ -625,6 +626,14 @@ struct MineRun {
     arena->pop_to(mark0);
   }
 };
+
+size_t fused_bump_cap(size_t bytes) {  // KMLS_FUSED_BUMP_MB: test knob forcing the fallback
+  if (const char* e = std::getenv("KMLS_FUSED_BUMP_MB")) {
+    const double mb = std::atof(e);
+    if (mb > 0) return std::min(bytes, (size_t)(mb * (1 << 20)));
+  }
+  return bytes;
+}
 
 bool fused_levels_enabled() {
   const char* e = std::getenv("KMLS_FUSED_LEVELS");
@@ -998,7 +1007,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     res = GpuMineResult();
     return false;
   }
-  const size_t bump_bytes = rem - (64ull << 20);
+  const size_t bump_bytes = fused_bump_cap(rem - (64ull << 20));
   char* bump_base = (char*)arena_->push(bump_bytes);
   std::shared_ptr<void> stage = pinned_->get(kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
   std::memset(stage.get(), 0, kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
@@ -1012,7 +1021,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   KMLS_HIP(hipMemsetAsync(d_cnt, 0, (size_t)I * 4, s));
   kern::item_support(d_items_, nnz_, (int32_t)I, d_cnt, s);
   kern::level_select(d_cnt, I, level1_threshold((uint64_t)n_tx_, cfg.min_support), d_ids, d_fcnt,
-                     d_rank_of, d_desc, s);
+                     d_rank_of, d_rrank /* scratch until root setup */, d_desc, s);
   KMLS_HIP(hipMemsetAsync(d_own_bm_, 0, need, s));
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of, d_own_bm_, Wp, 0, s);
   KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));

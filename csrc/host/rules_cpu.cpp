@@ -50,7 +50,7 @@ RuleSet association_rules_cpu(const int64_t* parent, const int32_t* item, const 
     return node;
   };
   const double T = (double)n_tx;
-  const int nth = std::max(1, threads > 0 ? threads : (int)std::thread::hardware_concurrency());
+  const int nth = std::max(1, threads > 0 ? threads : default_threads());
   std::vector<RuleSet> parts((size_t)nth);
   std::atomic<int64_t> next{0};
   std::atomic<bool> bad{false};

@@ -134,5 +134,28 @@ RuleSet association_rules_gpu(int device, const int64_t* parent, const int32_t* 
   return out;
 }
 
+CSR group_to_csr_gpu(int device, const int32_t* keys, const int32_t* vals, int64_t n,
+                     int32_t n_keys, bool dedup) {
+  KMLS_CHECK(n < (1ll << 31), "GPU group-by: more than 2^31 rows per call");
+  KMLS_HIP(hipSetDevice(device));
+  hipStream_t s;
+  KMLS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  struct StreamGuard { hipStream_t s; ~StreamGuard() { (void)hipStreamDestroy(s); } } sg{s};
+  DevBuf d_k(n * 4), d_v(n * 4), d_ptr((size_t)(n_keys + 1) * 8), d_idx(n * 4);
+  const size_t tb = kern::groupby_csr_temp_bytes(n, n_keys);
+  DevBuf d_tmp(tb);
+  KMLS_HIP(hipMemcpyAsync(d_k.p, keys, n * 4, hipMemcpyHostToDevice, s));
+  KMLS_HIP(hipMemcpyAsync(d_v.p, vals, n * 4, hipMemcpyHostToDevice, s));
+  const int64_t nnz = kern::groupby_csr(d_k.as<int32_t>(), d_v.as<int32_t>(), n, n_keys, dedup,
+                                        d_ptr.as<int64_t>(), d_idx.as<int32_t>(), d_tmp.p, tb, s);
+  CSR out;
+  out.ptr.resize((size_t)n_keys + 1);
+  out.idx.resize((size_t)nnz);
+  KMLS_HIP(hipMemcpyAsync(out.ptr.data(), d_ptr.p, out.ptr.size() * 8, hipMemcpyDeviceToHost, s));
+  if (nnz) KMLS_HIP(hipMemcpyAsync(out.idx.data(), d_idx.p, (size_t)nnz * 4, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  return out;
+}
+
 }  // namespace gpu
 }  // namespace kmls

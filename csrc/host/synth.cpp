@@ -124,7 +124,7 @@ void synth_transactions(int64_t n_tx, int64_t n_items, double mean_len, int n_ge
   const int64_t n_chunks = tx_end > tx_begin ? (tx_end - 1) / kChunk + 1 - ch0 : 0;
   std::vector<std::vector<int32_t>> c_items((size_t)n_chunks);
   std::vector<std::vector<int32_t>> c_lens((size_t)n_chunks);
-  const int nth = std::max(1, threads > 0 ? threads : (int)std::thread::hardware_concurrency());
+  const int nth = std::max(1, threads > 0 ? threads : default_threads());
   std::atomic<int64_t> next{0};
   auto worker = [&]() {
     std::vector<int32_t> buf;

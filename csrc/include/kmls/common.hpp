@@ -60,4 +60,8 @@ FrequentItems select_frequent(const uint32_t* item_counts, int64_t n_items, uint
     if (!(cond)) throw std::runtime_error(std::string("kmls: ") + (msg)); \
   } while (0)
 
+// Worker threads when a caller passes 0: OMP_NUM_THREADS if set (the GPU pool exports the
+// process's CPU share there; hardware_concurrency() reports the whole host), else all cores.
+int default_threads();
+
 }  // namespace kmls

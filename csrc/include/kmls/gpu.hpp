@@ -178,6 +178,11 @@ RuleSet association_rules_gpu(int device, const int64_t* parent, const int32_t* 
                               RuleMetric metric, double min_threshold, int max_antecedent,
                               double* kernel_ms);
 
+// Transaction builder on the GPU (kernels/groupby.hip): same CSR as group_to_csr(dedup,
+// sort_rows=true).
+CSR group_to_csr_gpu(int device, const int32_t* keys, const int32_t* vals, int64_t n,
+                     int32_t n_keys, bool dedup);
+
 // HBM-resident rule index + batched matcher kernel (serve_match_topk).
 class GpuRuleIndex {
  public:

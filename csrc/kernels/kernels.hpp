@@ -110,7 +110,8 @@ struct CopyOutArgs {
 // (closed form), iota rank/gid, root children buffers from the bump region.
 constexpr int64_t kSelectMaxItems = 16384;
 void level_select(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* ids,
-                  uint32_t* fcounts, int32_t* rank_of, FLevel* desc, hipStream_t s);
+                  uint32_t* fcounts, int32_t* rank_of, int32_t* rank_acc, FLevel* desc,
+                  hipStream_t s);
 struct RootSetupArgs {
   const uint64_t* bm;
   int32_t* rank;       // [n_items]
@@ -229,6 +230,14 @@ int rules_waves_per_block();
 void rules_pass(const RuleArgs& a, int grid, hipStream_t s);
 size_t rules_scan_temp_bytes(int64_t n);
 void rules_scan(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tb, hipStream_t s);
+
+// ---- transaction builder (groupby.hip) ----
+// CSR of vals grouped by keys in [0, n_keys): rows sorted (and duplicate-free when dedup).
+// Returns nnz (synchronises the stream).
+size_t groupby_csr_temp_bytes(int64_t n, int32_t n_keys);
+int64_t groupby_csr(const int32_t* d_keys, const int32_t* d_vals, int64_t n, int32_t n_keys,
+                    bool dedup, int64_t* d_ptr, int32_t* d_idx, void* d_tmp, size_t tmp_bytes,
+                    hipStream_t s);
 
 // ---- serving (serve.hip) ----
 void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,

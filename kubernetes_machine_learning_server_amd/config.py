@@ -39,6 +39,7 @@ class JobSettings:
     rules_mode: str = "full"     # full (all itemsets, as mlxtend) | pairs (SURVEY §0 fast path)
     num_gpus: int = 1
     min_confidence: float = 0.04  # legacy confidence rules (main.py:227)
+    checkpoint_dir: Optional[pathlib.Path] = None  # KMLS_CHECKPOINT_DIR: phase resume
 
     @property
     def dataset_list_file(self) -> pathlib.Path:
@@ -73,6 +74,8 @@ class JobSettings:
             rules_mode=_env("RULES_MODE", "full").lower(),
             num_gpus=int(_env("NUM_GPUS", "1")),
             min_confidence=float(_env("MIN_CONFIDENCE", "0.04")),
+            checkpoint_dir=(pathlib.Path(os.environ["KMLS_CHECKPOINT_DIR"])
+                            if os.environ.get("KMLS_CHECKPOINT_DIR") else None),
         )
 
 

@@ -27,6 +27,7 @@ from ..config import JobSettings
 from ..models.fpgrowth import ItemsetTrie, default_backend, mine_csr
 from ..serve.index import RuleIndexData, build_index_from_trie
 from ..utils.atomic_io import atomic_pickle, atomic_write_bytes
+from ..utils.checkpoint import PhaseCheckpoint
 from ..utils.timeutil import current_time_str, format_timedelta
 from . import preprocess as pp
 from . import rotation as rot
@@ -100,6 +101,21 @@ def mine_rules_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_su
     return idx, trie, info, (missing, dur)
 
 
+def resume_from_checkpoint(ck: PhaseCheckpoint, tx: pp.PlaylistTransactions, min_support: float,
+                           total_songs: int) -> Tuple[RuleIndexData, ItemsetTrie, str, Tuple[int, float]]:
+    z = ck.load("trie")
+    trie = ItemsetTrie(z["parent"], z["item"], z["count"], z["depth"], int(z["n_tx"]), min_support,
+                       {"backend": "checkpoint"}, tx.names)
+    idx = build_index_from_trie(trie.parent, trie.item, trie.count, trie.depth, tx.n_tx,
+                                len(tx.names), tx.names)
+    missing = total_songs - idx.n_keys
+    dur = float(z["seconds"])
+    print("Songs without recommendations:", missing)
+    print(f"Time elapsed in rule generation: {format_timedelta(dur)}")
+    info = f"min_support: {min_support} \tmissing songs: {missing} \ttime: {format_timedelta(dur)}"
+    return idx, trie, info, (missing, dur)
+
+
 def run_support_sweep(cfg: JobSettings, tx: pp.PlaylistTransactions, total_songs: int,
                       supports: Optional[List[float]] = None, out_csv: str = EXPERIMENT_CSV):
     """J14: the min_support sweep (main.py:450-473), written to ``fp_growth_experiment_results.csv``."""
@@ -163,10 +179,25 @@ def run(cfg: Optional[JobSettings] = None) -> Dict:
     tx = pp.group_tracks_by_playlist(t)
     if cfg.experiment_supports and rank == 0:
         run_support_sweep(cfg, tx, total_songs)
+    ck = PhaseCheckpoint.for_dataset(cfg.checkpoint_dir, selected, min_support=cfg.min_support,
+                                     rules_mode=cfg.rules_mode, sample_ratio=cfg.sample_ratio)
+    resumed = ck.has("trie") if rank == 0 else False
     if distributed:
+        import torch.distributed as dist
+        box = [resumed]
+        dist.broadcast_object_list(box, src=0)
+        resumed = box[0]
+    if resumed:  # a previous attempt on this dataset crashed after mining
+        res = resume_from_checkpoint(ck, tx, cfg.min_support, total_songs) if rank == 0 else None
+        say("Resumed mining results from checkpoint", ck.dir)
+    elif distributed:
         res = mine_rules_distributed(cfg, tx, cfg.min_support, total_songs)
     else:
         res = mine_rules(cfg, tx, cfg.min_support, total_songs)
+    if rank == 0 and not resumed and ck.enabled:
+        trie = res[1]
+        ck.save("trie", parent=trie.parent, item=trie.item, count=trie.count, depth=trie.depth,
+                n_tx=np.int64(trie.n_tx), seconds=np.float64(res[3][1]))
     summary: Dict = {}
     if rank == 0:
         idx, trie, info, (missing, dur) = res
@@ -177,9 +208,11 @@ def run(cfg: Optional[JobSettings] = None) -> Dict:
             save_itemsets(cfg, trie)
         _fault("before_marker")
         ts = rot.append_dataset_history(cfg, new_index, selected)
+        ck.clear()  # the run is complete: nothing to resume
         summary = {"dataset_index": new_index, "dataset": selected, "marker": ts,
                    "n_keys": idx.n_keys, "songs_without_recommendations": missing,
-                   "n_itemsets": len(trie), "rule_seconds": dur, "backend": trie.stats.get("backend")}
+                   "n_itemsets": len(trie), "rule_seconds": dur, "backend": trie.stats.get("backend"),
+                   "resumed": resumed}
         print("=== Run complete. Exiting, current time is ", current_time_str(), " ===")
     if distributed:
         import torch.distributed as dist

@@ -152,9 +152,22 @@ class PlaylistTransactions:
                 for r in range(self.n_tx)]
 
 
-def group_tracks_by_playlist(t: TracksTable) -> PlaylistTransactions:
-    """{pid: [track_name, ...]} as CSR over name codes (the miners' input)."""
-    ptr, items = native.load().group_to_csr(t.codes["pid"], t.codes["track_name"],
-                                            t.n_unique("pid"), True, True)
+GPU_GROUPBY_MIN_ROWS = 4_000_000  # below this the PCIe round trip costs more than the host sort
+
+
+def group_tracks_by_playlist(t: TracksTable, backend: str = "auto") -> PlaylistTransactions:
+    """{pid: [track_name, ...]} as CSR over name codes (the miners' input).
+
+    ``backend``: "cpu" (C++ group-by), "gpu" (HIP radix-sort group-by, kernels/groupby.hip) or
+    "auto" (GPU for >= 4M rows when a device is visible; env ``GROUPBY`` overrides)."""
+    import os
+    backend = os.environ.get("GROUPBY", backend).lower()
+    keys, vals = t.codes["pid"], t.codes["track_name"]
+    if backend == "auto":
+        backend = "gpu" if (len(keys) >= GPU_GROUPBY_MIN_ROWS and native.gpu_available()) else "cpu"
+    if backend == "gpu":
+        ptr, items = native.require_gpu().group_to_csr_gpu(keys, vals, t.n_unique("pid"), True)
+    else:
+        ptr, items = native.load().group_to_csr(keys, vals, t.n_unique("pid"), True, True)
     return PlaylistTransactions(np.asarray(ptr), np.asarray(items), t.uniques["track_name"],
                                 t.uniques["pid"])

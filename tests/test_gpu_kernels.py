@@ -112,7 +112,7 @@ def test_gpu_miner_chunked_levels(gpu_mod, monkeypatch):
     assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
 
 
-def test_fused_levels_repeat_and_small_arena(gpu_mod):
+def test_fused_levels_repeat_and_small_arena(gpu_mod, monkeypatch):
     """Repeated calls (epoch-tagged look-back state, persistent output buffers, streamed
     download sized from the previous call) and the fallback when the arena is too small."""
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
@@ -129,10 +129,11 @@ def test_fused_levels_repeat_and_small_arena(gpu_mod):
         keep.append(r)  # results stay valid while later calls run (pinned buffers not reused)
     for r in keep:
         assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
-    small = gpu_mod.GpuMiner(0, 360 << 20, 0)
+    monkeypatch.setenv("KMLS_FUSED_BUMP_MB", "64")  # device allocations overflow mid-way
+    small = gpu_mod.GpuMiner(0, 2 << 30, 0)
     small.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     r = small.mine(0.05)
-    assert r["stats"]["levels_path"].startswith("chunked (fused fallback")
+    assert "fallback: device overflow code 1" in r["stats"]["levels_path"], r["stats"]
     assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
 
 
@@ -274,3 +275,15 @@ def test_gpu_rules_deep_itemsets(gpu_mod, monkeypatch, scratch_bits):
     assert len(g) == len(c) and len(c) > 0
     for f in ("itemset", "antecedent", "consequent", "confidence", "lift"):
         np.testing.assert_array_equal(getattr(g, f), getattr(c, f))
+
+
+@pytest.mark.parametrize("n,n_keys,dedup", [(1000, 7, True), (300_000, 2246, True),
+                                             (2_000_000, 50_000, True), (100_000, 300, False)])
+def test_gpu_groupby_equals_host(gpu_mod, n, n_keys, dedup):
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, n_keys, size=n).astype(np.int32)
+    vals = rng.integers(0, 5000, size=n).astype(np.int32)
+    gp, gi = gpu_mod.group_to_csr_gpu(keys, vals, n_keys, dedup)
+    cp, ci = gpu_mod.group_to_csr(keys, vals, n_keys, dedup, True)
+    np.testing.assert_array_equal(gp, cp)
+    np.testing.assert_array_equal(gi, ci)

@@ -174,3 +174,24 @@ def test_csv_reader_quotes(tmp_path):
     assert t.uniques["track_name"] == ['City Of Stars - From "La La Land"', "Plain"]
     assert t.uniques["track_uri"] == ["u,1", "u2"]
     assert t.uniques["artist_name"] == ["A, B"]
+
+
+def test_checkpoint_resume_after_crash(pvc, tmp_path, monkeypatch):
+    """A crash after mining leaves a phase checkpoint; the restarted job (same dataset — the
+    rotation cursor did not advance) resumes from it and produces the same artifacts."""
+    ckdir = tmp_path / "ckpt"
+    cfg = job_settings(pvc, checkpoint_dir=ckdir)
+    monkeypatch.setenv("KMLS_FAULT", "before_recommendations")
+    with pytest.raises(RuntimeError, match="injected fault"):
+        job.run(cfg)
+    assert any(ckdir.rglob("trie.npz"))
+    monkeypatch.delenv("KMLS_FAULT")
+    s = job.run(cfg)
+    assert s["resumed"] is True and s["dataset_index"] == 1
+    assert not any(ckdir.rglob("trie.npz"))  # cleared after success
+    rec_resumed = load(cfg.pickles_folder / "recommendations.pickle")
+    clean = job_settings(tmp_path / "clean")
+    make_datasets(tmp_path / "clean")
+    s2 = job.run(clean)
+    assert s2["resumed"] is False
+    assert load(clean.pickles_folder / "recommendations.pickle") == rec_resumed
