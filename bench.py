@@ -131,7 +131,11 @@ def main() -> int:
             "model": f"fpgrowth-{args.shape}-shape",
             "global_batch": int(tx.n_tx),
             "seq_len": int(tx.n_items),
-            "parallelism": f"tx-dp{world}+item-shard{world}" if world > 1 else "single",
+            "parallelism": ({"replicate": f"dp{world}-replicated-data+root-class-partition",
+                             "tx": f"tx-dp{world}+per-level-count-allreduce",
+                             "item": f"tx-dp{world}+item-shard{world}"}.get(
+                                 getattr(dm, "mode", "item")) if world > 1 and not args.cpu
+                            else "single"),
             "min_support": args.min_support,
             "max_len": args.max_len,
             "n_itemsets": n_itemsets,
@@ -139,6 +143,7 @@ def main() -> int:
             "max_depth": int(st.get("max_depth", 0)),
             "level2": "mfma-i8" if args.mfma else "popcount-bitgemm",
             "levels3plus": "persistent-dfs" if args.persistent else "level-wise",
+            "levels_path": st.get("levels_path"),
         },
         "verified_vs_cpu_miner": verified,
         "reference_seconds_ds2_0.05": REF_SECONDS_DS2_005,

@@ -179,6 +179,16 @@ void register_gpu_bindings(py::module_& m) {
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("pairs_only") = false,
          py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
          py::arg("persistent") = false)
+      .def("mine_partition", [](gpu::GpuMiner& g, double ms, int max_len, bool download, int rank,
+                                int world) {
+        gpu::GpuMineResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = g.mine_partition(make_cfg(ms, max_len, false, true, false), download, rank, world);
+        }
+        return result_to_dict(std::move(r));
+      }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("download") = true,
+         py::arg("rank") = 0, py::arg("world") = 1)
       .def("mine_txdp", [](gpu::GpuMiner& g, gpu::Comm* comm, int64_t global_n_tx, double ms,
                            int max_len, bool download, bool mfma, int support_tiles) {
         gpu::GpuMineResult r;

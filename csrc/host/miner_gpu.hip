@@ -859,7 +859,8 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     if (F <= 32768 && cfg.level2_gram) {
       uint32_t* gram = (uint32_t*)arena_->push((size_t)F * F * sizeof(uint32_t));
       KMLS_HIP(hipMemsetAsync(gram, 0, (size_t)F * F * sizeof(uint32_t), s));
-      if (cfg.level2_mfma)
+      // matrix cores for long rows (large T): the int8 MFMA path moves 8x more MACs per byte
+      if (cfg.level2_mfma || Wp >= 4096)
         kern::pair_gram_mfma_i8((const uint64_t*)bm_dev, Wp, F, gram, s);
       else
         kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);
@@ -946,7 +947,8 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
 // encode, level-2 gram and the root descriptor are all produced on the device, so together with
 // the fused level loop one mining call has no host round trip before the final one.  Returns
 // false (nothing committed) when the fused loop overflowed; mine() then runs the host path.
-bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res) {
+bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res, int part_rank,
+                             int part_world) {
   hipStream_t s = (hipStream_t)stream_;
   auto t0 = std::chrono::steady_clock::now();
   const int64_t I = n_items_;
@@ -1026,8 +1028,15 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of, d_own_bm_, Wp, 0, s);
   KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));
   kern::pair_gram_popcount_dev(d_own_bm_, Wp, &d_desc[1].n_rows, I, d_gram, s);
+  int32_t* d_prank = nullptr;
+  if (part_world > 1) {  // replicated-data partition of the root classes, computed on device
+    int64_t* d_cost = (int64_t*)arena_->push((size_t)I * 8);
+    d_prank = (int32_t*)arena_->push((size_t)I * 4);
+    kern::level_partition(d_gram, I, d_desc, run.minsup, I, d_cost, d_prank, s);
+  }
   kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
-                         run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap};
+                         run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
+                         d_prank, part_world, part_rank};
   kern::level_root_setup(d_desc, d_ctl, ra, s);
   // frequent-item tables for the frequent() API: staged to pinned memory while levels run
   std::shared_ptr<void> fstage = pinned_->get((size_t)I * 12);
@@ -1076,25 +1085,42 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   res.phases.push_back({"prologue(support+select+encode+gram)", elapsed(e0, e1)});
   res.phases.push_back({"levels", elapsed(e1, e2)});
   res.stats.n_frequent_items = F;
-  res.stats.n_itemsets = N;
+  // level-1 nodes are replicated on every rank of a partition; rank 0 counts them
+  res.stats.n_itemsets = (part_world > 1 && part_rank != 0) ? N - F : N;
   res.stats.n_candidates = run.n_candidates;
   res.stats.max_depth = F ? run.max_depth : 0;
   res.stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   res.arena_high_water = (int64_t)arena_->high_water();
-  res.levels_path = "fused-resident";
+  res.levels_path = part_world > 1 ? "fused-resident-partition" : "fused-resident";
   arena_->pop_to(mark);
   return true;
+}
+
+bool GpuMiner::resident_ok(const MineConfig& cfg) const {
+  return fused_levels_enabled() && !cfg.persistent && cfg.level2_gram && !cfg.level2_mfma &&
+         !cfg.pairs_only && cfg.max_len != 1 && n_items_ >= 2 &&
+         n_items_ <= kern::kSelectMaxItems && (size_t)n_items_ * words_local() * 8 <= (1ull << 30) &&
+         n_tx_ > 0;
+}
+
+GpuMineResult GpuMiner::mine_partition(const MineConfig& cfg, bool download, int rank, int world) {
+  KMLS_HIP(hipSetDevice(device_));
+  fused_fallback_.clear();
+  GpuMineResult r;
+  if (!resident_ok(cfg))
+    throw std::runtime_error("mine_partition: data not eligible for the device-resident path");
+  if (!mine_resident(cfg, download, r, rank, world))
+    throw std::runtime_error("mine_partition: fused path overflowed (" + fused_fallback_ + ")");
+  return r;
 }
 
 GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download) {
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
   fused_fallback_.clear();
-  if (fused_levels_enabled() && !cfg.persistent && cfg.level2_gram && !cfg.level2_mfma &&
-      !cfg.pairs_only && cfg.max_len != 1 && n_items_ >= 2 && n_items_ <= kern::kSelectMaxItems &&
-      (size_t)n_items_ * words_local() * 8 <= (1ull << 30) && n_tx_ > 0) {
+  if (resident_ok(cfg)) {
     GpuMineResult r;
-    if (mine_resident(cfg, download, r)) return r;
+    if (mine_resident(cfg, download, r, 0, 1)) return r;
   }
   auto t0 = std::chrono::steady_clock::now();
   Event e0, e1, e2;

@@ -124,6 +124,11 @@ class GpuMiner {
                              const uint8_t* owned_mask, bool emit_level1, bool download);
   // Convenience single-GPU path: A + B + C + D.
   GpuMineResult mine(const MineConfig& cfg, bool download);
+  // Replicated-data multi-GPU step (small datasets): every rank holds the full CSR, runs the
+  // device-resident prologue, and expands only the root classes the device-side snake
+  // partition assigns to `rank` — no collective inside; the caller all-reduces the count.
+  bool resident_ok(const MineConfig& cfg) const;
+  GpuMineResult mine_partition(const MineConfig& cfg, bool download, int rank, int world);
   // Transaction-data-parallel mining (large T): this rank holds a transaction shard; supports
   // are counted in `support_tiles` tiles whose all-reduces overlap the next tile's histogram
   // (comm stream); bitmaps stay shard-local ([F][Ws] words), and every level's candidate
@@ -162,7 +167,8 @@ class GpuMiner {
   unsigned int* abort_host_ = nullptr;       // watchdog flag (pinned, device-mapped)
   const unsigned int* abort_dev_ = nullptr;
   int n_cus_ = 256;
-  bool mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res);
+  bool mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res, int part_rank,
+                     int part_world);
   std::string fused_fallback_;
   std::unique_ptr<OutBufs> out_;  // output trie kept allocated across mine() calls
   Comm* comm_ = nullptr;          // set during mine_txdp: level counts are all-reduced

@@ -15,6 +15,7 @@
 // tiles of one tile-row share an XCD L2.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -69,8 +70,11 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma(const unsigned long long
 
   v16i acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
   const int shift = 16 * h;
-  const int64_t n2 = Wp >> 1;  // 16-byte chunks per row (Wp is a multiple of 4 words)
-  for (int64_t w2 = 0; w2 < n2; w2 += 2) {
+  // split-K: blockIdx.y owns word slice [kw0, kw1) (multiples of 4 words); partial Gram tiles
+  // are combined with integer atomics, so the result is exact and order-independent
+  const int64_t slice = (((Wp + gridDim.y - 1) / gridDim.y) + 3) & ~(int64_t)3;
+  const int64_t kw0 = (int64_t)blockIdx.y * slice, kw1 = min(Wp, kw0 + slice);
+  for (int64_t w2 = kw0 >> 1; w2 < (kw1 >> 1); w2 += 2) {
     ulonglong2 A0[2], A1[2], B0[2], B1[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -106,13 +110,24 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma(const unsigned long long
     const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
     const int64_t rA = rowb0 + row, rB = rowb0 + 32 + row;
     const int64_t cA = colb0 + r, cB = colb0 + 32 + r;
-    if (rA < F) {
-      if (cA < F && cA > rA) out[rA * F + cA] = (uint32_t)acc00[reg];
-      if (cB < F && cB > rA) out[rA * F + cB] = (uint32_t)acc01[reg];
-    }
-    if (rB < F) {
-      if (cA < F && cA > rB) out[rB * F + cA] = (uint32_t)acc10[reg];
-      if (cB < F && cB > rB) out[rB * F + cB] = (uint32_t)acc11[reg];
+    if (gridDim.y == 1) {
+      if (rA < F) {
+        if (cA < F && cA > rA) out[rA * F + cA] = (uint32_t)acc00[reg];
+        if (cB < F && cB > rA) out[rA * F + cB] = (uint32_t)acc01[reg];
+      }
+      if (rB < F) {
+        if (cA < F && cA > rB) out[rB * F + cA] = (uint32_t)acc10[reg];
+        if (cB < F && cB > rB) out[rB * F + cB] = (uint32_t)acc11[reg];
+      }
+    } else {
+      if (rA < F) {
+        if (cA < F && cA > rA && acc00[reg]) atomicAdd(&out[rA * F + cA], (uint32_t)acc00[reg]);
+        if (cB < F && cB > rA && acc01[reg]) atomicAdd(&out[rA * F + cB], (uint32_t)acc01[reg]);
+      }
+      if (rB < F) {
+        if (cA < F && cA > rB && acc10[reg]) atomicAdd(&out[rB * F + cA], (uint32_t)acc10[reg]);
+        if (cB < F && cB > rB && acc11[reg]) atomicAdd(&out[rB * F + cB], (uint32_t)acc11[reg]);
+      }
     }
   }
 }
@@ -124,7 +139,9 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
   if (Wp % 4 != 0) throw std::runtime_error("kmls: pair_gram_mfma_i8 needs Wp % 4 == 0");
   const int64_t nt = (F + kTile - 1) / kTile;
   const int64_t blocks = nt * (nt + 1) / 2;
-  hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)blocks), dim3(256), 0, s,
+  // split K until the grid covers the chip (~4 blocks per CU), slices >= 1024 words
+  const int64_t ks = std::max<int64_t>(1, std::min<int64_t>((1024 + blocks - 1) / blocks, Wp / 1024));
+  hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
                      (const unsigned long long*)bm, Wp, F, nt, blocks, out);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e));

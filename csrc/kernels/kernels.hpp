@@ -125,8 +125,14 @@ struct RootSetupArgs {
   uint8_t* out_depth;
   int64_t Wp;
   int64_t out_cap;
+  const int32_t* prank;  // partition rank of each root class (world > 1), see level_partition
+  int world;
+  int my_rank;
 };
 void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s);
+// rank root classes by estimated cost (n_a^2 + 1 from the gram, desc) for the snake partition
+void level_partition(const uint32_t* gram, int64_t ld, FLevel* desc, uint32_t minsup,
+                     int64_t F_max, int64_t* cost, int32_t* prank, hipStream_t s);
 int level_grid(int n_cus);
 int64_t level_tile();
 int64_t level_scan_tile();

@@ -491,11 +491,86 @@ __global__ __launch_bounds__(256) void k_select_scatter(const uint32_t* __restri
   if (threadIdx.x == 0 && s_F) atomicAdd((unsigned long long*)&desc[1].n_rows, (unsigned long long)s_F);
 }
 
+// Root-class partition for replicated-data multi-GPU mining (identical on every rank, so no
+// collective): cost(a) = n_a^2 + 1 with n_a = frequent extensions of item a (gram row), ranked
+// by (cost desc, a asc) and dealt in snake order — the device twin of dist_miner.lpt_partition.
+__global__ __launch_bounds__(256) void k_root_costs(const uint32_t* __restrict__ gram, int64_t ld,
+                                                    const FLevel* desc, uint32_t minsup,
+                                                    int64_t* __restrict__ cost) {
+  __shared__ int64_t s_w[4];
+  const int64_t F = desc[1].n_rows;
+  const int64_t a = blockIdx.x;
+  if (a >= F) return;
+  int64_t n = 0;
+  for (int64_t b = a + 1 + threadIdx.x; b < F; b += blockDim.x) n += gram[a * ld + b] >= minsup;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t t = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    cost[a] = t * t + 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rank_desc(const int64_t* __restrict__ cost,
+                                                   const FLevel* desc, int32_t* __restrict__ rank) {
+  __shared__ int64_t s_c[256];
+  const int64_t F = desc[1].n_rows;
+  const int64_t j0 = (int64_t)blockIdx.y * 256;
+  if (j0 >= F || (int64_t)blockIdx.x * 256 >= F) return;
+  const int64_t jn = min((int64_t)256, F - j0);
+  if ((int64_t)threadIdx.x < jn) s_c[threadIdx.x] = cost[j0 + threadIdx.x];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= F) return;
+  const int64_t ci = cost[i];
+  int32_t r = 0;
+  for (int64_t jj = 0; jj < jn; ++jj) {
+    const int64_t cj = s_c[jj], j = j0 + jj;
+    r += (cj > ci || (cj == ci && j < i)) ? 1 : 0;
+  }
+  if (r) atomicAdd(&rank[i], r);
+}
+
 __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* ctl,
                                                            RootSetupArgs a) {
   __shared__ int ok;
+  __shared__ int64_t s_scan[1024];
+  __shared__ int64_t s_carry;
   const int64_t F = desc[1].n_rows;
-  const int64_t n_cand = F * (F - 1) / 2;
+  // root candidate offsets: every class owned → closed form; else a block scan of the owned
+  // classes' lengths (F - a - 1)
+  int64_t n_cand;
+  if (a.world <= 1) {
+    n_cand = F * (F - 1) / 2;
+    for (int64_t i = threadIdx.x; i <= F; i += blockDim.x) a.cand_off[i] = i * (2 * F - i - 1) / 2;
+  } else {
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (int64_t base = 0; base <= F; base += blockDim.x) {
+      const int64_t i = base + threadIdx.x;
+      int64_t v = 0;
+      if (i < F) {
+        const int64_t k = a.prank[i], rnd = k / a.world, p = k % a.world;
+        const int64_t owner = (rnd % 2 == 0) ? p : a.world - 1 - p;
+        v = owner == a.my_rank ? F - i - 1 : 0;
+      }
+      s_scan[threadIdx.x] = v;
+      __syncthreads();
+      for (int off = 1; off < (int)blockDim.x; off <<= 1) {  // Hillis-Steele inclusive
+        const int64_t add = (int)threadIdx.x >= off ? s_scan[threadIdx.x - off] : 0;
+        __syncthreads();
+        s_scan[threadIdx.x] += add;
+        __syncthreads();
+      }
+      if (i <= F) a.cand_off[i] = s_carry + s_scan[threadIdx.x] - v;
+      __syncthreads();
+      if (threadIdx.x == blockDim.x - 1) s_carry += s_scan[threadIdx.x];
+      __syncthreads();
+    }
+    n_cand = s_carry;
+  }
   if (threadIdx.x == 0) {
     FLevel& r = desc[1];
     r.bm = a.bm;
@@ -520,16 +595,13 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
   }
   __syncthreads();
   if (!ok) return;
-  for (int64_t i = threadIdx.x; i <= F; i += blockDim.x) {
-    a.cand_off[i] = i * (2 * F - i - 1) / 2;  // Σ_{a < i} (F - a - 1)
-    if (i < F) {
-      a.rank[i] = (int32_t)i;
-      a.gid[i] = i;
-      a.out_parent[i] = -1;
-      a.out_item[i] = a.ids[i];
-      a.out_count[i] = a.fcounts[i];
-      a.out_depth[i] = 1;
-    }
+  for (int64_t i = threadIdx.x; i < F; i += blockDim.x) {
+    a.rank[i] = (int32_t)i;
+    a.gid[i] = i;
+    a.out_parent[i] = -1;
+    a.out_item[i] = a.ids[i];
+    a.out_count[i] = a.fcounts[i];
+    a.out_depth[i] = 1;
   }
 }
 
@@ -580,6 +652,16 @@ void level_select(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* id
   hipLaunchKernelGGL(k_select_rank, dim3(nb, nb), dim3(256), 0, s, cnt, n_items, c1, rank_acc);
   hipLaunchKernelGGL(k_select_scatter, dim3(nb), dim3(256), 0, s, cnt, n_items, c1, rank_acc, ids,
                      fcounts, rank_of, desc);
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_partition(const uint32_t* gram, int64_t ld, FLevel* desc, uint32_t minsup,
+                     int64_t F_max, int64_t* cost, int32_t* prank, hipStream_t s) {
+  KMLS_HIP(hipMemsetAsync(prank, 0, (size_t)F_max * 4, s));
+  hipLaunchKernelGGL(k_root_costs, dim3((unsigned)std::max<int64_t>(F_max, 1)), dim3(256), 0, s,
+                     gram, ld, desc, minsup, cost);
+  const unsigned nb = (unsigned)((F_max + 255) / 256);
+  hipLaunchKernelGGL(k_rank_desc, dim3(nb, nb), dim3(256), 0, s, cost, desc, prank);
   KMLS_HIP(hipGetLastError());
 }
 

@@ -76,6 +76,58 @@ __global__ __launch_bounds__(kBlock) void k_item_support(const int32_t* __restri
   }
 }
 
+// Large vocabularies (1M items, Zipf popularity): a dense LDS histogram does not fit, and plain
+// global atomics serialise on the hottest items (the top item alone is ~2% of all occurrences).
+// Each block privatises whatever items it sees in an LDS open-addressing table (4096 slots, 8
+// probes); misses fall through to a global atomic; the table is flushed once per block.
+constexpr int kHashSlots = 4096;
+
+__device__ __forceinline__ void hash_count(int32_t x, int32_t* hk, uint32_t* hv,
+                                           uint32_t* __restrict__ counts) {
+  const uint32_t h = ((uint32_t)x * 2654435761u) >> 20;  // 12 bits
+#pragma unroll 1
+  for (int p = 0; p < 8; ++p) {
+    const uint32_t slot = (h + p) & (kHashSlots - 1);
+    int32_t k = hk[slot];
+    if (k == -1) {
+      k = atomicCAS(&hk[slot], -1, x);
+      if (k == -1) k = x;
+    }
+    if (k == x) {
+      atomicAdd(&hv[slot], 1u);
+      return;
+    }
+  }
+  atomicAdd(&counts[x], 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_item_support_hash(const int32_t* __restrict__ items,
+                                                              int64_t nnz,
+                                                              uint32_t* __restrict__ counts) {
+  __shared__ int32_t hk[kHashSlots];
+  __shared__ uint32_t hv[kHashSlots];
+  for (int i = threadIdx.x; i < kHashSlots; i += blockDim.x) {
+    hk[i] = -1;
+    hv[i] = 0;
+  }
+  __syncthreads();
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = nnz >> 2;
+  const int4* v = reinterpret_cast<const int4*>(items);
+  for (int64_t i = gtid; i < n4; i += nthr) {
+    const int4 q = v[i];
+    hash_count(q.x, hk, hv, counts);
+    hash_count(q.y, hk, hv, counts);
+    hash_count(q.z, hk, hv, counts);
+    hash_count(q.w, hk, hv, counts);
+  }
+  for (int64_t i = (n4 << 2) + gtid; i < nnz; i += nthr) hash_count(items[i], hk, hv, counts);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHashSlots; i += blockDim.x)
+    if (hk[i] >= 0 && hv[i]) atomicAdd(&counts[hk[i]], hv[i]);
+}
+
 // ----------------------------------------------------------------------------------------
 // O4 bitmap encode: bit t of row rank_of[item] for every (t, item) of the CSR shard.
 // One wave64 per transaction (lanes stride its items), so a 2k-transaction shard already
@@ -214,13 +266,16 @@ __global__ __launch_bounds__(kBlock) void k_pair_gram_popcount(
   uint32_t acc[4][4] = {};
   // staging map: thread → (row = tid>>2, words (tid&3)*4 .. +3)
   const int lr = threadIdx.x >> 2, lk = (threadIdx.x & 3) * 4;
-  for (int64_t k0 = 0; k0 < Wp; k0 += kGK) {
+  // split-K over blockIdx.y (word slices, multiples of kGK); partials combine with atomics
+  const int64_t slice = (((Wp + gridDim.y - 1) / gridDim.y) + kGK - 1) / kGK * kGK;
+  const int64_t kb = (int64_t)blockIdx.y * slice, ke = min(Wp, kb + slice);
+  for (int64_t k0 = kb; k0 < ke; k0 += kGK) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t kk = k0 + lk + i;
       const int64_t ra = r0 + lr, rb = q0 + lr;
-      As[lk + i][lr] = (ra < F && kk < Wp) ? bm[ra * Wp + kk] : 0ull;
-      Bs[lk + i][lr] = (rb < F && kk < Wp) ? bm[rb * Wp + kk] : 0ull;
+      As[lk + i][lr] = (ra < F && kk < ke) ? bm[ra * Wp + kk] : 0ull;
+      Bs[lk + i][lr] = (rb < F && kk < ke) ? bm[rb * Wp + kk] : 0ull;
     }
     __syncthreads();
 #pragma unroll 4
@@ -242,7 +297,10 @@ __global__ __launch_bounds__(kBlock) void k_pair_gram_popcount(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t q = q0 + tx * 4 + j;
-      if (q < F && q > r) out[r * ld + q] = acc[i][j];
+      if (q < F && q > r) {
+        if (gridDim.y == 1) out[r * ld + q] = acc[i][j];
+        else if (acc[i][j]) atomicAdd(&out[r * ld + q], acc[i][j]);
+      }
     }
   }
 }
@@ -273,15 +331,26 @@ int team_size(int64_t Wp) {
 void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* counts,
                   hipStream_t s) {
   if (nnz <= 0) return;
+  // the kernels read int4 vectors: peel a misaligned head (tile sub-ranges start anywhere)
+  const int64_t mis = ((uintptr_t)items & 15) / 4;
+  const int64_t head = mis ? std::min<int64_t>(nnz, 4 - mis) : 0;
+  if (head) {
+    hipLaunchKernelGGL(k_item_support<false>, dim3(1), dim3(64), 0, s, items, head, n_items, counts);
+    items += head;
+    nnz -= head;
+    if (nnz <= 0) {
+      KMLS_HIP(hipGetLastError());
+      return;
+    }
+  }
   const size_t lds = (size_t)n_items * sizeof(uint32_t);
   if (lds <= 64 * 1024) {
     const int g = grid_for(nnz, kBlock * 64, 1024);
     hipLaunchKernelGGL(k_item_support<true>, dim3(g), dim3(kBlock), lds, s, items, nnz, n_items,
                        counts);
   } else {
-    const int g = grid_for(nnz, kBlock * 4, 8192);
-    hipLaunchKernelGGL(k_item_support<false>, dim3(g), dim3(kBlock), 0, s, items, nnz, n_items,
-                       counts);
+    const int g = grid_for(nnz, kBlock * 64, 1024);
+    hipLaunchKernelGGL(k_item_support_hash, dim3(g), dim3(kBlock), 0, s, items, nnz, counts);
   }
   KMLS_HIP(hipGetLastError());
 }
@@ -409,7 +478,8 @@ void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out
   if (F < 2) return;
   const int64_t nt = (F + kGT - 1) / kGT;
   const int64_t blocks = nt * (nt + 1) / 2;
-  hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks), dim3(kBlock), 0, s,
+  const int64_t ks = std::max<int64_t>(1, std::min<int64_t>((1024 + blocks - 1) / blocks, Wp / 1024));
+  hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks, (unsigned)ks), dim3(kBlock), 0, s,
                      (const unsigned long long*)bm, Wp, F, nt, out, F, (const int64_t*)nullptr);
   KMLS_HIP(hipGetLastError());
 }
@@ -419,7 +489,8 @@ void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, i
   if (F_max < 2) return;
   const int64_t nt = (F_max + kGT - 1) / kGT;
   const int64_t blocks = nt * (nt + 1) / 2;
-  hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks), dim3(kBlock), 0, s,
+  const int64_t ks = std::max<int64_t>(1, std::min<int64_t>((1024 + blocks - 1) / blocks, Wp / 1024));
+  hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks, (unsigned)ks), dim3(kBlock), 0, s,
                      (const unsigned long long*)bm, Wp, F_max, nt, out, F_max, dF);
   KMLS_HIP(hipGetLastError());
 }

@@ -171,3 +171,43 @@ def group_tracks_by_playlist(t: TracksTable, backend: str = "auto") -> PlaylistT
         ptr, items = native.load().group_to_csr(keys, vals, t.n_unique("pid"), True, True)
     return PlaylistTransactions(np.asarray(ptr), np.asarray(items), t.uniques["track_name"],
                                 t.uniques["pid"])
+
+
+# ---- J16: helpers the reference defines but never calls (kept for API parity) -------------------
+def save_most_frequent_tracks_dict(sorted_most_frequent: List[Dict],
+                                   best_percentage: float = 0.1) -> List[str]:
+    """Names of the first ``int(len * 0.1)`` tracks of a popularity-sorted list
+    (``save_most_frequent_tracks_dict``, machine-learning/main.py:186-193; unused there)."""
+    k = int(len(sorted_most_frequent) * best_percentage)
+    return [t["track_name"] for t in sorted_most_frequent[:k]]
+
+
+def group_tracks_by_playlist_and_generate_homogeneous_data(t: TracksTable) -> Dict[str, List[str]]:
+    """``{pid: [track_name, ...]}`` with duplicates and row order kept, as polars'
+    ``group_by(pid).agg(list)`` (main.py:195-207).  The miners use the CSR form instead."""
+    pid, name = t.codes["pid"], t.codes["track_name"]
+    order = np.argsort(pid, kind="stable")
+    bounds = np.flatnonzero(np.diff(pid[order])) + 1
+    out: Dict[str, List[str]] = {}
+    for grp in np.split(order, bounds):
+        if len(grp):
+            out[t.uniques["pid"][int(pid[grp[0]])]] = [t.uniques["track_name"][int(c)] for c in name[grp]]
+    return out
+
+
+def group_tracks_by_playlist_and_generate_heterogeneous_data(t: TracksTable):
+    """Per-pid tables of the remaining columns (main.py:209-222, unused there; the reference's
+    version filters the whole frame once per pid, O(P*N)).  One stable sort here; returns
+    ``{pid: pandas.DataFrame}`` without the columns the reference drops
+    (track_uri, album_name, artist_uri)."""
+    import pandas as pd
+    keep = [c for c in t.codes if c not in ("pid", "track_uri", "album_name", "artist_uri")]
+    pid = t.codes["pid"]
+    order = np.argsort(pid, kind="stable")
+    bounds = np.flatnonzero(np.diff(pid[order])) + 1
+    out = {}
+    for grp in np.split(order, bounds):
+        if len(grp):
+            out[t.uniques["pid"][int(pid[grp[0]])]] = pd.DataFrame(
+                {c: [t.uniques[c][int(x)] for x in t.codes[c][grp]] for c in keep})
+    return out

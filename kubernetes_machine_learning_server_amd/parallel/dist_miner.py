@@ -21,6 +21,13 @@ no parallelism).  Here the mining step is split across the N GPUs of a node:
 
 With N == 1 every collective is skipped and the native single-GPU ``mine`` path runs.
 
+**Replicated mode** (``mode="replicate"``, the default for small data on N > 1 GPUs, e.g. the
+ds1/ds2 headline): the whole CSR is tiny (240k rows), so every rank holds all of it and runs the
+device-resident single-GPU prologue (supports, selection, bitmaps, level-2 gram — no
+collective), then expands only the root classes that a device-side snake partition of the
+estimated class costs assigns to it (``GpuMiner.mine_partition``).  One collective per step
+(the itemset-count all-reduce) instead of four plus host round trips.
+
 **Transaction-DP mode** (``mode="tx"``, the default for T >= 4M — BASELINE configs 3 and 5):
 replicating [F][T/64] bitmaps stops paying when T is large (100M transactions x 756 frequent
 items = 9.4 GB per GPU), so each rank keeps only its own shard's bitmap words and the C++
@@ -96,7 +103,11 @@ class _GpuOps:
         N = native.require_gpu()
         self.dev = torch.device("cuda", dm.device)
         self.comm = None
-        if dm.mode == "tx":
+        if dm.mode == "replicate":
+            torch.cuda.set_device(dm.device)
+            self.stream = None
+            self.g = N.GpuMiner(dm.device, arena_bytes, 0)
+        elif dm.mode == "tx":
             torch.cuda.set_device(dm.device)
             uid = [N.comm_unique_id() if dm.rank == 0 and dm.world > 1 else b"\0" * 128]
             if dm.world > 1:
@@ -119,6 +130,9 @@ class _GpuOps:
     def ctx(self):
         import contextlib
         return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
+    def mine_partition(self, dm: "DistMiner", download: bool):
+        return self.g.mine_partition(dm.min_support, dm.max_len, download, dm.rank, dm.world)
 
     def mine_txdp(self, dm: "DistMiner", download: bool):
         return self.g.mine_txdp(self.comm, dm.n_tx, dm.min_support, dm.max_len, download,
@@ -222,19 +236,26 @@ class DistMiner:
                  global_n_tx: Optional[int] = None, support_tiles: int = 4):
         """``global_n_tx`` given ⇒ (tx_ptr, items) already hold only this rank's shard (tx mode;
         large datasets are generated/loaded per shard).  ``mode``: "item" (replicated bitmaps,
-        item-sharded DFS), "tx" (transaction-DP, see module doc) or "auto"."""
+        item-sharded DFS), "replicate" (full data on every rank, device-side class partition),
+        "tx" (transaction-DP, see module doc) or "auto"."""
         self.world = dist.get_world_size() if (dist is not None and dist.is_initialized()) else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
         self.n_tx = int(global_n_tx) if global_n_tx is not None else len(tx_ptr) - 1
+        self.n_items = int(n_items)
         if mode == "auto":
-            mode = "tx" if (global_n_tx is not None or self.n_tx >= (4 << 20)) else "item"
+            if global_n_tx is not None or self.n_tx >= (4 << 20):
+                mode = "tx"
+            elif self.world > 1 and backend == "gpu" and self.n_items <= 16384 and not mfma \
+                    and not persistent and not force_protocol:
+                mode = "replicate"
+            else:
+                mode = "item"
         if mode == "tx" and backend != "gpu":
             raise ValueError("mode='tx' needs the GPU backend (native RCCL communicator)")
         if global_n_tx is not None and mode != "tx":
             raise ValueError("pre-sharded input (global_n_tx) requires mode='tx'")
         self.mode = mode
         self.support_tiles = int(support_tiles)
-        self.n_items = int(n_items)
         self.min_support = float(min_support)
         self.max_len = int(max_len)
         self.mfma = bool(mfma)
@@ -244,7 +265,10 @@ class DistMiner:
         self.persistent = bool(persistent)
         lo, hi, ts = shard_bounds(self.n_tx, self.world, self.rank)
         self.lo, self.hi, self.ts = lo, hi, ts
-        if global_n_tx is not None:  # already this rank's shard
+        if mode == "replicate":  # every rank mines from the full (small) dataset
+            sptr = np.ascontiguousarray(tx_ptr, dtype=np.int64)
+            sitems = np.ascontiguousarray(items, dtype=np.int32)
+        elif global_n_tx is not None:  # already this rank's shard
             sptr = np.ascontiguousarray(np.asarray(tx_ptr) - tx_ptr[0], dtype=np.int64)
             sitems = np.ascontiguousarray(items[tx_ptr[0]:tx_ptr[-1]], dtype=np.int32)
         else:
@@ -261,6 +285,15 @@ class DistMiner:
 
     # ------------------------------------------------------------------------------------
     def step(self, download: bool = True) -> Dict:
+        if self.mode == "replicate":
+            r = self.ops.mine_partition(self, download)
+            st = dict(r["stats"])
+            tot = torch.tensor([int(st["n_itemsets"])], dtype=torch.int64, device=self.ops.dev)
+            if self.world > 1:
+                dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+            st["global_itemsets"] = int(tot.item())
+            self.last = r
+            return {"stats": st, "trie": r}
         if self.mode == "tx":
             r = self.ops.mine_txdp(self, download and self.rank == 0)
             st = dict(r["stats"])

@@ -4,6 +4,8 @@ Every kernel is checked against an independent CPU reference of the same op: pai
 numpy one-hot Gram (fp64/int64), the full miner vs the C++ CPU miner (itself checked against
 the mlxtend-faithful oracle in test_miner_cpu.py), the serve kernel vs the C++ matcher.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -287,3 +289,77 @@ def test_gpu_groupby_equals_host(gpu_mod, n, n_keys, dedup):
     cp, ci = gpu_mod.group_to_csr(keys, vals, n_keys, dedup, True)
     np.testing.assert_array_equal(gp, cp)
     np.testing.assert_array_equal(gi, ci)
+
+
+def test_mine_partition_union_equals_full(gpu_mod):
+    """Replicated-data partition: the ranks' sub-tries (device-side snake partition of root
+    classes) are disjoint and their union is the full result."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    tx = generate("ds2_weak", seed=6)
+    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.03)
+    ref = _trie_dict(c)
+    for world in (2, 3, 8):
+        union, total = {}, 0
+        g = gpu_mod.GpuMiner(0, 1 << 31, 0)
+        g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+        for rank in range(world):
+            r = g.mine_partition(0.03, rank=rank, world=world)
+            assert r["stats"]["levels_path"] == "fused-resident-partition"
+            total += r["stats"]["n_itemsets"]
+            part = _trie_dict(r)
+            F = r["stats"]["n_frequent_items"]
+            mine = {k: v for k, v in part.items() if len(k) > 1}
+            assert not (set(mine) & set(union)), "ranks overlap"
+            union.update(part)
+        assert total == len(ref) and union == ref
+
+
+def test_split_k_grams_and_hash_supports(gpu_mod):
+    """Long rows (split-K gram, both kernels) and a 1M-item vocabulary (LDS-hash supports)."""
+    import torch
+    T, I = 700_000, 1_000_000
+    ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 2)
+    g = gpu_mod.GpuMiner(0, 1 << 31, torch.cuda.current_stream().cuda_stream or 0)
+    g.load_csr(ptr, items, I)
+    cnt = torch.zeros(I, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    g.item_support(cnt.data_ptr())
+    g.synchronize()
+    host = cnt.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(host, np.bincount(items, minlength=I))
+    F = g.select(host, T, 0.004)
+    assert 50 <= F <= 2000
+    Wp = g.words_local()
+    bm = torch.zeros((F, Wp), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    g.encode_bitmaps(bm.data_ptr(), Wp, 0)
+    ids, counts, _ = g.frequent()
+    rank_of = -np.ones(I, np.int64)
+    rank_of[ids] = np.arange(F)
+    rows = np.repeat(np.arange(T), np.diff(ptr))
+    rr = rank_of[items]
+    keep = rr >= 0
+    X = np.zeros((T, F), np.float32)
+    X[rows[keep], rr[keep]] = 1.0
+    ref = np.triu((X.T @ X).astype(np.int64), 1)
+    for mfma in (False, True):
+        gram = torch.zeros((F, F), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        g.pair_counts(bm.data_ptr(), Wp, gram.data_ptr(), mfma)
+        g.synchronize()
+        np.testing.assert_array_equal(np.triu(gram.cpu().numpy().astype(np.int64), 1), ref)
+
+
+def test_replicated_mode_multiprocess(gpu_mod):
+    """bench.py's N>1 path (DistMiner mode='replicate') in 3 real processes on one GPU."""
+    import subprocess
+    import sys
+    import pathlib
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = dict(os.environ, PYTHONPATH=str(root) + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=3", "--master-addr=127.0.0.1", "--master-port=29613",
+                        str(root / "scripts" / "replicate_check.py")],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=str(root))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "replicate_check OK" in r.stdout

@@ -195,3 +195,20 @@ def test_checkpoint_resume_after_crash(pvc, tmp_path, monkeypatch):
     s2 = job.run(clean)
     assert s2["resumed"] is False
     assert load(clean.pickles_folder / "recommendations.pickle") == rec_resumed
+
+
+def test_unused_reference_helpers(pvc):
+    """J16 parity: the reference's never-called helpers behave as written there."""
+    t = pp.clean_df(pp.read_tracks(str(pvc / "datasets" / "2023_spotify_ds1.csv"), verbose=False))
+    top = pp.get_most_frequent_tracks(t)
+    names = pp.save_most_frequent_tracks_dict(top)
+    assert names == [x["track_name"] for x in top[:int(len(top) * 0.1)]]
+    homo = pp.group_tracks_by_playlist_and_generate_homogeneous_data(t)
+    tx = pp.group_tracks_by_playlist(t, backend="cpu")
+    assert len(homo) == tx.n_tx
+    for pid, row in zip(tx.pids[:20], tx.as_lists()[:20]):
+        assert sorted(set(homo[pid])) == sorted(set(row))
+    het = pp.group_tracks_by_playlist_and_generate_heterogeneous_data(t)
+    first = next(iter(het.values()))
+    assert "track_name" in first.columns and "track_uri" not in first.columns
+    assert sum(len(v) for v in het.values()) == t.n_rows
