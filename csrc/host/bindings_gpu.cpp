@@ -145,6 +145,7 @@ void register_gpu_bindings(py::module_& m) {
       .def("words_local", &gpu::GpuMiner::words_local)
       .def("encode_bitmaps", &gpu::GpuMiner::encode_bitmaps, py::call_guard<py::gil_scoped_release>())
       .def("pair_counts", &gpu::GpuMiner::pair_counts, py::call_guard<py::gil_scoped_release>())
+      .def("bitgemm_rect", &gpu::GpuMiner::bitgemm_rect, py::call_guard<py::gil_scoped_release>())
       .def("mine_bitmaps", [](gpu::GpuMiner& g, uintptr_t bm, int64_t Wp, double ms, int max_len,
                               bool pairs_only, py::object owned, bool emit_level1, bool download,
                               bool gram, bool mfma, bool persistent) {

@@ -778,6 +778,13 @@ void GpuMiner::pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev
     kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp_total, F, (uint32_t*)out_dev, s);
 }
 
+void GpuMiner::bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp,
+                            uintptr_t C, int64_t ldc) {
+  KMLS_HIP(hipSetDevice(device_));
+  kern::bitgemm_rect((const uint64_t*)A, Fa, (const uint64_t*)B, Fb, Wp, (uint32_t*)C, ldc,
+                     (hipStream_t)stream_);
+}
+
 GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineConfig& cfg,
                                      const uint8_t* owned_mask, bool emit_level1,
                                      bool download) {

@@ -143,6 +143,9 @@ class GpuMiner {
   // count[F][F] (row-major, only i<j valid) via the bit-GEMM kernels. Used by the rule-map
   // fast path and by the multi-GPU pair all-reduce.
   void pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev, bool use_mfma);
+  // C[Fa][ldc] += popcount(A_i & B_j) over Wp words (ring-pass pair counting)
+  void bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp, uintptr_t C,
+                    int64_t ldc);
 
   uintptr_t stream() const { return (uintptr_t)stream_; }
   void synchronize();

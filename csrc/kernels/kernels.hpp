@@ -55,6 +55,9 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
 // same with F read from the device (grid and row stride sized for F_max)
 void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, int64_t F_max,
                             uint32_t* out, hipStream_t s);
+// C[i][j] += popcount(A_i & B_j) (rectangular, accumulating; C zeroed by the caller once)
+void bitgemm_rect(const uint64_t* A, int64_t Fa, const uint64_t* B, int64_t Fb, int64_t Wp,
+                  uint32_t* C, int64_t ldc, hipStream_t s);
 // dense Gram (F x F, i<j valid) → per-candidate counts in (a, b) row-major candidate order
 void gram_to_cand(const uint32_t* gram, int64_t F, const int64_t* cand_off, int64_t c0, int64_t c1,
                   uint32_t* cnt, hipStream_t s);

@@ -305,6 +305,55 @@ __global__ __launch_bounds__(kBlock) void k_pair_gram_popcount(
   }
 }
 
+// Rectangular bit-GEMM C[i][j] += popcount(A_i & B_j) over Wp words (the ring-pass pair
+// counter's per-step product of the owned rows against a rotating transaction block).  Same
+// LDS tiling as the square kernel; split-K over blockIdx.y with integer atomics.
+__global__ __launch_bounds__(kBlock) void k_bitgemm_rect(const unsigned long long* __restrict__ A,
+                                                         int64_t Fa, const unsigned long long* __restrict__ B,
+                                                         int64_t Fb, int64_t Wp, int64_t ntb,
+                                                         uint32_t* __restrict__ C, int64_t ldc) {
+  __shared__ unsigned long long As[kGK][kGT + 2];
+  __shared__ unsigned long long Bs[kGK][kGT + 2];
+  const int64_t ti = blockIdx.x / ntb, tj = blockIdx.x % ntb;
+  const int64_t r0 = ti * kGT, q0 = tj * kGT;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  uint32_t acc[4][4] = {};
+  const int lr = threadIdx.x >> 2, lk = (threadIdx.x & 3) * 4;
+  const int64_t slice = (((Wp + gridDim.y - 1) / gridDim.y) + kGK - 1) / kGK * kGK;
+  const int64_t kb = (int64_t)blockIdx.y * slice, ke = min(Wp, kb + slice);
+  for (int64_t k0 = kb; k0 < ke; k0 += kGK) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t kk = k0 + lk + i;
+      const int64_t ra = r0 + lr, rb = q0 + lr;
+      As[lk + i][lr] = (ra < Fa && kk < ke) ? A[ra * Wp + kk] : 0ull;
+      Bs[lk + i][lr] = (rb < Fb && kk < ke) ? B[rb * Wp + kk] : 0ull;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < kGK; ++k) {
+      unsigned long long a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { a[i] = As[k][ty * 4 + i]; b[i] = Bs[k][tx * 4 + i]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += (uint32_t)__popcll(a[i] & b[j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t r = r0 + ty * 4 + i;
+    if (r >= Fa) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t q = q0 + tx * 4 + j;
+      if (q < Fb && acc[i][j]) atomicAdd(&C[r * ldc + q], acc[i][j]);
+    }
+  }
+}
+
 // gram (dense F x F, i<j valid) → per-candidate counts in (a, b) row-major candidate order
 __global__ void k_gram_to_cand(const uint32_t* __restrict__ gram, int64_t F,
                                const int64_t* __restrict__ cand_off, int64_t c0, int64_t c1,
@@ -492,6 +541,18 @@ void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, i
   const int64_t ks = std::max<int64_t>(1, std::min<int64_t>((1024 + blocks - 1) / blocks, Wp / 1024));
   hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks, (unsigned)ks), dim3(kBlock), 0, s,
                      (const unsigned long long*)bm, Wp, F_max, nt, out, F_max, dF);
+  KMLS_HIP(hipGetLastError());
+}
+
+void bitgemm_rect(const uint64_t* A, int64_t Fa, const uint64_t* B, int64_t Fb, int64_t Wp,
+                  uint32_t* C, int64_t ldc, hipStream_t s) {
+  if (Fa <= 0 || Fb <= 0 || Wp <= 0) return;
+  const int64_t nta = (Fa + kGT - 1) / kGT, ntb = (Fb + kGT - 1) / kGT;
+  const int64_t blocks = nta * ntb;
+  const int64_t ks = std::max<int64_t>(1, std::min<int64_t>((1024 + blocks - 1) / blocks, Wp / 1024));
+  hipLaunchKernelGGL(k_bitgemm_rect, dim3((unsigned)blocks, (unsigned)ks), dim3(kBlock), 0, s,
+                     (const unsigned long long*)A, Fa, (const unsigned long long*)B, Fb, Wp, ntb, C,
+                     ldc);
   KMLS_HIP(hipGetLastError());
 }
 

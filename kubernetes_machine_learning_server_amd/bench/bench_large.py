@@ -38,6 +38,8 @@ def main(argv=None) -> int:
     ap.add_argument("--rules", action="store_true", help="also time rules + index + hot reload")
     ap.add_argument("--min-confidence", type=float, default=0.3)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--pairs", default="", choices=["", "allreduce", "reduce_scatter", "alltoall", "ring"],
+                    help="pairs-only pipeline (RULES_MODE=pairs) with this distributed strategy")
     args = ap.parse_args(argv)
 
     import numpy as np
@@ -58,7 +60,9 @@ def main(argv=None) -> int:
     shape = SHAPES[args.shape]
     T = args.n_tx or shape.n_tx
     t0 = time.perf_counter()
-    if args.mode == "item":
+    if args.pairs:
+        args.mode = "item"  # transaction-sharded protocol; the shard is generated per rank
+    if args.mode == "item" and not args.pairs:
         ptr, items = N.synth_transactions(T, shape.n_items, shape.mean_len, shape.n_genres,
                                           shape.genre_affinity, 0.85, args.seed)
         kw = {}
@@ -80,6 +84,29 @@ def main(argv=None) -> int:
             dist.barrier()
             torch.cuda.synchronize()
 
+    if args.pairs:
+        for _ in range(args.warmup):
+            dm.pair_rows(args.pairs)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ids, r0, r1, rows = dm.pair_rows(args.pairs)
+        dm.synchronize()
+        barrier()
+        ms = (time.perf_counter() - t0) * 1000.0 / max(1, args.steps)
+        if world > 1:
+            t = torch.tensor([ms], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms = float(t.item())
+        if rank == 0:
+            print(json.dumps({"bench": "large-pairs", "shape": args.shape, "n_tx": T,
+                              "n_gpus": world, "pairs_mode": args.pairs,
+                              "n_frequent_items": int(len(ids)), "rows_owned": int(r1 - r0),
+                              "ms_per_step": round(ms, 3),
+                              "tx_per_s": round(T / (ms / 1000.0), 1)}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
     r = None
     for _ in range(args.warmup):
         r = dm.step(download=True)

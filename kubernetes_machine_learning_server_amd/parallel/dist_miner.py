@@ -115,7 +115,7 @@ class _GpuOps:
             self.comm = N.Comm(dm.rank, dm.world, uid[0], dm.device)
             self.stream = None
             self.g = N.GpuMiner(dm.device, arena_bytes, 0)
-        elif dm.world > 1 or dm.force_protocol:
+        elif dm.world > 1 or dm.force_protocol or dm.mode == "item":
             # every torch op of the protocol (allocations, fills, collectives) and every native
             # kernel run on ONE stream, so they are ordered without extra synchronisation
             torch.cuda.set_device(dm.device)
@@ -252,8 +252,8 @@ class DistMiner:
                 mode = "item"
         if mode == "tx" and backend != "gpu":
             raise ValueError("mode='tx' needs the GPU backend (native RCCL communicator)")
-        if global_n_tx is not None and mode != "tx":
-            raise ValueError("pre-sharded input (global_n_tx) requires mode='tx'")
+        if global_n_tx is not None and mode not in ("tx", "item"):
+            raise ValueError("pre-sharded input (global_n_tx) requires mode 'tx' or 'item'")
         self.mode = mode
         self.support_tiles = int(support_tiles)
         self.min_support = float(min_support)
@@ -308,6 +308,28 @@ class DistMiner:
             self.last = r
             return {"stats": st, "trie": r}
         return self._step_protocol(download)
+
+    def pair_rows(self, mode: str = "reduce_scatter"):
+        """Pairs-only step (``RULES_MODE=pairs``: the reference's rule map is the pair-support
+        matrix): tx-sharded supports + all-reduce, selection, shard bitmaps, then one of the
+        ``parallel.pairs`` strategies.  Returns (ids, row0, row1, rows) — this rank's owned rows
+        of the symmetric support matrix over the frequent items ``ids`` (Eclat order)."""
+        from .pairs import PairCounter
+        if self.mode != "item":
+            raise ValueError("pair_rows runs on the transaction-sharded protocol (mode='item')")
+        ops = self.ops
+        with ops.ctx():
+            counts = ops.supports()
+            if self.world > 1:
+                dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+            host_counts = counts.cpu().numpy().view(np.uint32)
+            F, ids, fcounts, minsup = ops.select(host_counts, self.n_tx, self.min_support)
+            ops.sel = (ids, fcounts, minsup)
+            X = ops.encode(F, self.ts // 64)
+            r0, r1, rows = PairCounter(getattr(ops, "g", None)).count(X, mode)
+            if hasattr(rows, "cpu"):
+                rows = rows.cpu()
+        return ids, r0, r1, np.asarray(rows)
 
     def _step_protocol(self, download: bool) -> Dict:
         ops = self.ops

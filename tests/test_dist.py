@@ -84,3 +84,49 @@ def test_shard_bounds_and_lpt():
     loads = [cost[own == r].sum() for r in range(3)]
     assert max(loads) - min(loads) <= cost.max()  # greedy dealing bound
     assert (lpt_partition(cost, 3) == own).all()  # deterministic across ranks
+
+
+def _pairs_worker(rank, world, port, mode, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), OMP_NUM_THREADS="1")
+    import torch.distributed as dist
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tx = generate("ds2_weak", seed=4)
+        dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, 0.03, backend="cpu", mode="item")
+        ids, r0, r1, rows = dm.pair_rows(mode)
+        out_q.put((rank, np.asarray(ids), r0, r1, rows))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["allreduce", "reduce_scatter", "alltoall", "ring"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_pair_strategies_equal_full_gram(world, mode):
+    """DP all-reduce, reduce-scatter (item ownership), all-to-all (Ulysses analog)
+    and the ring pass (context-parallel analog) all produce the owned row blocks of XᵀX."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pairs_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    tx = generate("ds2_weak", seed=4)
+    ids = parts[0][1]
+    X = np.zeros((tx.n_tx, tx.n_items), np.float64)
+    for t in range(tx.n_tx):
+        X[t, tx.items[tx.tx_ptr[t]:tx.tx_ptr[t + 1]]] = 1.0
+    G = (X[:, ids].T @ X[:, ids]).astype(np.int64)
+    covered = 0
+    for rank, pids, r0, r1, rows in sorted(parts, key=lambda p: p[0]):
+        np.testing.assert_array_equal(pids, ids)
+        np.testing.assert_array_equal(rows.astype(np.int64), G[r0:r1])
+        covered += r1 - r0
+    assert covered == len(ids)

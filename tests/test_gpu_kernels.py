@@ -363,3 +363,19 @@ def test_replicated_mode_multiprocess(gpu_mod):
                        capture_output=True, text=True, timeout=600, env=env, cwd=str(root))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "replicate_check OK" in r.stdout
+
+
+@pytest.mark.parametrize("mode", ["allreduce", "reduce_scatter", "alltoall", "ring"])
+def test_pair_rows_gpu_world1(gpu_mod, mode):
+    """Pairs-only protocol on the GPU path (rectangular HIP bit-GEMM on the protocol stream)."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+    tx = generate("ds2_weak", seed=4)
+    dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, 0.03, mode="item", force_protocol=True)
+    ids, r0, r1, rows = dm.pair_rows(mode)
+    X = np.zeros((tx.n_tx, tx.n_items), np.float64)
+    for t in range(tx.n_tx):
+        X[t, tx.items[tx.tx_ptr[t]:tx.tx_ptr[t + 1]]] = 1.0
+    G = (X[:, ids].T @ X[:, ids]).astype(np.int64)
+    assert (r0, r1) == (0, len(ids))
+    np.testing.assert_array_equal(rows.astype(np.int64), G)
