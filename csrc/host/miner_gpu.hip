@@ -462,7 +462,7 @@ struct MineRun {
     h_ctl->status_cap = (unsigned long long)ob->status_cap;
     KMLS_HIP(hipMemcpyAsync(d_desc, h_desc, stage_bytes - (size_t)(Fr + 1) * 8, hipMemcpyHostToDevice, s));
     KMLS_HIP(hipMemcpyAsync(d_off, h_off, (size_t)(Fr + 1) * 8, hipMemcpyHostToDevice, s));
-    if (!levels_loop(d_desc, d_ctl, out_cap, false)) {
+    if (!levels_loop(d_desc, d_ctl, out_cap)) {
       arena->pop_to(mark);
       return false;
     }
@@ -471,29 +471,22 @@ struct MineRun {
   }
 
   // The level loop shared by the host- and device-prepared fused paths: count level 1 (root),
-  // then scan+count per level, one host sync per batch of levels.  copy_level0: also stream the
-  // level-1 trie nodes (written on the device by the resident prologue).
-  bool levels_loop(kern::FLevel* d_desc, kern::FCtl* d_ctl, int64_t out_cap, bool copy_level0) {
+  // then scan+count per level, one host sync per batch of levels.  Streamed download: the count
+  // kernels write every survivor straight into the pinned host arrays as well (no copy-out
+  // kernel, no cross-stream event per level); level-1 nodes are written by the resident
+  // prologue's root setup or were queued by stream_out() on the host-prepared path.
+  bool levels_loop(kern::FLevel* d_desc, kern::FCtl* d_ctl, int64_t out_cap) {
     constexpr int kMaxLv = 64;
     const int grid = kern::level_grid(n_cus);
-    kern::CopyOutArgs co{out_parent.p, out_item.p, out_count.p, out_depth.p,
-                         h_parent, h_item, h_count, h_depth, stream_dl ? host_cap : 0};
     auto count_level = [&](int L) {
       kern::LevelCountArgs a{Wp, minsup, L == 1 ? gram : nullptr, F, d_ids, out_parent.p,
-                             out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1)};
+                             out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1),
+                             stream_dl ? h_parent : nullptr, stream_dl ? h_item : nullptr,
+                             stream_dl ? h_count : nullptr, stream_dl ? h_depth : nullptr,
+                             stream_dl ? host_cap : 0};
       kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a, grid, s);
-      if (stream_dl) {
-        KMLS_HIP(hipEventRecord(ob->ev, s));
-        KMLS_HIP(hipStreamWaitEvent(ob->copy_s, ob->ev, 0));
-        kern::level_copyout(&d_desc[L], &d_desc[L + 1], d_ctl, co, ob->copy_s);
-      }
     };
     const int L_allowed = std::min(kMaxLv - 2, max_len ? max_len - 1 : kMaxLv - 2);
-    if (copy_level0 && stream_dl) {
-      KMLS_HIP(hipEventRecord(ob->ev, s));
-      KMLS_HIP(hipStreamWaitEvent(ob->copy_s, ob->ev, 0));
-      kern::level_copyout(&d_desc[0], &d_desc[1], d_ctl, co, ob->copy_s);
-    }
     count_level(1);
     int last = 1;
     int target = std::min(L_allowed, std::max(ob->depth_hint, 2));
@@ -675,6 +668,8 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
   KMLS_HIP(hipHostMalloc((void**)&abort_host_, 64, hipHostMallocMapped));
   *abort_host_ = 0u;
   KMLS_HIP(hipHostGetDevicePointer((void**)&abort_dev_, abort_host_, 0));
+  KMLS_HIP(hipHostMalloc((void**)&h_scalar_, 64));
+  KMLS_HIP(hipMalloc((void**)&d_pair_, 2 * sizeof(uint64_t)));
   hipDeviceProp_t prop;
   KMLS_HIP(hipGetDeviceProperties(&prop, device));
   n_cus_ = std::max(1, prop.multiProcessorCount);
@@ -688,6 +683,8 @@ GpuMiner::~GpuMiner() {
   if (d_ids_) (void)hipFree(d_ids_);
   if (d_own_bm_) (void)hipFree(d_own_bm_);
   if (abort_host_) (void)hipHostFree(abort_host_);
+  if (h_scalar_) (void)hipHostFree(h_scalar_);
+  if (d_pair_) (void)hipFree(d_pair_);
   out_.reset();
   arena_.reset();
   if (own_stream_) (void)hipStreamDestroy((hipStream_t)stream_);
@@ -813,8 +810,8 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   run.max_len = cfg.pairs_only ? 2 : cfg.max_len;
   run.d_ids = d_ids_;
   run.F = F;
-  KMLS_HIP(hipHostMalloc((void**)&run.h_scalar, 64));
-  KMLS_HIP(hipMalloc((void**)&run.d_pair, 2 * sizeof(uint64_t)));
+  run.h_scalar = h_scalar_;  // persistent: a per-call hipHostFree costs ~200 us (it syncs)
+  run.d_pair = d_pair_;
   // level-1 nodes: gid = Eclat rank
   run.ensure_out(std::max<int64_t>({F * 8, (int64_t)1 << 16, last_nodes_ + (last_nodes_ >> 3)}));
   if (download) {  // pinned host arrays sized from the previous trie; levels stream into them
@@ -903,10 +900,6 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   }
   arena_->pop_to(mark);
   KMLS_HIP(hipStreamSynchronize(out_->copy_s));
-  (void)hipHostFree(run.h_scalar);
-  run.h_scalar = nullptr;
-  (void)hipFree(run.d_pair);
-  run.d_pair = nullptr;
   res.h_parent.reset();
   res.h_item.reset();
   res.h_count.reset();
@@ -944,8 +937,6 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   res.stats.max_depth = F ? run.max_depth : 0;
   res.arena_high_water = (int64_t)arena_->high_water();
   arena_->pop_to(mark);
-  (void)hipHostFree(run.h_scalar);
-  (void)hipFree(run.d_pair);
   return res;
 }
 
@@ -965,9 +956,10 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   KMLS_HIP(hipEventRecord(e0.e, s));
   const size_t mark = arena_->mark();
   uint32_t* d_cnt = (uint32_t*)arena_->push((size_t)I * 4);
-  int32_t* d_rank_of = (int32_t*)arena_->push((size_t)I * 4);
-  int32_t* d_ids = (int32_t*)arena_->push((size_t)I * 4);
-  uint32_t* d_fcnt = (uint32_t*)arena_->push((size_t)I * 4);
+  const int64_t tab_stride = (I + 63) & ~(int64_t)63;  // ids | counts | rank_of, one D2H copy
+  int32_t* d_ids = (int32_t*)arena_->push((size_t)tab_stride * 12);
+  uint32_t* d_fcnt = (uint32_t*)(d_ids + tab_stride);
+  int32_t* d_rank_of = d_ids + 2 * tab_stride;
   uint32_t* d_gram = (uint32_t*)arena_->push((size_t)I * I * 4);
   int32_t* d_rrank = (int32_t*)arena_->push((size_t)I * 4);
   int64_t* d_rgid = (int64_t*)arena_->push((size_t)I * 8);
@@ -993,8 +985,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   run.pinned = pinned_;
   run.n_cus = n_cus_;
   run.persistent = false;
-  KMLS_HIP(hipHostMalloc((void**)&run.h_scalar, 64));
-  struct ScalarGuard { int64_t*& p; ~ScalarGuard() { if (p) (void)hipHostFree(p); p = nullptr; } } sgd{run.h_scalar};
+  run.h_scalar = h_scalar_;
   const int64_t cap_nodes = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 16ll << 20);
   run.ensure_out(cap_nodes);
   const int64_t out_cap = std::min<int64_t>({run.out_parent.cap, run.out_item.cap, run.out_count.cap, run.out_depth.cap});
@@ -1043,15 +1034,17 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   }
   kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
                          run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
-                         d_prank, part_world, part_rank};
+                         d_prank, part_world, part_rank,
+                         run.stream_dl ? run.h_parent : nullptr, run.stream_dl ? run.h_item : nullptr,
+                         run.stream_dl ? run.h_count : nullptr, run.stream_dl ? run.h_depth : nullptr,
+                         run.stream_dl ? run.host_cap : 0};
   kern::level_root_setup(d_desc, d_ctl, ra, s);
-  // frequent-item tables for the frequent() API: staged to pinned memory while levels run
-  std::shared_ptr<void> fstage = pinned_->get((size_t)I * 12);
-  KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)I * 4, hipMemcpyDeviceToHost, s));
-  KMLS_HIP(hipMemcpyAsync((char*)fstage.get() + I * 4, d_fcnt, (size_t)I * 4, hipMemcpyDeviceToHost, s));
-  KMLS_HIP(hipMemcpyAsync((char*)fstage.get() + I * 8, d_rank_of, (size_t)I * 4, hipMemcpyDeviceToHost, s));
+  // frequent-item tables for the frequent() API (ids | counts | rank_of, one contiguous block):
+  // staged to pinned memory while the levels run
+  std::shared_ptr<void> fstage = pinned_->get((size_t)tab_stride * 12);
+  KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));
   KMLS_HIP(hipEventRecord(e1.e, s));
-  const bool ok = run.levels_loop(d_desc, d_ctl, out_cap, true);
+  const bool ok = run.levels_loop(d_desc, d_ctl, out_cap);
   if (!ok) {
     fused_fallback_ = run.fallback_reason;
     arena_->pop_to(mark);
@@ -1063,8 +1056,8 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   {
     const int32_t* hs = (const int32_t*)fstage.get();
     fi_.ids.assign(hs, hs + F);
-    fi_.counts.assign((const uint32_t*)(hs + I), (const uint32_t*)(hs + I) + F);
-    fi_.rank_of.assign(hs + 2 * I, hs + 3 * I);
+    fi_.counts.assign((const uint32_t*)(hs + tab_stride), (const uint32_t*)(hs + tab_stride) + F);
+    fi_.rank_of.assign(hs + 2 * tab_stride, hs + 2 * tab_stride + I);
   }
   fi_.minsup2 = run.minsup;
   global_n_tx_ = n_tx_;

@@ -169,6 +169,8 @@ class GpuMiner {
   int64_t rows_hint_ = 0;  // learned persistent-DFS pool capacity
   unsigned int* abort_host_ = nullptr;       // watchdog flag (pinned, device-mapped)
   const unsigned int* abort_dev_ = nullptr;
+  int64_t* h_scalar_ = nullptr;   // pinned readback scratch (allocated once: hipHostFree syncs)
+  uint64_t* d_pair_ = nullptr;    // device [survivors, next-level candidates]
   int n_cus_ = 256;
   bool mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res, int part_rank,
                      int part_world);

@@ -95,12 +95,8 @@ struct LevelCountArgs {
   uint32_t* out_count;
   uint8_t* out_depth;
   uint8_t child_depth;
-};
-struct CopyOutArgs {
-  const int64_t* d_parent;
-  const int32_t* d_item;
-  const uint32_t* d_count;
-  const uint8_t* d_depth;
+  // streamed download: survivors are also written straight into these pinned host arrays
+  // (nullptr = off); a node >= host_cap sets FCtl::dl_overflow (host copies at the end)
   int64_t* h_parent;
   int32_t* h_item;
   uint32_t* h_count;
@@ -131,6 +127,12 @@ struct RootSetupArgs {
   const int32_t* prank;  // partition rank of each root class (world > 1), see level_partition
   int world;
   int my_rank;
+  // level-1 nodes also go straight to the pinned host arrays (nullptr = off)
+  int64_t* h_parent;
+  int32_t* h_item;
+  uint32_t* h_count;
+  uint8_t* h_depth;
+  int64_t host_cap;
 };
 void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s);
 // rank root classes by estimated cost (n_a^2 + 1 from the gram, desc) for the snake partition
@@ -143,8 +145,6 @@ void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long lon
                 unsigned epoch, int64_t Wp, int64_t out_cap, int grid, hipStream_t s);
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
                  const LevelCountArgs& a, int grid, hipStream_t s);
-void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const CopyOutArgs& a,
-                   hipStream_t s);
 
 // ---- persistent DFS (dfs_persistent.hip) ----
 struct DfsTask {

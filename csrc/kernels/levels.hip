@@ -16,7 +16,9 @@
 //                 the same kernel.  This fuses the chunked path's count, flag scan (2 rocprim
 //                 kernels), child_totals and materialise launches, and reads each parent row
 //                 pair once into L1/L2 for both phases.
-//   k_level_copyout: streams a finished level of the trie to pinned host memory (side stream).
+//   Streamed download: the materialise phase also writes each survivor's trie node straight
+//                 into pinned host memory (coalesced PCIe writes), so finished levels reach the
+//                 host while deeper levels run, with no copy kernel or cross-stream event.
 //
 // Look-back status words pack (epoch:24 | flag:2 | value:38) in one 64-bit word, so publishing
 // needs no fence, and the per-call epoch makes re-zeroing the status array unnecessary.
@@ -384,10 +386,23 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
         crank[s] = rb;
         cgid[s] = node;
         cprow[s] = (int32_t)a;
-        A.out_parent[node] = gid[a];
-        A.out_item[node] = A.ids[rb];
-        A.out_count[node] = s_cnt[threadIdx.x];
+        const int64_t par = gid[a];
+        const int32_t it = A.ids[rb];
+        const uint32_t cnt = s_cnt[threadIdx.x];
+        A.out_parent[node] = par;
+        A.out_item[node] = it;
+        A.out_count[node] = cnt;
         A.out_depth[node] = A.child_depth;
+        if (A.h_item) {  // streamed download: consecutive survivors → coalesced PCIe writes
+          if (node < A.host_cap) {
+            A.h_parent[node] = par;
+            A.h_item[node] = it;
+            A.h_count[node] = cnt;
+            A.h_depth[node] = A.child_depth;
+          } else {
+            ctl->dl_overflow = 1u;
+          }
+        }
       }
     }
     // ---- phase 3: survivors' bitmaps (team per survivor) ----
@@ -413,27 +428,6 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
       atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
     }
     __syncthreads();
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_level_copyout(const FLevel* __restrict__ lv,
-                                                          const FLevel* __restrict__ nx,
-                                                          FCtl* ctl, CopyOutArgs A) {
-  if (ctl->overflow) return;
-  const int64_t base = lv->child_base;
-  const int64_t S = nx->n_rows;
-  if (S <= 0) return;
-  if (base + S > A.host_cap) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&ctl->dl_overflow, 1u);
-    return;
-  }
-  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < base + S; i += nthr) {
-    A.h_parent[i] = A.d_parent[i];
-    A.h_item[i] = A.d_item[i];
-    A.h_count[i] = A.d_count[i];
-    A.h_depth[i] = A.d_depth[i];
   }
 }
 
@@ -602,6 +596,16 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     a.out_item[i] = a.ids[i];
     a.out_count[i] = a.fcounts[i];
     a.out_depth[i] = 1;
+    if (a.h_item) {
+      if (i < a.host_cap) {
+        a.h_parent[i] = -1;
+        a.h_item[i] = a.ids[i];
+        a.h_count[i] = a.fcounts[i];
+        a.h_depth[i] = 1;
+      } else {
+        ctl->dl_overflow = 1u;
+      }
+    }
   }
 }
 
@@ -634,12 +638,6 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
     case 32: hipLaunchKernelGGL(k_level_count<32>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
     default: hipLaunchKernelGGL(k_level_count<64>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
   }
-  KMLS_HIP(hipGetLastError());
-}
-
-void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const CopyOutArgs& a,
-                   hipStream_t s) {
-  hipLaunchKernelGGL(k_level_copyout, dim3(64), dim3(kBlock), 0, s, lv, nx, ctl, a);
   KMLS_HIP(hipGetLastError());
 }
 
