@@ -27,9 +27,13 @@ py::array_t<T> pinned_array(const std::shared_ptr<void>& buf, int64_t n) {
 
 py::dict result_to_dict(gpu::GpuMineResult&& r) {
   py::dict d;
-  d["parent"] = pinned_array<int64_t>(r.h_parent, r.n_nodes);
-  d["item"] = pinned_array<int32_t>(r.h_item, r.n_nodes);
-  d["count"] = pinned_array<uint32_t>(r.h_count, r.n_nodes);
+  // element widths follow the download format (compact on the device-resident path)
+  if (r.par_w == 4) d["parent"] = pinned_array<int32_t>(r.h_parent, r.n_nodes);
+  else d["parent"] = pinned_array<int64_t>(r.h_parent, r.n_nodes);
+  if (r.item_w == 2) d["item"] = pinned_array<uint16_t>(r.h_item, r.n_nodes);
+  else d["item"] = pinned_array<int32_t>(r.h_item, r.n_nodes);
+  if (r.cnt_w == 2) d["count"] = pinned_array<uint16_t>(r.h_count, r.n_nodes);
+  else d["count"] = pinned_array<uint32_t>(r.h_count, r.n_nodes);
   d["depth"] = pinned_array<uint8_t>(r.h_depth, r.n_nodes);
   py::dict s;
   s["n_frequent_items"] = r.stats.n_frequent_items;

@@ -142,6 +142,7 @@ struct OutBufs {
   hipEvent_t ev = nullptr;
   // fused level path (levels.hip): look-back status words (epoch-tagged, zeroed once)
   unsigned long long* status = nullptr;
+  int32_t* tile_row = nullptr;   // [status_cap] count tile → first row (written by level_scan)
   int64_t status_cap = 1 << 20;  // tiles per launch (256M candidates / 2G rows)
   unsigned epoch = 0;
   int depth_hint = 6;            // levels enqueued before the first completion check
@@ -150,6 +151,7 @@ struct OutBufs {
     KMLS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     KMLS_HIP(hipMalloc((void**)&status, (size_t)status_cap * sizeof(unsigned long long)));
     KMLS_HIP(hipMemset(status, 0, (size_t)status_cap * sizeof(unsigned long long)));
+    KMLS_HIP(hipMalloc((void**)&tile_row, (size_t)status_cap * sizeof(int32_t)));
   }
   unsigned next_epoch(hipStream_t s) {
     if (++epoch >= (1u << 24) - 1) {  // 24-bit tag wraps: forget every old word
@@ -161,6 +163,7 @@ struct OutBufs {
   ~OutBufs() {
     if (copy_s) (void)hipStreamSynchronize(copy_s);
     if (status) (void)hipFree(status);
+    if (tile_row) (void)hipFree(tile_row);
     if (ev) (void)hipEventDestroy(ev);
     if (copy_s) (void)hipStreamDestroy(copy_s);
   }
@@ -203,10 +206,7 @@ struct MineRun {
   // streamed download: [0, streamed) already queued to the pinned host arrays on ob->copy_s
   bool stream_dl = false;
   int64_t host_cap = 0, streamed = 0;
-  int64_t* h_parent = nullptr;
-  int32_t* h_item = nullptr;
-  uint32_t* h_count = nullptr;
-  uint8_t* h_depth = nullptr;
+  kern::HostTrie ht{};  // pinned host arrays + element widths (stream_out needs full widths)
 
   explicit MineRun(OutBufs* o)
       : ob(o), out_parent(o->parent), out_item(o->item), out_count(o->count), out_depth(o->depth) {}
@@ -237,13 +237,15 @@ struct MineRun {
       stream_dl = false;
       return;
     }
+    if (ht.par_w != 8 || ht.item_w != 4 || ht.cnt_w != 4)
+      throw std::logic_error("stream_out: compact host trie on a memcpy download path");
     const int64_t a = streamed, n = out_size - streamed;
     KMLS_HIP(hipEventRecord(ob->ev, s));
     KMLS_HIP(hipStreamWaitEvent(ob->copy_s, ob->ev, 0));
-    KMLS_HIP(hipMemcpyAsync(h_parent + a, out_parent.p + a, n * sizeof(int64_t), hipMemcpyDeviceToHost, ob->copy_s));
-    KMLS_HIP(hipMemcpyAsync(h_item + a, out_item.p + a, n * sizeof(int32_t), hipMemcpyDeviceToHost, ob->copy_s));
-    KMLS_HIP(hipMemcpyAsync(h_count + a, out_count.p + a, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ob->copy_s));
-    KMLS_HIP(hipMemcpyAsync(h_depth + a, out_depth.p + a, n * sizeof(uint8_t), hipMemcpyDeviceToHost, ob->copy_s));
+    KMLS_HIP(hipMemcpyAsync((int64_t*)ht.parent + a, out_parent.p + a, n * sizeof(int64_t), hipMemcpyDeviceToHost, ob->copy_s));
+    KMLS_HIP(hipMemcpyAsync((int32_t*)ht.item + a, out_item.p + a, n * sizeof(int32_t), hipMemcpyDeviceToHost, ob->copy_s));
+    KMLS_HIP(hipMemcpyAsync((uint32_t*)ht.count + a, out_count.p + a, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ob->copy_s));
+    KMLS_HIP(hipMemcpyAsync(ht.depth + a, out_depth.p + a, n * sizeof(uint8_t), hipMemcpyDeviceToHost, ob->copy_s));
     streamed = out_size;
   }
 
@@ -481,10 +483,9 @@ struct MineRun {
     auto count_level = [&](int L) {
       kern::LevelCountArgs a{Wp, minsup, L == 1 ? gram : nullptr, F, d_ids, out_parent.p,
                              out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1),
-                             stream_dl ? h_parent : nullptr, stream_dl ? h_item : nullptr,
-                             stream_dl ? h_count : nullptr, stream_dl ? h_depth : nullptr,
-                             stream_dl ? host_cap : 0};
-      kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a, grid, s);
+                             stream_dl ? ht : kern::HostTrie{}};
+      kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a,
+                        L == 1 ? nullptr : ob->tile_row, grid, s);
     };
     const int L_allowed = std::min(kMaxLv - 2, max_len ? max_len - 1 : kMaxLv - 2);
     count_level(1);
@@ -497,7 +498,7 @@ struct MineRun {
     while (true) {
       for (int L = last + 1; L <= target; ++L) {
         kern::level_scan(&d_desc[L - 1], &d_desc[L], &d_desc[L + 1], d_ctl, ob->status,
-                         ob->next_epoch(s), Wp, out_cap, grid, s);
+                         ob->next_epoch(s), Wp, out_cap, ob->tile_row, grid, s);
         count_level(L);
         last = L;
       }
@@ -820,10 +821,8 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     res.h_item = pinned_->get((size_t)run.host_cap * sizeof(int32_t));
     res.h_count = pinned_->get((size_t)run.host_cap * sizeof(uint32_t));
     res.h_depth = pinned_->get((size_t)run.host_cap * sizeof(uint8_t));
-    run.h_parent = (int64_t*)res.h_parent.get();
-    run.h_item = (int32_t*)res.h_item.get();
-    run.h_count = (uint32_t*)res.h_count.get();
-    run.h_depth = (uint8_t*)res.h_depth.get();
+    run.ht = kern::HostTrie{res.h_parent.get(), res.h_item.get(), res.h_count.get(),
+                            (uint8_t*)res.h_depth.get(), run.host_cap, 8, 4, 4};
     run.stream_dl = true;
   }
   {
@@ -991,14 +990,24 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   const int64_t out_cap = std::min<int64_t>({run.out_parent.cap, run.out_item.cap, run.out_count.cap, run.out_depth.cap});
   if (download) {
     run.host_cap = std::max<int64_t>({I * 8, (int64_t)1 << 16, last_nodes_ + (last_nodes_ >> 3)});
-    res.h_parent = pinned_->get((size_t)run.host_cap * sizeof(int64_t));
-    res.h_item = pinned_->get((size_t)run.host_cap * sizeof(int32_t));
-    res.h_count = pinned_->get((size_t)run.host_cap * sizeof(uint32_t));
+    // compact element widths (kernels.hpp HostTrie): the download is PCIe-bound on the
+    // headline shape (0.25 ms of 1.1 ms at 17 B/itemset)
+    static const bool compact = [] {
+      const char* e = std::getenv("KMLS_COMPACT_DL");
+      return !(e && e[0] == '0');
+    }();
+    const int pw = compact && run.host_cap < (int64_t)INT32_MAX ? 4 : 8;
+    const int iw = compact && I <= 65536 ? 2 : 4;
+    const int cw = compact && n_tx_ <= 65535 ? 2 : 4;
+    res.h_parent = pinned_->get((size_t)run.host_cap * pw);
+    res.h_item = pinned_->get((size_t)run.host_cap * iw);
+    res.h_count = pinned_->get((size_t)run.host_cap * cw);
     res.h_depth = pinned_->get((size_t)run.host_cap * sizeof(uint8_t));
-    run.h_parent = (int64_t*)res.h_parent.get();
-    run.h_item = (int32_t*)res.h_item.get();
-    run.h_count = (uint32_t*)res.h_count.get();
-    run.h_depth = (uint8_t*)res.h_depth.get();
+    run.ht = kern::HostTrie{res.h_parent.get(), res.h_item.get(), res.h_count.get(),
+                            (uint8_t*)res.h_depth.get(), run.host_cap, pw, iw, cw};
+    res.par_w = pw;
+    res.item_w = iw;
+    res.cnt_w = cw;
     run.stream_dl = true;
   }
   const size_t rem = arena_->capacity() - arena_->used();
@@ -1035,9 +1044,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
                          run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
                          d_prank, part_world, part_rank,
-                         run.stream_dl ? run.h_parent : nullptr, run.stream_dl ? run.h_item : nullptr,
-                         run.stream_dl ? run.h_count : nullptr, run.stream_dl ? run.h_depth : nullptr,
-                         run.stream_dl ? run.host_cap : 0};
+                         run.stream_dl ? run.ht : kern::HostTrie{}};
   kern::level_root_setup(d_desc, d_ctl, ra, s);
   // frequent-item tables for the frequent() API (ids | counts | rank_of, one contiguous block):
   // staged to pinned memory while the levels run
@@ -1067,6 +1074,9 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   last_nodes_ = N;
   if (download && !run.stream_dl) {
     KMLS_HIP(hipStreamSynchronize(out_->copy_s));
+    res.par_w = 8;
+    res.item_w = 4;
+    res.cnt_w = 4;
     res.h_parent = pinned_->get((size_t)N * sizeof(int64_t));
     res.h_item = pinned_->get((size_t)N * sizeof(int32_t));
     res.h_count = pinned_->get((size_t)N * sizeof(uint32_t));

@@ -65,6 +65,7 @@ struct GpuMineResult {
   ItemsetTrie trie;           // host vectors (unused when the pinned arrays below are set)
   int64_t n_nodes = 0;
   std::shared_ptr<void> h_parent, h_item, h_count, h_depth;  // pinned, n_nodes entries
+  int par_w = 8, item_w = 4, cnt_w = 4;  // element bytes of h_parent / h_item / h_count
   MineStats stats;
   std::vector<Phase> phases;  // hipEvent-timed phases
   int64_t arena_high_water = 0;

@@ -84,6 +84,19 @@ struct FCtl {
   unsigned int overflow;           // 1 bump, 2 spin, 3/4 capacity → host falls back
   unsigned int dl_overflow;        // pinned host arrays too small → host copies at the end
 };
+// Pinned host trie written directly by the level kernels (streamed download).  Element widths
+// are chosen per call so that only the bytes the data needs cross PCIe: parent 4 B while node
+// ids < 2^31, item 2 B while item ids < 2^16, count 2 B while T < 2^16 (the reference's playlist
+// datasets: 9 B/itemset instead of 17 B).  A node >= cap sets FCtl::dl_overflow and the host
+// falls back to one full-width copy at the end.
+struct HostTrie {
+  void* parent;
+  void* item;
+  void* count;
+  uint8_t* depth;
+  int64_t cap;
+  int par_w, item_w, cnt_w;  // bytes: 4|8, 2|4, 2|4
+};
 struct LevelCountArgs {
   int64_t Wp;
   uint32_t minsup;
@@ -95,13 +108,7 @@ struct LevelCountArgs {
   uint32_t* out_count;
   uint8_t* out_depth;
   uint8_t child_depth;
-  // streamed download: survivors are also written straight into these pinned host arrays
-  // (nullptr = off); a node >= host_cap sets FCtl::dl_overflow (host copies at the end)
-  int64_t* h_parent;
-  int32_t* h_item;
-  uint32_t* h_count;
-  uint8_t* h_depth;
-  int64_t host_cap;
+  HostTrie h;  // streamed download (h.item == nullptr: off)
 };
 // device-resident prologue (single GPU, small vocabularies): selection + root descriptor
 // without a host round trip.  select: items with cnt >= c1, ranked by (count asc, id asc)
@@ -127,12 +134,7 @@ struct RootSetupArgs {
   const int32_t* prank;  // partition rank of each root class (world > 1), see level_partition
   int world;
   int my_rank;
-  // level-1 nodes also go straight to the pinned host arrays (nullptr = off)
-  int64_t* h_parent;
-  int32_t* h_item;
-  uint32_t* h_count;
-  uint8_t* h_depth;
-  int64_t host_cap;
+  HostTrie h;  // level-1 nodes also go straight to the pinned host arrays (h.item == nullptr: off)
 };
 void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s);
 // rank root classes by estimated cost (n_a^2 + 1 from the gram, desc) for the snake partition
@@ -141,10 +143,13 @@ void level_partition(const uint32_t* gram, int64_t ld, FLevel* desc, uint32_t mi
 int level_grid(int n_cus);
 int64_t level_tile();
 int64_t level_scan_tile();
+// tile_row[status_cap]: the scan of level L records the first row of every count tile of L,
+// so count(L) skips its per-tile search (pass nullptr to count the root level)
 void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status,
-                unsigned epoch, int64_t Wp, int64_t out_cap, int grid, hipStream_t s);
+                unsigned epoch, int64_t Wp, int64_t out_cap, int32_t* tile_row, int grid,
+                hipStream_t s);
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
-                 const LevelCountArgs& a, int grid, hipStream_t s);
+                 const LevelCountArgs& a, const int32_t* tile_row, int grid, hipStream_t s);
 
 // ---- persistent DFS (dfs_persistent.hip) ----
 struct DfsTask {

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -110,6 +111,22 @@ __device__ int64_t lookback(unsigned long long* st, int64_t t, unsigned epoch, i
   return excl;
 }
 
+// One trie node into the pinned host arrays (widths per HostTrie); false if past the capacity.
+__device__ __forceinline__ void host_store(const HostTrie& h, FCtl* ctl, int64_t node, int64_t par,
+                                           int32_t it, uint32_t cnt, uint8_t dep) {
+  if (node >= h.cap) {
+    ctl->dl_overflow = 1u;
+    return;
+  }
+  if (h.par_w == 4) ((int32_t*)h.parent)[node] = (int32_t)par;
+  else ((int64_t*)h.parent)[node] = par;
+  if (h.item_w == 2) ((uint16_t*)h.item)[node] = (uint16_t)it;
+  else ((int32_t*)h.item)[node] = it;
+  if (h.cnt_w == 2) ((uint16_t*)h.count)[node] = (uint16_t)cnt;
+  else ((uint32_t*)h.count)[node] = cnt;
+  h.depth[node] = dep;
+}
+
 // Bump allocation from the device region (256-byte aligned); nullptr + overflow flag if full.
 __device__ void* bump(FCtl* ctl, unsigned long long bytes) {
   bytes = (bytes + 255ull) & ~255ull;
@@ -119,6 +136,36 @@ __device__ void* bump(FCtl* ctl, unsigned long long bytes) {
     return nullptr;
   }
   return ctl->bump_base + off;
+}
+
+// Several bump allocations with ONE device atomic (each a serial ~1-2 µs round trip on the
+// critical path of a level's last tile); out[i] = nullptr + overflow flag if the region is full.
+template <int N>
+__device__ void bump_n(FCtl* ctl, const unsigned long long (&bytes)[N], void* (&out)[N]) {
+  unsigned long long off[N], tot = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    off[i] = tot;
+    tot += (bytes[i] + 255ull) & ~255ull;
+  }
+  const unsigned long long base = atomicAdd(&ctl->bump_top, tot);
+  const bool ok = base + tot <= ctl->bump_cap;
+  if (!ok) atomicExch(&ctl->overflow, 1u);
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = ok ? (void*)(ctl->bump_base + base + off[i]) : nullptr;
+}
+
+// Tile of a persistent level kernel.  When the grid covers every tile, tile = blockIdx.x (no
+// atomic): a look-back only waits on lower block indices, which in-order dispatch has already
+// placed even when fewer blocks than the grid are resident (sgpr-limited occupancy).  Otherwise
+// every tile comes from the ticket counter — never a mix: a resident block holding a ticket
+// tile could then spin on a block-index tile whose block cannot be dispatched.
+__device__ __forceinline__ int64_t next_tile(unsigned int* ticket, bool first, int64_t n_tiles,
+                                             int64_t* s_ticket) {
+  if (n_tiles <= (int64_t)gridDim.x) return first ? (int64_t)blockIdx.x : n_tiles;
+  if (threadIdx.x == 0) *s_ticket = (int64_t)atomicAdd(ticket, 1u);
+  __syncthreads();
+  return *s_ticket;
 }
 
 // Block-wide exclusive scan of one int64 per thread (256 threads = 4 waves); returns the
@@ -159,7 +206,8 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
                                                        FLevel* __restrict__ nx, FCtl* ctl,
                                                        unsigned long long* __restrict__ status,
                                                        unsigned epoch, int64_t Wp,
-                                                       int64_t out_cap) {
+                                                       int64_t out_cap,
+                                                       int32_t* __restrict__ tile_row) {
   __shared__ int64_t s_w[kBlock / 64];
   __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
@@ -185,10 +233,8 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
   const int64_t* __restrict__ pco = pv->cand_off;
   const int64_t* __restrict__ ppos = pv->pos;
   int64_t* __restrict__ co = lv->cand_off;
-  while (true) {
-    if (threadIdx.x == 0) s_ticket = (int64_t)atomicAdd(&lv->scan_ticket, 1u);
-    __syncthreads();
-    const int64_t t = s_ticket;
+  for (bool first = true;; first = false) {
+    const int64_t t = next_tile(&lv->scan_ticket, first, n_tiles, &s_ticket);
     if (t >= n_tiles) return;
     const int64_t s0 = t * kScanTile + (int64_t)threadIdx.x * kScanItems;
     int64_t len[kScanItems];
@@ -215,7 +261,12 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
       const int64_t s = s0 + i;
-      if (s < n) co[s] = run;
+      if (s < n) {
+        co[s] = run;
+        // count-tile → first row map: row s owns every tile start in [run, run + len)
+        for (int64_t ct = (run + kTile - 1) / kTile; ct * kTile < run + len[i]; ++ct)
+          if (ct < (int64_t)ctl->status_cap) tile_row[ct] = (int32_t)s;
+      }
       run += len[i];
     }
     if (t == n_tiles - 1 && threadIdx.x == 0) {
@@ -223,14 +274,20 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
       co[n] = total;
       lv->n_cand = total;
       const int64_t tiles = (total + kTile - 1) / kTile;
-      if (lv->child_base + total > out_cap || tiles > (int64_t)ctl->status_cap) {
+      if (lv->child_base + total > out_cap || tiles > (int64_t)ctl->status_cap ||
+          n > (int64_t)INT32_MAX) {
         atomicExch(&ctl->overflow, 4u);
       } else if (total > 0) {
-        lv->pos = (int64_t*)bump(ctl, (unsigned long long)(total + 1) * 8ull);
-        nx->bm = (const uint64_t*)bump(ctl, (unsigned long long)total * (unsigned long long)Wp * 8ull);
-        nx->rank = (const int32_t*)bump(ctl, (unsigned long long)total * 4ull);
-        nx->gid = (const int64_t*)bump(ctl, (unsigned long long)total * 8ull);
-        nx->prow = (const int32_t*)bump(ctl, (unsigned long long)total * 4ull);
+        const unsigned long long T = (unsigned long long)total;
+        const unsigned long long sz[5] = {(T + 1) * 8ull, T * (unsigned long long)Wp * 8ull, T * 4ull,
+                                          T * 8ull, T * 4ull};
+        void* p[5];
+        bump_n<5>(ctl, sz, p);
+        lv->pos = (int64_t*)p[0];
+        nx->bm = (const uint64_t*)p[1];
+        nx->rank = (const int32_t*)p[2];
+        nx->gid = (const int64_t*)p[3];
+        nx->prow = (const int32_t*)p[4];
       }
     }
     __syncthreads();
@@ -242,7 +299,8 @@ template <int TS>
 __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
                                                         FLevel* __restrict__ nx, FCtl* ctl,
                                                         unsigned long long* __restrict__ status,
-                                                        unsigned epoch, LevelCountArgs A) {
+                                                        unsigned epoch, LevelCountArgs A,
+                                                        const int32_t* __restrict__ tile_row) {
   __shared__ int64_t s_off[kWin];
   __shared__ uint32_t s_cnt[kTile];
   __shared__ int32_t s_lpos[kTile];
@@ -282,14 +340,14 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   const int team = threadIdx.x / TS;
   constexpr int kTeams = kBlock / TS;
   constexpr int kPer = kTile / kTeams;
-  while (true) {
-    if (threadIdx.x == 0) s_ticket = (int64_t)atomicAdd(&lv->count_ticket, 1u);
-    __syncthreads();
-    const int64_t t = s_ticket;
+  for (bool first = true;; first = false) {
+    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket);
     if (t >= n_tiles) return;
     const int64_t c0 = t * kTile;
     const int cn = (int)min((int64_t)kTile, n_cand - c0);
-    if (threadIdx.x < 64) {  // row of the tile's first candidate: 64-ary search by wave 0
+    if (tile_row) {  // first row of the tile, recorded by this level's scan
+      if (threadIdx.x == 0) s_r0 = tile_row[t];
+    } else if (threadIdx.x < 64) {  // root level: 64-ary search by wave 0
       const int64_t c = c0;
       int64_t lo = 0, hi = n_rows;  // invariant: co[lo] <= c < co[hi]
       while (hi - lo > 64) {
@@ -393,16 +451,8 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
         A.out_item[node] = it;
         A.out_count[node] = cnt;
         A.out_depth[node] = A.child_depth;
-        if (A.h_item) {  // streamed download: consecutive survivors → coalesced PCIe writes
-          if (node < A.host_cap) {
-            A.h_parent[node] = par;
-            A.h_item[node] = it;
-            A.h_count[node] = cnt;
-            A.h_depth[node] = A.child_depth;
-          } else {
-            ctl->dl_overflow = 1u;
-          }
-        }
+        // streamed download: consecutive survivors → coalesced PCIe writes
+        if (A.h.item) host_store(A.h, ctl, node, par, it, cnt, A.child_depth);
       }
     }
     // ---- phase 3: survivors' bitmaps (team per survivor) ----
@@ -418,6 +468,171 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
         const ulonglong2 u = x[w], v = y[w];
         z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
       }
+    }
+    if (t == n_tiles - 1 && threadIdx.x == 0) {
+      const int64_t S = base + tile_total;
+      pos[n_cand] = S;
+      nx->n_rows = S;
+      nx->child_base = child_base + S;
+      nx->cand_off = (int64_t*)bump(ctl, (unsigned long long)(S + 1) * 8ull);
+      atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Short-row variant (n2 = Wp/2 <= kSmallChunks 16-byte chunks, i.e. T <= 4096 transactions —
+// the reference's playlist datasets): a team-per-candidate AND+popcount leaves most of every
+// 64-lane wave waiting on short dependent loops, so here
+//   * phase 1: ONE thread per candidate; the whole row pair is loaded with independent 16-byte
+//     loads (unrolled, many in flight) and popcounted in registers — no cross-lane reduction;
+//   * phase 3: the tile's survivors are contiguous in the child level, so their bitmaps are
+//     written as one flat, fully coalesced [S_tile][n2] stream (survivor j = idx / n2 through a
+//     multiply-high by a host-computed magic; exact for idx, n2 < 2^16).
+// Decode, block scan, look-back and trie/host writes are identical to k_level_count.
+constexpr int kSmallChunks = 32;
+
+__global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict__ lv,
+                                                              FLevel* __restrict__ nx, FCtl* ctl,
+                                                              unsigned long long* __restrict__ status,
+                                                              unsigned epoch, LevelCountArgs A,
+                                                              uint32_t n2_magic,
+                                                              const int32_t* __restrict__ tile_row) {
+  __shared__ int64_t s_off[kWin];
+  __shared__ uint32_t s_cnt[kTile];
+  __shared__ int32_t s_src[kTile];   // survivor j of the tile → candidate slot
+  __shared__ int64_t s_a[kTile];
+  __shared__ int64_t s_b[kTile];
+  __shared__ int64_t s_w[kBlock / 64];
+  __shared__ int64_t s_r0;
+  __shared__ int64_t s_base;
+  __shared__ int64_t s_ticket;
+  if (ctl->overflow) return;
+  const int64_t n_cand = lv->n_cand;
+  const int64_t n_rows = lv->n_rows;
+  const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
+  const int64_t child_base = lv->child_base;
+  if (n_tiles == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      nx->n_rows = 0;
+      nx->child_base = child_base;
+      nx->cand_off = (int64_t*)bump(ctl, 8ull);
+      if (nx->cand_off) nx->cand_off[0] = 0;
+    }
+    return;
+  }
+  if ((int64_t)blockIdx.x >= n_tiles) return;
+  const int64_t* __restrict__ co = lv->cand_off;
+  const ulonglong2* __restrict__ bm2 = (const ulonglong2*)lv->bm;
+  const int32_t* __restrict__ rank = lv->rank;
+  const int64_t* __restrict__ gid = lv->gid;
+  int64_t* __restrict__ pos = lv->pos;
+  ulonglong2* __restrict__ cbm2 = (ulonglong2*)nx->bm;
+  int32_t* __restrict__ crank = (int32_t*)nx->rank;
+  int64_t* __restrict__ cgid = (int64_t*)nx->gid;
+  int32_t* __restrict__ cprow = (int32_t*)nx->prow;
+  const int n2 = (int)(A.Wp >> 1);
+  for (bool first = true;; first = false) {
+    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket);
+    if (t >= n_tiles) return;
+    const int64_t c0 = t * kTile;
+    const int cn = (int)min((int64_t)kTile, n_cand - c0);
+    if (tile_row) {  // first row of the tile, recorded by this level's scan
+      if (threadIdx.x == 0) s_r0 = tile_row[t];
+    } else if (threadIdx.x < 64) {  // root level: 64-ary search by wave 0
+      const int64_t c = c0;
+      int64_t lo = 0, hi = n_rows;
+      while (hi - lo > 64) {
+        const int64_t step = (hi - lo + 63) / 64;
+        const int64_t p = lo + (int64_t)threadIdx.x * step;
+        const unsigned long long bal = __ballot(p < hi && co[p] <= c);
+        const int last = 63 - __builtin_clzll(bal);
+        const int64_t nlo = lo + (int64_t)last * step;
+        hi = min(hi, nlo + step);
+        lo = nlo;
+      }
+      const int64_t p = lo + threadIdx.x;
+      const unsigned long long bal = __ballot(p < hi && co[p] <= c);
+      if (threadIdx.x == 0) s_r0 = lo + (63 - __builtin_clzll(bal));
+    }
+    __syncthreads();
+    const int64_t r0 = s_r0;
+    const int64_t nw = min((int64_t)kWin, n_rows + 1 - r0);
+    for (int64_t i = threadIdx.x; i < nw; i += kBlock) s_off[i] = co[r0 + i];
+    __syncthreads();
+    // ---- decode + phase 1: one thread per candidate ----
+    uint32_t k = 0;
+    int64_t a = 0, b = 0;
+    const bool live = (int)threadIdx.x < cn;
+    if (live) {
+      const int64_t c = c0 + threadIdx.x;
+      int64_t oa;
+      if (nw >= 2 && s_off[nw - 1] > c) {
+        int64_t lo = 0, hi = nw - 1;
+        while (hi - lo > 1) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (s_off[mid] <= c) lo = mid; else hi = mid;
+        }
+        a = r0 + lo;
+        oa = s_off[lo];
+      } else {
+        a = find_row_g(co, r0, n_rows, c);
+        oa = co[a];
+      }
+      b = a + 1 + (c - oa);
+      s_a[threadIdx.x] = a;
+      s_b[threadIdx.x] = b;
+      if (A.gram) {
+        k = A.gram[a * A.F + b];
+      } else {
+        const ulonglong2* x = bm2 + a * n2;
+        const ulonglong2* y = bm2 + b * n2;
+#pragma unroll 8
+        for (int w = 0; w < n2; ++w) {
+          const ulonglong2 u = x[w], v = y[w];
+          k += (uint32_t)__popcll(u.x & v.x) + (uint32_t)__popcll(u.y & v.y);
+        }
+      }
+    }
+    // ---- phase 2: survivor positions (block scan + look-back) ----
+    const int flag = (live && k >= A.minsup) ? 1 : 0;
+    int64_t tile_total;
+    const int64_t lx = block_excl_scan(flag, s_w, &tile_total);
+    if (flag) s_src[lx] = (int32_t)threadIdx.x;
+    if (threadIdx.x < 64) {
+      const int64_t bb = lookback(status, t, epoch, tile_total, ctl);
+      if (threadIdx.x == 0) s_base = bb;
+    }
+    __syncthreads();
+    const int64_t base = s_base;
+    if (live) {
+      pos[c0 + threadIdx.x] = base + lx;
+      if (flag) {
+        const int64_t s = base + lx;
+        const int32_t rb = rank[b];
+        const int64_t node = child_base + s;
+        crank[s] = rb;
+        cgid[s] = node;
+        cprow[s] = (int32_t)a;
+        const int64_t par = gid[a];
+        const int32_t it = A.ids[rb];
+        A.out_parent[node] = par;
+        A.out_item[node] = it;
+        A.out_count[node] = k;
+        A.out_depth[node] = A.child_depth;
+        if (A.h.item) host_store(A.h, ctl, node, par, it, k, A.child_depth);
+      }
+    }
+    // ---- phase 3: survivors' bitmaps as one coalesced [S_tile][n2] stream ----
+    const int total = (int)tile_total * n2;
+    ulonglong2* __restrict__ z = cbm2 + base * n2;
+    for (int idx = threadIdx.x; idx < total; idx += kBlock) {
+      const int j = (int)__umulhi((uint32_t)idx, n2_magic);
+      const int w = idx - j * n2;
+      const int i = s_src[j];
+      const ulonglong2 u = bm2[s_a[i] * n2 + w], v = bm2[s_b[i] * n2 + w];
+      z[idx] = make_ulonglong2(u.x & v.x, u.y & v.y);
     }
     if (t == n_tiles - 1 && threadIdx.x == 0) {
       const int64_t S = base + tile_total;
@@ -579,11 +794,16 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
       atomicExch(&ctl->overflow, 4u);
       ok = 0;
     } else if (n_cand > 0) {
-      r.pos = (int64_t*)bump(ctl, (unsigned long long)(n_cand + 1) * 8ull);
-      desc[2].bm = (const uint64_t*)bump(ctl, (unsigned long long)n_cand * (unsigned long long)a.Wp * 8ull);
-      desc[2].rank = (const int32_t*)bump(ctl, (unsigned long long)n_cand * 4ull);
-      desc[2].gid = (const int64_t*)bump(ctl, (unsigned long long)n_cand * 8ull);
-      desc[2].prow = (const int32_t*)bump(ctl, (unsigned long long)n_cand * 4ull);
+      const unsigned long long T = (unsigned long long)n_cand;
+      const unsigned long long sz[5] = {(T + 1) * 8ull, T * (unsigned long long)a.Wp * 8ull, T * 4ull,
+                                        T * 8ull, T * 4ull};
+      void* p[5];
+      bump_n<5>(ctl, sz, p);
+      r.pos = (int64_t*)p[0];
+      desc[2].bm = (const uint64_t*)p[1];
+      desc[2].rank = (const int32_t*)p[2];
+      desc[2].gid = (const int64_t*)p[3];
+      desc[2].prow = (const int32_t*)p[4];
       if (ctl->overflow) ok = 0;
     }
   }
@@ -596,16 +816,7 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     a.out_item[i] = a.ids[i];
     a.out_count[i] = a.fcounts[i];
     a.out_depth[i] = 1;
-    if (a.h_item) {
-      if (i < a.host_cap) {
-        a.h_parent[i] = -1;
-        a.h_item[i] = a.ids[i];
-        a.h_count[i] = a.fcounts[i];
-        a.h_depth[i] = 1;
-      } else {
-        ctl->dl_overflow = 1u;
-      }
-    }
+    if (a.h.item) host_store(a.h, ctl, i, -1, a.ids[i], a.fcounts[i], 1);
   }
 }
 
@@ -623,20 +834,33 @@ int team_size_for(int64_t Wp) {  // lanes per candidate: ~4-8 16-byte chunks per
 int level_grid(int n_cus) { return std::max(64, n_cus * 8); }  // 8 x 256-thread blocks per CU
 
 void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status,
-                unsigned epoch, int64_t Wp, int64_t out_cap, int grid, hipStream_t s) {
+                unsigned epoch, int64_t Wp, int64_t out_cap, int32_t* tile_row, int grid,
+                hipStream_t s) {
   hipLaunchKernelGGL(k_level_scan, dim3(grid), dim3(kBlock), 0, s, pv, lv, nx, ctl, status, epoch,
-                     Wp, out_cap);
+                     Wp, out_cap, tile_row);
   KMLS_HIP(hipGetLastError());
 }
 
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
-                 const LevelCountArgs& a, int grid, hipStream_t s) {
+                 const LevelCountArgs& a, const int32_t* tile_row, int grid, hipStream_t s) {
+  static const bool small_ok = [] {
+    const char* e = std::getenv("KMLS_COUNT_SMALL");
+    return !(e && e[0] == '0');
+  }();
+  const int64_t n2 = a.Wp >> 1;
+  if (small_ok && n2 >= 1 && n2 <= kSmallChunks) {
+    const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)n2 - 1) / (uint64_t)n2);
+    hipLaunchKernelGGL(k_level_count_small, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status,
+                       epoch, a, magic, tile_row);
+    KMLS_HIP(hipGetLastError());
+    return;
+  }
   switch (team_size_for(a.Wp)) {
-    case 4: hipLaunchKernelGGL(k_level_count<4>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
-    case 8: hipLaunchKernelGGL(k_level_count<8>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
-    case 16: hipLaunchKernelGGL(k_level_count<16>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
-    case 32: hipLaunchKernelGGL(k_level_count<32>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
-    default: hipLaunchKernelGGL(k_level_count<64>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a); break;
+    case 4: hipLaunchKernelGGL(k_level_count<4>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
+    case 8: hipLaunchKernelGGL(k_level_count<8>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
+    case 16: hipLaunchKernelGGL(k_level_count<16>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
+    case 32: hipLaunchKernelGGL(k_level_count<32>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
+    default: hipLaunchKernelGGL(k_level_count<64>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
   }
   KMLS_HIP(hipGetLastError());
 }

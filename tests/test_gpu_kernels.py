@@ -88,6 +88,27 @@ def test_gpu_miner_matches_cpu(gpu_mod, shape, ms, use_mfma, fused, monkeypatch)
         assert np.array_equal(np.bincount(r["depth"]), np.bincount(c["depth"]))
 
 
+def test_compact_download_widths(gpu_mod):
+    """The resident path streams the trie to the host at the narrowest exact widths
+    (kernels.hpp HostTrie); the first call (pinned arrays sized from a previous call) overflows
+    them and falls back to the full-width copy — both must hold the same trie."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    tx = generate("ds2_weak", seed=4)
+    g = gpu_mod.GpuMiner(0, 1 << 31, 0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    first = g.mine(0.03)
+    second = g.mine(0.03)
+    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.03)
+    assert second["stats"]["levels_path"] == "fused-resident"
+    if first["stats"]["n_itemsets"] > (1 << 16):  # first call's host arrays were too small
+        assert first["parent"].dtype == np.int64 and first["count"].dtype == np.uint32
+    assert second["parent"].dtype == np.int32
+    assert second["item"].dtype == np.uint16 and second["count"].dtype == np.uint16
+    for r in (first, second):
+        assert _trie_dict(r) == _trie_dict(c)
+        np.testing.assert_array_equal(r["depth"], first["depth"])
+
+
 def test_gpu_miner_max_len_and_pairs(gpu_mod):
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     tx = generate("ds2_weak", seed=2)
@@ -356,7 +377,10 @@ def test_replicated_mode_multiprocess(gpu_mod):
     import sys
     import pathlib
     root = pathlib.Path(__file__).resolve().parents[1]
-    env = dict(os.environ, PYTHONPATH=str(root) + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    # three processes share one GPU: fixed arenas (the default takes half of the free HBM at
+    # construction, which races between processes starting together)
+    env = dict(os.environ, PYTHONPATH=str(root) + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               KMLS_ARENA_GB="16")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node=3", "--master-addr=127.0.0.1", "--master-port=29613",
                         str(root / "scripts" / "replicate_check.py")],
