@@ -143,12 +143,14 @@ struct OutBufs {
   // fused level path (levels.hip): look-back status words (epoch-tagged, zeroed once)
   unsigned long long* status = nullptr;
   int32_t* tile_row = nullptr;   // [status_cap] count tile → first row (written by level_scan)
+  unsigned long long* trace = nullptr;  // KMLS_LEVEL_TRACE diagnostics ([status_cap][8])
   int64_t status_cap = 1 << 20;  // tiles per launch (256M candidates / 2G rows)
   unsigned epoch = 0;
   int depth_hint = 6;            // levels enqueued before the first completion check
   OutBufs() {
     KMLS_HIP(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
-    KMLS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    // device-scope release: a cross-stream fork needs no system-scope L2 writeback
+    KMLS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice));
     KMLS_HIP(hipMalloc((void**)&status, (size_t)status_cap * sizeof(unsigned long long)));
     KMLS_HIP(hipMemset(status, 0, (size_t)status_cap * sizeof(unsigned long long)));
     KMLS_HIP(hipMalloc((void**)&tile_row, (size_t)status_cap * sizeof(int32_t)));
@@ -164,6 +166,7 @@ struct OutBufs {
     if (copy_s) (void)hipStreamSynchronize(copy_s);
     if (status) (void)hipFree(status);
     if (tile_row) (void)hipFree(tile_row);
+    if (trace) (void)hipFree(trace);
     if (ev) (void)hipEventDestroy(ev);
     if (copy_s) (void)hipStreamDestroy(copy_s);
   }
@@ -186,6 +189,18 @@ struct Event {
 };
 
 constexpr int64_t kCandCap = 32ll << 20;  // candidates per chunk
+
+// streamed-download mode of the fused levels: "deferred" (default) = each count launch carries
+// copy blocks that move the previous level's nodes to the host while its tiles compute;
+// "inline" = survivors are written to the host by the tile blocks themselves (every launch
+// then waits for its own PCIe writes to drain)
+bool deferred_dl() {
+  static const bool v = [] {
+    const char* e = std::getenv("KMLS_DL_MODE");
+    return !(e && std::string(e) == "inline");
+  }();
+  return v;
+}
 size_t fused_bump_cap(size_t bytes);
 
 struct MineRun {
@@ -404,7 +419,7 @@ struct MineRun {
     constexpr int kMaxLv = 64;
     const int64_t Fr = root.n;
     const size_t mark = arena->mark();
-    const int64_t row_bytes = Wp * 8 + 4 + 8 + 4 + 8;  // child bitmap + rank + gid + prow + pos
+    const int64_t row_bytes = Wp * 8 + 4 + 8 + 4 + 4 + 8;  // child bitmap + rank + gid + prow + slot + pos
     const size_t root_need = (size_t)(root_total + 1) * (size_t)row_bytes + (size_t)(Fr + 1) * 8 +
                              kMaxLv * sizeof(kern::FLevel) + 4096;
     const size_t free_b = arena->capacity() - arena->used();
@@ -425,10 +440,11 @@ struct MineRun {
     kern::FCtl* d_ctl = (kern::FCtl*)arena->push(sizeof(kern::FCtl));
     int64_t* d_off = (int64_t*)arena->push((size_t)(Fr + 1) * 8);
     int64_t* d_pos = (int64_t*)arena->push((size_t)(root_total + 1) * 8);
-    uint64_t* c_bm = (uint64_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * Wp * 8);
+    uint64_t* c_bm = (uint64_t*)arena->push((size_t)((std::max<int64_t>(root_total, 1) + 63) & ~63ll) * Wp * 8);
     int32_t* c_rank = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
     int64_t* c_gid = (int64_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 8);
     int32_t* c_prow = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
+    int32_t* c_slot = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
     const size_t rem = arena->capacity() - arena->used();
     const size_t bump_bytes = fused_bump_cap(rem > (320ull << 20) ? rem - (64ull << 20) : 0);
     if (bump_bytes < (16ull << 20)) {
@@ -459,6 +475,7 @@ struct MineRun {
     h_desc[2].rank = c_rank;
     h_desc[2].gid = c_gid;
     h_desc[2].prow = c_prow;
+    h_desc[2].slot = c_slot;
     h_ctl->bump_base = bump_base;
     h_ctl->bump_cap = bump_bytes;
     h_ctl->status_cap = (unsigned long long)ob->status_cap;
@@ -477,13 +494,35 @@ struct MineRun {
   // kernels write every survivor straight into the pinned host arrays as well (no copy-out
   // kernel, no cross-stream event per level); level-1 nodes are written by the resident
   // prologue's root setup or were queued by stream_out() on the host-prepared path.
+  // deferred download: copy level L's children (nodes [desc[L].child_base, + desc[L+1].n_rows))
+  void copy_level(kern::FLevel* d_desc, kern::FCtl* d_ctl, int L) {
+    kern::level_copyout(&d_desc[L], &d_desc[L + 1], d_ctl, out_parent.p, out_item.p, out_count.p,
+                        out_depth.p, ht, s);
+  }
+
   bool levels_loop(kern::FLevel* d_desc, kern::FCtl* d_ctl, int64_t out_cap) {
     constexpr int kMaxLv = 64;
     const int grid = kern::level_grid(n_cus);
+    // diagnostics: KMLS_LEVEL_TRACE=<L> records per-tile phase timestamps of level L's count
+    // kernel and writes them to KMLS_LEVEL_TRACE_FILE (uint64 [tiles][8]) after the call
+    static const int trace_level = [] {
+      const char* e = std::getenv("KMLS_LEVEL_TRACE");
+      return e ? std::atoi(e) : 0;
+    }();
+    unsigned long long* d_trace = nullptr;
+    if (trace_level > 0) {
+      if (!ob->trace) {
+        KMLS_HIP(hipMalloc((void**)&ob->trace, (size_t)ob->status_cap * 64));
+      }
+      KMLS_HIP(hipMemsetAsync(ob->trace, 0, (size_t)ob->status_cap * 64, s));
+      d_trace = ob->trace;
+    }
+    const bool deferred = stream_dl && deferred_dl();
     auto count_level = [&](int L) {
       kern::LevelCountArgs a{Wp, minsup, L == 1 ? gram : nullptr, F, d_ids, out_parent.p,
                              out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1),
-                             stream_dl ? ht : kern::HostTrie{}};
+                             stream_dl ? ht : kern::HostTrie{},
+                             L == trace_level ? d_trace : nullptr, deferred};
       kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a,
                         L == 1 ? nullptr : ob->tile_row, grid, s);
     };
@@ -502,6 +541,7 @@ struct MineRun {
         count_level(L);
         last = L;
       }
+      if (deferred) copy_level(d_desc, d_ctl, last);  // the last launch's children
       KMLS_HIP(hipMemcpyAsync(b_desc, d_desc, kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl),
                               hipMemcpyDeviceToHost, s));
       KMLS_HIP(hipStreamSynchronize(s));
@@ -520,6 +560,16 @@ struct MineRun {
       break;
     }
     KMLS_HIP(hipStreamSynchronize(ob->copy_s));
+    if (d_trace && trace_level <= last) {
+      const int64_t tiles = (b_desc[trace_level].n_cand + kern::level_tile() - 1) / kern::level_tile();
+      std::vector<unsigned long long> h((size_t)tiles * 8);
+      KMLS_HIP(hipMemcpy(h.data(), d_trace, h.size() * 8, hipMemcpyDeviceToHost));
+      const char* path = std::getenv("KMLS_LEVEL_TRACE_FILE");
+      if (FILE* f = std::fopen(path ? path : "level_trace.bin", "wb")) {
+        std::fwrite(h.data(), 8, h.size(), f);
+        std::fclose(f);
+      }
+    }
     if (!ok) return false;
     last_desc.assign(b_desc, b_desc + kMaxLv);
     const int64_t new_size = b_desc[last + 1].child_base;
@@ -1044,7 +1094,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
                          run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
                          d_prank, part_world, part_rank,
-                         run.stream_dl ? run.ht : kern::HostTrie{}};
+                         run.stream_dl && !deferred_dl() ? run.ht : kern::HostTrie{}};
   kern::level_root_setup(d_desc, d_ctl, ra, s);
   // frequent-item tables for the frequent() API (ids | counts | rank_of, one contiguous block):
   // staged to pinned memory while the levels run

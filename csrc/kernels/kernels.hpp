@@ -74,7 +74,11 @@ struct FLevel {  // device-resident descriptor of one level (rows = itemsets of 
   int64_t* pos;            // [n_cand + 1] survivor index of each candidate
   int64_t child_base;      // trie id of this level's first child
   unsigned int scan_ticket, count_ticket;
-  char pad[40];
+  // row → bitmap row (nullptr: identity).  The short-row count kernel writes each candidate's
+  // AND row in place at its candidate index (no compaction pass), so a level's rows point into
+  // the candidate-indexed bitmap array of the parent's expansion.
+  const int32_t* slot;
+  char pad[32];
 };
 struct FCtl {
   char* bump_base;
@@ -109,7 +113,13 @@ struct LevelCountArgs {
   uint8_t* out_depth;
   uint8_t child_depth;
   HostTrie h;  // streamed download (h.item == nullptr: off)
+  unsigned long long* trace;  // per-tile phase timestamps [tile][8] (nullptr: off; diagnostics)
+  // deferred download: the launch carries kCopyBlocks extra blocks that copy the PREVIOUS
+  // level's nodes (this level's rows, finished by the previous launch) from the device trie to
+  // the host trie while the tile blocks run; false = survivors written to the host inline
+  bool deferred_dl;
 };
+constexpr int kCopyBlocks = 64;
 // device-resident prologue (single GPU, small vocabularies): selection + root descriptor
 // without a host round trip.  select: items with cnt >= c1, ranked by (count asc, id asc)
 // (= select_frequent), F → desc[1].n_rows.  root_setup: level-1 trie nodes, root cand_off
@@ -148,6 +158,11 @@ int64_t level_scan_tile();
 void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status,
                 unsigned epoch, int64_t Wp, int64_t out_cap, int32_t* tile_row, int grid,
                 hipStream_t s);
+// side-stream download: trie nodes [lv->child_base, +nx->n_rows) (one finished level) from the
+// device trie arrays into the pinned host trie (widths per HostTrie)
+void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t* d_parent,
+                   const int32_t* d_item, const uint32_t* d_count, const uint8_t* d_depth,
+                   const HostTrie& h, hipStream_t s);
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
                  const LevelCountArgs& a, const int32_t* tile_row, int grid, hipStream_t s);
 

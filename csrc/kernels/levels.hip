@@ -127,6 +127,18 @@ __device__ __forceinline__ void host_store(const HostTrie& h, FCtl* ctl, int64_t
   h.depth[node] = dep;
 }
 
+// Copy role of the deferred download (LevelCountArgs::deferred_dl): trie nodes
+// [desc[L-1].child_base, + desc[L].n_rows) — level L's rows, finished by the previous launch —
+// from the device trie arrays to the host trie.  Runs in kCopyBlocks dedicated blocks, so the
+// PCIe writes drain while this launch's tile blocks compute instead of stalling them.
+__device__ void copy_prev_level(const FLevel* lv, FCtl* ctl, const LevelCountArgs& A, int cb) {
+  const FLevel* pv = lv - 1;
+  const int64_t base = pv->child_base, n = lv->n_rows;
+  for (int64_t i = base + (int64_t)cb * blockDim.x + threadIdx.x; i < base + n;
+       i += (int64_t)kCopyBlocks * blockDim.x)
+    host_store(A.h, ctl, i, A.out_parent[i], A.out_item[i], A.out_count[i], A.out_depth[i]);
+}
+
 // Bump allocation from the device region (256-byte aligned); nullptr + overflow flag if full.
 __device__ void* bump(FCtl* ctl, unsigned long long bytes) {
   bytes = (bytes + 255ull) & ~255ull;
@@ -161,8 +173,8 @@ __device__ void bump_n(FCtl* ctl, const unsigned long long (&bytes)[N], void* (&
 // every tile comes from the ticket counter — never a mix: a resident block holding a ticket
 // tile could then spin on a block-index tile whose block cannot be dispatched.
 __device__ __forceinline__ int64_t next_tile(unsigned int* ticket, bool first, int64_t n_tiles,
-                                             int64_t* s_ticket) {
-  if (n_tiles <= (int64_t)gridDim.x) return first ? (int64_t)blockIdx.x : n_tiles;
+                                             int64_t* s_ticket, int64_t grid) {
+  if (n_tiles <= grid) return first ? (int64_t)blockIdx.x : n_tiles;
   if (threadIdx.x == 0) *s_ticket = (int64_t)atomicAdd(ticket, 1u);
   __syncthreads();
   return *s_ticket;
@@ -234,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
   const int64_t* __restrict__ ppos = pv->pos;
   int64_t* __restrict__ co = lv->cand_off;
   for (bool first = true;; first = false) {
-    const int64_t t = next_tile(&lv->scan_ticket, first, n_tiles, &s_ticket);
+    const int64_t t = next_tile(&lv->scan_ticket, first, n_tiles, &s_ticket, (int64_t)gridDim.x);
     if (t >= n_tiles) return;
     const int64_t s0 = t * kScanTile + (int64_t)threadIdx.x * kScanItems;
     int64_t len[kScanItems];
@@ -279,15 +291,17 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
         atomicExch(&ctl->overflow, 4u);
       } else if (total > 0) {
         const unsigned long long T = (unsigned long long)total;
-        const unsigned long long sz[5] = {(T + 1) * 8ull, T * (unsigned long long)Wp * 8ull, T * 4ull,
-                                          T * 8ull, T * 4ull};
-        void* p[5];
-        bump_n<5>(ctl, sz, p);
+        const unsigned long long T64 = (T + 63ull) & ~63ull;  // 64-interleaved candidate rows
+        const unsigned long long sz[6] = {(T + 1) * 8ull, T64 * (unsigned long long)Wp * 8ull, T * 4ull,
+                                          T * 8ull, T * 4ull, T * 4ull};
+        void* p[6];
+        bump_n<6>(ctl, sz, p);
         lv->pos = (int64_t*)p[0];
         nx->bm = (const uint64_t*)p[1];
         nx->rank = (const int32_t*)p[2];
         nx->gid = (const int64_t*)p[3];
         nx->prow = (const int32_t*)p[4];
+        nx->slot = (const int32_t*)p[5];
       }
     }
     __syncthreads();
@@ -311,6 +325,11 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
   if (ctl->overflow) return;
+  const int64_t tgrid = (int64_t)gridDim.x - (A.deferred_dl ? kCopyBlocks : 0);  // tile blocks
+  if ((int64_t)blockIdx.x >= tgrid) {
+    copy_prev_level(lv, ctl, A, (int)(blockIdx.x - tgrid));
+    return;
+  }
   const int64_t n_cand = lv->n_cand;
   const int64_t n_rows = lv->n_rows;
   const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
@@ -341,7 +360,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   constexpr int kTeams = kBlock / TS;
   constexpr int kPer = kTile / kTeams;
   for (bool first = true;; first = false) {
-    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket);
+    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket, tgrid);
     if (t >= n_tiles) return;
     const int64_t c0 = t * kTile;
     const int cn = (int)min((int64_t)kTile, n_cand - c0);
@@ -452,7 +471,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
         A.out_count[node] = cnt;
         A.out_depth[node] = A.child_depth;
         // streamed download: consecutive survivors → coalesced PCIe writes
-        if (A.h.item) host_store(A.h, ctl, node, par, it, cnt, A.child_depth);
+        if (A.h.item && !A.deferred_dl) host_store(A.h, ctl, node, par, it, cnt, A.child_depth);
       }
     }
     // ---- phase 3: survivors' bitmaps (team per survivor) ----
@@ -483,32 +502,39 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
 
 // ---------------------------------------------------------------------------------------------
 // Short-row variant (n2 = Wp/2 <= kSmallChunks 16-byte chunks, i.e. T <= 4096 transactions —
-// the reference's playlist datasets): a team-per-candidate AND+popcount leaves most of every
-// 64-lane wave waiting on short dependent loops, so here
-//   * phase 1: ONE thread per candidate; the whole row pair is loaded with independent 16-byte
-//     loads (unrolled, many in flight) and popcounted in registers — no cross-lane reduction;
-//   * phase 3: the tile's survivors are contiguous in the child level, so their bitmaps are
-//     written as one flat, fully coalesced [S_tile][n2] stream (survivor j = idx / n2 through a
-//     multiply-high by a host-computed magic; exact for idx, n2 < 2^16).
-// Decode, block scan, look-back and trie/host writes are identical to k_level_count.
+// the reference's playlist datasets).  Per-tile phase traces (KMLS_LEVEL_TRACE, see
+// profiles/r1_s3_level_traces.md) showed the team kernel latency-bound: about one tile per
+// resident block on the big levels, each a chain of dependent memory round trips, and the
+// survivor-materialise phase (re-reading both parent rows after the look-back) the longest
+// link.  Here
+//   * phase 1: ONE thread per candidate ANDs its row pair with independent 16-byte loads,
+//     popcounts in registers (no cross-lane reduction) and writes the AND row straight to the
+//     child bitmap array at the CANDIDATE index (fire-and-forget stores; non-survivors waste
+//     their row, 2-35 % of candidates on the headline levels).  Child rows then reach their
+//     bitmap through FLevel::slot, so there is no compaction pass at all.  Candidate rows are
+//     stored 64-interleaved (chunk w of slot c at ((c/64)*n2 + w)*64 + c%64): the 64 lanes of
+//     a wave write 64 consecutive slots, and the next level's lanes read siblings with
+//     consecutive slots, so both directions are coalesced 1 KB accesses;
+//   * the root level (pair counts from the gram) computes AND rows only for survivors.
+// Decode, look-back, trie/host writes and the tile→row map are shared with k_level_count.
 constexpr int kSmallChunks = 32;
 
 __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict__ lv,
                                                               FLevel* __restrict__ nx, FCtl* ctl,
                                                               unsigned long long* __restrict__ status,
                                                               unsigned epoch, LevelCountArgs A,
-                                                              uint32_t n2_magic,
                                                               const int32_t* __restrict__ tile_row) {
   __shared__ int64_t s_off[kWin];
-  __shared__ uint32_t s_cnt[kTile];
-  __shared__ int32_t s_src[kTile];   // survivor j of the tile → candidate slot
-  __shared__ int64_t s_a[kTile];
-  __shared__ int64_t s_b[kTile];
   __shared__ int64_t s_w[kBlock / 64];
   __shared__ int64_t s_r0;
   __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
   if (ctl->overflow) return;
+  const int64_t tgrid = (int64_t)gridDim.x - (A.deferred_dl ? kCopyBlocks : 0);  // tile blocks
+  if ((int64_t)blockIdx.x >= tgrid) {
+    copy_prev_level(lv, ctl, A, (int)(blockIdx.x - tgrid));
+    return;
+  }
   const int64_t n_cand = lv->n_cand;
   const int64_t n_rows = lv->n_rows;
   const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
@@ -525,6 +551,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
   if ((int64_t)blockIdx.x >= n_tiles) return;
   const int64_t* __restrict__ co = lv->cand_off;
   const ulonglong2* __restrict__ bm2 = (const ulonglong2*)lv->bm;
+  const int32_t* __restrict__ slot = lv->slot;
   const int32_t* __restrict__ rank = lv->rank;
   const int64_t* __restrict__ gid = lv->gid;
   int64_t* __restrict__ pos = lv->pos;
@@ -532,10 +559,13 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
   int32_t* __restrict__ crank = (int32_t*)nx->rank;
   int64_t* __restrict__ cgid = (int64_t*)nx->gid;
   int32_t* __restrict__ cprow = (int32_t*)nx->prow;
+  int32_t* __restrict__ cslot = (int32_t*)nx->slot;
   const int n2 = (int)(A.Wp >> 1);
   for (bool first = true;; first = false) {
-    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket);
+    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket, tgrid);
     if (t >= n_tiles) return;
+    unsigned long long* tr = (A.trace && threadIdx.x == 0) ? A.trace + t * 8 : nullptr;
+    if (tr) tr[0] = wall_clock64();
     const int64_t c0 = t * kTile;
     const int cn = (int)min((int64_t)kTile, n_cand - c0);
     if (tile_row) {  // first row of the tile, recorded by this level's scan
@@ -561,12 +591,13 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
     const int64_t nw = min((int64_t)kWin, n_rows + 1 - r0);
     for (int64_t i = threadIdx.x; i < nw; i += kBlock) s_off[i] = co[r0 + i];
     __syncthreads();
-    // ---- decode + phase 1: one thread per candidate ----
+    if (tr) tr[1] = wall_clock64();
+    // ---- decode + phase 1: one thread per candidate, AND row written in place ----
     uint32_t k = 0;
     int64_t a = 0, b = 0;
     const bool live = (int)threadIdx.x < cn;
+    const int64_t c = c0 + threadIdx.x;
     if (live) {
-      const int64_t c = c0 + threadIdx.x;
       int64_t oa;
       if (nw >= 2 && s_off[nw - 1] > c) {
         int64_t lo = 0, hi = nw - 1;
@@ -581,33 +612,60 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
         oa = co[a];
       }
       b = a + 1 + (c - oa);
-      s_a[threadIdx.x] = a;
-      s_b[threadIdx.x] = b;
-      if (A.gram) {
-        k = A.gram[a * A.F + b];
-      } else {
-        const ulonglong2* x = bm2 + a * n2;
-        const ulonglong2* y = bm2 + b * n2;
-#pragma unroll 8
-        for (int w = 0; w < n2; ++w) {
-          const ulonglong2 u = x[w], v = y[w];
-          k += (uint32_t)__popcll(u.x & v.x) + (uint32_t)__popcll(u.y & v.y);
+      const bool need_row = A.gram ? (k = A.gram[a * A.F + b]) >= A.minsup : true;
+      if (need_row) {
+        // parent rows: row-major at the root, 64-interleaved candidate slots below it
+        const ulonglong2* __restrict__ x;
+        const ulonglong2* __restrict__ y;
+        int sxy;
+        if (slot) {
+          const int64_t sa = slot[a], sb = slot[b];
+          x = bm2 + ((sa >> 6) * n2 << 6) + (sa & 63);
+          y = bm2 + ((sb >> 6) * n2 << 6) + (sb & 63);
+          sxy = 64;
+        } else {
+          x = bm2 + a * n2;
+          y = bm2 + b * n2;
+          sxy = 1;
         }
+        ulonglong2* __restrict__ z = cbm2 + ((c >> 6) * n2 << 6) + (c & 63);
+        // batches of kB chunk pairs: all loads of a batch are issued before its stores (a
+        // load/store-interleaved loop compiles to one full memory round trip per chunk)
+        constexpr int kB = 6;
+        uint32_t kk = 0;
+        for (int w0 = 0; w0 < n2; w0 += kB) {
+          ulonglong2 u[kB], v[kB];
+#pragma unroll
+          for (int q = 0; q < kB; ++q)
+            if (w0 + q < n2) {
+              u[q] = x[(w0 + q) * sxy];
+              v[q] = y[(w0 + q) * sxy];
+            }
+#pragma unroll
+          for (int q = 0; q < kB; ++q)
+            if (w0 + q < n2) {
+              const ulonglong2 r = make_ulonglong2(u[q].x & v[q].x, u[q].y & v[q].y);
+              kk += (uint32_t)__popcll(r.x) + (uint32_t)__popcll(r.y);
+              z[(w0 + q) << 6] = r;
+            }
+        }
+        if (!A.gram) k = kk;
       }
     }
-    // ---- phase 2: survivor positions (block scan + look-back) ----
+    // ---- phase 2: survivor positions (block scan + look-back), trie + host writes ----
     const int flag = (live && k >= A.minsup) ? 1 : 0;
     int64_t tile_total;
     const int64_t lx = block_excl_scan(flag, s_w, &tile_total);
-    if (flag) s_src[lx] = (int32_t)threadIdx.x;
+    if (tr) tr[2] = wall_clock64();
     if (threadIdx.x < 64) {
       const int64_t bb = lookback(status, t, epoch, tile_total, ctl);
       if (threadIdx.x == 0) s_base = bb;
     }
     __syncthreads();
+    if (tr) tr[3] = wall_clock64();
     const int64_t base = s_base;
     if (live) {
-      pos[c0 + threadIdx.x] = base + lx;
+      pos[c] = base + lx;
       if (flag) {
         const int64_t s = base + lx;
         const int32_t rb = rank[b];
@@ -615,25 +673,17 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
         crank[s] = rb;
         cgid[s] = node;
         cprow[s] = (int32_t)a;
+        cslot[s] = (int32_t)c;
         const int64_t par = gid[a];
         const int32_t it = A.ids[rb];
         A.out_parent[node] = par;
         A.out_item[node] = it;
         A.out_count[node] = k;
         A.out_depth[node] = A.child_depth;
-        if (A.h.item) host_store(A.h, ctl, node, par, it, k, A.child_depth);
+        if (A.h.item && !A.deferred_dl) host_store(A.h, ctl, node, par, it, k, A.child_depth);
       }
     }
-    // ---- phase 3: survivors' bitmaps as one coalesced [S_tile][n2] stream ----
-    const int total = (int)tile_total * n2;
-    ulonglong2* __restrict__ z = cbm2 + base * n2;
-    for (int idx = threadIdx.x; idx < total; idx += kBlock) {
-      const int j = (int)__umulhi((uint32_t)idx, n2_magic);
-      const int w = idx - j * n2;
-      const int i = s_src[j];
-      const ulonglong2 u = bm2[s_a[i] * n2 + w], v = bm2[s_b[i] * n2 + w];
-      z[idx] = make_ulonglong2(u.x & v.x, u.y & v.y);
-    }
+    if (tr) tr[4] = wall_clock64();
     if (t == n_tiles - 1 && threadIdx.x == 0) {
       const int64_t S = base + tile_total;
       pos[n_cand] = S;
@@ -642,8 +692,32 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
       nx->cand_off = (int64_t*)bump(ctl, (unsigned long long)(S + 1) * 8ull);
       atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
     }
+    if (tr) tr[5] = wall_clock64();
     __syncthreads();
+    if (tr) {
+      tr[6] = wall_clock64();
+      tr[7] = (unsigned long long)tile_total | ((unsigned long long)cn << 32);
+    }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deferred-download tail: the last launched level's children have no following count launch to
+// carry them, so this copies trie nodes [lv->child_base, + nx->n_rows) after the level loop.
+__global__ __launch_bounds__(kBlock) void k_level_copyout(const FLevel* __restrict__ lv,
+                                                          const FLevel* __restrict__ nx, FCtl* ctl,
+                                                          const int64_t* __restrict__ d_parent,
+                                                          const int32_t* __restrict__ d_item,
+                                                          const uint32_t* __restrict__ d_count,
+                                                          const uint8_t* __restrict__ d_depth,
+                                                          HostTrie h) {
+  if (ctl->overflow) return;
+  const int64_t base = lv->child_base;
+  const int64_t S = nx->n_rows;
+  if (S <= 0) return;
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < base + S; i += nthr)
+    host_store(h, ctl, i, d_parent[i], d_item[i], d_count[i], d_depth[i]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -795,15 +869,17 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
       ok = 0;
     } else if (n_cand > 0) {
       const unsigned long long T = (unsigned long long)n_cand;
-      const unsigned long long sz[5] = {(T + 1) * 8ull, T * (unsigned long long)a.Wp * 8ull, T * 4ull,
-                                        T * 8ull, T * 4ull};
-      void* p[5];
-      bump_n<5>(ctl, sz, p);
+      const unsigned long long T64 = (T + 63ull) & ~63ull;  // 64-interleaved candidate rows
+      const unsigned long long sz[6] = {(T + 1) * 8ull, T64 * (unsigned long long)a.Wp * 8ull, T * 4ull,
+                                        T * 8ull, T * 4ull, T * 4ull};
+      void* p[6];
+      bump_n<6>(ctl, sz, p);
       r.pos = (int64_t*)p[0];
       desc[2].bm = (const uint64_t*)p[1];
       desc[2].rank = (const int32_t*)p[2];
       desc[2].gid = (const int64_t*)p[3];
       desc[2].prow = (const int32_t*)p[4];
+      desc[2].slot = (const int32_t*)p[5];
       if (ctl->overflow) ok = 0;
     }
   }
@@ -843,15 +919,15 @@ void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long lon
 
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
                  const LevelCountArgs& a, const int32_t* tile_row, int grid, hipStream_t s) {
+  if (a.deferred_dl) grid += kCopyBlocks;
   static const bool small_ok = [] {
     const char* e = std::getenv("KMLS_COUNT_SMALL");
     return !(e && e[0] == '0');
   }();
   const int64_t n2 = a.Wp >> 1;
   if (small_ok && n2 >= 1 && n2 <= kSmallChunks) {
-    const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)n2 - 1) / (uint64_t)n2);
     hipLaunchKernelGGL(k_level_count_small, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status,
-                       epoch, a, magic, tile_row);
+                       epoch, a, tile_row);
     KMLS_HIP(hipGetLastError());
     return;
   }
@@ -862,6 +938,14 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
     case 32: hipLaunchKernelGGL(k_level_count<32>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
     default: hipLaunchKernelGGL(k_level_count<64>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
   }
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t* d_parent,
+                   const int32_t* d_item, const uint32_t* d_count, const uint8_t* d_depth,
+                   const HostTrie& h, hipStream_t s) {
+  hipLaunchKernelGGL(k_level_copyout, dim3(128), dim3(kBlock), 0, s, lv, nx, ctl, d_parent, d_item,
+                     d_count, d_depth, h);
   KMLS_HIP(hipGetLastError());
 }
 
