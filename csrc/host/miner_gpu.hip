@@ -1068,22 +1068,27 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   }
   const size_t bump_bytes = fused_bump_cap(rem - (64ull << 20));
   char* bump_base = (char*)arena_->push(bump_bytes);
-  std::shared_ptr<void> stage = pinned_->get(kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
-  std::memset(stage.get(), 0, kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
-  kern::FCtl* h_ctl = (kern::FCtl*)((kern::FLevel*)stage.get() + kMaxLv);
-  h_ctl->bump_base = bump_base;
-  h_ctl->bump_cap = bump_bytes;
-  h_ctl->status_cap = (unsigned long long)out_->status_cap;
-  KMLS_HIP(hipMemcpyAsync(d_desc, stage.get(), kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl),
-                          hipMemcpyHostToDevice, s));
-  // prologue, all on the device
-  KMLS_HIP(hipMemsetAsync(d_cnt, 0, (size_t)I * 4, s));
+  // prologue, all on the device: one init launch (histogram + bitmap buffer zeroed, level
+  // descriptors zeroed, control block set), supports, selection (small vocabularies: one launch
+  // that also writes the frequent-item tables to pinned host memory), bitmaps, gram
+  kern::FCtl init{};
+  init.bump_base = bump_base;
+  init.bump_cap = bump_bytes;
+  init.status_cap = (unsigned long long)out_->status_cap;
+  kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl, init, s);
   kern::item_support(d_items_, nnz_, (int32_t)I, d_cnt, s);
-  kern::level_select(d_cnt, I, level1_threshold((uint64_t)n_tx_, cfg.min_support), d_ids, d_fcnt,
-                     d_rank_of, d_rrank /* scratch until root setup */, d_desc, s);
-  KMLS_HIP(hipMemsetAsync(d_own_bm_, 0, need, s));
+  // frequent-item tables for the frequent() API (ids | counts | rank_of, tab_stride apart)
+  std::shared_ptr<void> fstage = pinned_->get((size_t)tab_stride * 12);
+  const uint32_t c1 = level1_threshold((uint64_t)n_tx_, cfg.min_support);
+  const bool fused_select = I <= kern::kSelectFusedMax;
+  if (fused_select)
+    kern::level_select_fused(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_desc,
+                             (int32_t*)fstage.get(), tab_stride, s);
+  else
+    kern::level_select(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_rrank /* scratch until root setup */,
+                       d_desc, s);
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of, d_own_bm_, Wp, 0, s);
-  KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));
+  if (kern::pair_gram_dev_needs_zero(Wp, I)) KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));
   kern::pair_gram_popcount_dev(d_own_bm_, Wp, &d_desc[1].n_rows, I, d_gram, s);
   int32_t* d_prank = nullptr;
   if (part_world > 1) {  // replicated-data partition of the root classes, computed on device
@@ -1094,12 +1099,11 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
                          run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
                          d_prank, part_world, part_rank,
-                         run.stream_dl && !deferred_dl() ? run.ht : kern::HostTrie{}};
+                         run.stream_dl && !deferred_dl() ? run.ht : kern::HostTrie{},
+                         fused_select ? (int32_t*)fstage.get() : nullptr, tab_stride};
   kern::level_root_setup(d_desc, d_ctl, ra, s);
-  // frequent-item tables for the frequent() API (ids | counts | rank_of, one contiguous block):
-  // staged to pinned memory while the levels run
-  std::shared_ptr<void> fstage = pinned_->get((size_t)tab_stride * 12);
-  KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));
+  if (!fused_select)  // staged to pinned memory while the levels run
+    KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));
   KMLS_HIP(hipEventRecord(e1.e, s));
   const bool ok = run.levels_loop(d_desc, d_ctl, out_cap);
   if (!ok) {

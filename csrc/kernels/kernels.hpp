@@ -55,6 +55,8 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
 // same with F read from the device (grid and row stride sized for F_max)
 void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, int64_t F_max,
                             uint32_t* out, hipStream_t s);
+// false when every i<j<F entry is written directly (no split-K atomics): no zero-fill needed
+bool pair_gram_dev_needs_zero(int64_t Wp, int64_t F_max);
 // C[i][j] += popcount(A_i & B_j) (rectangular, accumulating; C zeroed by the caller once)
 void bitgemm_rect(const uint64_t* A, int64_t Fa, const uint64_t* B, int64_t Fb, int64_t Wp,
                   uint32_t* C, int64_t ldc, hipStream_t s);
@@ -125,6 +127,20 @@ constexpr int kCopyBlocks = 64;
 // (= select_frequent), F → desc[1].n_rows.  root_setup: level-1 trie nodes, root cand_off
 // (closed form), iota rank/gid, root children buffers from the bump region.
 constexpr int64_t kSelectMaxItems = 16384;
+// one launch for the per-call device state of the resident path: zero the support histogram
+// and the bitmap buffer, zero the level descriptors and initialise the control block (replaces
+// two memsets and a host→device descriptor copy)
+void level_prologue_init(uint32_t* cnt, int64_t n_items, uint64_t* bm, int64_t bm_words,
+                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl& init, hipStream_t s);
+// selection in one launch for small vocabularies (n_items <= kSelectFusedMax): every thread
+// ranks its item against all others (no rank accumulator, no memset) and also writes rank_of
+// (the third of the frequent-item tables ids | counts | rank_of, `tab_stride` apart) straight
+// to pinned host memory `host_tab` (nullptr: skip); the root setup writes the other two.
+// Falls back to level_select above that size.
+constexpr int64_t kSelectFusedMax = 4096;
+void level_select_fused(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* ids,
+                        uint32_t* fcounts, int32_t* rank_of, FLevel* desc, int32_t* host_tab,
+                        int64_t tab_stride, hipStream_t s);
 void level_select(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* ids,
                   uint32_t* fcounts, int32_t* rank_of, int32_t* rank_acc, FLevel* desc,
                   hipStream_t s);
@@ -145,6 +161,8 @@ struct RootSetupArgs {
   int world;
   int my_rank;
   HostTrie h;  // level-1 nodes also go straight to the pinned host arrays (h.item == nullptr: off)
+  int32_t* host_tab;   // frequent-item ids | counts (tab_stride apart) to pinned host (or nullptr)
+  int64_t tab_stride;
 };
 void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s);
 // rank root classes by estimated cost (n_a^2 + 1 from the gram, desc) for the snake partition

@@ -747,6 +747,61 @@ __global__ __launch_bounds__(256) void k_select_rank(const uint32_t* __restrict_
   if (r) atomicAdd(&rank_acc[i], r);
 }
 
+__global__ __launch_bounds__(256) void k_prologue_init(uint32_t* __restrict__ cnt, int64_t n_items,
+                                                       uint64_t* __restrict__ bm, int64_t bm_words,
+                                                       FLevel* __restrict__ desc, int n_desc,
+                                                       FCtl* __restrict__ ctl, FCtl init) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = tid; i < n_items; i += nthr) cnt[i] = 0u;
+  for (int64_t i = tid; i < bm_words; i += nthr) bm[i] = 0ull;
+  const int64_t dwords = (int64_t)n_desc * (int64_t)(sizeof(FLevel) / 8);
+  for (int64_t i = tid; i < dwords; i += nthr) ((unsigned long long*)desc)[i] = 0ull;
+  if (tid == 0) *ctl = init;
+}
+
+// 16 lanes per item, each comparing against every 16th item (a one-thread-per-item loop ran
+// one wave per SIMD on 9 CUs: 113 µs at 2171 items); partial ranks meet in a 16-lane shuffle.
+__global__ __launch_bounds__(256) void k_select_fused(const uint32_t* __restrict__ cnt,
+                                                      int64_t n_items, uint32_t c1,
+                                                      int32_t* __restrict__ ids,
+                                                      uint32_t* __restrict__ fcounts,
+                                                      int32_t* __restrict__ rank_of, FLevel* desc,
+                                                      int32_t* __restrict__ host_tab,
+                                                      int64_t tab_stride) {
+  __shared__ unsigned int s_F;
+  __shared__ uint32_t s_c[kSelectFusedMax];  // the whole histogram (a global load per compare
+                                             // made the loop one memory latency per step)
+  if (threadIdx.x == 0) s_F = 0;
+  for (int64_t j = threadIdx.x; j < n_items; j += blockDim.x) s_c[j] = cnt[j];
+  __syncthreads();
+  const int p = threadIdx.x & 15;
+  const int64_t i = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const uint32_t ci = i < n_items ? s_c[i] : 0u;
+  int32_t r = 0;
+  if (i < n_items && ci >= c1) {
+    const int ii = (int)i;
+    for (int j = p; j < (int)n_items; j += 16) {
+      const uint32_t cj = s_c[j];
+      r += (cj >= c1 && (cj < ci || (cj == ci && j < ii))) ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) r += __shfl_xor(r, off, 16);
+  if (p == 0 && i < n_items) {
+    const bool f = ci >= c1;
+    rank_of[i] = f ? r : -1;
+    if (host_tab) host_tab[2 * tab_stride + i] = f ? r : -1;
+    if (f) {  // (ids/counts reach host_tab from the root setup, in rank order: coalesced)
+      ids[r] = (int32_t)i;
+      fcounts[r] = ci;
+      atomicAdd(&s_F, 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_F) atomicAdd((unsigned long long*)&desc[1].n_rows, (unsigned long long)s_F);
+}
+
 __global__ __launch_bounds__(256) void k_select_scatter(const uint32_t* __restrict__ cnt,
                                                         int64_t n_items, uint32_t c1,
                                                         const int32_t* __restrict__ rank_acc,
@@ -893,6 +948,10 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     a.out_count[i] = a.fcounts[i];
     a.out_depth[i] = 1;
     if (a.h.item) host_store(a.h, ctl, i, -1, a.ids[i], a.fcounts[i], 1);
+    if (a.host_tab) {
+      a.host_tab[i] = a.ids[i];
+      ((uint32_t*)a.host_tab)[a.tab_stride + i] = a.fcounts[i];
+    }
   }
 }
 
@@ -958,6 +1017,25 @@ void level_select(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* id
   hipLaunchKernelGGL(k_select_rank, dim3(nb, nb), dim3(256), 0, s, cnt, n_items, c1, rank_acc);
   hipLaunchKernelGGL(k_select_scatter, dim3(nb), dim3(256), 0, s, cnt, n_items, c1, rank_acc, ids,
                      fcounts, rank_of, desc);
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_prologue_init(uint32_t* cnt, int64_t n_items, uint64_t* bm, int64_t bm_words,
+                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl& init, hipStream_t s) {
+  const int64_t work = std::max<int64_t>(std::max<int64_t>(n_items, bm_words), 1);
+  const unsigned blocks = (unsigned)std::min<int64_t>((work + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_prologue_init, dim3(blocks), dim3(256), 0, s, cnt, n_items, bm, bm_words,
+                     desc, n_desc, ctl, init);
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_select_fused(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* ids,
+                        uint32_t* fcounts, int32_t* rank_of, FLevel* desc, int32_t* host_tab,
+                        int64_t tab_stride, hipStream_t s) {
+  if (n_items > kSelectFusedMax) throw std::runtime_error("level_select_fused: vocabulary too large");
+  const unsigned nb = (unsigned)((n_items + 15) / 16);
+  hipLaunchKernelGGL(k_select_fused, dim3(nb), dim3(256), 0, s, cnt, n_items, c1, ids, fcounts,
+                     rank_of, desc, host_tab, tab_stride);
   KMLS_HIP(hipGetLastError());
 }
 

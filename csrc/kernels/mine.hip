@@ -533,12 +533,22 @@ void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out
   KMLS_HIP(hipGetLastError());
 }
 
+namespace {
+int64_t gram_split_k(int64_t Wp, int64_t F_max) {
+  const int64_t nt = (F_max + kGT - 1) / kGT;
+  const int64_t blocks = nt * (nt + 1) / 2;
+  return std::max<int64_t>(1, std::min<int64_t>((1024 + blocks - 1) / blocks, Wp / 1024));
+}
+}  // namespace
+
+bool pair_gram_dev_needs_zero(int64_t Wp, int64_t F_max) { return gram_split_k(Wp, F_max) > 1; }
+
 void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, int64_t F_max,
                             uint32_t* out, hipStream_t s) {
   if (F_max < 2) return;
   const int64_t nt = (F_max + kGT - 1) / kGT;
   const int64_t blocks = nt * (nt + 1) / 2;
-  const int64_t ks = std::max<int64_t>(1, std::min<int64_t>((1024 + blocks - 1) / blocks, Wp / 1024));
+  const int64_t ks = gram_split_k(Wp, F_max);
   hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks, (unsigned)ks), dim3(kBlock), 0, s,
                      (const unsigned long long*)bm, Wp, F_max, nt, out, F_max, dF);
   KMLS_HIP(hipGetLastError());
