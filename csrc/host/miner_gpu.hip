@@ -190,6 +190,23 @@ struct Event {
 
 constexpr int64_t kCandCap = 32ll << 20;  // candidates per chunk
 
+// Host wait for a stream: hipStreamSynchronize, or a hipStreamQuery busy-poll with
+// KMLS_SPIN_SYNC=1 (measured: no gain on the headline step, so off by default).
+void sync_stream(hipStream_t s) {
+  static const bool spin = [] {
+    const char* e = std::getenv("KMLS_SPIN_SYNC");
+    return e && e[0] == '1';
+  }();
+  if (!spin) {
+    KMLS_HIP(hipStreamSynchronize(s));
+    return;
+  }
+  hipError_t e;
+  while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+  }
+  if (e != hipSuccess) KMLS_HIP(e);
+}
+
 // streamed-download mode of the fused levels: "deferred" (default) = each count launch carries
 // copy blocks that move the previous level's nodes to the host while its tiles compute;
 // "inline" = survivors are written to the host by the tile blocks themselves (every launch
@@ -494,10 +511,13 @@ struct MineRun {
   // kernels write every survivor straight into the pinned host arrays as well (no copy-out
   // kernel, no cross-stream event per level); level-1 nodes are written by the resident
   // prologue's root setup or were queued by stream_out() on the host-prepared path.
-  // deferred download: copy level L's children (nodes [desc[L].child_base, + desc[L+1].n_rows))
-  void copy_level(kern::FLevel* d_desc, kern::FCtl* d_ctl, int L) {
+  // end of a level batch: the deferred download of level L's children (nodes
+  // [desc[L].child_base, + desc[L+1].n_rows)) and the descriptor readback, in one launch
+  void finish_batch(kern::FLevel* d_desc, kern::FCtl* d_ctl, int L, bool deferred, void* h_back,
+                    size_t back_bytes) {
     kern::level_copyout(&d_desc[L], &d_desc[L + 1], d_ctl, out_parent.p, out_item.p, out_count.p,
-                        out_depth.p, ht, s);
+                        out_depth.p, deferred ? ht : kern::HostTrie{}, d_desc, h_back, back_bytes,
+                        s);
   }
 
   bool levels_loop(kern::FLevel* d_desc, kern::FCtl* d_ctl, int64_t out_cap) {
@@ -541,10 +561,14 @@ struct MineRun {
         count_level(L);
         last = L;
       }
-      if (deferred) copy_level(d_desc, d_ctl, last);  // the last launch's children
-      KMLS_HIP(hipMemcpyAsync(b_desc, d_desc, kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl),
-                              hipMemcpyDeviceToHost, s));
-      KMLS_HIP(hipStreamSynchronize(s));
+      // d_ctl directly follows d_desc (kMaxLv * 128 bytes, arena alignment 256)
+      if ((char*)d_ctl != (char*)(d_desc + kMaxLv))
+        throw std::logic_error("levels_loop: control block must follow the descriptors");
+      finish_batch(d_desc, d_ctl, last, deferred, b_desc,
+                   (kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl) + 15) & ~(size_t)15);
+      t_presync = std::chrono::steady_clock::now();
+      sync_stream(s);
+      t_postsync = std::chrono::steady_clock::now();
       if (b_ctl->overflow) {
         ok = false;
         fallback_reason = "device overflow code " + std::to_string(b_ctl->overflow) +
@@ -585,6 +609,7 @@ struct MineRun {
     return true;
   }
   std::vector<kern::FLevel> last_desc;  // host copy of the descriptors after levels_loop
+  std::chrono::steady_clock::time_point t_presync, t_postsync;  // host-side profile
 
   int64_t fast_hint = 0;
   std::string fallback_reason;
@@ -1075,6 +1100,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   init.bump_base = bump_base;
   init.bump_cap = bump_bytes;
   init.status_cap = (unsigned long long)out_->status_cap;
+  const auto t_launch = std::chrono::steady_clock::now();
   kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl, init, s);
   kern::item_support(d_items_, nnz_, (int32_t)I, d_cnt, s);
   // frequent-item tables for the frequent() API (ids | counts | rank_of, tab_stride apart)
@@ -1148,6 +1174,14 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   KMLS_HIP(hipStreamSynchronize(out_->copy_s));
   res.phases.push_back({"prologue(support+select+encode+gram)", elapsed(e0, e1)});
   res.phases.push_back({"levels", elapsed(e1, e2)});
+  {  // host-side profile (ms): before the first launch, enqueue until the sync, after the sync
+    const auto t_end = std::chrono::steady_clock::now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    res.phases.push_back({"host_pre_launch", ms(t0, t_launch)});
+    res.phases.push_back({"host_enqueue_to_sync", ms(t_launch, run.t_presync)});
+    res.phases.push_back({"host_sync_wait", ms(run.t_presync, run.t_postsync)});
+    res.phases.push_back({"host_post_sync", ms(run.t_postsync, t_end)});
+  }
   res.stats.n_frequent_items = F;
   // level-1 nodes are replicated on every rank of a partition; rank 0 counts them
   res.stats.n_itemsets = (part_world > 1 && part_rank != 0) ? N - F : N;

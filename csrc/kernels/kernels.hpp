@@ -176,11 +176,13 @@ int64_t level_scan_tile();
 void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status,
                 unsigned epoch, int64_t Wp, int64_t out_cap, int32_t* tile_row, int grid,
                 hipStream_t s);
-// side-stream download: trie nodes [lv->child_base, +nx->n_rows) (one finished level) from the
-// device trie arrays into the pinned host trie (widths per HostTrie)
+// trie nodes [lv->child_base, +nx->n_rows) (the last launched level's children) from the device
+// trie arrays into the pinned host trie (h.item == nullptr: skip), plus an optional readback of
+// rb_bytes (multiple of 16) from rb_src to pinned rb_dst
 void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t* d_parent,
                    const int32_t* d_item, const uint32_t* d_count, const uint8_t* d_depth,
-                   const HostTrie& h, hipStream_t s);
+                   const HostTrie& h, const void* rb_src, void* rb_dst, size_t rb_bytes,
+                   hipStream_t s);
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
                  const LevelCountArgs& a, const int32_t* tile_row, int grid, hipStream_t s);
 

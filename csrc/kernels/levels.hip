@@ -704,14 +704,22 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
 // ---------------------------------------------------------------------------------------------
 // Deferred-download tail: the last launched level's children have no following count launch to
 // carry them, so this copies trie nodes [lv->child_base, + nx->n_rows) after the level loop.
+// The last block also copies the level descriptors + control block (`rb_words` 16-byte words
+// from rb_src) to pinned host memory: the host's one readback per call, without a
+// hipMemcpyAsync (whose host-side cost dominated the step's idle gap).
 __global__ __launch_bounds__(kBlock) void k_level_copyout(const FLevel* __restrict__ lv,
                                                           const FLevel* __restrict__ nx, FCtl* ctl,
                                                           const int64_t* __restrict__ d_parent,
                                                           const int32_t* __restrict__ d_item,
                                                           const uint32_t* __restrict__ d_count,
                                                           const uint8_t* __restrict__ d_depth,
-                                                          HostTrie h) {
-  if (ctl->overflow) return;
+                                                          HostTrie h, const uint4* __restrict__ rb_src,
+                                                          uint4* __restrict__ rb_dst, int rb_words) {
+  if (rb_dst && blockIdx.x == gridDim.x - 1) {
+    for (int i = threadIdx.x; i < rb_words; i += blockDim.x) rb_dst[i] = rb_src[i];
+    return;
+  }
+  if (!h.item || ctl->overflow) return;
   const int64_t base = lv->child_base;
   const int64_t S = nx->n_rows;
   if (S <= 0) return;
@@ -1002,9 +1010,12 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
 
 void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t* d_parent,
                    const int32_t* d_item, const uint32_t* d_count, const uint8_t* d_depth,
-                   const HostTrie& h, hipStream_t s) {
-  hipLaunchKernelGGL(k_level_copyout, dim3(128), dim3(kBlock), 0, s, lv, nx, ctl, d_parent, d_item,
-                     d_count, d_depth, h);
+                   const HostTrie& h, const void* rb_src, void* rb_dst, size_t rb_bytes,
+                   hipStream_t s) {
+  if (rb_bytes % 16) throw std::runtime_error("level_copyout: readback size not a multiple of 16");
+  hipLaunchKernelGGL(k_level_copyout, dim3(rb_dst ? 129 : 128), dim3(kBlock), 0, s, lv, nx, ctl,
+                     d_parent, d_item, d_count, d_depth, h, (const uint4*)rb_src, (uint4*)rb_dst,
+                     (int)(rb_bytes / 16));
   KMLS_HIP(hipGetLastError());
 }
 
