@@ -147,6 +147,7 @@ struct OutBufs {
   int64_t status_cap = 1 << 20;  // tiles per launch (256M candidates / 2G rows)
   unsigned epoch = 0;
   int depth_hint = 6;            // levels enqueued before the first completion check
+  std::vector<int64_t> cand_hint;  // candidates per level in the previous call (kernel choice)
   OutBufs() {
     KMLS_HIP(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
     // device-scope release: a cross-stream fork needs no system-scope L2 writeback
@@ -436,7 +437,7 @@ struct MineRun {
     constexpr int kMaxLv = 64;
     const int64_t Fr = root.n;
     const size_t mark = arena->mark();
-    const int64_t row_bytes = Wp * 8 + 4 + 8 + 4 + 4 + 8;  // child bitmap + rank + gid + prow + slot + pos
+    const int64_t row_bytes = Wp * 8 + 4 + 8 + 4 + 4;  // child bitmap + rank + gid + prow + slot
     const size_t root_need = (size_t)(root_total + 1) * (size_t)row_bytes + (size_t)(Fr + 1) * 8 +
                              kMaxLv * sizeof(kern::FLevel) + 4096;
     const size_t free_b = arena->capacity() - arena->used();
@@ -456,7 +457,7 @@ struct MineRun {
     kern::FLevel* d_desc = (kern::FLevel*)arena->push(kMaxLv * sizeof(kern::FLevel));
     kern::FCtl* d_ctl = (kern::FCtl*)arena->push(sizeof(kern::FCtl));
     int64_t* d_off = (int64_t*)arena->push((size_t)(Fr + 1) * 8);
-    int64_t* d_pos = (int64_t*)arena->push((size_t)(root_total + 1) * 8);
+    int64_t* d_rend = (int64_t*)arena->push((size_t)(Fr + 1) * 8);
     uint64_t* c_bm = (uint64_t*)arena->push((size_t)((std::max<int64_t>(root_total, 1) + 63) & ~63ll) * Wp * 8);
     int32_t* c_rank = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
     int64_t* c_gid = (int64_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 8);
@@ -486,7 +487,7 @@ struct MineRun {
     r.gid = root.gid;
     r.cand_off = d_off;
     r.n_cand = root_total;
-    r.pos = d_pos;
+    r.row_end = d_rend;
     r.child_base = out_size;
     h_desc[2].bm = c_bm;
     h_desc[2].rank = c_rank;
@@ -543,8 +544,9 @@ struct MineRun {
                              out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1),
                              stream_dl ? ht : kern::HostTrie{},
                              L == trace_level ? d_trace : nullptr, deferred};
+      const int64_t hint = L < (int)ob->cand_hint.size() ? ob->cand_hint[L] : -1;
       kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a,
-                        L == 1 ? nullptr : ob->tile_row, grid, s);
+                        L == 1 ? nullptr : ob->tile_row, grid, hint, s);
     };
     const int L_allowed = std::min(kMaxLv - 2, max_len ? max_len - 1 : kMaxLv - 2);
     count_level(1);
@@ -596,6 +598,8 @@ struct MineRun {
     }
     if (!ok) return false;
     last_desc.assign(b_desc, b_desc + kMaxLv);
+    ob->cand_hint.assign((size_t)last + 1, -1);
+    for (int L = 1; L <= last; ++L) ob->cand_hint[L] = b_desc[L].n_cand;
     const int64_t new_size = b_desc[last + 1].child_base;
     for (int L = 1; L <= last; ++L)
       if (b_desc[L + 1].n_rows > 0) max_depth = std::max(max_depth, L + 1);

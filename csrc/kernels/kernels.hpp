@@ -73,7 +73,8 @@ struct FLevel {  // device-resident descriptor of one level (rows = itemsets of 
   const int32_t* prow;     // row in the parent level
   int64_t* cand_off;       // [n_rows + 1]
   int64_t n_cand;
-  int64_t* pos;            // [n_cand + 1] survivor index of each candidate
+  int64_t* row_end;        // [n_rows] child-level index one past each row's children (rows
+                           // with candidates only): the next scan's class ends
   int64_t child_base;      // trie id of this level's first child
   unsigned int scan_ticket, count_ticket;
   // row → bitmap row (nullptr: identity).  The short-row count kernel writes each candidate's
@@ -183,8 +184,11 @@ void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t*
                    const int32_t* d_item, const uint32_t* d_count, const uint8_t* d_depth,
                    const HostTrie& h, const void* rb_src, void* rb_dst, size_t rb_bytes,
                    hipStream_t s);
+// cand_hint: expected candidate count of the level (the previous call's; -1 unknown) — picks
+// the register/latency trade-off of the short-row kernel, never affects results
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
-                 const LevelCountArgs& a, const int32_t* tile_row, int grid, hipStream_t s);
+                 const LevelCountArgs& a, const int32_t* tile_row, int grid, int64_t cand_hint,
+                 hipStream_t s);
 
 // ---- persistent DFS (dfs_persistent.hip) ----
 struct DfsTask {

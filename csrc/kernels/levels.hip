@@ -242,8 +242,7 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
   // 2048 of them per launch cost more than a small level's whole scan.
   if ((int64_t)blockIdx.x >= n_tiles) return;
   const int32_t* __restrict__ prow = lv->prow;
-  const int64_t* __restrict__ pco = pv->cand_off;
-  const int64_t* __restrict__ ppos = pv->pos;
+  const int64_t* __restrict__ pend = pv->row_end;
   int64_t* __restrict__ co = lv->cand_off;
   for (bool first = true;; first = false) {
     const int64_t t = next_tile(&lv->scan_ticket, first, n_tiles, &s_ticket, (int64_t)gridDim.x);
@@ -256,8 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
       const int64_t s = s0 + i;
       int64_t l = 0;
       if (s < n) {
-        const int64_t a = prow[s];
-        l = ppos[pco[a + 1]] - s - 1;  // siblings after s in its class
+        l = pend[prow[s]] - s - 1;  // siblings after s in its class
       }
       len[i] = l;
       sum += l;
@@ -292,11 +290,12 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
       } else if (total > 0) {
         const unsigned long long T = (unsigned long long)total;
         const unsigned long long T64 = (T + 63ull) & ~63ull;  // 64-interleaved candidate rows
-        const unsigned long long sz[6] = {(T + 1) * 8ull, T64 * (unsigned long long)Wp * 8ull, T * 4ull,
+        const unsigned long long sz[6] = {(unsigned long long)n * 8ull,
+                                          T64 * (unsigned long long)Wp * 8ull, T * 4ull,
                                           T * 8ull, T * 4ull, T * 4ull};
         void* p[6];
         bump_n<6>(ctl, sz, p);
-        lv->pos = (int64_t*)p[0];
+        lv->row_end = (int64_t*)p[0];
         nx->bm = (const uint64_t*)p[1];
         nx->rank = (const int32_t*)p[2];
         nx->gid = (const int64_t*)p[3];
@@ -348,7 +347,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   const unsigned long long* __restrict__ bm = (const unsigned long long*)lv->bm;
   const int32_t* __restrict__ rank = lv->rank;
   const int64_t* __restrict__ gid = lv->gid;
-  int64_t* __restrict__ pos = lv->pos;
+  int64_t* __restrict__ row_end = lv->row_end;
   unsigned long long* __restrict__ cbm = (unsigned long long*)nx->bm;
   int32_t* __restrict__ crank = (int32_t*)nx->rank;
   int64_t* __restrict__ cgid = (int64_t*)nx->gid;
@@ -390,9 +389,10 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
     for (int64_t i = threadIdx.x; i < nw; i += kBlock) s_off[i] = co[r0 + i];
     __syncthreads();
     // one decode per candidate, shared by the count and materialise phases
+    bool row_last = false;  // this thread's candidate is the last of its row
     if ((int)threadIdx.x < cn) {
       const int64_t c = c0 + threadIdx.x;
-      int64_t a, oa;
+      int64_t a, oa, ob;
       if (nw >= 2 && s_off[nw - 1] > c) {  // row in window: largest k < nw-1 with s_off[k] <= c
         int64_t lo = 0, hi = nw - 1;
         while (hi - lo > 1) {
@@ -401,10 +401,13 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
         }
         a = r0 + lo;
         oa = s_off[lo];
+        ob = s_off[lo + 1];
       } else {
         a = find_row_g(co, r0, n_rows, c);
         oa = co[a];
+        ob = co[a + 1];
       }
+      row_last = c + 1 == ob;
       s_a[threadIdx.x] = a;
       s_b[threadIdx.x] = a + 1 + (c - oa);
     }
@@ -454,7 +457,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
     __syncthreads();
     const int64_t base = s_base;
     if ((int)threadIdx.x < cn) {
-      pos[c0 + threadIdx.x] = base + lx;
+      if (row_last) row_end[s_a[threadIdx.x]] = base + lx + flag;
       if (flag) {  // per-survivor scalars: one thread each
         const int64_t a = s_a[threadIdx.x], b = s_b[threadIdx.x];
         const int64_t s = base + lx;
@@ -490,7 +493,6 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
     }
     if (t == n_tiles - 1 && threadIdx.x == 0) {
       const int64_t S = base + tile_total;
-      pos[n_cand] = S;
       nx->n_rows = S;
       nx->child_base = child_base + S;
       nx->cand_off = (int64_t*)bump(ctl, (unsigned long long)(S + 1) * 8ull);
@@ -519,6 +521,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
 // Decode, look-back, trie/host writes and the tile→row map are shared with k_level_count.
 constexpr int kSmallChunks = 32;
 
+template <int KB>
 __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict__ lv,
                                                               FLevel* __restrict__ nx, FCtl* ctl,
                                                               unsigned long long* __restrict__ status,
@@ -554,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
   const int32_t* __restrict__ slot = lv->slot;
   const int32_t* __restrict__ rank = lv->rank;
   const int64_t* __restrict__ gid = lv->gid;
-  int64_t* __restrict__ pos = lv->pos;
+  int64_t* __restrict__ row_end = lv->row_end;
   ulonglong2* __restrict__ cbm2 = (ulonglong2*)nx->bm;
   int32_t* __restrict__ crank = (int32_t*)nx->rank;
   int64_t* __restrict__ cgid = (int64_t*)nx->gid;
@@ -595,10 +598,11 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
     // ---- decode + phase 1: one thread per candidate, AND row written in place ----
     uint32_t k = 0;
     int64_t a = 0, b = 0;
+    bool row_last = false;  // this thread's candidate is the last of its row
     const bool live = (int)threadIdx.x < cn;
     const int64_t c = c0 + threadIdx.x;
     if (live) {
-      int64_t oa;
+      int64_t oa, ob;
       if (nw >= 2 && s_off[nw - 1] > c) {
         int64_t lo = 0, hi = nw - 1;
         while (hi - lo > 1) {
@@ -607,10 +611,13 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
         }
         a = r0 + lo;
         oa = s_off[lo];
+        ob = s_off[lo + 1];
       } else {
         a = find_row_g(co, r0, n_rows, c);
         oa = co[a];
+        ob = co[a + 1];
       }
+      row_last = c + 1 == ob;
       b = a + 1 + (c - oa);
       const bool need_row = A.gram ? (k = A.gram[a * A.F + b]) >= A.minsup : true;
       if (need_row) {
@@ -630,8 +637,10 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
         }
         ulonglong2* __restrict__ z = cbm2 + ((c >> 6) * n2 << 6) + (c & 63);
         // batches of kB chunk pairs: all loads of a batch are issued before its stores (a
-        // load/store-interleaved loop compiles to one full memory round trip per chunk)
-        constexpr int kB = 6;
+        // load/store-interleaved loop compiles to one full memory round trip per chunk).  KB
+        // trades registers (occupancy, for the big levels) against round trips per candidate
+        // (the latency of the small ones)
+        constexpr int kB = KB;
         uint32_t kk = 0;
         for (int w0 = 0; w0 < n2; w0 += kB) {
           ulonglong2 u[kB], v[kB];
@@ -665,7 +674,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
     if (tr) tr[3] = wall_clock64();
     const int64_t base = s_base;
     if (live) {
-      pos[c] = base + lx;
+      if (row_last) row_end[a] = base + lx + flag;
       if (flag) {
         const int64_t s = base + lx;
         const int32_t rb = rank[b];
@@ -686,7 +695,6 @@ __global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict
     if (tr) tr[4] = wall_clock64();
     if (t == n_tiles - 1 && threadIdx.x == 0) {
       const int64_t S = base + tile_total;
-      pos[n_cand] = S;
       nx->n_rows = S;
       nx->child_base = child_base + S;
       nx->cand_off = (int64_t*)bump(ctl, (unsigned long long)(S + 1) * 8ull);
@@ -933,11 +941,12 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     } else if (n_cand > 0) {
       const unsigned long long T = (unsigned long long)n_cand;
       const unsigned long long T64 = (T + 63ull) & ~63ull;  // 64-interleaved candidate rows
-      const unsigned long long sz[6] = {(T + 1) * 8ull, T64 * (unsigned long long)a.Wp * 8ull, T * 4ull,
+      const unsigned long long sz[6] = {(unsigned long long)F * 8ull,
+                                        T64 * (unsigned long long)a.Wp * 8ull, T * 4ull,
                                         T * 8ull, T * 4ull, T * 4ull};
       void* p[6];
       bump_n<6>(ctl, sz, p);
-      r.pos = (int64_t*)p[0];
+      r.row_end = (int64_t*)p[0];
       desc[2].bm = (const uint64_t*)p[1];
       desc[2].rank = (const int32_t*)p[2];
       desc[2].gid = (const int64_t*)p[3];
@@ -985,7 +994,8 @@ void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long lon
 }
 
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
-                 const LevelCountArgs& a, const int32_t* tile_row, int grid, hipStream_t s) {
+                 const LevelCountArgs& a, const int32_t* tile_row, int grid, int64_t cand_hint,
+                 hipStream_t s) {
   if (a.deferred_dl) grid += kCopyBlocks;
   static const bool small_ok = [] {
     const char* e = std::getenv("KMLS_COUNT_SMALL");
@@ -993,8 +1003,14 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
   }();
   const int64_t n2 = a.Wp >> 1;
   if (small_ok && n2 >= 1 && n2 <= kSmallChunks) {
-    hipLaunchKernelGGL(k_level_count_small, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status,
-                       epoch, a, tile_row);
+    // a level expected to be small (the previous call's size: steady-state re-mining) is
+    // latency-bound: load each candidate's whole row pair in one batch
+    if (cand_hint >= 0 && cand_hint <= 64 * kTile && n2 <= 18)
+      hipLaunchKernelGGL(k_level_count_small<18>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl,
+                         status, epoch, a, tile_row);
+    else
+      hipLaunchKernelGGL(k_level_count_small<6>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl,
+                         status, epoch, a, tile_row);
     KMLS_HIP(hipGetLastError());
     return;
   }
