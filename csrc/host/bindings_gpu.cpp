@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include "kmls/gpu.hpp"
+#include "kmls/trace.hpp"
 
 namespace py = pybind11;
 
@@ -70,6 +71,9 @@ using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 
 void register_gpu_bindings(py::module_& m) {
   m.def("gpu_available", &gpu::available);
+  m.def("roctx_enabled", &trace::enabled);
+  m.def("roctx_push", [](const std::string& n) { trace::push(n.c_str()); });
+  m.def("roctx_pop", &trace::pop);
   m.def("gpu_device_count", &gpu::device_count);
   m.def("gpu_device_name", &gpu::device_name);
 

@@ -20,6 +20,7 @@
 
 #include "../kernels/kernels.hpp"
 #include "kmls/gpu.hpp"
+#include "kmls/trace.hpp"
 
 #define KMLS_HIP(expr)                                                                  \
   do {                                                                                  \
@@ -720,7 +721,19 @@ size_t default_arena_bytes() {
     const double gb = std::atof(e);
     if (gb > 0) return std::min(free_b - (free_b >> 4), (size_t)(gb * (1ull << 30)));
   }
-  // half of free HBM by default (the other half stays with torch / RCCL buffers)
+  if (const char* e = std::getenv("KMLS_ARENA_INIT_MB")) {  // initial size of a growing arena
+    const double mb = std::atof(e);
+    if (mb > 0) return std::min(free_b / 2, (size_t)(mb * (1 << 20)));
+  }
+  // 8 GiB by default: hipMalloc maps HBM eagerly (~10 ms/GiB), and a job's one-shot mining
+  // call should not pay for half of a 288 GB card.  The arena grows on demand (grow_arena) up to
+  // half of the free HBM (the other half stays with torch / RCCL buffers).
+  return std::min(free_b / 2, (size_t)8 << 30);
+}
+
+size_t max_arena_bytes() {
+  size_t free_b = 0, total_b = 0;
+  KMLS_HIP(hipMemGetInfo(&free_b, &total_b));
   return free_b / 2;
 }
 
@@ -743,6 +756,8 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
     stream_ = (void*)s;
     own_stream_ = true;
   }
+  arena_auto_ = arena_bytes == 0 && !std::getenv("KMLS_ARENA_GB");
+  if (arena_auto_) arena_max_ = max_arena_bytes();
   arena_ = std::make_unique<DeviceArena>(arena_bytes ? arena_bytes : default_arena_bytes());
   pinned_ = make_pinned_pool();
   KMLS_HIP(hipHostMalloc((void**)&abort_host_, 64, hipHostMallocMapped));
@@ -771,6 +786,25 @@ GpuMiner::~GpuMiner() {
 }
 
 size_t GpuMiner::arena_capacity() const { return arena_->capacity(); }
+
+bool GpuMiner::grow_arena(size_t min_bytes) {
+  if (!arena_auto_ || arena_->used() != 0) return false;
+  const size_t cap = arena_->capacity();
+  if (cap >= arena_max_) return false;
+  const size_t want = std::min(arena_max_, std::max(min_bytes, cap * 4));
+  KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_));
+  arena_.reset();
+  arena_ = std::make_unique<DeviceArena>(want);
+  return true;
+}
+
+namespace {
+// a fused-path failure that more arena would fix (bump region or arena sizing), not a data limit
+bool arena_limited(const std::string& why) {
+  return why.empty() || why.find("overflow code 1") != std::string::npos ||
+         why.find("arena") != std::string::npos;
+}
+}  // namespace
 
 void GpuMiner::synchronize() { KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_)); }
 
@@ -1026,6 +1060,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
 bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res, int part_rank,
                              int part_world) {
   hipStream_t s = (hipStream_t)stream_;
+  trace::Range rg_call("kmls.mine_resident");
   auto t0 = std::chrono::steady_clock::now();
   const int64_t I = n_items_;
   const int64_t Wp = words_local();
@@ -1105,6 +1140,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   init.bump_cap = bump_bytes;
   init.status_cap = (unsigned long long)out_->status_cap;
   const auto t_launch = std::chrono::steady_clock::now();
+  trace::push("kmls.prologue(enqueue)");
   kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl, init, s);
   kern::item_support(d_items_, nnz_, (int32_t)I, d_cnt, s);
   // frequent-item tables for the frequent() API (ids | counts | rank_of, tab_stride apart)
@@ -1135,7 +1171,12 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   if (!fused_select)  // staged to pinned memory while the levels run
     KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));
   KMLS_HIP(hipEventRecord(e1.e, s));
-  const bool ok = run.levels_loop(d_desc, d_ctl, out_cap);
+  trace::pop();
+  bool ok;
+  {
+    trace::Range rg("kmls.levels");
+    ok = run.levels_loop(d_desc, d_ctl, out_cap);
+  }
   if (!ok) {
     fused_fallback_ = run.fallback_reason;
     arena_->pop_to(mark);
@@ -1211,8 +1252,11 @@ GpuMineResult GpuMiner::mine_partition(const MineConfig& cfg, bool download, int
   GpuMineResult r;
   if (!resident_ok(cfg))
     throw std::runtime_error("mine_partition: data not eligible for the device-resident path");
-  if (!mine_resident(cfg, download, r, rank, world))
-    throw std::runtime_error("mine_partition: fused path overflowed (" + fused_fallback_ + ")");
+  if (!mine_resident(cfg, download, r, rank, world)) {
+    const bool retry = arena_limited(fused_fallback_) && grow_arena(0);
+    if (!retry || !mine_resident(cfg, download, r, rank, world))
+      throw std::runtime_error("mine_partition: fused path overflowed (" + fused_fallback_ + ")");
+  }
   return r;
 }
 
@@ -1223,6 +1267,10 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download) {
   if (resident_ok(cfg)) {
     GpuMineResult r;
     if (mine_resident(cfg, download, r, 0, 1)) return r;
+    if (arena_limited(fused_fallback_) && grow_arena(0)) {  // retry once with a bigger arena
+      fused_fallback_.clear();
+      if (mine_resident(cfg, download, r, 0, 1)) return r;
+    }
   }
   auto t0 = std::chrono::steady_clock::now();
   Event e0, e1, e2;

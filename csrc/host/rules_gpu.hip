@@ -10,6 +10,7 @@
 
 #include "../kernels/kernels.hpp"
 #include "kmls/gpu.hpp"
+#include "kmls/trace.hpp"
 
 #define KMLS_HIP(expr)                                                                  \
   do {                                                                                  \
@@ -35,6 +36,7 @@ RuleSet association_rules_gpu(int device, const int64_t* parent, const int32_t* 
                               const uint32_t* count, const uint8_t* depth, int64_t n, int64_t n_tx,
                               RuleMetric metric, double min_threshold, int max_antecedent,
                               double* kernel_ms) {
+  trace::Range rg_("kmls.rules_gpu");
   RuleSet out;
   if (n == 0 || n_tx == 0) return out;
   KMLS_CHECK(n < (1ll << 31) - 1, "GPU rules: trie larger than 2^31 nodes");
@@ -136,6 +138,7 @@ RuleSet association_rules_gpu(int device, const int64_t* parent, const int32_t* 
 
 CSR group_to_csr_gpu(int device, const int32_t* keys, const int32_t* vals, int64_t n,
                      int32_t n_keys, bool dedup) {
+  trace::Range rg_("kmls.groupby_gpu");
   KMLS_CHECK(n < (1ll << 31), "GPU group-by: more than 2^31 rows per call");
   KMLS_HIP(hipSetDevice(device));
   hipStream_t s;

@@ -175,6 +175,11 @@ class GpuMiner {
   int n_cus_ = 256;
   bool mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res, int part_rank,
                      int part_world);
+  // default-sized arenas start at 8 GiB and grow (x4, up to arena_max_) when the fused path
+  // runs out of room; false if fixed-size, busy or already at the maximum
+  bool grow_arena(size_t min_bytes);
+  bool arena_auto_ = false;
+  size_t arena_max_ = 0;
   std::string fused_fallback_;
   std::unique_ptr<OutBufs> out_;  // output trie kept allocated across mine() calls
   Comm* comm_ = nullptr;          // set during mine_txdp: level counts are all-reduced

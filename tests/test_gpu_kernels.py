@@ -403,3 +403,19 @@ def test_pair_rows_gpu_world1(gpu_mod, mode):
     G = (X[:, ids].T @ X[:, ids]).astype(np.int64)
     assert (r0, r1) == (0, len(ids))
     np.testing.assert_array_equal(rows.astype(np.int64), G)
+
+
+def test_default_arena_grows_on_demand(gpu_mod, monkeypatch):
+    """A default-sized arena starts small (KMLS_ARENA_INIT_MB here; 8 GiB normally) and grows
+    when the device-resident path runs out of room, instead of falling back or failing."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    monkeypatch.setenv("KMLS_ARENA_INIT_MB", "520")
+    tx = generate("ds2", seed=3)
+    g = gpu_mod.GpuMiner(0)
+    assert g.arena_capacity < (600 << 20)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    r = g.mine(0.05)
+    assert r["stats"]["levels_path"] == "fused-resident", r["stats"]
+    assert g.arena_capacity >= (2000 << 20)
+    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.05)
+    assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
