@@ -779,6 +779,7 @@ GpuMiner::~GpuMiner() {
   if (d_own_bm_) (void)hipFree(d_own_bm_);
   if (abort_host_) (void)hipHostFree(abort_host_);
   if (h_scalar_) (void)hipHostFree(h_scalar_);
+  if (sup_scratch_) (void)hipFree(sup_scratch_);
   if (d_pair_) (void)hipFree(d_pair_);
   out_.reset();
   arena_.reset();
@@ -786,6 +787,30 @@ GpuMiner::~GpuMiner() {
 }
 
 size_t GpuMiner::arena_capacity() const { return arena_->capacity(); }
+
+// Per-item supports (accumulated into `counts`): the partitioned histogram for large
+// vocabularies and inputs (kern::item_support_partitioned, scratch owned by the miner), else the
+// LDS/hash kernels.  KMLS_SUPPORT_PARTITIONED=0 forces the latter (A/B).
+void GpuMiner::support_counts(const int32_t* items, int64_t nnz, uint32_t* counts, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  static const bool partitioned = [] {
+    const char* e = std::getenv("KMLS_SUPPORT_PARTITIONED");
+    return !(e && e[0] == '0');
+  }();
+  const size_t need = partitioned && nnz >= (4ll << 20) ? kern::support_scratch_bytes(nnz, n_items_) : 0;
+  if (need) {
+    if (need > sup_scratch_bytes_) {
+      if (sup_scratch_) KMLS_HIP(hipFree(sup_scratch_));
+      sup_scratch_ = nullptr;
+      KMLS_HIP(hipMalloc(&sup_scratch_, need));
+      sup_scratch_bytes_ = need;
+    }
+    if (kern::item_support_partitioned(items, nnz, (int32_t)n_items_, counts, sup_scratch_,
+                                       sup_scratch_bytes_, s))
+      return;
+  }
+  kern::item_support(items, nnz, (int32_t)n_items_, counts, s);
+}
 
 bool GpuMiner::grow_arena(size_t min_bytes) {
   if (!arena_auto_ || arena_->used() != 0) return false;
@@ -846,7 +871,7 @@ void GpuMiner::item_support(uintptr_t counts_dev) {
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
   KMLS_HIP(hipMemsetAsync((void*)counts_dev, 0, (size_t)n_items_ * sizeof(uint32_t), s));
-  kern::item_support(d_items_, nnz_, (int32_t)n_items_, (uint32_t*)counts_dev, s);
+  support_counts(d_items_, nnz_, (uint32_t*)counts_dev, s);
 }
 
 int64_t GpuMiner::select(const uint32_t* global_counts, int64_t global_n_tx, double min_support) {
@@ -1142,7 +1167,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   const auto t_launch = std::chrono::steady_clock::now();
   trace::push("kmls.prologue(enqueue)");
   kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl, init, s);
-  kern::item_support(d_items_, nnz_, (int32_t)I, d_cnt, s);
+  support_counts(d_items_, nnz_, d_cnt, s);
   // frequent-item tables for the frequent() API (ids | counts | rank_of, tab_stride apart)
   std::shared_ptr<void> fstage = pinned_->get((size_t)tab_stride * 12);
   const uint32_t c1 = level1_threshold((uint64_t)n_tx_, cfg.min_support);
@@ -1327,7 +1352,7 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
   for (int k = 0; k < K; ++k) {
     const int64_t a = tile_nnz_[(size_t)(64 * k / K)], b = tile_nnz_[(size_t)(64 * (k + 1) / K)];
     uint32_t* part = d_part + (size_t)k * (size_t)std::max<int64_t>(n_items_, 1);
-    kern::item_support(d_items_ + a, b - a, (int32_t)n_items_, part, s);
+    support_counts(d_items_ + a, b - a, part, s);
     KMLS_HIP(hipEventRecord(evs[(size_t)k], s));
     KMLS_HIP(hipStreamWaitEvent(cs, evs[(size_t)k], 0));
     if (comm) comm->all_reduce(part, part, (size_t)n_items_, CommDtype::U32, false, cs);

@@ -178,6 +178,9 @@ class GpuMiner {
   // default-sized arenas start at 8 GiB and grow (x4, up to arena_max_) when the fused path
   // runs out of room; false if fixed-size, busy or already at the maximum
   bool grow_arena(size_t min_bytes);
+  void support_counts(const int32_t* items, int64_t nnz, uint32_t* counts, void* stream);
+  void* sup_scratch_ = nullptr;  // partitioned-histogram scratch (grown on demand)
+  size_t sup_scratch_bytes_ = 0;
   bool arena_auto_ = false;
   size_t arena_max_ = 0;
   std::string fused_fallback_;

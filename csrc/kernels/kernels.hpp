@@ -11,6 +11,12 @@ namespace kern {
 // ---- mining (mine.hip) ----
 void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* counts,
                   hipStream_t s);
+// partitioned histogram for large vocabularies (16384 < n_items <= 2M): no per-item global
+// atomics; needs support_scratch_bytes() of device scratch (0 → not applicable).  Returns false
+// (nothing launched) when it does not apply.
+size_t support_scratch_bytes(int64_t nnz, int64_t n_items);
+bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* counts,
+                              void* scratch, size_t scratch_bytes, hipStream_t s);
 void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                    const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
                    hipStream_t s);

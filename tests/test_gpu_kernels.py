@@ -419,3 +419,19 @@ def test_default_arena_grows_on_demand(gpu_mod, monkeypatch):
     assert g.arena_capacity >= (2000 << 20)
     c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.05)
     assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
+
+
+@pytest.mark.parametrize("T,I", [(100_000, 1_000_000), (300_000, 1_012_345), (200_000, 40_000)])
+def test_support_histograms_large_vocab(gpu_mod, T, I):
+    """Both large-vocabulary support paths against np.bincount: the LDS-hash kernel (nnz < 4M)
+    and the partitioned histogram (nnz >= 4M; vocabulary sizes not a multiple of 32768)."""
+    import torch
+    ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 7)
+    g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
+    g.load_csr(ptr, items, I)
+    cnt = torch.zeros(I, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    g.item_support(cnt.data_ptr())
+    g.synchronize()
+    np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32),
+                                  np.bincount(items, minlength=I))
