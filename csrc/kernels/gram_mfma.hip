@@ -5,8 +5,8 @@
 // v_mfma_i32_32x32x32_i8 (gfx950): lane l (r = l&31, h = l>>5) supplies A[row r][k = 16h + j]
 // and B[k = 16h + j][col r], j = 0..15, as 16 int8 in 4 VGPRs; C/D (16 i32 / lane):
 // col = l&31, row = (reg&3) + 8*(reg>>2) + 4*h.  Bits are unpacked to int8 in registers
-// (4 bits → one dword: ((n * 0x00204081) & 0x01010101)), so HBM/L2 traffic stays at 1 bit per
-// (item, transaction) — 8x fewer bytes than an int8 one-hot operand.
+// (each byte of bits → 8 int8 through an LDS lookup table), so HBM/L2 traffic stays at 1 bit
+// per (item, transaction) — 8x fewer bytes than an int8 one-hot operand.
 //
 // Tiling: 256-thread block = 4 waves (2x2) → 128x128 output tile; each wave 64x64 = 2x2 MFMA
 // tiles (4 accumulators, 64 AGPRs) so every unpacked fragment feeds 2 MFMAs.  Row words are
@@ -29,17 +29,21 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ uint32_t nib(uint32_t x) { return (x * 0x00204081u) & 0x01010101u; }
-
-// 16 bits → 16 int8 {0,1} (k order = bit order)
-__device__ __forceinline__ v4i unpack16(uint32_t bits) {
+// 16 bits → 16 int8 {0,1} (k order = bit order) through a 256-entry byte → 8-bytes table in LDS:
+// two ds_read_b64 per fragment instead of 12 VALU (PMC counters showed the arithmetic unpack at
+// 15 VALU instructions per MFMA and the matrix cores 40 % busy; the table moves the expansion to
+// the LDS pipe, well inside its budget at one fragment per 2 MFMAs)
+__device__ __forceinline__ v4i unpack16(uint32_t bits, const uint2* __restrict__ lut) {
+  const uint2 lo = lut[bits & 0xFFu], hi = lut[(bits >> 8) & 0xFFu];
   v4i r;
-  r.x = (int)nib(bits & 0xF);
-  r.y = (int)nib((bits >> 4) & 0xF);
-  r.z = (int)nib((bits >> 8) & 0xF);
-  r.w = (int)nib((bits >> 12) & 0xF);
+  r.x = (int)lo.x;
+  r.y = (int)lo.y;
+  r.z = (int)hi.x;
+  r.w = (int)hi.y;
   return r;
 }
+
+__device__ __forceinline__ uint32_t nib(uint32_t x) { return (x * 0x00204081u) & 0x01010101u; }
 
 constexpr int kTile = 128;
 
@@ -47,6 +51,10 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma(const unsigned long long
                                                          int64_t Wp, int64_t F, int64_t n_tiles,
                                                          int64_t n_blocks,
                                                          uint32_t* __restrict__ out) {
+  __shared__ uint2 lut[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x)
+    lut[i] = make_uint2(nib((uint32_t)i & 0xFu), nib((uint32_t)i >> 4));
+  __syncthreads();
   // XCD-aware bijective remap (cdna_hip_programming.md §5): consecutive logical tiles go to
   // the same XCD (blockIdx % 8 labels an XCD group).
   const int64_t orig = blockIdx.x;
@@ -74,15 +82,31 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma(const unsigned long long
   // are combined with integer atomics, so the result is exact and order-independent
   const int64_t slice = (((Wp + gridDim.y - 1) / gridDim.y) + 3) & ~(int64_t)3;
   const int64_t kw0 = (int64_t)blockIdx.y * slice, kw1 = min(Wp, kw0 + slice);
+  // software-pipelined: the next 4-word chunk's row loads are issued before this chunk's 32
+  // MFMAs, so one chunk of HBM/L2 latency hides behind ~1000 matrix-core cycles per wave
+  auto load = [&](int64_t w2, ulonglong2 (&A0)[2], ulonglong2 (&A1)[2], ulonglong2 (&B0)[2],
+                  ulonglong2 (&B1)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool in = w2 + u < (kw1 >> 1);
+      A0[u] = va0 && in ? pa0[w2 + u] : make_ulonglong2(0, 0);
+      A1[u] = va1 && in ? pa1[w2 + u] : make_ulonglong2(0, 0);
+      B0[u] = vb0 && in ? pb0[w2 + u] : make_ulonglong2(0, 0);
+      B1[u] = vb1 && in ? pb1[w2 + u] : make_ulonglong2(0, 0);
+    }
+  };
+  ulonglong2 nA0[2], nA1[2], nB0[2], nB1[2];
+  if ((kw0 >> 1) < (kw1 >> 1)) load(kw0 >> 1, nA0, nA1, nB0, nB1);
   for (int64_t w2 = kw0 >> 1; w2 < (kw1 >> 1); w2 += 2) {
     ulonglong2 A0[2], A1[2], B0[2], B1[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      A0[u] = va0 ? pa0[w2 + u] : make_ulonglong2(0, 0);
-      A1[u] = va1 ? pa1[w2 + u] : make_ulonglong2(0, 0);
-      B0[u] = vb0 ? pb0[w2 + u] : make_ulonglong2(0, 0);
-      B1[u] = vb1 ? pb1[w2 + u] : make_ulonglong2(0, 0);
+      A0[u] = nA0[u];
+      A1[u] = nA1[u];
+      B0[u] = nB0[u];
+      B1[u] = nB1[u];
     }
+    if (w2 + 2 < (kw1 >> 1)) load(w2 + 2, nA0, nA1, nB0, nB1);
 #pragma unroll
     for (int wd = 0; wd < 4; ++wd) {
       const unsigned long long xa0 = (wd & 1) ? A0[wd >> 1].y : A0[wd >> 1].x;
@@ -92,10 +116,10 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma(const unsigned long long
 #pragma unroll
       for (int half = 0; half < 2; ++half) {  // 32 transactions per MFMA K-step
         const int sh = 32 * half + shift;
-        const v4i fa0 = unpack16((uint32_t)(xa0 >> sh) & 0xFFFFu);
-        const v4i fa1 = unpack16((uint32_t)(xa1 >> sh) & 0xFFFFu);
-        const v4i fb0 = unpack16((uint32_t)(xb0 >> sh) & 0xFFFFu);
-        const v4i fb1 = unpack16((uint32_t)(xb1 >> sh) & 0xFFFFu);
+        const v4i fa0 = unpack16((uint32_t)(xa0 >> sh) & 0xFFFFu, lut);
+        const v4i fa1 = unpack16((uint32_t)(xa1 >> sh) & 0xFFFFu, lut);
+        const v4i fb0 = unpack16((uint32_t)(xb0 >> sh) & 0xFFFFu, lut);
+        const v4i fb1 = unpack16((uint32_t)(xb1 >> sh) & 0xFFFFu, lut);
         acc00 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb0, acc00, 0, 0, 0);
         acc01 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb1, acc01, 0, 0, 0);
         acc10 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb0, acc10, 0, 0, 0);
@@ -139,8 +163,17 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
   if (Wp % 4 != 0) throw std::runtime_error("kmls: pair_gram_mfma_i8 needs Wp % 4 == 0");
   const int64_t nt = (F + kTile - 1) / kTile;
   const int64_t blocks = nt * (nt + 1) / 2;
-  // split K until the grid covers the chip (~4 blocks per CU), slices >= 1024 words
-  const int64_t ks = std::max<int64_t>(1, std::min<int64_t>((1024 + blocks - 1) / blocks, Wp / 1024));
+  // split K so that the grid fills the resident block slots in ONE round (a 1.3-round grid left
+  // a third of the chip idle in the second round), slices >= 1024 words
+  static const int64_t slots = [] {
+    int dev = 0, per_cu = 1;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)1024;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pair_gram_mfma, 256, 0) != hipSuccess)
+      per_cu = 2;
+    return (int64_t)std::max(1, per_cu) * std::max(1, p.multiProcessorCount);
+  }();
+  const int64_t ks = std::max<int64_t>(1, std::min<int64_t>(slots / blocks, Wp / 1024));
   hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
                      (const unsigned long long*)bm, Wp, F, nt, blocks, out);
   hipError_t e = hipGetLastError();
