@@ -522,7 +522,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
 constexpr int kSmallChunks = 32;
 
 template <int KB>
-__global__ __launch_bounds__(kBlock) void k_level_count_small(FLevel* __restrict__ lv,
+__global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(FLevel* __restrict__ lv,
                                                               FLevel* __restrict__ nx, FCtl* ctl,
                                                               unsigned long long* __restrict__ status,
                                                               unsigned epoch, LevelCountArgs A,
