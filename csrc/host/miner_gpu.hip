@@ -149,6 +149,7 @@ struct OutBufs {
   unsigned epoch = 0;
   int depth_hint = 6;            // levels enqueued before the first completion check
   std::vector<int64_t> cand_hint;  // candidates per level in the previous call (kernel choice)
+  std::vector<int64_t> rows_hint;  // rows per level in the previous call (scan grid)
   OutBufs() {
     KMLS_HIP(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
     // device-scope release: a cross-stream fork needs no system-scope L2 writeback
@@ -525,6 +526,16 @@ struct MineRun {
   bool levels_loop(kern::FLevel* d_desc, kern::FCtl* d_ctl, int64_t out_cap) {
     constexpr int kMaxLv = 64;
     const int grid = kern::level_grid(n_cus);
+    // launch only as many persistent blocks as the previous call's level needed (x2 margin; a
+    // bigger level still completes through the ticket counter): dispatching and retiring
+    // ~2k idle workgroups is a visible part of a small level's kernel
+    auto grid_for_tiles = [&](int64_t tiles_hint) {
+      if (tiles_hint < 0) return grid;
+      return (int)std::min<int64_t>(grid, std::max<int64_t>(32, 2 * tiles_hint + 16));
+    };
+    auto hint_at = [](const std::vector<int64_t>& v, int L) {
+      return L < (int)v.size() ? v[L] : (int64_t)-1;
+    };
     // diagnostics: KMLS_LEVEL_TRACE=<L> records per-tile phase timestamps of level L's count
     // kernel and writes them to KMLS_LEVEL_TRACE_FILE (uint64 [tiles][8]) after the call
     static const int trace_level = [] {
@@ -545,9 +556,10 @@ struct MineRun {
                              out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1),
                              stream_dl ? ht : kern::HostTrie{},
                              L == trace_level ? d_trace : nullptr, deferred};
-      const int64_t hint = L < (int)ob->cand_hint.size() ? ob->cand_hint[L] : -1;
+      const int64_t hint = hint_at(ob->cand_hint, L);
+      const int g = grid_for_tiles(hint < 0 ? -1 : (hint + kern::level_tile() - 1) / kern::level_tile());
       kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a,
-                        L == 1 ? nullptr : ob->tile_row, grid, hint, s);
+                        L == 1 ? nullptr : ob->tile_row, g, hint, s);
     };
     const int L_allowed = std::min(kMaxLv - 2, max_len ? max_len - 1 : kMaxLv - 2);
     count_level(1);
@@ -559,8 +571,12 @@ struct MineRun {
     bool ok = true;
     while (true) {
       for (int L = last + 1; L <= target; ++L) {
+        const int64_t rows = hint_at(ob->rows_hint, L);
         kern::level_scan(&d_desc[L - 1], &d_desc[L], &d_desc[L + 1], d_ctl, ob->status,
-                         ob->next_epoch(s), Wp, out_cap, ob->tile_row, grid, s);
+                         ob->next_epoch(s), Wp, out_cap, ob->tile_row,
+                         grid_for_tiles(rows < 0 ? -1 : (rows + kern::level_scan_tile() - 1) /
+                                                            kern::level_scan_tile()),
+                         s);
         count_level(L);
         last = L;
       }
@@ -600,7 +616,11 @@ struct MineRun {
     if (!ok) return false;
     last_desc.assign(b_desc, b_desc + kMaxLv);
     ob->cand_hint.assign((size_t)last + 1, -1);
-    for (int L = 1; L <= last; ++L) ob->cand_hint[L] = b_desc[L].n_cand;
+    ob->rows_hint.assign((size_t)last + 1, -1);
+    for (int L = 1; L <= last; ++L) {
+      ob->cand_hint[L] = b_desc[L].n_cand;
+      ob->rows_hint[L] = b_desc[L].n_rows;
+    }
     const int64_t new_size = b_desc[last + 1].child_base;
     for (int L = 1; L <= last; ++L)
       if (b_desc[L + 1].n_rows > 0) max_depth = std::max(max_depth, L + 1);

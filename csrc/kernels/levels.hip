@@ -1005,7 +1005,11 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
   if (small_ok && n2 >= 1 && n2 <= kSmallChunks) {
     // a level expected to be small (the previous call's size: steady-state re-mining) is
     // latency-bound: load each candidate's whole row pair in one batch
-    if (cand_hint >= 0 && cand_hint <= 64 * kTile && n2 <= 18)
+    static const bool kb18 = [] {
+      const char* e = std::getenv("KMLS_KB18");
+      return !(e && e[0] == '0');
+    }();
+    if (kb18 && cand_hint >= 0 && cand_hint <= 64 * kTile && n2 <= 18)
       hipLaunchKernelGGL(k_level_count_small<18>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl,
                          status, epoch, a, tile_row);
     else
