@@ -366,9 +366,13 @@ __global__ __launch_bounds__(kBlock) void k_extend_materialize(
 constexpr int kGT = 64;   // tile rows/cols
 constexpr int kGK = 16;   // words per K stage
 
+// KGK words per K stage: 16 for long rows; short rows (the playlist datasets, Wp <= 48) take
+// the whole row in ONE stage, so the block's latency chain is one load round trip, not three
+template <int KGK>
 __global__ __launch_bounds__(kBlock) void k_pair_gram_popcount(
     const unsigned long long* __restrict__ bm, int64_t Wp, int64_t F_host, int64_t n_tiles,
     uint32_t* __restrict__ out, int64_t ld, const int64_t* __restrict__ dF) {
+  constexpr int kGK = KGK;
   __shared__ unsigned long long As[kGK][kGT + 2];
   __shared__ unsigned long long Bs[kGK][kGT + 2];
   // F from the device when the selection ran there (grid sized for an upper bound)
@@ -381,14 +385,15 @@ __global__ __launch_bounds__(kBlock) void k_pair_gram_popcount(
   if (q0 >= F) return;  // block-uniform
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   uint32_t acc[4][4] = {};
-  // staging map: thread → (row = tid>>2, words (tid&3)*4 .. +3)
-  const int lr = threadIdx.x >> 2, lk = (threadIdx.x & 3) * 4;
+  // staging map: thread → (row = tid>>2, words (tid&3)*(kGK/4) .. +kGK/4-1)
+  constexpr int kPerT = kGK / 4;
+  const int lr = threadIdx.x >> 2, lk = (threadIdx.x & 3) * kPerT;
   // split-K over blockIdx.y (word slices, multiples of kGK); partials combine with atomics
   const int64_t slice = (((Wp + gridDim.y - 1) / gridDim.y) + kGK - 1) / kGK * kGK;
   const int64_t kb = (int64_t)blockIdx.y * slice, ke = min(Wp, kb + slice);
   for (int64_t k0 = kb; k0 < ke; k0 += kGK) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kPerT; ++i) {
       const int64_t kk = k0 + lk + i;
       const int64_t ra = r0 + lr, rb = q0 + lr;
       As[lk + i][lr] = (ra < F && kk < ke) ? bm[ra * Wp + kk] : 0ull;
@@ -511,7 +516,9 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
   }
   const size_t lds = (size_t)n_items * sizeof(uint32_t);
   if (lds <= 64 * 1024) {
-    const int g = grid_for(nnz, kBlock * 64, 1024);
+    // 16 items per thread: a 240k-item playlist dataset spreads over ~60 blocks (64 per thread
+    // left 15 blocks latency-bound); the per-block flush is n_items atomics at most
+    const int g = grid_for(nnz, kBlock * 16, 1024);
     hipLaunchKernelGGL(k_item_support<true>, dim3(g), dim3(kBlock), lds, s, items, nnz, n_items,
                        counts);
   } else {
@@ -676,8 +683,12 @@ void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out
   const int64_t nt = (F + kGT - 1) / kGT;
   const int64_t blocks = nt * (nt + 1) / 2;
   const int64_t ks = std::max<int64_t>(1, std::min<int64_t>((1024 + blocks - 1) / blocks, Wp / 1024));
-  hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks, (unsigned)ks), dim3(kBlock), 0, s,
-                     (const unsigned long long*)bm, Wp, F, nt, out, F, (const int64_t*)nullptr);
+  if (Wp <= 48 && ks == 1)
+    hipLaunchKernelGGL(k_pair_gram_popcount<48>, dim3((unsigned)blocks, 1), dim3(kBlock), 0, s,
+                       (const unsigned long long*)bm, Wp, F, nt, out, F, (const int64_t*)nullptr);
+  else
+    hipLaunchKernelGGL(k_pair_gram_popcount<16>, dim3((unsigned)blocks, (unsigned)ks), dim3(kBlock), 0, s,
+                       (const unsigned long long*)bm, Wp, F, nt, out, F, (const int64_t*)nullptr);
   KMLS_HIP(hipGetLastError());
 }
 
@@ -697,8 +708,12 @@ void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, i
   const int64_t nt = (F_max + kGT - 1) / kGT;
   const int64_t blocks = nt * (nt + 1) / 2;
   const int64_t ks = gram_split_k(Wp, F_max);
-  hipLaunchKernelGGL(k_pair_gram_popcount, dim3((unsigned)blocks, (unsigned)ks), dim3(kBlock), 0, s,
-                     (const unsigned long long*)bm, Wp, F_max, nt, out, F_max, dF);
+  if (Wp <= 48 && ks == 1)
+    hipLaunchKernelGGL(k_pair_gram_popcount<48>, dim3((unsigned)blocks, 1), dim3(kBlock), 0, s,
+                       (const unsigned long long*)bm, Wp, F_max, nt, out, F_max, dF);
+  else
+    hipLaunchKernelGGL(k_pair_gram_popcount<16>, dim3((unsigned)blocks, (unsigned)ks), dim3(kBlock), 0, s,
+                       (const unsigned long long*)bm, Wp, F_max, nt, out, F_max, dF);
   KMLS_HIP(hipGetLastError());
 }
 
