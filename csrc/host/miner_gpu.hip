@@ -146,7 +146,9 @@ struct OutBufs {
   int32_t* tile_row = nullptr;   // [status_cap] count tile → first row (written by level_scan)
   unsigned long long* trace = nullptr;  // KMLS_LEVEL_TRACE diagnostics ([status_cap][8])
   int64_t status_cap = 1 << 20;  // tiles per launch (256M candidates / 2G rows)
-  unsigned epoch = 0;
+  // look-back tags: tag = epoch_base (per call, in FCtl) + launch index (kernel argument)
+  unsigned epoch_base = 0;
+  unsigned launch_idx = 0;
   int depth_hint = 6;            // levels enqueued before the first completion check
   std::vector<int64_t> cand_hint;  // candidates per level in the previous call (kernel choice)
   std::vector<int64_t> rows_hint;  // rows per level in the previous call (scan grid)
@@ -158,12 +160,21 @@ struct OutBufs {
     KMLS_HIP(hipMemset(status, 0, (size_t)status_cap * sizeof(unsigned long long)));
     KMLS_HIP(hipMalloc((void**)&tile_row, (size_t)status_cap * sizeof(int32_t)));
   }
-  unsigned next_epoch(hipStream_t s) {
-    if (++epoch >= (1u << 24) - 1) {  // 24-bit tag wraps: forget every old word
+  static constexpr unsigned kLaunchesPerCall = 256;
+  // start a fused call: a fresh 256-tag window (the 24-bit tag wraps after ~65k calls: then the
+  // status words are zeroed so no stale word can match)
+  unsigned begin_call(hipStream_t s) {
+    epoch_base += kLaunchesPerCall;
+    if (epoch_base + kLaunchesPerCall >= (1u << 24)) {
       KMLS_HIP(hipMemsetAsync(status, 0, (size_t)status_cap * sizeof(unsigned long long), s));
-      epoch = 1;
+      epoch_base = kLaunchesPerCall;
     }
-    return epoch;
+    launch_idx = 0;
+    return epoch_base;
+  }
+  unsigned next_epoch(hipStream_t) {
+    if (++launch_idx >= kLaunchesPerCall) throw std::logic_error("kmls: too many level launches");
+    return launch_idx;
   }
   ~OutBufs() {
     if (copy_s) (void)hipStreamSynchronize(copy_s);
@@ -242,6 +253,7 @@ struct MineRun {
   bool stream_dl = false;
   int64_t host_cap = 0, streamed = 0;
   kern::HostTrie ht{};  // pinned host arrays + element widths (stream_out needs full widths)
+  std::shared_ptr<void> back;  // pinned descriptor + control-block readback (FCtl::rb_dst)
 
   explicit MineRun(OutBufs* o)
       : ob(o), out_parent(o->parent), out_item(o->item), out_count(o->count), out_depth(o->depth) {}
@@ -499,6 +511,10 @@ struct MineRun {
     h_ctl->bump_base = bump_base;
     h_ctl->bump_cap = bump_bytes;
     h_ctl->status_cap = (unsigned long long)ob->status_cap;
+    h_ctl->epoch_base = ob->begin_call(s);
+    h_ctl->h = ht;
+    back = pinned->get(kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
+    h_ctl->rb_dst = back.get();
     KMLS_HIP(hipMemcpyAsync(d_desc, h_desc, stage_bytes - (size_t)(Fr + 1) * 8, hipMemcpyHostToDevice, s));
     KMLS_HIP(hipMemcpyAsync(d_off, h_off, (size_t)(Fr + 1) * 8, hipMemcpyHostToDevice, s));
     if (!levels_loop(d_desc, d_ctl, out_cap)) {
@@ -516,11 +532,10 @@ struct MineRun {
   // prologue's root setup or were queued by stream_out() on the host-prepared path.
   // end of a level batch: the deferred download of level L's children (nodes
   // [desc[L].child_base, + desc[L+1].n_rows)) and the descriptor readback, in one launch
-  void finish_batch(kern::FLevel* d_desc, kern::FCtl* d_ctl, int L, bool deferred, void* h_back,
+  void finish_batch(kern::FLevel* d_desc, kern::FCtl* d_ctl, int L, bool deferred,
                     size_t back_bytes) {
     kern::level_copyout(&d_desc[L], &d_desc[L + 1], d_ctl, out_parent.p, out_item.p, out_count.p,
-                        out_depth.p, deferred ? ht : kern::HostTrie{}, d_desc, h_back, back_bytes,
-                        s);
+                        out_depth.p, deferred, d_desc, back_bytes, s);
   }
 
   bool levels_loop(kern::FLevel* d_desc, kern::FCtl* d_ctl, int64_t out_cap) {
@@ -554,8 +569,7 @@ struct MineRun {
     auto count_level = [&](int L) {
       kern::LevelCountArgs a{Wp, minsup, L == 1 ? gram : nullptr, F, d_ids, out_parent.p,
                              out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1),
-                             stream_dl ? ht : kern::HostTrie{},
-                             L == trace_level ? d_trace : nullptr, deferred};
+                             stream_dl, L == trace_level ? d_trace : nullptr, deferred};
       const int64_t hint = hint_at(ob->cand_hint, L);
       const int g = grid_for_tiles(hint < 0 ? -1 : (hint + kern::level_tile() - 1) / kern::level_tile());
       kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a,
@@ -565,7 +579,7 @@ struct MineRun {
     count_level(1);
     int last = 1;
     int target = std::min(L_allowed, std::max(ob->depth_hint, 2));
-    std::shared_ptr<void> back = pinned->get(kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
+    if (!back) throw std::logic_error("levels_loop: no readback buffer (FCtl::rb_dst)");
     kern::FLevel* b_desc = (kern::FLevel*)back.get();
     kern::FCtl* b_ctl = (kern::FCtl*)(b_desc + kMaxLv);
     bool ok = true;
@@ -583,8 +597,7 @@ struct MineRun {
       // d_ctl directly follows d_desc (kMaxLv * 128 bytes, arena alignment 256)
       if ((char*)d_ctl != (char*)(d_desc + kMaxLv))
         throw std::logic_error("levels_loop: control block must follow the descriptors");
-      finish_batch(d_desc, d_ctl, last, deferred, b_desc,
-                   (kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl) + 15) & ~(size_t)15);
+      finish_batch(d_desc, d_ctl, last, deferred, kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
       t_presync = std::chrono::steady_clock::now();
       sync_stream(s);
       t_postsync = std::chrono::steady_clock::now();
@@ -784,6 +797,7 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
   *abort_host_ = 0u;
   KMLS_HIP(hipHostGetDevicePointer((void**)&abort_dev_, abort_host_, 0));
   KMLS_HIP(hipHostMalloc((void**)&h_scalar_, 64));
+  KMLS_HIP(hipHostMalloc((void**)&call_params_, sizeof(kern::FCtl)));
   KMLS_HIP(hipMalloc((void**)&d_pair_, 2 * sizeof(uint64_t)));
   hipDeviceProp_t prop;
   KMLS_HIP(hipGetDeviceProperties(&prop, device));
@@ -799,6 +813,7 @@ GpuMiner::~GpuMiner() {
   if (d_own_bm_) (void)hipFree(d_own_bm_);
   if (abort_host_) (void)hipHostFree(abort_host_);
   if (h_scalar_) (void)hipHostFree(h_scalar_);
+  if (call_params_) (void)hipHostFree(call_params_);
   if (sup_scratch_) (void)hipFree(sup_scratch_);
   if (d_pair_) (void)hipFree(d_pair_);
   out_.reset();
@@ -1180,21 +1195,28 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   // prologue, all on the device: one init launch (histogram + bitmap buffer zeroed, level
   // descriptors zeroed, control block set), supports, selection (small vocabularies: one launch
   // that also writes the frequent-item tables to pinned host memory), bitmaps, gram
-  kern::FCtl init{};
+  // frequent-item tables for the frequent() API (ids | counts | rank_of, tab_stride apart)
+  std::shared_ptr<void> fstage = pinned_->get((size_t)tab_stride * 12);
+  run.back = pinned_->get(kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
+  kern::FCtl& init = *call_params_;  // pinned; the init kernel copies it into d_ctl
+  std::memset(&init, 0, sizeof(init));
   init.bump_base = bump_base;
   init.bump_cap = bump_bytes;
   init.status_cap = (unsigned long long)out_->status_cap;
+  init.epoch_base = out_->begin_call(s);
+  init.h = run.ht;
+  init.host_tab = (int32_t*)fstage.get();
+  init.tab_stride = tab_stride;
+  init.rb_dst = run.back.get();
   const auto t_launch = std::chrono::steady_clock::now();
   trace::push("kmls.prologue(enqueue)");
-  kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl, init, s);
+  kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl,
+                            call_params_, s);
   support_counts(d_items_, nnz_, d_cnt, s);
-  // frequent-item tables for the frequent() API (ids | counts | rank_of, tab_stride apart)
-  std::shared_ptr<void> fstage = pinned_->get((size_t)tab_stride * 12);
   const uint32_t c1 = level1_threshold((uint64_t)n_tx_, cfg.min_support);
   const bool fused_select = I <= kern::kSelectFusedMax;
   if (fused_select)
-    kern::level_select_fused(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_desc,
-                             (int32_t*)fstage.get(), tab_stride, s);
+    kern::level_select_fused(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_desc, d_ctl, s);
   else
     kern::level_select(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_rrank /* scratch until root setup */,
                        d_desc, s);
@@ -1210,8 +1232,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
                          run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
                          d_prank, part_world, part_rank,
-                         run.stream_dl && !deferred_dl() ? run.ht : kern::HostTrie{},
-                         fused_select ? (int32_t*)fstage.get() : nullptr, tab_stride};
+                         run.stream_dl && !deferred_dl(), fused_select};
   kern::level_root_setup(d_desc, d_ctl, ra, s);
   if (!fused_select)  // staged to pinned memory while the levels run
     KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));

@@ -95,6 +95,9 @@ class Comm {
 };
 
 struct OutBufs;  // persistent device trie buffers + download stream (miner_gpu.hip)
+}  // namespace gpu
+namespace kern { struct FCtl; }
+namespace gpu {
 
 // Resident-data GPU miner.  Typical use: load() once (CSR → HBM), mine() many times.
 // Multi-GPU: every rank calls the same sequence; collectives are done by the Python layer
@@ -171,6 +174,7 @@ class GpuMiner {
   unsigned int* abort_host_ = nullptr;       // watchdog flag (pinned, device-mapped)
   const unsigned int* abort_dev_ = nullptr;
   int64_t* h_scalar_ = nullptr;   // pinned readback scratch (allocated once: hipHostFree syncs)
+  kern::FCtl* call_params_ = nullptr;  // pinned per-call control block (read by the init kernel)
   uint64_t* d_pair_ = nullptr;    // device [survivors, next-level candidates]
   int n_cus_ = 256;
   bool mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res, int part_rank,

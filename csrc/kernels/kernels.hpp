@@ -89,14 +89,6 @@ struct FLevel {  // device-resident descriptor of one level (rows = itemsets of 
   const int32_t* slot;
   char pad[32];
 };
-struct FCtl {
-  char* bump_base;
-  unsigned long long bump_cap, bump_top;
-  unsigned long long status_cap;   // look-back tiles available
-  unsigned long long candidates;   // Σ n_cand over the counted levels
-  unsigned int overflow;           // 1 bump, 2 spin, 3/4 capacity → host falls back
-  unsigned int dl_overflow;        // pinned host arrays too small → host copies at the end
-};
 // Pinned host trie written directly by the level kernels (streamed download).  Element widths
 // are chosen per call so that only the bytes the data needs cross PCIe: parent 4 B while node
 // ids < 2^31, item 2 B while item ids < 2^16, count 2 B while T < 2^16 (the reference's playlist
@@ -110,6 +102,25 @@ struct HostTrie {
   int64_t cap;
   int par_w, item_w, cnt_w;  // bytes: 4|8, 2|4, 2|4
 };
+// Control block of one fused mining call.  Everything that changes from call to call (epoch
+// base, pinned host destinations) lives here rather than in kernel arguments, so the launch
+// sequence of a call is invariant and can be captured once as a hipGraph and replayed.
+struct FCtl {
+  char* bump_base;
+  unsigned long long bump_cap, bump_top;
+  unsigned long long status_cap;   // look-back tiles available
+  unsigned long long candidates;   // Σ n_cand over the counted levels
+  unsigned int overflow;           // 1 bump, 2 spin, 3/4 capacity → host falls back
+  unsigned int dl_overflow;        // pinned host arrays too small → host copies at the end
+  unsigned int epoch_base;         // look-back tag of launch i = epoch_base + i (24 bits)
+  unsigned int pad0;
+  HostTrie h;                      // streamed download destination (pinned)
+  int32_t* host_tab;               // frequent-item tables ids | counts | rank_of (pinned)
+  int64_t tab_stride;
+  void* rb_dst;                    // descriptor + control-block readback (pinned)
+  char pad1[8];
+};
+static_assert(sizeof(FCtl) % 16 == 0, "FCtl is read back in 16-byte words");
 struct LevelCountArgs {
   int64_t Wp;
   uint32_t minsup;
@@ -121,7 +132,7 @@ struct LevelCountArgs {
   uint32_t* out_count;
   uint8_t* out_depth;
   uint8_t child_depth;
-  HostTrie h;  // streamed download (h.item == nullptr: off)
+  bool download;  // stream the trie to FCtl::h
   unsigned long long* trace;  // per-tile phase timestamps [tile][8] (nullptr: off; diagnostics)
   // deferred download: the launch carries kCopyBlocks extra blocks that copy the PREVIOUS
   // level's nodes (this level's rows, finished by the previous launch) from the device trie to
@@ -135,19 +146,20 @@ constexpr int kCopyBlocks = 64;
 // (closed form), iota rank/gid, root children buffers from the bump region.
 constexpr int64_t kSelectMaxItems = 16384;
 // one launch for the per-call device state of the resident path: zero the support histogram
-// and the bitmap buffer, zero the level descriptors and initialise the control block (replaces
-// two memsets and a host→device descriptor copy)
+// and the bitmap buffer, zero the level descriptors and copy the control block from `params`
+// (pinned host memory the host fills before the call; read at execution time, so a captured
+// graph picks up each call's values)
 void level_prologue_init(uint32_t* cnt, int64_t n_items, uint64_t* bm, int64_t bm_words,
-                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl& init, hipStream_t s);
+                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl* params, hipStream_t s);
 // selection in one launch for small vocabularies (n_items <= kSelectFusedMax): every thread
 // ranks its item against all others (no rank accumulator, no memset) and also writes rank_of
-// (the third of the frequent-item tables ids | counts | rank_of, `tab_stride` apart) straight
-// to pinned host memory `host_tab` (nullptr: skip); the root setup writes the other two.
+// (the third of the frequent-item tables ids | counts | rank_of) straight to FCtl::host_tab
+// (nullptr: skip); the root setup writes the other two.
 // Falls back to level_select above that size.
 constexpr int64_t kSelectFusedMax = 4096;
 void level_select_fused(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* ids,
-                        uint32_t* fcounts, int32_t* rank_of, FLevel* desc, int32_t* host_tab,
-                        int64_t tab_stride, hipStream_t s);
+                        uint32_t* fcounts, int32_t* rank_of, FLevel* desc, const FCtl* ctl,
+                        hipStream_t s);
 void level_select(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* ids,
                   uint32_t* fcounts, int32_t* rank_of, int32_t* rank_acc, FLevel* desc,
                   hipStream_t s);
@@ -167,9 +179,8 @@ struct RootSetupArgs {
   const int32_t* prank;  // partition rank of each root class (world > 1), see level_partition
   int world;
   int my_rank;
-  HostTrie h;  // level-1 nodes also go straight to the pinned host arrays (h.item == nullptr: off)
-  int32_t* host_tab;   // frequent-item ids | counts (tab_stride apart) to pinned host (or nullptr)
-  int64_t tab_stride;
+  bool download;   // level-1 nodes also go straight to FCtl::h (inline download mode)
+  bool host_tab;   // frequent-item ids | counts to FCtl::host_tab
 };
 void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s);
 // rank root classes by estimated cost (n_a^2 + 1 from the gram, desc) for the snake partition
@@ -184,12 +195,11 @@ void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long lon
                 unsigned epoch, int64_t Wp, int64_t out_cap, int32_t* tile_row, int grid,
                 hipStream_t s);
 // trie nodes [lv->child_base, +nx->n_rows) (the last launched level's children) from the device
-// trie arrays into the pinned host trie (h.item == nullptr: skip), plus an optional readback of
-// rb_bytes (multiple of 16) from rb_src to pinned rb_dst
+// trie arrays into FCtl::h (download), plus a readback of rb_bytes (multiple of 16; 0 = none)
+// from rb_src to FCtl::rb_dst
 void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t* d_parent,
                    const int32_t* d_item, const uint32_t* d_count, const uint8_t* d_depth,
-                   const HostTrie& h, const void* rb_src, void* rb_dst, size_t rb_bytes,
-                   hipStream_t s);
+                   bool download, const void* rb_src, size_t rb_bytes, hipStream_t s);
 // cand_hint: expected candidate count of the level (the previous call's; -1 unknown) — picks
 // the register/latency trade-off of the short-row kernel, never affects results
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,

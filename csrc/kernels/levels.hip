@@ -136,7 +136,7 @@ __device__ void copy_prev_level(const FLevel* lv, FCtl* ctl, const LevelCountArg
   const int64_t base = pv->child_base, n = lv->n_rows;
   for (int64_t i = base + (int64_t)cb * blockDim.x + threadIdx.x; i < base + n;
        i += (int64_t)kCopyBlocks * blockDim.x)
-    host_store(A.h, ctl, i, A.out_parent[i], A.out_item[i], A.out_count[i], A.out_depth[i]);
+    host_store(ctl->h, ctl, i, A.out_parent[i], A.out_item[i], A.out_count[i], A.out_depth[i]);
 }
 
 // Bump allocation from the device region (256-byte aligned); nullptr + overflow flag if full.
@@ -224,6 +224,7 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
   __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
   if (ctl->overflow) return;
+  epoch = (ctl->epoch_base + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
   const int64_t n = lv->n_rows;
   const int64_t n_tiles = (n + kScanTile - 1) / kScanTile;
   if (n_tiles > (int64_t)ctl->status_cap) {
@@ -324,6 +325,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
   if (ctl->overflow) return;
+  epoch = (ctl->epoch_base + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
   const int64_t tgrid = (int64_t)gridDim.x - (A.deferred_dl ? kCopyBlocks : 0);  // tile blocks
   if ((int64_t)blockIdx.x >= tgrid) {
     copy_prev_level(lv, ctl, A, (int)(blockIdx.x - tgrid));
@@ -474,7 +476,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
         A.out_count[node] = cnt;
         A.out_depth[node] = A.child_depth;
         // streamed download: consecutive survivors → coalesced PCIe writes
-        if (A.h.item && !A.deferred_dl) host_store(A.h, ctl, node, par, it, cnt, A.child_depth);
+        if (A.download && !A.deferred_dl) host_store(ctl->h, ctl, node, par, it, cnt, A.child_depth);
       }
     }
     // ---- phase 3: survivors' bitmaps (team per survivor) ----
@@ -533,6 +535,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
   __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
   if (ctl->overflow) return;
+  epoch = (ctl->epoch_base + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
   const int64_t tgrid = (int64_t)gridDim.x - (A.deferred_dl ? kCopyBlocks : 0);  // tile blocks
   if ((int64_t)blockIdx.x >= tgrid) {
     copy_prev_level(lv, ctl, A, (int)(blockIdx.x - tgrid));
@@ -689,7 +692,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
         A.out_item[node] = it;
         A.out_count[node] = k;
         A.out_depth[node] = A.child_depth;
-        if (A.h.item && !A.deferred_dl) host_store(A.h, ctl, node, par, it, k, A.child_depth);
+        if (A.download && !A.deferred_dl) host_store(ctl->h, ctl, node, par, it, k, A.child_depth);
       }
     }
     if (tr) tr[4] = wall_clock64();
@@ -721,13 +724,15 @@ __global__ __launch_bounds__(kBlock) void k_level_copyout(const FLevel* __restri
                                                           const int32_t* __restrict__ d_item,
                                                           const uint32_t* __restrict__ d_count,
                                                           const uint8_t* __restrict__ d_depth,
-                                                          HostTrie h, const uint4* __restrict__ rb_src,
-                                                          uint4* __restrict__ rb_dst, int rb_words) {
-  if (rb_dst && blockIdx.x == gridDim.x - 1) {
+                                                          bool download, const uint4* __restrict__ rb_src,
+                                                          int rb_words) {
+  if (rb_words && blockIdx.x == gridDim.x - 1) {
+    uint4* __restrict__ rb_dst = (uint4*)ctl->rb_dst;
     for (int i = threadIdx.x; i < rb_words; i += blockDim.x) rb_dst[i] = rb_src[i];
     return;
   }
-  if (!h.item || ctl->overflow) return;
+  if (!download || ctl->overflow) return;
+  const HostTrie h = ctl->h;
   const int64_t base = lv->child_base;
   const int64_t S = nx->n_rows;
   if (S <= 0) return;
@@ -766,14 +771,15 @@ __global__ __launch_bounds__(256) void k_select_rank(const uint32_t* __restrict_
 __global__ __launch_bounds__(256) void k_prologue_init(uint32_t* __restrict__ cnt, int64_t n_items,
                                                        uint64_t* __restrict__ bm, int64_t bm_words,
                                                        FLevel* __restrict__ desc, int n_desc,
-                                                       FCtl* __restrict__ ctl, FCtl init) {
+                                                       FCtl* __restrict__ ctl,
+                                                       const FCtl* __restrict__ params) {
   const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int64_t i = tid; i < n_items; i += nthr) cnt[i] = 0u;
   for (int64_t i = tid; i < bm_words; i += nthr) bm[i] = 0ull;
   const int64_t dwords = (int64_t)n_desc * (int64_t)(sizeof(FLevel) / 8);
   for (int64_t i = tid; i < dwords; i += nthr) ((unsigned long long*)desc)[i] = 0ull;
-  if (tid == 0) *ctl = init;
+  if (tid == 0) *ctl = *params;
 }
 
 // 16 lanes per item, each comparing against every 16th item (a one-thread-per-item loop ran
@@ -783,8 +789,9 @@ __global__ __launch_bounds__(256) void k_select_fused(const uint32_t* __restrict
                                                       int32_t* __restrict__ ids,
                                                       uint32_t* __restrict__ fcounts,
                                                       int32_t* __restrict__ rank_of, FLevel* desc,
-                                                      int32_t* __restrict__ host_tab,
-                                                      int64_t tab_stride) {
+                                                      const FCtl* __restrict__ ctl) {
+  int32_t* __restrict__ host_tab = ctl->host_tab;
+  const int64_t tab_stride = ctl->tab_stride;
   __shared__ unsigned int s_F;
   __shared__ uint32_t s_c[kSelectFusedMax];  // the whole histogram (a global load per compare
                                              // made the loop one memory latency per step)
@@ -964,10 +971,10 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     a.out_item[i] = a.ids[i];
     a.out_count[i] = a.fcounts[i];
     a.out_depth[i] = 1;
-    if (a.h.item) host_store(a.h, ctl, i, -1, a.ids[i], a.fcounts[i], 1);
+    if (a.download) host_store(ctl->h, ctl, i, -1, a.ids[i], a.fcounts[i], 1);
     if (a.host_tab) {
-      a.host_tab[i] = a.ids[i];
-      ((uint32_t*)a.host_tab)[a.tab_stride + i] = a.fcounts[i];
+      ctl->host_tab[i] = a.ids[i];
+      ((uint32_t*)ctl->host_tab)[ctl->tab_stride + i] = a.fcounts[i];
     }
   }
 }
@@ -1030,11 +1037,10 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
 
 void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t* d_parent,
                    const int32_t* d_item, const uint32_t* d_count, const uint8_t* d_depth,
-                   const HostTrie& h, const void* rb_src, void* rb_dst, size_t rb_bytes,
-                   hipStream_t s) {
+                   bool download, const void* rb_src, size_t rb_bytes, hipStream_t s) {
   if (rb_bytes % 16) throw std::runtime_error("level_copyout: readback size not a multiple of 16");
-  hipLaunchKernelGGL(k_level_copyout, dim3(rb_dst ? 129 : 128), dim3(kBlock), 0, s, lv, nx, ctl,
-                     d_parent, d_item, d_count, d_depth, h, (const uint4*)rb_src, (uint4*)rb_dst,
+  hipLaunchKernelGGL(k_level_copyout, dim3(rb_bytes ? 129 : 128), dim3(kBlock), 0, s, lv, nx, ctl,
+                     d_parent, d_item, d_count, d_depth, download, (const uint4*)rb_src,
                      (int)(rb_bytes / 16));
   KMLS_HIP(hipGetLastError());
 }
@@ -1052,21 +1058,21 @@ void level_select(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* id
 }
 
 void level_prologue_init(uint32_t* cnt, int64_t n_items, uint64_t* bm, int64_t bm_words,
-                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl& init, hipStream_t s) {
+                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl* params, hipStream_t s) {
   const int64_t work = std::max<int64_t>(std::max<int64_t>(n_items, bm_words), 1);
   const unsigned blocks = (unsigned)std::min<int64_t>((work + 255) / 256, 2048);
   hipLaunchKernelGGL(k_prologue_init, dim3(blocks), dim3(256), 0, s, cnt, n_items, bm, bm_words,
-                     desc, n_desc, ctl, init);
+                     desc, n_desc, ctl, params);
   KMLS_HIP(hipGetLastError());
 }
 
 void level_select_fused(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* ids,
-                        uint32_t* fcounts, int32_t* rank_of, FLevel* desc, int32_t* host_tab,
-                        int64_t tab_stride, hipStream_t s) {
+                        uint32_t* fcounts, int32_t* rank_of, FLevel* desc, const FCtl* ctl,
+                        hipStream_t s) {
   if (n_items > kSelectFusedMax) throw std::runtime_error("level_select_fused: vocabulary too large");
   const unsigned nb = (unsigned)((n_items + 15) / 16);
   hipLaunchKernelGGL(k_select_fused, dim3(nb), dim3(256), 0, s, cnt, n_items, c1, ids, fcounts,
-                     rank_of, desc, host_tab, tab_stride);
+                     rank_of, desc, ctl);
   KMLS_HIP(hipGetLastError());
 }
 
