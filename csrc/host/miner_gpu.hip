@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <chrono>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -254,6 +255,11 @@ struct MineRun {
   int64_t host_cap = 0, streamed = 0;
   kern::HostTrie ht{};  // pinned host arrays + element widths (stream_out needs full widths)
   std::shared_ptr<void> back;  // pinned descriptor + control-block readback (FCtl::rb_dst)
+  // hipGraph mode (mine_resident): the first batch of levels is captured (graph_capture; the
+  // caller's end_capture instantiates and launches it) or already launched as a replay
+  bool graph_capture = false, graph_replay = false;
+  int graph_last = 0;                        // replay: last level the graph enqueues
+  std::function<void(int)> end_capture;      // capture: called with the batch's last level
 
   explicit MineRun(OutBufs* o)
       : ob(o), out_parent(o->parent), out_item(o->item), out_count(o->count), out_depth(o->depth) {}
@@ -576,14 +582,20 @@ struct MineRun {
                         L == 1 ? nullptr : ob->tile_row, g, hint, s);
     };
     const int L_allowed = std::min(kMaxLv - 2, max_len ? max_len - 1 : kMaxLv - 2);
-    count_level(1);
     int last = 1;
     int target = std::min(L_allowed, std::max(ob->depth_hint, 2));
+    if (graph_replay) {  // the replayed graph already holds count(1) .. count(graph_last)
+      last = graph_last;
+      target = graph_last;
+    } else {
+      count_level(1);
+    }
     if (!back) throw std::logic_error("levels_loop: no readback buffer (FCtl::rb_dst)");
     kern::FLevel* b_desc = (kern::FLevel*)back.get();
     kern::FCtl* b_ctl = (kern::FCtl*)(b_desc + kMaxLv);
     bool ok = true;
-    while (true) {
+    for (bool first = true;; first = false) {
+     if (!(first && graph_replay)) {
       for (int L = last + 1; L <= target; ++L) {
         const int64_t rows = hint_at(ob->rows_hint, L);
         kern::level_scan(&d_desc[L - 1], &d_desc[L], &d_desc[L + 1], d_ctl, ob->status,
@@ -598,6 +610,8 @@ struct MineRun {
       if ((char*)d_ctl != (char*)(d_desc + kMaxLv))
         throw std::logic_error("levels_loop: control block must follow the descriptors");
       finish_batch(d_desc, d_ctl, last, deferred, kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
+      if (first && graph_capture) end_capture(last);
+     }
       t_presync = std::chrono::steady_clock::now();
       sync_stream(s);
       t_postsync = std::chrono::steady_clock::now();
@@ -779,6 +793,24 @@ float elapsed(const Event& a, const Event& b) {
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
+// The captured launch sequence of the last steady-state resident call (see mine_resident).
+struct GraphCache {
+  std::vector<uint64_t> key;
+  hipGraphExec_t exec = nullptr;
+  int last = 0;             // last level the graph enqueues
+  unsigned launch_idx = 0;  // look-back launch indices the graph consumes
+  void reset(hipGraphExec_t e, std::vector<uint64_t> k, int l, unsigned li) {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    exec = e;
+    key = std::move(k);
+    last = l;
+    launch_idx = li;
+  }
+  ~GraphCache() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+  }
+};
+
 GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(device) {
   KMLS_HIP(hipSetDevice(device));
   if (stream) {
@@ -806,6 +838,8 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
 
 GpuMiner::~GpuMiner() {
   (void)hipSetDevice(device_);
+  if (stream_) (void)hipStreamSynchronize((hipStream_t)stream_);
+  graph_.reset();
   if (d_tx_ptr_) (void)hipFree(d_tx_ptr_);
   if (d_items_) (void)hipFree(d_items_);
   if (d_rank_of_) (void)hipFree(d_rank_of_);
@@ -1209,39 +1243,108 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   init.tab_stride = tab_stride;
   init.rb_dst = run.back.get();
   const auto t_launch = std::chrono::steady_clock::now();
-  trace::push("kmls.prologue(enqueue)");
-  kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl,
-                            call_params_, s);
-  support_counts(d_items_, nnz_, d_cnt, s);
   const uint32_t c1 = level1_threshold((uint64_t)n_tx_, cfg.min_support);
   const bool fused_select = I <= kern::kSelectFusedMax;
-  if (fused_select)
-    kern::level_select_fused(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_desc, d_ctl, s);
-  else
-    kern::level_select(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_rrank /* scratch until root setup */,
-                       d_desc, s);
-  kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of, d_own_bm_, Wp, 0, s);
-  if (kern::pair_gram_dev_needs_zero(Wp, I)) KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));
-  kern::pair_gram_popcount_dev(d_own_bm_, Wp, &d_desc[1].n_rows, I, d_gram, s);
-  int32_t* d_prank = nullptr;
-  if (part_world > 1) {  // replicated-data partition of the root classes, computed on device
-    int64_t* d_cost = (int64_t*)arena_->push((size_t)I * 8);
-    d_prank = (int32_t*)arena_->push((size_t)I * 4);
-    kern::level_partition(d_gram, I, d_desc, run.minsup, I, d_cost, d_prank, s);
+  // The call's launches (prologue + the first batch of levels) are invariant once the data,
+  // configuration, buffers and per-level launch plan repeat: they are captured once as a
+  // hipGraph and replayed (KMLS_GRAPH=0 disables), which takes ~35 kernel launches off the
+  // host path of every steady-state call.  All per-call state reaches the kernels through the
+  // pinned parameter block read by the init kernel.
+  static const bool graphs = [] {
+    const char* e = std::getenv("KMLS_GRAPH");
+    return !(e && e[0] == '0');
+  }();
+  static const bool tracing = std::getenv("KMLS_LEVEL_TRACE") != nullptr;
+  const bool use_graph = graphs && fused_select && !tracing;
+  std::vector<uint64_t> key;
+  if (use_graph) {
+    auto u = [](const void* p) { return (uint64_t)(uintptr_t)p; };
+    key = {u(d_desc), u(d_cnt), u(d_own_bm_), (uint64_t)need, u(d_items_), u(d_tx_ptr_),
+           (uint64_t)nnz_, (uint64_t)n_tx_, (uint64_t)I, (uint64_t)Wp, run.minsup, c1,
+           (uint64_t)cfg.max_len, (uint64_t)run.stream_dl, (uint64_t)deferred_dl(),
+           (uint64_t)part_rank, (uint64_t)part_world, u(run.out_parent.p), u(run.out_item.p),
+           u(run.out_count.p), u(run.out_depth.p), (uint64_t)out_cap, u(out_->status),
+           u(out_->tile_row), (uint64_t)n_cus_, (uint64_t)out_->depth_hint, u(call_params_),
+           (uint64_t)out_->cand_hint.size()};
+    for (int64_t v : out_->cand_hint) key.push_back((uint64_t)v);
+    for (int64_t v : out_->rows_hint) key.push_back((uint64_t)v);
   }
-  kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
-                         run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
-                         d_prank, part_world, part_rank,
-                         run.stream_dl && !deferred_dl(), fused_select};
-  kern::level_root_setup(d_desc, d_ctl, ra, s);
-  if (!fused_select)  // staged to pinned memory while the levels run
-    KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));
-  KMLS_HIP(hipEventRecord(e1.e, s));
+  const bool replay = use_graph && graph_ && graph_->exec && graph_->key == key;
+  auto enqueue_prologue = [&]() {
+    kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl,
+                              call_params_, s);
+    support_counts(d_items_, nnz_, d_cnt, s);
+    if (fused_select)
+      kern::level_select_fused(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_desc, d_ctl, s);
+    else
+      kern::level_select(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_rrank /* scratch until root setup */,
+                         d_desc, s);
+    kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of, d_own_bm_, Wp, 0, s);
+    if (kern::pair_gram_dev_needs_zero(Wp, I)) KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));
+    kern::pair_gram_popcount_dev(d_own_bm_, Wp, &d_desc[1].n_rows, I, d_gram, s);
+    int32_t* d_prank = nullptr;
+    if (part_world > 1) {  // replicated-data partition of the root classes, computed on device
+      int64_t* d_cost = (int64_t*)arena_->push((size_t)I * 8);
+      d_prank = (int32_t*)arena_->push((size_t)I * 4);
+      kern::level_partition(d_gram, I, d_desc, run.minsup, I, d_cost, d_prank, s);
+    }
+    kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
+                           run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
+                           d_prank, part_world, part_rank,
+                           run.stream_dl && !deferred_dl(), fused_select};
+    kern::level_root_setup(d_desc, d_ctl, ra, s);
+    if (!fused_select)  // staged to pinned memory while the levels run
+      KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));
+  };
+  auto abort_capture = [&]() {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(s, &g);
+    if (g) (void)hipGraphDestroy(g);
+  };
+  trace::push("kmls.prologue(enqueue)");
+  if (replay) {
+    run.graph_replay = true;
+    run.graph_last = graph_->last;
+    out_->launch_idx = graph_->launch_idx;  // later (non-graph) launches of this call continue
+    KMLS_HIP(hipGraphLaunch(graph_->exec, s));
+  } else if (use_graph) {
+    KMLS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    try {
+      enqueue_prologue();
+    } catch (...) {
+      abort_capture();
+      throw;
+    }
+    run.graph_capture = true;
+    run.end_capture = [&](int last) {
+      hipGraph_t g = nullptr;
+      KMLS_HIP(hipStreamEndCapture(s, &g));
+      hipGraphExec_t ex = nullptr;
+      const hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      KMLS_HIP(ie);
+      if (!graph_) graph_ = std::make_unique<GraphCache>();
+      graph_->reset(ex, key, last, out_->launch_idx);
+      KMLS_HIP(hipGraphLaunch(ex, s));
+    };
+  } else {
+    enqueue_prologue();
+    KMLS_HIP(hipEventRecord(e1.e, s));
+  }
   trace::pop();
   bool ok;
   {
     trace::Range rg("kmls.levels");
-    ok = run.levels_loop(d_desc, d_ctl, out_cap);
+    try {
+      ok = run.levels_loop(d_desc, d_ctl, out_cap);
+    } catch (...) {
+      if (run.graph_capture) {
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone)
+          abort_capture();
+      }
+      throw;
+    }
   }
   if (!ok) {
     fused_fallback_ = run.fallback_reason;
@@ -1283,8 +1386,12 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   }
   KMLS_HIP(hipStreamSynchronize(s));
   KMLS_HIP(hipStreamSynchronize(out_->copy_s));
-  res.phases.push_back({"prologue(support+select+encode+gram)", elapsed(e0, e1)});
-  res.phases.push_back({"levels", elapsed(e1, e2)});
+  if (use_graph) {
+    res.phases.push_back({replay ? "mine(graph replay)" : "mine(graph capture)", elapsed(e0, e2)});
+  } else {
+    res.phases.push_back({"prologue(support+select+encode+gram)", elapsed(e0, e1)});
+    res.phases.push_back({"levels", elapsed(e1, e2)});
+  }
   {  // host-side profile (ms): before the first launch, enqueue until the sync, after the sync
     const auto t_end = std::chrono::steady_clock::now();
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };

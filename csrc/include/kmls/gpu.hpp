@@ -95,6 +95,7 @@ class Comm {
 };
 
 struct OutBufs;  // persistent device trie buffers + download stream (miner_gpu.hip)
+struct GraphCache;  // captured launch sequence of the resident path (miner_gpu.hip)
 }  // namespace gpu
 namespace kern { struct FCtl; }
 namespace gpu {
@@ -189,6 +190,7 @@ class GpuMiner {
   size_t arena_max_ = 0;
   std::string fused_fallback_;
   std::unique_ptr<OutBufs> out_;  // output trie kept allocated across mine() calls
+  std::unique_ptr<GraphCache> graph_;  // steady-state hipGraph of mine_resident
   Comm* comm_ = nullptr;          // set during mine_txdp: level counts are all-reduced
   std::vector<int64_t> tile_tx_;  // 65 evenly spaced transaction boundaries of the shard
   std::vector<int64_t> tile_nnz_; // and their item offsets

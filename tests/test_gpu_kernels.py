@@ -435,3 +435,28 @@ def test_support_histograms_large_vocab(gpu_mod, T, I):
     g.synchronize()
     np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32),
                                   np.bincount(items, minlength=I))
+
+
+def test_graph_replay_matches_eager(gpu_mod):
+    """Steady-state resident calls replay a captured hipGraph (third call on: the launch plan
+    repeats); results must match the CPU miner on every call, including when the configuration
+    alternates (key mismatch → recapture) and when results of earlier calls are still alive."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    tx = generate("ds2_weak", seed=6)
+    ref = {ms: gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms) for ms in (0.05, 0.04)}
+    g = gpu_mod.GpuMiner(0, 1 << 31, 0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    kept, phases = [], []
+    for ms in (0.05, 0.05, 0.05, 0.05, 0.04, 0.04, 0.04, 0.05, 0.05):
+        r = g.mine(ms)
+        assert r["stats"]["levels_path"] == "fused-resident", r["stats"]
+        assert r["stats"]["n_itemsets"] == ref[ms]["stats"]["n_itemsets"]
+        assert np.array_equal(np.sort(r["count"]), np.sort(ref[ms]["count"]))
+        phases.append(next(k for k in r["stats"]["phases_ms"] if k.startswith("mine(graph")
+                           or k.startswith("prologue")))
+        kept.append((ms, r))
+    assert "mine(graph replay)" in phases[2:4], phases
+    for ms, r in kept:  # pinned results of replayed calls stay valid
+        assert np.array_equal(np.sort(r["count"]), np.sort(ref[ms]["count"]))
+    small = [(ms, r) for ms, r in kept if r["stats"]["n_itemsets"] < 300_000][-1]
+    assert _trie_dict(small[1]) == _trie_dict(ref[small[0]])
