@@ -235,6 +235,23 @@ bool deferred_dl() {
 }
 size_t fused_bump_cap(size_t bytes);
 
+// deferred-download copy blocks per count launch (KMLS_COPY_BLOCKS, default kern::kCopyBlocks)
+bool copy_last() {  // KMLS_COPY_LAST=1: copy blocks at the end of the grid (A/B)
+  static const bool v = [] {
+    const char* e = std::getenv("KMLS_COPY_LAST");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+int copy_blocks() {
+  static const int v = [] {
+    const char* e = std::getenv("KMLS_COPY_BLOCKS");
+    const int n = e ? std::atoi(e) : 0;
+    return n > 0 ? std::min(n, 1024) : kern::kCopyBlocks;
+  }();
+  return v;
+}
+
 struct MineRun {
   hipStream_t s;
   DeviceArena* arena;
@@ -575,7 +592,8 @@ struct MineRun {
     auto count_level = [&](int L) {
       kern::LevelCountArgs a{Wp, minsup, L == 1 ? gram : nullptr, F, d_ids, out_parent.p,
                              out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1),
-                             stream_dl, L == trace_level ? d_trace : nullptr, deferred};
+                             stream_dl, L == trace_level ? d_trace : nullptr, deferred,
+                             copy_blocks(), copy_last()};
       const int64_t hint = hint_at(ob->cand_hint, L);
       const int g = grid_for_tiles(hint < 0 ? -1 : (hint + kern::level_tile() - 1) / kern::level_tile());
       kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a,
@@ -1261,7 +1279,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     auto u = [](const void* p) { return (uint64_t)(uintptr_t)p; };
     key = {u(d_desc), u(d_cnt), u(d_own_bm_), (uint64_t)need, u(d_items_), u(d_tx_ptr_),
            (uint64_t)nnz_, (uint64_t)n_tx_, (uint64_t)I, (uint64_t)Wp, run.minsup, c1,
-           (uint64_t)cfg.max_len, (uint64_t)run.stream_dl, (uint64_t)deferred_dl(),
+           (uint64_t)cfg.max_len, (uint64_t)run.stream_dl, (uint64_t)deferred_dl(), (uint64_t)copy_blocks(), (uint64_t)copy_last(),
            (uint64_t)part_rank, (uint64_t)part_world, u(run.out_parent.p), u(run.out_item.p),
            u(run.out_count.p), u(run.out_depth.p), (uint64_t)out_cap, u(out_->status),
            u(out_->tile_row), (uint64_t)n_cus_, (uint64_t)out_->depth_hint, u(call_params_),

@@ -138,8 +138,15 @@ struct LevelCountArgs {
   // level's nodes (this level's rows, finished by the previous launch) from the device trie to
   // the host trie while the tile blocks run; false = survivors written to the host inline
   bool deferred_dl;
+  int copy_blocks;  // copy blocks of the grid when deferred_dl (default kCopyBlocks)
+  bool copy_last;   // copy blocks at the end of the grid instead of leading it (A/B)
 };
-constexpr int kCopyBlocks = 64;
+// Few copy blocks on purpose: GPU writes to pinned host memory share the L2 -> fabric write path
+// with the tiles' HBM stores, and a saturated PCIe link backs that path up (a level-6 trace showed
+// tile phase 1 at 42 µs with 64 copy blocks vs 19 µs without concurrent copies).  Headline A/B,
+// ms/step by copy blocks per launch: 4: 0.78, 8: 0.68, 12: 0.66, 16: 0.65-0.66, 24: 0.69, 32: 0.70,
+// 64: 0.71, 128: 0.71 (KMLS_COPY_BLOCKS overrides).
+constexpr int kCopyBlocks = 16;
 // device-resident prologue (single GPU, small vocabularies): selection + root descriptor
 // without a host round trip.  select: items with cnt >= c1, ranked by (count asc, id asc)
 // (= select_frequent), F → desc[1].n_rows.  root_setup: level-1 trie nodes, root cand_off

@@ -127,16 +127,90 @@ __device__ __forceinline__ void host_store(const HostTrie& h, FCtl* ctl, int64_t
   h.depth[node] = dep;
 }
 
+// Trie nodes [base, base + n) from the device trie arrays to the host trie; this thread copies
+// relative nodes first, first + step, ... in rounds of kCopyBatch whose loads are all issued
+// before its stores: CDNA's vmcnt counts stores too, so a load/store-interleaved loop waited for
+// every PCIe write of one node before the loads of the next could be consumed.  Widths are
+// uniform per call, so each width combination gets its own straight-line loop (32-bit indices
+// from uniform bases keep the batch within the count kernels' register budget).
+constexpr int kCopyBatch = 8;
+template <typename PT, typename IT, typename CT>
+__device__ __forceinline__ void copy_nodes_t(const HostTrie& h, const int64_t* __restrict__ par,
+                                             const int32_t* __restrict__ item,
+                                             const uint32_t* __restrict__ cnt,
+                                             const uint8_t* __restrict__ dep, int64_t base,
+                                             uint32_t n, uint32_t first, uint32_t step) {
+  par += base;
+  item += base;
+  cnt += base;
+  dep += base;
+  PT* __restrict__ hp = (PT*)h.parent + base;
+  IT* __restrict__ hi = (IT*)h.item + base;
+  CT* __restrict__ hc = (CT*)h.count + base;
+  uint8_t* __restrict__ hd = h.depth + base;
+  for (uint32_t r0 = first; r0 < n; r0 += step * kCopyBatch) {
+    int64_t p[kCopyBatch];
+    int32_t it[kCopyBatch];
+    uint32_t c[kCopyBatch];
+    uint8_t d[kCopyBatch];
+#pragma unroll
+    for (int u = 0; u < kCopyBatch; ++u) {
+      const uint32_t r = r0 + u * step;
+      if (r < n) {
+        p[u] = par[r];
+        it[u] = item[r];
+        c[u] = cnt[r];
+        d[u] = dep[r];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kCopyBatch; ++u) {
+      const uint32_t r = r0 + u * step;
+      if (r < n) {
+        hp[r] = (PT)p[u];
+        hi[r] = (IT)it[u];
+        hc[r] = (CT)c[u];
+        hd[r] = d[u];
+      }
+    }
+  }
+}
+__device__ void copy_nodes(const HostTrie& h, FCtl* ctl, const int64_t* __restrict__ par,
+                           const int32_t* __restrict__ item, const uint32_t* __restrict__ cnt,
+                           const uint8_t* __restrict__ dep, int64_t base, int64_t n,
+                           int64_t first, int64_t step) {
+  if (base + n > h.cap) {  // past the host capacity: flag it (the host retries bigger)
+    if (first == 0) ctl->dl_overflow = 1u;
+    n = max((int64_t)0, h.cap - base);
+  }
+  if (first >= n) return;
+  const uint32_t un = (uint32_t)n, uf = (uint32_t)first, us = (uint32_t)step;
+  const int sel = (h.par_w == 4 ? 4 : 0) | (h.item_w == 2 ? 2 : 0) | (h.cnt_w == 2 ? 1 : 0);
+  switch (sel) {
+    case 7: copy_nodes_t<int32_t, uint16_t, uint16_t>(h, par, item, cnt, dep, base, un, uf, us); break;
+    case 6: copy_nodes_t<int32_t, uint16_t, uint32_t>(h, par, item, cnt, dep, base, un, uf, us); break;
+    case 5: copy_nodes_t<int32_t, int32_t, uint16_t>(h, par, item, cnt, dep, base, un, uf, us); break;
+    case 4: copy_nodes_t<int32_t, int32_t, uint32_t>(h, par, item, cnt, dep, base, un, uf, us); break;
+    case 3: copy_nodes_t<int64_t, uint16_t, uint16_t>(h, par, item, cnt, dep, base, un, uf, us); break;
+    case 2: copy_nodes_t<int64_t, uint16_t, uint32_t>(h, par, item, cnt, dep, base, un, uf, us); break;
+    case 1: copy_nodes_t<int64_t, int32_t, uint16_t>(h, par, item, cnt, dep, base, un, uf, us); break;
+    default: copy_nodes_t<int64_t, int32_t, uint32_t>(h, par, item, cnt, dep, base, un, uf, us); break;
+  }
+}
+
 // Copy role of the deferred download (LevelCountArgs::deferred_dl): trie nodes
 // [desc[L-1].child_base, + desc[L].n_rows) — level L's rows, finished by the previous launch —
-// from the device trie arrays to the host trie.  Runs in kCopyBlocks dedicated blocks, so the
-// PCIe writes drain while this launch's tile blocks compute instead of stalling them.
+// from the device trie arrays to the host trie.  Runs in the first kCopyBlocks blocks of the
+// launch (dispatched before any tile block, so the PCIe writes start at once and drain while the
+// tiles compute instead of waiting for tile blocks to retire).
 __device__ void copy_prev_level(const FLevel* lv, FCtl* ctl, const LevelCountArgs& A, int cb) {
   const FLevel* pv = lv - 1;
   const int64_t base = pv->child_base, n = lv->n_rows;
-  for (int64_t i = base + (int64_t)cb * blockDim.x + threadIdx.x; i < base + n;
-       i += (int64_t)kCopyBlocks * blockDim.x)
-    host_store(ctl->h, ctl, i, A.out_parent[i], A.out_item[i], A.out_count[i], A.out_depth[i]);
+  // the destination in registers: host_store's flat stores may alias *ctl as far as the compiler
+  // knows, so reading ctl->h in the loop reloaded it (a dependent round trip) for every node
+  const HostTrie h = ctl->h;
+  copy_nodes(h, ctl, A.out_parent, A.out_item, A.out_count, A.out_depth, base, n,
+             (int64_t)cb * blockDim.x + threadIdx.x, (int64_t)A.copy_blocks * blockDim.x);
 }
 
 // Bump allocation from the device region (256-byte aligned); nullptr + overflow flag if full.
@@ -173,8 +247,8 @@ __device__ void bump_n(FCtl* ctl, const unsigned long long (&bytes)[N], void* (&
 // every tile comes from the ticket counter — never a mix: a resident block holding a ticket
 // tile could then spin on a block-index tile whose block cannot be dispatched.
 __device__ __forceinline__ int64_t next_tile(unsigned int* ticket, bool first, int64_t n_tiles,
-                                             int64_t* s_ticket, int64_t grid) {
-  if (n_tiles <= grid) return first ? (int64_t)blockIdx.x : n_tiles;
+                                             int64_t* s_ticket, int64_t grid, int64_t bid) {
+  if (n_tiles <= grid) return first ? bid : n_tiles;
   if (threadIdx.x == 0) *s_ticket = (int64_t)atomicAdd(ticket, 1u);
   __syncthreads();
   return *s_ticket;
@@ -246,7 +320,8 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
   const int64_t* __restrict__ pend = pv->row_end;
   int64_t* __restrict__ co = lv->cand_off;
   for (bool first = true;; first = false) {
-    const int64_t t = next_tile(&lv->scan_ticket, first, n_tiles, &s_ticket, (int64_t)gridDim.x);
+    const int64_t t = next_tile(&lv->scan_ticket, first, n_tiles, &s_ticket, (int64_t)gridDim.x,
+                                (int64_t)blockIdx.x);
     if (t >= n_tiles) return;
     const int64_t s0 = t * kScanTile + (int64_t)threadIdx.x * kScanItems;
     int64_t len[kScanItems];
@@ -326,17 +401,20 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   __shared__ int64_t s_ticket;
   if (ctl->overflow) return;
   epoch = (ctl->epoch_base + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
-  const int64_t tgrid = (int64_t)gridDim.x - (A.deferred_dl ? kCopyBlocks : 0);  // tile blocks
-  if ((int64_t)blockIdx.x >= tgrid) {
-    copy_prev_level(lv, ctl, A, (int)(blockIdx.x - tgrid));
+  const int cbk = A.deferred_dl ? A.copy_blocks : 0;  // copy blocks (lead the grid by default)
+  const int64_t tgrid = (int64_t)gridDim.x - cbk;     // tile blocks
+  const int64_t cb0 = A.copy_last ? tgrid : 0;
+  if ((int64_t)blockIdx.x >= cb0 && (int64_t)blockIdx.x < cb0 + cbk) {
+    copy_prev_level(lv, ctl, A, (int)(blockIdx.x - cb0));
     return;
   }
+  const int64_t bid = A.copy_last ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - cbk;
   const int64_t n_cand = lv->n_cand;
   const int64_t n_rows = lv->n_rows;
   const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
   const int64_t child_base = lv->child_base;
   if (n_tiles == 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bid == 0 && threadIdx.x == 0) {
       nx->n_rows = 0;
       nx->child_base = child_base;
       nx->cand_off = (int64_t*)bump(ctl, 8ull);
@@ -344,7 +422,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
     }
     return;
   }
-  if ((int64_t)blockIdx.x >= n_tiles) return;  // idle blocks: no ticket atomic (see scan)
+  if (bid >= n_tiles) return;  // idle blocks: no ticket atomic (see scan)
   const int64_t* __restrict__ co = lv->cand_off;
   const unsigned long long* __restrict__ bm = (const unsigned long long*)lv->bm;
   const int32_t* __restrict__ rank = lv->rank;
@@ -361,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   constexpr int kTeams = kBlock / TS;
   constexpr int kPer = kTile / kTeams;
   for (bool first = true;; first = false) {
-    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket, tgrid);
+    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket, tgrid, bid);
     if (t >= n_tiles) return;
     const int64_t c0 = t * kTile;
     const int cn = (int)min((int64_t)kTile, n_cand - c0);
@@ -536,17 +614,20 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
   __shared__ int64_t s_ticket;
   if (ctl->overflow) return;
   epoch = (ctl->epoch_base + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
-  const int64_t tgrid = (int64_t)gridDim.x - (A.deferred_dl ? kCopyBlocks : 0);  // tile blocks
-  if ((int64_t)blockIdx.x >= tgrid) {
-    copy_prev_level(lv, ctl, A, (int)(blockIdx.x - tgrid));
+  const int cbk = A.deferred_dl ? A.copy_blocks : 0;  // copy blocks (lead the grid by default)
+  const int64_t tgrid = (int64_t)gridDim.x - cbk;     // tile blocks
+  const int64_t cb0 = A.copy_last ? tgrid : 0;
+  if ((int64_t)blockIdx.x >= cb0 && (int64_t)blockIdx.x < cb0 + cbk) {
+    copy_prev_level(lv, ctl, A, (int)(blockIdx.x - cb0));
     return;
   }
+  const int64_t bid = A.copy_last ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - cbk;
   const int64_t n_cand = lv->n_cand;
   const int64_t n_rows = lv->n_rows;
   const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
   const int64_t child_base = lv->child_base;
   if (n_tiles == 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bid == 0 && threadIdx.x == 0) {
       nx->n_rows = 0;
       nx->child_base = child_base;
       nx->cand_off = (int64_t*)bump(ctl, 8ull);
@@ -554,7 +635,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
     }
     return;
   }
-  if ((int64_t)blockIdx.x >= n_tiles) return;
+  if (bid >= n_tiles) return;
   const int64_t* __restrict__ co = lv->cand_off;
   const ulonglong2* __restrict__ bm2 = (const ulonglong2*)lv->bm;
   const int32_t* __restrict__ slot = lv->slot;
@@ -568,7 +649,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
   int32_t* __restrict__ cslot = (int32_t*)nx->slot;
   const int n2 = (int)(A.Wp >> 1);
   for (bool first = true;; first = false) {
-    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket, tgrid);
+    const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket, tgrid, bid);
     if (t >= n_tiles) return;
     unsigned long long* tr = (A.trace && threadIdx.x == 0) ? A.trace + t * 8 : nullptr;
     if (tr) tr[0] = wall_clock64();
@@ -737,8 +818,8 @@ __global__ __launch_bounds__(kBlock) void k_level_copyout(const FLevel* __restri
   const int64_t S = nx->n_rows;
   if (S <= 0) return;
   const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = base + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < base + S; i += nthr)
-    host_store(h, ctl, i, d_parent[i], d_item[i], d_count[i], d_depth[i]);
+  copy_nodes(h, ctl, d_parent, d_item, d_count, d_depth, base, S,
+             (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nthr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1003,7 +1084,7 @@ void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long lon
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
                  const LevelCountArgs& a, const int32_t* tile_row, int grid, int64_t cand_hint,
                  hipStream_t s) {
-  if (a.deferred_dl) grid += kCopyBlocks;
+  if (a.deferred_dl) grid += a.copy_blocks;
   static const bool small_ok = [] {
     const char* e = std::getenv("KMLS_COUNT_SMALL");
     return !(e && e[0] == '0');

@@ -284,20 +284,23 @@ class DistMiner:
         self.ops.synchronize()
 
     # ------------------------------------------------------------------------------------
-    def step(self, download: bool = True) -> Dict:
+    def step(self, download: bool = True, reduce_count: bool = True) -> Dict:
+        """One mining call.  Replicated mode leaves every rank's sub-trie on its own host;
+        ``reduce_count=False`` skips the per-step all-reduce of the itemset count (a statistic,
+        not part of the mined result: ``global_itemsets()`` reduces the last step's count once)."""
         if self.mode == "replicate":
             r = self.ops.mine_partition(self, download)
             st = dict(r["stats"])
-            tot = torch.tensor([int(st["n_itemsets"])], dtype=torch.int64, device=self.ops.dev)
-            if self.world > 1:
-                dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-            st["global_itemsets"] = int(tot.item())
+            self._local_count = int(st["n_itemsets"])
+            if reduce_count:
+                st["global_itemsets"] = self.global_itemsets()
             self.last = r
             return {"stats": st, "trie": r}
         if self.mode == "tx":
             r = self.ops.mine_txdp(self, download and self.rank == 0)
             st = dict(r["stats"])
             st["global_itemsets"] = int(st["n_itemsets"])  # identical trie on every rank
+            self._last_global = st["global_itemsets"]
             self.last = r
             return {"stats": st, "trie": r}
         if self.world == 1 and self.backend == "gpu" and not self.force_protocol:
@@ -305,9 +308,19 @@ class DistMiner:
                             self.persistent)
             st = dict(r["stats"])
             st["global_itemsets"] = int(st["n_itemsets"])
+            self._last_global = st["global_itemsets"]
             self.last = r
             return {"stats": st, "trie": r}
         return self._step_protocol(download)
+
+    def global_itemsets(self) -> int:
+        """Itemsets mined by the last step over all ranks (one all-reduce in replicated mode)."""
+        if self.mode == "replicate":
+            tot = torch.tensor([self._local_count], dtype=torch.int64, device=self.ops.dev)
+            if self.world > 1:
+                dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+            return int(tot.item())
+        return int(self._last_global)
 
     def pair_rows(self, mode: str = "reduce_scatter"):
         """Pairs-only step (``RULES_MODE=pairs``: the reference's rule map is the pair-support
@@ -346,6 +359,7 @@ class DistMiner:
             ph["supports_allreduce"] = time.perf_counter() - t0
             if F == 0:
                 st = {"n_itemsets": 0, "global_itemsets": 0, "n_frequent_items": 0, "max_depth": 0}
+                self._last_global = 0
                 return {"stats": st, "trie": {"parent": np.zeros(0, np.int64),
                                               "item": np.zeros(0, np.int32),
                                               "count": np.zeros(0, np.uint32),
@@ -377,6 +391,7 @@ class DistMiner:
                 dist.all_reduce(tot, op=dist.ReduceOp.SUM)
             st = dict(r["stats"])
             st["global_itemsets"] = int(tot.item())
+            self._last_global = st["global_itemsets"]
             st["host_phases_s"] = ph
         self.last = r
         return {"stats": st, "trie": r}
