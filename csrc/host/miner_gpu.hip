@@ -596,6 +596,9 @@ struct MineRun {
                              copy_blocks(), copy_last()};
       const int64_t hint = hint_at(ob->cand_hint, L);
       const int g = grid_for_tiles(hint < 0 ? -1 : (hint + kern::level_tile() - 1) / kern::level_tile());
+      // the count kernels load tile_row[block] speculatively: every block index must be in bounds
+      if ((int64_t)g + kern::kCopyBlocks + 64 > ob->status_cap)
+        throw std::logic_error("levels_loop: count grid exceeds the tile_row capacity");
       kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a,
                         L == 1 ? nullptr : ob->tile_row, g, hint, s);
     };

@@ -297,11 +297,19 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
   __shared__ int64_t s_w[kBlock / 64];
   __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
-  if (ctl->overflow) return;
-  epoch = (ctl->epoch_base + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
+  // descriptor fields in one batch above the first branch (see k_level_count_small)
+  const unsigned ovf = ctl->overflow;
+  const unsigned ebase = ctl->epoch_base;
+  const unsigned long long scap = ctl->status_cap;
   const int64_t n = lv->n_rows;
+  const int32_t* __restrict__ prow = lv->prow;
+  const int64_t* __restrict__ pend = pv->row_end;
+  int64_t* __restrict__ co = lv->cand_off;
+  asm volatile("" ::"s"(ebase), "s"(scap), "s"(n), "s"(prow), "s"(pend), "s"(co));
+  if (ovf) return;
+  epoch = (ebase + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
   const int64_t n_tiles = (n + kScanTile - 1) / kScanTile;
-  if (n_tiles > (int64_t)ctl->status_cap) {
+  if (n_tiles > (int64_t)scap) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&ctl->overflow, 3u);
     return;
   }
@@ -316,9 +324,6 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
   // Idle blocks leave before touching the ticket: same-address device atomics serialise, and
   // 2048 of them per launch cost more than a small level's whole scan.
   if ((int64_t)blockIdx.x >= n_tiles) return;
-  const int32_t* __restrict__ prow = lv->prow;
-  const int64_t* __restrict__ pend = pv->row_end;
-  int64_t* __restrict__ co = lv->cand_off;
   for (bool first = true;; first = false) {
     const int64_t t = next_tile(&lv->scan_ticket, first, n_tiles, &s_ticket, (int64_t)gridDim.x,
                                 (int64_t)blockIdx.x);
@@ -351,7 +356,7 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
         co[s] = run;
         // count-tile → first row map: row s owns every tile start in [run, run + len)
         for (int64_t ct = (run + kTile - 1) / kTile; ct * kTile < run + len[i]; ++ct)
-          if (ct < (int64_t)ctl->status_cap) tile_row[ct] = (int32_t)s;
+          if (ct < (int64_t)scap) tile_row[ct] = (int32_t)s;
       }
       run += len[i];
     }
@@ -360,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
       co[n] = total;
       lv->n_cand = total;
       const int64_t tiles = (total + kTile - 1) / kTile;
-      if (lv->child_base + total > out_cap || tiles > (int64_t)ctl->status_cap ||
+      if (lv->child_base + total > out_cap || tiles > (int64_t)scap ||
           n > (int64_t)INT32_MAX) {
         atomicExch(&ctl->overflow, 4u);
       } else if (total > 0) {
@@ -612,30 +617,15 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
   __shared__ int64_t s_r0;
   __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
-  if (ctl->overflow) return;
-  epoch = (ctl->epoch_base + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
-  const int cbk = A.deferred_dl ? A.copy_blocks : 0;  // copy blocks (lead the grid by default)
-  const int64_t tgrid = (int64_t)gridDim.x - cbk;     // tile blocks
-  const int64_t cb0 = A.copy_last ? tgrid : 0;
-  if ((int64_t)blockIdx.x >= cb0 && (int64_t)blockIdx.x < cb0 + cbk) {
-    copy_prev_level(lv, ctl, A, (int)(blockIdx.x - cb0));
-    return;
-  }
-  const int64_t bid = A.copy_last ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - cbk;
+  // Every descriptor field the first tile needs, loaded as one batch before the first branch
+  // (an early-return on ctl->overflow first made these a chain of dependent round trips — about
+  // a microsecond each, on every launch), plus the tile→row entry of this block's tile in
+  // block-index mode (bid < grid <= status_cap, so the speculative load stays in bounds).
+  const unsigned ovf = ctl->overflow;
+  const unsigned ebase = ctl->epoch_base;
   const int64_t n_cand = lv->n_cand;
   const int64_t n_rows = lv->n_rows;
-  const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
   const int64_t child_base = lv->child_base;
-  if (n_tiles == 0) {
-    if (bid == 0 && threadIdx.x == 0) {
-      nx->n_rows = 0;
-      nx->child_base = child_base;
-      nx->cand_off = (int64_t*)bump(ctl, 8ull);
-      if (nx->cand_off) nx->cand_off[0] = 0;
-    }
-    return;
-  }
-  if (bid >= n_tiles) return;
   const int64_t* __restrict__ co = lv->cand_off;
   const ulonglong2* __restrict__ bm2 = (const ulonglong2*)lv->bm;
   const int32_t* __restrict__ slot = lv->slot;
@@ -647,6 +637,34 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
   int64_t* __restrict__ cgid = (int64_t*)nx->gid;
   int32_t* __restrict__ cprow = (int32_t*)nx->prow;
   int32_t* __restrict__ cslot = (int32_t*)nx->slot;
+  const int cbk = A.deferred_dl ? A.copy_blocks : 0;  // copy blocks (lead the grid by default)
+  const int64_t tgrid = (int64_t)gridDim.x - cbk;     // tile blocks
+  const int64_t cb0 = A.copy_last ? tgrid : 0;
+  const bool copy_role = (int64_t)blockIdx.x >= cb0 && (int64_t)blockIdx.x < cb0 + cbk;
+  const int64_t bid = A.copy_last ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - cbk;
+  const int32_t r0_spec = (tile_row && !copy_role) ? tile_row[bid] : 0;
+  // keep the batch above the branch (the compiler otherwise sinks each load to its first use)
+  asm volatile("" ::"s"(n_cand), "s"(n_rows), "s"(child_base), "s"(co), "s"(bm2), "s"(slot),
+               "s"(rank), "s"(gid), "s"(row_end));
+  asm volatile("" ::"s"(cbm2), "s"(crank), "s"(cgid), "s"(cprow), "s"(cslot), "s"(r0_spec),
+               "s"(ebase));
+  if (ovf) return;
+  epoch = (ebase + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
+  if (copy_role) {
+    copy_prev_level(lv, ctl, A, (int)(blockIdx.x - cb0));
+    return;
+  }
+  const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
+  if (n_tiles == 0) {
+    if (bid == 0 && threadIdx.x == 0) {
+      nx->n_rows = 0;
+      nx->child_base = child_base;
+      nx->cand_off = (int64_t*)bump(ctl, 8ull);
+      if (nx->cand_off) nx->cand_off[0] = 0;
+    }
+    return;
+  }
+  if (bid >= n_tiles) return;
   const int n2 = (int)(A.Wp >> 1);
   for (bool first = true;; first = false) {
     const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket, tgrid, bid);
@@ -656,7 +674,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
     const int64_t c0 = t * kTile;
     const int cn = (int)min((int64_t)kTile, n_cand - c0);
     if (tile_row) {  // first row of the tile, recorded by this level's scan
-      if (threadIdx.x == 0) s_r0 = tile_row[t];
+      if (threadIdx.x == 0) s_r0 = (first && n_tiles <= tgrid) ? (int64_t)r0_spec : tile_row[t];
     } else if (threadIdx.x < 64) {  // root level: 64-ary search by wave 0
       const int64_t c = c0;
       int64_t lo = 0, hi = n_rows;
