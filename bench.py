@@ -42,6 +42,8 @@ def main() -> int:
     ap.add_argument("--max-len", type=int, default=0, help="truncate itemset size (0 = all)")
     ap.add_argument("--mfma", action="store_true", help="level-2 on the i8 matrix cores")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="wait for every call before launching the next (no launch-ahead)")
     ap.add_argument("--cpu", action="store_true", help="native CPU miner (no GPU)")
     ap.add_argument("--persistent", action="store_true",
                     help="levels >= 3 in the persistent work-queue DFS kernel (A/B option)")
@@ -83,20 +85,25 @@ def main() -> int:
         dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, args.min_support, device=local_rank,
                        max_len=args.max_len, mfma=args.mfma, persistent=args.persistent)
 
-        def step():  # the itemset count is reduced over ranks once, after the timed loop
-            return dm.step(download=True, reduce_count=False)["stats"]
+        def step(prefetch=False):  # the itemset count is reduced over ranks once, after timing
+            return dm.step(download=True, reduce_count=False,
+                           prefetch=prefetch and not args.no_prefetch)["stats"]
 
         sync = dm.synchronize
         dtype = "uint64-bitmap/int32-count"
 
+    # Steady-state loop: each step launches the next step's (identical) call before waiting for
+    # its own (prefetch), so the GPU never idles on the host between calls.  The last warmup step
+    # and the last timed step launch nothing ahead: exactly `steps` calls run inside the timed
+    # bracket, and none is in flight when it opens.
     st = None
-    for _ in range(args.warmup):
-        st = step()
+    for i in range(args.warmup):
+        st = step(i < args.warmup - 1) if not args.cpu else step()
     barrier_sync()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st = step()
+    for i in range(args.steps):
+        st = step(i < args.steps - 1) if not args.cpu else step()
     sync()
     barrier_sync()
     t1 = time.perf_counter()
@@ -146,6 +153,8 @@ def main() -> int:
             "level2": "mfma-i8" if args.mfma else "popcount-bitgemm",
             "levels3plus": "persistent-dfs" if args.persistent else "level-wise",
             "levels_path": st.get("levels_path"),
+            "step_overlap": ("none" if args.cpu or args.no_prefetch else
+                             "launch-ahead: step k+1's call is launched before step k's is waited for"),
         },
         "verified_vs_cpu_miner": verified,
         "reference_seconds_ds2_0.05": REF_SECONDS_DS2_005,

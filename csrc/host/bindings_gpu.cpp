@@ -177,27 +177,28 @@ void register_gpu_bindings(py::module_& m) {
          py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
          py::arg("persistent") = false)
       .def("mine", [](gpu::GpuMiner& g, double ms, int max_len, bool pairs_only, bool download,
-                      bool gram, bool mfma, bool persistent) {
+                      bool gram, bool mfma, bool persistent, bool prefetch) {
         MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma, persistent);
         gpu::GpuMineResult r;
         {
           py::gil_scoped_release nogil;
-          r = g.mine(c, download);
+          r = g.mine(c, download, prefetch);
         }
         return result_to_dict(std::move(r));
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("pairs_only") = false,
          py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
-         py::arg("persistent") = false)
+         py::arg("persistent") = false, py::arg("prefetch") = false)
       .def("mine_partition", [](gpu::GpuMiner& g, double ms, int max_len, bool download, int rank,
-                                int world) {
+                                int world, bool prefetch) {
         gpu::GpuMineResult r;
         {
           py::gil_scoped_release nogil;
-          r = g.mine_partition(make_cfg(ms, max_len, false, true, false), download, rank, world);
+          r = g.mine_partition(make_cfg(ms, max_len, false, true, false), download, rank, world,
+                               prefetch);
         }
         return result_to_dict(std::move(r));
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("download") = true,
-         py::arg("rank") = 0, py::arg("world") = 1)
+         py::arg("rank") = 0, py::arg("world") = 1, py::arg("prefetch") = false)
       .def("mine_txdp", [](gpu::GpuMiner& g, gpu::Comm* comm, int64_t global_n_tx, double ms,
                            int max_len, bool download, bool mfma, int support_tiles) {
         gpu::GpuMineResult r;

@@ -253,6 +253,9 @@ int copy_blocks() {
 }
 
 struct MineRun {
+  hipEvent_t wait_ev = nullptr;  // set: wait for this event instead of the stream (a call was
+                                 // launched ahead behind this one)
+  bool no_more_batches = false;  // ... and so no further level batch may be enqueued
   hipStream_t s;
   DeviceArena* arena;
   int64_t Wp;
@@ -634,7 +637,8 @@ struct MineRun {
       if (first && graph_capture) end_capture(last);
      }
       t_presync = std::chrono::steady_clock::now();
-      sync_stream(s);
+      if (wait_ev) KMLS_HIP(hipEventSynchronize(wait_ev));
+      else sync_stream(s);
       t_postsync = std::chrono::steady_clock::now();
       if (b_ctl->overflow) {
         ok = false;
@@ -645,6 +649,11 @@ struct MineRun {
         break;
       }
       if (last < L_allowed && b_desc[last + 1].n_rows >= 2) {
+        if (no_more_batches) {
+          ok = false;
+          fallback_reason = "pipelined call needs more levels than its replayed plan";
+          break;
+        }
         target = std::min(L_allowed, last + 4);
         continue;
       }
@@ -832,6 +841,19 @@ struct GraphCache {
   }
 };
 
+// A steady-state resident call launched ahead (mine(prefetch=true)): its graph replay is on the
+// stream behind the call that launched it, writing to its own pinned buffers.  The next
+// mine_resident() with the same launch key adopts it instead of launching.
+struct Prefetch {
+  std::vector<uint64_t> key;
+  bool download = false;
+  int64_t host_cap = 0;
+  int pw = 0, iw = 0, cw = 0;
+  std::shared_ptr<void> h_parent, h_item, h_count, h_depth;  // pinned host trie
+  std::shared_ptr<void> fstage, back;                          // tables, readback
+  std::chrono::steady_clock::time_point t_launch;
+};
+
 GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(device) {
   KMLS_HIP(hipSetDevice(device));
   if (stream) {
@@ -850,7 +872,10 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
   *abort_host_ = 0u;
   KMLS_HIP(hipHostGetDevicePointer((void**)&abort_dev_, abort_host_, 0));
   KMLS_HIP(hipHostMalloc((void**)&h_scalar_, 64));
-  KMLS_HIP(hipHostMalloc((void**)&call_params_, sizeof(kern::FCtl)));
+  KMLS_HIP(hipHostMalloc((void**)&call_params_, 2 * sizeof(kern::FCtl)));
+  std::memset(call_params_, 0, 2 * sizeof(kern::FCtl));
+  KMLS_HIP(hipMalloc((void**)&d_call_seq_, 64));
+  KMLS_HIP(hipMemset(d_call_seq_, 0, 64));
   KMLS_HIP(hipMalloc((void**)&d_pair_, 2 * sizeof(uint64_t)));
   hipDeviceProp_t prop;
   KMLS_HIP(hipGetDeviceProperties(&prop, device));
@@ -860,6 +885,7 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
 GpuMiner::~GpuMiner() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize((hipStream_t)stream_);
+  pre_.reset();
   graph_.reset();
   if (d_tx_ptr_) (void)hipFree(d_tx_ptr_);
   if (d_items_) (void)hipFree(d_items_);
@@ -869,6 +895,7 @@ GpuMiner::~GpuMiner() {
   if (abort_host_) (void)hipHostFree(abort_host_);
   if (h_scalar_) (void)hipHostFree(h_scalar_);
   if (call_params_) (void)hipHostFree(call_params_);
+  if (d_call_seq_) (void)hipFree(d_call_seq_);
   if (sup_scratch_) (void)hipFree(sup_scratch_);
   if (d_pair_) (void)hipFree(d_pair_);
   out_.reset();
@@ -923,9 +950,17 @@ bool arena_limited(const std::string& why) {
 
 void GpuMiner::synchronize() { KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_)); }
 
+// Wait for a launched-ahead call and drop it (its buffers return to the pinned pool).
+void GpuMiner::drain_prefetch() {
+  if (!pre_) return;
+  KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_));
+  pre_.reset();
+}
+
 void GpuMiner::load_csr(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                         int64_t n_items) {
   KMLS_HIP(hipSetDevice(device_));
+  drain_prefetch();
   hipStream_t s = (hipStream_t)stream_;
   if (d_tx_ptr_) KMLS_HIP(hipFree(d_tx_ptr_));
   if (d_items_) KMLS_HIP(hipFree(d_items_));
@@ -1014,6 +1049,7 @@ void GpuMiner::bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, in
 GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineConfig& cfg,
                                      const uint8_t* owned_mask, bool emit_level1,
                                      bool download) {
+  drain_prefetch();  // a launched-ahead resident call shares the device buffers
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
   GpuMineResult res;
@@ -1173,10 +1209,19 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
 // the fused level loop one mining call has no host round trip before the final one.  Returns
 // false (nothing committed) when the fused loop overflowed; mine() then runs the host path.
 bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res, int part_rank,
-                             int part_world) {
+                             int part_world, bool prefetch) {
   hipStream_t s = (hipStream_t)stream_;
   trace::Range rg_call("kmls.mine_resident");
   auto t0 = std::chrono::steady_clock::now();
+  // a call launched ahead by the previous mine(prefetch): adopted below if its launch key matches
+  std::unique_ptr<Prefetch> adopt = std::move(pre_);
+  struct AdoptGuard {  // leaving with an un-consumed launched-ahead call (exception, early
+    hipStream_t s;     // return): wait for it before its pinned buffers go back to the pool
+    std::unique_ptr<Prefetch>& a;
+    ~AdoptGuard() {
+      if (a) (void)hipStreamSynchronize(s);
+    }
+  } adopt_guard{s, adopt};
   const int64_t I = n_items_;
   const int64_t Wp = words_local();
   constexpr int kMaxLv = 64;
@@ -1217,6 +1262,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   const int64_t cap_nodes = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 16ll << 20);
   run.ensure_out(cap_nodes);
   const int64_t out_cap = std::min<int64_t>({run.out_parent.cap, run.out_item.cap, run.out_count.cap, run.out_depth.cap});
+  bool adopt_bufs = adopt && !download && !adopt->download;  // the host trie it writes is ours
   if (download) {
     run.host_cap = std::max<int64_t>({I * 8, (int64_t)1 << 16, last_nodes_ + (last_nodes_ >> 3)});
     // compact element widths (kernels.hpp HostTrie): the download is PCIe-bound on the
@@ -1228,10 +1274,19 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     const int pw = compact && run.host_cap < (int64_t)INT32_MAX ? 4 : 8;
     const int iw = compact && I <= 65536 ? 2 : 4;
     const int cw = compact && n_tx_ <= 65535 ? 2 : 4;
-    res.h_parent = pinned_->get((size_t)run.host_cap * pw);
-    res.h_item = pinned_->get((size_t)run.host_cap * iw);
-    res.h_count = pinned_->get((size_t)run.host_cap * cw);
-    res.h_depth = pinned_->get((size_t)run.host_cap * sizeof(uint8_t));
+    adopt_bufs = adopt && adopt->download && adopt->host_cap == run.host_cap && adopt->pw == pw &&
+                 adopt->iw == iw && adopt->cw == cw;
+    if (adopt_bufs) {
+      res.h_parent = adopt->h_parent;
+      res.h_item = adopt->h_item;
+      res.h_count = adopt->h_count;
+      res.h_depth = adopt->h_depth;
+    } else {
+      res.h_parent = pinned_->get((size_t)run.host_cap * pw);
+      res.h_item = pinned_->get((size_t)run.host_cap * iw);
+      res.h_count = pinned_->get((size_t)run.host_cap * cw);
+      res.h_depth = pinned_->get((size_t)run.host_cap * sizeof(uint8_t));
+    }
     run.ht = kern::HostTrie{res.h_parent.get(), res.h_item.get(), res.h_count.get(),
                             (uint8_t*)res.h_depth.get(), run.host_cap, pw, iw, cw};
     res.par_w = pw;
@@ -1241,6 +1296,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   }
   const size_t rem = arena_->capacity() - arena_->used();
   if (rem < (512ull << 20)) {
+    if (adopt) KMLS_HIP(hipStreamSynchronize(s));
     arena_->pop_to(mark);
     res = GpuMineResult();
     return false;
@@ -1251,18 +1307,22 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   // descriptors zeroed, control block set), supports, selection (small vocabularies: one launch
   // that also writes the frequent-item tables to pinned host memory), bitmaps, gram
   // frequent-item tables for the frequent() API (ids | counts | rank_of, tab_stride apart)
-  std::shared_ptr<void> fstage = pinned_->get((size_t)tab_stride * 12);
-  run.back = pinned_->get(kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl));
-  kern::FCtl& init = *call_params_;  // pinned; the init kernel copies it into d_ctl
-  std::memset(&init, 0, sizeof(init));
-  init.bump_base = bump_base;
-  init.bump_cap = bump_bytes;
-  init.status_cap = (unsigned long long)out_->status_cap;
-  init.epoch_base = out_->begin_call(s);
-  init.h = run.ht;
-  init.host_tab = (int32_t*)fstage.get();
-  init.tab_stride = tab_stride;
-  init.rb_dst = run.back.get();
+  const size_t back_bytes = kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl);
+  std::shared_ptr<void> fstage = adopt ? adopt->fstage : pinned_->get((size_t)tab_stride * 12);
+  run.back = adopt ? adopt->back : pinned_->get(back_bytes);
+  // the control block of a call: slot (call index & 1) of the pinned parameter pair (the init
+  // kernel copies it into d_ctl); `bump`/`status` are the same for every call
+  auto fill_params = [&](kern::FCtl& init, const kern::HostTrie& ht, void* tab, void* back) {
+    std::memset(&init, 0, sizeof(init));
+    init.bump_base = bump_base;
+    init.bump_cap = bump_bytes;
+    init.status_cap = (unsigned long long)out_->status_cap;
+    init.epoch_base = out_->begin_call(s);
+    init.h = ht;
+    init.host_tab = (int32_t*)tab;
+    init.tab_stride = tab_stride;
+    init.rb_dst = back;
+  };
   const auto t_launch = std::chrono::steady_clock::now();
   const uint32_t c1 = level1_threshold((uint64_t)n_tx_, cfg.min_support);
   const bool fused_select = I <= kern::kSelectFusedMax;
@@ -1293,7 +1353,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   const bool replay = use_graph && graph_ && graph_->exec && graph_->key == key;
   auto enqueue_prologue = [&]() {
     kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl,
-                              call_params_, s);
+                              call_params_, d_call_seq_, s);
     support_counts(d_items_, nnz_, d_cnt, s);
     if (fused_select)
       kern::level_select_fused(d_cnt, I, c1, d_ids, d_fcnt, d_rank_of, d_desc, d_ctl, s);
@@ -1323,17 +1383,33 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     if (g) (void)hipGraphDestroy(g);
   };
   trace::push("kmls.prologue(enqueue)");
-  if (replay) {
+  const bool adopted = adopt && adopt_bufs && replay && adopt->key == key;
+  if (adopt && !adopted) {  // launched ahead under another plan: let it finish, then drop it
+    KMLS_HIP(hipStreamSynchronize(s));
+    adopt.reset();
+  }
+  if (!adopted) {
+    fill_params(call_params_[call_seq_ & 1], run.ht, fstage.get(), run.back.get());
+    // eager and capture calls re-sync the device call counter (slot parity) with the host's
+    if (!replay) KMLS_HIP(hipMemsetD32Async((hipDeviceptr_t)d_call_seq_, (int)(uint32_t)call_seq_, 1, s));
+  }
+  if (adopted) {  // already on the stream, behind the call that launched it
+    run.graph_replay = true;
+    run.graph_last = graph_->last;
+    out_->launch_idx = graph_->launch_idx;
+  } else if (replay) {
     run.graph_replay = true;
     run.graph_last = graph_->last;
     out_->launch_idx = graph_->launch_idx;  // later (non-graph) launches of this call continue
     KMLS_HIP(hipGraphLaunch(graph_->exec, s));
+    ++call_seq_;
   } else if (use_graph) {
     KMLS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     try {
       enqueue_prologue();
     } catch (...) {
       abort_capture();
+      if (graph_) graph_->reset(nullptr, {}, 0, 0);
       throw;
     }
     run.graph_capture = true;
@@ -1352,6 +1428,41 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     enqueue_prologue();
     KMLS_HIP(hipEventRecord(e1.e, s));
   }
+  if (!adopted && !replay) ++call_seq_;  // the eager / captured init launch
+  // Launch the next identical call before waiting for this one (steady-state replay only): its
+  // GPU work then overlaps this call's completion on the host (readback, result assembly,
+  // Python) and the launch latency of the next call.  This call's end is marked by an event.
+  Event ev_cur;
+  if (prefetch && (replay || adopted) && graph_ && graph_->exec && graph_->key == key) {
+    auto p = std::make_unique<Prefetch>();
+    p->key = key;
+    p->download = download;
+    kern::HostTrie ht2 = run.ht;
+    if (download) {
+      p->host_cap = run.host_cap;
+      p->pw = res.par_w;
+      p->iw = res.item_w;
+      p->cw = res.cnt_w;
+      p->h_parent = pinned_->get((size_t)run.host_cap * p->pw);
+      p->h_item = pinned_->get((size_t)run.host_cap * p->iw);
+      p->h_count = pinned_->get((size_t)run.host_cap * p->cw);
+      p->h_depth = pinned_->get((size_t)run.host_cap);
+      ht2 = kern::HostTrie{p->h_parent.get(), p->h_item.get(), p->h_count.get(),
+                           (uint8_t*)p->h_depth.get(), run.host_cap, p->pw, p->iw, p->cw};
+    }
+    p->fstage = pinned_->get((size_t)tab_stride * 12);
+    p->back = pinned_->get(back_bytes);
+    KMLS_HIP(hipEventRecord(ev_cur.e, s));
+    fill_params(call_params_[call_seq_ & 1], ht2, p->fstage.get(), p->back.get());
+    KMLS_HIP(hipGraphLaunch(graph_->exec, s));
+    ++call_seq_;
+    out_->launch_idx = graph_->launch_idx;
+    p->t_launch = std::chrono::steady_clock::now();
+    pre_ = std::move(p);
+    run.wait_ev = ev_cur.e;
+    run.no_more_batches = true;  // a later batch would run behind the launched-ahead call
+  }
+  const bool pipelined = adopted || pre_;
   trace::pop();
   bool ok;
   {
@@ -1364,8 +1475,20 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
         if (hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone)
           abort_capture();
       }
+      // the host call counter may now be ahead of the device's: no replay until a re-sync
+      if (graph_) graph_->reset(nullptr, {}, 0, 0);
       throw;
     }
+  }
+  // A pipelined call that cannot finish within its replayed plan (more levels than last time,
+  // a device overflow, a host-trie overflow needing the full-width copy) is redone on its own:
+  // the launched-ahead call has reused the device buffers by now.
+  if (pre_ && (!ok || (download && !run.stream_dl))) {
+    drain_prefetch();
+    arena_->pop_to(mark);
+    res = GpuMineResult();
+    if (graph_) graph_->reset(nullptr, {}, 0, 0);
+    return mine_resident(cfg, download, res, part_rank, part_world, false);
   }
   if (!ok) {
     fused_fallback_ = run.fallback_reason;
@@ -1383,7 +1506,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   }
   fi_.minsup2 = run.minsup;
   global_n_tx_ = n_tx_;
-  KMLS_HIP(hipEventRecord(e2.e, s));
+  if (!pipelined) KMLS_HIP(hipEventRecord(e2.e, s));
   const int64_t N = run.out_size;
   res.n_nodes = N;
   last_nodes_ = N;
@@ -1405,9 +1528,13 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   } else if (!download) {
     res.h_parent.reset();
   }
-  KMLS_HIP(hipStreamSynchronize(s));
+  if (!pre_) KMLS_HIP(hipStreamSynchronize(s));  // else: waited for this call's end event
   KMLS_HIP(hipStreamSynchronize(out_->copy_s));
-  if (use_graph) {
+  if (pipelined) {  // GPU events would span the neighbouring call: host clock instead
+    res.phases.push_back({adopted ? "mine(graph replay, adopted)" : "mine(graph replay, launched next)",
+                          std::chrono::duration<double, std::milli>(
+                              std::chrono::steady_clock::now() - (adopted ? adopt->t_launch : t_launch)).count()});
+  } else if (use_graph) {
     res.phases.push_back({replay ? "mine(graph replay)" : "mine(graph capture)", elapsed(e0, e2)});
   } else {
     res.phases.push_back({"prologue(support+select+encode+gram)", elapsed(e0, e1)});
@@ -1429,6 +1556,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   res.stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   res.arena_high_water = (int64_t)arena_->high_water();
   res.levels_path = part_world > 1 ? "fused-resident-partition" : "fused-resident";
+  adopt.reset();  // consumed: its buffers now belong to `res`
   arena_->pop_to(mark);
   return true;
 }
@@ -1440,13 +1568,14 @@ bool GpuMiner::resident_ok(const MineConfig& cfg) const {
          n_tx_ > 0;
 }
 
-GpuMineResult GpuMiner::mine_partition(const MineConfig& cfg, bool download, int rank, int world) {
+GpuMineResult GpuMiner::mine_partition(const MineConfig& cfg, bool download, int rank, int world,
+                                       bool prefetch) {
   KMLS_HIP(hipSetDevice(device_));
   fused_fallback_.clear();
   GpuMineResult r;
   if (!resident_ok(cfg))
     throw std::runtime_error("mine_partition: data not eligible for the device-resident path");
-  if (!mine_resident(cfg, download, r, rank, world)) {
+  if (!mine_resident(cfg, download, r, rank, world, prefetch)) {
     const bool retry = arena_limited(fused_fallback_) && grow_arena(0);
     if (!retry || !mine_resident(cfg, download, r, rank, world))
       throw std::runtime_error("mine_partition: fused path overflowed (" + fused_fallback_ + ")");
@@ -1454,18 +1583,19 @@ GpuMineResult GpuMiner::mine_partition(const MineConfig& cfg, bool download, int
   return r;
 }
 
-GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download) {
+GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download, bool prefetch) {
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
   fused_fallback_.clear();
   if (resident_ok(cfg)) {
     GpuMineResult r;
-    if (mine_resident(cfg, download, r, 0, 1)) return r;
+    if (mine_resident(cfg, download, r, 0, 1, prefetch)) return r;
     if (arena_limited(fused_fallback_) && grow_arena(0)) {  // retry once with a bigger arena
       fused_fallback_.clear();
       if (mine_resident(cfg, download, r, 0, 1)) return r;
     }
   }
+  drain_prefetch();
   auto t0 = std::chrono::steady_clock::now();
   Event e0, e1, e2;
   KMLS_HIP(hipEventRecord(e0.e, s));
@@ -1503,6 +1633,7 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download) {
 
 GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineConfig& cfg,
                                   bool download, int support_tiles) {
+  drain_prefetch();  // a launched-ahead resident call shares the device buffers
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
   auto t0 = std::chrono::steady_clock::now();

@@ -96,6 +96,7 @@ class Comm {
 
 struct OutBufs;  // persistent device trie buffers + download stream (miner_gpu.hip)
 struct GraphCache;  // captured launch sequence of the resident path (miner_gpu.hip)
+struct Prefetch;    // a resident call launched ahead of its mine() (miner_gpu.hip)
 }  // namespace gpu
 namespace kern { struct FCtl; }
 namespace gpu {
@@ -128,12 +129,16 @@ class GpuMiner {
   GpuMineResult mine_bitmaps(uintptr_t bm_dev, int64_t Wp_total, const MineConfig& cfg,
                              const uint8_t* owned_mask, bool emit_level1, bool download);
   // Convenience single-GPU path: A + B + C + D.
-  GpuMineResult mine(const MineConfig& cfg, bool download);
+  // prefetch: after launching this call, launch the next identical call (steady-state graph
+  // replay only) before waiting, so its GPU work overlaps this call's host-side completion; the
+  // next mine() with the same configuration adopts it.  At most one call is in flight ahead.
+  GpuMineResult mine(const MineConfig& cfg, bool download, bool prefetch = false);
   // Replicated-data multi-GPU step (small datasets): every rank holds the full CSR, runs the
   // device-resident prologue, and expands only the root classes the device-side snake
   // partition assigns to `rank` — no collective inside; the caller all-reduces the count.
   bool resident_ok(const MineConfig& cfg) const;
-  GpuMineResult mine_partition(const MineConfig& cfg, bool download, int rank, int world);
+  GpuMineResult mine_partition(const MineConfig& cfg, bool download, int rank, int world,
+                               bool prefetch = false);
   // Transaction-data-parallel mining (large T): this rank holds a transaction shard; supports
   // are counted in `support_tiles` tiles whose all-reduces overlap the next tile's histogram
   // (comm stream); bitmaps stay shard-local ([F][Ws] words), and every level's candidate
@@ -175,11 +180,15 @@ class GpuMiner {
   unsigned int* abort_host_ = nullptr;       // watchdog flag (pinned, device-mapped)
   const unsigned int* abort_dev_ = nullptr;
   int64_t* h_scalar_ = nullptr;   // pinned readback scratch (allocated once: hipHostFree syncs)
-  kern::FCtl* call_params_ = nullptr;  // pinned per-call control block (read by the init kernel)
+  kern::FCtl* call_params_ = nullptr;  // pinned per-call control blocks [2] (read by the init kernel)
+  unsigned int* d_call_seq_ = nullptr;  // device call counter: the init kernel reads slot seq & 1
+  uint64_t call_seq_ = 0;               // host mirror (init launches enqueued)
+  std::unique_ptr<Prefetch> pre_;       // a launched-ahead steady-state call (mine(prefetch))
+  void drain_prefetch();
   uint64_t* d_pair_ = nullptr;    // device [survivors, next-level candidates]
   int n_cus_ = 256;
   bool mine_resident(const MineConfig& cfg, bool download, GpuMineResult& res, int part_rank,
-                     int part_world);
+                     int part_world, bool prefetch = false);
   // default-sized arenas start at 8 GiB and grow (x4, up to arena_max_) when the fused path
   // runs out of room; false if fixed-size, busy or already at the maximum
   bool grow_arena(size_t min_bytes);

@@ -155,9 +155,11 @@ constexpr int64_t kSelectMaxItems = 16384;
 // one launch for the per-call device state of the resident path: zero the support histogram
 // and the bitmap buffer, zero the level descriptors and copy the control block from `params`
 // (pinned host memory the host fills before the call; read at execution time, so a captured
-// graph picks up each call's values)
+// graph picks up each call's values).  `params` holds two slots: the kernel reads slot
+// (*seq & 1) and increments the device call counter *seq.
 void level_prologue_init(uint32_t* cnt, int64_t n_items, uint64_t* bm, int64_t bm_words,
-                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl* params, hipStream_t s);
+                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl* params,
+                         unsigned int* seq, hipStream_t s);
 // selection in one launch for small vocabularies (n_items <= kSelectFusedMax): every thread
 // ranks its item against all others (no rank accumulator, no memset) and also writes rank_of
 // (the third of the frequent-item tables ids | counts | rank_of) straight to FCtl::host_tab

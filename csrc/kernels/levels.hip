@@ -871,14 +871,21 @@ __global__ __launch_bounds__(256) void k_prologue_init(uint32_t* __restrict__ cn
                                                        uint64_t* __restrict__ bm, int64_t bm_words,
                                                        FLevel* __restrict__ desc, int n_desc,
                                                        FCtl* __restrict__ ctl,
-                                                       const FCtl* __restrict__ params) {
+                                                       const FCtl* __restrict__ params,
+                                                       unsigned int* __restrict__ seq) {
   const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int64_t i = tid; i < n_items; i += nthr) cnt[i] = 0u;
   for (int64_t i = tid; i < bm_words; i += nthr) bm[i] = 0ull;
   const int64_t dwords = (int64_t)n_desc * (int64_t)(sizeof(FLevel) / 8);
   for (int64_t i = tid; i < dwords; i += nthr) ((unsigned long long*)desc)[i] = 0ull;
-  if (tid == 0) *ctl = *params;
+  // two parameter slots, alternating per call (the host fills slot (call index & 1)), so the
+  // host can prepare and launch call n+1 while call n is still running
+  if (tid == 0) {
+    const unsigned int k = *seq;
+    *ctl = params[k & 1u];
+    *seq = k + 1u;
+  }
 }
 
 // 16 lanes per item, each comparing against every 16th item (a one-thread-per-item loop ran
@@ -1157,11 +1164,12 @@ void level_select(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32_t* id
 }
 
 void level_prologue_init(uint32_t* cnt, int64_t n_items, uint64_t* bm, int64_t bm_words,
-                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl* params, hipStream_t s) {
+                         FLevel* desc, int n_desc, FCtl* ctl, const FCtl* params,
+                         unsigned int* seq, hipStream_t s) {
   const int64_t work = std::max<int64_t>(std::max<int64_t>(n_items, bm_words), 1);
   const unsigned blocks = (unsigned)std::min<int64_t>((work + 255) / 256, 2048);
   hipLaunchKernelGGL(k_prologue_init, dim3(blocks), dim3(256), 0, s, cnt, n_items, bm, bm_words,
-                     desc, n_desc, ctl, params);
+                     desc, n_desc, ctl, params, seq);
   KMLS_HIP(hipGetLastError());
 }
 

@@ -131,8 +131,9 @@ class _GpuOps:
         import contextlib
         return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
 
-    def mine_partition(self, dm: "DistMiner", download: bool):
-        return self.g.mine_partition(dm.min_support, dm.max_len, download, dm.rank, dm.world)
+    def mine_partition(self, dm: "DistMiner", download: bool, prefetch: bool = False):
+        return self.g.mine_partition(dm.min_support, dm.max_len, download, dm.rank, dm.world,
+                                     prefetch)
 
     def mine_txdp(self, dm: "DistMiner", download: bool):
         return self.g.mine_txdp(self.comm, dm.n_tx, dm.min_support, dm.max_len, download,
@@ -284,12 +285,16 @@ class DistMiner:
         self.ops.synchronize()
 
     # ------------------------------------------------------------------------------------
-    def step(self, download: bool = True, reduce_count: bool = True) -> Dict:
+    def step(self, download: bool = True, reduce_count: bool = True,
+             prefetch: bool = False) -> Dict:
         """One mining call.  Replicated mode leaves every rank's sub-trie on its own host;
         ``reduce_count=False`` skips the per-step all-reduce of the itemset count (a statistic,
-        not part of the mined result: ``global_itemsets()`` reduces the last step's count once)."""
+        not part of the mined result: ``global_itemsets()`` reduces the last step's count once).
+        ``prefetch=True`` (GPU, resident path): the next identical call is launched before this
+        one is waited for, so its GPU work overlaps this call's host-side completion; the next
+        ``step()`` adopts it (the steady-state loop of a serving / benchmark process)."""
         if self.mode == "replicate":
-            r = self.ops.mine_partition(self, download)
+            r = self.ops.mine_partition(self, download, prefetch)
             st = dict(r["stats"])
             self._local_count = int(st["n_itemsets"])
             if reduce_count:
@@ -305,7 +310,7 @@ class DistMiner:
             return {"stats": st, "trie": r}
         if self.world == 1 and self.backend == "gpu" and not self.force_protocol:
             r = self.g.mine(self.min_support, self.max_len, False, download, True, self.mfma,
-                            self.persistent)
+                            self.persistent, prefetch)
             st = dict(r["stats"])
             st["global_itemsets"] = int(st["n_itemsets"])
             self._last_global = st["global_itemsets"]

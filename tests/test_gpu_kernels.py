@@ -460,3 +460,41 @@ def test_graph_replay_matches_eager(gpu_mod):
         assert np.array_equal(np.sort(r["count"]), np.sort(ref[ms]["count"]))
     small = [(ms, r) for ms, r in kept if r["stats"]["n_itemsets"] < 300_000][-1]
     assert _trie_dict(small[1]) == _trie_dict(ref[small[0]])
+
+
+def test_prefetch_pipeline_matches_sync(gpu_mod):
+    """mine(prefetch=True) launches the next identical call before waiting for the current one;
+    the next mine() adopts it.  Every pipelined result (kept alive across later calls) must equal
+    the CPU miner's, a configuration change must drop the launched-ahead call cleanly, and the
+    partition entry point must pipeline the same way."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    tx = generate("ds2_weak", seed=7)
+    ref = {ms: gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms) for ms in (0.05, 0.04)}
+    g = gpu_mod.GpuMiner(0, 1 << 31, 0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    kept, phases = [], []
+    plan = [(0.05, False)] * 3 + [(0.05, True)] * 5 + [(0.05, False), (0.04, True), (0.04, True),
+                                                      (0.05, True), (0.05, True), (0.05, False)]
+    for ms, pre in plan:
+        r = g.mine(ms, prefetch=pre)
+        assert r["stats"]["n_itemsets"] == ref[ms]["stats"]["n_itemsets"], (ms, pre)
+        phases.append(next(k for k in r["stats"]["phases_ms"] if k.startswith("mine(")))
+        kept.append((ms, r))
+    assert any("adopted" in p for p in phases), phases
+    g.synchronize()
+    for ms, r in kept:  # every result buffer stayed intact while later calls ran
+        assert np.array_equal(np.sort(r["count"]), np.sort(ref[ms]["count"]))
+    assert _trie_dict(kept[6][1]) == _trie_dict(ref[0.05])
+    # replicated-partition entry point: 2 ranks' pipelined sub-tries cover the full result
+    total = 0
+    for rank in (0, 1):
+        h = gpu_mod.GpuMiner(0, 1 << 31, 0)
+        h.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+        counts = []
+        for i in range(6):
+            r = h.mine_partition(0.05, 0, True, rank, 2, i < 5)
+            counts.append(r["stats"]["n_itemsets"])
+        assert len(set(counts)) == 1, counts
+        total += counts[-1]
+        del h
+    assert total == ref[0.05]["stats"]["n_itemsets"]
