@@ -1364,15 +1364,18 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     if (kern::pair_gram_dev_needs_zero(Wp, I)) KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));
     kern::pair_gram_popcount_dev(d_own_bm_, Wp, &d_desc[1].n_rows, I, d_gram, s);
     int32_t* d_prank = nullptr;
+    const int64_t* part_cost = nullptr;
     if (part_world > 1) {  // replicated-data partition of the root classes, computed on device
       int64_t* d_cost = (int64_t*)arena_->push((size_t)I * 8);
       d_prank = (int32_t*)arena_->push((size_t)I * 4);
       kern::level_partition(d_gram, I, d_desc, run.minsup, I, d_cost, d_prank, s);
+      part_cost = d_cost;
     }
     kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
                            run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
                            d_prank, part_world, part_rank,
-                           run.stream_dl && !deferred_dl(), fused_select};
+                           run.stream_dl && !deferred_dl(), fused_select,
+                           d_prank ? nullptr : part_cost};
     kern::level_root_setup(d_desc, d_ctl, ra, s);
     if (!fused_select)  // staged to pinned memory while the levels run
       KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));

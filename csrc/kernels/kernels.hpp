@@ -190,9 +190,13 @@ struct RootSetupArgs {
   int my_rank;
   bool download;   // level-1 nodes also go straight to FCtl::h (inline download mode)
   bool host_tab;   // frequent-item ids | counts to FCtl::host_tab
+  const int64_t* cost;  // world > 1 and non-null: rank the root classes here from these costs
+                        // (F <= kRootRankMax; prank unused) instead of reading prank
 };
+constexpr int64_t kRootRankMax = 8192;
 void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s);
-// rank root classes by estimated cost (n_a^2 + 1 from the gram, desc) for the snake partition
+// rank root classes by estimated cost (n_a^2 + 1 from the gram, desc) for the snake partition;
+// with prank == nullptr only the costs are computed (the root setup ranks them)
 void level_partition(const uint32_t* gram, int64_t ld, FLevel* desc, uint32_t minsup,
                      int64_t F_max, int64_t* cost, int32_t* prank, hipStream_t s);
 int level_grid(int n_cus);

@@ -980,24 +980,44 @@ __global__ __launch_bounds__(256) void k_root_costs(const uint32_t* __restrict__
   }
 }
 
+// rank(i) = #{j : cost_j > cost_i or (cost_j == cost_i and j < i)} — (cost desc, item asc).
+// Block b ranks items [64b, 64b + 64): wave w compares them against the w-th quarter of all
+// costs (32-bit, staged through LDS and read 8 at a time so the loop is not bound by one LDS
+// round trip per compare), the partial ranks are summed in LDS and written directly.  (A 2-D
+// grid accumulating partial ranks needed a zeroed accumulator: two fill kernels plus the
+// ranking launch on every multi-GPU step.  Ranking inside the one-block root setup cost 30 µs:
+// a CU retires only 64 lane-ops per cycle.)
+constexpr int kRankChunk = 8192;
 __global__ __launch_bounds__(256) void k_rank_desc(const int64_t* __restrict__ cost,
                                                    const FLevel* desc, int32_t* __restrict__ rank) {
-  __shared__ int64_t s_c[256];
+  __shared__ __attribute__((aligned(16))) int32_t s_c[kRankChunk];
+  __shared__ int32_t s_r[4][64];
   const int64_t F = desc[1].n_rows;
-  const int64_t j0 = (int64_t)blockIdx.y * 256;
-  if (j0 >= F || (int64_t)blockIdx.x * 256 >= F) return;
-  const int64_t jn = min((int64_t)256, F - j0);
-  if ((int64_t)threadIdx.x < jn) s_c[threadIdx.x] = cost[j0 + threadIdx.x];
-  __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= F) return;
-  const int64_t ci = cost[i];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  if ((int64_t)blockIdx.x * 64 >= F) return;
+  const int32_t ci = i < F ? (int32_t)cost[i] : 0;  // n^2 + 1 <= F^2 + 1 fits 32 bits
   int32_t r = 0;
-  for (int64_t jj = 0; jj < jn; ++jj) {
-    const int64_t cj = s_c[jj], j = j0 + jj;
-    r += (cj > ci || (cj == ci && j < i)) ? 1 : 0;
+  for (int64_t j0 = 0; j0 < F; j0 += kRankChunk) {
+    const int32_t jn = (int32_t)min((int64_t)kRankChunk, F - j0);
+    __syncthreads();
+    for (int32_t j = threadIdx.x; j < jn; j += blockDim.x) s_c[j] = (int32_t)cost[j0 + j];
+    __syncthreads();
+    const int32_t q = ((jn + 31) / 32) * 8, jb = w * q, je = min(jn, jb + q);  // 8-aligned quarters
+    const int32_t il = (int32_t)(i - j0);  // this item's index relative to the chunk
+    int32_t j = jb;
+    for (; j + 8 <= je; j += 8) {
+      const int4 c0 = *(const int4*)&s_c[j];
+      const int4 c1 = *(const int4*)&s_c[j + 4];
+      const int32_t cj[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) r += (cj[u] > ci || (cj[u] == ci && j + u < il)) ? 1 : 0;
+    }
+    for (; j < je; ++j) r += (s_c[j] > ci || (s_c[j] == ci && j < il)) ? 1 : 0;
   }
-  if (r) atomicAdd(&rank[i], r);
+  s_r[w][lane] = r;
+  __syncthreads();
+  if (w == 0 && i < F) rank[i] = s_r[0][lane] + s_r[1][lane] + s_r[2][lane] + s_r[3][lane];
 }
 
 __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* ctl,
@@ -1005,6 +1025,7 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
   __shared__ int ok;
   __shared__ int64_t s_scan[1024];
   __shared__ int64_t s_carry;
+  __shared__ __attribute__((aligned(16))) int32_t s_cost[kRootRankMax];
   const int64_t F = desc[1].n_rows;
   // root candidate offsets: every class owned → closed form; else a block scan of the owned
   // classes' lengths (F - a - 1)
@@ -1014,12 +1035,36 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     for (int64_t i = threadIdx.x; i <= F; i += blockDim.x) a.cand_off[i] = i * (2 * F - i - 1) / 2;
   } else {
     if (threadIdx.x == 0) s_carry = 0;
+    // in-kernel ranking (cost desc, item asc): costs n^2 + 1 <= F^2 + 1 fit in 32 bits
+    const bool own_rank = a.cost && F <= kRootRankMax;
+    if (own_rank)
+      for (int64_t i = threadIdx.x; i < F; i += blockDim.x) s_cost[i] = (int32_t)a.cost[i];
     __syncthreads();
     for (int64_t base = 0; base <= F; base += blockDim.x) {
       const int64_t i = base + threadIdx.x;
       int64_t v = 0;
       if (i < F) {
-        const int64_t k = a.prank[i], rnd = k / a.world, p = k % a.world;
+        int64_t k;
+        if (own_rank) {
+          // 8 costs per step from two 16-byte LDS reads (same address in every lane: broadcast),
+          // so the loop is not bound by one LDS round trip per compare
+          const int32_t ci = s_cost[i], ii = (int32_t)i;
+          const int32_t F8 = (int32_t)F & ~7;
+          int32_t r = 0;
+          for (int32_t j = 0; j < F8; j += 8) {
+            const int4 c0 = *(const int4*)&s_cost[j];
+            const int4 c1 = *(const int4*)&s_cost[j + 4];
+            const int32_t cj[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) r += (cj[q] > ci || (cj[q] == ci && j + q < ii)) ? 1 : 0;
+          }
+          for (int32_t j = F8; j < (int32_t)F; ++j)
+            r += (s_cost[j] > ci || (s_cost[j] == ci && j < ii)) ? 1 : 0;
+          k = r;
+        } else {
+          k = a.prank[i];
+        }
+        const int64_t rnd = k / a.world, p = k % a.world;
         const int64_t owner = (rnd % 2 == 0) ? p : a.world - 1 - p;
         v = owner == a.my_rank ? F - i - 1 : 0;
       }
@@ -1185,11 +1230,10 @@ void level_select_fused(const uint32_t* cnt, int64_t n_items, uint32_t c1, int32
 
 void level_partition(const uint32_t* gram, int64_t ld, FLevel* desc, uint32_t minsup,
                      int64_t F_max, int64_t* cost, int32_t* prank, hipStream_t s) {
-  KMLS_HIP(hipMemsetAsync(prank, 0, (size_t)F_max * 4, s));
   hipLaunchKernelGGL(k_root_costs, dim3((unsigned)std::max<int64_t>(F_max, 1)), dim3(256), 0, s,
                      gram, ld, desc, minsup, cost);
-  const unsigned nb = (unsigned)((F_max + 255) / 256);
-  hipLaunchKernelGGL(k_rank_desc, dim3(nb, nb), dim3(256), 0, s, cost, desc, prank);
+  const unsigned nb = (unsigned)std::max<int64_t>((F_max + 63) / 64, 1);
+  if (prank) hipLaunchKernelGGL(k_rank_desc, dim3(nb), dim3(256), 0, s, cost, desc, prank);
   KMLS_HIP(hipGetLastError());
 }
 
