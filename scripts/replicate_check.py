@@ -29,6 +29,14 @@ def main():
         ok = ok and np.array_equal(np.sort(merged["count"]), np.sort(ref["count"]))
         print("replicate_check", "OK" if ok else "MISMATCH", r["stats"]["global_itemsets"],
               ref["stats"]["n_itemsets"], flush=True)
+    # bench.py's timed loop: launch-ahead steps without the per-step count all-reduce, then one
+    # reduction of the last step's per-rank counts
+    for i in range(4):
+        st = dm.step(download=True, reduce_count=False, prefetch=i < 3)["stats"]
+    ok = ok and dm.global_itemsets() == int(ref["stats"]["n_itemsets"])
+    ok = ok and "adopted" in "".join(st.get("phases_ms", {}).keys())
+    if rank == 0:
+        print("replicate_check pipelined", "OK" if ok else "MISMATCH", flush=True)
     dist.barrier()
     dist.destroy_process_group()
     return 0 if ok else 1

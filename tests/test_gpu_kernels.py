@@ -387,6 +387,7 @@ def test_replicated_mode_multiprocess(gpu_mod):
                        capture_output=True, text=True, timeout=600, env=env, cwd=str(root))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "replicate_check OK" in r.stdout
+    assert "replicate_check pipelined OK" in r.stdout
 
 
 @pytest.mark.parametrize("mode", ["allreduce", "reduce_scatter", "alltoall", "ring"])
