@@ -236,6 +236,11 @@ bool deferred_dl() {
 size_t fused_bump_cap(size_t bytes);
 
 // deferred-download copy blocks per count launch (KMLS_COPY_BLOCKS, default kern::kCopyBlocks)
+// KMLS_GRAM_POPCOUNT=1: long rows too use the VALU popcount gram (A/B against the MFMA gram)
+bool gram_popcount_forced() {
+  const char* e = std::getenv("KMLS_GRAM_POPCOUNT");
+  return e && e[0] == '1';
+}
 bool copy_last() {  // KMLS_COPY_LAST=1: copy blocks at the end of the grid (A/B)
   static const bool v = [] {
     const char* e = std::getenv("KMLS_COPY_LAST");
@@ -1024,6 +1029,14 @@ int64_t GpuMiner::words_local() const {
 
 void GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_off) {
   KMLS_HIP(hipSetDevice(device_));
+  // long shards: LDS-slab encode (KMLS_ENCODE_TILED=0 keeps the atomic kernel, for A/B)
+  const char* te = std::getenv("KMLS_ENCODE_TILED");
+  const bool tiled = !(te && te[0] == '0');
+  const int64_t F = (int64_t)fi_.ids.size();
+  if (tiled && n_tx_ >= (1 << 16) &&
+      kern::encode_bitmap_tiled(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev,
+                                Wp_total, word_off, F, (hipStream_t)stream_))
+    return;
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev, Wp_total,
                       word_off, (hipStream_t)stream_);
 }
@@ -1127,7 +1140,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       uint32_t* gram = (uint32_t*)arena_->push((size_t)F * F * sizeof(uint32_t));
       KMLS_HIP(hipMemsetAsync(gram, 0, (size_t)F * F * sizeof(uint32_t), s));
       // matrix cores for long rows (large T): the int8 MFMA path moves 8x more MACs per byte
-      if (cfg.level2_mfma || Wp >= 4096)
+      if (gram_popcount_forced() ? cfg.level2_mfma : (cfg.level2_mfma || Wp >= 4096))
         kern::pair_gram_mfma_i8((const uint64_t*)bm_dev, Wp, F, gram, s);
       else
         kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -156,7 +157,144 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma(const unsigned long long
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// FP4 variant: the 0/1 operands are exact in OCP e2m1 (1.0 = nibble 0x2), and the block-scaled
+// v_mfma_scale_f32_32x32x64_f8f6f4 with FP4 operands runs at twice the i8 rate (4x bf16 per clock,
+// MI355X_MICROARCH.md matrix-core table) with K = 64 transactions = one bitmap word per MFMA.
+// Lane l (r = l&31, h = l>>5) supplies the 32 elements of word half h of its row (A: row r of the
+// tile, B: column r); whatever order the hardware assigns to elements inside a fragment, A and B
+// are expanded identically, so every product pairs the same transaction.  Bits are expanded
+// through a byte → 8-nibble LDS table (one ds_read_b32 per 8 transactions, half the bytes of the
+// i8 expansion).  The f32 accumulators hold integers exactly while a block's K slice stays below
+// 2^24 transactions (enforced by the split-K below); the epilogue converts them back to u32.
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ v8i unpack32_fp4(uint32_t bits, const uint32_t* __restrict__ lut) {
+  v8i r;
+  r[0] = (int)lut[bits & 0xFFu];
+  r[1] = (int)lut[(bits >> 8) & 0xFFu];
+  r[2] = (int)lut[(bits >> 16) & 0xFFu];
+  r[3] = (int)lut[bits >> 24];
+  r[4] = 0;
+  r[5] = 0;
+  r[6] = 0;
+  r[7] = 0;
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_pair_gram_fp4(const unsigned long long* __restrict__ bm,
+                                                        int64_t Wp, int64_t F, int64_t n_tiles,
+                                                        int64_t n_blocks, int scale,
+                                                        uint32_t* __restrict__ out) {
+  __shared__ uint32_t lut[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v |= ((uint32_t)(i >> b) & 1u) << (4 * b + 1);  // 1 → 0x2 (1.0)
+    lut[i] = v;
+  }
+  __syncthreads();
+  const int64_t orig = blockIdx.x;  // XCD-aware remap, as in k_pair_gram_mfma
+  const int64_t q = n_blocks / 8, rr = n_blocks % 8, xcd = orig % 8;
+  int64_t idx = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  int64_t ti = 0;
+  while (idx >= n_tiles - ti) { idx -= n_tiles - ti; ++ti; }
+  const int64_t tj = ti + idx;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t a0 = ti * kTile + wr * 64 + r, a1 = a0 + 32;
+  const int64_t b0 = tj * kTile + wc * 64 + r, b1 = b0 + 32;
+  const bool va0 = a0 < F, va1 = a1 < F, vb0 = b0 < F, vb1 = b1 < F;
+  const ulonglong2* pa0 = reinterpret_cast<const ulonglong2*>(bm + (va0 ? a0 : 0) * Wp);
+  const ulonglong2* pa1 = reinterpret_cast<const ulonglong2*>(bm + (va1 ? a1 : 0) * Wp);
+  const ulonglong2* pb0 = reinterpret_cast<const ulonglong2*>(bm + (vb0 ? b0 : 0) * Wp);
+  const ulonglong2* pb1 = reinterpret_cast<const ulonglong2*>(bm + (vb1 ? b1 : 0) * Wp);
+
+  v16f acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
+  const int shift = 32 * h;
+  const int64_t slice = (((Wp + gridDim.y - 1) / gridDim.y) + 3) & ~(int64_t)3;
+  const int64_t kw0 = (int64_t)blockIdx.y * slice, kw1 = min(Wp, kw0 + slice);
+  auto load = [&](int64_t w2, ulonglong2 (&A0)[2], ulonglong2 (&A1)[2], ulonglong2 (&B0)[2],
+                  ulonglong2 (&B1)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool in = w2 + u < (kw1 >> 1);
+      A0[u] = va0 && in ? pa0[w2 + u] : make_ulonglong2(0, 0);
+      A1[u] = va1 && in ? pa1[w2 + u] : make_ulonglong2(0, 0);
+      B0[u] = vb0 && in ? pb0[w2 + u] : make_ulonglong2(0, 0);
+      B1[u] = vb1 && in ? pb1[w2 + u] : make_ulonglong2(0, 0);
+    }
+  };
+  ulonglong2 nA0[2], nA1[2], nB0[2], nB1[2];
+  if ((kw0 >> 1) < (kw1 >> 1)) load(kw0 >> 1, nA0, nA1, nB0, nB1);
+  for (int64_t w2 = kw0 >> 1; w2 < (kw1 >> 1); w2 += 2) {
+    ulonglong2 A0[2], A1[2], B0[2], B1[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      A0[u] = nA0[u];
+      A1[u] = nA1[u];
+      B0[u] = nB0[u];
+      B1[u] = nB1[u];
+    }
+    if (w2 + 2 < (kw1 >> 1)) load(w2 + 2, nA0, nA1, nB0, nB1);
+#pragma unroll
+    for (int wd = 0; wd < 4; ++wd) {  // one 64-transaction word per MFMA K-step
+      const unsigned long long xa0 = (wd & 1) ? A0[wd >> 1].y : A0[wd >> 1].x;
+      const unsigned long long xa1 = (wd & 1) ? A1[wd >> 1].y : A1[wd >> 1].x;
+      const unsigned long long xb0 = (wd & 1) ? B0[wd >> 1].y : B0[wd >> 1].x;
+      const unsigned long long xb1 = (wd & 1) ? B1[wd >> 1].y : B1[wd >> 1].x;
+      const v8i fa0 = unpack32_fp4((uint32_t)(xa0 >> shift), lut);
+      const v8i fa1 = unpack32_fp4((uint32_t)(xa1 >> shift), lut);
+      const v8i fb0 = unpack32_fp4((uint32_t)(xb0 >> shift), lut);
+      const v8i fb1 = unpack32_fp4((uint32_t)(xb1 >> shift), lut);
+      acc00 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa0, fb0, acc00, 4, 4, 0, scale, 0, scale);
+      acc01 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa0, fb1, acc01, 4, 4, 0, scale, 0, scale);
+      acc10 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa1, fb0, acc10, 4, 4, 0, scale, 0, scale);
+      acc11 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa1, fb1, acc11, 4, 4, 0, scale, 0, scale);
+    }
+  }
+  const int64_t rowb0 = ti * kTile + wr * 64, colb0 = tj * kTile + wc * 64;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    const int64_t rA = rowb0 + row, rB = rowb0 + 32 + row;
+    const int64_t cA = colb0 + r, cB = colb0 + 32 + r;
+    const uint32_t v00 = (uint32_t)acc00[reg], v01 = (uint32_t)acc01[reg];
+    const uint32_t v10 = (uint32_t)acc10[reg], v11 = (uint32_t)acc11[reg];
+    if (gridDim.y == 1) {
+      if (rA < F) {
+        if (cA < F && cA > rA) out[rA * F + cA] = v00;
+        if (cB < F && cB > rA) out[rA * F + cB] = v01;
+      }
+      if (rB < F) {
+        if (cA < F && cA > rB) out[rB * F + cA] = v10;
+        if (cB < F && cB > rB) out[rB * F + cB] = v11;
+      }
+    } else {
+      if (rA < F) {
+        if (cA < F && cA > rA && v00) atomicAdd(&out[rA * F + cA], v00);
+        if (cB < F && cB > rA && v01) atomicAdd(&out[rA * F + cB], v01);
+      }
+      if (rB < F) {
+        if (cA < F && cA > rB && v10) atomicAdd(&out[rB * F + cA], v10);
+        if (cB < F && cB > rB && v11) atomicAdd(&out[rB * F + cB], v11);
+      }
+    }
+  }
+}
+
 }  // namespace
+
+// KMLS_GRAM_FP4=1: the FP4 (e2m1, block-scaled MFMA) variant; KMLS_GRAM_FP4_SCALE overrides the
+// e8m0 scale byte (127 = 1.0)
+static bool gram_fp4() {
+  const char* e = std::getenv("KMLS_GRAM_FP4");
+  return e && e[0] == '1';
+}
 
 void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s) {
   if (F < 2) return;
@@ -173,9 +311,18 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
       per_cu = 2;
     return (int64_t)std::max(1, per_cu) * std::max(1, p.multiProcessorCount);
   }();
-  const int64_t ks = std::max<int64_t>(1, std::min<int64_t>(slots / blocks, Wp / 1024));
-  hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
-                     (const unsigned long long*)bm, Wp, F, nt, blocks, out);
+  int64_t ks = std::max<int64_t>(1, std::min<int64_t>(slots / blocks, Wp / 1024));
+  if (gram_fp4()) {
+    // exact f32 accumulation: every block's K slice < 2^24 transactions (2^18 words)
+    ks = std::max<int64_t>(ks, (Wp + (1 << 18) - 1) >> 18);
+    const char* se = std::getenv("KMLS_GRAM_FP4_SCALE");
+    const int scale = se ? std::atoi(se) : 127;
+    hipLaunchKernelGGL(k_pair_gram_fp4, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
+                       (const unsigned long long*)bm, Wp, F, nt, blocks, scale, out);
+  } else {
+    hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
+                       (const unsigned long long*)bm, Wp, F, nt, blocks, out);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e));
 }

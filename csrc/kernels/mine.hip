@@ -269,6 +269,63 @@ __global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restr
   }
 }
 
+// Tiled encode for long shards (large T, F <= kEncodeTileMaxF): block b owns the 64*TW
+// transactions of word columns [b*TW, b*TW + TW) and builds that F x TW slab of the bitmap in LDS
+// (ds_or_b64), then writes it out as whole 8*TW-byte row segments.  The atomic kernel above does
+// one fabric atomic per (transaction, frequent item) with 64 waves contending for each word
+// column; here the only global traffic is the CSR read and one coalesced write of every word.
+// Items are taken kEncodeU per thread per round (loads issued together), each item's
+// transaction found by binary search over the tile's LDS copy of tx_ptr.
+constexpr int kEncodeU = 8;
+__global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restrict__ tx_ptr,
+                                                        const int32_t* __restrict__ items,
+                                                        int64_t n_tx,
+                                                        const int32_t* __restrict__ rank_of,
+                                                        unsigned long long* __restrict__ bm,
+                                                        int64_t Wp, int64_t word_off, int64_t F,
+                                                        int tw_log2) {
+  extern __shared__ unsigned long long s_bm[];  // [F][TW], then tx_ptr[64*TW + 1]
+  const int TW = 1 << tw_log2;
+  const int64_t tile_tx = 64ll << tw_log2;
+  const int64_t t0 = (int64_t)blockIdx.x * tile_tx;
+  const int nt = (int)min(tile_tx, n_tx - t0);
+  int64_t* s_ptr = (int64_t*)(s_bm + F * TW);
+  for (int64_t i = threadIdx.x; i < F * TW; i += blockDim.x) s_bm[i] = 0ull;
+  for (int i = threadIdx.x; i <= nt; i += blockDim.x) s_ptr[i] = tx_ptr[t0 + i];
+  __syncthreads();
+  const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
+  for (int64_t pb = p0; pb < p1; pb += (int64_t)blockDim.x * kEncodeU) {
+    int32_t it[kEncodeU];
+#pragma unroll
+    for (int u = 0; u < kEncodeU; ++u) {
+      const int64_t p = pb + (int64_t)u * blockDim.x + threadIdx.x;
+      it[u] = p < p1 ? items[p] : -1;
+    }
+    int32_t rk[kEncodeU];
+#pragma unroll
+    for (int u = 0; u < kEncodeU; ++u) rk[u] = it[u] >= 0 ? rank_of[it[u]] : -1;
+#pragma unroll
+    for (int u = 0; u < kEncodeU; ++u) {
+      if (rk[u] < 0) continue;
+      const int64_t p = pb + (int64_t)u * blockDim.x + threadIdx.x;
+      int lo = 0, hi = nt;  // largest lt with s_ptr[lt] <= p
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (s_ptr[mid] <= p) lo = mid; else hi = mid;
+      }
+      atomicOr(&s_bm[(int64_t)rk[u] * TW + (lo >> 6)], 1ull << (lo & 63));
+    }
+  }
+  __syncthreads();
+  // only this shard's words (ceil(n_tx/64) of them): a neighbouring shard may own the next ones
+  const int64_t wbase = word_off + (t0 >> 6);
+  const int64_t wn = min((int64_t)TW, min(Wp - wbase, ((n_tx + 63) >> 6) - (t0 >> 6)));
+  for (int64_t i = threadIdx.x; i < F * TW; i += blockDim.x) {
+    const int64_t row = i >> tw_log2, w = i & (TW - 1);
+    if (w < wn) bm[row * Wp + wbase + w] = s_bm[i];
+  }
+}
+
 // flag(i) = (i < n && cnt[i] >= minsup); scanning n+1 flags gives pos[n] = #survivors directly
 struct FlagOp {
   const uint32_t* cnt;
@@ -526,6 +583,24 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
     hipLaunchKernelGGL(k_item_support_hash, dim3(g), dim3(kBlock), 0, s, items, nnz, counts);
   }
   KMLS_HIP(hipGetLastError());
+}
+
+bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
+                         const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
+                         int64_t F, hipStream_t s) {
+  if (n_tx <= 0 || F <= 0 || F > kEncodeTileMaxF) return false;
+  // words per tile: the F x TW slab within 48 KB of LDS (3 blocks per CU), TW <= 8
+  int tw_log2 = 3;
+  while (tw_log2 > 0 && F * (8ll << tw_log2) > 48 * 1024) --tw_log2;
+  const int64_t TW = 1ll << tw_log2;
+  const size_t lds = (size_t)F * TW * 8 + (size_t)(64 * TW + 1) * 8;
+  if (lds > 64 * 1024) return false;
+  const int64_t blocks = (n_tx + 64 * TW - 1) / (64 * TW);
+  if (blocks > INT32_MAX) return false;
+  hipLaunchKernelGGL(k_encode_tile, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr, items,
+                     n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2);
+  KMLS_HIP(hipGetLastError());
+  return true;
 }
 
 void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,

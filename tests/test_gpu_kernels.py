@@ -30,11 +30,14 @@ def _onehot(tx):
     return X
 
 
-@pytest.mark.parametrize("use_mfma", [False, True])
+@pytest.mark.parametrize("use_mfma", [False, True, "fp4"])
 @pytest.mark.parametrize("shape,ms,n_tx", [("tiny", 0.02, None), ("ds2_weak", 0.03, None),
                                              ("tiny", 0.01, 5000), ("ds2", 0.05, 777)])
-def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma):
+def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     import torch
+    if use_mfma == "fp4":  # the e2m1 block-scaled MFMA variant of the matrix-core gram
+        monkeypatch.setenv("KMLS_GRAM_FP4", "1")
+        use_mfma = True
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     tx = generate(shape, seed=11, n_tx=n_tx)
     # run the miner on torch's current stream so torch allocations/fills are ordered with it
@@ -499,3 +502,38 @@ def test_prefetch_pipeline_matches_sync(gpu_mod):
         total += counts[-1]
         del h
     assert total == ref[0.05]["stats"]["n_itemsets"]
+
+
+@pytest.mark.parametrize("tiled", ["1", "0"])
+def test_encode_long_shard_matches_onehot(gpu_mod, tiled, monkeypatch):
+    """Bitmap encode of a long shard (>= 65536 transactions: the LDS-slab kernel, or the atomic
+    kernel with KMLS_ENCODE_TILED=0) equals the one-hot matrix of the frequent items bit for bit,
+    including a word offset into a wider buffer."""
+    import torch
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    monkeypatch.setenv("KMLS_ENCODE_TILED", tiled)
+    tx = generate("tiny", seed=12, n_tx=70001)
+    g = gpu_mod.GpuMiner(0, 1 << 28, torch.cuda.current_stream().cuda_stream or 0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    cnt = torch.zeros(tx.n_items, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    g.item_support(cnt.data_ptr())
+    g.synchronize()
+    F = g.select(cnt.cpu().numpy().view(np.uint32), tx.n_tx, 0.02)
+    ids, counts, _ = g.frequent()
+    assert F > 4
+    Wl = g.words_local()
+    off = 3
+    Wp = Wl + off + 1
+    bm = torch.zeros((F, Wp), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    g.encode_bitmaps(bm.data_ptr(), Wp, off)
+    g.synchronize()
+    words = bm.cpu().numpy().view(np.uint64)
+    assert not words[:, :off].any() and not words[:, off + Wl:].any()
+    bits = np.unpackbits(words[:, off:off + Wl].copy().view(np.uint8), axis=1,
+                         bitorder="little")[:, :tx.n_tx]
+    X = np.zeros((tx.n_tx, tx.n_items), dtype=np.uint8)
+    for t in range(tx.n_tx):
+        X[t, tx.items[tx.tx_ptr[t]:tx.tx_ptr[t + 1]]] = 1
+    np.testing.assert_array_equal(bits, X[:, ids].T)
