@@ -171,6 +171,141 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma(const unsigned long long
 }
 
 // ---------------------------------------------------------------------------------------------
+// LDS-staged variant (the default; KMLS_GRAM_LDS=0 selects the direct kernel above): same MFMA
+// tiling, split-K stripes and epilogue as k_pair_gram_mfma, but the operand words reach the
+// waves through LDS.  In the direct kernel every 16-byte load instruction touches 32 rows = 32
+// cache lines and uses 16 B of each; here a block stages one 16-word stripe of its 256 rows (128 A + 128 B) with coalesced loads
+// (8 lanes per 128-byte line, every line loaded once per block instead of once per wave) into a
+// double-buffered LDS slab, and the next stripe's loads are in flight in registers while the
+// current stripe's 128 MFMAs per wave run.  Rows are padded to 144 B so the ds_read_b128 lane
+// groups of the MFMA fragment reads (16 rows at one column) hit distinct banks.
+constexpr int kStageRowB = 144;                 // bytes per staged row (128 + 16 pad)
+constexpr int kStageB = 2 * kTile * kStageRowB;  // one stripe of A and B rows
+
+__global__ __launch_bounds__(256, 2) void k_pair_gram_lds(const unsigned long long* __restrict__ bm,
+                                                          int64_t Wp, int64_t F, int64_t n_tiles,
+                                                          int64_t n_blocks,
+                                                          uint32_t* __restrict__ out) {
+  __shared__ uint2 lut[256];
+  __shared__ __attribute__((aligned(16))) unsigned char stage[2][kStageB];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x)
+    lut[i] = make_uint2(nib((uint32_t)i & 0xFu), nib((uint32_t)i >> 4));
+  const int64_t orig = blockIdx.x;
+  const int64_t q = n_blocks / 8, rr = n_blocks % 8, xcd = orig % 8;
+  int64_t idx = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  int64_t ti = 0;
+  while (idx >= n_tiles - ti) { idx -= n_tiles - ti; ++ti; }
+  const int64_t tj = ti + idx;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+
+  // staging role: thread t copies 16-byte segment (t & 7) of local rows (t >> 3) + 32 k,
+  // k = 0..7 (local rows 0..127 = A tile rows, 128..255 = B tile rows)
+  const int seg = tid & 7, lrow0 = tid >> 3;
+  const int64_t W2 = Wp >> 1;  // row length in 16-byte units
+  const ulonglong2* src[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int lr = lrow0 + 32 * k;
+    const int64_t grow = lr < kTile ? ti * kTile + lr : tj * kTile + (lr - kTile);
+    src[k] = grow < F ? reinterpret_cast<const ulonglong2*>(bm + grow * Wp) + seg : nullptr;
+  }
+  const int64_t ks = gridDim.y, y = blockIdx.y;
+  const int64_t n_stripes = (Wp + kStripe - 1) / kStripe;
+  const int64_t my_stripes = y < n_stripes ? (n_stripes - y + ks - 1) / ks : 0;
+  auto gload = [&](int64_t it, ulonglong2 (&R)[8]) {
+    const int64_t u = (it * ks + y) * (kStripe / 2) + seg;  // 16-byte unit of this thread
+    const bool in = u < W2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      R[k] = (src[k] && in) ? src[k][u - seg] : make_ulonglong2(0, 0);
+  };
+  auto swrite = [&](int buf, const ulonglong2 (&R)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      *reinterpret_cast<ulonglong2*>(&stage[buf][(lrow0 + 32 * k) * kStageRowB + seg * 16]) = R[k];
+  };
+
+  v16i acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
+  const int shift = 16 * h;
+  const int la0 = wr * 64 + r, la1 = la0 + 32;
+  const int lb0 = kTile + wc * 64 + r, lb1 = lb0 + 32;
+  ulonglong2 R[8];
+  if (my_stripes > 0) gload(0, R);
+  for (int64_t it = 0; it < my_stripes; ++it) {
+    const int buf = (int)(it & 1);
+    swrite(buf, R);
+    __syncthreads();  // stripe `it` visible; buffer buf^1 (stripe it-1) no longer read
+    if (it + 1 < my_stripes) gload(it + 1, R);
+    const unsigned char* sb = stage[buf];
+    const ulonglong2* pa0 = reinterpret_cast<const ulonglong2*>(sb + la0 * kStageRowB);
+    const ulonglong2* pa1 = reinterpret_cast<const ulonglong2*>(sb + la1 * kStageRowB);
+    const ulonglong2* pb0 = reinterpret_cast<const ulonglong2*>(sb + lb0 * kStageRowB);
+    const ulonglong2* pb1 = reinterpret_cast<const ulonglong2*>(sb + lb1 * kStageRowB);
+#pragma unroll 2
+    for (int c = 0; c < (int)(kStripe / 2); c += 2) {  // 4-word chunks
+      ulonglong2 A0[2], A1[2], B0[2], B1[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        A0[u] = pa0[c + u];
+        A1[u] = pa1[c + u];
+        B0[u] = pb0[c + u];
+        B1[u] = pb1[c + u];
+      }
+#pragma unroll
+      for (int wd = 0; wd < 4; ++wd) {
+        const unsigned long long xa0 = (wd & 1) ? A0[wd >> 1].y : A0[wd >> 1].x;
+        const unsigned long long xa1 = (wd & 1) ? A1[wd >> 1].y : A1[wd >> 1].x;
+        const unsigned long long xb0 = (wd & 1) ? B0[wd >> 1].y : B0[wd >> 1].x;
+        const unsigned long long xb1 = (wd & 1) ? B1[wd >> 1].y : B1[wd >> 1].x;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int sh = 32 * half + shift;
+          const v4i fa0 = unpack16((uint32_t)(xa0 >> sh) & 0xFFFFu, lut);
+          const v4i fa1 = unpack16((uint32_t)(xa1 >> sh) & 0xFFFFu, lut);
+          const v4i fb0 = unpack16((uint32_t)(xb0 >> sh) & 0xFFFFu, lut);
+          const v4i fb1 = unpack16((uint32_t)(xb1 >> sh) & 0xFFFFu, lut);
+          acc00 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb0, acc00, 0, 0, 0);
+          acc01 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb1, acc01, 0, 0, 0);
+          acc10 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb0, acc10, 0, 0, 0);
+          acc11 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb1, acc11, 0, 0, 0);
+        }
+      }
+    }
+  }
+  const int64_t rowb0 = ti * kTile + wr * 64, colb0 = tj * kTile + wc * 64;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    const int64_t rA = rowb0 + row, rB = rowb0 + 32 + row;
+    const int64_t cA = colb0 + r, cB = colb0 + 32 + r;
+    if (gridDim.y == 1) {
+      if (rA < F) {
+        if (cA < F && cA > rA) out[rA * F + cA] = (uint32_t)acc00[reg];
+        if (cB < F && cB > rA) out[rA * F + cB] = (uint32_t)acc01[reg];
+      }
+      if (rB < F) {
+        if (cA < F && cA > rB) out[rB * F + cA] = (uint32_t)acc10[reg];
+        if (cB < F && cB > rB) out[rB * F + cB] = (uint32_t)acc11[reg];
+      }
+    } else {
+      if (rA < F) {
+        if (cA < F && cA > rA && acc00[reg]) atomicAdd(&out[rA * F + cA], (uint32_t)acc00[reg]);
+        if (cB < F && cB > rA && acc01[reg]) atomicAdd(&out[rA * F + cB], (uint32_t)acc01[reg]);
+      }
+      if (rB < F) {
+        if (cA < F && cA > rB && acc10[reg]) atomicAdd(&out[rB * F + cA], (uint32_t)acc10[reg]);
+        if (cB < F && cB > rB && acc11[reg]) atomicAdd(&out[rB * F + cB], (uint32_t)acc11[reg]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // FP4 variant: the 0/1 operands are exact in OCP e2m1 (1.0 = nibble 0x2), and the block-scaled
 // v_mfma_scale_f32_32x32x64_f8f6f4 with FP4 operands runs at twice the i8 rate (4x bf16 per clock,
 // MI355X_MICROARCH.md matrix-core table) with K = 64 transactions = one bitmap word per MFMA.
@@ -320,6 +455,12 @@ static bool gram_fp4() {
   const char* e = std::getenv("KMLS_GRAM_FP4");
   return e && e[0] == '1';
 }
+// default: the LDS-staged variant (coalesced stripe loads; 100M x 754 items: 101 -> 23 ms);
+// KMLS_GRAM_LDS=0 selects the direct-load kernel (A/B)
+static bool gram_lds() {
+  const char* e = std::getenv("KMLS_GRAM_LDS");
+  return !(e && e[0] == '0');
+}
 
 void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s) {
   if (F < 2) return;
@@ -345,6 +486,18 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
     const int scale = se ? std::atoi(se) : 127;
     hipLaunchKernelGGL(k_pair_gram_fp4, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
                        (const unsigned long long*)bm, Wp, F, nt, blocks, scale, out);
+  } else if (gram_lds()) {
+    static const int64_t slots_lds = [] {
+      int dev = 0, per_cu = 1;
+      hipDeviceProp_t p;
+      if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)512;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pair_gram_lds, 256, 0) != hipSuccess)
+        per_cu = 2;
+      return (int64_t)std::max(1, per_cu) * std::max(1, p.multiProcessorCount);
+    }();
+    const int64_t ks_lds = std::max<int64_t>(1, std::min<int64_t>(slots_lds / blocks, Wp / 256));
+    hipLaunchKernelGGL(k_pair_gram_lds, dim3((unsigned)blocks, (unsigned)ks_lds), dim3(256), 0, s,
+                       (const unsigned long long*)bm, Wp, F, nt, blocks, out);
   } else {
     hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
                        (const unsigned long long*)bm, Wp, F, nt, blocks, out);

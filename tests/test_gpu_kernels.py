@@ -30,13 +30,17 @@ def _onehot(tx):
     return X
 
 
-@pytest.mark.parametrize("use_mfma", [False, True, "fp4"])
+@pytest.mark.parametrize("use_mfma", [False, True, "fp4", "direct"])
 @pytest.mark.parametrize("shape,ms,n_tx", [("tiny", 0.02, None), ("ds2_weak", 0.03, None),
-                                             ("tiny", 0.01, 5000), ("ds2", 0.05, 777)])
+                                             ("tiny", 0.01, 5000), ("ds2", 0.05, 777),
+                                             ("ds2_weak", 0.03, 70000)])
 def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     import torch
     if use_mfma == "fp4":  # the e2m1 block-scaled MFMA variant of the matrix-core gram
         monkeypatch.setenv("KMLS_GRAM_FP4", "1")
+        use_mfma = True
+    if use_mfma == "direct":  # the direct-load MFMA gram (the default stages stripes in LDS)
+        monkeypatch.setenv("KMLS_GRAM_LDS", "0")
         use_mfma = True
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     tx = generate(shape, seed=11, n_tx=n_tx)
@@ -61,7 +65,8 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     g.synchronize()
     got = np.triu(gram.cpu().numpy().astype(np.int64), 1)
     Xf = X[:, ids]
-    ref = np.triu(Xf.T @ Xf, 1)
+    # float64 BLAS product: exact (counts < 2^53) and seconds instead of numpy's int64 loop
+    ref = np.triu(np.rint(Xf.T.astype(np.float64) @ Xf.astype(np.float64)).astype(np.int64), 1)
     np.testing.assert_array_equal(got, ref)
     # bitmap rows popcount == supports
     pc = np.array([bin(int(w) & (2**64 - 1)).count("1") for w in bm.cpu().numpy().ravel()])
