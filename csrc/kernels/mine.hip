@@ -352,29 +352,38 @@ __device__ __forceinline__ int64_t find_row(const int64_t* __restrict__ cand_off
 // ----------------------------------------------------------------------------------------
 // O8 |S|>=3: team-per-candidate AND + popcount (TS lanes of a wave64 per candidate)
 // ----------------------------------------------------------------------------------------
+// Long rows with few candidates (the 10M-100M shapes: a few hundred candidates of 1.5M words)
+// split each candidate's row into `split` contiguous slices, one team each, so the grid still
+// fills the chip; partial counts are combined with integer atomics (cnt zeroed by the host).
 template <int TS>
 __global__ __launch_bounds__(kBlock) void k_extend_count(const unsigned long long* __restrict__ bm,
                                                          int64_t Wp,
                                                          const int64_t* __restrict__ cand_off,
                                                          int64_t n_rows, int64_t c0, int64_t c1,
+                                                         int64_t split,
                                                          uint32_t* __restrict__ cnt) {
   const int tl = threadIdx.x & (TS - 1);
   const int64_t team = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / TS;
   const int64_t nteams = ((int64_t)gridDim.x * blockDim.x) / TS;
-  for (int64_t c = c0 + team; c < c1; c += nteams) {
+  const int64_t n2 = Wp >> 1;
+  for (int64_t wi = team; wi < (c1 - c0) * split; wi += nteams) {
+    const int64_t c = c0 + wi / split, part = wi % split;
     const int64_t a = find_row(cand_off, n_rows, c);
     const int64_t b = a + 1 + (c - cand_off[a]);
     const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
     const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
+    const int64_t lo = n2 * part / split, hi = n2 * (part + 1) / split;
     uint32_t s = 0;
-    const int64_t n2 = Wp >> 1;
-    for (int64_t w = tl; w < n2; w += TS) {
+    for (int64_t w = lo + tl; w < hi; w += TS) {
       const ulonglong2 u = x[w], v = y[w];
       s += (uint32_t)__popcll(u.x & v.x) + (uint32_t)__popcll(u.y & v.y);
     }
 #pragma unroll
     for (int off = TS >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, TS);
-    if (tl == 0) cnt[c - c0] = s;
+    if (tl == 0) {
+      if (split == 1) cnt[c - c0] = s;
+      else if (s) atomicAdd(&cnt[c - c0], s);
+    }
   }
 }
 
@@ -383,11 +392,13 @@ __global__ __launch_bounds__(kBlock) void k_extend_materialize(
     const unsigned long long* __restrict__ bm, int64_t Wp, const int64_t* __restrict__ cand_off,
     int64_t n_rows, const int32_t* __restrict__ rank, const int64_t* __restrict__ gid,
     const int32_t* __restrict__ ids, int64_t c0, int64_t c1, const uint32_t* __restrict__ cnt,
-    uint32_t minsup, const int64_t* __restrict__ pos, LevelOut o) {
+    uint32_t minsup, const int64_t* __restrict__ pos, int64_t split, LevelOut o) {
   const int tl = threadIdx.x & (TS - 1);
   const int64_t team = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / TS;
   const int64_t nteams = ((int64_t)gridDim.x * blockDim.x) / TS;
-  for (int64_t c = c0 + team; c < c1; c += nteams) {
+  const int64_t n2 = Wp >> 1;
+  for (int64_t wi = team; wi < (c1 - c0) * split; wi += nteams) {
+    const int64_t c = c0 + wi / split, part = wi % split;
     const uint32_t k = cnt[c - c0];
     if (k < minsup) continue;  // team-uniform
     const int64_t a = find_row(cand_off, n_rows, c);
@@ -396,12 +407,12 @@ __global__ __launch_bounds__(kBlock) void k_extend_materialize(
     const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
     const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
     ulonglong2* z = reinterpret_cast<ulonglong2*>(o.bm + s * Wp);
-    const int64_t n2 = Wp >> 1;
-    for (int64_t w = tl; w < n2; w += TS) {
+    const int64_t lo = n2 * part / split, hi = n2 * (part + 1) / split;
+    for (int64_t w = lo + tl; w < hi; w += TS) {
       const ulonglong2 u = x[w], v = y[w];
       z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
     }
-    if (tl == 0) {
+    if (tl == 0 && part == 0) {
       const int32_t rb = rank[b];
       o.rank[s] = rb;
       o.gid[s] = o.out_base + s;
@@ -728,14 +739,24 @@ void child_totals(const int64_t* cand_off, int64_t a0, int64_t a1, int64_t c0, c
     default: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                             \
   }
 
+// row slices per candidate: enough (candidate, slice) teams for ~8 wave64 teams per CU, each
+// slice >= 2048 16-byte units (32 KB per row)
+static int64_t extend_split(int64_t Wp, int64_t n_cand, int ts) {
+  if (ts != 64 || n_cand <= 0) return 1;
+  const int64_t want = (256 * 8 + n_cand - 1) / n_cand;
+  return std::max<int64_t>(1, std::min<int64_t>(want, (Wp >> 1) / 2048));
+}
+
 void extend_count(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
                   int64_t c0, int64_t c1, uint32_t* cnt, hipStream_t s) {
   if (c1 <= c0) return;
   const int ts = team_size(Wp);
   const int64_t teams_per_block = kBlock / ts;
-  const int g = grid_for(c1 - c0, (int)teams_per_block, 256 * 32);
+  const int64_t split = extend_split(Wp, c1 - c0, ts);
+  if (split > 1) KMLS_HIP(hipMemsetAsync(cnt, 0, (size_t)(c1 - c0) * sizeof(uint32_t), s));
+  const int g = grid_for((c1 - c0) * split, (int)teams_per_block, 256 * 32);
   KMLS_TEAM_DISPATCH(ts, k_extend_count, dim3(g), dim3(kBlock), 0, s,
-                     (const unsigned long long*)bm, Wp, cand_off, n_rows, c0, c1, cnt);
+                     (const unsigned long long*)bm, Wp, cand_off, n_rows, c0, c1, split, cnt);
   KMLS_HIP(hipGetLastError());
 }
 
@@ -746,10 +767,11 @@ void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off,
   if (c1 <= c0) return;
   const int ts = team_size(Wp);
   const int64_t teams_per_block = kBlock / ts;
-  const int g = grid_for(c1 - c0, (int)teams_per_block, 256 * 32);
+  const int64_t split = extend_split(Wp, c1 - c0, ts);
+  const int g = grid_for((c1 - c0) * split, (int)teams_per_block, 256 * 32);
   KMLS_TEAM_DISPATCH(ts, k_extend_materialize, dim3(g), dim3(kBlock), 0, s,
                      (const unsigned long long*)bm, Wp, cand_off, n_rows, rank, gid, ids, c0, c1,
-                     cnt, minsup, pos, o);
+                     cnt, minsup, pos, split, o);
   KMLS_HIP(hipGetLastError());
 }
 
