@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstdio>
 #include <cstring>
 
 #include "kmls/gpu.hpp"
@@ -95,6 +96,58 @@ PYBIND11_MODULE(_native, m) {
     return d;
   }, py::arg("tx_ptr"), py::arg("items"), py::arg("n_items"), py::arg("min_support"),
      py::arg("max_len") = 0, py::arg("threads") = 0, py::arg("pairs_only") = false);
+
+  m.def("mine_cpu_count", [](I64 tx_ptr, I32 items, int64_t n_items, double min_support,
+                             int max_len, int64_t cap, int threads) {
+    KMLS_CHECK(tx_ptr.size() >= 1, "tx_ptr must have T+1 entries");
+    CountResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = mine_cpu_count(tx_ptr.data(), items.data(), tx_ptr.size() - 1, n_items, min_support,
+                         max_len, cap, threads);
+    }
+    py::dict s;
+    s["n_frequent_items"] = r.n_frequent_items; s["n_itemsets"] = r.n_itemsets;
+    s["max_depth"] = r.max_depth; s["capped"] = r.capped; s["seconds"] = r.seconds;
+    s["per_level"] = r.per_level;
+    return s;
+  }, py::arg("tx_ptr"), py::arg("items"), py::arg("n_items"), py::arg("min_support"),
+     py::arg("max_len") = 0, py::arg("cap") = (int64_t)1 << 62, py::arg("threads") = 0);
+
+  m.def("trie_digest", [](py::array parent, py::array item, py::array count, py::object depth,
+                          int min_depth) {
+    const int64_t n = (int64_t)item.size();
+    KMLS_CHECK((int64_t)parent.size() == n && (int64_t)count.size() == n, "trie arrays differ in size");
+    auto cont = [](const py::array& a) {
+      KMLS_CHECK(a.flags() & py::array::c_style, "trie_digest: arrays must be C-contiguous");
+      return a.data();
+    };
+    const uint8_t* dp = nullptr;
+    U8 d8;
+    if (!depth.is_none()) {
+      d8 = depth.cast<U8>();
+      KMLS_CHECK((int64_t)d8.size() == n, "depth size differs");
+      dp = d8.data();
+    }
+    const void *pp = cont(parent), *ip = cont(item), *cp = cont(count);
+    const int pw = (int)parent.itemsize(), iw = (int)item.itemsize(), cw = (int)count.itemsize();
+    TrieDigest r;
+    {
+      py::gil_scoped_release nogil;
+      r = trie_digest(pp, pw, ip, iw, cp, cw, dp, n, min_depth);
+    }
+    char buf[64];
+    std::snprintf(buf, sizeof buf, "%016llx%016llx", (unsigned long long)r.sum,
+                  (unsigned long long)r.xr);
+    py::dict out;
+    out["n"] = r.n;
+    out["digest"] = std::string(buf);
+    out["sum"] = r.sum;
+    out["xor"] = r.xr;
+    out["per_depth"] = r.per_depth;
+    return out;
+  }, py::arg("parent"), py::arg("item"), py::arg("count"), py::arg("depth") = py::none(),
+     py::arg("min_depth") = 0);
 
   m.def("synth_transactions", [](int64_t n_tx, int64_t n_items, double mean_len, int n_genres,
                                  double affinity, double zipf_s, uint64_t seed, int threads,

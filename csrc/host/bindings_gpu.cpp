@@ -48,12 +48,21 @@ py::dict result_to_dict(gpu::GpuMineResult&& r) {
   for (auto& p : r.phases) ph[py::str(p.name)] = p.ms;
   s["phases_ms"] = ph;
   d["stats"] = s;
+  if (r.idx_nnz >= 0) {  // rule map built on the device (cfg.rule_index)
+    py::dict ix;
+    ix["nnz"] = r.idx_nnz;
+    ix["row_ptr"] = pinned_array<int64_t>(r.h_idx_row_ptr, r.n_items_idx);
+    ix["cons"] = pinned_array<int32_t>(r.h_idx_cons, r.idx_nnz);
+    ix["count"] = pinned_array<uint32_t>(r.h_idx_cnt, r.idx_nnz);
+    d["index"] = ix;
+  }
   return d;
 }
 
 MineConfig make_cfg(double ms, int max_len, bool pairs_only, bool gram, bool mfma,
-                    bool persistent = false) {
+                    bool persistent = false, bool rule_index = false) {
   MineConfig c;
+  c.rule_index = rule_index;
   c.persistent = persistent;
   c.min_support = ms;
   c.max_len = max_len;
@@ -176,9 +185,13 @@ void register_gpu_bindings(py::module_& m) {
          py::arg("pairs_only") = false, py::arg("owned") = py::none(), py::arg("emit_level1") = true,
          py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
          py::arg("persistent") = false)
+      .def("set_tie_rank", [](gpu::GpuMiner& g, I32 tie) {
+        py::gil_scoped_release nogil;
+        g.set_tie_rank(tie.data(), tie.size());
+      }, py::arg("tie"))
       .def("mine", [](gpu::GpuMiner& g, double ms, int max_len, bool pairs_only, bool download,
-                      bool gram, bool mfma, bool persistent, bool prefetch) {
-        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma, persistent);
+                      bool gram, bool mfma, bool persistent, bool prefetch, bool rule_index) {
+        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma, persistent, rule_index);
         gpu::GpuMineResult r;
         {
           py::gil_scoped_release nogil;
@@ -187,18 +200,20 @@ void register_gpu_bindings(py::module_& m) {
         return result_to_dict(std::move(r));
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("pairs_only") = false,
          py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
-         py::arg("persistent") = false, py::arg("prefetch") = false)
+         py::arg("persistent") = false, py::arg("prefetch") = false,
+         py::arg("rule_index") = false)
       .def("mine_partition", [](gpu::GpuMiner& g, double ms, int max_len, bool download, int rank,
-                                int world, bool prefetch) {
+                                int world, bool prefetch, bool rule_index) {
         gpu::GpuMineResult r;
         {
           py::gil_scoped_release nogil;
-          r = g.mine_partition(make_cfg(ms, max_len, false, true, false), download, rank, world,
-                               prefetch);
+          r = g.mine_partition(make_cfg(ms, max_len, false, true, false, false, rule_index),
+                               download, rank, world, prefetch);
         }
         return result_to_dict(std::move(r));
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("download") = true,
-         py::arg("rank") = 0, py::arg("world") = 1, py::arg("prefetch") = false)
+         py::arg("rank") = 0, py::arg("world") = 1, py::arg("prefetch") = false,
+         py::arg("rule_index") = false)
       .def("mine_txdp", [](gpu::GpuMiner& g, gpu::Comm* comm, int64_t global_n_tx, double ms,
                            int max_len, bool download, bool mfma, int support_tiles) {
         gpu::GpuMineResult r;

@@ -133,7 +133,106 @@ void expand_member(const Ctx& cx, const std::vector<Member>& cls, size_t i, int 
   }
 }
 
+// Count-only variant of expand_member: no trie, per-level totals, stops once the shared
+// counter passes `cap` (for calibration / feasibility probes of outputs too big to hold).
+struct CountCtx {
+  const uint64_t* top_bm;
+  int64_t W;
+  uint32_t minsup;
+  int max_len;
+  int64_t cap;
+  std::atomic<int64_t>* total;
+};
+
+void count_member(const CountCtx& cx, const std::vector<Member>& cls, size_t i, int depth,
+                  std::vector<uint64_t>& arena, size_t top, std::vector<int64_t>& per_level) {
+  if (cx.total->load(std::memory_order_relaxed) > cx.cap) return;
+  const int64_t W = cx.W;
+  const size_t need = top + (cls.size() - i - 1) * (size_t)W;
+  if (arena.size() < need) arena.resize(need + (need >> 1) + 1024);
+  const Member a = cls[i];
+  auto res = [&](int64_t off) {
+    return off >= 0 ? arena.data() + off : cx.top_bm + (-1 - off) * W;
+  };
+  std::vector<Member> child;
+  size_t cur = top;
+  for (size_t j = i + 1; j < cls.size(); ++j) {
+    const uint64_t* x = res(a.off);
+    const uint64_t* y = res(cls[j].off);
+    uint64_t* o = arena.data() + cur;
+    uint32_t c = 0;
+    for (int64_t w = 0; w < W; ++w) {
+      uint64_t v = x[w] & y[w];
+      o[w] = v;
+      c += (uint32_t)__builtin_popcountll(v);
+    }
+    if (c >= cx.minsup) {
+      child.push_back(Member{cls[j].rank, c, (int64_t)cur, 0});
+      cur += (size_t)W;
+    }
+  }
+  if (!child.empty()) {
+    if ((int)per_level.size() < depth + 2) per_level.resize((size_t)depth + 2, 0);
+    per_level[(size_t)depth + 1] += (int64_t)child.size();
+    cx.total->fetch_add((int64_t)child.size(), std::memory_order_relaxed);
+  }
+  if (child.size() >= 2 && (cx.max_len == 0 || depth + 1 < cx.max_len)) {
+    for (size_t k = 0; k + 1 < child.size(); ++k)
+      count_member(cx, child, k, depth + 1, arena, cur, per_level);
+  }
+}
+
 }  // namespace
+
+CountResult mine_cpu_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
+                           int64_t n_items, double min_support, int max_len, int64_t cap,
+                           int threads) {
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint32_t> cnt((size_t)n_items);
+  count_items(tx_ptr, items, n_tx, n_items, cnt.data());
+  FrequentItems fi = select_frequent(cnt.data(), n_items, (uint64_t)n_tx, min_support);
+  const int64_t F = (int64_t)fi.ids.size();
+  const int64_t W = (n_tx + 63) / 64;
+  std::vector<uint64_t> bm((size_t)(F * W), 0);
+  encode_bitmaps_cpu(tx_ptr, items, n_tx, fi.rank_of.data(), bm.data(), W);
+  CountResult r;
+  r.per_level.assign(2, 0);
+  r.per_level[1] = F;
+  std::atomic<int64_t> total{F};
+  if (F >= 2 && max_len != 1) {
+    CountCtx cx{bm.data(), W, fi.minsup2, max_len, cap, &total};
+    int nth = threads > 0 ? threads : default_threads();
+    nth = std::max(1, std::min<int>(nth, (int)F));
+    std::atomic<int64_t> next{0};
+    std::vector<Member> root((size_t)F);
+    for (int64_t j = 0; j < F; ++j) root[(size_t)j] = Member{(int32_t)j, fi.counts[j], -1 - j, 0};
+    std::vector<std::vector<int64_t>> lv((size_t)nth);
+    auto worker = [&](int t) {
+      std::vector<uint64_t> arena;
+      while (true) {
+        int64_t i = next.fetch_add(1);
+        if (i >= F - 1 || total.load(std::memory_order_relaxed) > cap) break;
+        count_member(cx, root, (size_t)i, 1, arena, 0, lv[(size_t)t]);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nth; ++t) pool.emplace_back(worker, t);
+    for (auto& th : pool) th.join();
+    for (auto& v : lv) {
+      if (v.size() > r.per_level.size()) r.per_level.resize(v.size(), 0);
+      for (size_t d = 2; d < v.size(); ++d) r.per_level[d] += v[d];
+    }
+  }
+  r.n_frequent_items = F;
+  r.n_itemsets = 0;
+  for (size_t d = 1; d < r.per_level.size(); ++d) r.n_itemsets += r.per_level[d];
+  r.capped = total.load() > cap;
+  r.max_depth = 0;
+  for (size_t d = 1; d < r.per_level.size(); ++d)
+    if (r.per_level[d] > 0) r.max_depth = (int)d;
+  r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return r;
+}
 
 ItemsetTrie mine_cpu_bitmaps(const uint64_t* bm, int64_t F, int64_t W, const FrequentItems& fi,
                              int max_len, int threads, const uint8_t* owned, MineStats* stats) {

@@ -856,6 +856,7 @@ struct Prefetch {
   int pw = 0, iw = 0, cw = 0;
   std::shared_ptr<void> h_parent, h_item, h_count, h_depth;  // pinned host trie
   std::shared_ptr<void> fstage, back;                          // tables, readback
+  std::shared_ptr<void> i_rp, i_cons, i_cnt, i_meta;           // pinned rule-map CSR
   std::chrono::steady_clock::time_point t_launch;
 };
 
@@ -885,6 +886,7 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
   hipDeviceProp_t prop;
   KMLS_HIP(hipGetDeviceProperties(&prop, device));
   n_cus_ = std::max(1, prop.multiProcessorCount);
+  if (const char* e = std::getenv("KMLS_IDX_CAP")) idx_cap_ = std::max(16ll, std::atoll(e));  // test knob
 }
 
 GpuMiner::~GpuMiner() {
@@ -903,6 +905,8 @@ GpuMiner::~GpuMiner() {
   if (d_call_seq_) (void)hipFree(d_call_seq_);
   if (sup_scratch_) (void)hipFree(sup_scratch_);
   if (d_pair_) (void)hipFree(d_pair_);
+  if (d_tie_) (void)hipFree(d_tie_);
+  if (d_inv_tie_) (void)hipFree(d_inv_tie_);
   out_.reset();
   arena_.reset();
   if (own_stream_) (void)hipStreamDestroy((hipStream_t)stream_);
@@ -955,6 +959,26 @@ bool arena_limited(const std::string& why) {
 
 void GpuMiner::synchronize() { KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_)); }
 
+void GpuMiner::set_tie_rank(const int32_t* tie, int64_t n) {
+  KMLS_CHECK(n == n_items_, "set_tie_rank: size != n_items (load_csr first)");
+  std::vector<int32_t> inv((size_t)n, -1);
+  for (int64_t i = 0; i < n; ++i) {
+    KMLS_CHECK(tie[i] >= 0 && tie[i] < n && inv[(size_t)tie[i]] < 0,
+               "set_tie_rank: not a permutation of [0, n_items)");
+    inv[(size_t)tie[i]] = (int32_t)i;
+  }
+  drain_prefetch();
+  KMLS_HIP(hipSetDevice(device_));
+  KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_));
+  if (!d_tie_) {
+    KMLS_HIP(hipMalloc((void**)&d_tie_, (size_t)std::max<int64_t>(n, 1) * 4));
+    KMLS_HIP(hipMalloc((void**)&d_inv_tie_, (size_t)std::max<int64_t>(n, 1) * 4));
+  }
+  KMLS_HIP(hipMemcpy(d_tie_, tie, (size_t)n * 4, hipMemcpyHostToDevice));
+  KMLS_HIP(hipMemcpy(d_inv_tie_, inv.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+  if (graph_) graph_->reset(nullptr, {}, 0, 0);
+}
+
 // Wait for a launched-ahead call and drop it (its buffers return to the pinned pool).
 void GpuMiner::drain_prefetch() {
   if (!pre_) return;
@@ -971,6 +995,10 @@ void GpuMiner::load_csr(const int64_t* tx_ptr, const int32_t* items, int64_t n_t
   if (d_items_) KMLS_HIP(hipFree(d_items_));
   d_tx_ptr_ = nullptr;
   d_items_ = nullptr;
+  if (d_tie_) KMLS_HIP(hipFree(d_tie_));  // a tie key belongs to one vocabulary: set it again
+  if (d_inv_tie_) KMLS_HIP(hipFree(d_inv_tie_));
+  d_tie_ = d_inv_tie_ = nullptr;
+  if (graph_) graph_->reset(nullptr, {}, 0, 0);
   n_tx_ = n_tx;
   n_items_ = n_items;
   const int64_t base = tx_ptr[0];
@@ -1252,6 +1280,38 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   int64_t* d_roff = (int64_t*)arena_->push((size_t)(I + 1) * 8);
   kern::FLevel* d_desc = (kern::FLevel*)arena_->push(kMaxLv * sizeof(kern::FLevel));
   kern::FCtl* d_ctl = (kern::FCtl*)arena_->push(sizeof(kern::FCtl));
+  // rule map (O10 pairs_to_csr) scratch and output, from the same arena
+  kern::PairsArgs pa{};
+  const int64_t icap = idx_cap_;
+  if (cfg.rule_index) {
+    if (!big_lds_) {
+      kern::pairs_enable_big_lds();
+      big_lds_ = true;
+    }
+    if (!idx_scan_bytes_) idx_scan_bytes_ = kern::pairs_scan_temp_bytes(I);
+    pa.gram = d_gram;
+    pa.ld = I;
+    pa.dF = &d_desc[1].n_rows;
+    pa.F_max = I;
+    pa.minsup = level2_threshold((uint64_t)n_tx_, cfg.min_support);
+    pa.ids = d_ids;
+    pa.rank_of = d_rank_of;
+    pa.n_items = I;
+    pa.tie = d_tie_;
+    pa.inv_tie = d_inv_tie_;
+    pa.len_r = (uint32_t*)arena_->push((size_t)I * 4);
+    pa.cursor = (uint32_t*)arena_->push((size_t)I * 4);
+    pa.len_id = (int64_t*)arena_->push((size_t)(I + 1) * 8);
+    pa.scan_temp = arena_->push(idx_scan_bytes_);
+    pa.scan_temp_bytes = idx_scan_bytes_;
+    pa.status = (unsigned int*)arena_->push(256);
+    pa.row_ptr = (int64_t*)arena_->push((size_t)(I + 1) * 8);
+    pa.ent = (unsigned long long*)arena_->push((size_t)icap * 8);
+    pa.ent_cap = icap;
+    pa.cons = (int32_t*)arena_->push((size_t)icap * 4);
+    pa.cnt = (uint32_t*)arena_->push((size_t)icap * 4);
+    pa.host = &d_ctl->ph;
+  }
   const size_t need = (size_t)std::max<int64_t>(I, 1) * Wp * sizeof(uint64_t);
   if (need > own_bm_bytes_) {
     if (d_own_bm_) KMLS_HIP(hipFree(d_own_bm_));
@@ -1323,10 +1383,43 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   const size_t back_bytes = kMaxLv * sizeof(kern::FLevel) + sizeof(kern::FCtl);
   std::shared_ptr<void> fstage = adopt ? adopt->fstage : pinned_->get((size_t)tab_stride * 12);
   run.back = adopt ? adopt->back : pinned_->get(back_bytes);
+  // pinned rule-map CSR of this call (the launched-ahead call gets its own set)
+  struct IdxHost {
+    std::shared_ptr<void> rp, cons, cnt, meta;
+    kern::PairsHost ph() const {
+      if (!meta) return kern::PairsHost{};
+      return kern::PairsHost{(int64_t*)rp.get(), (int32_t*)cons.get(), (uint32_t*)cnt.get(), cap,
+                             (int64_t*)meta.get()};
+    }
+    int64_t cap = 0;
+  };
+  auto new_idx_host = [&]() {
+    IdxHost h;
+    if (cfg.rule_index) {
+      h.cap = icap;
+      h.rp = pinned_->get((size_t)(I + 1) * 8);
+      h.cons = pinned_->get((size_t)icap * 4);
+      h.cnt = pinned_->get((size_t)icap * 4);
+      h.meta = pinned_->get(64);
+    }
+    return h;
+  };
+  IdxHost ih;
+  if (adopt && cfg.rule_index && adopt->i_meta) {
+    ih.rp = adopt->i_rp;
+    ih.cons = adopt->i_cons;
+    ih.cnt = adopt->i_cnt;
+    ih.meta = adopt->i_meta;
+    ih.cap = icap;
+  } else {
+    ih = new_idx_host();
+  }
   // the control block of a call: slot (call index & 1) of the pinned parameter pair (the init
   // kernel copies it into d_ctl); `bump`/`status` are the same for every call
-  auto fill_params = [&](kern::FCtl& init, const kern::HostTrie& ht, void* tab, void* back) {
+  auto fill_params = [&](kern::FCtl& init, const kern::HostTrie& ht, void* tab, void* back,
+                         const IdxHost& ixh) {
     std::memset(&init, 0, sizeof(init));
+    init.ph = ixh.ph();
     init.bump_base = bump_base;
     init.bump_cap = bump_bytes;
     init.status_cap = (unsigned long long)out_->status_cap;
@@ -1362,6 +1455,13 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
            (uint64_t)out_->cand_hint.size()};
     for (int64_t v : out_->cand_hint) key.push_back((uint64_t)v);
     for (int64_t v : out_->rows_hint) key.push_back((uint64_t)v);
+    key.push_back((uint64_t)cfg.rule_index);
+    if (cfg.rule_index) {
+      key.push_back((uint64_t)icap);
+      key.push_back(u(pa.ent));
+      key.push_back(u(pa.len_r));
+      key.push_back(u(d_tie_));
+    }
   }
   const bool replay = use_graph && graph_ && graph_->exec && graph_->key == key;
   auto enqueue_prologue = [&]() {
@@ -1376,6 +1476,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of, d_own_bm_, Wp, 0, s);
     if (kern::pair_gram_dev_needs_zero(Wp, I)) KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));
     kern::pair_gram_popcount_dev(d_own_bm_, Wp, &d_desc[1].n_rows, I, d_gram, s);
+    if (cfg.rule_index) kern::pairs_to_csr(pa, s);
     int32_t* d_prank = nullptr;
     const int64_t* part_cost = nullptr;
     if (part_world > 1) {  // replicated-data partition of the root classes, computed on device
@@ -1405,7 +1506,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     adopt.reset();
   }
   if (!adopted) {
-    fill_params(call_params_[call_seq_ & 1], run.ht, fstage.get(), run.back.get());
+    fill_params(call_params_[call_seq_ & 1], run.ht, fstage.get(), run.back.get(), ih);
     // eager and capture calls re-sync the device call counter (slot parity) with the host's
     if (!replay) KMLS_HIP(hipMemsetD32Async((hipDeviceptr_t)d_call_seq_, (int)(uint32_t)call_seq_, 1, s));
   }
@@ -1468,8 +1569,13 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     }
     p->fstage = pinned_->get((size_t)tab_stride * 12);
     p->back = pinned_->get(back_bytes);
+    const IdxHost ih2 = new_idx_host();
+    p->i_rp = ih2.rp;
+    p->i_cons = ih2.cons;
+    p->i_cnt = ih2.cnt;
+    p->i_meta = ih2.meta;
     KMLS_HIP(hipEventRecord(ev_cur.e, s));
-    fill_params(call_params_[call_seq_ & 1], ht2, p->fstage.get(), p->back.get());
+    fill_params(call_params_[call_seq_ & 1], ht2, p->fstage.get(), p->back.get(), ih2);
     KMLS_HIP(hipGraphLaunch(graph_->exec, s));
     ++call_seq_;
     out_->launch_idx = graph_->launch_idx;
@@ -1546,6 +1652,24 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   }
   if (!pre_) KMLS_HIP(hipStreamSynchronize(s));  // else: waited for this call's end event
   KMLS_HIP(hipStreamSynchronize(out_->copy_s));
+  if (cfg.rule_index) {
+    const int64_t* meta = (const int64_t*)ih.meta.get();
+    const int64_t nnz = meta[0], st = meta[1];
+    if (st != 0) {  // entry or host capacity exceeded: grow and redo this call on its own
+      KMLS_CHECK(!(st & 2), "rule map: a row exceeds the device sort capacity");
+      drain_prefetch();
+      arena_->pop_to(mark);
+      res = GpuMineResult();
+      if (graph_) graph_->reset(nullptr, {}, 0, 0);
+      idx_cap_ = std::max<int64_t>(idx_cap_ * 2, nnz + (nnz >> 3) + 1024);
+      return mine_resident(cfg, download, res, part_rank, part_world, false);
+    }
+    res.idx_nnz = nnz;
+    res.n_items_idx = I + 1;
+    res.h_idx_row_ptr = ih.rp;
+    res.h_idx_cons = ih.cons;
+    res.h_idx_cnt = ih.cnt;
+  }
   if (pipelined) {  // GPU events would span the neighbouring call: host clock instead
     res.phases.push_back({adopted ? "mine(graph replay, adopted)" : "mine(graph replay, launched next)",
                           std::chrono::duration<double, std::milli>(

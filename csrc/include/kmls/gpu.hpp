@@ -70,6 +70,10 @@ struct GpuMineResult {
   std::vector<Phase> phases;  // hipEvent-timed phases
   int64_t arena_high_water = 0;
   std::string levels_path = "none";  // "fused" | "chunked" | "persistent" | "none"
+  // rule map (cfg.rule_index): CSR by item id, rows sorted by (count desc, tie key asc); pinned
+  int64_t idx_nnz = -1;  // -1: not built
+  int64_t n_items_idx = 0;  // row_ptr has n_items_idx entries (n_items + 1)
+  std::shared_ptr<void> h_idx_row_ptr, h_idx_cons, h_idx_cnt;
 };
 
 // Native RCCL communicator (comm_rccl.cpp) over the librccl torch already loaded.
@@ -157,6 +161,11 @@ class GpuMiner {
   void bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp, uintptr_t C,
                     int64_t ldc);
 
+  // Tie key of the rule-map rows (e.g. the rank of each item's name, so equal scores order by
+  // consequent name as serve/index.py does); must be a permutation of [0, n_items).  Unset:
+  // item id order.
+  void set_tie_rank(const int32_t* tie, int64_t n);
+
   uintptr_t stream() const { return (uintptr_t)stream_; }
   void synchronize();
   size_t arena_capacity() const;
@@ -204,6 +213,11 @@ class GpuMiner {
   std::vector<int64_t> tile_tx_;  // 65 evenly spaced transaction boundaries of the shard
   std::vector<int64_t> tile_nnz_; // and their item offsets
   int64_t last_nodes_ = 0;        // size of the previous trie (pinned download sizing)
+  int32_t* d_tie_ = nullptr;      // rule-map tie key (item id -> rank) and its inverse
+  int32_t* d_inv_tie_ = nullptr;
+  int64_t idx_cap_ = 1 << 20;     // rule-map entry capacity (grown after an overflow)
+  size_t idx_scan_bytes_ = 0;
+  bool big_lds_ = false;
 };
 
 // Association rules on the GPU (rules_gpu.hip / kernels/rules.hip): same output and order as

@@ -48,6 +48,30 @@ ItemsetTrie mine_cpu_bitmaps(const uint64_t* bm, int64_t F, int64_t W, const Fre
 void encode_bitmaps_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                         const int32_t* rank_of, uint64_t* bm, int64_t W);
 
+// Count-only search: per-level itemset totals without a trie; stops once the running total
+// exceeds `cap` (capped = true, counts are then a lower bound).  For feasibility probes.
+struct CountResult {
+  std::vector<int64_t> per_level;  // [d] = #frequent itemsets of size d (index 0 unused)
+  int64_t n_frequent_items = 0, n_itemsets = 0;
+  int max_depth = 0;
+  bool capped = false;
+  double seconds = 0.0;
+};
+CountResult mine_cpu_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
+                           int64_t n_items, double min_support, int max_len, int64_t cap,
+                           int threads);
+
+// Order-independent content digest of an itemset trie (digest.cpp): equal digests <=> (with
+// overwhelming probability) the same multiset of (itemset, support).  Element widths in bytes:
+// parent 4|8, item 2|4|8, count 2|4.
+struct TrieDigest {
+  int64_t n = 0;
+  uint64_t sum = 0, xr = 0;
+  std::vector<int64_t> per_depth;
+};
+TrieDigest trie_digest(const void* parent, int pw, const void* item, int iw, const void* count,
+                       int cw, const uint8_t* depth, int64_t n, int min_depth = 0);
+
 // Pair supports among frequent items (rule-map fast path).
 struct PairTable {
   std::vector<int32_t> a, b;     // item ids, a has lower Eclat rank than b

@@ -108,6 +108,14 @@ struct HostTrie {
   int64_t cap;
   int par_w, item_w, cnt_w;  // bytes: 4|8, 2|4, 2|4
 };
+// Pinned destinations of the rule-map CSR (pairs.hip; meta == nullptr: no copy-out).
+struct PairsHost {   // pinned destinations of the finished CSR (meta == nullptr: no copy-out)
+  int64_t* row_ptr;  // [n_items + 1]
+  int32_t* cons;     // [cap]
+  uint32_t* cnt;     // [cap]
+  int64_t cap;
+  int64_t* meta;     // [0] = nnz, [1] = status (1 entry overflow, 2 row > sort max, 4 host cap)
+};
 // Control block of one fused mining call.  Everything that changes from call to call (epoch
 // base, pinned host destinations) lives here rather than in kernel arguments, so the launch
 // sequence of a call is invariant and can be captured once as a hipGraph and replayed.
@@ -125,6 +133,8 @@ struct FCtl {
   int64_t tab_stride;
   void* rb_dst;                    // descriptor + control-block readback (pinned)
   char pad1[8];
+  PairsHost ph;                    // rule-map CSR download destination (pinned)
+  char pad2[8];
 };
 static_assert(sizeof(FCtl) % 16 == 0, "FCtl is read back in 16-byte words");
 struct LevelCountArgs {
@@ -224,6 +234,41 @@ void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t*
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
                  const LevelCountArgs& a, const int32_t* tile_row, int grid, int64_t cand_hint,
                  hipStream_t s);
+
+// ---- rule map = pair-support CSR (pairs.hip, O10 pairs_to_csr) ----
+// Longest row the device sorts (rows are <= F-1 long; longer rows set status bit 2 and the
+// host sorts that index instead).
+constexpr int64_t kPairsSortMax = 16384;
+struct PairsArgs {
+  const uint32_t* gram;  // upper triangle (i < j < F valid), row stride ld, Eclat rank order
+  int64_t ld;
+  const int64_t* dF;     // F on the device (nullptr: F_host)
+  int64_t F_host;
+  int64_t F_max;         // grid sizing bound on F
+  uint32_t minsup;
+  const int32_t* ids;      // rank -> item id
+  const int32_t* rank_of;  // item id -> rank or -1
+  int64_t n_items;
+  const int32_t* tie;      // item id -> tie rank (nullptr: the id)
+  const int32_t* inv_tie;  // tie rank -> item id (nullptr: identity)
+  // scratch
+  uint32_t* len_r;         // [F_max]
+  uint32_t* cursor;        // [F_max]
+  int64_t* len_id;         // [n_items + 1]
+  void* scan_temp;
+  size_t scan_temp_bytes;  // pairs_scan_temp_bytes(n_items)
+  unsigned long long* ent; // [ent_cap] unsorted keys
+  int64_t ent_cap;
+  unsigned int* status;    // [1]
+  // output (device)
+  int64_t* row_ptr;        // [n_items + 1], by item id
+  int32_t* cons;           // [ent_cap]
+  uint32_t* cnt;           // [ent_cap]
+  const PairsHost* host;   // device-visible (e.g. &FCtl::ph of the call); nullptr: no copy-out
+};
+size_t pairs_scan_temp_bytes(int64_t n_items);
+void pairs_to_csr(const PairsArgs& a, hipStream_t s);
+void pairs_enable_big_lds();  // once per process/device before the first pairs_to_csr
 
 // ---- persistent DFS (dfs_persistent.hip) ----
 struct DfsTask {

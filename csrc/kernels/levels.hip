@@ -835,7 +835,8 @@ __global__ __launch_bounds__(kBlock) void k_level_copyout(const FLevel* __restri
   const int64_t base = lv->child_base;
   const int64_t S = nx->n_rows;
   if (S <= 0) return;
-  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  // the readback block (last, when present) copies no nodes: stride over the copy blocks only
+  const int64_t nthr = (int64_t)(gridDim.x - (rb_words ? 1 : 0)) * blockDim.x;
   copy_nodes(h, ctl, d_parent, d_item, d_count, d_depth, base, S,
              (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nthr);
 }

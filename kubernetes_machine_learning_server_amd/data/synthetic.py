@@ -42,15 +42,24 @@ class Shape:
     genre_affinity: float  # probability that a track is drawn from the playlist's genres
     dup_names: int = 48     # names shared by 2 URIs (ds2: 48)
     dup_rows: float = 0.01  # fraction of extra duplicate rows inside a playlist (collapsed by encoder)
+    p_two_genres: float = 0.35  # probability that a playlist mixes two genres
+    len_sigma: float = 0.6      # log-normal sigma of playlist lengths
+    calib_v2: bool = False  # deterministic curve quantiles + tail-only length rescale
 
 
 SHAPES: Dict[str, Shape] = {
     # published ds2 shape (relatorio.pdf p.6); ds1 is assumed to be the same size (753 vs 755
-    # keys).  Clustering (12 genres, affinity 0.97) is calibrated so that the mlxtend-faithful
-    # oracle needs about as long on the build host as the published 20.31 s (mlxtend, ds2,
-    # min_support 0.05): 1.16M frequent itemsets, depth 14 (see bench/calibrate.py).
-    "ds2": Shape("ds2", 2246, 2171, 240249 / 2246 / 1.01, 12, 0.97),
-    "ds1": Shape("ds1", 2246, 2171, 240249 / 2246 / 1.01, 12, 0.97),
+    # keys).  Calibrated by bench/calibrate.py (profiles/r2_calibration.md) against all three
+    # constraints the reference documents: the p.5 key curve, the sweep being minable from
+    # min_support 0.03 (9.4M itemsets there; <= 1e7) and the published 20.31 s at 0.05, which
+    # the replayed reference timed region approaches as closely as constraint 2 allows
+    # (78k itemsets, depth 10 at 0.05).
+    "ds2": Shape("ds2", 2246, 2171, 240249 / 2246 / 1.01, 6, 0.97, calib_v2=True),
+    "ds1": Shape("ds1", 2246, 2171, 240249 / 2246 / 1.01, 6, 0.97, calib_v2=True),
+    # round-1 headline shape, kept as a dense stress test: 12 genres at affinity 0.97 give
+    # 1.16M itemsets (depth 14) at 0.05 but 40M at 0.04 -- too clustered for the reference's
+    # own 0.03 sweep to have been minable, so it is not a fair stand-in for ds1/ds2
+    "ds_dense": Shape("ds_dense", 2246, 2171, 240249 / 2246 / 1.01, 12, 0.97),
     # weakly clustered variant (same support curve, 2k itemsets @0.05)
     "ds2_weak": Shape("ds2_weak", 2246, 2171, 240249 / 2246 / 1.01, 24, 0.80),
     # SURVEY §6.3 sanity shape (milder clustering)
@@ -68,13 +77,23 @@ def _target_counts(shape: Shape, rng: np.random.Generator) -> np.ndarray:
     """Per-item target playlist counts, sampled from the published survival curve."""
     sup = np.array([s for s, _ in _DS2_CURVE])
     frac = np.array([n for _, n in _DS2_CURVE], dtype=np.float64) / 2171.0
-    u = np.sort(rng.random(shape.n_items))[::-1]  # survival quantiles
+    if shape.calib_v2:  # evenly spaced survival quantiles: no sampling noise on the key curve
+        u = (np.arange(shape.n_items, 0, -1) - 0.5) / shape.n_items
+    else:
+        u = np.sort(rng.random(shape.n_items))[::-1]  # survival quantiles
     # interpolate log(support) against log(survival)
     ls = np.interp(np.log(u), np.log(frac[::-1]), np.log(sup[::-1]))
     counts = np.exp(ls) * shape.n_tx
-    # rescale so that the mean playlist length matches the shape
+    # match the mean playlist length; calib_v2 puts the whole correction on the
+    # items below the lowest published key threshold (0.03), so the key curve itself is kept
     total = shape.mean_len * shape.n_tx
-    counts *= total / counts.sum()
+    if shape.calib_v2:
+        lo = counts < 0.028 * shape.n_tx
+        hi_sum = counts[~lo].sum()
+        scale = max(total - hi_sum, 0.0) / max(counts[lo].sum(), 1e-9)
+        counts[lo] = np.minimum(counts[lo] * scale, 0.028 * shape.n_tx)
+    else:
+        counts *= total / counts.sum()
     return np.maximum(counts, 1.0)
 
 
@@ -126,8 +145,10 @@ def generate(shape: "Shape | str", seed: int = 0, n_tx: Optional[int] = None,
     item_genre = rng.integers(0, shape.n_genres, size=I)
     rank_of = rng.permutation(I)  # item i gets the rank_of[i]-th largest target
     tgt = target[rank_of]
-    lens = np.clip(rng.lognormal(np.log(shape.mean_len) - 0.18, 0.6, size=T), 2, I).astype(np.int64)
-    n_g = 1 + (rng.random(T) < 0.35)
+    sig = shape.len_sigma
+    lens = np.clip(rng.lognormal(np.log(shape.mean_len) - sig * sig / 2, sig, size=T), 2,
+                   I).astype(np.int64)
+    n_g = 1 + (rng.random(T) < shape.p_two_genres)
     g1 = rng.integers(0, shape.n_genres, size=T)
     g2 = np.where(n_g > 1, rng.integers(0, shape.n_genres, size=T), g1)
     # boost so that ~genre_affinity of a playlist's tracks come from its genres

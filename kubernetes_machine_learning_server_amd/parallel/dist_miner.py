@@ -131,9 +131,10 @@ class _GpuOps:
         import contextlib
         return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
 
-    def mine_partition(self, dm: "DistMiner", download: bool, prefetch: bool = False):
+    def mine_partition(self, dm: "DistMiner", download: bool, prefetch: bool = False,
+                       rule_index: bool = False):
         return self.g.mine_partition(dm.min_support, dm.max_len, download, dm.rank, dm.world,
-                                     prefetch)
+                                     prefetch, rule_index)
 
     def mine_txdp(self, dm: "DistMiner", download: bool):
         return self.g.mine_txdp(self.comm, dm.n_tx, dm.min_support, dm.max_len, download,
@@ -284,9 +285,14 @@ class DistMiner:
     def synchronize(self):
         self.ops.synchronize()
 
+    def set_tie_rank(self, tie: np.ndarray) -> None:
+        """Tie key of the device rule map's rows (``serve.index.name_tie_rank``)."""
+        if self.g is not None:
+            self.g.set_tie_rank(np.ascontiguousarray(tie, np.int32))
+
     # ------------------------------------------------------------------------------------
     def step(self, download: bool = True, reduce_count: bool = True,
-             prefetch: bool = False) -> Dict:
+             prefetch: bool = False, rule_index: bool = False) -> Dict:
         """One mining call.  Replicated mode leaves every rank's sub-trie on its own host;
         ``reduce_count=False`` skips the per-step all-reduce of the itemset count (a statistic,
         not part of the mined result: ``global_itemsets()`` reduces the last step's count once).
@@ -310,7 +316,7 @@ class DistMiner:
             return {"stats": st, "trie": r}
         if self.world == 1 and self.backend == "gpu" and not self.force_protocol:
             r = self.g.mine(self.min_support, self.max_len, False, download, True, self.mfma,
-                            self.persistent, prefetch)
+                            self.persistent, prefetch, rule_index)
             st = dict(r["stats"])
             st["global_itemsets"] = int(st["n_itemsets"])
             self._last_global = st["global_itemsets"]

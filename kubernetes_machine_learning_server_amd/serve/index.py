@@ -128,6 +128,27 @@ class RuleIndexData:
         return cls(int(z["n_items"]), z["row_ptr"], z["cons"], z["score"], z["is_key"], names)
 
 
+def name_tie_rank(names: Sequence[str]) -> np.ndarray:
+    """Rank of every item's name in sorted order (stable: equal names keep id order) — the
+    tie key of index rows, here and in the device rule-map kernel (``GpuMiner.set_tie_rank``)."""
+    n = len(names)
+    r = np.empty(n, np.int32)
+    r[np.argsort(np.asarray(names, dtype=object), kind="stable")] = np.arange(n, dtype=np.int32)
+    return r
+
+
+def index_from_device_csr(ix: Dict, n_items: int, single_ids: np.ndarray, n_tx: int,
+                          names: Optional[Sequence[str]] = None) -> RuleIndexData:
+    """RuleIndexData from the device-built rule map (``mine(..., rule_index=True)["index"]``):
+    rows are already in index order; keys are the frequent single items."""
+    is_key = np.zeros(n_items, np.uint8)
+    is_key[np.asarray(single_ids, np.int64)] = 1
+    score = np.asarray(ix["count"], np.float64) / float(n_tx)
+    return RuleIndexData(int(n_items), np.array(ix["row_ptr"], np.int64),
+                         np.array(ix["cons"], np.int32), score, is_key,
+                         list(names) if names is not None else None)
+
+
 def build_index_from_pairs(n_items: int, single_ids: np.ndarray, pair_a: np.ndarray,
                            pair_b: np.ndarray, pair_count: np.ndarray, n_tx: int,
                            names: Optional[Sequence[str]] = None) -> RuleIndexData:
@@ -141,8 +162,7 @@ def build_index_from_pairs(n_items: int, single_ids: np.ndarray, pair_a: np.ndar
     dst = np.concatenate([b, a])
     cnt = np.concatenate([c, c])
     if names is not None:
-        name_rank = np.empty(n_items, np.int64)
-        name_rank[np.argsort(np.asarray(names, dtype=object), kind="stable")] = np.arange(n_items)
+        name_rank = name_tie_rank(names).astype(np.int64)
         tie = name_rank[dst] if len(dst) else dst
     else:
         tie = dst

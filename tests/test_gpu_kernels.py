@@ -23,6 +23,17 @@ def _trie_dict(r):
     return out
 
 
+def _digest(gpu_mod, r):
+    return gpu_mod.trie_digest(r["parent"], r["item"], r["count"], r["depth"])
+
+
+def assert_same_itemsets(gpu_mod, r, c):
+    """Content equality of two tries: (itemset, support) multiset digest + per-size counts."""
+    dr, dc = _digest(gpu_mod, r), _digest(gpu_mod, c)
+    assert dr["per_depth"] == dc["per_depth"]
+    assert dr["digest"] == dc["digest"]
+
+
 def _onehot(tx):
     X = np.zeros((tx.n_tx, tx.n_items), dtype=np.int64)
     for t in range(tx.n_tx):
@@ -76,7 +87,8 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
 @pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("use_mfma", [False, True])
 @pytest.mark.parametrize("shape,ms", [("tiny", 0.05), ("tiny", 0.02), ("ds2_weak", 0.05),
-                                      ("ds2_weak", 0.03), ("ds2", 0.07), ("ds2", 0.05)])
+                                      ("ds2_weak", 0.03), ("ds2", 0.07), ("ds2", 0.05),
+                                      ("ds_dense", 0.05)])
 def test_gpu_miner_matches_cpu(gpu_mod, shape, ms, use_mfma, fused, monkeypatch):
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     monkeypatch.setenv("KMLS_FUSED_LEVELS", fused)
@@ -89,11 +101,9 @@ def test_gpu_miner_matches_cpu(gpu_mod, shape, ms, use_mfma, fused, monkeypatch)
     c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
     assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
     assert r["stats"]["max_depth"] == c["stats"]["max_depth"]
+    assert_same_itemsets(gpu_mod, r, c)
     if c["stats"]["n_itemsets"] < 300_000:
         assert _trie_dict(r) == _trie_dict(c)
-    else:  # order-independent multiset check on big outputs
-        assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
-        assert np.array_equal(np.bincount(r["depth"]), np.bincount(c["depth"]))
 
 
 def test_compact_download_widths(gpu_mod):
@@ -542,3 +552,61 @@ def test_encode_long_shard_matches_onehot(gpu_mod, tiled, monkeypatch):
     for t in range(tx.n_tx):
         X[t, tx.items[tx.tx_ptr[t]:tx.tx_ptr[t + 1]]] = 1
     np.testing.assert_array_equal(bits, X[:, ids].T)
+
+
+def _cpu_index(gpu_mod, tx, ms, names):
+    from kubernetes_machine_learning_server_amd.serve.index import build_index_from_trie
+    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, 2)
+    return build_index_from_trie(c["parent"], c["item"], c["count"], c["depth"], tx.n_tx,
+                                 tx.n_items, names)
+
+
+def _assert_index_equal(ix, ref, n_tx):
+    np.testing.assert_array_equal(np.asarray(ix["row_ptr"]), ref.row_ptr)
+    np.testing.assert_array_equal(np.asarray(ix["cons"]), ref.cons)
+    np.testing.assert_array_equal(np.asarray(ix["count"], np.int64),
+                                  np.rint(ref.score * n_tx).astype(np.int64))
+
+
+@pytest.mark.parametrize("tie", ["names", "ids"])
+@pytest.mark.parametrize("shape,ms,max_len", [("tiny", 0.05, 0), ("ds1", 0.05, 0),
+                                              ("ds1", 0.01, 2), ("ds2_weak", 0.03, 0),
+                                              ("ds_dense", 0.05, 0)])
+def test_rule_index_on_device(gpu_mod, shape, ms, max_len, tie):
+    """O10 pairs_to_csr: the rule map built from the resident gram == the CPU-built index
+    (rows by item id, sorted by count desc then the tie key asc), and the mined trie is
+    unaffected by building it."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.serve.index import name_tie_rank
+    tx = generate(shape, seed=2)
+    g = gpu_mod.GpuMiner(0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    names = tx.names if tie == "names" else None
+    if names:
+        g.set_tie_rank(name_tie_rank(names))
+    ref = _cpu_index(gpu_mod, tx, ms, names)
+    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, max_len)
+    # call 1 sizes the pinned host trie (full-width copy when it outgrows the first guess);
+    # call 2 streams at compact widths, with the last level copied by the final copy-out
+    for _ in range(2):
+        r = g.mine(ms, max_len, rule_index=True)
+        assert r["stats"]["levels_path"].startswith("fused"), r["stats"]
+        _assert_index_equal(r["index"], ref, tx.n_tx)
+        assert r["index"]["nnz"] == ref.nnz
+        assert_same_itemsets(gpu_mod, r, c)
+
+
+def test_rule_index_regrow_and_prefetch(gpu_mod, monkeypatch):
+    """A too-small entry capacity regrows and redoes the call; launch-ahead calls adopt their
+    own pinned CSR buffers (graph replay)."""
+    monkeypatch.setenv("KMLS_IDX_CAP", "64")
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.serve.index import name_tie_rank
+    tx = generate("ds1", seed=4)
+    g = gpu_mod.GpuMiner(0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    g.set_tie_rank(name_tie_rank(tx.names))
+    ref = _cpu_index(gpu_mod, tx, 0.05, tx.names)
+    outs = [g.mine(0.05, rule_index=True, prefetch=(i < 4)) for i in range(5)]
+    for r in outs:
+        _assert_index_equal(r["index"], ref, tx.n_tx)
