@@ -7,9 +7,15 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
+#include "kmls/comm_host.hpp"
 #include "kmls/gpu.hpp"
 #include "kmls/host.hpp"
 
@@ -37,7 +43,33 @@ using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
 using F64 = py::array_t<double, py::array::c_style | py::array::forcecast>;
 using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 
+// KMLS_SEGV_TRACE=1: a SIGSEGV/SIGBUS prints the faulting address and the native backtrace
+// (addresses resolve with addr2line against the .so) before the default action.
+static void segv_trace(int sig, siginfo_t* si, void*) {
+  char buf[96];
+  const int n = std::snprintf(buf, sizeof buf, "kmls: signal %d at address %p\n", sig, si->si_addr);
+  (void)!write(2, buf, (size_t)n);
+  void* frames[64];
+  const int k = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, k, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+static void install_segv_trace() {
+  const char* e = std::getenv("KMLS_SEGV_TRACE");
+  if (!e || e[0] != '1') return;
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof sa);
+  sa.sa_sigaction = segv_trace;
+  sa.sa_flags = SA_SIGINFO;
+  sigaction(SIGSEGV, &sa, nullptr);
+  sigaction(SIGBUS, &sa, nullptr);
+}
+
 PYBIND11_MODULE(_native, m) {
+  install_segv_trace();
+  m.def("install_segv_trace", &install_segv_trace);
   m.doc() = "kmls native runtime: CSV ingest, CPU/HIP FP-Growth miners, rule-index matchers";
 
   // ---------------- ingest ----------------
@@ -97,6 +129,26 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("tx_ptr"), py::arg("items"), py::arg("n_items"), py::arg("min_support"),
      py::arg("max_len") = 0, py::arg("threads") = 0, py::arg("pairs_only") = false);
 
+  m.def("mine_cpu_txdp", [](I64 tx_ptr, I32 items, int64_t n_items, int64_t n_tx_global,
+                            double min_support, int max_len, py::object comm) {
+    KMLS_CHECK(tx_ptr.size() >= 1, "tx_ptr must have T+1 entries");
+    ShmComm* c = comm.is_none() ? nullptr : comm.cast<ShmComm*>();
+    MineStats st;
+    ItemsetTrie t;
+    {
+      py::gil_scoped_release nogil;
+      t = mine_cpu_txdp(tx_ptr.data(), items.data(), tx_ptr.size() - 1, n_items, n_tx_global,
+                        min_support, max_len, c, &st);
+    }
+    py::dict d = trie_to_dict(std::move(t));
+    py::dict s;
+    s["n_frequent_items"] = st.n_frequent_items; s["n_itemsets"] = st.n_itemsets;
+    s["n_candidates"] = st.n_candidates; s["max_depth"] = st.max_depth;
+    d["stats"] = s;
+    return d;
+  }, py::arg("tx_ptr"), py::arg("items"), py::arg("n_items"), py::arg("n_tx_global"),
+     py::arg("min_support"), py::arg("max_len") = 0, py::arg("comm") = py::none());
+
   m.def("mine_cpu_count", [](I64 tx_ptr, I32 items, int64_t n_items, double min_support,
                              int max_len, int64_t cap, int threads) {
     KMLS_CHECK(tx_ptr.size() >= 1, "tx_ptr must have T+1 entries");
@@ -129,6 +181,7 @@ PYBIND11_MODULE(_native, m) {
       KMLS_CHECK((int64_t)d8.size() == n, "depth size differs");
       dp = d8.data();
     }
+    install_segv_trace();
     const void *pp = cont(parent), *ip = cont(item), *cp = cont(count);
     const int pw = (int)parent.itemsize(), iw = (int)item.itemsize(), cw = (int)count.itemsize();
     TrieDigest r;

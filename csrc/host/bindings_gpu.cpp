@@ -122,19 +122,52 @@ void register_gpu_bindings(py::module_& m) {
      py::arg("device") = 0);
 
   m.def("comm_unique_id", []() { return py::bytes(gpu::comm_unique_id()); });
+  m.def("host_comm_unique_id", []() { return py::bytes(host_comm_unique_id()); });
   py::class_<gpu::Comm>(m, "Comm")
-      .def(py::init([](int rank, int world, py::bytes uid, int device) {
+      .def(py::init([](int rank, int world, py::bytes uid, int device, const std::string& backend) {
              std::string u = uid;
              py::gil_scoped_release nogil;
-             return new gpu::Comm(rank, world, u, device);
-           }), py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"))
+             return new gpu::Comm(rank, world, u, device, backend);
+           }), py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"),
+           py::arg("backend") = "rccl")
       .def_property_readonly("rank", &gpu::Comm::rank)
       .def_property_readonly("world", &gpu::Comm::world)
+      .def_property_readonly("backend", &gpu::Comm::backend)
       .def("all_reduce_u32", [](gpu::Comm& c, uintptr_t buf, size_t n, uintptr_t stream) {
         py::gil_scoped_release nogil;
         c.all_reduce((void*)buf, (void*)buf, n, gpu::CommDtype::U32, false, (void*)stream);
       })
+      .def("wait_stream", [](gpu::Comm& c, uintptr_t stream) {
+        py::gil_scoped_release nogil;
+        c.wait_stream((void*)stream);
+      })
       .def("abort", &gpu::Comm::abort);
+
+  // host shared-memory communicator on its own (CPU multi-process tests of the backend)
+  py::class_<ShmComm>(m, "ShmComm")
+      .def(py::init([](int rank, int world, py::bytes uid) {
+             std::string u = uid;
+             py::gil_scoped_release nogil;
+             return new ShmComm(rank, world, u);
+           }), py::arg("rank"), py::arg("world"), py::arg("uid"))
+      .def("all_reduce", [](ShmComm& c, py::array buf, bool max_op) {
+        KMLS_CHECK(buf.flags() & py::array::c_style, "buffer must be C-contiguous");
+        KMLS_CHECK(buf.writeable(), "buffer must be writeable");
+        const auto k = buf.dtype().kind();
+        const size_t e = (size_t)buf.itemsize();
+        int kind = -1;
+        if (k == 'u' && e == 4) kind = 0;
+        else if (k == 'i' && e == 8) kind = 1;
+        else if (k == 'u' && e == 8) kind = 2;
+        else if (k == 'f' && e == 8) kind = 3;
+        KMLS_CHECK(kind >= 0, "dtype must be uint32, int64, uint64 or float64");
+        void* p = buf.mutable_data();
+        const size_t n = (size_t)buf.size();
+        py::gil_scoped_release nogil;
+        c.all_reduce(p, n, e, kind, max_op);
+      }, py::arg("buf"), py::arg("max_op") = false)
+      .def("barrier", &ShmComm::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &ShmComm::abort);
 
   py::class_<gpu::GpuMiner>(m, "GpuMiner")
       .def(py::init<int, size_t, uintptr_t>(), py::arg("device") = 0, py::arg("arena_bytes") = 0,

@@ -68,8 +68,7 @@ DeviceArena::~DeviceArena() {
 void* DeviceArena::push(size_t bytes) {
   size_t off = (top_ + 255) & ~(size_t)255;
   if (off + bytes > cap_)
-    throw std::runtime_error("kmls: device arena exhausted (" + std::to_string(off + bytes) +
-                             " > " + std::to_string(cap_) + " bytes); raise KMLS_ARENA_GB");
+    throw ArenaExhausted(off + bytes, cap_);
   top_ = off + bytes;
   hw_ = std::max(hw_, top_);
   return base_ + off;
@@ -303,7 +302,8 @@ struct MineRun {
 
   void read_pair(int64_t& S, int64_t& next_total) {
     KMLS_HIP(hipMemcpyAsync(h_scalar, d_pair, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    KMLS_HIP(hipStreamSynchronize(s));
+    if (comm) comm->wait_stream(s);  // bounded: a dead peer aborts instead of hanging
+    else KMLS_HIP(hipStreamSynchronize(s));
     S = h_scalar[0];
     next_total = h_scalar[1];
   }
@@ -688,8 +688,8 @@ struct MineRun {
       if (b_desc[L + 1].n_rows > 0) max_depth = std::max(max_depth, L + 1);
     n_candidates += (int64_t)b_ctl->candidates;
     out_size = new_size;
-    if (stream_dl) {
-      if (b_ctl->dl_overflow) stream_dl = false;  // final full copy
+    if (stream_dl) {  // final full copy when the pinned arrays were too small
+      if (b_ctl->dl_overflow || out_size > host_cap) stream_dl = false;
       else streamed = out_size;
     }
     ob->depth_hint = std::max(2, max_depth);
@@ -759,12 +759,14 @@ struct MineRun {
       ensure_out(out_size + S);
       Level C;
       C.n = S;
-      uint64_t* cbm = (uint64_t*)arena->push((size_t)S * Wp * sizeof(uint64_t));
-      int32_t* crank = (int32_t*)arena->push((size_t)S * sizeof(int32_t));
-      int64_t* cgid = (int64_t*)arena->push((size_t)S * sizeof(int64_t));
-      int32_t* cend = (int32_t*)arena->push((size_t)S * sizeof(int32_t));
-      int64_t* clen = (int64_t*)arena->push((size_t)(S + 1) * sizeof(int64_t));
-      KMLS_HIP(hipMemsetAsync(clen + S, 0, sizeof(int64_t), s));
+      // children at the max_len depth are leaves: trie nodes only (no bitmaps / class rows)
+      const bool leaf = max_len && depth + 1 >= max_len;
+      uint64_t* cbm = leaf ? nullptr : (uint64_t*)arena->push((size_t)S * Wp * sizeof(uint64_t));
+      int32_t* crank = leaf ? nullptr : (int32_t*)arena->push((size_t)S * sizeof(int32_t));
+      int64_t* cgid = leaf ? nullptr : (int64_t*)arena->push((size_t)S * sizeof(int64_t));
+      int32_t* cend = leaf ? nullptr : (int32_t*)arena->push((size_t)S * sizeof(int32_t));
+      int64_t* clen = leaf ? nullptr : (int64_t*)arena->push((size_t)(S + 1) * sizeof(int64_t));
+      if (clen) KMLS_HIP(hipMemsetAsync(clen + S, 0, sizeof(int64_t), s));
       kern::LevelOut o{cbm, crank, cgid, cend, clen, out_parent.p, out_item.p, out_count.p,
                        out_depth.p, out_size, (uint8_t)(depth + 1)};
       kern::extend_materialize(L.bm, Wp, cand_off, L.n, L.rank, L.gid, d_ids, c0, c1, cnt, minsup,
@@ -772,6 +774,10 @@ struct MineRun {
       out_size += S;
       stream_out();
       max_depth = std::max(max_depth, depth + 1);
+      if (leaf) {
+        arena->pop_to(mark);
+        continue;
+      }
       C.bm = cbm;
       C.rank = crank;
       C.gid = cgid;
@@ -907,6 +913,11 @@ GpuMiner::~GpuMiner() {
   if (d_pair_) (void)hipFree(d_pair_);
   if (d_tie_) (void)hipFree(d_tie_);
   if (d_inv_tie_) (void)hipFree(d_inv_tie_);
+  for (void* e : tile_ev_) (void)hipEventDestroy((hipEvent_t)e);
+  if (comm_s_) {
+    (void)hipStreamSynchronize((hipStream_t)comm_s_);
+    (void)hipStreamDestroy((hipStream_t)comm_s_);
+  }
   out_.reset();
   arena_.reset();
   if (own_stream_) (void)hipStreamDestroy((hipStream_t)stream_);
@@ -1758,7 +1769,19 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download, bool prefetch
   KMLS_HIP(hipMemsetAsync(d_own_bm_, 0, need, s));
   encode_bitmaps((uintptr_t)d_own_bm_, Wp, 0);
   KMLS_HIP(hipEventRecord(e2.e, s));
-  GpuMineResult r = mine_bitmaps((uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
+  GpuMineResult r;
+  for (int attempt = 0;; ++attempt) {
+    const size_t mark = arena_->mark();
+    try {
+      r = mine_bitmaps((uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
+      break;
+    } catch (const ArenaExhausted& ex) {
+      // a default-sized arena grows (up to its maximum) and the chunked search reruns
+      KMLS_HIP(hipStreamSynchronize(s));
+      arena_->pop_to(mark);
+      if (attempt >= 3 || mark != 0 || !grow_arena(ex.needed + (ex.needed >> 1))) throw;
+    }
+  }
   if (!fused_fallback_.empty() && r.levels_path.find("fallback") == std::string::npos)
     r.levels_path += " (resident fallback: " + fused_fallback_ + ")";
   std::vector<Phase> ph;
@@ -1780,35 +1803,38 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
   Event e0, e1, e2;
   KMLS_HIP(hipEventRecord(e0.e, s));
   const size_t mark = arena_->mark();
-  // 1. supports in K tiles; tile k's all-reduce (comm stream) overlaps tile k+1's histogram
+  // 1. supports in K tiles; tile k's all-reduce (comm stream) overlaps tile k+1's histogram.
+  //    The comm stream and the tile events live as long as the miner (no per-call creation).
   const int K = std::max(1, std::min(64, support_tiles));
   const size_t vec = (size_t)std::max<int64_t>(n_items_, 1) * sizeof(uint32_t);
   uint32_t* d_part = (uint32_t*)arena_->push(vec * K);
   KMLS_HIP(hipMemsetAsync(d_part, 0, vec * K, s));
-  hipStream_t cs = nullptr;
-  KMLS_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-  std::vector<hipEvent_t> evs((size_t)K);
-  for (auto& e : evs) KMLS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (!comm_s_) KMLS_HIP(hipStreamCreateWithFlags((hipStream_t*)&comm_s_, hipStreamNonBlocking));
+  hipStream_t cs = (hipStream_t)comm_s_;
+  while ((int)tile_ev_.size() < K + 1) {
+    hipEvent_t e;
+    KMLS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    tile_ev_.push_back((void*)e);
+  }
   for (int k = 0; k < K; ++k) {
     const int64_t a = tile_nnz_[(size_t)(64 * k / K)], b = tile_nnz_[(size_t)(64 * (k + 1) / K)];
     uint32_t* part = d_part + (size_t)k * (size_t)std::max<int64_t>(n_items_, 1);
     support_counts(d_items_ + a, b - a, part, s);
-    KMLS_HIP(hipEventRecord(evs[(size_t)k], s));
-    KMLS_HIP(hipStreamWaitEvent(cs, evs[(size_t)k], 0));
+    KMLS_HIP(hipEventRecord((hipEvent_t)tile_ev_[(size_t)k], s));
+    KMLS_HIP(hipStreamWaitEvent(cs, (hipEvent_t)tile_ev_[(size_t)k], 0));
     if (comm) comm->all_reduce(part, part, (size_t)n_items_, CommDtype::U32, false, cs);
   }
-  hipEvent_t done;
-  KMLS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+  hipEvent_t done = (hipEvent_t)tile_ev_[(size_t)K];
   KMLS_HIP(hipEventRecord(done, cs));
   KMLS_HIP(hipStreamWaitEvent(s, done, 0));
   for (int k = 1; k < K; ++k)
     kern::add_u32(d_part, d_part + (size_t)k * (size_t)std::max<int64_t>(n_items_, 1), n_items_, s);
+  // the selection (rank by support over up to millions of items) runs on the host: one 4 B/item
+  // readback per call, the same on every rank
   std::vector<uint32_t> cnt((size_t)n_items_);
   KMLS_HIP(hipMemcpyAsync(cnt.data(), d_part, cnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  KMLS_HIP(hipStreamSynchronize(s));
-  for (auto& e : evs) (void)hipEventDestroy(e);
-  (void)hipEventDestroy(done);
-  (void)hipStreamDestroy(cs);
+  if (comm) comm->wait_stream(s);
+  else KMLS_HIP(hipStreamSynchronize(s));
   arena_->pop_to(mark);
   // 2. selection from global supports (identical on every rank)
   const int64_t F = select(cnt.data(), global_n_tx, cfg.min_support);

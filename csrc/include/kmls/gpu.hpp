@@ -6,10 +6,12 @@
 #include <cstdint>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <string>
 #include <utility>
 #include <vector>
 
+#include "kmls/comm_host.hpp"
 #include "kmls/common.hpp"
 #include "kmls/host.hpp"
 
@@ -24,6 +26,15 @@ namespace gpu {
 bool available();
 int device_count();
 std::string device_name(int dev);
+
+// Thrown by DeviceArena::push when the arena is full (callers with a growable arena retry).
+struct ArenaExhausted : std::runtime_error {
+  size_t needed, cap;
+  ArenaExhausted(size_t n, size_t c)
+      : std::runtime_error("kmls: device arena exhausted (" + std::to_string(n) + " > " +
+                           std::to_string(c) + " bytes); raise KMLS_ARENA_GB"),
+        needed(n), cap(c) {}
+};
 
 // Bump/stack allocator over one big hipMalloc (DFS-of-batches needs strictly LIFO buffers).
 class DeviceArena {
@@ -82,20 +93,33 @@ size_t comm_dtype_bytes(CommDtype t);
 std::string comm_unique_id();  // 128 opaque bytes, broadcast by the caller (torch.distributed)
 class Comm {
  public:
-  Comm(int rank, int world, const std::string& uid, int device);
+  // backend "rccl" (uid from comm_unique_id) or "host" (uid from host_comm_unique_id)
+  Comm(int rank, int world, const std::string& uid, int device, const std::string& backend = "rccl");
   ~Comm();
   Comm(const Comm&) = delete;
   Comm& operator=(const Comm&) = delete;
   int rank() const { return rank_; }
   int world() const { return world_; }
+  const std::string& backend() const { return backend_; }
   // stream-ordered collectives on `stream` (a hipStream_t); in place when send == recv
   void all_reduce(const void* send, void* recv, size_t count, CommDtype t, bool max_op,
                   void* stream);
   void all_gather(const void* send, void* recv, size_t count, CommDtype t, void* stream);
+  // bounded host wait for `stream` (KMLS_COMM_TIMEOUT_S): aborts the communicator and throws
+  // when a collective never completes (a peer died)
+  void wait_stream(void* stream);
   void abort();
+
  private:
+  void progress(const char* what);
+  void* stage(size_t bytes);
   int rank_ = 0, world_ = 1;
+  double timeout_s_ = 300.0;
+  std::string backend_;
   void* comm_ = nullptr;
+  std::unique_ptr<ShmComm> host_;
+  void* staging_ = nullptr;  // pinned (host backend)
+  size_t staging_bytes_ = 0;
 };
 
 struct OutBufs;  // persistent device trie buffers + download stream (miner_gpu.hip)
@@ -216,6 +240,8 @@ class GpuMiner {
   int32_t* d_tie_ = nullptr;      // rule-map tie key (item id -> rank) and its inverse
   int32_t* d_inv_tie_ = nullptr;
   int64_t idx_cap_ = 1 << 20;     // rule-map entry capacity (grown after an overflow)
+  void* comm_s_ = nullptr;        // tx-DP: support-tile all-reduce stream (created once)
+  std::vector<void*> tile_ev_;    // tx-DP: support-tile events (created once)
   size_t idx_scan_bytes_ = 0;
   bool big_lds_ = false;
 };

@@ -48,6 +48,14 @@ ItemsetTrie mine_cpu_bitmaps(const uint64_t* bm, int64_t F, int64_t W, const Fre
 void encode_bitmaps_cpu(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                         const int32_t* rank_of, uint64_t* bm, int64_t W);
 
+class ShmComm;
+// Transaction-data-parallel CPU miner (miner_cpu_txdp.cpp): this rank holds a transaction shard;
+// supports and every level's candidate counts are all-reduced through `comm` (nullptr: world
+// size 1), so every rank returns the identical global trie (level order, parents first).
+ItemsetTrie mine_cpu_txdp(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx_local,
+                          int64_t n_items, int64_t n_tx_global, double min_support, int max_len,
+                          ShmComm* comm, MineStats* stats);
+
 // Count-only search: per-level itemset totals without a trie; stops once the running total
 // exceeds `cap` (capped = true, counts are then a lower bound).  For feasibility probes.
 struct CountResult {

@@ -826,6 +826,14 @@ __global__ __launch_bounds__(kBlock) void k_level_copyout(const FLevel* __restri
                                                           bool download, const uint4* __restrict__ rb_src,
                                                           int rb_words) {
   if (rb_words && blockIdx.x == gridDim.x - 1) {
+    // The copy blocks of this same launch flag a host-capacity overflow, possibly after this
+    // block has read the control block: decide it here too (it depends only on sizes), or the
+    // host would trust a truncated download.
+    if (threadIdx.x == 0 && download && !ctl->overflow &&
+        lv->child_base + nx->n_rows > ctl->h.cap)
+      ctl->dl_overflow = 1u;
+    __threadfence();
+    __syncthreads();
     uint4* __restrict__ rb_dst = (uint4*)ctl->rb_dst;
     for (int i = threadIdx.x; i < rb_words; i += blockDim.x) rb_dst[i] = rb_src[i];
     return;

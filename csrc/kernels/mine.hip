@@ -404,21 +404,25 @@ __global__ __launch_bounds__(kBlock) void k_extend_materialize(
     const int64_t a = find_row(cand_off, n_rows, c);
     const int64_t b = a + 1 + (c - cand_off[a]);
     const int64_t s = pos[c - c0];
-    const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
-    const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
-    ulonglong2* z = reinterpret_cast<ulonglong2*>(o.bm + s * Wp);
-    const int64_t lo = n2 * part / split, hi = n2 * (part + 1) / split;
-    for (int64_t w = lo + tl; w < hi; w += TS) {
-      const ulonglong2 u = x[w], v = y[w];
-      z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
+    if (o.bm) {  // leaf level (max_len reached): no child bitmaps, rows or classes
+      const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
+      const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
+      ulonglong2* z = reinterpret_cast<ulonglong2*>(o.bm + s * Wp);
+      const int64_t lo = n2 * part / split, hi = n2 * (part + 1) / split;
+      for (int64_t w = lo + tl; w < hi; w += TS) {
+        const ulonglong2 u = x[w], v = y[w];
+        z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
+      }
     }
     if (tl == 0 && part == 0) {
       const int32_t rb = rank[b];
-      o.rank[s] = rb;
-      o.gid[s] = o.out_base + s;
-      const int64_t re = pos[cand_off[a + 1] - c0];
-      o.row_end[s] = (int32_t)re;
-      o.len[s] = re - s - 1;
+      if (o.bm) {
+        o.rank[s] = rb;
+        o.gid[s] = o.out_base + s;
+        const int64_t re = pos[cand_off[a + 1] - c0];
+        o.row_end[s] = (int32_t)re;
+        o.len[s] = re - s - 1;
+      }
       o.out_parent[o.out_base + s] = gid[a];
       o.out_item[o.out_base + s] = ids[rb];
       o.out_count[o.out_base + s] = k;
@@ -767,7 +771,7 @@ void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off,
   if (c1 <= c0) return;
   const int ts = team_size(Wp);
   const int64_t teams_per_block = kBlock / ts;
-  const int64_t split = extend_split(Wp, c1 - c0, ts);
+  const int64_t split = o.bm ? extend_split(Wp, c1 - c0, ts) : 1;  // leaves copy no words
   const int g = grid_for((c1 - c0) * split, (int)teams_per_block, 256 * 32);
   KMLS_TEAM_DISPATCH(ts, k_extend_materialize, dim3(g), dim3(kBlock), 0, s,
                      (const unsigned long long*)bm, Wp, cand_off, n_rows, rank, gid, ids, c0, c1,

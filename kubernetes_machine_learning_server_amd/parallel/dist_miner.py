@@ -28,7 +28,9 @@ collective), then expands only the root classes that a device-side snake partiti
 estimated class costs assigns to it (``GpuMiner.mine_partition``).  One collective per step
 (the itemset-count all-reduce) instead of four plus host round trips.
 
-**Transaction-DP mode** (``mode="tx"``, the default for T >= 4M — BASELINE configs 3 and 5):
+**Transaction-DP mode** (``mode="tx"``, the default for T >= 4M — BASELINE configs 3 and 5;
+``backend="cpu"`` runs the same level loop natively on the host over the shared-memory
+communicator, the multi-process CPU test tier):
 replicating [F][T/64] bitmaps stops paying when T is large (100M transactions x 756 frequent
 items = 9.4 GB per GPU), so each rank keeps only its own shard's bitmap words and the C++
 level loop all-reduces every level's candidate counts through a native RCCL communicator
@@ -53,6 +55,18 @@ try:  # torch is only needed for the multi-GPU path
 except Exception:  # pragma: no cover
     torch = None
     dist = None
+
+
+def comm_backend() -> str:
+    """Native communicator of the tx-DP level loop: ``KMLS_COMM`` (``rccl`` | ``host``); default
+    RCCL when the process group runs on it, else the host shared-memory backend (gloo process
+    groups, several ranks sharing one GPU)."""
+    env = os.environ.get("KMLS_COMM", "").strip().lower()
+    if env in ("rccl", "host"):
+        return env
+    if dist is not None and dist.is_initialized() and dist.get_backend() == "nccl":
+        return "rccl"
+    return "host"
 
 
 def shard_bounds(n_tx: int, world: int, rank: int, align: int = 256) -> Tuple[int, int, int]:
@@ -109,10 +123,12 @@ class _GpuOps:
             self.g = N.GpuMiner(dm.device, arena_bytes, 0)
         elif dm.mode == "tx":
             torch.cuda.set_device(dm.device)
-            uid = [N.comm_unique_id() if dm.rank == 0 and dm.world > 1 else b"\0" * 128]
+            backend = comm_backend()
+            make_uid = N.host_comm_unique_id if backend == "host" else N.comm_unique_id
+            uid = [make_uid() if dm.rank == 0 and dm.world > 1 else b"\0" * 128]
             if dm.world > 1:
                 dist.broadcast_object_list(uid, src=0)
-            self.comm = N.Comm(dm.rank, dm.world, uid[0], dm.device)
+            self.comm = N.Comm(dm.rank, dm.world, uid[0], dm.device, backend)
             self.stream = None
             self.g = N.GpuMiner(dm.device, arena_bytes, 0)
         elif dm.world > 1 or dm.force_protocol or dm.mode == "item":
@@ -184,6 +200,15 @@ class _CpuOps:
         self.tx_ptr, self.items = tx_ptr, items
         self.n_items = dm.n_items
         self.rank_of = None
+        self.comm = None
+        if dm.mode == "tx" and dm.world > 1:  # native level loop over the shared-memory comm
+            uid = [self.N.host_comm_unique_id() if dm.rank == 0 else b"\0" * 128]
+            dist.broadcast_object_list(uid, src=0)
+            self.comm = self.N.ShmComm(dm.rank, dm.world, uid[0])
+
+    def mine_txdp(self, dm: "DistMiner", download: bool):
+        return self.N.mine_cpu_txdp(self.tx_ptr, self.items, self.n_items, dm.n_tx,
+                                    dm.min_support, dm.max_len, self.comm)
 
     def ctx(self):
         import contextlib
@@ -252,8 +277,6 @@ class DistMiner:
                 mode = "replicate"
             else:
                 mode = "item"
-        if mode == "tx" and backend != "gpu":
-            raise ValueError("mode='tx' needs the GPU backend (native RCCL communicator)")
         if global_n_tx is not None and mode not in ("tx", "item"):
             raise ValueError("pre-sharded input (global_n_tx) requires mode 'tx' or 'item'")
         self.mode = mode

@@ -130,3 +130,98 @@ def test_pair_strategies_equal_full_gram(world, mode):
         np.testing.assert_array_equal(rows.astype(np.int64), G[r0:r1])
         covered += r1 - r0
     assert covered == len(ids)
+
+
+# ---------------------------------------------------------------------------------------------
+# native shared-memory communicator (KMLS_COMM=host backend) and the tx-DP level loop
+def _shm_worker(rank, world, uid, die_rank, out_q):
+    os.environ["KMLS_COMM_TIMEOUT_S"] = "4"
+    from kubernetes_machine_learning_server_amd.ops import native
+    N = native.load()
+    c = N.ShmComm(rank, world, uid)
+    a = np.arange(10_000_000 // 7, dtype=np.uint32) + rank  # > one 8 MB slot: chunked
+    c.all_reduce(a, False)
+    b = np.full(5, float(rank), np.float64)
+    c.all_reduce(b, True)
+    res = {"rank": rank, "sum_ok": bool((a == np.arange(a.size, dtype=np.uint32) * world +
+                                          sum(range(world))).all()),
+           "max": b.tolist()}
+    if rank == die_rank:
+        out_q.put(res)
+        return  # leaves without entering the next collective
+    try:
+        c.barrier()
+        res["after"] = "ok"
+    except RuntimeError as e:
+        res["after"] = str(e)
+    out_q.put(res)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shm_comm_collectives_and_abort(world):
+    """Host communicator: chunked all-reduce (sum, max) over processes, then a rank that leaves
+    makes every other rank's next wait raise (bounded by KMLS_COMM_TIMEOUT_S), not hang."""
+    from kubernetes_machine_learning_server_amd.ops import native
+    uid = native.load().host_comm_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shm_worker, args=(r, world, uid, world - 1, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in res:
+        assert r["sum_ok"] and r["max"] == [float(world - 1)] * 5
+    for r in res[:-1]:
+        assert "timed out" in r["after"] or "aborted" in r["after"], r
+
+
+def _txdp_worker(rank, world, port, shape, ms, max_len, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), OMP_NUM_THREADS="1")
+    import torch.distributed as dist
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.ops import native
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tx = generate(shape, seed=5)
+        dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, ms, max_len=max_len, backend="cpu",
+                       mode="tx")
+        r = dm.step()["trie"]
+        d = native.load().trie_digest(r["parent"], r["item"], r["count"], r["depth"])
+        out_q.put((rank, d["digest"], d["n"], (dm.lo, dm.hi)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,shape,ms,max_len", [(2, "ds2_weak", 0.03, 0), (4, "tiny", 0.02, 0),
+                                                     (3, "ds1", 0.05, 4)])
+def test_txdp_level_loop_multi_process(world, shape, ms, max_len):
+    """Transaction-DP protocol with the native level loop (supports + every level's candidate
+    counts all-reduced through the host communicator): every rank builds the identical global
+    trie, whose (itemset, support) digest equals the single-process CPU miner's."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.ops import native
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_txdp_worker, args=(r, world, port, shape, ms, max_len, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    tx = generate(shape, seed=5)
+    N = native.load()
+    ref = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, max_len)
+    rd = N.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])
+    assert {r[1] for r in res} == {rd["digest"]}
+    assert all(r[2] == rd["n"] for r in res)
+    spans = sorted(r[3] for r in res)
+    assert spans[0][0] == 0 and spans[-1][1] == tx.n_tx  # the shards cover every transaction

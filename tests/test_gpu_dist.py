@@ -1,0 +1,82 @@
+"""Multi-process GPU tests of the transaction-DP protocol (run on a real MI355X via gpurun).
+
+The GPU boxes have ONE MI355X, so the ranks share it: every rank runs the native tx-DP level
+loop (GpuMiner.mine_txdp: tiled supports, shard-local bitmaps, each level's candidate counts
+all-reduced in C++) through the host-staged communicator (KMLS_COMM=host: D2H, shared-memory
+reduction, H2D).  RCCL itself needs one GPU per rank; its code path is the same Comm interface.
+The merged result is checked by content against the single-process CPU miner.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(shape):
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate, generate_large
+    if shape == "large":
+        return generate_large("10Mx1M", seed=7, n_tx=400_000, n_items=200_000), 0.002
+    return generate(shape, seed=5), 0.05
+
+
+def _worker(rank, world, port, shape, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), KMLS_COMM="host", KMLS_COMM_TIMEOUT_S="120")
+    import torch.distributed as dist
+    from kubernetes_machine_learning_server_amd.ops import native
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tx, ms = _data(shape)
+        dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, ms, device=0, mode="tx")
+        assert dm.ops.comm.backend == "host"
+        out = []
+        for _ in range(2):  # the second call reuses the comm stream/events and the arena
+            r = dm.step(download=True)
+            st = r["stats"]
+            d = None
+            if rank == 0:
+                t = r["trie"]
+                d = native.load().trie_digest(t["parent"], t["item"], t["count"], t["depth"])["digest"]
+            out.append((int(st["n_itemsets"]), d, st.get("levels_path")))
+        out_q.put((rank, out, (dm.lo, dm.hi)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,shape", [(2, "ds1"), (4, "ds1"), (2, "large"), (4, "large")])
+def test_txdp_multi_rank_on_one_gpu(world, shape):
+    from kubernetes_machine_learning_server_amd.ops import native
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shape, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    tx, ms = _data(shape)
+    N = native.load()
+    ref = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
+    rd = N.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])
+    for rank, out, _ in res:
+        for n, d, path in out:
+            assert n == rd["n"], (rank, n, rd["n"], path)
+            if rank == 0:
+                assert d == rd["digest"], path
+    spans = sorted(r[2] for r in res)
+    assert spans[0][0] == 0 and spans[-1][1] == tx.n_tx

@@ -144,7 +144,7 @@ def test_gpu_miner_chunked_levels(gpu_mod, monkeypatch):
     """Force many candidates per level (multi-chunk path) on a larger synthetic set."""
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     monkeypatch.setenv("KMLS_FUSED_LEVELS", "0")
-    tx = generate("ds2", seed=9)
+    tx = generate("ds_dense", seed=9)
     g = gpu_mod.GpuMiner(0, 8 << 30, 0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     r = g.mine(0.045)
@@ -157,7 +157,7 @@ def test_fused_levels_repeat_and_small_arena(gpu_mod, monkeypatch):
     """Repeated calls (epoch-tagged look-back state, persistent output buffers, streamed
     download sized from the previous call) and the fallback when the arena is too small."""
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    tx = generate("ds2", seed=3)
+    tx = generate("ds_dense", seed=3)
     c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.05)
     g = gpu_mod.GpuMiner(0, 4 << 30, 0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
@@ -284,7 +284,7 @@ def test_gpu_rules_equal_cpu(gpu_mod, metric, thr, strict, max_ante):
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     from kubernetes_machine_learning_server_amd.models.fpgrowth import mine_csr
     from kubernetes_machine_learning_server_amd.models.rules import rules_from_trie
-    tx = generate("ds2", seed=1)
+    tx = generate("ds_dense", seed=1)
     trie = mine_csr(tx.tx_ptr, tx.items, tx.n_items, 0.06, backend="cpu")
     assert int(trie.depth.max()) >= 10
     g = rules_from_trie(trie, metric, thr, max_antecedent=max_ante, strict=strict, backend="gpu")
@@ -429,7 +429,7 @@ def test_default_arena_grows_on_demand(gpu_mod, monkeypatch):
     when the device-resident path runs out of room, instead of falling back or failing."""
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     monkeypatch.setenv("KMLS_ARENA_INIT_MB", "520")
-    tx = generate("ds2", seed=3)
+    tx = generate("ds_dense", seed=3)
     g = gpu_mod.GpuMiner(0)
     assert g.arena_capacity < (600 << 20)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
@@ -610,3 +610,20 @@ def test_rule_index_regrow_and_prefetch(gpu_mod, monkeypatch):
     outs = [g.mine(0.05, rule_index=True, prefetch=(i < 4)) for i in range(5)]
     for r in outs:
         _assert_index_equal(r["index"], ref, tx.n_tx)
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_max_len_leaf_levels(gpu_mod, fused, monkeypatch):
+    """Truncated mining (mlxtend max_len): the last allowed level is written as trie leaves
+    without child bitmaps (chunked path) and must equal the CPU miner's truncated result."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    monkeypatch.setenv("KMLS_FUSED_LEVELS", fused)
+    tx = generate("ds1", seed=6)
+    g = gpu_mod.GpuMiner(0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    for ml in (3, 4):
+        c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.02, ml)
+        for _ in range(2):
+            r = g.mine(0.02, ml)
+            assert int(r["stats"]["max_depth"]) == ml
+            assert_same_itemsets(gpu_mod, r, c)
