@@ -168,8 +168,6 @@ def main() -> int:
     ap.add_argument("--no-rule-map", action="store_true",
                     help="leave the rule-map build out of the step (A/B only)")
     ap.add_argument("--cpu", action="store_true", help="native CPU miner (no GPU)")
-    ap.add_argument("--persistent", action="store_true",
-                    help="levels >= 3 in the persistent work-queue DFS kernel (A/B option)")
     ap.add_argument("--no-config2", action="store_true", help="skip BASELINE config 2 (0.01)")
     ap.add_argument("--serve-qps", default="2000,10000",
                     help="offered QPS points for the serving half ('' = skip)")
@@ -218,7 +216,7 @@ def main() -> int:
     else:
         from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
         dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, args.min_support, device=local_rank,
-                       max_len=args.max_len, mfma=args.mfma, persistent=args.persistent)
+                       max_len=args.max_len, mfma=args.mfma)
         dm.set_tie_rank(tie)
 
         def step(prefetch=False):  # the itemset count is reduced over ranks once, after timing
@@ -310,7 +308,7 @@ def main() -> int:
             "rule_map_in_step": rule_map,
             "n_rules": int(r["index"]["nnz"]) if rule_map and "index" in r else None,
             "level2": "mfma-i8" if args.mfma else "popcount-bitgemm",
-            "levels3plus": "persistent-dfs" if args.persistent else "level-wise",
+            "levels3plus": "level-wise",
             "levels_path": st.get("levels_path"),
             "step_overlap": ("none" if args.cpu or args.no_prefetch else
                              "launch-ahead: step k+1's call is launched before step k's is waited for"),

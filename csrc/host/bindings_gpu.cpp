@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "../kernels/kernels.hpp"
 #include "kmls/gpu.hpp"
 #include "kmls/trace.hpp"
 
@@ -60,10 +61,9 @@ py::dict result_to_dict(gpu::GpuMineResult&& r) {
 }
 
 MineConfig make_cfg(double ms, int max_len, bool pairs_only, bool gram, bool mfma,
-                    bool persistent = false, bool rule_index = false) {
+                    bool rule_index = false) {
   MineConfig c;
   c.rule_index = rule_index;
-  c.persistent = persistent;
   c.min_support = ms;
   c.max_len = max_len;
   c.pairs_only = pairs_only;
@@ -84,6 +84,7 @@ void register_gpu_bindings(py::module_& m) {
   m.def("roctx_push", [](const std::string& n) { trace::push(n.c_str()); });
   m.def("roctx_pop", &trace::pop);
   m.def("gpu_device_count", &gpu::device_count);
+  m.def("extend_split_launches", &kern::extend_split_launches);
   m.def("gpu_device_name", &gpu::device_name);
 
   m.def("association_rules_gpu", [](I64 parent, I32 item, U32 count, U8 depth, int64_t n_tx,
@@ -198,8 +199,8 @@ void register_gpu_bindings(py::module_& m) {
       .def("bitgemm_rect", &gpu::GpuMiner::bitgemm_rect, py::call_guard<py::gil_scoped_release>())
       .def("mine_bitmaps", [](gpu::GpuMiner& g, uintptr_t bm, int64_t Wp, double ms, int max_len,
                               bool pairs_only, py::object owned, bool emit_level1, bool download,
-                              bool gram, bool mfma, bool persistent) {
-        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma, persistent);
+                              bool gram, bool mfma) {
+        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma);
         std::vector<uint8_t> own;
         const uint8_t* po = nullptr;
         if (!owned.is_none()) {
@@ -216,15 +217,14 @@ void register_gpu_bindings(py::module_& m) {
         return result_to_dict(std::move(r));
       }, py::arg("bm"), py::arg("Wp"), py::arg("min_support"), py::arg("max_len") = 0,
          py::arg("pairs_only") = false, py::arg("owned") = py::none(), py::arg("emit_level1") = true,
-         py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
-         py::arg("persistent") = false)
+         py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false)
       .def("set_tie_rank", [](gpu::GpuMiner& g, I32 tie) {
         py::gil_scoped_release nogil;
         g.set_tie_rank(tie.data(), tie.size());
       }, py::arg("tie"))
       .def("mine", [](gpu::GpuMiner& g, double ms, int max_len, bool pairs_only, bool download,
-                      bool gram, bool mfma, bool persistent, bool prefetch, bool rule_index) {
-        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma, persistent, rule_index);
+                      bool gram, bool mfma, bool prefetch, bool rule_index) {
+        MineConfig c = make_cfg(ms, max_len, pairs_only, gram, mfma, rule_index);
         gpu::GpuMineResult r;
         {
           py::gil_scoped_release nogil;
@@ -233,14 +233,13 @@ void register_gpu_bindings(py::module_& m) {
         return result_to_dict(std::move(r));
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("pairs_only") = false,
          py::arg("download") = true, py::arg("gram") = true, py::arg("mfma") = false,
-         py::arg("persistent") = false, py::arg("prefetch") = false,
-         py::arg("rule_index") = false)
+         py::arg("prefetch") = false, py::arg("rule_index") = false)
       .def("mine_partition", [](gpu::GpuMiner& g, double ms, int max_len, bool download, int rank,
                                 int world, bool prefetch, bool rule_index) {
         gpu::GpuMineResult r;
         {
           py::gil_scoped_release nogil;
-          r = g.mine_partition(make_cfg(ms, max_len, false, true, false, false, rule_index),
+          r = g.mine_partition(make_cfg(ms, max_len, false, true, false, rule_index),
                                download, rank, world, prefetch);
         }
         return result_to_dict(std::move(r));

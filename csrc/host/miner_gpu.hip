@@ -290,12 +290,7 @@ struct MineRun {
   int64_t n_candidates = 0;
   int max_depth = 1;
   int64_t* h_scalar = nullptr;  // pinned [2]
-  bool persistent = true;       // levels >= 3 through the persistent DFS kernel
-  int64_t rows_hint = 0;        // persistent pool capacity (rows = trie nodes)
   int n_cus = 256;
-  bool overflowed = false;
-  unsigned int* abort_host = nullptr;  // mapped pinned watchdog flag
-  const unsigned int* abort_dev = nullptr;
 
   uint64_t* d_pair = nullptr;   // device [survivors, next-level candidates]
   Comm* comm = nullptr;         // tx-DP: candidate counts are shard-partial → all-reduce
@@ -335,143 +330,6 @@ struct MineRun {
     out_count.reserve(n, s);
     out_depth.reserve(n, s);
   }
-
-  // Expand every row of level L (itemsets of size `depth`).  `len` (device, L.n+1 entries,
-  // len[L.n] == 0) holds each row's candidate count and `total` their sum — both produced by
-  // the parent chunk (or the host at the root), so a chunk costs ONE host readback: the
-  // survivor count and the child level's candidate total, read together.
-  // Levels >= 3 in one persistent launch (dfs_persistent.hip): seed = every class of L.
-  // Returns false (nothing emitted) when the pool/queue capacity was exceeded: the caller then
-  // runs the exact level-wise path for L, and the next call starts with a larger pool.
-  bool run_persistent(const Level& L, int depth) {
-    const size_t mark = arena->mark();
-    const int64_t task_cap_min = L.n + 4096;
-    // bytes per pool row: bitmap + rank + gid + compaction (pos + 4 staged outputs)
-    const int64_t per_row = Wp * 8 + 4 + 8 + 17 + 25 + 16;  // pool + staged outputs + sort
-    const int64_t avail = (int64_t)(arena->capacity() - arena->used()) - (64ll << 20) -
-                          task_cap_min * (int64_t)(sizeof(kern::DfsTask) + 4);
-    int64_t row_cap = std::max<int64_t>(rows_hint, 1 << 20);
-    if (avail <= 0) return false;
-    row_cap = std::min<int64_t>(row_cap, avail / (per_row + (int64_t)(sizeof(kern::DfsTask) + 4) / 2));
-    if (row_cap < 4096) return false;
-    const int64_t task_cap = row_cap / 2 + task_cap_min;
-    ensure_out(out_size + row_cap);
-    kern::DfsArgs a{};
-    a.seed_bm = L.bm;
-    a.seed_rank = L.rank;
-    a.seed_gid = L.gid;
-    a.seed_row_end = L.row_end;
-    a.seed_rows = L.n;
-    a.seed_depth = depth;
-    a.seed_items = (int32_t*)arena->push((size_t)std::max<int64_t>(L.n, 1) * sizeof(int32_t));
-    a.tasks = (kern::DfsTask*)arena->push((size_t)task_cap * sizeof(kern::DfsTask));
-    a.ready = (unsigned int*)arena->push((size_t)task_cap * sizeof(unsigned int));
-    a.task_cap = task_cap;
-    a.ctl = (kern::DfsCtl*)arena->push(sizeof(kern::DfsCtl));
-    a.pool_bm = (uint64_t*)arena->push((size_t)row_cap * Wp * sizeof(uint64_t));
-    a.pool_rank = (int32_t*)arena->push((size_t)row_cap * sizeof(int32_t));
-    a.pool_gid = (int64_t*)arena->push((size_t)row_cap * sizeof(int64_t));
-    a.row_cap = row_cap;
-    a.out_parent = out_parent.p;
-    a.out_item = out_item.p;
-    a.out_count = out_count.p;
-    a.out_depth = out_depth.p;
-    a.out_base = out_size;
-    a.ids = d_ids;
-    a.Wp = Wp;
-    a.minsup = minsup;
-    a.max_len = max_len;
-    a.n_cus = n_cus;
-    {
-      const char* e = std::getenv("KMLS_DFS_TIMEOUT_MS");
-      const double ms = e ? std::atof(e) : 20000.0;
-      a.timeout_ticks = (unsigned long long)(ms * 1e5);  // 100 MHz
-    }
-    const bool debug = std::getenv("KMLS_DFS_DEBUG") != nullptr;
-    const int n_waves = n_cus * 2 * 4;
-    unsigned int* crumbs = (unsigned int*)arena->push((size_t)n_waves * 4 * sizeof(unsigned int));
-    a.wave_state = debug ? crumbs : nullptr;
-    a.abort_flag = abort_dev;
-    *abort_host = 0u;
-    KMLS_HIP(hipMemsetAsync(a.ready, 0, (size_t)task_cap * sizeof(unsigned int), s));
-    KMLS_HIP(hipMemsetAsync(a.ctl, 0, sizeof(kern::DfsCtl), s));
-    KMLS_HIP(hipMemsetAsync(out_depth.p + out_size, 0, (size_t)row_cap, s));  // holes = depth 0
-    if (debug) KMLS_HIP(hipMemsetAsync(crumbs, 0, (size_t)n_waves * 4 * sizeof(unsigned int), s));
-    const auto t_launch = std::chrono::steady_clock::now();
-    kern::dfs_persistent(a, s);
-    // host watchdog: poll completion; past the deadline raise the mapped abort flag so every
-    // wave leaves its loops, then report
-    {
-      const double limit_ms = (double)a.timeout_ticks / 1e5 + 2000.0;
-      bool aborted = false;
-      while (true) {
-        hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) KMLS_HIP(q);
-        const double el = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_launch).count();
-        if (!aborted && el > limit_ms) {
-          __atomic_store_n(abort_host, 1u, __ATOMIC_SEQ_CST);
-          aborted = true;
-          fprintf(stderr, "[dfs] watchdog: kernel exceeded %.0f ms, abort raised\n", limit_ms);
-        }
-        if (aborted && el > limit_ms + 10000.0)
-          throw std::runtime_error("kmls: persistent DFS kernel hung (abort not honoured)");
-        if (el > 2.0) std::this_thread::sleep_for(std::chrono::microseconds(aborted ? 1000 : 10));
-      }
-    }
-    kern::DfsCtl h;
-    KMLS_HIP(hipMemcpyAsync(&h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
-    KMLS_HIP(hipStreamSynchronize(s));
-    if (debug || h.timeout || h.aborted || h.bad_task) {
-      fprintf(stderr,
-              "[dfs] seed_rows=%lld depth=%d row_cap=%lld task_cap=%lld | q_head=%llu q_tail=%llu "
-              "pending=%llu row_top=%llu cands=%llu overflow=%u timeout=%u aborted=%u bad=%u "
-              "exited=%u max_depth=%u\n",
-              (long long)L.n, depth, (long long)row_cap, (long long)task_cap, h.q_head, h.q_tail,
-              h.pending, h.row_top, h.candidates, h.overflow, h.timeout, h.aborted, h.bad_task,
-              h.exited, h.max_depth);
-      if (debug) {
-        std::vector<unsigned int> ws((size_t)n_waves * 4);
-        KMLS_HIP(hipMemcpy(ws.data(), crumbs, ws.size() * sizeof(unsigned int), hipMemcpyDeviceToHost));
-        int hist[10] = {0};
-        for (int w = 0; w < n_waves; ++w) hist[std::min(9u, ws[4 * w])]++;
-        fprintf(stderr, "[dfs] waves: polling=%d expanding=%d retiring=%d exited=%d\n", hist[1],
-                hist[2], hist[3], hist[9]);
-      }
-    }
-    if (h.timeout || h.aborted) throw std::runtime_error("kmls: persistent DFS kernel timed out");
-    if (h.bad_task) throw std::runtime_error("kmls: persistent DFS kernel read a corrupt task");
-    if (h.overflow) {
-      rows_hint = std::max<int64_t>(row_cap * 4, (int64_t)h.row_top * 2);
-      arena->pop_to(mark);
-      return false;
-    }
-    // compact the holes left by per-wave row chunks
-    const int64_t rows = (int64_t)h.row_top;
-    if (rows > 0) {
-      const size_t tb = kern::dfs_compact_temp_bytes(rows);
-      void* tmp = arena->push(tb);
-      int64_t* par2 = (int64_t*)arena->push((size_t)rows * sizeof(int64_t));
-      int32_t* item2 = (int32_t*)arena->push((size_t)rows * sizeof(int32_t));
-      uint32_t* cnt2 = (uint32_t*)arena->push((size_t)rows * sizeof(uint32_t));
-      uint8_t* dep2 = (uint8_t*)arena->push((size_t)rows);
-      const int64_t V = kern::dfs_compact(rows, out_size, out_parent.p, out_item.p, out_count.p,
-                                          out_depth.p, tmp, tb, par2, item2, cnt2, dep2,
-                                          (unsigned long long*)h_scalar, s);
-      KMLS_HIP(hipMemcpyAsync(out_parent.p + out_size, par2, V * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-      KMLS_HIP(hipMemcpyAsync(out_item.p + out_size, item2, V * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-      KMLS_HIP(hipMemcpyAsync(out_count.p + out_size, cnt2, V * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-      KMLS_HIP(hipMemcpyAsync(out_depth.p + out_size, dep2, V * sizeof(uint8_t), hipMemcpyDeviceToDevice, s));
-      out_size += V;
-      stream_out();
-    }
-    n_candidates += (int64_t)h.candidates;
-    max_depth = std::max<int>(max_depth, (int)h.max_depth);
-    rows_hint = std::max<int64_t>(rows_hint, rows + (rows >> 2));
-    arena->pop_to(mark);
-    return true;
-  }
-
 
   // ---- fused, host-sync-free level expansion (levels.hip) -----------------------------------
   // All levels are enqueued back to back (2 kernels per level, sizes stay on the device); the
@@ -707,9 +565,12 @@ struct MineRun {
     return h_scalar[0];
   }
 
+  // Expand every row of level L (itemsets of size `depth`).  `len` (device, L.n+1 entries,
+  // len[L.n] == 0) holds each row's candidate count and `total` their sum — both produced by
+  // the parent chunk (or the host at the root), so a chunk costs ONE host readback: the
+  // survivor count and the child level's candidate total, read together.
   void process(const Level& L, int depth, const int64_t* len, int64_t total) {
     if (L.n < 2 || total == 0 || (max_len && depth >= max_len)) return;
-    if (persistent && depth >= 2 && run_persistent(L, depth)) return;
     const size_t mark0 = arena->mark();
     int64_t* cand_off = (int64_t*)arena->push((size_t)(L.n + 1) * sizeof(int64_t));
     const size_t tb = kern::scan_temp_bytes(L.n);
@@ -880,9 +741,6 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
   if (arena_auto_) arena_max_ = max_arena_bytes();
   arena_ = std::make_unique<DeviceArena>(arena_bytes ? arena_bytes : default_arena_bytes());
   pinned_ = make_pinned_pool();
-  KMLS_HIP(hipHostMalloc((void**)&abort_host_, 64, hipHostMallocMapped));
-  *abort_host_ = 0u;
-  KMLS_HIP(hipHostGetDevicePointer((void**)&abort_dev_, abort_host_, 0));
   KMLS_HIP(hipHostMalloc((void**)&h_scalar_, 64));
   KMLS_HIP(hipHostMalloc((void**)&call_params_, 2 * sizeof(kern::FCtl)));
   std::memset(call_params_, 0, 2 * sizeof(kern::FCtl));
@@ -905,7 +763,6 @@ GpuMiner::~GpuMiner() {
   if (d_rank_of_) (void)hipFree(d_rank_of_);
   if (d_ids_) (void)hipFree(d_ids_);
   if (d_own_bm_) (void)hipFree(d_own_bm_);
-  if (abort_host_) (void)hipHostFree(abort_host_);
   if (h_scalar_) (void)hipHostFree(h_scalar_);
   if (call_params_) (void)hipHostFree(call_params_);
   if (d_call_seq_) (void)hipFree(d_call_seq_);
@@ -914,6 +771,12 @@ GpuMiner::~GpuMiner() {
   if (d_tie_) (void)hipFree(d_tie_);
   if (d_inv_tie_) (void)hipFree(d_inv_tie_);
   for (void* e : tile_ev_) (void)hipEventDestroy((hipEvent_t)e);
+  for (void* e : idx_ev_)
+    if (e) (void)hipEventDestroy((hipEvent_t)e);
+  if (idx_s_) {
+    (void)hipStreamSynchronize((hipStream_t)idx_s_);
+    (void)hipStreamDestroy((hipStream_t)idx_s_);
+  }
   if (comm_s_) {
     (void)hipStreamSynchronize((hipStream_t)comm_s_);
     (void)hipStreamDestroy((hipStream_t)comm_s_);
@@ -1114,12 +977,8 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   if (!out_) out_ = std::make_unique<OutBufs>();
   runp = std::make_unique<MineRun>(out_.get());
   MineRun& run = *runp;
-  run.persistent = cfg.persistent && comm_ == nullptr;
   run.comm = comm_;
-  run.rows_hint = rows_hint_;
   run.n_cus = n_cus_;
-  run.abort_host = abort_host_;
-  run.abort_dev = abort_dev_;
   run.s = s;
   run.arena = arena_.get();
   run.Wp = Wp;
@@ -1194,7 +1053,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     root.gid = d_gid;
     root.row_end = d_end;
     bool done = false;
-    if (!run.persistent && comm_ == nullptr && fused_levels_enabled()) {
+    if (comm_ == nullptr && fused_levels_enabled()) {
       std::vector<int64_t> off((size_t)F + 1, 0);
       for (int64_t a = 0; a < F; ++a) off[a + 1] = off[a] + root_len[a];
       run.pinned = pinned_;
@@ -1202,23 +1061,13 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       done = run.run_fast(root, off, root_total);
     }
     if (!done) run.process(root, 1, d_len, root_total);
-    res.levels_path = done ? "fused" : (run.persistent ? "persistent" : (comm_ ? "chunked-txdp" : "chunked"));
+    res.levels_path = done ? "fused" : (comm_ ? "chunked-txdp" : "chunked");
     if (!done && !run.fallback_reason.empty()) res.levels_path += " (fused fallback: " + run.fallback_reason + ")";
     KMLS_HIP(hipStreamSynchronize(s));  // host staging vectors die at scope end
   } else {
     KMLS_HIP(hipEventRecord(e1.e, s));
   }
-  rows_hint_ = run.rows_hint;
-  if (!run.overflowed || attempt >= 6) {
-    if (run.overflowed) throw std::runtime_error("kmls: persistent DFS capacity overflow");
-    break;
-  }
-  arena_->pop_to(mark);
-  KMLS_HIP(hipStreamSynchronize(out_->copy_s));
-  res.h_parent.reset();
-  res.h_item.reset();
-  res.h_count.reset();
-  res.h_depth.reset();
+  break;  // one pass (the loop scopes the run's state)
   }
   MineRun& run = *runp;
   KMLS_HIP(hipEventRecord(e2.e, s));
@@ -1299,7 +1148,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
       kern::pairs_enable_big_lds();
       big_lds_ = true;
     }
-    if (!idx_scan_bytes_) idx_scan_bytes_ = kern::pairs_scan_temp_bytes(I);
+    if (!idx_scan_bytes_) idx_scan_bytes_ = kern::pairs_scratch_bytes(I, I);
     pa.gram = d_gram;
     pa.ld = I;
     pa.dF = &d_desc[1].n_rows;
@@ -1310,12 +1159,8 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     pa.n_items = I;
     pa.tie = d_tie_;
     pa.inv_tie = d_inv_tie_;
-    pa.len_r = (uint32_t*)arena_->push((size_t)I * 4);
-    pa.cursor = (uint32_t*)arena_->push((size_t)I * 4);
-    pa.len_id = (int64_t*)arena_->push((size_t)(I + 1) * 8);
-    pa.scan_temp = arena_->push(idx_scan_bytes_);
-    pa.scan_temp_bytes = idx_scan_bytes_;
-    pa.status = (unsigned int*)arena_->push(256);
+    pa.scratch = arena_->push(idx_scan_bytes_);
+    pa.scratch_bytes = idx_scan_bytes_;
     pa.row_ptr = (int64_t*)arena_->push((size_t)(I + 1) * 8);
     pa.ent = (unsigned long long*)arena_->push((size_t)icap * 8);
     pa.ent_cap = icap;
@@ -1341,7 +1186,6 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   run.gram = d_gram;
   run.pinned = pinned_;
   run.n_cus = n_cus_;
-  run.persistent = false;
   run.h_scalar = h_scalar_;
   const int64_t cap_nodes = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 16ll << 20);
   run.ensure_out(cap_nodes);
@@ -1470,11 +1314,17 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     if (cfg.rule_index) {
       key.push_back((uint64_t)icap);
       key.push_back(u(pa.ent));
-      key.push_back(u(pa.len_r));
+      key.push_back(u(pa.scratch));
       key.push_back(u(d_tie_));
     }
   }
   const bool replay = use_graph && graph_ && graph_->exec && graph_->key == key;
+  // the rule map forks off the captured prologue (joined before the capture ends)
+  const bool fork_idx = cfg.rule_index && use_graph && !replay;
+  if (fork_idx && !idx_s_) {
+    KMLS_HIP(hipStreamCreateWithFlags((hipStream_t*)&idx_s_, hipStreamNonBlocking));
+    for (auto& e : idx_ev_) KMLS_HIP(hipEventCreateWithFlags((hipEvent_t*)&e, hipEventDisableTiming));
+  }
   auto enqueue_prologue = [&]() {
     kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl,
                               call_params_, d_call_seq_, s);
@@ -1487,20 +1337,26 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of, d_own_bm_, Wp, 0, s);
     if (kern::pair_gram_dev_needs_zero(Wp, I)) KMLS_HIP(hipMemsetAsync(d_gram, 0, (size_t)I * I * 4, s));
     kern::pair_gram_popcount_dev(d_own_bm_, Wp, &d_desc[1].n_rows, I, d_gram, s);
-    if (cfg.rule_index) kern::pairs_to_csr(pa, s);
+    if (cfg.rule_index) {
+      if (fork_idx) {  // captured: the rule map runs on a side branch of the graph, beside the levels
+        KMLS_HIP(hipEventRecord((hipEvent_t)idx_ev_[0], s));
+        KMLS_HIP(hipStreamWaitEvent((hipStream_t)idx_s_, (hipEvent_t)idx_ev_[0], 0));
+        kern::pairs_to_csr(pa, (hipStream_t)idx_s_);
+        KMLS_HIP(hipEventRecord((hipEvent_t)idx_ev_[1], (hipStream_t)idx_s_));
+      } else {
+        kern::pairs_to_csr(pa, s);
+      }
+    }
     int32_t* d_prank = nullptr;
-    const int64_t* part_cost = nullptr;
     if (part_world > 1) {  // replicated-data partition of the root classes, computed on device
       int64_t* d_cost = (int64_t*)arena_->push((size_t)I * 8);
       d_prank = (int32_t*)arena_->push((size_t)I * 4);
       kern::level_partition(d_gram, I, d_desc, run.minsup, I, d_cost, d_prank, s);
-      part_cost = d_cost;
     }
     kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
                            run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
                            d_prank, part_world, part_rank,
-                           run.stream_dl && !deferred_dl(), fused_select,
-                           d_prank ? nullptr : part_cost};
+                           run.stream_dl && !deferred_dl(), fused_select};
     kern::level_root_setup(d_desc, d_ctl, ra, s);
     if (!fused_select)  // staged to pinned memory while the levels run
       KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));
@@ -1542,6 +1398,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     }
     run.graph_capture = true;
     run.end_capture = [&](int last) {
+      if (fork_idx) KMLS_HIP(hipStreamWaitEvent(s, (hipEvent_t)idx_ev_[1], 0));  // join
       hipGraph_t g = nullptr;
       KMLS_HIP(hipStreamEndCapture(s, &g));
       hipGraphExec_t ex = nullptr;
@@ -1713,7 +1570,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
 }
 
 bool GpuMiner::resident_ok(const MineConfig& cfg) const {
-  return fused_levels_enabled() && !cfg.persistent && cfg.level2_gram && !cfg.level2_mfma &&
+  return fused_levels_enabled() && cfg.level2_gram && !cfg.level2_mfma &&
          !cfg.pairs_only && cfg.max_len != 1 && n_items_ >= 2 &&
          n_items_ <= kern::kSelectMaxItems && (size_t)n_items_ * words_local() * 8 <= (1ull << 30) &&
          n_tx_ > 0;

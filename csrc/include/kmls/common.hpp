@@ -40,8 +40,6 @@ struct MineConfig {
   bool pairs_only = false;  // stop after 2-itemsets (rule-map fast path)
   bool level2_gram = true;  // GPU: level 2 through the tiled bit-GEMM
   bool level2_mfma = false; // GPU: ... on the i8 matrix cores instead of VALU popcount
-  bool persistent = false;  // GPU: levels >= 3 in one persistent work-queue launch (A/B option;
-                            // level-wise wins on many-tiny-class trees, profiles/r1_dfs_ab.md)
   bool rule_index = false;  // GPU resident path: also build the rule map (pair-support CSR,
                             // machine-learning/main.py:282-304) on the device and download it
 };

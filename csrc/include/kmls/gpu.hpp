@@ -209,9 +209,6 @@ class GpuMiner {
   uint64_t* d_own_bm_ = nullptr;  // single-GPU bitmap buffer
   size_t own_bm_bytes_ = 0;
   std::shared_ptr<PinnedPool> pinned_;
-  int64_t rows_hint_ = 0;  // learned persistent-DFS pool capacity
-  unsigned int* abort_host_ = nullptr;       // watchdog flag (pinned, device-mapped)
-  const unsigned int* abort_dev_ = nullptr;
   int64_t* h_scalar_ = nullptr;   // pinned readback scratch (allocated once: hipHostFree syncs)
   kern::FCtl* call_params_ = nullptr;  // pinned per-call control blocks [2] (read by the init kernel)
   unsigned int* d_call_seq_ = nullptr;  // device call counter: the init kernel reads slot seq & 1
@@ -242,6 +239,8 @@ class GpuMiner {
   int64_t idx_cap_ = 1 << 20;     // rule-map entry capacity (grown after an overflow)
   void* comm_s_ = nullptr;        // tx-DP: support-tile all-reduce stream (created once)
   std::vector<void*> tile_ev_;    // tx-DP: support-tile events (created once)
+  void* idx_s_ = nullptr;         // rule-map side stream (a forked branch of the captured graph)
+  void* idx_ev_[2] = {nullptr, nullptr};  // fork / join
   size_t idx_scan_bytes_ = 0;
   bool big_lds_ = false;
 };

@@ -40,6 +40,8 @@ void flag_scan(const uint32_t* cnt, uint32_t minsup, int64_t n, int64_t* pos, vo
 // absolute); writes cnt[c - c0]
 void extend_count(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
                   int64_t c0, int64_t c1, uint32_t* cnt, hipStream_t s);
+// extend_count launches so far that split long rows into slices (atomic partial counts)
+long long extend_split_launches();
 // out2[0] = survivors of chunk, out2[1] = next level's candidate total (one readback)
 void child_totals(const int64_t* cand_off, int64_t a0, int64_t a1, int64_t c0, const int64_t* pos,
                   int64_t nc, uint64_t* out2, hipStream_t s);
@@ -206,10 +208,7 @@ struct RootSetupArgs {
   int my_rank;
   bool download;   // level-1 nodes also go straight to FCtl::h (inline download mode)
   bool host_tab;   // frequent-item ids | counts to FCtl::host_tab
-  const int64_t* cost;  // world > 1 and non-null: rank the root classes here from these costs
-                        // (F <= kRootRankMax; prank unused) instead of reading prank
 };
-constexpr int64_t kRootRankMax = 8192;
 void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s);
 // rank root classes by estimated cost (n_a^2 + 1 from the gram, desc) for the snake partition;
 // with prank == nullptr only the costs are computed (the root setup ranks them)
@@ -251,82 +250,19 @@ struct PairsArgs {
   int64_t n_items;
   const int32_t* tie;      // item id -> tie rank (nullptr: the id)
   const int32_t* inv_tie;  // tie rank -> item id (nullptr: identity)
-  // scratch
-  uint32_t* len_r;         // [F_max]
-  uint32_t* cursor;        // [F_max]
-  int64_t* len_id;         // [n_items + 1]
-  void* scan_temp;
-  size_t scan_temp_bytes;  // pairs_scan_temp_bytes(n_items)
-  unsigned long long* ent; // [ent_cap] unsorted keys
+  void* scratch;            // pairs_scratch_bytes(F_max, n_items)
+  size_t scratch_bytes;
+  unsigned long long* ent;  // [ent_cap] unsorted keys
   int64_t ent_cap;
-  unsigned int* status;    // [1]
   // output (device)
   int64_t* row_ptr;        // [n_items + 1], by item id
   int32_t* cons;           // [ent_cap]
   uint32_t* cnt;           // [ent_cap]
   const PairsHost* host;   // device-visible (e.g. &FCtl::ph of the call); nullptr: no copy-out
 };
-size_t pairs_scan_temp_bytes(int64_t n_items);
+size_t pairs_scratch_bytes(int64_t F_max, int64_t n_items);
 void pairs_to_csr(const PairsArgs& a, hipStream_t s);
 void pairs_enable_big_lds();  // once per process/device before the first pairs_to_csr
-
-// ---- persistent DFS (dfs_persistent.hip) ----
-struct DfsTask {
-  const unsigned long long* bm;  // class members' bitmaps [n][Wp]
-  const int32_t* rank;           // members' last item (original item id inside the DFS kernel)
-  const int64_t* gid;            // members' global trie node ids
-  int32_t n, depth, a0, a1;      // class size, members' itemset size, rows [a0, a1) to expand
-};
-struct DfsCtl {  // zeroed before every launch; hot counters on separate 128-byte lines
-  unsigned long long q_head;     char pad0[120];
-  unsigned long long q_tail;     char pad1[120];
-  unsigned long long pending;    char pad2[120];
-  unsigned long long row_top;    char pad3[120];
-  unsigned int idle;             char pad4[124];
-  unsigned long long candidates;
-  unsigned int overflow, timeout, max_depth, bad_task, aborted, exited;
-};
-struct DfsArgs {
-  // seed level (classes = runs of equal row_end)
-  const uint64_t* seed_bm;
-  const int32_t* seed_rank;
-  const int64_t* seed_gid;
-  const int32_t* seed_row_end;
-  int32_t* seed_items;  // scratch [seed_rows]: original item ids of the seed rows
-  int64_t seed_rows;
-  int seed_depth;
-  // queue + pool
-  DfsTask* tasks;
-  unsigned int* ready;
-  int64_t task_cap;
-  DfsCtl* ctl;
-  uint64_t* pool_bm;
-  int32_t* pool_rank;
-  int64_t* pool_gid;
-  int64_t row_cap;
-  // output trie (node id = out_base + pool row)
-  int64_t* out_parent;
-  int32_t* out_item;
-  uint32_t* out_count;
-  uint8_t* out_depth;
-  int64_t out_base;
-  const int32_t* ids;
-  int64_t Wp;
-  uint32_t minsup;
-  int max_len;
-  int n_cus;
-  unsigned long long timeout_ticks;  // 100 MHz wall-clock ticks
-  const unsigned int* abort_flag;    // host-mapped pinned word; host watchdog sets it to 1
-  unsigned int* wave_state;          // per-wave breadcrumbs (debug): [state, idx_lo, a, n]
-};
-void dfs_persistent(const DfsArgs& a, hipStream_t s);
-// DFS region [out_base, out_base+rows): drop holes (depth 0), order rows by depth (stable:
-// parents before children) into par2/item2/cnt2/dep2 with in-region parents remapped.
-// Returns the number of valid nodes (synchronises the stream).
-size_t dfs_compact_temp_bytes(int64_t rows);
-int64_t dfs_compact(int64_t rows, int64_t out_base, int64_t* par, int32_t* item, uint32_t* cnt,
-                    uint8_t* dep, void* temp, size_t temp_bytes, int64_t* par2, int32_t* item2,
-                    uint32_t* cnt2, uint8_t* dep2, unsigned long long* h_holes, hipStream_t s);
 
 // ---- association rules (rules.hip) ----
 struct RuleArgs {

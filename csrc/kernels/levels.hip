@@ -1034,7 +1034,6 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
   __shared__ int ok;
   __shared__ int64_t s_scan[1024];
   __shared__ int64_t s_carry;
-  __shared__ __attribute__((aligned(16))) int32_t s_cost[kRootRankMax];
   const int64_t F = desc[1].n_rows;
   // root candidate offsets: every class owned → closed form; else a block scan of the owned
   // classes' lengths (F - a - 1)
@@ -1044,35 +1043,12 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     for (int64_t i = threadIdx.x; i <= F; i += blockDim.x) a.cand_off[i] = i * (2 * F - i - 1) / 2;
   } else {
     if (threadIdx.x == 0) s_carry = 0;
-    // in-kernel ranking (cost desc, item asc): costs n^2 + 1 <= F^2 + 1 fit in 32 bits
-    const bool own_rank = a.cost && F <= kRootRankMax;
-    if (own_rank)
-      for (int64_t i = threadIdx.x; i < F; i += blockDim.x) s_cost[i] = (int32_t)a.cost[i];
     __syncthreads();
     for (int64_t base = 0; base <= F; base += blockDim.x) {
       const int64_t i = base + threadIdx.x;
       int64_t v = 0;
       if (i < F) {
-        int64_t k;
-        if (own_rank) {
-          // 8 costs per step from two 16-byte LDS reads (same address in every lane: broadcast),
-          // so the loop is not bound by one LDS round trip per compare
-          const int32_t ci = s_cost[i], ii = (int32_t)i;
-          const int32_t F8 = (int32_t)F & ~7;
-          int32_t r = 0;
-          for (int32_t j = 0; j < F8; j += 8) {
-            const int4 c0 = *(const int4*)&s_cost[j];
-            const int4 c1 = *(const int4*)&s_cost[j + 4];
-            const int32_t cj[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-#pragma unroll
-            for (int q = 0; q < 8; ++q) r += (cj[q] > ci || (cj[q] == ci && j + q < ii)) ? 1 : 0;
-          }
-          for (int32_t j = F8; j < (int32_t)F; ++j)
-            r += (s_cost[j] > ci || (s_cost[j] == ci && j < ii)) ? 1 : 0;
-          k = r;
-        } else {
-          k = a.prank[i];
-        }
+        const int64_t k = a.prank[i];  // cost rank from level_partition (k_rank_desc)
         const int64_t rnd = k / a.world, p = k % a.world;
         const int64_t owner = (rnd % 2 == 0) ? p : a.world - 1 - p;
         v = owner == a.my_rank ? F - i - 1 : 0;

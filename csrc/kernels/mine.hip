@@ -11,6 +11,9 @@
 // All kernels are wave64-native: teams are power-of-two lane groups inside a 64-lane wave,
 // reductions use __shfl_xor within the team, block sizes are multiples of 64.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdlib>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -745,11 +748,18 @@ void child_totals(const int64_t* cand_off, int64_t a0, int64_t a1, int64_t c0, c
 
 // row slices per candidate: enough (candidate, slice) teams for ~8 wave64 teams per CU, each
 // slice >= 2048 16-byte units (32 KB per row)
+std::atomic<long long> g_split_launches{0};  // extend_count launches that split rows (tests)
+
 static int64_t extend_split(int64_t Wp, int64_t n_cand, int ts) {
   if (ts != 64 || n_cand <= 0) return 1;
+  const char* fe = std::getenv("KMLS_EXTEND_SPLIT");  // test knob: slices per row
+  const int64_t forced = fe ? (int64_t)std::atoll(fe) : 0;
+  if (forced > 0) return std::max<int64_t>(1, std::min<int64_t>(forced, (Wp >> 1) / 64));
   const int64_t want = (256 * 8 + n_cand - 1) / n_cand;
   return std::max<int64_t>(1, std::min<int64_t>(want, (Wp >> 1) / 2048));
 }
+
+long long extend_split_launches() { return g_split_launches.load(); }
 
 void extend_count(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
                   int64_t c0, int64_t c1, uint32_t* cnt, hipStream_t s) {
@@ -757,7 +767,10 @@ void extend_count(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64
   const int ts = team_size(Wp);
   const int64_t teams_per_block = kBlock / ts;
   const int64_t split = extend_split(Wp, c1 - c0, ts);
-  if (split > 1) KMLS_HIP(hipMemsetAsync(cnt, 0, (size_t)(c1 - c0) * sizeof(uint32_t), s));
+  if (split > 1) {
+    KMLS_HIP(hipMemsetAsync(cnt, 0, (size_t)(c1 - c0) * sizeof(uint32_t), s));
+    g_split_launches.fetch_add(1);
+  }
   const int g = grid_for((c1 - c0) * split, (int)teams_per_block, 256 * 32);
   KMLS_TEAM_DISPATCH(ts, k_extend_count, dim3(g), dim3(kBlock), 0, s,
                      (const unsigned long long*)bm, Wp, cand_off, n_rows, c0, c1, split, cnt);

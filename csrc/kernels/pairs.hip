@@ -94,19 +94,77 @@ __global__ __launch_bounds__(256) void k_pairs_count(const uint32_t* __restrict_
   }
 }
 
-// per item id: its row length (frequent items) or 0; slot n_items is the scan's total slot
+// per item id: its row length (frequent items) or 0; slot n_items is the scan's total slot.
+// Rows longer than the small sort's capacity are listed for the big-row sort.
+__device__ __forceinline__ int64_t len_of_item(const int32_t* __restrict__ rank_of, int64_t i,
+                                               int64_t n_items, int64_t F,
+                                               const uint32_t* __restrict__ len_r,
+                                               unsigned int* __restrict__ n_long,
+                                               int32_t* __restrict__ long_rows) {
+  if (i >= n_items) return 0;
+  const int32_t r = rank_of[i];
+  if (r < 0 || r >= F) return 0;
+  const uint32_t v = len_r[r];
+  if (v > (uint32_t)kSortSmall) long_rows[atomicAdd(n_long, 1u)] = r;
+  return v;
+}
+
 __global__ void k_pairs_len_by_id(const int32_t* __restrict__ rank_of, int64_t n_items,
                                   const int64_t* __restrict__ dF, int64_t F_host,
-                                  const uint32_t* __restrict__ len_r, int64_t* __restrict__ len_id) {
+                                  const uint32_t* __restrict__ len_r, int64_t* __restrict__ len_id,
+                                  unsigned int* __restrict__ n_long, int32_t* __restrict__ long_rows) {
   const int64_t F = dF ? *dF : F_host;
   const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n_items; i += nthr) {
-    int64_t v = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n_items; i += nthr)
+    len_id[i] = len_of_item(rank_of, i, n_items, F, len_r, n_long, long_rows);
+}
+
+// Small vocabularies (the resident path): lengths by item id + exclusive scan → row_ptr in ONE
+// block (1024 threads, a contiguous run of items each), instead of a lengths pass and a
+// multi-launch device scan.
+constexpr int kScanThreads = 1024;
+constexpr int64_t kScanSmallMax = 64 * kScanThreads;
+__global__ __launch_bounds__(kScanThreads) void k_pairs_scan_small(
+    const int32_t* __restrict__ rank_of, int64_t n_items, const int64_t* __restrict__ dF,
+    int64_t F_host, const uint32_t* __restrict__ len_r, int64_t* __restrict__ row_ptr,
+    unsigned int* __restrict__ n_long, int32_t* __restrict__ long_rows) {
+  __shared__ int64_t s_w[kScanThreads / 64];
+  const int64_t F = dF ? *dF : F_host;
+  const int64_t n = n_items + 1;
+  const int64_t per = (n + kScanThreads - 1) / kScanThreads;
+  const int64_t i0 = (int64_t)threadIdx.x * per;
+  int64_t sum = 0;
+  for (int64_t k = 0; k < per; ++k) {
+    const int64_t i = i0 + k;
+    if (i < n) sum += len_of_item(rank_of, i, n_items, F, len_r, n_long, long_rows);
+  }
+  // block exclusive scan of the per-thread sums: wave64 inclusive scan, then wave totals
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t inc = sum;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t run = 0;
+    for (int k = 0; k < kScanThreads / 64; ++k) {
+      const int64_t t = s_w[k];
+      s_w[k] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+  int64_t pre = s_w[w] + inc - sum;
+  for (int64_t k = 0; k < per; ++k) {  // second pass re-reads the (cached) lengths
+    const int64_t i = i0 + k;
+    if (i >= n) break;
+    row_ptr[i] = pre;
     if (i < n_items) {
       const int32_t r = rank_of[i];
-      if (r >= 0 && r < F) v = len_r[r];
+      if (r >= 0 && r < F) pre += len_r[r];
     }
-    len_id[i] = v;
   }
 }
 
@@ -233,13 +291,18 @@ __global__ __launch_bounds__(1024) void k_pairs_sort_big(
     const int64_t* __restrict__ dF, int64_t F_host, const uint32_t* __restrict__ len_r,
     const int32_t* __restrict__ ids, const int32_t* __restrict__ inv_tie,
     const int64_t* __restrict__ row_ptr, const unsigned long long* __restrict__ ent, int64_t ent_cap,
-    int32_t* __restrict__ cons, uint32_t* __restrict__ cnt, unsigned int* __restrict__ status) {
+    int32_t* __restrict__ cons, uint32_t* __restrict__ cnt, unsigned int* __restrict__ status,
+    const unsigned int* __restrict__ n_long, const int32_t* __restrict__ long_rows) {
   extern __shared__ unsigned long long s_dyn[];
   const int64_t F = dF ? *dF : F_host;
-  const int64_t r = blockIdx.x;
-  if (r < F && threadIdx.x == 0 && len_r[r] > (uint32_t)kSortBig) atomicOr(status, 2u);
-  sort_row<kSortBig>(s_dyn, r, F, len_r, ids, inv_tie, row_ptr, ent, ent_cap, cons, cnt,
-                     kSortSmall);
+  const unsigned int nl = *n_long;
+  for (unsigned int i = blockIdx.x; i < nl; i += gridDim.x) {
+    const int64_t r = long_rows[i];
+    if (threadIdx.x == 0 && len_r[r] > (uint32_t)kSortBig) atomicOr(status, 2u);
+    sort_row<kSortBig>(s_dyn, r, F, len_r, ids, inv_tie, row_ptr, ent, ent_cap, cons, cnt,
+                       kSortSmall);
+    __syncthreads();
+  }
 }
 
 __global__ void k_pairs_copyout(const int64_t* __restrict__ row_ptr, int64_t n_items,
@@ -266,45 +329,74 @@ __global__ void k_pairs_copyout(const int64_t* __restrict__ row_ptr, int64_t n_i
 
 }  // namespace
 
-size_t pairs_scan_temp_bytes(int64_t n_items) {
+namespace {
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+size_t cub_scan_bytes(int64_t n_items) {
+  if (n_items + 1 <= kScanSmallMax) return 0;
   size_t b = 0;
   KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int64_t*)nullptr,
                                             (int64_t*)nullptr, (int)(n_items + 1)));
-  return b + 256;
+  return b;
+}
+}  // namespace
+
+// scratch: [status | n_long | len_r | cursor] (zeroed by ONE memset) | long_rows | len_id | cub
+size_t pairs_scratch_bytes(int64_t F_max, int64_t n_items) {
+  return 256 + align256((size_t)F_max * 8) + align256((size_t)F_max * 4) +
+         align256((size_t)(n_items + 1) * 8) + align256(cub_scan_bytes(n_items)) + 256;
 }
 
 void pairs_to_csr(const PairsArgs& a, hipStream_t s) {
   if (a.F_max <= 0) throw std::runtime_error("pairs_to_csr: F_max must be > 0");
+  if (a.scratch_bytes < pairs_scratch_bytes(a.F_max, a.n_items))
+    throw std::runtime_error("pairs_to_csr: scratch too small");
+  char* p = (char*)a.scratch;
+  unsigned int* status = (unsigned int*)p;
+  unsigned int* n_long = status + 1;
+  uint32_t* len_r = (uint32_t*)(p + 256);
+  uint32_t* cursor = len_r + a.F_max;
+  const size_t zero_bytes = 256 + (size_t)a.F_max * 8;
+  p += 256 + align256((size_t)a.F_max * 8);
+  int32_t* long_rows = (int32_t*)p;
+  p += align256((size_t)a.F_max * 4);
+  int64_t* len_id = (int64_t*)p;
+  p += align256((size_t)(a.n_items + 1) * 8);
+  void* cub_tmp = p;
   const unsigned nt = (unsigned)((a.F_max + kPT - 1) / kPT);
-  KMLS_HIP(hipMemsetAsync(a.len_r, 0, (size_t)a.F_max * 4, s));
-  KMLS_HIP(hipMemsetAsync(a.cursor, 0, (size_t)a.F_max * 4, s));
-  KMLS_HIP(hipMemsetAsync(a.status, 0, 4, s));
+  KMLS_HIP(hipMemsetAsync(a.scratch, 0, zero_bytes, s));
   hipLaunchKernelGGL(k_pairs_count, dim3(nt, nt), dim3(256), 0, s, a.gram, a.ld, a.dF, a.F_host,
-                     a.minsup, a.len_r);
+                     a.minsup, len_r);
   KMLS_HIP(hipGetLastError());
-  const unsigned nb = (unsigned)std::min<int64_t>((a.n_items + 256) / 256, 4096);
-  hipLaunchKernelGGL(k_pairs_len_by_id, dim3(nb), dim3(256), 0, s, a.rank_of, a.n_items, a.dF,
-                     a.F_host, a.len_r, a.len_id);
-  KMLS_HIP(hipGetLastError());
-  size_t tb = a.scan_temp_bytes;
-  KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(a.scan_temp, tb, a.len_id, a.row_ptr,
-                                            (int)(a.n_items + 1), s));
+  if (a.n_items + 1 <= kScanSmallMax) {
+    hipLaunchKernelGGL(k_pairs_scan_small, dim3(1), dim3(kScanThreads), 0, s, a.rank_of, a.n_items,
+                       a.dF, a.F_host, len_r, a.row_ptr, n_long, long_rows);
+    KMLS_HIP(hipGetLastError());
+  } else {
+    const unsigned nb = (unsigned)std::min<int64_t>((a.n_items + 256) / 256, 4096);
+    hipLaunchKernelGGL(k_pairs_len_by_id, dim3(nb), dim3(256), 0, s, a.rank_of, a.n_items, a.dF,
+                       a.F_host, len_r, len_id, n_long, long_rows);
+    KMLS_HIP(hipGetLastError());
+    size_t tb = cub_scan_bytes(a.n_items);
+    KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp, tb, len_id, a.row_ptr,
+                                              (int)(a.n_items + 1), s));
+  }
   hipLaunchKernelGGL(k_pairs_fill, dim3(nt, nt), dim3(256), 0, s, a.gram, a.ld, a.dF, a.F_host,
-                     a.minsup, a.ids, a.tie, a.row_ptr, a.cursor, a.ent, a.ent_cap, a.status);
+                     a.minsup, a.ids, a.tie, a.row_ptr, cursor, a.ent, a.ent_cap, status);
   KMLS_HIP(hipGetLastError());
   const unsigned rows = (unsigned)a.F_max;
-  hipLaunchKernelGGL(k_pairs_sort_small, dim3(rows), dim3(256), 0, s, a.dF, a.F_host, a.len_r,
+  hipLaunchKernelGGL(k_pairs_sort_small, dim3(rows), dim3(256), 0, s, a.dF, a.F_host, len_r,
                      a.ids, a.inv_tie, a.row_ptr, a.ent, a.ent_cap, a.cons, a.cnt);
   KMLS_HIP(hipGetLastError());
   if (a.F_max > kSortSmall + 1) {  // a row can only exceed 2048 entries if F > 2049
-    hipLaunchKernelGGL(k_pairs_sort_big, dim3(rows), dim3(1024),
-                       (size_t)kSortBig * sizeof(unsigned long long), s, a.dF, a.F_host, a.len_r,
-                       a.ids, a.inv_tie, a.row_ptr, a.ent, a.ent_cap, a.cons, a.cnt, a.status);
+    hipLaunchKernelGGL(k_pairs_sort_big, dim3(64), dim3(1024),
+                       (size_t)kSortBig * sizeof(unsigned long long), s, a.dF, a.F_host, len_r,
+                       a.ids, a.inv_tie, a.row_ptr, a.ent, a.ent_cap, a.cons, a.cnt, status,
+                       n_long, long_rows);
     KMLS_HIP(hipGetLastError());
   }
   if (a.host) {
     hipLaunchKernelGGL(k_pairs_copyout, dim3(64), dim3(256), 0, s, a.row_ptr, a.n_items, a.cons,
-                       a.cnt, a.status, a.host);
+                       a.cnt, status, a.host);
     KMLS_HIP(hipGetLastError());
   }
 }

@@ -40,6 +40,8 @@ class JobSettings:
     num_gpus: int = 1
     min_confidence: float = 0.04  # legacy confidence rules (main.py:227)
     checkpoint_dir: Optional[pathlib.Path] = None  # KMLS_CHECKPOINT_DIR: phase resume
+    dist_timeout_s: float = 600.0      # KMLS_DIST_TIMEOUT_S: process-group init + collectives
+    sweep_timeout_s: float = 86400.0   # KMLS_SWEEP_TIMEOUT_S: ranks waiting for rank 0's sweep
 
     @property
     def dataset_list_file(self) -> pathlib.Path:
@@ -76,6 +78,8 @@ class JobSettings:
             min_confidence=float(_env("MIN_CONFIDENCE", "0.04")),
             checkpoint_dir=(pathlib.Path(os.environ["KMLS_CHECKPOINT_DIR"])
                             if os.environ.get("KMLS_CHECKPOINT_DIR") else None),
+            dist_timeout_s=float(_env("KMLS_DIST_TIMEOUT_S", "600")),
+            sweep_timeout_s=float(_env("KMLS_SWEEP_TIMEOUT_S", "86400")),
         )
 
 

@@ -72,25 +72,50 @@ def mine_rules(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float
 
 
 def mine_rules_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float,
-                           total_songs: int) -> Optional[Tuple[RuleIndexData, ItemsetTrie, str, Tuple[int, float]]]:
-    """Multi-GPU mining (torchrun); returns the result on rank 0, None elsewhere."""
+                           total_songs: int, ck: Optional[PhaseCheckpoint] = None
+                           ) -> Optional[Tuple[RuleIndexData, ItemsetTrie, str, Tuple[int, float]]]:
+    """Multi-GPU mining (torchrun); returns the result on rank 0, None elsewhere.
+
+    Phase checkpoints: after mining, every rank saves its frequent-item order and
+    its own sub-trie (tx mode: rank 0's global trie) under the run's checkpoint key.  A restarted
+    job whose ranks ALL find their sub-trie (and an unchanged frequent order) skips mining and
+    goes straight to the merge; a partial set is ignored (every rank re-mines)."""
+    import torch
     import torch.distributed as dist
     from ..parallel.dist_miner import DistMiner, gather_trie
     t0 = time.perf_counter()
     rank, world = dist.get_rank(), dist.get_world_size()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dm = DistMiner(tx.tx_ptr, tx.items, len(tx.names), min_support, device=local,
-                   max_len=2 if cfg.rules_mode == "pairs" else 0)
-    r = dm.step(download=True)
-    F = int(r["stats"].get("n_frequent_items", 0))
-    if dm.mode == "tx":  # every rank holds the identical global trie; rank 0 downloaded it
-        merged = r["trie"] if rank == 0 else None
+                   max_len=2 if cfg.rules_mode == "pairs" else 0,
+                   backend="cpu" if cfg.miner == "cpu" else "gpu")
+    phase = f"subtrie_r{rank}of{world}_{dm.mode}"
+    have = 1 if (ck is not None and ck.has(phase)) else 0
+    flag = torch.tensor([have], dtype=torch.int64,
+                        device=torch.device("cuda", local) if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:  # every rank has its phase output: no re-mining
+        z = ck.load(phase)
+        sub = {k: z[k] for k in ("parent", "item", "count", "depth")}
+        st = {"n_frequent_items": int(z["n_frequent"]), "backend": "checkpoint"}
+        if rank == 0:
+            print("Resumed per-rank sub-tries from checkpoint", ck.dir)
     else:
-        merged = gather_trie(r["trie"], rank, world, F)
+        r = dm.step(download=True)
+        sub = {k: np.asarray(v) for k, v in r["trie"].items() if k in ("parent", "item", "count", "depth")}
+        st = dict(r["stats"])
+        if ck is not None and ck.enabled and (dm.mode != "tx" or rank == 0):
+            ck.save(phase, n_frequent=np.int64(st.get("n_frequent_items", 0)), **sub)
+        _fault("after_mining_phase")
+    F = int(st.get("n_frequent_items", 0))
+    if dm.mode == "tx":  # every rank holds the identical global trie; rank 0 downloaded it
+        merged = sub if rank == 0 else None
+    else:
+        merged = gather_trie(sub, rank, world, F)
     if rank != 0:
         return None
     trie = ItemsetTrie(merged["parent"], merged["item"], merged["count"], merged["depth"],
-                       tx.n_tx, min_support, dict(r["stats"]), tx.names)
+                       tx.n_tx, min_support, st, tx.names)
     idx = build_index_from_trie(trie.parent, trie.item, trie.count, trie.depth, tx.n_tx,
                                 len(tx.names), tx.names)
     missing = total_songs - idx.n_keys
@@ -144,13 +169,25 @@ def run(cfg: Optional[JobSettings] = None) -> Dict:
     cfg = cfg or JobSettings.from_env()
     distributed = cfg.num_gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) > 1
     rank = 0
+    side = None  # gloo group for long host-side waits (the sweep), off the RCCL watchdog
     if distributed:
+        import datetime
         import torch
         import torch.distributed as dist
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # bounded rendezvous and collectives: a rank that never joins or dies
+        # fails the job within KMLS_DIST_TIMEOUT_S instead of hanging it; K8s then re-runs it.
+        # MINER=cpu runs the same protocol over gloo (the CPU test tier)
+        timeout = datetime.timedelta(seconds=cfg.dist_timeout_s)
+        if cfg.miner == "cpu":
+            dist.init_process_group("gloo", timeout=timeout)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
         rank = dist.get_rank()
+        if cfg.experiment_supports:
+            side = dist.new_group(backend="gloo",
+                                  timeout=datetime.timedelta(seconds=cfg.sweep_timeout_s))
     say = print if rank == 0 else (lambda *a, **k: None)
     say("=== Starting execution on ", current_time_str(), " ===")
     datasets = rot.get_dataset_list(cfg) if rank == 0 else None
@@ -177,8 +214,12 @@ def run(cfg: Optional[JobSettings] = None) -> Dict:
         pp.validate_and_map_artists_names_to_ids(t)  # every rank fails the same way
     _fault("after_best_tracks")
     tx = pp.group_tracks_by_playlist(t)
-    if cfg.experiment_supports and rank == 0:
-        run_support_sweep(cfg, tx, total_songs)
+    if cfg.experiment_supports:
+        if rank == 0:
+            run_support_sweep(cfg, tx, total_songs)
+        if side is not None:  # the other ranks wait here (gloo, long timeout), not in RCCL
+            import torch.distributed as dist
+            dist.barrier(group=side)
     ck = PhaseCheckpoint.for_dataset(cfg.checkpoint_dir, selected, min_support=cfg.min_support,
                                      rules_mode=cfg.rules_mode, sample_ratio=cfg.sample_ratio)
     resumed = ck.has("trie") if rank == 0 else False
@@ -191,7 +232,7 @@ def run(cfg: Optional[JobSettings] = None) -> Dict:
         res = resume_from_checkpoint(ck, tx, cfg.min_support, total_songs) if rank == 0 else None
         say("Resumed mining results from checkpoint", ck.dir)
     elif distributed:
-        res = mine_rules_distributed(cfg, tx, cfg.min_support, total_songs)
+        res = mine_rules_distributed(cfg, tx, cfg.min_support, total_songs, ck)
     else:
         res = mine_rules(cfg, tx, cfg.min_support, total_songs)
     if rank == 0 and not resumed and ck.enabled:

@@ -22,6 +22,7 @@ from typing import Dict, Hashable, List, Optional, Sequence
 import numpy as np
 
 from ..ops import native
+from ..utils.atomic_io import atomic_write_bytes
 
 
 @dataclasses.dataclass
@@ -118,7 +119,8 @@ class RuleIndexData:
         np.savez(buf, n_items=np.int64(self.n_items), row_ptr=self.row_ptr, cons=self.cons,
                  score=self.score, is_key=self.is_key, names_utf8=enc,
                  n_names=np.int64(len(names)))
-        pathlib.Path(path).write_bytes(buf.getvalue())
+        # tmp + fsync + rename, like the pickles: a reader never sees a truncated index
+        atomic_write_bytes(path, buf.getvalue())
 
     @classmethod
     def load(cls, path) -> "RuleIndexData":

@@ -66,10 +66,15 @@ def read_pickle_dict(cfg: ApiSettings, prefer_index: bool = True):
     idx_path = cfg.pickles_folder / RULES_INDEX_FILE
     use_idx = (prefer_index and idx_path.exists() and
                (not rec_path.exists() or idx_path.stat().st_mtime >= rec_path.stat().st_mtime))
+    index = None
     if use_idx:
-        index = RuleIndexData.load(idx_path)
-        source = "rules.idx"
-    else:
+        try:
+            index = RuleIndexData.load(idx_path)
+            source = "rules.idx"
+        except Exception as e:  # unreadable index: the pickle is the reference artifact
+            logger.error(f"Rule index {idx_path} unreadable ({e!r}); falling back to the pickle")
+            index = None
+    if index is None:
         with open(rec_path, "rb") as f:
             rec = pickle.load(f)
         index = RuleIndexData.from_rec_dict(rec)

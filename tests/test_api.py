@@ -191,3 +191,20 @@ def test_concurrent_requests_during_reloads(pvc):
         th[0].join()
     assert not errors
     assert app.state.mgr.reload_counter > 1
+
+
+def test_corrupt_rule_index_falls_back_to_pickle(pvc):
+    """rules.idx is written atomically; a corrupt/truncated one (crash of a foreign writer) is
+    skipped in favour of recommendations.pickle, so a fresh replica still becomes ready."""
+    import os
+    idx = pvc / "api-data" / "pickles" / "rules.idx"
+    assert idx.exists()
+    idx.write_bytes(idx.read_bytes()[:100])  # truncated
+    t = (pvc / "api-data" / "pickles" / "recommendations.pickle").stat().st_mtime
+    os.utime(idx, (t + 5, t + 5))  # newer than the pickle: the loader tries it first
+    with TestClient(create_app(api_settings(pvc))) as c:
+        assert c.get("/readyz").status_code == 200
+        rec = rec_dict(pvc)
+        seed = next(k for k, v in rec.items() if v)
+        got = c.post("/api/recommend/", json={"songs": [seed]}).json()["songs"]
+        assert got == oracle.recommend_oracle(rec, [seed], 10)

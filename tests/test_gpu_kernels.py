@@ -225,205 +225,6 @@ def test_dist_protocol_path_on_gpu(gpu_mod):
         assert st["global_itemsets"] == c["stats"]["n_itemsets"]
 
 
-@pytest.mark.parametrize("shape,ms", [("ds2", 0.05), ("ds2_weak", 0.03), ("tiny", 0.02),
-                                      ("ds2", 0.06)])
-def test_persistent_dfs_equals_level_wise(gpu_mod, shape, ms):
-    """Persistent work-queue DFS == level-wise path == CPU miner (first call also exercises the
-    capacity-overflow re-run: the initial pool holds 1M rows)."""
-    from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    tx = generate(shape, seed=21)
-    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
-    g = gpu_mod.GpuMiner(0, 4 << 30, 0)
-    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
-    for _ in range(2):
-        p = g.mine(ms, persistent=True)
-        assert p["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
-        assert p["stats"]["max_depth"] == c["stats"]["max_depth"]
-        assert np.array_equal(np.sort(p["count"]), np.sort(c["count"]))
-        # parents precede children (trie order used by every consumer)
-        assert (p["parent"] < np.arange(len(p["parent"]))).all()
-    lw = g.mine(ms, persistent=False)  # default path
-    assert lw["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
-    if c["stats"]["n_itemsets"] < 300_000:
-        assert _trie_dict(p) == _trie_dict(c)
-
-
-@pytest.mark.parametrize("tiles", [1, 4])
-def test_txdp_mode_world1(gpu_mod, tiles):
-    """Transaction-DP path (tiled supports, shard-local bitmaps, per-level count all-reduce
-    through the native communicator — a copy at world size 1) equals the CPU miner."""
-    from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
-    tx = generate("ds2_weak", seed=4)
-    dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, 0.03, mode="tx", support_tiles=tiles)
-    r = dm.step(download=True)
-    assert r["stats"]["levels_path"] == "chunked-txdp"
-    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.03)
-    assert _trie_dict(r["trie"]) == _trie_dict(c)
-
-
-def test_txdp_presharded_large(gpu_mod):
-    """Pre-sharded input (global_n_tx) on a 2M-transaction slice of the 10M x 1M shape."""
-    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
-    T = 2_000_000
-    ptr, items = gpu_mod.synth_transactions(T, 1_000_000, 40.0, 2000, 0.85, 0.85, 1)
-    dm = DistMiner(ptr, items, 1_000_000, 0.002, mode="tx", global_n_tx=T)
-    r = dm.step(download=True)
-    c = gpu_mod.mine_cpu(ptr, items, 1_000_000, 0.002)
-    assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
-    assert _trie_dict(r["trie"]) == _trie_dict(c)
-
-
-@pytest.mark.parametrize("metric,thr,strict,max_ante", [("confidence", 0.6, False, 0),
-                                                        ("confidence", 0.5, True, 0),
-                                                        ("lift", 1.2, False, 2),
-                                                        ("leverage", 0.0, False, 0)])
-def test_gpu_rules_equal_cpu(gpu_mod, metric, thr, strict, max_ante):
-    """HIP rule_score (hash + subset DP + ballot compaction) is bit-identical to the CPU engine,
-    including deep itemsets (k > 12 → per-wave global subset tables)."""
-    from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    from kubernetes_machine_learning_server_amd.models.fpgrowth import mine_csr
-    from kubernetes_machine_learning_server_amd.models.rules import rules_from_trie
-    tx = generate("ds_dense", seed=1)
-    trie = mine_csr(tx.tx_ptr, tx.items, tx.n_items, 0.06, backend="cpu")
-    assert int(trie.depth.max()) >= 10
-    g = rules_from_trie(trie, metric, thr, max_antecedent=max_ante, strict=strict, backend="gpu")
-    c = rules_from_trie(trie, metric, thr, max_antecedent=max_ante, strict=strict, backend="cpu")
-    assert len(g) == len(c) and len(c) > 0
-    for f in ("itemset", "antecedent", "consequent", "confidence", "lift"):
-        np.testing.assert_array_equal(getattr(g, f), getattr(c, f))
-
-
-@pytest.mark.parametrize("scratch_bits", ["18", "14"])
-def test_gpu_rules_deep_itemsets(gpu_mod, monkeypatch, scratch_bits):
-    """16-item cliques: itemsets up to size 16 exercise the per-wave global subset tables
-    (13 <= k <= scratch_bits) and the hash-walk path (k > scratch_bits)."""
-    from kubernetes_machine_learning_server_amd.models.fpgrowth import mine_csr
-    from kubernetes_machine_learning_server_amd.models.rules import rules_from_trie
-    monkeypatch.setenv("KMLS_RULES_SCRATCH_BITS", scratch_bits)
-    rng = np.random.default_rng(0)
-    rows = []
-    for t in range(40):
-        core = list(range(16)) if t < 24 else list(rng.choice(16, size=12, replace=False))
-        rows.append(sorted(set(core) | set(rng.choice(np.arange(16, 60), size=5).tolist())))
-    ptr = np.zeros(len(rows) + 1, np.int64)
-    ptr[1:] = np.cumsum([len(r) for r in rows])
-    items = np.concatenate([np.array(r, np.int32) for r in rows])
-    trie = mine_csr(ptr, items, 60, 0.5, backend="cpu")
-    assert int(trie.depth.max()) == 16
-    g = rules_from_trie(trie, "confidence", 0.95, backend="gpu")
-    c = rules_from_trie(trie, "confidence", 0.95, backend="cpu")
-    assert len(g) == len(c) and len(c) > 0
-    for f in ("itemset", "antecedent", "consequent", "confidence", "lift"):
-        np.testing.assert_array_equal(getattr(g, f), getattr(c, f))
-
-
-@pytest.mark.parametrize("n,n_keys,dedup", [(1000, 7, True), (300_000, 2246, True),
-                                             (2_000_000, 50_000, True), (100_000, 300, False)])
-def test_gpu_groupby_equals_host(gpu_mod, n, n_keys, dedup):
-    rng = np.random.default_rng(n)
-    keys = rng.integers(0, n_keys, size=n).astype(np.int32)
-    vals = rng.integers(0, 5000, size=n).astype(np.int32)
-    gp, gi = gpu_mod.group_to_csr_gpu(keys, vals, n_keys, dedup)
-    cp, ci = gpu_mod.group_to_csr(keys, vals, n_keys, dedup, True)
-    np.testing.assert_array_equal(gp, cp)
-    np.testing.assert_array_equal(gi, ci)
-
-
-def test_mine_partition_union_equals_full(gpu_mod):
-    """Replicated-data partition: the ranks' sub-tries (device-side snake partition of root
-    classes) are disjoint and their union is the full result."""
-    from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    tx = generate("ds2_weak", seed=6)
-    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.03)
-    ref = _trie_dict(c)
-    for world in (2, 3, 8):
-        union, total = {}, 0
-        g = gpu_mod.GpuMiner(0, 1 << 31, 0)
-        g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
-        for rank in range(world):
-            r = g.mine_partition(0.03, rank=rank, world=world)
-            assert r["stats"]["levels_path"] == "fused-resident-partition"
-            total += r["stats"]["n_itemsets"]
-            part = _trie_dict(r)
-            F = r["stats"]["n_frequent_items"]
-            mine = {k: v for k, v in part.items() if len(k) > 1}
-            assert not (set(mine) & set(union)), "ranks overlap"
-            union.update(part)
-        assert total == len(ref) and union == ref
-
-
-def test_split_k_grams_and_hash_supports(gpu_mod):
-    """Long rows (split-K gram, both kernels) and a 1M-item vocabulary (LDS-hash supports)."""
-    import torch
-    T, I = 700_000, 1_000_000
-    ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 2)
-    g = gpu_mod.GpuMiner(0, 1 << 31, torch.cuda.current_stream().cuda_stream or 0)
-    g.load_csr(ptr, items, I)
-    cnt = torch.zeros(I, dtype=torch.int32, device="cuda")
-    torch.cuda.synchronize()
-    g.item_support(cnt.data_ptr())
-    g.synchronize()
-    host = cnt.cpu().numpy().view(np.uint32)
-    np.testing.assert_array_equal(host, np.bincount(items, minlength=I))
-    F = g.select(host, T, 0.004)
-    assert 50 <= F <= 2000
-    Wp = g.words_local()
-    bm = torch.zeros((F, Wp), dtype=torch.int64, device="cuda")
-    torch.cuda.synchronize()
-    g.encode_bitmaps(bm.data_ptr(), Wp, 0)
-    ids, counts, _ = g.frequent()
-    rank_of = -np.ones(I, np.int64)
-    rank_of[ids] = np.arange(F)
-    rows = np.repeat(np.arange(T), np.diff(ptr))
-    rr = rank_of[items]
-    keep = rr >= 0
-    X = np.zeros((T, F), np.float32)
-    X[rows[keep], rr[keep]] = 1.0
-    ref = np.triu((X.T @ X).astype(np.int64), 1)
-    for mfma in (False, True):
-        gram = torch.zeros((F, F), dtype=torch.int32, device="cuda")
-        torch.cuda.synchronize()
-        g.pair_counts(bm.data_ptr(), Wp, gram.data_ptr(), mfma)
-        g.synchronize()
-        np.testing.assert_array_equal(np.triu(gram.cpu().numpy().astype(np.int64), 1), ref)
-
-
-def test_replicated_mode_multiprocess(gpu_mod):
-    """bench.py's N>1 path (DistMiner mode='replicate') in 3 real processes on one GPU."""
-    import subprocess
-    import sys
-    import pathlib
-    root = pathlib.Path(__file__).resolve().parents[1]
-    # three processes share one GPU: fixed arenas (the default takes half of the free HBM at
-    # construction, which races between processes starting together)
-    env = dict(os.environ, PYTHONPATH=str(root) + os.pathsep + os.environ.get("PYTHONPATH", ""),
-               KMLS_ARENA_GB="16")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                        "--nproc-per-node=3", "--master-addr=127.0.0.1", "--master-port=29613",
-                        str(root / "scripts" / "replicate_check.py")],
-                       capture_output=True, text=True, timeout=600, env=env, cwd=str(root))
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "replicate_check OK" in r.stdout
-    assert "replicate_check pipelined OK" in r.stdout
-
-
-@pytest.mark.parametrize("mode", ["allreduce", "reduce_scatter", "alltoall", "ring"])
-def test_pair_rows_gpu_world1(gpu_mod, mode):
-    """Pairs-only protocol on the GPU path (rectangular HIP bit-GEMM on the protocol stream)."""
-    from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
-    tx = generate("ds2_weak", seed=4)
-    dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, 0.03, mode="item", force_protocol=True)
-    ids, r0, r1, rows = dm.pair_rows(mode)
-    X = np.zeros((tx.n_tx, tx.n_items), np.float64)
-    for t in range(tx.n_tx):
-        X[t, tx.items[tx.tx_ptr[t]:tx.tx_ptr[t + 1]]] = 1.0
-    G = (X[:, ids].T @ X[:, ids]).astype(np.int64)
-    assert (r0, r1) == (0, len(ids))
-    np.testing.assert_array_equal(rows.astype(np.int64), G)
-
-
 def test_default_arena_grows_on_demand(gpu_mod, monkeypatch):
     """A default-sized arena starts small (KMLS_ARENA_INIT_MB here; 8 GiB normally) and grows
     when the device-resident path runs out of room, instead of falling back or failing."""
@@ -627,3 +428,22 @@ def test_max_len_leaf_levels(gpu_mod, fused, monkeypatch):
             r = g.mine(0.02, ml)
             assert int(r["stats"]["max_depth"]) == ml
             assert_same_itemsets(gpu_mod, r, c)
+
+
+@pytest.mark.parametrize("split", ["2", "3"])
+def test_extend_split_k_long_rows(gpu_mod, monkeypatch, split):
+    """Split-K extend (long rows sliced across teams, atomic partial counts, slice-0-only
+    metadata): forced on a long-row chunked run, including an odd chunk remainder, and the trie
+    must equal the CPU miner's."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate_large
+    monkeypatch.setenv("KMLS_FUSED_LEVELS", "0")
+    monkeypatch.setenv("KMLS_EXTEND_SPLIT", split)
+    tx = generate_large("10Mx1M", seed=11, n_tx=300_000 + 64 * 7, n_items=50_000)
+    before = gpu_mod.extend_split_launches()
+    g = gpu_mod.GpuMiner(0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    r = g.mine(0.003)
+    assert gpu_mod.extend_split_launches() > before, "the split path did not run"
+    c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.003)
+    assert int(c["stats"]["max_depth"]) >= 3
+    assert_same_itemsets(gpu_mod, r, c)

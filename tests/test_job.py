@@ -212,3 +212,68 @@ def test_unused_reference_helpers(pvc):
     first = next(iter(het.values()))
     assert "track_name" in first.columns and "track_uri" not in first.columns
     assert sum(len(v) for v in het.values()) == t.n_rows
+
+
+def rec_dict(root):
+    with open(root / "api-data" / "pickles" / "recommendations.pickle", "rb") as f:
+        return pickle.load(f)
+
+
+def _dist_job_worker(rank, world, port, root, fault, out_q):
+    import os as _os
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
+    if fault:
+        _os.environ["KMLS_FAULT"] = fault
+    else:
+        _os.environ.pop("KMLS_FAULT", None)
+    import pathlib as _pl
+    from kubernetes_machine_learning_server_amd.job import main as _job
+    from tests.helpers import job_settings as _js
+    cfg = _js(_pl.Path(root), num_gpus=world, checkpoint_dir=_pl.Path(root) / "ck",
+              dist_timeout_s=120.0)
+    try:
+        out_q.put((rank, _job.run(cfg), None))
+    except Exception as e:  # noqa: BLE001 — the injected fault
+        out_q.put((rank, None, repr(e)))
+
+
+def _run_dist_job(root, world, fault=""):
+    import socket
+    import torch.multiprocessing as tmp_mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = tmp_mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_job_worker, args=(r, world, port, str(root), fault, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+def test_distributed_job_phase_checkpoints(tmp_path):
+    """torchrun-style job at world size 2 (gloo + the CPU protocol): the per-rank sub-trie
+    phase is checkpointed; after a crash between mining and publishing, the restarted job
+    resumes from every rank's sub-trie (no re-mining) and publishes the same artifacts as a
+    single-process run."""
+    make_datasets(tmp_path, shapes=("ds2_weak", "tiny"), seeds=(3, 4))
+    res = _run_dist_job(tmp_path, 2, fault="after_mining_phase")
+    assert all("injected fault" in (r[2] or "") for r in res)
+    ck_files = list((tmp_path / "ck").rglob("subtrie_r*of2_*.npz"))
+    assert len(ck_files) == 2, ck_files
+    res = _run_dist_job(tmp_path, 2)
+    summary = res[0][1]
+    assert summary and summary["dataset_index"] == 1
+    assert summary["backend"] == "checkpoint"  # merged from the sub-tries, not re-mined
+    single = tmp_path / "single"
+    make_datasets(single, shapes=("ds2_weak", "tiny"), seeds=(3, 4))
+    ref = job.run(job_settings(single))
+    assert summary["n_itemsets"] == ref["n_itemsets"] and summary["n_keys"] == ref["n_keys"]
+    assert rec_dict(tmp_path) == rec_dict(single)
+    assert not list((tmp_path / "ck").rglob("*.npz"))  # cleared after success
