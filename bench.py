@@ -169,7 +169,7 @@ def main() -> int:
                     help="leave the rule-map build out of the step (A/B only)")
     ap.add_argument("--cpu", action="store_true", help="native CPU miner (no GPU)")
     ap.add_argument("--no-config2", action="store_true", help="skip BASELINE config 2 (0.01)")
-    ap.add_argument("--serve-qps", default="2000,10000",
+    ap.add_argument("--serve-qps", default="2000,5000,10000",
                     help="offered QPS points for the serving half ('' = skip)")
     ap.add_argument("--serve-duration", type=float, default=3.0)
     ap.add_argument("--serve-backend", default="auto")

@@ -281,11 +281,7 @@ class GpuRuleIndex {
   int32_t* d_cons_ = nullptr;
   uint32_t* d_score_ = nullptr;  // dense rank of the score (exact order key), see serve.hip
   uint8_t* d_is_key_ = nullptr;
-  // staging buffers (grown on demand)
-  int64_t cap_q_ = 0, cap_s_ = 0, cap_o_ = 0;
-  int64_t* d_q_ptr_ = nullptr;
-  int32_t* d_seeds_ = nullptr;
-  int32_t* d_out_ = nullptr;
+  // mapped pinned staging (queries in, results out; grown on demand)
   int32_t* h_pinned_ = nullptr;
   int64_t cap_pinned_ = 0;
 };

@@ -232,6 +232,13 @@ def main(argv=None) -> int:
     port = _free_port()
     proc = start_server(base, a.backend, a.workers, port)
     try:
+        import urllib.request
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/readyz", timeout=5) as r:
+            ready = json.loads(r.read())
+        print(json.dumps({"bench": "serve_ready", "backend": a.backend,
+                          "gpu_index": ready.get("gpu_index"),
+                          "gpu_min_batch": ready.get("gpu_min_batch"),
+                          "crossover_us": ready.get("crossover_us")}), flush=True)
         measure(port, 200, 2.0, 1, queries)  # warm-up
         for qps in [float(x) for x in a.qps.split(",")]:
             r = measure(port, qps, a.duration, a.clients, queries)

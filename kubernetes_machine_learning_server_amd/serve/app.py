@@ -170,7 +170,11 @@ def create_app(cfg: Optional[ApiSettings] = None) -> FastAPI:
         if cfg.serve_backend == "python":
             # the reference's own matcher (dict-of-dicts + defaultdict + sorted), for A/B benches
             res = _python_match(snap, seeds, k)
-        elif snap.gpu_index is not None:
+        elif (snap.gpu_index is not None and snap.gpu_min_batch is not None
+              and inflight[0] >= batcher._gpu_min(snap)):
+            # enough requests in flight to fill a batch the HIP matcher answers faster (the
+            # crossover measured on this index): queue for the micro-batcher.  Below that the
+            # queue hop would only add latency, so the C++ matcher answers inline.
             ids, n = await batcher.submit(snap, M.seed_ids(snap, seeds), k)
             res = None if n < 0 else [snap.index.names[i] for i in ids[:n]]
             metrics.batch.set(batcher.last_batch)
@@ -184,13 +188,19 @@ def create_app(cfg: Optional[ApiSettings] = None) -> FastAPI:
         metrics.requests.labels("rules").inc()
         return res
 
+    inflight = [0]  # requests of this worker between validation and response
+
     @app.post("/api/recommend/", tags=["recommend"])
     async def get_recommendations(request: Annotated[SongRequest, Body(openapi_examples=OPENAPI_EXAMPLES)]):
         t0 = time.perf_counter()
         if not request.songs:
             metrics.requests.labels("empty").inc()
             raise HTTPException(status_code=400, detail="The songs list cannot be empty.")
-        songs = await recommend_tracks_for_track(request.songs)
+        inflight[0] += 1
+        try:
+            songs = await recommend_tracks_for_track(request.songs)
+        finally:
+            inflight[0] -= 1
         metrics.latency.observe(time.perf_counter() - t0)
         return {"songs": songs, "model_date": mgr.cache_value, "version": cfg.version}
 
@@ -218,7 +228,9 @@ def create_app(cfg: Optional[ApiSettings] = None) -> FastAPI:
         if snap is None:
             return JSONResponse({"ready": False, "error": mgr.last_error}, status_code=503)
         return {"ready": True, "model_date": snap.marker, "keys": snap.index.n_keys,
-                "source": snap.source, "gpu_index": snap.gpu_index is not None}
+                "source": snap.source, "gpu_index": snap.gpu_index is not None,
+                "gpu_min_batch": snap.gpu_min_batch,
+                "crossover_us": {str(b): v for b, v in (snap.crossover or {}).items()}}
 
     @app.get("/metrics", include_in_schema=False)
     def prometheus_metrics():

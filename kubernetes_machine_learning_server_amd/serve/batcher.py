@@ -62,9 +62,9 @@ class MicroBatcher:
                 except asyncio.QueueEmpty:
                     break
             self._load = 0.8 * self._load + 0.2 * len(items)
-            gpu = first[0].gpu_index is not None
-            if (gpu and self.max_wait > 0 and len(items) < self.gpu_min_batch
-                    and self._load * 4 >= self.gpu_min_batch):
+            gmin = self._gpu_min(first[0])
+            if (gmin is not None and self.max_wait > 0 and len(items) < gmin
+                    and self._load * 4 >= gmin):
                 deadline = time.perf_counter() + self.max_wait
                 while len(items) < self.max_batch:
                     rem = deadline - time.perf_counter()
@@ -81,7 +81,8 @@ class MicroBatcher:
             for (_, k), grp in groups.items():
                 snap = grp[0][0]
                 try:
-                    if snap.gpu_index is not None and len(grp) >= self.gpu_min_batch:
+                    gmin = self._gpu_min(snap)
+                    if gmin is not None and len(grp) >= gmin:
                         ids, n = await loop.run_in_executor(None, self._run_batch, snap, grp, k)
                     else:
                         ids, n = self._run_batch(snap, grp, k)
@@ -93,6 +94,16 @@ class MicroBatcher:
                         if not it[3].done():
                             it[3].set_exception(e)
 
+    def _gpu_min(self, snap) -> Optional[int]:
+        """Smallest batch routed to the HIP matcher for this snapshot: its measured crossover
+        (state.measure_crossover), never below GPU_MIN_BATCH; None = CPU only."""
+        if snap.gpu_index is None:
+            return None
+        m = getattr(snap, "gpu_min_batch", self.gpu_min_batch)
+        if m is None:
+            return None
+        return max(int(m), 1) if m == 1 else max(int(m), self.gpu_min_batch)
+
     def _run_batch(self, snap, grp: List, k: int):
         lens = [len(it[1]) for it in grp]
         q_ptr = np.zeros(len(grp) + 1, np.int64)
@@ -101,7 +112,8 @@ class MicroBatcher:
         self.batches += 1
         self.queries += len(grp)
         self.last_batch = len(grp)
-        if snap.gpu_index is not None and len(grp) >= self.gpu_min_batch:
+        gmin = self._gpu_min(snap)
+        if gmin is not None and len(grp) >= gmin:
             self.gpu_batches += 1
             ids, n = snap.gpu_index.query_batch(q_ptr, seeds.astype(np.int32), k)
             if (n == -2).any():  # kernel table overflow: answer those on the CPU

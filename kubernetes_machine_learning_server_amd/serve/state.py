@@ -39,6 +39,10 @@ class ModelSnapshot:  # immutable; _py_rec (python backend cache) is set once vi
     n_recommendations: int
     source: str  # "rules.idx" | "pickle"
     gpu_index: Any = None  # _native.GpuRuleIndex when SERVE_BACKEND uses the GPU
+    # smallest batch the HIP matcher answers faster than the C++ one on THIS index (measured
+    # when the snapshot is built; None = the GPU never wins, every batch stays on the CPU)
+    gpu_min_batch: Optional[int] = None
+    crossover: Any = None  # the measurement behind gpu_min_batch
 
     @property
     def best_track_names(self) -> List[str]:
@@ -81,6 +85,40 @@ def read_pickle_dict(cfg: ApiSettings, prefer_index: bool = True):
         source = "pickle"
     logger.info(f"Recommendations loaded: {index.n_keys}")
     return best_tracks, index, source
+
+
+def measure_crossover(index, gpu_index, k: int = 10, reps: int = 5, seed: int = 0):
+    """Time the C++ and HIP batch matchers on sample queries of this index (1-5 key seeds)
+    for batch sizes 1..1024; returns (smallest batch where the GPU is faster, {B: (cpu_us,
+    gpu_us)}).  The auto router (SERVE_BACKEND=auto) sends only batches at least that large to
+    the GPU, so at loads that never build such batches the GPU is provably never used."""
+    import numpy as np
+    keys = np.nonzero(index.is_key)[0]
+    if len(keys) == 0:
+        return None, {}
+    rng = np.random.default_rng(seed)
+    host = index.native()
+    res = {}
+    best = None
+    for B in (1, 4, 16, 64, 256, 1024):
+        lens = rng.integers(1, 6, size=B)
+        q_ptr = np.zeros(B + 1, np.int64)
+        np.cumsum(lens, out=q_ptr[1:])
+        seeds = keys[rng.integers(0, len(keys), int(q_ptr[-1]))].astype(np.int32)
+        gpu_index.query_batch(q_ptr, seeds, k)  # warm
+        tc, tg = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            host.query_batch(q_ptr, seeds, k)
+            tc.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            gpu_index.query_batch(q_ptr, seeds, k)
+            tg.append(time.perf_counter() - t0)
+        c, g = float(np.median(tc)) * 1e6, float(np.median(tg)) * 1e6
+        res[B] = (round(c, 2), round(g, 2))
+        if best is None and g < c:
+            best = B
+    return best, res
 
 
 class ReloadManager:
@@ -138,6 +176,12 @@ class ReloadManager:
         try:
             best, index, source = read_pickle_dict(self.cfg)
             gpu_index = self._gpu_factory(index) if self._gpu_factory else None
+            gmb, cross = None, None
+            if gpu_index is not None:
+                if self.cfg.serve_backend == "hip":  # forced: every batch on the GPU
+                    gmb = 1
+                else:
+                    gmb, cross = measure_crossover(index, gpu_index)
         except Exception as e:  # keep serving the previous snapshot; retry next tick
             self.failed_reloads += 1
             self.last_error = f"{type(e).__name__}: {e}"
@@ -145,7 +189,11 @@ class ReloadManager:
             return False
         # the marker may have moved while we were reading: re-read, and only commit the value
         # we read BEFORE loading (a later change triggers another reload next tick)
-        snap = ModelSnapshot(best, index, marker, time.time(), index.n_keys, source, gpu_index)
+        snap = ModelSnapshot(best, index, marker, time.time(), index.n_keys, source, gpu_index,
+                             gmb, cross)
+        if gpu_index is not None:
+            logger.info(f"HIP matcher crossover: batches >= {gmb} go to the GPU" if gmb else
+                        "HIP matcher never beats the C++ matcher on this index: CPU only")
         self.snapshot = snap  # single reference assignment = atomic swap
         self.reload_counter += 1
         self.last_error = None

@@ -208,3 +208,44 @@ def test_corrupt_rule_index_falls_back_to_pickle(pvc):
         seed = next(k for k, v in rec.items() if v)
         got = c.post("/api/recommend/", json={"songs": [seed]}).json()["songs"]
         assert got == oracle.recommend_oracle(rec, [seed], 10)
+
+
+class _FakeGpuIndex:
+    """Stands in for _native.GpuRuleIndex (CPU-only tests): answers with the C++ matcher and
+    counts the batches it was given."""
+
+    def __init__(self, index):
+        self.host = index.native()
+        self.calls = 0
+
+    def query_batch(self, q_ptr, seeds, k):
+        self.calls += 1
+        return self.host.query_batch(q_ptr, seeds, k)
+
+
+@pytest.mark.parametrize("backend,expect_gpu", [("auto", False), ("hip", True)])
+def test_router_uses_gpu_only_past_the_measured_crossover(pvc, monkeypatch, backend, expect_gpu):
+    """SERVE_BACKEND=auto sends work to the HIP matcher only when enough requests are in flight
+    to fill a batch at least as large as the crossover measured on the index; one-at-a-time
+    traffic never touches it.  SERVE_BACKEND=hip forces every request through it."""
+    from kubernetes_machine_learning_server_amd.serve import app as app_mod
+    from kubernetes_machine_learning_server_amd.serve import state as state_mod
+    made = []
+
+    def factory(cfg):
+        def build(index):
+            g = _FakeGpuIndex(index)
+            made.append(g)
+            return g
+        return build
+    monkeypatch.setattr(app_mod, "_gpu_factory", factory)
+    monkeypatch.setattr(state_mod, "measure_crossover", lambda index, g: (256, {256: (47.0, 33.0)}))
+    rec = rec_dict(pvc)
+    seeds = [k for k, v in rec.items() if v][:20]
+    with TestClient(create_app(api_settings(pvc, serve_backend=backend))) as c:
+        ready = c.get("/readyz").json()
+        assert ready["gpu_index"] and ready["gpu_min_batch"] == (1 if backend == "hip" else 256)
+        for sd in seeds:
+            got = c.post("/api/recommend/", json={"songs": [sd]}).json()["songs"]
+            assert got == oracle.recommend_oracle(rec, [sd], 10)
+    assert made and (made[-1].calls > 0) == expect_gpu
