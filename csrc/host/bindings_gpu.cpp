@@ -196,6 +196,22 @@ void register_gpu_bindings(py::module_& m) {
       .def("words_local", &gpu::GpuMiner::words_local)
       .def("encode_bitmaps", &gpu::GpuMiner::encode_bitmaps, py::call_guard<py::gil_scoped_release>())
       .def("pair_counts", &gpu::GpuMiner::pair_counts, py::call_guard<py::gil_scoped_release>())
+      .def("rule_map_from_gram",
+           [](gpu::GpuMiner& g, uintptr_t gram, int64_t ld, uint32_t minsup) {
+             gpu::GpuMiner::RuleMap m;
+             {
+               py::gil_scoped_release nogil;
+               m = g.rule_map_from_gram(gram, ld, minsup);
+             }
+             py::dict d;
+             d["nnz"] = m.nnz;
+             d["status"] = m.status;
+             d["row_ptr"] = py::array_t<int64_t>((py::ssize_t)m.row_ptr.size(), m.row_ptr.data());
+             d["cons"] = py::array_t<int32_t>((py::ssize_t)m.cons.size(), m.cons.data());
+             d["count"] = py::array_t<uint32_t>((py::ssize_t)m.cnt.size(), m.cnt.data());
+             return d;
+           },
+           py::arg("gram"), py::arg("ld"), py::arg("minsup"))
       .def("bitgemm_rect", &gpu::GpuMiner::bitgemm_rect, py::call_guard<py::gil_scoped_release>())
       .def("mine_bitmaps", [](gpu::GpuMiner& g, uintptr_t bm, int64_t Wp, double ms, int max_len,
                               bool pairs_only, py::object owned, bool emit_level1, bool download,

@@ -761,6 +761,7 @@ GpuMiner::~GpuMiner() {
   if (d_tx_ptr_) (void)hipFree(d_tx_ptr_);
   if (d_items_) (void)hipFree(d_items_);
   if (d_rank_of_) (void)hipFree(d_rank_of_);
+  if (d_fmask_) (void)hipFree(d_fmask_);
   if (d_ids_) (void)hipFree(d_ids_);
   if (d_own_bm_) (void)hipFree(d_own_bm_);
   if (h_scalar_) (void)hipHostFree(h_scalar_);
@@ -913,6 +914,15 @@ int64_t GpuMiner::select(const uint32_t* global_counts, int64_t global_n_tx, dou
   fi_ = select_frequent(global_counts, n_items_, (uint64_t)global_n_tx, min_support);
   if (d_rank_of_) KMLS_HIP(hipFree(d_rank_of_));
   if (d_ids_) KMLS_HIP(hipFree(d_ids_));
+  if (d_fmask_) KMLS_HIP(hipFree(d_fmask_));
+  d_fmask_ = nullptr;
+  if (n_items_ >= (1 << 16)) {  // frequent-item bit mask for the encode gather (kernels.hpp)
+    std::vector<uint32_t> mask((size_t)(n_items_ + 31) / 32, 0u);
+    for (int32_t id : fi_.ids) mask[(size_t)id >> 5] |= 1u << (id & 31);
+    KMLS_HIP(hipMalloc((void**)&d_fmask_, mask.size() * sizeof(uint32_t)));
+    KMLS_HIP(hipMemcpyAsync(d_fmask_, mask.data(), mask.size() * sizeof(uint32_t),
+                            hipMemcpyHostToDevice, s));
+  }
   KMLS_HIP(hipMalloc((void**)&d_rank_of_, (size_t)std::max<int64_t>(n_items_, 1) * sizeof(int32_t)));
   KMLS_HIP(hipMalloc((void**)&d_ids_, std::max<size_t>(fi_.ids.size(), 1) * sizeof(int32_t)));
   KMLS_HIP(hipMemcpyAsync(d_rank_of_, fi_.rank_of.data(), (size_t)n_items_ * sizeof(int32_t),
@@ -935,12 +945,31 @@ void GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_o
   const char* te = std::getenv("KMLS_ENCODE_TILED");
   const bool tiled = !(te && te[0] == '0');
   const int64_t F = (int64_t)fi_.ids.size();
+  const char* me = std::getenv("KMLS_ENCODE_MASK");  // =0: no frequent-item mask (A/B)
+  const uint32_t* fmask = (me && me[0] == '0') ? nullptr : d_fmask_;
   if (tiled && n_tx_ >= (1 << 16) &&
       kern::encode_bitmap_tiled(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev,
-                                Wp_total, word_off, F, (hipStream_t)stream_))
+                                Wp_total, word_off, F, (hipStream_t)stream_, fmask))
     return;
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev, Wp_total,
-                      word_off, (hipStream_t)stream_);
+                      word_off, (hipStream_t)stream_, fmask);
+}
+
+// Encode into a bitmap buffer with stale contents.  The LDS-slab encode writes every word of
+// the transaction columns (zeros included), so only the row padding past ceil(n_tx/64) words is
+// cleared — at 100M transactions a full memset was a 9 GB write ahead of a 9 GB encode.
+void GpuMiner::encode_bitmaps_fresh(uint64_t* bm, int64_t F, int64_t Wp) {
+  hipStream_t s = (hipStream_t)stream_;
+  const char* te = std::getenv("KMLS_ENCODE_TILED");
+  const bool tiled = !(te && te[0] == '0') && n_tx_ >= (1 << 16) && F > 0 &&
+                     F <= kern::kEncodeTileMaxF;
+  const int64_t used = (n_tx_ + 63) / 64;
+  if (!tiled) {
+    KMLS_HIP(hipMemsetAsync(bm, 0, (size_t)std::max<int64_t>(F, 1) * Wp * 8, s));
+  } else if (Wp > used) {
+    KMLS_HIP(hipMemset2DAsync(bm + used, (size_t)Wp * 8, 0, (size_t)(Wp - used) * 8, (size_t)F, s));
+  }
+  encode_bitmaps((uintptr_t)bm, Wp, 0);
 }
 
 void GpuMiner::pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev, bool use_mfma) {
@@ -952,6 +981,80 @@ void GpuMiner::pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev
     kern::pair_gram_mfma_i8((const uint64_t*)bm_dev, Wp_total, F, (uint32_t*)out_dev, s);
   else
     kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp_total, F, (uint32_t*)out_dev, s);
+}
+
+GpuMiner::RuleMap GpuMiner::rule_map_from_gram(uintptr_t gram_dev, int64_t ld, uint32_t minsup) {
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  const int64_t F = (int64_t)fi_.ids.size();
+  KMLS_CHECK(F > 0 && ld >= F, "rule_map_from_gram: select() first, ld >= F");
+  if (!big_lds_) {
+    kern::pairs_enable_big_lds();
+    big_lds_ = true;
+  }
+  // exact entry count first (2 x the frequent pairs), so one pass fills buffers of that size
+  const int64_t I = n_items_;
+  std::vector<void*> bufs;
+  auto dalloc = [&](size_t b) {
+    void* p = nullptr;
+    KMLS_HIP(hipMalloc(&p, std::max<size_t>(b, 256)));
+    bufs.push_back(p);
+    return p;
+  };
+  RuleMap out;
+  try {
+    int64_t cap = std::max<int64_t>(F, 1024);
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      for (void* p : bufs) (void)hipFree(p);
+      bufs.clear();
+      kern::PairsArgs pa{};
+      pa.gram = (const uint32_t*)gram_dev;
+      pa.ld = ld;
+      pa.dF = nullptr;
+      pa.F_host = F;
+      pa.F_max = F;
+      pa.minsup = minsup;
+      pa.ids = d_ids_;
+      pa.rank_of = d_rank_of_;
+      pa.n_items = I;
+      pa.tie = d_tie_;
+      pa.inv_tie = d_inv_tie_;
+      pa.scratch_bytes = kern::pairs_scratch_bytes(F, I);
+      pa.scratch = dalloc(pa.scratch_bytes);
+      pa.row_ptr = (int64_t*)dalloc((size_t)(I + 1) * 8);
+      pa.ent = (unsigned long long*)dalloc((size_t)cap * 8);
+      pa.ent_cap = cap;
+      pa.cons = (int32_t*)dalloc((size_t)cap * 4);
+      pa.cnt = (uint32_t*)dalloc((size_t)cap * 4);
+      pa.host = nullptr;
+      kern::pairs_to_csr(pa, s);
+      out.row_ptr.resize((size_t)I + 1);
+      KMLS_HIP(hipMemcpyAsync(out.row_ptr.data(), pa.row_ptr, (size_t)(I + 1) * 8,
+                              hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(&out.status, pa.scratch, 4, hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipStreamSynchronize(s));
+      out.nnz = out.row_ptr[(size_t)I];
+      if (out.nnz > cap && (out.status & 1u)) {  // sized from the exact total, retry once
+        cap = out.nnz;
+        continue;
+      }
+      out.cons.resize((size_t)out.nnz);
+      out.cnt.resize((size_t)out.nnz);
+      if (out.nnz) {
+        KMLS_HIP(hipMemcpyAsync(out.cons.data(), pa.cons, (size_t)out.nnz * 4,
+                                hipMemcpyDeviceToHost, s));
+        KMLS_HIP(hipMemcpyAsync(out.cnt.data(), pa.cnt, (size_t)out.nnz * 4,
+                                hipMemcpyDeviceToHost, s));
+      }
+      KMLS_HIP(hipStreamSynchronize(s));
+      break;
+    }
+  } catch (...) {
+    for (void* p : bufs) (void)hipFree(p);
+    throw;
+  }
+  for (void* p : bufs) (void)hipFree(p);
+  return out;
 }
 
 void GpuMiner::bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp,
@@ -1623,8 +1726,7 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download, bool prefetch
     KMLS_HIP(hipMalloc((void**)&d_own_bm_, need));
     own_bm_bytes_ = need;
   }
-  KMLS_HIP(hipMemsetAsync(d_own_bm_, 0, need, s));
-  encode_bitmaps((uintptr_t)d_own_bm_, Wp, 0);
+  encode_bitmaps_fresh(d_own_bm_, F, Wp);
   KMLS_HIP(hipEventRecord(e2.e, s));
   GpuMineResult r;
   for (int attempt = 0;; ++attempt) {
@@ -1704,8 +1806,7 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
     KMLS_HIP(hipMalloc((void**)&d_own_bm_, need));
     own_bm_bytes_ = need;
   }
-  KMLS_HIP(hipMemsetAsync(d_own_bm_, 0, need, s));
-  encode_bitmaps((uintptr_t)d_own_bm_, Wp, 0);
+  encode_bitmaps_fresh(d_own_bm_, F, Wp);
   KMLS_HIP(hipEventRecord(e2.e, s));
   // 4. level loop with all-reduced candidate counts
   comm_ = comm;

@@ -151,6 +151,7 @@ class GpuMiner {
   // (uint64[F][Wp]) at word offset `word_off` of rows of stride `Wp_total` words.
   int64_t words_local() const;  // padded words for the local shard
   void encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_off);
+  void encode_bitmaps_fresh(uint64_t* bm, int64_t F, int64_t Wp);  // stale buffer ok
   // Phase D: full mining over replicated bitmaps (uint64[F][Wp_total]) covering `n_tx_total`.
   //   owned_mask: optional uint8[F] (top-level classes to expand; level-1 nodes always emitted
   //   by rank 0 only when emit_level1).
@@ -181,6 +182,18 @@ class GpuMiner {
   // count[F][F] (row-major, only i<j valid) via the bit-GEMM kernels. Used by the rule-map
   // fast path and by the multi-GPU pair all-reduce.
   void pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev, bool use_mfma);
+  // Rule map (O10 pairs_to_csr) from a pair-count matrix already on the device (upper triangle,
+  // rank order of the last select(), row stride ld): CSR by item id, rows by (count desc, tie
+  // key asc).  For callers that own the gram (the large-shape pairs pipeline); the resident
+  // mining call builds the same map inside its own launch sequence (MineConfig::rule_index).
+  struct RuleMap {
+    int64_t nnz = 0;
+    unsigned status = 0;  // 1 entry overflow, 2 row longer than the device sort
+    std::vector<int64_t> row_ptr;
+    std::vector<int32_t> cons;
+    std::vector<uint32_t> cnt;
+  };
+  RuleMap rule_map_from_gram(uintptr_t gram_dev, int64_t ld, uint32_t minsup);
   // C[Fa][ldc] += popcount(A_i & B_j) over Wp words (ring-pass pair counting)
   void bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp, uintptr_t C,
                     int64_t ldc);
@@ -205,6 +218,7 @@ class GpuMiner {
   FrequentItems fi_;
   int64_t global_n_tx_ = 0;
   int32_t* d_rank_of_ = nullptr;
+  uint32_t* d_fmask_ = nullptr;  // frequent-item bit mask (large vocabularies, select())
   int32_t* d_ids_ = nullptr;
   uint64_t* d_own_bm_ = nullptr;  // single-GPU bitmap buffer
   size_t own_bm_bytes_ = 0;

@@ -19,13 +19,16 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
                               void* scratch, size_t scratch_bytes, hipStream_t s);
 void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                    const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
-                   hipStream_t s);
-// LDS-slab encode for long shards with F <= kEncodeTileMaxF frequent rows: writes EVERY word of
+                   hipStream_t s, const uint32_t* fmask = nullptr);
+// fmask (optional): bit i set iff item i is frequent; tested before the rank_of gather, so the
+// (mostly infrequent) items of a million-item vocabulary read a 128 KB L2-resident mask instead
+// of a 4 MB table.
+// LDS-slab encode for long shards (F <= kEncodeTileMaxF frequent rows, in row bands): writes EVERY word of
 // the word columns it covers (zeros included); false (nothing launched) if not applicable
-constexpr int64_t kEncodeTileMaxF = 6144;
+constexpr int64_t kEncodeTileMaxF = 1 << 20;  // row bands past one LDS slab
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
-                         int64_t F, hipStream_t s);
+                         int64_t F, hipStream_t s, const uint32_t* fmask = nullptr);
 // dst[i] += src[i]
 void add_u32(uint32_t* dst, const uint32_t* src, int64_t n, hipStream_t s);
 // exclusive prefix sum over int64[n+1] (in[n] == 0) into out[n+1] (out[n] = total)

@@ -744,6 +744,9 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
         // (the latency of the small ones)
         constexpr int kB = KB;
         uint32_t kk = 0;
+        // a row that fits one batch stays in registers until its count is known, so only
+        // survivors' rows are written (a multi-batch row streams out unconditionally)
+        const bool one_batch = n2 <= kB;
         for (int w0 = 0; w0 < n2; w0 += kB) {
           ulonglong2 u[kB], v[kB];
 #pragma unroll
@@ -755,10 +758,15 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
 #pragma unroll
           for (int q = 0; q < kB; ++q)
             if (w0 + q < n2) {
-              const ulonglong2 r = make_ulonglong2(u[q].x & v[q].x, u[q].y & v[q].y);
-              kk += (uint32_t)__popcll(r.x) + (uint32_t)__popcll(r.y);
-              z[(w0 + q) << 6] = r;
+              u[q] = make_ulonglong2(u[q].x & v[q].x, u[q].y & v[q].y);
+              kk += (uint32_t)__popcll(u[q].x) + (uint32_t)__popcll(u[q].y);
             }
+          const bool keep = !one_batch || A.gram || kk >= A.minsup;
+          if (keep) {
+#pragma unroll
+            for (int q = 0; q < kB; ++q)
+              if (w0 + q < n2) z[(w0 + q) << 6] = u[q];
+          }
         }
         if (!A.gram) k = kk;
       }
@@ -1152,7 +1160,12 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
       const char* e = std::getenv("KMLS_KB18");
       return !(e && e[0] == '0');
     }();
-    if (kb18 && cand_hint >= 0 && cand_hint <= 64 * kTile && n2 <= 18)
+    // KMLS_KB18_TILES: A/B knob for the size bound of the one-batch variant (default 64 tiles)
+    static const int64_t kb18_tiles = [] {
+      const char* e = std::getenv("KMLS_KB18_TILES");
+      return e ? std::atoll(e) : (int64_t)64;
+    }();
+    if (kb18 && cand_hint >= 0 && cand_hint <= kb18_tiles * kTile && n2 <= 18)
       hipLaunchKernelGGL(k_level_count_small<18>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl,
                          status, epoch, a, tile_row);
     else

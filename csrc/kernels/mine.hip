@@ -258,7 +258,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restr
                                                           int64_t n_tx,
                                                           const int32_t* __restrict__ rank_of,
                                                           unsigned long long* __restrict__ bm,
-                                                          int64_t Wp, int64_t word_off) {
+                                                          int64_t Wp, int64_t word_off,
+                                                          const uint32_t* __restrict__ fmask) {
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < n_tx; t += nwaves) {
@@ -266,7 +267,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restr
     const int64_t w = word_off + (t >> 6);
     const int64_t p1 = tx_ptr[t + 1];
     for (int64_t p = tx_ptr[t] + lane; p < p1; p += 64) {
-      const int32_t r = rank_of[items[p]];
+      const int32_t it = items[p];
+      if (fmask && !((fmask[it >> 5] >> (it & 31)) & 1u)) continue;
+      const int32_t r = rank_of[it];
       if (r >= 0) atomicOr(&bm[(int64_t)r * Wp + w], bit);
     }
   }
@@ -278,7 +281,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restr
 // one fabric atomic per (transaction, frequent item) with 64 waves contending for each word
 // column; here the only global traffic is the CSR read and one coalesced write of every word.
 // Items are taken kEncodeU per thread per round (loads issued together), each item's
-// transaction found by binary search over the tile's LDS copy of tx_ptr.
+// transaction found by binary search over the tile's LDS copy of tx_ptr.  More frequent rows than
+// one slab holds (config 5: ~15k) split into row bands, one block per (tile, band) with the band
+// index fastest, so a tile's bands run together and re-read its items from L2, not HBM.
 constexpr int kEncodeU = 8;
 __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restrict__ tx_ptr,
                                                         const int32_t* __restrict__ items,
@@ -286,14 +291,19 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
                                                         const int32_t* __restrict__ rank_of,
                                                         unsigned long long* __restrict__ bm,
                                                         int64_t Wp, int64_t word_off, int64_t F,
-                                                        int tw_log2) {
-  extern __shared__ unsigned long long s_bm[];  // [F][TW], then tx_ptr[64*TW + 1]
+                                                        int tw_log2, int band_rows,
+                                                        const uint32_t* __restrict__ fmask) {
+  extern __shared__ unsigned long long s_bm[];  // [band rows][TW], then tx_ptr[64*TW + 1]
   const int TW = 1 << tw_log2;
   const int64_t tile_tx = 64ll << tw_log2;
-  const int64_t t0 = (int64_t)blockIdx.x * tile_tx;
+  const int64_t n_bands = (F + band_rows - 1) / band_rows;
+  const int64_t tile = (int64_t)blockIdx.x / n_bands;
+  const int32_t r0 = (int32_t)(((int64_t)blockIdx.x - tile * n_bands) * band_rows);
+  const int32_t nr = (int32_t)min((int64_t)band_rows, F - r0);
+  const int64_t t0 = tile * tile_tx;
   const int nt = (int)min(tile_tx, n_tx - t0);
-  int64_t* s_ptr = (int64_t*)(s_bm + F * TW);
-  for (int64_t i = threadIdx.x; i < F * TW; i += blockDim.x) s_bm[i] = 0ull;
+  int64_t* s_ptr = (int64_t*)(s_bm + (int64_t)band_rows * TW);
+  for (int64_t i = threadIdx.x; i < (int64_t)nr * TW; i += blockDim.x) s_bm[i] = 0ull;
   for (int i = threadIdx.x; i <= nt; i += blockDim.x) s_ptr[i] = tx_ptr[t0 + i];
   __syncthreads();
   const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
@@ -306,10 +316,13 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
     }
     int32_t rk[kEncodeU];
 #pragma unroll
-    for (int u = 0; u < kEncodeU; ++u) rk[u] = it[u] >= 0 ? rank_of[it[u]] : -1;
+    for (int u = 0; u < kEncodeU; ++u)
+      if (fmask && it[u] >= 0 && !((fmask[it[u] >> 5] >> (it[u] & 31)) & 1u)) it[u] = -1;
+#pragma unroll
+    for (int u = 0; u < kEncodeU; ++u) rk[u] = it[u] >= 0 ? rank_of[it[u]] - r0 : -1;
 #pragma unroll
     for (int u = 0; u < kEncodeU; ++u) {
-      if (rk[u] < 0) continue;
+      if (rk[u] < 0 || rk[u] >= nr) continue;
       const int64_t p = pb + (int64_t)u * blockDim.x + threadIdx.x;
       int lo = 0, hi = nt;  // largest lt with s_ptr[lt] <= p
       while (hi - lo > 1) {
@@ -323,9 +336,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
   // only this shard's words (ceil(n_tx/64) of them): a neighbouring shard may own the next ones
   const int64_t wbase = word_off + (t0 >> 6);
   const int64_t wn = min((int64_t)TW, min(Wp - wbase, ((n_tx + 63) >> 6) - (t0 >> 6)));
-  for (int64_t i = threadIdx.x; i < F * TW; i += blockDim.x) {
+  for (int64_t i = threadIdx.x; i < (int64_t)nr * TW; i += blockDim.x) {
     const int64_t row = i >> tw_log2, w = i & (TW - 1);
-    if (w < wn) bm[row * Wp + wbase + w] = s_bm[i];
+    if (w < wn) bm[(r0 + row) * Wp + wbase + w] = s_bm[i];
   }
 }
 
@@ -605,28 +618,32 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
 
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
-                         int64_t F, hipStream_t s) {
+                         int64_t F, hipStream_t s, const uint32_t* fmask) {
   if (n_tx <= 0 || F <= 0 || F > kEncodeTileMaxF) return false;
-  // words per tile: the F x TW slab within 48 KB of LDS (3 blocks per CU), TW <= 8
-  int tw_log2 = 3;
-  while (tw_log2 > 0 && F * (8ll << tw_log2) > 48 * 1024) --tw_log2;
+  // words per tile: the slab within 48 KB of LDS (3 blocks per CU).  One band of F rows at
+  // TW = 8 or 4 words (64/32-byte row segments); past 1536 rows, bands of 1536 rows at TW = 4
+  // (narrower segments would make the write-out scattered 8-byte stores).
+  constexpr int64_t kSlab = 48 * 1024;
+  int tw_log2 = F * 64 <= kSlab ? 3 : 2;
   const int64_t TW = 1ll << tw_log2;
-  const size_t lds = (size_t)F * TW * 8 + (size_t)(64 * TW + 1) * 8;
-  if (lds > 64 * 1024) return false;
-  const int64_t blocks = (n_tx + 64 * TW - 1) / (64 * TW);
+  const int64_t band = std::min<int64_t>(F, kSlab / (8 * TW));
+  const int64_t n_bands = (F + band - 1) / band;
+  const size_t lds = (size_t)band * TW * 8 + (size_t)(64 * TW + 1) * 8;
+  const int64_t blocks = (n_tx + 64 * TW - 1) / (64 * TW) * n_bands;
   if (blocks > INT32_MAX) return false;
   hipLaunchKernelGGL(k_encode_tile, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr, items,
-                     n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2);
+                     n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2, (int)band,
+                     fmask);
   KMLS_HIP(hipGetLastError());
   return true;
 }
 
 void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                    const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
-                   hipStream_t s) {
+                   hipStream_t s, const uint32_t* fmask) {
   if (n_tx <= 0) return;
   hipLaunchKernelGGL(k_encode_bitmap, dim3(grid_for(n_tx, kBlock / 64, 8192)), dim3(kBlock), 0, s,
-                     tx_ptr, items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off);
+                     tx_ptr, items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, fmask);
   KMLS_HIP(hipGetLastError());
 }
 

@@ -406,6 +406,33 @@ def test_rule_index_on_device(gpu_mod, shape, ms, max_len, tie):
         assert_same_itemsets(gpu_mod, r, c)
 
 
+@pytest.mark.parametrize("shape,ms,n_tx,mfma", [("ds1", 0.05, None, True),
+                                                ("ds2_weak", 0.02, 70000, False)])
+def test_rule_map_from_gram(gpu_mod, shape, ms, n_tx, mfma):
+    """The standalone device rule map (large-shape pipeline: caller-owned gram, banded encode
+    into a stale buffer) == the CPU-built index; a too-small first capacity guess is redone at
+    the exact size."""
+    import torch
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    tx = generate(shape, seed=6, n_tx=n_tx)
+    g = gpu_mod.GpuMiner(0, 1 << 28, torch.cuda.current_stream().cuda_stream or 0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    counts = np.bincount(tx.items, minlength=tx.n_items).astype(np.uint32)
+    F = g.select(counts, tx.n_tx, ms)
+    ids, fc, minsup = g.frequent()
+    Wp = g.words_local()
+    bm = torch.zeros((F, Wp), dtype=torch.int64, device="cuda")
+    gram = torch.empty((F, F), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    g.encode_bitmaps(bm.data_ptr(), Wp, 0)
+    g.pair_counts(bm.data_ptr(), Wp, gram.data_ptr(), mfma)
+    rm = g.rule_map_from_gram(gram.data_ptr(), F, int(minsup))
+    assert rm["status"] == 0
+    ref = _cpu_index(gpu_mod, tx, ms, None)
+    _assert_index_equal(rm, ref, tx.n_tx)
+    assert rm["nnz"] == ref.nnz
+
+
 def test_rule_index_regrow_and_prefetch(gpu_mod, monkeypatch):
     """A too-small entry capacity regrows and redoes the call; launch-ahead calls adopt their
     own pinned CSR buffers (graph replay)."""
@@ -458,22 +485,29 @@ def test_extend_split_k_long_rows(gpu_mod, monkeypatch, split):
     assert_same_itemsets(gpu_mod, r, c)
 
 
-def test_encode_tiled_long_shard(gpu_mod):
+@pytest.mark.parametrize("T,I,ms,min_f", [(300_000 + 37, 60_000, 0.002, 0),
+                                            (200_000 + 37, 100_000, 0.0005, 3000)])
+def test_encode_tiled_long_shard(gpu_mod, T, I, ms, min_f):
     """The LDS-slab encode produces the same tid-bitmaps as the host encoder, on a long shard
-    with an odd tail tile."""
+    with an odd tail tile; the second case has a million-style vocabulary (frequent-item mask
+    in front of the rank gather) and more frequent rows than one LDS slab (row bands).  The
+    buffer starts as all ones: the tiled encode must write every word of the shard's columns
+    (the tx-DP path no longer clears the bitmap first)."""
     import torch
-    T, I = 300_000 + 37, 60_000
     ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 9)
     g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(ptr, items, I)
     counts = np.bincount(items, minlength=I).astype(np.uint32)
-    F = g.select(counts, T, 0.002)
+    F = g.select(counts, T, ms)
+    assert F >= min_f, F
     ids, fc, minsup = g.frequent()
     Wp = g.words_local()
-    bm = torch.zeros((F, Wp), dtype=torch.int64, device="cuda")
+    used = (T + 63) // 64
+    bm = torch.full((F, Wp), -1, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
     g.encode_bitmaps(bm.data_ptr(), Wp, 0)
     g.synchronize()
-    sel = gpu_mod.select_frequent(counts, T, 0.002)
+    sel = gpu_mod.select_frequent(counts, T, ms)
     ref = gpu_mod.encode_bitmaps_cpu(ptr, items, sel[2], F, Wp)
-    np.testing.assert_array_equal(bm.cpu().numpy().view(np.uint64), ref.reshape(F, Wp))
+    np.testing.assert_array_equal(bm.cpu().numpy().view(np.uint64)[:, :used],
+                                  ref.reshape(F, Wp)[:, :used])
