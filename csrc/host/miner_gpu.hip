@@ -939,7 +939,7 @@ int64_t GpuMiner::words_local() const {
   return (w + 3) & ~(int64_t)3;  // 32-byte rows: 16-B team loads and the MFMA 4-word stride
 }
 
-void GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_off) {
+bool GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_off) {
   KMLS_HIP(hipSetDevice(device_));
   // long shards: LDS-slab encode (KMLS_ENCODE_TILED=0 keeps the atomic kernel, for A/B)
   const char* te = std::getenv("KMLS_ENCODE_TILED");
@@ -949,10 +949,11 @@ void GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_o
   const uint32_t* fmask = (me && me[0] == '0') ? nullptr : d_fmask_;
   if (tiled && n_tx_ >= (1 << 16) &&
       kern::encode_bitmap_tiled(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev,
-                                Wp_total, word_off, F, (hipStream_t)stream_, fmask))
-    return;
+                                Wp_total, word_off, F, (hipStream_t)stream_, fmask, d_ids_))
+    return true;
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev, Wp_total,
                       word_off, (hipStream_t)stream_, fmask);
+  return false;
 }
 
 // Encode into a bitmap buffer with stale contents.  The LDS-slab encode writes every word of
@@ -969,7 +970,10 @@ void GpuMiner::encode_bitmaps_fresh(uint64_t* bm, int64_t F, int64_t Wp) {
   } else if (Wp > used) {
     KMLS_HIP(hipMemset2DAsync(bm + used, (size_t)Wp * 8, 0, (size_t)(Wp - used) * 8, (size_t)F, s));
   }
-  encode_bitmaps((uintptr_t)bm, Wp, 0);
+  if (!encode_bitmaps((uintptr_t)bm, Wp, 0) && tiled) {  // the tiled kernel declined: clear, redo
+    KMLS_HIP(hipMemsetAsync(bm, 0, (size_t)std::max<int64_t>(F, 1) * Wp * 8, s));
+    encode_bitmaps((uintptr_t)bm, Wp, 0);
+  }
 }
 
 void GpuMiner::pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev, bool use_mfma) {

@@ -150,7 +150,7 @@ class GpuMiner {
   // Phase C: tid-bitmaps of frequent items for the resident shard, into an external buffer
   // (uint64[F][Wp]) at word offset `word_off` of rows of stride `Wp_total` words.
   int64_t words_local() const;  // padded words for the local shard
-  void encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_off);
+  bool encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_off);  // true: tiled
   void encode_bitmaps_fresh(uint64_t* bm, int64_t F, int64_t Wp);  // stale buffer ok
   // Phase D: full mining over replicated bitmaps (uint64[F][Wp_total]) covering `n_tx_total`.
   //   owned_mask: optional uint8[F] (top-level classes to expand; level-1 nodes always emitted
@@ -295,6 +295,10 @@ class GpuRuleIndex {
   int32_t* d_cons_ = nullptr;
   uint32_t* d_score_ = nullptr;  // dense rank of the score (exact order key), see serve.hip
   uint8_t* d_is_key_ = nullptr;
+  int32_t* d_id_cons_ = nullptr;  // per row: consequents sorted by id (long-merge kernel)
+  int32_t* d_id_pos_ = nullptr;   // ... and their index in the score-ordered row
+  std::vector<int64_t> h_row_ptr_;  // host copies: per-query merge size decides the kernel
+  std::vector<uint8_t> h_is_key_;
   // mapped pinned staging (queries in, results out; grown on demand)
   int32_t* h_pinned_ = nullptr;
   int64_t cap_pinned_ = 0;

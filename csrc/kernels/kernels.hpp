@@ -28,7 +28,8 @@ void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
 constexpr int64_t kEncodeTileMaxF = 1 << 20;  // row bands past one LDS slab
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
-                         int64_t F, hipStream_t s, const uint32_t* fmask = nullptr);
+                         int64_t F, hipStream_t s, const uint32_t* fmask = nullptr,
+                         const int32_t* ids = nullptr);  // ids: rank -> id (LDS-hash lookup)
 // dst[i] += src[i]
 void add_u32(uint32_t* dst, const uint32_t* src, int64_t n, hipStream_t s);
 // exclusive prefix sum over int64[n+1] (in[n] == 0) into out[n+1] (out[n] = total)
@@ -315,6 +316,15 @@ int64_t groupby_csr(const int32_t* d_keys, const int32_t* d_vals, int64_t n, int
 void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,
                       const uint8_t* is_key, int64_t n_items, const int64_t* q_ptr,
                       const int32_t* seeds, int64_t B, int k, int32_t* out, hipStream_t s);
+// long-row queries (qlist: indices into the batch, each with <= 256 seeds): one workgroup
+// each, threshold-pruned exact merge; id_cons/id_pos = each row's consequents sorted by id and
+// their index in the score-ordered row
+void serve_topk_big(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,
+                    const uint8_t* is_key, int64_t n_items, const int32_t* id_cons,
+                    const int32_t* id_pos, const int64_t* q_ptr, const int32_t* seeds,
+                    const int32_t* qlist, int64_t nq, int k, int32_t* out, hipStream_t s);
+constexpr int kServeWaveMerge = 512;  // merged entries the wave kernel takes (its table / 2)
+constexpr int kServeMaxSeeds = 256;
 
 }  // namespace kern
 }  // namespace kmls

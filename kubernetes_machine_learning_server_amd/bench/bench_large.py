@@ -200,8 +200,12 @@ def rule_map_main(args) -> int:
     ptr, items = N.synth_transactions(T, I, shape.mean_len, shape.n_genres, shape.genre_affinity,
                                       0.85, args.seed)
     gen_s = time.perf_counter() - t0
-    stream = torch.cuda.current_stream()
-    g = N.GpuMiner(0, 1 << 30, stream.cuda_stream or 0)
+    # one non-default torch stream shared with the miner: torch fills, the native kernels and the
+    # timing events are all ordered on it (the default stream's handle is 0, which would give the
+    # miner a private stream)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    g = N.GpuMiner(0, 1 << 30, stream.cuda_stream)
     t0 = time.perf_counter()
     g.load_csr(ptr, items, I)
     load_s = time.perf_counter() - t0

@@ -200,7 +200,7 @@ def test_gpu_serve_matches_cpu(gpu_mod):
         ids, n = gidx.query_batch(q_ptr, seeds, k)
         cids, cn = host.query_batch(q_ptr, seeds, k)
         ok = n != -2  # the host answers the overflow queries (MicroBatcher does this)
-        assert (n[~ok] == -2).all() and ok.sum() >= B - 16
+        assert (n[~ok] == -2).all() and ok.sum() >= B - 2
         assert n[9] == -2  # 300 seeds
         np.testing.assert_array_equal(n[ok], cn[ok])
         np.testing.assert_array_equal(ids[ok], cids[ok])
@@ -209,6 +209,59 @@ def test_gpu_serve_matches_cpu(gpu_mod):
         cids, cn = host.query_batch(q_ptr[:B + 1], seeds[:q_ptr[B]], 10)
         np.testing.assert_array_equal(n, cn)
         np.testing.assert_array_equal(ids, cids)
+
+
+def _long_row_index(rng, n_items=3000, n_keys=150, max_row=2500, n_scores=40, sort_rows=True):
+    """Rule index with rows of 100..max_row entries and few distinct scores (many ties, the
+    same consequent at different scores in different rows)."""
+    from kubernetes_machine_learning_server_amd.serve.index import RuleIndexData
+    keys = rng.choice(n_items, n_keys, replace=False)
+    row_ptr = np.zeros(n_items + 1, np.int64)
+    rows = {}
+    for kk in keys:
+        n = int(rng.integers(100, max_row))
+        cons = rng.choice(np.setdiff1d(np.arange(n_items), [kk]), n, replace=False)
+        sc = rng.integers(1, n_scores + 1, n).astype(np.float64) / 1000.0
+        if sort_rows:
+            o = np.argsort(-sc, kind="stable")
+            cons, sc = cons[o], sc[o]
+        rows[int(kk)] = (cons.astype(np.int32), sc)
+    for i in range(n_items):
+        row_ptr[i + 1] = row_ptr[i] + (len(rows[i][0]) if i in rows else 0)
+    cons = np.concatenate([rows[i][0] for i in sorted(rows)])
+    score = np.concatenate([rows[i][1] for i in sorted(rows)])
+    is_key = np.zeros(n_items, np.uint8)
+    is_key[keys] = 1
+    return RuleIndexData(n_items, row_ptr, cons, score, is_key, None), keys
+
+
+@pytest.mark.parametrize("sort_rows", [True, False])
+def test_gpu_serve_long_rows(gpu_mod, sort_rows):
+    """Long-merge queries (rows of thousands of entries: the HBM-scale indexes) on the
+    workgroup kernel: threshold-pruned merge + first positions completed from earlier rows'
+    suffixes == the C++ matcher, ties included.  Unsorted rows (a reference-format pickle)
+    must not use the pruning: those queries go to the host (-2)."""
+    rng = np.random.default_rng(3)
+    idx, keys = _long_row_index(rng, sort_rows=sort_rows)
+    host = idx.native()
+    gidx = gpu_mod.GpuRuleIndex(0, host)
+    B = 300
+    lens = rng.integers(1, 13, size=B)
+    lens[0], lens[1] = 200, 256  # many long rows in one query
+    q_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    seeds = np.where(rng.random(q_ptr[-1]) < 0.85, rng.choice(keys, q_ptr[-1]),
+                     rng.integers(0, idx.n_items, q_ptr[-1])).astype(np.int32)
+    seeds[q_ptr[2] + 1] = seeds[q_ptr[2]]  # a repeated seed
+    for k in (1, 10, 40):
+        ids, n = gidx.query_batch(q_ptr, seeds, k)
+        cids, cn = host.query_batch(q_ptr, seeds, k)
+        ok = n != -2
+        if sort_rows:
+            assert ok.sum() >= B - 2, (n == -2).sum()
+        else:
+            assert (~ok).sum() >= B // 2  # long merges without pruning: host path
+        np.testing.assert_array_equal(n[ok], cn[ok])
+        np.testing.assert_array_equal(ids[ok], cids[ok])
 
 
 def test_dist_miner_world1(gpu_mod):
@@ -485,15 +538,18 @@ def test_extend_split_k_long_rows(gpu_mod, monkeypatch, split):
     assert_same_itemsets(gpu_mod, r, c)
 
 
+@pytest.mark.parametrize("hash_lookup", ["1", "0"])
 @pytest.mark.parametrize("T,I,ms,min_f", [(300_000 + 37, 60_000, 0.002, 0),
                                             (200_000 + 37, 100_000, 0.0005, 3000)])
-def test_encode_tiled_long_shard(gpu_mod, T, I, ms, min_f):
+def test_encode_tiled_long_shard(gpu_mod, T, I, ms, min_f, hash_lookup, monkeypatch):
     """The LDS-slab encode produces the same tid-bitmaps as the host encoder, on a long shard
     with an odd tail tile; the second case has a million-style vocabulary (frequent-item mask
     in front of the rank gather) and more frequent rows than one LDS slab (row bands).  The
     buffer starts as all ones: the tiled encode must write every word of the shard's columns
-    (the tx-DP path no longer clears the bitmap first)."""
+    (the tx-DP path no longer clears the bitmap first).  Both frequent-item lookups: the LDS
+    hash of the band's ids, and the bit mask + rank gather."""
     import torch
+    monkeypatch.setenv("KMLS_ENCODE_HASH", hash_lookup)
     ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 9)
     g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(ptr, items, I)
