@@ -949,7 +949,7 @@ bool GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_o
   const uint32_t* fmask = (me && me[0] == '0') ? nullptr : d_fmask_;
   if (tiled && n_tx_ >= (1 << 16) &&
       kern::encode_bitmap_tiled(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev,
-                                Wp_total, word_off, F, (hipStream_t)stream_, fmask, d_ids_))
+                                Wp_total, word_off, F, (hipStream_t)stream_, fmask))
     return true;
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev, Wp_total,
                       word_off, (hipStream_t)stream_, fmask);

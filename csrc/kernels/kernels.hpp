@@ -28,8 +28,7 @@ void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
 constexpr int64_t kEncodeTileMaxF = 1 << 20;  // row bands past one LDS slab
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
-                         int64_t F, hipStream_t s, const uint32_t* fmask = nullptr,
-                         const int32_t* ids = nullptr);  // ids: rank -> id (LDS-hash lookup)
+                         int64_t F, hipStream_t s, const uint32_t* fmask = nullptr);
 // dst[i] += src[i]
 void add_u32(uint32_t* dst, const uint32_t* src, int64_t n, hipStream_t s);
 // exclusive prefix sum over int64[n+1] (in[n] == 0) into out[n+1] (out[n] = total)

@@ -275,34 +275,25 @@ __global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restr
   }
 }
 
-// Tiled encode for long shards (large T): block b owns the 64*TW transactions of word columns
-// [b*TW, b*TW + TW) and builds that (band rows) x TW slab of the bitmap in LDS (ds_or_b64), then
-// writes it out as whole 8*TW-byte row segments.  The atomic kernel above does one fabric atomic
-// per (transaction, frequent item) with 64 waves contending for each word column; here the only
-// global traffic is the CSR read and one coalesced write of every word.
-//   * frequent-item lookup: kHash — the band's frequent ids in an LDS open-addressing table
-//     (id -> band row), so an item costs LDS probes instead of two dependent L2/HBM gathers
-//     (a 1M-vocabulary rank_of table does not stay in L2); else the frequent-id bit mask
-//     (128 KB, L2-resident) in front of the rank_of gather;
-//   * items: kEncodeU per thread per round, the next round's loads issued before this round's
-//     lookups (their latency overlaps), each item's transaction found by binary search over the
-//     tile's LDS copy of tx_ptr;
-//   * row bands: more frequent rows than one slab holds (config 5: ~15k) split into bands, one
-//     block per (tile, band) with the band index fastest, so a tile's bands run together and
-//     re-read its items from L2, not HBM.
+// Tiled encode for long shards (large T, F <= kEncodeTileMaxF): block b owns the 64*TW
+// transactions of word columns [b*TW, b*TW + TW) and builds that F x TW slab of the bitmap in LDS
+// (ds_or_b64), then writes it out as whole 8*TW-byte row segments.  The atomic kernel above does
+// one fabric atomic per (transaction, frequent item) with 64 waves contending for each word
+// column; here the only global traffic is the CSR read and one coalesced write of every word.
+// Items are taken kEncodeU per thread per round (loads issued together), each item's
+// transaction found by binary search over the tile's LDS copy of tx_ptr.  More frequent rows than
+// one slab holds (config 5: ~15k) split into row bands, one block per (tile, band) with the band
+// index fastest, so a tile's bands run together and re-read its items from L2, not HBM.
 constexpr int kEncodeU = 8;
-template <bool kHash>
 __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restrict__ tx_ptr,
                                                         const int32_t* __restrict__ items,
                                                         int64_t n_tx,
                                                         const int32_t* __restrict__ rank_of,
-                                                        const int32_t* __restrict__ ids,
                                                         unsigned long long* __restrict__ bm,
                                                         int64_t Wp, int64_t word_off, int64_t F,
-                                                        int tw_log2, int band_rows, int hs_log2,
+                                                        int tw_log2, int band_rows,
                                                         const uint32_t* __restrict__ fmask) {
-  // LDS: [band rows][TW] u64 | tx_ptr[64*TW + 1] i64 | hash keys i32[HS] | hash rows i32[HS]
-  extern __shared__ unsigned long long s_bm[];
+  extern __shared__ unsigned long long s_bm[];  // [band rows][TW], then tx_ptr[64*TW + 1]
   const int TW = 1 << tw_log2;
   const int64_t tile_tx = 64ll << tw_log2;
   const int64_t n_bands = (F + band_rows - 1) / band_rows;
@@ -312,60 +303,23 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
   const int64_t t0 = tile * tile_tx;
   const int nt = (int)min(tile_tx, n_tx - t0);
   int64_t* s_ptr = (int64_t*)(s_bm + (int64_t)band_rows * TW);
-  int32_t* s_hk = (int32_t*)(s_ptr + 64 * TW + 1);
-  const int HS = kHash ? 1 << hs_log2 : 0;
-  int32_t* s_hv = s_hk + HS;
   for (int64_t i = threadIdx.x; i < (int64_t)nr * TW; i += blockDim.x) s_bm[i] = 0ull;
   for (int i = threadIdx.x; i <= nt; i += blockDim.x) s_ptr[i] = tx_ptr[t0 + i];
-  if constexpr (kHash) {
-    for (int i = threadIdx.x; i < HS; i += blockDim.x) s_hk[i] = -1;
-    __syncthreads();
-    for (int r = threadIdx.x; r < nr; r += blockDim.x) {
-      const int32_t id = ids[r0 + r];
-      uint32_t h = ((uint32_t)id * 2654435761u) >> (32 - hs_log2);
-      while (atomicCAS(&s_hk[h], -1, id) != -1) h = (h + 1) & (HS - 1);
-      s_hv[h] = r;
-    }
-  }
   __syncthreads();
   const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
-  const int64_t step = (int64_t)blockDim.x * kEncodeU;
-  int32_t nx[kEncodeU];
-#pragma unroll
-  for (int u = 0; u < kEncodeU; ++u) {
-    const int64_t p = p0 + (int64_t)u * blockDim.x + threadIdx.x;
-    nx[u] = p < p1 ? items[p] : -1;
-  }
-  for (int64_t pb = p0; pb < p1; pb += step) {
+  for (int64_t pb = p0; pb < p1; pb += (int64_t)blockDim.x * kEncodeU) {
     int32_t it[kEncodeU];
 #pragma unroll
     for (int u = 0; u < kEncodeU; ++u) {
-      it[u] = nx[u];
-      const int64_t p = pb + step + (int64_t)u * blockDim.x + threadIdx.x;
-      nx[u] = p < p1 ? items[p] : -1;
+      const int64_t p = pb + (int64_t)u * blockDim.x + threadIdx.x;
+      it[u] = p < p1 ? items[p] : -1;
     }
     int32_t rk[kEncodeU];
-    if constexpr (kHash) {
 #pragma unroll
-      for (int u = 0; u < kEncodeU; ++u) {
-        rk[u] = -1;
-        if (it[u] < 0) continue;
-        uint32_t h = ((uint32_t)it[u] * 2654435761u) >> (32 - hs_log2);
-        for (int32_t k = s_hk[h]; k != -1; k = s_hk[h]) {
-          if (k == it[u]) {
-            rk[u] = s_hv[h];
-            break;
-          }
-          h = (h + 1) & (HS - 1);
-        }
-      }
-    } else {
+    for (int u = 0; u < kEncodeU; ++u)
+      if (fmask && it[u] >= 0 && !((fmask[it[u] >> 5] >> (it[u] & 31)) & 1u)) it[u] = -1;
 #pragma unroll
-      for (int u = 0; u < kEncodeU; ++u)
-        if (fmask && it[u] >= 0 && !((fmask[it[u] >> 5] >> (it[u] & 31)) & 1u)) it[u] = -1;
-#pragma unroll
-      for (int u = 0; u < kEncodeU; ++u) rk[u] = it[u] >= 0 ? rank_of[it[u]] - r0 : -1;
-    }
+    for (int u = 0; u < kEncodeU; ++u) rk[u] = it[u] >= 0 ? rank_of[it[u]] - r0 : -1;
 #pragma unroll
     for (int u = 0; u < kEncodeU; ++u) {
       if (rk[u] < 0 || rk[u] >= nr) continue;
@@ -664,45 +618,22 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
 
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
-                         int64_t F, hipStream_t s, const uint32_t* fmask, const int32_t* ids) {
+                         int64_t F, hipStream_t s, const uint32_t* fmask) {
   if (n_tx <= 0 || F <= 0 || F > kEncodeTileMaxF) return false;
-  // Slab within ~48 KB of LDS (3 blocks per CU).  Without the hash: one band of F rows at TW = 8
-  // or 4 words (64/32-byte row segments); past 1536 rows, bands of 1536 rows at TW = 4
-  // (narrower segments would make the write-out scattered 8-byte stores).  With the hash (ids
-  // given): TW = 8 and bands of <= 512 rows, leaving room for the table (2x the band, pow2).
-  // KMLS_ENCODE_TW / KMLS_ENCODE_BAND / KMLS_ENCODE_HASH=0: A/B knobs.
-  auto env_int = [](const char* n, int64_t d) {
-    const char* e = std::getenv(n);
-    return e ? std::atoll(e) : d;
-  };
-  const bool hash = ids && env_int("KMLS_ENCODE_HASH", 1) != 0;
+  // words per tile: the slab within 48 KB of LDS (3 blocks per CU).  One band of F rows at
+  // TW = 8 or 4 words (64/32-byte row segments); past 1536 rows, bands of 1536 rows at TW = 4
+  // (narrower segments would make the write-out scattered 8-byte stores).
   constexpr int64_t kSlab = 48 * 1024;
-  int tw_log2, hs_log2 = 0;
-  int64_t band;
-  if (hash) {
-    tw_log2 = (int)env_int("KMLS_ENCODE_TW", 3);
-    band = std::min<int64_t>(F, env_int("KMLS_ENCODE_BAND", 512));
-    hs_log2 = 1;
-    while ((1ll << hs_log2) < 2 * band) ++hs_log2;
-  } else {
-    tw_log2 = F * 64 <= kSlab ? 3 : 2;
-    band = std::min<int64_t>(F, kSlab / (8ll << tw_log2));
-  }
+  int tw_log2 = F * 64 <= kSlab ? 3 : 2;
   const int64_t TW = 1ll << tw_log2;
+  const int64_t band = std::min<int64_t>(F, kSlab / (8 * TW));
   const int64_t n_bands = (F + band - 1) / band;
-  const size_t lds = (size_t)band * TW * 8 + (size_t)(64 * TW + 1) * 8 +
-                     (hash ? (size_t)8 << hs_log2 : 0);
-  if (lds > 64 * 1024) return false;
+  const size_t lds = (size_t)band * TW * 8 + (size_t)(64 * TW + 1) * 8;
   const int64_t blocks = (n_tx + 64 * TW - 1) / (64 * TW) * n_bands;
   if (blocks > INT32_MAX) return false;
-  if (hash)
-    hipLaunchKernelGGL(k_encode_tile<true>, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr,
-                       items, n_tx, rank_of, ids, (unsigned long long*)bm, Wp, word_off, F,
-                       tw_log2, (int)band, hs_log2, fmask);
-  else
-    hipLaunchKernelGGL(k_encode_tile<false>, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr,
-                       items, n_tx, rank_of, ids, (unsigned long long*)bm, Wp, word_off, F,
-                       tw_log2, (int)band, hs_log2, fmask);
+  hipLaunchKernelGGL(k_encode_tile, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr, items,
+                     n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2, (int)band,
+                     fmask);
   KMLS_HIP(hipGetLastError());
   return true;
 }

@@ -538,18 +538,15 @@ def test_extend_split_k_long_rows(gpu_mod, monkeypatch, split):
     assert_same_itemsets(gpu_mod, r, c)
 
 
-@pytest.mark.parametrize("hash_lookup", ["1", "0"])
 @pytest.mark.parametrize("T,I,ms,min_f", [(300_000 + 37, 60_000, 0.002, 0),
                                             (200_000 + 37, 100_000, 0.0005, 3000)])
-def test_encode_tiled_long_shard(gpu_mod, T, I, ms, min_f, hash_lookup, monkeypatch):
+def test_encode_tiled_long_shard(gpu_mod, T, I, ms, min_f):
     """The LDS-slab encode produces the same tid-bitmaps as the host encoder, on a long shard
     with an odd tail tile; the second case has a million-style vocabulary (frequent-item mask
     in front of the rank gather) and more frequent rows than one LDS slab (row bands).  The
     buffer starts as all ones: the tiled encode must write every word of the shard's columns
-    (the tx-DP path no longer clears the bitmap first).  Both frequent-item lookups: the LDS
-    hash of the band's ids, and the bit mask + rank gather."""
+    (the tx-DP path no longer clears the bitmap first)."""
     import torch
-    monkeypatch.setenv("KMLS_ENCODE_HASH", hash_lookup)
     ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 9)
     g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(ptr, items, I)
