@@ -142,8 +142,8 @@ struct OutBufs {
   hipStream_t copy_s = nullptr;
   hipEvent_t ev = nullptr;
   // fused level path (levels.hip): look-back status words (epoch-tagged, zeroed once)
-  unsigned long long* status = nullptr;
-  int32_t* tile_row = nullptr;   // [status_cap] count tile → first row (written by level_scan)
+  unsigned long long* status = nullptr;  // [3 * status_cap]: three words per tile (SegAgg)
+  int32_t* tile_row = nullptr;   // [2][status_cap] count tile → first row, by level parity
   unsigned long long* trace = nullptr;  // KMLS_LEVEL_TRACE diagnostics ([status_cap][8])
   int64_t status_cap = 1 << 20;  // tiles per launch (256M candidates / 2G rows)
   // look-back tags: tag = epoch_base (per call, in FCtl) + launch index (kernel argument)
@@ -151,14 +151,13 @@ struct OutBufs {
   unsigned launch_idx = 0;
   int depth_hint = 6;            // levels enqueued before the first completion check
   std::vector<int64_t> cand_hint;  // candidates per level in the previous call (kernel choice)
-  std::vector<int64_t> rows_hint;  // rows per level in the previous call (scan grid)
   OutBufs() {
     KMLS_HIP(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
     // device-scope release: a cross-stream fork needs no system-scope L2 writeback
     KMLS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice));
-    KMLS_HIP(hipMalloc((void**)&status, (size_t)status_cap * sizeof(unsigned long long)));
-    KMLS_HIP(hipMemset(status, 0, (size_t)status_cap * sizeof(unsigned long long)));
-    KMLS_HIP(hipMalloc((void**)&tile_row, (size_t)status_cap * sizeof(int32_t)));
+    KMLS_HIP(hipMalloc((void**)&status, (size_t)status_cap * 3 * sizeof(unsigned long long)));
+    KMLS_HIP(hipMemset(status, 0, (size_t)status_cap * 3 * sizeof(unsigned long long)));
+    KMLS_HIP(hipMalloc((void**)&tile_row, (size_t)status_cap * 2 * sizeof(int32_t)));
   }
   static constexpr unsigned kLaunchesPerCall = 256;
   // start a fused call: a fresh 256-tag window (the 24-bit tag wraps after ~65k calls: then the
@@ -166,7 +165,7 @@ struct OutBufs {
   unsigned begin_call(hipStream_t s) {
     epoch_base += kLaunchesPerCall;
     if (epoch_base + kLaunchesPerCall >= (1u << 24)) {
-      KMLS_HIP(hipMemsetAsync(status, 0, (size_t)status_cap * sizeof(unsigned long long), s));
+      KMLS_HIP(hipMemsetAsync(status, 0, (size_t)status_cap * 3 * sizeof(unsigned long long), s));
       epoch_base = kLaunchesPerCall;
     }
     launch_idx = 0;
@@ -340,7 +339,7 @@ struct MineRun {
     constexpr int kMaxLv = 64;
     const int64_t Fr = root.n;
     const size_t mark = arena->mark();
-    const int64_t row_bytes = Wp * 8 + 4 + 8 + 4 + 4;  // child bitmap + rank + gid + prow + slot
+    const int64_t row_bytes = Wp * 8 + 4 + 8 + 4 + 8;  // child bitmap + rank + gid + slot + cand_off
     const size_t root_need = (size_t)(root_total + 1) * (size_t)row_bytes + (size_t)(Fr + 1) * 8 +
                              kMaxLv * sizeof(kern::FLevel) + 4096;
     const size_t free_b = arena->capacity() - arena->used();
@@ -360,12 +359,11 @@ struct MineRun {
     kern::FLevel* d_desc = (kern::FLevel*)arena->push(kMaxLv * sizeof(kern::FLevel));
     kern::FCtl* d_ctl = (kern::FCtl*)arena->push(sizeof(kern::FCtl));
     int64_t* d_off = (int64_t*)arena->push((size_t)(Fr + 1) * 8);
-    int64_t* d_rend = (int64_t*)arena->push((size_t)(Fr + 1) * 8);
     uint64_t* c_bm = (uint64_t*)arena->push((size_t)((std::max<int64_t>(root_total, 1) + 63) & ~63ll) * Wp * 8);
     int32_t* c_rank = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
     int64_t* c_gid = (int64_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 8);
-    int32_t* c_prow = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
     int32_t* c_slot = (int32_t*)arena->push((size_t)std::max<int64_t>(root_total, 1) * 4);
+    int64_t* c_co = (int64_t*)arena->push((size_t)(root_total + 1) * 8);
     const size_t rem = arena->capacity() - arena->used();
     const size_t bump_bytes = fused_bump_cap(rem > (320ull << 20) ? rem - (64ull << 20) : 0);
     if (bump_bytes < (16ull << 20)) {
@@ -390,13 +388,12 @@ struct MineRun {
     r.gid = root.gid;
     r.cand_off = d_off;
     r.n_cand = root_total;
-    r.row_end = d_rend;
     r.child_base = out_size;
     h_desc[2].bm = c_bm;
     h_desc[2].rank = c_rank;
     h_desc[2].gid = c_gid;
-    h_desc[2].prow = c_prow;
     h_desc[2].slot = c_slot;
+    h_desc[2].cand_off = c_co;
     h_ctl->bump_base = bump_base;
     h_ctl->bump_cap = bump_bytes;
     h_ctl->status_cap = (unsigned long long)ob->status_cap;
@@ -459,16 +456,19 @@ struct MineRun {
       kern::LevelCountArgs a{Wp, minsup, L == 1 ? gram : nullptr, F, d_ids, out_parent.p,
                              out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1),
                              stream_dl, L == trace_level ? d_trace : nullptr, deferred,
-                             copy_blocks(), copy_last()};
+                             copy_blocks(), copy_last(), L == 1, out_cap};
       const int64_t hint = hint_at(ob->cand_hint, L);
       const int g = grid_for_tiles(hint < 0 ? -1 : (hint + kern::level_tile() - 1) / kern::level_tile());
       // the count kernels load tile_row[block] speculatively: every block index must be in bounds
       if ((int64_t)g + kern::kCopyBlocks + 64 > ob->status_cap)
         throw std::logic_error("levels_loop: count grid exceeds the tile_row capacity");
+      int32_t* tr_cur = ob->tile_row + (size_t)(L & 1) * (size_t)ob->status_cap;
+      int32_t* tr_nx = ob->tile_row + (size_t)((L + 1) & 1) * (size_t)ob->status_cap;
       kern::level_count(&d_desc[L], &d_desc[L + 1], d_ctl, ob->status, ob->next_epoch(s), a,
-                        L == 1 ? nullptr : ob->tile_row, g, hint, s);
+                        L == 1 ? nullptr : tr_cur, tr_nx, g, hint, s);
     };
-    const int L_allowed = std::min(kMaxLv - 2, max_len ? max_len - 1 : kMaxLv - 2);
+    // count(L) writes desc[L + 2] (the next level's buffers)
+    const int L_allowed = std::min(kMaxLv - 3, max_len ? max_len - 1 : kMaxLv - 3);
     int last = 1;
     int target = std::min(L_allowed, std::max(ob->depth_hint, 2));
     if (graph_replay) {  // the replayed graph already holds count(1) .. count(graph_last)
@@ -484,12 +484,6 @@ struct MineRun {
     for (bool first = true;; first = false) {
      if (!(first && graph_replay)) {
       for (int L = last + 1; L <= target; ++L) {
-        const int64_t rows = hint_at(ob->rows_hint, L);
-        kern::level_scan(&d_desc[L - 1], &d_desc[L], &d_desc[L + 1], d_ctl, ob->status,
-                         ob->next_epoch(s), Wp, out_cap, ob->tile_row,
-                         grid_for_tiles(rows < 0 ? -1 : (rows + kern::level_scan_tile() - 1) /
-                                                            kern::level_scan_tile()),
-                         s);
         count_level(L);
         last = L;
       }
@@ -536,11 +530,7 @@ struct MineRun {
     if (!ok) return false;
     last_desc.assign(b_desc, b_desc + kMaxLv);
     ob->cand_hint.assign((size_t)last + 1, -1);
-    ob->rows_hint.assign((size_t)last + 1, -1);
-    for (int L = 1; L <= last; ++L) {
-      ob->cand_hint[L] = b_desc[L].n_cand;
-      ob->rows_hint[L] = b_desc[L].n_rows;
-    }
+    for (int L = 1; L <= last; ++L) ob->cand_hint[L] = b_desc[L].n_cand;
     const int64_t new_size = b_desc[last + 1].child_base;
     for (int L = 1; L <= last; ++L)
       if (b_desc[L + 1].n_rows > 0) max_depth = std::max(max_depth, L + 1);
@@ -1161,11 +1151,26 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     root.row_end = d_end;
     bool done = false;
     if (comm_ == nullptr && fused_levels_enabled()) {
-      std::vector<int64_t> off((size_t)F + 1, 0);
-      for (int64_t a = 0; a < F; ++a) off[a + 1] = off[a] + root_len[a];
+      // the fused levels take the root rows in descending rank, each owning its pairs with
+      // the rows before it (levels.hip header): row r = rank F-1-r, root class of rank F-1-r
+      std::vector<int32_t> rrank((size_t)F);
+      std::vector<int64_t> rgid((size_t)F), off((size_t)F + 1, 0);
+      for (int64_t r = 0; r < F; ++r) {
+        rrank[(size_t)r] = (int32_t)(F - 1 - r);
+        rgid[(size_t)r] = F - 1 - r;
+        off[(size_t)r + 1] = off[(size_t)r] + (root_len[(size_t)(F - 1 - r)] ? r : 0);
+      }
+      int32_t* d_rrank = (int32_t*)arena_->push(F * sizeof(int32_t));
+      int64_t* d_rgid = (int64_t*)arena_->push(F * sizeof(int64_t));
+      KMLS_HIP(hipMemcpyAsync(d_rrank, rrank.data(), F * sizeof(int32_t), hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(d_rgid, rgid.data(), F * sizeof(int64_t), hipMemcpyHostToDevice, s));
+      Level froot = root;
+      froot.rank = d_rrank;
+      froot.gid = d_rgid;
       run.pinned = pinned_;
       run.fast_hint = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 16ll << 20);
-      done = run.run_fast(root, off, root_total);
+      done = run.run_fast(froot, off, off[(size_t)F]);
+      KMLS_HIP(hipStreamSynchronize(s));  // the pageable staging vectors die at scope end
     }
     if (!done) run.process(root, 1, d_len, root_total);
     res.levels_path = done ? "fused" : (comm_ ? "chunked-txdp" : "chunked");
@@ -1416,7 +1421,6 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
            u(out_->tile_row), (uint64_t)n_cus_, (uint64_t)out_->depth_hint, u(call_params_),
            (uint64_t)out_->cand_hint.size()};
     for (int64_t v : out_->cand_hint) key.push_back((uint64_t)v);
-    for (int64_t v : out_->rows_hint) key.push_back((uint64_t)v);
     key.push_back((uint64_t)cfg.rule_index);
     if (cfg.rule_index) {
       key.push_back((uint64_t)icap);

@@ -88,10 +88,10 @@ struct FLevel {  // device-resident descriptor of one level (rows = itemsets of 
   const int32_t* rank;     // last item's Eclat rank
   const int64_t* gid;      // trie node id
   const int32_t* prow;     // row in the parent level
-  int64_t* cand_off;       // [n_rows + 1]
+  int64_t* cand_off;       // [n_rows + 1] owner-major: row b's candidates pair it with its
+                           // earlier siblings (written by the previous level's count)
   int64_t n_cand;
-  int64_t* row_end;        // [n_rows] child-level index one past each row's children (rows
-                           // with candidates only): the next scan's class ends
+  int64_t* row_end;        // unused (round-1 scan layout)
   int64_t child_base;      // trie id of this level's first child
   unsigned int scan_ticket, count_ticket;
   // row → bitmap row (nullptr: identity).  The short-row count kernel writes each candidate's
@@ -161,6 +161,8 @@ struct LevelCountArgs {
   bool deferred_dl;
   int copy_blocks;  // copy blocks of the grid when deferred_dl (default kCopyBlocks)
   bool copy_last;   // copy blocks at the end of the grid instead of leading it (A/B)
+  bool root;        // level 1: rows = frequent items in descending rank, bitmap rows by rank
+  int64_t out_cap;  // device trie capacity (nodes)
 };
 // Few copy blocks on purpose: GPU writes to pinned host memory share the L2 -> fabric write path
 // with the tiles' HBM stores, and a saturated PCIe link backs that path up (a level-6 trace showed
@@ -219,12 +221,6 @@ void level_partition(const uint32_t* gram, int64_t ld, FLevel* desc, uint32_t mi
                      int64_t F_max, int64_t* cost, int32_t* prank, hipStream_t s);
 int level_grid(int n_cus);
 int64_t level_tile();
-int64_t level_scan_tile();
-// tile_row[status_cap]: the scan of level L records the first row of every count tile of L,
-// so count(L) skips its per-tile search (pass nullptr to count the root level)
-void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status,
-                unsigned epoch, int64_t Wp, int64_t out_cap, int32_t* tile_row, int grid,
-                hipStream_t s);
 // trie nodes [lv->child_base, +nx->n_rows) (the last launched level's children) from the device
 // trie arrays into FCtl::h (download), plus a readback of rb_bytes (multiple of 16; 0 = none)
 // from rb_src to FCtl::rb_dst
@@ -233,9 +229,13 @@ void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t*
                    bool download, const void* rb_src, size_t rb_bytes, hipStream_t s);
 // cand_hint: expected candidate count of the level (the previous call's; -1 unknown) — picks
 // the register/latency trade-off of the short-row kernel, never affects results
+// count level L (lv = &desc[L], nx = &desc[L+1]; desc[L+2] receives the next buffers).
+// tile_row: count tile → first row of level L, written by count(L-1) (nullptr at the root);
+// tile_row_nx: the same map for level L+1, written here (double-buffered by the caller).
+// status: 3 words per tile.
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
-                 const LevelCountArgs& a, const int32_t* tile_row, int grid, int64_t cand_hint,
-                 hipStream_t s);
+                 const LevelCountArgs& a, const int32_t* tile_row, int32_t* tile_row_nx, int grid,
+                 int64_t cand_hint, hipStream_t s);
 
 // ---- rule map = pair-support CSR (pairs.hip, O10 pairs_to_csr) ----
 // Longest row the device sorts (rows are <= F-1 long; longer rows set status bit 2 and the

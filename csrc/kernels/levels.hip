@@ -4,26 +4,31 @@
 // level: survivor counts size the child buffers, candidate totals size the next launch.  Here
 // every size lives in a device-resident descriptor (FLevel) and every launch is a fixed grid of
 // persistent blocks that pull tiles from a ticket counter, so the host enqueues all levels back
-// to back and synchronises ONCE per mining call.  Two kernels per level:
+// to back and synchronises ONCE per mining call.  ONE kernel per level:
 //
-//   k_level_scan  (level L >= 2): len[s] = #siblings after s in its class (from the parent
-//                 level's survivor positions), single-pass decoupled-look-back exclusive scan →
-//                 cand_off, n_cand; the last tile bump-allocates the level's outputs.
-//   k_level_count (every level): per 256-candidate tile — decode (a, b) against an LDS window of
-//                 cand_off, wave64-team AND+popcount (or a gram lookup at the root), block scan
-//                 of the survivor flags + decoupled look-back → global survivor index, then
-//                 materialise survivors (child bitmap, rank, gid, parent row, trie append) in
-//                 the same kernel.  This fuses the chunked path's count, flag scan (2 rocprim
-//                 kernels), child_totals and materialise launches, and reads each parent row
-//                 pair once into L1/L2 for both phases.
-//   Streamed download: the materialise phase also writes each survivor's trie node straight
-//                 into pinned host memory (coalesced PCIe writes), so finished levels reach the
-//                 host while deeper levels run, with no copy kernel or cross-stream event.
+//   k_level_count: per 256-candidate tile — decode (a, b) against an LDS window of cand_off,
+//     AND+popcount (or a gram lookup at the root), block scan of the survivor flags + decoupled
+//     look-back → global survivor index, then materialise survivors (child bitmap, rank, gid,
+//     trie append) AND lay out the next level: every survivor's candidate offset, the next
+//     level's tile → first-row map, and (last tile) the next level's buffers.
 //
-// Look-back status words pack (epoch:24 | flag:2 | value:38) in one 64-bit word, so publishing
-// needs no fence, and the per-call epoch makes re-zeroing the status array unnecessary.
-// Every spin is bounded: a bug sets FCtl::overflow and the host falls back to the chunked path
-// instead of hanging the GPU.
+// Candidate order ("owner-major"): rows of a class are ordered by DESCENDING frequency rank and
+// row b owns the candidates (a, b) with every EARLIER sibling a.  The child (a, b) extends b's
+// itemset by a's last item (trie parent = b), so a row's candidate count is its number of earlier
+// siblings — known as soon as the survivors before it are: the previous round's separate scan
+// kernel (candidates = LATER siblings, known only when the class is complete) folds into the
+// count's look-back.  Paths still run from the least to the most frequent item, so the classes
+// and candidate totals are those of ascending-frequency Eclat.  The look-back carries a
+// segmented-scan state per tile (survivors, next-level candidates, survivors of the open owner,
+// see SegAgg), published as three 64-bit words that each carry the epoch and the flag.
+//
+// Streamed download: the materialise phase also writes each survivor's trie node straight into
+// pinned host memory (coalesced PCIe writes), so finished levels reach the host while deeper
+// levels run, with no copy kernel or cross-stream event.
+//
+// Status words pack (epoch:24 | flag:2 | value:38), so publishing needs no fence, and the per-call
+// epoch makes re-zeroing the status array unnecessary.  Every spin is bounded: a bug sets
+// FCtl::overflow and the host falls back to the chunked path instead of hanging the GPU.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,8 +53,6 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kTile = 256;              // candidates per count tile
-constexpr int kScanItems = 8;           // rows per thread in the scan
-constexpr int kScanTile = kBlock * kScanItems;
 constexpr int kWin = 1024;              // LDS cand_off window (rows) per count tile
 constexpr unsigned long long kValMask = (1ull << 38) - 1;
 constexpr long long kSpinLimit = 1ll << 26;
@@ -66,29 +69,82 @@ __device__ __forceinline__ unsigned long long pack(unsigned epoch, unsigned flag
          (v & kValMask);
 }
 
+// Tile aggregate of the segmented scan that lays out the next level (a segment = the survivors
+// of one owner row b; segments start at the owner's first candidate, a "head"):
+//   S  survivors, C  next-level candidates = sum over survivors of their earlier siblings
+//   counted inside this tile's span (a continuing first segment counted from 0), O  survivors
+//   since the last head (all S when the tile has no head), F  survivors before the first head
+//   (the part of the first segment that continues the previous tile), H  a head is present.
+// x ⊕ y (x first) is associative with identity 0; an inclusive prefix needs only (S, C, O).
+struct SegAgg {  // S, O, F count rows (< 2^31: level rows are int32-indexed), C candidates
+  int32_t S, O, F;
+  bool H;
+  int64_t C;
+};
+__device__ __forceinline__ SegAgg seg_cat(const SegAgg& x, const SegAgg& y) {
+  SegAgg r;
+  r.S = x.S + y.S;
+  r.C = x.C + y.C + (int64_t)x.O * y.F;  // y's continuing survivors: x.O more earlier siblings each
+  r.O = y.H ? y.O : x.O + y.S;
+  r.F = x.H ? x.F : x.S + y.F;
+  r.H = x.H || y.H;
+  return r;
+}
+__device__ __forceinline__ SegAgg seg_shfl_xor(const SegAgg& v, int off) {
+  SegAgg p;
+  p.S = __shfl_xor(v.S, off, 64);
+  p.C = __shfl_xor(v.C, off, 64);
+  p.O = __shfl_xor(v.O, off, 64);
+  p.F = __shfl_xor(v.F, off, 64);
+  p.H = __shfl_xor((int)v.H, off, 64) != 0;
+  return p;
+}
+// three words per tile: S | C | aggregate (H:1 @37, F:18 @18, O:18 @0) or prefix O
+__device__ __forceinline__ void seg_publish(unsigned long long* my, unsigned e, unsigned flag,
+                                            const SegAgg& v) {
+  const unsigned long long w2 =
+      flag == 2 ? (unsigned long long)v.O
+                : ((unsigned long long)v.H << 37) | ((unsigned long long)v.F << 18) |
+                      (unsigned long long)v.O;
+  st_relaxed(my + 0, pack(e, flag, (unsigned long long)v.S));
+  st_relaxed(my + 1, pack(e, flag, (unsigned long long)v.C));
+  st_relaxed(my + 2, pack(e, flag, w2));
+}
+
 // Wave-parallel decoupled look-back for tile t (called by all 64 lanes of wave 0): each round
-// inspects 64 predecessors at once (lane 0 = nearest), sums their aggregates up to the nearest
-// inclusive prefix, and only spins while one of those is unpublished.  A one-thread walk costs
-// one memory latency per predecessor — O(tiles) per tile, which made the first version of this
-// kernel latency-bound.  Returns the tile's exclusive prefix (same value in every lane).
-__device__ int64_t lookback(unsigned long long* st, int64_t t, unsigned epoch, int64_t agg,
-                            FCtl* ctl) {
+// inspects 64 predecessors at once (lane 0 = nearest), folds them newest-last up to the nearest
+// inclusive prefix (an xor butterfly in which the higher lane — the older tile — is always the
+// left operand), and only spins while one of those is unpublished or half-written (its three
+// words must agree on epoch and flag).  Returns the tile's exclusive prefix (every lane).
+__device__ SegAgg lookback_seg(unsigned long long* st, int64_t t, unsigned epoch, const SegAgg& agg,
+                               FCtl* ctl) {
   const unsigned e = epoch & 0xFFFFFFu;
   const int lane = threadIdx.x & 63;
+  unsigned long long* my = st + 3 * t;
+  const SegAgg zero{0, 0, 0, false, 0};
   if (t == 0) {
-    if (lane == 0) st_relaxed(&st[0], pack(e, 2, (unsigned long long)agg));
-    return 0;
+    if (lane == 0) seg_publish(my, e, 2, agg);
+    return zero;
   }
-  if (lane == 0) st_relaxed(&st[t], pack(e, 1, (unsigned long long)agg));
-  int64_t excl = 0;
+  if (lane == 0) seg_publish(my, e, 1, agg);
+  SegAgg acc = zero;
   int64_t end = t;  // window = predecessors [end-64, end)
   long long spins = 0;
   while (true) {
     const int64_t j = end - 1 - lane;
-    unsigned long long w = j >= 0 ? ld_relaxed(&st[j]) : pack(e, 2, 0);  // virtual P(0) before tile 0
-    const unsigned we = (unsigned)(w >> 40), wf = (unsigned)(w >> 38) & 3u;
-    const bool valid = we == e && wf != 0;
-    const unsigned long long pmask = __ballot(valid && wf == 2);
+    unsigned long long w0, w1, w2;
+    if (j >= 0) {
+      w0 = ld_relaxed(st + 3 * j);
+      w1 = ld_relaxed(st + 3 * j + 1);
+      w2 = ld_relaxed(st + 3 * j + 2);
+    } else {  // virtual P(0) before tile 0
+      w0 = w1 = w2 = pack(e, 2, 0);
+    }
+    const unsigned f0 = (unsigned)(w0 >> 38) & 3u;
+    const bool valid = (unsigned)(w0 >> 40) == e && (unsigned)(w1 >> 40) == e &&
+                       (unsigned)(w2 >> 40) == e && f0 != 0 &&
+                       ((unsigned)(w1 >> 38) & 3u) == f0 && ((unsigned)(w2 >> 38) & 3u) == f0;
+    const unsigned long long pmask = __ballot(valid && f0 == 2);
     const unsigned long long imask = __ballot(!valid);
     const int first_p = pmask ? __builtin_ctzll(pmask) : 64;
     const unsigned long long need = first_p >= 63 ? ~0ull : ((1ull << (first_p + 1)) - 1ull);
@@ -100,15 +156,31 @@ __device__ int64_t lookback(unsigned long long* st, int64_t t, unsigned epoch, i
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    int64_t v = lane <= first_p ? (int64_t)(w & kValMask) : 0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    excl += v;
+    SegAgg v = zero;
+    if (lane <= first_p) {
+      v.S = (int32_t)(w0 & kValMask);
+      v.C = (int64_t)(w1 & kValMask);
+      const unsigned long long x = w2 & kValMask;
+      if (f0 == 2) {
+        v.O = (int32_t)x;
+        v.H = true;
+      } else {
+        v.O = (int32_t)(x & 0x3FFFFull);
+        v.F = (int32_t)((x >> 18) & 0x3FFFFull);
+        v.H = (x >> 37) & 1ull;
+      }
+    }
+#pragma unroll 1
+    for (int off = 1; off < 64; off <<= 1) {
+      const SegAgg p = seg_shfl_xor(v, off);
+      v = (lane & off) ? seg_cat(v, p) : seg_cat(p, v);
+    }
+    acc = seg_cat(v, acc);
     if (first_p < 64) break;
     end -= 64;
   }
-  if (lane == 0) st_relaxed(&st[t], pack(e, 2, (unsigned long long)(excl + agg)));
-  return excl;
+  if (lane == 0) seg_publish(my, e, 2, seg_cat(acc, agg));
+  return acc;
 }
 
 // One trie node into the pinned host arrays (widths per HostTrie); false if past the capacity.
@@ -286,124 +358,149 @@ __device__ __forceinline__ int64_t find_row_g(const int64_t* __restrict__ off, i
   return lo;
 }
 
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_level_scan(FLevel* __restrict__ pv,
-                                                       FLevel* __restrict__ lv,
-                                                       FLevel* __restrict__ nx, FCtl* ctl,
-                                                       unsigned long long* __restrict__ status,
-                                                       unsigned epoch, int64_t Wp,
-                                                       int64_t out_cap,
-                                                       int32_t* __restrict__ tile_row) {
-  __shared__ int64_t s_w[kBlock / 64];
-  __shared__ int64_t s_base;
-  __shared__ int64_t s_ticket;
-  // descriptor fields in one batch above the first branch (see k_level_count_small)
-  const unsigned ovf = ctl->overflow;
-  const unsigned ebase = ctl->epoch_base;
-  const unsigned long long scap = ctl->status_cap;
-  const int64_t n = lv->n_rows;
-  const int32_t* __restrict__ prow = lv->prow;
-  const int64_t* __restrict__ pend = pv->row_end;
-  int64_t* __restrict__ co = lv->cand_off;
-  asm volatile("" ::"s"(ebase), "s"(scap), "s"(n), "s"(prow), "s"(pend), "s"(co));
-  if (ovf) return;
-  epoch = (ebase + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
-  const int64_t n_tiles = (n + kScanTile - 1) / kScanTile;
-  if (n_tiles > (int64_t)scap) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&ctl->overflow, 3u);
-    return;
-  }
-  if (n == 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      lv->n_cand = 0;
-      nx->n_rows = 0;
-      nx->child_base = lv->child_base;
-    }
-    return;
-  }
-  // Idle blocks leave before touching the ticket: same-address device atomics serialise, and
-  // 2048 of them per launch cost more than a small level's whole scan.
-  if ((int64_t)blockIdx.x >= n_tiles) return;
-  for (bool first = true;; first = false) {
-    const int64_t t = next_tile(&lv->scan_ticket, first, n_tiles, &s_ticket, (int64_t)gridDim.x,
-                                (int64_t)blockIdx.x);
-    if (t >= n_tiles) return;
-    const int64_t s0 = t * kScanTile + (int64_t)threadIdx.x * kScanItems;
-    int64_t len[kScanItems];
-    int64_t sum = 0;
+// Buffers for the rows that counting T candidates can produce (the next level): child bitmaps at
+// candidate slots (64-interleaved, see k_level_count_small), last-item rank, trie id, bitmap
+// slot, and the children's own cand_off — one device atomic for all five.
+__device__ void alloc_level(FCtl* ctl, FLevel* nx, int64_t T, int64_t Wp) {
+  const unsigned long long t = (unsigned long long)T;
+  const unsigned long long T64 = (t + 63ull) & ~63ull;
+  const unsigned long long sz[5] = {T64 * (unsigned long long)Wp * 8ull, t * 4ull, t * 8ull,
+                                    t * 4ull, (t + 1ull) * 8ull};
+  void* p[5];
+  bump_n<5>(ctl, sz, p);
+  nx->bm = (const uint64_t*)p[0];
+  nx->rank = (const int32_t*)p[1];
+  nx->gid = (const int64_t*)p[2];
+  nx->slot = (const int32_t*)p[3];
+  nx->cand_off = (int64_t*)p[4];
+}
+
+__device__ __forceinline__ int block_incl_max(int v, int32_t* s_wm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-      const int64_t s = s0 + i;
-      int64_t l = 0;
-      if (s < n) {
-        l = pend[prow[s]] - s - 1;  // siblings after s in its class
-      }
-      len[i] = l;
-      sum += l;
-    }
-    int64_t tile_total;
-    const int64_t excl = block_excl_scan(sum, s_w, &tile_total);
-    if (threadIdx.x < 64) {
-      const int64_t b = lookback(status, t, epoch, tile_total, ctl);
-      if (threadIdx.x == 0) s_base = b;
-    }
-    __syncthreads();
-    int64_t run = s_base + excl;
-#pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-      const int64_t s = s0 + i;
-      if (s < n) {
-        co[s] = run;
-        // count-tile → first row map: row s owns every tile start in [run, run + len)
-        for (int64_t ct = (run + kTile - 1) / kTile; ct * kTile < run + len[i]; ++ct)
-          if (ct < (int64_t)scap) tile_row[ct] = (int32_t)s;
-      }
-      run += len[i];
-    }
-    if (t == n_tiles - 1 && threadIdx.x == 0) {
-      const int64_t total = s_base + tile_total;
-      co[n] = total;
-      lv->n_cand = total;
-      const int64_t tiles = (total + kTile - 1) / kTile;
-      if (lv->child_base + total > out_cap || tiles > (int64_t)scap ||
-          n > (int64_t)INT32_MAX) {
-        atomicExch(&ctl->overflow, 4u);
-      } else if (total > 0) {
-        const unsigned long long T = (unsigned long long)total;
-        const unsigned long long T64 = (T + 63ull) & ~63ull;  // 64-interleaved candidate rows
-        const unsigned long long sz[6] = {(unsigned long long)n * 8ull,
-                                          T64 * (unsigned long long)Wp * 8ull, T * 4ull,
-                                          T * 8ull, T * 4ull, T * 4ull};
-        void* p[6];
-        bump_n<6>(ctl, sz, p);
-        lv->row_end = (int64_t*)p[0];
-        nx->bm = (const uint64_t*)p[1];
-        nx->rank = (const int32_t*)p[2];
-        nx->gid = (const int64_t*)p[3];
-        nx->prow = (const int32_t*)p[4];
-        nx->slot = (const int32_t*)p[5];
-      }
-    }
-    __syncthreads();
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x = max(x, y);
   }
+  if (lane == 63) s_wm[w] = x;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kBlock / 64; ++i)
+    if (i < w) x = max(x, s_wm[i]);
+  return x;
+}
+
+struct EpiSmem {
+  int64_t w1[kBlock / 64], w2[kBlock / 64];
+  int32_t wm[kBlock / 64];
+  int32_t lx[kBlock];    // survivors before each candidate in the tile
+  int32_t hp[kBlock];    // last head at or before it (-1: continuing segment)
+  int32_t len0[kBlock];  // earlier siblings of its survivor inside the tile's span
+  int64_t cl[kBlock];    // candidates of the tile's earlier survivors (carry 0)
+  int fh, lh;
+  int64_t base, cex, carry;
+};
+
+// Survivor layout of one count tile and the next level's candidate layout (thread i = candidate
+// i of the tile; every thread of the block calls this).  Returns the survivor's row index in the
+// next level (-1 when the candidate failed) after writing its candidate offset and tile→row
+// entries; the last tile sets the next level's sizes and allocates its children's buffers.
+// Per-candidate intermediates go through LDS so that little stays live in registers across the
+// look-back (its fold is the register peak of the count kernels).
+__device__ int64_t tile_epilogue(EpiSmem& sm, int64_t t, int64_t n_tiles, bool live, int flag,
+                                 bool head, unsigned long long* status, unsigned epoch, FCtl* ctl,
+                                 FLevel* nx, int64_t* co_nx, int32_t* tile_row_nx, int64_t scap,
+                                 int64_t child_base, int64_t n_cand, int64_t Wp, int64_t out_cap) {
+  const int tid = threadIdx.x;
+  if (tid == 0) sm.fh = kBlock;
+  int64_t S;
+  const int64_t lx = block_excl_scan(flag, sm.w1, &S);
+  const int hv = (live && head) ? tid : -1;
+  const int hp = block_incl_max(hv, sm.wm);  // last head at or before this candidate
+  sm.lx[tid] = (int32_t)lx;
+  sm.hp[tid] = hp;
+  if (hv >= 0) atomicMin(&sm.fh, hv);
+  if (tid == kBlock - 1) sm.lh = hp;
+  __syncthreads();
+  const int fh = sm.fh, lh = sm.lh;
+  const bool H = fh < kBlock;
+  const int64_t Fh = H ? (int64_t)sm.lx[fh] : S;
+  const int64_t O = H ? S - (int64_t)sm.lx[lh] : S;
+  const int32_t len0 = flag ? (hp < 0 ? (int32_t)lx : (int32_t)lx - sm.lx[hp]) : 0;
+  sm.len0[tid] = len0;
+  int64_t C0;
+  sm.cl[tid] = block_excl_scan((int64_t)len0, sm.w2, &C0);
+  if (tid < 64) {
+    const SegAgg p = lookback_seg(status, t, epoch, SegAgg{(int32_t)S, (int32_t)O, (int32_t)Fh, H, C0}, ctl);
+    if (tid == 0) {
+      sm.base = p.S;
+      sm.cex = p.C;
+      sm.carry = p.O;
+    }
+  }
+  __syncthreads();
+  int64_t s = -1;
+  if (flag) {
+    const int64_t base = sm.base, cex = sm.cex, carry = sm.carry;
+    const int64_t l = sm.lx[tid];
+    const bool cont = sm.hp[tid] < 0;  // in the segment continuing from the previous tile
+    const int64_t f = sm.fh < kBlock ? (int64_t)sm.lx[sm.fh] : 0;  // = Fh when a head exists
+    s = base + l;
+    const int64_t len = sm.len0[tid] + (cont ? carry : 0);                      // earlier siblings
+    const int64_t co = cex + sm.cl[tid] + carry * (cont ? l : f);  // its first candidate
+    co_nx[s] = co;
+    for (int64_t ct = (co + kTile - 1) / kTile; ct * kTile < co + len; ++ct)
+      if (ct < scap) tile_row_nx[ct] = (int32_t)s;
+  }
+  if (t == n_tiles - 1 && tid == 0) {
+    const int64_t base = sm.base, carry = sm.carry;
+    int64_t Ssum = 0, C0s = 0;
+    (void)Ssum;
+    (void)C0s;
+    const int64_t St = base + S;
+    const int64_t Ct = sm.cex + C0 + carry * Fh;
+    nx->n_rows = St;
+    nx->child_base = child_base + St;
+    nx->n_cand = Ct;
+    co_nx[St] = Ct;
+    atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
+    if (child_base + St + Ct > out_cap || (Ct + kTile - 1) / kTile > scap ||
+        St > (int64_t)INT32_MAX || Ct > (int64_t)INT32_MAX)
+      atomicExch(&ctl->overflow, 4u);
+    else
+      alloc_level(ctl, nx + 1, Ct, Wp);
+  }
+  return s;
+}
+
+// A level without candidates: empty next level, and a one-entry cand_off for the level after
+__device__ void empty_level(FCtl* ctl, FLevel* nx, int64_t child_base) {
+  nx->n_rows = 0;
+  nx->n_cand = 0;
+  nx->child_base = child_base;
+  if (nx->cand_off) nx->cand_off[0] = 0;
+  alloc_level(ctl, nx + 1, 0, 0);
 }
 
 // ---------------------------------------------------------------------------------------------
+// Long rows (T > 4096 transactions): a team of TS lanes per candidate; survivors' rows are written
+// compactly at their next-level row index (the next level reads rows row-major).
 template <int TS>
 __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
                                                         FLevel* __restrict__ nx, FCtl* ctl,
                                                         unsigned long long* __restrict__ status,
                                                         unsigned epoch, LevelCountArgs A,
-                                                        const int32_t* __restrict__ tile_row) {
+                                                        const int32_t* __restrict__ tile_row,
+                                                        int32_t* __restrict__ tile_row_nx) {
   __shared__ int64_t s_off[kWin];
   __shared__ uint32_t s_cnt[kTile];
-  __shared__ int32_t s_lpos[kTile];
-  __shared__ int64_t s_a[kTile];   // candidate → parent row a
-  __shared__ int64_t s_b[kTile];   // candidate → sibling row b
-  __shared__ int64_t s_w[kBlock / 64];
+  __shared__ int64_t s_a[kTile];   // candidate → earlier sibling a
+  __shared__ int64_t s_b[kTile];   // candidate → owner row b
+  __shared__ int64_t s_row[kTile];  // candidate → survivor's next-level row (-1: failed)
   __shared__ int64_t s_r0;
-  __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
+  __shared__ EpiSmem epi;
   if (ctl->overflow) return;
   epoch = (ctl->epoch_base + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
   const int cbk = A.deferred_dl ? A.copy_blocks : 0;  // copy blocks (lead the grid by default)
@@ -419,36 +516,34 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
   const int64_t child_base = lv->child_base;
   if (n_tiles == 0) {
-    if (bid == 0 && threadIdx.x == 0) {
-      nx->n_rows = 0;
-      nx->child_base = child_base;
-      nx->cand_off = (int64_t*)bump(ctl, 8ull);
-      if (nx->cand_off) nx->cand_off[0] = 0;
-    }
+    if (bid == 0 && threadIdx.x == 0) empty_level(ctl, nx, child_base);
     return;
   }
-  if (bid >= n_tiles) return;  // idle blocks: no ticket atomic (see scan)
+  if (bid >= n_tiles) return;  // idle blocks: no ticket atomic
   const int64_t* __restrict__ co = lv->cand_off;
   const unsigned long long* __restrict__ bm = (const unsigned long long*)lv->bm;
   const int32_t* __restrict__ rank = lv->rank;
   const int64_t* __restrict__ gid = lv->gid;
-  int64_t* __restrict__ row_end = lv->row_end;
   unsigned long long* __restrict__ cbm = (unsigned long long*)nx->bm;
   int32_t* __restrict__ crank = (int32_t*)nx->rank;
   int64_t* __restrict__ cgid = (int64_t*)nx->gid;
-  int32_t* __restrict__ cprow = (int32_t*)nx->prow;
+  int64_t* __restrict__ co_nx = nx->cand_off;
+  const int64_t scap = (int64_t)ctl->status_cap;
   const int64_t Wp = A.Wp;
   const int64_t n2 = Wp >> 1;
   const int tl = threadIdx.x & (TS - 1);
   const int team = threadIdx.x / TS;
   constexpr int kTeams = kBlock / TS;
   constexpr int kPer = kTile / kTeams;
+  // bitmap row of a level row: the root's rows are the frequent items in descending rank order
+  // over a bitmap stored by rank; deeper levels are compact
+  auto brow = [&](int64_t r) { return A.root ? (int64_t)rank[r] : r; };
   for (bool first = true;; first = false) {
     const int64_t t = next_tile(&lv->count_ticket, first, n_tiles, &s_ticket, tgrid, bid);
     if (t >= n_tiles) return;
     const int64_t c0 = t * kTile;
     const int cn = (int)min((int64_t)kTile, n_cand - c0);
-    if (tile_row) {  // first row of the tile, recorded by this level's scan
+    if (tile_row) {  // first row of the tile, recorded by the previous level's count
       if (threadIdx.x == 0) s_r0 = tile_row[t];
     } else if (threadIdx.x < 64) {  // root level: 64-ary search by wave 0
       const int64_t c = c0;
@@ -468,33 +563,34 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
     }
     __syncthreads();
     // window co[r0 .. r0 + nw) in LDS; a candidate past the window searches HBM (rare: only
-    // when the tile spans more than kWin rows, i.e. many empty class tails)
+    // when the tile spans more than kWin rows)
     const int64_t r0 = s_r0;
     const int64_t nw = min((int64_t)kWin, n_rows + 1 - r0);
     for (int64_t i = threadIdx.x; i < nw; i += kBlock) s_off[i] = co[r0 + i];
     __syncthreads();
-    // one decode per candidate, shared by the count and materialise phases
-    bool row_last = false;  // this thread's candidate is the last of its row
-    if ((int)threadIdx.x < cn) {
+    // one decode per candidate: owner b = the row whose range holds c, a = an earlier sibling
+    bool head = false;
+    const bool live = (int)threadIdx.x < cn;
+    if (live) {
       const int64_t c = c0 + threadIdx.x;
-      int64_t a, oa, ob;
+      int64_t b, oa, ob;
       if (nw >= 2 && s_off[nw - 1] > c) {  // row in window: largest k < nw-1 with s_off[k] <= c
         int64_t lo = 0, hi = nw - 1;
         while (hi - lo > 1) {
           const int64_t mid = (lo + hi) >> 1;
           if (s_off[mid] <= c) lo = mid; else hi = mid;
         }
-        a = r0 + lo;
+        b = r0 + lo;
         oa = s_off[lo];
         ob = s_off[lo + 1];
       } else {
-        a = find_row_g(co, r0, n_rows, c);
-        oa = co[a];
-        ob = co[a + 1];
+        b = find_row_g(co, r0, n_rows, c);
+        oa = co[b];
+        ob = co[b + 1];
       }
-      row_last = c + 1 == ob;
-      s_a[threadIdx.x] = a;
-      s_b[threadIdx.x] = a + 1 + (c - oa);
+      head = c == oa;
+      s_a[threadIdx.x] = b - (ob - c);
+      s_b[threadIdx.x] = b;
     }
     __syncthreads();
     // ---- phase 1: supports (team per candidate, 2 candidates in flight) ----
@@ -504,15 +600,17 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
       const bool two = i1 < cn;
       if (A.gram) {
         if (tl == 0) {
-          s_cnt[i0] = A.gram[s_a[i0] * A.F + s_b[i0]];
-          if (two) s_cnt[i1] = A.gram[s_a[i1] * A.F + s_b[i1]];
+          for (int q = 0; q < (two ? 2 : 1); ++q) {
+            const int64_t ra = rank[s_a[i0 + q]], rb = rank[s_b[i0 + q]];
+            s_cnt[i0 + q] = A.gram[min(ra, rb) * A.F + max(ra, rb)];
+          }
         }
         continue;
       }
-      const ulonglong2* x0 = reinterpret_cast<const ulonglong2*>(bm + s_a[i0] * Wp);
-      const ulonglong2* y0 = reinterpret_cast<const ulonglong2*>(bm + s_b[i0] * Wp);
-      const ulonglong2* x1 = reinterpret_cast<const ulonglong2*>(bm + s_a[two ? i1 : i0] * Wp);
-      const ulonglong2* y1 = reinterpret_cast<const ulonglong2*>(bm + s_b[two ? i1 : i0] * Wp);
+      const ulonglong2* x0 = reinterpret_cast<const ulonglong2*>(bm + brow(s_a[i0]) * Wp);
+      const ulonglong2* y0 = reinterpret_cast<const ulonglong2*>(bm + brow(s_b[i0]) * Wp);
+      const ulonglong2* x1 = reinterpret_cast<const ulonglong2*>(bm + brow(s_a[two ? i1 : i0]) * Wp);
+      const ulonglong2* y1 = reinterpret_cast<const ulonglong2*>(bm + brow(s_b[two ? i1 : i0]) * Wp);
       uint32_t k0 = 0, k1 = 0;
       for (int64_t w = tl; w < n2; w += TS) {
         const ulonglong2 u0 = x0[w], v0 = y0[w], u1 = x1[w], v1 = y1[w];
@@ -530,58 +628,41 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
       }
     }
     __syncthreads();
-    // ---- phase 2: survivor positions (block scan + look-back) ----
-    const int flag = ((int)threadIdx.x < cn && s_cnt[threadIdx.x] >= A.minsup) ? 1 : 0;
-    int64_t tile_total;
-    const int64_t lx = block_excl_scan(flag, s_w, &tile_total);
-    s_lpos[threadIdx.x] = (int32_t)lx;
-    if (threadIdx.x < 64) {
-      const int64_t b = lookback(status, t, epoch, tile_total, ctl);
-      if (threadIdx.x == 0) s_base = b;
+    // ---- phase 2: survivor rows + next-level layout (block scans + segmented look-back) ----
+    const int flag = (live && s_cnt[threadIdx.x] >= A.minsup) ? 1 : 0;
+    const int64_t s = tile_epilogue(epi, t, n_tiles, live, flag, head, status, epoch, ctl, nx,
+                                    co_nx, tile_row_nx, scap, child_base, n_cand, Wp, A.out_cap);
+    s_row[threadIdx.x] = s;
+    if (flag) {  // per-survivor scalars: one thread each
+      const int64_t a = s_a[threadIdx.x], b = s_b[threadIdx.x];
+      const int32_t ra = rank[a];
+      const int64_t node = child_base + s;
+      crank[s] = ra;
+      cgid[s] = node;
+      const int64_t par = gid[b];
+      const int32_t it = A.ids[ra];
+      const uint32_t cnt = s_cnt[threadIdx.x];
+      A.out_parent[node] = par;
+      A.out_item[node] = it;
+      A.out_count[node] = cnt;
+      A.out_depth[node] = A.child_depth;
+      // streamed download: consecutive survivors → coalesced PCIe writes
+      if (A.download && !A.deferred_dl) host_store(ctl->h, ctl, node, par, it, cnt, A.child_depth);
     }
     __syncthreads();
-    const int64_t base = s_base;
-    if ((int)threadIdx.x < cn) {
-      if (row_last) row_end[s_a[threadIdx.x]] = base + lx + flag;
-      if (flag) {  // per-survivor scalars: one thread each
-        const int64_t a = s_a[threadIdx.x], b = s_b[threadIdx.x];
-        const int64_t s = base + lx;
-        const int32_t rb = rank[b];
-        const int64_t node = child_base + s;
-        crank[s] = rb;
-        cgid[s] = node;
-        cprow[s] = (int32_t)a;
-        const int64_t par = gid[a];
-        const int32_t it = A.ids[rb];
-        const uint32_t cnt = s_cnt[threadIdx.x];
-        A.out_parent[node] = par;
-        A.out_item[node] = it;
-        A.out_count[node] = cnt;
-        A.out_depth[node] = A.child_depth;
-        // streamed download: consecutive survivors → coalesced PCIe writes
-        if (A.download && !A.deferred_dl) host_store(ctl->h, ctl, node, par, it, cnt, A.child_depth);
-      }
-    }
-    // ---- phase 3: survivors' bitmaps (team per survivor) ----
+    // ---- phase 3: survivors' bitmaps (team per survivor), compact at their row ----
     for (int j = 0; j < kPer; ++j) {
       const int i = team * kPer + j;
       if (i >= cn) break;
-      if (s_cnt[i] < A.minsup) continue;  // team-uniform
-      const int64_t s = base + s_lpos[i];
-      const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + s_a[i] * Wp);
-      const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + s_b[i] * Wp);
-      ulonglong2* z = reinterpret_cast<ulonglong2*>(cbm + s * Wp);
+      const int64_t srow = s_row[i];
+      if (srow < 0) continue;  // team-uniform
+      const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + brow(s_a[i]) * Wp);
+      const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + brow(s_b[i]) * Wp);
+      ulonglong2* z = reinterpret_cast<ulonglong2*>(cbm + srow * Wp);
       for (int64_t w = tl; w < n2; w += TS) {
         const ulonglong2 u = x[w], v = y[w];
         z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
       }
-    }
-    if (t == n_tiles - 1 && threadIdx.x == 0) {
-      const int64_t S = base + tile_total;
-      nx->n_rows = S;
-      nx->child_base = child_base + S;
-      nx->cand_off = (int64_t*)bump(ctl, (unsigned long long)(S + 1) * 8ull);
-      atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
     }
     __syncthreads();
   }
@@ -596,14 +677,14 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
 // link.  Here
 //   * phase 1: ONE thread per candidate ANDs its row pair with independent 16-byte loads,
 //     popcounts in registers (no cross-lane reduction) and writes the AND row straight to the
-//     child bitmap array at the CANDIDATE index (fire-and-forget stores; non-survivors waste
-//     their row, 2-35 % of candidates on the headline levels).  Child rows then reach their
-//     bitmap through FLevel::slot, so there is no compaction pass at all.  Candidate rows are
-//     stored 64-interleaved (chunk w of slot c at ((c/64)*n2 + w)*64 + c%64): the 64 lanes of
-//     a wave write 64 consecutive slots, and the next level's lanes read siblings with
-//     consecutive slots, so both directions are coalesced 1 KB accesses;
+//     child bitmap array at the CANDIDATE index (fire-and-forget stores; a row that fits one
+//     load batch is held until its count is known, so only survivors' rows are written).
+//     Child rows then reach their bitmap through FLevel::slot, so there is no compaction pass at
+//     all.  Candidate rows are stored 64-interleaved (chunk w of slot c at ((c/64)*n2 + w)*64 +
+//     c%64): the 64 lanes of a wave write 64 consecutive slots, and the next level's lanes read
+//     siblings with consecutive slots, so both directions are coalesced 1 KB accesses;
 //   * the root level (pair counts from the gram) computes AND rows only for survivors.
-// Decode, look-back, trie/host writes and the tile→row map are shared with k_level_count.
+// Decode, look-back, trie/host writes and the next level's layout are shared with k_level_count.
 constexpr int kSmallChunks = 32;
 
 template <int KB>
@@ -611,18 +692,19 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
                                                               FLevel* __restrict__ nx, FCtl* ctl,
                                                               unsigned long long* __restrict__ status,
                                                               unsigned epoch, LevelCountArgs A,
-                                                              const int32_t* __restrict__ tile_row) {
+                                                              const int32_t* __restrict__ tile_row,
+                                                              int32_t* __restrict__ tile_row_nx) {
   __shared__ int64_t s_off[kWin];
-  __shared__ int64_t s_w[kBlock / 64];
   __shared__ int64_t s_r0;
-  __shared__ int64_t s_base;
   __shared__ int64_t s_ticket;
+  __shared__ EpiSmem epi;
   // Every descriptor field the first tile needs, loaded as one batch before the first branch
   // (an early-return on ctl->overflow first made these a chain of dependent round trips — about
   // a microsecond each, on every launch), plus the tile→row entry of this block's tile in
   // block-index mode (bid < grid <= status_cap, so the speculative load stays in bounds).
   const unsigned ovf = ctl->overflow;
   const unsigned ebase = ctl->epoch_base;
+  const int64_t scap = (int64_t)ctl->status_cap;
   const int64_t n_cand = lv->n_cand;
   const int64_t n_rows = lv->n_rows;
   const int64_t child_base = lv->child_base;
@@ -631,12 +713,11 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
   const int32_t* __restrict__ slot = lv->slot;
   const int32_t* __restrict__ rank = lv->rank;
   const int64_t* __restrict__ gid = lv->gid;
-  int64_t* __restrict__ row_end = lv->row_end;
   ulonglong2* __restrict__ cbm2 = (ulonglong2*)nx->bm;
   int32_t* __restrict__ crank = (int32_t*)nx->rank;
   int64_t* __restrict__ cgid = (int64_t*)nx->gid;
-  int32_t* __restrict__ cprow = (int32_t*)nx->prow;
   int32_t* __restrict__ cslot = (int32_t*)nx->slot;
+  int64_t* __restrict__ co_nx = nx->cand_off;
   const int cbk = A.deferred_dl ? A.copy_blocks : 0;  // copy blocks (lead the grid by default)
   const int64_t tgrid = (int64_t)gridDim.x - cbk;     // tile blocks
   const int64_t cb0 = A.copy_last ? tgrid : 0;
@@ -645,9 +726,8 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
   const int32_t r0_spec = (tile_row && !copy_role) ? tile_row[bid] : 0;
   // keep the batch above the branch (the compiler otherwise sinks each load to its first use)
   asm volatile("" ::"s"(n_cand), "s"(n_rows), "s"(child_base), "s"(co), "s"(bm2), "s"(slot),
-               "s"(rank), "s"(gid), "s"(row_end));
-  asm volatile("" ::"s"(cbm2), "s"(crank), "s"(cgid), "s"(cprow), "s"(cslot), "s"(r0_spec),
-               "s"(ebase));
+               "s"(rank), "s"(gid));
+  asm volatile("" ::"s"(cbm2), "s"(crank), "s"(cgid), "s"(cslot), "s"(r0_spec), "s"(ebase));
   if (ovf) return;
   epoch = (ebase + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
   if (copy_role) {
@@ -656,12 +736,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
   }
   const int64_t n_tiles = (n_cand + kTile - 1) / kTile;
   if (n_tiles == 0) {
-    if (bid == 0 && threadIdx.x == 0) {
-      nx->n_rows = 0;
-      nx->child_base = child_base;
-      nx->cand_off = (int64_t*)bump(ctl, 8ull);
-      if (nx->cand_off) nx->cand_off[0] = 0;
-    }
+    if (bid == 0 && threadIdx.x == 0) empty_level(ctl, nx, child_base);
     return;
   }
   if (bid >= n_tiles) return;
@@ -673,7 +748,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
     if (tr) tr[0] = wall_clock64();
     const int64_t c0 = t * kTile;
     const int cn = (int)min((int64_t)kTile, n_cand - c0);
-    if (tile_row) {  // first row of the tile, recorded by this level's scan
+    if (tile_row) {  // first row of the tile, recorded by the previous level's count
       if (threadIdx.x == 0) s_r0 = (first && n_tiles <= tgrid) ? (int64_t)r0_spec : tile_row[t];
     } else if (threadIdx.x < 64) {  // root level: 64-ary search by wave 0
       const int64_t c = c0;
@@ -699,8 +774,8 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
     if (tr) tr[1] = wall_clock64();
     // ---- decode + phase 1: one thread per candidate, AND row written in place ----
     uint32_t k = 0;
-    int64_t a = 0, b = 0;
-    bool row_last = false;  // this thread's candidate is the last of its row
+    int32_t a = 0, b = 0;  // level rows are int32-indexed (the count kernels check the sizes)
+    bool head = false;  // this candidate is its owner's first
     const bool live = (int)threadIdx.x < cn;
     const int64_t c = c0 + threadIdx.x;
     if (live) {
@@ -711,19 +786,24 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
           const int64_t mid = (lo + hi) >> 1;
           if (s_off[mid] <= c) lo = mid; else hi = mid;
         }
-        a = r0 + lo;
+        b = (int32_t)(r0 + lo);
         oa = s_off[lo];
         ob = s_off[lo + 1];
       } else {
-        a = find_row_g(co, r0, n_rows, c);
-        oa = co[a];
-        ob = co[a + 1];
+        b = (int32_t)find_row_g(co, r0, n_rows, c);
+        oa = co[b];
+        ob = co[b + 1];
       }
-      row_last = c + 1 == ob;
-      b = a + 1 + (c - oa);
-      const bool need_row = A.gram ? (k = A.gram[a * A.F + b]) >= A.minsup : true;
+      head = c == oa;
+      a = (int32_t)(b - (ob - c));
+      bool need_row = true;
+      if (A.gram) {  // root: pair counts by rank (rows are in descending rank order)
+        const int64_t ra = rank[a], rb = rank[b];
+        k = A.gram[min(ra, rb) * A.F + max(ra, rb)];
+        need_row = k >= A.minsup;
+      }
       if (need_row) {
-        // parent rows: row-major at the root, 64-interleaved candidate slots below it
+        // parent rows: by rank at the root (row-major), 64-interleaved candidate slots below it
         const ulonglong2* __restrict__ x;
         const ulonglong2* __restrict__ y;
         int sxy;
@@ -733,8 +813,8 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
           y = bm2 + ((sb >> 6) * n2 << 6) + (sb & 63);
           sxy = 64;
         } else {
-          x = bm2 + a * n2;
-          y = bm2 + b * n2;
+          x = bm2 + (A.root ? (int64_t)rank[a] : a) * n2;
+          y = bm2 + (A.root ? (int64_t)rank[b] : b) * n2;
           sxy = 1;
         }
         ulonglong2* __restrict__ z = cbm2 + ((c >> 6) * n2 << 6) + (c & 63);
@@ -771,50 +851,32 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
         if (!A.gram) k = kk;
       }
     }
-    // ---- phase 2: survivor positions (block scan + look-back), trie + host writes ----
+    // ---- phase 2: survivor rows + next-level layout, trie + host writes ----
     const int flag = (live && k >= A.minsup) ? 1 : 0;
-    int64_t tile_total;
-    const int64_t lx = block_excl_scan(flag, s_w, &tile_total);
     if (tr) tr[2] = wall_clock64();
-    if (threadIdx.x < 64) {
-      const int64_t bb = lookback(status, t, epoch, tile_total, ctl);
-      if (threadIdx.x == 0) s_base = bb;
-    }
-    __syncthreads();
+    const int64_t s = tile_epilogue(epi, t, n_tiles, live, flag, head, status, epoch, ctl, nx,
+                                    co_nx, tile_row_nx, scap, child_base, n_cand, A.Wp, A.out_cap);
     if (tr) tr[3] = wall_clock64();
-    const int64_t base = s_base;
-    if (live) {
-      if (row_last) row_end[a] = base + lx + flag;
-      if (flag) {
-        const int64_t s = base + lx;
-        const int32_t rb = rank[b];
-        const int64_t node = child_base + s;
-        crank[s] = rb;
-        cgid[s] = node;
-        cprow[s] = (int32_t)a;
-        cslot[s] = (int32_t)c;
-        const int64_t par = gid[a];
-        const int32_t it = A.ids[rb];
-        A.out_parent[node] = par;
-        A.out_item[node] = it;
-        A.out_count[node] = k;
-        A.out_depth[node] = A.child_depth;
-        if (A.download && !A.deferred_dl) host_store(ctl->h, ctl, node, par, it, k, A.child_depth);
-      }
+    if (flag) {
+      const int32_t ra = rank[a];
+      const int64_t node = child_base + s;
+      crank[s] = ra;
+      cgid[s] = node;
+      cslot[s] = (int32_t)c;
+      const int64_t par = gid[b];
+      const int32_t it = A.ids[ra];
+      A.out_parent[node] = par;
+      A.out_item[node] = it;
+      A.out_count[node] = k;
+      A.out_depth[node] = A.child_depth;
+      if (A.download && !A.deferred_dl) host_store(ctl->h, ctl, node, par, it, k, A.child_depth);
     }
     if (tr) tr[4] = wall_clock64();
-    if (t == n_tiles - 1 && threadIdx.x == 0) {
-      const int64_t S = base + tile_total;
-      nx->n_rows = S;
-      nx->child_base = child_base + S;
-      nx->cand_off = (int64_t*)bump(ctl, (unsigned long long)(S + 1) * 8ull);
-      atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
-    }
     if (tr) tr[5] = wall_clock64();
     __syncthreads();
     if (tr) {
       tr[6] = wall_clock64();
-      tr[7] = (unsigned long long)tile_total | ((unsigned long long)cn << 32);
+      tr[7] = (unsigned long long)cn;
     }
   }
 }
@@ -1043,12 +1105,13 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
   __shared__ int64_t s_scan[1024];
   __shared__ int64_t s_carry;
   const int64_t F = desc[1].n_rows;
-  // root candidate offsets: every class owned → closed form; else a block scan of the owned
-  // classes' lengths (F - a - 1)
+  // root rows in descending rank (row r = frequent item of rank F-1-r); row r owns its pairs
+  // with the r rows before it (owner-major order, see the header).  Every class owned → closed
+  // form; else a block scan of the owned rows' lengths (row r ↔ root class of rank F-1-r)
   int64_t n_cand;
   if (a.world <= 1) {
     n_cand = F * (F - 1) / 2;
-    for (int64_t i = threadIdx.x; i <= F; i += blockDim.x) a.cand_off[i] = i * (2 * F - i - 1) / 2;
+    for (int64_t i = threadIdx.x; i <= F; i += blockDim.x) a.cand_off[i] = i * (i - 1) / 2;
   } else {
     if (threadIdx.x == 0) s_carry = 0;
     __syncthreads();
@@ -1056,10 +1119,10 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
       const int64_t i = base + threadIdx.x;
       int64_t v = 0;
       if (i < F) {
-        const int64_t k = a.prank[i];  // cost rank from level_partition (k_rank_desc)
+        const int64_t k = a.prank[F - 1 - i];  // cost rank from level_partition (k_rank_desc)
         const int64_t rnd = k / a.world, p = k % a.world;
         const int64_t owner = (rnd % 2 == 0) ? p : a.world - 1 - p;
-        v = owner == a.my_rank ? F - i - 1 : 0;
+        v = owner == a.my_rank ? i : 0;
       }
       s_scan[threadIdx.x] = v;
       __syncthreads();
@@ -1086,31 +1149,21 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     r.child_base = F;
     desc[0].child_base = 0;  // level-1 trie nodes [0, F) for the copy-out of "level 0"
     ok = 1;
-    if (F + n_cand > a.out_cap || (n_cand + kTile - 1) / kTile > (int64_t)ctl->status_cap) {
+    if (F + n_cand > a.out_cap || (n_cand + kTile - 1) / kTile > (int64_t)ctl->status_cap ||
+        n_cand > (int64_t)INT32_MAX) {
       atomicExch(&ctl->overflow, 4u);
       ok = 0;
-    } else if (n_cand > 0) {
-      const unsigned long long T = (unsigned long long)n_cand;
-      const unsigned long long T64 = (T + 63ull) & ~63ull;  // 64-interleaved candidate rows
-      const unsigned long long sz[6] = {(unsigned long long)F * 8ull,
-                                        T64 * (unsigned long long)a.Wp * 8ull, T * 4ull,
-                                        T * 8ull, T * 4ull, T * 4ull};
-      void* p[6];
-      bump_n<6>(ctl, sz, p);
-      r.row_end = (int64_t*)p[0];
-      desc[2].bm = (const uint64_t*)p[1];
-      desc[2].rank = (const int32_t*)p[2];
-      desc[2].gid = (const int64_t*)p[3];
-      desc[2].prow = (const int32_t*)p[4];
-      desc[2].slot = (const int32_t*)p[5];
+    } else {
+      alloc_level(ctl, &desc[2], n_cand, a.Wp);
       if (ctl->overflow) ok = 0;
     }
   }
   __syncthreads();
   if (!ok) return;
   for (int64_t i = threadIdx.x; i < F; i += blockDim.x) {
-    a.rank[i] = (int32_t)i;
-    a.gid[i] = i;
+    // row i ↔ rank F-1-i; level-1 trie node ids stay the ranks
+    a.rank[i] = (int32_t)(F - 1 - i);
+    a.gid[i] = F - 1 - i;
     a.out_parent[i] = -1;
     a.out_item[i] = a.ids[i];
     a.out_count[i] = a.fcounts[i];
@@ -1136,17 +1189,9 @@ int team_size_for(int64_t Wp) {  // lanes per candidate: ~4-8 16-byte chunks per
 
 int level_grid(int n_cus) { return std::max(64, n_cus * 8); }  // 8 x 256-thread blocks per CU
 
-void level_scan(FLevel* pv, FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status,
-                unsigned epoch, int64_t Wp, int64_t out_cap, int32_t* tile_row, int grid,
-                hipStream_t s) {
-  hipLaunchKernelGGL(k_level_scan, dim3(grid), dim3(kBlock), 0, s, pv, lv, nx, ctl, status, epoch,
-                     Wp, out_cap, tile_row);
-  KMLS_HIP(hipGetLastError());
-}
-
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
-                 const LevelCountArgs& a, const int32_t* tile_row, int grid, int64_t cand_hint,
-                 hipStream_t s) {
+                 const LevelCountArgs& a, const int32_t* tile_row, int32_t* tile_row_nx, int grid,
+                 int64_t cand_hint, hipStream_t s) {
   if (a.deferred_dl) grid += a.copy_blocks;
   static const bool small_ok = [] {
     const char* e = std::getenv("KMLS_COUNT_SMALL");
@@ -1167,19 +1212,19 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
     }();
     if (kb18 && cand_hint >= 0 && cand_hint <= kb18_tiles * kTile && n2 <= 18)
       hipLaunchKernelGGL(k_level_count_small<18>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl,
-                         status, epoch, a, tile_row);
+                         status, epoch, a, tile_row, tile_row_nx);
     else
       hipLaunchKernelGGL(k_level_count_small<6>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl,
-                         status, epoch, a, tile_row);
+                         status, epoch, a, tile_row, tile_row_nx);
     KMLS_HIP(hipGetLastError());
     return;
   }
   switch (team_size_for(a.Wp)) {
-    case 4: hipLaunchKernelGGL(k_level_count<4>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
-    case 8: hipLaunchKernelGGL(k_level_count<8>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
-    case 16: hipLaunchKernelGGL(k_level_count<16>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
-    case 32: hipLaunchKernelGGL(k_level_count<32>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
-    default: hipLaunchKernelGGL(k_level_count<64>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row); break;
+    case 4: hipLaunchKernelGGL(k_level_count<4>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row, tile_row_nx); break;
+    case 8: hipLaunchKernelGGL(k_level_count<8>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row, tile_row_nx); break;
+    case 16: hipLaunchKernelGGL(k_level_count<16>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row, tile_row_nx); break;
+    case 32: hipLaunchKernelGGL(k_level_count<32>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row, tile_row_nx); break;
+    default: hipLaunchKernelGGL(k_level_count<64>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl, status, epoch, a, tile_row, tile_row_nx); break;
   }
   KMLS_HIP(hipGetLastError());
 }
@@ -1241,7 +1286,6 @@ void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream
 }
 
 int64_t level_tile() { return kTile; }
-int64_t level_scan_tile() { return kScanTile; }
 
 }  // namespace kern
 }  // namespace kmls
