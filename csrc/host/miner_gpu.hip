@@ -456,7 +456,8 @@ struct MineRun {
       kern::LevelCountArgs a{Wp, minsup, L == 1 ? gram : nullptr, F, d_ids, out_parent.p,
                              out_item.p, out_count.p, out_depth.p, (uint8_t)(L + 1),
                              stream_dl, L == trace_level ? d_trace : nullptr, deferred,
-                             copy_blocks(), copy_last(), L == 1, out_cap};
+                             copy_blocks(), copy_last(), L == 1, out_cap,
+                             max_len > 0 && L + 1 >= max_len};
       const int64_t hint = hint_at(ob->cand_hint, L);
       const int g = grid_for_tiles(hint < 0 ? -1 : (hint + kern::level_tile() - 1) / kern::level_tile());
       // the count kernels load tile_row[block] speculatively: every block index must be in bounds

@@ -163,6 +163,7 @@ struct LevelCountArgs {
   bool copy_last;   // copy blocks at the end of the grid instead of leading it (A/B)
   bool root;        // level 1: rows = frequent items in descending rank, bitmap rows by rank
   int64_t out_cap;  // device trie capacity (nodes)
+  bool leaf;        // last level allowed by max_len: survivors only, no next-level layout
 };
 // Few copy blocks on purpose: GPU writes to pinned host memory share the L2 -> fabric write path
 // with the tiles' HBM stores, and a saturated PCIe link backs that path up (a level-6 trace showed

@@ -411,7 +411,8 @@ struct EpiSmem {
 __device__ int64_t tile_epilogue(EpiSmem& sm, int64_t t, int64_t n_tiles, bool live, int flag,
                                  bool head, unsigned long long* status, unsigned epoch, FCtl* ctl,
                                  FLevel* nx, int64_t* co_nx, int32_t* tile_row_nx, int64_t scap,
-                                 int64_t child_base, int64_t n_cand, int64_t Wp, int64_t out_cap) {
+                                 int64_t child_base, int64_t n_cand, int64_t Wp, int64_t out_cap,
+                                 bool leaf) {
   const int tid = threadIdx.x;
   if (tid == 0) sm.fh = kBlock;
   int64_t S;
@@ -441,7 +442,8 @@ __device__ int64_t tile_epilogue(EpiSmem& sm, int64_t t, int64_t n_tiles, bool l
   }
   __syncthreads();
   int64_t s = -1;
-  if (flag) {
+  if (flag && leaf) s = sm.base + sm.lx[tid];  // max_len reached: no next level to lay out
+  if (flag && !leaf) {
     const int64_t base = sm.base, cex = sm.cex, carry = sm.carry;
     const int64_t l = sm.lx[tid];
     const bool cont = sm.hp[tid] < 0;  // in the segment continuing from the previous tile
@@ -462,9 +464,10 @@ __device__ int64_t tile_epilogue(EpiSmem& sm, int64_t t, int64_t n_tiles, bool l
     const int64_t Ct = sm.cex + C0 + carry * Fh;
     nx->n_rows = St;
     nx->child_base = child_base + St;
-    nx->n_cand = Ct;
-    co_nx[St] = Ct;
+    nx->n_cand = leaf ? 0 : Ct;
     atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
+    if (leaf) return s;
+    co_nx[St] = Ct;
     if (child_base + St + Ct > out_cap || (Ct + kTile - 1) / kTile > scap ||
         St > (int64_t)INT32_MAX || Ct > (int64_t)INT32_MAX)
       atomicExch(&ctl->overflow, 4u);
@@ -631,7 +634,8 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
     // ---- phase 2: survivor rows + next-level layout (block scans + segmented look-back) ----
     const int flag = (live && s_cnt[threadIdx.x] >= A.minsup) ? 1 : 0;
     const int64_t s = tile_epilogue(epi, t, n_tiles, live, flag, head, status, epoch, ctl, nx,
-                                    co_nx, tile_row_nx, scap, child_base, n_cand, Wp, A.out_cap);
+                                    co_nx, tile_row_nx, scap, child_base, n_cand, Wp, A.out_cap,
+                                    A.leaf);
     s_row[threadIdx.x] = s;
     if (flag) {  // per-survivor scalars: one thread each
       const int64_t a = s_a[threadIdx.x], b = s_b[threadIdx.x];
@@ -655,7 +659,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
       const int i = team * kPer + j;
       if (i >= cn) break;
       const int64_t srow = s_row[i];
-      if (srow < 0) continue;  // team-uniform
+      if (srow < 0 || A.leaf) continue;  // team-uniform
       const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + brow(s_a[i]) * Wp);
       const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + brow(s_b[i]) * Wp);
       ulonglong2* z = reinterpret_cast<ulonglong2*>(cbm + srow * Wp);
@@ -800,7 +804,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
       if (A.gram) {  // root: pair counts by rank (rows are in descending rank order)
         const int64_t ra = rank[a], rb = rank[b];
         k = A.gram[min(ra, rb) * A.F + max(ra, rb)];
-        need_row = k >= A.minsup;
+        need_row = k >= A.minsup && !A.leaf;
       }
       if (need_row) {
         // parent rows: by rank at the root (row-major), 64-interleaved candidate slots below it
@@ -841,7 +845,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
               u[q] = make_ulonglong2(u[q].x & v[q].x, u[q].y & v[q].y);
               kk += (uint32_t)__popcll(u[q].x) + (uint32_t)__popcll(u[q].y);
             }
-          const bool keep = !one_batch || A.gram || kk >= A.minsup;
+          const bool keep = !A.leaf && (!one_batch || A.gram || kk >= A.minsup);
           if (keep) {
 #pragma unroll
             for (int q = 0; q < kB; ++q)
@@ -855,7 +859,8 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
     const int flag = (live && k >= A.minsup) ? 1 : 0;
     if (tr) tr[2] = wall_clock64();
     const int64_t s = tile_epilogue(epi, t, n_tiles, live, flag, head, status, epoch, ctl, nx,
-                                    co_nx, tile_row_nx, scap, child_base, n_cand, A.Wp, A.out_cap);
+                                    co_nx, tile_row_nx, scap, child_base, n_cand, A.Wp, A.out_cap,
+                                    A.leaf);
     if (tr) tr[3] = wall_clock64();
     if (flag) {
       const int32_t ra = rank[a];
