@@ -142,7 +142,7 @@ struct OutBufs {
   hipStream_t copy_s = nullptr;
   hipEvent_t ev = nullptr;
   // fused level path (levels.hip): look-back status words (epoch-tagged, zeroed once)
-  unsigned long long* status = nullptr;  // [3 * status_cap]: three words per tile (SegAgg)
+  unsigned long long* status = nullptr;  // [2 * status_cap]: two words per tile (SegAgg)
   int32_t* tile_row = nullptr;   // [2][status_cap] count tile → first row, by level parity
   unsigned long long* trace = nullptr;  // KMLS_LEVEL_TRACE diagnostics ([status_cap][8])
   int64_t status_cap = 1 << 20;  // tiles per launch (256M candidates / 2G rows)
@@ -155,17 +155,17 @@ struct OutBufs {
     KMLS_HIP(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
     // device-scope release: a cross-stream fork needs no system-scope L2 writeback
     KMLS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice));
-    KMLS_HIP(hipMalloc((void**)&status, (size_t)status_cap * 3 * sizeof(unsigned long long)));
-    KMLS_HIP(hipMemset(status, 0, (size_t)status_cap * 3 * sizeof(unsigned long long)));
+    KMLS_HIP(hipMalloc((void**)&status, (size_t)status_cap * 2 * sizeof(unsigned long long)));
+    KMLS_HIP(hipMemset(status, 0, (size_t)status_cap * 2 * sizeof(unsigned long long)));
     KMLS_HIP(hipMalloc((void**)&tile_row, (size_t)status_cap * 2 * sizeof(int32_t)));
   }
-  static constexpr unsigned kLaunchesPerCall = 256;
-  // start a fused call: a fresh 256-tag window (the 24-bit tag wraps after ~65k calls: then the
+  static constexpr unsigned kLaunchesPerCall = 64;  // level launches per call (<= 61 levels)
+  // start a fused call: a fresh 64-tag window (the 16-bit tag wraps after 1024 calls: then the
   // status words are zeroed so no stale word can match)
   unsigned begin_call(hipStream_t s) {
     epoch_base += kLaunchesPerCall;
-    if (epoch_base + kLaunchesPerCall >= (1u << 24)) {
-      KMLS_HIP(hipMemsetAsync(status, 0, (size_t)status_cap * 3 * sizeof(unsigned long long), s));
+    if (epoch_base + kLaunchesPerCall >= (1u << 16)) {
+      KMLS_HIP(hipMemsetAsync(status, 0, (size_t)status_cap * 2 * sizeof(unsigned long long), s));
       epoch_base = kLaunchesPerCall;
     }
     launch_idx = 0;

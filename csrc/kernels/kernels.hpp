@@ -233,7 +233,7 @@ void level_copyout(const FLevel* lv, const FLevel* nx, FCtl* ctl, const int64_t*
 // count level L (lv = &desc[L], nx = &desc[L+1]; desc[L+2] receives the next buffers).
 // tile_row: count tile → first row of level L, written by count(L-1) (nullptr at the root);
 // tile_row_nx: the same map for level L+1, written here (double-buffered by the caller).
-// status: 3 words per tile.
+// status: 2 words per tile.
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
                  const LevelCountArgs& a, const int32_t* tile_row, int32_t* tile_row_nx, int grid,
                  int64_t cand_hint, hipStream_t s);

@@ -54,7 +54,7 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kTile = 256;              // candidates per count tile
 constexpr int kWin = 1024;              // LDS cand_off window (rows) per count tile
-constexpr unsigned long long kValMask = (1ull << 38) - 1;
+constexpr unsigned long long kValMask = (1ull << 46) - 1;  // status word payload
 constexpr long long kSpinLimit = 1ll << 26;
 
 __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
@@ -63,11 +63,14 @@ __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long lon
 __device__ __forceinline__ void st_relaxed(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// status word: epoch:16 | flag:2 (1 aggregate, 2 inclusive prefix) | payload:46
 __device__ __forceinline__ unsigned long long pack(unsigned epoch, unsigned flag,
                                                    unsigned long long v) {
-  return ((unsigned long long)(epoch & 0xFFFFFFu) << 40) | ((unsigned long long)flag << 38) |
+  return ((unsigned long long)(epoch & 0xFFFFu) << 48) | ((unsigned long long)flag << 46) |
          (v & kValMask);
 }
+__device__ __forceinline__ unsigned w_epoch(unsigned long long w) { return (unsigned)(w >> 48); }
+__device__ __forceinline__ unsigned w_flag(unsigned long long w) { return (unsigned)(w >> 46) & 3u; }
 
 // Tile aggregate of the segmented scan that lays out the next level (a segment = the survivors
 // of one owner row b; segments start at the owner's first candidate, a "head"):
@@ -99,28 +102,66 @@ __device__ __forceinline__ SegAgg seg_shfl_xor(const SegAgg& v, int off) {
   p.H = __shfl_xor((int)v.H, off, 64) != 0;
   return p;
 }
-// three words per tile: S | C | aggregate (H:1 @37, F:18 @18, O:18 @0) or prefix O
+// Two words per tile.  An aggregate fits ONE word (S, O, F <= 256 and C <= 256*255/2: 9+9+9+1+15
+// bits), so the common case of the look-back reads one word per predecessor; an inclusive prefix
+// (S, C, O < 2^28: a level has at most status_cap * 256 = 2^28 candidates) spans both, w1 written
+// before w0 and accepted only when both carry the flag.
 __device__ __forceinline__ void seg_publish(unsigned long long* my, unsigned e, unsigned flag,
                                             const SegAgg& v) {
-  const unsigned long long w2 =
-      flag == 2 ? (unsigned long long)v.O
-                : ((unsigned long long)v.H << 37) | ((unsigned long long)v.F << 18) |
-                      (unsigned long long)v.O;
-  st_relaxed(my + 0, pack(e, flag, (unsigned long long)v.S));
-  st_relaxed(my + 1, pack(e, flag, (unsigned long long)v.C));
-  st_relaxed(my + 2, pack(e, flag, w2));
+  if (flag == 1) {
+    st_relaxed(my, pack(e, 1, (unsigned long long)v.S | ((unsigned long long)v.O << 9) |
+                                  ((unsigned long long)v.F << 18) | ((unsigned long long)v.H << 27) |
+                                  ((unsigned long long)v.C << 28)));
+  } else {
+    const unsigned long long o = (unsigned long long)v.O;
+    st_relaxed(my + 1, pack(e, 2, (unsigned long long)v.C | ((o >> 18) << 28)));
+    st_relaxed(my, pack(e, 2, (unsigned long long)v.S | ((o & 0x3FFFFull) << 28)));
+  }
+}
+__device__ __forceinline__ bool seg_valid(unsigned long long w0, unsigned long long w1, unsigned e) {
+  const unsigned f = w_flag(w0);
+  return w_epoch(w0) == e && f != 0 && (f == 1 || (w_epoch(w1) == e && w_flag(w1) == 2));
+}
+__device__ __forceinline__ SegAgg seg_decode(unsigned long long w0, unsigned long long w1) {
+  SegAgg v;
+  const unsigned long long x = w0 & kValMask;
+  if (w_flag(w0) == 1) {
+    v.S = (int32_t)(x & 0x1FFull);
+    v.O = (int32_t)((x >> 9) & 0x1FFull);
+    v.F = (int32_t)((x >> 18) & 0x1FFull);
+    v.H = (x >> 27) & 1ull;
+    v.C = (int64_t)(x >> 28);
+  } else {
+    const unsigned long long y = w1 & kValMask;
+    v.S = (int32_t)(x & 0xFFFFFFFull);
+    v.O = (int32_t)((x >> 28) | ((y >> 28) << 18));
+    v.F = 0;
+    v.H = true;
+    v.C = (int64_t)(y & 0xFFFFFFFull);
+  }
+  return v;
+}
+// fold of the 64 lanes' values, the higher lane (older tile) always the left operand (an xor
+// butterfly: every lane ends with the whole fold)
+__device__ __forceinline__ SegAgg wave_fold(SegAgg v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll 1
+  for (int off = 1; off < 64; off <<= 1) {
+    const SegAgg p = seg_shfl_xor(v, off);
+    v = (lane & off) ? seg_cat(v, p) : seg_cat(p, v);
+  }
+  return v;
 }
 
 // Wave-parallel decoupled look-back for tile t (called by all 64 lanes of wave 0): each round
-// inspects 64 predecessors at once (lane 0 = nearest), folds them newest-last up to the nearest
-// inclusive prefix (an xor butterfly in which the higher lane — the older tile — is always the
-// left operand), and only spins while one of those is unpublished or half-written (its three
-// words must agree on epoch and flag).  Returns the tile's exclusive prefix (every lane).
+// inspects 64 predecessors at once (lane 0 = nearest), folds them up to the nearest inclusive
+// prefix, and only spins while one of those is unpublished or half-written.  Returns the tile's
+// exclusive prefix (every lane).
 __device__ SegAgg lookback_seg(unsigned long long* st, int64_t t, unsigned epoch, const SegAgg& agg,
                                FCtl* ctl) {
-  const unsigned e = epoch & 0xFFFFFFu;
+  const unsigned e = epoch & 0xFFFFu;
   const int lane = threadIdx.x & 63;
-  unsigned long long* my = st + 3 * t;
+  unsigned long long* my = st + 2 * t;
   const SegAgg zero{0, 0, 0, false, 0};
   if (t == 0) {
     if (lane == 0) seg_publish(my, e, 2, agg);
@@ -132,19 +173,13 @@ __device__ SegAgg lookback_seg(unsigned long long* st, int64_t t, unsigned epoch
   long long spins = 0;
   while (true) {
     const int64_t j = end - 1 - lane;
-    unsigned long long w0, w1, w2;
+    unsigned long long w0 = pack(e, 2, 0), w1 = w0;  // virtual P(0) before tile 0
     if (j >= 0) {
-      w0 = ld_relaxed(st + 3 * j);
-      w1 = ld_relaxed(st + 3 * j + 1);
-      w2 = ld_relaxed(st + 3 * j + 2);
-    } else {  // virtual P(0) before tile 0
-      w0 = w1 = w2 = pack(e, 2, 0);
+      w0 = ld_relaxed(st + 2 * j);
+      w1 = ld_relaxed(st + 2 * j + 1);
     }
-    const unsigned f0 = (unsigned)(w0 >> 38) & 3u;
-    const bool valid = (unsigned)(w0 >> 40) == e && (unsigned)(w1 >> 40) == e &&
-                       (unsigned)(w2 >> 40) == e && f0 != 0 &&
-                       ((unsigned)(w1 >> 38) & 3u) == f0 && ((unsigned)(w2 >> 38) & 3u) == f0;
-    const unsigned long long pmask = __ballot(valid && f0 == 2);
+    const bool valid = seg_valid(w0, w1, e);
+    const unsigned long long pmask = __ballot(valid && w_flag(w0) == 2);
     const unsigned long long imask = __ballot(!valid);
     const int first_p = pmask ? __builtin_ctzll(pmask) : 64;
     const unsigned long long need = first_p >= 63 ? ~0ull : ((1ull << (first_p + 1)) - 1ull);
@@ -156,26 +191,7 @@ __device__ SegAgg lookback_seg(unsigned long long* st, int64_t t, unsigned epoch
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    SegAgg v = zero;
-    if (lane <= first_p) {
-      v.S = (int32_t)(w0 & kValMask);
-      v.C = (int64_t)(w1 & kValMask);
-      const unsigned long long x = w2 & kValMask;
-      if (f0 == 2) {
-        v.O = (int32_t)x;
-        v.H = true;
-      } else {
-        v.O = (int32_t)(x & 0x3FFFFull);
-        v.F = (int32_t)((x >> 18) & 0x3FFFFull);
-        v.H = (x >> 37) & 1ull;
-      }
-    }
-#pragma unroll 1
-    for (int off = 1; off < 64; off <<= 1) {
-      const SegAgg p = seg_shfl_xor(v, off);
-      v = (lane & off) ? seg_cat(v, p) : seg_cat(p, v);
-    }
-    acc = seg_cat(v, acc);
+    acc = seg_cat(wave_fold(lane <= first_p ? seg_decode(w0, w1) : zero), acc);
     if (first_p < 64) break;
     end -= 64;
   }
@@ -375,106 +391,148 @@ __device__ void alloc_level(FCtl* ctl, FLevel* nx, int64_t T, int64_t Wp) {
   nx->cand_off = (int64_t*)p[4];
 }
 
-__device__ __forceinline__ int block_incl_max(int v, int32_t* s_wm) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int x = v;
+struct EpiSmem {
+  uint8_t fl[kBlock];     // per candidate: bit 0 survivor, bit 1 its owner's first candidate
+  int64_t srow[kBlock];   // per candidate: survivor's next-level row (-1: failed)
+};
+
+// Wave-inclusive scan helpers (64 lanes)
+__device__ __forceinline__ int32_t wave_incl_sum(int32_t x) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(x, off, 64);
-    if (lane >= off) x = max(x, y);
+    const int32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
   }
-  if (lane == 63) s_wm[w] = x;
-  __syncthreads();
+  return x;
+}
+__device__ __forceinline__ int64_t wave_incl_sum64(int64_t x) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int i = 0; i < kBlock / 64; ++i)
-    if (i < w) x = max(x, s_wm[i]);
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
   return x;
 }
 
-struct EpiSmem {
-  int64_t w1[kBlock / 64], w2[kBlock / 64];
-  int32_t wm[kBlock / 64];
-  int32_t lx[kBlock];    // survivors before each candidate in the tile
-  int32_t hp[kBlock];    // last head at or before it (-1: continuing segment)
-  int32_t len0[kBlock];  // earlier siblings of its survivor inside the tile's span
-  int64_t cl[kBlock];    // candidates of the tile's earlier survivors (carry 0)
-  int fh, lh;
-  int64_t base, cex, carry;
-};
-
-// Survivor layout of one count tile and the next level's candidate layout (thread i = candidate
-// i of the tile; every thread of the block calls this).  Returns the survivor's row index in the
-// next level (-1 when the candidate failed) after writing its candidate offset and tile→row
-// entries; the last tile sets the next level's sizes and allocates its children's buffers.
-// Per-candidate intermediates go through LDS so that little stays live in registers across the
-// look-back (its fold is the register peak of the count kernels).
+// Survivor layout of one count tile and the next level's candidate layout.  Every thread of the
+// block calls this with its candidate's flags (thread i = candidate i of the tile); WAVE 0 alone
+// does the tile's scans with shuffles (4 candidates per lane: survivors before each candidate,
+// the segmented count of earlier siblings, their prefix), publishes the aggregate, runs the
+// look-back and writes the next level's candidate offsets and tile→row entries, so the block
+// meets only twice.  Returns the survivor's row index in the next level (-1: failed); the last
+// tile sets the next level's sizes and allocates its children's buffers (not at a leaf level).
 __device__ int64_t tile_epilogue(EpiSmem& sm, int64_t t, int64_t n_tiles, bool live, int flag,
                                  bool head, unsigned long long* status, unsigned epoch, FCtl* ctl,
                                  FLevel* nx, int64_t* co_nx, int32_t* tile_row_nx, int64_t scap,
                                  int64_t child_base, int64_t n_cand, int64_t Wp, int64_t out_cap,
                                  bool leaf) {
   const int tid = threadIdx.x;
-  if (tid == 0) sm.fh = kBlock;
-  int64_t S;
-  const int64_t lx = block_excl_scan(flag, sm.w1, &S);
-  const int hv = (live && head) ? tid : -1;
-  const int hp = block_incl_max(hv, sm.wm);  // last head at or before this candidate
-  sm.lx[tid] = (int32_t)lx;
-  sm.hp[tid] = hp;
-  if (hv >= 0) atomicMin(&sm.fh, hv);
-  if (tid == kBlock - 1) sm.lh = hp;
+  sm.fl[tid] = (uint8_t)((flag ? 1 : 0) | ((live && head) ? 2 : 0));
   __syncthreads();
-  const int fh = sm.fh, lh = sm.lh;
-  const bool H = fh < kBlock;
-  const int64_t Fh = H ? (int64_t)sm.lx[fh] : S;
-  const int64_t O = H ? S - (int64_t)sm.lx[lh] : S;
-  const int32_t len0 = flag ? (hp < 0 ? (int32_t)lx : (int32_t)lx - sm.lx[hp]) : 0;
-  sm.len0[tid] = len0;
-  int64_t C0;
-  sm.cl[tid] = block_excl_scan((int64_t)len0, sm.w2, &C0);
   if (tid < 64) {
-    const SegAgg p = lookback_seg(status, t, epoch, SegAgg{(int32_t)S, (int32_t)O, (int32_t)Fh, H, C0}, ctl);
-    if (tid == 0) {
-      sm.base = p.S;
-      sm.cex = p.C;
-      sm.carry = p.O;
+    const int lane = tid;
+    const uint32_t packed = *reinterpret_cast<const uint32_t*>(&sm.fl[4 * lane]);
+    int f[4], h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = (packed >> (8 * j)) & 1;
+      h[j] = (packed >> (8 * j + 1)) & 1;
+    }
+    const int nf = f[0] + f[1] + f[2] + f[3];
+    const bool lh_any = (h[0] | h[1] | h[2] | h[3]) != 0;
+    // survivors in this lane after its last head (all of them without a head)
+    int tail = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tail = h[j] ? f[j] : tail + f[j];
+    const int32_t incl = wave_incl_sum(nf);
+    const int32_t lx0 = incl - nf;               // survivors before this lane
+    const int32_t S = __shfl(incl, 63, 64);
+    const unsigned long long hmask = __ballot(lh_any);
+    // open-segment survivors entering this lane: from the nearest earlier lane with a head
+    // (its tail, plus every survivor of the lanes in between), or from the tile start
+    const unsigned long long before = hmask & ((1ull << lane) - 1ull);
+    const int src = before ? 63 - __builtin_clzll(before) : -1;
+    const int32_t tail_src = __shfl(tail, src < 0 ? 0 : src, 64);
+    const int32_t incl_src = __shfl(incl, src < 0 ? 0 : src, 64);
+    const int32_t run0 = src < 0 ? lx0 : tail_src + (lx0 - incl_src);
+    // this lane's items: earlier siblings inside the tile's span (len0) and their sum
+    int32_t lsum = 0, before_first = lx0;
+    {
+      int32_t run = run0, l = lx0;
+      bool seen = false;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (h[j]) {
+          run = 0;
+          if (!seen) before_first = l;
+          seen = true;
+        }
+        if (f[j]) lsum += run;
+        run += f[j];
+        l += f[j];
+      }
+    }
+    const int64_t cincl = wave_incl_sum64(lsum);
+    const int64_t C0 = __shfl(cincl, 63, 64);
+    // tile aggregate: F = survivors before the first head, O = survivors since the last head
+    const bool H = hmask != 0;
+    int32_t Fh = S, O = S;
+    if (H) {
+      Fh = __shfl(before_first, __builtin_ctzll(hmask), 64);
+      O = __shfl(tail + (S - incl), 63 - __builtin_clzll(hmask), 64);  // last head lane on
+    }
+    const SegAgg p = lookback_seg(status, t, epoch, SegAgg{S, O, Fh, H, C0}, ctl);
+    const int64_t base = p.S, cex = p.C, carry = p.O;
+    // second pass over the lane's items (recomputed: little stays live across the look-back)
+    {
+      int32_t run = run0, l = lx0;
+      bool cont = src < 0;  // no head yet: the segment continuing from the previous tile
+      int64_t cl = cincl - lsum;  // candidates of this lane's earlier survivors (carry 0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int fj = (packed >> (8 * j)) & 1, hj = (packed >> (8 * j + 1)) & 1;
+        if (hj) {
+          run = 0;
+          cont = false;
+        }
+        int64_t srow = -1;
+        if (fj) {
+          srow = base + l;
+          if (!leaf) {
+            const int64_t len = run + (cont ? carry : 0);  // earlier siblings
+            const int64_t co = cex + cl + carry * (cont ? (int64_t)l : (int64_t)Fh);
+            co_nx[srow] = co;
+            for (int64_t c = (co + kTile - 1) / kTile; c * kTile < co + len; ++c)
+              if (c < scap) tile_row_nx[c] = (int32_t)srow;
+          }
+          cl += run;
+        }
+        sm.srow[4 * lane + j] = srow;
+        run += fj;
+        l += fj;
+      }
+    }
+    if (t == n_tiles - 1 && lane == 0) {
+      const int64_t St = base + S;
+      const int64_t Ct = cex + C0 + carry * Fh;
+      nx->n_rows = St;
+      nx->child_base = child_base + St;
+      nx->n_cand = leaf ? 0 : Ct;
+      atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
+      if (!leaf) {
+        co_nx[St] = Ct;
+        if (child_base + St + Ct > out_cap || (Ct + kTile - 1) / kTile > scap ||
+            Ct >= (1ll << 28))
+          atomicExch(&ctl->overflow, 4u);
+        else
+          alloc_level(ctl, nx + 1, Ct, Wp);
+      }
     }
   }
   __syncthreads();
-  int64_t s = -1;
-  if (flag && leaf) s = sm.base + sm.lx[tid];  // max_len reached: no next level to lay out
-  if (flag && !leaf) {
-    const int64_t base = sm.base, cex = sm.cex, carry = sm.carry;
-    const int64_t l = sm.lx[tid];
-    const bool cont = sm.hp[tid] < 0;  // in the segment continuing from the previous tile
-    const int64_t f = sm.fh < kBlock ? (int64_t)sm.lx[sm.fh] : 0;  // = Fh when a head exists
-    s = base + l;
-    const int64_t len = sm.len0[tid] + (cont ? carry : 0);                      // earlier siblings
-    const int64_t co = cex + sm.cl[tid] + carry * (cont ? l : f);  // its first candidate
-    co_nx[s] = co;
-    for (int64_t ct = (co + kTile - 1) / kTile; ct * kTile < co + len; ++ct)
-      if (ct < scap) tile_row_nx[ct] = (int32_t)s;
-  }
-  if (t == n_tiles - 1 && tid == 0) {
-    const int64_t base = sm.base, carry = sm.carry;
-    int64_t Ssum = 0, C0s = 0;
-    (void)Ssum;
-    (void)C0s;
-    const int64_t St = base + S;
-    const int64_t Ct = sm.cex + C0 + carry * Fh;
-    nx->n_rows = St;
-    nx->child_base = child_base + St;
-    nx->n_cand = leaf ? 0 : Ct;
-    atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
-    if (leaf) return s;
-    co_nx[St] = Ct;
-    if (child_base + St + Ct > out_cap || (Ct + kTile - 1) / kTile > scap ||
-        St > (int64_t)INT32_MAX || Ct > (int64_t)INT32_MAX)
-      atomicExch(&ctl->overflow, 4u);
-    else
-      alloc_level(ctl, nx + 1, Ct, Wp);
-  }
-  return s;
+  return sm.srow[tid];
 }
 
 // A level without candidates: empty next level, and a one-entry cand_off for the level after
@@ -505,7 +563,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   __shared__ int64_t s_ticket;
   __shared__ EpiSmem epi;
   if (ctl->overflow) return;
-  epoch = (ctl->epoch_base + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
+  epoch = (ctl->epoch_base + epoch) & 0xFFFFu;  // per-call base (FCtl) + launch index
   const int cbk = A.deferred_dl ? A.copy_blocks : 0;  // copy blocks (lead the grid by default)
   const int64_t tgrid = (int64_t)gridDim.x - cbk;     // tile blocks
   const int64_t cb0 = A.copy_last ? tgrid : 0;
@@ -692,7 +750,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
 constexpr int kSmallChunks = 32;
 
 template <int KB>
-__global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(FLevel* __restrict__ lv,
+__global__ __launch_bounds__(kBlock, KB <= 6 ? 4 : 1) void k_level_count_small(FLevel* __restrict__ lv,
                                                               FLevel* __restrict__ nx, FCtl* ctl,
                                                               unsigned long long* __restrict__ status,
                                                               unsigned epoch, LevelCountArgs A,
@@ -733,7 +791,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 5 : 1) void k_level_count_small(F
                "s"(rank), "s"(gid));
   asm volatile("" ::"s"(cbm2), "s"(crank), "s"(cgid), "s"(cslot), "s"(r0_spec), "s"(ebase));
   if (ovf) return;
-  epoch = (ebase + epoch) & 0xFFFFFFu;  // per-call base (FCtl) + launch index
+  epoch = (ebase + epoch) & 0xFFFFu;  // per-call base (FCtl) + launch index
   if (copy_role) {
     copy_prev_level(lv, ctl, A, (int)(blockIdx.x - cb0));
     return;
@@ -1155,7 +1213,7 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     desc[0].child_base = 0;  // level-1 trie nodes [0, F) for the copy-out of "level 0"
     ok = 1;
     if (F + n_cand > a.out_cap || (n_cand + kTile - 1) / kTile > (int64_t)ctl->status_cap ||
-        n_cand > (int64_t)INT32_MAX) {
+        n_cand >= (1ll << 28)) {
       atomicExch(&ctl->overflow, 4u);
       ok = 0;
     } else {
