@@ -282,6 +282,7 @@ struct MineRun {
   // caller's end_capture instantiates and launches it) or already launched as a replay
   bool graph_capture = false, graph_replay = false;
   int graph_last = 0;                        // replay: last level the graph enqueues
+  bool root_from_gram = false;                // level 2 was built by level_root_fill
   std::function<void(int)> end_capture;      // capture: called with the batch's last level
 
   explicit MineRun(OutBufs* o)
@@ -475,7 +476,7 @@ struct MineRun {
     if (graph_replay) {  // the replayed graph already holds count(1) .. count(graph_last)
       last = graph_last;
       target = graph_last;
-    } else {
+    } else if (!root_from_gram) {
       count_level(1);
     }
     if (!back) throw std::logic_error("levels_loop: no readback buffer (FCtl::rb_dst)");
@@ -1251,6 +1252,9 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   int32_t* d_rrank = (int32_t*)arena_->push((size_t)I * 4);
   int64_t* d_rgid = (int64_t*)arena_->push((size_t)I * 8);
   int64_t* d_roff = (int64_t*)arena_->push((size_t)(I + 1) * 8);
+  int32_t* d_m = (int32_t*)arena_->push((size_t)I * 4);         // gram-driven root (levels.hip)
+  int64_t* d_soff = (int64_t*)arena_->push((size_t)(I + 1) * 8);
+  int64_t* d_coff = (int64_t*)arena_->push((size_t)(I + 1) * 8);
   kern::FLevel* d_desc = (kern::FLevel*)arena_->push(kMaxLv * sizeof(kern::FLevel));
   kern::FCtl* d_ctl = (kern::FCtl*)arena_->push(sizeof(kern::FCtl));
   // rule map (O10 pairs_to_csr) scratch and output, from the same arena
@@ -1290,6 +1294,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   if (!out_) out_ = std::make_unique<OutBufs>();
   MineRun run(out_.get());
   run.s = s;
+  run.root_from_gram = true;  // the resident prologue builds level 2 from the gram
   run.arena = arena_.get();
   run.Wp = Wp;
   run.minsup = level2_threshold((uint64_t)n_tx_, cfg.min_support);
@@ -1465,11 +1470,15 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
       d_prank = (int32_t*)arena_->push((size_t)I * 4);
       kern::level_partition(d_gram, I, d_desc, run.minsup, I, d_cost, d_prank, s);
     }
+    // level 2 straight from the gram: frequent pairs per root row, offsets, then the rows
+    kern::level_root_rows(d_gram, I, d_desc, run.minsup, d_prank, part_world, part_rank, I, d_m, s);
     kern::RootSetupArgs ra{d_own_bm_, d_rrank, d_rgid, d_roff, d_ids, d_fcnt, run.out_parent.p,
                            run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
                            d_prank, part_world, part_rank,
-                           run.stream_dl && !deferred_dl(), fused_select};
+                           run.stream_dl && !deferred_dl(), fused_select, d_m, d_soff, d_coff,
+                           cfg.max_len == 2, kern::level_rows_interleaved(Wp)};
     kern::level_root_setup(d_desc, d_ctl, ra, s);
+    kern::level_root_fill(d_desc, d_ctl, d_gram, I, run.minsup, ra, out_->tile_row, I, s);
     if (!fused_select)  // staged to pinned memory while the levels run
       KMLS_HIP(hipMemcpyAsync(fstage.get(), d_ids, (size_t)tab_stride * 12, hipMemcpyDeviceToHost, s));
   };

@@ -214,8 +214,26 @@ struct RootSetupArgs {
   int my_rank;
   bool download;   // level-1 nodes also go straight to FCtl::h (inline download mode)
   bool host_tab;   // frequent-item ids | counts to FCtl::host_tab
+  // gram-driven root (level_root_rows → setup → level_root_fill, instead of counting level 1
+  // with the look-back kernel): m = frequent pairs per root row; soff/coff [F+1] = the rows'
+  // survivor and next-level candidate offsets, filled here.  m == nullptr: counted root.
+  const int32_t* m;
+  int64_t* soff;
+  int64_t* coff;
+  bool leaf;       // max_len == 2: level 2 is the last level
+  bool interleaved;  // level_rows_interleaved(Wp): the count kernel family of the levels below
 };
+// true when the levels run the short-row count kernel (64-interleaved candidate-slot rows)
+bool level_rows_interleaved(int64_t Wp);
 void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s);
+// frequent pairs per root row (row r = rank F-1-r; rows a rank does not own count 0)
+void level_root_rows(const uint32_t* gram, int64_t ld, const FLevel* desc, uint32_t minsup,
+                     const int32_t* prank, int world, int my_rank, int64_t F_max, int32_t* m,
+                     hipStream_t s);
+// level 2 from the gram: one block per root row writes its frequent pairs as level-2 rows
+// (trie nodes, AND bitmaps at their own slots, candidate offsets and tile→row entries of level 2)
+void level_root_fill(FLevel* desc, FCtl* ctl, const uint32_t* gram, int64_t ld, uint32_t minsup,
+                     const RootSetupArgs& a, int32_t* tile_row_nx, int64_t F_max, hipStream_t s);
 // rank root classes by estimated cost (n_a^2 + 1 from the gram, desc) for the snake partition;
 // with prank == nullptr only the costs are computed (the root setup ranks them)
 void level_partition(const uint32_t* gram, int64_t ld, FLevel* desc, uint32_t minsup,

@@ -1202,6 +1202,37 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     }
     n_cand = s_carry;
   }
+  // gram-driven root: survivor and next-level candidate offsets of the root rows (row r's m
+  // frequent pairs become m level-2 rows with 0..m-1 earlier siblings: m(m-1)/2 candidates)
+  int64_t S2 = 0, C2 = 0;
+  if (a.m) {
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+      int64_t* outp = pass == 0 ? a.soff : a.coff;
+      for (int64_t base = 0; base <= F; base += blockDim.x) {
+        const int64_t i = base + threadIdx.x;
+        const int64_t mi = i < F ? (int64_t)a.m[i] : 0;
+        const int64_t v = pass == 0 ? mi : mi * (mi - 1) / 2;
+        s_scan[threadIdx.x] = v;
+        __syncthreads();
+        for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+          const int64_t add = (int)threadIdx.x >= off ? s_scan[threadIdx.x - off] : 0;
+          __syncthreads();
+          s_scan[threadIdx.x] += add;
+          __syncthreads();
+        }
+        if (i <= F) outp[i] = s_carry + s_scan[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == blockDim.x - 1) s_carry += s_scan[threadIdx.x];
+        __syncthreads();
+      }
+      if (pass == 0) S2 = s_carry; else C2 = s_carry;
+      __syncthreads();
+      if (threadIdx.x == 0) s_carry = 0;
+      __syncthreads();
+    }
+  }
   if (threadIdx.x == 0) {
     FLevel& r = desc[1];
     r.bm = a.bm;
@@ -1212,13 +1243,32 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     r.child_base = F;
     desc[0].child_base = 0;  // level-1 trie nodes [0, F) for the copy-out of "level 0"
     ok = 1;
-    if (F + n_cand > a.out_cap || (n_cand + kTile - 1) / kTile > (int64_t)ctl->status_cap ||
-        n_cand >= (1ll << 28)) {
-      atomicExch(&ctl->overflow, 4u);
-      ok = 0;
+    if (!a.m) {
+      if (F + n_cand > a.out_cap || (n_cand + kTile - 1) / kTile > (int64_t)ctl->status_cap ||
+          n_cand >= (1ll << 28)) {
+        atomicExch(&ctl->overflow, 4u);
+        ok = 0;
+      } else {
+        alloc_level(ctl, &desc[2], n_cand, a.Wp);
+        if (ctl->overflow) ok = 0;
+      }
     } else {
-      alloc_level(ctl, &desc[2], n_cand, a.Wp);
-      if (ctl->overflow) ok = 0;
+      // level 2 exists now: its rows, and the buffers of its children (unless it is the last)
+      FLevel& l2 = desc[2];
+      atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
+      if (F + S2 + C2 > a.out_cap || (C2 + kTile - 1) / kTile > (int64_t)ctl->status_cap ||
+          C2 >= (1ll << 28) || S2 >= (1ll << 28)) {
+        atomicExch(&ctl->overflow, 4u);
+        ok = 0;
+      } else {
+        alloc_level(ctl, &l2, S2, a.Wp);
+        l2.n_rows = S2;
+        l2.child_base = F + S2;
+        l2.n_cand = a.leaf ? 0 : C2;
+        if (!a.leaf) alloc_level(ctl, &desc[3], C2, a.Wp);
+        if (ctl->overflow) ok = 0;
+        else if (!a.leaf) l2.cand_off[S2] = C2;
+      }
     }
   }
   __syncthreads();
@@ -1239,6 +1289,115 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
   }
 }
 
+// Frequent pairs per root row: block r scans gram row rank F-1-r beyond the diagonal (its
+// pairs with the more frequent items = the root rows before r), contiguous and coalesced.
+__global__ __launch_bounds__(256) void k_root_rows(const uint32_t* __restrict__ gram, int64_t ld,
+                                                   const FLevel* desc, uint32_t minsup,
+                                                   const int32_t* __restrict__ prank, int world,
+                                                   int my_rank, int32_t* __restrict__ m) {
+  __shared__ int32_t s_w[4];
+  const int64_t F = desc[1].n_rows;
+  const int64_t r = blockIdx.x;
+  if (r >= F) return;
+  const int64_t rb = F - 1 - r;
+  bool own = true;
+  if (world > 1) {
+    const int64_t k = prank[rb];
+    const int64_t rnd = k / world, p = k % world;
+    own = ((rnd % 2 == 0) ? p : world - 1 - p) == my_rank;
+  }
+  int32_t n = 0;
+  if (own)
+    for (int64_t ra = rb + 1 + threadIdx.x; ra < F; ra += blockDim.x) n += gram[rb * ld + ra] >= minsup;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) m[r] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// Level 2 from the gram (one block per root row r = owner b): the row's pairs with the earlier
+// rows a (a ascending) that are frequent become level-2 rows soff[r] + idx, each with idx earlier
+// siblings, i.e. candidates coff[r] + idx(idx-1)/2 ...; their AND bitmaps go to their own slots.
+__global__ __launch_bounds__(256) void k_root_fill(FLevel* desc, FCtl* ctl,
+                                                   const uint32_t* __restrict__ gram, int64_t ld,
+                                                   uint32_t minsup, RootSetupArgs A,
+                                                   int32_t* __restrict__ tile_row_nx) {
+  __shared__ int64_t s_w[kBlock / 64];
+  __shared__ int64_t s_run;
+  if (ctl->overflow) return;
+  const int64_t F = desc[1].n_rows;
+  const int64_t r = blockIdx.x;
+  if (r >= F || A.m[r] == 0) return;
+  const FLevel& l2 = desc[2];
+  const int64_t rb = F - 1 - r;
+  const int64_t s0 = A.soff[r], c0 = A.coff[r];
+  const int64_t child_base = desc[1].child_base;
+  const int64_t scap = (int64_t)ctl->status_cap;
+  const int n2 = (int)(A.Wp >> 1);
+  const ulonglong2* __restrict__ bm2 = (const ulonglong2*)A.bm;
+  ulonglong2* __restrict__ cbm2 = (ulonglong2*)l2.bm;
+  int32_t* __restrict__ crank = (int32_t*)l2.rank;
+  int64_t* __restrict__ cgid = (int64_t*)l2.gid;
+  int32_t* __restrict__ cslot = (int32_t*)l2.slot;
+  int64_t* __restrict__ co_nx = l2.cand_off;
+  const HostTrie h = ctl->h;
+  if (threadIdx.x == 0) s_run = 0;
+  for (int64_t a0 = 0; a0 < r; a0 += kBlock) {
+    const int64_t a = a0 + threadIdx.x;
+    const int64_t ra = F - 1 - a;  // a < r: rank ra > rb
+    uint32_t k = 0;
+    int flag = 0;
+    if (a < r) {
+      k = gram[rb * ld + ra];
+      flag = k >= minsup ? 1 : 0;
+    }
+    int64_t tot;
+    const int64_t lx = block_excl_scan(flag, s_w, &tot);
+    const int64_t idx = s_run + lx;
+    if (flag) {
+      const int64_t s = s0 + idx;
+      const int64_t node = child_base + s;
+      crank[s] = (int32_t)ra;
+      cgid[s] = node;
+      cslot[s] = (int32_t)s;
+      const int32_t it = A.ids[ra];
+      A.out_parent[node] = rb;
+      A.out_item[node] = it;
+      A.out_count[node] = k;
+      A.out_depth[node] = 2;
+      if (A.download) host_store(h, ctl, node, rb, it, k, 2);
+      if (!A.leaf) {
+        const int64_t co = c0 + idx * (idx - 1) / 2;
+        co_nx[s] = co;
+        for (int64_t ct = (co + kTile - 1) / kTile; ct * kTile < co + idx; ++ct)
+          if (ct < scap) tile_row_nx[ct] = (int32_t)s;
+        const ulonglong2* __restrict__ x = bm2 + ra * n2;
+        const ulonglong2* __restrict__ y = bm2 + rb * n2;
+        // the short-row count kernel reads 64-interleaved slots, the team kernel compact rows
+        ulonglong2* __restrict__ z = A.interleaved ? cbm2 + ((s >> 6) * n2 << 6) + (s & 63)
+                                                  : cbm2 + s * n2;
+        const int zs = A.interleaved ? 64 : 1;
+        for (int w0 = 0; w0 < n2; w0 += 6) {
+          ulonglong2 u[6], v[6];
+#pragma unroll
+          for (int q = 0; q < 6; ++q)
+            if (w0 + q < n2) {
+              u[q] = x[w0 + q];
+              v[q] = y[w0 + q];
+            }
+#pragma unroll
+          for (int q = 0; q < 6; ++q)
+            if (w0 + q < n2) z[(w0 + q) * zs] = make_ulonglong2(u[q].x & v[q].x, u[q].y & v[q].y);
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_run += tot;
+    __syncthreads();
+  }
+}
+
 int team_size_for(int64_t Wp) {  // lanes per candidate: ~4-8 16-byte chunks per lane
   const int64_t chunks = Wp >> 1;  // 16-byte chunks per row
   if (chunks >= 256) return 64;
@@ -1252,16 +1411,27 @@ int team_size_for(int64_t Wp) {  // lanes per candidate: ~4-8 16-byte chunks per
 
 int level_grid(int n_cus) { return std::max(64, n_cus * 8); }  // 8 x 256-thread blocks per CU
 
+namespace {
+bool small_rows_ok() {
+  static const bool ok = [] {
+    const char* e = std::getenv("KMLS_COUNT_SMALL");
+    return !(e && e[0] == '0');
+  }();
+  return ok;
+}
+}  // namespace
+
+bool level_rows_interleaved(int64_t Wp) {
+  const int64_t n2 = Wp >> 1;
+  return small_rows_ok() && n2 >= 1 && n2 <= kSmallChunks;
+}
+
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
                  const LevelCountArgs& a, const int32_t* tile_row, int32_t* tile_row_nx, int grid,
                  int64_t cand_hint, hipStream_t s) {
   if (a.deferred_dl) grid += a.copy_blocks;
-  static const bool small_ok = [] {
-    const char* e = std::getenv("KMLS_COUNT_SMALL");
-    return !(e && e[0] == '0');
-  }();
   const int64_t n2 = a.Wp >> 1;
-  if (small_ok && n2 >= 1 && n2 <= kSmallChunks) {
+  if (level_rows_interleaved(a.Wp)) {
     // a level expected to be small (the previous call's size: steady-state re-mining) is
     // latency-bound: load each candidate's whole row pair in one batch
     static const bool kb18 = [] {
@@ -1345,6 +1515,21 @@ void level_partition(const uint32_t* gram, int64_t ld, FLevel* desc, uint32_t mi
 
 void level_root_setup(FLevel* desc, FCtl* ctl, const RootSetupArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_level_root_setup, dim3(1), dim3(1024), 0, s, desc, ctl, a);
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_root_rows(const uint32_t* gram, int64_t ld, const FLevel* desc, uint32_t minsup,
+                     const int32_t* prank, int world, int my_rank, int64_t F_max, int32_t* m,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_root_rows, dim3((unsigned)std::max<int64_t>(F_max, 1)), dim3(256), 0, s,
+                     gram, ld, desc, minsup, prank, world, my_rank, m);
+  KMLS_HIP(hipGetLastError());
+}
+
+void level_root_fill(FLevel* desc, FCtl* ctl, const uint32_t* gram, int64_t ld, uint32_t minsup,
+                     const RootSetupArgs& a, int32_t* tile_row_nx, int64_t F_max, hipStream_t s) {
+  hipLaunchKernelGGL(k_root_fill, dim3((unsigned)std::max<int64_t>(F_max, 1)), dim3(kBlock), 0, s,
+                     desc, ctl, gram, ld, minsup, a, tile_row_nx);
   KMLS_HIP(hipGetLastError());
 }
 
