@@ -1476,7 +1476,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
                            run.out_item.p, run.out_count.p, run.out_depth.p, Wp, out_cap,
                            d_prank, part_world, part_rank,
                            run.stream_dl && !deferred_dl(), fused_select, d_m, d_soff, d_coff,
-                           cfg.max_len == 2, kern::level_rows_interleaved(Wp)};
+                           cfg.max_len == 2, kern::level_rows_interleaved(Wp), run.stream_dl};
     kern::level_root_setup(d_desc, d_ctl, ra, s);
     kern::level_root_fill(d_desc, d_ctl, d_gram, I, run.minsup, ra, out_->tile_row, I, s);
     if (!fused_select)  // staged to pinned memory while the levels run

@@ -222,6 +222,8 @@ struct RootSetupArgs {
   int64_t* coff;
   bool leaf;       // max_len == 2: level 2 is the last level
   bool interleaved;  // level_rows_interleaved(Wp): the count kernel family of the levels below
+  bool dl_level1;    // download requested: with no root count kernel (whose copy blocks carry
+                     // level 1 in deferred mode) the setup writes the level-1 nodes itself
 };
 // true when the levels run the short-row count kernel (64-interleaved candidate-slot rows)
 bool level_rows_interleaved(int64_t Wp);

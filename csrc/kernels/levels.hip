@@ -1256,6 +1256,7 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
       // level 2 exists now: its rows, and the buffers of its children (unless it is the last)
       FLevel& l2 = desc[2];
       atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
+      if (a.leaf) C2 = 0;  // level 2 is the last: no candidates below it
       if (F + S2 + C2 > a.out_cap || (C2 + kTile - 1) / kTile > (int64_t)ctl->status_cap ||
           C2 >= (1ll << 28) || S2 >= (1ll << 28)) {
         atomicExch(&ctl->overflow, 4u);
@@ -1281,7 +1282,7 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     a.out_item[i] = a.ids[i];
     a.out_count[i] = a.fcounts[i];
     a.out_depth[i] = 1;
-    if (a.download) host_store(ctl->h, ctl, i, -1, a.ids[i], a.fcounts[i], 1);
+    if (a.m ? a.dl_level1 : a.download) host_store(ctl->h, ctl, i, -1, a.ids[i], a.fcounts[i], 1);
     if (a.host_tab) {
       ctl->host_tab[i] = a.ids[i];
       ((uint32_t*)ctl->host_tab)[ctl->tab_stride + i] = a.fcounts[i];
