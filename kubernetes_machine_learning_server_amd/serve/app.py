@@ -78,10 +78,22 @@ def _python_match(snap, seeds, k):
     return recommend_oracle(rec, seeds, k)
 
 
-def _gpu_factory(cfg: ApiSettings):
-    """HBM index builder for SERVE_BACKEND=hip|auto (None → CPU matcher only)."""
+def _gpu_factory(cfg: ApiSettings, allow_owner: bool = True):
+    """HBM index builder for SERVE_BACKEND=hip|auto (None → CPU matcher only).  Under the
+    multi-worker runner (KMLS_GPU_OWNER_SOCKET set) a worker never opens the GPU: its "GPU index"
+    is a client of the one GPU-owning process (serve/gpu_owner.py)."""
     if cfg.serve_backend in ("cpu", "python"):
         return None
+    owner = os.environ.get("KMLS_GPU_OWNER_SOCKET")
+    if allow_owner and owner:
+        from .gpu_owner import OwnerClient
+        from .index import index_fingerprint
+
+        def build_client(index):
+            if not os.path.exists(owner):  # the owner found no GPU (or is gone)
+                return None
+            return OwnerClient(owner, index_fingerprint(index))
+        return build_client
     from ..ops import native
     if not native.gpu_available():
         if cfg.serve_backend == "hip":

@@ -41,15 +41,40 @@ def _worker(host: str, port: int, reuse_port: bool, log_level: str) -> None:
     server.run(sockets=[sock])
 
 
+def _owner(path: str) -> None:
+    from .gpu_owner import owner_main
+    sys.exit(owner_main(path))
+
+
+def _start_owner(ctx, workers: int):
+    """The GPU-owning matcher process (serve/gpu_owner.py) for multi-worker GPU serving: started
+    first; workers find its socket through KMLS_GPU_OWNER_SOCKET.  This launcher never touches
+    the GPU itself (a process that has initialised HIP must not fork+exec workers)."""
+    backend = os.environ.get("SERVE_BACKEND", "auto").lower()
+    if workers <= 1 or backend not in ("auto", "hip") or os.environ.get("KMLS_GPU_OWNER") == "0":
+        return None
+    path = os.environ.get("KMLS_GPU_OWNER_SOCKET") or f"/tmp/kmls_gpu_owner_{os.getpid()}.sock"
+    os.environ["KMLS_GPU_OWNER_SOCKET"] = path
+    p = ctx.Process(target=_owner, args=(path,), daemon=False)
+    p.start()
+    deadline = time.time() + float(os.environ.get("KMLS_GPU_OWNER_WAIT_S", "180"))
+    while time.time() < deadline and p.is_alive() and not os.path.exists(path):
+        time.sleep(0.1)
+    return p
+
+
 def run(host: str = "0.0.0.0", port: int = 80, workers: int = 1, log_level: str = "info") -> int:
     if workers <= 1:
         _worker(host, port, False, log_level)
         return 0
     ctx = mp.get_context("spawn")
+    owner = _start_owner(ctx, workers)
     procs: List[mp.Process] = [ctx.Process(target=_worker, args=(host, port, True, log_level),
                                            daemon=False) for _ in range(workers)]
     for p in procs:
         p.start()
+    if owner is not None:
+        procs.append(owner)
 
     def stop(signum, frame):
         for p in procs:

@@ -176,6 +176,11 @@ class ReloadManager:
         try:
             best, index, source = read_pickle_dict(self.cfg)
             gpu_index = self._gpu_factory(index) if self._gpu_factory else None
+            if gpu_index is not None and hasattr(gpu_index, "wait_ready"):
+                # GPU-owner client: the owner must have loaded this very model first
+                if not gpu_index.wait_ready():
+                    logger.error("GPU owner has not loaded this model: CPU matcher only")
+                    gpu_index = None
             gmb, cross = None, None
             if gpu_index is not None:
                 if self.cfg.serve_backend == "hip":  # forced: every batch on the GPU
