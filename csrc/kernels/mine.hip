@@ -159,14 +159,43 @@ __device__ __forceinline__ void part_chunk(int64_t nnz, int64_t* b0, int64_t* b1
 __global__ __launch_bounds__(kBlock) void k_part_hist(const int32_t* __restrict__ items,
                                                       int64_t nnz, int P,
                                                       int64_t* __restrict__ blk_cnt) {
-  __shared__ uint32_t h[kPartMax];
-  if (threadIdx.x < kPartMax) h[threadIdx.x] = 0;
+  // per-wave bins (no cross-wave LDS contention), 16-byte loads, two in flight per thread
+  __shared__ uint32_t h[kBlock / 64][kPartMax];
+  const int w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < (kBlock / 64) * kPartMax; i += kBlock) (&h[0][0])[i] = 0;
   __syncthreads();
   int64_t b0, b1;
   part_chunk(nnz, &b0, &b1);
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) atomicAdd(&h[items[i] >> kPartBits], 1u);
+  uint32_t* hw = h[w];
+  const int64_t head = ((4 - (int64_t)(((uintptr_t)(items + b0) >> 2) & 3)) & 3);
+  const int64_t a0 = min(b1, b0 + head);
+  for (int64_t i = b0 + threadIdx.x; i < a0; i += blockDim.x) atomicAdd(&hw[items[i] >> kPartBits], 1u);
+  const int4* __restrict__ v = reinterpret_cast<const int4*>(items + a0);
+  const int64_t n4 = (b1 - a0) >> 2;
+  for (int64_t j = threadIdx.x; j < n4; j += 2 * (int64_t)blockDim.x) {
+    const int4 x = v[j];
+    const bool two = j + blockDim.x < n4;
+    const int4 y = two ? v[j + blockDim.x] : make_int4(0, 0, 0, 0);
+    atomicAdd(&hw[x.x >> kPartBits], 1u);
+    atomicAdd(&hw[x.y >> kPartBits], 1u);
+    atomicAdd(&hw[x.z >> kPartBits], 1u);
+    atomicAdd(&hw[x.w >> kPartBits], 1u);
+    if (two) {
+      atomicAdd(&hw[y.x >> kPartBits], 1u);
+      atomicAdd(&hw[y.y >> kPartBits], 1u);
+      atomicAdd(&hw[y.z >> kPartBits], 1u);
+      atomicAdd(&hw[y.w >> kPartBits], 1u);
+    }
+  }
+  for (int64_t i = a0 + (n4 << 2) + threadIdx.x; i < b1; i += blockDim.x)
+    atomicAdd(&hw[items[i] >> kPartBits], 1u);
   __syncthreads();
-  if ((int)threadIdx.x < P) blk_cnt[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+  if ((int)threadIdx.x < P) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) t += h[k][threadIdx.x];
+    blk_cnt[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = t;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) blk_cnt[(int64_t)P * gridDim.x] = 0;  // scan sentinel
 }
 
@@ -239,12 +268,30 @@ __global__ __launch_bounds__(1024) void k_part_count(const uint16_t* __restrict_
   const int64_t s0 = off[(int64_t)p * G], s1 = off[(int64_t)(p + 1) * G];
   const int64_t len = s1 - s0, sl = (len + M - 1) / M;
   const int64_t a = s0 + min(len, (int64_t)m * sl), b = s0 + min(len, (int64_t)(m + 1) * sl);
-  for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) atomicAdd(&h[part[i]], 1u);
+  // 16-byte loads (8 ids) over the aligned body: more loads in flight than one 2-byte id per
+  // thread per iteration
+  const int64_t head = ((8 - (int64_t)(((uintptr_t)(part + a) >> 1) & 7)) & 7);
+  const int64_t a0 = min(b, a + head);
+  for (int64_t i = a + threadIdx.x; i < a0; i += blockDim.x) atomicAdd(&h[part[i]], 1u);
+  const uint4* __restrict__ v = reinterpret_cast<const uint4*>(part + a0);
+  const int64_t n8 = (b - a0) >> 3;
+  for (int64_t j = threadIdx.x; j < n8; j += blockDim.x) {
+    const uint4 x = v[j];
+    atomicAdd(&h[x.x & 0xFFFFu], 1u);
+    atomicAdd(&h[x.x >> 16], 1u);
+    atomicAdd(&h[x.y & 0xFFFFu], 1u);
+    atomicAdd(&h[x.y >> 16], 1u);
+    atomicAdd(&h[x.z & 0xFFFFu], 1u);
+    atomicAdd(&h[x.z >> 16], 1u);
+    atomicAdd(&h[x.w & 0xFFFFu], 1u);
+    atomicAdd(&h[x.w >> 16], 1u);
+  }
+  for (int64_t i = a0 + (n8 << 3) + threadIdx.x; i < b; i += blockDim.x) atomicAdd(&h[part[i]], 1u);
   __syncthreads();
   const int64_t id0 = (int64_t)p << kPartBits;
   for (int i = threadIdx.x; i < kPartBins; i += blockDim.x) {
-    const uint32_t v = h[i];
-    if (v && id0 + i < n_items) atomicAdd(&counts[id0 + i], v);
+    const uint32_t val = h[i];
+    if (val && id0 + i < n_items) atomicAdd(&counts[id0 + i], val);
   }
 }
 
@@ -307,7 +354,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
   for (int i = threadIdx.x; i <= nt; i += blockDim.x) s_ptr[i] = tx_ptr[t0 + i];
   __syncthreads();
   const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
-  for (int64_t pb = p0; pb < p1; pb += (int64_t)blockDim.x * kEncodeU) {
+  const int64_t step = (int64_t)blockDim.x * kEncodeU;
+  for (int64_t pb = p0; pb < p1; pb += step) {
     int32_t it[kEncodeU];
 #pragma unroll
     for (int u = 0; u < kEncodeU; ++u) {
