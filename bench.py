@@ -191,13 +191,22 @@ def main() -> int:
     tie = name_tie_rank(names) if names else np.arange(tx.n_items, dtype=np.int32)
     rule_map = not args.no_rule_map and not args.cpu
 
+    # KMLS_BENCH_DIST=gloo rehearses the N-rank path on fewer GPUs (ranks share devices round
+    # robin; the step itself needs no collective, so only the bracket and the merge use gloo)
+    dist_backend = os.environ.get("KMLS_BENCH_DIST", "nccl")
+    device = local_rank
     if world > 1:
         import datetime
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
-                                timeout=datetime.timedelta(seconds=300))
+        if dist_backend != "nccl":
+            device = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        if dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device),
+                                    timeout=datetime.timedelta(seconds=300))
+        else:
+            dist.init_process_group(dist_backend, timeout=datetime.timedelta(seconds=300))
 
     def barrier_sync():
         if world > 1:
@@ -215,7 +224,7 @@ def main() -> int:
         dm = None
     else:
         from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
-        dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, args.min_support, device=local_rank,
+        dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, args.min_support, device=device,
                        max_len=args.max_len, mfma=args.mfma)
         dm.set_tie_rank(tie)
 
@@ -252,7 +261,8 @@ def main() -> int:
     if world > 1:
         import torch
         import torch.distributed as dist
-        t = torch.tensor([ms_step], dtype=torch.float64, device="cuda")
+        t = torch.tensor([ms_step], dtype=torch.float64,
+                         device="cuda" if dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms_step = float(t.item())
         parts = [None] * world
