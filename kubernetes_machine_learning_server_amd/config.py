@@ -37,6 +37,9 @@ class JobSettings:
     experiment_supports: bool = False
     miner: str = "auto"          # gpu | cpu | oracle | auto
     rules_mode: str = "full"     # full (all itemsets, as mlxtend) | pairs (SURVEY §0 fast path)
+    # RULES_MODE=pairs on several GPUs: how the pair matrix is formed (parallel/pairs.py:
+    # allreduce | reduce_scatter | alltoall | ring), or "trie" (mine 2-itemsets, gather sub-tries)
+    pairs_strategy: str = "reduce_scatter"
     num_gpus: int = 1
     min_confidence: float = 0.04  # legacy confidence rules (main.py:227)
     checkpoint_dir: Optional[pathlib.Path] = None  # KMLS_CHECKPOINT_DIR: phase resume
@@ -74,6 +77,7 @@ class JobSettings:
             experiment_supports=_env("EXPERIMENT_SUPPORTS", "false").lower() in ("1", "true", "yes"),
             miner=_env("MINER", "auto").lower(),
             rules_mode=_env("RULES_MODE", "full").lower(),
+            pairs_strategy=_env("PAIRS_STRATEGY", "reduce_scatter").lower(),
             num_gpus=int(_env("NUM_GPUS", "1")),
             min_confidence=float(_env("MIN_CONFIDENCE", "0.04")),
             checkpoint_dir=(pathlib.Path(os.environ["KMLS_CHECKPOINT_DIR"])

@@ -71,6 +71,53 @@ def mine_rules(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float
     return idx, trie, info, (missing, dur)
 
 
+def mine_pairs_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float,
+                           total_songs: int
+                           ) -> Optional[Tuple[RuleIndexData, ItemsetTrie, str, Tuple[int, float]]]:
+    """RULES_MODE=pairs on several GPUs: the rule map is the pair-support matrix, so
+    the job forms it with one of the ``parallel.pairs`` strategies over transaction shards
+    (reduce-scatter by default; ring = the context-parallel analog, alltoall = Ulysses) — each
+    rank ends with the complete rows of its item block — and gathers only the frequent pairs of
+    its rows to rank 0, which builds the same index and 2-itemset trie as a single process."""
+    import torch.distributed as dist
+    from ..parallel.dist_miner import DistMiner, gather_arrays
+    from ..serve.index import build_index_from_pairs
+    t0 = time.perf_counter()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dm = DistMiner(tx.tx_ptr, tx.items, len(tx.names), min_support, device=local, max_len=2,
+                   backend="cpu" if cfg.miner == "cpu" else "gpu", mode="item")
+    ids, r0, r1, rows = dm.pair_rows(cfg.pairs_strategy)
+    fcounts, minsup = np.asarray(dm.ops.sel[1]), int(dm.ops.sel[2])
+    rows = np.asarray(rows, np.int64)[: r1 - r0]
+    upper = np.arange(rows.shape[1])[None, :] > np.arange(r0, r1)[:, None]  # each pair once
+    ii, jj = np.nonzero((rows >= minsup) & upper)
+    pa, pb = (ii + r0).astype(np.int64), jj.astype(np.int64)  # ranks, a < b
+    pc = rows[ii, jj].astype(np.int64)
+    got = gather_arrays({"a": pa, "b": pb, "c": pc}, rank, world)
+    if rank != 0:
+        return None
+    ids = np.asarray(ids, np.int64)
+    F = len(ids)
+    pa, pb, pc = got["a"], got["b"], got["c"]
+    order = np.lexsort((pb, pa))  # trie: level-2 nodes grouped by parent rank
+    pa, pb, pc = pa[order], pb[order], pc[order]
+    trie = ItemsetTrie(np.concatenate([np.full(F, -1, np.int64), pa]),
+                       np.concatenate([ids, ids[pb]]).astype(np.int32),
+                       np.concatenate([fcounts.astype(np.int64), pc]).astype(np.uint32),
+                       np.concatenate([np.ones(F, np.uint8), np.full(len(pa), 2, np.uint8)]),
+                       tx.n_tx, min_support,
+                       {"n_frequent_items": F, "backend": f"pairs-{cfg.pairs_strategy}-x{world}"},
+                       tx.names)
+    idx = build_index_from_pairs(len(tx.names), ids, ids[pa], ids[pb], pc, tx.n_tx, tx.names)
+    missing = total_songs - idx.n_keys
+    dur = time.perf_counter() - t0
+    print("Songs without recommendations:", missing)
+    print(f"Time elapsed in rule generation: {format_timedelta(dur)}")
+    info = f"min_support: {min_support} \tmissing songs: {missing} \ttime: {format_timedelta(dur)}"
+    return idx, trie, info, (missing, dur)
+
+
 def mine_rules_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float,
                            total_songs: int, ck: Optional[PhaseCheckpoint] = None
                            ) -> Optional[Tuple[RuleIndexData, ItemsetTrie, str, Tuple[int, float]]]:
@@ -231,6 +278,8 @@ def run(cfg: Optional[JobSettings] = None) -> Dict:
     if resumed:  # a previous attempt on this dataset crashed after mining
         res = resume_from_checkpoint(ck, tx, cfg.min_support, total_songs) if rank == 0 else None
         say("Resumed mining results from checkpoint", ck.dir)
+    elif distributed and cfg.rules_mode == "pairs" and cfg.pairs_strategy != "trie":
+        res = mine_pairs_distributed(cfg, tx, cfg.min_support, total_songs)
     elif distributed:
         res = mine_rules_distributed(cfg, tx, cfg.min_support, total_songs, ck)
     else:

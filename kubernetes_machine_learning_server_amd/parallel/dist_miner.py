@@ -430,6 +430,34 @@ class DistMiner:
         return {"stats": st, "trie": r}
 
 
+def gather_arrays(arrs: Dict[str, np.ndarray], rank: int, world: int
+                  ) -> Optional[Dict[str, np.ndarray]]:
+    """Concatenate equally-keyed 1-D arrays of every rank on rank 0 (rank order), by tensor
+    collectives: one all-gather of the lengths, one per field of buffers padded to the longest."""
+    if world == 1:
+        return {k: np.asarray(v) for k, v in arrs.items()}
+    dev = (torch.device("cuda", torch.cuda.current_device())
+           if dist.get_backend() == "nccl" else torch.device("cpu"))
+    n = len(next(iter(arrs.values()))) if arrs else 0
+    n_local = torch.tensor([n], dtype=torch.int64, device=dev)
+    sizes = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(sizes, n_local)
+    sizes = sizes.cpu().numpy()
+    cap = max(int(sizes.max()), 1)
+    out: Dict[str, np.ndarray] = {}
+    for k, a in arrs.items():
+        a = np.ascontiguousarray(a)
+        buf = torch.zeros(cap, dtype=getattr(torch, str(a.dtype)), device=dev)
+        if len(a):
+            buf[:len(a)] = torch.from_numpy(a).to(dev)
+        allb = torch.empty(world * cap, dtype=buf.dtype, device=dev)
+        dist.all_gather_into_tensor(allb, buf)
+        if rank == 0:
+            h = allb.cpu().numpy()
+            out[k] = np.concatenate([h[q * cap:q * cap + int(sizes[q])] for q in range(world)])
+    return out if rank == 0 else None
+
+
 def gather_trie(r: Dict, rank: int, world: int, n_frequent: int) -> Optional[Dict[str, np.ndarray]]:
     """Concatenate per-rank sub-tries on rank 0 (level-1 nodes 0..F-1 are shared; every rank's
     local ids >= F are rebased).

@@ -219,7 +219,7 @@ def rec_dict(root):
         return pickle.load(f)
 
 
-def _dist_job_worker(rank, world, port, root, fault, out_q):
+def _dist_job_worker(rank, world, port, root, fault, out_q, extra=None):
     import os as _os
     _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                        WORLD_SIZE=str(world), LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
@@ -231,14 +231,14 @@ def _dist_job_worker(rank, world, port, root, fault, out_q):
     from kubernetes_machine_learning_server_amd.job import main as _job
     from tests.helpers import job_settings as _js
     cfg = _js(_pl.Path(root), num_gpus=world, checkpoint_dir=_pl.Path(root) / "ck",
-              dist_timeout_s=120.0)
+              dist_timeout_s=120.0, **(extra or {}))
     try:
         out_q.put((rank, _job.run(cfg), None))
     except Exception as e:  # noqa: BLE001 — the injected fault
         out_q.put((rank, None, repr(e)))
 
 
-def _run_dist_job(root, world, fault=""):
+def _run_dist_job(root, world, fault="", extra=None):
     import socket
     import torch.multiprocessing as tmp_mp
     s = socket.socket()
@@ -247,7 +247,7 @@ def _run_dist_job(root, world, fault=""):
     s.close()
     ctx = tmp_mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_job_worker, args=(r, world, port, str(root), fault, q))
+    procs = [ctx.Process(target=_dist_job_worker, args=(r, world, port, str(root), fault, q, extra))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -277,3 +277,21 @@ def test_distributed_job_phase_checkpoints(tmp_path):
     assert summary["n_itemsets"] == ref["n_itemsets"] and summary["n_keys"] == ref["n_keys"]
     assert rec_dict(tmp_path) == rec_dict(single)
     assert not list((tmp_path / "ck").rglob("*.npz"))  # cleared after success
+
+
+@pytest.mark.parametrize("strategy", ["reduce_scatter", "ring", "alltoall"])
+def test_distributed_pairs_job_strategies(tmp_path, strategy):
+    """RULES_MODE=pairs at world size 2: the job forms the pair matrix with a parallel.pairs
+    strategy (item blocks per rank; ring = context-parallel, alltoall = Ulysses analog) and
+    publishes the same recommendations as a single-process pairs run."""
+    make_datasets(tmp_path, shapes=("ds2_weak", "tiny"), seeds=(3, 4))
+    res = _run_dist_job(tmp_path, 2, extra={"rules_mode": "pairs", "pairs_strategy": strategy})
+    assert all(r[2] is None for r in res), res
+    summary = res[0][1]
+    assert summary["backend"] == f"pairs-{strategy}-x2"
+    single = tmp_path / "single"
+    make_datasets(single, shapes=("ds2_weak", "tiny"), seeds=(3, 4))
+    ref = job.run(job_settings(single, rules_mode="pairs"))
+    assert summary["n_itemsets"] == ref["n_itemsets"] and summary["n_keys"] == ref["n_keys"]
+    assert rec_dict(tmp_path) == rec_dict(single)
+
