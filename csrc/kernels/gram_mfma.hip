@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -182,14 +183,50 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma(const unsigned long long
 constexpr int kStageRowB = 144;                 // bytes per staged row (128 + 16 pad)
 constexpr int kStageB = 2 * kTile * kStageRowB;  // one stripe of A and B rows
 
+// ---------------------------------------------------------------------------------------------
+// FP4 variant: the 0/1 operands are exact in OCP e2m1 (1.0 = nibble 0x2), and the block-scaled
+// v_mfma_scale_f32_32x32x64_f8f6f4 with FP4 operands runs at twice the i8 rate (4x bf16 per clock,
+// MI355X_MICROARCH.md matrix-core table) with K = 64 transactions = one bitmap word per MFMA.
+// Lane l (r = l&31, h = l>>5) supplies the 32 elements of word half h of its row (A: row r of the
+// tile, B: column r); whatever order the hardware assigns to elements inside a fragment, A and B
+// are expanded identically, so every product pairs the same transaction.  Bits are expanded
+// through a byte → 8-nibble LDS table (one ds_read_b32 per 8 transactions, half the bytes of the
+// i8 expansion).  The f32 accumulators hold integers exactly while a block's K slice stays below
+// 2^24 transactions (enforced by the split-K below); the epilogue converts them back to u32.
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ v8i unpack32_fp4(uint32_t bits, const uint32_t* __restrict__ lut) {
+  v8i r;
+  r[0] = (int)lut[bits & 0xFFu];
+  r[1] = (int)lut[(bits >> 8) & 0xFFu];
+  r[2] = (int)lut[(bits >> 16) & 0xFFu];
+  r[3] = (int)lut[bits >> 24];
+  r[4] = 0;
+  r[5] = 0;
+  r[6] = 0;
+  r[7] = 0;
+  return r;
+}
+
+template <bool FP4>
 __global__ __launch_bounds__(256, 2) void k_pair_gram_lds(const unsigned long long* __restrict__ bm,
                                                           int64_t Wp, int64_t F, int64_t n_tiles,
-                                                          int64_t n_blocks,
+                                                          int64_t n_blocks, int scale,
                                                           uint32_t* __restrict__ out) {
-  __shared__ uint2 lut[256];
+  __shared__ uint2 lut[256];     // i8: byte -> 8 bytes
+  __shared__ uint32_t lut4[256];  // FP4: byte -> 8 e2m1 nibbles (1.0 = 0x2)
   __shared__ __attribute__((aligned(16))) unsigned char stage[2][kStageB];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x)
-    lut[i] = make_uint2(nib((uint32_t)i & 0xFu), nib((uint32_t)i >> 4));
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    if constexpr (FP4) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) v |= ((uint32_t)(i >> b) & 1u) << (4 * b + 1);
+      lut4[i] = v;
+    } else {
+      lut[i] = make_uint2(nib((uint32_t)i & 0xFu), nib((uint32_t)i >> 4));
+    }
+  }
   const int64_t orig = blockIdx.x;
   const int64_t q = n_blocks / 8, rr = n_blocks % 8, xcd = orig % 8;
   int64_t idx = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
@@ -230,7 +267,8 @@ __global__ __launch_bounds__(256, 2) void k_pair_gram_lds(const unsigned long lo
       *reinterpret_cast<ulonglong2*>(&stage[buf][(lrow0 + 32 * k) * kStageRowB + seg * 16]) = R[k];
   };
 
-  v16i acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
+  using Acc = typename std::conditional<FP4, v16f, v16i>::type;
+  Acc acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
   const int shift = 16 * h;
   const int la0 = wr * 64 + r, la1 = la0 + 32;
   const int lb0 = kTile + wc * 64 + r, lb1 = lb0 + 32;
@@ -262,17 +300,29 @@ __global__ __launch_bounds__(256, 2) void k_pair_gram_lds(const unsigned long lo
         const unsigned long long xa1 = (wd & 1) ? A1[wd >> 1].y : A1[wd >> 1].x;
         const unsigned long long xb0 = (wd & 1) ? B0[wd >> 1].y : B0[wd >> 1].x;
         const unsigned long long xb1 = (wd & 1) ? B1[wd >> 1].y : B1[wd >> 1].x;
+        if constexpr (FP4) {  // one K=64 block-scaled MFMA per word: lane half h = word half h
+          const int sh4 = 32 * h;
+          const v8i fa0 = unpack32_fp4((uint32_t)(xa0 >> sh4), lut4);
+          const v8i fa1 = unpack32_fp4((uint32_t)(xa1 >> sh4), lut4);
+          const v8i fb0 = unpack32_fp4((uint32_t)(xb0 >> sh4), lut4);
+          const v8i fb1 = unpack32_fp4((uint32_t)(xb1 >> sh4), lut4);
+          acc00 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa0, fb0, acc00, 4, 4, 0, scale, 0, scale);
+          acc01 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa0, fb1, acc01, 4, 4, 0, scale, 0, scale);
+          acc10 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa1, fb0, acc10, 4, 4, 0, scale, 0, scale);
+          acc11 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa1, fb1, acc11, 4, 4, 0, scale, 0, scale);
+        } else {
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const int sh = 32 * half + shift;
-          const v4i fa0 = unpack16((uint32_t)(xa0 >> sh) & 0xFFFFu, lut);
-          const v4i fa1 = unpack16((uint32_t)(xa1 >> sh) & 0xFFFFu, lut);
-          const v4i fb0 = unpack16((uint32_t)(xb0 >> sh) & 0xFFFFu, lut);
-          const v4i fb1 = unpack16((uint32_t)(xb1 >> sh) & 0xFFFFu, lut);
-          acc00 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb0, acc00, 0, 0, 0);
-          acc01 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb1, acc01, 0, 0, 0);
-          acc10 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb0, acc10, 0, 0, 0);
-          acc11 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb1, acc11, 0, 0, 0);
+          for (int half = 0; half < 2; ++half) {
+            const int sh = 32 * half + shift;
+            const v4i fa0 = unpack16((uint32_t)(xa0 >> sh) & 0xFFFFu, lut);
+            const v4i fa1 = unpack16((uint32_t)(xa1 >> sh) & 0xFFFFu, lut);
+            const v4i fb0 = unpack16((uint32_t)(xb0 >> sh) & 0xFFFFu, lut);
+            const v4i fb1 = unpack16((uint32_t)(xb1 >> sh) & 0xFFFFu, lut);
+            acc00 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb0, acc00, 0, 0, 0);
+            acc01 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb1, acc01, 0, 0, 0);
+            acc10 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb0, acc10, 0, 0, 0);
+            acc11 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb1, acc11, 0, 0, 0);
+          }
         }
       }
     }
@@ -303,32 +353,6 @@ __global__ __launch_bounds__(256, 2) void k_pair_gram_lds(const unsigned long lo
       }
     }
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// FP4 variant: the 0/1 operands are exact in OCP e2m1 (1.0 = nibble 0x2), and the block-scaled
-// v_mfma_scale_f32_32x32x64_f8f6f4 with FP4 operands runs at twice the i8 rate (4x bf16 per clock,
-// MI355X_MICROARCH.md matrix-core table) with K = 64 transactions = one bitmap word per MFMA.
-// Lane l (r = l&31, h = l>>5) supplies the 32 elements of word half h of its row (A: row r of the
-// tile, B: column r); whatever order the hardware assigns to elements inside a fragment, A and B
-// are expanded identically, so every product pairs the same transaction.  Bits are expanded
-// through a byte → 8-nibble LDS table (one ds_read_b32 per 8 transactions, half the bytes of the
-// i8 expansion).  The f32 accumulators hold integers exactly while a block's K slice stays below
-// 2^24 transactions (enforced by the split-K below); the epilogue converts them back to u32.
-typedef int v8i __attribute__((ext_vector_type(8)));
-typedef float v16f __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ v8i unpack32_fp4(uint32_t bits, const uint32_t* __restrict__ lut) {
-  v8i r;
-  r[0] = (int)lut[bits & 0xFFu];
-  r[1] = (int)lut[(bits >> 8) & 0xFFu];
-  r[2] = (int)lut[(bits >> 16) & 0xFFu];
-  r[3] = (int)lut[bits >> 24];
-  r[4] = 0;
-  r[5] = 0;
-  r[6] = 0;
-  r[7] = 0;
-  return r;
 }
 
 __global__ __launch_bounds__(256) void k_pair_gram_fp4(const unsigned long long* __restrict__ bm,
@@ -451,9 +475,12 @@ __global__ __launch_bounds__(256) void k_pair_gram_fp4(const unsigned long long*
 
 // KMLS_GRAM_FP4=1: the FP4 (e2m1, block-scaled MFMA) variant; KMLS_GRAM_FP4_SCALE overrides the
 // e8m0 scale byte (127 = 1.0)
-static bool gram_fp4() {
+// (=1: the LDS-staged kernel with FP4 operands; =direct: the direct-load FP4 kernel)
+static int gram_fp4() {
   const char* e = std::getenv("KMLS_GRAM_FP4");
-  return e && e[0] == '1';
+  if (!e) return 0;
+  if (e[0] == '1') return 1;
+  return std::string(e) == "direct" ? 2 : 0;
 }
 // default: the LDS-staged variant (coalesced stripe loads; 100M x 754 items: 101 -> 23 ms);
 // KMLS_GRAM_LDS=0 selects the direct-load kernel (A/B)
@@ -478,26 +505,35 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
     return (int64_t)std::max(1, per_cu) * std::max(1, p.multiProcessorCount);
   }();
   int64_t ks = std::max<int64_t>(1, std::min<int64_t>(slots / blocks, Wp / 1024));
-  if (gram_fp4()) {
+  const char* se = std::getenv("KMLS_GRAM_FP4_SCALE");
+  const int scale = se ? std::atoi(se) : 127;
+  const int fp4 = gram_fp4();
+  if (fp4 == 2) {
     // exact f32 accumulation: every block's stripes hold < 2^24 transactions (<= 2^17 words
     // at this split, with margin for the rounding of stripes)
     ks = std::max<int64_t>(ks, (Wp + (1 << 17) - 1) >> 17);
-    const char* se = std::getenv("KMLS_GRAM_FP4_SCALE");
-    const int scale = se ? std::atoi(se) : 127;
     hipLaunchKernelGGL(k_pair_gram_fp4, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
                        (const unsigned long long*)bm, Wp, F, nt, blocks, scale, out);
-  } else if (gram_lds()) {
+  } else if (gram_lds() || fp4 == 1) {
     static const int64_t slots_lds = [] {
       int dev = 0, per_cu = 1;
       hipDeviceProp_t p;
       if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)512;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pair_gram_lds, 256, 0) != hipSuccess)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pair_gram_lds<false>, 256, 0) != hipSuccess)
         per_cu = 2;
       return (int64_t)std::max(1, per_cu) * std::max(1, p.multiProcessorCount);
     }();
-    const int64_t ks_lds = std::max<int64_t>(1, std::min<int64_t>(slots_lds / blocks, Wp / 256));
-    hipLaunchKernelGGL(k_pair_gram_lds, dim3((unsigned)blocks, (unsigned)ks_lds), dim3(256), 0, s,
-                       (const unsigned long long*)bm, Wp, F, nt, blocks, out);
+    int64_t ks_lds = std::max<int64_t>(1, std::min<int64_t>(slots_lds / blocks, Wp / 256));
+    if (fp4 == 1) {
+      // f32 accumulators are exact below 2^24: a block's interleaved stripes (16 words = 1024
+      // transactions each) must number < 2^14
+      ks_lds = std::max<int64_t>(ks_lds, ((Wp + kStripe - 1) / kStripe + 16383) / 16384 + 1);
+      hipLaunchKernelGGL(k_pair_gram_lds<true>, dim3((unsigned)blocks, (unsigned)ks_lds), dim3(256),
+                         0, s, (const unsigned long long*)bm, Wp, F, nt, blocks, scale, out);
+    } else {
+      hipLaunchKernelGGL(k_pair_gram_lds<false>, dim3((unsigned)blocks, (unsigned)ks_lds), dim3(256),
+                         0, s, (const unsigned long long*)bm, Wp, F, nt, blocks, scale, out);
+    }
   } else {
     hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
                        (const unsigned long long*)bm, Wp, F, nt, blocks, out);

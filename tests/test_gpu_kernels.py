@@ -41,14 +41,17 @@ def _onehot(tx):
     return X
 
 
-@pytest.mark.parametrize("use_mfma", [False, True, "fp4", "direct"])
+@pytest.mark.parametrize("use_mfma", [False, True, "fp4", "fp4direct", "direct"])
 @pytest.mark.parametrize("shape,ms,n_tx", [("tiny", 0.02, None), ("ds2_weak", 0.03, None),
                                              ("tiny", 0.01, 5000), ("ds2", 0.05, 777),
                                              ("ds2_weak", 0.03, 70000)])
 def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     import torch
-    if use_mfma == "fp4":  # the e2m1 block-scaled MFMA variant of the matrix-core gram
+    if use_mfma == "fp4":  # the e2m1 block-scaled MFMA gram, LDS-staged stripes
         monkeypatch.setenv("KMLS_GRAM_FP4", "1")
+        use_mfma = True
+    if use_mfma == "fp4direct":  # the same operands with direct (unstaged) loads
+        monkeypatch.setenv("KMLS_GRAM_FP4", "direct")
         use_mfma = True
     if use_mfma == "direct":  # the direct-load MFMA gram (the default stages stripes in LDS)
         monkeypatch.setenv("KMLS_GRAM_LDS", "0")
@@ -82,6 +85,34 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     # bitmap rows popcount == supports
     pc = np.array([bin(int(w) & (2**64 - 1)).count("1") for w in bm.cpu().numpy().ravel()])
     np.testing.assert_array_equal(pc.reshape(max(F, 1), Wp).sum(1)[:F], counts)
+
+
+@pytest.mark.parametrize("fp4", ["1", "direct"])
+def test_pair_gram_fp4_exact_past_2_24_transactions(gpu_mod, fp4, monkeypatch):
+    """FP4 operands accumulate in f32, exact only below 2^24 per block: with more transactions
+    than that the split-K must keep every block's slice under it.  Checked against the popcount
+    gram (integer arithmetic) on 17M transactions."""
+    import torch
+    T, I = (1 << 24) + 4099, 300
+    ptr, items = gpu_mod.synth_transactions(T, I, 3.0, 4, 0.9, 0.85, 21)
+    g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
+    g.load_csr(ptr, items, I)
+    counts = np.bincount(items, minlength=I).astype(np.uint32)
+    F = g.select(counts, T, 0.001)
+    Wp = g.words_local()
+    bm = torch.zeros((F, Wp), dtype=torch.int64, device="cuda")
+    ref = torch.zeros((F, F), dtype=torch.int32, device="cuda")
+    got = torch.zeros((F, F), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    g.encode_bitmaps(bm.data_ptr(), Wp, 0)
+    g.pair_counts(bm.data_ptr(), Wp, ref.data_ptr(), False)
+    monkeypatch.setenv("KMLS_GRAM_FP4", fp4)
+    g.pair_counts(bm.data_ptr(), Wp, got.data_ptr(), True)
+    g.synchronize()
+    iu = np.triu_indices(F, 1)
+    r, o = ref.cpu().numpy()[iu], got.cpu().numpy()[iu]
+    assert r.max() > (1 << 24) // 64  # counts large enough that f32 rounding would show
+    np.testing.assert_array_equal(o, r)
 
 
 @pytest.mark.parametrize("fused", ["1", "0"])
