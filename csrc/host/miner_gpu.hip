@@ -899,6 +899,45 @@ void GpuMiner::item_support(uintptr_t counts_dev) {
   support_counts(d_items_, nnz_, (uint32_t*)counts_dev, s);
 }
 
+// Device-side selection from device-resident (all-reduced) supports: only the F frequent ids
+// and counts cross PCIe (kern::select_large), not the n_items support vector.
+int64_t GpuMiner::select_device(const uint32_t* d_counts, int64_t global_n_tx, double min_support,
+                                Comm* comm) {
+  hipStream_t s = (hipStream_t)stream_;
+  global_n_tx_ = global_n_tx;
+  const int64_t I = std::max<int64_t>(n_items_, 1);
+  if (d_rank_of_) KMLS_HIP(hipFree(d_rank_of_));
+  if (d_ids_) KMLS_HIP(hipFree(d_ids_));
+  if (d_fmask_) KMLS_HIP(hipFree(d_fmask_));
+  d_fmask_ = nullptr;
+  KMLS_HIP(hipMalloc((void**)&d_rank_of_, (size_t)I * sizeof(int32_t)));
+  KMLS_HIP(hipMalloc((void**)&d_ids_, (size_t)I * sizeof(int32_t)));
+  if (n_items_ >= (1 << 16)) KMLS_HIP(hipMalloc((void**)&d_fmask_, (size_t)(I + 31) / 32 * 4));
+  const size_t mark = arena_->mark();
+  const size_t tb = kern::select_large_temp_bytes(I);
+  void* tmp = arena_->push(tb);
+  uint32_t* d_fc = (uint32_t*)arena_->push((size_t)I * 4);
+  unsigned long long* dF = (unsigned long long*)arena_->push(256);
+  const uint32_t c1 = level1_threshold((uint64_t)global_n_tx, min_support);
+  kern::select_large(d_counts, n_items_, c1, tmp, tb, d_ids_, d_fc, d_rank_of_, d_fmask_, dF, s);
+  KMLS_HIP(hipMemcpyAsync(h_scalar_, dF, 8, hipMemcpyDeviceToHost, s));
+  if (comm) comm->wait_stream(s);
+  else KMLS_HIP(hipStreamSynchronize(s));
+  const int64_t F = h_scalar_[0];
+  fi_.ids.assign((size_t)F, 0);
+  fi_.counts.assign((size_t)F, 0u);
+  if (F) {
+    KMLS_HIP(hipMemcpyAsync(fi_.ids.data(), d_ids_, (size_t)F * 4, hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipMemcpyAsync(fi_.counts.data(), d_fc, (size_t)F * 4, hipMemcpyDeviceToHost, s));
+  }
+  KMLS_HIP(hipStreamSynchronize(s));
+  arena_->pop_to(mark);
+  fi_.rank_of.assign((size_t)n_items_, -1);
+  for (int64_t r = 0; r < F; ++r) fi_.rank_of[(size_t)fi_.ids[(size_t)r]] = (int32_t)r;
+  fi_.minsup2 = level2_threshold((uint64_t)global_n_tx, min_support);
+  return F;
+}
+
 int64_t GpuMiner::select(const uint32_t* global_counts, int64_t global_n_tx, double min_support) {
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
@@ -1808,13 +1847,24 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
     kern::add_u32(d_part, d_part + (size_t)k * (size_t)std::max<int64_t>(n_items_, 1), n_items_, s);
   // the selection (rank by support over up to millions of items) runs on the host: one 4 B/item
   // readback per call, the same on every rank
-  std::vector<uint32_t> cnt((size_t)n_items_);
-  KMLS_HIP(hipMemcpyAsync(cnt.data(), d_part, cnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  if (comm) comm->wait_stream(s);
-  else KMLS_HIP(hipStreamSynchronize(s));
-  arena_->pop_to(mark);
-  // 2. selection from global supports (identical on every rank)
-  const int64_t F = select(cnt.data(), global_n_tx, cfg.min_support);
+  // 2. selection from the global supports (identical on every rank), on the device: only the
+  //    frequent ids/counts come back (KMLS_SELECT_DEVICE=0: the host path, A/B)
+  static const bool dev_select = [] {
+    const char* e = std::getenv("KMLS_SELECT_DEVICE");
+    return !(e && e[0] == '0');
+  }();
+  int64_t F;
+  if (dev_select) {
+    F = select_device(d_part, global_n_tx, cfg.min_support, comm);
+    arena_->pop_to(mark);
+  } else {
+    std::vector<uint32_t> cnt((size_t)n_items_);
+    KMLS_HIP(hipMemcpyAsync(cnt.data(), d_part, cnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (comm) comm->wait_stream(s);
+    else KMLS_HIP(hipStreamSynchronize(s));
+    arena_->pop_to(mark);
+    F = select(cnt.data(), global_n_tx, cfg.min_support);
+  }
   KMLS_HIP(hipEventRecord(e1.e, s));
   // 3. shard-local bitmaps
   const int64_t Wp = words_local();

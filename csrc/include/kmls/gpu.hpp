@@ -147,6 +147,8 @@ class GpuMiner {
   // Phase B: frequent-item selection from GLOBAL supports (host array) + global T.
   // Returns F.  `owned` (optional, size F): which top-level classes this rank mines.
   int64_t select(const uint32_t* global_counts, int64_t global_n_tx, double min_support);
+  int64_t select_device(const uint32_t* d_counts, int64_t global_n_tx, double min_support,
+                        Comm* comm = nullptr);
   // Phase C: tid-bitmaps of frequent items for the resident shard, into an external buffer
   // (uint64[F][Wp]) at word offset `word_off` of rows of stride `Wp_total` words.
   int64_t words_local() const;  // padded words for the local shard

@@ -29,6 +29,12 @@ constexpr int64_t kEncodeTileMaxF = 1 << 20;  // row bands past one LDS slab
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
                          int64_t F, hipStream_t s, const uint32_t* fmask = nullptr);
+// frequent items (count >= c1) ranked by (count asc, id asc) on the device: ids / fcounts [F],
+// rank_of [n_items] (-1 = infrequent), fmask (optional bit mask), *dF = F
+size_t select_large_temp_bytes(int64_t n_items);
+void select_large(const uint32_t* cnt, int64_t n_items, uint32_t c1, void* tmp, size_t tmp_bytes,
+                  int32_t* ids, uint32_t* fcounts, int32_t* rank_of, uint32_t* fmask,
+                  unsigned long long* dF, hipStream_t s);
 // dst[i] += src[i]
 void add_u32(uint32_t* dst, const uint32_t* src, int64_t n, hipStream_t s);
 // exclusive prefix sum over int64[n+1] (in[n] == 0) into out[n+1] (out[n] = total)

@@ -737,6 +737,71 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
   return true;
 }
 
+// ----------------------------------------------------------------------------------------
+// Device selection for large vocabularies (the tx-DP call): frequent items ranked by (count asc,
+// id asc) = select_frequent, without copying the support vector to the host.  One 64-bit key per
+// item (count << 32 | id; ~0 for infrequent items, which sort last), a radix sort, and a scatter
+// of the first F keys into ids / counts / rank_of / the frequent-item mask.
+__global__ void k_sel_keys(const uint32_t* __restrict__ cnt, int64_t n_items, uint32_t c1,
+                           unsigned long long* __restrict__ keys, int32_t* __restrict__ rank_of,
+                           uint32_t* __restrict__ fmask, unsigned long long* __restrict__ dF) {
+  __shared__ unsigned int s_n;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_items) {
+    const uint32_t c = cnt[i];
+    const bool f = c >= c1;
+    keys[i] = f ? (((unsigned long long)c << 32) | (unsigned long long)i) : ~0ull;
+    rank_of[i] = -1;
+    if (f) atomicAdd(&s_n, 1u);
+  }
+  if (fmask && i < (n_items + 31) / 32) fmask[i] = 0u;
+  __syncthreads();
+  if (threadIdx.x == 0 && s_n) atomicAdd(dF, (unsigned long long)s_n);
+}
+
+__global__ void k_sel_scatter(const unsigned long long* __restrict__ keys, int64_t n_items,
+                              const unsigned long long* __restrict__ dF, int32_t* __restrict__ ids,
+                              uint32_t* __restrict__ fcounts, int32_t* __restrict__ rank_of,
+                              uint32_t* __restrict__ fmask) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= (int64_t)*dF || r >= n_items) return;
+  const unsigned long long k = keys[r];
+  const int32_t id = (int32_t)(k & 0xFFFFFFFFull);
+  ids[r] = id;
+  fcounts[r] = (uint32_t)(k >> 32);
+  rank_of[id] = (int32_t)r;
+  if (fmask) atomicOr(&fmask[id >> 5], 1u << (id & 31));
+}
+
+size_t select_large_temp_bytes(int64_t n_items) {
+  size_t b = 0;
+  KMLS_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b, (const unsigned long long*)nullptr,
+                                             (unsigned long long*)nullptr, (int)n_items));
+  return 2 * (((size_t)n_items * 8 + 255) & ~(size_t)255) + 256 + b;
+}
+
+void select_large(const uint32_t* cnt, int64_t n_items, uint32_t c1, void* tmp, size_t tmp_bytes,
+                  int32_t* ids, uint32_t* fcounts, int32_t* rank_of, uint32_t* fmask,
+                  unsigned long long* dF, hipStream_t s) {
+  if (tmp_bytes < select_large_temp_bytes(n_items))
+    throw std::runtime_error("select_large: scratch too small");
+  const size_t kb = ((size_t)n_items * 8 + 255) & ~(size_t)255;
+  unsigned long long* keys = (unsigned long long*)tmp;
+  unsigned long long* sorted = (unsigned long long*)((char*)tmp + kb);
+  void* cub = (char*)tmp + 2 * kb + 256;
+  size_t cb = tmp_bytes - 2 * kb - 256;
+  KMLS_HIP(hipMemsetAsync(dF, 0, 8, s));
+  const unsigned nb = (unsigned)((n_items + 255) / 256);
+  hipLaunchKernelGGL(k_sel_keys, dim3(nb), dim3(256), 0, s, cnt, n_items, c1, keys, rank_of, fmask,
+                     dF);
+  KMLS_HIP(hipcub::DeviceRadixSort::SortKeys(cub, cb, keys, sorted, (int)n_items, 0, 64, s));
+  hipLaunchKernelGGL(k_sel_scatter, dim3(nb), dim3(256), 0, s, sorted, n_items, dF, ids, fcounts,
+                     rank_of, fmask);
+  KMLS_HIP(hipGetLastError());
+}
+
 size_t scan_temp_bytes(int64_t n) {
   size_t bytes = 0;
   KMLS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int64_t*)nullptr,
