@@ -339,13 +339,23 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
                                                         unsigned long long* __restrict__ bm,
                                                         int64_t Wp, int64_t word_off, int64_t F,
                                                         int tw_log2, int band_rows,
-                                                        const uint32_t* __restrict__ fmask) {
+                                                        const uint32_t* __restrict__ fmask,
+                                                        bool xcd_order) {
   extern __shared__ unsigned long long s_bm[];  // [band rows][TW], then tx_ptr[64*TW + 1]
   const int TW = 1 << tw_log2;
   const int64_t tile_tx = 64ll << tw_log2;
   const int64_t n_bands = (F + band_rows - 1) / band_rows;
-  const int64_t tile = (int64_t)blockIdx.x / n_bands;
-  const int32_t r0 = (int32_t)(((int64_t)blockIdx.x - tile * n_bands) * band_rows);
+  // XCD-aware order: the hardware deals consecutive workgroups round-robin over the 8 XCDs, so
+  // neighbouring tiles (which write the two halves of the same 128-byte lines of every row)
+  // would meet in different L2s and reach HBM as partial lines.  Logical block L runs on XCD
+  // L / ceil(nb / 8): each XCD walks a contiguous run of tiles.
+  int64_t lb = blockIdx.x;
+  if (xcd_order) {
+    const int64_t nb = gridDim.x, q = nb / 8, rr = nb % 8, x = lb % 8;
+    lb = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + lb / 8;
+  }
+  const int64_t tile = lb / n_bands;
+  const int32_t r0 = (int32_t)((lb - tile * n_bands) * band_rows);
   const int32_t nr = (int32_t)min((int64_t)band_rows, F - r0);
   const int64_t t0 = tile * tile_tx;
   const int nt = (int)min(tile_tx, n_tx - t0);
@@ -355,12 +365,21 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
   __syncthreads();
   const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
   const int64_t step = (int64_t)blockDim.x * kEncodeU;
+  // the next round's item loads are issued before this round's gathers and LDS work, so their
+  // HBM latency overlaps the dependent chain of the current round
+  int32_t nx[kEncodeU];
+#pragma unroll
+  for (int u = 0; u < kEncodeU; ++u) {
+    const int64_t p = p0 + (int64_t)u * blockDim.x + threadIdx.x;
+    nx[u] = p < p1 ? items[p] : -1;
+  }
   for (int64_t pb = p0; pb < p1; pb += step) {
     int32_t it[kEncodeU];
 #pragma unroll
     for (int u = 0; u < kEncodeU; ++u) {
-      const int64_t p = pb + (int64_t)u * blockDim.x + threadIdx.x;
-      it[u] = p < p1 ? items[p] : -1;
+      it[u] = nx[u];
+      const int64_t p = pb + step + (int64_t)u * blockDim.x + threadIdx.x;
+      nx[u] = p < p1 ? items[p] : -1;
     }
     int32_t rk[kEncodeU];
 #pragma unroll
@@ -668,11 +687,14 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
                          int64_t F, hipStream_t s, const uint32_t* fmask) {
   if (n_tx <= 0 || F <= 0 || F > kEncodeTileMaxF) return false;
-  // words per tile: the slab within 48 KB of LDS (3 blocks per CU).  One band of F rows at
-  // TW = 8 or 4 words (64/32-byte row segments); past 1536 rows, bands of 1536 rows at TW = 4
-  // (narrower segments would make the write-out scattered 8-byte stores).
+  // words per tile: the slab within 48 KB of LDS.  TW = 4 words (32-byte row segments, the
+  // measured optimum); past 1536 rows, bands of 1536 rows (narrower segments would make the
+  // write-out scattered 8-byte stores).
   constexpr int64_t kSlab = 48 * 1024;
-  int tw_log2 = F * 64 <= kSlab ? 3 : 2;
+  int tw_log2 = 2;  // TW = 4: measured ahead of 8 and 2 at 100M x 754 (19.5 / 18.3 / 23.2 ms)
+  if (const char* e = std::getenv("KMLS_ENCODE_TW")) tw_log2 = std::max(0, std::min(3, std::atoi(e)));  // A/B
+  const char* xe = std::getenv("KMLS_ENCODE_XCD");  // =0: hardware block order (A/B)
+  const bool xcd = !(xe && xe[0] == '0');
   const int64_t TW = 1ll << tw_log2;
   const int64_t band = std::min<int64_t>(F, kSlab / (8 * TW));
   const int64_t n_bands = (F + band - 1) / band;
@@ -681,7 +703,7 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
   if (blocks > INT32_MAX) return false;
   hipLaunchKernelGGL(k_encode_tile, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr, items,
                      n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2, (int)band,
-                     fmask);
+                     fmask, xcd);
   KMLS_HIP(hipGetLastError());
   return true;
 }
