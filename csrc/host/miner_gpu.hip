@@ -754,6 +754,8 @@ GpuMiner::~GpuMiner() {
   if (d_items_) (void)hipFree(d_items_);
   if (d_rank_of_) (void)hipFree(d_rank_of_);
   if (d_fmask_) (void)hipFree(d_fmask_);
+  if (d_fgroup_) (void)hipFree(d_fgroup_);
+  if (d_c2r_) (void)hipFree(d_c2r_);
   if (d_ids_) (void)hipFree(d_ids_);
   if (d_own_bm_) (void)hipFree(d_own_bm_);
   if (h_scalar_) (void)hipHostFree(h_scalar_);
@@ -935,7 +937,28 @@ int64_t GpuMiner::select_device(const uint32_t* d_counts, int64_t global_n_tx, d
   fi_.rank_of.assign((size_t)n_items_, -1);
   for (int64_t r = 0; r < F; ++r) fi_.rank_of[(size_t)fi_.ids[(size_t)r]] = (int32_t)r;
   fi_.minsup2 = level2_threshold((uint64_t)global_n_tx, min_support);
+  build_encode_tables(F);
   return F;
+}
+
+// Encode lookup tables (kern::frequent_groups) for the selection just made; small vocabularies
+// or wide frequent sets keep the mask + rank gathers.
+void GpuMiner::build_encode_tables(int64_t F) {
+  if (d_fgroup_) KMLS_HIP(hipFree(d_fgroup_));
+  if (d_c2r_) KMLS_HIP(hipFree(d_c2r_));
+  d_fgroup_ = nullptr;
+  d_c2r_ = nullptr;
+  if (!d_fmask_ || F <= 0 || F > kern::kEncodeGroupMaxF) return;
+  hipStream_t s = (hipStream_t)stream_;
+  const int64_t G = (n_items_ + 31) / 32;
+  KMLS_HIP(hipMalloc((void**)&d_fgroup_, (size_t)G * 8));
+  KMLS_HIP(hipMalloc((void**)&d_c2r_, (size_t)F * 4));
+  const size_t mark = arena_->mark();
+  const size_t tb = kern::frequent_groups_temp_bytes(n_items_);
+  void* tmp = arena_->push(tb);
+  kern::frequent_groups(d_fmask_, n_items_, d_rank_of_, d_fgroup_, d_c2r_, tmp, tb, s);
+  KMLS_HIP(hipStreamSynchronize(s));  // the scratch returns to the arena
+  arena_->pop_to(mark);
 }
 
 int64_t GpuMiner::select(const uint32_t* global_counts, int64_t global_n_tx, double min_support) {
@@ -962,6 +985,7 @@ int64_t GpuMiner::select(const uint32_t* global_counts, int64_t global_n_tx, dou
     KMLS_HIP(hipMemcpyAsync(d_ids_, fi_.ids.data(), fi_.ids.size() * sizeof(int32_t),
                             hipMemcpyHostToDevice, s));
   KMLS_HIP(hipStreamSynchronize(s));
+  build_encode_tables((int64_t)fi_.ids.size());
   return (int64_t)fi_.ids.size();
 }
 
@@ -978,9 +1002,12 @@ bool GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_o
   const int64_t F = (int64_t)fi_.ids.size();
   const char* me = std::getenv("KMLS_ENCODE_MASK");  // =0: no frequent-item mask (A/B)
   const uint32_t* fmask = (me && me[0] == '0') ? nullptr : d_fmask_;
+  const char* ge = std::getenv("KMLS_ENCODE_GROUP");  // =0: mask + rank gathers (A/B)
+  const bool grp = fmask && !(ge && ge[0] == '0');
   if (tiled && n_tx_ >= (1 << 16) &&
       kern::encode_bitmap_tiled(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev,
-                                Wp_total, word_off, F, (hipStream_t)stream_, fmask))
+                                Wp_total, word_off, F, (hipStream_t)stream_, fmask,
+                                grp ? d_fgroup_ : nullptr, grp ? d_c2r_ : nullptr))
     return true;
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev, Wp_total,
                       word_off, (hipStream_t)stream_, fmask);

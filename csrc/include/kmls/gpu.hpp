@@ -221,6 +221,9 @@ class GpuMiner {
   int64_t global_n_tx_ = 0;
   int32_t* d_rank_of_ = nullptr;
   uint32_t* d_fmask_ = nullptr;  // frequent-item bit mask (large vocabularies, select())
+  unsigned long long* d_fgroup_ = nullptr;  // encode tables (kern::frequent_groups)
+  int32_t* d_c2r_ = nullptr;
+  void build_encode_tables(int64_t F);
   int32_t* d_ids_ = nullptr;
   uint64_t* d_own_bm_ = nullptr;  // single-GPU bitmap buffer
   size_t own_bm_bytes_ = 0;

@@ -28,7 +28,15 @@ void encode_bitmap(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
 constexpr int64_t kEncodeTileMaxF = 1 << 20;  // row bands past one LDS slab
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
-                         int64_t F, hipStream_t s, const uint32_t* fmask = nullptr);
+                         int64_t F, hipStream_t s, const uint32_t* fmask = nullptr,
+                         const unsigned long long* fgroup = nullptr, const int32_t* c2r = nullptr);
+// fgroup/c2r (frequent_groups; used when F <= kEncodeGroupMaxF): one 8-byte gather per item
+// instead of the mask gather followed by the rank gather
+constexpr int64_t kEncodeGroupMaxF = 2048;
+size_t frequent_groups_temp_bytes(int64_t n_items);
+void frequent_groups(const uint32_t* fmask, int64_t n_items, const int32_t* rank_of,
+                     unsigned long long* fgroup, int32_t* c2r, void* tmp, size_t tmp_bytes,
+                     hipStream_t s);
 // frequent items (count >= c1) ranked by (count asc, id asc) on the device: ids / fcounts [F],
 // rank_of [n_items] (-1 = infrequent), fmask (optional bit mask), *dF = F
 size_t select_large_temp_bytes(int64_t n_items);

@@ -340,8 +340,11 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
                                                         int64_t Wp, int64_t word_off, int64_t F,
                                                         int tw_log2, int band_rows,
                                                         const uint32_t* __restrict__ fmask,
-                                                        bool xcd_order) {
-  extern __shared__ unsigned long long s_bm[];  // [band rows][TW], then tx_ptr[64*TW + 1]
+                                                        bool xcd_order,
+                                                        const unsigned long long* __restrict__ fgroup,
+                                                        const int32_t* __restrict__ c2r) {
+  // [band rows][TW], then tx_ptr[64*TW + 1], then (fgroup path) c2r[F]
+  extern __shared__ unsigned long long s_bm[];
   const int TW = 1 << tw_log2;
   const int64_t tile_tx = 64ll << tw_log2;
   const int64_t n_bands = (F + band_rows - 1) / band_rows;
@@ -362,6 +365,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
   int64_t* s_ptr = (int64_t*)(s_bm + (int64_t)band_rows * TW);
   for (int64_t i = threadIdx.x; i < (int64_t)nr * TW; i += blockDim.x) s_bm[i] = 0ull;
   for (int i = threadIdx.x; i <= nt; i += blockDim.x) s_ptr[i] = tx_ptr[t0 + i];
+  int32_t* s_c2r = (int32_t*)(s_ptr + 64 * TW + 1);
+  if (fgroup)
+    for (int i = threadIdx.x; i < (int)F; i += blockDim.x) s_c2r[i] = c2r[i];
   __syncthreads();
   const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
   const int64_t step = (int64_t)blockDim.x * kEncodeU;
@@ -382,11 +388,25 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
       nx[u] = p < p1 ? items[p] : -1;
     }
     int32_t rk[kEncodeU];
+    if (fgroup) {
+      // one 8-byte gather per item: the frequent bits of its 32-id group and the number of
+      // frequent ids before the group; the rank comes from the LDS compact-index → rank table
 #pragma unroll
-    for (int u = 0; u < kEncodeU; ++u)
-      if (fmask && it[u] >= 0 && !((fmask[it[u] >> 5] >> (it[u] & 31)) & 1u)) it[u] = -1;
+      for (int u = 0; u < kEncodeU; ++u) {
+        rk[u] = -1;
+        if (it[u] < 0) continue;
+        const unsigned long long g = fgroup[it[u] >> 5];
+        const uint32_t m = (uint32_t)g, b = (uint32_t)it[u] & 31u;
+        if ((m >> b) & 1u)
+          rk[u] = s_c2r[(uint32_t)(g >> 32) + (uint32_t)__popc(m & ((1u << b) - 1u))] - r0;
+      }
+    } else {
 #pragma unroll
-    for (int u = 0; u < kEncodeU; ++u) rk[u] = it[u] >= 0 ? rank_of[it[u]] - r0 : -1;
+      for (int u = 0; u < kEncodeU; ++u)
+        if (fmask && it[u] >= 0 && !((fmask[it[u] >> 5] >> (it[u] & 31)) & 1u)) it[u] = -1;
+#pragma unroll
+      for (int u = 0; u < kEncodeU; ++u) rk[u] = it[u] >= 0 ? rank_of[it[u]] - r0 : -1;
+    }
 #pragma unroll
     for (int u = 0; u < kEncodeU; ++u) {
       if (rk[u] < 0 || rk[u] >= nr) continue;
@@ -685,8 +705,10 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
 
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
-                         int64_t F, hipStream_t s, const uint32_t* fmask) {
+                         int64_t F, hipStream_t s, const uint32_t* fmask,
+                         const unsigned long long* fgroup, const int32_t* c2r) {
   if (n_tx <= 0 || F <= 0 || F > kEncodeTileMaxF) return false;
+  if (F > kEncodeGroupMaxF) fgroup = nullptr, c2r = nullptr;  // c2r must fit LDS beside the slab
   // words per tile: the slab within 48 KB of LDS.  TW = 4 words (32-byte row segments, the
   // measured optimum); past 1536 rows, bands of 1536 rows (narrower segments would make the
   // write-out scattered 8-byte stores).
@@ -698,12 +720,12 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
   const int64_t TW = 1ll << tw_log2;
   const int64_t band = std::min<int64_t>(F, kSlab / (8 * TW));
   const int64_t n_bands = (F + band - 1) / band;
-  const size_t lds = (size_t)band * TW * 8 + (size_t)(64 * TW + 1) * 8;
+  const size_t lds = (size_t)band * TW * 8 + (size_t)(64 * TW + 1) * 8 + (fgroup ? (size_t)F * 4 : 0);
   const int64_t blocks = (n_tx + 64 * TW - 1) / (64 * TW) * n_bands;
   if (blocks > INT32_MAX) return false;
   hipLaunchKernelGGL(k_encode_tile, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr, items,
                      n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2, (int)band,
-                     fmask, xcd);
+                     fmask, xcd, fgroup, c2r);
   KMLS_HIP(hipGetLastError());
   return true;
 }
@@ -821,6 +843,49 @@ void select_large(const uint32_t* cnt, int64_t n_items, uint32_t c1, void* tmp, 
   KMLS_HIP(hipcub::DeviceRadixSort::SortKeys(cub, cb, keys, sorted, (int)n_items, 0, 64, s));
   hipLaunchKernelGGL(k_sel_scatter, dim3(nb), dim3(256), 0, s, sorted, n_items, dF, ids, fcounts,
                      rank_of, fmask);
+  KMLS_HIP(hipGetLastError());
+}
+
+// Encode lookup tables from the frequent-item mask (any selection path): per 32-id group its mask
+// bits and the number of frequent ids before it (one 8-byte gather per item in the encode), and
+// compact index (frequent ids in id order) → Eclat rank.
+__global__ void k_grp_pop(const uint32_t* __restrict__ fmask, int64_t G, int64_t* __restrict__ pop) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < G) pop[g] = __popc(fmask[g]);
+  if (g == G) pop[G] = 0;
+}
+__global__ void k_grp_fill(const uint32_t* __restrict__ fmask, int64_t G,
+                           const int64_t* __restrict__ pre, const int32_t* __restrict__ rank_of,
+                           unsigned long long* __restrict__ fgroup, int32_t* __restrict__ c2r) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const uint32_t m = fmask[g];
+  const int64_t base = pre[g];
+  fgroup[g] = (unsigned long long)m | ((unsigned long long)base << 32);
+  uint32_t x = m;
+  for (int j = 0; x; ++j, x &= x - 1u)
+    c2r[base + j] = rank_of[g * 32 + __builtin_ctz(x)];
+}
+
+size_t frequent_groups_temp_bytes(int64_t n_items) {
+  const int64_t G = (n_items + 31) / 32;
+  return 2 * (((size_t)(G + 1) * 8 + 255) & ~(size_t)255) + scan_temp_bytes(G);
+}
+
+void frequent_groups(const uint32_t* fmask, int64_t n_items, const int32_t* rank_of,
+                     unsigned long long* fgroup, int32_t* c2r, void* tmp, size_t tmp_bytes,
+                     hipStream_t s) {
+  const int64_t G = (n_items + 31) / 32;
+  if (tmp_bytes < frequent_groups_temp_bytes(n_items))
+    throw std::runtime_error("frequent_groups: scratch too small");
+  const size_t ab = ((size_t)(G + 1) * 8 + 255) & ~(size_t)255;
+  int64_t* pop = (int64_t*)tmp;
+  int64_t* pre = (int64_t*)((char*)tmp + ab);
+  void* cub = (char*)tmp + 2 * ab;
+  const unsigned nb = (unsigned)((G + 1 + 255) / 256);
+  hipLaunchKernelGGL(k_grp_pop, dim3(nb), dim3(256), 0, s, fmask, G, pop);
+  exclusive_scan_i64(pop, pre, G, cub, scan_temp_bytes(G), s);
+  hipLaunchKernelGGL(k_grp_fill, dim3(nb), dim3(256), 0, s, fmask, G, pre, rank_of, fgroup, c2r);
   KMLS_HIP(hipGetLastError());
 }
 

@@ -570,11 +570,13 @@ def test_extend_split_k_long_rows(gpu_mod, monkeypatch, split):
 
 
 @pytest.mark.parametrize("T,I,ms,min_f", [(300_000 + 37, 60_000, 0.002, 0),
+                                            (200_000 + 37, 100_000, 0.002, 100),
                                             (200_000 + 37, 100_000, 0.0005, 3000)])
 def test_encode_tiled_long_shard(gpu_mod, T, I, ms, min_f):
     """The LDS-slab encode produces the same tid-bitmaps as the host encoder, on a long shard
     with an odd tail tile; the second case has a million-style vocabulary (frequent-item mask
-    in front of the rank gather) and more frequent rows than one LDS slab (row bands).  The
+    in front of the rank gather, or the one-gather group tables when F <= 2048) and more
+    frequent rows than one LDS slab (row bands).  The
     buffer starts as all ones: the tiled encode must write every word of the shard's columns
     (the tx-DP path no longer clears the bitmap first)."""
     import torch
