@@ -146,7 +146,7 @@ def run_serve(shape: str, qps_list, duration: float, backend: str) -> dict:
         for q in qps_list:
             r = bs.measure(port, q, duration, 4, queries)
             res["points"].append({k: r[k] for k in ("offered_qps", "achieved_qps", "p50_ms",
-                                                    "p99_ms", "errors")})
+                                                    "p99_ms", "errors", "client_send_lag_p99_ms")})
     finally:
         bs.stop_server(proc)
     return res
