@@ -355,6 +355,178 @@ __global__ __launch_bounds__(256, 2) void k_pair_gram_lds(const unsigned long lo
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Wide-tile variant (KMLS_GRAM_TILE=256): each wave owns a 128x128 output block = 4x4 MFMA tiles
+// (16 accumulators, 256 AGPRs, one wave per SIMD), so every unpacked fragment feeds 4 MFMAs
+// instead of 2.  In the 128-tile kernel the LUT expansion (one fragment per MFMA) kept the LDS
+// pipe as busy as the matrix cores (r2_large_pmc.md: 63 % MFMA busy, 0.4 conflict cycles per LDS
+// instruction); here it is half of that, and the 256-row block tiles also halve the bitmap words
+// read per output (each staged row feeds 256 outputs).  Stripes are 8 words (512 transactions)
+// so a thread stages 8 x 16 B per stripe; rows are padded to 80 B in LDS.
+constexpr int kWTile = 256;
+constexpr int64_t kWStripe = 8;
+constexpr int kWRowB = 80;                        // bytes per staged row (64 + 16 pad)
+constexpr int kWStageB = 2 * kWTile * kWRowB;     // one stripe of A and B rows (40 KB)
+
+template <bool FP4>
+__global__ __launch_bounds__(256, 1) void k_pair_gram_wide(const unsigned long long* __restrict__ bm,
+                                                           int64_t Wp, int64_t F, int64_t n_tiles,
+                                                           int64_t n_blocks, int scale,
+                                                           uint32_t* __restrict__ out) {
+  __shared__ uint2 lut[256];
+  __shared__ uint32_t lut4[256];
+  __shared__ __attribute__((aligned(16))) unsigned char stage[2][kWStageB];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    if constexpr (FP4) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) v |= ((uint32_t)(i >> b) & 1u) << (4 * b + 1);
+      lut4[i] = v;
+    } else {
+      lut[i] = make_uint2(nib((uint32_t)i & 0xFu), nib((uint32_t)i >> 4));
+    }
+  }
+  const int64_t orig = blockIdx.x;
+  const int64_t q = n_blocks / 8, rr = n_blocks % 8, xcd = orig % 8;
+  int64_t idx = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  int64_t ti = 0;
+  while (idx >= n_tiles - ti) { idx -= n_tiles - ti; ++ti; }
+  const int64_t tj = ti + idx;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+
+  // staging role: thread t copies 16-byte segment (t & 3) of local rows (t >> 2) + 64 k, k = 0..7
+  // (local rows 0..255 = A tile rows, 256..511 = B tile rows)
+  const int seg = tid & 3, lrow0 = tid >> 2;
+  const int64_t W2 = Wp >> 1;
+  const ulonglong2* src[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int lr = lrow0 + 64 * k;
+    const int64_t grow = lr < kWTile ? ti * kWTile + lr : tj * kWTile + (lr - kWTile);
+    src[k] = grow < F ? reinterpret_cast<const ulonglong2*>(bm + grow * Wp) : nullptr;
+  }
+  const int64_t ks = gridDim.y, y = blockIdx.y;
+  const int64_t n_stripes = (Wp + kWStripe - 1) / kWStripe;
+  const int64_t my_stripes = y < n_stripes ? (n_stripes - y + ks - 1) / ks : 0;
+  auto gload = [&](int64_t it, ulonglong2 (&R)[8]) {
+    const int64_t u = (it * ks + y) * (kWStripe / 2) + seg;
+    const bool in = u < W2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) R[k] = (src[k] && in) ? src[k][u] : make_ulonglong2(0, 0);
+  };
+  auto swrite = [&](int buf, const ulonglong2 (&R)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      *reinterpret_cast<ulonglong2*>(&stage[buf][(lrow0 + 64 * k) * kWRowB + seg * 16]) = R[k];
+  };
+
+  using Acc = typename std::conditional<FP4, v16f, v16i>::type;
+  Acc acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = Acc{};
+  const int la = wr * 128 + r;           // + 32 m: A fragment rows
+  const int lb = kWTile + wc * 128 + r;  // + 32 n: B fragment columns
+  ulonglong2 R[8];
+  if (my_stripes > 0) gload(0, R);
+  for (int64_t it = 0; it < my_stripes; ++it) {
+    const int buf = (int)(it & 1);
+    swrite(buf, R);
+    __syncthreads();  // stripe `it` visible; buffer buf^1 (stripe it-1) no longer read
+    if (it + 1 < my_stripes) gload(it + 1, R);
+    const unsigned char* sb = stage[buf];
+    if constexpr (FP4) {
+      // software-pipelined over the stripe's 8 words: word s+1's fragments are unpacked (LDS
+      // table reads) before word s's 16 MFMAs issue, so with one wave per SIMD the table latency
+      // hides behind ~512 matrix-core cycles instead of stalling them
+      const int sh4 = 32 * h;
+      ulonglong2 A[4], B[4];
+      v8i fa[2][4], fb[2][4];
+      auto rows = [&](int c) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          A[m] = *reinterpret_cast<const ulonglong2*>(sb + (la + 32 * m) * kWRowB + c * 16);
+          B[m] = *reinterpret_cast<const ulonglong2*>(sb + (lb + 32 * m) * kWRowB + c * 16);
+        }
+      };
+      auto unpack = [&](int wd, v8i (&xa)[4], v8i (&xb)[4]) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          xa[m] = unpack32_fp4((uint32_t)((wd ? A[m].y : A[m].x) >> sh4), lut4);
+          xb[m] = unpack32_fp4((uint32_t)((wd ? B[m].y : B[m].x) >> sh4), lut4);
+        }
+      };
+      rows(0);
+      unpack(0, fa[0], fb[0]);
+#pragma unroll
+      for (int w = 0; w < (int)kWStripe; ++w) {
+        const int cur = w & 1;
+        if (w + 1 < (int)kWStripe) {
+          if (((w + 1) & 1) == 0) rows((w + 1) >> 1);
+          unpack((w + 1) & 1, fa[cur ^ 1], fb[cur ^ 1]);
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            acc[m][n] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[cur][m], fb[cur][n], acc[m][n],
+                                                                        4, 4, 0, scale, 0, scale);
+      }
+    } else {
+#pragma unroll 1
+      for (int c = 0; c < (int)(kWStripe / 2); ++c) {  // 2-word chunks
+        ulonglong2 A[4], B[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          A[m] = *reinterpret_cast<const ulonglong2*>(sb + (la + 32 * m) * kWRowB + c * 16);
+          B[m] = *reinterpret_cast<const ulonglong2*>(sb + (lb + 32 * m) * kWRowB + c * 16);
+        }
+        for (int wd = 0; wd < 2; ++wd) {
+#pragma unroll 1
+          for (int half = 0; half < 2; ++half) {
+            const int sh = 32 * half + 16 * h;
+            v4i fa[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+              fa[m] = unpack16((uint32_t)((wd ? A[m].y : A[m].x) >> sh) & 0xFFFFu, lut);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+              const v4i fb = unpack16((uint32_t)((wd ? B[n].y : B[n].x) >> sh) & 0xFFFFu, lut);
+#pragma unroll
+              for (int m = 0; m < 4; ++m)
+                acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m], fb, acc[m][n], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+  }
+  // epilogue: row = (reg&3) + 8*(reg>>2) + 4h within a 32x32 MFMA tile, col = lane&31
+  const int64_t rowb = ti * kWTile + wr * 128, colb = tj * kWTile + wc * 128;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int64_t rw = rowb + 32 * m + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int64_t cl = colb + 32 * n + r;
+        const uint32_t v = (uint32_t)acc[m][n][reg];
+        if (rw < F && cl < F && cl > rw) {
+          if (gridDim.y == 1) out[rw * F + cl] = v;
+          else if (v) atomicAdd(&out[rw * F + cl], v);
+        }
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_pair_gram_fp4(const unsigned long long* __restrict__ bm,
                                                         int64_t Wp, int64_t F, int64_t n_tiles,
                                                         int64_t n_blocks, int scale,
@@ -488,6 +660,11 @@ static bool gram_lds() {
   const char* e = std::getenv("KMLS_GRAM_LDS");
   return !(e && e[0] == '0');
 }
+// KMLS_GRAM_TILE=256: the wide-tile LDS-staged kernel (4x4 MFMA tiles per wave)
+static bool gram_wide() {
+  const char* e = std::getenv("KMLS_GRAM_TILE");
+  return e && std::string(e) == "256";
+}
 
 void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s) {
   if (F < 2) return;
@@ -514,6 +691,26 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
     ks = std::max<int64_t>(ks, (Wp + (1 << 17) - 1) >> 17);
     hipLaunchKernelGGL(k_pair_gram_fp4, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
                        (const unsigned long long*)bm, Wp, F, nt, blocks, scale, out);
+  } else if (gram_wide()) {
+    const int64_t ntw = (F + kWTile - 1) / kWTile;
+    const int64_t bw = ntw * (ntw + 1) / 2;
+    static const int64_t slots_w = [] {
+      int dev = 0;
+      hipDeviceProp_t p;
+      if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)256;
+      return (int64_t)std::max(1, p.multiProcessorCount);  // one 4-wave block per CU (256 AGPRs)
+    }();
+    const int64_t n_stripes = (Wp + kWStripe - 1) / kWStripe;
+    int64_t ksw = std::max<int64_t>(1, std::min<int64_t>(slots_w / bw, Wp / 256));
+    // FP4: a block's f32 accumulators stay exact while its stripes (512 transactions each)
+    // number < 2^15
+    if (fp4 == 1) ksw = std::max<int64_t>(ksw, (n_stripes + 32767) / 32768 + 1);
+    if (fp4 == 1)
+      hipLaunchKernelGGL(k_pair_gram_wide<true>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
+                         (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out);
+    else
+      hipLaunchKernelGGL(k_pair_gram_wide<false>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
+                         (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out);
   } else if (gram_lds() || fp4 == 1) {
     static const int64_t slots_lds = [] {
       int dev = 0, per_cu = 1;

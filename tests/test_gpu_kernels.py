@@ -41,7 +41,7 @@ def _onehot(tx):
     return X
 
 
-@pytest.mark.parametrize("use_mfma", [False, True, "fp4", "fp4direct", "direct"])
+@pytest.mark.parametrize("use_mfma", [False, True, "fp4", "fp4direct", "direct", "wide", "widefp4"])
 @pytest.mark.parametrize("shape,ms,n_tx", [("tiny", 0.02, None), ("ds2_weak", 0.03, None),
                                              ("tiny", 0.01, 5000), ("ds2", 0.05, 777),
                                              ("ds2_weak", 0.03, 70000)])
@@ -52,6 +52,11 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
         use_mfma = True
     if use_mfma == "fp4direct":  # the same operands with direct (unstaged) loads
         monkeypatch.setenv("KMLS_GRAM_FP4", "direct")
+        use_mfma = True
+    if use_mfma in ("wide", "widefp4"):  # 256-row block tiles, 4x4 MFMA tiles per wave
+        monkeypatch.setenv("KMLS_GRAM_TILE", "256")
+        if use_mfma == "widefp4":
+            monkeypatch.setenv("KMLS_GRAM_FP4", "1")
         use_mfma = True
     if use_mfma == "direct":  # the direct-load MFMA gram (the default stages stripes in LDS)
         monkeypatch.setenv("KMLS_GRAM_LDS", "0")
@@ -87,7 +92,7 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     np.testing.assert_array_equal(pc.reshape(max(F, 1), Wp).sum(1)[:F], counts)
 
 
-@pytest.mark.parametrize("fp4", ["1", "direct"])
+@pytest.mark.parametrize("fp4", ["1", "direct", "wide"])
 def test_pair_gram_fp4_exact_past_2_24_transactions(gpu_mod, fp4, monkeypatch):
     """FP4 operands accumulate in f32, exact only below 2^24 per block: with more transactions
     than that the split-K must keep every block's slice under it.  Checked against the popcount
@@ -106,6 +111,9 @@ def test_pair_gram_fp4_exact_past_2_24_transactions(gpu_mod, fp4, monkeypatch):
     torch.cuda.synchronize()
     g.encode_bitmaps(bm.data_ptr(), Wp, 0)
     g.pair_counts(bm.data_ptr(), Wp, ref.data_ptr(), False)
+    if fp4 == "wide":
+        monkeypatch.setenv("KMLS_GRAM_TILE", "256")
+        fp4 = "1"
     monkeypatch.setenv("KMLS_GRAM_FP4", fp4)
     g.pair_counts(bm.data_ptr(), Wp, got.data_ptr(), True)
     g.synchronize()
