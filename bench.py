@@ -128,6 +128,78 @@ def run_config2(N, tx, names, tie, steps: int, verify: bool) -> dict:
     return out
 
 
+# digest of the 10M x 1M @0.001 itemsets of the seeded synthetic data (924 itemsets, depth 4),
+# computed by the CPU miner (N.mine_cpu) over the whole dataset on the build host; the GPU
+# tx-DP result must equal it at every N
+C3_DIGEST = "d3b31400a6ebfffbbdac749329a5c1e6"
+
+
+def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: int = 1) -> dict:
+    """BASELINE config 3 (10M transactions x 1M items, min_support 0.001) on all ranks of the job:
+    transaction-DP mining (each rank generates and encodes only its shard; supports, gram and
+    per-level candidate counts all-reduced), so support/encode/gram work shrinks with N.  The
+    communicator is the host-staged one unless KMLS_BENCH_C3_COMM names another (the native
+    RCCL communicator has not run with more than one rank on real GPUs yet).  Verified by the
+    itemset digest, which must not depend on N."""
+    import torch
+    import torch.distributed as dist
+    from kubernetes_machine_learning_server_amd.data.synthetic import SHAPES
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner, shard_bounds
+    comm = os.environ.get("KMLS_BENCH_C3_COMM", "host")
+    prev = os.environ.get("KMLS_COMM")
+    os.environ["KMLS_COMM"] = comm
+    try:
+        shape = SHAPES["10Mx1M"]
+        T = shape.n_tx
+        lo, hi, _ = shard_bounds(T, world, rank)
+        ptr, items = N.synth_transactions(T, shape.n_items, shape.mean_len, shape.n_genres,
+                                          shape.genre_affinity, 0.85, 0, 0, lo, hi)
+        dm = DistMiner(ptr, items, shape.n_items, 0.001, device=device, mode="tx",
+                       support_tiles=4, global_n_tx=T)
+
+        def bar():
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+                torch.cuda.synchronize()
+        r = None
+        for _ in range(warmup):
+            r = dm.step(download=True)
+        bar()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r = dm.step(download=True)
+        dm.synchronize()
+        bar()
+        ms = (time.perf_counter() - t0) * 1000.0 / max(1, steps)
+        if world > 1:
+            t = torch.tensor([ms], dtype=torch.float64,
+                             device="cuda" if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms = float(t.item())
+        st = r["stats"]
+        out = {"model": "fpgrowth-10Mx1M-synthetic", "global_batch": T, "seq_len": shape.n_items,
+               "min_support": 0.001, "n_gpus": world, "parallelism": f"tx-dp{world}",
+               "comm": comm, "steps": steps, "ms_per_step": round(ms, 3),
+               "tx_per_s": round(T / (ms / 1000.0), 1),
+               "n_frequent_items": int(st.get("n_frequent_items", 0)),
+               "phases_ms": {k: round(v, 3) for k, v in (st.get("phases_ms") or {}).items()}}
+        if rank == 0:
+            d = _digest_of(N, r["trie"])
+            n = int(d["n"])
+            out["n_itemsets"] = n
+            out["itemsets_per_s"] = round(n / (ms / 1000.0), 1)
+            out["digest"] = d["digest"]
+            out["verified_digest"] = (d["digest"] == C3_DIGEST) if C3_DIGEST else None
+        del dm
+        return out
+    finally:
+        if prev is None:
+            os.environ.pop("KMLS_COMM", None)
+        else:
+            os.environ["KMLS_COMM"] = prev
+
+
 def run_serve(shape: str, qps_list, duration: float, backend: str) -> dict:
     """p50/p99 of POST /api/recommend/ at fixed offered QPS (the real uvicorn app over a PVC
     populated by the real job on the same synthetic data)."""
@@ -169,6 +241,8 @@ def main() -> int:
                     help="leave the rule-map build out of the step (A/B only)")
     ap.add_argument("--cpu", action="store_true", help="native CPU miner (no GPU)")
     ap.add_argument("--no-config2", action="store_true", help="skip BASELINE config 2 (0.01)")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="skip BASELINE config 3 (10M x 1M tx-DP over all ranks)")
     ap.add_argument("--serve-qps", default="2000,5000,10000",
                     help="offered QPS points for the serving half ('' = skip)")
     ap.add_argument("--serve-duration", type=float, default=3.0)
@@ -331,6 +405,13 @@ def main() -> int:
     }
     if "phases_ms" in st:
         out["phases_ms"] = st["phases_ms"]
+    if not args.cpu and not args.no_config3:
+        try:
+            c3 = run_config3(N, world, rank, device)
+        except Exception as e:  # the headline stands on its own
+            c3 = {"error": repr(e)[:300]}
+        if rank == 0:
+            out["config3"] = c3
     if world == 1 and not args.cpu and not args.no_config2 and rank == 0:
         out["config2"] = run_config2(N, tx, names, tie, steps=10, verify=not args.no_verify)
     if world == 1 and rank == 0 and args.serve_qps:

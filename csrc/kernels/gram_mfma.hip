@@ -368,11 +368,13 @@ constexpr int64_t kWStripe = 8;
 constexpr int kWRowB = 80;                        // bytes per staged row (64 + 16 pad)
 constexpr int kWStageB = 2 * kWTile * kWRowB;     // one stripe of A and B rows (40 KB)
 
-template <bool FP4>
+// MODE 0: i8 operands (LUT unpack), 1: FP4 operands (LUT unpack), 2: FP4 masked nibbles (below)
+template <int MODE>
 __global__ __launch_bounds__(256, 1) void k_pair_gram_wide(const unsigned long long* __restrict__ bm,
                                                            int64_t Wp, int64_t F, int64_t n_tiles,
                                                            int64_t n_blocks, int scale,
                                                            uint32_t* __restrict__ out) {
+  constexpr bool FP4 = MODE != 0;
   __shared__ uint2 lut[256];
   __shared__ uint32_t lut4[256];
   __shared__ __attribute__((aligned(16))) unsigned char stage[2][kWStageB];
@@ -441,7 +443,47 @@ __global__ __launch_bounds__(256, 1) void k_pair_gram_wide(const unsigned long l
     __syncthreads();  // stripe `it` visible; buffer buf^1 (stripe it-1) no longer read
     if (it + 1 < my_stripes) gload(it + 1, R);
     const unsigned char* sb = stage[buf];
-    if constexpr (FP4) {
+    if constexpr (MODE == 2) {
+      // Masked nibbles, no unpack: a lane's 16 raw bytes ARE 32 FP4 elements (nibble e = bits
+      // 4e..4e+3).  Masking every nibble to one bit position j leaves element value bit_j * v_j
+      // (e2m1 0b0001 = 0.5, 0b0010 = 1.0, 0b0100 = 2.0; bit 3 is the sign bit, so it is shifted
+      // down to bit 2 first), and the block scale s_j = 1 / v_j (e8m0 128 / 127 / 126) makes every
+      // coinciding pair contribute exactly 1.0.  Four MFMAs (j = 0..3) cover the 256 transactions
+      // of a 4-word chunk: lane half h holds words 2h, 2h+1.  Operand preparation is one AND per
+      // VGPR (two for j = 3) and one ds_read_b128 per fragment per 4 words, instead of four LDS
+      // table reads per fragment per word: the LDS pipe leaves the matrix cores' way.
+#pragma unroll
+      for (int c = 0; c < (int)(kWStripe / 4); ++c) {  // 4-word chunks
+        v4i A[4], B[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          A[m] = *reinterpret_cast<const v4i*>(sb + (la + 32 * m) * kWRowB + c * 32 + h * 16);
+          B[m] = *reinterpret_cast<const v4i*>(sb + (lb + 32 * m) * kWRowB + c * 32 + h * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int msk = j == 0 ? 0x11111111 : j == 1 ? 0x22222222 : 0x44444444;
+          const int sc = j == 0 ? 128 : j == 1 ? 127 : 126;
+          v8i fa[4], fb[4];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              fa[m][d] = (j == 3 ? (int)((uint32_t)A[m][d] >> 1) : A[m][d]) & msk;
+              fb[m][d] = (j == 3 ? (int)((uint32_t)B[m][d] >> 1) : B[m][d]) & msk;
+              fa[m][d + 4] = 0;
+              fb[m][d + 4] = 0;
+            }
+          }
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+              acc[m][n] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[m], fb[n], acc[m][n], 4, 4,
+                                                                          0, sc, 0, sc);
+        }
+      }
+    } else if constexpr (FP4) {
       // software-pipelined over the stripe's 8 words: word s+1's fragments are unpacked (LDS
       // table reads) before word s's 16 MFMAs issue, so with one wave per SIMD the table latency
       // hides behind ~512 matrix-core cycles instead of stalling them
@@ -645,12 +687,17 @@ __global__ __launch_bounds__(256) void k_pair_gram_fp4(const unsigned long long*
 
 }  // namespace
 
-// KMLS_GRAM_FP4=1: the FP4 (e2m1, block-scaled MFMA) variant; KMLS_GRAM_FP4_SCALE overrides the
-// e8m0 scale byte (127 = 1.0)
-// (=1: the LDS-staged kernel with FP4 operands; =direct: the direct-load FP4 kernel)
+// Operand format of the MFMA gram (KMLS_GRAM_FP4):
+//   unset / "mask": masked-nibble FP4 operands in the wide-tile kernel (the default: 100M x 754
+//                   items 23.1 -> 14.3 ms, config-5 width 679 -> 387 ms; profiles/r2_gram_wide.md)
+//   "0": i8 operands (LUT unpack) — the 128-tile LDS-staged kernel, or the wide one with
+//        KMLS_GRAM_TILE=256, or the direct-load one with KMLS_GRAM_LDS=0
+//   "1": FP4 operands through the LUT unpack (128-tile LDS-staged, or wide with KMLS_GRAM_TILE=256)
+//   "direct": FP4 LUT operands, direct (unstaged) loads
+// KMLS_GRAM_FP4_SCALE overrides the e8m0 scale byte of the LUT FP4 paths (127 = 1.0).
 static int gram_fp4() {
   const char* e = std::getenv("KMLS_GRAM_FP4");
-  if (!e) return 0;
+  if (!e || !e[0] || std::string(e) == "mask") return 3;
   if (e[0] == '1') return 1;
   return std::string(e) == "direct" ? 2 : 0;
 }
@@ -691,7 +738,7 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
     ks = std::max<int64_t>(ks, (Wp + (1 << 17) - 1) >> 17);
     hipLaunchKernelGGL(k_pair_gram_fp4, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
                        (const unsigned long long*)bm, Wp, F, nt, blocks, scale, out);
-  } else if (gram_wide()) {
+  } else if (gram_wide() || fp4 == 3) {
     const int64_t ntw = (F + kWTile - 1) / kWTile;
     const int64_t bw = ntw * (ntw + 1) / 2;
     static const int64_t slots_w = [] {
@@ -704,12 +751,15 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
     int64_t ksw = std::max<int64_t>(1, std::min<int64_t>(slots_w / bw, Wp / 256));
     // FP4: a block's f32 accumulators stay exact while its stripes (512 transactions each)
     // number < 2^15
-    if (fp4 == 1) ksw = std::max<int64_t>(ksw, (n_stripes + 32767) / 32768 + 1);
-    if (fp4 == 1)
-      hipLaunchKernelGGL(k_pair_gram_wide<true>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
+    if (fp4 == 1 || fp4 == 3) ksw = std::max<int64_t>(ksw, (n_stripes + 32767) / 32768 + 1);
+    if (fp4 == 3)
+      hipLaunchKernelGGL(k_pair_gram_wide<2>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
+                         (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out);
+    else if (fp4 == 1)
+      hipLaunchKernelGGL(k_pair_gram_wide<1>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
                          (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out);
     else
-      hipLaunchKernelGGL(k_pair_gram_wide<false>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
+      hipLaunchKernelGGL(k_pair_gram_wide<0>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
                          (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out);
   } else if (gram_lds() || fp4 == 1) {
     static const int64_t slots_lds = [] {

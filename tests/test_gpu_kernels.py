@@ -41,25 +41,28 @@ def _onehot(tx):
     return X
 
 
-@pytest.mark.parametrize("use_mfma", [False, True, "fp4", "fp4direct", "direct", "wide", "widefp4"])
+# MFMA gram variants (KMLS_GRAM_FP4 / KMLS_GRAM_TILE / KMLS_GRAM_LDS): True = the default
+# (masked-nibble FP4, wide tiles); the others are the A/B kernels kept selectable
+_GRAM_ENV = {
+    True: {},
+    "i8": {"KMLS_GRAM_FP4": "0"},                                   # 128-tile LDS-staged i8
+    "direct": {"KMLS_GRAM_FP4": "0", "KMLS_GRAM_LDS": "0"},         # direct-load i8
+    "fp4": {"KMLS_GRAM_FP4": "1"},                                  # 128-tile LDS, FP4 LUT unpack
+    "fp4direct": {"KMLS_GRAM_FP4": "direct"},                       # direct-load FP4 LUT unpack
+    "wide": {"KMLS_GRAM_FP4": "0", "KMLS_GRAM_TILE": "256"},        # wide tiles, i8
+    "widefp4": {"KMLS_GRAM_FP4": "1", "KMLS_GRAM_TILE": "256"},     # wide tiles, FP4 LUT unpack
+}
+
+
+@pytest.mark.parametrize("use_mfma", [False] + list(_GRAM_ENV))
 @pytest.mark.parametrize("shape,ms,n_tx", [("tiny", 0.02, None), ("ds2_weak", 0.03, None),
                                              ("tiny", 0.01, 5000), ("ds2", 0.05, 777),
                                              ("ds2_weak", 0.03, 70000)])
 def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     import torch
-    if use_mfma == "fp4":  # the e2m1 block-scaled MFMA gram, LDS-staged stripes
-        monkeypatch.setenv("KMLS_GRAM_FP4", "1")
-        use_mfma = True
-    if use_mfma == "fp4direct":  # the same operands with direct (unstaged) loads
-        monkeypatch.setenv("KMLS_GRAM_FP4", "direct")
-        use_mfma = True
-    if use_mfma in ("wide", "widefp4"):  # 256-row block tiles, 4x4 MFMA tiles per wave
-        monkeypatch.setenv("KMLS_GRAM_TILE", "256")
-        if use_mfma == "widefp4":
-            monkeypatch.setenv("KMLS_GRAM_FP4", "1")
-        use_mfma = True
-    if use_mfma == "direct":  # the direct-load MFMA gram (the default stages stripes in LDS)
-        monkeypatch.setenv("KMLS_GRAM_LDS", "0")
+    if use_mfma is not False:
+        for k, v in _GRAM_ENV[use_mfma].items():
+            monkeypatch.setenv(k, v)
         use_mfma = True
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     tx = generate(shape, seed=11, n_tx=n_tx)
@@ -92,7 +95,7 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     np.testing.assert_array_equal(pc.reshape(max(F, 1), Wp).sum(1)[:F], counts)
 
 
-@pytest.mark.parametrize("fp4", ["1", "direct", "wide"])
+@pytest.mark.parametrize("fp4", ["1", "direct", "wide", "mask"])
 def test_pair_gram_fp4_exact_past_2_24_transactions(gpu_mod, fp4, monkeypatch):
     """FP4 operands accumulate in f32, exact only below 2^24 per block: with more transactions
     than that the split-K must keep every block's slice under it.  Checked against the popcount
