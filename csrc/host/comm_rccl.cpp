@@ -132,7 +132,15 @@ Comm::Comm(int rank, int world, const std::string& uid, int device, const std::s
   if (backend != "rccl" && backend != "host")
     throw std::runtime_error("kmls comm: backend must be 'rccl' or 'host'");
   if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("kmls comm: hipSetDevice");
-  if (world == 1) return;  // collectives degenerate to copies; no communicator needed
+  // one rank: collectives degenerate to copies and no communicator is needed — unless
+  // KMLS_COMM_FORCE=1 asks for a real one-rank RCCL communicator (tests the RCCL path: loading,
+  // non-blocking init, the collectives and teardown, on a one-GPU box)
+  const char* fe = std::getenv("KMLS_COMM_FORCE");
+  const bool force = fe && fe[0] == '1' && backend == "rccl";
+  if (world == 1 && !force) {
+    direct_ = true;
+    return;
+  }
   if (backend == "host") {
     host_ = std::make_unique<ShmComm>(rank, world, uid);
     return;
@@ -188,7 +196,7 @@ void Comm::abort() {
 // never completes) aborts the communicator and raises instead of hanging the job.
 void Comm::wait_stream(void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (world_ == 1) {
+  if (direct_) {
     if (hipStreamSynchronize(s) != hipSuccess) throw std::runtime_error("kmls comm: stream sync failed");
     return;
   }
@@ -222,7 +230,7 @@ void* Comm::stage(size_t bytes) {
 void Comm::all_reduce(const void* send, void* recv, size_t count, CommDtype t, bool max_op,
                       void* stream) {
   const size_t bytes = count * comm_dtype_bytes(t);
-  if (world_ == 1) {
+  if (direct_) {
     if (send != recv)
       (void)hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
     return;
@@ -248,7 +256,7 @@ void Comm::all_reduce(const void* send, void* recv, size_t count, CommDtype t, b
 
 void Comm::all_gather(const void* send, void* recv, size_t count, CommDtype t, void* stream) {
   const size_t bytes = count * comm_dtype_bytes(t);
-  if (world_ == 1) {
+  if (direct_) {
     if (send != recv)
       (void)hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
     return;

@@ -114,6 +114,7 @@ class Comm {
   void progress(const char* what);
   void* stage(size_t bytes);
   int rank_ = 0, world_ = 1;
+  bool direct_ = false;  // one rank, no communicator: collectives are local copies
   double timeout_s_ = 300.0;
   std::string backend_;
   void* comm_ = nullptr;

@@ -569,6 +569,120 @@ __global__ __launch_bounds__(256, 1) void k_pair_gram_wide(const unsigned long l
   }
 }
 
+// Masked-nibble FP4 with two waves per SIMD (KMLS_GRAM_FP4=mask8): 512-thread blocks of 8 waves
+// (2 row x 4 column groups), each wave a 128x64 output block = 4x2 MFMA tiles (8 accumulators,
+// 128 AGPRs), so each SIMD holds two waves and one issues while the other waits on an operand or
+// the matrix pipe.  Same 256-row block tiles, stripes and LDS slab as k_pair_gram_wide; a fragment
+// now feeds 2 or 4 MFMAs instead of 4.
+__global__ __launch_bounds__(512, 1) void k_pair_gram_mask8(const unsigned long long* __restrict__ bm,
+                                                            int64_t Wp, int64_t F, int64_t n_tiles,
+                                                            int64_t n_blocks,
+                                                            uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) unsigned char stage[2][kWStageB];
+  const int64_t orig = blockIdx.x;
+  const int64_t q = n_blocks / 8, rr = n_blocks % 8, xcd = orig % 8;
+  int64_t idx = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  int64_t ti = 0;
+  while (idx >= n_tiles - ti) { idx -= n_tiles - ti; ++ti; }
+  const int64_t tj = ti + idx;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int r = lane & 31, h = lane >> 5;
+  // staging: thread t copies 16-byte segment (t & 3) of local rows (t >> 2) + 128 k, k = 0..3
+  const int seg = tid & 3, lrow0 = tid >> 2;
+  const int64_t W2 = Wp >> 1;
+  const ulonglong2* src[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int lr = lrow0 + 128 * k;
+    const int64_t grow = lr < kWTile ? ti * kWTile + lr : tj * kWTile + (lr - kWTile);
+    src[k] = grow < F ? reinterpret_cast<const ulonglong2*>(bm + grow * Wp) : nullptr;
+  }
+  const int64_t ks = gridDim.y, y = blockIdx.y;
+  const int64_t n_stripes = (Wp + kWStripe - 1) / kWStripe;
+  const int64_t my_stripes = y < n_stripes ? (n_stripes - y + ks - 1) / ks : 0;
+  auto gload = [&](int64_t it, ulonglong2 (&R)[4]) {
+    const int64_t u = (it * ks + y) * (kWStripe / 2) + seg;
+    const bool in = u < W2;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) R[k] = (src[k] && in) ? src[k][u] : make_ulonglong2(0, 0);
+  };
+  auto swrite = [&](int buf, const ulonglong2 (&R)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      *reinterpret_cast<ulonglong2*>(&stage[buf][(lrow0 + 128 * k) * kWRowB + seg * 16]) = R[k];
+  };
+  v16f acc[4][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[m][n] = v16f{};
+  const int la = wr * 128 + r;          // + 32 m
+  const int lb = kWTile + wc * 64 + r;  // + 32 n
+  ulonglong2 R[4];
+  if (my_stripes > 0) gload(0, R);
+  for (int64_t it = 0; it < my_stripes; ++it) {
+    const int buf = (int)(it & 1);
+    swrite(buf, R);
+    __syncthreads();
+    if (it + 1 < my_stripes) gload(it + 1, R);
+    const unsigned char* sb = stage[buf];
+#pragma unroll
+    for (int c = 0; c < (int)(kWStripe / 4); ++c) {
+      v4i A[4], B[2];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        A[m] = *reinterpret_cast<const v4i*>(sb + (la + 32 * m) * kWRowB + c * 32 + h * 16);
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        B[n] = *reinterpret_cast<const v4i*>(sb + (lb + 32 * n) * kWRowB + c * 32 + h * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int msk = j == 0 ? 0x11111111 : j == 1 ? 0x22222222 : 0x44444444;
+        const int sc = j == 0 ? 128 : j == 1 ? 127 : 126;
+        v8i fa[4], fb[2];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            fa[m][d] = (j == 3 ? (int)((uint32_t)A[m][d] >> 1) : A[m][d]) & msk;
+            fa[m][d + 4] = 0;
+          }
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            fb[n][d] = (j == 3 ? (int)((uint32_t)B[n][d] >> 1) : B[n][d]) & msk;
+            fb[n][d + 4] = 0;
+          }
+        }
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            acc[m][n] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[m], fb[n], acc[m][n], 4, 4, 0,
+                                                                        sc, 0, sc);
+      }
+    }
+  }
+  const int64_t rowb = ti * kWTile + wr * 128, colb = tj * kWTile + wc * 64;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int64_t rw = rowb + 32 * m + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int64_t cl = colb + 32 * n + r;
+        const uint32_t v = (uint32_t)acc[m][n][reg];
+        if (rw < F && cl < F && cl > rw) {
+          if (gridDim.y == 1) out[rw * F + cl] = v;
+          else if (v) atomicAdd(&out[rw * F + cl], v);
+        }
+      }
+}
+
 __global__ __launch_bounds__(256) void k_pair_gram_fp4(const unsigned long long* __restrict__ bm,
                                                         int64_t Wp, int64_t F, int64_t n_tiles,
                                                         int64_t n_blocks, int scale,
@@ -698,6 +812,7 @@ __global__ __launch_bounds__(256) void k_pair_gram_fp4(const unsigned long long*
 static int gram_fp4() {
   const char* e = std::getenv("KMLS_GRAM_FP4");
   if (!e || !e[0] || std::string(e) == "mask") return 3;
+  if (std::string(e) == "mask8") return 4;  // masked nibbles, 8 waves (2 per SIMD), A/B
   if (e[0] == '1') return 1;
   return std::string(e) == "direct" ? 2 : 0;
 }
@@ -738,7 +853,7 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
     ks = std::max<int64_t>(ks, (Wp + (1 << 17) - 1) >> 17);
     hipLaunchKernelGGL(k_pair_gram_fp4, dim3((unsigned)blocks, (unsigned)ks), dim3(256), 0, s,
                        (const unsigned long long*)bm, Wp, F, nt, blocks, scale, out);
-  } else if (gram_wide() || fp4 == 3) {
+  } else if (gram_wide() || fp4 >= 3) {
     const int64_t ntw = (F + kWTile - 1) / kWTile;
     const int64_t bw = ntw * (ntw + 1) / 2;
     static const int64_t slots_w = [] {
@@ -751,8 +866,11 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
     int64_t ksw = std::max<int64_t>(1, std::min<int64_t>(slots_w / bw, Wp / 256));
     // FP4: a block's f32 accumulators stay exact while its stripes (512 transactions each)
     // number < 2^15
-    if (fp4 == 1 || fp4 == 3) ksw = std::max<int64_t>(ksw, (n_stripes + 32767) / 32768 + 1);
-    if (fp4 == 3)
+    if (fp4 == 1 || fp4 >= 3) ksw = std::max<int64_t>(ksw, (n_stripes + 32767) / 32768 + 1);
+    if (fp4 == 4)
+      hipLaunchKernelGGL(k_pair_gram_mask8, dim3((unsigned)bw, (unsigned)ksw), dim3(512), 0, s,
+                         (const unsigned long long*)bm, Wp, F, ntw, bw, out);
+    else if (fp4 == 3)
       hipLaunchKernelGGL(k_pair_gram_wide<2>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
                          (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out);
     else if (fp4 == 1)

@@ -125,7 +125,9 @@ class _GpuOps:
             torch.cuda.set_device(dm.device)
             backend = comm_backend()
             make_uid = N.host_comm_unique_id if backend == "host" else N.comm_unique_id
-            uid = [make_uid() if dm.rank == 0 and dm.world > 1 else b"\0" * 128]
+            # KMLS_COMM_FORCE=1: a real one-rank RCCL communicator (the RCCL path's test hook)
+            forced = dm.world == 1 and backend == "rccl" and os.environ.get("KMLS_COMM_FORCE") == "1"
+            uid = [make_uid() if dm.rank == 0 and (dm.world > 1 or forced) else b"\0" * 128]
             if dm.world > 1:
                 dist.broadcast_object_list(uid, src=0)
             self.comm = N.Comm(dm.rank, dm.world, uid[0], dm.device, backend)

@@ -80,3 +80,34 @@ def test_txdp_multi_rank_on_one_gpu(world, shape):
                 assert d == rd["digest"], path
     spans = sorted(r[2] for r in res)
     assert spans[0][0] == 0 and spans[-1][1] == tx.n_tx
+
+
+def _rccl_worker(shape, out_q):
+    os.environ.update(KMLS_COMM="rccl", KMLS_COMM_FORCE="1", KMLS_COMM_TIMEOUT_S="60")
+    from kubernetes_machine_learning_server_amd.ops import native
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+    tx, ms = _data(shape)
+    dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, ms, device=0, mode="tx")
+    assert dm.ops.comm.backend == "rccl"
+    t = dm.step(download=True)["trie"]
+    out_q.put(native.load().trie_digest(t["parent"], t["item"], t["count"], t["depth"])["digest"])
+
+
+@pytest.mark.parametrize("shape", ["ds1", "large"])
+def test_txdp_through_a_one_rank_rccl_communicator(shape):
+    """The native RCCL communicator (dlopen of the RCCL library, non-blocking init polled against
+    the deadline, all-reduces of supports, gram and per-level counts, teardown) forced on for one
+    rank: the multi-GPU transport itself needs one GPU per rank, but everything around it runs
+    here.  In a child process, so a failure of the library cannot take the test session down."""
+    from kubernetes_machine_learning_server_amd.ops import native
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(shape, q))
+    p.start()
+    d = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    tx, ms = _data(shape)
+    N = native.load()
+    ref = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
+    assert d == N.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])["digest"]
