@@ -13,11 +13,15 @@ Every run is verified against the native CPU miner by CONTENT: an order-independ
 all (itemset, support) pairs (``_native.trie_digest``) and an exact comparison of the rule map
 with the CPU-built index.
 
-Multi-GPU (``torchrun --nproc-per-node N``, one rank per GPU, RCCL): the replicated mode of
-``parallel.dist_miner`` — every rank holds the (small) dataset, ranks split the level-2 root
-classes by estimated cost on the device, and each mines and downloads its own sub-trie (strong
-scaling; the union over ranks is the full result, verified by combining the per-rank digests
-with one all-reduce after the timed loop).
+Multi-GPU (``torchrun --nproc-per-node N``, one rank per GPU): **weak scaling** by default —
+every rank mines its own ds1-shape dataset (rank 0 the seed's data, rank r a relabelled copy
+with permuted item ids and transaction order, so the same itemset count and depth but no
+shared bitmap word) with the native single-GPU path (``DistMiner(mode="local")``); ``value`` is
+the job total (sum of itemsets ÷ the slowest rank's step) and every rank verifies its own
+result by digest against the CPU miner.  A ds-sized problem is a ~0.3 ms chain of dependent
+level launches, so splitting ONE dataset over GPUs cannot scale; that strong-scaled form (the
+replicated root-class partition, ``--scaling strong``) is still timed at N > 1 and reported in
+the ``strong`` block, verified by combining the per-rank digests.
 
 Data: synthetic playlists of the reference's ds1/ds2 shape (2,246 playlists × 2,171 tracks,
 240k rows), calibrated by ``bench/calibrate.py`` to the published key curve, to the
@@ -247,6 +251,10 @@ def main() -> int:
                     help="offered QPS points for the serving half ('' = skip)")
     ap.add_argument("--serve-duration", type=float, default=3.0)
     ap.add_argument("--serve-backend", default="auto")
+    ap.add_argument("--scaling", choices=("weak", "strong"),
+                    default=os.environ.get("KMLS_BENCH_SCALING", "weak"),
+                    help="N>1: weak = one dataset per GPU (the job total; a 'strong' block "
+                         "reports one dataset split over the ranks); strong = that split only")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -255,21 +263,29 @@ def main() -> int:
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
-    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate, relabel
     from kubernetes_machine_learning_server_amd.ops import native
     from kubernetes_machine_learning_server_amd.serve.index import name_tie_rank
 
-    tx = generate(args.shape, seed=args.seed)
+    base_tx = generate(args.shape, seed=args.seed)
     N = native.load()
+    weak = args.scaling == "weak" and world > 1
+    # weak scaling: rank r mines its own dataset (rank 0 = the seed's data; rank r = a
+    # relabelled copy: permuted item ids and transaction order, same itemset count and depth)
+    tx = relabel(base_tx, rank) if weak else base_tx
     names = tx.names
     tie = name_tie_rank(names) if names else np.arange(tx.n_items, dtype=np.int32)
     rule_map = not args.no_rule_map and not args.cpu
 
     # KMLS_BENCH_DIST=gloo rehearses the N-rank path on fewer GPUs (ranks share devices round
     # robin; the step itself needs no collective, so only the bracket and the merge use gloo)
-    dist_backend = os.environ.get("KMLS_BENCH_DIST", "nccl")
+    dist_backend = os.environ.get("KMLS_BENCH_DIST", "gloo" if args.cpu else "nccl")
     device = local_rank
-    if world > 1:
+    if world > 1 and args.cpu:  # the CPU tier of the N-rank path (gloo, no device)
+        import datetime
+        import torch.distributed as dist
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
+    elif world > 1:
         import datetime
         import torch
         import torch.distributed as dist
@@ -286,9 +302,60 @@ def main() -> int:
         if world > 1:
             import torch
             import torch.distributed as dist
-            torch.cuda.synchronize()
+            if not args.cpu:
+                torch.cuda.synchronize()
             dist.barrier()
-            torch.cuda.synchronize()
+            if not args.cpu:
+                torch.cuda.synchronize()
+
+    def max_over_ranks(v: float) -> float:
+        if world == 1:
+            return v
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([v], dtype=torch.float64,
+                         device="cuda" if dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(obj):
+        if world == 1:
+            return [obj]
+        import torch.distributed as dist
+        parts = [None] * world
+        dist.all_gather_object(parts, obj)
+        return parts
+
+    def make_miner(mode: str, data, tie_):
+        from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+        m = DistMiner(data.tx_ptr, data.items, data.n_items, args.min_support, device=device,
+                      max_len=args.max_len, mfma=args.mfma, mode=mode)
+        m.set_tie_rank(tie_)
+        return m
+
+    def timed_loop(step, sync, warmup: int, steps: int):
+        """Steady-state loop: each step launches the next step's (identical) call before
+        waiting for its own (prefetch), so the GPU never idles on the host between calls.  The
+        last warmup step and the last timed step launch nothing ahead: exactly `steps` calls
+        run inside the timed bracket, and none is in flight when it opens."""
+        r = None
+        for i in range(warmup):
+            r = step(i < warmup - 1)
+        barrier_sync()
+        sync()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            r = step(i < steps - 1)
+        sync()
+        barrier_sync()
+        return r, (time.perf_counter() - t0) * 1000.0 / max(steps, 1)
+
+    def dm_step(m):
+        def step(prefetch=False):  # the itemset count is reduced over ranks once, after timing
+            return m.step(download=True, reduce_count=False,
+                          prefetch=prefetch and not args.no_prefetch,
+                          rule_index=rule_map)["trie"]
+        return step
 
     if args.cpu:
         step = lambda prefetch=False: N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items,
@@ -297,68 +364,81 @@ def main() -> int:
         dtype = "uint64-bitmap/int32-count (CPU)"
         dm = None
     else:
-        from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
-        dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, args.min_support, device=device,
-                       max_len=args.max_len, mfma=args.mfma)
-        dm.set_tie_rank(tie)
-
-        def step(prefetch=False):  # the itemset count is reduced over ranks once, after timing
-            return dm.step(download=True, reduce_count=False,
-                           prefetch=prefetch and not args.no_prefetch,
-                           rule_index=rule_map)["trie"]
-
-        sync = dm.synchronize
+        dm = make_miner("local" if weak else "auto", tx, tie)
+        step, sync = dm_step(dm), dm.synchronize
         dtype = "uint64-bitmap/int32-count"
 
-    # Steady-state loop: each step launches the next step's (identical) call before waiting for
-    # its own (prefetch), so the GPU never idles on the host between calls.  The last warmup step
-    # and the last timed step launch nothing ahead: exactly `steps` calls run inside the timed
-    # bracket, and none is in flight when it opens.
-    r = None
-    for i in range(args.warmup):
-        r = step(i < args.warmup - 1)
-    barrier_sync()
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        r = step(i < args.steps - 1)
-    sync()
-    barrier_sync()
-    t1 = time.perf_counter()
-    ms_step = (t1 - t0) * 1000.0 / max(args.steps, 1)
+    r, ms_step = timed_loop(step, sync, args.warmup, args.steps)
+    ms_step = max_over_ranks(ms_step)
     st = r["stats"]
 
-    # content digest of the last step's result; replicated mode: level-1 nodes are on every
-    # rank, counted by rank 0 only, and the per-rank (sum, xor) parts combine exactly
-    d = _digest_of(N, r, 0 if rank == 0 else 2)
-    n_itemsets, dsum, dxor = int(d["n"]), int(d["sum"]), int(d["xor"])
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        t = torch.tensor([ms_step], dtype=torch.float64,
-                         device="cuda" if dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms_step = float(t.item())
-        parts = [None] * world
-        dist.all_gather_object(parts, (n_itemsets, dsum, dxor))
-        n_itemsets = sum(p[0] for p in parts)
-        dsum = sum(p[1] for p in parts) % (1 << 64)
-        dxor = 0
-        for p in parts:
-            dxor ^= p[2]
-    digest = f"{dsum:016x}{dxor:016x}"
-
-    verified = verified_ix = None
-    if rank == 0 and not args.no_verify:
-        ref = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, args.min_support, args.max_len)
+    def cpu_check(data, res, digest_hex, n):
+        """(digest ok, rule map ok) of one result against the native CPU miner on `data`."""
+        if args.no_verify:
+            return None, None
+        ref = N.mine_cpu(data.tx_ptr, data.items, data.n_items, args.min_support, args.max_len)
         rd = _digest_of(N, ref)
-        verified = rd["digest"] == digest and int(rd["n"]) == n_itemsets
-        if rule_map and "index" in r:
-            verified_ix = _index_equal(r["index"], _cpu_index(N, tx, args.min_support, names))
+        ok = rd["digest"] == digest_hex and int(rd["n"]) == n
+        ok_ix = None
+        if rule_map and "index" in res:
+            ok_ix = _index_equal(res["index"], _cpu_index(N, data, args.min_support, data.names))
+        return ok, ok_ix
+
+    def merged_digest(res, world_: int):
+        """Digest of a replicated-mode result over ranks: level-1 nodes are on every rank and
+        counted by rank 0 only; the per-rank (sum, xor) parts combine exactly."""
+        d = _digest_of(N, res, 0 if rank == 0 else 2)
+        parts = gather((int(d["n"]), int(d["sum"]), int(d["xor"]))) if world_ > 1 else \
+            [(int(d["n"]), int(d["sum"]), int(d["xor"]))]
+        n = sum(q[0] for q in parts)
+        dsum = sum(q[1] for q in parts) % (1 << 64)
+        dxor = 0
+        for q in parts:
+            dxor ^= q[2]
+        return n, f"{dsum:016x}{dxor:016x}"
+
+    if weak:  # every rank verifies its own dataset's result; the job total is the sum
+        d = _digest_of(N, r)
+        n_own, digest = int(d["n"]), d["digest"]
+        ok, ok_ix = cpu_check(tx, r, digest, n_own)
+        parts = gather((n_own, ok, ok_ix, digest))
+        n_itemsets = sum(q[0] for q in parts)
+        verified = None if args.no_verify else all(bool(q[1]) for q in parts)
+        verified_ix = (None if args.no_verify or not rule_map else
+                       all(bool(q[2]) for q in parts))
+        digest = parts[0][3]
+        n_per_dataset = parts[0][0]
+    else:
+        n_itemsets, digest = merged_digest(r, world)
+        n_per_dataset = n_itemsets
+        verified = verified_ix = None
+        if rank == 0:
+            verified, verified_ix = cpu_check(tx, r, digest, n_itemsets)
+
+    # strong-scaling companion at N > 1: ONE dataset (rank 0's) split over the ranks by the
+    # replicated root-class partition, timed the same way
+    strong = None
+    if weak and not args.cpu:
+        dm_s = make_miner("replicate", base_tx,
+                          name_tie_rank(base_tx.names) if base_tx.names else
+                          np.arange(base_tx.n_items, dtype=np.int32))
+        rs, ms_s = timed_loop(dm_step(dm_s), dm_s.synchronize, args.warmup, args.steps)
+        ms_s = max_over_ranks(ms_s)
+        n_s, dig_s = merged_digest(rs, world)
+        ok_s = None
+        if rank == 0 and not args.no_verify:
+            ok_s = cpu_check(base_tx, {}, dig_s, n_s)[0]
+        strong = {"parallelism": f"dp{world}-replicated-data+root-class-partition",
+                  "global_batch": int(base_tx.n_tx), "ms_per_step": round(ms_s, 4),
+                  "value": round(n_s / (ms_s / 1000.0), 1), "n_itemsets": n_s,
+                  "verified_digest": ok_s}
+        del dm_s
+
     value = n_itemsets / (ms_step / 1000.0)
-    ref_rate = n_itemsets / REF_SECONDS_DS2_005
+    ref_rate = n_per_dataset / REF_SECONDS_DS2_005  # one reference pod mining one dataset
     headline_cfg = args.shape in ("ds1", "ds2") and abs(args.min_support - 0.05) < 1e-12 and \
         not args.max_len
+    n_data = world if weak else 1
     out = {
         "metric": "itemsets/sec mined (FP-Growth, all frequent itemsets + supports, rule map built)",
         "value": round(value, 1),
@@ -368,18 +448,21 @@ def main() -> int:
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if (weak or world == 1) else "strong",
         "vs_baseline": round(value / ref_rate, 2) if headline_cfg else None,
-        "vs_reference_replay": round(REPLAY_SECONDS_DS1_005 * 1e3 / ms_step, 1)
+        "vs_reference_replay": round(n_data * REPLAY_SECONDS_DS1_005 * 1e3 / ms_step, 1)
         if headline_cfg and args.shape == "ds1" and args.seed == 0 else None,
         "dtype": dtype,
         "data": "synthetic (ds1 shape calibrated to relatorio.pdf p.5-6 + the 0.03 sweep; "
-                "random-init item vocab; bench/calibrate.py)",
+                "random-init item vocab; bench/calibrate.py)" +
+                ("; weak scaling: one dataset per GPU, rank r>0 mines a relabelled copy "
+                 "(permuted item ids and transaction order; same itemset count)" if weak else ""),
         "config": {
             "model": f"fpgrowth-{args.shape}-shape",
-            "global_batch": int(tx.n_tx),
+            "global_batch": int(tx.n_tx) * n_data,
             "seq_len": int(tx.n_items),
-            "parallelism": ({"replicate": f"dp{world}-replicated-data+root-class-partition",
+            "parallelism": (f"dp{world}-one-dataset-per-gpu" if weak else
+                            {"replicate": f"dp{world}-replicated-data+root-class-partition",
                              "tx": f"tx-dp{world}+per-level-count-allreduce",
                              "item": f"tx-dp{world}+item-shard{world}"}.get(
                                  getattr(dm, "mode", "item")) if world > 1 and dm is not None
@@ -387,6 +470,7 @@ def main() -> int:
             "min_support": args.min_support,
             "max_len": args.max_len,
             "n_itemsets": n_itemsets,
+            "n_itemsets_per_dataset": n_per_dataset,
             "n_frequent_items": int(st.get("n_frequent_items", 0)),
             "max_depth": int(st.get("max_depth", 0)),
             "rule_map_in_step": rule_map,
@@ -403,6 +487,8 @@ def main() -> int:
         "reference_seconds_ds2_0.05": REF_SECONDS_DS2_005,
         "reference_replay_seconds_same_data": REPLAY_SECONDS_DS1_005,
     }
+    if strong is not None:
+        out["strong"] = strong
     if "phases_ms" in st:
         out["phases_ms"] = st["phases_ms"]
     if not args.cpu and not args.no_config3:

@@ -126,6 +126,33 @@ class Transactions:
         return X
 
 
+def relabel(tx: Transactions, key: int) -> Transactions:
+    """A distinct copy of ``tx`` of identical mining difficulty: item ids permuted and
+    transactions shuffled by a ``key``-seeded permutation (``key == 0`` returns ``tx``).  The
+    frequent itemsets are the images of the original ones under the item permutation, so the
+    itemset count and depth are unchanged while every bitmap word differs — the per-GPU dataset
+    of the weak-scaled bench (one dataset per rank, none shared)."""
+    if key == 0:
+        return tx
+    rng = np.random.default_rng(0x5EED0000 + int(key))
+    perm = rng.permutation(tx.n_items).astype(np.int32)      # old id -> new id
+    order = rng.permutation(tx.n_tx)                          # new row -> old row
+    lens = np.diff(tx.tx_ptr)[order]
+    ptr = np.zeros(tx.n_tx + 1, np.int64)
+    np.cumsum(lens, out=ptr[1:])
+    row = np.repeat(np.arange(tx.n_tx, dtype=np.int64), lens)
+    src = np.concatenate([np.arange(tx.tx_ptr[o], tx.tx_ptr[o + 1]) for o in order]) \
+        if tx.n_tx else np.zeros(0, np.int64)
+    new = perm[tx.items[src]]
+    srt = np.lexsort((new, row))                               # rows ascending again
+    names = None
+    if tx.names is not None:
+        names = [""] * tx.n_items
+        for old, nid in enumerate(perm.tolist()):
+            names[nid] = tx.names[old]
+    return Transactions(ptr, np.ascontiguousarray(new[srt], np.int32), tx.n_items, names)
+
+
 def generate(shape: "Shape | str", seed: int = 0, n_tx: Optional[int] = None,
              n_items: Optional[int] = None, calib_iters: int = 4) -> Transactions:
     """Generate clustered playlists of a named shape as CSR.

@@ -189,19 +189,41 @@ def resume_from_checkpoint(ck: PhaseCheckpoint, tx: pp.PlaylistTransactions, min
 
 
 def run_support_sweep(cfg: JobSettings, tx: pp.PlaylistTransactions, total_songs: int,
-                      supports: Optional[List[float]] = None, out_csv: str = EXPERIMENT_CSV):
-    """J14: the min_support sweep (main.py:450-473), written to ``fp_growth_experiment_results.csv``."""
+                      supports: Optional[List[float]] = None, out_csv: str = EXPERIMENT_CSV,
+                      group=None):
+    """J14: the min_support sweep (main.py:450-473), written to ``fp_growth_experiment_results.csv``.
+
+    Multi-GPU (``group`` = the job's gloo side group): the sweep points are dealt over the ranks
+    in snake order (low supports cost the most) and every rank mines its points on its own GPU
+    with no collective (dataset-parallel, like ``DistMiner(mode="local")``); one gather over the
+    side group brings the rows to rank 0, which writes them in grid order."""
     import pandas as pd
     supports = supports if supports is not None else np.arange(0.03, 0.2, 0.0025).tolist()
+    world, rank = 1, 0
+    if group is not None:
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+    mine_idx = [i for i in range(len(supports))
+                if ((i // world) % 2 == 0 and i % world == rank) or
+                   ((i // world) % 2 == 1 and world - 1 - i % world == rank)]
     rows = []
-    for ms in supports:
-        ms = round(ms, 3)
-        print(f"Calculating for min_support: {ms}")
-        _, trie, _, (missing, dur) = mine_rules(cfg, tx, ms, total_songs)
-        rows.append({"min_support": ms, "songs_without_recommendations": missing,
-                     "duration": dur, "n_itemsets": len(trie)})
-        pd.DataFrame(rows).to_csv(out_csv, index=False)
-    return rows
+    for i in mine_idx:
+        ms = round(supports[i], 3)
+        if rank == 0:
+            print(f"Calculating for min_support: {ms}")
+        _, trie, _, (missing, dur) = mine_rules(cfg, tx, ms, total_songs, verbose=rank == 0)
+        rows.append((i, {"min_support": ms, "songs_without_recommendations": missing,
+                         "duration": dur, "n_itemsets": len(trie)}))
+        if world == 1:
+            pd.DataFrame([r for _, r in rows]).to_csv(out_csv, index=False)
+    if world > 1:
+        import torch.distributed as dist
+        parts = [None] * world
+        dist.all_gather_object(parts, rows, group=group)
+        rows = sorted((r for part in parts for r in part), key=lambda x: x[0])
+        if rank == 0:
+            pd.DataFrame([r for _, r in rows]).to_csv(out_csv, index=False)
+    return [r for _, r in rows]
 
 
 def save_itemsets(cfg: JobSettings, trie: ItemsetTrie) -> None:
@@ -261,12 +283,10 @@ def run(cfg: Optional[JobSettings] = None) -> Dict:
         pp.validate_and_map_artists_names_to_ids(t)  # every rank fails the same way
     _fault("after_best_tracks")
     tx = pp.group_tracks_by_playlist(t)
-    if cfg.experiment_supports:
-        if rank == 0:
-            run_support_sweep(cfg, tx, total_songs)
-        if side is not None:  # the other ranks wait here (gloo, long timeout), not in RCCL
-            import torch.distributed as dist
-            dist.barrier(group=side)
+    if cfg.experiment_supports:  # every rank mines its share; the gather runs on gloo
+        if distributed and cfg.miner != "cpu":
+            os.environ.setdefault("KMLS_DEVICE", os.environ.get("LOCAL_RANK", "0"))
+        run_support_sweep(cfg, tx, total_songs, group=side)
     ck = PhaseCheckpoint.for_dataset(cfg.checkpoint_dir, selected, min_support=cfg.min_support,
                                      rules_mode=cfg.rules_mode, sample_ratio=cfg.sample_ratio)
     resumed = ck.has("trie") if rank == 0 else False

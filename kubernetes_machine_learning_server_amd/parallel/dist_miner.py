@@ -38,6 +38,12 @@ level loop all-reduces every level's candidate counts through a native RCCL comm
 per-item supports are counted in tiles whose all-reduces run on a side stream while the next
 tile's histogram runs (the overlap the north star asks for).  Every rank ends with the same
 global trie; rank 0 downloads it.
+
+**Dataset-parallel mode** (``mode="local"``): each rank mines its own whole dataset with the
+native single-GPU path and no collective — the job's min_support sweep split over the GPUs
+(``job.main.run_support_sweep``) and the weak-scaled bench (one dataset per GPU).  A ds-sized problem is a
+0.3 ms chain of dependent level launches, so N independent datasets is the form of it that
+scales with GPUs; ``replicate`` stays the strong-scaled form of one dataset.
 """
 from __future__ import annotations
 
@@ -133,7 +139,7 @@ class _GpuOps:
             self.comm = N.Comm(dm.rank, dm.world, uid[0], dm.device, backend)
             self.stream = None
             self.g = N.GpuMiner(dm.device, arena_bytes, 0)
-        elif dm.world > 1 or dm.force_protocol or dm.mode == "item":
+        elif (dm.world > 1 and dm.mode != "local") or dm.force_protocol or dm.mode == "item":
             # every torch op of the protocol (allocations, fills, collectives) and every native
             # kernel run on ONE stream, so they are ordered without extra synchronisation
             torch.cuda.set_device(dm.device)
@@ -266,7 +272,8 @@ class DistMiner:
         """``global_n_tx`` given ⇒ (tx_ptr, items) already hold only this rank's shard (tx mode;
         large datasets are generated/loaded per shard).  ``mode``: "item" (replicated bitmaps,
         item-sharded DFS), "replicate" (full data on every rank, device-side class partition),
-        "tx" (transaction-DP, see module doc) or "auto"."""
+        "tx" (transaction-DP, see module doc), "local" (every rank mines its OWN whole dataset
+        with no collective: the dataset-parallel job / the weak-scaled bench) or "auto"."""
         self.world = dist.get_world_size() if (dist is not None and dist.is_initialized()) else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
         self.n_tx = int(global_n_tx) if global_n_tx is not None else len(tx_ptr) - 1
@@ -279,6 +286,8 @@ class DistMiner:
                 mode = "replicate"
             else:
                 mode = "item"
+        if mode not in ("tx", "item", "replicate", "local"):
+            raise ValueError(f"unknown mode {mode!r}")
         if global_n_tx is not None and mode not in ("tx", "item"):
             raise ValueError("pre-sharded input (global_n_tx) requires mode 'tx' or 'item'")
         self.mode = mode
@@ -291,7 +300,7 @@ class DistMiner:
         self.force_protocol = force_protocol
         lo, hi, ts = shard_bounds(self.n_tx, self.world, self.rank)
         self.lo, self.hi, self.ts = lo, hi, ts
-        if mode == "replicate":  # every rank mines from the full (small) dataset
+        if mode in ("replicate", "local"):  # every rank mines from its full (small) dataset
             sptr = np.ascontiguousarray(tx_ptr, dtype=np.int64)
             sitems = np.ascontiguousarray(items, dtype=np.int32)
         elif global_n_tx is not None:  # already this rank's shard
@@ -338,7 +347,16 @@ class DistMiner:
             self._last_global = st["global_itemsets"]
             self.last = r
             return {"stats": st, "trie": r}
-        if self.world == 1 and self.backend == "gpu" and not self.force_protocol:
+        if self.mode == "local" and self.backend != "gpu":  # own dataset, native CPU miner
+            r = self.ops.N.mine_cpu(self.ops.tx_ptr, self.ops.items, self.n_items,
+                                    self.min_support, self.max_len)
+            st = dict(r["stats"])
+            st["global_itemsets"] = int(st["n_itemsets"])
+            self._last_global = st["global_itemsets"]
+            self.last = r
+            return {"stats": st, "trie": r}
+        if (self.world == 1 or self.mode == "local") and self.backend == "gpu" \
+                and not self.force_protocol:
             r = self.g.mine(self.min_support, self.max_len, False, download, True, self.mfma,
                             prefetch, rule_index)
             st = dict(r["stats"])

@@ -225,3 +225,43 @@ def test_txdp_level_loop_multi_process(world, shape, ms, max_len):
     assert all(r[2] == rd["n"] for r in res)
     spans = sorted(r[3] for r in res)
     assert spans[0][0] == 0 and spans[-1][1] == tx.n_tx  # the shards cover every transaction
+
+
+def test_relabel_keeps_itemsets():
+    """The weak-scaled bench's per-rank dataset: permuted ids + shuffled rows, same itemsets."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate, relabel
+    from kubernetes_machine_learning_server_amd.ops import native
+    N = native.load()
+    tx = generate("ds2_weak", seed=1)
+    r0 = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.03, 0)
+    for key in (1, 5):
+        t2 = relabel(tx, key)
+        assert not np.array_equal(t2.items, tx.items)
+        assert sorted(t2.names) == sorted(tx.names)
+        r = N.mine_cpu(t2.tx_ptr, t2.items, t2.n_items, 0.03, 0)
+        assert r["stats"]["n_itemsets"] == r0["stats"]["n_itemsets"]
+        assert np.array_equal(np.bincount(r["depth"]), np.bincount(r0["depth"]))
+
+
+def test_bench_weak_scaling_two_ranks_cpu():
+    """bench.py's N-rank contract on the CPU tier: torchrun, one JSON line from rank 0, the job
+    total over one dataset per rank, every rank's result verified by digest."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=root)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--cpu", "--steps", "2",
+           "--warmup", "1", "--serve-qps", ""]
+    p = subprocess.run(cmd, env=env, cwd="/tmp", capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["scaling"] == "weak" and out["verified_digest"] is True
+    cfg = out["config"]
+    assert cfg["n_itemsets"] == 2 * cfg["n_itemsets_per_dataset"] == 2 * 77905
+    assert cfg["global_batch"] == 2 * 2246 and cfg["parallelism"] == "dp2-one-dataset-per-gpu"
+    assert abs(out["value"] - cfg["n_itemsets"] / (out["ms_per_step"] / 1e3)) / out["value"] < 1e-3

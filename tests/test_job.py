@@ -228,6 +228,7 @@ def _dist_job_worker(rank, world, port, root, fault, out_q, extra=None):
     else:
         _os.environ.pop("KMLS_FAULT", None)
     import pathlib as _pl
+    _os.chdir(root)  # the J14 sweep writes its CSV to the working directory (as the reference)
     from kubernetes_machine_learning_server_amd.job import main as _job
     from tests.helpers import job_settings as _js
     cfg = _js(_pl.Path(root), num_gpus=world, checkpoint_dir=_pl.Path(root) / "ck",
@@ -295,3 +296,27 @@ def test_distributed_pairs_job_strategies(tmp_path, strategy):
     assert summary["n_itemsets"] == ref["n_itemsets"] and summary["n_keys"] == ref["n_keys"]
     assert rec_dict(tmp_path) == rec_dict(single)
 
+
+
+def test_distributed_support_sweep(tmp_path):
+    """EXPERIMENT_SUPPORTS at world size 2: the sweep points are split over the ranks, each
+    mined locally; rank 0 writes every point in grid order, equal to a single-process sweep."""
+    import pandas as pd
+    make_datasets(tmp_path, shapes=("ds2_weak", "tiny"), seeds=(3, 4))
+    res = _run_dist_job(tmp_path, 2, extra={"experiment_supports": True})
+    assert all(r[2] is None for r in res), res
+    df = pd.read_csv(tmp_path / job.EXPERIMENT_CSV)
+    grid = [round(x, 3) for x in np.arange(0.03, 0.2, 0.0025).tolist()]
+    assert df["min_support"].tolist() == grid
+    single = tmp_path / "single"
+    make_datasets(single, shapes=("ds2_weak", "tiny"), seeds=(3, 4))
+    cfg = job_settings(single)
+    t = pp.clean_df(pp.read_tracks(str(single / "datasets" / "2023_spotify_ds1.csv"), verbose=False))
+    tx = pp.group_tracks_by_playlist(t)
+    rows = job.run_support_sweep(cfg, tx, t.n_unique("track_uri"), grid[::7],
+                                 str(tmp_path / "one.csv"))
+    got = df.set_index("min_support")
+    for r in rows:
+        assert got.loc[r["min_support"], "songs_without_recommendations"] == \
+            r["songs_without_recommendations"]
+        assert got.loc[r["min_support"], "n_itemsets"] == r["n_itemsets"]
