@@ -295,6 +295,81 @@ __global__ __launch_bounds__(1024) void k_part_count(const uint16_t* __restrict_
   }
 }
 
+// Pass 3, balanced: every block takes an equal slice of the whole partition-major id array, so
+// a partition holding a Zipf head item (its partition is ~1.6x the mean length) gets
+// proportionally more blocks; a slice that straddles a boundary histograms each partition in
+// turn.  kDedup: each thread sorts its 8 ids (a 19-comparator network) and adds a run length
+// per distinct id, so the head item's repeats inside one thread cost one LDS atomic, not up to
+// eight same-address ones serialised across the wave.
+__device__ __forceinline__ void cswap(uint32_t& a, uint32_t& b) {
+  const uint32_t lo = min(a, b), hi = max(a, b);
+  a = lo;
+  b = hi;
+}
+
+template <bool kDedup>
+__global__ __launch_bounds__(1024) void k_part_count_bal(const uint16_t* __restrict__ part,
+                                                         const int64_t* __restrict__ off, int G,
+                                                         int P, int64_t n_items,
+                                                         uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[kPartBins];
+  __shared__ int64_t bnd[kPartMax + 1];
+  if ((int)threadIdx.x <= P) bnd[threadIdx.x] = off[(int64_t)threadIdx.x * G];
+  __syncthreads();
+  const int64_t total = bnd[P];
+  const int64_t sl = (total + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = min(total, (int64_t)blockIdx.x * sl), hi = min(total, lo + sl);
+  int p = 0;
+  while (p < P - 1 && bnd[p + 1] <= lo) ++p;
+  for (; p < P && bnd[p] < hi; ++p) {
+    const int64_t a = max(lo, bnd[p]), b = min(hi, bnd[p + 1]);
+    if (a >= b) continue;
+    for (int i = threadIdx.x; i < kPartBins; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const int64_t head = ((8 - (int64_t)(((uintptr_t)(part + a) >> 1) & 7)) & 7);
+    const int64_t a0 = min(b, a + head);
+    for (int64_t i = a + threadIdx.x; i < a0; i += blockDim.x) atomicAdd(&h[part[i]], 1u);
+    const uint4* __restrict__ v = reinterpret_cast<const uint4*>(part + a0);
+    const int64_t n8 = (b - a0) >> 3;
+    for (int64_t j = threadIdx.x; j < n8; j += blockDim.x) {
+      const uint4 x = v[j];
+      uint32_t e[8] = {x.x & 0xFFFFu, x.x >> 16, x.y & 0xFFFFu, x.y >> 16,
+                       x.z & 0xFFFFu, x.z >> 16, x.w & 0xFFFFu, x.w >> 16};
+      if (kDedup) {
+        cswap(e[0], e[1]); cswap(e[2], e[3]); cswap(e[4], e[5]); cswap(e[6], e[7]);
+        cswap(e[0], e[2]); cswap(e[1], e[3]); cswap(e[4], e[6]); cswap(e[5], e[7]);
+        cswap(e[1], e[2]); cswap(e[5], e[6]); cswap(e[0], e[4]); cswap(e[3], e[7]);
+        cswap(e[1], e[5]); cswap(e[2], e[6]);
+        cswap(e[1], e[4]); cswap(e[3], e[6]);
+        cswap(e[2], e[4]); cswap(e[3], e[5]);
+        cswap(e[3], e[4]);
+        uint32_t run = 1;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          if (e[k] == e[k + 1]) {
+            ++run;
+          } else {
+            atomicAdd(&h[e[k]], run);
+            run = 1;
+          }
+        }
+        atomicAdd(&h[e[7]], run);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) atomicAdd(&h[e[k]], 1u);
+      }
+    }
+    for (int64_t i = a0 + (n8 << 3) + threadIdx.x; i < b; i += blockDim.x) atomicAdd(&h[part[i]], 1u);
+    __syncthreads();
+    const int64_t id0 = (int64_t)p << kPartBits;
+    for (int i = threadIdx.x; i < kPartBins; i += blockDim.x) {
+      const uint32_t val = h[i];
+      if (val && id0 + i < n_items) atomicAdd(&counts[id0 + i], val);
+    }
+    __syncthreads();
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // O4 bitmap encode: bit t of row rank_of[item] for every (t, item) of the CSR shard.
 // One wave64 per transaction (lanes stride its items), so a 2k-transaction shard already
@@ -342,8 +417,10 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
                                                         const uint32_t* __restrict__ fmask,
                                                         bool xcd_order,
                                                         const unsigned long long* __restrict__ fgroup,
-                                                        const int32_t* __restrict__ c2r) {
-  // [band rows][TW], then tx_ptr[64*TW + 1], then (fgroup path) c2r[F]
+                                                        const int32_t* __restrict__ c2r,
+                                                        int txmap_cap) {
+  // [band rows][TW], then tx_ptr[64*TW + 1], then (fgroup path) c2r[F], then (txmap_cap > 0)
+  // the tile's item-position -> local-transaction map, one byte per item
   extern __shared__ unsigned long long s_bm[];
   const int TW = 1 << tw_log2;
   const int64_t tile_tx = 64ll << tw_log2;
@@ -368,8 +445,21 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
   int32_t* s_c2r = (int32_t*)(s_ptr + 64 * TW + 1);
   if (fgroup)
     for (int i = threadIdx.x; i < (int)F; i += blockDim.x) s_c2r[i] = c2r[i];
+  uint8_t* s_tx = (uint8_t*)(s_c2r + (fgroup ? F : 0));
   __syncthreads();
   const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
+  // item -> transaction without a per-item binary search (8 dependent LDS reads for 256
+  // transactions): each wave stamps its transactions' local index over their item ranges
+  // (TW <= 4, so a local index fits one byte); tiles with more items than the map fall back
+  const bool use_map = txmap_cap > 0 && (p1 - p0) <= txmap_cap && nt <= 256;
+  if (use_map) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int lt = wv; lt < nt; lt += (int)(blockDim.x >> 6)) {
+      const int a = (int)(s_ptr[lt] - p0), b = (int)(s_ptr[lt + 1] - p0);
+      for (int q = a + lane; q < b; q += 64) s_tx[q] = (uint8_t)lt;
+    }
+    __syncthreads();
+  }
   const int64_t step = (int64_t)blockDim.x * kEncodeU;
   // the next round's item loads are issued before this round's gathers and LDS work, so their
   // HBM latency overlaps the dependent chain of the current round
@@ -412,9 +502,13 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
       if (rk[u] < 0 || rk[u] >= nr) continue;
       const int64_t p = pb + (int64_t)u * blockDim.x + threadIdx.x;
       int lo = 0, hi = nt;  // largest lt with s_ptr[lt] <= p
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (s_ptr[mid] <= p) lo = mid; else hi = mid;
+      if (use_map) {
+        lo = s_tx[p - p0];
+      } else {
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (s_ptr[mid] <= p) lo = mid; else hi = mid;
+        }
       }
       atomicOr(&s_bm[(int64_t)rk[u] * TW + (lo >> 6)], 1ull << (lo & 63));
     }
@@ -720,12 +814,17 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
   const int64_t TW = 1ll << tw_log2;
   const int64_t band = std::min<int64_t>(F, kSlab / (8 * TW));
   const int64_t n_bands = (F + band - 1) / band;
-  const size_t lds = (size_t)band * TW * 8 + (size_t)(64 * TW + 1) * 8 + (fgroup ? (size_t)F * 4 : 0);
+  // item -> transaction byte map (KMLS_ENCODE_TXMAP=0: per-item binary search, A/B): sized for
+  // a tile of 64*TW transactions of up to 32 items each on average
+  const char* me = std::getenv("KMLS_ENCODE_TXMAP");
+  const int txmap_cap = (tw_log2 <= 2 && !(me && me[0] == '0')) ? (int)(64 * TW * 32) : 0;
+  const size_t lds = (size_t)band * TW * 8 + (size_t)(64 * TW + 1) * 8 +
+                     (fgroup ? (size_t)F * 4 : 0) + (size_t)txmap_cap;
   const int64_t blocks = (n_tx + 64 * TW - 1) / (64 * TW) * n_bands;
   if (blocks > INT32_MAX) return false;
   hipLaunchKernelGGL(k_encode_tile, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr, items,
                      n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2, (int)band,
-                     fmask, xcd, fgroup, c2r);
+                     fmask, xcd, fgroup, c2r, txmap_cap);
   KMLS_HIP(hipGetLastError());
   return true;
 }
@@ -774,9 +873,24 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
   exclusive_scan_i64(blk, off, n, q, tb, s);
   hipLaunchKernelGGL(k_part_scatter, dim3(kPartGrid), dim3(kBlock), 0, s, items, nnz, (int)P, off,
                      part);
-  const int M = (int)std::max<int64_t>(1, (512 + P - 1) / P);
-  hipLaunchKernelGGL(k_part_count, dim3((unsigned)(P * M)), dim3(1024), 0, s, part, off,
-                     kPartGrid, M, (int64_t)n_items, counts);
+  // pass 3: KMLS_SUPPORT_COUNT = bal (default: equal global slices, per-thread dedup of 8 ids),
+  // balnd (equal slices, no dedup) or part (M blocks per partition) — A/B switches
+  const char* ce = std::getenv("KMLS_SUPPORT_COUNT");
+  const std::string cm = ce ? ce : "bal";
+  if (cm == "part") {
+    const int M = (int)std::max<int64_t>(1, (512 + P - 1) / P);
+    hipLaunchKernelGGL(k_part_count, dim3((unsigned)(P * M)), dim3(1024), 0, s, part, off,
+                       kPartGrid, M, (int64_t)n_items, counts);
+  } else {
+    // one 128 KB-LDS block per CU: 512 equal slices = 2 rounds over the 256 CUs
+    const unsigned B = (unsigned)std::min<int64_t>(512, std::max<int64_t>(1, nnz / 65536));
+    if (cm == "balnd")
+      hipLaunchKernelGGL(k_part_count_bal<false>, dim3(B), dim3(1024), 0, s, part, off, kPartGrid,
+                         (int)P, (int64_t)n_items, counts);
+    else
+      hipLaunchKernelGGL(k_part_count_bal<true>, dim3(B), dim3(1024), 0, s, part, off, kPartGrid,
+                         (int)P, (int64_t)n_items, counts);
+  }
   KMLS_HIP(hipGetLastError());
   return true;
 }
