@@ -212,16 +212,30 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(const int32_t* __restri
   int64_t b0, b1;
   part_chunk(nnz, &b0, &b1);
   if ((int)threadIdx.x < P) base[threadIdx.x] = off[(int64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  // the next tile's ids are loaded while this tile is sorted and written (register double
+  // buffer), so each block keeps a tile of loads in flight through its LDS phases
+  int32_t xn[kPer];
+  {
+    const int n_t = (int)min((int64_t)kPartTile, b1 - b0);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int li = j * kBlock + (int)threadIdx.x;
+      xn[j] = li < n_t ? items[b0 + li] : -1;
+    }
+  }
   for (int64_t t0 = b0; t0 < b1; t0 += kPartTile) {
     const int n_t = (int)min((int64_t)kPartTile, b1 - t0);
     if (threadIdx.x < kPartMax) cnt[threadIdx.x] = 0;
     __syncthreads();
     int32_t x[kPer];
     uint32_t loc[kPer];
+    const int64_t t1 = t0 + kPartTile;
+    const int n_n = (int)max((int64_t)0, min((int64_t)kPartTile, b1 - t1));
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int li = j * kBlock + (int)threadIdx.x;
-      x[j] = li < n_t ? items[t0 + li] : -1;
+      x[j] = xn[j];
+      xn[j] = li < n_n ? items[t1 + li] : -1;
     }
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
@@ -298,16 +312,8 @@ __global__ __launch_bounds__(1024) void k_part_count(const uint16_t* __restrict_
 // Pass 3, balanced: every block takes an equal slice of the whole partition-major id array, so
 // a partition holding a Zipf head item (its partition is ~1.6x the mean length) gets
 // proportionally more blocks; a slice that straddles a boundary histograms each partition in
-// turn.  kDedup: each thread sorts its 8 ids (a 19-comparator network) and adds a run length
-// per distinct id, so the head item's repeats inside one thread cost one LDS atomic, not up to
-// eight same-address ones serialised across the wave.
-__device__ __forceinline__ void cswap(uint32_t& a, uint32_t& b) {
-  const uint32_t lo = min(a, b), hi = max(a, b);
-  a = lo;
-  b = hi;
-}
-
-template <bool kDedup>
+// turn.  (A per-thread sort + run-length dedup of the 8 ids, against same-address LDS atomics
+// on head items, measured no faster at 100M x 1M: 8.97 vs 8.70 ms support; removed.)
 __global__ __launch_bounds__(1024) void k_part_count_bal(const uint16_t* __restrict__ part,
                                                          const int64_t* __restrict__ off, int G,
                                                          int P, int64_t n_items,
@@ -333,31 +339,14 @@ __global__ __launch_bounds__(1024) void k_part_count_bal(const uint16_t* __restr
     const int64_t n8 = (b - a0) >> 3;
     for (int64_t j = threadIdx.x; j < n8; j += blockDim.x) {
       const uint4 x = v[j];
-      uint32_t e[8] = {x.x & 0xFFFFu, x.x >> 16, x.y & 0xFFFFu, x.y >> 16,
-                       x.z & 0xFFFFu, x.z >> 16, x.w & 0xFFFFu, x.w >> 16};
-      if (kDedup) {
-        cswap(e[0], e[1]); cswap(e[2], e[3]); cswap(e[4], e[5]); cswap(e[6], e[7]);
-        cswap(e[0], e[2]); cswap(e[1], e[3]); cswap(e[4], e[6]); cswap(e[5], e[7]);
-        cswap(e[1], e[2]); cswap(e[5], e[6]); cswap(e[0], e[4]); cswap(e[3], e[7]);
-        cswap(e[1], e[5]); cswap(e[2], e[6]);
-        cswap(e[1], e[4]); cswap(e[3], e[6]);
-        cswap(e[2], e[4]); cswap(e[3], e[5]);
-        cswap(e[3], e[4]);
-        uint32_t run = 1;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-          if (e[k] == e[k + 1]) {
-            ++run;
-          } else {
-            atomicAdd(&h[e[k]], run);
-            run = 1;
-          }
-        }
-        atomicAdd(&h[e[7]], run);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) atomicAdd(&h[e[k]], 1u);
-      }
+      atomicAdd(&h[x.x & 0xFFFFu], 1u);
+      atomicAdd(&h[x.x >> 16], 1u);
+      atomicAdd(&h[x.y & 0xFFFFu], 1u);
+      atomicAdd(&h[x.y >> 16], 1u);
+      atomicAdd(&h[x.z & 0xFFFFu], 1u);
+      atomicAdd(&h[x.z >> 16], 1u);
+      atomicAdd(&h[x.w & 0xFFFFu], 1u);
+      atomicAdd(&h[x.w >> 16], 1u);
     }
     for (int64_t i = a0 + (n8 << 3) + threadIdx.x; i < b; i += blockDim.x) atomicAdd(&h[part[i]], 1u);
     __syncthreads();
@@ -873,23 +862,18 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
   exclusive_scan_i64(blk, off, n, q, tb, s);
   hipLaunchKernelGGL(k_part_scatter, dim3(kPartGrid), dim3(kBlock), 0, s, items, nnz, (int)P, off,
                      part);
-  // pass 3: KMLS_SUPPORT_COUNT = bal (default: equal global slices, per-thread dedup of 8 ids),
-  // balnd (equal slices, no dedup) or part (M blocks per partition) — A/B switches
+  // pass 3: equal global slices (default) or KMLS_SUPPORT_COUNT=part, M blocks per partition
+  // (A/B; 8.79 vs 8.70 ms support at 100M x 1M)
   const char* ce = std::getenv("KMLS_SUPPORT_COUNT");
-  const std::string cm = ce ? ce : "bal";
-  if (cm == "part") {
+  if (ce && std::string(ce) == "part") {
     const int M = (int)std::max<int64_t>(1, (512 + P - 1) / P);
     hipLaunchKernelGGL(k_part_count, dim3((unsigned)(P * M)), dim3(1024), 0, s, part, off,
                        kPartGrid, M, (int64_t)n_items, counts);
   } else {
     // one 128 KB-LDS block per CU: 512 equal slices = 2 rounds over the 256 CUs
     const unsigned B = (unsigned)std::min<int64_t>(512, std::max<int64_t>(1, nnz / 65536));
-    if (cm == "balnd")
-      hipLaunchKernelGGL(k_part_count_bal<false>, dim3(B), dim3(1024), 0, s, part, off, kPartGrid,
-                         (int)P, (int64_t)n_items, counts);
-    else
-      hipLaunchKernelGGL(k_part_count_bal<true>, dim3(B), dim3(1024), 0, s, part, off, kPartGrid,
-                         (int)P, (int64_t)n_items, counts);
+    hipLaunchKernelGGL(k_part_count_bal, dim3(B), dim3(1024), 0, s, part, off, kPartGrid, (int)P,
+                       (int64_t)n_items, counts);
   }
   KMLS_HIP(hipGetLastError());
   return true;

@@ -362,6 +362,24 @@ def test_support_histograms_large_vocab(gpu_mod, T, I):
                                   np.bincount(items, minlength=I))
 
 
+@pytest.mark.parametrize("mode", ["bal", "part"])
+def test_support_partitioned_count_modes(gpu_mod, monkeypatch, mode):
+    """Pass 3 of the partitioned histogram in each A/B form (equal global slices,
+    M blocks per partition) on a Zipf-headed 1M vocabulary whose hot
+    items repeat inside a thread's 8 ids, against np.bincount."""
+    import torch
+    monkeypatch.setenv("KMLS_SUPPORT_COUNT", mode)
+    ptr, items = gpu_mod.synth_transactions(400_000, 1_000_003, 30.0, 50, 0.95, 1.1, 11)
+    g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
+    g.load_csr(ptr, items, 1_000_003)
+    cnt = torch.zeros(1_000_003, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    g.item_support(cnt.data_ptr())
+    g.synchronize()
+    np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32),
+                                  np.bincount(items, minlength=1_000_003))
+
+
 def test_graph_replay_matches_eager(gpu_mod):
     """Steady-state resident calls replay a captured hipGraph (third call on: the launch plan
     repeats); results must match the CPU miner on every call, including when the configuration
