@@ -216,11 +216,13 @@ def run_serve(shape: str, qps_list, duration: float, backend: str) -> dict:
     queries = bs.make_queries(base, 20000)
     port = bs._free_port()
     proc = bs.start_server(base, backend, 4, port)
-    res = {"backend": backend, "workers": 4, "duration_s": duration, "points": []}
+    # 8 open-loop client processes: at 10k QPS, 4 asyncio clients (2.5k each) measured their own
+    # event-loop lag as latency on a loaded box (profiles/r2_s7_serve_clients.md)
+    res = {"backend": backend, "workers": 4, "clients": 8, "duration_s": duration, "points": []}
     try:
         bs.measure(port, 200, 1.0, 1, queries)
         for q in qps_list:
-            r = bs.measure(port, q, duration, 4, queries)
+            r = bs.measure(port, q, duration, 8, queries)
             res["points"].append({k: r[k] for k in ("offered_qps", "achieved_qps", "p50_ms",
                                                     "p99_ms", "errors", "client_send_lag_p99_ms")})
     finally:

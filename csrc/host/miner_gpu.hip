@@ -756,6 +756,8 @@ GpuMiner::~GpuMiner() {
   if (d_fmask_) (void)hipFree(d_fmask_);
   if (d_fgroup_) (void)hipFree(d_fgroup_);
   if (d_c2r_) (void)hipFree(d_c2r_);
+  if (d_lk_mask_) (void)hipFree(d_lk_mask_);
+  if (d_lk_hash_) (void)hipFree(d_lk_hash_);
   if (d_ids_) (void)hipFree(d_ids_);
   if (d_own_bm_) (void)hipFree(d_own_bm_);
   if (h_scalar_) (void)hipHostFree(h_scalar_);
@@ -948,8 +950,15 @@ void GpuMiner::build_encode_tables(int64_t F) {
   if (d_c2r_) KMLS_HIP(hipFree(d_c2r_));
   d_fgroup_ = nullptr;
   d_c2r_ = nullptr;
+  lk_valid_ = false;
   if (!d_fmask_ || F <= 0 || F > kern::kEncodeGroupMaxF) return;
   hipStream_t s = (hipStream_t)stream_;
+  if (F <= kern::kEncodeLookupMaxF && n_items_ <= (1 << 21)) {
+    if (!d_lk_mask_) KMLS_HIP(hipMalloc((void**)&d_lk_mask_, kern::kEncodeLookupMaskBits / 8));
+    if (!d_lk_hash_) KMLS_HIP(hipMalloc((void**)&d_lk_hash_, kern::kEncodeLookupSlots * 4));
+    kern::encode_lookup_build(d_ids_, F, n_items_, d_lk_mask_, d_lk_hash_, s);
+    lk_valid_ = true;
+  }
   const int64_t G = (n_items_ + 31) / 32;
   KMLS_HIP(hipMalloc((void**)&d_fgroup_, (size_t)G * 8));
   KMLS_HIP(hipMalloc((void**)&d_c2r_, (size_t)F * 4));
@@ -1004,10 +1013,16 @@ bool GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_o
   const uint32_t* fmask = (me && me[0] == '0') ? nullptr : d_fmask_;
   const char* ge = std::getenv("KMLS_ENCODE_GROUP");  // =0: mask + rank gathers (A/B)
   const bool grp = fmask && !(ge && ge[0] == '0');
+  // default: LDS lookup tables where they apply; KMLS_ENCODE_LOOKUP=group keeps the 8-byte
+  // group gather (A/B)
+  const char* le = std::getenv("KMLS_ENCODE_LOOKUP");
+  const bool lk = grp && lk_valid_ && !(le && std::string(le) == "group");
   if (tiled && n_tx_ >= (1 << 16) &&
       kern::encode_bitmap_tiled(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev,
                                 Wp_total, word_off, F, (hipStream_t)stream_, fmask,
-                                grp ? d_fgroup_ : nullptr, grp ? d_c2r_ : nullptr))
+                                grp ? d_fgroup_ : nullptr, grp ? d_c2r_ : nullptr,
+                                lk ? d_lk_mask_ : nullptr, lk ? d_lk_hash_ : nullptr,
+                                kern::encode_lookup_shift(n_items_)))
     return true;
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev, Wp_total,
                       word_off, (hipStream_t)stream_, fmask);

@@ -224,6 +224,9 @@ class GpuMiner {
   uint32_t* d_fmask_ = nullptr;  // frequent-item bit mask (large vocabularies, select())
   unsigned long long* d_fgroup_ = nullptr;  // encode tables (kern::frequent_groups)
   int32_t* d_c2r_ = nullptr;
+  uint32_t* d_lk_mask_ = nullptr;  // encode LDS lookup tables (kern::encode_lookup_build)
+  uint32_t* d_lk_hash_ = nullptr;
+  bool lk_valid_ = false;
   void build_encode_tables(int64_t F);
   int32_t* d_ids_ = nullptr;
   uint64_t* d_own_bm_ = nullptr;  // single-GPU bitmap buffer

@@ -395,6 +395,24 @@ __global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restr
 // transaction found by binary search over the tile's LDS copy of tx_ptr.  More frequent rows than
 // one slab holds (config 5: ~15k) split into row bands, one block per (tile, band) with the band
 // index fastest, so a tile's bands run together and re-read its items from L2, not HBM.
+// encode LDS lookup tables (kernels.hpp: encode_lookup_build): coarse mask + packed hash
+static_assert(kEncodeLookupSlots == 4096, "the probe start is the top 12 bits of the hash");
+__global__ __launch_bounds__(kBlock) void k_encode_lookup_build(const int32_t* __restrict__ ids,
+                                                                int64_t F, int shift,
+                                                                uint32_t* __restrict__ mask,
+                                                                uint32_t* __restrict__ hash) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= F) return;
+  const uint32_t id = (uint32_t)ids[r];
+  const uint32_t b = id >> shift;
+  atomicOr(&mask[b >> 5], 1u << (b & 31));
+  const uint32_t v = (id << 11) | (uint32_t)r;
+  uint32_t slot = (id * 0x9E3779B1u) >> 20;
+  // F < slots / 2: an empty slot is always found
+  while (atomicCAS(&hash[slot], 0xFFFFFFFFu, v) != 0xFFFFFFFFu)
+    slot = (slot + 1) & (uint32_t)(kEncodeLookupSlots - 1);
+}
+
 constexpr int kEncodeU = 8;
 __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restrict__ tx_ptr,
                                                         const int32_t* __restrict__ items,
@@ -407,7 +425,10 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
                                                         bool xcd_order,
                                                         const unsigned long long* __restrict__ fgroup,
                                                         const int32_t* __restrict__ c2r,
-                                                        int txmap_cap) {
+                                                        int txmap_cap,
+                                                        const uint32_t* __restrict__ lk_mask,
+                                                        const uint32_t* __restrict__ lk_hash,
+                                                        int lk_shift) {
   // [band rows][TW], then tx_ptr[64*TW + 1], then (fgroup path) c2r[F], then (txmap_cap > 0)
   // the tile's item-position -> local-transaction map, one byte per item
   extern __shared__ unsigned long long s_bm[];
@@ -435,6 +456,16 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
   if (fgroup)
     for (int i = threadIdx.x; i < (int)F; i += blockDim.x) s_c2r[i] = c2r[i];
   uint8_t* s_tx = (uint8_t*)(s_c2r + (fgroup ? F : 0));
+  uint32_t* s_lkm = (uint32_t*)(((uintptr_t)(s_tx + txmap_cap) + 15) & ~(uintptr_t)15);
+  uint32_t* s_lkh = s_lkm + kEncodeLookupMaskBits / 32;
+  if (lk_hash) {
+    const uint4* m4 = reinterpret_cast<const uint4*>(lk_mask);
+    const uint4* h4 = reinterpret_cast<const uint4*>(lk_hash);
+    for (int i = threadIdx.x; i < (int)(kEncodeLookupMaskBits / 128); i += blockDim.x)
+      reinterpret_cast<uint4*>(s_lkm)[i] = m4[i];
+    for (int i = threadIdx.x; i < (int)(kEncodeLookupSlots / 4); i += blockDim.x)
+      reinterpret_cast<uint4*>(s_lkh)[i] = h4[i];
+  }
   __syncthreads();
   const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
   // item -> transaction without a per-item binary search (8 dependent LDS reads for 256
@@ -467,7 +498,27 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
       nx[u] = p < p1 ? items[p] : -1;
     }
     int32_t rk[kEncodeU];
-    if (fgroup) {
+    if (lk_hash) {
+      // coarse LDS bit test, then (frequent ids and their bucket mates only) a linear probe of
+      // the LDS hash: no global gather per item
+#pragma unroll
+      for (int u = 0; u < kEncodeU; ++u) {
+        rk[u] = -1;
+        if (it[u] < 0) continue;
+        const uint32_t b = (uint32_t)it[u] >> lk_shift;
+        if (!((s_lkm[b >> 5] >> (b & 31)) & 1u)) continue;
+        uint32_t slot = ((uint32_t)it[u] * 0x9E3779B1u) >> 20;
+        for (;;) {
+          const uint32_t e = s_lkh[slot];
+          if (e == 0xFFFFFFFFu) break;
+          if ((e >> 11) == (uint32_t)it[u]) {
+            rk[u] = (int32_t)(e & 2047u) - r0;
+            break;
+          }
+          slot = (slot + 1) & (uint32_t)(kEncodeLookupSlots - 1);
+        }
+      }
+    } else if (fgroup) {
       // one 8-byte gather per item: the frequent bits of its 32-id group and the number of
       // frequent ids before the group; the rank comes from the LDS compact-index → rank table
 #pragma unroll
@@ -786,12 +837,33 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
   KMLS_HIP(hipGetLastError());
 }
 
+int encode_lookup_shift(int64_t n_items) {
+  int sh = 0;
+  while ((std::max<int64_t>(n_items, 1) - 1) >> sh >= kEncodeLookupMaskBits) ++sh;
+  return sh;
+}
+
+void encode_lookup_build(const int32_t* ids, int64_t F, int64_t n_items, uint32_t* mask,
+                         uint32_t* hash, hipStream_t s) {
+  KMLS_HIP(hipMemsetAsync(mask, 0, kEncodeLookupMaskBits / 8, s));
+  KMLS_HIP(hipMemsetAsync(hash, 0xFF, kEncodeLookupSlots * 4, s));
+  if (F <= 0) return;
+  if (F > kEncodeLookupMaxF || n_items > (1 << 21))
+    throw std::runtime_error("encode_lookup_build: F or n_items out of range");
+  hipLaunchKernelGGL(k_encode_lookup_build, dim3((unsigned)((F + kBlock - 1) / kBlock)), dim3(kBlock),
+                     0, s, ids, F, encode_lookup_shift(n_items), mask, hash);
+  KMLS_HIP(hipGetLastError());
+}
+
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
                          int64_t F, hipStream_t s, const uint32_t* fmask,
-                         const unsigned long long* fgroup, const int32_t* c2r) {
+                         const unsigned long long* fgroup, const int32_t* c2r,
+                         const uint32_t* lk_mask, const uint32_t* lk_hash, int lk_shift) {
   if (n_tx <= 0 || F <= 0 || F > kEncodeTileMaxF) return false;
   if (F > kEncodeGroupMaxF) fgroup = nullptr, c2r = nullptr;  // c2r must fit LDS beside the slab
+  if (F > kEncodeLookupMaxF || !lk_mask) lk_hash = nullptr;
+  if (lk_hash) fgroup = nullptr, c2r = nullptr;
   // words per tile: the slab within 48 KB of LDS.  TW = 4 words (32-byte row segments, the
   // measured optimum); past 1536 rows, bands of 1536 rows (narrower segments would make the
   // write-out scattered 8-byte stores).
@@ -808,12 +880,13 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
   const char* me = std::getenv("KMLS_ENCODE_TXMAP");
   const int txmap_cap = (tw_log2 <= 2 && !(me && me[0] == '0')) ? (int)(64 * TW * 32) : 0;
   const size_t lds = (size_t)band * TW * 8 + (size_t)(64 * TW + 1) * 8 +
-                     (fgroup ? (size_t)F * 4 : 0) + (size_t)txmap_cap;
+                     (fgroup ? (size_t)F * 4 : 0) + (size_t)txmap_cap +
+                     (lk_hash ? (size_t)(16 + kEncodeLookupMaskBits / 8 + kEncodeLookupSlots * 4) : 0);
   const int64_t blocks = (n_tx + 64 * TW - 1) / (64 * TW) * n_bands;
   if (blocks > INT32_MAX) return false;
   hipLaunchKernelGGL(k_encode_tile, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr, items,
                      n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2, (int)band,
-                     fmask, xcd, fgroup, c2r, txmap_cap);
+                     fmask, xcd, fgroup, c2r, txmap_cap, lk_mask, lk_hash, lk_shift);
   KMLS_HIP(hipGetLastError());
   return true;
 }

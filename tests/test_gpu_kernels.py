@@ -599,17 +599,22 @@ def test_extend_split_k_long_rows(gpu_mod, monkeypatch, split):
     assert_same_itemsets(gpu_mod, r, c)
 
 
+@pytest.mark.parametrize("lookup", ["lds", "group"])
 @pytest.mark.parametrize("T,I,ms,min_f", [(300_000 + 37, 60_000, 0.002, 0),
                                             (200_000 + 37, 100_000, 0.002, 100),
+                                            (300_000 + 37, 1_000_003, 0.001, 50),
                                             (200_000 + 37, 100_000, 0.0005, 3000)])
-def test_encode_tiled_long_shard(gpu_mod, T, I, ms, min_f):
+def test_encode_tiled_long_shard(gpu_mod, monkeypatch, T, I, ms, min_f, lookup):
     """The LDS-slab encode produces the same tid-bitmaps as the host encoder, on a long shard
     with an odd tail tile; the second case has a million-style vocabulary (frequent-item mask
     in front of the rank gather, or the one-gather group tables when F <= 2048) and more
-    frequent rows than one LDS slab (row bands).  The
+    frequent rows than one LDS slab (row bands).  ``lookup``: the LDS mask + hash tables
+    (default where F < 2048) or the 8-byte group gather (KMLS_ENCODE_LOOKUP=group).  The
     buffer starts as all ones: the tiled encode must write every word of the shard's columns
     (the tx-DP path no longer clears the bitmap first)."""
     import torch
+    if lookup == "group":
+        monkeypatch.setenv("KMLS_ENCODE_LOOKUP", "group")
     ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 9)
     g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(ptr, items, I)
