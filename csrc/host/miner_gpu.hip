@@ -622,8 +622,9 @@ struct MineRun {
       if (clen) KMLS_HIP(hipMemsetAsync(clen + S, 0, sizeof(int64_t), s));
       kern::LevelOut o{cbm, crank, cgid, cend, clen, out_parent.p, out_item.p, out_count.p,
                        out_depth.p, out_size, (uint8_t)(depth + 1)};
+      int64_t* surv = leaf ? nullptr : (int64_t*)arena->push((size_t)S * sizeof(int64_t));
       kern::extend_materialize(L.bm, Wp, cand_off, L.n, L.rank, L.gid, d_ids, c0, c1, cnt, minsup,
-                               pos, o, s);
+                               pos, o, s, S, surv);
       out_size += S;
       stream_out();
       max_depth = std::max(max_depth, depth + 1);
@@ -1013,10 +1014,10 @@ bool GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_o
   const uint32_t* fmask = (me && me[0] == '0') ? nullptr : d_fmask_;
   const char* ge = std::getenv("KMLS_ENCODE_GROUP");  // =0: mask + rank gathers (A/B)
   const bool grp = fmask && !(ge && ge[0] == '0');
-  // default: LDS lookup tables where they apply; KMLS_ENCODE_LOOKUP=group keeps the 8-byte
-  // group gather (A/B)
+  // KMLS_ENCODE_LOOKUP=lds: LDS mask + hash tables instead of the 8-byte group gather (A/B:
+  // 20.5 vs 13.2 ms at 100M x 754 frequent items, profiles/r2_s8_encode_materialize.md)
   const char* le = std::getenv("KMLS_ENCODE_LOOKUP");
-  const bool lk = grp && lk_valid_ && !(le && std::string(le) == "group");
+  const bool lk = grp && lk_valid_ && le && std::string(le) == "lds";
   if (tiled && n_tx_ >= (1 << 16) &&
       kern::encode_bitmap_tiled(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev,
                                 Wp_total, word_off, F, (hipStream_t)stream_, fmask,

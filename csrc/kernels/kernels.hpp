@@ -36,7 +36,8 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
 // frequent mask of kEncodeLookupMaskBits bits (bit b: some frequent id has id >> lk_shift == b)
 // and an open-addressing hash of kEncodeLookupSlots packed (id << 11 | rank) words.  Both are
 // staged in LDS per tile, so an item costs one LDS bit test and (frequent or bucket-mate) a
-// short probe, instead of a random 8-byte gather from L2.
+// short probe, instead of a random 8-byte gather from L2.  A/B only (KMLS_ENCODE_LOOKUP=lds):
+// measured slower than the L2 gather (20.5 vs 13.2 ms at 100M).
 constexpr int64_t kEncodeLookupMaxF = 2047;
 constexpr int64_t kEncodeLookupMaskBits = 65536;
 constexpr int64_t kEncodeLookupSlots = 4096;
@@ -92,7 +93,10 @@ struct LevelOut {
 void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
                         const int32_t* rank, const int64_t* gid, const int32_t* ids,
                         int64_t c0, int64_t c1, const uint32_t* cnt, uint32_t minsup,
-                        const int64_t* pos, const LevelOut& o, hipStream_t s);
+                        const int64_t* pos, const LevelOut& o, hipStream_t s,
+                        int64_t n_surv = -1, int64_t* surv_scratch = nullptr);
+// n_surv (the survivor count, known on the host) + surv_scratch (n_surv int64): long rows are
+// copied by a grid over (survivor, slice) pairs sized by n_surv, not over all candidates
 // dense upper-triangular pair counts over a single class of F rows (level 2 bit-GEMM)
 void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
 void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);

@@ -668,6 +668,60 @@ __global__ __launch_bounds__(kBlock) void k_extend_materialize(
   }
 }
 
+// Survivor-driven materialize for long rows.  The candidate-driven kernel above gives each
+// candidate one team, so at level 2 of a 100M-transaction shard (284k candidates, ~160
+// survivors of 1.56M words each) a handful of wave64 teams copy 12.5 MB rows alone.  Here the
+// survivors are listed first (k_surv_index: surv[pos[c]] = c) and the grid runs over
+// (survivor, slice) pairs, so every survivor's AND row is streamed by many teams at once.
+__global__ __launch_bounds__(kBlock) void k_surv_index(const uint32_t* __restrict__ cnt,
+                                                       uint32_t minsup,
+                                                       const int64_t* __restrict__ pos,
+                                                       int64_t c0, int64_t nc,
+                                                       int64_t* __restrict__ surv) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nc;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (cnt[i] >= minsup) surv[pos[i]] = c0 + i;
+}
+
+__global__ __launch_bounds__(kBlock) void k_materialize_surv(
+    const unsigned long long* __restrict__ bm, int64_t Wp, const int64_t* __restrict__ cand_off,
+    int64_t n_rows, const int32_t* __restrict__ rank, const int64_t* __restrict__ gid,
+    const int32_t* __restrict__ ids, int64_t c0, const uint32_t* __restrict__ cnt,
+    const int64_t* __restrict__ pos, const int64_t* __restrict__ surv, int64_t n_surv,
+    int64_t split, LevelOut o) {
+  constexpr int TS = 64;
+  const int tl = threadIdx.x & (TS - 1);
+  const int64_t team = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / TS;
+  const int64_t nteams = ((int64_t)gridDim.x * blockDim.x) / TS;
+  const int64_t n2 = Wp >> 1;
+  for (int64_t wi = team; wi < n_surv * split; wi += nteams) {
+    const int64_t s = wi / split, part = wi % split;
+    const int64_t c = surv[s];
+    const int64_t a = find_row(cand_off, n_rows, c);
+    const int64_t b = a + 1 + (c - cand_off[a]);
+    const ulonglong2* x = reinterpret_cast<const ulonglong2*>(bm + a * Wp);
+    const ulonglong2* y = reinterpret_cast<const ulonglong2*>(bm + b * Wp);
+    ulonglong2* z = reinterpret_cast<ulonglong2*>(o.bm + s * Wp);
+    const int64_t lo = n2 * part / split, hi = n2 * (part + 1) / split;
+    for (int64_t w = lo + tl; w < hi; w += TS) {
+      const ulonglong2 u = x[w], v = y[w];
+      z[w] = make_ulonglong2(u.x & v.x, u.y & v.y);
+    }
+    if (tl == 0 && part == 0) {
+      const int32_t rb = rank[b];
+      o.rank[s] = rb;
+      o.gid[s] = o.out_base + s;
+      const int64_t re = pos[cand_off[a + 1] - c0];
+      o.row_end[s] = (int32_t)re;
+      o.len[s] = re - s - 1;
+      o.out_parent[o.out_base + s] = gid[a];
+      o.out_item[o.out_base + s] = ids[rb];
+      o.out_count[o.out_base + s] = cnt[c - c0];
+      o.out_depth[o.out_base + s] = o.depth;
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // O8 level 2: tiled bit-GEMM  G[i][j] = popcount(row_i & row_j), 64x64 output tile / block,
 // K staged through LDS in transposed [k][row] layout (16 words per stage).
@@ -1168,10 +1222,26 @@ void extend_count(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64
 void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off, int64_t n_rows,
                         const int32_t* rank, const int64_t* gid, const int32_t* ids, int64_t c0,
                         int64_t c1, const uint32_t* cnt, uint32_t minsup, const int64_t* pos,
-                        const LevelOut& o, hipStream_t s) {
+                        const LevelOut& o, hipStream_t s, int64_t n_surv, int64_t* surv) {
   if (c1 <= c0) return;
   const int ts = team_size(Wp);
   const int64_t teams_per_block = kBlock / ts;
+  // long rows with a known survivor count: survivor-driven grid (KMLS_MATERIALIZE=cand keeps
+  // the candidate-driven one, A/B)
+  const char* me = std::getenv("KMLS_MATERIALIZE");
+  if (o.bm && ts == 64 && n_surv > 0 && surv && !(me && std::string(me) == "cand")) {
+    hipLaunchKernelGGL(k_surv_index, dim3(grid_for(c1 - c0, kBlock, 2048)), dim3(kBlock), 0, s,
+                       cnt, minsup, pos, c0, c1 - c0, surv);
+    // >= 8192 teams over the survivors' rows, slices of >= 1024 16-byte chunks
+    const int64_t sp = std::max<int64_t>(
+        1, std::min<int64_t>((8192 + n_surv - 1) / n_surv, (Wp >> 1) / 1024));
+    const int g = grid_for(n_surv * sp, kBlock / 64, 256 * 32);
+    hipLaunchKernelGGL(k_materialize_surv, dim3(g), dim3(kBlock), 0, s,
+                       (const unsigned long long*)bm, Wp, cand_off, n_rows, rank, gid, ids, c0, cnt,
+                       pos, surv, n_surv, sp, o);
+    KMLS_HIP(hipGetLastError());
+    return;
+  }
   const int64_t split = o.bm ? extend_split(Wp, c1 - c0, ts) : 1;  // leaves copy no words
   const int g = grid_for((c1 - c0) * split, (int)teams_per_block, 256 * 32);
   KMLS_TEAM_DISPATCH(ts, k_extend_materialize, dim3(g), dim3(kBlock), 0, s,

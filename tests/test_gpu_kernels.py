@@ -608,13 +608,13 @@ def test_encode_tiled_long_shard(gpu_mod, monkeypatch, T, I, ms, min_f, lookup):
     """The LDS-slab encode produces the same tid-bitmaps as the host encoder, on a long shard
     with an odd tail tile; the second case has a million-style vocabulary (frequent-item mask
     in front of the rank gather, or the one-gather group tables when F <= 2048) and more
-    frequent rows than one LDS slab (row bands).  ``lookup``: the LDS mask + hash tables
-    (default where F < 2048) or the 8-byte group gather (KMLS_ENCODE_LOOKUP=group).  The
+    frequent rows than one LDS slab (row bands).  ``lookup``: the 8-byte group gather
+    (default where F <= 2048) or the LDS mask + hash tables (KMLS_ENCODE_LOOKUP=lds, A/B).  The
     buffer starts as all ones: the tiled encode must write every word of the shard's columns
     (the tx-DP path no longer clears the bitmap first)."""
     import torch
-    if lookup == "group":
-        monkeypatch.setenv("KMLS_ENCODE_LOOKUP", "group")
+    if lookup == "lds":
+        monkeypatch.setenv("KMLS_ENCODE_LOOKUP", "lds")
     ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 9)
     g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(ptr, items, I)
