@@ -144,12 +144,12 @@ __global__ __launch_bounds__(kBlock) void k_item_support_hash(const int32_t* __r
 //                      slice of the partition's ids; one global atomic per nonzero bin per block.
 // ~2.5 passes over the int32 items instead of one fabric atomic per item.
 // ----------------------------------------------------------------------------------------
-// 16384-id partitions: a 1M vocabulary splits 62 ways, so the scatter's LDS counting-sort atomics
-// (64 lanes into P counters) collide about half as often as with 31 partitions of 32768 ids
-// (PMC: 6.2e8 LDS bank-conflict cycles for 3.5e8 LDS instructions in k_part_scatter at 15 bits)
-constexpr int kPartBits = 14;
+// 32768-id partitions (a 1M vocabulary splits 31 ways).  16384-id partitions (62 ways, fewer
+// counter collisions in the scatter's LDS counting sort) measured slower: scatter 1.12 -> 1.25
+// ms and count 0.38 -> 0.42 ms per 686M-item tile (profiles/r2_s8_support_partitions.md)
+constexpr int kPartBits = 15;
 constexpr int kPartBins = 1 << kPartBits;
-constexpr int kPartMax = 128;    // partitions: n_items <= 2M
+constexpr int kPartMax = 64;     // partitions: n_items <= 2M
 constexpr int kPartGrid = 1024;  // blocks of passes 1 and 2
 constexpr int kPartTile = 4096;  // items per LDS counting-sort tile (16 per thread)
 
@@ -424,7 +424,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_lookup_build(const int32_t* _
     slot = (slot + 1) & (uint32_t)(kEncodeLookupSlots - 1);
 }
 
-constexpr int kEncodeU = 8;
+template <int kEncodeU>
 __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restrict__ tx_ptr,
                                                         const int32_t* __restrict__ items,
                                                         int64_t n_tx,
@@ -949,9 +949,16 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
                      (lk_hash ? (size_t)(16 + kEncodeLookupMaskBits / 8 + kEncodeLookupSlots * 4) : 0);
   const int64_t blocks = (n_tx + 64 * TW - 1) / (64 * TW) * n_bands;
   if (blocks > INT32_MAX) return false;
-  hipLaunchKernelGGL(k_encode_tile, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr, items,
-                     n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2, (int)band,
-                     fmask, xcd, fgroup, c2r, txmap_cap, lk_mask, lk_hash, lk_shift);
+  // items per thread per round (KMLS_ENCODE_U=16: twice the gathers in flight, A/B)
+  const char* ue = std::getenv("KMLS_ENCODE_U");
+  if (ue && std::atoi(ue) == 16)
+    hipLaunchKernelGGL(k_encode_tile<16>, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr,
+                       items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2,
+                       (int)band, fmask, xcd, fgroup, c2r, txmap_cap, lk_mask, lk_hash, lk_shift);
+  else
+    hipLaunchKernelGGL(k_encode_tile<8>, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr,
+                       items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2,
+                       (int)band, fmask, xcd, fgroup, c2r, txmap_cap, lk_mask, lk_hash, lk_shift);
   KMLS_HIP(hipGetLastError());
   return true;
 }
