@@ -373,7 +373,8 @@ template <int MODE>
 __global__ __launch_bounds__(256, 1) void k_pair_gram_wide(const unsigned long long* __restrict__ bm,
                                                            int64_t Wp, int64_t F, int64_t n_tiles,
                                                            int64_t n_blocks, int scale,
-                                                           uint32_t* __restrict__ out) {
+                                                           uint32_t* __restrict__ out,
+                                                           int xcd_2d) {
   constexpr bool FP4 = MODE != 0;
   __shared__ uint2 lut[256];
   __shared__ uint32_t lut4[256];
@@ -388,9 +389,23 @@ __global__ __launch_bounds__(256, 1) void k_pair_gram_wide(const unsigned long l
       lut[i] = make_uint2(nib((uint32_t)i & 0xFu), nib((uint32_t)i >> 4));
     }
   }
-  const int64_t orig = blockIdx.x;
-  const int64_t q = n_blocks / 8, rr = n_blocks % 8, xcd = orig % 8;
-  int64_t idx = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  int64_t idx, y;
+  if (xcd_2d) {
+    // XCD-aware over the whole (tile pair, K slice) grid: the hardware deals linear workgroup
+    // ids round-robin over the 8 XCDs, so remap them such that the bw tile-pair blocks of one
+    // K slice (which stage the same stripes of the same row tiles) share an XCD and its L2
+    const int64_t n = (int64_t)gridDim.x * gridDim.y;
+    const int64_t h = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const int64_t q2 = n / 8, r2 = n % 8, x8 = h % 8;
+    const int64_t li = (x8 < r2 ? x8 * (q2 + 1) : r2 * (q2 + 1) + (x8 - r2) * q2) + h / 8;
+    y = li / gridDim.x;
+    idx = li % gridDim.x;
+  } else {
+    const int64_t orig = blockIdx.x;
+    const int64_t q = n_blocks / 8, rr = n_blocks % 8, xcd = orig % 8;
+    idx = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+    y = blockIdx.y;
+  }
   int64_t ti = 0;
   while (idx >= n_tiles - ti) { idx -= n_tiles - ti; ++ti; }
   const int64_t tj = ti + idx;
@@ -412,7 +427,7 @@ __global__ __launch_bounds__(256, 1) void k_pair_gram_wide(const unsigned long l
     const int64_t grow = lr < kWTile ? ti * kWTile + lr : tj * kWTile + (lr - kWTile);
     src[k] = grow < F ? reinterpret_cast<const ulonglong2*>(bm + grow * Wp) : nullptr;
   }
-  const int64_t ks = gridDim.y, y = blockIdx.y;
+  const int64_t ks = gridDim.y;
   const int64_t n_stripes = (Wp + kWStripe - 1) / kWStripe;
   const int64_t my_stripes = y < n_stripes ? (n_stripes - y + ks - 1) / ks : 0;
   auto gload = [&](int64_t it, ulonglong2 (&R)[8]) {
@@ -863,6 +878,9 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
       return (int64_t)std::max(1, p.multiProcessorCount);  // one 4-wave block per CU (256 AGPRs)
     }();
     const int64_t n_stripes = (Wp + kWStripe - 1) / kWStripe;
+    // KMLS_GRAM_XCD=2d: XCD-aware remap over the 2-D grid (A/B)
+    const char* xe = std::getenv("KMLS_GRAM_XCD");
+    const int xcd2 = (xe && std::string(xe) == "2d") ? 1 : 0;
     int64_t ksw = std::max<int64_t>(1, std::min<int64_t>(slots_w / bw, Wp / 256));
     // FP4: a block's f32 accumulators stay exact while its stripes (512 transactions each)
     // number < 2^15
@@ -872,13 +890,13 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
                          (const unsigned long long*)bm, Wp, F, ntw, bw, out);
     else if (fp4 == 3)
       hipLaunchKernelGGL(k_pair_gram_wide<2>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
-                         (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out);
+                         (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out, xcd2);
     else if (fp4 == 1)
       hipLaunchKernelGGL(k_pair_gram_wide<1>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
-                         (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out);
+                         (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out, xcd2);
     else
       hipLaunchKernelGGL(k_pair_gram_wide<0>, dim3((unsigned)bw, (unsigned)ksw), dim3(256), 0, s,
-                         (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out);
+                         (const unsigned long long*)bm, Wp, F, ntw, bw, scale, out, xcd2);
   } else if (gram_lds() || fp4 == 1) {
     static const int64_t slots_lds = [] {
       int dev = 0, per_cu = 1;
