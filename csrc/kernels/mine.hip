@@ -574,6 +574,112 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
   }
 }
 
+// Multi-band encode for wide frequent sets (config 5: ~15k rows, more than one LDS slab).  The
+// band-per-block kernel above re-reads every tile's items and redoes both lookup gathers for
+// each of its row bands (10 bands at config 5).  Here one block owns a tile and all its bands:
+// pass A looks every item up once and appends (rank, local transaction) pairs of the frequent
+// ones to LDS (wave-aggregated append); pass B builds each band's slab from the pairs and writes
+// it out.  A tile with more than kMbCap items is done in item chunks; chunks after the first
+// OR their nonzero words into the words the first chunk stored.
+constexpr int kMbCap = 8192;
+constexpr int kMbBand = 1024;
+__global__ __launch_bounds__(kBlock) void k_encode_multiband(const int64_t* __restrict__ tx_ptr,
+                                                             const int32_t* __restrict__ items,
+                                                             int64_t n_tx,
+                                                             const int32_t* __restrict__ rank_of,
+                                                             unsigned long long* __restrict__ bm,
+                                                             int64_t Wp, int64_t word_off,
+                                                             int64_t F,
+                                                             const uint32_t* __restrict__ fmask) {
+  constexpr int TW = 4;
+  __shared__ unsigned long long s_bm[kMbBand * TW];
+  __shared__ int64_t s_ptr[64 * TW + 1];
+  __shared__ uint32_t s_pair[kMbCap];
+  __shared__ uint32_t s_n;
+  int64_t lb = blockIdx.x;  // XCD-aware tile order, as in k_encode_tile
+  {
+    const int64_t nb = gridDim.x, q = nb / 8, rr = nb % 8, x = lb % 8;
+    lb = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + lb / 8;
+  }
+  const int64_t t0 = lb * 64 * TW;
+  const int nt = (int)min((int64_t)(64 * TW), n_tx - t0);
+  for (int i = threadIdx.x; i <= nt; i += blockDim.x) s_ptr[i] = tx_ptr[t0 + i];
+  __syncthreads();
+  const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
+  const int64_t wbase = word_off + (t0 >> 6);
+  const int64_t wn = min((int64_t)TW, min(Wp - wbase, ((n_tx + 63) >> 6) - (t0 >> 6)));
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  bool first = true;
+  for (int64_t pc = p0; pc < p1 || first; pc += kMbCap) {
+    const int64_t pe = min(p1, pc + kMbCap);
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    // pass A: lookups (mask gather, then rank gather for the frequent ids) and the append
+    for (int64_t pb = pc; pb < pe; pb += (int64_t)blockDim.x * 4) {
+      int32_t it[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t p = pb + (int64_t)u * blockDim.x + threadIdx.x;
+        it[u] = p < pe ? items[p] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (it[u] >= 0 && fmask && !((fmask[it[u] >> 5] >> (it[u] & 31)) & 1u)) it[u] = -1;
+      int32_t rk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) rk[u] = it[u] >= 0 ? rank_of[it[u]] : -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool v = rk[u] >= 0;
+        uint32_t e = 0;
+        if (v) {
+          const int64_t p = pb + (int64_t)u * blockDim.x + threadIdx.x;
+          int lo = 0, hi = nt;  // largest lt with s_ptr[lt] <= p
+          while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_ptr[mid] <= p) lo = mid; else hi = mid;
+          }
+          e = ((uint32_t)rk[u] << 8) | (uint32_t)lo;
+        }
+        const unsigned long long bal = __ballot(v);
+        uint32_t base = 0;
+        if (lane == 0 && bal) base = atomicAdd(&s_n, (uint32_t)__popcll(bal));
+        base = __shfl(base, 0, 64);
+        if (v) s_pair[base + (uint32_t)__popcll(bal & lt_mask)] = e;
+      }
+    }
+    __syncthreads();
+    const int np = (int)s_n;
+    // pass B: one slab per band from the pairs
+    for (int64_t r0 = 0; r0 < F; r0 += kMbBand) {
+      const int nr = (int)min((int64_t)kMbBand, F - r0);
+      for (int i = threadIdx.x; i < nr * TW; i += blockDim.x) s_bm[i] = 0ull;
+      __syncthreads();
+      for (int i = threadIdx.x; i < np; i += blockDim.x) {
+        const uint32_t e = s_pair[i];
+        const int64_t rr = (int64_t)(e >> 8) - r0;
+        if (rr >= 0 && rr < nr) {
+          const uint32_t lt = e & 255u;
+          atomicOr(&s_bm[rr * TW + (lt >> 6)], 1ull << (lt & 63));
+        }
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < nr * TW; i += blockDim.x) {
+        const int row = i >> 2, w = i & 3;
+        if (w >= wn) continue;
+        unsigned long long* dst = &bm[(r0 + row) * Wp + wbase + w];
+        if (first) *dst = s_bm[i];
+        else if (s_bm[i]) atomicOr(dst, s_bm[i]);
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
+    first = false;
+    if (pe >= p1) break;
+  }
+}
+
 // flag(i) = (i < n && cnt[i] >= minsup); scanning n+1 flags gives pos[n] = #survivors directly
 struct FlagOp {
   const uint32_t* cnt;
@@ -926,6 +1032,17 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
                          const unsigned long long* fgroup, const int32_t* c2r,
                          const uint32_t* lk_mask, const uint32_t* lk_hash, int lk_shift) {
   if (n_tx <= 0 || F <= 0 || F > kEncodeTileMaxF) return false;
+  // frequent sets wider than one slab: the multi-band kernel (one block per tile, every band;
+  // KMLS_ENCODE_MULTIBAND=0 keeps one block per (tile, band), A/B)
+  const char* mb = std::getenv("KMLS_ENCODE_MULTIBAND");
+  if (F > 1536 && F < (1 << 24) && !(mb && mb[0] == '0')) {
+    const int64_t tiles = (n_tx + 255) / 256;
+    if (tiles > INT32_MAX) return false;
+    hipLaunchKernelGGL(k_encode_multiband, dim3((unsigned)tiles), dim3(kBlock), 0, s, tx_ptr, items,
+                       n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, fmask);
+    KMLS_HIP(hipGetLastError());
+    return true;
+  }
   if (F > kEncodeGroupMaxF) fgroup = nullptr, c2r = nullptr;  // c2r must fit LDS beside the slab
   if (F > kEncodeLookupMaxF || !lk_mask) lk_hash = nullptr;
   if (lk_hash) fgroup = nullptr, c2r = nullptr;

@@ -599,7 +599,7 @@ def test_extend_split_k_long_rows(gpu_mod, monkeypatch, split):
     assert_same_itemsets(gpu_mod, r, c)
 
 
-@pytest.mark.parametrize("lookup", ["lds", "group"])
+@pytest.mark.parametrize("lookup", ["lds", "group", "no-multiband"])
 @pytest.mark.parametrize("T,I,ms,min_f", [(300_000 + 37, 60_000, 0.002, 0),
                                             (200_000 + 37, 100_000, 0.002, 100),
                                             (300_000 + 37, 1_000_003, 0.001, 50),
@@ -615,6 +615,8 @@ def test_encode_tiled_long_shard(gpu_mod, monkeypatch, T, I, ms, min_f, lookup):
     import torch
     if lookup == "lds":
         monkeypatch.setenv("KMLS_ENCODE_LOOKUP", "lds")
+    if lookup == "no-multiband":  # wide frequent sets: one block per (tile, band), A/B
+        monkeypatch.setenv("KMLS_ENCODE_MULTIBAND", "0")
     ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 9)
     g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(ptr, items, I)
