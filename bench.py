@@ -138,7 +138,8 @@ def run_config2(N, tx, names, tie, steps: int, verify: bool) -> dict:
 C3_DIGEST = "d3b31400a6ebfffbbdac749329a5c1e6"
 
 
-def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: int = 1) -> dict:
+def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: int = 1,
+                comm: str = "") -> dict:
     """BASELINE config 3 (10M transactions x 1M items, min_support 0.001) on all ranks of the job:
     transaction-DP mining (each rank generates and encodes only its shard; supports, gram and
     per-level candidate counts all-reduced), so support/encode/gram work shrinks with N.  The
@@ -149,9 +150,12 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
     import torch.distributed as dist
     from kubernetes_machine_learning_server_amd.data.synthetic import SHAPES
     from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner, shard_bounds
-    comm = os.environ.get("KMLS_BENCH_C3_COMM", "host")
+    comm = comm or os.environ.get("KMLS_BENCH_C3_COMM", "host")
     prev = os.environ.get("KMLS_COMM")
+    prev_to = os.environ.get("KMLS_COMM_TIMEOUT_S")
     os.environ["KMLS_COMM"] = comm
+    if comm == "rccl" and prev_to is None:  # bounded: a stuck RCCL init or wait raises
+        os.environ["KMLS_COMM_TIMEOUT_S"] = "60"
     try:
         shape = SHAPES["10Mx1M"]
         T = shape.n_tx
@@ -202,6 +206,8 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
             os.environ.pop("KMLS_COMM", None)
         else:
             os.environ["KMLS_COMM"] = prev
+        if prev_to is None:
+            os.environ.pop("KMLS_COMM_TIMEOUT_S", None)
 
 
 def run_serve(shape: str, qps_list, duration: float, backend: str) -> dict:
@@ -500,6 +506,16 @@ def main() -> int:
             c3 = {"error": repr(e)[:300]}
         if rank == 0:
             out["config3"] = c3
+        # the same tx-DP run over the native RCCL communicator (xGMI), when the ranks are on
+        # an RCCL process group: every level's count all-reduce goes through RCCL on the
+        # miner's stream (init and waits bounded at 60 s; an error is reported, not raised)
+        if world > 1 and dist_backend == "nccl" and os.environ.get("KMLS_BENCH_C3_RCCL", "1") != "0":
+            try:
+                c3r = run_config3(N, world, rank, device, comm="rccl")
+            except Exception as e:
+                c3r = {"error": repr(e)[:300]}
+            if rank == 0:
+                out["config3_rccl"] = c3r
     if world == 1 and not args.cpu and not args.no_config2 and rank == 0:
         out["config2"] = run_config2(N, tx, names, tie, steps=10, verify=not args.no_verify)
     if world == 1 and rank == 0 and args.serve_qps:

@@ -1864,7 +1864,11 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
   const size_t mark = arena_->mark();
   // 1. supports in K tiles; tile k's all-reduce (comm stream) overlaps tile k+1's histogram.
   //    The comm stream and the tile events live as long as the miner (no per-call creation).
-  const int K = std::max(1, std::min(64, support_tiles));
+  //    One rank has no all-reduce to overlap: one tile, so the partitioned histogram's fixed
+  //    per-pass costs (per-block bin flushes, scans) are paid once (KMLS_SUPPORT_TILES forces K).
+  int K = std::max(1, std::min(64, support_tiles));
+  if (!comm || comm->world() <= 1) K = 1;
+  if (const char* te = std::getenv("KMLS_SUPPORT_TILES")) K = std::max(1, std::min(64, std::atoi(te)));
   const size_t vec = (size_t)std::max<int64_t>(n_items_, 1) * sizeof(uint32_t);
   uint32_t* d_part = (uint32_t*)arena_->push(vec * K);
   KMLS_HIP(hipMemsetAsync(d_part, 0, vec * K, s));

@@ -9,3 +9,4 @@ KMLS_GRAM_FP4=mask16 step l100_mask16 600 $L100
 RM10="python3 -m kubernetes_machine_learning_server_amd.bench.bench_large --rule-map --min-support 0.0002 --steps 1 --warmup 1 --shape 10Mx1M"
 step rm10_mask 600 $RM10
 KMLS_GRAM_FP4=mask16 step rm10_mask16 600 $RM10
+KMLS_SUPPORT_TILES=4 step l100_tiles4 600 $L100
