@@ -584,120 +584,8 @@ __global__ __launch_bounds__(256, 1) void k_pair_gram_wide(const unsigned long l
   }
 }
 
-// Masked-nibble FP4 with 16-word stripes (KMLS_GRAM_FP4=mask16): the wide kernel's MODE 2 with
-// stripes of 1024 transactions (144-byte padded rows, 147 KB of LDS for the double buffer, one
-// block per CU as before), so each block barrier is amortised over 4 chunks (64 MFMAs per wave
-// per chunk) instead of 2.  Thread t stages 16-byte segment (t & 7) of rows (t >> 3) + 32 k, k < 16.
-constexpr int64_t kW16Stripe = 16;
-constexpr int kW16RowB = 144;
-constexpr int kW16StageB = 2 * kWTile * kW16RowB;  // 72 KB per buffer
-__global__ __launch_bounds__(256, 1) void k_pair_gram_mask16(const unsigned long long* __restrict__ bm,
-                                                             int64_t Wp, int64_t F, int64_t n_tiles,
-                                                             uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) unsigned char stage[2][kW16StageB];
-  int64_t idx, y;
-  {  // XCD-aware over the whole grid, as k_pair_gram_wide's default
-    const int64_t n = (int64_t)gridDim.x * gridDim.y;
-    const int64_t hh = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-    const int64_t q2 = n / 8, r2 = n % 8, x8 = hh % 8;
-    const int64_t li = (x8 < r2 ? x8 * (q2 + 1) : r2 * (q2 + 1) + (x8 - r2) * q2) + hh / 8;
-    y = li / gridDim.x;
-    idx = li % gridDim.x;
-  }
-  int64_t ti = 0;
-  while (idx >= n_tiles - ti) { idx -= n_tiles - ti; ++ti; }
-  const int64_t tj = ti + idx;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int r = lane & 31, h = lane >> 5;
-  const int seg = tid & 7, lrow0 = tid >> 3;
-  const int64_t W2 = Wp >> 1;
-  const ulonglong2* src[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int lr = lrow0 + 32 * k;
-    const int64_t grow = lr < kWTile ? ti * kWTile + lr : tj * kWTile + (lr - kWTile);
-    src[k] = grow < F ? reinterpret_cast<const ulonglong2*>(bm + grow * Wp) : nullptr;
-  }
-  const int64_t ks = gridDim.y;
-  const int64_t n_stripes = (Wp + kW16Stripe - 1) / kW16Stripe;
-  const int64_t my_stripes = y < n_stripes ? (n_stripes - y + ks - 1) / ks : 0;
-  ulonglong2 R[16];
-  auto gload = [&](int64_t it) {
-    const int64_t u = (it * ks + y) * (kW16Stripe / 2) + seg;
-    const bool in = u < W2;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) R[k] = (src[k] && in) ? src[k][u] : make_ulonglong2(0, 0);
-  };
-  v16f acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = v16f{};
-  const int la = wr * 128 + r;
-  const int lb = kWTile + wc * 128 + r;
-  if (my_stripes > 0) gload(0);
-  for (int64_t it = 0; it < my_stripes; ++it) {
-    const int buf = (int)(it & 1);
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      *reinterpret_cast<ulonglong2*>(&stage[buf][(lrow0 + 32 * k) * kW16RowB + seg * 16]) = R[k];
-    __syncthreads();  // stripe `it` visible; buffer buf^1 (stripe it-1) no longer read
-    if (it + 1 < my_stripes) gload(it + 1);
-    const unsigned char* sb = stage[buf];
-#pragma unroll
-    for (int c = 0; c < (int)(kW16Stripe / 4); ++c) {  // 4-word chunks
-      v4i A[4], B[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        A[m] = *reinterpret_cast<const v4i*>(sb + (la + 32 * m) * kW16RowB + c * 32 + h * 16);
-        B[m] = *reinterpret_cast<const v4i*>(sb + (lb + 32 * m) * kW16RowB + c * 32 + h * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int msk = j == 0 ? 0x11111111 : j == 1 ? 0x22222222 : 0x44444444;
-        const int sc = j == 0 ? 128 : j == 1 ? 127 : 126;
-        v8i fa[4], fb[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            fa[m][d] = (j == 3 ? (int)((uint32_t)A[m][d] >> 1) : A[m][d]) & msk;
-            fb[m][d] = (j == 3 ? (int)((uint32_t)B[m][d] >> 1) : B[m][d]) & msk;
-            fa[m][d + 4] = 0;
-            fb[m][d + 4] = 0;
-          }
-        }
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-          for (int m = 0; m < 4; ++m)
-            acc[m][n] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[m], fb[n], acc[m][n], 4, 4,
-                                                                        0, sc, 0, sc);
-      }
-    }
-  }
-  const int64_t rowb = ti * kWTile + wr * 128, colb = tj * kWTile + wc * 128;
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int64_t rw = rowb + 32 * m + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        const int64_t cl = colb + 32 * n + r;
-        const uint32_t v = (uint32_t)acc[m][n][reg];
-        if (rw < F && cl < F && cl > rw) {
-          if (gridDim.y == 1) out[rw * F + cl] = v;
-          else if (v) atomicAdd(&out[rw * F + cl], v);
-        }
-      }
-    }
-  }
-}
-
+// (A 16-word-stripe variant of MODE 2, half the block barriers per transaction, measured no
+// faster: 100M gram 14.18 vs 14.24 ms, config-5 10M gram 402 vs 385 ms; removed.)
 // Masked-nibble FP4 with two waves per SIMD (KMLS_GRAM_FP4=mask8): 512-thread blocks of 8 waves
 // (2 row x 4 column groups), each wave a 128x64 output block = 4x2 MFMA tiles (8 accumulators,
 // 128 AGPRs), so each SIMD holds two waves and one issues while the other waits on an operand or
@@ -942,7 +830,6 @@ static int gram_fp4() {
   const char* e = std::getenv("KMLS_GRAM_FP4");
   if (!e || !e[0] || std::string(e) == "mask") return 3;
   if (std::string(e) == "mask8") return 4;  // masked nibbles, 8 waves (2 per SIMD), A/B
-  if (std::string(e) == "mask16") return 5;  // masked nibbles, 16-word stripes, A/B
   if (e[0] == '1') return 1;
   return std::string(e) == "direct" ? 2 : 0;
 }
@@ -1002,14 +889,7 @@ void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out,
     // FP4: a block's f32 accumulators stay exact while its stripes (512 transactions each)
     // number < 2^15
     if (fp4 == 1 || fp4 >= 3) ksw = std::max<int64_t>(ksw, (n_stripes + 32767) / 32768 + 1);
-    if (fp4 == 5) {
-      // 1024-transaction stripes: a block's f32 accumulators stay exact below 2^14 stripes
-      const int64_t ns16 = (Wp + kW16Stripe - 1) / kW16Stripe;
-      const int64_t k16 = std::max<int64_t>(std::max<int64_t>(1, std::min<int64_t>(slots_w / bw, Wp / 512)),
-                                            (ns16 + 16383) / 16384 + 1);
-      hipLaunchKernelGGL(k_pair_gram_mask16, dim3((unsigned)bw, (unsigned)k16), dim3(256), 0, s,
-                         (const unsigned long long*)bm, Wp, F, ntw, out);
-    } else if (fp4 == 4)
+    if (fp4 == 4)
       hipLaunchKernelGGL(k_pair_gram_mask8, dim3((unsigned)bw, (unsigned)ksw), dim3(512), 0, s,
                          (const unsigned long long*)bm, Wp, F, ntw, bw, out);
     else if (fp4 == 3)

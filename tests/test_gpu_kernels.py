@@ -52,7 +52,6 @@ _GRAM_ENV = {
     "wide": {"KMLS_GRAM_FP4": "0", "KMLS_GRAM_TILE": "256"},        # wide tiles, i8
     "widefp4": {"KMLS_GRAM_FP4": "1", "KMLS_GRAM_TILE": "256"},     # wide tiles, FP4 LUT unpack
     "mask8": {"KMLS_GRAM_FP4": "mask8"},                            # masked FP4, 2 waves / SIMD
-    "mask16": {"KMLS_GRAM_FP4": "mask16"},                          # masked FP4, 16-word stripes
 }
 
 
@@ -97,7 +96,7 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     np.testing.assert_array_equal(pc.reshape(max(F, 1), Wp).sum(1)[:F], counts)
 
 
-@pytest.mark.parametrize("fp4", ["1", "direct", "wide", "mask", "mask8", "mask16"])
+@pytest.mark.parametrize("fp4", ["1", "direct", "wide", "mask", "mask8"])
 def test_pair_gram_fp4_exact_past_2_24_transactions(gpu_mod, fp4, monkeypatch):
     """FP4 operands accumulate in f32, exact only below 2^24 per block: with more transactions
     than that the split-K must keep every block's slice under it.  Checked against the popcount
