@@ -425,7 +425,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_lookup_build(const int32_t* _
 }
 
 template <int kEncodeU>
-__global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restrict__ tx_ptr,
+__global__ __launch_bounds__(1024) void k_encode_tile(const int64_t* __restrict__ tx_ptr,
                                                         const int32_t* __restrict__ items,
                                                         int64_t n_tx,
                                                         const int32_t* __restrict__ rank_of,
@@ -583,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_tile(const int64_t* __restric
 // OR their nonzero words into the words the first chunk stored.
 constexpr int kMbCap = 8192;
 constexpr int kMbBand = 1024;
-__global__ __launch_bounds__(kBlock) void k_encode_multiband(const int64_t* __restrict__ tx_ptr,
+__global__ __launch_bounds__(1024) void k_encode_multiband(const int64_t* __restrict__ tx_ptr,
                                                              const int32_t* __restrict__ items,
                                                              int64_t n_tx,
                                                              const int32_t* __restrict__ rank_of,
@@ -1008,6 +1008,17 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
   KMLS_HIP(hipGetLastError());
 }
 
+// Encode block size: the tile kernels are LDS-bound to a few blocks per CU (37 KB slab + maps
+// per block; 66 KB for the multi-band kernel) at 40 VGPRs, so more waves per block are more
+// waves per CU on the same LDS (KMLS_ENCODE_BLOCK = 256 / 512 / 1024 overrides, A/B)
+static unsigned encode_block(unsigned dflt) {
+  if (const char* e = std::getenv("KMLS_ENCODE_BLOCK")) {
+    const int v = std::atoi(e);
+    if (v == 256 || v == 512 || v == 1024) return (unsigned)v;
+  }
+  return dflt;
+}
+
 int encode_lookup_shift(int64_t n_items) {
   int sh = 0;
   while ((std::max<int64_t>(n_items, 1) - 1) >> sh >= kEncodeLookupMaskBits) ++sh;
@@ -1038,8 +1049,8 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
   if (F > 1536 && F < (1 << 24) && !(mb && mb[0] == '0')) {
     const int64_t tiles = (n_tx + 255) / 256;
     if (tiles > INT32_MAX) return false;
-    hipLaunchKernelGGL(k_encode_multiband, dim3((unsigned)tiles), dim3(kBlock), 0, s, tx_ptr, items,
-                       n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, fmask);
+    hipLaunchKernelGGL(k_encode_multiband, dim3((unsigned)tiles), dim3(encode_block(1024)), 0, s,
+                       tx_ptr, items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, fmask);
     KMLS_HIP(hipGetLastError());
     return true;
   }
@@ -1068,12 +1079,13 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
   if (blocks > INT32_MAX) return false;
   // items per thread per round (KMLS_ENCODE_U=16: twice the gathers in flight, A/B)
   const char* ue = std::getenv("KMLS_ENCODE_U");
+  const unsigned eb = encode_block(512);
   if (ue && std::atoi(ue) == 16)
-    hipLaunchKernelGGL(k_encode_tile<16>, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr,
+    hipLaunchKernelGGL(k_encode_tile<16>, dim3((unsigned)blocks), dim3(eb), lds, s, tx_ptr,
                        items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2,
                        (int)band, fmask, xcd, fgroup, c2r, txmap_cap, lk_mask, lk_hash, lk_shift);
   else
-    hipLaunchKernelGGL(k_encode_tile<8>, dim3((unsigned)blocks), dim3(kBlock), lds, s, tx_ptr,
+    hipLaunchKernelGGL(k_encode_tile<8>, dim3((unsigned)blocks), dim3(eb), lds, s, tx_ptr,
                        items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2,
                        (int)band, fmask, xcd, fgroup, c2r, txmap_cap, lk_mask, lk_hash, lk_shift);
   KMLS_HIP(hipGetLastError());
