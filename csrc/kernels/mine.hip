@@ -150,7 +150,8 @@ __global__ __launch_bounds__(kBlock) void k_item_support_hash(const int32_t* __r
 constexpr int kPartBits = 15;
 constexpr int kPartBins = 1 << kPartBits;
 constexpr int kPartMax = 64;     // partitions: n_items <= 2M
-constexpr int kPartGrid = 1024;  // blocks of passes 1 and 2
+constexpr int kPartGrid = 1024;  // blocks of passes 1 and 2 (KMLS_SUPPORT_GRID: up to kPartGridMax)
+constexpr int kPartGridMax = 2048;
 constexpr int kPartTile = 4096;  // items per LDS counting-sort tile (16 per thread)
 
 __device__ __forceinline__ void part_chunk(int64_t nnz, int64_t* b0, int64_t* b1) {
@@ -1115,7 +1116,7 @@ void add_u32(uint32_t* dst, const uint32_t* src, int64_t n, hipStream_t s) {
 size_t support_scratch_bytes(int64_t nnz, int64_t n_items) {
   const int64_t P = (n_items + kPartBins - 1) / kPartBins;
   if (P > kPartMax || n_items <= 16384) return 0;
-  const int64_t n = P * kPartGrid;
+  const int64_t n = P * kPartGridMax;
   return ((size_t)nnz * 2 + 255) / 256 * 256 + (size_t)(n + 1) * 8 * 2 + scan_temp_bytes(n) + 256;
 }
 
@@ -1123,7 +1124,12 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
                               void* scratch, size_t scratch_bytes, hipStream_t s) {
   const int64_t P = ((int64_t)n_items + kPartBins - 1) / kPartBins;
   if (nnz <= 0 || P > kPartMax || scratch_bytes < support_scratch_bytes(nnz, n_items)) return false;
-  const int64_t n = P * kPartGrid;
+  // blocks of passes 1-2: 1024 = 4 resident blocks per CU (the scatter's 93 VGPRs allow 5);
+  // KMLS_SUPPORT_GRID overrides (A/B)
+  int64_t G = kPartGrid;
+  if (const char* ge = std::getenv("KMLS_SUPPORT_GRID"))
+    G = std::max<int64_t>(64, std::min<int64_t>(kPartGridMax, std::atoll(ge)));
+  const int64_t n = P * G;
   char* q = (char*)scratch;
   uint16_t* part = (uint16_t*)q;
   q += ((size_t)nnz * 2 + 255) / 256 * 256;
@@ -1132,9 +1138,9 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
   int64_t* off = (int64_t*)q;
   q += (size_t)(n + 1) * 8;
   const size_t tb = scan_temp_bytes(n);
-  hipLaunchKernelGGL(k_part_hist, dim3(kPartGrid), dim3(kBlock), 0, s, items, nnz, (int)P, blk);
+  hipLaunchKernelGGL(k_part_hist, dim3((unsigned)G), dim3(kBlock), 0, s, items, nnz, (int)P, blk);
   exclusive_scan_i64(blk, off, n, q, tb, s);
-  hipLaunchKernelGGL(k_part_scatter, dim3(kPartGrid), dim3(kBlock), 0, s, items, nnz, (int)P, off,
+  hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)G), dim3(kBlock), 0, s, items, nnz, (int)P, off,
                      part);
   // pass 3: equal global slices (default) or KMLS_SUPPORT_COUNT=part, M blocks per partition
   // (A/B; 8.79 vs 8.70 ms support at 100M x 1M)
@@ -1142,11 +1148,11 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
   if (ce && std::string(ce) == "part") {
     const int M = (int)std::max<int64_t>(1, (512 + P - 1) / P);
     hipLaunchKernelGGL(k_part_count, dim3((unsigned)(P * M)), dim3(1024), 0, s, part, off,
-                       kPartGrid, M, (int64_t)n_items, counts);
+                       (int)G, M, (int64_t)n_items, counts);
   } else {
     // one 128 KB-LDS block per CU: 512 equal slices = 2 rounds over the 256 CUs
     const unsigned B = (unsigned)std::min<int64_t>(512, std::max<int64_t>(1, nnz / 65536));
-    hipLaunchKernelGGL(k_part_count_bal, dim3(B), dim3(1024), 0, s, part, off, kPartGrid, (int)P,
+    hipLaunchKernelGGL(k_part_count_bal, dim3(B), dim3(1024), 0, s, part, off, (int)G, (int)P,
                        (int64_t)n_items, counts);
   }
   KMLS_HIP(hipGetLastError());
