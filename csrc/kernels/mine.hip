@@ -1009,9 +1009,10 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
   KMLS_HIP(hipGetLastError());
 }
 
-// Encode block size: the tile kernels are LDS-bound to a few blocks per CU (37 KB slab + maps
-// per block; 66 KB for the multi-band kernel) at 40 VGPRs, so more waves per block are more
-// waves per CU on the same LDS (KMLS_ENCODE_BLOCK = 256 / 512 / 1024 overrides, A/B)
+// Encode block size: the tile kernel is LDS-bound to 4 blocks per CU (37 KB slab + maps per
+// block) at 40 VGPRs, so more waves per block are more waves per CU on the same LDS: 512
+// threads measured 12.3 ms at 100M against 13.1 (256) and 15.9 (1024).  The multi-band kernel
+// stays at 256 (12.4 ms at config-5 10M vs 13.2 at 1024).  KMLS_ENCODE_BLOCK overrides (A/B)
 static unsigned encode_block(unsigned dflt) {
   if (const char* e = std::getenv("KMLS_ENCODE_BLOCK")) {
     const int v = std::atoi(e);
@@ -1050,7 +1051,7 @@ bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_
   if (F > 1536 && F < (1 << 24) && !(mb && mb[0] == '0')) {
     const int64_t tiles = (n_tx + 255) / 256;
     if (tiles > INT32_MAX) return false;
-    hipLaunchKernelGGL(k_encode_multiband, dim3((unsigned)tiles), dim3(encode_block(1024)), 0, s,
+    hipLaunchKernelGGL(k_encode_multiband, dim3((unsigned)tiles), dim3(encode_block(256)), 0, s,
                        tx_ptr, items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, fmask);
     KMLS_HIP(hipGetLastError());
     return true;
@@ -1125,7 +1126,8 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
   const int64_t P = ((int64_t)n_items + kPartBins - 1) / kPartBins;
   if (nnz <= 0 || P > kPartMax || scratch_bytes < support_scratch_bytes(nnz, n_items)) return false;
   // blocks of passes 1-2: 1024 = 4 resident blocks per CU (the scatter's 93 VGPRs allow 5);
-  // KMLS_SUPPORT_GRID overrides (A/B)
+  // 1280 / 2048 measured no faster (support 8.73 / 8.62 vs 8.37 ms at 100M). KMLS_SUPPORT_GRID
+  // overrides (A/B)
   int64_t G = kPartGrid;
   if (const char* ge = std::getenv("KMLS_SUPPORT_GRID"))
     G = std::max<int64_t>(64, std::min<int64_t>(kPartGridMax, std::atoll(ge)));
