@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-2 s10: mask16 gram + one-tile support A/B at 100M / config 5, then the full GPU suite,
 # smoke() and the driver's bench line on this tree.
-source "$(dirname "$0")/gpu_round.sh"
+source "$(dirname "$0")/../gpu_round.sh"
 export PYTHONUNBUFFERED=1
 L100="python3 -m kubernetes_machine_learning_server_amd.bench.bench_large --shape 100Mx1M --steps 3 --warmup 1 --mfma"
 step l100_default 600 $L100

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-2 s2: support/encode kernel tests, 100M support with the scatter prefetch, a 100M
 # kernel trace, serve 10k QPS with more client processes / workers.
-source "$(dirname "$0")/gpu_round.sh"
+source "$(dirname "$0")/../gpu_round.sh"
 export PYTHONUNBUFFERED=1
 step pytest_sup 600 python -u -m pytest tests/test_gpu_kernels.py -q -x --timeout 300 --timeout-method thread -k "support or encode"
 L100="python3 -m kubernetes_machine_learning_server_amd.bench.bench_large --shape 100Mx1M --steps 3 --warmup 1 --mfma"

@@ -1,10 +1,10 @@
 #!/usr/bin/env bash
-# Round-2 s3: encode LDS lookup tables (tests + 100M A/B vs the group gather), 100M kernel trace.
-source "$(dirname "$0")/gpu_round.sh"
+# Round-2 s5: 14-bit support partitions (support tests, 100M timing), bench default line.
+source "$(dirname "$0")/../gpu_round.sh"
 export PYTHONUNBUFFERED=1
-step pytest_enc 600 python -u -m pytest tests/test_gpu_kernels.py -q -x --timeout 300 --timeout-method thread -k "support or encode"
+step pytest_sup 600 python -u -m pytest tests/test_gpu_kernels.py -q -x --timeout 300 --timeout-method thread -k "support"
 L100="python3 -m kubernetes_machine_learning_server_amd.bench.bench_large --shape 100Mx1M --steps 3 --warmup 1 --mfma"
-step l100_lookup 600 $L100
-KMLS_ENCODE_LOOKUP=group step l100_group 600 $L100
+step l100_p14 600 $L100
 step ktrace100 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/kt100 -o run -- python3 -m kubernetes_machine_learning_server_amd.bench.bench_large --shape 100Mx1M --steps 2 --warmup 1 --mfma
 f=$(find /tmp/kt100 -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp "$f" gpurun_out/kt100_kernel_stats.csv; rm -rf /tmp/kt100
+step bench 600 python -u bench.py --gpus 1 --steps 20 --warmup 5

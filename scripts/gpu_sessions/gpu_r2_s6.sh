@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Round-2 s6: encode A/B at 100M: items per thread (8 / 16), tile width (TW 2 / 4 / 8).
-source "$(dirname "$0")/gpu_round.sh"
+source "$(dirname "$0")/../gpu_round.sh"
 export PYTHONUNBUFFERED=1
 step pytest_enc 600 python -u -m pytest tests/test_gpu_kernels.py -q -x --timeout 300 --timeout-method thread -k "encode"
 L100="python3 -m kubernetes_machine_learning_server_amd.bench.bench_large --shape 100Mx1M --steps 3 --warmup 1 --mfma"

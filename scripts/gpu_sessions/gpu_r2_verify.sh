@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-2 re-entry check of HEAD: full GPU suite, smoke(), the driver's default bench line, the
 # weak-scaled N-rank bench rehearsed at 2 ranks on one GPU (gloo bracket), encode tx-map A/B.
-source "$(dirname "$0")/gpu_round.sh"
+source "$(dirname "$0")/../gpu_round.sh"
 export PYTHONUNBUFFERED=1
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
