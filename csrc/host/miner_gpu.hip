@@ -689,22 +689,45 @@ float elapsed(const Event& a, const Event& b) {
 
 // ------------------------------------------------------------------------------------------
 // The captured launch sequence of the last steady-state resident call (see mine_resident).
+// Two executable instances of the captured call: consecutive launches alternate between them,
+// so a call launched ahead (prefetch) is never a relaunch of the exec that is still running
+// (KMLS_GRAPH_TWIN=0: one instance, A/B).
 struct GraphCache {
   std::vector<uint64_t> key;
   hipGraphExec_t exec = nullptr;
+  hipGraphExec_t twin = nullptr;
+  unsigned flip = 0;
   int last = 0;             // last level the graph enqueues
   unsigned launch_idx = 0;  // look-back launch indices the graph consumes
-  void reset(hipGraphExec_t e, std::vector<uint64_t> k, int l, unsigned li) {
+  void reset(hipGraphExec_t e, std::vector<uint64_t> k, int l, unsigned li,
+             hipGraphExec_t t = nullptr) {
     if (exec) (void)hipGraphExecDestroy(exec);
+    if (twin) (void)hipGraphExecDestroy(twin);
     exec = e;
+    twin = t;
+    flip = 0;
     key = std::move(k);
     last = l;
     launch_idx = li;
   }
+  hipGraphExec_t next() {  // the instance for the next launch
+    const hipGraphExec_t x = (twin && (flip & 1u)) ? twin : exec;
+    ++flip;
+    return x;
+  }
   ~GraphCache() {
     if (exec) (void)hipGraphExecDestroy(exec);
+    if (twin) (void)hipGraphExecDestroy(twin);
   }
 };
+
+static bool graph_twin_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("KMLS_GRAPH_TWIN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // A steady-state resident call launched ahead (mine(prefetch=true)): its graph replay is on the
 // stream behind the call that launched it, writing to its own pinned buffers.  The next
@@ -1524,6 +1547,15 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     KMLS_HIP(hipStreamCreateWithFlags((hipStream_t*)&idx_s_, hipStreamNonBlocking));
     for (auto& e : idx_ev_) KMLS_HIP(hipEventCreateWithFlags((hipEvent_t*)&e, hipEventDisableTiming));
   }
+  // Node order of the captured graph: the rule-map branch depends only on the gram, but with its
+  // nodes created before the levels' the level branch started ~44 µs after the gram (the
+  // profiled step timeline, profiles/r2_s12_ds1_step_timeline.md); creating them last lets the
+  // root level start right behind the gram (KMLS_RULEMAP_LATE=0: the old order, A/B)
+  static const bool rulemap_late = [] {
+    const char* e = std::getenv("KMLS_RULEMAP_LATE");
+    return !(e && e[0] == '0');
+  }();
+  bool pairs_pending = false;
   auto enqueue_prologue = [&]() {
     kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl,
                               call_params_, d_call_seq_, s);
@@ -1540,8 +1572,12 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
       if (fork_idx) {  // captured: the rule map runs on a side branch of the graph, beside the levels
         KMLS_HIP(hipEventRecord((hipEvent_t)idx_ev_[0], s));
         KMLS_HIP(hipStreamWaitEvent((hipStream_t)idx_s_, (hipEvent_t)idx_ev_[0], 0));
-        kern::pairs_to_csr(pa, (hipStream_t)idx_s_);
-        KMLS_HIP(hipEventRecord((hipEvent_t)idx_ev_[1], (hipStream_t)idx_s_));
+        if (rulemap_late) {
+          pairs_pending = true;  // its nodes are created after the levels' (end_capture)
+        } else {
+          kern::pairs_to_csr(pa, (hipStream_t)idx_s_);
+          KMLS_HIP(hipEventRecord((hipEvent_t)idx_ev_[1], (hipStream_t)idx_s_));
+        }
       } else {
         kern::pairs_to_csr(pa, s);
       }
@@ -1588,7 +1624,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     run.graph_replay = true;
     run.graph_last = graph_->last;
     out_->launch_idx = graph_->launch_idx;  // later (non-graph) launches of this call continue
-    KMLS_HIP(hipGraphLaunch(graph_->exec, s));
+    KMLS_HIP(hipGraphLaunch(graph_->next(), s));
     ++call_seq_;
   } else if (use_graph) {
     KMLS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
@@ -1601,16 +1637,24 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     }
     run.graph_capture = true;
     run.end_capture = [&](int last) {
+      if (pairs_pending) {  // the rule-map branch, created after the levels' nodes
+        kern::pairs_to_csr(pa, (hipStream_t)idx_s_);
+        KMLS_HIP(hipEventRecord((hipEvent_t)idx_ev_[1], (hipStream_t)idx_s_));
+        pairs_pending = false;
+      }
       if (fork_idx) KMLS_HIP(hipStreamWaitEvent(s, (hipEvent_t)idx_ev_[1], 0));  // join
       hipGraph_t g = nullptr;
       KMLS_HIP(hipStreamEndCapture(s, &g));
-      hipGraphExec_t ex = nullptr;
+      hipGraphExec_t ex = nullptr, tw = nullptr;
       const hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+      if (ie == hipSuccess && graph_twin_enabled() &&
+          hipGraphInstantiate(&tw, g, nullptr, nullptr, 0) != hipSuccess)
+        tw = nullptr;
       (void)hipGraphDestroy(g);
       KMLS_HIP(ie);
       if (!graph_) graph_ = std::make_unique<GraphCache>();
-      graph_->reset(ex, key, last, out_->launch_idx);
-      KMLS_HIP(hipGraphLaunch(ex, s));
+      graph_->reset(ex, key, last, out_->launch_idx, tw);
+      KMLS_HIP(hipGraphLaunch(graph_->next(), s));
     };
   } else {
     enqueue_prologue();
@@ -1647,7 +1691,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     p->i_meta = ih2.meta;
     KMLS_HIP(hipEventRecord(ev_cur.e, s));
     fill_params(call_params_[call_seq_ & 1], ht2, p->fstage.get(), p->back.get(), ih2);
-    KMLS_HIP(hipGraphLaunch(graph_->exec, s));
+    KMLS_HIP(hipGraphLaunch(graph_->next(), s));
     ++call_seq_;
     out_->launch_idx = graph_->launch_idx;
     p->t_launch = std::chrono::steady_clock::now();

@@ -1,0 +1,14 @@
+#!/usr/bin/env bash
+# Round-2 s13: twin graph executables for launched-ahead calls (graph/prefetch tests, bench A/B,
+# timeline with the twin).
+source "$(dirname "$0")/../gpu_round.sh"
+export PYTHONUNBUFFERED=1
+step pytest_graph 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_e2e.py -q -x --timeout 300 --timeout-method thread -k "graph or prefetch or replay or resident"
+B="python3 bench.py --steps 50 --warmup 5 --no-config2 --no-config3 --serve-qps "
+step bench_twin 300 $B ""
+KMLS_GRAPH_TWIN=0 step bench_single 300 $B ""
+step bench_twin2 300 $B ""
+step trace_twin 300 rocprofv3 --kernel-trace -d /tmp/prof_k -o run -- python3 bench.py --steps 30 --warmup 3 --no-verify --no-config2 --no-config3 --serve-qps ""
+python3 scripts/rocpd_timeline.py /tmp/prof_k/run_results.db > gpurun_out/ktrace_timeline_s13.md 2>&1
+cp /tmp/prof_k/run_results.db gpurun_out/tb13_results.db 2>/dev/null
+rm -rf /tmp/prof_k
