@@ -691,7 +691,7 @@ float elapsed(const Event& a, const Event& b) {
 // The captured launch sequence of the last steady-state resident call (see mine_resident).
 // Two executable instances of the captured call: consecutive launches alternate between them,
 // so a call launched ahead (prefetch) is never a relaunch of the exec that is still running
-// (KMLS_GRAPH_TWIN=0: one instance, A/B).
+// (KMLS_GRAPH_TWIN=1; off by default until measured on the GPU).
 struct GraphCache {
   std::vector<uint64_t> key;
   hipGraphExec_t exec = nullptr;
@@ -724,7 +724,7 @@ struct GraphCache {
 static bool graph_twin_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("KMLS_GRAPH_TWIN");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
@@ -1550,10 +1550,10 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   // Node order of the captured graph: the rule-map branch depends only on the gram, but with its
   // nodes created before the levels' the level branch started ~44 µs after the gram (the
   // profiled step timeline, profiles/r2_s12_ds1_step_timeline.md); creating them last lets the
-  // root level start right behind the gram (KMLS_RULEMAP_LATE=0: the old order, A/B)
+  // root level start right behind the gram (KMLS_RULEMAP_LATE=1; off by default until measured)
   static const bool rulemap_late = [] {
     const char* e = std::getenv("KMLS_RULEMAP_LATE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   bool pairs_pending = false;
   auto enqueue_prologue = [&]() {
