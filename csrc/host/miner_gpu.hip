@@ -1550,10 +1550,11 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   // Node order of the captured graph: the rule-map branch depends only on the gram, but with its
   // nodes created before the levels' the level branch started ~44 µs after the gram (the
   // profiled step timeline, profiles/r2_s12_ds1_step_timeline.md); creating them last lets the
-  // root level start right behind the gram (KMLS_RULEMAP_LATE=1; off by default until measured)
+  // root level start right behind the gram: 0.2566 -> 0.2485 ms/step (medians of 4 interleaved
+  // runs, profiles/r2_s15_graph_interleaved.log).  KMLS_RULEMAP_LATE=0: the old order (A/B)
   static const bool rulemap_late = [] {
     const char* e = std::getenv("KMLS_RULEMAP_LATE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   bool pairs_pending = false;
   auto enqueue_prologue = [&]() {
