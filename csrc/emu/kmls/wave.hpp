@@ -1,0 +1,23 @@
+// Emulator version of kmls/wave.hpp (csrc/emu/hip/hip_runtime.h): same helpers, no inline asm.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace kmls {
+namespace kern {
+
+inline unsigned vzero() { return 0u; }
+
+inline unsigned long long bcast64(unsigned long long v, int src) {
+  return emu::xchg(v, src);
+}
+inline unsigned long long shfl_xor64(unsigned long long v, int m) {
+  return emu::xchg(v, emu::tl->lane ^ m);
+}
+inline unsigned uni(unsigned v) { return (unsigned)__builtin_amdgcn_readfirstlane((int)v); }
+inline unsigned long long uni64(unsigned long long v) {
+  return ((unsigned long long)uni((unsigned)(v >> 32)) << 32) | uni((unsigned)v);
+}
+
+}  // namespace kern
+}  // namespace kmls

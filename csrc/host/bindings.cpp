@@ -162,6 +162,10 @@ PYBIND11_MODULE(_native, m) {
     s["n_frequent_items"] = r.n_frequent_items; s["n_itemsets"] = r.n_itemsets;
     s["max_depth"] = r.max_depth; s["capped"] = r.capped; s["seconds"] = r.seconds;
     s["per_level"] = r.per_level;
+    char buf[64];
+    std::snprintf(buf, sizeof buf, "%016llx%016llx", (unsigned long long)r.digest_sum,
+                  (unsigned long long)r.digest_xor);
+    s["digest"] = std::string(buf);
     return s;
   }, py::arg("tx_ptr"), py::arg("items"), py::arg("n_items"), py::arg("min_support"),
      py::arg("max_len") = 0, py::arg("cap") = (int64_t)1 << 62, py::arg("threads") = 0);

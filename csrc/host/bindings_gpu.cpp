@@ -273,6 +273,46 @@ void register_gpu_bindings(py::module_& m) {
         return result_to_dict(std::move(r));
       }, py::arg("comm"), py::arg("global_n_tx"), py::arg("min_support"), py::arg("max_len") = 0,
          py::arg("download") = true, py::arg("mfma") = false, py::arg("support_tiles") = 4)
+      .def("mine_deep", [](gpu::GpuMiner& g, double ms, int max_len, int rank, int world,
+                           py::object comm, unsigned long long budget0, unsigned long long budget,
+                           unsigned split_min, int blocks_per_cu, int stack_mb) {
+        gpu::DeepOpts o;
+        o.budget0 = budget0;
+        o.budget = budget;
+        o.split_min = split_min;
+        o.blocks_per_cu = blocks_per_cu;
+        o.stack_mb = stack_mb;
+        gpu::Comm* c = comm.is_none() ? nullptr : comm.cast<gpu::Comm*>();
+        gpu::DeepResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = g.mine_deep(ms, max_len, rank, world, c, o);
+        }
+        py::dict d;
+        d["per_level"] = r.per_level;
+        d["n_itemsets"] = r.n_itemsets;
+        d["n_frequent_items"] = r.n_frequent_items;
+        d["max_depth"] = r.max_depth;
+        d["candidates"] = r.candidates;
+        d["chunks"] = r.chunks;
+        d["level2_tasks"] = r.level2_tasks;
+        char buf[64];
+        std::snprintf(buf, sizeof buf, "%016llx%016llx", (unsigned long long)r.digest_sum,
+                      (unsigned long long)r.digest_xor);
+        d["digest"] = std::string(buf);
+        d["round_tasks"] = r.round_tasks;
+        d["round_ms"] = r.round_ms;
+        py::dict ph;
+        ph["prologue"] = r.ms_prologue;
+        ph["level2_classes"] = r.ms_root;
+        ph["rounds"] = r.ms_rounds;
+        ph["combine"] = r.ms_combine;
+        ph["total"] = r.ms_total;
+        d["phases_ms"] = ph;
+        return d;
+      }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("rank") = 0, py::arg("world") = 1,
+         py::arg("comm") = py::none(), py::arg("budget0") = 4096ull, py::arg("budget") = 4096ull,
+         py::arg("split_min") = 4u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0)
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
   py::class_<gpu::GpuRuleIndex>(m, "GpuRuleIndex")

@@ -1,0 +1,150 @@
+// Host driver of the count-only deep miner (kernels/deep.hip): full FP-Growth output size and
+// content digest at supports whose itemsets cannot be materialised (BASELINE config 2: ds1 at
+// 0.01-0.02, 1e9-1e10 itemsets; the reference mines all sizes, machine-learning/main.py:272, and
+// sweeps min_support downwards, main.py:450-473).
+//
+// Call sequence (one rank = one GPU; every rank runs the same prologue on the full data):
+//   supports -> selection -> bitmaps [F][Wp] -> transposed root block ->
+//   level-2 classes (deterministic: count pass, host scan, fill pass) -> this rank's share of the
+//   level-3 tasks (task t = (root i, member k) goes to rank t % world) ->
+//   rounds of k_deep_count (ticket dequeue, per-task step budget, spills become the next round's
+//   tasks) until no task is left -> per-size counts + digest, all-reduced over the ranks.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "deep_run.hpp"
+#include "kmls/digest.hpp"
+#include "kmls/gpu.hpp"
+
+#define KMLS_HIP(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +      \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__));     \
+  } while (0)
+
+namespace kmls {
+namespace gpu {
+
+DeepResult GpuMiner::mine_deep(double min_support, int max_len, int rank, int world, Comm* comm,
+                               const DeepOpts& opt) {
+  drain_prefetch();
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  KMLS_CHECK(world >= 1 && rank >= 0 && rank < world, "mine_deep: bad rank/world");
+  KMLS_CHECK(comm == nullptr || comm->world() == world, "mine_deep: comm world differs");
+  const int W_real = (int)((n_tx_ + 63) / 64);
+  KMLS_CHECK(W_real <= kern::deep_max_words(),
+             "mine_deep: transactions longer than 4096 (use the level-wise tx-DP miner)");
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(now() - t).count();
+  };
+  DeepResult res;
+  const auto t0 = now();
+
+  // ---- prologue: supports, selection, bitmaps ----
+  const size_t mark = arena_->mark();
+  uint32_t* d_cnt = (uint32_t*)arena_->push((size_t)std::max<int64_t>(n_items_, 1) * 4);
+  item_support((uintptr_t)d_cnt);
+  std::vector<uint32_t> cnt((size_t)n_items_);
+  KMLS_HIP(hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * 4, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  arena_->pop_to(mark);
+  const int64_t F = select(cnt.data(), n_tx_, min_support);
+  const int64_t Wp = words_local();
+  const size_t need_bm = (size_t)std::max<int64_t>(F, 1) * Wp * 8;
+  if (need_bm > own_bm_bytes_) {
+    if (d_own_bm_) KMLS_HIP(hipFree(d_own_bm_));
+    KMLS_HIP(hipMalloc((void**)&d_own_bm_, need_bm));
+    own_bm_bytes_ = need_bm;
+  }
+  if (F) encode_bitmaps_fresh(d_own_bm_, F, Wp);
+  const uint32_t minsup = fi_.minsup2;
+  res.n_frequent_items = F;
+  std::vector<uint64_t> per(64, 0);
+  uint64_t dsum = 0, dxor = 0;
+  if (rank == 0) {  // level 1 (every rank holds it; rank 0 counts it)
+    per[1] = (uint64_t)F;
+    for (int64_t r = 0; r < F; ++r) {
+      const DigestTerms t = digest_terms(item_mix((uint64_t)fi_.ids[(size_t)r]), fi_.counts[(size_t)r]);
+      dsum += t.sum;
+      dxor ^= t.xr;
+    }
+  }
+  if (!deep_) deep_.reset(new DeepBufs());
+  deep_->device = device_;
+  DeepInput in;
+  in.bm = d_own_bm_;
+  in.Wp = Wp;
+  in.F = F;
+  in.W_real = W_real;
+  in.d_ids = d_ids_;
+  in.minsup = minsup;
+  in.max_len = max_len;
+  in.n_cus = n_cus_;
+  in.stream = s;
+  res.ms_prologue = ms_since(t0);
+  DeepLocal loc = deep_run(*deep_, in, rank, world, opt);
+  DeepBufs& b = *deep_;
+  for (int d = 2; d < 64; ++d) per[(size_t)d] += loc.per_depth[(size_t)d];
+  dsum += loc.dsum;
+  dxor ^= loc.dxor;
+  uint64_t cands = loc.candidates;
+  res.chunks = (int64_t)loc.chunks;
+  res.level2_tasks = loc.level2_tasks;
+  res.round_tasks = loc.round_tasks;
+  res.round_ms = loc.round_ms;
+  res.ms_root = loc.ms_root;
+  res.ms_rounds = loc.ms_rounds;
+  if (b.xor_cap < world) {
+    if (b.d_xor) KMLS_HIP(hipFree(b.d_xor));
+    KMLS_HIP(hipMalloc((void**)&b.d_xor, (size_t)world * 8));
+    b.xor_cap = world;
+  }
+
+  // ---- combine over ranks (RCCL or the host communicator, stream-ordered) ----
+  const auto t3 = now();
+  if (comm && world > 1) {
+    std::vector<uint64_t> red(66);
+    std::copy(per.begin(), per.end(), red.begin());
+    red[64] = dsum;
+    red[65] = cands;
+    KMLS_HIP(hipMemcpyAsync(b.d_red, red.data(), 66 * 8, hipMemcpyHostToDevice, s));
+    KMLS_HIP(hipMemcpyAsync(b.d_xor + rank, &dxor, 8, hipMemcpyHostToDevice, s));
+    comm->all_reduce(b.d_red, b.d_red, 66, CommDtype::U64, false, s);
+    comm->all_gather(b.d_xor + rank, b.d_xor, 1, CommDtype::U64, s);
+    std::vector<uint64_t> xs((size_t)world);
+    KMLS_HIP(hipMemcpyAsync(red.data(), b.d_red, 66 * 8, hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipMemcpyAsync(xs.data(), b.d_xor, (size_t)world * 8, hipMemcpyDeviceToHost, s));
+    comm->wait_stream(s);
+    std::copy(red.begin(), red.begin() + 64, per.begin());
+    dsum = red[64];
+    cands = red[65];
+    dxor = 0;
+    for (uint64_t x : xs) dxor ^= x;
+  }
+  res.ms_combine = ms_since(t3);
+  res.per_level.assign(per.begin(), per.end());
+  while (res.per_level.size() > 2 && res.per_level.back() == 0) res.per_level.pop_back();
+  res.n_itemsets = 0;
+  for (size_t d = 1; d < res.per_level.size(); ++d) res.n_itemsets += (int64_t)res.per_level[d];
+  res.max_depth = 0;
+  for (size_t d = 1; d < res.per_level.size(); ++d)
+    if (res.per_level[d]) res.max_depth = (int)d;
+  res.digest_sum = dsum;
+  res.digest_xor = dxor;
+  res.candidates = (int64_t)cands;
+  res.ms_total = ms_since(t0);
+  return res;
+}
+
+}  // namespace gpu
+}  // namespace kmls

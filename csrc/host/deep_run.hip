@@ -1,0 +1,229 @@
+// Device orchestration of the count-only deep miner (see deep_run.hpp and kernels/deep.hip).
+#include "deep_run.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
+#define KMLS_HIP(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +      \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__));     \
+  } while (0)
+
+namespace kmls {
+namespace gpu {
+
+DeepBufs::~DeepBufs() {
+  (void)hipSetDevice(device);
+  for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)heap[0],
+                  (void*)heap[1], (void*)root, (void*)ctl, (void*)d_red, (void*)d_xor,
+                  (void*)d_m, (void*)d_off, (void*)d_toff})
+    if (p) (void)hipFree(p);
+  if (h_ctl) (void)hipHostFree(h_ctl);
+}
+
+void DeepBufsDeleter::operator()(DeepBufs* p) const { delete p; }
+
+namespace {
+
+size_t env_bytes_mb(const char* name, size_t dflt_mb) {
+  if (const char* e = std::getenv(name)) {
+    const double v = std::atof(e);
+    if (v > 0) return (size_t)(v * (double)(1ull << 20));
+  }
+  return dflt_mb << 20;
+}
+
+template <typename T>
+void grow(T*& p, int64_t& cap_elems, int64_t need) {
+  if (cap_elems >= need && p) return;
+  if (p) KMLS_HIP(hipFree(p));
+  p = nullptr;
+  KMLS_HIP(hipMalloc((void**)&p, (size_t)std::max<int64_t>(need, 1) * sizeof(T)));
+  cap_elems = need;
+}
+
+}  // namespace
+
+DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const DeepOpts& opt) {
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(now() - t).count();
+  };
+  hipStream_t s = in.stream;
+  const int64_t F = in.F;
+  const int W = kern::deep_row_words(in.W_real);
+  const int64_t Fpad = (F + 15) / 16 * 16;
+  DeepLocal res;
+
+  // ---- buffers (kept across calls) ----
+  const auto t0 = now();
+  const int blocks_per_cu = opt.blocks_per_cu > 0 ? opt.blocks_per_cu : 3;
+  const int grid = std::max(1, in.n_cus * blocks_per_cu);
+  const int64_t waves = (int64_t)grid * kern::deep_waves_per_block();
+  const size_t stack_need = std::max<size_t>(
+      opt.stack_mb > 0 ? (size_t)opt.stack_mb << 20 : env_bytes_mb("KMLS_DEEP_STACK_MB", 4),
+      4 * kern::deep_row_block_bytes(W, F));
+  const int fcap = std::max(4096, kern::deep_min_fcap());
+  if (b.waves < waves || b.stack_bytes < stack_need || b.fcap < fcap) {
+    if (b.stacks) KMLS_HIP(hipFree(b.stacks));
+    if (b.fstacks) KMLS_HIP(hipFree(b.fstacks));
+    b.stacks = nullptr;
+    b.fstacks = nullptr;
+    KMLS_HIP(hipMalloc((void**)&b.stacks, (size_t)waves * stack_need));
+    KMLS_HIP(hipMalloc((void**)&b.fstacks, (size_t)waves * fcap * sizeof(kern::DeepFrame)));
+    b.waves = waves;
+    b.stack_bytes = stack_need;
+    b.fcap = fcap;
+  }
+  const int64_t q_cap = (int64_t)(env_bytes_mb("KMLS_DEEP_QUEUE_MB", 512) / sizeof(kern::DeepFrame));
+  if (b.q_cap < q_cap) {
+    for (auto& q : b.q) {
+      if (q) KMLS_HIP(hipFree(q));
+      q = nullptr;
+      KMLS_HIP(hipMalloc((void**)&q, (size_t)q_cap * sizeof(kern::DeepFrame)));
+    }
+    b.q_cap = q_cap;
+  }
+  const size_t heap_cap = env_bytes_mb("KMLS_DEEP_HEAP_MB", 4096);
+  if (b.heap_cap < heap_cap) {
+    for (auto& h : b.heap) {
+      if (h) KMLS_HIP(hipFree(h));
+      h = nullptr;
+      KMLS_HIP(hipMalloc((void**)&h, heap_cap));
+    }
+    b.heap_cap = heap_cap;
+  }
+  if (!b.ctl) {
+    KMLS_HIP(hipMalloc((void**)&b.ctl, sizeof(kern::DeepCtl)));
+    KMLS_HIP(hipHostMalloc((void**)&b.h_ctl, sizeof(kern::DeepCtl)));
+    KMLS_HIP(hipMalloc((void**)&b.d_red, 66 * 8));
+  }
+  if (b.f_cap < F + 1) {
+    int64_t c1 = b.f_cap, c2 = b.f_cap, c3 = b.f_cap;
+    grow(b.d_m, c1, F + 1);
+    grow(b.d_off, c2, F + 1);
+    grow(b.d_toff, c3, F + 1);
+    b.f_cap = F + 1;
+  }
+  KMLS_HIP(hipMemsetAsync(b.ctl, 0, sizeof(kern::DeepCtl), s));
+  res.ms_alloc = ms_since(t0);
+
+  // ---- level 2: root classes (deterministic on every rank) ----
+  const auto t1 = now();
+  int64_t n_tasks = 0;
+  if (F >= 2 && in.max_len != 1) {
+    const size_t root_blk = (size_t)(W + 1) * (size_t)Fpad * 8;
+    auto ensure_root = [&](size_t bytes, size_t keep) {  // keep: leading bytes to preserve
+      if (b.root_bytes >= bytes) return;
+      const size_t nb = std::max(bytes, b.root_bytes * 2);
+      char* p = nullptr;
+      KMLS_HIP(hipMalloc((void**)&p, nb));
+      if (b.root && keep) KMLS_HIP(hipMemcpyAsync(p, b.root, keep, hipMemcpyDeviceToDevice, s));
+      KMLS_HIP(hipStreamSynchronize(s));
+      if (b.root) KMLS_HIP(hipFree(b.root));
+      b.root = p;
+      b.root_bytes = nb;
+    };
+    ensure_root(root_blk, 0);
+    kern::deep_transpose(in.bm, in.Wp, F, W, in.W_real, in.d_ids, (uint64_t*)b.root, Fpad, s);
+    kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, b.d_m, nullptr, nullptr,
+                    nullptr, false, s);
+    std::vector<int32_t> m((size_t)F, 0);
+    KMLS_HIP(hipMemcpyAsync(m.data(), b.d_m, (size_t)F * 4, hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+    std::vector<int64_t> off((size_t)F + 1, 0), toff((size_t)F + 1, 0);
+    int64_t pairs = 0;
+    off[0] = (int64_t)root_blk;
+    for (int64_t i = 0; i < F; ++i) {
+      const int64_t mi = m[(size_t)i];
+      if (mi < 0 || mi > F) throw std::runtime_error("deep_run: bad level-2 class size");
+      pairs += mi;
+      off[(size_t)i + 1] = off[(size_t)i] + (int64_t)(W + 1) * ((mi + 15) / 16 * 16) * 8;
+      toff[(size_t)i + 1] = toff[(size_t)i] + std::max<int64_t>(mi - 1, 0);
+    }
+    if (rank == 0) res.per_depth[2] = (uint64_t)pairs;
+    const bool deeper = in.max_len == 0 || in.max_len >= 3;
+    ensure_root((size_t)off[(size_t)F], root_blk);
+    KMLS_HIP(hipMemcpyAsync(b.d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, s));
+    KMLS_HIP(hipMemcpyAsync(b.d_toff, toff.data(), toff.size() * 8, hipMemcpyHostToDevice, s));
+    kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, b.d_m, b.d_off, b.root,
+                    rank == 0 ? b.ctl : nullptr, true, s);
+    const int64_t T = toff[(size_t)F];
+    n_tasks = deeper ? (T - rank + world - 1) / world : 0;
+    if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
+    if (n_tasks > 0)
+      kern::deep_root_tasks(b.d_off, b.d_m, b.d_toff, F, b.root, (const uint64_t*)b.root, Fpad, W,
+                            rank, world, b.q[0], s);
+    KMLS_HIP(hipStreamSynchronize(s));  // pageable off/toff die at scope end
+    res.level2_tasks = T;
+  }
+  res.ms_root = ms_since(t1);
+
+  // ---- rounds ----
+  const auto t2 = now();
+  kern::DeepArgs a{};
+  a.stacks = b.stacks;
+  a.stack_bytes = b.stack_bytes;
+  a.fstacks = b.fstacks;
+  a.fcap = b.fcap;
+  a.ctl = b.ctl;
+  a.W = W;
+  a.minsup = in.minsup;
+  a.max_len = in.max_len;
+  a.split_min = opt.split_min;
+  a.out_cap = b.q_cap;
+  a.heap_cap = b.heap_cap;
+  {
+    int khz = 0;
+    KMLS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, b.device));
+    double secs = 120.0;
+    if (const char* e = std::getenv("KMLS_DEEP_ROUND_TIMEOUT_S")) secs = std::max(1.0, std::atof(e));
+    a.timeout_ticks = (unsigned long long)(secs * 1000.0 * (double)std::max(khz, 1));
+  }
+  int cur = 0;
+  int64_t n_in = n_tasks;
+  for (int round = 0; n_in > 0; ++round) {
+    if (round >= 4096) throw std::runtime_error("deep_run: no progress after 4096 rounds");
+    const auto tr = now();
+    KMLS_HIP(hipMemsetAsync(b.ctl, 0, 3 * sizeof(unsigned long long), s));  // ticket, n_out, heap
+    a.in = b.q[cur];
+    a.n_in = n_in;
+    a.out = b.q[cur ^ 1];
+    a.heap = b.heap[round & 1];
+    a.budget = round == 0 ? opt.budget0 : opt.budget;
+    kern::deep_count(a, (int)std::min<int64_t>(grid, (n_in + kern::deep_waves_per_block() - 1) /
+                                                         kern::deep_waves_per_block()), s);
+    KMLS_HIP(hipMemcpyAsync(b.h_ctl, b.ctl, sizeof(kern::DeepCtl), hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+    if (b.h_ctl->error & 4)
+      throw std::runtime_error("deep_run: round " + std::to_string(round) +
+                               " ran past KMLS_DEEP_ROUND_TIMEOUT_S and gave up");
+    if (b.h_ctl->error)
+      throw std::runtime_error("deep_run: round " + std::to_string(round) + " overflowed (" +
+                               ((b.h_ctl->error & 1) ? "task queue" : "spill heap") +
+                               "); raise KMLS_DEEP_QUEUE_MB / KMLS_DEEP_HEAP_MB");
+    res.round_tasks.push_back(n_in);
+    res.round_ms.push_back(ms_since(tr));
+    n_in = (int64_t)b.h_ctl->n_out;
+    cur ^= 1;
+  }
+  KMLS_HIP(hipMemcpyAsync(b.h_ctl, b.ctl, sizeof(kern::DeepCtl), hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  res.ms_rounds = ms_since(t2);
+  for (int d = 3; d < 64; ++d) res.per_depth[(size_t)d] += b.h_ctl->per_depth[d];
+  res.dsum = b.h_ctl->digest_sum;  // level-2 terms (rank 0) + the rounds
+  res.dxor = b.h_ctl->digest_xor;
+  res.candidates = b.h_ctl->candidates;
+  res.chunks = b.h_ctl->chunks;
+  return res;
+}
+
+}  // namespace gpu
+}  // namespace kmls

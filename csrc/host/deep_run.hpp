@@ -1,0 +1,67 @@
+// Device orchestration of the count-only deep miner (deep_run.hip): level-2 classes, the rank's
+// level-3 tasks, and the spill rounds of k_deep_count.  Free of GpuMiner so the CPU wave
+// emulator (csrc/emu, tests only) can drive the same code over host memory.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../kernels/kernels.hpp"
+#include "kmls/gpu.hpp"
+
+namespace kmls {
+namespace gpu {
+
+// device buffers of the deep miner, kept across calls (allocation maps HBM eagerly)
+struct DeepBufs {
+  int device = 0;
+  char* stacks = nullptr;
+  size_t stack_bytes = 0;  // per wave
+  int64_t waves = 0;
+  kern::DeepFrame* fstacks = nullptr;
+  int fcap = 0;
+  kern::DeepFrame* q[2] = {nullptr, nullptr};
+  int64_t q_cap = 0;
+  char* heap[2] = {nullptr, nullptr};
+  size_t heap_cap = 0;
+  char* root = nullptr;  // root block + level-2 blocks
+  size_t root_bytes = 0;
+  int32_t* d_m = nullptr;  // [F] level-2 class sizes
+  int64_t* d_off = nullptr;  // [F + 1] block byte offsets
+  int64_t* d_toff = nullptr;  // [F + 1] task offsets
+  int64_t f_cap = 0;
+  kern::DeepCtl* ctl = nullptr;
+  kern::DeepCtl* h_ctl = nullptr;  // pinned readback
+  uint64_t* d_red = nullptr;       // [66]: per_depth[64], digest_sum, candidates (all-reduce)
+  uint64_t* d_xor = nullptr;       // [world] (all-gather)
+  int xor_cap = 0;
+  ~DeepBufs();
+};
+
+struct DeepInput {
+  const uint64_t* bm = nullptr;   // device [F][Wp] frequent-item bitmaps (rank order)
+  int64_t Wp = 0, F = 0;
+  int W_real = 0;                 // ceil(T / 64)
+  const int32_t* d_ids = nullptr; // device [F] rank -> original item id
+  uint32_t minsup = 0;            // count threshold for |S| >= 2
+  int max_len = 0;
+  int n_cus = 256;
+  hipStream_t stream = nullptr;
+};
+
+// This rank's share: counts of sizes >= 2 (size 2 on rank 0 only), digest terms, stats.
+struct DeepLocal {
+  std::vector<uint64_t> per_depth = std::vector<uint64_t>(64, 0);
+  uint64_t dsum = 0, dxor = 0, candidates = 0, chunks = 0;
+  int64_t level2_tasks = 0;
+  std::vector<int64_t> round_tasks;
+  std::vector<double> round_ms;
+  double ms_alloc = 0, ms_root = 0, ms_rounds = 0;
+};
+
+DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const DeepOpts& opt);
+
+}  // namespace gpu
+}  // namespace kmls

@@ -5,25 +5,21 @@
 // does not depend on the order in which a miner's trie lists the items of an itemset); the
 // itemset's digest mixes that with its support count; the trie digest is (count, sum, xor) of
 // the mixed itemset digests -- a multiset hash, independent of node order and additive over
-// disjoint parts (sum mod 2^64, xor), so per-rank sub-tries combine without moving them.  Parents must come
-// before children (every miner's trie is built that way).
+// disjoint parts (sum mod 2^64, xor), so per-rank sub-tries combine without moving them.  The
+// count-only miners (mine_cpu_count, the GPU deep miner) produce the same digest without a
+// trie (kmls/digest.hpp).  Parents must come before children (every miner's trie is built
+// that way).
 #include <cstring>
 #include <string>
 #include <stdexcept>
 #include <vector>
 
+#include "kmls/digest.hpp"
 #include "kmls/host.hpp"
 
 namespace kmls {
 
 namespace {
-
-inline uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
 
 inline int64_t load_int(const void* p, int w, int64_t i) {
   switch (w) {
@@ -31,31 +27,45 @@ inline int64_t load_int(const void* p, int w, int64_t i) {
     case 4: return ((const int32_t*)p)[i];
     case 8: return ((const int64_t*)p)[i];
   }
-  throw std::runtime_error("trie_digest: unsupported element width");
+  throw std::runtime_error("trie_digest: unsupported element width " + std::to_string(w));
+}
+
+inline uint64_t load_uint(const void* p, int w, int64_t i) {
+  switch (w) {
+    case 2: return ((const uint16_t*)p)[i];
+    case 4: return ((const uint32_t*)p)[i];
+    case 8: return ((const uint64_t*)p)[i];
+  }
+  throw std::runtime_error("trie_digest: unsupported count width " + std::to_string(w));
 }
 
 }  // namespace
 
 TrieDigest trie_digest(const void* parent, int pw, const void* item, int iw, const void* count,
                        int cw, const uint8_t* depth, int64_t n, int min_depth) {
+  if (pw != 4 && pw != 8)
+    throw std::runtime_error("trie_digest: parent width must be 4 or 8 bytes, got " + std::to_string(pw));
+  if (cw != 2 && cw != 4 && cw != 8)
+    throw std::runtime_error("trie_digest: count width must be 2, 4 or 8 bytes, got " + std::to_string(cw));
+  if (iw != 2 && iw != 4 && iw != 8)
+    throw std::runtime_error("trie_digest: item width must be 2, 4 or 8 bytes, got " + std::to_string(iw));
   TrieDigest d;
   std::vector<uint64_t> h((size_t)n);
   for (int64_t i = 0; i < n; ++i) {
     // parent: signed (-1 = root); 2-byte parents never occur
     int64_t p = pw == 4 ? (int64_t)((const int32_t*)parent)[i] : ((const int64_t*)parent)[i];
     const uint64_t it = (uint64_t)load_int(item, iw, i);
-    const uint64_t c = cw == 2 ? (uint64_t)((const uint16_t*)count)[i]
-                               : (uint64_t)((const uint32_t*)count)[i];
+    const uint64_t c = load_uint(count, cw, i);
     if (p >= i || p < -1)
       throw std::runtime_error("trie_digest: node " + std::to_string(i) + " has parent " +
                                std::to_string(p) + " (parents must precede children)");
-    const uint64_t set = (p >= 0 ? h[(size_t)p] : 0ull) + mix64(it * 0x100000001B3ull + 7);
+    const uint64_t set = (p >= 0 ? h[(size_t)p] : 0ull) + item_mix(it);
     h[(size_t)i] = set;
     const int dep = depth ? depth[i] : 0;
     if (depth && dep < min_depth) continue;  // parent-chain only (e.g. replicated level 1)
-    const uint64_t dg = mix64(set ^ mix64(c + 0x51ED270B27ull));
-    d.sum += mix64(dg);
-    d.xr ^= mix64(dg ^ 0xA5A5A5A5DEADBEEFull);
+    const DigestTerms t = digest_terms(set, c);
+    d.sum += t.sum;
+    d.xr ^= t.xr;
     ++d.n;
     if ((int)d.per_depth.size() <= dep) d.per_depth.resize((size_t)dep + 1, 0);
     d.per_depth[(size_t)dep]++;

@@ -14,8 +14,10 @@
 #include <vector>
 
 #include <cstdlib>
+#include <functional>
 
 #include "kmls/common.hpp"
+#include "kmls/digest.hpp"
 #include "kmls/host.hpp"
 
 namespace kmls {
@@ -133,10 +135,19 @@ void expand_member(const Ctx& cx, const std::vector<Member>& cls, size_t i, int 
   }
 }
 
-// Count-only variant of expand_member: no trie, per-level totals, stops once the shared
-// counter passes `cap` (for calibration / feasibility probes of outputs too big to hold).
+// Count-only search: no trie; per-level totals plus the content digest of every frequent itemset
+// (kmls/digest.hpp: the same digest trie_digest computes from a miner's trie), so a count-only
+// GPU result is checked by content, not just by number.  Stops once the shared counter passes
+// `cap` (calibration / feasibility probes of outputs too big to hold).
+struct CMember {
+  int32_t rank;
+  int64_t off;  // >= 0: offset into the thread arena; < 0: level-2 row (-1 - off) of the shared store
+  uint64_t h;   // set hash of the member's itemset
+};
+
 struct CountCtx {
-  const uint64_t* top_bm;
+  const uint64_t* l2_bm;  // [#pairs][W] level-2 bitmaps (shared, read-only)
+  const int32_t* ids;     // rank -> original item id
   int64_t W;
   uint32_t minsup;
   int max_len;
@@ -144,41 +155,53 @@ struct CountCtx {
   std::atomic<int64_t>* total;
 };
 
-void count_member(const CountCtx& cx, const std::vector<Member>& cls, size_t i, int depth,
-                  std::vector<uint64_t>& arena, size_t top, std::vector<int64_t>& per_level) {
+struct CountAcc {
+  std::vector<int64_t> per_level;
+  uint64_t sum = 0, xr = 0;
+  void add(int depth, uint64_t h, uint32_t c) {
+    if ((int)per_level.size() <= depth) per_level.resize((size_t)depth + 1, 0);
+    per_level[(size_t)depth]++;
+    const DigestTerms t = digest_terms(h, c);
+    sum += t.sum;
+    xr ^= t.xr;
+  }
+};
+
+// expand member i of class `cls` (itemsets of size `depth`): every later member j gives the
+// candidate cls[i] ∪ cls[j]
+void count_member(const CountCtx& cx, const std::vector<CMember>& cls, size_t i, int depth,
+                  std::vector<uint64_t>& arena, size_t top, CountAcc& acc) {
   if (cx.total->load(std::memory_order_relaxed) > cx.cap) return;
   const int64_t W = cx.W;
   const size_t need = top + (cls.size() - i - 1) * (size_t)W;
   if (arena.size() < need) arena.resize(need + (need >> 1) + 1024);
-  const Member a = cls[i];
   auto res = [&](int64_t off) {
-    return off >= 0 ? arena.data() + off : cx.top_bm + (-1 - off) * W;
+    return off >= 0 ? arena.data() + off : cx.l2_bm + (-1 - off) * W;
   };
-  std::vector<Member> child;
+  const CMember a = cls[i];
+  std::vector<CMember> child;
   size_t cur = top;
+  const uint64_t* x = res(a.off);  // the arena does not move inside this loop (reserved above)
   for (size_t j = i + 1; j < cls.size(); ++j) {
-    const uint64_t* x = res(a.off);
     const uint64_t* y = res(cls[j].off);
     uint64_t* o = arena.data() + cur;
     uint32_t c = 0;
     for (int64_t w = 0; w < W; ++w) {
-      uint64_t v = x[w] & y[w];
+      const uint64_t v = x[w] & y[w];
       o[w] = v;
       c += (uint32_t)__builtin_popcountll(v);
     }
     if (c >= cx.minsup) {
-      child.push_back(Member{cls[j].rank, c, (int64_t)cur, 0});
+      const uint64_t h = a.h + item_mix((uint64_t)cx.ids[cls[j].rank]);
+      acc.add(depth + 1, h, c);
+      child.push_back(CMember{cls[j].rank, (int64_t)cur, h});
       cur += (size_t)W;
     }
   }
-  if (!child.empty()) {
-    if ((int)per_level.size() < depth + 2) per_level.resize((size_t)depth + 2, 0);
-    per_level[(size_t)depth + 1] += (int64_t)child.size();
-    cx.total->fetch_add((int64_t)child.size(), std::memory_order_relaxed);
-  }
+  if (!child.empty()) cx.total->fetch_add((int64_t)child.size(), std::memory_order_relaxed);
   if (child.size() >= 2 && (cx.max_len == 0 || depth + 1 < cx.max_len)) {
     for (size_t k = 0; k + 1 < child.size(); ++k)
-      count_member(cx, child, k, depth + 1, arena, cur, per_level);
+      count_member(cx, child, k, depth + 1, arena, cur, acc);
   }
 }
 
@@ -196,33 +219,90 @@ CountResult mine_cpu_count(const int64_t* tx_ptr, const int32_t* items, int64_t 
   std::vector<uint64_t> bm((size_t)(F * W), 0);
   encode_bitmaps_cpu(tx_ptr, items, n_tx, fi.rank_of.data(), bm.data(), W);
   CountResult r;
-  r.per_level.assign(2, 0);
-  r.per_level[1] = F;
+  CountAcc all;
+  for (int64_t j = 0; j < F; ++j) all.add(1, item_mix((uint64_t)fi.ids[j]), fi.counts[j]);
   std::atomic<int64_t> total{F};
-  if (F >= 2 && max_len != 1) {
-    CountCtx cx{bm.data(), W, fi.minsup2, max_len, cap, &total};
-    int nth = threads > 0 ? threads : default_threads();
-    nth = std::max(1, std::min<int>(nth, (int)F));
-    std::atomic<int64_t> next{0};
-    std::vector<Member> root((size_t)F);
-    for (int64_t j = 0; j < F; ++j) root[(size_t)j] = Member{(int32_t)j, fi.counts[j], -1 - j, 0};
-    std::vector<std::vector<int64_t>> lv((size_t)nth);
-    auto worker = [&](int t) {
-      std::vector<uint64_t> arena;
-      while (true) {
-        int64_t i = next.fetch_add(1);
-        if (i >= F - 1 || total.load(std::memory_order_relaxed) > cap) break;
-        count_member(cx, root, (size_t)i, 1, arena, 0, lv[(size_t)t]);
-      }
-    };
+  int nth = threads > 0 ? threads : default_threads();
+  nth = std::max(1, std::min<int>(nth, (int)std::max<int64_t>(F, 1)));
+  auto run_pool = [&](const std::function<void(int)>& fn) {
     std::vector<std::thread> pool;
-    for (int t = 0; t < nth; ++t) pool.emplace_back(worker, t);
+    for (int t = 0; t < nth; ++t) pool.emplace_back(fn, t);
     for (auto& th : pool) th.join();
-    for (auto& v : lv) {
-      if (v.size() > r.per_level.size()) r.per_level.resize(v.size(), 0);
-      for (size_t d = 2; d < v.size(); ++d) r.per_level[d] += v[d];
+  };
+  if (F >= 2 && max_len != 1) {
+    // level 2 (parallel over root classes): every root item's class of frequent pairs, stored
+    // once and shared, so level-3 classes become the unit of dynamic scheduling (a dense root
+    // class no longer lands on one thread)
+    std::vector<std::vector<uint64_t>> l2b((size_t)F);
+    std::vector<std::vector<int32_t>> l2r((size_t)F);
+    std::vector<std::vector<uint32_t>> l2c((size_t)F);
+    std::atomic<int64_t> next{0};
+    run_pool([&](int) {
+      std::vector<uint64_t> row((size_t)W);
+      while (true) {
+        const int64_t i = next.fetch_add(1);
+        if (i >= F - 1) break;
+        const uint64_t* x = bm.data() + i * W;
+        for (int64_t j = i + 1; j < F; ++j) {
+          const uint64_t* y = bm.data() + j * W;
+          uint32_t c = 0;
+          for (int64_t w = 0; w < W; ++w) {
+            row[(size_t)w] = x[w] & y[w];
+            c += (uint32_t)__builtin_popcountll(row[(size_t)w]);
+          }
+          if (c >= fi.minsup2) {
+            l2b[(size_t)i].insert(l2b[(size_t)i].end(), row.begin(), row.end());
+            l2r[(size_t)i].push_back((int32_t)j);
+            l2c[(size_t)i].push_back(c);
+          }
+        }
+      }
+    });
+    std::vector<int64_t> base((size_t)F + 1, 0);
+    for (int64_t i = 0; i < F; ++i) base[(size_t)i + 1] = base[(size_t)i] + (int64_t)l2r[(size_t)i].size();
+    std::vector<uint64_t> l2((size_t)(base[(size_t)F] * W));
+    std::vector<std::vector<CMember>> cls((size_t)F);
+    for (int64_t i = 0; i < F; ++i) {
+      std::copy(l2b[(size_t)i].begin(), l2b[(size_t)i].end(), l2.begin() + base[(size_t)i] * W);
+      std::vector<uint64_t>().swap(l2b[(size_t)i]);
+      const uint64_t hi = item_mix((uint64_t)fi.ids[(size_t)i]);
+      for (size_t k = 0; k < l2r[(size_t)i].size(); ++k) {
+        const uint64_t h = hi + item_mix((uint64_t)fi.ids[(size_t)l2r[(size_t)i][k]]);
+        all.add(2, h, l2c[(size_t)i][k]);
+        cls[(size_t)i].push_back(CMember{l2r[(size_t)i][k], -1 - (base[(size_t)i] + (int64_t)k), h});
+      }
+    }
+    total.fetch_add(base[(size_t)F]);
+    // levels >= 3: tasks (root class i, member k)
+    if (max_len == 0 || max_len > 2) {
+      std::vector<std::pair<int32_t, int32_t>> tasks;
+      for (int64_t i = 0; i < F; ++i)
+        for (size_t k = 0; k + 1 < cls[(size_t)i].size(); ++k) tasks.push_back({(int32_t)i, (int32_t)k});
+      CountCtx cx{l2.data(), fi.ids.data(), W, fi.minsup2, max_len, cap, &total};
+      std::vector<CountAcc> acc((size_t)nth);
+      std::atomic<int64_t> nt{0};
+      run_pool([&](int t) {
+        std::vector<uint64_t> arena;
+        while (true) {
+          const int64_t q = nt.fetch_add(1);
+          if (q >= (int64_t)tasks.size() || total.load(std::memory_order_relaxed) > cap) break;
+          count_member(cx, cls[(size_t)tasks[(size_t)q].first], (size_t)tasks[(size_t)q].second, 2,
+                       arena, 0, acc[(size_t)t]);
+        }
+      });
+      for (auto& a : acc) {
+        if (a.per_level.size() > all.per_level.size()) all.per_level.resize(a.per_level.size(), 0);
+        for (size_t d = 0; d < a.per_level.size(); ++d) all.per_level[d] += a.per_level[d];
+        all.sum += a.sum;
+        all.xr ^= a.xr;
+      }
     }
   }
+  r.per_level = all.per_level;
+  if (r.per_level.size() < 2) r.per_level.resize(2, 0);
+  r.per_level[0] = 0;
+  r.digest_sum = all.sum;
+  r.digest_xor = all.xr;
   r.n_frequent_items = F;
   r.n_itemsets = 0;
   for (size_t d = 1; d < r.per_level.size(); ++d) r.n_itemsets += r.per_level[d];

@@ -124,6 +124,29 @@ class Comm {
 };
 
 struct OutBufs;  // persistent device trie buffers + download stream (miner_gpu.hip)
+struct DeepBufs;  // count-only deep miner buffers (deep_gpu.hip)
+struct DeepBufsDeleter {
+  void operator()(DeepBufs* p) const;
+};
+
+// Count-only deep mining (deep_gpu.hip, kernels/deep.hip): per-size itemset counts and the
+// content digest (kmls/digest.hpp; equal to trie_digest of the full trie) without a trie.
+struct DeepOpts {
+  unsigned long long budget0 = 4096;  // 64-lane passes a first-round task may take before spilling
+  unsigned long long budget = 4096;   // ... in later rounds
+  unsigned split_min = 4;             // spilled frames above this many members split per member
+  int blocks_per_cu = 0;              // 0 = 3 (12 waves per CU)
+  int stack_mb = 0;                   // per-wave stack (0: KMLS_DEEP_STACK_MB or 4)
+};
+struct DeepResult {
+  std::vector<uint64_t> per_level;  // [d] = frequent itemsets of size d (index 0 unused)
+  int64_t n_itemsets = 0, n_frequent_items = 0, candidates = 0, chunks = 0, level2_tasks = 0;
+  int max_depth = 0;
+  uint64_t digest_sum = 0, digest_xor = 0;
+  std::vector<int64_t> round_tasks;
+  std::vector<double> round_ms;
+  double ms_prologue = 0, ms_root = 0, ms_rounds = 0, ms_combine = 0, ms_total = 0;
+};
 struct GraphCache;  // captured launch sequence of the resident path (miner_gpu.hip)
 struct Prefetch;    // a resident call launched ahead of its mine() (miner_gpu.hip)
 }  // namespace gpu
@@ -178,6 +201,11 @@ class GpuMiner {
   // ever replicating bitmaps.  comm == nullptr behaves as world size 1.
   GpuMineResult mine_txdp(Comm* comm, int64_t global_n_tx, const MineConfig& cfg, bool download,
                           int support_tiles);
+  // Count-only full mining (short transactions, T <= 4096): every rank holds the full CSR and
+  // builds the level-2 classes; rank r mines level-3 tasks t with t % world == r; counts and
+  // digests are combined through `comm` (nullptr: world must be 1, or the caller combines).
+  DeepResult mine_deep(double min_support, int max_len, int rank, int world, Comm* comm,
+                       const DeepOpts& opts);
 
   // Frequent items of the last select(): ids (ascending support) and counts.
   const FrequentItems& frequent() const { return fi_; }
@@ -252,6 +280,7 @@ class GpuMiner {
   size_t arena_max_ = 0;
   std::string fused_fallback_;
   std::unique_ptr<OutBufs> out_;  // output trie kept allocated across mine() calls
+  std::unique_ptr<DeepBufs, DeepBufsDeleter> deep_;  // count-only deep miner buffers
   std::unique_ptr<GraphCache> graph_;  // steady-state hipGraph of mine_resident
   Comm* comm_ = nullptr;          // set during mine_txdp: level counts are all-reduced
   std::vector<int64_t> tile_tx_;  // 65 evenly spaced transaction boundaries of the shard

@@ -56,14 +56,16 @@ ItemsetTrie mine_cpu_txdp(const int64_t* tx_ptr, const int32_t* items, int64_t n
                           int64_t n_items, int64_t n_tx_global, double min_support, int max_len,
                           ShmComm* comm, MineStats* stats);
 
-// Count-only search: per-level itemset totals without a trie; stops once the running total
-// exceeds `cap` (capped = true, counts are then a lower bound).  For feasibility probes.
+// Count-only search: per-level itemset totals and the content digest (the one trie_digest gives
+// for the full trie) without a trie; stops once the running total exceeds `cap` (capped = true,
+// counts are then a lower bound).  The CPU reference of the GPU count-only (deep) miner.
 struct CountResult {
   std::vector<int64_t> per_level;  // [d] = #frequent itemsets of size d (index 0 unused)
   int64_t n_frequent_items = 0, n_itemsets = 0;
   int max_depth = 0;
   bool capped = false;
   double seconds = 0.0;
+  uint64_t digest_sum = 0, digest_xor = 0;  // content digest (kmls/digest.hpp); partial if capped
 };
 CountResult mine_cpu_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                            int64_t n_items, double min_support, int max_len, int64_t cap,

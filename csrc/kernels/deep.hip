@@ -1,0 +1,646 @@
+// Count-only deep FP-Growth mining on CDNA4: every frequent itemset of every size is found and its
+// support computed, the per-size totals and the content digest (kmls/digest.hpp) accumulated on
+// the device, and nothing is materialised for the host.  For the reference's datasets (short
+// transactions, T <= 4096, i.e. <= 64 bitmap words) at supports where the output has 1e9-1e10
+// itemsets (BASELINE config 2, ds1 @ 0.01-0.02), a level-wise miner cannot hold one level in HBM.
+//
+// Design (one wave = one independent depth-first worker, no inter-wave hand-off inside a launch):
+// * A class (prefix P, members P∪{x_k}) lives in a BLOCK: W bitmap words x `pad` slots stored
+//   word-major ([w][slot]), then one item-hash word per slot.  Lanes that read consecutive
+//   member slots of one word row read contiguous memory, so every bitmap load is coalesced.
+// * A FRAME is (block, first slot, members, prefix hash, prefix size).  Each wave keeps a frame
+//   stack and a LIFO stack of blocks in its own HBM region; a block is freed when the frames that
+//   reference it are done and it is on top.
+// * Row step (big frames, > kCap pairs): member s0 against every later member, lane = candidate:
+//   the member's words are a broadcast, the candidates' words one coalesced row per word.
+// * Batch step (small frames, the deep levels): the top frames are popped together until their
+//   member PAIRS fill up to kCap lanes, so a wave64 instruction still carries 64 candidates when
+//   classes have 5-20 members.  Survivors of one (frame, member) group stay contiguous in the
+//   child block (lane order = pair order), so each group becomes a child frame.
+// * Load balance: tasks are dequeued by ticket.  A wave that exceeds its step budget on one task
+//   SPILLS its remaining frames to a heap as new tasks (big frames split into one task per
+//   member) and the host runs another round; heavy dense subtrees are thus cut into many tasks.
+// * All bitmap words of a candidate stay in VGPRs (WT <= 64 words), so a survivor's child row is
+//   written without re-reading its parents.
+// Counts are exact (popcount of at most 4096 bits per row, u32).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <type_traits>
+
+#include "kernels.hpp"
+#include "kmls/digest.hpp"
+#include <kmls/wave.hpp>
+
+namespace kmls {
+namespace kern {
+
+namespace {
+
+constexpr int kWaves = 4;            // independent waves per workgroup
+constexpr int kCap = 256;            // candidate pairs per batch step
+constexpr int kBatchFrames = 64;     // frames one batch step may take
+constexpr int kBStack = 96;          // blocks on one wave's memory stack
+constexpr unsigned kSingle = 1u << 8;  // frame flag: expand only its first member
+
+// frame meta: bits 0..7 prefix size, bit 8 single, bits 16..31 block-stack index + 1 (0 = external)
+__device__ __forceinline__ unsigned meta_depth(unsigned m) { return m & 0xffu; }
+__device__ __forceinline__ unsigned meta_bidx(unsigned m) { return m >> 16; }
+
+constexpr unsigned long long roundup16(unsigned long long x) { return (x + 15) & ~15ull; }
+
+// every lane gets frame `p` (read as 8 dwords by lanes 0-7: a vector load, then broadcast)
+__device__ __forceinline__ DeepFrame load_frame(const DeepFrame* p, int lane) {
+  const unsigned* w = (const unsigned*)p;
+  const unsigned v = lane < 8 ? w[(lane & 7) + vzero()] : 0u;
+  DeepFrame f;
+  f.blk = ((unsigned long long)__shfl(v, 1, 64) << 32) | __shfl(v, 0, 64);
+  f.hash = ((unsigned long long)__shfl(v, 3, 64) << 32) | __shfl(v, 2, 64);
+  f.pad = __shfl(v, 4, 64);
+  f.s0 = __shfl(v, 5, 64);
+  f.m = __shfl(v, 6, 64);
+  f.meta = __shfl(v, 7, 64);
+  f.blk = uni64(f.blk);
+  f.hash = uni64(f.hash);
+  f.pad = uni(f.pad);
+  f.s0 = uni(f.s0);
+  f.m = uni(f.m);
+  f.meta = uni(f.meta);
+  return f;
+}
+
+__device__ __forceinline__ void store_frame(DeepFrame* p, const DeepFrame& f) {
+  p->blk = f.blk;
+  p->hash = f.hash;
+  p->pad = f.pad;
+  p->s0 = f.s0;
+  p->m = f.m;
+  p->meta = f.meta;
+}
+
+struct WaveLds {
+  unsigned long long f_hash[kBatchFrames];
+  unsigned f_s0[kBatchFrames], f_m[kBatchFrames], f_meta[kBatchFrames];
+  unsigned P[kBatchFrames + 1], G[kBatchFrames + 1];
+  unsigned g_cnt[kCap], g_start[kCap];
+  unsigned long long b_base[kBStack];
+  unsigned b_live[kBStack];
+  unsigned long long depth_cnt[64];
+};
+
+// candidate (slot sa, slot sb) of one block: AND of every word (kept in v) and its popcount.
+// blk and pad are wave-uniform, so each word row's base is an SGPR pair and the two slot offsets
+// are the only address VGPRs (global_load saddr + voffset form).
+// WT is the exact row width (the host pads rows to an instantiated width with zero words), so
+// the loads are unrolled without guards and all 2*WT of them can be in flight.
+template <int WT>
+__device__ __forceinline__ unsigned and_count(const unsigned long long* blk, unsigned long long pad,
+                                              unsigned sa, unsigned sb, int /*W*/,
+                                              unsigned long long (&v)[WT]) {
+  unsigned c = 0;
+#pragma unroll
+  for (int w = 0; w < WT; ++w) {
+    const unsigned long long* row = blk + (unsigned long long)w * pad;
+    v[w] = row[sa] & row[sb];
+  }
+#pragma unroll
+  for (int w = 0; w < WT; ++w) c += (unsigned)__popcll(v[w]);
+  return c;
+}
+
+template <int WT>
+__device__ __forceinline__ void write_row(unsigned long long* cb, unsigned long long cpad,
+                                          unsigned pos, int /*W*/,
+                                          const unsigned long long (&v)[WT],
+                                          unsigned long long ih) {
+#pragma unroll
+  for (int w = 0; w < WT; ++w) cb[(unsigned long long)w * cpad + pos] = v[w];
+  cb[(unsigned long long)WT * cpad + pos] = ih;
+}
+
+struct WaveState {
+  unsigned nf;                 // frames on the stack
+  unsigned nb;                 // blocks on the memory stack
+  unsigned long long mem_top;  // bytes used in the wave's stack region
+};
+
+// pop the top frame: its block loses a live frame
+__device__ __forceinline__ void release_frame(WaveLds& L, unsigned meta, int lane) {
+  const unsigned b = meta_bidx(meta);
+  if (b && lane == 0) L.b_live[b - 1] -= 1;
+}
+
+__device__ __forceinline__ void free_blocks(WaveLds& L, WaveState& st) {
+  __builtin_amdgcn_wave_barrier();
+  while (st.nb > 0) {
+    const unsigned live = uni(L.b_live[st.nb - 1 + vzero()]);
+    if (live) break;
+    st.mem_top = uni64(L.b_base[st.nb - 1 + vzero()]);
+    st.nb -= 1;
+  }
+}
+
+// Copy every frame on the stack to the spill heap and queue it as next-round task(s): frames of
+// more than split_min members become one single-member task each (over one shared copy).
+// Returns false (error set) when the heap or the out queue is full.
+__device__ bool spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st, WaveLds& L,
+                             int lane) {
+  const int W = a.W;
+  for (unsigned f = 0; f < st.nf; ++f) {
+    const DeepFrame fr = load_frame(fst + f, lane);
+    const unsigned m = fr.m;
+    const unsigned long long npad = roundup16(m);
+    const unsigned long long bytes = (unsigned long long)(W + 1) * npad * 8ull;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&a.ctl->heap_top, bytes);
+    base = uni64(bcast64(base, 0));
+    if (base + bytes > a.heap_cap) {
+      if (lane == 0) atomicOr(&a.ctl->error, 2u);
+      return false;
+    }
+    const unsigned long long* src = (const unsigned long long*)fr.blk;
+    unsigned long long* dst = (unsigned long long*)(a.heap + base);
+    const unsigned long long tot = (unsigned long long)(W + 1) * m;
+    for (unsigned long long e = lane; e < tot; e += 64) {
+      const unsigned long long w = e / m, k = e - w * m;
+      dst[w * npad + k] = src[w * fr.pad + fr.s0 + k];
+    }
+    const bool single = (fr.meta & kSingle) != 0;
+    const bool split = !single && m > a.split_min;
+    const unsigned nt = split ? m - 1 : 1;
+    unsigned long long t0 = 0;
+    if (lane == 0) t0 = atomicAdd(&a.ctl->n_out, (unsigned long long)nt);
+    t0 = uni64(bcast64(t0, 0));
+    if (t0 + nt > (unsigned long long)a.out_cap) {
+      if (lane == 0) atomicOr(&a.ctl->error, 1u);
+      return false;
+    }
+    for (unsigned k = lane; k < nt; k += 64) {
+      DeepFrame o;
+      o.blk = (unsigned long long)dst;
+      o.hash = fr.hash;
+      o.pad = (unsigned)npad;
+      o.s0 = split ? k : 0u;
+      o.m = split ? m - k : m;
+      o.meta = meta_depth(fr.meta) | ((split || single) ? kSingle : 0u);
+      store_frame(a.out + t0 + k, o);
+    }
+  }
+  st.nf = 0;
+  st.nb = 0;
+  st.mem_top = 0;
+  return true;
+}
+
+// waves per SIMD the count kernel is compiled for: the candidate's words stay in VGPRs (2 per
+// word), so 40-word rows fit 4 waves/SIMD (128 VGPRs) and 64-word rows 3 (168)
+template <int WT>
+constexpr int deep_waves_per_simd() { return WT <= 16 ? 4 : (WT <= 40 ? 3 : 2); }
+
+template <int WT>
+__global__ __launch_bounds__(256, deep_waves_per_simd<WT>()) void k_deep_count(DeepArgs a) {
+  __shared__ WaveLds lds[kWaves];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  WaveLds& L = lds[wid];
+  const unsigned long long gw = (unsigned long long)blockIdx.x * kWaves + wid;
+  DeepFrame* fst = a.fstacks + gw * (unsigned long long)a.fcap;
+  char* stack = a.stacks + gw * a.stack_bytes;
+  const int W = a.W;
+  const unsigned minsup = a.minsup;
+  const unsigned long long lanelt = (1ull << lane) - 1ull;
+
+  for (int d = lane; d < 64; d += 64) L.depth_cnt[d] = 0;
+  unsigned long long dsum = 0, dxor = 0, cands = 0, chunks_total = 0;
+  __builtin_amdgcn_wave_barrier();
+
+  WaveState st{0, 0, 0};
+  bool failed = false;
+  const unsigned long long t_start = wall_clock64();
+  while (!failed) {
+    unsigned long long t = 0;
+    if (lane == 0) t = atomicAdd(&a.ctl->next_task, 1ull);
+    t = uni64(bcast64(t, 0));
+    if (t >= (unsigned long long)a.n_in) break;
+    {
+      const DeepFrame tf = load_frame(a.in + t, lane);
+      if (lane == 0) store_frame(fst, tf);
+      // lanes exchange frames through memory: coherent within a wave in program order (one L1);
+      // the wave barriers mark those hand-offs (the CPU emulator synchronises its lanes there)
+      __builtin_amdgcn_wave_barrier();
+      st.nf = 1;
+      st.nb = 0;
+      st.mem_top = 0;
+    }
+    unsigned long long budget_used = 0;
+    while (st.nf > 0) {
+      __builtin_amdgcn_wave_barrier();
+      // bounded: a round that runs past its deadline gives up (error bit 2) instead of holding
+      // the GPU; the host reports it
+      if (wall_clock64() - t_start > a.timeout_ticks) {
+        if (lane == 0) atomicOr(&a.ctl->error, 4u);
+        failed = true;
+        break;
+      }
+      DeepFrame top = load_frame(fst + st.nf - 1, lane);
+      const unsigned m = top.m;
+      const unsigned long long pairs = (unsigned long long)m * (m - 1) / 2;
+      const bool row_mode = (top.meta & kSingle) || pairs > (unsigned long long)kCap;
+      const unsigned long long need =
+          (unsigned long long)(W + 1) * roundup16(row_mode ? m : kCap) * 8ull;
+      if (budget_used >= a.budget || st.mem_top + need > a.stack_bytes ||
+          st.nf + kCap + 2 > (unsigned)a.fcap || st.nb + 1 >= (unsigned)kBStack) {
+        if (!spill_frames(a, fst, st, L, lane)) failed = true;
+        break;
+      }
+      const unsigned depth = meta_depth(top.meta);  // prefix size: members are depth+1 itemsets
+      const bool deeper = a.max_len == 0 || (int)depth + 3 <= a.max_len;  // children expandable
+      unsigned long long* cb = (unsigned long long*)(stack + st.mem_top);
+      if (row_mode) {
+        // ---- row step: member s0 against members s0+1 .. s0+m-1 ----
+        const unsigned nc = m - 1;
+        const unsigned long long cpad = roundup16(nc);
+        const unsigned long long* blk = (const unsigned long long*)top.blk;
+        const unsigned long long* ihp = blk + (unsigned long long)W * top.pad;
+        const unsigned ia = top.s0;
+        const unsigned long long ih_a = ihp[ia + vzero()];
+        const unsigned long long h_a = top.hash + ih_a;
+        unsigned S = 0;
+        for (unsigned c0 = 0; c0 < nc; c0 += 64) {
+          const bool act = c0 + lane < nc;
+          const unsigned jb = act ? ia + 1 + c0 + lane : ia;
+          unsigned long long v[WT];
+          const unsigned c = and_count<WT>(blk, top.pad, ia + vzero(), jb, W, v);
+          const bool surv = act && c >= minsup;
+          const unsigned long long mask = __ballot(surv);
+          if (surv) {
+            const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
+            const unsigned long long ih_b = ihp[jb];
+            write_row<WT>(cb, cpad, pos, W, v, ih_b);
+            const DigestTerms dt = digest_terms(h_a + ih_b, c);
+            dsum += dt.sum;
+            dxor ^= dt.xr;
+          }
+          S += (unsigned)__popcll(mask);
+          ++chunks_total;
+        }
+        cands += nc;
+        if (lane == 0 && S) L.depth_cnt[depth + 2] += S;
+        budget_used += (nc + 63) / 64;
+        // parent: done with member s0
+        if ((top.meta & kSingle) || m <= 2) {
+          release_frame(L, top.meta, lane);
+          st.nf -= 1;
+        } else {
+          top.s0 += 1;
+          top.m -= 1;
+          if (lane == 0) store_frame(fst + st.nf - 1, top);
+        }
+        if (S >= 2 && deeper) {
+          if (lane == 0) {
+            L.b_base[st.nb] = st.mem_top;
+            L.b_live[st.nb] = 1;
+            DeepFrame c;
+            c.blk = (unsigned long long)cb;
+            c.hash = h_a;
+            c.pad = (unsigned)cpad;
+            c.s0 = 0;
+            c.m = S;
+            c.meta = (depth + 1) | ((st.nb + 1) << 16);
+            store_frame(fst + st.nf, c);
+          }
+          st.nb += 1;
+          st.nf += 1;
+          st.mem_top += (unsigned long long)(W + 1) * cpad * 8ull;
+        }
+        free_blocks(L, st);
+        continue;
+      }
+      // ---- batch step: the top frames' member pairs, up to kCap lanes ----
+      // (frames of the top frame's block only: sibling classes, so the block base stays uniform)
+      unsigned k = 0, P = 0;
+      {
+        // frame f (from the top) is read by lane f: vector loads, then two wave scans
+        unsigned fm = 0, fmeta = kSingle;
+        if (lane < kBatchFrames && (unsigned)lane < st.nf) {
+          const DeepFrame* p = fst + (st.nf - 1 - lane);
+          fm = p->m;
+          fmeta = p->meta;
+          if (p->blk != top.blk) fmeta |= kSingle;  // another block: ends the batch
+          L.f_hash[lane] = p->hash;
+          L.f_s0[lane] = p->s0;
+          L.f_m[lane] = fm;
+          L.f_meta[lane] = fmeta;
+        }
+        const unsigned fp = (fmeta & kSingle) ? 0xffffffffu : fm * (fm - 1) / 2;
+        // inclusive scan of pairs over lanes (lanes >= nf carry "infinite")
+        unsigned incl = fp;
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned o = __shfl_up(incl, off, 64);
+          if (lane >= off) incl = (o == 0xffffffffu || incl == 0xffffffffu || o + incl < o)
+                                      ? 0xffffffffu : o + incl;
+        }
+        const unsigned long long okm = __ballot(incl <= (unsigned)kCap && (unsigned)lane < st.nf);
+        // frames 0 .. k-1 fit (prefix property: the first failing lane ends the run)
+        k = okm == ~0ull ? 64u : (unsigned)__builtin_ctzll(~okm);
+        if (k == 0) k = 1;  // top frame always fits (pairs <= kCap, not single)
+        k = uni(k);
+        P = uni(__shfl(incl, (int)k - 1, 64));
+        const unsigned excl = incl - fp;
+        if ((unsigned)lane < k) {
+          L.P[lane] = excl;
+        }
+        if (lane == 0) L.P[k] = P;
+        // member-group prefix (m - 1 per frame)
+        unsigned gm = ((unsigned)lane < k) ? fm - 1 : 0u;
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned o = __shfl_up(gm, off, 64);
+          if (lane >= off) gm += o;
+        }
+        const unsigned gtot = __shfl(gm, (int)k - 1, 64);
+        if ((unsigned)lane < k) L.G[lane] = gm - (fm - 1);
+        if (lane == 0) L.G[k] = gtot;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const unsigned NG = uni(L.G[k + vzero()]);
+      for (unsigned g = lane; g < NG; g += 64) {
+        L.g_cnt[g] = 0;
+        L.g_start[g] = 0xffffffffu;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long cpad = roundup16(P);
+      const unsigned long long* bblk = (const unsigned long long*)top.blk;
+      const unsigned long long bpad = top.pad;
+      unsigned S = 0;
+      for (unsigned c0 = 0; c0 < P; c0 += 64) {
+        const unsigned p = c0 + lane;
+        const bool act = p < P;
+        // frame of pair p: largest f < k with P[f] <= p
+        unsigned f = 0;
+        for (unsigned step = 32; step; step >>= 1)
+          if (f + step < k && L.P[f + step] <= p) f += step;
+        if (!act) f = 0;
+        const unsigned fmm = L.f_m[f];
+        const unsigned q = act ? p - L.P[f] : 0u;
+        // triangular decode of q into (i, j), i < j < fmm, row-major over i
+        const float twoM = 2.0f * (float)fmm - 1.0f;
+        unsigned i = (unsigned)((twoM - sqrtf(twoM * twoM - 8.0f * (float)q)) * 0.5f);
+        auto row0 = [&](unsigned r) { return r * fmm - r * (r + 1) / 2; };
+        while (i > 0 && row0(i) > q) --i;
+        while (i + 1 < fmm && row0(i + 1) <= q) ++i;
+        const unsigned j = q - row0(i) + i + 1;
+        const unsigned sa = L.f_s0[f] + i, sb = L.f_s0[f] + (act ? j : i);
+        unsigned long long v[WT];
+        const unsigned c = and_count<WT>(bblk, bpad, sa, sb, W, v);
+        const bool surv = act && c >= minsup;
+        const unsigned long long mask = __ballot(surv);
+        if (surv) {
+          const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
+          const unsigned long long* ihp = bblk + (unsigned long long)W * bpad;
+          const unsigned long long ih_a = ihp[sa], ih_b = ihp[sb];
+          write_row<WT>(cb, cpad, pos, W, v, ih_b);
+          const DigestTerms dt = digest_terms(L.f_hash[f] + ih_a + ih_b, c);
+          dsum += dt.sum;
+          dxor ^= dt.xr;
+          atomicAdd(&L.depth_cnt[meta_depth(L.f_meta[f]) + 2], 1ull);
+          const unsigned g = L.G[f] + i;
+          atomicAdd(&L.g_cnt[g], 1u);
+          atomicMin(&L.g_start[g], pos);
+        }
+        S += (unsigned)__popcll(mask);
+        ++chunks_total;
+      }
+      cands += P;
+      budget_used += (P + 63) / 64;
+      // the k consumed frames leave the stack
+      if ((unsigned)lane < k) {
+        const unsigned b = meta_bidx(L.f_meta[lane]);
+        if (b) atomicSub(&L.b_live[b - 1], 1u);
+      }
+      st.nf -= k;
+      __builtin_amdgcn_wave_barrier();
+      // child frames: groups with >= 2 survivors
+      unsigned pushed = 0;
+      const unsigned nbi = st.nb;
+      for (unsigned g0 = 0; g0 < NG; g0 += 64) {
+        const unsigned g = g0 + lane;
+        bool mk = false;
+        unsigned f = 0;
+        if (g < NG) {
+          for (unsigned step = 32; step; step >>= 1)
+            if (f + step < k && L.G[f + step] <= g) f += step;
+          mk = L.g_cnt[g] >= 2 && (a.max_len == 0 || (int)meta_depth(L.f_meta[f]) + 3 <= a.max_len);
+        }
+        const unsigned long long mask = __ballot(mk);
+        if (mk) {
+          const unsigned slot = st.nf + pushed + (unsigned)__popcll(mask & lanelt);
+          const unsigned i = g - L.G[f];
+          const unsigned long long ih_a = bblk[(unsigned long long)W * bpad + L.f_s0[f] + i];
+          DeepFrame c;
+          c.blk = (unsigned long long)cb;
+          c.hash = L.f_hash[f] + ih_a;
+          c.pad = (unsigned)cpad;
+          c.s0 = L.g_start[g];
+          c.m = L.g_cnt[g];
+          c.meta = (meta_depth(L.f_meta[f]) + 1) | ((nbi + 1) << 16);
+          store_frame(fst + slot, c);
+        }
+        pushed += (unsigned)__popcll(mask);
+      }
+      pushed = uni(pushed);
+      if (pushed) {
+        if (lane == 0) {
+          L.b_base[st.nb] = st.mem_top;
+          L.b_live[st.nb] = pushed;
+        }
+        st.nb += 1;
+        st.nf += pushed;
+        st.mem_top += (unsigned long long)(W + 1) * cpad * 8ull;
+      }
+      free_blocks(L, st);
+    }
+  }
+  // flush: wave reduction of the digest terms, per-depth counts from LDS
+  for (int off = 32; off; off >>= 1) {
+    dsum += shfl_xor64(dsum, off);
+    dxor ^= shfl_xor64(dxor, off);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    atomicAdd(&a.ctl->digest_sum, dsum);
+    atomicXor(&a.ctl->digest_xor, dxor);
+    atomicAdd(&a.ctl->candidates, cands);
+    atomicAdd(&a.ctl->chunks, chunks_total);
+  }
+  for (int d = lane; d < 64; d += 64)
+    if (L.depth_cnt[d]) atomicAdd(&a.ctl->per_depth[d], L.depth_cnt[d]);
+}
+
+// ---- root level: level-2 classes (deterministic, so every rank builds the same task list) ----
+
+// bm [F][Wp] row-major -> root block [W][Fpad] word-major + item hashes [Fpad]
+// (rows padded with zero words from W_real up to the instantiated width W)
+__global__ void k_deep_transpose(const unsigned long long* bm, long long Wp, long long F, int W,
+                                 int W_real, const int32_t* ids, unsigned long long* root,
+                                 long long Fpad) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long tot = (long long)(W + 1) * Fpad;
+  if (e >= tot) return;
+  const long long w = e / Fpad, i = e - w * Fpad;
+  unsigned long long v = 0;
+  if (i < F) v = w == W ? item_mix((unsigned long long)ids[i]) : (w < W_real ? bm[i * Wp + w] : 0ull);
+  root[e] = v;
+}
+
+// one wave per root item i: its frequent pairs with every later item j (lane = candidate);
+// fill == false: count only (m[i]); fill == true: write block i (slots in j order) and, when
+// ctl != nullptr, add the level-2 digest terms
+template <int WT>
+__global__ __launch_bounds__(256, deep_waves_per_simd<WT>()) void k_deep_root(const unsigned long long* root, long long Fpad,
+                                                   long long F, int W, unsigned minsup,
+                                                   int32_t* m_out, const long long* blk_off,
+                                                   char* base, DeepCtl* ctl, int fill) {
+  const int lane = threadIdx.x & 63;
+  const long long i = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (i >= F) return;
+  const unsigned long long* ihp = root + (unsigned long long)W * Fpad;
+  const unsigned long long h_a = ihp[i];
+  const long long nc = F - 1 - i;
+  unsigned long long* cb = fill ? (unsigned long long*)(base + blk_off[i]) : nullptr;
+  const unsigned long long cpad = roundup16((unsigned long long)(fill ? m_out[i] : 0));
+  unsigned S = 0;
+  unsigned long long dsum = 0, dxor = 0;
+  const unsigned long long lanelt = (1ull << lane) - 1ull;
+  for (long long c0 = 0; c0 < nc; c0 += 64) {
+    const bool act = c0 + lane < nc;
+    const long long jb = act ? i + 1 + c0 + lane : i;
+    unsigned long long v[WT];
+    const unsigned c = and_count<WT>(root, (unsigned long long)Fpad, (unsigned)i + vzero(), (unsigned)jb, W, v);
+    const bool surv = act && c >= minsup;
+    const unsigned long long mask = __ballot(surv);
+    if (surv && fill) {
+      const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
+      const unsigned long long ih_b = ihp[jb];
+      write_row<WT>(cb, cpad, pos, W, v, ih_b);
+      if (ctl) {
+        const DigestTerms dt = digest_terms(h_a + ih_b, c);
+        dsum += dt.sum;
+        dxor ^= dt.xr;
+      }
+    }
+    S += (unsigned)__popcll(mask);
+  }
+  if (!fill) {
+    if (lane == 0) m_out[i] = (int32_t)S;
+    return;
+  }
+  if (ctl) {
+    for (int off = 32; off; off >>= 1) {
+      dsum += shfl_xor64(dsum, off);
+      dxor ^= shfl_xor64(dxor, off);
+    }
+    if (lane == 0 && S) {
+      atomicAdd(&ctl->digest_sum, dsum);
+      atomicXor(&ctl->digest_xor, dxor);
+    }
+  }
+}
+
+// this rank's share of the level-3 tasks: task t = (root i, member k), t = task_off[i] + k,
+// taken by rank t % world (interleaved, so each root class is spread over the ranks)
+__global__ void k_deep_root_tasks(const long long* blk_off, const int32_t* m, const long long* task_off,
+                                  long long F, char* base, const unsigned long long* root,
+                                  long long Fpad, int W, int rank, int world, DeepFrame* out) {
+  const long long i = blockIdx.x;
+  if (i >= F) return;
+  const int mi = m[i];
+  if (mi < 2) return;
+  const unsigned long long h = root[(unsigned long long)W * Fpad + i];
+  for (int k = threadIdx.x; k < mi - 1; k += blockDim.x) {
+    const long long t = task_off[i] + k;
+    if (t % world != rank) continue;
+    DeepFrame f;
+    f.blk = (unsigned long long)(base + blk_off[i]);
+    f.hash = h;
+    f.pad = (unsigned)roundup16((unsigned long long)mi);
+    f.s0 = (unsigned)k;
+    f.m = (unsigned)(mi - k);
+    f.meta = 1u | kSingle;
+    store_frame(out + t / world, f);
+  }
+}
+
+// instantiated row widths (words); deep_row_words() rounds W up to one of them
+template <typename Fn>
+void by_width(int W, Fn&& fn) {
+  switch (W) {
+    case 4: fn(std::integral_constant<int, 4>{}); break;
+    case 8: fn(std::integral_constant<int, 8>{}); break;
+    case 12: fn(std::integral_constant<int, 12>{}); break;
+    case 16: fn(std::integral_constant<int, 16>{}); break;
+    case 20: fn(std::integral_constant<int, 20>{}); break;
+    case 24: fn(std::integral_constant<int, 24>{}); break;
+    case 28: fn(std::integral_constant<int, 28>{}); break;
+    case 32: fn(std::integral_constant<int, 32>{}); break;
+    case 36: fn(std::integral_constant<int, 36>{}); break;
+    case 40: fn(std::integral_constant<int, 40>{}); break;
+    case 48: fn(std::integral_constant<int, 48>{}); break;
+    case 56: fn(std::integral_constant<int, 56>{}); break;
+    case 64: fn(std::integral_constant<int, 64>{}); break;
+    default: break;  // deep_row_words() never returns another width
+  }
+}
+
+}  // namespace
+
+int deep_max_words() { return 64; }
+int deep_row_words(int W) {
+  if (W <= 40) return W <= 0 ? 4 : (W + 3) / 4 * 4;
+  return (W + 7) / 8 * 8;
+}
+int deep_waves_per_block() { return kWaves; }
+int deep_min_fcap() { return kCap + 64; }
+
+size_t deep_row_block_bytes(int W, int64_t m) {
+  return (size_t)(W + 1) * (size_t)roundup16((unsigned long long)std::max<int64_t>(m, kCap)) * 8;
+}
+
+void deep_transpose(const uint64_t* bm, int64_t Wp, int64_t F, int W, int W_real,
+                    const int32_t* ids, uint64_t* root, int64_t Fpad, hipStream_t s) {
+  const int64_t tot = (int64_t)(W + 1) * Fpad;
+  hipLaunchKernelGGL(k_deep_transpose, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                     (const unsigned long long*)bm, (long long)Wp, (long long)F, W, W_real, ids,
+                     (unsigned long long*)root, (long long)Fpad);
+}
+
+void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t minsup,
+               int32_t* m, const int64_t* blk_off, char* base, DeepCtl* ctl, bool fill,
+               hipStream_t s) {
+  const unsigned grid = (unsigned)((F + 3) / 4);
+  if (!grid) return;
+  by_width(W, [&](auto wt) {
+    hipLaunchKernelGGL(k_deep_root<decltype(wt)::value>, dim3(grid), dim3(256), 0, s,
+                       (const unsigned long long*)root, (long long)Fpad, (long long)F, W, minsup,
+                       m, (const long long*)blk_off, base, ctl, fill ? 1 : 0);
+  });
+}
+
+void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
+                     char* base, const uint64_t* root, int64_t Fpad, int W, int rank, int world,
+                     DeepFrame* out, hipStream_t s) {
+  if (F <= 0) return;
+  hipLaunchKernelGGL(k_deep_root_tasks, dim3((unsigned)F), dim3(256), 0, s,
+                     (const long long*)blk_off, m, (const long long*)task_off, (long long)F, base,
+                     (const unsigned long long*)root, (long long)Fpad, W, rank, world, out);
+}
+
+void deep_count(const DeepArgs& a, int grid, hipStream_t s) {
+  by_width(a.W, [&](auto wt) {
+    hipLaunchKernelGGL(k_deep_count<decltype(wt)::value>, dim3((unsigned)grid),
+                       dim3(64 * kWaves), 0, s, a);
+  });
+}
+
+}  // namespace kern
+}  // namespace kmls

@@ -8,6 +8,60 @@
 namespace kmls {
 namespace kern {
 
+// ---- count-only deep mining (deep.hip) ----
+struct DeepFrame {  // one class: members P ∪ {x_k}, k in [s0, s0 + m), of a word-major block
+  unsigned long long blk;   // device address: W words x pad slots ([w][slot]), then pad item hashes
+  unsigned long long hash;  // set hash of the prefix P
+  unsigned pad;             // slot stride (multiple of 16)
+  unsigned s0;              // first member slot
+  unsigned m;               // members
+  unsigned meta;            // bits 0-7 |P|, bit 8 single (expand member s0 only), 16-31 block index
+};
+static_assert(sizeof(DeepFrame) == 32, "DeepFrame is read as 8 dwords");
+struct DeepCtl {  // per-round control + accumulated results (zeroed once per call)
+  unsigned long long next_task;   // dequeue ticket (zeroed per round)
+  unsigned long long n_out;       // tasks spilled to the out queue (zeroed per round)
+  unsigned long long heap_top;    // bytes of the out heap used (zeroed per round)
+  unsigned long long digest_sum, digest_xor;
+  unsigned long long candidates, chunks;
+  unsigned long long per_depth[64];
+  unsigned error;                 // bit 0 out queue full, bit 1 heap full, bit 2 timeout
+  unsigned pad_[3];
+};
+struct DeepArgs {
+  const DeepFrame* in;
+  long long n_in;
+  DeepFrame* out;
+  long long out_cap;
+  char* heap;
+  unsigned long long heap_cap;
+  char* stacks;                   // per wave: stack_bytes of blocks
+  unsigned long long stack_bytes;
+  DeepFrame* fstacks;             // per wave: fcap frames
+  int fcap;
+  DeepCtl* ctl;
+  int W;
+  unsigned minsup;
+  unsigned long long budget;      // 64-lane passes per task before it spills
+  int max_len;                    // 0 = all sizes
+  unsigned split_min;             // spilled frames above this many members split per member
+  unsigned long long timeout_ticks;  // wall_clock64 ticks a wave may run (then error bit 2)
+};
+int deep_max_words();
+int deep_row_words(int W);  // instantiated row width >= W (blocks are padded with zero words)
+int deep_waves_per_block();
+int deep_min_fcap();
+size_t deep_row_block_bytes(int W, int64_t m);  // stack room one step over m members may need
+void deep_transpose(const uint64_t* bm, int64_t Wp, int64_t F, int W, int W_real,
+                    const int32_t* ids, uint64_t* root, int64_t Fpad, hipStream_t s);
+void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t minsup,
+               int32_t* m, const int64_t* blk_off, char* base, DeepCtl* ctl, bool fill,
+               hipStream_t s);
+void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
+                     char* base, const uint64_t* root, int64_t Fpad, int W, int rank, int world,
+                     DeepFrame* out, hipStream_t s);
+void deep_count(const DeepArgs& a, int grid, hipStream_t s);
+
 // ---- mining (mine.hip) ----
 void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* counts,
                   hipStream_t s);

@@ -1,0 +1,56 @@
+"""The count-only deep GPU miner's own kernel source, run on the CPU wave emulator (csrc/emu).
+
+csrc/kernels/deep.hip and csrc/host/deep_run.hip are compiled by g++ against the emulator's HIP
+shim (one host thread per lane, cross-lane ops through barriers) with AddressSanitizer and
+UBSan; the per-size counts and the content digest must equal the CPU count miner's.  Small step
+budgets force spill rounds; world > 1 splits the level-3 tasks over simulated ranks.
+"""
+import os
+import pathlib
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+BIN = ROOT / "build" / "emu" / "deep_emu"
+
+
+def _build():
+    srcs = [ROOT / "csrc/kernels/deep.hip", ROOT / "csrc/host/deep_run.hip"]
+    host = [ROOT / f"csrc/host/{f}" for f in ("miner_cpu.cpp", "synth.cpp", "digest.cpp")]
+    main = ROOT / "csrc/tests/deep_emu_main.cpp"
+    deps = srcs + host + [main] + list((ROOT / "csrc/emu").rglob("*")) + \
+        list((ROOT / "csrc/include").rglob("*.hpp")) + [ROOT / "csrc/kernels/kernels.hpp",
+                                                        ROOT / "csrc/host/deep_run.hpp"]
+    if BIN.exists() and BIN.stat().st_mtime >= max(p.stat().st_mtime for p in deps if p.is_file()):
+        return
+    BIN.parent.mkdir(parents=True, exist_ok=True)
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+           "-fno-omit-frame-pointer", f"-I{ROOT / 'csrc/emu'}", f"-I{ROOT / 'csrc/include'}",
+           "-x", "c++"] + [str(s) for s in srcs] + ["-x", "none"] + [str(h) for h in host] + \
+          [str(main), "-lpthread", "-o", str(BIN)]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+
+
+@pytest.fixture(scope="module")
+def emu_bin():
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not available")
+    _build()
+    return BIN
+
+
+@pytest.mark.parametrize("args", [
+    # n_tx n_items mean_len genres affinity min_support [budget0 budget split_min stack_mb world max_len]
+    "400 60 20 3 0.9 0.05",
+    "400 60 20 3 0.9 0.05 1 1 2",          # every task spills, per-member splits
+    "300 50 25 2 0.95 0.08 1 2 4 1 3 0",   # 3 simulated ranks + spills
+    "300 50 25 2 0.95 0.08 4 4 64 1 1 4",  # max_len
+])
+def test_deep_kernel_on_emulator(emu_bin, args):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([str(emu_bin)] + args.split(), capture_output=True, text=True,
+                       timeout=900, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert '"ok": true' in r.stdout

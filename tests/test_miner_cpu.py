@@ -140,3 +140,16 @@ def test_ds2_shape_calibration():
     curve = dict(item_support_curve(tx, [0.03, 0.05, 0.1]))
     assert abs(curve[0.05] - 755) < 80 and abs(curve[0.03] - 1571) < 120
     assert abs(curve[0.1] - 121) < 30
+
+
+@pytest.mark.parametrize("ms,max_len", [(0.05, 0), (0.04, 0), (0.04, 3), (0.05, 2)])
+def test_count_digest_equals_trie_digest(native_mod, ms, max_len):
+    """mine_cpu_count's digest (no trie) is the digest of the full CPU trie."""
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    tx = generate("ds1", seed=0)
+    c = native_mod.mine_cpu_count(tx.tx_ptr, tx.items, tx.n_items, ms, max_len)
+    r = native_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, max_len)
+    d = native_mod.trie_digest(r["parent"], r["item"], r["count"], r["depth"])
+    assert c["digest"] == d["digest"]
+    assert c["per_level"][1:] == d["per_depth"][1:]
+    assert c["n_itemsets"] == d["n"]
