@@ -332,4 +332,5 @@ PYBIND11_MODULE(_native, m) {
 
   // ---------------- HIP runtime ----------------
   register_gpu_bindings(m);
+  register_front_bindings(m);
 }

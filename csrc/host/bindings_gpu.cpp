@@ -315,7 +315,7 @@ void register_gpu_bindings(py::module_& m) {
          py::arg("split_min") = 4u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0)
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
-  py::class_<gpu::GpuRuleIndex>(m, "GpuRuleIndex")
+  py::class_<gpu::GpuRuleIndex, std::shared_ptr<gpu::GpuRuleIndex>>(m, "GpuRuleIndex")
       .def(py::init<int, const RuleIndex&, uintptr_t>(), py::arg("device"), py::arg("index"),
            py::arg("stream") = 0)
       .def_property_readonly("nnz", &gpu::GpuRuleIndex::nnz)

@@ -20,6 +20,7 @@ namespace pybind11 { class module_; }
 namespace kmls {
 
 void register_gpu_bindings(pybind11::module_& m);
+void register_front_bindings(pybind11::module_& m);  // bindings_front.cpp
 
 namespace gpu {
 

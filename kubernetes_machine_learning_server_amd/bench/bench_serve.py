@@ -1,14 +1,24 @@
 """Serving benchmark: p50/p99 latency of POST /api/recommend/ at fixed offered QPS.
 
-BASELINE.json's second metric.  Open-loop load (requests are issued on a fixed schedule, not
-when the previous one returns, so queueing shows up as latency): ``--clients`` processes each
-run an asyncio/aiohttp loop at QPS/clients.  The server is the real uvicorn app (``--workers``
-processes) over a PVC directory populated by the real job on ds1-shaped synthetic data.
-Backends: ``hip`` (HBM index + micro-batched HIP matcher), ``cpu`` (C++ matcher), ``python``
-(the reference's own dict/defaultdict/sorted matcher, rest_api/app/main.py:224-254) — all in
-the same harness.  Also ``--matcher-only``: in-process matcher throughput without HTTP.
+BASELINE.json's second metric (config 4: 10k QPS, HBM-resident rule index, 1 MI355X).
 
-  python -m kubernetes_machine_learning_server_amd.bench.bench_serve --backend cpu --qps 1000,5000
+* Load: the native open-loop generator (``_native.loadgen``, csrc/host/loadgen.cpp): request i
+  is due at t0 + i/QPS on keep-alive connection i % C; latency is measured from that SCHEDULED
+  time, so server stalls show up as latency (no coordinated omission).  ``--client python``
+  keeps the older aiohttp client processes for comparison.
+* Server: ``--front native`` (default; C++ HTTP I/O threads in front of the FastAPI app, GPU
+  matching in-process, serve/front.py) or ``--front uvicorn`` (the pure FastAPI stack,
+  ``--workers`` processes), over a PVC directory populated by the real job on ds1-shaped data.
+* Backends: ``hip`` (every request through the HIP matcher over the HBM index), ``auto`` (HIP
+  only for batches past the crossover measured at load), ``cpu`` (C++ matcher), ``python`` (the
+  reference's own dict/defaultdict/sorted matcher, rest_api/app/main.py:224-254).
+* ``--capacity``: the QPS is raised (x2, then bisected) to the highest rate answered with
+  p99 < 5 ms and no errors.
+* The bench process never initialises the GPU itself (the PVC is mined by the CPU miner, whose
+  artifact is identical): the server is a fresh child process.
+* ``--matcher-only``: in-process matcher throughput without HTTP.
+
+  python -m kubernetes_machine_learning_server_amd.bench.bench_serve --backend auto --qps 2000,10000 --capacity
 """
 from __future__ import annotations
 
@@ -24,14 +34,14 @@ import subprocess
 import sys
 import tempfile
 import time
-from typing import List
+from typing import List, Optional
 
 import numpy as np
 
 ROOT = pathlib.Path(__file__).resolve().parents[2]
 
 
-def prepare_pvc(root: pathlib.Path, shape: str = "ds1", ms: float = 0.05, miner: str = "auto"):
+def prepare_pvc(root: pathlib.Path, shape: str = "ds1", ms: float = 0.05, miner: str = "cpu"):
     from ..config import JobSettings
     from ..data.synthetic import generate, to_reference_csv
     from ..job import main as job
@@ -70,13 +80,15 @@ def _free_port() -> int:
     return p
 
 
-def start_server(base: pathlib.Path, backend: str, workers: int, port: int):
+def start_server(base: pathlib.Path, backend: str, workers: int, port: int,
+                 front: str = "native", threads: int = 4):
     env = dict(os.environ)
     env.update(BASE_DIR=str(base) + "/", PICKLE_DIR="pickles/", SERVE_BACKEND=backend,
                KMLS_LOG_LEVEL="ERROR", POLLING_WAIT_IN_MINUTES="60",
                PYTHONPATH=str(ROOT) + os.pathsep + env.get("PYTHONPATH", ""))
     cmd = [sys.executable, "-m", "kubernetes_machine_learning_server_amd.serve", "--host",
-           "127.0.0.1", "--port", str(port), "--workers", str(workers), "--log-level", "error"]
+           "127.0.0.1", "--port", str(port), "--front", front, "--threads", str(threads),
+           "--workers", str(workers), "--log-level", "error"]
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                             start_new_session=True)
     import urllib.request
@@ -138,6 +150,95 @@ def _client(port: int, qps: float, duration: float, queries, t_start: float, out
         return lat, errs
     lat, errs = asyncio.run(run())
     out_q.put((lat, errs))
+
+
+def request_bytes(queries, port: int) -> List[bytes]:
+    """Complete HTTP/1.1 requests for the native load generator (keep-alive)."""
+    out = []
+    for q in queries:
+        body = json.dumps({"songs": q}, ensure_ascii=False).encode("utf-8")
+        out.append(b"POST /api/recommend/ HTTP/1.1\r\nhost: 127.0.0.1:%d\r\n"
+                   b"content-type: application/json\r\ncontent-length: %d\r\n\r\n"
+                   % (port, len(body)) + body)
+    return out
+
+
+def measure_native(port: int, qps: float, duration: float, queries, connections: int = 64,
+                   threads: int = 2) -> dict:
+    from ..ops import native
+    N = native.load()
+    r = N.loadgen("127.0.0.1", port, request_bytes(queries, port), float(qps), float(duration),
+                  connections, threads, 5.0)
+    a = np.asarray(r["lat_ns"], np.float64) / 1e6
+    lag = np.asarray(r["lag_ns"], np.float64) / 1e6
+    if len(a) == 0:
+        a = lag = np.full(1, np.inf)
+    unanswered = int(r["offered"] - r["completed"])
+    return {"offered_qps": qps, "completed": int(r["completed"]), "errors": int(r["errors"]),
+            "unanswered": unanswered, "achieved_qps": round(r["completed"] / duration, 1),
+            "p50_ms": round(float(np.percentile(a, 50)), 3),
+            "p90_ms": round(float(np.percentile(a, 90)), 3),
+            "p99_ms": round(float(np.percentile(a, 99)), 3),
+            "p999_ms": round(float(np.percentile(a, 99.9)), 3),
+            "max_ms": round(float(a.max()), 3), "mean_ms": round(float(a.mean()), 3),
+            "send_lag_p99_ms": round(float(np.percentile(lag, 99)), 3),
+            "latency_from": "scheduled send time", "connections": connections}
+
+
+def capacity(port: int, queries, start_qps: float = 10000.0, duration: float = 2.0,
+             p99_ms: float = 5.0, max_qps: float = 400000.0, connections: int = 128,
+             threads: int = 2) -> dict:
+    """Highest offered QPS answered with p99 < p99_ms (from scheduled time) and no errors:
+    doubling from start_qps, then two bisection steps."""
+    ok_q, ok_r, bad_q, trail = None, None, None, []
+
+    def good(r):
+        return r["errors"] == 0 and r["unanswered"] == 0 and r["p99_ms"] < p99_ms
+
+    q = start_qps
+    while q <= max_qps:
+        r = measure_native(port, q, duration, queries, connections, threads)
+        trail.append({k: r[k] for k in ("offered_qps", "achieved_qps", "p50_ms", "p99_ms",
+                                        "errors", "unanswered")})
+        if good(r):
+            ok_q, ok_r = q, r
+            q *= 2
+        else:
+            bad_q = q
+            break
+    if ok_q is not None and bad_q is not None:
+        for _ in range(2):
+            mid = (ok_q + bad_q) / 2
+            r = measure_native(port, mid, duration, queries, connections, threads)
+            trail.append({k: r[k] for k in ("offered_qps", "achieved_qps", "p50_ms", "p99_ms",
+                                            "errors", "unanswered")})
+            if good(r):
+                ok_q, ok_r = mid, r
+            else:
+                bad_q = mid
+    return {"max_qps_p99_under_ms": p99_ms, "capacity_qps": ok_q,
+            "at_capacity": ok_r and {k: ok_r[k] for k in ("p50_ms", "p99_ms", "achieved_qps")},
+            "limit_hit": bad_q is None, "trail": trail}
+
+
+def cpu_info(server_pid: Optional[int] = None) -> dict:
+    out = {"os_cpu_count": os.cpu_count()}
+    try:
+        out["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except Exception:
+        pass
+    if server_pid:
+        try:
+            import psutil
+            p = psutil.Process(server_pid)
+            t = p.cpu_times()
+            out["server_cpu_s"] = round(t.user + t.system, 3)
+            out["server_threads"] = p.num_threads()
+        except Exception:
+            pass
+    t = os.times()
+    out["bench_cpu_s"] = round(t.user + t.system, 3)
+    return out
 
 
 def measure(port: int, qps: float, duration: float, clients: int, queries) -> dict:
@@ -212,11 +313,17 @@ def matcher_bench(base: pathlib.Path, n_queries: int = 20000) -> dict:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--backend", default="cpu", help="hip | cpu | python | auto")
-    ap.add_argument("--qps", default="1000,5000,10000")
-    ap.add_argument("--duration", type=float, default=10.0)
-    ap.add_argument("--workers", type=int, default=4)
-    ap.add_argument("--clients", type=int, default=4)
+    ap.add_argument("--backend", default="auto", help="hip | cpu | python | auto")
+    ap.add_argument("--qps", default="2000,5000,10000")
+    ap.add_argument("--duration", type=float, default=5.0)
+    ap.add_argument("--front", choices=("native", "uvicorn"), default="native")
+    ap.add_argument("--threads", type=int, default=4, help="native front I/O threads")
+    ap.add_argument("--workers", type=int, default=4, help="uvicorn front workers")
+    ap.add_argument("--client", choices=("native", "python"), default="native")
+    ap.add_argument("--clients", type=int, default=8, help="python client processes")
+    ap.add_argument("--connections", type=int, default=64)
+    ap.add_argument("--capacity", action="store_true", help="find the max QPS with p99 < 5 ms")
+    ap.add_argument("--json-out", default=None, help="also write the summary JSON here")
     ap.add_argument("--matcher-only", action="store_true")
     ap.add_argument("--pvc", default=None, help="reuse a populated PVC dir")
     a = ap.parse_args(argv)
@@ -228,26 +335,67 @@ def main(argv=None) -> int:
     if a.matcher_only:
         print(json.dumps({"bench": "matcher", **matcher_bench(base)}), flush=True)
         return 0
+    summary = run_serve_bench(base, a.backend, [float(x) for x in a.qps.split(",") if x],
+                              a.duration, a.front, a.threads, a.workers, a.client, a.clients,
+                              a.connections, a.capacity, verbose=True)
+    print(json.dumps({"bench": "serve_summary", **summary}), flush=True)
+    if a.json_out:
+        pathlib.Path(a.json_out).write_text(json.dumps(summary))
+    return 0
+
+
+def run_serve_bench(base: pathlib.Path, backend: str, qps_list, duration: float,
+                    front: str = "native", threads: int = 4, workers: int = 4,
+                    client: str = "native", clients: int = 8, connections: int = 64,
+                    with_capacity: bool = True, verbose: bool = False) -> dict:
+    """Start the server (a fresh child process), run the fixed-QPS points and the capacity
+    search, stop the server.  Returns the summary dict (bench.py's ``serve`` block)."""
     queries = make_queries(base, 50000)
     port = _free_port()
-    proc = start_server(base, a.backend, a.workers, port)
+    t_start = time.time()
+    proc = start_server(base, backend, workers, port, front=front, threads=threads)
+    res = {"backend": backend, "front": front,
+           "threads" if front == "native" else "workers": threads if front == "native" else workers,
+           "client": client, "duration_s": duration, "points": []}
     try:
         import urllib.request
         with urllib.request.urlopen(f"http://127.0.0.1:{port}/readyz", timeout=5) as r:
             ready = json.loads(r.read())
-        print(json.dumps({"bench": "serve_ready", "backend": a.backend,
-                          "gpu_index": ready.get("gpu_index"),
-                          "gpu_min_batch": ready.get("gpu_min_batch"),
-                          "crossover_us": ready.get("crossover_us")}), flush=True)
-        measure(port, 200, 2.0, 1, queries)  # warm-up
-        for qps in [float(x) for x in a.qps.split(",")]:
-            r = measure(port, qps, a.duration, a.clients, queries)
-            r.update(bench="serve", backend=a.backend, workers=a.workers, clients=a.clients,
-                     duration_s=a.duration)
-            print(json.dumps(r), flush=True)
+        res["server_ready_s"] = round(time.time() - t_start, 2)
+        res["gpu_index"] = ready.get("gpu_index")
+        res["gpu_min_batch"] = ready.get("gpu_min_batch")
+        res["crossover_us"] = ready.get("crossover_us")
+        if verbose:
+            print(json.dumps({"bench": "serve_ready", **{k: res[k] for k in
+                  ("backend", "gpu_index", "gpu_min_batch", "crossover_us")}}), flush=True)
+        # warm-up
+        if client == "native":
+            measure_native(port, 500, 1.0, queries, connections)
+        else:
+            measure(port, 200, 1.0, 1, queries)
+        for qps in qps_list:
+            if client == "native":
+                r = measure_native(port, qps, duration, queries, connections)
+            else:
+                r = measure(port, qps, duration, clients, queries)
+            res["points"].append(r)
+            if verbose:
+                print(json.dumps({"bench": "serve", **r}), flush=True)
+        if with_capacity and client == "native":
+            res["capacity"] = capacity(port, queries, start_qps=max(qps_list or [10000.0]) * 2)
+            if verbose:
+                print(json.dumps({"bench": "capacity", **res["capacity"]}), flush=True)
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+                m = r.read().decode()
+            res["front_stats"] = {ln.split()[0][len("kmls_front_"):]: int(float(ln.split()[1]))
+                                  for ln in m.splitlines() if ln.startswith("kmls_front_")}
+        except Exception:
+            pass
+        res["cpu"] = cpu_info(proc.pid)
     finally:
         stop_server(proc)
-    return 0
+    return res
 
 
 if __name__ == "__main__":

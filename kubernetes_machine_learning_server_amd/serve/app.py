@@ -78,22 +78,13 @@ def _python_match(snap, seeds, k):
     return recommend_oracle(rec, seeds, k)
 
 
-def _gpu_factory(cfg: ApiSettings, allow_owner: bool = True):
-    """HBM index builder for SERVE_BACKEND=hip|auto (None → CPU matcher only).  Under the
-    multi-worker runner (KMLS_GPU_OWNER_SOCKET set) a worker never opens the GPU: its "GPU index"
-    is a client of the one GPU-owning process (serve/gpu_owner.py)."""
-    if cfg.serve_backend in ("cpu", "python"):
+def _gpu_factory(cfg: ApiSettings):
+    """HBM index builder for SERVE_BACKEND=hip|auto (None → CPU matcher only).  The GPU serving
+    process is the native front (serve/front.py: one process, the HIP matcher micro-batched
+    across its I/O threads in-process); uvicorn workers of the multi-process runner stay on the
+    C++ matcher (KMLS_NO_GPU=1 is set for them), so no two processes share one card's index."""
+    if cfg.serve_backend in ("cpu", "python") or os.environ.get("KMLS_NO_GPU") == "1":
         return None
-    owner = os.environ.get("KMLS_GPU_OWNER_SOCKET")
-    if allow_owner and owner:
-        from .gpu_owner import OwnerClient
-        from .index import index_fingerprint
-
-        def build_client(index):
-            if not os.path.exists(owner):  # the owner found no GPU (or is gone)
-                return None
-            return OwnerClient(owner, index_fingerprint(index))
-        return build_client
     from ..ops import native
     if not native.gpu_available():
         if cfg.serve_backend == "hip":
@@ -124,7 +115,10 @@ class _Metrics:
                                  registry=self.registry)
 
 
-def create_app(cfg: Optional[ApiSettings] = None) -> FastAPI:
+def create_app(cfg: Optional[ApiSettings] = None, native_front: bool = False) -> FastAPI:
+    """``native_front``: the app sits behind serve/front.py, which answers the hot route itself
+    (and owns the GPU batching); requests that reach this app's route are the rare ones the
+    front hands over, answered here by the C++ matcher."""
     cfg = cfg or ApiSettings.from_env()
     _setup_logging()
     logger.info("API is starting up")
@@ -166,6 +160,7 @@ def create_app(cfg: Optional[ApiSettings] = None) -> FastAPI:
     app.state.cfg = cfg
     app.state.batcher = batcher
     app.state.metrics = metrics
+    app.state.front = None  # serve/front.py sets its _native.HttpFront here
 
     @app.get("/test", tags=["util"], include_in_schema=False)
     def redirect_to_doc():
@@ -182,7 +177,7 @@ def create_app(cfg: Optional[ApiSettings] = None) -> FastAPI:
         if cfg.serve_backend == "python":
             # the reference's own matcher (dict-of-dicts + defaultdict + sorted), for A/B benches
             res = _python_match(snap, seeds, k)
-        elif (snap.gpu_index is not None and snap.gpu_min_batch is not None
+        elif (not native_front and snap.gpu_index is not None and snap.gpu_min_batch is not None
               and inflight[0] >= batcher._gpu_min(snap)):
             # enough requests in flight to fill a batch the HIP matcher answers faster (the
             # crossover measured on this index): queue for the micro-batcher.  Below that the
@@ -252,8 +247,12 @@ def create_app(cfg: Optional[ApiSettings] = None) -> FastAPI:
         if snap is not None:
             metrics.keys.set(snap.index.n_keys)
             metrics.nnz.set(snap.index.nnz)
-        return PlainTextResponse(generate_latest(metrics.registry).decode(),
-                                 media_type="text/plain; version=0.0.4")
+        text = generate_latest(metrics.registry).decode()
+        front = app.state.front
+        if front is not None:  # the native front's own counters (its hot route bypasses this app)
+            for k, v in front.stats().items():
+                text += f"# TYPE kmls_front_{k} counter\nkmls_front_{k} {v}\n"
+        return PlainTextResponse(text, media_type="text/plain; version=0.0.4")
 
     return app
 

@@ -189,16 +189,3 @@ def build_index_from_trie(parent, item, count, depth, n_tx: int, n_items: int,
     m2 = depth == 2
     return build_index_from_pairs(n_items, item[m1], item[parent[m2]], item[m2], count[m2],
                                   n_tx, names)
-
-
-def index_fingerprint(ix: RuleIndexData) -> int:
-    """64-bit content fingerprint of a rule index (row_ptr, consequents, scores, keys): the GPU
-    owner answers a worker only when both hold the same model (serve/gpu_owner.py)."""
-    import zlib
-    c, a = 0, 1
-    for arr in (ix.row_ptr, ix.cons, ix.score, ix.is_key):
-        b = memoryview(np.ascontiguousarray(arr)).cast("B")
-        c = zlib.crc32(b, c)
-        a = zlib.adler32(b, a)
-    return ((c & 0xFFFFFFFF) << 32) | (a & 0xFFFFFFFF)
-

@@ -9,11 +9,12 @@ C++ matcher (``_native.RuleIndex.query``) or, batched across requests, by the HI
 Static fallback (A8, ``main.py:205-222``): a seeded sample of K best tracks.  The reference
 seeds the GLOBAL RNG with the process-salted ``hash(tuple(sorted(seeds)))`` (different on each
 replica, Appendix B.8) and raises if fewer than K best tracks exist (B.5).  Here the seed is a
-stable SHA-256 of the sorted seeds, a private ``random.Random`` is used, and K is clamped.
+stable FNV-1a 64 hash of the sorted seeds, a private ``random.Random`` is used, and K is clamped.
+The native serving front (csrc/host/http_front.cpp) computes the same seed and reproduces
+``random.Random(seed).sample`` bit-exactly, so both paths return the same fallback list.
 """
 from __future__ import annotations
 
-import hashlib
 import random
 from typing import List, Optional, Sequence
 
@@ -24,9 +25,15 @@ from .state import ModelSnapshot
 NO_RECOMMENDATIONS = "No recommendations available at the moment"
 
 
+_FNV_OFFSET, _FNV_PRIME, _M64 = 0xCBF29CE484222325, 0x100000001B3, (1 << 64) - 1
+
+
 def stable_seed(seeds: Sequence[str]) -> int:
-    h = hashlib.sha256("\x1f".join(sorted(seeds)).encode("utf-8")).digest()
-    return int.from_bytes(h[:8], "little")
+    """FNV-1a 64 of ``"\\x1f".join(sorted(seeds))`` in UTF-8 (== _native.fallback_seed)."""
+    h = _FNV_OFFSET
+    for b in "\x1f".join(sorted(seeds)).encode("utf-8"):
+        h = ((h ^ b) * _FNV_PRIME) & _M64
+    return h
 
 
 def static_recommendation(snap: Optional[ModelSnapshot], seeds: Sequence[str], k: int) -> List[str]:

@@ -1,12 +1,15 @@
-"""Multi-process server launcher: one SO_REUSEPORT socket per worker process.
+"""Server launchers.
 
-uvicorn's own ``--workers N`` mode binds the socket in the supervisor and hands the fd to the
-workers; the inherited socket object reports ``proto == 0``, so asyncio's transport never sets
-TCP_NODELAY on accepted connections and every response pays Nagle + the client's 40 ms delayed
-ACK (measured: p50 44 ms at 500 QPS vs 1 ms with one worker).  Here each worker creates its own
-``socket(AF_INET, SOCK_STREAM, IPPROTO_TCP)`` with SO_REUSEPORT on the same port — the kernel
-load-balances connections across workers and NODELAY is applied — and serves it with
-``uvicorn.Server``.  Each worker is a full app instance (its own model snapshot / HBM index).
+* ``native`` (default): serve/front.py — one process, C++ HTTP I/O threads, the FastAPI app
+  behind them for every route the front does not answer itself, GPU matching in-process.
+* ``uvicorn``: the pure FastAPI/uvicorn stack (the reference's own serving stack),
+  ``workers`` processes.  uvicorn's own ``--workers N`` mode binds the socket in the supervisor
+  and hands the fd to the workers; the inherited socket object reports ``proto == 0``, so
+  asyncio's transport never sets TCP_NODELAY on accepted connections and every response pays
+  Nagle + the client's 40 ms delayed ACK.  Here each worker creates its own
+  ``socket(AF_INET, SOCK_STREAM, IPPROTO_TCP)`` with SO_REUSEPORT on the same port — the kernel
+  load-balances connections and NODELAY is applied.  Multi-worker uvicorn stays on the C++
+  matcher (the GPU belongs to one process: use the native front for HIP serving).
 """
 from __future__ import annotations
 
@@ -14,8 +17,6 @@ import multiprocessing as mp
 import os
 import signal
 import socket
-import sys
-import time
 from typing import List
 
 
@@ -41,40 +42,17 @@ def _worker(host: str, port: int, reuse_port: bool, log_level: str) -> None:
     server.run(sockets=[sock])
 
 
-def _owner(path: str) -> None:
-    from .gpu_owner import owner_main
-    sys.exit(owner_main(path))
-
-
-def _start_owner(ctx, workers: int):
-    """The GPU-owning matcher process (serve/gpu_owner.py) for multi-worker GPU serving: started
-    first; workers find its socket through KMLS_GPU_OWNER_SOCKET.  This launcher never touches
-    the GPU itself (a process that has initialised HIP must not fork+exec workers)."""
-    backend = os.environ.get("SERVE_BACKEND", "auto").lower()
-    if workers <= 1 or backend not in ("auto", "hip") or os.environ.get("KMLS_GPU_OWNER") == "0":
-        return None
-    path = os.environ.get("KMLS_GPU_OWNER_SOCKET") or f"/tmp/kmls_gpu_owner_{os.getpid()}.sock"
-    os.environ["KMLS_GPU_OWNER_SOCKET"] = path
-    p = ctx.Process(target=_owner, args=(path,), daemon=False)
-    p.start()
-    deadline = time.time() + float(os.environ.get("KMLS_GPU_OWNER_WAIT_S", "180"))
-    while time.time() < deadline and p.is_alive() and not os.path.exists(path):
-        time.sleep(0.1)
-    return p
-
-
 def run(host: str = "0.0.0.0", port: int = 80, workers: int = 1, log_level: str = "info") -> int:
+    """uvicorn front (``--front uvicorn``)."""
     if workers <= 1:
         _worker(host, port, False, log_level)
         return 0
+    os.environ["KMLS_NO_GPU"] = "1"  # inherited by the spawned workers
     ctx = mp.get_context("spawn")
-    owner = _start_owner(ctx, workers)
     procs: List[mp.Process] = [ctx.Process(target=_worker, args=(host, port, True, log_level),
                                            daemon=False) for _ in range(workers)]
     for p in procs:
         p.start()
-    if owner is not None:
-        procs.append(owner)
 
     def stop(signum, frame):
         for p in procs:

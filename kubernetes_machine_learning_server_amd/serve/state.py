@@ -133,6 +133,8 @@ class ReloadManager:
         self._lock = threading.Lock()
         self._gpu_factory = gpu_factory
         self.last_reload_seconds = 0.0
+        # called with every new snapshot right after the swap (the native front's model push)
+        self.listeners: List[Any] = []
 
     # -- reference-compatible accessors -------------------------------------------------
     @property
@@ -176,11 +178,6 @@ class ReloadManager:
         try:
             best, index, source = read_pickle_dict(self.cfg)
             gpu_index = self._gpu_factory(index) if self._gpu_factory else None
-            if gpu_index is not None and hasattr(gpu_index, "wait_ready"):
-                # GPU-owner client: the owner must have loaded this very model first
-                if not gpu_index.wait_ready():
-                    logger.error("GPU owner has not loaded this model: CPU matcher only")
-                    gpu_index = None
             gmb, cross = None, None
             if gpu_index is not None:
                 if self.cfg.serve_backend == "hip":  # forced: every batch on the GPU
@@ -200,6 +197,11 @@ class ReloadManager:
             logger.info(f"HIP matcher crossover: batches >= {gmb} go to the GPU" if gmb else
                         "HIP matcher never beats the C++ matcher on this index: CPU only")
         self.snapshot = snap  # single reference assignment = atomic swap
+        for fn in list(self.listeners):
+            try:
+                fn(snap)
+            except Exception as e:  # a listener must not undo a good reload
+                logger.error(f"snapshot listener failed: {e!r}")
         self.reload_counter += 1
         self.last_error = None
         self.last_reload_seconds = time.perf_counter() - t0

@@ -249,85 +249,3 @@ def test_router_uses_gpu_only_past_the_measured_crossover(pvc, monkeypatch, back
             got = c.post("/api/recommend/", json={"songs": [sd]}).json()["songs"]
             assert got == oracle.recommend_oracle(rec, [sd], 10)
     assert made and (made[-1].calls > 0) == expect_gpu
-
-
-def _start_owner(tmp_path, source):
-    from kubernetes_machine_learning_server_amd.serve.gpu_owner import GpuOwner
-    owner = GpuOwner(str(tmp_path / "owner.sock"), source)
-    th = threading.Thread(target=owner.serve_forever, daemon=True)
-    th.start()
-    return owner, th
-
-
-def test_gpu_owner_fuses_worker_batches(pvc, tmp_path):
-    """One GPU-owning process answers every worker (serve/gpu_owner.py): concurrent clients'
-    batches go through shared memory, come back equal to the C++ matcher, and are fused into
-    fewer launches; a client holding another model gets -2 (its CPU path answers)."""
-    from kubernetes_machine_learning_server_amd.serve.gpu_owner import OwnerClient
-    from kubernetes_machine_learning_server_amd.serve.index import RuleIndexData, index_fingerprint
-    idx = RuleIndexData.load(pvc / "api-data" / "pickles" / "rules.idx")
-    fake = _FakeGpuIndex(idx)
-    fp = index_fingerprint(idx)
-    owner, th = _start_owner(tmp_path, lambda: (fp, fake))
-    try:
-        keys = np.nonzero(idx.is_key)[0].astype(np.int32)
-        rng = np.random.default_rng(0)
-        errors = []
-
-        def worker(seed):
-            r = np.random.default_rng(seed)
-            cl = OwnerClient(owner.path, fp)
-            assert cl.wait_ready(5.0)
-            for _ in range(30):
-                B = int(r.integers(1, 40))
-                lens = r.integers(1, 5, size=B)
-                q = np.zeros(B + 1, np.int64)
-                np.cumsum(lens, out=q[1:])
-                s = keys[r.integers(0, len(keys), int(q[-1]))]
-                got = cl.query_batch(q, s, 10)
-                want = idx.native().query_batch(q, s, 10)
-                if not (np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])):
-                    errors.append(seed)
-            cl.close()
-        ts = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-        assert not errors
-        assert owner.queries >= 4 * 30 and owner.batches <= 4 * 30
-        other = OwnerClient(owner.path, fp ^ 1)  # a worker still on another model
-        q = np.array([0, 1], np.int64)
-        ids, n = other.query_batch(q, keys[:1], 10)
-        assert (n == -2).all() and not other.wait_ready(0.2)
-        other.close()
-        del rng
-    finally:
-        owner.stop()
-        th.join(timeout=5)
-
-
-def test_app_workers_use_the_gpu_owner(pvc, tmp_path, monkeypatch):
-    """With KMLS_GPU_OWNER_SOCKET set (the multi-worker runner), a worker's HIP backend is a
-    client of the owner: requests are answered through it, identically to the reference."""
-    from kubernetes_machine_learning_server_amd.serve import state as state_mod
-    from kubernetes_machine_learning_server_amd.serve.gpu_owner import OwnerClient
-    from kubernetes_machine_learning_server_amd.serve.index import RuleIndexData, index_fingerprint
-    idx = RuleIndexData.load(pvc / "api-data" / "pickles" / "rules.idx")
-    fake = _FakeGpuIndex(idx)
-    owner, th = _start_owner(tmp_path, lambda: (index_fingerprint(idx), fake))
-    monkeypatch.setenv("KMLS_GPU_OWNER_SOCKET", owner.path)
-    monkeypatch.setattr(state_mod, "measure_crossover", lambda index, g: (1, {}))
-    try:
-        rec = rec_dict(pvc)
-        seeds = [k for k, v in rec.items() if v][:10]
-        with TestClient(create_app(api_settings(pvc, serve_backend="hip"))) as c:
-            snap = c.app.state.mgr.snapshot
-            assert isinstance(snap.gpu_index, OwnerClient)
-            for sd in seeds:
-                got = c.post("/api/recommend/", json={"songs": [sd]}).json()["songs"]
-                assert got == oracle.recommend_oracle(rec, [sd], 10)
-        assert fake.calls > 0 and owner.queries >= len(seeds)
-    finally:
-        owner.stop()
-        th.join(timeout=5)

@@ -1,0 +1,252 @@
+"""Native serving front (csrc/host/http_front.cpp + serve/front.py) against the FastAPI app.
+
+The front answers POST /api/recommend/ itself; every response must be byte-identical (body) to
+the one the FastAPI app gives for the same request (FastAPI TestClient over the same PVC), and
+everything else (400/422/404, /docs, /test, /, /readyz, /metrics) must come from the app
+unchanged.  Also: HTTP/1.1 framing (keep-alive, pipelining, chunked bodies, Expect:
+100-continue, HTTP/1.0), JSON escaping of odd names, the CPython-exact fallback sampler, and hot
+reload through the front.
+"""
+import json
+import os
+import pickle
+import random
+import socket
+import subprocess
+import sys
+import time
+import http.client
+
+import numpy as np
+import pytest
+from fastapi.testclient import TestClient
+
+from kubernetes_machine_learning_server_amd.job import main as job
+from kubernetes_machine_learning_server_amd.serve.app import create_app
+from tests.helpers import api_settings, job_settings, make_datasets
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class Server:
+    def __init__(self, base, backend="cpu", poll_min="60", version="V-test"):
+        self.port = _free_port()
+        env = dict(os.environ, BASE_DIR=str(base) + "/", PICKLE_DIR="pickles/",
+                   SERVE_BACKEND=backend, KMLS_LOG_LEVEL="ERROR", POLLING_WAIT_IN_MINUTES=poll_min,
+                   VERSION=version, K_BEST_TRACKS="10",
+                   PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        self.p = subprocess.Popen([sys.executable, "-m", "kubernetes_machine_learning_server_amd.serve",
+                                   "--host", "127.0.0.1", "--port", str(self.port), "--front",
+                                   "native", "--threads", "2"], env=env,
+                                  stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                  start_new_session=True)
+        t0 = time.time()
+        while time.time() - t0 < 120:
+            if self.p.poll() is not None:
+                raise RuntimeError(self.p.stderr.read().decode()[-3000:])
+            try:
+                c = http.client.HTTPConnection("127.0.0.1", self.port, timeout=5)
+                c.request("GET", "/healthz")
+                if c.getresponse().status == 200:
+                    return
+            except OSError:
+                time.sleep(0.1)
+        raise RuntimeError("front did not start")
+
+    def conn(self):
+        return http.client.HTTPConnection("127.0.0.1", self.port, timeout=10)
+
+    def post(self, body, path="/api/recommend/", ctype="application/json", conn=None):
+        c = conn or self.conn()
+        data = body if isinstance(body, (bytes, str)) else json.dumps(body)
+        c.request("POST", path, body=data, headers={"content-type": ctype})
+        r = c.getresponse()
+        return r.status, dict(r.getheaders()), r.read()
+
+    def stop(self):
+        os.killpg(self.p.pid, 15)
+        try:
+            self.p.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            os.killpg(self.p.pid, 9)
+
+
+@pytest.fixture(scope="module")
+def pvc(tmp_path_factory):
+    root = tmp_path_factory.mktemp("front")
+    make_datasets(root)
+    job.run(job_settings(root))
+    return root
+
+
+@pytest.fixture(scope="module")
+def server(pvc):
+    s = Server(pvc / "api-data")
+    yield s
+    s.stop()
+
+
+def _queries(pvc, n=150, seed=0):
+    with open(pvc / "api-data" / "pickles" / "recommendations.pickle", "rb") as f:
+        rec = pickle.load(f)
+    keys = list(rec)
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        q = [keys[int(i)] for i in rng.integers(0, len(keys), int(rng.integers(1, 5)))]
+        if rng.random() < 0.3:
+            q = ["not a song %d" % int(rng.integers(1e6))] + (q if rng.random() < 0.3 else [])
+        out.append(q)
+    return out
+
+
+def test_native_route_is_byte_identical_to_fastapi(pvc, server):
+    qs = _queries(pvc)
+    with TestClient(create_app(api_settings(pvc))) as tc:
+        for q in qs:
+            want = tc.post("/api/recommend/", json={"songs": q})
+            st, hd, body = server.post({"songs": q})
+            assert st == 200 == want.status_code
+            assert body == want.content, (q, body, want.content)
+            assert hd["content-type"] == "application/json"
+
+
+def test_slow_path_is_fastapi(pvc, server):
+    with TestClient(create_app(api_settings(pvc))) as tc:
+        cases = [({"songs": []}, None), ({"nope": 1}, None), ({"songs": [1, 2]}, None),
+                 (b"{not json", None), ({"songs": ["a"]}, "text/plain"), ([1, 2], None)]
+        for body, ctype in cases:
+            data = body if isinstance(body, bytes) else json.dumps(body)
+            want = tc.post("/api/recommend/", content=data,
+                           headers={"content-type": ctype or "application/json"})
+            st, _, got = server.post(data, ctype=ctype or "application/json")
+            assert st == want.status_code, (body, st, got)
+            assert json.loads(got) == want.json()
+    c = server.conn()
+    for path, status in (("/test", 307), ("/healthz", 200), ("/readyz", 200), ("/docs", 200),
+                         ("/openapi.json", 200), ("/nope", 404), ("/", 200), ("/metrics", 200)):
+        c.request("GET", path)
+        r = c.getresponse()
+        body = r.read()
+        assert r.status == status, path
+        if path == "/metrics":
+            assert b"kmls_front_requests" in body and b"kmls_recommend_requests_total" in body
+    st, hd, _ = server.post({"songs": ["x"]}, path="/api/recommend")
+    assert st == 307 and hd["location"].endswith("/api/recommend/")
+
+
+def _raw(port, data, wait=0.5):
+    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    s.sendall(data)
+    time.sleep(wait)
+    s.settimeout(2)
+    out = b""
+    try:
+        while True:
+            b = s.recv(65536)
+            if not b:
+                break
+            out += b
+    except socket.timeout:
+        pass
+    s.close()
+    return out
+
+
+def test_http_framing(server):
+    body = json.dumps({"songs": ["x"]}).encode()
+    req = (b"POST /api/recommend/ HTTP/1.1\r\nhost: x\r\ncontent-type: application/json\r\n"
+           b"content-length: %d\r\n\r\n" % len(body)) + body
+    # pipelining: two requests in one packet, two answers in order
+    out = _raw(server.port, req + req + b"GET /healthz HTTP/1.1\r\nhost: x\r\n\r\n")
+    assert out.count(b"HTTP/1.1 200 OK") == 3 and out.endswith(b'{"status":"ok"}')
+    # chunked request body
+    chunked = (b"POST /api/recommend/ HTTP/1.1\r\nhost: x\r\ncontent-type: application/json\r\n"
+               b"transfer-encoding: chunked\r\n\r\n%x\r\n%s\r\n0\r\n\r\n" % (len(body), body))
+    assert _raw(server.port, chunked).startswith(b"HTTP/1.1 200 OK")
+    # Expect: 100-continue before the body
+    s = socket.create_connection(("127.0.0.1", server.port), timeout=10)
+    s.sendall(b"POST /api/recommend/ HTTP/1.1\r\nhost: x\r\ncontent-type: application/json\r\n"
+              b"expect: 100-continue\r\ncontent-length: %d\r\n\r\n" % len(body))
+    assert s.recv(100).startswith(b"HTTP/1.1 100 Continue")
+    s.sendall(body)
+    time.sleep(0.3)
+    assert b"200 OK" in s.recv(65536)
+    s.close()
+    # HTTP/1.0: answered, then closed
+    out = _raw(server.port, b"POST /api/recommend/ HTTP/1.0\r\ncontent-type: application/json\r\n"
+                            b"content-length: %d\r\n\r\n" % len(body) + body)
+    assert b"200 OK" in out and b"connection: close" in out.lower()
+    # garbage request line
+    assert _raw(server.port, b"HELLO\r\n\r\n").startswith(b"HTTP/1.1 400")
+
+
+def test_odd_names_escape_like_json_dumps(tmp_path):
+    pk = tmp_path / "api-data" / "pickles"
+    pk.mkdir(parents=True)
+    names = ['quote"s', "back\\slash", "tab\there", "ctl\x01\x1f", "émoji 🎵", "nl\nx", "plain"]
+    rec = {n: {m: 0.5 - 0.01 * j for j, m in enumerate(names) if m != n} for n in names}
+    (pk / "recommendations.pickle").write_bytes(pickle.dumps(rec))
+    (pk / "best_tracks.pickle").write_bytes(pickle.dumps(
+        [{"track_name": n, "count": 10 - i} for i, n in enumerate(names)]))
+    (tmp_path / "api-data" / "last_execution.txt").write_text('2025 "date"\n')
+    s = Server(tmp_path / "api-data", version="vé\"1")
+    try:
+        with TestClient(create_app(api_settings(tmp_path, version="vé\"1"))) as tc:
+            for q in ([names[0]], [names[4], names[1]], ["unknown 🎵"], [names[3], "zz"]):
+                want = tc.post("/api/recommend/", json={"songs": q}).content
+                assert s.post({"songs": q})[2] == want, q
+                # the same request with \\u escapes in the JSON body
+                raw = json.dumps({"songs": q}, ensure_ascii=True)
+                assert s.post(raw)[2] == want, q
+    finally:
+        s.stop()
+
+
+def test_fallback_sampler_matches_cpython(native_mod):
+    rng = random.Random(5)
+    for _ in range(500):
+        seed = rng.getrandbits(64)
+        n = rng.choice([1, 7, 63, 85, 86, 500])
+        k = min(n, rng.choice([1, 6, 10, 25]))
+        assert list(native_mod.python_random_sample(seed, n, k)) == \
+            random.Random(seed).sample(range(n), k)
+    from kubernetes_machine_learning_server_amd.serve.matcher import stable_seed
+    for q in (["a", "b"], ["b", "a"], ["é", "x\x1f"], []):
+        assert native_mod.fallback_seed(q) == stable_seed(q)
+
+
+def test_hot_reload_through_front(tmp_path):
+    make_datasets(tmp_path)
+    job.run(job_settings(tmp_path))
+    s = Server(tmp_path / "api-data", poll_min="0.01")  # 1 s polling
+    try:
+        m1 = (tmp_path / "api-data" / "last_execution.txt").read_text()
+        assert json.loads(s.post({"songs": ["x"]})[2])["model_date"] == m1
+        time.sleep(1.1)
+        job.run(job_settings(tmp_path))  # dataset 2, new marker
+        m2 = (tmp_path / "api-data" / "last_execution.txt").read_text()
+        assert m2 != m1
+        t0 = time.time()
+        while time.time() - t0 < 20:
+            if json.loads(s.post({"songs": ["x"]})[2])["model_date"] == m2:
+                break
+            time.sleep(0.2)
+        assert json.loads(s.post({"songs": ["x"]})[2])["model_date"] == m2
+    finally:
+        s.stop()
+
+
+def test_loadgen_measures_from_schedule(server):
+    from kubernetes_machine_learning_server_amd.bench.bench_serve import measure_native
+    r = measure_native(server.port, 2000, 1.0, [["x"], ["y", "z"]], connections=8)
+    assert r["completed"] == 2000 and r["errors"] == 0 and r["unanswered"] == 0
+    assert 0 < r["p50_ms"] < 50
