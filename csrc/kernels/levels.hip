@@ -104,8 +104,11 @@ __device__ __forceinline__ SegAgg seg_shfl_xor(const SegAgg& v, int off) {
 }
 // Two words per tile.  An aggregate fits ONE word (S, O, F <= 256 and C <= 256*255/2: 9+9+9+1+15
 // bits), so the common case of the look-back reads one word per predecessor; an inclusive prefix
-// (S, C, O < 2^28: a level has at most status_cap * 256 = 2^28 candidates) spans both, w1 written
-// before w0 and accepted only when both carry the flag.
+// spans both, w1 written before w0 and accepted only when both carry the flag.  S and O count
+// this level's rows (< 2^28: a level has at most status_cap * 256 = 2^28 candidates) but C, the
+// NEXT level's candidate total, is quadratic in the survivors per class: it gets 36 bits and
+// saturates there, so a prefix past the limit reads as >= 2^28 and the last tile's capacity
+// guard (Ct >= 2^28 -> overflow 4 -> chunked path) fires instead of accepting wrapped offsets.
 __device__ __forceinline__ void seg_publish(unsigned long long* my, unsigned e, unsigned flag,
                                             const SegAgg& v) {
   if (flag == 1) {
@@ -114,7 +117,8 @@ __device__ __forceinline__ void seg_publish(unsigned long long* my, unsigned e, 
                                   ((unsigned long long)v.C << 28)));
   } else {
     const unsigned long long o = (unsigned long long)v.O;
-    st_relaxed(my + 1, pack(e, 2, (unsigned long long)v.C | ((o >> 18) << 28)));
+    const unsigned long long c = v.C >= (1ll << 36) ? (1ull << 36) - 1 : (unsigned long long)v.C;
+    st_relaxed(my + 1, pack(e, 2, c | ((o >> 18) << 36)));
     st_relaxed(my, pack(e, 2, (unsigned long long)v.S | ((o & 0x3FFFFull) << 28)));
   }
 }
@@ -134,10 +138,10 @@ __device__ __forceinline__ SegAgg seg_decode(unsigned long long w0, unsigned lon
   } else {
     const unsigned long long y = w1 & kValMask;
     v.S = (int32_t)(x & 0xFFFFFFFull);
-    v.O = (int32_t)((x >> 28) | ((y >> 28) << 18));
+    v.O = (int32_t)((x >> 28) | ((y >> 36) << 18));
     v.F = 0;
     v.H = true;
-    v.C = (int64_t)(y & 0xFFFFFFFull);
+    v.C = (int64_t)(y & 0xFFFFFFFFFull);
   }
   return v;
 }

@@ -25,7 +25,7 @@ import numpy as np
 
 from ..config import JobSettings
 from ..models.fpgrowth import ItemsetTrie, default_backend, mine_csr
-from ..serve.index import RuleIndexData, build_index_from_trie
+from ..serve.index import RuleIndexData, build_index_from_trie, index_from_device_csr
 from ..utils.atomic_io import atomic_pickle, atomic_write_bytes
 from ..utils.checkpoint import PhaseCheckpoint
 from ..utils.timeutil import current_time_str, format_timedelta
@@ -55,13 +55,25 @@ def _fault(point: str) -> None:
 def mine_rules(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float,
                total_songs: int, backend: Optional[str] = None, verbose: bool = True
                ) -> Tuple[RuleIndexData, ItemsetTrie, str, Tuple[int, float]]:
-    """``calculate_and_save_fp_growth_fast`` (main.py:262-313): mine + rule map + timing."""
+    """``calculate_and_save_fp_growth_fast`` (main.py:262-313): mine + rule map + timing.
+
+    On the GPU the rule map (the ``songs_to_song_sets`` loop, main.py:282-304, = the pair-support
+    rows) is built by the device kernel inside the mining call (``pairs_to_csr``) and becomes
+    ``rules.idx`` / ``recommendations.pickle`` directly; the CPU and oracle miners build it on the
+    host from the trie (same rows, same order)."""
     t0 = time.perf_counter()
     backend = backend or (default_backend() if cfg.miner == "auto" else cfg.miner)
     trie = mine_csr(tx.tx_ptr, tx.items, len(tx.names), min_support, backend=backend,
-                    pairs_only=(cfg.rules_mode == "pairs"), columns=tx.names)
-    idx = build_index_from_trie(trie.parent, trie.item, trie.count, trie.depth, tx.n_tx,
-                                len(tx.names), tx.names)
+                    pairs_only=(cfg.rules_mode == "pairs"), columns=tx.names,
+                    rule_index=(backend == "gpu"))
+    dev_map = trie.stats.pop("device_rule_map", None) if isinstance(trie.stats, dict) else None
+    if dev_map is not None:
+        idx = index_from_device_csr(dev_map, len(tx.names), trie.item[trie.depth == 1], tx.n_tx,
+                                    tx.names)
+        trie.stats["rule_map"] = "device"
+    else:
+        idx = build_index_from_trie(trie.parent, trie.item, trie.count, trie.depth, tx.n_tx,
+                                    len(tx.names), tx.names)
     missing = total_songs - idx.n_keys
     dur = time.perf_counter() - t0
     if verbose:
@@ -322,7 +334,7 @@ def run(cfg: Optional[JobSettings] = None) -> Dict:
         summary = {"dataset_index": new_index, "dataset": selected, "marker": ts,
                    "n_keys": idx.n_keys, "songs_without_recommendations": missing,
                    "n_itemsets": len(trie), "rule_seconds": dur, "backend": trie.stats.get("backend"),
-                   "resumed": resumed}
+                   "rule_map": trie.stats.get("rule_map", "host"), "resumed": resumed}
         print("=== Run complete. Exiting, current time is ", current_time_str(), " ===")
     if distributed:
         import torch.distributed as dist

@@ -145,8 +145,14 @@ def _gpu_miner():
 
 def mine_csr(tx_ptr: np.ndarray, items: np.ndarray, n_items: int, min_support: float,
              max_len: Optional[int] = None, backend: str = "auto", pairs_only: bool = False,
-             columns: Optional[Sequence] = None, mfma: bool = False) -> ItemsetTrie:
-    """Mine CSR transactions (rows duplicate-free, item ids in [0, n_items))."""
+             columns: Optional[Sequence] = None, mfma: bool = False,
+             rule_index: bool = False) -> ItemsetTrie:
+    """Mine CSR transactions (rows duplicate-free, item ids in [0, n_items)).
+
+    ``rule_index`` (GPU backend): the mining call also builds the rule map on the device
+    (``pairs_to_csr``, rows ordered by score desc then consequent name when ``columns`` are
+    given); it is returned as ``trie.stats["device_rule_map"]`` (absent if the device could not
+    build it, e.g. after a fallback, or on the CPU backends)."""
     if not (0.0 < min_support):
         raise ValueError("`min_support` must be a positive number within the interval `(0, 1]`. "
                          f"Got {min_support}.")
@@ -169,11 +175,19 @@ def mine_csr(tx_ptr: np.ndarray, items: np.ndarray, n_items: int, min_support: f
     elif backend == "gpu":
         g = _gpu_miner()
         g.load_csr(tx_ptr, items, int(n_items))
-        r = g.mine(float(min_support), ml, bool(pairs_only), True, True, bool(mfma))
+        if rule_index:
+            from ..serve.index import name_tie_rank
+            tie = (name_tie_rank([str(c) for c in columns]) if columns is not None else
+                   np.arange(int(n_items), dtype=np.int32))
+            g.set_tie_rank(np.ascontiguousarray(tie, np.int32))
+        r = g.mine(float(min_support), ml, bool(pairs_only), True, True, bool(mfma), False,
+                   bool(rule_index))
     else:
         raise ValueError(f"unknown backend {backend!r}")
     st = dict(r["stats"])
     st["backend"] = backend
+    if rule_index and "index" in r:
+        st["device_rule_map"] = r["index"]
     return ItemsetTrie(r["parent"], r["item"], r["count"], r["depth"], n_tx, min_support, st,
                        columns)
 

@@ -25,6 +25,7 @@ def test_job_gpu_artifacts_equal_cpu(tmp_path, gpu_mod, rules_mode):
     gpu_cfg = job_settings(tmp_path, miner="gpu", rules_mode=rules_mode, min_support=0.05)
     st = job.run(gpu_cfg)
     assert st["dataset_index"] == 1
+    assert st["rule_map"] == "device"  # the deployed artifact comes from pairs_to_csr
     cpu_cfg = job_settings(tmp_path, miner="cpu", rules_mode=rules_mode, min_support=0.05)
     cpu_cfg.base_dir = tmp_path / "api-cpu"
     cpu_cfg.pickles_folder = cpu_cfg.base_dir / "pickles"
@@ -32,9 +33,16 @@ def test_job_gpu_artifacts_equal_cpu(tmp_path, gpu_mod, rules_mode):
     for name in ("recommendations.pickle", "best_tracks.pickle", "artistsMapping.pickle",
                  "trackIdsToInfo.pickle"):
         assert _load(gpu_cfg.pickles_folder / name) == _load(cpu_cfg.pickles_folder / name), name
+    # same key order and same row order (serve-time tie order), not just dict equality
+    g_rec = _load(gpu_cfg.pickles_folder / "recommendations.pickle")
+    c_rec = _load(cpu_cfg.pickles_folder / "recommendations.pickle")
+    assert list(g_rec) == list(c_rec)
+    assert all(list(g_rec[k].items()) == list(c_rec[k].items()) for k in c_rec)
     gi = RuleIndexData.load(gpu_cfg.pickles_folder / "rules.idx")
     ci = RuleIndexData.load(cpu_cfg.pickles_folder / "rules.idx")
-    assert gi.to_rec_dict() == ci.to_rec_dict()
+    for a in ("row_ptr", "cons", "score", "is_key"):
+        assert (getattr(gi, a) == getattr(ci, a)).all(), a
+    assert gi.names == ci.names
 
 
 def test_api_hip_backend_serves_job_output(tmp_path, gpu_mod):

@@ -634,3 +634,23 @@ def test_encode_tiled_long_shard(gpu_mod, monkeypatch, T, I, ms, min_f, lookup):
     ref = gpu_mod.encode_bitmaps_cpu(ptr, items, sel[2], F, Wp)
     np.testing.assert_array_equal(bm.cpu().numpy().view(np.uint64)[:, :used],
                                   ref.reshape(F, Wp)[:, :used])
+
+
+def test_level_candidate_total_past_2_28_falls_back(gpu_mod):
+    """64 transactions holding the same 1200 items: every itemset is frequent, and the level-3
+    candidate total C(1200, 3) = 287,280,400 passes 2^28.  The fused path's look-back prefix
+    saturates instead of wrapping, its capacity guard fires (overflow 4) and the chunked path
+    produces the exact binomial counts; the deep count-only miner agrees."""
+    from math import comb
+    T, I = 64, 1200
+    tx_ptr = np.arange(T + 1, dtype=np.int64) * I
+    items = np.tile(np.arange(I, dtype=np.int32), T)
+    g = gpu_mod.GpuMiner(0)
+    g.load_csr(tx_ptr, items, I)
+    r = g.mine(0.5, 3, download=False)
+    want = I + comb(I, 2) + comb(I, 3)
+    assert r["stats"]["n_itemsets"] == want
+    assert "overflow code 4" in r["stats"].get("levels_path", "") or \
+        "fallback" in r["stats"].get("levels_path", ""), r["stats"].get("levels_path")
+    d = g.mine_deep(0.5, 3)
+    assert d["per_level"][1:4] == [I, comb(I, 2), comb(I, 3)]
