@@ -78,6 +78,24 @@ using U32 = py::array_t<uint32_t, py::array::c_style | py::array::forcecast>;
 using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 }  // namespace
 
+static gpu::CommDtype comm_dtype(const std::string& s) {
+  if (s == "u32") return gpu::CommDtype::U32;
+  if (s == "u64") return gpu::CommDtype::U64;
+  if (s == "i64") return gpu::CommDtype::I64;
+  if (s == "f64") return gpu::CommDtype::F64;
+  throw std::invalid_argument("comm dtype must be u32, u64, i64 or f64");
+}
+
+static int shm_kind(const py::array& buf) {
+  const auto k = buf.dtype().kind();
+  const size_t e = (size_t)buf.itemsize();
+  if (k == 'u' && e == 4) return 0;
+  if (k == 'i' && e == 8) return 1;
+  if (k == 'u' && e == 8) return 2;
+  if (k == 'f' && e == 8) return 3;
+  throw std::invalid_argument("dtype must be uint32, int64, uint64 or float64");
+}
+
 void register_gpu_bindings(py::module_& m) {
   m.def("gpu_available", &gpu::available);
   m.def("roctx_enabled", &trace::enabled);
@@ -142,6 +160,42 @@ void register_gpu_bindings(py::module_& m) {
         py::gil_scoped_release nogil;
         c.wait_stream((void*)stream);
       })
+      // device-pointer collectives (u32/u64/i64/f64 by name), ordered on `stream`
+      .def("all_reduce", [](gpu::Comm& c, uintptr_t send, uintptr_t recv, size_t n,
+                            const std::string& dt, bool max_op, uintptr_t stream) {
+        const gpu::CommDtype t = comm_dtype(dt);
+        py::gil_scoped_release nogil;
+        c.all_reduce((void*)send, (void*)recv, n, t, max_op, (void*)stream);
+      }, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"),
+         py::arg("max_op") = false, py::arg("stream") = 0)
+      .def("all_gather", [](gpu::Comm& c, uintptr_t send, uintptr_t recv, size_t n,
+                            const std::string& dt, uintptr_t stream) {
+        const gpu::CommDtype t = comm_dtype(dt);
+        py::gil_scoped_release nogil;
+        c.all_gather((void*)send, (void*)recv, n, t, (void*)stream);
+      }, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"),
+         py::arg("stream") = 0)
+      .def("reduce_scatter", [](gpu::Comm& c, uintptr_t send, uintptr_t recv, size_t n,
+                                const std::string& dt, bool max_op, uintptr_t stream) {
+        const gpu::CommDtype t = comm_dtype(dt);
+        py::gil_scoped_release nogil;
+        c.reduce_scatter((void*)send, (void*)recv, n, t, max_op, (void*)stream);
+      }, py::arg("send"), py::arg("recv"), py::arg("recv_count"), py::arg("dtype"),
+         py::arg("max_op") = false, py::arg("stream") = 0)
+      .def("all_to_all", [](gpu::Comm& c, uintptr_t send, uintptr_t recv, size_t n,
+                            const std::string& dt, uintptr_t stream) {
+        const gpu::CommDtype t = comm_dtype(dt);
+        py::gil_scoped_release nogil;
+        c.all_to_all((void*)send, (void*)recv, n, t, (void*)stream);
+      }, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"),
+         py::arg("stream") = 0)
+      .def("sendrecv", [](gpu::Comm& c, uintptr_t send, int send_peer, uintptr_t recv,
+                          int recv_peer, size_t n, const std::string& dt, uintptr_t stream) {
+        const gpu::CommDtype t = comm_dtype(dt);
+        py::gil_scoped_release nogil;
+        c.sendrecv((void*)send, send_peer, (void*)recv, recv_peer, n, t, (void*)stream);
+      }, py::arg("send"), py::arg("send_peer"), py::arg("recv"), py::arg("recv_peer"),
+         py::arg("count"), py::arg("dtype"), py::arg("stream") = 0)
       .def("abort", &gpu::Comm::abort);
 
   // host shared-memory communicator on its own (CPU multi-process tests of the backend)
@@ -167,6 +221,45 @@ void register_gpu_bindings(py::module_& m) {
         py::gil_scoped_release nogil;
         c.all_reduce(p, n, e, kind, max_op);
       }, py::arg("buf"), py::arg("max_op") = false)
+      .def("reduce_scatter", [](ShmComm& c, py::array send, bool max_op) {
+        KMLS_CHECK(send.flags() & py::array::c_style, "buffer must be C-contiguous");
+        const int kind = shm_kind(send);
+        const size_t e = (size_t)send.itemsize(), n = (size_t)send.size();
+        KMLS_CHECK(n % (size_t)c.world() == 0, "send size must be a multiple of world");
+        py::array out(send.dtype(), std::vector<py::ssize_t>{(py::ssize_t)(n / c.world())});
+        const void* sp = send.data();
+        void* op = out.mutable_data();
+        {
+          py::gil_scoped_release nogil;
+          c.reduce_scatter(sp, op, n / c.world(), e, kind, max_op);
+        }
+        return out;
+      }, py::arg("send"), py::arg("max_op") = false)
+      .def("all_to_all", [](ShmComm& c, py::array send) {
+        KMLS_CHECK(send.flags() & py::array::c_style, "buffer must be C-contiguous");
+        const size_t bytes = (size_t)send.nbytes();
+        KMLS_CHECK(bytes % (size_t)c.world() == 0, "send size must be a multiple of world");
+        py::array out(send.dtype(), std::vector<py::ssize_t>{(py::ssize_t)send.size()});
+        const void* sp = send.data();
+        void* op = out.mutable_data();
+        {
+          py::gil_scoped_release nogil;
+          c.all_to_all(sp, op, bytes / c.world());
+        }
+        return out;
+      })
+      .def("sendrecv", [](ShmComm& c, py::array send, int send_peer, int recv_peer) {
+        KMLS_CHECK(send.flags() & py::array::c_style, "buffer must be C-contiguous");
+        py::array out(send.dtype(), std::vector<py::ssize_t>{(py::ssize_t)send.size()});
+        const void* sp = send.data();
+        void* op = out.mutable_data();
+        const size_t bytes = (size_t)send.nbytes();
+        {
+          py::gil_scoped_release nogil;
+          c.sendrecv(sp, bytes, send_peer, op, bytes, recv_peer);
+        }
+        return out;
+      })
       .def("barrier", &ShmComm::barrier, py::call_guard<py::gil_scoped_release>())
       .def("abort", &ShmComm::abort);
 

@@ -205,4 +205,67 @@ void ShmComm::all_gather(const void* send, void* recv, size_t bytes) {
   }
 }
 
+
+void ShmComm::reduce_scatter(const void* send, void* recv, size_t count, size_t elem, int kind,
+                             bool max_op) {
+  const char* src = (const char*)send;
+  char* dst = (char*)recv;
+  const size_t per = slot_bytes_ / elem;
+  for (size_t off = 0; off < count; off += per) {
+    const size_t n = std::min(per, count - off);
+    // every destination block in turn: each rank publishes its chunk of block d, rank d sums
+    for (int d = 0; d < world_; ++d) {
+      std::memcpy(slot(rank_), src + ((size_t)d * count + off) * elem, n * elem);
+      barrier();
+      if (d == rank_) {
+        void* o = dst + off * elem;
+        std::memcpy(o, slot(0), n * elem);
+        for (int r = 1; r < world_; ++r) {
+          const void* sl = slot(r);
+          switch (kind) {
+            case 0: reduce_into((uint32_t*)o, (const uint32_t*)sl, n, max_op); break;
+            case 1: reduce_into((int64_t*)o, (const int64_t*)sl, n, max_op); break;
+            case 2: reduce_into((uint64_t*)o, (const uint64_t*)sl, n, max_op); break;
+            case 3: reduce_into((double*)o, (const double*)sl, n, max_op); break;
+            default: throw std::runtime_error("kmls shm comm: bad dtype");
+          }
+        }
+      }
+      barrier();
+    }
+  }
+}
+
+void ShmComm::all_to_all(const void* send, void* recv, size_t bytes) {
+  const char* s = (const char*)send;
+  char* d = (char*)recv;
+  const size_t per = slot_bytes_ / (size_t)world_;  // a slot holds one chunk of every block
+  if (per == 0) throw std::runtime_error("kmls shm comm: slot smaller than world");
+  for (size_t off = 0; off < bytes; off += per) {
+    const size_t n = std::min(per, bytes - off);
+    for (int b = 0; b < world_; ++b) std::memcpy(slot(rank_) + (size_t)b * per, s + (size_t)b * bytes + off, n);
+    barrier();
+    for (int r = 0; r < world_; ++r) std::memcpy(d + (size_t)r * bytes + off, slot(r) + (size_t)rank_ * per, n);
+    barrier();
+  }
+}
+
+void ShmComm::sendrecv(const void* send, size_t send_bytes, int send_peer, void* recv,
+                       size_t recv_bytes, int recv_peer) {
+  (void)send_peer;  // the slot of this rank is read by whoever names it as recv_peer
+  const char* s = (const char*)send;
+  char* d = (char*)recv;
+  const size_t total = std::max(send_bytes, recv_bytes);
+  // every rank runs the same number of rounds: the longest message of any rank is unknown
+  // here, so the rounds follow max(send, recv) of this pair and the callers keep sizes equal
+  // within a call (ring shifts of equal-size blocks)
+  for (size_t off = 0; off < total; off += slot_bytes_) {
+    const size_t n = std::min(slot_bytes_, total - off);
+    if (off < send_bytes) std::memcpy(slot(rank_), s + off, std::min(n, send_bytes - off));
+    barrier();
+    if (off < recv_bytes) std::memcpy(d + off, slot(recv_peer), std::min(n, recv_bytes - off));
+    barrier();
+  }
+}
+
 }  // namespace kmls

@@ -47,6 +47,12 @@ struct Rccl {
                             hipStream_t) = nullptr;
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
                             hipStream_t) = nullptr;
+  ncclResult_t (*ReduceScatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t,
+                                ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
 };
 
@@ -79,6 +85,11 @@ Rccl& rccl() {
   r.CommAbort = (decltype(r.CommAbort))sym("ncclCommAbort");
   r.AllReduce = (decltype(r.AllReduce))sym("ncclAllReduce");
   r.AllGather = (decltype(r.AllGather))sym("ncclAllGather");
+  r.ReduceScatter = (decltype(r.ReduceScatter))sym("ncclReduceScatter");
+  r.Send = (decltype(r.Send))sym("ncclSend");
+  r.Recv = (decltype(r.Recv))sym("ncclRecv");
+  r.GroupStart = (decltype(r.GroupStart))sym("ncclGroupStart");
+  r.GroupEnd = (decltype(r.GroupEnd))sym("ncclGroupEnd");
   r.GetErrorString = (decltype(r.GetErrorString))sym("ncclGetErrorString");
   init = true;
   return r;
@@ -278,6 +289,96 @@ void Comm::all_gather(const void* send, void* recv, size_t count, CommDtype t, v
                                           (hipStream_t)stream);
   if (r == ncclInProgress) progress("AllGather");
   else check(r, "AllGather");
+}
+
+void Comm::reduce_scatter(const void* send, void* recv, size_t recv_count, CommDtype t,
+                          bool max_op, void* stream) {
+  const size_t eb = comm_dtype_bytes(t), bytes = recv_count * eb;
+  hipStream_t s = (hipStream_t)stream;
+  if (direct_) {
+    if (send != recv) (void)hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s);
+    return;
+  }
+  if (host_) {
+    if (!recv_count) return;
+    char* h = (char*)stage(bytes * (size_t)(world_ + 1));
+    if (hipMemcpyAsync(h, send, bytes * (size_t)world_, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      throw std::runtime_error("kmls comm: staging copy failed");
+    host_->reduce_scatter(h, h + bytes * (size_t)world_, recv_count, eb, kind_of(t), max_op);
+    if (hipMemcpyAsync(recv, h + bytes * (size_t)world_, bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      throw std::runtime_error("kmls comm: staging copy failed");
+    return;
+  }
+  const ncclResult_t r = rccl().ReduceScatter(send, recv, recv_count, dtype_of(t),
+                                              max_op ? ncclMax : ncclSum, (ncclComm_t)comm_, s);
+  if (r == ncclInProgress) progress("ReduceScatter");
+  else check(r, "ReduceScatter");
+}
+
+void Comm::all_to_all(const void* send, void* recv, size_t count, CommDtype t, void* stream) {
+  const size_t eb = comm_dtype_bytes(t), bytes = count * eb;
+  hipStream_t s = (hipStream_t)stream;
+  if (direct_) {
+    if (send != recv) (void)hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s);
+    return;
+  }
+  if (host_) {
+    if (!count) return;
+    char* h = (char*)stage(2 * bytes * (size_t)world_);
+    if (hipMemcpyAsync(h, send, bytes * (size_t)world_, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      throw std::runtime_error("kmls comm: staging copy failed");
+    host_->all_to_all(h, h + bytes * (size_t)world_, bytes);
+    if (hipMemcpyAsync(recv, h + bytes * (size_t)world_, bytes * (size_t)world_,
+                       hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      throw std::runtime_error("kmls comm: staging copy failed");
+    return;
+  }
+  // grouped point-to-point: one send and one receive per peer, every xGMI link busy at once
+  check(rccl().GroupStart(), "GroupStart");
+  for (int p = 0; p < world_; ++p) {
+    const ncclResult_t a = rccl().Send((const char*)send + (size_t)p * bytes, count, dtype_of(t), p,
+                                       (ncclComm_t)comm_, s);
+    if (a != ncclSuccess && a != ncclInProgress) check(a, "Send");
+    const ncclResult_t b = rccl().Recv((char*)recv + (size_t)p * bytes, count, dtype_of(t), p,
+                                       (ncclComm_t)comm_, s);
+    if (b != ncclSuccess && b != ncclInProgress) check(b, "Recv");
+  }
+  const ncclResult_t e = rccl().GroupEnd();
+  if (e == ncclInProgress) progress("AllToAll");
+  else check(e, "GroupEnd");
+}
+
+void Comm::sendrecv(const void* send, int send_peer, void* recv, int recv_peer, size_t count,
+                    CommDtype t, void* stream) {
+  const size_t bytes = count * comm_dtype_bytes(t);
+  hipStream_t s = (hipStream_t)stream;
+  if (direct_) {
+    if (send != recv) (void)hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s);
+    return;
+  }
+  if (host_) {
+    char* h = (char*)stage(2 * bytes);
+    if (hipMemcpyAsync(h, send, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      throw std::runtime_error("kmls comm: staging copy failed");
+    host_->sendrecv(h, bytes, send_peer, h + bytes, bytes, recv_peer);
+    if (hipMemcpyAsync(recv, h + bytes, bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      throw std::runtime_error("kmls comm: staging copy failed");
+    return;
+  }
+  check(rccl().GroupStart(), "GroupStart");
+  const ncclResult_t a = rccl().Send(send, count, dtype_of(t), send_peer, (ncclComm_t)comm_, s);
+  if (a != ncclSuccess && a != ncclInProgress) check(a, "Send");
+  const ncclResult_t b = rccl().Recv(recv, count, dtype_of(t), recv_peer, (ncclComm_t)comm_, s);
+  if (b != ncclSuccess && b != ncclInProgress) check(b, "Recv");
+  const ncclResult_t e = rccl().GroupEnd();
+  if (e == ncclInProgress) progress("SendRecv");
+  else check(e, "GroupEnd");
 }
 
 size_t comm_dtype_bytes(CommDtype t) {

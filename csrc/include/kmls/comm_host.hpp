@@ -22,6 +22,15 @@ class ShmComm {
   void all_reduce(void* buf, size_t count, size_t elem, int kind, bool max_op);
   // recv = world x bytes (rank order)
   void all_gather(const void* send, void* recv, size_t bytes);
+  // send = world blocks of `count` elements; recv = the sum (max) of every rank's block `rank`
+  void reduce_scatter(const void* send, void* recv, size_t count, size_t elem, int kind,
+                      bool max_op);
+  // send = world blocks of `bytes`; recv block r = rank r's block `rank`
+  void all_to_all(const void* send, void* recv, size_t bytes);
+  // every rank calls it together: this rank's `send` goes to `send_peer`, `recv` gets what
+  // `recv_peer` sent (ring shifts, pairwise exchanges)
+  void sendrecv(const void* send, size_t send_bytes, int send_peer, void* recv, size_t recv_bytes,
+                int recv_peer);
   void barrier();
   void abort();
   bool aborted() const;

@@ -106,6 +106,16 @@ class Comm {
   void all_reduce(const void* send, void* recv, size_t count, CommDtype t, bool max_op,
                   void* stream);
   void all_gather(const void* send, void* recv, size_t count, CommDtype t, void* stream);
+  // send = world blocks of recv_count elements; recv = the reduction of every rank's block
+  // `rank` (row-block ownership of a matrix summed over transaction shards)
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, CommDtype t, bool max_op,
+                      void* stream);
+  // send = world blocks of `count` elements; recv block r = rank r's block `rank`
+  void all_to_all(const void* send, void* recv, size_t count, CommDtype t, void* stream);
+  // collective point-to-point: every rank sends to send_peer and receives from recv_peer
+  // (equal sizes within a call: ring shifts of the context-parallel pass)
+  void sendrecv(const void* send, int send_peer, void* recv, int recv_peer, size_t count,
+                CommDtype t, void* stream);
   // bounded host wait for `stream` (KMLS_COMM_TIMEOUT_S): aborts the communicator and throws
   // when a collective never completes (a peer died)
   void wait_stream(void* stream);

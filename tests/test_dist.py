@@ -179,6 +179,47 @@ def test_shm_comm_collectives_and_abort(world):
         assert "timed out" in r["after"] or "aborted" in r["after"], r
 
 
+def _shm_p2p_worker(rank, world, uid, out_q):
+    os.environ["KMLS_COMM_TIMEOUT_S"] = "20"
+    from kubernetes_machine_learning_server_amd.ops import native
+    c = native.load().ShmComm(rank, world, uid)
+    n = 3_000_001  # blocks of 12 MB (u32): past one 8 MB slot, chunked
+    send = (np.arange(world * n, dtype=np.uint64) * (rank + 1)).astype(np.uint32)
+    rs = c.reduce_scatter(send)
+    a2a_send = np.arange(world * 1000, dtype=np.int64) + 10_000 * rank
+    a2a = c.all_to_all(a2a_send)
+    ring = c.sendrecv(np.full(2_500_000, rank, np.int64), (rank + 1) % world, (rank - 1) % world)
+    out_q.put((rank, rs[:5].tolist(), int(rs[-1]), a2a.tolist(), int(ring[0]), int(ring[-1])))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_shm_comm_reduce_scatter_alltoall_sendrecv(world):
+    """Host communicator's new collectives against numpy: reduce-scatter of row blocks (the
+    config-5 gram), all-to-all (the item re-shard) and a ring shift (the context-parallel pass),
+    all past one shared-memory slot."""
+    from kubernetes_machine_learning_server_amd.ops import native
+    uid = native.load().host_comm_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shm_p2p_worker, args=(r, world, uid, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 3_000_001
+    tot = sum(r + 1 for r in range(world))
+    for rank, head, last, a2a, r0, r1 in res:
+        full = (np.arange(world * n, dtype=np.uint64) * tot).astype(np.uint32)
+        blk = full[rank * n:(rank + 1) * n]
+        assert head == blk[:5].tolist() and last == int(blk[-1])
+        want = np.concatenate([np.arange(rank * 1000, (rank + 1) * 1000) + 10_000 * src
+                               for src in range(world)])
+        assert a2a == want.tolist()
+        assert r0 == r1 == (rank - 1) % world
+
+
 def _txdp_worker(rank, world, port, shape, ms, max_len, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), OMP_NUM_THREADS="1")
