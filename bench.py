@@ -1,268 +1,143 @@
 #!/usr/bin/env python3
-"""Headline benchmark: FP-Growth itemsets/sec mined on MI355X (BASELINE.json metric).
+"""Headline benchmark (BASELINE.json metric): FP-Growth itemsets/sec mined on MI355X, plus the
+serving half (p50 /api/recommend/ at fixed QPS).
 
-One "step" = the reference's whole timed region (``machine-learning/main.py:264-308``:
-one-hot encode + fpgrowth + rule-map loop), on the device:
-per-item supports (HIP histogram) → frequent-item selection → tid-bitmap encode (the one-hot
-analogue) → level-2 co-occurrence bit-GEMM → every deeper level (AND+popcount kernels) →
-download of the complete itemset trie (every frequent itemset + its support) to host memory,
-plus the rule map (``songs_to_song_sets``, main.py:282-304) built on the device from the pair
-supports (pairs_to_csr: per-song rows sorted by score) and downloaded as a CSR.
+Headline step = FULL mining of one ds1-shape dataset at min_support 0.02: every frequent itemset
+of every size (1,414,082,373 itemsets, up to 19 items) and its support is computed on the
+device — per-item supports → frequent-item selection → tid-bitmap encode (the reference's
+one-hot) → level-2 classes → a persistent depth-first wave-per-task miner
+(``csrc/kernels/deep.hip``) that counts per size and folds every (itemset, support) into an
+order-independent digest instead of materialising 1.4e9 trie nodes (count-only; the digest equals
+the digest of the full trie, ``kmls/digest.hpp``).  Verified: per-size counts and digest equal to
+the native CPU miner's whole-problem count (``bench/bench_mine.CPU_REF``).
 
-Every run is verified against the native CPU miner by CONTENT: an order-independent digest of
-all (itemset, support) pairs (``_native.trie_digest``) and an exact comparison of the rule map
-with the CPU-built index.
+Multi-GPU (``torchrun --nproc-per-node N``, one rank per GPU): **strong scaling** — the SAME
+problem is split over the ranks (rank r mines level-3 tasks t ≡ r mod N; every rank builds the
+deterministic level-2 classes itself), and the per-size counts + digest sums are all-reduced,
+digest xors all-gathered, over RCCL (torch.distributed on the nccl group); every rank ends with
+the whole-problem result and verifies it.  ``value`` = itemsets of the problem ÷ the slowest
+rank's step.
 
-Multi-GPU (``torchrun --nproc-per-node N``, one rank per GPU): **weak scaling** by default —
-every rank mines its own ds1-shape dataset (rank 0 the seed's data, rank r a relabelled copy
-with permuted item ids and transaction order, so the same itemset count and depth but no
-shared bitmap word) with the native single-GPU path (``DistMiner(mode="local")``); ``value`` is
-the job total (sum of itemsets ÷ the slowest rank's step) and every rank verifies its own
-result by digest against the CPU miner.  A ds-sized problem is a ~0.3 ms chain of dependent
-level launches, so splitting ONE dataset over GPUs cannot scale; that strong-scaled form (the
-replicated root-class partition, ``--scaling strong``) is still timed at N > 1 and reported in
-the ``strong`` block, verified by combining the per-rank digests.
+Secondary fields:
+* ``serve``       — config 4, run FIRST in a fresh child process (this process has not touched
+                    the GPU yet): native HTTP front + open-loop native load generator, latency
+                    from the scheduled send time, fixed QPS points and the capacity (max QPS with
+                    p99 < 5 ms).
+* ``levelwise_0.05`` — the round-2 headline form (ds1 @0.05 through the level-wise graph path,
+                    trie download + device rule map in the step, verified against the CPU miner);
+                    at N > 1 one relabelled dataset per rank (weak scaling).
+* ``config2``     — ds1 @0.01: deployed rule map, truncated-at-4 trie, full count-only mining
+                    with the size cap raised within a time budget (N = 1).
+* ``config3``     — 10M x 1M @0.001 transaction-DP over all ranks.
+* ``native_rccl`` — at N > 1 the headline combine once more through the native RCCL
+                    communicator (``csrc/host/comm_rccl.cpp``), digest compared.
 
-Data: synthetic playlists of the reference's ds1/ds2 shape (2,246 playlists × 2,171 tracks,
-240k rows), calibrated by ``bench/calibrate.py`` to the published key curve, to the
-reference's own 0.03 sweep being minable (9.4M itemsets there) and as close to the published
-20.31 s (mlxtend, ds2 @0.05, relatorio.pdf p.6) as that allows: the replayed reference timed
-region takes 7.24 s on the build host for this data (profiles/r2_calibration.md).
-``vs_baseline`` = value ÷ (itemsets ÷ 20.31 s) = 20.31 s ÷ step time; ``vs_reference_replay``
-uses the 7.24 s replay instead (the conservative ratio).
-
-BASELINE config 2 (ds1 @ min_support 0.01, 1 GPU) is reported in ``config2`` (world size 1):
-the complete deployed artifact (the rule map at 0.01, exact by SURVEY §0) timed and verified,
-and full mining truncated at 4 items (1.0e8 itemsets) timed and digest-verified.  Full mining
-at 0.01 is not computable by any miner: a partial CPU count passes 3e9 itemsets with a
-frequent 27-itemset (2^27 subsets on its own).
-The serving half of the metric (p50 /api/recommend/ at fixed QPS) is in ``serve``.
+Data: synthetic playlists of the reference's ds1/ds2 shape (2,246 playlists × 2,171 tracks),
+calibrated by ``bench/calibrate.py``; random-init item vocabulary.
+``vs_baseline`` = value ÷ the reference's published itemsets/s (77,905 itemsets of this data at
+0.05 ÷ 20.31 s, relatorio.pdf p.6); ``vs_reference_replay`` uses the 7.24 s replay of the
+reference timed region on this data (profiles/r2_calibration.md).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
+import threading
 import time
 
-import numpy as np
-
 REF_SECONDS_DS2_005 = 20.313968  # relatorio.pdf p.6, mlxtend fpgrowth + rule map, ds2 @0.05
-# replay of the reference timed region on this data (bench/calibrate.py, build host CPU)
-REPLAY_SECONDS_DS1_005 = 7.24
-# ds1 @0.01: partial CPU count, capped (profiles/r2_calibration.md)
-FULL_001_LOWER_BOUND = 3_000_000_025
+REPLAY_SECONDS_DS1_005 = 7.24    # replay of the reference timed region on this data
+ITEMSETS_DS1_005 = 77905         # itemsets of the synthetic ds1 @0.05 (the published point)
+REF_RATE = ITEMSETS_DS1_005 / REF_SECONDS_DS2_005
+REPLAY_RATE = ITEMSETS_DS1_005 / REPLAY_SECONDS_DS1_005
 
 
-def _digest_of(N, r, min_depth=0):
-    return N.trie_digest(r["parent"], r["item"], r["count"], r["depth"], min_depth)
+class Watchdog:
+    """Bounded sections: if a section overruns, rank 0 prints the line built so far (with the
+    section named) and every rank exits, instead of the whole job hanging."""
+
+    def __init__(self, out: dict, rank: int):
+        self.out, self.rank = out, rank
+        self.name, self.deadline = None, None
+        self.lock = threading.Lock()
+        threading.Thread(target=self._run, daemon=True).start()
+
+    def _run(self):
+        while True:
+            time.sleep(1.0)
+            with self.lock:
+                if self.deadline is None or time.time() < self.deadline:
+                    continue
+                name = self.name
+            if self.rank == 0:
+                self.out.setdefault("errors", {})[name] = "timed out"
+                print(json.dumps(self.out), flush=True)
+            print(f"[bench] section {name} timed out; exiting", file=sys.stderr, flush=True)
+            os._exit(0 if "value" in self.out else 1)
+
+    def arm(self, name: str, seconds: float):
+        with self.lock:
+            self.name, self.deadline = name, time.time() + seconds
+
+    def disarm(self):
+        with self.lock:
+            self.name, self.deadline = None, None
 
 
-def _index_equal(ix, ref) -> bool:
-    """Device rule map == CPU-built index (row_ptr, consequents, counts)."""
-    rp = np.asarray(ix["row_ptr"], np.int64)
-    if len(rp) != len(ref.row_ptr) or not np.array_equal(rp, ref.row_ptr):
-        return False
-    return (np.array_equal(np.asarray(ix["cons"], np.int32), ref.cons) and
-            np.array_equal(np.asarray(ix["count"], np.int64),
-                           np.rint(ref.score * ref._n_tx).astype(np.int64)))
-
-
-def _cpu_index(N, tx, ms, names, max_len=2):
-    from kubernetes_machine_learning_server_amd.serve.index import build_index_from_trie
-    r = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, max_len)
-    ref = build_index_from_trie(r["parent"], r["item"], r["count"], r["depth"], tx.n_tx,
-                                tx.n_items, names)
-    ref._n_tx = tx.n_tx
-    return ref
-
-
-def run_config2(N, tx, names, tie, steps: int, verify: bool) -> dict:
-    """BASELINE config 2: ds1 @ min_support 0.01 on 1 GPU."""
-    ms = 0.01
-    g = N.GpuMiner(0)
-    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
-    g.set_tie_rank(tie)
-    out = {"min_support": ms, "model": "fpgrowth-ds1-shape", "global_batch": int(tx.n_tx),
-           "seq_len": int(tx.n_items)}
-    # (a) the deployed artifact: rule map = 1- and 2-itemsets, built and downloaded as a CSR
-    for _ in range(2):
-        r = g.mine(ms, 2, download=True, rule_index=True)
-    g.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        r = g.mine(ms, 2, download=True, rule_index=True)
-    g.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    st = r["stats"]
-    a = {"ms_per_step": round(dt * 1e3, 4), "steps": steps,
-         "n_keys": int(st["n_frequent_items"]), "n_rules": int(r["index"]["nnz"]),
-         "n_itemsets": int(st["n_itemsets"])}
-    if verify:
-        ref = _cpu_index(N, tx, ms, names)
-        a["verified_vs_cpu_index"] = _index_equal(r["index"], ref)
-        cpu = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, 2)
-        a["verified_digest"] = _digest_of(N, r)["digest"] == _digest_of(N, cpu)["digest"]
-    out["rule_map"] = a
-    # (b) full mining truncated at 4 items (every frequent itemset of size <= 4 + supports)
-    for _ in range(1):
-        r = g.mine(ms, 4, download=True, rule_index=True)
-    g.synchronize()
-    k = max(1, steps // 4)
-    t0 = time.perf_counter()
-    for _ in range(k):
-        r = g.mine(ms, 4, download=True, rule_index=True)
-    g.synchronize()
-    dt = (time.perf_counter() - t0) / k
-    st = r["stats"]
-    d = _digest_of(N, r)
-    b = {"max_len": 4, "ms_per_step": round(dt * 1e3, 3), "steps": k,
-         "n_itemsets": int(st["n_itemsets"]), "itemsets_per_s": round(st["n_itemsets"] / dt, 1),
-         "per_level": d["per_depth"][1:], "levels_path": st.get("levels_path")}
-    del r
-    if verify:
-        cpu = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, 4)
-        b["verified_digest"] = d["digest"] == _digest_of(N, cpu)["digest"]
-        del cpu
-    out["mine_max_len4"] = b
-    out["full_mining"] = {"feasible": False, "itemsets_lower_bound": FULL_001_LOWER_BOUND,
-                          "note": "partial CPU count (capped at 3e9) reaches a frequent "
-                                  "27-itemset; see profiles/r2_calibration.md"}
+def run_serve_child(qps: str, duration: float, backend: str, timeout: float = 420.0) -> dict:
+    """Config 4 in a fresh child process (PVC populated by the real job on the CPU miner, the
+    native-front server as its own child, the native open-loop load generator)."""
+    fd, path = tempfile.mkstemp(prefix="kmls_serve_", suffix=".json")
+    os.close(fd)
+    cmd = [sys.executable, "-m", "kubernetes_machine_learning_server_amd.bench.bench_serve",
+           "--backend", backend, "--qps", qps, "--duration", str(duration), "--capacity",
+           "--json-out", path]
+    try:
+        p = subprocess.run(cmd, stdout=sys.stderr, stderr=sys.stderr, timeout=timeout)
+        if p.returncode != 0:
+            return {"error": f"bench_serve exited {p.returncode}"}
+        with open(path) as f:
+            s = json.load(f)
+    except subprocess.TimeoutExpired:
+        return {"error": f"bench_serve timed out after {timeout:.0f} s"}
+    finally:
+        os.unlink(path)
+    keep = ("offered_qps", "achieved_qps", "p50_ms", "p90_ms", "p99_ms", "p999_ms", "max_ms",
+            "errors", "unanswered", "send_lag_p99_ms")
+    out = {k: s.get(k) for k in ("backend", "front", "threads", "client", "duration_s",
+                                 "gpu_index", "gpu_min_batch", "server_ready_s", "cpu")}
+    out["latency_from"] = "scheduled send time (open loop)"
+    out["points"] = [{k: p_.get(k) for k in keep} for p_ in s.get("points", [])]
+    cap = s.get("capacity") or {}
+    out["capacity"] = {k: cap.get(k) for k in ("capacity_qps", "max_qps_p99_under_ms",
+                                               "at_capacity", "limit_hit")}
+    out["front_stats"] = s.get("front_stats")
     return out
-
-
-# digest of the 10M x 1M @0.001 itemsets of the seeded synthetic data (924 itemsets, depth 4),
-# computed by the CPU miner (N.mine_cpu) over the whole dataset on the build host; the GPU
-# tx-DP result must equal it at every N
-C3_DIGEST = "d3b31400a6ebfffbbdac749329a5c1e6"
-
-
-def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: int = 1,
-                comm: str = "") -> dict:
-    """BASELINE config 3 (10M transactions x 1M items, min_support 0.001) on all ranks of the job:
-    transaction-DP mining (each rank generates and encodes only its shard; supports, gram and
-    per-level candidate counts all-reduced), so support/encode/gram work shrinks with N.  The
-    communicator is the host-staged one unless KMLS_BENCH_C3_COMM names another (the native
-    RCCL communicator has not run with more than one rank on real GPUs yet).  Verified by the
-    itemset digest, which must not depend on N."""
-    import torch
-    import torch.distributed as dist
-    from kubernetes_machine_learning_server_amd.data.synthetic import SHAPES
-    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner, shard_bounds
-    comm = comm or os.environ.get("KMLS_BENCH_C3_COMM", "host")
-    prev = os.environ.get("KMLS_COMM")
-    prev_to = os.environ.get("KMLS_COMM_TIMEOUT_S")
-    os.environ["KMLS_COMM"] = comm
-    if comm == "rccl" and prev_to is None:  # bounded: a stuck RCCL init or wait raises
-        os.environ["KMLS_COMM_TIMEOUT_S"] = "60"
-    try:
-        shape = SHAPES["10Mx1M"]
-        T = shape.n_tx
-        lo, hi, _ = shard_bounds(T, world, rank)
-        ptr, items = N.synth_transactions(T, shape.n_items, shape.mean_len, shape.n_genres,
-                                          shape.genre_affinity, 0.85, 0, 0, lo, hi)
-        dm = DistMiner(ptr, items, shape.n_items, 0.001, device=device, mode="tx",
-                       support_tiles=4, global_n_tx=T)
-
-        def bar():
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-                torch.cuda.synchronize()
-        r = None
-        for _ in range(warmup):
-            r = dm.step(download=True)
-        bar()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            r = dm.step(download=True)
-        dm.synchronize()
-        bar()
-        ms = (time.perf_counter() - t0) * 1000.0 / max(1, steps)
-        if world > 1:
-            t = torch.tensor([ms], dtype=torch.float64,
-                             device="cuda" if dist.get_backend() == "nccl" else "cpu")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            ms = float(t.item())
-        st = r["stats"]
-        out = {"model": "fpgrowth-10Mx1M-synthetic", "global_batch": T, "seq_len": shape.n_items,
-               "min_support": 0.001, "n_gpus": world, "parallelism": f"tx-dp{world}",
-               "comm": comm, "steps": steps, "ms_per_step": round(ms, 3),
-               "tx_per_s": round(T / (ms / 1000.0), 1),
-               "n_frequent_items": int(st.get("n_frequent_items", 0)),
-               "phases_ms": {k: round(v, 3) for k, v in (st.get("phases_ms") or {}).items()}}
-        if rank == 0:
-            d = _digest_of(N, r["trie"])
-            n = int(d["n"])
-            out["n_itemsets"] = n
-            out["itemsets_per_s"] = round(n / (ms / 1000.0), 1)
-            out["digest"] = d["digest"]
-            out["verified_digest"] = (d["digest"] == C3_DIGEST) if C3_DIGEST else None
-        del dm
-        return out
-    finally:
-        if prev is None:
-            os.environ.pop("KMLS_COMM", None)
-        else:
-            os.environ["KMLS_COMM"] = prev
-        if prev_to is None:
-            os.environ.pop("KMLS_COMM_TIMEOUT_S", None)
-
-
-def run_serve(shape: str, qps_list, duration: float, backend: str) -> dict:
-    """p50/p99 of POST /api/recommend/ at fixed offered QPS (the real uvicorn app over a PVC
-    populated by the real job on the same synthetic data)."""
-    import pathlib
-    import tempfile
-    from kubernetes_machine_learning_server_amd.bench import bench_serve as bs
-    root = pathlib.Path(tempfile.mkdtemp(prefix="kmls_bench_serve_"))
-    bs.prepare_pvc(root, shape=shape)
-    base = root / "api-data"
-    queries = bs.make_queries(base, 20000)
-    port = bs._free_port()
-    proc = bs.start_server(base, backend, 4, port)
-    # 8 open-loop client processes: at 10k QPS, 4 asyncio clients (2.5k each) measured their own
-    # event-loop lag as latency on a loaded box (profiles/r2_s7_serve_clients.md)
-    res = {"backend": backend, "workers": 4, "clients": 8, "duration_s": duration, "points": []}
-    try:
-        bs.measure(port, 200, 1.0, 1, queries)
-        for q in qps_list:
-            r = bs.measure(port, q, duration, 8, queries)
-            res["points"].append({k: r[k] for k in ("offered_qps", "achieved_qps", "p50_ms",
-                                                    "p99_ms", "errors", "client_send_lag_p99_ms")})
-    finally:
-        bs.stop_server(proc)
-    return res
 
 
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--shape", default="ds1")
-    ap.add_argument("--min-support", type=float, default=0.05)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--min-support", type=float, default=0.02)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--max-len", type=int, default=0, help="truncate itemset size (0 = all)")
-    ap.add_argument("--mfma", action="store_true", help="level-2 on the i8 matrix cores")
-    ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--no-prefetch", action="store_true",
-                    help="wait for every call before launching the next (no launch-ahead)")
-    ap.add_argument("--no-rule-map", action="store_true",
-                    help="leave the rule-map build out of the step (A/B only)")
-    ap.add_argument("--cpu", action="store_true", help="native CPU miner (no GPU)")
-    ap.add_argument("--no-config2", action="store_true", help="skip BASELINE config 2 (0.01)")
-    ap.add_argument("--no-config3", action="store_true",
-                    help="skip BASELINE config 3 (10M x 1M tx-DP over all ranks)")
+    ap.add_argument("--no-verify", action="store_true", help="skip the CPU-miner checks")
     ap.add_argument("--serve-qps", default="2000,5000,10000",
                     help="offered QPS points for the serving half ('' = skip)")
-    ap.add_argument("--serve-duration", type=float, default=3.0)
+    ap.add_argument("--serve-duration", type=float, default=4.0)
     ap.add_argument("--serve-backend", default="auto")
-    ap.add_argument("--scaling", choices=("weak", "strong"),
-                    default=os.environ.get("KMLS_BENCH_SCALING", "weak"),
-                    help="N>1: weak = one dataset per GPU (the job total; a 'strong' block "
-                         "reports one dataset split over the ranks); strong = that split only")
+    ap.add_argument("--no-levelwise", action="store_true")
+    ap.add_argument("--no-config2", action="store_true")
+    ap.add_argument("--no-config3", action="store_true")
+    ap.add_argument("--cpu", action="store_true",
+                    help="CPU tier of the headline (native CPU count miner, gloo): no GPU")
+    ap.add_argument("--comm", default=os.environ.get("KMLS_BENCH_COMM", "torch"),
+                    help="N>1 headline combine: torch (torch.distributed/RCCL) | rccl | host")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -271,31 +146,28 @@ def main() -> int:
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
-    from kubernetes_machine_learning_server_amd.data.synthetic import generate, relabel
+    # ---- config 4 first, in a fresh child: this process has not touched the GPU yet ----
+    serve = None
+    if world == 1 and args.serve_qps and not args.cpu:
+        t = time.time()
+        serve = run_serve_child(args.serve_qps, args.serve_duration, args.serve_backend)
+        serve["wall_s"] = round(time.time() - t, 1)
+
+    import numpy as np
+    import torch
+    from kubernetes_machine_learning_server_amd.bench import bench_mine as bm
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
     from kubernetes_machine_learning_server_amd.ops import native
-    from kubernetes_machine_learning_server_amd.serve.index import name_tie_rank
 
-    base_tx = generate(args.shape, seed=args.seed)
-    N = native.load()
-    weak = args.scaling == "weak" and world > 1
-    # weak scaling: rank r mines its own dataset (rank 0 = the seed's data; rank r = a
-    # relabelled copy: permuted item ids and transaction order, same itemset count and depth)
-    tx = relabel(base_tx, rank) if weak else base_tx
-    names = tx.names
-    tie = name_tie_rank(names) if names else np.arange(tx.n_items, dtype=np.int32)
-    rule_map = not args.no_rule_map and not args.cpu
-
-    # KMLS_BENCH_DIST=gloo rehearses the N-rank path on fewer GPUs (ranks share devices round
-    # robin; the step itself needs no collective, so only the bracket and the merge use gloo)
+    # KMLS_BENCH_DIST=gloo rehearses the N-rank path with ranks sharing GPUs (round robin)
     dist_backend = os.environ.get("KMLS_BENCH_DIST", "gloo" if args.cpu else "nccl")
     device = local_rank
-    if world > 1 and args.cpu:  # the CPU tier of the N-rank path (gloo, no device)
+    if world > 1 and args.cpu:
         import datetime
         import torch.distributed as dist
         dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
     elif world > 1:
         import datetime
-        import torch
         import torch.distributed as dist
         if dist_backend != "nccl":
             device = local_rank % max(1, torch.cuda.device_count())
@@ -307,11 +179,9 @@ def main() -> int:
             dist.init_process_group(dist_backend, timeout=datetime.timedelta(seconds=300))
 
     def barrier_sync():
+        if not args.cpu:
+            torch.cuda.synchronize()
         if world > 1:
-            import torch
-            import torch.distributed as dist
-            if not args.cpu:
-                torch.cuda.synchronize()
             dist.barrier()
             if not args.cpu:
                 torch.cuda.synchronize()
@@ -319,8 +189,6 @@ def main() -> int:
     def max_over_ranks(v: float) -> float:
         if world == 1:
             return v
-        import torch
-        import torch.distributed as dist
         t = torch.tensor([v], dtype=torch.float64,
                          device="cuda" if dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -329,205 +197,127 @@ def main() -> int:
     def gather(obj):
         if world == 1:
             return [obj]
-        import torch.distributed as dist
         parts = [None] * world
         dist.all_gather_object(parts, obj)
         return parts
 
-    def make_miner(mode: str, data, tie_):
-        from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
-        m = DistMiner(data.tx_ptr, data.items, data.n_items, args.min_support, device=device,
-                      max_len=args.max_len, mfma=args.mfma, mode=mode)
-        m.set_tie_rank(tie_)
-        return m
+    N = native.load() if args.cpu else native.require_gpu()
+    tx = generate("ds1", seed=args.seed)
+    out: dict = {}
+    wd = Watchdog(out, rank)
 
-    def timed_loop(step, sync, warmup: int, steps: int):
-        """Steady-state loop: each step launches the next step's (identical) call before
-        waiting for its own (prefetch), so the GPU never idles on the host between calls.  The
-        last warmup step and the last timed step launch nothing ahead: exactly `steps` calls
-        run inside the timed bracket, and none is in flight when it opens."""
-        r = None
-        for i in range(warmup):
-            r = step(i < warmup - 1)
-        barrier_sync()
-        sync()
-        t0 = time.perf_counter()
-        for i in range(steps):
-            r = step(i < steps - 1)
-        sync()
-        barrier_sync()
-        return r, (time.perf_counter() - t0) * 1000.0 / max(steps, 1)
-
-    def dm_step(m):
-        def step(prefetch=False):  # the itemset count is reduced over ranks once, after timing
-            return m.step(download=True, reduce_count=False,
-                          prefetch=prefetch and not args.no_prefetch,
-                          rule_index=rule_map)["trie"]
-        return step
-
-    if args.cpu:
-        step = lambda prefetch=False: N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items,
-                                                 args.min_support, args.max_len)
-        sync = lambda: None
-        dtype = "uint64-bitmap/int32-count (CPU)"
-        dm = None
-    else:
-        dm = make_miner("local" if weak else "auto", tx, tie)
-        step, sync = dm_step(dm), dm.synchronize
-        dtype = "uint64-bitmap/int32-count"
-
-    r, ms_step = timed_loop(step, sync, args.warmup, args.steps)
-    ms_step = max_over_ranks(ms_step)
-    st = r["stats"]
-
-    def cpu_check(data, res, digest_hex, n):
-        """(digest ok, rule map ok) of one result against the native CPU miner on `data`."""
-        if args.no_verify:
-            return None, None
-        ref = N.mine_cpu(data.tx_ptr, data.items, data.n_items, args.min_support, args.max_len)
-        rd = _digest_of(N, ref)
-        ok = rd["digest"] == digest_hex and int(rd["n"]) == n
-        ok_ix = None
-        if rule_map and "index" in res:
-            ok_ix = _index_equal(res["index"], _cpu_index(N, data, args.min_support, data.names))
-        return ok, ok_ix
-
-    def merged_digest(res, world_: int):
-        """Digest of a replicated-mode result over ranks: level-1 nodes are on every rank and
-        counted by rank 0 only; the per-rank (sum, xor) parts combine exactly."""
-        d = _digest_of(N, res, 0 if rank == 0 else 2)
-        parts = gather((int(d["n"]), int(d["sum"]), int(d["xor"]))) if world_ > 1 else \
-            [(int(d["n"]), int(d["sum"]), int(d["xor"]))]
-        n = sum(q[0] for q in parts)
-        dsum = sum(q[1] for q in parts) % (1 << 64)
-        dxor = 0
-        for q in parts:
-            dxor ^= q[2]
-        return n, f"{dsum:016x}{dxor:016x}"
-
-    if weak:  # every rank verifies its own dataset's result; the job total is the sum
-        d = _digest_of(N, r)
-        n_own, digest = int(d["n"]), d["digest"]
-        ok, ok_ix = cpu_check(tx, r, digest, n_own)
-        parts = gather((n_own, ok, ok_ix, digest))
-        n_itemsets = sum(q[0] for q in parts)
-        verified = None if args.no_verify else all(bool(q[1]) for q in parts)
-        verified_ix = (None if args.no_verify or not rule_map else
-                       all(bool(q[2]) for q in parts))
-        digest = parts[0][3]
-        n_per_dataset = parts[0][0]
-    else:
-        n_itemsets, digest = merged_digest(r, world)
-        n_per_dataset = n_itemsets
-        verified = verified_ix = None
-        if rank == 0:
-            verified, verified_ix = cpu_check(tx, r, digest, n_itemsets)
-
-    # strong-scaling companion at N > 1: ONE dataset (rank 0's) split over the ranks by the
-    # replicated root-class partition, timed the same way
-    strong = None
-    if weak and not args.cpu:
-        dm_s = make_miner("replicate", base_tx,
-                          name_tie_rank(base_tx.names) if base_tx.names else
-                          np.arange(base_tx.n_items, dtype=np.int32))
-        rs, ms_s = timed_loop(dm_step(dm_s), dm_s.synchronize, args.warmup, args.steps)
-        ms_s = max_over_ranks(ms_s)
-        n_s, dig_s = merged_digest(rs, world)
-        ok_s = None
-        if rank == 0 and not args.no_verify:
-            ok_s = cpu_check(base_tx, {}, dig_s, n_s)[0]
-        strong = {"parallelism": f"dp{world}-replicated-data+root-class-partition",
-                  "global_batch": int(base_tx.n_tx), "ms_per_step": round(ms_s, 4),
-                  "value": round(n_s / (ms_s / 1000.0), 1), "n_itemsets": n_s,
-                  "verified_digest": ok_s}
-        del dm_s
-
-    value = n_itemsets / (ms_step / 1000.0)
-    ref_rate = n_per_dataset / REF_SECONDS_DS2_005  # one reference pod mining one dataset
-    headline_cfg = args.shape in ("ds1", "ds2") and abs(args.min_support - 0.05) < 1e-12 and \
-        not args.max_len
-    n_data = world if weak else 1
-    out = {
-        "metric": "itemsets/sec mined (FP-Growth, all frequent itemsets + supports, rule map built)",
+    # ---- headline: full mining of ONE dataset, split over the ranks ----
+    wd.arm("headline", 900)
+    h = bm.run_deep(tx, args.min_support, world, rank, device, args.warmup, args.steps,
+                    barrier_sync, max_over_ranks, comm=args.comm if world > 1 else None,
+                    cpu=args.cpu)
+    wd.disarm()
+    deep_miner = h.pop("_miner")
+    if args.seed != 0:
+        h["verified_digest"] = None
+    ms_step = h["ms_per_step"]
+    value = h["n_itemsets"] / (ms_step / 1000.0)
+    out.update({
+        "metric": "itemsets/sec mined (FP-Growth, every frequent itemset of every size + its "
+                  "support, one dataset split over the GPUs)",
         "value": round(value, 1),
         "unit": "itemsets/s",
-        "n_gpus": world if not args.cpu else 0,
+        "n_gpus": 0 if args.cpu else world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_step, 4),
+        "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak" if (weak or world == 1) else "strong",
-        "vs_baseline": round(value / ref_rate, 2) if headline_cfg else None,
-        "vs_reference_replay": round(n_data * REPLAY_SECONDS_DS1_005 * 1e3 / ms_step, 1)
-        if headline_cfg and args.shape == "ds1" and args.seed == 0 else None,
-        "dtype": dtype,
-        "data": "synthetic (ds1 shape calibrated to relatorio.pdf p.5-6 + the 0.03 sweep; "
-                "random-init item vocab; bench/calibrate.py)" +
-                ("; weak scaling: one dataset per GPU, rank r>0 mines a relabelled copy "
-                 "(permuted item ids and transaction order; same itemset count)" if weak else ""),
+        "scaling": "strong",
+        "vs_baseline": round(value / REF_RATE, 1),
+        "vs_reference_replay": round(value / REPLAY_RATE, 1),
+        "baseline_basis": "reference itemsets/s = 77,905 itemsets (this data @0.05) / 20.31 s "
+                          "(relatorio.pdf p.6); replay = the reference timed region replayed "
+                          "on this data, 7.24 s (profiles/r2_calibration.md)",
+        "dtype": "uint64 tid-bitmaps / exact integer supports" + (" (CPU)" if args.cpu else ""),
+        "data": "synthetic (ds1 shape: 2,246 playlists x 2,171 tracks, calibrated to "
+                "relatorio.pdf p.5-6; random-init item vocab; bench/calibrate.py)",
         "config": {
-            "model": f"fpgrowth-{args.shape}-shape",
-            "global_batch": int(tx.n_tx) * n_data,
+            "model": "fpgrowth-ds1-shape",
+            "global_batch": int(tx.n_tx),
             "seq_len": int(tx.n_items),
-            "parallelism": (f"dp{world}-one-dataset-per-gpu" if weak else
-                            {"replicate": f"dp{world}-replicated-data+root-class-partition",
-                             "tx": f"tx-dp{world}+per-level-count-allreduce",
-                             "item": f"tx-dp{world}+item-shard{world}"}.get(
-                                 getattr(dm, "mode", "item")) if world > 1 and dm is not None
-                            else "single"),
+            "parallelism": (f"dp{world}-level3-task-split+count-allreduce({h['comm']})"
+                            if world > 1 else "single"),
             "min_support": args.min_support,
-            "max_len": args.max_len,
-            "n_itemsets": n_itemsets,
-            "n_itemsets_per_dataset": n_per_dataset,
-            "n_frequent_items": int(st.get("n_frequent_items", 0)),
-            "max_depth": int(st.get("max_depth", 0)),
-            "rule_map_in_step": rule_map,
-            "n_rules": int(r["index"]["nnz"]) if rule_map and "index" in r else None,
-            "level2": "mfma-i8" if args.mfma else "popcount-bitgemm",
-            "levels3plus": "level-wise",
-            "levels_path": st.get("levels_path"),
-            "step_overlap": ("none" if args.cpu or args.no_prefetch else
-                             "launch-ahead: step k+1's call is launched before step k's is waited for"),
+            "max_len": 0,
+            "output": "count-only: per-size counts + content digest of every (itemset, support)",
+            "n_itemsets": h["n_itemsets"],
+            "n_frequent_items": h["n_frequent_items"],
+            "max_depth": h["max_depth"],
+            "miner": ("cpu count miner (mine_cpu_count)" if args.cpu else
+                      "deep: persistent wave-per-task DFS over tid-projected classes (deep.hip)"),
         },
-        "verified_digest": verified,
-        "digest": digest,
-        "verified_rule_map_vs_cpu": verified_ix,
-        "reference_seconds_ds2_0.05": REF_SECONDS_DS2_005,
-        "reference_replay_seconds_same_data": REPLAY_SECONDS_DS1_005,
-    }
-    if strong is not None:
-        out["strong"] = strong
-    if "phases_ms" in st:
-        out["phases_ms"] = st["phases_ms"]
-    if not args.cpu and not args.no_config3:
+        "verified_digest": h["verified_digest"],
+        "digest": h["digest"],
+        "per_level": h["per_level"],
+        "deep": {k: h[k] for k in ("candidates", "chunks", "level2_tasks", "rank0_phases_ms",
+                                   "rank0_rounds")},
+    })
+    if serve is not None:
+        out["serve"] = serve
+
+    # ---- the round-2 headline form (level-wise, trie + rule map in the step) ----
+    if args.cpu:  # the GPU sections below have no CPU tier
+        args.no_levelwise = args.no_config2 = args.no_config3 = True
+    if not args.no_levelwise:
+        wd.arm("levelwise_0.05", 300)
         try:
-            c3 = run_config3(N, world, rank, device)
-        except Exception as e:  # the headline stands on its own
-            c3 = {"error": repr(e)[:300]}
-        if rank == 0:
-            out["config3"] = c3
-        # the same tx-DP run over the native RCCL communicator (xGMI), when the ranks are on
-        # an RCCL process group: every level's count all-reduce goes through RCCL on the
-        # miner's stream (init and waits bounded at 60 s; an error is reported, not raised)
-        if world > 1 and dist_backend == "nccl" and os.environ.get("KMLS_BENCH_C3_RCCL", "1") != "0":
-            try:
-                c3r = run_config3(N, world, rank, device, comm="rccl")
-            except Exception as e:
-                c3r = {"error": repr(e)[:300]}
+            lw = bm.run_levelwise(N, tx, 0.05, world, rank, device, 5, 20, barrier_sync,
+                                  max_over_ranks, gather, weak=world > 1,
+                                  verify=not args.no_verify)
+            lw["vs_baseline_same_config"] = round(
+                world * REF_SECONDS_DS2_005 * 1e3 / lw["ms_per_step"], 1)
+            lw["vs_reference_replay_same_config"] = round(
+                world * REPLAY_SECONDS_DS1_005 * 1e3 / lw["ms_per_step"], 1)
+            out["levelwise_0.05"] = lw
+        except Exception as e:
+            out.setdefault("errors", {})["levelwise_0.05"] = repr(e)[:300]
+        wd.disarm()
+
+    # ---- BASELINE config 2 (1 GPU) ----
+    if world == 1 and not args.no_config2:
+        from kubernetes_machine_learning_server_amd.serve.index import name_tie_rank
+        wd.arm("config2", 400)
+        try:
+            tie = name_tie_rank(tx.names) if tx.names else np.arange(tx.n_items, dtype=np.int32)
+            out["config2"] = bm.run_config2(N, tx, tx.names, tie, steps=10,
+                                            verify=not args.no_verify, deep_miner=deep_miner)
+        except Exception as e:
+            out.setdefault("errors", {})["config2"] = repr(e)[:300]
+        wd.disarm()
+
+    # ---- BASELINE config 3 (all ranks) ----
+    if not args.no_config3:
+        wd.arm("config3", 300)
+        try:
+            c3 = bm.run_config3(N, world, rank, device)
             if rank == 0:
-                out["config3_rccl"] = c3r
-    if world == 1 and not args.cpu and not args.no_config2 and rank == 0:
-        out["config2"] = run_config2(N, tx, names, tie, steps=10, verify=not args.no_verify)
-    if world == 1 and rank == 0 and args.serve_qps:
+                out["config3"] = c3
+        except Exception as e:
+            out.setdefault("errors", {})["config3"] = repr(e)[:300]
+        wd.disarm()
+
+    # ---- the headline combine through the native RCCL communicator ----
+    if world > 1 and dist_backend == "nccl" and args.comm != "rccl" and not args.cpu:
+        os.environ.setdefault("KMLS_COMM_TIMEOUT_S", "60")
+        wd.arm("native_rccl", 240)
         try:
-            out["serve"] = run_serve(args.shape, [float(q) for q in args.serve_qps.split(",")],
-                                     args.serve_duration, args.serve_backend)
-        except Exception as e:  # the mining numbers stand on their own
-            out["serve"] = {"error": repr(e)[:300]}
+            r2 = bm.run_deep(tx, args.min_support, world, rank, device, 1, 3, barrier_sync,
+                             max_over_ranks, comm="rccl")
+            r2.pop("_miner")
+            out["native_rccl"] = {"ms_per_step": r2["ms_per_step"],
+                                  "digest_equal": r2["digest"] == h["digest"]}
+        except Exception as e:
+            out.setdefault("errors", {})["native_rccl"] = repr(e)[:300]
+        wd.disarm()
+
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        import torch.distributed as dist
         dist.destroy_process_group()
     return 0
 

@@ -150,13 +150,13 @@ PYBIND11_MODULE(_native, m) {
      py::arg("min_support"), py::arg("max_len") = 0, py::arg("comm") = py::none());
 
   m.def("mine_cpu_count", [](I64 tx_ptr, I32 items, int64_t n_items, double min_support,
-                             int max_len, int64_t cap, int threads) {
+                             int max_len, int64_t cap, int threads, int rank, int world) {
     KMLS_CHECK(tx_ptr.size() >= 1, "tx_ptr must have T+1 entries");
     CountResult r;
     {
       py::gil_scoped_release nogil;
       r = mine_cpu_count(tx_ptr.data(), items.data(), tx_ptr.size() - 1, n_items, min_support,
-                         max_len, cap, threads);
+                         max_len, cap, threads, rank, world);
     }
     py::dict s;
     s["n_frequent_items"] = r.n_frequent_items; s["n_itemsets"] = r.n_itemsets;
@@ -168,7 +168,8 @@ PYBIND11_MODULE(_native, m) {
     s["digest"] = std::string(buf);
     return s;
   }, py::arg("tx_ptr"), py::arg("items"), py::arg("n_items"), py::arg("min_support"),
-     py::arg("max_len") = 0, py::arg("cap") = (int64_t)1 << 62, py::arg("threads") = 0);
+     py::arg("max_len") = 0, py::arg("cap") = (int64_t)1 << 62, py::arg("threads") = 0,
+     py::arg("rank") = 0, py::arg("world") = 1);
 
   m.def("trie_digest", [](py::array parent, py::array item, py::array count, py::object depth,
                           int min_depth) {

@@ -404,8 +404,8 @@ void register_gpu_bindings(py::module_& m) {
         d["phases_ms"] = ph;
         return d;
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("rank") = 0, py::arg("world") = 1,
-         py::arg("comm") = py::none(), py::arg("budget0") = 4096ull, py::arg("budget") = 4096ull,
-         py::arg("split_min") = 4u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0)
+         py::arg("comm") = py::none(), py::arg("budget0") = 1024ull, py::arg("budget") = 1024ull,
+         py::arg("split_min") = 8u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0)
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
   py::class_<gpu::GpuRuleIndex, std::shared_ptr<gpu::GpuRuleIndex>>(m, "GpuRuleIndex")

@@ -87,6 +87,7 @@ DeepResult GpuMiner::mine_deep(double min_support, int max_len, int rank, int wo
   in.F = F;
   in.W_real = W_real;
   in.d_ids = d_ids_;
+  in.counts = fi_.counts.data();
   in.minsup = minsup;
   in.max_len = max_len;
   in.n_cus = n_cus_;

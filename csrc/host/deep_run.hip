@@ -62,9 +62,21 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   const int64_t Fpad = (F + 15) / 16 * 16;
   DeepLocal res;
 
+  // width tier of every root class: its rows are projected onto tid(item), |tid(item)| = support
+  std::vector<int> wt((size_t)F, W);
+  int widest = 1;
+  for (int64_t i = 0; i < F; ++i) {
+    const int64_t words = ((int64_t)in.counts[(size_t)i] + 63) / 64;
+    wt[(size_t)i] = std::min(W, kern::deep_tier((int)std::max<int64_t>(words, 1)));
+    widest = std::max(widest, wt[(size_t)i]);
+  }
+  const int maxt = kern::deep_count_maxt(widest);
+  res.maxt = maxt;
+
   // ---- buffers (kept across calls) ----
   const auto t0 = now();
-  const int blocks_per_cu = opt.blocks_per_cu > 0 ? opt.blocks_per_cu : 3;
+  // one 4-wave block per SIMD slot of the kernel instance (blocks_per_cu picks the instance)
+  const int blocks_per_cu = kern::deep_count_wps(maxt, opt.blocks_per_cu);
   const int grid = std::max(1, in.n_cus * blocks_per_cu);
   const int64_t waves = (int64_t)grid * kern::deep_waves_per_block();
   const size_t stack_need = std::max<size_t>(
@@ -145,7 +157,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       const int64_t mi = m[(size_t)i];
       if (mi < 0 || mi > F) throw std::runtime_error("deep_run: bad level-2 class size");
       pairs += mi;
-      off[(size_t)i + 1] = off[(size_t)i] + (int64_t)(W + 1) * ((mi + 15) / 16 * 16) * 8;
+      off[(size_t)i + 1] = off[(size_t)i] + (int64_t)(wt[(size_t)i] + 1) * ((mi + 15) / 16 * 16) * 8;
       toff[(size_t)i + 1] = toff[(size_t)i] + std::max<int64_t>(mi - 1, 0);
     }
     if (rank == 0) res.per_depth[2] = (uint64_t)pairs;
@@ -174,7 +186,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   a.fstacks = b.fstacks;
   a.fcap = b.fcap;
   a.ctl = b.ctl;
-  a.W = W;
+  a.W = W;  // root width; every frame carries its own block width
   a.minsup = in.minsup;
   a.max_len = in.max_len;
   a.split_min = opt.split_min;
@@ -198,7 +210,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     a.out = b.q[cur ^ 1];
     a.heap = b.heap[round & 1];
     a.budget = round == 0 ? opt.budget0 : opt.budget;
-    kern::deep_count(a, (int)std::min<int64_t>(grid, (n_in + kern::deep_waves_per_block() - 1) /
+    kern::deep_count(a, maxt, blocks_per_cu, (int)std::min<int64_t>(grid, (n_in + kern::deep_waves_per_block() - 1) /
                                                          kern::deep_waves_per_block()), s);
     KMLS_HIP(hipMemcpyAsync(b.h_ctl, b.ctl, sizeof(kern::DeepCtl), hipMemcpyDeviceToHost, s));
     KMLS_HIP(hipStreamSynchronize(s));
@@ -206,8 +218,9 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       throw std::runtime_error("deep_run: round " + std::to_string(round) +
                                " ran past KMLS_DEEP_ROUND_TIMEOUT_S and gave up");
     if (b.h_ctl->error)
-      throw std::runtime_error("deep_run: round " + std::to_string(round) + " overflowed (" +
-                               ((b.h_ctl->error & 1) ? "task queue" : "spill heap") +
+      throw std::runtime_error("deep_run: round " + std::to_string(round) + " failed (" +
+                               ((b.h_ctl->error & 8) ? "bad block width" :
+                                (b.h_ctl->error & 1) ? "task queue overflow" : "spill heap overflow") +
                                "); raise KMLS_DEEP_QUEUE_MB / KMLS_DEEP_HEAP_MB");
     res.round_tasks.push_back(n_in);
     res.round_ms.push_back(ms_since(tr));

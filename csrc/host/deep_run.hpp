@@ -45,6 +45,7 @@ struct DeepInput {
   int64_t Wp = 0, F = 0;
   int W_real = 0;                 // ceil(T / 64)
   const int32_t* d_ids = nullptr; // device [F] rank -> original item id
+  const uint32_t* counts = nullptr;  // host [F] supports (root class i's tid projection width)
   uint32_t minsup = 0;            // count threshold for |S| >= 2
   int max_len = 0;
   int n_cus = 256;
@@ -56,6 +57,7 @@ struct DeepLocal {
   std::vector<uint64_t> per_depth = std::vector<uint64_t>(64, 0);
   uint64_t dsum = 0, dxor = 0, candidates = 0, chunks = 0;
   int64_t level2_tasks = 0;
+  int maxt = 0;  // widest block tier of the count kernel instance
   std::vector<int64_t> round_tasks;
   std::vector<double> round_ms;
   double ms_alloc = 0, ms_root = 0, ms_rounds = 0;

@@ -15,6 +15,7 @@
 
 #include <cstdlib>
 #include <functional>
+#include <stdexcept>
 
 #include "kmls/common.hpp"
 #include "kmls/digest.hpp"
@@ -209,7 +210,8 @@ void count_member(const CountCtx& cx, const std::vector<CMember>& cls, size_t i,
 
 CountResult mine_cpu_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                            int64_t n_items, double min_support, int max_len, int64_t cap,
-                           int threads) {
+                           int threads, int rank, int world) {
+  if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("mine_cpu_count: bad rank/world");
   auto t0 = std::chrono::steady_clock::now();
   std::vector<uint32_t> cnt((size_t)n_items);
   count_items(tx_ptr, items, n_tx, n_items, cnt.data());
@@ -220,7 +222,8 @@ CountResult mine_cpu_count(const int64_t* tx_ptr, const int32_t* items, int64_t 
   encode_bitmaps_cpu(tx_ptr, items, n_tx, fi.rank_of.data(), bm.data(), W);
   CountResult r;
   CountAcc all;
-  for (int64_t j = 0; j < F; ++j) all.add(1, item_mix((uint64_t)fi.ids[j]), fi.counts[j]);
+  if (rank == 0)
+    for (int64_t j = 0; j < F; ++j) all.add(1, item_mix((uint64_t)fi.ids[j]), fi.counts[j]);
   std::atomic<int64_t> total{F};
   int nth = threads > 0 ? threads : default_threads();
   nth = std::max(1, std::min<int>(nth, (int)std::max<int64_t>(F, 1)));
@@ -268,7 +271,7 @@ CountResult mine_cpu_count(const int64_t* tx_ptr, const int32_t* items, int64_t 
       const uint64_t hi = item_mix((uint64_t)fi.ids[(size_t)i]);
       for (size_t k = 0; k < l2r[(size_t)i].size(); ++k) {
         const uint64_t h = hi + item_mix((uint64_t)fi.ids[(size_t)l2r[(size_t)i][k]]);
-        all.add(2, h, l2c[(size_t)i][k]);
+        if (rank == 0) all.add(2, h, l2c[(size_t)i][k]);
         cls[(size_t)i].push_back(CMember{l2r[(size_t)i][k], -1 - (base[(size_t)i] + (int64_t)k), h});
       }
     }
@@ -276,8 +279,11 @@ CountResult mine_cpu_count(const int64_t* tx_ptr, const int32_t* items, int64_t 
     // levels >= 3: tasks (root class i, member k)
     if (max_len == 0 || max_len > 2) {
       std::vector<std::pair<int32_t, int32_t>> tasks;
+      uint64_t tasks_seen = 0;
       for (int64_t i = 0; i < F; ++i)
-        for (size_t k = 0; k + 1 < cls[(size_t)i].size(); ++k) tasks.push_back({(int32_t)i, (int32_t)k});
+        for (size_t k = 0; k + 1 < cls[(size_t)i].size(); ++k) {
+          if ((int64_t)(tasks_seen++ % (uint64_t)world) == rank) tasks.push_back({(int32_t)i, (int32_t)k});
+        }
       CountCtx cx{l2.data(), fi.ids.data(), W, fi.minsup2, max_len, cap, &total};
       std::vector<CountAcc> acc((size_t)nth);
       std::atomic<int64_t> nt{0};

@@ -143,10 +143,11 @@ struct DeepBufsDeleter {
 // Count-only deep mining (deep_gpu.hip, kernels/deep.hip): per-size itemset counts and the
 // content digest (kmls/digest.hpp; equal to trie_digest of the full trie) without a trie.
 struct DeepOpts {
-  unsigned long long budget0 = 4096;  // 64-lane passes a first-round task may take before spilling
-  unsigned long long budget = 4096;   // ... in later rounds
-  unsigned split_min = 4;             // spilled frames above this many members split per member
-  int blocks_per_cu = 0;              // 0 = 3 (12 waves per CU)
+  // (defaults: the best of the r3e sweep at ds1 @0.02, profiles/r3_deep_sweep_projected.log)
+  unsigned long long budget0 = 1024;  // 64-lane passes a first-round task may take before spilling
+  unsigned long long budget = 1024;   // ... in later rounds
+  unsigned split_min = 8;             // spilled frames above this many members split per member
+  int blocks_per_cu = 0;              // 0 = the kernel instance's occupancy (deep_waves_per_simd)
   int stack_mb = 0;                   // per-wave stack (0: KMLS_DEEP_STACK_MB or 4)
 };
 struct DeepResult {

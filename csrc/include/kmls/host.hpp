@@ -59,6 +59,9 @@ ItemsetTrie mine_cpu_txdp(const int64_t* tx_ptr, const int32_t* items, int64_t n
 // Count-only search: per-level itemset totals and the content digest (the one trie_digest gives
 // for the full trie) without a trie; stops once the running total exceeds `cap` (capped = true,
 // counts are then a lower bound).  The CPU reference of the GPU count-only (deep) miner.
+// rank/world: this rank's share of a split problem (levels 1-2 on rank 0, level-3 task q on
+// rank q % world); summing per_level / digest_sum and xoring digest_xor over the ranks gives
+// the whole problem.
 struct CountResult {
   std::vector<int64_t> per_level;  // [d] = #frequent itemsets of size d (index 0 unused)
   int64_t n_frequent_items = 0, n_itemsets = 0;
@@ -69,7 +72,7 @@ struct CountResult {
 };
 CountResult mine_cpu_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                            int64_t n_items, double min_support, int max_len, int64_t cap,
-                           int threads);
+                           int threads, int rank = 0, int world = 1);
 
 // Order-independent content digest of an itemset trie (digest.cpp): equal digests <=> (with
 // overwhelming probability) the same multiset of (itemset, support).  Element widths in bytes:

@@ -5,12 +5,21 @@
 // itemsets (BASELINE config 2, ds1 @ 0.01-0.02), a level-wise miner cannot hold one level in HBM.
 //
 // Design (one wave = one independent depth-first worker, no inter-wave hand-off inside a launch):
-// * A class (prefix P, members P∪{x_k}) lives in a BLOCK: W bitmap words x `pad` slots stored
+// * A class (prefix P, members P∪{x_k}) lives in a BLOCK: WT bitmap words x `pad` slots stored
 //   word-major ([w][slot]), then one item-hash word per slot.  Lanes that read consecutive
 //   member slots of one word row read contiguous memory, so every bitmap load is coalesced.
-// * A FRAME is (block, first slot, members, prefix hash, prefix size).  Each wave keeps a frame
-//   stack and a LIFO stack of blocks in its own HBM region; a block is freed when the frames that
-//   reference it are done and it is on top.
+// * TID PROJECTION: every member row of a class is a subset of tid(P).  When a class is created
+//   from the row of member a (root classes from the item's own row, row steps from member s0),
+//   its rows are stored COMPRESSED onto the positions of that row's set bits (parallel bit
+//   extract with per-word move masks computed once per class, Hacker's Delight 7-4), so a class
+//   whose prefix has support s holds ceil(s/64) words (rounded up to a width tier) instead of
+//   ceil(T/64).  At ds1 @0.02 the 36-word rows become 1-10 words at the root and shrink further
+//   down the tree: the bytes every AND+popcount reads and every survivor writes drop with them.
+//   The width of a block travels in its frames; one launch dispatches each step on the frame's
+//   tier (wave-uniform switch), so the words of a candidate stay in VGPRs with unguarded loads.
+// * A FRAME is (block, first slot, members, prefix hash, prefix size | width).  Each wave keeps a
+//   frame stack and a LIFO stack of blocks in its own HBM region; a block is freed when the
+//   frames that reference it are done and it is on top.
 // * Row step (big frames, > kCap pairs): member s0 against every later member, lane = candidate:
 //   the member's words are a broadcast, the candidates' words one coalesced row per word.
 // * Batch step (small frames, the deep levels): the top frames are popped together until their
@@ -20,8 +29,6 @@
 // * Load balance: tasks are dequeued by ticket.  A wave that exceeds its step budget on one task
 //   SPILLS its remaining frames to a heap as new tasks (big frames split into one task per
 //   member) and the host runs another round; heavy dense subtrees are thus cut into many tasks.
-// * All bitmap words of a candidate stay in VGPRs (WT <= 64 words), so a survivor's child row is
-//   written without re-reading its parents.
 // Counts are exact (popcount of at most 4096 bits per row, u32).
 #include <hip/hip_runtime.h>
 
@@ -44,9 +51,21 @@ constexpr int kBatchFrames = 64;     // frames one batch step may take
 constexpr int kBStack = 96;          // blocks on one wave's memory stack
 constexpr unsigned kSingle = 1u << 8;  // frame flag: expand only its first member
 
-// frame meta: bits 0..7 prefix size, bit 8 single, bits 16..31 block-stack index + 1 (0 = external)
+// frame meta: bits 0..7 prefix size, bit 8 single, bits 9..15 block width (words), bits 16..31
+// block-stack index + 1 (0 = external)
 __device__ __forceinline__ unsigned meta_depth(unsigned m) { return m & 0xffu; }
+__device__ __forceinline__ unsigned meta_width(unsigned m) { return (m >> 9) & 0x7fu; }
 __device__ __forceinline__ unsigned meta_bidx(unsigned m) { return m >> 16; }
+__host__ __device__ constexpr unsigned make_meta(unsigned depth, bool single, unsigned width,
+                                                 unsigned bidx) {
+  return depth | (single ? kSingle : 0u) | (width << 9) | (bidx << 16);
+}
+
+// block widths the kernels are instantiated for (words); tier(n) = smallest >= n
+__host__ __device__ constexpr unsigned tier_of(unsigned n) {
+  return n <= 1 ? 1 : n <= 2 ? 2 : n <= 3 ? 3 : n <= 4 ? 4 : n <= 6 ? 6 : n <= 8 ? 8
+       : n <= 12 ? 12 : n <= 16 ? 16 : n <= 24 ? 24 : n <= 32 ? 32 : n <= 48 ? 48 : 64;
+}
 
 constexpr unsigned long long roundup16(unsigned long long x) { return (x + 15) & ~15ull; }
 
@@ -79,24 +98,53 @@ __device__ __forceinline__ void store_frame(DeepFrame* p, const DeepFrame& f) {
   p->meta = f.meta;
 }
 
-struct WaveLds {
-  unsigned long long f_hash[kBatchFrames];
-  unsigned f_s0[kBatchFrames], f_m[kBatchFrames], f_meta[kBatchFrames];
-  unsigned P[kBatchFrames + 1], G[kBatchFrames + 1];
-  unsigned g_cnt[kCap], g_start[kCap];
-  unsigned long long b_base[kBStack];
-  unsigned b_live[kBStack];
-  unsigned long long depth_cnt[64];
+// ---- tid projection ----
+// Per-word move masks of the compress-right network for a fixed mask R (Hacker's Delight 7-4):
+// compress(x) = 6 rounds of  t = x & mv[i];  x = (x ^ t) | (t >> 2^i),  for x already inside R.
+template <int NW>
+struct ProjLds {
+  unsigned long long mv[6][NW];  // [round][word]
+  unsigned n[NW];                // popcount of R's word
 };
+
+// lanes w < WT: word w of the uniform row R = blk[w][ia]; returns |R| (uniform)
+template <int WT, int NW>
+__device__ __forceinline__ unsigned proj_setup(ProjLds<NW>& P, const unsigned long long* blk,
+                                               unsigned long long pad, unsigned ia, int lane) {
+  static_assert(WT <= NW && NW <= 64, "projection words");
+  unsigned n = 0;
+  if (lane < WT) {
+    unsigned long long m = blk[(unsigned long long)lane * pad + ia];
+    n = (unsigned)__popcll(m);
+    unsigned long long mk = ~m << 1;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      unsigned long long mp = mk ^ (mk << 1);
+      mp ^= mp << 2;
+      mp ^= mp << 4;
+      mp ^= mp << 8;
+      mp ^= mp << 16;
+      mp ^= mp << 32;
+      const unsigned long long mv = mp & m;
+      P.mv[i][lane] = mv;
+      m = (m ^ mv) | (mv >> (1u << i));
+      mk &= ~mp;
+    }
+    P.n[lane] = n;
+  }
+  for (int off = 32; off; off >>= 1) n += __shfl_xor(n, off, 64);
+  __builtin_amdgcn_wave_barrier();
+  return uni(n);
+}
 
 // candidate (slot sa, slot sb) of one block: AND of every word (kept in v) and its popcount.
 // blk and pad are wave-uniform, so each word row's base is an SGPR pair and the two slot offsets
-// are the only address VGPRs (global_load saddr + voffset form).
-// WT is the exact row width (the host pads rows to an instantiated width with zero words), so
-// the loads are unrolled without guards and all 2*WT of them can be in flight.
+// are the only address VGPRs (global_load saddr + voffset form).  WT is the block's exact width
+// (rows are padded with zero words up to their tier), so the loads are unrolled without guards
+// and all 2*WT of them can be in flight.
 template <int WT>
 __device__ __forceinline__ unsigned and_count(const unsigned long long* blk, unsigned long long pad,
-                                              unsigned sa, unsigned sb, int /*W*/,
+                                              unsigned sa, unsigned sb,
                                               unsigned long long (&v)[WT]) {
   unsigned c = 0;
 #pragma unroll
@@ -111,13 +159,67 @@ __device__ __forceinline__ unsigned and_count(const unsigned long long* blk, uns
 
 template <int WT>
 __device__ __forceinline__ void write_row(unsigned long long* cb, unsigned long long cpad,
-                                          unsigned pos, int /*W*/,
-                                          const unsigned long long (&v)[WT],
+                                          unsigned pos, const unsigned long long (&v)[WT],
                                           unsigned long long ih) {
 #pragma unroll
   for (int w = 0; w < WT; ++w) cb[(unsigned long long)w * cpad + pos] = v[w];
   cb[(unsigned long long)WT * cpad + pos] = ih;
 }
+
+// the survivor's row compressed onto R (v inside R word by word), written as wt_out words
+// (zero-padded) + the item hash.  The bit offsets depend on R only, so the loop is uniform and
+// the stores are predicated on `surv`.
+template <int WT, int NW>
+__device__ __forceinline__ void write_proj(unsigned long long* cb, unsigned long long cpad,
+                                           unsigned pos, bool surv,
+                                           const unsigned long long (&v)[WT],
+                                           const ProjLds<NW>& P, unsigned wt_out,
+                                           unsigned long long ih) {
+  unsigned long long acc = 0;
+  unsigned fill = 0, q = 0;
+  // (the masks are re-read from LDS per call: hoisted out of the caller's candidate loop they
+  // would hold 12 VGPRs per word)
+  const unsigned z = vzero();
+#pragma unroll
+  for (int w = 0; w < WT; ++w) {
+    const unsigned n = uni(P.n[w + z]);
+    if (n == 0) continue;
+    unsigned long long x = v[w];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const unsigned long long t = x & P.mv[i][w + z];
+      x = (x ^ t) | (t >> (1u << i));
+    }
+    acc |= x << fill;
+    if (fill + n >= 64) {
+      if (surv) cb[(unsigned long long)q * cpad + pos] = acc;
+      ++q;
+      acc = fill ? (x >> (64 - fill)) : 0ull;
+      fill = fill + n - 64;
+    } else {
+      fill += n;
+    }
+  }
+  if (fill) {
+    if (surv) cb[(unsigned long long)q * cpad + pos] = acc;
+    ++q;
+  }
+  for (; q < wt_out; ++q)
+    if (surv) cb[(unsigned long long)q * cpad + pos] = 0ull;
+  if (surv) cb[(unsigned long long)wt_out * cpad + pos] = ih;
+}
+
+template <int MAXT>
+struct WaveLds {
+  unsigned long long f_hash[kBatchFrames];
+  unsigned f_s0[kBatchFrames], f_m[kBatchFrames], f_meta[kBatchFrames];
+  unsigned P[kBatchFrames + 1], G[kBatchFrames + 1];
+  unsigned g_cnt[kCap], g_start[kCap];
+  unsigned long long b_base[kBStack];
+  unsigned b_live[kBStack];
+  unsigned long long depth_cnt[64];
+  ProjLds<MAXT> proj;
+};
 
 struct WaveState {
   unsigned nf;                 // frames on the stack
@@ -125,13 +227,19 @@ struct WaveState {
   unsigned long long mem_top;  // bytes used in the wave's stack region
 };
 
+struct WaveAcc {
+  unsigned long long dsum, dxor, cands, chunks, budget_used;
+};
+
 // pop the top frame: its block loses a live frame
-__device__ __forceinline__ void release_frame(WaveLds& L, unsigned meta, int lane) {
+template <int MAXT>
+__device__ __forceinline__ void release_frame(WaveLds<MAXT>& L, unsigned meta, int lane) {
   const unsigned b = meta_bidx(meta);
   if (b && lane == 0) L.b_live[b - 1] -= 1;
 }
 
-__device__ __forceinline__ void free_blocks(WaveLds& L, WaveState& st) {
+template <int MAXT>
+__device__ __forceinline__ void free_blocks(WaveLds<MAXT>& L, WaveState& st) {
   __builtin_amdgcn_wave_barrier();
   while (st.nb > 0) {
     const unsigned live = uni(L.b_live[st.nb - 1 + vzero()]);
@@ -144,14 +252,13 @@ __device__ __forceinline__ void free_blocks(WaveLds& L, WaveState& st) {
 // Copy every frame on the stack to the spill heap and queue it as next-round task(s): frames of
 // more than split_min members become one single-member task each (over one shared copy).
 // Returns false (error set) when the heap or the out queue is full.
-__device__ bool spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st, WaveLds& L,
-                             int lane) {
-  const int W = a.W;
+__device__ __forceinline__ bool spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st, int lane) {
   for (unsigned f = 0; f < st.nf; ++f) {
     const DeepFrame fr = load_frame(fst + f, lane);
     const unsigned m = fr.m;
+    const unsigned wt = meta_width(fr.meta);
     const unsigned long long npad = roundup16(m);
-    const unsigned long long bytes = (unsigned long long)(W + 1) * npad * 8ull;
+    const unsigned long long bytes = (unsigned long long)(wt + 1) * npad * 8ull;
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(&a.ctl->heap_top, bytes);
     base = uni64(bcast64(base, 0));
@@ -161,7 +268,7 @@ __device__ bool spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st, W
     }
     const unsigned long long* src = (const unsigned long long*)fr.blk;
     unsigned long long* dst = (unsigned long long*)(a.heap + base);
-    const unsigned long long tot = (unsigned long long)(W + 1) * m;
+    const unsigned long long tot = (unsigned long long)(wt + 1) * m;
     for (unsigned long long e = lane; e < tot; e += 64) {
       const unsigned long long w = e / m, k = e - w * m;
       dst[w * npad + k] = src[w * fr.pad + fr.s0 + k];
@@ -183,7 +290,7 @@ __device__ bool spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st, W
       o.pad = (unsigned)npad;
       o.s0 = split ? k : 0u;
       o.m = split ? m - k : m;
-      o.meta = meta_depth(fr.meta) | ((split || single) ? kSingle : 0u);
+      o.meta = make_meta(meta_depth(fr.meta), split || single, wt, 0);
       store_frame(a.out + t0 + k, o);
     }
   }
@@ -193,26 +300,272 @@ __device__ bool spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st, W
   return true;
 }
 
-// waves per SIMD the count kernel is compiled for: the candidate's words stay in VGPRs (2 per
-// word), so 40-word rows fit 4 waves/SIMD (128 VGPRs) and 64-word rows 3 (168)
-template <int WT>
-constexpr int deep_waves_per_simd() { return WT <= 16 ? 4 : (WT <= 40 ? 3 : 2); }
+// ---- row step: member s0 against members s0+1 .. s0+m-1 (lane = candidate) ----
+// The child class (prefix P ∪ {a}) is projected onto row a when that narrows its tier.
+template <int WT, int MAXT>
+__device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, WaveState& st,
+                                         WaveLds<MAXT>& L, DeepFrame top, char* stack, int lane,
+                                         WaveAcc& acc) {
+  const unsigned long long lanelt = (1ull << lane) - 1ull;
+  const unsigned m = top.m;
+  const unsigned depth = meta_depth(top.meta);  // prefix size: members are depth+1 itemsets
+  const bool deeper = a.max_len == 0 || (int)depth + 3 <= a.max_len;  // children expandable
+  const unsigned nc = m - 1;
+  const unsigned long long cpad = roundup16(nc);
+  const unsigned long long* blk = (const unsigned long long*)top.blk;
+  const unsigned long long* ihp = blk + (unsigned long long)WT * top.pad;
+  const unsigned ia = top.s0;
+  const unsigned long long ih_a = ihp[ia + vzero()];
+  const unsigned long long h_a = top.hash + ih_a;
+  unsigned wt_out = WT;
+  if (WT > 1 && deeper && nc >= 2) {
+    const unsigned s = proj_setup<WT>(L.proj, blk, top.pad, ia, lane);
+    wt_out = tier_of((s + 63) / 64);
+  }
+  const bool proj = wt_out < (unsigned)WT;
+  unsigned long long* cb = (unsigned long long*)(stack + st.mem_top);
+  unsigned S = 0;
+  for (unsigned c0 = 0; c0 < nc; c0 += 64) {
+    const bool act = c0 + lane < nc;
+    const unsigned jb = act ? ia + 1 + c0 + lane : ia;
+    unsigned long long v[WT];
+    const unsigned c = and_count<WT>(blk, top.pad, ia + vzero(), jb, v);
+    const bool surv = act && c >= a.minsup;
+    const unsigned long long mask = __ballot(surv);
+    const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
+    unsigned long long ih_b = 0;
+    if (surv) {
+      ih_b = ihp[jb];
+      const DigestTerms dt = digest_terms(h_a + ih_b, c);
+      acc.dsum += dt.sum;
+      acc.dxor ^= dt.xr;
+    }
+    if (deeper) {
+      if (proj) {
+        write_proj<WT>(cb, cpad, pos, surv, v, L.proj, wt_out, ih_b);
+      } else if (surv) {
+        write_row<WT>(cb, cpad, pos, v, ih_b);
+      }
+    }
+    S += (unsigned)__popcll(mask);
+    ++acc.chunks;
+  }
+  acc.cands += nc;
+  if (lane == 0 && S) L.depth_cnt[depth + 2] += S;
+  acc.budget_used += (nc + 63) / 64;
+  // parent: done with member s0
+  if ((top.meta & kSingle) || m <= 2) {
+    release_frame(L, top.meta, lane);
+    st.nf -= 1;
+  } else {
+    top.s0 += 1;
+    top.m -= 1;
+    if (lane == 0) store_frame(fst + st.nf - 1, top);
+  }
+  if (S >= 2 && deeper) {
+    if (lane == 0) {
+      L.b_base[st.nb] = st.mem_top;
+      L.b_live[st.nb] = 1;
+      DeepFrame c;
+      c.blk = (unsigned long long)cb;
+      c.hash = h_a;
+      c.pad = (unsigned)cpad;
+      c.s0 = 0;
+      c.m = S;
+      c.meta = make_meta(depth + 1, false, wt_out, st.nb + 1);
+      store_frame(fst + st.nf, c);
+    }
+    st.nb += 1;
+    st.nf += 1;
+    st.mem_top += (unsigned long long)(wt_out + 1) * cpad * 8ull;
+  }
+}
 
-template <int WT>
-__global__ __launch_bounds__(256, deep_waves_per_simd<WT>()) void k_deep_count(DeepArgs a) {
-  __shared__ WaveLds lds[kWaves];
+// ---- batch step: the top frames' member pairs, up to kCap lanes ----
+// (frames of the top frame's block only: sibling classes, so the block base and width stay
+// uniform)
+template <int WT, int MAXT>
+__device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, WaveState& st,
+                                           WaveLds<MAXT>& L, DeepFrame top, char* stack,
+                                           int lane, WaveAcc& acc) {
+  const unsigned long long lanelt = (1ull << lane) - 1ull;
+  unsigned long long* cb = (unsigned long long*)(stack + st.mem_top);
+  unsigned k = 0, P = 0;
+  {
+    // frame f (from the top) is read by lane f: vector loads, then two wave scans
+    unsigned fm = 0, fmeta = kSingle;
+    if (lane < kBatchFrames && (unsigned)lane < st.nf) {
+      const DeepFrame* p = fst + (st.nf - 1 - lane);
+      fm = p->m;
+      fmeta = p->meta;
+      if (p->blk != top.blk) fmeta |= kSingle;  // another block: ends the batch
+      L.f_hash[lane] = p->hash;
+      L.f_s0[lane] = p->s0;
+      L.f_m[lane] = fm;
+      L.f_meta[lane] = fmeta;
+    }
+    const unsigned fp = (fmeta & kSingle) ? 0xffffffffu : fm * (fm - 1) / 2;
+    // inclusive scan of pairs over lanes (lanes >= nf carry "infinite")
+    unsigned incl = fp;
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl = (o == 0xffffffffu || incl == 0xffffffffu || o + incl < o)
+                                  ? 0xffffffffu : o + incl;
+    }
+    const unsigned long long okm = __ballot(incl <= (unsigned)kCap && (unsigned)lane < st.nf);
+    // frames 0 .. k-1 fit (prefix property: the first failing lane ends the run)
+    k = okm == ~0ull ? 64u : (unsigned)__builtin_ctzll(~okm);
+    if (k == 0) k = 1;  // top frame always fits (pairs <= kCap, not single)
+    k = uni(k);
+    P = uni(__shfl(incl, (int)k - 1, 64));
+    const unsigned excl = incl - fp;
+    if ((unsigned)lane < k) L.P[lane] = excl;
+    if (lane == 0) L.P[k] = P;
+    // member-group prefix (m - 1 per frame)
+    unsigned gm = ((unsigned)lane < k) ? fm - 1 : 0u;
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned o = __shfl_up(gm, off, 64);
+      if (lane >= off) gm += o;
+    }
+    const unsigned gtot = __shfl(gm, (int)k - 1, 64);
+    if ((unsigned)lane < k) L.G[lane] = gm - (fm - 1);
+    if (lane == 0) L.G[k] = gtot;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const unsigned NG = uni(L.G[k + vzero()]);
+  for (unsigned g = lane; g < NG; g += 64) {
+    L.g_cnt[g] = 0;
+    L.g_start[g] = 0xffffffffu;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const unsigned long long cpad = roundup16(P);
+  const unsigned long long* bblk = (const unsigned long long*)top.blk;
+  const unsigned long long bpad = top.pad;
+  const unsigned long long* ihp = bblk + (unsigned long long)WT * bpad;
+  unsigned S = 0;
+  for (unsigned c0 = 0; c0 < P; c0 += 64) {
+    const unsigned p = c0 + lane;
+    const bool act = p < P;
+    // frame of pair p: largest f < k with P[f] <= p
+    unsigned f = 0;
+    for (unsigned step = 32; step; step >>= 1)
+      if (f + step < k && L.P[f + step] <= p) f += step;
+    if (!act) f = 0;
+    const unsigned fmm = L.f_m[f];
+    const unsigned q = act ? p - L.P[f] : 0u;
+    // triangular decode of q into (i, j), i < j < fmm, row-major over i
+    const float twoM = 2.0f * (float)fmm - 1.0f;
+    unsigned i = (unsigned)((twoM - sqrtf(twoM * twoM - 8.0f * (float)q)) * 0.5f);
+    auto row0 = [&](unsigned r) { return r * fmm - r * (r + 1) / 2; };
+    while (i > 0 && row0(i) > q) --i;
+    while (i + 1 < fmm && row0(i + 1) <= q) ++i;
+    const unsigned j = q - row0(i) + i + 1;
+    const unsigned sa = L.f_s0[f] + i, sb = L.f_s0[f] + (act ? j : i);
+    unsigned long long v[WT];
+    const unsigned c = and_count<WT>(bblk, bpad, sa, sb, v);
+    const bool surv = act && c >= a.minsup;
+    const unsigned long long mask = __ballot(surv);
+    if (surv) {
+      const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
+      const unsigned long long ih_a = ihp[sa], ih_b = ihp[sb];
+      write_row<WT>(cb, cpad, pos, v, ih_b);
+      const DigestTerms dt = digest_terms(L.f_hash[f] + ih_a + ih_b, c);
+      acc.dsum += dt.sum;
+      acc.dxor ^= dt.xr;
+      atomicAdd(&L.depth_cnt[meta_depth(L.f_meta[f]) + 2], 1ull);
+      const unsigned g = L.G[f] + i;
+      atomicAdd(&L.g_cnt[g], 1u);
+      atomicMin(&L.g_start[g], pos);
+    }
+    S += (unsigned)__popcll(mask);
+    ++acc.chunks;
+  }
+  acc.cands += P;
+  acc.budget_used += (P + 63) / 64;
+  // the k consumed frames leave the stack
+  if ((unsigned)lane < k) {
+    const unsigned b = meta_bidx(L.f_meta[lane]);
+    if (b) atomicSub(&L.b_live[b - 1], 1u);
+  }
+  st.nf -= k;
+  __builtin_amdgcn_wave_barrier();
+  // child frames: groups with >= 2 survivors
+  unsigned pushed = 0;
+  const unsigned nbi = st.nb;
+  for (unsigned g0 = 0; g0 < NG; g0 += 64) {
+    const unsigned g = g0 + lane;
+    bool mk = false;
+    unsigned f = 0;
+    if (g < NG) {
+      for (unsigned step = 32; step; step >>= 1)
+        if (f + step < k && L.G[f + step] <= g) f += step;
+      mk = L.g_cnt[g] >= 2 && (a.max_len == 0 || (int)meta_depth(L.f_meta[f]) + 3 <= a.max_len);
+    }
+    const unsigned long long mask = __ballot(mk);
+    if (mk) {
+      const unsigned slot = st.nf + pushed + (unsigned)__popcll(mask & lanelt);
+      const unsigned i = g - L.G[f];
+      const unsigned long long ih_a = ihp[L.f_s0[f] + i];
+      DeepFrame c;
+      c.blk = (unsigned long long)cb;
+      c.hash = L.f_hash[f] + ih_a;
+      c.pad = (unsigned)cpad;
+      c.s0 = L.g_start[g];
+      c.m = L.g_cnt[g];
+      c.meta = make_meta(meta_depth(L.f_meta[f]) + 1, false, WT, nbi + 1);
+      store_frame(fst + slot, c);
+    }
+    pushed += (unsigned)__popcll(mask);
+  }
+  pushed = uni(pushed);
+  if (pushed) {
+    if (lane == 0) {
+      L.b_base[st.nb] = st.mem_top;
+      L.b_live[st.nb] = pushed;
+    }
+    st.nb += 1;
+    st.nf += pushed;
+    st.mem_top += (unsigned long long)(WT + 1) * cpad * 8ull;
+  }
+}
+
+// one step of the top frame, dispatched on its block width (wave-uniform)
+template <int MAXT, int T0, int... Ts>
+__device__ __forceinline__ void step_tier(unsigned wt, bool row_mode, const DeepArgs& a,
+                                          DeepFrame* fst, WaveState& st, WaveLds<MAXT>& L,
+                                          const DeepFrame& top, char* stack, int lane,
+                                          WaveAcc& acc) {
+  if constexpr (T0 <= MAXT) {
+    if (wt == (unsigned)T0) {
+      if (row_mode)
+        row_step<T0, MAXT>(a, fst, st, L, top, stack, lane, acc);
+      else
+        batch_step<T0, MAXT>(a, fst, st, L, top, stack, lane, acc);
+      return;
+    }
+  }
+  if constexpr (sizeof...(Ts) > 0) step_tier<MAXT, Ts...>(wt, row_mode, a, fst, st, L, top, stack,
+                                                          lane, acc);
+}
+
+// waves per SIMD the count kernel is compiled for by default: the register budget that keeps
+// the widest tier of the launch free of scratch spills (blocks_per_cu may select the other
+// instance of a width class)
+template <int MAXT>
+constexpr int deep_waves_per_simd() { return MAXT <= 8 ? 4 : (MAXT <= 16 ? 3 : 2); }
+
+template <int MAXT, int WPS>
+__global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
+  __shared__ WaveLds<MAXT> lds[kWaves];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  WaveLds& L = lds[wid];
+  WaveLds<MAXT>& L = lds[wid];
   const unsigned long long gw = (unsigned long long)blockIdx.x * kWaves + wid;
   DeepFrame* fst = a.fstacks + gw * (unsigned long long)a.fcap;
   char* stack = a.stacks + gw * a.stack_bytes;
-  const int W = a.W;
-  const unsigned minsup = a.minsup;
-  const unsigned long long lanelt = (1ull << lane) - 1ull;
 
   for (int d = lane; d < 64; d += 64) L.depth_cnt[d] = 0;
-  unsigned long long dsum = 0, dxor = 0, cands = 0, chunks_total = 0;
+  WaveAcc acc{0, 0, 0, 0, 0};
   __builtin_amdgcn_wave_barrier();
 
   WaveState st{0, 0, 0};
@@ -233,7 +586,7 @@ __global__ __launch_bounds__(256, deep_waves_per_simd<WT>()) void k_deep_count(D
       st.nb = 0;
       st.mem_top = 0;
     }
-    unsigned long long budget_used = 0;
+    acc.budget_used = 0;
     while (st.nf > 0) {
       __builtin_amdgcn_wave_barrier();
       // bounded: a round that runs past its deadline gives up (error bit 2) instead of holding
@@ -243,235 +596,39 @@ __global__ __launch_bounds__(256, deep_waves_per_simd<WT>()) void k_deep_count(D
         failed = true;
         break;
       }
-      DeepFrame top = load_frame(fst + st.nf - 1, lane);
+      const DeepFrame top = load_frame(fst + st.nf - 1, lane);
       const unsigned m = top.m;
+      const unsigned wt = meta_width(top.meta);
       const unsigned long long pairs = (unsigned long long)m * (m - 1) / 2;
       const bool row_mode = (top.meta & kSingle) || pairs > (unsigned long long)kCap;
       const unsigned long long need =
-          (unsigned long long)(W + 1) * roundup16(row_mode ? m : kCap) * 8ull;
-      if (budget_used >= a.budget || st.mem_top + need > a.stack_bytes ||
+          (unsigned long long)(wt + 1) * roundup16(row_mode ? m : kCap) * 8ull;
+      if (acc.budget_used >= a.budget || st.mem_top + need > a.stack_bytes ||
           st.nf + kCap + 2 > (unsigned)a.fcap || st.nb + 1 >= (unsigned)kBStack) {
-        if (!spill_frames(a, fst, st, L, lane)) failed = true;
+        if (!spill_frames(a, fst, st, lane)) failed = true;
         break;
       }
-      const unsigned depth = meta_depth(top.meta);  // prefix size: members are depth+1 itemsets
-      const bool deeper = a.max_len == 0 || (int)depth + 3 <= a.max_len;  // children expandable
-      unsigned long long* cb = (unsigned long long*)(stack + st.mem_top);
-      if (row_mode) {
-        // ---- row step: member s0 against members s0+1 .. s0+m-1 ----
-        const unsigned nc = m - 1;
-        const unsigned long long cpad = roundup16(nc);
-        const unsigned long long* blk = (const unsigned long long*)top.blk;
-        const unsigned long long* ihp = blk + (unsigned long long)W * top.pad;
-        const unsigned ia = top.s0;
-        const unsigned long long ih_a = ihp[ia + vzero()];
-        const unsigned long long h_a = top.hash + ih_a;
-        unsigned S = 0;
-        for (unsigned c0 = 0; c0 < nc; c0 += 64) {
-          const bool act = c0 + lane < nc;
-          const unsigned jb = act ? ia + 1 + c0 + lane : ia;
-          unsigned long long v[WT];
-          const unsigned c = and_count<WT>(blk, top.pad, ia + vzero(), jb, W, v);
-          const bool surv = act && c >= minsup;
-          const unsigned long long mask = __ballot(surv);
-          if (surv) {
-            const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
-            const unsigned long long ih_b = ihp[jb];
-            write_row<WT>(cb, cpad, pos, W, v, ih_b);
-            const DigestTerms dt = digest_terms(h_a + ih_b, c);
-            dsum += dt.sum;
-            dxor ^= dt.xr;
-          }
-          S += (unsigned)__popcll(mask);
-          ++chunks_total;
-        }
-        cands += nc;
-        if (lane == 0 && S) L.depth_cnt[depth + 2] += S;
-        budget_used += (nc + 63) / 64;
-        // parent: done with member s0
-        if ((top.meta & kSingle) || m <= 2) {
-          release_frame(L, top.meta, lane);
-          st.nf -= 1;
-        } else {
-          top.s0 += 1;
-          top.m -= 1;
-          if (lane == 0) store_frame(fst + st.nf - 1, top);
-        }
-        if (S >= 2 && deeper) {
-          if (lane == 0) {
-            L.b_base[st.nb] = st.mem_top;
-            L.b_live[st.nb] = 1;
-            DeepFrame c;
-            c.blk = (unsigned long long)cb;
-            c.hash = h_a;
-            c.pad = (unsigned)cpad;
-            c.s0 = 0;
-            c.m = S;
-            c.meta = (depth + 1) | ((st.nb + 1) << 16);
-            store_frame(fst + st.nf, c);
-          }
-          st.nb += 1;
-          st.nf += 1;
-          st.mem_top += (unsigned long long)(W + 1) * cpad * 8ull;
-        }
-        free_blocks(L, st);
-        continue;
+      if (wt == 0 || wt > (unsigned)MAXT) {  // never produced by the host or the steps
+        if (lane == 0) atomicOr(&a.ctl->error, 8u);
+        failed = true;
+        break;
       }
-      // ---- batch step: the top frames' member pairs, up to kCap lanes ----
-      // (frames of the top frame's block only: sibling classes, so the block base stays uniform)
-      unsigned k = 0, P = 0;
-      {
-        // frame f (from the top) is read by lane f: vector loads, then two wave scans
-        unsigned fm = 0, fmeta = kSingle;
-        if (lane < kBatchFrames && (unsigned)lane < st.nf) {
-          const DeepFrame* p = fst + (st.nf - 1 - lane);
-          fm = p->m;
-          fmeta = p->meta;
-          if (p->blk != top.blk) fmeta |= kSingle;  // another block: ends the batch
-          L.f_hash[lane] = p->hash;
-          L.f_s0[lane] = p->s0;
-          L.f_m[lane] = fm;
-          L.f_meta[lane] = fmeta;
-        }
-        const unsigned fp = (fmeta & kSingle) ? 0xffffffffu : fm * (fm - 1) / 2;
-        // inclusive scan of pairs over lanes (lanes >= nf carry "infinite")
-        unsigned incl = fp;
-        for (int off = 1; off < 64; off <<= 1) {
-          const unsigned o = __shfl_up(incl, off, 64);
-          if (lane >= off) incl = (o == 0xffffffffu || incl == 0xffffffffu || o + incl < o)
-                                      ? 0xffffffffu : o + incl;
-        }
-        const unsigned long long okm = __ballot(incl <= (unsigned)kCap && (unsigned)lane < st.nf);
-        // frames 0 .. k-1 fit (prefix property: the first failing lane ends the run)
-        k = okm == ~0ull ? 64u : (unsigned)__builtin_ctzll(~okm);
-        if (k == 0) k = 1;  // top frame always fits (pairs <= kCap, not single)
-        k = uni(k);
-        P = uni(__shfl(incl, (int)k - 1, 64));
-        const unsigned excl = incl - fp;
-        if ((unsigned)lane < k) {
-          L.P[lane] = excl;
-        }
-        if (lane == 0) L.P[k] = P;
-        // member-group prefix (m - 1 per frame)
-        unsigned gm = ((unsigned)lane < k) ? fm - 1 : 0u;
-        for (int off = 1; off < 64; off <<= 1) {
-          const unsigned o = __shfl_up(gm, off, 64);
-          if (lane >= off) gm += o;
-        }
-        const unsigned gtot = __shfl(gm, (int)k - 1, 64);
-        if ((unsigned)lane < k) L.G[lane] = gm - (fm - 1);
-        if (lane == 0) L.G[k] = gtot;
-      }
-      __builtin_amdgcn_wave_barrier();
-      const unsigned NG = uni(L.G[k + vzero()]);
-      for (unsigned g = lane; g < NG; g += 64) {
-        L.g_cnt[g] = 0;
-        L.g_start[g] = 0xffffffffu;
-      }
-      __builtin_amdgcn_wave_barrier();
-      const unsigned long long cpad = roundup16(P);
-      const unsigned long long* bblk = (const unsigned long long*)top.blk;
-      const unsigned long long bpad = top.pad;
-      unsigned S = 0;
-      for (unsigned c0 = 0; c0 < P; c0 += 64) {
-        const unsigned p = c0 + lane;
-        const bool act = p < P;
-        // frame of pair p: largest f < k with P[f] <= p
-        unsigned f = 0;
-        for (unsigned step = 32; step; step >>= 1)
-          if (f + step < k && L.P[f + step] <= p) f += step;
-        if (!act) f = 0;
-        const unsigned fmm = L.f_m[f];
-        const unsigned q = act ? p - L.P[f] : 0u;
-        // triangular decode of q into (i, j), i < j < fmm, row-major over i
-        const float twoM = 2.0f * (float)fmm - 1.0f;
-        unsigned i = (unsigned)((twoM - sqrtf(twoM * twoM - 8.0f * (float)q)) * 0.5f);
-        auto row0 = [&](unsigned r) { return r * fmm - r * (r + 1) / 2; };
-        while (i > 0 && row0(i) > q) --i;
-        while (i + 1 < fmm && row0(i + 1) <= q) ++i;
-        const unsigned j = q - row0(i) + i + 1;
-        const unsigned sa = L.f_s0[f] + i, sb = L.f_s0[f] + (act ? j : i);
-        unsigned long long v[WT];
-        const unsigned c = and_count<WT>(bblk, bpad, sa, sb, W, v);
-        const bool surv = act && c >= minsup;
-        const unsigned long long mask = __ballot(surv);
-        if (surv) {
-          const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
-          const unsigned long long* ihp = bblk + (unsigned long long)W * bpad;
-          const unsigned long long ih_a = ihp[sa], ih_b = ihp[sb];
-          write_row<WT>(cb, cpad, pos, W, v, ih_b);
-          const DigestTerms dt = digest_terms(L.f_hash[f] + ih_a + ih_b, c);
-          dsum += dt.sum;
-          dxor ^= dt.xr;
-          atomicAdd(&L.depth_cnt[meta_depth(L.f_meta[f]) + 2], 1ull);
-          const unsigned g = L.G[f] + i;
-          atomicAdd(&L.g_cnt[g], 1u);
-          atomicMin(&L.g_start[g], pos);
-        }
-        S += (unsigned)__popcll(mask);
-        ++chunks_total;
-      }
-      cands += P;
-      budget_used += (P + 63) / 64;
-      // the k consumed frames leave the stack
-      if ((unsigned)lane < k) {
-        const unsigned b = meta_bidx(L.f_meta[lane]);
-        if (b) atomicSub(&L.b_live[b - 1], 1u);
-      }
-      st.nf -= k;
-      __builtin_amdgcn_wave_barrier();
-      // child frames: groups with >= 2 survivors
-      unsigned pushed = 0;
-      const unsigned nbi = st.nb;
-      for (unsigned g0 = 0; g0 < NG; g0 += 64) {
-        const unsigned g = g0 + lane;
-        bool mk = false;
-        unsigned f = 0;
-        if (g < NG) {
-          for (unsigned step = 32; step; step >>= 1)
-            if (f + step < k && L.G[f + step] <= g) f += step;
-          mk = L.g_cnt[g] >= 2 && (a.max_len == 0 || (int)meta_depth(L.f_meta[f]) + 3 <= a.max_len);
-        }
-        const unsigned long long mask = __ballot(mk);
-        if (mk) {
-          const unsigned slot = st.nf + pushed + (unsigned)__popcll(mask & lanelt);
-          const unsigned i = g - L.G[f];
-          const unsigned long long ih_a = bblk[(unsigned long long)W * bpad + L.f_s0[f] + i];
-          DeepFrame c;
-          c.blk = (unsigned long long)cb;
-          c.hash = L.f_hash[f] + ih_a;
-          c.pad = (unsigned)cpad;
-          c.s0 = L.g_start[g];
-          c.m = L.g_cnt[g];
-          c.meta = (meta_depth(L.f_meta[f]) + 1) | ((nbi + 1) << 16);
-          store_frame(fst + slot, c);
-        }
-        pushed += (unsigned)__popcll(mask);
-      }
-      pushed = uni(pushed);
-      if (pushed) {
-        if (lane == 0) {
-          L.b_base[st.nb] = st.mem_top;
-          L.b_live[st.nb] = pushed;
-        }
-        st.nb += 1;
-        st.nf += pushed;
-        st.mem_top += (unsigned long long)(W + 1) * cpad * 8ull;
-      }
+      step_tier<MAXT, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64>(wt, row_mode, a, fst, st, L, top,
+                                                               stack, lane, acc);
       free_blocks(L, st);
     }
   }
   // flush: wave reduction of the digest terms, per-depth counts from LDS
   for (int off = 32; off; off >>= 1) {
-    dsum += shfl_xor64(dsum, off);
-    dxor ^= shfl_xor64(dxor, off);
+    acc.dsum += shfl_xor64(acc.dsum, off);
+    acc.dxor ^= shfl_xor64(acc.dxor, off);
   }
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) {
-    atomicAdd(&a.ctl->digest_sum, dsum);
-    atomicXor(&a.ctl->digest_xor, dxor);
-    atomicAdd(&a.ctl->candidates, cands);
-    atomicAdd(&a.ctl->chunks, chunks_total);
+    atomicAdd(&a.ctl->digest_sum, acc.dsum);
+    atomicXor(&a.ctl->digest_xor, acc.dxor);
+    atomicAdd(&a.ctl->candidates, acc.cands);
+    atomicAdd(&a.ctl->chunks, acc.chunks);
   }
   for (int d = lane; d < 64; d += 64)
     if (L.depth_cnt[d]) atomicAdd(&a.ctl->per_depth[d], L.depth_cnt[d]);
@@ -494,21 +651,33 @@ __global__ void k_deep_transpose(const unsigned long long* bm, long long Wp, lon
 }
 
 // one wave per root item i: its frequent pairs with every later item j (lane = candidate);
-// fill == false: count only (m[i]); fill == true: write block i (slots in j order) and, when
+// fill == false: count only (m[i]); fill == true: write block i (slots in j order), projected
+// onto row i (the block's width comes from its byte size: blk_off[i+1] - blk_off[i]) and, when
 // ctl != nullptr, add the level-2 digest terms
 template <int WT>
-__global__ __launch_bounds__(256, deep_waves_per_simd<WT>()) void k_deep_root(const unsigned long long* root, long long Fpad,
-                                                   long long F, int W, unsigned minsup,
-                                                   int32_t* m_out, const long long* blk_off,
-                                                   char* base, DeepCtl* ctl, int fill) {
+__global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* root, long long Fpad,
+                                                   long long F, unsigned minsup, int32_t* m_out,
+                                                   const long long* blk_off, char* base,
+                                                   DeepCtl* ctl, int fill) {
+  __shared__ ProjLds<WT> projs[kWaves];
   const int lane = threadIdx.x & 63;
   const long long i = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (i >= F) return;
-  const unsigned long long* ihp = root + (unsigned long long)W * Fpad;
+  if (i >= F) return;  // wave-uniform
+  ProjLds<WT>& PL = projs[threadIdx.x >> 6];
+  const unsigned long long* ihp = root + (unsigned long long)WT * Fpad;
   const unsigned long long h_a = ihp[i];
   const long long nc = F - 1 - i;
-  unsigned long long* cb = fill ? (unsigned long long*)(base + blk_off[i]) : nullptr;
-  const unsigned long long cpad = roundup16((unsigned long long)(fill ? m_out[i] : 0));
+  unsigned long long* cb = nullptr;
+  unsigned long long cpad = 0;
+  unsigned wt_out = WT;
+  if (fill) {
+    cpad = roundup16((unsigned long long)m_out[i]);
+    if (cpad == 0) return;  // wave-uniform: no frequent pair
+    cb = (unsigned long long*)(base + blk_off[i]);
+    wt_out = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * cpad)) - 1u;
+    if (wt_out < (unsigned)WT) proj_setup<WT>(PL, root, (unsigned long long)Fpad, (unsigned)i, lane);
+  }
+  const bool proj = wt_out < (unsigned)WT;
   unsigned S = 0;
   unsigned long long dsum = 0, dxor = 0;
   const unsigned long long lanelt = (1ull << lane) - 1ull;
@@ -516,14 +685,17 @@ __global__ __launch_bounds__(256, deep_waves_per_simd<WT>()) void k_deep_root(co
     const bool act = c0 + lane < nc;
     const long long jb = act ? i + 1 + c0 + lane : i;
     unsigned long long v[WT];
-    const unsigned c = and_count<WT>(root, (unsigned long long)Fpad, (unsigned)i + vzero(), (unsigned)jb, W, v);
+    const unsigned c = and_count<WT>(root, (unsigned long long)Fpad, (unsigned)i + vzero(), (unsigned)jb, v);
     const bool surv = act && c >= minsup;
     const unsigned long long mask = __ballot(surv);
-    if (surv && fill) {
+    if (fill) {
       const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
-      const unsigned long long ih_b = ihp[jb];
-      write_row<WT>(cb, cpad, pos, W, v, ih_b);
-      if (ctl) {
+      const unsigned long long ih_b = surv ? ihp[jb] : 0ull;
+      if (proj)
+        write_proj<WT>(cb, cpad, pos, surv, v, PL, wt_out, ih_b);
+      else if (surv)
+        write_row<WT>(cb, cpad, pos, v, ih_b);
+      if (ctl && surv) {
         const DigestTerms dt = digest_terms(h_a + ih_b, c);
         dsum += dt.sum;
         dxor ^= dt.xr;
@@ -557,47 +729,51 @@ __global__ void k_deep_root_tasks(const long long* blk_off, const int32_t* m, co
   const int mi = m[i];
   if (mi < 2) return;
   const unsigned long long h = root[(unsigned long long)W * Fpad + i];
+  const unsigned long long pad = roundup16((unsigned long long)mi);
+  const unsigned wt = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * pad)) - 1u;
   for (int k = threadIdx.x; k < mi - 1; k += blockDim.x) {
     const long long t = task_off[i] + k;
     if (t % world != rank) continue;
     DeepFrame f;
     f.blk = (unsigned long long)(base + blk_off[i]);
     f.hash = h;
-    f.pad = (unsigned)roundup16((unsigned long long)mi);
+    f.pad = (unsigned)pad;
     f.s0 = (unsigned)k;
     f.m = (unsigned)(mi - k);
-    f.meta = 1u | kSingle;
+    f.meta = make_meta(1, true, wt, 0);
     store_frame(out + t / world, f);
   }
 }
 
-// instantiated row widths (words); deep_row_words() rounds W up to one of them
+// instantiated widths: the tiers (root blocks, and the count kernel's widest tier)
 template <typename Fn>
-void by_width(int W, Fn&& fn) {
+void by_tier(int W, Fn&& fn) {
   switch (W) {
+    case 1: fn(std::integral_constant<int, 1>{}); break;
+    case 2: fn(std::integral_constant<int, 2>{}); break;
+    case 3: fn(std::integral_constant<int, 3>{}); break;
     case 4: fn(std::integral_constant<int, 4>{}); break;
+    case 6: fn(std::integral_constant<int, 6>{}); break;
     case 8: fn(std::integral_constant<int, 8>{}); break;
     case 12: fn(std::integral_constant<int, 12>{}); break;
     case 16: fn(std::integral_constant<int, 16>{}); break;
-    case 20: fn(std::integral_constant<int, 20>{}); break;
     case 24: fn(std::integral_constant<int, 24>{}); break;
-    case 28: fn(std::integral_constant<int, 28>{}); break;
     case 32: fn(std::integral_constant<int, 32>{}); break;
-    case 36: fn(std::integral_constant<int, 36>{}); break;
-    case 40: fn(std::integral_constant<int, 40>{}); break;
     case 48: fn(std::integral_constant<int, 48>{}); break;
-    case 56: fn(std::integral_constant<int, 56>{}); break;
     case 64: fn(std::integral_constant<int, 64>{}); break;
-    default: break;  // deep_row_words() never returns another width
+    default: break;  // deep_tier() never returns another width
   }
 }
 
 }  // namespace
 
 int deep_max_words() { return 64; }
-int deep_row_words(int W) {
-  if (W <= 40) return W <= 0 ? 4 : (W + 3) / 4 * 4;
-  return (W + 7) / 8 * 8;
+int deep_tier(int words) { return (int)tier_of((unsigned)std::max(words, 1)); }
+int deep_row_words(int W) { return deep_tier(W); }
+int deep_count_maxt(int widest) { return widest <= 8 ? 8 : widest <= 16 ? 16 : widest <= 32 ? 32 : 64; }
+int deep_waves_per_simd(int maxt) {
+  return maxt <= 8 ? deep_waves_per_simd<8>() : maxt <= 16 ? deep_waves_per_simd<16>()
+       : maxt <= 32 ? deep_waves_per_simd<32>() : deep_waves_per_simd<64>();
 }
 int deep_waves_per_block() { return kWaves; }
 int deep_min_fcap() { return kCap + 64; }
@@ -619,9 +795,9 @@ void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t mi
                hipStream_t s) {
   const unsigned grid = (unsigned)((F + 3) / 4);
   if (!grid) return;
-  by_width(W, [&](auto wt) {
+  by_tier(W, [&](auto wt) {
     hipLaunchKernelGGL(k_deep_root<decltype(wt)::value>, dim3(grid), dim3(256), 0, s,
-                       (const unsigned long long*)root, (long long)Fpad, (long long)F, W, minsup,
+                       (const unsigned long long*)root, (long long)Fpad, (long long)F, minsup,
                        m, (const long long*)blk_off, base, ctl, fill ? 1 : 0);
   });
 }
@@ -635,11 +811,25 @@ void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* ta
                      (const unsigned long long*)root, (long long)Fpad, W, rank, world, out);
 }
 
-void deep_count(const DeepArgs& a, int grid, hipStream_t s) {
-  by_width(a.W, [&](auto wt) {
-    hipLaunchKernelGGL(k_deep_count<decltype(wt)::value>, dim3((unsigned)grid),
-                       dim3(64 * kWaves), 0, s, a);
-  });
+int deep_count_wps(int maxt, int want) {
+  const int mt = deep_count_maxt(maxt);
+  if (mt == 8 && (want == 4 || want == 5)) return want;
+  if (mt == 16 && (want == 3 || want == 4)) return want;
+  if (mt == 32 && (want == 2 || want == 3)) return want;
+  return deep_waves_per_simd(mt);
+}
+
+void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s) {
+  const int mt = deep_count_maxt(maxt);
+  const int w = deep_count_wps(mt, wps);
+  const dim3 g((unsigned)grid), b(64 * kWaves);
+  if (mt == 8 && w == 5) hipLaunchKernelGGL((k_deep_count<8, 5>), g, b, 0, s, a);
+  else if (mt == 8) hipLaunchKernelGGL((k_deep_count<8, 4>), g, b, 0, s, a);
+  else if (mt == 16 && w == 4) hipLaunchKernelGGL((k_deep_count<16, 4>), g, b, 0, s, a);
+  else if (mt == 16) hipLaunchKernelGGL((k_deep_count<16, 3>), g, b, 0, s, a);
+  else if (mt == 32 && w == 3) hipLaunchKernelGGL((k_deep_count<32, 3>), g, b, 0, s, a);
+  else if (mt == 32) hipLaunchKernelGGL((k_deep_count<32, 2>), g, b, 0, s, a);
+  else hipLaunchKernelGGL((k_deep_count<64, 2>), g, b, 0, s, a);
 }
 
 }  // namespace kern

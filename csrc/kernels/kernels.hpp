@@ -15,7 +15,8 @@ struct DeepFrame {  // one class: members P ∪ {x_k}, k in [s0, s0 + m), of a w
   unsigned pad;             // slot stride (multiple of 16)
   unsigned s0;              // first member slot
   unsigned m;               // members
-  unsigned meta;            // bits 0-7 |P|, bit 8 single (expand member s0 only), 16-31 block index
+  unsigned meta;            // bits 0-7 |P|, bit 8 single (expand member s0 only), 9-15 block
+                            // width (words), 16-31 block index
 };
 static_assert(sizeof(DeepFrame) == 32, "DeepFrame is read as 8 dwords");
 struct DeepCtl {  // per-round control + accumulated results (zeroed once per call)
@@ -25,7 +26,8 @@ struct DeepCtl {  // per-round control + accumulated results (zeroed once per ca
   unsigned long long digest_sum, digest_xor;
   unsigned long long candidates, chunks;
   unsigned long long per_depth[64];
-  unsigned error;                 // bit 0 out queue full, bit 1 heap full, bit 2 timeout
+  unsigned error;                 // bit 0 out queue full, bit 1 heap full, bit 2 timeout,
+                                  // bit 3 a frame of an uninstantiated width
   unsigned pad_[3];
 };
 struct DeepArgs {
@@ -48,7 +50,11 @@ struct DeepArgs {
   unsigned long long timeout_ticks;  // wall_clock64 ticks a wave may run (then error bit 2)
 };
 int deep_max_words();
-int deep_row_words(int W);  // instantiated row width >= W (blocks are padded with zero words)
+int deep_tier(int words);     // smallest instantiated block width >= words
+int deep_row_words(int W);    // root block width for W-word rows (a tier)
+int deep_count_maxt(int widest);    // count kernel instance covering block widths <= widest
+int deep_waves_per_simd(int maxt);  // its default occupancy (and blocks per CU)
+int deep_count_wps(int maxt, int want);  // instance occupancy: `want` if instantiated
 int deep_waves_per_block();
 int deep_min_fcap();
 size_t deep_row_block_bytes(int W, int64_t m);  // stack room one step over m members may need
@@ -60,7 +66,7 @@ void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t mi
 void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
                      char* base, const uint64_t* root, int64_t Fpad, int W, int rank, int world,
                      DeepFrame* out, hipStream_t s);
-void deep_count(const DeepArgs& a, int grid, hipStream_t s);
+void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s);
 
 // ---- mining (mine.hip) ----
 void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* counts,

@@ -65,6 +65,7 @@ int main(int argc, char** argv) {
     in.F = F;
     in.W_real = (int)W;
     in.d_ids = fi.ids.data();
+    in.counts = fi.counts.data();
     in.minsup = fi.minsup2;
     in.max_len = max_len;
     in.n_cus = 2;

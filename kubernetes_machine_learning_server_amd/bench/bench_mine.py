@@ -1,0 +1,334 @@
+"""Mining sections of ``bench.py`` (the headline itself lives in bench.py).
+
+* ``run_deep``       — count-only full mining of one dataset, split over the ranks (the headline
+                       and the config-2 family); verified by the itemset digest.
+* ``run_levelwise``  — the round-2 headline form: ds1 @0.05 through the level-wise graph path
+                       with the trie download and the device rule map in the step, verified
+                       against the native CPU miner; at N > 1 one relabelled dataset per rank
+                       (weak scaling, a secondary field of the bench line).
+* ``run_config2``    — BASELINE config 2 (ds1 @0.01): the deployed rule map, mining truncated at
+                       4 items, and full mining at 0.01 with the size cap raised until a time
+                       budget is spent (per-level counts up to the cap).
+* ``run_config3``    — BASELINE config 3 (10M x 1M @0.001) transaction-DP over all ranks.
+
+Reference timed region: ``machine-learning/main.py:264-308`` (encode + fpgrowth + rule map);
+all sizes mined (``main.py:272``), support sweep downwards (``main.py:450-473``).
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Callable, Dict, Optional
+
+import numpy as np
+
+# Whole-problem references computed on the build host by the native CPU miner
+# (``mine_cpu_count``, 6 threads, 88 s; profiles/r3_config2_cpu_ref.md) on
+# ``generate("ds1", seed=0)``: (digest, n_itemsets, per-level counts from size 1).
+CPU_REF = {
+    0.02: ("5645ebcc74e7a31e9f474dfbb0c9e0bb", 1414082373,
+           [2032, 81637, 897824, 5004384, 18407680, 51371444, 114076602, 200624405, 274917544,
+            289754387, 232392862, 139994181, 62090008, 19642215, 4215542, 566649, 41695, 1275,
+            7]),
+}
+# digest of the 10M x 1M @0.001 itemsets of the seeded synthetic data (924 itemsets, depth 4),
+# computed by the CPU miner (N.mine_cpu) over the whole dataset on the build host; the GPU
+# tx-DP result must equal it at every N
+C3_DIGEST = "d3b31400a6ebfffbbdac749329a5c1e6"
+
+
+def digest_of(N, r, min_depth=0):
+    return N.trie_digest(r["parent"], r["item"], r["count"], r["depth"], min_depth)
+
+
+def index_equal(ix, ref) -> bool:
+    """Device rule map == CPU-built index (row_ptr, consequents, counts)."""
+    rp = np.asarray(ix["row_ptr"], np.int64)
+    if len(rp) != len(ref.row_ptr) or not np.array_equal(rp, ref.row_ptr):
+        return False
+    return (np.array_equal(np.asarray(ix["cons"], np.int32), ref.cons) and
+            np.array_equal(np.asarray(ix["count"], np.int64),
+                           np.rint(ref.score * ref._n_tx).astype(np.int64)))
+
+
+def cpu_index(N, tx, ms, names, max_len=2):
+    from ..serve.index import build_index_from_trie
+    r = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, max_len)
+    ref = build_index_from_trie(r["parent"], r["item"], r["count"], r["depth"], tx.n_tx,
+                                tx.n_items, names)
+    ref._n_tx = tx.n_tx
+    return ref
+
+
+# ---------------------------------------------------------------------------------------------
+# count-only full mining (headline)
+# ---------------------------------------------------------------------------------------------
+class CpuCountMiner:
+    """The CPU tier of the headline (``bench.py --cpu``, tests): the native CPU count miner on
+    this rank's share of the level-3 tasks, combined like the GPU partials (gloo)."""
+
+    comm_backend = "torch"
+
+    def __init__(self, tx, rank: int, world: int, threads: int = 0):
+        from ..ops import native
+        self.N, self.tx, self.rank, self.world, self.threads = native.load(), tx, rank, world, \
+            threads
+
+    def mine(self, ms: float, max_len: int = 0) -> Dict:
+        from ..parallel.deep import allreduce_partial
+        t = self.tx
+        d = dict(self.N.mine_cpu_count(t.tx_ptr, t.items, t.n_items, ms, max_len, 1 << 62,
+                                       self.threads, self.rank, self.world))
+        d.update(candidates=0, chunks=0, level2_tasks=0, round_tasks=[],
+                 phases_ms={"total": d["seconds"] * 1e3})
+        return allreduce_partial(d, self.world) if self.world > 1 else d
+
+    def synchronize(self) -> None:
+        pass
+
+
+def run_deep(tx, ms: float, world: int, rank: int, device: int, warmup: int, steps: int,
+             barrier_sync: Callable[[], None], max_over_ranks: Callable[[float], float],
+             comm: Optional[str] = None, max_len: int = 0, cpu: bool = False, **opts) -> Dict:
+    """Time `steps` whole-problem calls (every itemset of every size of `tx` at `ms`, split
+    over the ranks, per-size counts + digest combined over RCCL) after `warmup` untimed ones."""
+    if cpu:
+        dm = CpuCountMiner(tx, rank, world)
+    else:
+        from ..parallel.deep import DeepMiner
+        dm = DeepMiner(tx.tx_ptr, tx.items, tx.n_items, device=device, rank=rank, world=world,
+                       comm_backend=comm, **opts)
+    r = None
+    for _ in range(warmup):
+        r = dm.mine(ms, max_len)
+    dm.synchronize()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = dm.mine(ms, max_len)
+    dm.synchronize()
+    barrier_sync()
+    ms_step = max_over_ranks((time.perf_counter() - t0) * 1000.0 / max(1, steps))
+    out = {"ms_per_step": round(ms_step, 3), "n_itemsets": int(r["n_itemsets"]),
+           "per_level": [int(x) for x in r["per_level"][1:]], "digest": r["digest"],
+           "max_depth": int(r["max_depth"]), "n_frequent_items": int(r["n_frequent_items"]),
+           "candidates": int(r["candidates"]), "chunks": int(r["chunks"]),
+           "level2_tasks": int(r["level2_tasks"]), "comm": dm.comm_backend,
+           "rank0_phases_ms": {k: round(v, 3) for k, v in r["phases_ms"].items()},
+           "rank0_rounds": len(r["round_tasks"])}
+    ref = CPU_REF.get(ms) if not max_len else None
+    out["verified_digest"] = (r["digest"] == ref[0] and int(r["n_itemsets"]) == ref[1]) \
+        if ref else None
+    out["_miner"] = dm
+    return out
+
+
+def deep_capped(dm, ms: float, budget_s: float, start_len: int = 4, max_cap: int = 64) -> Dict:
+    """Full mining at `ms` with the itemset size cap raised one at a time while a call stays
+    under `budget_s` (the last completed cap's counts, timed)."""
+    last, trail = None, []
+    L = start_len
+    while L <= max_cap:
+        t = time.perf_counter()
+        r = dm.mine(ms, L)
+        dt = time.perf_counter() - t
+        trail.append({"max_len": L, "s": round(dt, 3), "n_itemsets": int(r["n_itemsets"])})
+        last = (L, dt, r)
+        if int(r["max_depth"]) < L:  # the cap no longer binds: this is the complete result
+            break
+        if dt * 4 > budget_s:  # the next size is usually several times larger
+            break
+        L += 1
+    L, dt, r = last
+    return {"max_len": L, "complete": int(r["max_depth"]) < L, "s": round(dt, 3),
+            "n_itemsets": int(r["n_itemsets"]), "itemsets_per_s": round(r["n_itemsets"] / dt, 1),
+            "per_level": [int(x) for x in r["per_level"][1:]], "digest": r["digest"],
+            "trail": trail}
+
+
+# ---------------------------------------------------------------------------------------------
+# level-wise path (round-2 headline form)
+# ---------------------------------------------------------------------------------------------
+def run_levelwise(N, tx, ms: float, world: int, rank: int, device: int, warmup: int,
+                  steps: int, barrier_sync, max_over_ranks, gather, weak: bool,
+                  verify: bool = True, prefetch: bool = True) -> Dict:
+    """ds1 @`ms` through the level-wise path: supports → encode → gram → every level → trie
+    download + device rule map, launch-ahead steady state.  weak: one dataset per rank (rank r
+    mines a relabelled copy), job total = sum of itemsets ÷ slowest rank."""
+    from ..data.synthetic import relabel
+    from ..parallel.dist_miner import DistMiner
+    from ..serve.index import name_tie_rank
+    data = relabel(tx, rank) if weak else tx
+    tie = name_tie_rank(data.names) if data.names else np.arange(data.n_items, dtype=np.int32)
+    m = DistMiner(data.tx_ptr, data.items, data.n_items, ms, device=device,
+                  mode="local" if weak else "auto")
+    m.set_tie_rank(tie)
+
+    def step(pf=False):
+        return m.step(download=True, reduce_count=False, prefetch=pf and prefetch,
+                      rule_index=True)["trie"]
+
+    r = None
+    for i in range(warmup):
+        r = step(i < warmup - 1)
+    barrier_sync()
+    m.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        r = step(i < steps - 1)
+    m.synchronize()
+    barrier_sync()
+    ms_step = max_over_ranks((time.perf_counter() - t0) * 1000.0 / max(steps, 1))
+    st = r["stats"]
+    d = digest_of(N, r)
+    ok = ok_ix = None
+    if verify:
+        ref = N.mine_cpu(data.tx_ptr, data.items, data.n_items, ms, 0)
+        ok = digest_of(N, ref)["digest"] == d["digest"]
+        ok_ix = index_equal(r["index"], cpu_index(N, data, ms, data.names))
+    parts = gather((int(d["n"]), ok, ok_ix))
+    n_total = sum(p[0] for p in parts)
+    out = {"min_support": ms, "parallelism": f"dp{world}-one-dataset-per-gpu" if weak else
+           "single", "ms_per_step": round(ms_step, 4), "n_itemsets": n_total,
+           "n_itemsets_per_dataset": int(d["n"]),
+           "itemsets_per_s": round(n_total / (ms_step / 1000.0), 1),
+           "n_rules": int(r["index"]["nnz"]), "digest": d["digest"],
+           "verified_digest": None if not verify else all(bool(p[1]) for p in parts),
+           "verified_rule_map_vs_cpu": None if not verify else all(bool(p[2]) for p in parts),
+           "levels_path": st.get("levels_path"),
+           "step_overlap": "launch-ahead: step k+1's call is launched before step k's is waited"
+                           " for" if prefetch else "none"}
+    if "phases_ms" in st:
+        out["phases_ms"] = st["phases_ms"]
+    del m
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE config 2
+# ---------------------------------------------------------------------------------------------
+def run_config2(N, tx, names, tie, steps: int, verify: bool, deep_miner=None,
+                full_budget_s: float = 20.0) -> Dict:
+    """BASELINE config 2: ds1 @ min_support 0.01 on 1 GPU."""
+    ms = 0.01
+    g = N.GpuMiner(0)
+    g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
+    g.set_tie_rank(tie)
+    out = {"min_support": ms, "model": "fpgrowth-ds1-shape", "global_batch": int(tx.n_tx),
+           "seq_len": int(tx.n_items)}
+    # (a) the deployed artifact: rule map = 1- and 2-itemsets, built and downloaded as a CSR
+    for _ in range(2):
+        r = g.mine(ms, 2, download=True, rule_index=True)
+    g.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = g.mine(ms, 2, download=True, rule_index=True)
+    g.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    st = r["stats"]
+    a = {"ms_per_step": round(dt * 1e3, 4), "steps": steps,
+         "n_keys": int(st["n_frequent_items"]), "n_rules": int(r["index"]["nnz"]),
+         "n_itemsets": int(st["n_itemsets"])}
+    if verify:
+        ref = cpu_index(N, tx, ms, names)
+        a["verified_vs_cpu_index"] = index_equal(r["index"], ref)
+        cpu = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, 2)
+        a["verified_digest"] = digest_of(N, r)["digest"] == digest_of(N, cpu)["digest"]
+    out["rule_map"] = a
+    # (b) every frequent itemset of size <= 4 + supports, materialised as a trie and downloaded
+    r = g.mine(ms, 4, download=True, rule_index=True)
+    g.synchronize()
+    k = max(1, steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        r = g.mine(ms, 4, download=True, rule_index=True)
+    g.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    st = r["stats"]
+    d4 = digest_of(N, r)
+    b = {"max_len": 4, "ms_per_step": round(dt * 1e3, 3), "steps": k,
+         "n_itemsets": int(st["n_itemsets"]), "itemsets_per_s": round(st["n_itemsets"] / dt, 1),
+         "per_level": d4["per_depth"][1:], "levels_path": st.get("levels_path")}
+    del r
+    if verify:
+        cpu = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, 4)
+        b["verified_digest"] = d4["digest"] == digest_of(N, cpu)["digest"]
+        del cpu
+    out["mine_max_len4"] = b
+    del g
+    # (c) full mining at 0.01, count-only: the size cap is raised while a call stays in budget
+    if deep_miner is not None:
+        f = deep_capped(deep_miner, ms, full_budget_s)
+        f["verified_max_len4_vs_trie"] = None
+        if f["trail"] and f["trail"][0]["max_len"] == 4:
+            r4 = deep_miner.mine(ms, 4)
+            f["verified_max_len4_vs_trie"] = r4["digest"] == d4["digest"]
+        out["full_mining"] = f
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE config 3
+# ---------------------------------------------------------------------------------------------
+def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: int = 1,
+                comm: str = "host") -> Dict:
+    """BASELINE config 3 (10M transactions x 1M items, min_support 0.001) on all ranks of the job:
+    transaction-DP mining (each rank generates and encodes only its shard; supports, gram and
+    per-level candidate counts all-reduced), so support/encode/gram work shrinks with N.
+    Verified by the itemset digest, which must not depend on N."""
+    import torch
+    import torch.distributed as dist
+    from ..data.synthetic import SHAPES
+    from ..parallel.dist_miner import DistMiner, shard_bounds
+    prev = os.environ.get("KMLS_COMM")
+    os.environ["KMLS_COMM"] = comm
+    try:
+        shape = SHAPES["10Mx1M"]
+        T = shape.n_tx
+        lo, hi, _ = shard_bounds(T, world, rank)
+        ptr, items = N.synth_transactions(T, shape.n_items, shape.mean_len, shape.n_genres,
+                                          shape.genre_affinity, 0.85, 0, 0, lo, hi)
+        dm = DistMiner(ptr, items, shape.n_items, 0.001, device=device, mode="tx",
+                       support_tiles=4, global_n_tx=T)
+
+        def bar():
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+                torch.cuda.synchronize()
+        r = None
+        for _ in range(warmup):
+            r = dm.step(download=True)
+        bar()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r = dm.step(download=True)
+        dm.synchronize()
+        bar()
+        ms = (time.perf_counter() - t0) * 1000.0 / max(1, steps)
+        if world > 1:
+            t = torch.tensor([ms], dtype=torch.float64,
+                             device="cuda" if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms = float(t.item())
+        st = r["stats"]
+        out = {"model": "fpgrowth-10Mx1M-synthetic", "global_batch": T, "seq_len": shape.n_items,
+               "min_support": 0.001, "n_gpus": world, "parallelism": f"tx-dp{world}",
+               "comm": comm, "steps": steps, "ms_per_step": round(ms, 3),
+               "tx_per_s": round(T / (ms / 1000.0), 1),
+               "n_frequent_items": int(st.get("n_frequent_items", 0)),
+               "phases_ms": {k: round(v, 3) for k, v in (st.get("phases_ms") or {}).items()}}
+        if rank == 0:
+            d = digest_of(N, r["trie"])
+            n = int(d["n"])
+            out["n_itemsets"] = n
+            out["itemsets_per_s"] = round(n / (ms / 1000.0), 1)
+            out["digest"] = d["digest"]
+            out["verified_digest"] = d["digest"] == C3_DIGEST
+        del dm
+        return out
+    finally:
+        if prev is None:
+            os.environ.pop("KMLS_COMM", None)
+        else:
+            os.environ["KMLS_COMM"] = prev

@@ -180,7 +180,11 @@ def mine_csr(tx_ptr: np.ndarray, items: np.ndarray, n_items: int, min_support: f
             tie = (name_tie_rank([str(c) for c in columns]) if columns is not None else
                    np.arange(int(n_items), dtype=np.int32))
             g.set_tie_rank(np.ascontiguousarray(tie, np.int32))
-        r = g.mine(float(min_support), ml, bool(pairs_only), True, True, bool(mfma), False,
+        # pairs-only == itemsets truncated at 2 items; as max_len it stays on the device-resident
+        # path, which is the one that builds the rule map
+        if pairs_only:
+            ml = 2 if ml == 0 else min(ml, 2)
+        r = g.mine(float(min_support), ml, False, True, True, bool(mfma), False,
                    bool(rule_index))
     else:
         raise ValueError(f"unknown backend {backend!r}")

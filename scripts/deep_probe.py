@@ -3,11 +3,17 @@
 full mining at lower supports (the BASELINE config-2 family), one JSON line per run.
 
   python scripts/deep_probe.py --supports 0.02 --reps 3 [--budget 4096 --budget0 4096]
+  python scripts/deep_probe.py --sweep 4096:4096:4:3,1024:1024:4:3 --supports 0.02
+      (budget0:budget:split_min:blocks_per_cu per config, min of --reps per config)
+  python scripts/deep_probe.py --world 8 --supports 0.02   (every rank's share, one GPU)
+
+A heartbeat line goes to stderr every 30 s while a call runs (long runs at 0.015 and below).
 """
 import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -18,14 +24,35 @@ CPU_REF = {
 }
 
 
+class Heartbeat:
+    def __init__(self, what: str, every: float = 30.0):
+        self.what, self.every, self.stop = what, every, threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.time()
+        while not self.stop.wait(self.every):
+            print(f"[deep_probe] {self.what}: {time.time() - t0:.0f} s", file=sys.stderr,
+                  flush=True)
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *a):
+        self.stop.set()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--supports", default="0.02")
     ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--budget", type=int, default=4096)
-    ap.add_argument("--budget0", type=int, default=4096)
-    ap.add_argument("--split-min", type=int, default=4)
+    ap.add_argument("--budget", type=int, default=0)
+    ap.add_argument("--budget0", type=int, default=0)
+    ap.add_argument("--split-min", type=int, default=0)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
+    ap.add_argument("--max-len", type=int, default=0)
+    ap.add_argument("--sweep", default="", help="b0:b:split:bpc,... configurations")
     ap.add_argument("--world", type=int, default=1, help="simulate a rank split on one GPU")
     ap.add_argument("--no-parity", action="store_true")
     a = ap.parse_args()
@@ -35,8 +62,15 @@ def main() -> int:
     tx = generate("ds1", seed=0)
     g = N.GpuMiner(0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
-    kw = dict(budget0=a.budget0, budget=a.budget, split_min=a.split_min,
-              blocks_per_cu=a.blocks_per_cu)
+
+    def opts(b0, b, sm, bpc):
+        kw = {}
+        for k, v in (("budget0", b0), ("budget", b), ("split_min", sm), ("blocks_per_cu", bpc)):
+            if v:
+                kw[k] = v
+        return kw
+
+    kw = opts(a.budget0, a.budget, a.split_min, a.blocks_per_cu)
     if not a.no_parity:
         t = time.perf_counter()
         d = g.mine_deep(0.03, **kw)
@@ -46,11 +80,31 @@ def main() -> int:
                           "ok": d["digest"] == c["digest"] and d["n_itemsets"] == c["n_itemsets"],
                           "s": round(dt, 4), "phases_ms": d["phases_ms"],
                           "rounds": len(d["round_tasks"])}), flush=True)
+    if a.sweep:
+        for cfg in a.sweep.split(","):
+            b0, b, sm, bpc = (int(x) for x in cfg.split(":"))
+            k = opts(b0, b, sm, bpc)
+            for ms in [float(x) for x in a.supports.split(",")]:
+                best, d = None, None
+                for _ in range(a.reps):
+                    t = time.perf_counter()
+                    d = g.mine_deep(ms, a.max_len, **k)
+                    dt = time.perf_counter() - t
+                    best = dt if best is None else min(best, dt)
+                ref = CPU_REF.get(ms)
+                print(json.dumps({"probe": "sweep", "cfg": cfg, "min_support": ms,
+                                  "best_s": round(best, 4), "n": d["n_itemsets"],
+                                  "ok": (d["digest"] == ref[0]) if ref and not a.max_len else None,
+                                  "chunks": d["chunks"], "n_rounds": len(d["round_tasks"]),
+                                  "round_ms": [round(x, 1) for x in d["round_ms"][:12]]}),
+                      flush=True)
+        return 0
     for ms in [float(x) for x in a.supports.split(",")]:
         for rep in range(a.reps):
             for r in range(a.world):
                 t = time.perf_counter()
-                d = g.mine_deep(ms, rank=r, world=a.world, **kw)
+                with Heartbeat(f"min_support {ms} rank {r}"):
+                    d = g.mine_deep(ms, a.max_len, rank=r, world=a.world, **kw)
                 dt = time.perf_counter() - t
                 ref = CPU_REF.get(ms)
                 out = {"probe": "deep", "min_support": ms, "rep": rep, "rank": r,
@@ -62,7 +116,7 @@ def main() -> int:
                        "round_tasks": d["round_tasks"][:12],
                        "round_ms": [round(x, 2) for x in d["round_ms"][:12]],
                        "n_rounds": len(d["round_tasks"])}
-                if ref and a.world == 1:
+                if ref and a.world == 1 and not a.max_len:
                     out["verified_vs_cpu"] = d["digest"] == ref[0] and d["n_itemsets"] == ref[1]
                 print(json.dumps(out), flush=True)
     return 0

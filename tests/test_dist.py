@@ -284,25 +284,31 @@ def test_relabel_keeps_itemsets():
         assert np.array_equal(np.bincount(r["depth"]), np.bincount(r0["depth"]))
 
 
-def test_bench_weak_scaling_two_ranks_cpu():
-    """bench.py's N-rank contract on the CPU tier: torchrun, one JSON line from rank 0, the job
-    total over one dataset per rank, every rank's result verified by digest."""
+def test_bench_strong_scaling_two_ranks_cpu():
+    """bench.py's N-rank contract on the CPU tier: torchrun, one JSON line from rank 0, ONE
+    dataset split over the ranks (level-3 tasks t = r mod N), per-size counts + digest combined
+    through torch.distributed (gloo here, RCCL on the GPU node) equal to the unsplit count."""
     import json
     import subprocess
     import sys
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    from kubernetes_machine_learning_server_amd.ops import native
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=root)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(root, "bench.py"), "--gpus", "2", "--cpu", "--steps", "2",
-           "--warmup", "1", "--serve-qps", ""]
+           "--warmup", "1", "--min-support", "0.04"]
     p = subprocess.run(cmd, env=env, cwd="/tmp", capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     out = json.loads(lines[0])
-    assert out["scaling"] == "weak" and out["verified_digest"] is True
-    cfg = out["config"]
-    assert cfg["n_itemsets"] == 2 * cfg["n_itemsets_per_dataset"] == 2 * 77905
-    assert cfg["global_batch"] == 2 * 2246 and cfg["parallelism"] == "dp2-one-dataset-per-gpu"
-    assert abs(out["value"] - cfg["n_itemsets"] / (out["ms_per_step"] / 1e3)) / out["value"] < 1e-3
+    tx = generate("ds1", seed=0)
+    ref = native.load().mine_cpu_count(tx.tx_ptr, tx.items, tx.n_items, 0.04)
+    assert out["scaling"] == "strong" and out["n_gpus"] == 0
+    assert out["digest"] == ref["digest"]
+    assert out["config"]["n_itemsets"] == ref["n_itemsets"] == 573225
+    assert out["per_level"] == list(ref["per_level"])[1:]
+    assert out["config"]["parallelism"].startswith("dp2-level3-task-split")
+    assert abs(out["value"] - ref["n_itemsets"] / (out["ms_per_step"] / 1e3)) / out["value"] < 1e-2

@@ -3,7 +3,8 @@
 csrc/kernels/deep.hip and csrc/host/deep_run.hip are compiled by g++ against the emulator's HIP
 shim (one host thread per lane, cross-lane ops through barriers) with AddressSanitizer and
 UBSan; the per-size counts and the content digest must equal the CPU count miner's.  Small step
-budgets force spill rounds; world > 1 splits the level-3 tasks over simulated ranks.
+budgets force spill rounds; world > 1 splits the level-3 tasks over simulated ranks; longer
+transaction lists exercise the tid projection across several width tiers.
 """
 import os
 import pathlib
@@ -47,6 +48,7 @@ def emu_bin():
     "400 60 20 3 0.9 0.05 1 1 2",          # every task spills, per-member splits
     "300 50 25 2 0.95 0.08 1 2 4 1 3 0",   # 3 simulated ranks + spills
     "300 50 25 2 0.95 0.08 4 4 64 1 1 4",  # max_len
+    "1500 60 16 3 0.9 0.06 2 2 4",         # 24-word root: projected tiers 3..12 below it
 ])
 def test_deep_kernel_on_emulator(emu_bin, args):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
