@@ -40,6 +40,7 @@ class JobSettings:
     # RULES_MODE=pairs on several GPUs: how the pair matrix is formed (parallel/pairs.py:
     # allreduce | reduce_scatter | alltoall | ring), or "trie" (mine 2-itemsets, gather sub-tries)
     pairs_strategy: str = "reduce_scatter"
+    dist_mode: str = "auto"      # KMLS_DIST_MODE: auto | tx | item | replicate (multi-GPU mining)
     num_gpus: int = 1
     min_confidence: float = 0.04  # legacy confidence rules (main.py:227)
     checkpoint_dir: Optional[pathlib.Path] = None  # KMLS_CHECKPOINT_DIR: phase resume
@@ -78,6 +79,7 @@ class JobSettings:
             miner=_env("MINER", "auto").lower(),
             rules_mode=_env("RULES_MODE", "full").lower(),
             pairs_strategy=_env("PAIRS_STRATEGY", "reduce_scatter").lower(),
+            dist_mode=_env("KMLS_DIST_MODE", "auto").lower(),
             num_gpus=int(_env("NUM_GPUS", "1")),
             min_confidence=float(_env("MIN_CONFIDENCE", "0.04")),
             checkpoint_dir=(pathlib.Path(os.environ["KMLS_CHECKPOINT_DIR"])

@@ -135,9 +135,10 @@ def mine_rules_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_su
                            ) -> Optional[Tuple[RuleIndexData, ItemsetTrie, str, Tuple[int, float]]]:
     """Multi-GPU mining (torchrun); returns the result on rank 0, None elsewhere.
 
-    Phase checkpoints: after mining, every rank saves its frequent-item order and
-    its own sub-trie (tx mode: rank 0's global trie) under the run's checkpoint key.  A restarted
-    job whose ranks ALL find their sub-trie (and an unchanged frequent order) skips mining and
+    Phase checkpoints: after mining, every rank saves its own sub-trie (tx mode:
+    rank 0 saves the global trie, which every rank holds) under the run's checkpoint key (dataset,
+    min_support, rules mode, sample ratio: the frequent order is a pure function of these).  A
+    restarted job whose ranks ALL find their phase output (tx mode: rank 0's) skips mining and
     goes straight to the merge; a partial set is ignored (every rank re-mines)."""
     import torch
     import torch.distributed as dist
@@ -147,16 +148,19 @@ def mine_rules_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_su
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dm = DistMiner(tx.tx_ptr, tx.items, len(tx.names), min_support, device=local,
                    max_len=2 if cfg.rules_mode == "pairs" else 0,
-                   backend="cpu" if cfg.miner == "cpu" else "gpu")
+                   backend="cpu" if cfg.miner == "cpu" else "gpu", mode=cfg.dist_mode)
     phase = f"subtrie_r{rank}of{world}_{dm.mode}"
-    have = 1 if (ck is not None and ck.has(phase)) else 0
+    tx_follower = dm.mode == "tx" and rank != 0  # needs nothing: rank 0 holds the global trie
+    have = 1 if (tx_follower or (ck is not None and ck.has(phase))) else 0
     flag = torch.tensor([have], dtype=torch.int64,
                         device=torch.device("cuda", local) if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if int(flag.item()) == 1:  # every rank has its phase output: no re-mining
-        z = ck.load(phase)
-        sub = {k: z[k] for k in ("parent", "item", "count", "depth")}
-        st = {"n_frequent_items": int(z["n_frequent"]), "backend": "checkpoint"}
+        sub, st = None, {"backend": "checkpoint"}
+        if not tx_follower:
+            z = ck.load(phase)
+            sub = {k: z[k] for k in ("parent", "item", "count", "depth")}
+            st["n_frequent_items"] = int(z["n_frequent"])
         if rank == 0:
             print("Resumed per-rank sub-tries from checkpoint", ck.dir)
     else:

@@ -258,17 +258,19 @@ def _run_dist_job(root, world, fault="", extra=None):
     return res
 
 
-def test_distributed_job_phase_checkpoints(tmp_path):
+@pytest.mark.parametrize("mode", ["auto", "tx"])
+def test_distributed_job_phase_checkpoints(tmp_path, mode):
     """torchrun-style job at world size 2 (gloo + the CPU protocol): the per-rank sub-trie
     phase is checkpointed; after a crash between mining and publishing, the restarted job
-    resumes from every rank's sub-trie (no re-mining) and publishes the same artifacts as a
-    single-process run."""
+    resumes from every rank's sub-trie (tx mode: rank 0's global trie) without re-mining and
+    publishes the same artifacts as a single-process run."""
     make_datasets(tmp_path, shapes=("ds2_weak", "tiny"), seeds=(3, 4))
-    res = _run_dist_job(tmp_path, 2, fault="after_mining_phase")
+    extra = {"dist_mode": mode}
+    res = _run_dist_job(tmp_path, 2, fault="after_mining_phase", extra=extra)
     assert all("injected fault" in (r[2] or "") for r in res)
     ck_files = list((tmp_path / "ck").rglob("subtrie_r*of2_*.npz"))
-    assert len(ck_files) == 2, ck_files
-    res = _run_dist_job(tmp_path, 2)
+    assert len(ck_files) == (1 if mode == "tx" else 2), ck_files
+    res = _run_dist_job(tmp_path, 2, extra=extra)
     summary = res[0][1]
     assert summary and summary["dataset_index"] == 1
     assert summary["backend"] == "checkpoint"  # merged from the sub-tries, not re-mined
