@@ -125,6 +125,11 @@ template <typename T> inline T atomicAdd(T* p, T v) { return __atomic_fetch_add(
 template <typename T> inline T atomicSub(T* p, T v) { return __atomic_fetch_sub(p, v, __ATOMIC_SEQ_CST); }
 template <typename T> inline T atomicOr(T* p, T v) { return __atomic_fetch_or(p, v, __ATOMIC_SEQ_CST); }
 template <typename T> inline T atomicXor(T* p, T v) { return __atomic_fetch_xor(p, v, __ATOMIC_SEQ_CST); }
+template <typename T> inline T atomicExch(T* p, T v) { return __atomic_exchange_n(p, v, __ATOMIC_SEQ_CST); }
+template <typename T> inline T atomicCAS(T* p, T cmp, T v) {
+  __atomic_compare_exchange_n(p, &cmp, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
+  return cmp;  // the old value (== the expected one on success)
+}
 template <typename T> inline T atomicMin(T* p, T v) {
   T old = __atomic_load_n(p, __ATOMIC_SEQ_CST);
   while (v < old && !__atomic_compare_exchange_n(p, &old, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {

@@ -19,5 +19,10 @@ inline unsigned long long uni64(unsigned long long v) {
   return ((unsigned long long)uni((unsigned)(v >> 32)) << 32) | uni((unsigned)v);
 }
 
+inline unsigned long long ld_agent(const unsigned long long* p) { return __atomic_load_n(p, __ATOMIC_SEQ_CST); }
+inline unsigned ld_agent(const unsigned* p) { return __atomic_load_n(p, __ATOMIC_SEQ_CST); }
+inline void fence_agent() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
+inline void wait_short() { std::this_thread::yield(); }
+
 }  // namespace kern
 }  // namespace kmls

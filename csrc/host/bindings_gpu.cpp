@@ -368,8 +368,11 @@ void register_gpu_bindings(py::module_& m) {
          py::arg("download") = true, py::arg("mfma") = false, py::arg("support_tiles") = 4)
       .def("mine_deep", [](gpu::GpuMiner& g, double ms, int max_len, int rank, int world,
                            py::object comm, unsigned long long budget0, unsigned long long budget,
-                           unsigned split_min, int blocks_per_cu, int stack_mb) {
+                           unsigned split_min, int blocks_per_cu, int stack_mb, bool steal,
+                           unsigned steal_idle) {
         gpu::DeepOpts o;
+        o.steal = steal;
+        o.steal_idle = steal_idle;
         o.budget0 = budget0;
         o.budget = budget;
         o.split_min = split_min;
@@ -394,6 +397,7 @@ void register_gpu_bindings(py::module_& m) {
                       (unsigned long long)r.digest_xor);
         d["digest"] = std::string(buf);
         d["round_tasks"] = r.round_tasks;
+        d["spilled_tasks"] = r.spilled_tasks;
         d["round_ms"] = r.round_ms;
         py::dict ph;
         ph["prologue"] = r.ms_prologue;
@@ -405,7 +409,8 @@ void register_gpu_bindings(py::module_& m) {
         return d;
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("rank") = 0, py::arg("world") = 1,
          py::arg("comm") = py::none(), py::arg("budget0") = 1024ull, py::arg("budget") = 1024ull,
-         py::arg("split_min") = 8u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0)
+         py::arg("split_min") = 8u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0,
+         py::arg("steal") = true, py::arg("steal_idle") = 1u)
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
   py::class_<gpu::GpuRuleIndex, std::shared_ptr<gpu::GpuRuleIndex>>(m, "GpuRuleIndex")

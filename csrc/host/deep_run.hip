@@ -21,7 +21,7 @@ namespace gpu {
 
 DeepBufs::~DeepBufs() {
   (void)hipSetDevice(device);
-  for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)heap[0],
+  for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)heap[0],
                   (void*)heap[1], (void*)root, (void*)ctl, (void*)d_red, (void*)d_xor,
                   (void*)d_m, (void*)d_off, (void*)d_toff})
     if (p) (void)hipFree(p);
@@ -101,6 +101,10 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       q = nullptr;
       KMLS_HIP(hipMalloc((void**)&q, (size_t)q_cap * sizeof(kern::DeepFrame)));
     }
+    if (b.ready) KMLS_HIP(hipFree(b.ready));
+    KMLS_HIP(hipMalloc((void**)&b.ready, (size_t)q_cap * sizeof(unsigned)));
+    KMLS_HIP(hipMemsetAsync(b.ready, 0, (size_t)q_cap * sizeof(unsigned), s));
+    b.epoch = 0;
     b.q_cap = q_cap;
   }
   const size_t heap_cap = env_bytes_mb("KMLS_DEEP_HEAP_MB", 4096);
@@ -199,6 +203,40 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     if (const char* e = std::getenv("KMLS_DEEP_ROUND_TIMEOUT_S")) secs = std::max(1.0, std::atof(e));
     a.timeout_ticks = (unsigned long long)(secs * 1000.0 * (double)std::max(khz, 1));
   }
+  if (opt.steal && n_tasks > 0) {
+    // one launch: spilled tasks are queued behind the level-3 tasks and taken by waiting waves
+    const auto tr = now();
+    KMLS_HIP(hipMemsetAsync(b.ctl, 0, 5 * sizeof(unsigned long long), s));
+    b.h_ctl->pending = (unsigned long long)n_tasks;
+    KMLS_HIP(hipMemcpyAsync(&b.ctl->pending, &b.h_ctl->pending, 8, hipMemcpyHostToDevice, s));
+    if (++b.epoch == 0) {  // 2^32 launches: restart the stamps
+      KMLS_HIP(hipMemsetAsync(b.ready, 0, (size_t)b.q_cap * sizeof(unsigned), s));
+      b.epoch = 1;
+    }
+    a.in = b.q[0];
+    a.n_in = n_tasks;
+    a.out = b.q[0];
+    a.heap = b.heap[0];
+    a.budget = std::max<unsigned long long>(opt.budget, 1);
+    a.ready = b.ready;
+    a.epoch = b.epoch;
+    a.steal = 1;
+    a.steal_idle = opt.steal_idle;
+    kern::deep_count(a, maxt, blocks_per_cu, grid, s);
+    KMLS_HIP(hipMemcpyAsync(b.h_ctl, b.ctl, sizeof(kern::DeepCtl), hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+    if (b.h_ctl->error & 4)
+      throw std::runtime_error("deep_run: the launch ran past KMLS_DEEP_ROUND_TIMEOUT_S and gave up");
+    if (b.h_ctl->error)
+      throw std::runtime_error(std::string("deep_run: launch failed (") +
+                               ((b.h_ctl->error & 8) ? "bad block width" :
+                                (b.h_ctl->error & 1) ? "task queue overflow" : "spill heap overflow") +
+                               "); raise KMLS_DEEP_QUEUE_MB / KMLS_DEEP_HEAP_MB");
+    res.round_tasks.push_back(n_tasks);
+    res.round_ms.push_back(ms_since(tr));
+    res.spilled_tasks = (int64_t)b.h_ctl->n_out;
+    n_tasks = 0;  // the rounds below have nothing left
+  }
   int cur = 0;
   int64_t n_in = n_tasks;
   for (int round = 0; n_in > 0; ++round) {
@@ -225,6 +263,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     res.round_tasks.push_back(n_in);
     res.round_ms.push_back(ms_since(tr));
     n_in = (int64_t)b.h_ctl->n_out;
+    res.spilled_tasks += n_in;
     cur ^= 1;
   }
   KMLS_HIP(hipMemcpyAsync(b.h_ctl, b.ctl, sizeof(kern::DeepCtl), hipMemcpyDeviceToHost, s));

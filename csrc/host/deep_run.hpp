@@ -24,6 +24,9 @@ struct DeepBufs {
   int fcap = 0;
   kern::DeepFrame* q[2] = {nullptr, nullptr};
   int64_t q_cap = 0;
+  unsigned* ready = nullptr;  // [q_cap] steal-mode publish flags (zeroed once at allocation)
+  unsigned epoch = 0;         // steal-mode launch stamp of the flags
+
   char* heap[2] = {nullptr, nullptr};
   size_t heap_cap = 0;
   char* root = nullptr;  // root block + level-2 blocks
@@ -59,6 +62,7 @@ struct DeepLocal {
   int64_t level2_tasks = 0;
   int maxt = 0;  // widest block tier of the count kernel instance
   std::vector<int64_t> round_tasks;
+  int64_t spilled_tasks = 0;  // tasks spilled inside the launch(es)
   std::vector<double> round_ms;
   double ms_alloc = 0, ms_root = 0, ms_rounds = 0;
 };

@@ -149,6 +149,10 @@ struct DeepOpts {
   unsigned split_min = 8;             // spilled frames above this many members split per member
   int blocks_per_cu = 0;              // 0 = the kernel instance's occupancy (deep_waves_per_simd)
   int stack_mb = 0;                   // per-wave stack (0: KMLS_DEEP_STACK_MB or 4)
+  bool steal = true;                  // one launch, spills taken by waiting waves (budget =
+                                      // passes between checks for a waiting wave); false =
+                                      // spill rounds (budget0/budget = per-task step budgets)
+  unsigned steal_idle = 1;            // steal: spill when this many waves wait (0 = always)
 };
 struct DeepResult {
   std::vector<uint64_t> per_level;  // [d] = frequent itemsets of size d (index 0 unused)
@@ -156,6 +160,7 @@ struct DeepResult {
   int max_depth = 0;
   uint64_t digest_sum = 0, digest_xor = 0;
   std::vector<int64_t> round_tasks;
+  int64_t spilled_tasks = 0;
   std::vector<double> round_ms;
   double ms_prologue = 0, ms_root = 0, ms_rounds = 0, ms_combine = 0, ms_total = 0;
 };

@@ -36,5 +36,18 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long v) {
   return ((unsigned long long)uni((unsigned)(v >> 32)) << 32) | uni((unsigned)v);
 }
 
+// Cross-wave hand-off (work queues inside one launch): loads that observe another CU's
+// stores go to L2 (agent-scope atomic load, no stale vector-L1 line); the fence orders this
+// wave's earlier stores before a later flag store (release) and invalidates L1 after a flag was
+// seen (acquire).
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fence_agent() { __threadfence(); }
+__device__ __forceinline__ void wait_short() { __builtin_amdgcn_s_sleep(8); }
+
 }  // namespace kern
 }  // namespace kmls

@@ -249,25 +249,56 @@ __device__ __forceinline__ void free_blocks(WaveLds<MAXT>& L, WaveState& st) {
   }
 }
 
-// Copy every frame on the stack to the spill heap and queue it as next-round task(s): frames of
-// more than split_min members become one single-member task each (over one shared copy).
-// Returns false (error set) when the heap or the out queue is full.
-__device__ __forceinline__ bool spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st, int lane) {
+// Copy every frame on the stack to the spill heap and queue it as task(s): frames of more than
+// split_min members become one single-member task each (over one shared copy).  Heap bytes and
+// queue slots are reserved for the whole stack before anything is written, so a spill either
+// happens completely or not at all.  Returns 0 (spilled: the stack is empty), 1 (optional spill
+// skipped: no room, the wave keeps its frames) or -1 (a required spill found no room: error set).
+// Steal mode publishes every task by its ready flag after a release fence.
+__device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st,
+                                            int lane, bool optional) {
+  unsigned long long bytes_tot = 0, nt_tot = 0;
+  for (unsigned f = 0; f < st.nf; ++f) {
+    const DeepFrame fr = load_frame(fst + f, lane);
+    bytes_tot += (unsigned long long)(meta_width(fr.meta) + 1) * roundup16(fr.m) * 8ull;
+    const bool single = (fr.meta & kSingle) != 0;
+    nt_tot += (!single && fr.m > a.split_min) ? fr.m - 1 : 1;
+  }
+  unsigned long long hbase = 0;
+  if (lane == 0) hbase = atomicAdd(&a.ctl->heap_top, bytes_tot);  // overshoot is harmless
+  hbase = uni64(bcast64(hbase, 0));
+  if (hbase + bytes_tot > a.heap_cap) {
+    if (!optional && lane == 0) atomicOr(&a.ctl->error, 2u);
+    return optional ? 1 : -1;
+  }
+  // queue slots: never reserved past the capacity (steal-mode readers wait on reserved slots)
+  const unsigned long long qcap = (unsigned long long)a.out_cap - (a.steal ? (unsigned long long)a.n_in : 0ull);
+  unsigned long long t0 = 0;
+  if (lane == 0) {
+    unsigned long long old = ld_agent(&a.ctl->n_out);
+    for (;;) {
+      if (old + nt_tot > qcap) { old = ~0ull; break; }
+      const unsigned long long seen = atomicCAS(&a.ctl->n_out, old, old + nt_tot);
+      if (seen == old) break;
+      old = seen;
+    }
+    t0 = old;
+    if (t0 != ~0ull && a.steal) atomicAdd(&a.ctl->pending, nt_tot);
+  }
+  t0 = uni64(bcast64(t0, 0));
+  if (t0 == ~0ull) {
+    if (!optional && lane == 0) atomicOr(&a.ctl->error, 1u);
+    return optional ? 1 : -1;
+  }
+  DeepFrame* out = a.out + (a.steal ? a.n_in : 0ll);
+  unsigned long long hoff = hbase, q = t0;
   for (unsigned f = 0; f < st.nf; ++f) {
     const DeepFrame fr = load_frame(fst + f, lane);
     const unsigned m = fr.m;
     const unsigned wt = meta_width(fr.meta);
     const unsigned long long npad = roundup16(m);
-    const unsigned long long bytes = (unsigned long long)(wt + 1) * npad * 8ull;
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(&a.ctl->heap_top, bytes);
-    base = uni64(bcast64(base, 0));
-    if (base + bytes > a.heap_cap) {
-      if (lane == 0) atomicOr(&a.ctl->error, 2u);
-      return false;
-    }
     const unsigned long long* src = (const unsigned long long*)fr.blk;
-    unsigned long long* dst = (unsigned long long*)(a.heap + base);
+    unsigned long long* dst = (unsigned long long*)(a.heap + hoff);
     const unsigned long long tot = (unsigned long long)(wt + 1) * m;
     for (unsigned long long e = lane; e < tot; e += 64) {
       const unsigned long long w = e / m, k = e - w * m;
@@ -276,13 +307,6 @@ __device__ __forceinline__ bool spill_frames(const DeepArgs& a, DeepFrame* fst, 
     const bool single = (fr.meta & kSingle) != 0;
     const bool split = !single && m > a.split_min;
     const unsigned nt = split ? m - 1 : 1;
-    unsigned long long t0 = 0;
-    if (lane == 0) t0 = atomicAdd(&a.ctl->n_out, (unsigned long long)nt);
-    t0 = uni64(bcast64(t0, 0));
-    if (t0 + nt > (unsigned long long)a.out_cap) {
-      if (lane == 0) atomicOr(&a.ctl->error, 1u);
-      return false;
-    }
     for (unsigned k = lane; k < nt; k += 64) {
       DeepFrame o;
       o.blk = (unsigned long long)dst;
@@ -291,13 +315,20 @@ __device__ __forceinline__ bool spill_frames(const DeepArgs& a, DeepFrame* fst, 
       o.s0 = split ? k : 0u;
       o.m = split ? m - k : m;
       o.meta = make_meta(meta_depth(fr.meta), split || single, wt, 0);
-      store_frame(a.out + t0 + k, o);
+      store_frame(out + q + k, o);
     }
+    hoff += (unsigned long long)(wt + 1) * npad * 8ull;
+    q += nt;
+  }
+  if (a.steal) {
+    fence_agent();  // release: the blocks and frames above before their ready flags
+    __builtin_amdgcn_wave_barrier();
+    for (unsigned long long k = lane; k < nt_tot; k += 64) atomicExch(&a.ready[t0 + k], a.epoch);
   }
   st.nf = 0;
   st.nb = 0;
   st.mem_top = 0;
-  return true;
+  return 0;
 }
 
 // ---- row step: member s0 against members s0+1 .. s0+m-1 (lane = candidate) ----
@@ -571,11 +602,43 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
   WaveState st{0, 0, 0};
   bool failed = false;
   const unsigned long long t_start = wall_clock64();
+  auto timed_out = [&]() {
+    if (wall_clock64() - t_start <= a.timeout_ticks) return false;
+    if (lane == 0) atomicOr(&a.ctl->error, 4u);
+    return true;
+  };
   while (!failed) {
     unsigned long long t = 0;
     if (lane == 0) t = atomicAdd(&a.ctl->next_task, 1ull);
     t = uni64(bcast64(t, 0));
-    if (t >= (unsigned long long)a.n_in) break;
+    if (!a.steal) {
+      if (t >= (unsigned long long)a.n_in) break;
+    } else {
+      // ticket t: wait until task t is published, or until no task is queued or running
+      // (pending == 0: nothing can be spilled any more, every reserved slot is done)
+      bool waiting = false, done = false;
+      for (;;) {
+        unsigned long long tail = 0, pend = 0, rdy = 0;
+        if (lane == 0) {
+          tail = (unsigned long long)a.n_in + ld_agent(&a.ctl->n_out);
+          // a failed wave never finishes its task: its error ends the wait of the others
+          pend = ld_agent(&a.ctl->error) ? 0ull : ld_agent(&a.ctl->pending);
+          rdy = t < (unsigned long long)a.n_in ? 1ull
+                : (t < tail && ld_agent(&a.ready[t - a.n_in]) == a.epoch) ? 1ull : 0ull;
+        }
+        rdy = uni64(bcast64(rdy, 0));
+        if (rdy) break;
+        pend = uni64(bcast64(pend, 0));
+        if (pend == 0) { done = true; break; }
+        if (!waiting && lane == 0) atomicAdd(&a.ctl->idle, 1ull);
+        waiting = true;
+        if (timed_out()) { failed = true; break; }
+        wait_short();
+      }
+      if (waiting && lane == 0) atomicSub(&a.ctl->idle, 1ull);
+      if (done || failed) break;
+      fence_agent();  // acquire: the task's frame and block as its producer wrote them
+    }
     {
       const DeepFrame tf = load_frame(a.in + t, lane);
       if (lane == 0) store_frame(fst, tf);
@@ -589,10 +652,9 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
     acc.budget_used = 0;
     while (st.nf > 0) {
       __builtin_amdgcn_wave_barrier();
-      // bounded: a round that runs past its deadline gives up (error bit 2) instead of holding
+      // bounded: a launch that runs past its deadline gives up (error bit 2) instead of holding
       // the GPU; the host reports it
-      if (wall_clock64() - t_start > a.timeout_ticks) {
-        if (lane == 0) atomicOr(&a.ctl->error, 4u);
+      if (timed_out()) {
         failed = true;
         break;
       }
@@ -603,10 +665,18 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
       const bool row_mode = (top.meta & kSingle) || pairs > (unsigned long long)kCap;
       const unsigned long long need =
           (unsigned long long)(wt + 1) * roundup16(row_mode ? m : kCap) * 8ull;
-      if (acc.budget_used >= a.budget || st.mem_top + need > a.stack_bytes ||
-          st.nf + kCap + 2 > (unsigned)a.fcap || st.nb + 1 >= (unsigned)kBStack) {
-        if (!spill_frames(a, fst, st, lane)) failed = true;
+      if (st.mem_top + need > a.stack_bytes || st.nf + kCap + 2 > (unsigned)a.fcap ||
+          st.nb + 1 >= (unsigned)kBStack || (!a.steal && acc.budget_used >= a.budget)) {
+        if (spill_frames(a, fst, st, lane, false) < 0) failed = true;
         break;
+      }
+      if (a.steal && acc.budget_used >= a.budget) {
+        // hand the stack to the waiting waves (a skipped spill keeps the frames)
+        unsigned long long idle = 0;
+        if (lane == 0) idle = ld_agent(&a.ctl->idle);
+        idle = uni64(bcast64(idle, 0));
+        acc.budget_used = 0;
+        if (idle >= a.steal_idle && spill_frames(a, fst, st, lane, true) == 0) break;
       }
       if (wt == 0 || wt > (unsigned)MAXT) {  // never produced by the host or the steps
         if (lane == 0) atomicOr(&a.ctl->error, 8u);
@@ -617,6 +687,7 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
                                                                stack, lane, acc);
       free_blocks(L, st);
     }
+    if (a.steal && !failed && lane == 0) atomicSub(&a.ctl->pending, 1ull);  // task t is done
   }
   // flush: wave reduction of the digest terms, per-depth counts from LDS
   for (int off = 32; off; off >>= 1) {

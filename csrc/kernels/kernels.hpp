@@ -23,6 +23,8 @@ struct DeepCtl {  // per-round control + accumulated results (zeroed once per ca
   unsigned long long next_task;   // dequeue ticket (zeroed per round)
   unsigned long long n_out;       // tasks spilled to the out queue (zeroed per round)
   unsigned long long heap_top;    // bytes of the out heap used (zeroed per round)
+  unsigned long long pending;     // steal mode: queued + running tasks (0 = the launch is done)
+  unsigned long long idle;        // steal mode: waves waiting for a task
   unsigned long long digest_sum, digest_xor;
   unsigned long long candidates, chunks;
   unsigned long long per_depth[64];
@@ -48,6 +50,13 @@ struct DeepArgs {
   int max_len;                    // 0 = all sizes
   unsigned split_min;             // spilled frames above this many members split per member
   unsigned long long timeout_ticks;  // wall_clock64 ticks a wave may run (then error bit 2)
+  // steal mode (one launch, no rounds): out == in, spilled tasks are appended at in[n_in + k]
+  // and published by ready[k] = epoch; waves that run out of tasks wait for them, and a busy
+  // wave spills its frames when it sees a waiting wave (checked every `budget` passes)
+  unsigned* ready;
+  unsigned epoch;
+  int steal;
+  unsigned steal_idle;            // spill when at least this many waves wait (0: always, tests)
 };
 int deep_max_words();
 int deep_tier(int words);     // smallest instantiated block width >= words

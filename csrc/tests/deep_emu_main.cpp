@@ -4,7 +4,7 @@
 // content digest must equal mine_cpu_count's.
 //
 //   deep_emu n_tx n_items mean_len genres affinity min_support [budget0 budget split_min stack_mb
-//            world max_len]
+//            world max_len steal steal_idle]
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -33,6 +33,8 @@ int main(int argc, char** argv) {
   if (argc > 10) opt.stack_mb = std::atoi(argv[10]);
   const int world = argc > 11 ? std::atoi(argv[11]) : 1;
   const int max_len = argc > 12 ? std::atoi(argv[12]) : 0;
+  opt.steal = argc > 13 ? std::atoi(argv[13]) != 0 : true;
+  if (argc > 14) opt.steal_idle = (unsigned)std::atoi(argv[14]);
   opt.blocks_per_cu = 1;
 
   std::vector<int64_t> ptr;
@@ -57,6 +59,7 @@ int main(int argc, char** argv) {
     dxor ^= t.xr;
   }
   int rounds = 0;
+  long long spilled = 0;
   for (int rank = 0; rank < world; ++rank) {
     gpu::DeepBufs b;
     gpu::DeepInput in;
@@ -74,6 +77,7 @@ int main(int argc, char** argv) {
     dsum += loc.dsum;
     dxor ^= loc.dxor;
     rounds += (int)loc.round_tasks.size();
+    spilled += (long long)loc.spilled_tasks;
   }
   CountResult c = mine_cpu_count(ptr.data(), items.data(), n_tx, n_items, ms, max_len, (int64_t)1 << 62, 2);
   bool ok = c.digest_sum == dsum && c.digest_xor == dxor;
@@ -81,8 +85,9 @@ int main(int argc, char** argv) {
     const uint64_t want = d < c.per_level.size() ? (uint64_t)c.per_level[d] : 0;
     if (want != per[d]) ok = false;
   }
-  std::printf("{\"F\": %lld, \"n_cpu\": %lld, \"rounds\": %d, \"ok\": %s, \"per_level\": [",
-              (long long)F, (long long)c.n_itemsets, rounds, ok ? "true" : "false");
+  std::printf("{\"F\": %lld, \"n_cpu\": %lld, \"rounds\": %d, \"spilled\": %lld, \"ok\": %s, "
+              "\"per_level\": [", (long long)F, (long long)c.n_itemsets, rounds, spilled,
+              ok ? "true" : "false");
   for (size_t d = 1; d < 20; ++d) std::printf("%s%llu", d > 1 ? ", " : "", (unsigned long long)per[d]);
   std::printf("], \"cpu\": [");
   for (size_t d = 1; d < c.per_level.size(); ++d) std::printf("%s%lld", d > 1 ? ", " : "", (long long)c.per_level[d]);

@@ -52,7 +52,9 @@ def main() -> int:
     ap.add_argument("--split-min", type=int, default=0)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--max-len", type=int, default=0)
-    ap.add_argument("--sweep", default="", help="b0:b:split:bpc,... configurations")
+    ap.add_argument("--sweep", default="",
+                    help="b0:b:split:bpc[:steal[:steal_idle]],... configurations")
+    ap.add_argument("--rounds", action="store_true", help="spill rounds instead of stealing")
     ap.add_argument("--world", type=int, default=1, help="simulate a rank split on one GPU")
     ap.add_argument("--no-parity", action="store_true")
     a = ap.parse_args()
@@ -63,14 +65,14 @@ def main() -> int:
     g = N.GpuMiner(0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
 
-    def opts(b0, b, sm, bpc):
-        kw = {}
+    def opts(b0, b, sm, bpc, steal=1, idle=1):
+        kw = {"steal": bool(steal), "steal_idle": idle}
         for k, v in (("budget0", b0), ("budget", b), ("split_min", sm), ("blocks_per_cu", bpc)):
             if v:
                 kw[k] = v
         return kw
 
-    kw = opts(a.budget0, a.budget, a.split_min, a.blocks_per_cu)
+    kw = opts(a.budget0, a.budget, a.split_min, a.blocks_per_cu, 0 if a.rounds else 1)
     if not a.no_parity:
         t = time.perf_counter()
         d = g.mine_deep(0.03, **kw)
@@ -82,8 +84,7 @@ def main() -> int:
                           "rounds": len(d["round_tasks"])}), flush=True)
     if a.sweep:
         for cfg in a.sweep.split(","):
-            b0, b, sm, bpc = (int(x) for x in cfg.split(":"))
-            k = opts(b0, b, sm, bpc)
+            k = opts(*(int(x) for x in cfg.split(":")))
             for ms in [float(x) for x in a.supports.split(",")]:
                 best, d = None, None
                 for _ in range(a.reps):
@@ -96,6 +97,7 @@ def main() -> int:
                                   "best_s": round(best, 4), "n": d["n_itemsets"],
                                   "ok": (d["digest"] == ref[0]) if ref and not a.max_len else None,
                                   "chunks": d["chunks"], "n_rounds": len(d["round_tasks"]),
+                                  "spilled": d["spilled_tasks"],
                                   "round_ms": [round(x, 1) for x in d["round_ms"][:12]]}),
                       flush=True)
         return 0
@@ -115,7 +117,7 @@ def main() -> int:
                        "level2_tasks": d["level2_tasks"], "phases_ms": d["phases_ms"],
                        "round_tasks": d["round_tasks"][:12],
                        "round_ms": [round(x, 2) for x in d["round_ms"][:12]],
-                       "n_rounds": len(d["round_tasks"])}
+                       "n_rounds": len(d["round_tasks"]), "spilled": d["spilled_tasks"]}
                 if ref and a.world == 1 and not a.max_len:
                     out["verified_vs_cpu"] = d["digest"] == ref[0] and d["n_itemsets"] == ref[1]
                 print(json.dumps(out), flush=True)

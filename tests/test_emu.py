@@ -3,7 +3,7 @@
 csrc/kernels/deep.hip and csrc/host/deep_run.hip are compiled by g++ against the emulator's HIP
 shim (one host thread per lane, cross-lane ops through barriers) with AddressSanitizer and
 UBSan; the per-size counts and the content digest must equal the CPU count miner's.  Small step
-budgets force spill rounds; world > 1 splits the level-3 tasks over simulated ranks; longer
+budgets force spills (in-launch work stealing, or spill rounds); world > 1 splits the level-3 tasks over simulated ranks; longer
 transaction lists exercise the tid projection across several width tiers.
 """
 import os
@@ -43,12 +43,15 @@ def emu_bin():
 
 
 @pytest.mark.parametrize("args", [
-    # n_tx n_items mean_len genres affinity min_support [budget0 budget split_min stack_mb world max_len]
+    # n_tx n_items mean_len genres affinity min_support [budget0 budget split_min stack_mb world
+    #   max_len steal steal_idle]
     "400 60 20 3 0.9 0.05",
-    "400 60 20 3 0.9 0.05 1 1 2",          # every task spills, per-member splits
-    "300 50 25 2 0.95 0.08 1 2 4 1 3 0",   # 3 simulated ranks + spills
-    "300 50 25 2 0.95 0.08 4 4 64 1 1 4",  # max_len
-    "1500 60 16 3 0.9 0.06 2 2 4",         # 24-word root: projected tiers 3..12 below it
+    "400 60 20 3 0.9 0.05 1 1 2 4 1 0 1 0",          # steal: every check spills, per-member splits
+    "300 50 25 2 0.95 0.08 1 1 4 1 3 0 1 0",         # 3 simulated ranks + eager in-launch spills
+    "300 50 25 2 0.95 0.08 4 4 64 1 1 4",            # max_len
+    "1500 60 16 3 0.9 0.06 2 2 4 4 1 0 1 0",         # 24-word root: projected tiers 3..12 below it
+    "400 60 20 3 0.9 0.05 1 1 2 4 1 0 0",            # spill rounds (steal off): every task spills
+    "300 50 25 2 0.95 0.08 1 2 4 1 3 0 0",           # spill rounds, 3 simulated ranks
 ])
 def test_deep_kernel_on_emulator(emu_bin, args):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")

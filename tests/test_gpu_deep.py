@@ -3,7 +3,8 @@
 Every case compares the per-size itemset counts AND the content digest (the multiset hash of
 every (itemset, support) pair, kmls/digest.hpp) with ``mine_cpu_count``, which is itself checked
 against ``trie_digest`` of the full CPU trie (and so against the mlxtend-faithful oracle, via
-test_miner_cpu.py).  Small step budgets force many spill rounds; rank splits are combined by
+test_miner_cpu.py).  Small step budgets force many spills (in-launch work stealing, the default,
+or spill rounds); rank splits are combined by
 hand (sum of counts and digest sums, xor of digest xors) and must equal the single-rank run.
 """
 import numpy as np
@@ -59,11 +60,26 @@ def test_deep_equals_full_trie_digest(gpu_mod):
 
 @pytest.mark.parametrize("budget0,budget,split_min", [(1, 1, 2), (2, 3, 64), (1, 8, 4)])
 def test_deep_spill_rounds(gpu_mod, budget0, budget, split_min):
-    """Tiny step budgets: every task spills, dense subtrees go through many rounds."""
+    """Spill rounds (steal off), tiny step budgets: every task spills, dense subtrees go through
+    many rounds."""
     tx = generate("ds1", seed=0)
     d = _gpu_miner(gpu_mod, tx).mine_deep(0.04, budget0=budget0, budget=budget,
-                                          split_min=split_min)
+                                          split_min=split_min, steal=False)
     assert len(d["round_tasks"]) >= 2
+    _same(d, _cpu(gpu_mod, tx, 0.04))
+
+
+@pytest.mark.parametrize("budget,split_min,steal_idle", [(1, 2, 0), (3, 64, 0), (8, 4, 1),
+                                                         (64, 8, 1)])
+def test_deep_work_stealing(gpu_mod, budget, split_min, steal_idle):
+    """One launch, spilled stacks taken by waiting waves; steal_idle 0 spills at every check
+    (tens of thousands of in-launch hand-offs through the ready flags)."""
+    tx = generate("ds1", seed=0)
+    d = _gpu_miner(gpu_mod, tx).mine_deep(0.04, budget=budget, split_min=split_min,
+                                          steal_idle=steal_idle)
+    assert len(d["round_tasks"]) == 1
+    if steal_idle == 0:
+        assert d["spilled_tasks"] > 0
     _same(d, _cpu(gpu_mod, tx, 0.04))
 
 
