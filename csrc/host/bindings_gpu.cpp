@@ -305,6 +305,25 @@ void register_gpu_bindings(py::module_& m) {
              return d;
            },
            py::arg("gram"), py::arg("ld"), py::arg("minsup"))
+      .def("gram_mirror", &gpu::GpuMiner::gram_mirror, py::arg("gram"), py::arg("ld"), py::arg("F"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("rule_map_rows",
+           [](gpu::GpuMiner& g, uintptr_t rows, int64_t ld, int64_t r0, int64_t nrows,
+              uint32_t minsup) {
+             gpu::GpuMiner::RuleMap m;
+             {
+               py::gil_scoped_release nogil;
+               m = g.rule_map_rows(rows, ld, r0, nrows, minsup);
+             }
+             py::dict d;
+             d["nnz"] = m.nnz;
+             d["status"] = m.status;
+             d["row_ptr"] = py::array_t<int64_t>((py::ssize_t)m.row_ptr.size(), m.row_ptr.data());
+             d["cons"] = py::array_t<int32_t>((py::ssize_t)m.cons.size(), m.cons.data());
+             d["count"] = py::array_t<uint32_t>((py::ssize_t)m.cnt.size(), m.cnt.data());
+             return d;
+           },
+           py::arg("rows"), py::arg("ld"), py::arg("r0"), py::arg("nrows"), py::arg("minsup"))
       .def("bitgemm_rect", &gpu::GpuMiner::bitgemm_rect, py::call_guard<py::gil_scoped_release>())
       .def("mine_bitmaps", [](gpu::GpuMiner& g, uintptr_t bm, int64_t Wp, double ms, int max_len,
                               bool pairs_only, py::object owned, bool emit_level1, bool download,

@@ -1158,6 +1158,75 @@ GpuMiner::RuleMap GpuMiner::rule_map_from_gram(uintptr_t gram_dev, int64_t ld, u
   return out;
 }
 
+void GpuMiner::gram_mirror(uintptr_t gram_dev, int64_t ld, int64_t F) {
+  KMLS_HIP(hipSetDevice(device_));
+  KMLS_CHECK(F >= 0 && ld >= F, "gram_mirror: ld >= F");
+  kern::gram_mirror((uint32_t*)gram_dev, ld, F, (hipStream_t)stream_);
+}
+
+GpuMiner::RuleMap GpuMiner::rule_map_rows(uintptr_t rows_dev, int64_t ld, int64_t r0, int64_t nrows,
+                                          uint32_t minsup) {
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  const int64_t F = (int64_t)fi_.ids.size();
+  KMLS_CHECK(ld >= F && r0 >= 0 && nrows >= 0 && r0 + nrows <= F,
+             "rule_map_rows: select() first; rows [r0, r0 + nrows) within F, ld >= F");
+  if (!big_lds_) {
+    kern::pairs_enable_big_lds();
+    big_lds_ = true;
+  }
+  RuleMap out;
+  out.row_ptr.assign((size_t)nrows + 1, 0);
+  if (nrows == 0) return out;
+  std::vector<void*> bufs;
+  auto dalloc = [&](size_t b) {
+    void* p = nullptr;
+    KMLS_HIP(hipMalloc(&p, std::max<size_t>(b, 256)));
+    bufs.push_back(p);
+    return p;
+  };
+  try {
+    // [status, n_long] | len_r[nrows] | long_rows[nrows] | row_ptr[nrows + 1]
+    char* meta = (char*)dalloc(256 + (size_t)nrows * 8 + (size_t)(nrows + 1) * 8 + 256);
+    unsigned* status = (unsigned*)meta;
+    unsigned* n_long = status + 1;
+    uint32_t* len_r = (uint32_t*)(meta + 256);
+    int32_t* long_rows = (int32_t*)(len_r + nrows);
+    int64_t* row_ptr = (int64_t*)(meta + 256 + (size_t)nrows * 8);
+    KMLS_HIP(hipMemsetAsync(meta, 0, 256, s));
+    kern::rows_count((const uint32_t*)rows_dev, ld, nrows, F, r0, minsup, len_r, n_long, long_rows, s);
+    std::vector<uint32_t> len((size_t)nrows);
+    unsigned hn[2] = {0, 0};
+    KMLS_HIP(hipMemcpyAsync(len.data(), len_r, (size_t)nrows * 4, hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipMemcpyAsync(hn, meta, 8, hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+    for (int64_t r = 0; r < nrows; ++r) out.row_ptr[(size_t)r + 1] = out.row_ptr[(size_t)r] + len[(size_t)r];
+    out.nnz = out.row_ptr[(size_t)nrows];
+    const int64_t cap = std::max<int64_t>(out.nnz, 1);
+    KMLS_HIP(hipMemcpyAsync(row_ptr, out.row_ptr.data(), (size_t)(nrows + 1) * 8,
+                            hipMemcpyHostToDevice, s));
+    auto* ent = (unsigned long long*)dalloc((size_t)cap * 8);
+    auto* cons = (int32_t*)dalloc((size_t)cap * 4);
+    auto* cnt = (uint32_t*)dalloc((size_t)cap * 4);
+    kern::rows_fill_sort((const uint32_t*)rows_dev, ld, nrows, F, r0, minsup, d_ids_, d_tie_,
+                         d_inv_tie_, len_r, row_ptr, ent, cap, cons, cnt, status, n_long,
+                         long_rows, hn[1] > 0, s);
+    out.cons.resize((size_t)out.nnz);
+    out.cnt.resize((size_t)out.nnz);
+    if (out.nnz) {
+      KMLS_HIP(hipMemcpyAsync(out.cons.data(), cons, (size_t)out.nnz * 4, hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipMemcpyAsync(out.cnt.data(), cnt, (size_t)out.nnz * 4, hipMemcpyDeviceToHost, s));
+    }
+    KMLS_HIP(hipMemcpyAsync(&out.status, status, 4, hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+  } catch (...) {
+    for (void* p : bufs) (void)hipFree(p);
+    throw;
+  }
+  for (void* p : bufs) (void)hipFree(p);
+  return out;
+}
+
 void GpuMiner::bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp,
                             uintptr_t C, int64_t ldc) {
   KMLS_HIP(hipSetDevice(device_));

@@ -242,6 +242,12 @@ class GpuMiner {
     std::vector<uint32_t> cnt;
   };
   RuleMap rule_map_from_gram(uintptr_t gram_dev, int64_t ld, uint32_t minsup);
+  // Multi-GPU rule map (one rank's share): gram_mirror fills the lower triangle of an
+  // upper-triangular gram; rule_map_rows builds the CSR of the row block [r0, r0 + nrows) x F of
+  // a FULL symmetric gram (row_ptr by local row, cons = item ids, rows ordered as the single-GPU
+  // map: count desc, tie key asc).
+  void gram_mirror(uintptr_t gram_dev, int64_t ld, int64_t F);
+  RuleMap rule_map_rows(uintptr_t rows_dev, int64_t ld, int64_t r0, int64_t nrows, uint32_t minsup);
   // C[Fa][ldc] += popcount(A_i & B_j) over Wp words (ring-pass pair counting)
   void bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp, uintptr_t C,
                     int64_t ldc);

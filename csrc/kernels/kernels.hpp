@@ -387,6 +387,18 @@ struct PairsArgs {
 size_t pairs_scratch_bytes(int64_t F_max, int64_t n_items);
 void pairs_to_csr(const PairsArgs& a, hipStream_t s);
 void pairs_enable_big_lds();  // once per process/device before the first pairs_to_csr
+// Multi-GPU rule map: the gram's lower triangle from its upper one (full symmetric rows), then
+// the CSR of a row block [r0, r0 + nrows) x F of it (rows by frequent rank, cons = item ids).
+void gram_mirror(uint32_t* gram, int64_t ld, int64_t F, hipStream_t s);
+void rows_count(const uint32_t* rows, int64_t ld, int64_t nrows, int64_t F, int64_t r0,
+                uint32_t minsup, uint32_t* len_r, unsigned int* n_long, int32_t* long_rows,
+                hipStream_t s);
+void rows_fill_sort(const uint32_t* rows, int64_t ld, int64_t nrows, int64_t F, int64_t r0,
+                    uint32_t minsup, const int32_t* ids, const int32_t* tie, const int32_t* inv_tie,
+                    const uint32_t* len_r, const int64_t* row_ptr, unsigned long long* ent,
+                    int64_t ent_cap, int32_t* cons, uint32_t* cnt, unsigned int* status,
+                    const unsigned int* n_long, const int32_t* long_rows, bool any_long,
+                    hipStream_t s);
 
 // ---- association rules (rules.hip) ----
 struct RuleArgs {

@@ -262,7 +262,7 @@ __device__ __forceinline__ void sort_row(unsigned long long* s, int64_t r, int64
   if (r >= F) return;
   const int64_t n = len_r[r];
   if (n <= lo_exclusive || n > CAP) return;
-  const int64_t base = row_ptr[ids[r]];
+  const int64_t base = ids ? row_ptr[ids[r]] : row_ptr[r];  // (row blocks: local row index)
   if (base + n > ent_cap) return;  // fill overflowed (status set): host redoes the call
   int P = 1;
   while (P < n) P <<= 1;
@@ -327,7 +327,147 @@ __global__ void k_pairs_copyout(const int64_t* __restrict__ row_ptr, int64_t n_i
   }
 }
 
+// ---- row blocks of the FULL symmetric gram (the multi-GPU rule map) ----
+// After the reduce-scatter, rank g holds rows [r0, r0 + nrows) of the summed gram, every column
+// (both triangles), so its rows of the rule map need no other rank's data.
+
+// lower triangle from the upper: 64x64 tiles through LDS (coalesced reads and writes)
+__global__ __launch_bounds__(256) void k_gram_mirror(uint32_t* __restrict__ gram, int64_t ld,
+                                                     int64_t F) {
+  const int64_t bi = blockIdx.y, bj = blockIdx.x;
+  if (bi > bj) return;
+  const int64_t i0 = bi * kPT, j0 = bj * kPT;
+  __shared__ uint32_t t[kPT][kPT + 1];
+  for (int e = threadIdx.x; e < kPT * kPT; e += blockDim.x) {
+    const int r = e / kPT, c = e % kPT;
+    const int64_t i = i0 + r, j = j0 + c;
+    t[r][c] = (i < F && j < F && j > i) ? gram[i * ld + j] : 0u;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kPT * kPT; e += blockDim.x) {
+    const int r = e / kPT, c = e % kPT;  // element (j0 + r, i0 + c) of the lower triangle
+    const int64_t j = j0 + r, i = i0 + c;
+    if (i < F && j < F && j > i) gram[j * ld + i] = t[c][r];
+  }
+}
+
+// row lengths: one block per row, survivors j != own row
+__global__ __launch_bounds__(256) void k_rows_count(const uint32_t* __restrict__ rows, int64_t ld,
+                                                    int64_t nrows, int64_t F, int64_t r0,
+                                                    uint32_t minsup, uint32_t* __restrict__ len_r,
+                                                    unsigned int* __restrict__ n_long,
+                                                    int32_t* __restrict__ long_rows) {
+  const int64_t r = blockIdx.x;
+  if (r >= nrows) return;
+  const uint32_t* row = rows + r * ld;
+  uint32_t n = 0;
+  for (int64_t j = threadIdx.x; j < F; j += blockDim.x) n += (row[j] >= minsup && j != r0 + r);
+  for (int off = 32; off; off >>= 1) n += __shfl_xor(n, off, 64);
+  __shared__ uint32_t s_w[4];
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    len_r[r] = tot;
+    if (tot > (uint32_t)kSortSmall) long_rows[atomicAdd(n_long, 1u)] = (int32_t)r;
+  }
+}
+
+// entries of one row in column order (block-wide compaction), keyed for the descending sort
+__global__ __launch_bounds__(256) void k_rows_fill(const uint32_t* __restrict__ rows, int64_t ld,
+                                                   int64_t nrows, int64_t F, int64_t r0,
+                                                   uint32_t minsup, const int32_t* __restrict__ ids,
+                                                   const int32_t* __restrict__ tie,
+                                                   const int64_t* __restrict__ row_ptr,
+                                                   unsigned long long* __restrict__ ent) {
+  const int64_t r = blockIdx.x;
+  if (r >= nrows) return;
+  const uint32_t* row = rows + r * ld;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ uint32_t s_w[4];
+  int64_t base = row_ptr[r];
+  for (int64_t c0 = 0; c0 < F; c0 += blockDim.x) {
+    const int64_t j = c0 + threadIdx.x;
+    const uint32_t v = j < F ? row[j] : 0u;
+    const bool keep = j < F && v >= minsup && j != r0 + r;
+    const unsigned long long m = __ballot(keep);
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int k = 0; k < w; ++k) pre += s_w[k];
+    const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    if (keep) {
+      const uint32_t pos = pre + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      ent[base + pos] = ((unsigned long long)v << 32) | ~tie_of(tie, ids[j]);
+    }
+    base += tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rows_sort_small(
+    int64_t nrows, const uint32_t* __restrict__ len_r, const int32_t* __restrict__ inv_tie,
+    const int64_t* __restrict__ row_ptr, const unsigned long long* __restrict__ ent, int64_t ent_cap,
+    int32_t* __restrict__ cons, uint32_t* __restrict__ cnt) {
+  __shared__ unsigned long long s[kSortSmall];
+  sort_row<kSortSmall>(s, blockIdx.x, nrows, len_r, nullptr, inv_tie, row_ptr, ent, ent_cap, cons,
+                       cnt, 0);
+}
+
+__global__ __launch_bounds__(1024) void k_rows_sort_big(
+    int64_t nrows, const uint32_t* __restrict__ len_r, const int32_t* __restrict__ inv_tie,
+    const int64_t* __restrict__ row_ptr, const unsigned long long* __restrict__ ent, int64_t ent_cap,
+    int32_t* __restrict__ cons, uint32_t* __restrict__ cnt, unsigned int* __restrict__ status,
+    const unsigned int* __restrict__ n_long, const int32_t* __restrict__ long_rows) {
+  extern __shared__ unsigned long long s_dyn[];
+  const unsigned int nl = *n_long;
+  for (unsigned int i = blockIdx.x; i < nl; i += gridDim.x) {
+    const int64_t r = long_rows[i];
+    if (threadIdx.x == 0 && len_r[r] > (uint32_t)kSortBig) atomicOr(status, 2u);
+    sort_row<kSortBig>(s_dyn, r, nrows, len_r, nullptr, inv_tie, row_ptr, ent, ent_cap, cons, cnt,
+                       kSortSmall);
+    __syncthreads();
+  }
+}
+
 }  // namespace
+
+void gram_mirror(uint32_t* gram, int64_t ld, int64_t F, hipStream_t s) {
+  if (F <= 1) return;
+  const unsigned nt = (unsigned)((F + kPT - 1) / kPT);
+  hipLaunchKernelGGL(k_gram_mirror, dim3(nt, nt), dim3(256), 0, s, gram, ld, F);
+  KMLS_HIP(hipGetLastError());
+}
+
+void rows_count(const uint32_t* rows, int64_t ld, int64_t nrows, int64_t F, int64_t r0,
+                uint32_t minsup, uint32_t* len_r, unsigned int* n_long, int32_t* long_rows,
+                hipStream_t s) {
+  if (nrows <= 0) return;
+  hipLaunchKernelGGL(k_rows_count, dim3((unsigned)nrows), dim3(256), 0, s, rows, ld, nrows, F, r0,
+                     minsup, len_r, n_long, long_rows);
+  KMLS_HIP(hipGetLastError());
+}
+
+void rows_fill_sort(const uint32_t* rows, int64_t ld, int64_t nrows, int64_t F, int64_t r0,
+                    uint32_t minsup, const int32_t* ids, const int32_t* tie, const int32_t* inv_tie,
+                    const uint32_t* len_r, const int64_t* row_ptr, unsigned long long* ent,
+                    int64_t ent_cap, int32_t* cons, uint32_t* cnt, unsigned int* status,
+                    const unsigned int* n_long, const int32_t* long_rows, bool any_long,
+                    hipStream_t s) {
+  if (nrows <= 0) return;
+  hipLaunchKernelGGL(k_rows_fill, dim3((unsigned)nrows), dim3(256), 0, s, rows, ld, nrows, F, r0,
+                     minsup, ids, tie, row_ptr, ent);
+  KMLS_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_rows_sort_small, dim3((unsigned)nrows), dim3(256), 0, s, nrows, len_r,
+                     inv_tie, row_ptr, ent, ent_cap, cons, cnt);
+  KMLS_HIP(hipGetLastError());
+  if (any_long) {
+    hipLaunchKernelGGL(k_rows_sort_big, dim3(64), dim3(1024),
+                       (size_t)kSortBig * sizeof(unsigned long long), s, nrows, len_r, inv_tie,
+                       row_ptr, ent, ent_cap, cons, cnt, status, n_long, long_rows);
+    KMLS_HIP(hipGetLastError());
+  }
+}
 
 namespace {
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -402,9 +542,9 @@ void pairs_to_csr(const PairsArgs& a, hipStream_t s) {
 }
 
 void pairs_enable_big_lds() {
-  KMLS_HIP(hipFuncSetAttribute((const void*)k_pairs_sort_big,
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(kSortBig * sizeof(unsigned long long))));
+  for (const void* f : {(const void*)k_pairs_sort_big, (const void*)k_rows_sort_big})
+    KMLS_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)(kSortBig * sizeof(unsigned long long))));
 }
 
 }  // namespace kern

@@ -41,7 +41,8 @@ def main(argv=None) -> int:
     ap.add_argument("--pairs", default="", choices=["", "allreduce", "reduce_scatter", "alltoall", "ring"],
                     help="pairs-only pipeline (RULES_MODE=pairs) with this distributed strategy")
     ap.add_argument("--rule-map", action="store_true",
-                    help="config 5: the deployed artifact (pair rule map) at HBM scale, 1 GPU")
+                    help="config 5: the deployed artifact (pair rule map) at HBM scale, every "
+                         "rank of the job (transaction shards, gram row reduce-scatter)")
     ap.add_argument("--verify-rows", type=int, default=64,
                     help="--rule-map: gram rows re-counted by the independent popcount kernel")
     args = ap.parse_args(argv)
@@ -177,159 +178,181 @@ def main(argv=None) -> int:
 
 
 def rule_map_main(args) -> int:
-    """BASELINE config 5 on one GPU: the reference's deployed artifact (the rule map = the
-    pair-support matrix, machine-learning/main.py:282-296) at a min_support that leaves >10k
-    frequent items of a 1M vocabulary, over 100M transactions — the bitmap alone is ~190 GB of
-    HBM.  Timed step: supports (partitioned histogram), selection, banded LDS-slab encode, MFMA
-    gram (upper triangle), device pairs_to_csr.  Then: the rules.idx write, a hot reload into
-    the C++ matcher and the HBM index, and batched queries.  Verification: ``--verify-rows``
-    rows of the MFMA gram re-counted by the popcount bit-GEMM (a different kernel), and sampled
-    rule-map rows checked against co-occurrence counts computed on the host from the CSR."""
+    """BASELINE config 5: the reference's deployed artifact (the rule map = the pair-support
+    matrix, machine-learning/main.py:282-296) at a min_support that leaves >10k frequent items of
+    a 1M vocabulary, over 100M transactions — the bitmap alone is ~185 GB of HBM at one GPU.
+
+    One process per GPU (``torchrun --nproc-per-node N``; N = 1 without torchrun): every rank
+    generates ONLY its transaction shard and runs ``parallel.rule_map.DistRuleMap``: shard
+    supports + all-reduce, selection, banded LDS-slab encode, MFMA gram of the shard, mirror,
+    reduce-scatter of full-row blocks over the native communicator (RCCL), the CSR of its rows,
+    gather to rank 0 by item id.  Timed step = that whole call, max over ranks.  Then on rank 0:
+    the rules.idx write, a hot reload into the C++ matcher and the HBM index, batched queries.
+    Verification: ``--verify-rows`` rows of every rank's shard gram re-counted by the popcount
+    bit-GEMM (a different kernel), and sampled rule-map rows checked against co-occurrence counts
+    computed on the host from every shard's CSR (all-reduced)."""
     import numpy as np
     import torch
+    import torch.distributed as dist
 
     from ..data.synthetic import SHAPES
     from ..ops import native
+    from ..parallel.dist_miner import shard_bounds
+    from ..parallel.rule_map import DistRuleMap
     from ..serve.index import RuleIndexData, index_from_device_csr
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     N = native.require_gpu()
-    torch.cuda.set_device(0)
+    dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    if world > 1:
+        import datetime
+        backend = os.environ.get("KMLS_BENCH_DIST", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev),
+                                    timeout=datetime.timedelta(seconds=600))
+        else:  # ranks sharing a GPU (rehearsal): gloo rendezvous + the host communicator
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
     shape = SHAPES[args.shape]
     T, I = args.n_tx or shape.n_tx, shape.n_items
+    lo, hi, _ = shard_bounds(T, world, rank)
     t0 = time.perf_counter()
     ptr, items = N.synth_transactions(T, I, shape.mean_len, shape.n_genres, shape.genre_affinity,
-                                      0.85, args.seed)
+                                      0.85, args.seed, 0, lo, hi)
     gen_s = time.perf_counter() - t0
-    # one non-default torch stream shared with the miner: torch fills, the native kernels and the
-    # timing events are all ordered on it (the default stream's handle is 0, which would give the
-    # miner a private stream)
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
-    g = N.GpuMiner(0, 1 << 30, stream.cuda_stream)
     t0 = time.perf_counter()
-    g.load_csr(ptr, items, I)
+    rm = DistRuleMap(ptr, items, I, T, args.min_support, device=dev)
     load_s = time.perf_counter() - t0
-    Wp = g.words_local()
-    used = (T + 63) // 64
     out = {"bench": "large-rule-map", "shape": args.shape, "n_tx": T, "n_items": I,
-           "nnz": int(len(items)), "n_gpus": 1, "min_support": args.min_support,
-           "gen_s": round(gen_s, 2), "load_s": round(load_s, 2)}
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-    held = {}  # bitmap + gram buffers kept across steps (a 185 GB hipMalloc alone takes seconds)
+           "nnz_local": int(len(items)), "n_gpus": world,
+           "parallelism": f"tx-shard{world}+gram-row-reduce-scatter({rm.comm_backend})"
+           if world > 1 else "single", "min_support": args.min_support,
+           "gen_s_local_shard": round(gen_s, 2), "load_s": round(load_s, 2)}
 
-    def buf(name, shape):
-        t = held.get(name)
-        if t is None or tuple(t.shape) != shape:
-            held.pop(name, None)
-            t = held[name] = torch.empty(shape, dtype=torch.int32 if name == "gram" else torch.int64,
-                                         device="cuda")
-        return t
-
-    def step():
-        ev[0].record()
-        cnt = torch.zeros(I, dtype=torch.int32, device="cuda")
-        g.item_support(cnt.data_ptr())
-        host = cnt.cpu().numpy().view(np.uint32)
-        ev[1].record()
-        F = g.select(host, T, args.min_support)
-        ids, fcounts, minsup = g.frequent()
-        bm = buf("bm", (F, Wp))
-        if Wp > used:
-            bm[:, used:] = 0
-        ev[2].record()
-        g.encode_bitmaps(bm.data_ptr(), Wp, 0)
-        ev[3].record()
-        gram = buf("gram", (F, F))
-        g.pair_counts(bm.data_ptr(), Wp, gram.data_ptr(), True)
-        ev[4].record()
-        rm = g.rule_map_from_gram(gram.data_ptr(), F, int(minsup))
-        ev[5].record()
+    def bar():
         torch.cuda.synchronize()
-        return F, ids, fcounts, int(minsup), bm, gram, rm
+        if world > 1:
+            dist.barrier()
 
+    r = None
     for _ in range(args.warmup):
-        step()
+        r = rm.step()
+    bar()
     t0 = time.perf_counter()
     for _ in range(max(1, args.steps)):
-        F, ids, fcounts, minsup, bm, gram, rm = step()
+        r = rm.step()
+    bar()
     ms = (time.perf_counter() - t0) * 1000.0 / max(1, args.steps)
-    names = ["supports+readback", "select", "encode_bitmap", "gram_mfma", "pairs_to_csr"]
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    g = rm.ops.g
+    ids, fcounts, minsup = g.frequent()
+    ids = np.asarray(ids)
+    F = len(ids)
+    Ws = rm.ops.Ws
     out.update({"ms_per_step": round(ms, 1), "n_frequent_items": int(F),
-                "bitmap_gb": round(F * Wp * 8 / 1e9, 1), "gram_gb": round(F * F * 4 / 1e9, 2),
-                "rule_map_entries": int(rm["nnz"]), "rule_map_status": int(rm["status"]),
-                "frequent_pairs": int(rm["nnz"]) // 2,
-                "phases_ms": {n: round(ev[i].elapsed_time(ev[i + 1]), 2)
-                              for i, n in enumerate(names)},
-                "hbm_gb_allocated": round(torch.cuda.max_memory_allocated() / 1e9, 1)})
-    # gram work: F(F+1)/2 row pairs x T bits
-    out["gram_tera_bitops_per_s"] = round(F * (F + 1) / 2 * T / (out["phases_ms"]["gram_mfma"] / 1e3) / 1e12, 1)
-    # 1. gram rows re-counted by the popcount bit-GEMM (independent kernel), full rows
+                "bitmap_gb_per_rank": round(F * Ws * 8 / 1e9, 1),
+                "bitmap_gb_total": round(F * Ws * 8 * world / 1e9, 1),
+                "gram_gb": round(F * F * 4 / 1e9, 2),
+                "hbm_gb_allocated_rank0": round(torch.cuda.max_memory_allocated() / 1e9, 1)})
+    if rank == 0:
+        out.update({"rule_map_entries": int(r["nnz"]), "rule_map_status": int(r["status"]),
+                    "frequent_pairs": int(r["nnz"]) // 2, "phases_ms_rank0": r["phases_ms"]})
+    # 1. each rank's shard gram rows re-counted by the popcount bit-GEMM (independent kernel)
+    bm, gram = rm.ops.held["bm"], rm.ops.held["gram"]
     k = min(args.verify_rows, F)
     chk = torch.zeros((k, F), dtype=torch.int32, device="cuda")
-    g.bitgemm_rect(bm.data_ptr(), k, bm.data_ptr(), F, Wp, chk.data_ptr(), F)
+    g.bitgemm_rect(bm.data_ptr(), k, bm.data_ptr(), F, Ws, chk.data_ptr(), F)
     torch.cuda.synchronize()
-    gm = gram[:k].cpu().numpy()
+    gm = gram[:k, :F].cpu().numpy()
     ck = chk.cpu().numpy()
-    iu = np.triu_indices(k, 1, F)
-    out["verified_gram_rows"] = bool(np.array_equal(gm[iu], ck[iu]))
-    out["verified_gram_diag_vs_supports"] = bool(np.array_equal(np.diag(ck[:, :k]), fcounts[:k]))
-    del bm, chk
-    held.clear()
-    # 2. sampled rule-map rows vs host co-occurrence counts from the CSR
+    # (the gram holds the mirrored shard counts before the reduce-scatter: full rows, so every
+    # off-diagonal entry of the k rows is compared — upper entries and their mirror images)
+    off = np.ones(gm.shape, bool)
+    off[np.arange(k), np.arange(k)] = False
+    ok_rows = bool(np.array_equal(gm[off], ck[off]))
+    del chk
+    # 2. sampled rule-map rows vs host co-occurrence counts, summed over the shards
     rng = np.random.default_rng(1)
     sample = np.sort(rng.choice(ids, size=min(6, F), replace=False)).astype(np.int32)
     pos = np.flatnonzero(np.isin(items, sample))
     tx_of = np.searchsorted(ptr, pos, side="right") - 1
     tids = {int(x): np.unique(tx_of[items[pos] == x]) for x in sample}
-    row_ptr, cons, rcount = rm["row_ptr"], rm["cons"], rm["count"]
-    ok = True
-    for x in sample:
-        row = slice(int(row_ptr[x]), int(row_ptr[x + 1]))
-        c_row, n_row = cons[row], rcount[row]
-        ok &= bool(np.all(np.diff(n_row.astype(np.int64)) <= 0))  # count desc
-        got = dict(zip(c_row.tolist(), n_row.tolist()))
-        for y in sample:
-            if y == x:
-                continue
-            want = int(np.intersect1d(tids[int(x)], tids[int(y)], assume_unique=True).size)
-            ok &= (got.get(int(y), 0) == want) if want >= minsup else (int(y) not in got)
-    out["verified_rule_map_sample"] = bool(ok)
-    # 3. artifact: rules.idx write, hot reload into the C++ matcher + HBM index, batched queries
-    ix = index_from_device_csr({"row_ptr": row_ptr, "cons": cons, "count": rcount}, I, ids, T)
-    with tempfile.TemporaryDirectory() as d:
-        path = os.path.join(d, "rules.idx")
-        t1 = time.perf_counter()
-        ix.save(path)
-        out["index_write_ms"] = round((time.perf_counter() - t1) * 1000, 1)
-        out["index_bytes"] = os.path.getsize(path)
-        t1 = time.perf_counter()
-        back = RuleIndexData.load(path)
-        host = back.native()
-        out["reload_cpu_ms"] = round((time.perf_counter() - t1) * 1000, 1)
-        t1 = time.perf_counter()
-        gidx = N.GpuRuleIndex(0, host)
-        out["reload_hbm_ms"] = round((time.perf_counter() - t1) * 1000, 1)
-        # rows here hold thousands of entries: past the HIP kernel's per-wave LDS table, so its
-        # queries take the host path inside query_batch (measured, not hidden)
-        for B in (1, 64, 1024):
-            lens = rng.integers(1, 6, size=B)
-            q_ptr = np.zeros(B + 1, np.int64)
-            np.cumsum(lens, out=q_ptr[1:])
-            seeds = ids[rng.integers(0, F, int(q_ptr[-1]))].astype(np.int32)
-            res = {}
-            for nm, fn in (("cpp", host.query_batch), ("hip", gidx.query_batch)):
-                fn(q_ptr, seeds, 10)
-                t1 = time.perf_counter()
-                reps = 3
-                for _ in range(reps):
-                    got = fn(q_ptr, seeds, 10)
-                res[nm] = ((time.perf_counter() - t1) / reps * 1e6, got)
-            same = bool(np.array_equal(res["cpp"][1][0], res["hip"][1][0]) and
-                        np.array_equal(res["cpp"][1][1], res["hip"][1][1]))
-            out[f"query_batch{B}_us"] = {"cpp": round(res["cpp"][0], 1),
-                                         "hip": round(res["hip"][0], 1), "same": same}
-        del gidx
-    print(json.dumps(out), flush=True)
+    co = np.zeros((len(sample), len(sample)), np.int64)
+    for a_, x in enumerate(sample):
+        for b_, y in enumerate(sample):
+            co[a_, b_] = np.intersect1d(tids[int(x)], tids[int(y)], assume_unique=True).size
+    flags = np.array([int(ok_rows)], np.int64)
+    if world > 1:
+        tco = torch.from_numpy(co)
+        tfl = torch.from_numpy(flags)
+        if dist.get_backend() == "nccl":
+            tco, tfl = tco.cuda(), tfl.cuda()
+        dist.all_reduce(tco)
+        dist.all_reduce(tfl, op=dist.ReduceOp.MIN)
+        co, flags = tco.cpu().numpy(), tfl.cpu().numpy()
+    out["verified_gram_rows_all_ranks"] = bool(flags[0])
+    if rank == 0:
+        row_ptr, cons, rcount = r["row_ptr"], r["cons"], r["count"]
+        ok = True
+        for a_, x in enumerate(sample):
+            row = slice(int(row_ptr[x]), int(row_ptr[x + 1]))
+            c_row, n_row = cons[row], rcount[row]
+            ok &= bool(np.all(np.diff(n_row.astype(np.int64)) <= 0))  # count desc
+            got = dict(zip(c_row.tolist(), n_row.tolist()))
+            for b_, y in enumerate(sample):
+                if y == x:
+                    continue
+                want = int(co[a_, b_])
+                ok &= (got.get(int(y), 0) == want) if want >= minsup else (int(y) not in got)
+        out["verified_rule_map_sample"] = bool(ok)
+    rm.release()
+    del bm, gram
+    if rank == 0:
+        # 3. artifact: rules.idx write, hot reload into the C++ matcher + HBM index, queries
+        ix = index_from_device_csr({"row_ptr": r["row_ptr"], "cons": r["cons"],
+                                    "count": r["count"]}, I, ids, T)
+        with tempfile.TemporaryDirectory() as d:
+            path = os.path.join(d, "rules.idx")
+            t1 = time.perf_counter()
+            ix.save(path)
+            out["index_write_ms"] = round((time.perf_counter() - t1) * 1000, 1)
+            out["index_bytes"] = os.path.getsize(path)
+            t1 = time.perf_counter()
+            back = RuleIndexData.load(path)
+            host = back.native()
+            out["reload_cpu_ms"] = round((time.perf_counter() - t1) * 1000, 1)
+            t1 = time.perf_counter()
+            gidx = N.GpuRuleIndex(dev, host)
+            out["reload_hbm_ms"] = round((time.perf_counter() - t1) * 1000, 1)
+            # rows here hold thousands of entries: past the HIP kernel's per-wave LDS table, so
+            # its queries take the host path inside query_batch (measured, not hidden)
+            for B in (1, 64, 1024):
+                lens = rng.integers(1, 6, size=B)
+                q_ptr = np.zeros(B + 1, np.int64)
+                np.cumsum(lens, out=q_ptr[1:])
+                seeds = ids[rng.integers(0, F, int(q_ptr[-1]))].astype(np.int32)
+                res = {}
+                for nm, fn in (("cpp", host.query_batch), ("hip", gidx.query_batch)):
+                    fn(q_ptr, seeds, 10)
+                    t1 = time.perf_counter()
+                    reps = 3
+                    for _ in range(reps):
+                        got = fn(q_ptr, seeds, 10)
+                    res[nm] = ((time.perf_counter() - t1) / reps * 1e6, got)
+                same = bool(np.array_equal(res["cpp"][1][0], res["hip"][1][0]) and
+                            np.array_equal(res["cpp"][1][1], res["hip"][1][1]))
+                out[f"query_batch{B}_us"] = {"cpp": round(res["cpp"][0], 1),
+                                             "hip": round(res["hip"][0], 1), "same": same}
+            del gidx
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
     return 0
 
 
