@@ -21,8 +21,10 @@ inline unsigned long long uni64(unsigned long long v) {
 
 inline unsigned long long ld_agent(const unsigned long long* p) { return __atomic_load_n(p, __ATOMIC_SEQ_CST); }
 inline unsigned ld_agent(const unsigned* p) { return __atomic_load_n(p, __ATOMIC_SEQ_CST); }
-inline void fence_agent() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
-inline void wait_short() { std::this_thread::yield(); }
+inline void st_agent(unsigned long long* p, unsigned long long v) { __atomic_store_n(p, v, __ATOMIC_SEQ_CST); }
+inline void st_agent(unsigned* p, unsigned v) { __atomic_store_n(p, v, __ATOMIC_SEQ_CST); }
+inline void wait_stores() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
+inline void wait_short(unsigned) { std::this_thread::yield(); }
 
 }  // namespace kern
 }  // namespace kmls

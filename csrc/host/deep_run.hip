@@ -21,7 +21,7 @@ namespace gpu {
 
 DeepBufs::~DeepBufs() {
   (void)hipSetDevice(device);
-  for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)heap[0],
+  for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)req, (void*)heap[0],
                   (void*)heap[1], (void*)root, (void*)ctl, (void*)d_red, (void*)d_xor,
                   (void*)d_m, (void*)d_off, (void*)d_toff})
     if (p) (void)hipFree(p);
@@ -206,11 +206,18 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   if (opt.steal && n_tasks > 0) {
     // one launch: spilled tasks are queued behind the level-3 tasks and taken by waiting waves
     const auto tr = now();
-    KMLS_HIP(hipMemsetAsync(b.ctl, 0, 5 * sizeof(unsigned long long), s));
+    KMLS_HIP(hipMemsetAsync(b.ctl, 0, 4 * sizeof(unsigned long long), s));
+    if (b.req_cap < waves) {
+      if (b.req) KMLS_HIP(hipFree(b.req));
+      KMLS_HIP(hipMalloc((void**)&b.req, (size_t)waves * sizeof(unsigned)));
+      KMLS_HIP(hipMemsetAsync(b.req, 0, (size_t)waves * sizeof(unsigned), s));
+      b.req_cap = waves;
+    }
     b.h_ctl->pending = (unsigned long long)n_tasks;
     KMLS_HIP(hipMemcpyAsync(&b.ctl->pending, &b.h_ctl->pending, 8, hipMemcpyHostToDevice, s));
-    if (++b.epoch == 0) {  // 2^32 launches: restart the stamps
+    if (++b.epoch >= (1u << 31)) {  // 2^31 launches: restart the stamps
       KMLS_HIP(hipMemsetAsync(b.ready, 0, (size_t)b.q_cap * sizeof(unsigned), s));
+      KMLS_HIP(hipMemsetAsync(b.req, 0, (size_t)b.req_cap * sizeof(unsigned), s));
       b.epoch = 1;
     }
     a.in = b.q[0];
@@ -221,7 +228,9 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     a.ready = b.ready;
     a.epoch = b.epoch;
     a.steal = 1;
-    a.steal_idle = opt.steal_idle;
+    a.steal_eager = opt.steal_idle == 0 ? 1 : 0;
+    a.req = b.req;
+    a.nwaves = waves;
     kern::deep_count(a, maxt, blocks_per_cu, grid, s);
     KMLS_HIP(hipMemcpyAsync(b.h_ctl, b.ctl, sizeof(kern::DeepCtl), hipMemcpyDeviceToHost, s));
     KMLS_HIP(hipStreamSynchronize(s));

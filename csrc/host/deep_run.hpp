@@ -25,6 +25,8 @@ struct DeepBufs {
   kern::DeepFrame* q[2] = {nullptr, nullptr};
   int64_t q_cap = 0;
   unsigned* ready = nullptr;  // [q_cap] steal-mode publish flags (zeroed once at allocation)
+  unsigned* req = nullptr;    // [req_cap] steal-mode mailboxes (one per wave)
+  int64_t req_cap = 0;
   unsigned epoch = 0;         // steal-mode launch stamp of the flags
 
   char* heap[2] = {nullptr, nullptr};

@@ -149,10 +149,11 @@ struct DeepOpts {
   unsigned split_min = 8;             // spilled frames above this many members split per member
   int blocks_per_cu = 0;              // 0 = the kernel instance's occupancy (deep_waves_per_simd)
   int stack_mb = 0;                   // per-wave stack (0: KMLS_DEEP_STACK_MB or 4)
-  bool steal = true;                  // one launch, spills taken by waiting waves (budget =
+  bool steal = false;                 // one launch, spills taken by waiting waves (budget =
                                       // passes between checks for a waiting wave); false =
                                       // spill rounds (budget0/budget = per-task step budgets)
-  unsigned steal_idle = 1;            // steal: spill when this many waves wait (0 = always)
+  unsigned steal_idle = 1;            // steal: 1 = hand over when a waiting wave asks; 0 = at
+                                      // every check (tests)
 };
 struct DeepResult {
   std::vector<uint64_t> per_level;  // [d] = frequent itemsets of size d (index 0 unused)

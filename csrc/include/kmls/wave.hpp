@@ -36,18 +36,32 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long v) {
   return ((unsigned long long)uni((unsigned)(v >> 32)) << 32) | uni((unsigned)v);
 }
 
-// Cross-wave hand-off (work queues inside one launch): loads that observe another CU's
-// stores go to L2 (agent-scope atomic load, no stale vector-L1 line); the fence orders this
-// wave's earlier stores before a later flag store (release) and invalidates L1 after a flag was
-// seen (acquire).
+// Cross-wave hand-off inside one launch (work queues).  The 8 XCDs' L2 caches are not coherent
+// with each other, and an agent-scope fence writes back / invalidates a whole L2, so hand-offs
+// avoid fences: the producer writes the handed-over data with agent-scope (write-through)
+// stores, waits for them to complete (wait_stores), then sets a flag with an atomic; the
+// consumer reads the flag and the small descriptors with agent-scope loads.  Bulk data read
+// afterwards with plain loads lives in 128-byte-aligned lines no wave of the launch has read
+// before it was published, so no cache holds a stale copy of it.
 __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void fence_agent() { __threadfence(); }
-__device__ __forceinline__ void wait_short() { __builtin_amdgcn_s_sleep(8); }
+__device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_stores() { __builtin_amdgcn_s_waitcnt(0); }
+__device__ __forceinline__ void wait_short(unsigned n) {
+  // s_sleep takes an immediate: a few fixed steps of backoff
+  if (n < 4) __builtin_amdgcn_s_sleep(2);
+  else if (n < 16) __builtin_amdgcn_s_sleep(16);
+  else __builtin_amdgcn_s_sleep(127);
+}
 
 }  // namespace kern
 }  // namespace kmls

@@ -50,6 +50,7 @@ constexpr int kCap = 256;            // candidate pairs per batch step
 constexpr int kBatchFrames = 64;     // frames one batch step may take
 constexpr int kBStack = 96;          // blocks on one wave's memory stack
 constexpr unsigned kSingle = 1u << 8;  // frame flag: expand only its first member
+constexpr unsigned kDone = 1u << 31;   // steal mode: ready-flag value epoch ^ kDone = no task
 
 // frame meta: bits 0..7 prefix size, bit 8 single, bits 9..15 block width (words), bits 16..31
 // block-stack index + 1 (0 = external)
@@ -87,6 +88,30 @@ __device__ __forceinline__ DeepFrame load_frame(const DeepFrame* p, int lane) {
   f.m = uni(f.m);
   f.meta = uni(f.meta);
   return f;
+}
+
+// the same frame through agent-scope loads (a frame another wave published in this launch:
+// its 128-byte line may hold older frames this CU already read)
+__device__ __forceinline__ DeepFrame load_frame_agent(const DeepFrame* p, int lane) {
+  const unsigned* w = (const unsigned*)p;
+  const unsigned v = lane < 8 ? ld_agent(w + (lane & 7)) : 0u;
+  DeepFrame f;
+  f.blk = uni64(((unsigned long long)__shfl(v, 1, 64) << 32) | __shfl(v, 0, 64));
+  f.hash = uni64(((unsigned long long)__shfl(v, 3, 64) << 32) | __shfl(v, 2, 64));
+  f.pad = uni(__shfl(v, 4, 64));
+  f.s0 = uni(__shfl(v, 5, 64));
+  f.m = uni(__shfl(v, 6, 64));
+  f.meta = uni(__shfl(v, 7, 64));
+  return f;
+}
+
+// a frame handed to another wave: write-through stores (see kmls/wave.hpp)
+__device__ __forceinline__ void publish_frame(DeepFrame* p, const DeepFrame& f) {
+  unsigned long long* w = (unsigned long long*)p;
+  st_agent(w + 0, f.blk);
+  st_agent(w + 1, f.hash);
+  st_agent(w + 2, ((unsigned long long)f.s0 << 32) | f.pad);
+  st_agent(w + 3, ((unsigned long long)f.meta << 32) | f.m);
 }
 
 __device__ __forceinline__ void store_frame(DeepFrame* p, const DeepFrame& f) {
@@ -249,16 +274,20 @@ __device__ __forceinline__ void free_blocks(WaveLds<MAXT>& L, WaveState& st) {
   }
 }
 
-// Copy every frame on the stack to the spill heap and queue it as task(s): frames of more than
-// split_min members become one single-member task each (over one shared copy).  Heap bytes and
-// queue slots are reserved for the whole stack before anything is written, so a spill either
-// happens completely or not at all.  Returns 0 (spilled: the stack is empty), 1 (optional spill
-// skipped: no room, the wave keeps its frames) or -1 (a required spill found no room: error set).
-// Steal mode publishes every task by its ready flag after a release fence.
+// Copy the bottom `ns` frames of the stack (all of them: ns = nf) to the spill heap and queue
+// them as task(s): frames of more than split_min members become one single-member task each
+// (over one shared copy).  Heap bytes and queue slots are reserved for all of them before
+// anything is written, so a spill either happens completely or not at all.  Returns 0 (spilled),
+// 1 (optional spill skipped: no room, the wave keeps its frames) or -1 (a required spill found
+// no room: error set).  Steal mode publishes every task by its ready flag.  A partial spill
+// (ns < nf: the oldest, largest open classes handed to waiting waves) drops the spilled frames'
+// block references and moves the remaining frames down; the wave keeps working on them.
+template <int MAXT>
 __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st,
-                                            int lane, bool optional) {
+                                            WaveLds<MAXT>& L, int lane, bool optional,
+                                            unsigned ns) {
   unsigned long long bytes_tot = 0, nt_tot = 0;
-  for (unsigned f = 0; f < st.nf; ++f) {
+  for (unsigned f = 0; f < ns; ++f) {
     const DeepFrame fr = load_frame(fst + f, lane);
     bytes_tot += (unsigned long long)(meta_width(fr.meta) + 1) * roundup16(fr.m) * 8ull;
     const bool single = (fr.meta & kSingle) != 0;
@@ -292,7 +321,7 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
   }
   DeepFrame* out = a.out + (a.steal ? a.n_in : 0ll);
   unsigned long long hoff = hbase, q = t0;
-  for (unsigned f = 0; f < st.nf; ++f) {
+  for (unsigned f = 0; f < ns; ++f) {
     const DeepFrame fr = load_frame(fst + f, lane);
     const unsigned m = fr.m;
     const unsigned wt = meta_width(fr.meta);
@@ -302,7 +331,10 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
     const unsigned long long tot = (unsigned long long)(wt + 1) * m;
     for (unsigned long long e = lane; e < tot; e += 64) {
       const unsigned long long w = e / m, k = e - w * m;
-      dst[w * npad + k] = src[w * fr.pad + fr.s0 + k];
+      if (a.steal)
+        st_agent(dst + w * npad + k, src[w * fr.pad + fr.s0 + k]);
+      else
+        dst[w * npad + k] = src[w * fr.pad + fr.s0 + k];
     }
     const bool single = (fr.meta & kSingle) != 0;
     const bool split = !single && m > a.split_min;
@@ -315,19 +347,42 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
       o.s0 = split ? k : 0u;
       o.m = split ? m - k : m;
       o.meta = make_meta(meta_depth(fr.meta), split || single, wt, 0);
-      store_frame(out + q + k, o);
+      if (a.steal)
+        publish_frame(out + q + k, o);
+      else
+        store_frame(out + q + k, o);
     }
     hoff += (unsigned long long)(wt + 1) * npad * 8ull;
     q += nt;
   }
   if (a.steal) {
-    fence_agent();  // release: the blocks and frames above before their ready flags
+    wait_stores();  // the write-through copies and frames above are complete before the flags
     __builtin_amdgcn_wave_barrier();
     for (unsigned long long k = lane; k < nt_tot; k += 64) atomicExch(&a.ready[t0 + k], a.epoch);
   }
-  st.nf = 0;
-  st.nb = 0;
-  st.mem_top = 0;
+  if (ns == st.nf) {
+    st.nf = 0;
+    st.nb = 0;
+    st.mem_top = 0;
+    return 0;
+  }
+  // partial: the spilled frames' blocks lose a reference; frames ns.. move down by ns (64 at a
+  // time, low to high: a chunk's loads happen before its stores, and it only overwrites frames
+  // an earlier chunk already moved)
+  if ((unsigned)lane < ns) {
+    const unsigned b = meta_bidx(fst[lane].meta);
+    if (b) atomicSub(&L.b_live[b - 1], 1u);
+  }
+  const unsigned rest = st.nf - ns;
+  for (unsigned c0 = 0; c0 < rest; c0 += 64) {
+    const bool act = c0 + lane < rest;
+    DeepFrame fr{};
+    if (act) fr = fst[ns + c0 + lane];
+    __builtin_amdgcn_wave_barrier();
+    if (act) store_frame(fst + c0 + lane, fr);
+    __builtin_amdgcn_wave_barrier();
+  }
+  st.nf = rest;
   return 0;
 }
 
@@ -614,33 +669,42 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
     if (!a.steal) {
       if (t >= (unsigned long long)a.n_in) break;
     } else {
-      // ticket t: wait until task t is published, or until no task is queued or running
-      // (pending == 0: nothing can be spilled any more, every reserved slot is done)
-      bool waiting = false, done = false;
-      for (;;) {
-        unsigned long long tail = 0, pend = 0, rdy = 0;
+      // ticket t: wait on its own flag (waiting waves poll distinct addresses: one address
+      // polled by thousands of waves serialises every device-scope access to it) until the task
+      // is published (epoch) or the launch is over (epoch ^ kDone, written by the wave that
+      // finished the last task over every ticket that can still be outstanding).  Meanwhile it
+      // asks busy waves, one mailbox at a time, to hand over their oldest open class.
+      bool done = false;
+      unsigned victim = (unsigned)((gw * 7919ull + 1) % (unsigned long long)a.nwaves);
+      for (unsigned n = 0;; ++n) {
+        unsigned rdy = 0, fin = 0;
         if (lane == 0) {
-          tail = (unsigned long long)a.n_in + ld_agent(&a.ctl->n_out);
+          if (t < (unsigned long long)a.n_in) {
+            rdy = 1u;
+          } else if (t < (unsigned long long)a.out_cap) {
+            const unsigned v = ld_agent(&a.ready[t - a.n_in]);
+            rdy = v == a.epoch;
+            fin = v == (a.epoch ^ kDone);
+          } else if ((n & 63) == 63) {  // past the queue's capacity: never published
+            fin = ld_agent(&a.ctl->pending) == 0ull;
+          }
           // a failed wave never finishes its task: its error ends the wait of the others
-          pend = ld_agent(&a.ctl->error) ? 0ull : ld_agent(&a.ctl->pending);
-          rdy = t < (unsigned long long)a.n_in ? 1ull
-                : (t < tail && ld_agent(&a.ready[t - a.n_in]) == a.epoch) ? 1ull : 0ull;
+          if (!rdy && !fin && (n & 255) == 255) fin = ld_agent(&a.ctl->error) != 0u;
+          if (!rdy && !fin && (n & 15) == 15) {
+            if (victim != (unsigned)gw) atomicExch(&a.req[victim], a.epoch);
+            victim = (victim + 97u) % (unsigned)a.nwaves;
+          }
         }
-        rdy = uni64(bcast64(rdy, 0));
-        if (rdy) break;
-        pend = uni64(bcast64(pend, 0));
-        if (pend == 0) { done = true; break; }
-        if (!waiting && lane == 0) atomicAdd(&a.ctl->idle, 1ull);
-        waiting = true;
+        if (uni(__shfl(rdy, 0, 64))) break;
+        if (uni(__shfl(fin, 0, 64))) { done = true; break; }
         if (timed_out()) { failed = true; break; }
-        wait_short();
+        wait_short(n);
       }
-      if (waiting && lane == 0) atomicSub(&a.ctl->idle, 1ull);
       if (done || failed) break;
-      fence_agent();  // acquire: the task's frame and block as its producer wrote them
     }
     {
-      const DeepFrame tf = load_frame(a.in + t, lane);
+      const DeepFrame tf = a.steal && t >= (unsigned long long)a.n_in ? load_frame_agent(a.in + t, lane)
+                                                                       : load_frame(a.in + t, lane);
       if (lane == 0) store_frame(fst, tf);
       // lanes exchange frames through memory: coherent within a wave in program order (one L1);
       // the wave barriers mark those hand-offs (the CPU emulator synchronises its lanes there)
@@ -667,16 +731,25 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
           (unsigned long long)(wt + 1) * roundup16(row_mode ? m : kCap) * 8ull;
       if (st.mem_top + need > a.stack_bytes || st.nf + kCap + 2 > (unsigned)a.fcap ||
           st.nb + 1 >= (unsigned)kBStack || (!a.steal && acc.budget_used >= a.budget)) {
-        if (spill_frames(a, fst, st, lane, false) < 0) failed = true;
+        if (spill_frames<MAXT>(a, fst, st, L, lane, false, st.nf) < 0) failed = true;
         break;
       }
       if (a.steal && acc.budget_used >= a.budget) {
-        // hand the stack to the waiting waves (a skipped spill keeps the frames)
-        unsigned long long idle = 0;
-        if (lane == 0) idle = ld_agent(&a.ctl->idle);
-        idle = uni64(bcast64(idle, 0));
+        // a waiting wave asked (this wave's own mailbox): hand over the bottom (oldest,
+        // largest) open class and keep the rest; a lone frame goes whole (a skipped spill keeps
+        // the frames).  steal_eager: at every check (tests)
+        unsigned want = a.steal_eager ? 1u : 0u;
+        if (!want && lane == 0) {
+          want = ld_agent(&a.req[gw]) == a.epoch;
+          if (want) st_agent(&a.req[gw], 0u);
+        }
+        want = uni(__shfl(want, 0, 64));
         acc.budget_used = 0;
-        if (idle >= a.steal_idle && spill_frames(a, fst, st, lane, true) == 0) break;
+        if (want && spill_frames<MAXT>(a, fst, st, L, lane, true, 1) == 0) {
+          free_blocks(L, st);
+          if (st.nf == 0) break;
+          continue;
+        }
       }
       if (wt == 0 || wt > (unsigned)MAXT) {  // never produced by the host or the steps
         if (lane == 0) atomicOr(&a.ctl->error, 8u);
@@ -687,7 +760,21 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
                                                                stack, lane, acc);
       free_blocks(L, st);
     }
-    if (a.steal && !failed && lane == 0) atomicSub(&a.ctl->pending, 1ull);  // task t is done
+    if (a.steal && !failed) {  // task t is done
+      unsigned long long left = 0;
+      if (lane == 0) left = atomicSub(&a.ctl->pending, 1ull);
+      left = uni64(bcast64(left, 0));
+      if (left == 1) {
+        // the last task: nothing can be spilled any more, so the tail is final and every
+        // ticket at or past it is dead; each wave holds at most one, so nwaves flags cover them
+        unsigned long long tail = 0;
+        if (lane == 0) tail = (unsigned long long)a.n_in + ld_agent(&a.ctl->n_out);
+        tail = uni64(bcast64(tail, 0));
+        for (unsigned long long k = lane; k < (unsigned long long)a.nwaves; k += 64)
+          if (tail + k < (unsigned long long)a.out_cap)
+            atomicExch(&a.ready[tail + k - a.n_in], a.epoch ^ kDone);
+      }
+    }
   }
   // flush: wave reduction of the digest terms, per-depth counts from LDS
   for (int off = 32; off; off >>= 1) {

@@ -24,7 +24,6 @@ struct DeepCtl {  // per-round control + accumulated results (zeroed once per ca
   unsigned long long n_out;       // tasks spilled to the out queue (zeroed per round)
   unsigned long long heap_top;    // bytes of the out heap used (zeroed per round)
   unsigned long long pending;     // steal mode: queued + running tasks (0 = the launch is done)
-  unsigned long long idle;        // steal mode: waves waiting for a task
   unsigned long long digest_sum, digest_xor;
   unsigned long long candidates, chunks;
   unsigned long long per_depth[64];
@@ -54,9 +53,11 @@ struct DeepArgs {
   // and published by ready[k] = epoch; waves that run out of tasks wait for them, and a busy
   // wave spills its frames when it sees a waiting wave (checked every `budget` passes)
   unsigned* ready;
-  unsigned epoch;
+  unsigned* req;                  // [nwaves] mailboxes: epoch = a waiting wave asks for work
+  long long nwaves;
+  unsigned epoch;                 // < 2^31
   int steal;
-  unsigned steal_idle;            // spill when at least this many waves wait (0: always, tests)
+  int steal_eager;                // hand over at every check, asked or not (tests)
 };
 int deep_max_words();
 int deep_tier(int words);     // smallest instantiated block width >= words

@@ -76,7 +76,7 @@ def test_deep_work_stealing(gpu_mod, budget, split_min, steal_idle):
     (tens of thousands of in-launch hand-offs through the ready flags)."""
     tx = generate("ds1", seed=0)
     d = _gpu_miner(gpu_mod, tx).mine_deep(0.04, budget=budget, split_min=split_min,
-                                          steal_idle=steal_idle)
+                                          steal=True, steal_idle=steal_idle)
     assert len(d["round_tasks"]) == 1
     if steal_idle == 0:
         assert d["spilled_tasks"] > 0
