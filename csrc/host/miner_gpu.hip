@@ -21,6 +21,7 @@
 
 #include "../kernels/kernels.hpp"
 #include "kmls/gpu.hpp"
+#include "kmls/hooks.hpp"
 #include "kmls/trace.hpp"
 
 #define KMLS_HIP(expr)                                                                  \
@@ -203,57 +204,22 @@ struct Event {
 
 constexpr int64_t kCandCap = 32ll << 20;  // candidates per chunk
 
-// Host wait for a stream: hipStreamSynchronize, or a hipStreamQuery busy-poll with
-// KMLS_SPIN_SYNC=1 (measured: no gain on the headline step, so off by default).
-void sync_stream(hipStream_t s) {
-  static const bool spin = [] {
-    const char* e = std::getenv("KMLS_SPIN_SYNC");
-    return e && e[0] == '1';
-  }();
-  if (!spin) {
-    KMLS_HIP(hipStreamSynchronize(s));
-    return;
-  }
-  hipError_t e;
-  while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
-  }
-  if (e != hipSuccess) KMLS_HIP(e);
-}
+// Host wait for a stream (a hipStreamQuery busy-poll measured no gain on the headline step).
+void sync_stream(hipStream_t s) { KMLS_HIP(hipStreamSynchronize(s)); }
 
-// streamed-download mode of the fused levels: "deferred" (default) = each count launch carries
-// copy blocks that move the previous level's nodes to the host while its tiles compute;
-// "inline" = survivors are written to the host by the tile blocks themselves (every launch
-// then waits for its own PCIe writes to drain)
-bool deferred_dl() {
-  static const bool v = [] {
-    const char* e = std::getenv("KMLS_DL_MODE");
-    return !(e && std::string(e) == "inline");
-  }();
-  return v;
-}
+// streamed download of the fused levels: each count launch carries copy blocks that move the
+// previous level's nodes to the host while its tiles compute (writing survivors to the host
+// from the tile blocks themselves made every launch wait for its own PCIe writes: measured
+// slower)
+bool deferred_dl() { return true; }
 size_t fused_bump_cap(size_t bytes);
 
-// deferred-download copy blocks per count launch (KMLS_COPY_BLOCKS, default kern::kCopyBlocks)
-// KMLS_GRAM_POPCOUNT=1: long rows too use the VALU popcount gram (A/B against the MFMA gram)
-bool gram_popcount_forced() {
-  const char* e = std::getenv("KMLS_GRAM_POPCOUNT");
-  return e && e[0] == '1';
-}
-bool copy_last() {  // KMLS_COPY_LAST=1: copy blocks at the end of the grid (A/B)
-  static const bool v = [] {
-    const char* e = std::getenv("KMLS_COPY_LAST");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-int copy_blocks() {
-  static const int v = [] {
-    const char* e = std::getenv("KMLS_COPY_BLOCKS");
-    const int n = e ? std::atoi(e) : 0;
-    return n > 0 ? std::min(n, 1024) : kern::kCopyBlocks;
-  }();
-  return v;
-}
+// long rows use the MFMA gram (the VALU popcount gram only below its crossover)
+bool gram_popcount_forced() { return false; }
+// deferred-download copy blocks per count launch, at the start of the grid (placing them at
+// the end measured no faster)
+bool copy_last() { return false; }
+int copy_blocks() { return kern::kCopyBlocks; }
 
 struct MineRun {
   hipEvent_t wait_ev = nullptr;  // set: wait for this event instead of the stream (a call was
@@ -643,18 +609,13 @@ struct MineRun {
   }
 };
 
-size_t fused_bump_cap(size_t bytes) {  // KMLS_FUSED_BUMP_MB: test knob forcing the fallback
-  if (const char* e = std::getenv("KMLS_FUSED_BUMP_MB")) {
-    const double mb = std::atof(e);
-    if (mb > 0) return std::min(bytes, (size_t)(mb * (1 << 20)));
-  }
-  return bytes;
+size_t fused_bump_cap(size_t bytes) {  // test hook fused_bump_mb: forces the chunked fallback
+  const long long mb = test_hook("fused_bump_mb", 0);
+  return mb > 0 ? std::min(bytes, (size_t)mb << 20) : bytes;
 }
 
-bool fused_levels_enabled() {
-  const char* e = std::getenv("KMLS_FUSED_LEVELS");
-  return !(e && e[0] == '0');
-}
+// test hook fused_levels=0: the chunked level path (the fallback of an overflowing fused call)
+bool fused_levels_enabled() { return test_hook("fused_levels", 1) != 0; }
 
 size_t default_arena_bytes() {
   size_t free_b = 0, total_b = 0;
@@ -663,10 +624,8 @@ size_t default_arena_bytes() {
     const double gb = std::atof(e);
     if (gb > 0) return std::min(free_b - (free_b >> 4), (size_t)(gb * (1ull << 30)));
   }
-  if (const char* e = std::getenv("KMLS_ARENA_INIT_MB")) {  // initial size of a growing arena
-    const double mb = std::atof(e);
-    if (mb > 0) return std::min(free_b / 2, (size_t)(mb * (1 << 20)));
-  }
+  if (const long long mb = test_hook("arena_init_mb", 0))  // initial size of a growing arena
+    return std::min(free_b / 2, (size_t)mb << 20);
   // 8 GiB by default: hipMalloc maps HBM eagerly (~10 ms/GiB), and a job's one-shot mining
   // call should not pay for half of a 288 GB card.  The arena grows on demand (grow_arena) up to
   // half of the free HBM (the other half stays with torch / RCCL buffers).
@@ -691,7 +650,8 @@ float elapsed(const Event& a, const Event& b) {
 // The captured launch sequence of the last steady-state resident call (see mine_resident).
 // Two executable instances of the captured call: consecutive launches alternate between them,
 // so a call launched ahead (prefetch) is never a relaunch of the exec that is still running
-// (KMLS_GRAPH_TWIN=1; off by default until measured on the GPU).
+// (measured no faster than one instance on the headline, profiles/r2_s15_graph_interleaved.log:
+// off).
 struct GraphCache {
   std::vector<uint64_t> key;
   hipGraphExec_t exec = nullptr;
@@ -721,13 +681,7 @@ struct GraphCache {
   }
 };
 
-static bool graph_twin_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("KMLS_GRAPH_TWIN");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+static bool graph_twin_enabled() { return false; }
 
 // A steady-state resident call launched ahead (mine(prefetch=true)): its graph replay is on the
 // stream behind the call that launched it, writing to its own pinned buffers.  The next
@@ -766,7 +720,7 @@ GpuMiner::GpuMiner(int device, size_t arena_bytes, uintptr_t stream) : device_(d
   hipDeviceProp_t prop;
   KMLS_HIP(hipGetDeviceProperties(&prop, device));
   n_cus_ = std::max(1, prop.multiProcessorCount);
-  if (const char* e = std::getenv("KMLS_IDX_CAP")) idx_cap_ = std::max(16ll, std::atoll(e));  // test knob
+  if (const long long c = test_hook("idx_cap", 0)) idx_cap_ = std::max(16ll, c);
 }
 
 GpuMiner::~GpuMiner() {
@@ -780,8 +734,6 @@ GpuMiner::~GpuMiner() {
   if (d_fmask_) (void)hipFree(d_fmask_);
   if (d_fgroup_) (void)hipFree(d_fgroup_);
   if (d_c2r_) (void)hipFree(d_c2r_);
-  if (d_lk_mask_) (void)hipFree(d_lk_mask_);
-  if (d_lk_hash_) (void)hipFree(d_lk_hash_);
   if (d_ids_) (void)hipFree(d_ids_);
   if (d_own_bm_) (void)hipFree(d_own_bm_);
   if (h_scalar_) (void)hipHostFree(h_scalar_);
@@ -811,14 +763,10 @@ size_t GpuMiner::arena_capacity() const { return arena_->capacity(); }
 
 // Per-item supports (accumulated into `counts`): the partitioned histogram for large
 // vocabularies and inputs (kern::item_support_partitioned, scratch owned by the miner), else the
-// LDS/hash kernels.  KMLS_SUPPORT_PARTITIONED=0 forces the latter (A/B).
+// LDS/hash kernels.
 void GpuMiner::support_counts(const int32_t* items, int64_t nnz, uint32_t* counts, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  static const bool partitioned = [] {
-    const char* e = std::getenv("KMLS_SUPPORT_PARTITIONED");
-    return !(e && e[0] == '0');
-  }();
-  const size_t need = partitioned && nnz >= (4ll << 20) ? kern::support_scratch_bytes(nnz, n_items_) : 0;
+  const size_t need = nnz >= (4ll << 20) ? kern::support_scratch_bytes(nnz, n_items_) : 0;
   if (need) {
     if (need > sup_scratch_bytes_) {
       if (sup_scratch_) KMLS_HIP(hipFree(sup_scratch_));
@@ -974,15 +922,8 @@ void GpuMiner::build_encode_tables(int64_t F) {
   if (d_c2r_) KMLS_HIP(hipFree(d_c2r_));
   d_fgroup_ = nullptr;
   d_c2r_ = nullptr;
-  lk_valid_ = false;
   if (!d_fmask_ || F <= 0 || F > kern::kEncodeGroupMaxF) return;
   hipStream_t s = (hipStream_t)stream_;
-  if (F <= kern::kEncodeLookupMaxF && n_items_ <= (1 << 21)) {
-    if (!d_lk_mask_) KMLS_HIP(hipMalloc((void**)&d_lk_mask_, kern::kEncodeLookupMaskBits / 8));
-    if (!d_lk_hash_) KMLS_HIP(hipMalloc((void**)&d_lk_hash_, kern::kEncodeLookupSlots * 4));
-    kern::encode_lookup_build(d_ids_, F, n_items_, d_lk_mask_, d_lk_hash_, s);
-    lk_valid_ = true;
-  }
   const int64_t G = (n_items_ + 31) / 32;
   KMLS_HIP(hipMalloc((void**)&d_fgroup_, (size_t)G * 8));
   KMLS_HIP(hipMalloc((void**)&d_c2r_, (size_t)F * 4));
@@ -1029,24 +970,16 @@ int64_t GpuMiner::words_local() const {
 
 bool GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_off) {
   KMLS_HIP(hipSetDevice(device_));
-  // long shards: LDS-slab encode (KMLS_ENCODE_TILED=0 keeps the atomic kernel, for A/B)
-  const char* te = std::getenv("KMLS_ENCODE_TILED");
-  const bool tiled = !(te && te[0] == '0');
+  // long shards: LDS-slab encode (test hook encode_tiled=0: the atomic kernel of short shards)
+  const bool tiled = test_hook("encode_tiled", 1) != 0;
   const int64_t F = (int64_t)fi_.ids.size();
-  const char* me = std::getenv("KMLS_ENCODE_MASK");  // =0: no frequent-item mask (A/B)
-  const uint32_t* fmask = (me && me[0] == '0') ? nullptr : d_fmask_;
-  const char* ge = std::getenv("KMLS_ENCODE_GROUP");  // =0: mask + rank gathers (A/B)
-  const bool grp = fmask && !(ge && ge[0] == '0');
-  // KMLS_ENCODE_LOOKUP=lds: LDS mask + hash tables instead of the 8-byte group gather (A/B:
-  // 20.5 vs 13.2 ms at 100M x 754 frequent items, profiles/r2_s8_encode_materialize.md)
-  const char* le = std::getenv("KMLS_ENCODE_LOOKUP");
-  const bool lk = grp && lk_valid_ && le && std::string(le) == "lds";
+  // frequent-item mask ahead of the rank gather, and (F <= 2048) the 8-byte group gather (an LDS
+  // mask + hash lookup measured slower: 20.5 vs 13.2 ms at 100M x 754 frequent items)
+  const uint32_t* fmask = d_fmask_;
   if (tiled && n_tx_ >= (1 << 16) &&
       kern::encode_bitmap_tiled(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev,
-                                Wp_total, word_off, F, (hipStream_t)stream_, fmask,
-                                grp ? d_fgroup_ : nullptr, grp ? d_c2r_ : nullptr,
-                                lk ? d_lk_mask_ : nullptr, lk ? d_lk_hash_ : nullptr,
-                                kern::encode_lookup_shift(n_items_)))
+                                Wp_total, word_off, F, (hipStream_t)stream_, fmask, d_fgroup_,
+                                d_c2r_))
     return true;
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev, Wp_total,
                       word_off, (hipStream_t)stream_, fmask);
@@ -1058,8 +991,7 @@ bool GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_o
 // cleared — at 100M transactions a full memset was a 9 GB write ahead of a 9 GB encode.
 void GpuMiner::encode_bitmaps_fresh(uint64_t* bm, int64_t F, int64_t Wp) {
   hipStream_t s = (hipStream_t)stream_;
-  const char* te = std::getenv("KMLS_ENCODE_TILED");
-  const bool tiled = !(te && te[0] == '0') && n_tx_ >= (1 << 16) && F > 0 &&
+  const bool tiled = test_hook("encode_tiled", 1) != 0 && n_tx_ >= (1 << 16) && F > 0 &&
                      F <= kern::kEncodeTileMaxF;
   const int64_t used = (n_tx_ + 63) / 64;
   if (!tiled) {
@@ -1079,7 +1011,7 @@ void GpuMiner::pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev
   hipStream_t s = (hipStream_t)stream_;
   KMLS_HIP(hipMemsetAsync((void*)out_dev, 0, (size_t)F * F * sizeof(uint32_t), s));
   if (use_mfma)
-    kern::pair_gram_mfma_i8((const uint64_t*)bm_dev, Wp_total, F, (uint32_t*)out_dev, s);
+    kern::pair_gram_mfma((const uint64_t*)bm_dev, Wp_total, F, (uint32_t*)out_dev, s);
   else
     kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp_total, F, (uint32_t*)out_dev, s);
 }
@@ -1312,7 +1244,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       KMLS_HIP(hipMemsetAsync(gram, 0, (size_t)F * F * sizeof(uint32_t), s));
       // matrix cores for long rows (large T): the int8 MFMA path moves 8x more MACs per byte
       if (gram_popcount_forced() ? cfg.level2_mfma : (cfg.level2_mfma || Wp >= 4096))
-        kern::pair_gram_mfma_i8((const uint64_t*)bm_dev, Wp, F, gram, s);
+        kern::pair_gram_mfma((const uint64_t*)bm_dev, Wp, F, gram, s);
       else
         kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);
       if (comm_) comm_->all_reduce(gram, gram, (size_t)F * F, CommDtype::U32, false, s);
@@ -1487,10 +1419,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     run.host_cap = std::max<int64_t>({I * 8, (int64_t)1 << 16, last_nodes_ + (last_nodes_ >> 3)});
     // compact element widths (kernels.hpp HostTrie): the download is PCIe-bound on the
     // headline shape (0.25 ms of 1.1 ms at 17 B/itemset)
-    static const bool compact = [] {
-      const char* e = std::getenv("KMLS_COMPACT_DL");
-      return !(e && e[0] == '0');
-    }();
+    constexpr bool compact = true;
     const int pw = compact && run.host_cap < (int64_t)INT32_MAX ? 4 : 8;
     const int iw = compact && I <= 65536 ? 2 : 4;
     const int cw = compact && n_tx_ <= 65535 ? 2 : 4;
@@ -1581,15 +1510,11 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   const bool fused_select = I <= kern::kSelectFusedMax;
   // The call's launches (prologue + the first batch of levels) are invariant once the data,
   // configuration, buffers and per-level launch plan repeat: they are captured once as a
-  // hipGraph and replayed (KMLS_GRAPH=0 disables), which takes ~35 kernel launches off the
-  // host path of every steady-state call.  All per-call state reaches the kernels through the
-  // pinned parameter block read by the init kernel.
-  static const bool graphs = [] {
-    const char* e = std::getenv("KMLS_GRAPH");
-    return !(e && e[0] == '0');
-  }();
+  // hipGraph and replayed, which takes ~35 kernel launches off the host path of every
+  // steady-state call (level tracing runs uncaptured).  All per-call state reaches the kernels
+  // through the pinned parameter block read by the init kernel.
   static const bool tracing = std::getenv("KMLS_LEVEL_TRACE") != nullptr;
-  const bool use_graph = graphs && fused_select && !tracing;
+  const bool use_graph = fused_select && !tracing;
   std::vector<uint64_t> key;
   if (use_graph) {
     auto u = [](const void* p) { return (uint64_t)(uintptr_t)p; };
@@ -1620,11 +1545,8 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   // nodes created before the levels' the level branch started ~44 µs after the gram (the
   // profiled step timeline, profiles/r2_s12_ds1_step_timeline.md); creating them last lets the
   // root level start right behind the gram: 0.2566 -> 0.2485 ms/step (medians of 4 interleaved
-  // runs, profiles/r2_s15_graph_interleaved.log).  KMLS_RULEMAP_LATE=0: the old order (A/B)
-  static const bool rulemap_late = [] {
-    const char* e = std::getenv("KMLS_RULEMAP_LATE");
-    return !(e && e[0] == '0');
-  }();
+  // runs, profiles/r2_s15_graph_interleaved.log)
+  constexpr bool rulemap_late = true;
   bool pairs_pending = false;
   auto enqueue_prologue = [&]() {
     kern::level_prologue_init(d_cnt, I, d_own_bm_, (int64_t)(need / 8), d_desc, kMaxLv, d_ctl,
@@ -1979,10 +1901,9 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
   // 1. supports in K tiles; tile k's all-reduce (comm stream) overlaps tile k+1's histogram.
   //    The comm stream and the tile events live as long as the miner (no per-call creation).
   //    One rank has no all-reduce to overlap: one tile, so the partitioned histogram's fixed
-  //    per-pass costs (per-block bin flushes, scans) are paid once (KMLS_SUPPORT_TILES forces K).
+  //    per-pass costs (per-block bin flushes, scans) are paid once.
   int K = std::max(1, std::min(64, support_tiles));
   if (!comm || comm->world() <= 1) K = 1;
-  if (const char* te = std::getenv("KMLS_SUPPORT_TILES")) K = std::max(1, std::min(64, std::atoi(te)));
   const size_t vec = (size_t)std::max<int64_t>(n_items_, 1) * sizeof(uint32_t);
   uint32_t* d_part = (uint32_t*)arena_->push(vec * K);
   KMLS_HIP(hipMemsetAsync(d_part, 0, vec * K, s));
@@ -2009,11 +1930,8 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
   // the selection (rank by support over up to millions of items) runs on the host: one 4 B/item
   // readback per call, the same on every rank
   // 2. selection from the global supports (identical on every rank), on the device: only the
-  //    frequent ids/counts come back (KMLS_SELECT_DEVICE=0: the host path, A/B)
-  static const bool dev_select = [] {
-    const char* e = std::getenv("KMLS_SELECT_DEVICE");
-    return !(e && e[0] == '0');
-  }();
+  //    frequent ids/counts come back
+  constexpr bool dev_select = true;
   int64_t F;
   if (dev_select) {
     F = select_device(d_part, global_n_tx, cfg.min_support, comm);

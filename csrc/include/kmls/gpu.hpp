@@ -144,12 +144,15 @@ struct DeepBufsDeleter {
 // content digest (kmls/digest.hpp; equal to trie_digest of the full trie) without a trie.
 struct DeepOpts {
   // (defaults: the best of the r3e sweep at ds1 @0.02, profiles/r3_deep_sweep_projected.log)
-  unsigned long long budget0 = 1024;  // 64-lane passes a first-round task may take before spilling
-  unsigned long long budget = 1024;   // ... in later rounds
+  unsigned long long budget0 = 1024;  // rounds: 64-lane passes a first-round task may take
+  unsigned long long budget = 256;    // steal: passes between mailbox checks (the r3j sweep:
+                                      // 50.0 ms at ds1 @0.02 vs 59.9 for the best rounds setting,
+                                      // 8-rank split 13.4 vs 18.1 ms); rounds: later-round budget
+                                      // (1024 there)
   unsigned split_min = 8;             // spilled frames above this many members split per member
   int blocks_per_cu = 0;              // 0 = the kernel instance's occupancy (deep_waves_per_simd)
   int stack_mb = 0;                   // per-wave stack (0: KMLS_DEEP_STACK_MB or 4)
-  bool steal = false;                 // one launch, spills taken by waiting waves (budget =
+  bool steal = true;                  // one launch, spills taken by waiting waves (budget =
                                       // passes between checks for a waiting wave); false =
                                       // spill rounds (budget0/budget = per-task step budgets)
   unsigned steal_idle = 1;            // steal: 1 = hand over when a waiting wave asks; 0 = at
@@ -276,9 +279,6 @@ class GpuMiner {
   uint32_t* d_fmask_ = nullptr;  // frequent-item bit mask (large vocabularies, select())
   unsigned long long* d_fgroup_ = nullptr;  // encode tables (kern::frequent_groups)
   int32_t* d_c2r_ = nullptr;
-  uint32_t* d_lk_mask_ = nullptr;  // encode LDS lookup tables (kern::encode_lookup_build)
-  uint32_t* d_lk_hash_ = nullptr;
-  bool lk_valid_ = false;
   void build_encode_tables(int64_t F);
   int32_t* d_ids_ = nullptr;
   uint64_t* d_own_bm_ = nullptr;  // single-GPU bitmap buffer

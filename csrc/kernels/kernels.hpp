@@ -99,21 +99,7 @@ constexpr int64_t kEncodeTileMaxF = 1 << 20;  // row bands past one LDS slab
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
                          int64_t F, hipStream_t s, const uint32_t* fmask = nullptr,
-                         const unsigned long long* fgroup = nullptr, const int32_t* c2r = nullptr,
-                         const uint32_t* lk_mask = nullptr, const uint32_t* lk_hash = nullptr,
-                         int lk_shift = 0);
-// LDS lookup tables (encode_lookup_build; F < kEncodeLookupMaxF, n_items < 2^21): a coarse
-// frequent mask of kEncodeLookupMaskBits bits (bit b: some frequent id has id >> lk_shift == b)
-// and an open-addressing hash of kEncodeLookupSlots packed (id << 11 | rank) words.  Both are
-// staged in LDS per tile, so an item costs one LDS bit test and (frequent or bucket-mate) a
-// short probe, instead of a random 8-byte gather from L2.  A/B only (KMLS_ENCODE_LOOKUP=lds):
-// measured slower than the L2 gather (20.5 vs 13.2 ms at 100M).
-constexpr int64_t kEncodeLookupMaxF = 2047;
-constexpr int64_t kEncodeLookupMaskBits = 65536;
-constexpr int64_t kEncodeLookupSlots = 4096;
-int encode_lookup_shift(int64_t n_items);
-void encode_lookup_build(const int32_t* ids, int64_t F, int64_t n_items, uint32_t* mask,
-                         uint32_t* hash, hipStream_t s);
+                         const unsigned long long* fgroup = nullptr, const int32_t* c2r = nullptr);
 // fgroup/c2r (frequent_groups; used when F <= kEncodeGroupMaxF): one 8-byte gather per item
 // instead of the mask gather followed by the rank gather
 constexpr int64_t kEncodeGroupMaxF = 2048;
@@ -169,7 +155,7 @@ void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off,
 // copied by a grid over (survivor, slice) pairs sized by n_surv, not over all candidates
 // dense upper-triangular pair counts over a single class of F rows (level 2 bit-GEMM)
 void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
-void pair_gram_mfma_i8(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
+void pair_gram_mfma(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
 // same with F read from the device (grid and row stride sized for F_max)
 void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, int64_t F_max,
                             uint32_t* out, hipStream_t s);

@@ -1416,19 +1416,9 @@ int team_size_for(int64_t Wp) {  // lanes per candidate: ~4-8 16-byte chunks per
 
 int level_grid(int n_cus) { return std::max(64, n_cus * 8); }  // 8 x 256-thread blocks per CU
 
-namespace {
-bool small_rows_ok() {
-  static const bool ok = [] {
-    const char* e = std::getenv("KMLS_COUNT_SMALL");
-    return !(e && e[0] == '0');
-  }();
-  return ok;
-}
-}  // namespace
-
 bool level_rows_interleaved(int64_t Wp) {
   const int64_t n2 = Wp >> 1;
-  return small_rows_ok() && n2 >= 1 && n2 <= kSmallChunks;
+  return n2 >= 1 && n2 <= kSmallChunks;
 }
 
 void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, unsigned epoch,
@@ -1439,16 +1429,8 @@ void level_count(FLevel* lv, FLevel* nx, FCtl* ctl, unsigned long long* status, 
   if (level_rows_interleaved(a.Wp)) {
     // a level expected to be small (the previous call's size: steady-state re-mining) is
     // latency-bound: load each candidate's whole row pair in one batch
-    static const bool kb18 = [] {
-      const char* e = std::getenv("KMLS_KB18");
-      return !(e && e[0] == '0');
-    }();
-    // KMLS_KB18_TILES: A/B knob for the size bound of the one-batch variant (default 64 tiles)
-    static const int64_t kb18_tiles = [] {
-      const char* e = std::getenv("KMLS_KB18_TILES");
-      return e ? std::atoll(e) : (int64_t)64;
-    }();
-    if (kb18 && cand_hint >= 0 && cand_hint <= kb18_tiles * kTile && n2 <= 18)
+    constexpr int64_t kb18_tiles = 64;  // size bound of the one-batch variant
+    if (cand_hint >= 0 && cand_hint <= kb18_tiles * kTile && n2 <= 18)
       hipLaunchKernelGGL(k_level_count_small<18>, dim3(grid), dim3(kBlock), 0, s, lv, nx, ctl,
                          status, epoch, a, tile_row, tile_row_nx);
     else

@@ -21,6 +21,7 @@
 #include <string>
 
 #include "kernels.hpp"
+#include "kmls/hooks.hpp"
 
 #define KMLS_HIP(expr)                                                                  \
   do {                                                                                  \
@@ -283,44 +284,6 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(const int32_t* __restri
   }
 }
 
-__global__ __launch_bounds__(1024) void k_part_count(const uint16_t* __restrict__ part,
-                                                     const int64_t* __restrict__ off, int G,
-                                                     int M, int64_t n_items,
-                                                     uint32_t* __restrict__ counts) {
-  __shared__ uint32_t h[kPartBins];
-  const int p = blockIdx.x / M, m = blockIdx.x % M;
-  for (int i = threadIdx.x; i < kPartBins; i += blockDim.x) h[i] = 0;
-  __syncthreads();
-  const int64_t s0 = off[(int64_t)p * G], s1 = off[(int64_t)(p + 1) * G];
-  const int64_t len = s1 - s0, sl = (len + M - 1) / M;
-  const int64_t a = s0 + min(len, (int64_t)m * sl), b = s0 + min(len, (int64_t)(m + 1) * sl);
-  // 16-byte loads (8 ids) over the aligned body: more loads in flight than one 2-byte id per
-  // thread per iteration
-  const int64_t head = ((8 - (int64_t)(((uintptr_t)(part + a) >> 1) & 7)) & 7);
-  const int64_t a0 = min(b, a + head);
-  for (int64_t i = a + threadIdx.x; i < a0; i += blockDim.x) atomicAdd(&h[part[i]], 1u);
-  const uint4* __restrict__ v = reinterpret_cast<const uint4*>(part + a0);
-  const int64_t n8 = (b - a0) >> 3;
-  for (int64_t j = threadIdx.x; j < n8; j += blockDim.x) {
-    const uint4 x = v[j];
-    atomicAdd(&h[x.x & 0xFFFFu], 1u);
-    atomicAdd(&h[x.x >> 16], 1u);
-    atomicAdd(&h[x.y & 0xFFFFu], 1u);
-    atomicAdd(&h[x.y >> 16], 1u);
-    atomicAdd(&h[x.z & 0xFFFFu], 1u);
-    atomicAdd(&h[x.z >> 16], 1u);
-    atomicAdd(&h[x.w & 0xFFFFu], 1u);
-    atomicAdd(&h[x.w >> 16], 1u);
-  }
-  for (int64_t i = a0 + (n8 << 3) + threadIdx.x; i < b; i += blockDim.x) atomicAdd(&h[part[i]], 1u);
-  __syncthreads();
-  const int64_t id0 = (int64_t)p << kPartBits;
-  for (int i = threadIdx.x; i < kPartBins; i += blockDim.x) {
-    const uint32_t val = h[i];
-    if (val && id0 + i < n_items) atomicAdd(&counts[id0 + i], val);
-  }
-}
-
 // Pass 3, balanced: every block takes an equal slice of the whole partition-major id array, so
 // a partition holding a Zipf head item (its partition is ~1.6x the mean length) gets
 // proportionally more blocks; a slice that straddles a boundary histograms each partition in
@@ -407,25 +370,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_bitmap(const int64_t* __restr
 // transaction found by binary search over the tile's LDS copy of tx_ptr.  More frequent rows than
 // one slab holds (config 5: ~15k) split into row bands, one block per (tile, band) with the band
 // index fastest, so a tile's bands run together and re-read its items from L2, not HBM.
-// encode LDS lookup tables (kernels.hpp: encode_lookup_build): coarse mask + packed hash
-static_assert(kEncodeLookupSlots == 4096, "the probe start is the top 12 bits of the hash");
-__global__ __launch_bounds__(kBlock) void k_encode_lookup_build(const int32_t* __restrict__ ids,
-                                                                int64_t F, int shift,
-                                                                uint32_t* __restrict__ mask,
-                                                                uint32_t* __restrict__ hash) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= F) return;
-  const uint32_t id = (uint32_t)ids[r];
-  const uint32_t b = id >> shift;
-  atomicOr(&mask[b >> 5], 1u << (b & 31));
-  const uint32_t v = (id << 11) | (uint32_t)r;
-  uint32_t slot = (id * 0x9E3779B1u) >> 20;
-  // F < slots / 2: an empty slot is always found
-  while (atomicCAS(&hash[slot], 0xFFFFFFFFu, v) != 0xFFFFFFFFu)
-    slot = (slot + 1) & (uint32_t)(kEncodeLookupSlots - 1);
-}
-
-template <int kEncodeU>
+constexpr int kEncodeU = 8;  // items per thread per round (16 measured no faster)
 __global__ __launch_bounds__(1024) void k_encode_tile(const int64_t* __restrict__ tx_ptr,
                                                         const int32_t* __restrict__ items,
                                                         int64_t n_tx,
@@ -437,10 +382,7 @@ __global__ __launch_bounds__(1024) void k_encode_tile(const int64_t* __restrict_
                                                         bool xcd_order,
                                                         const unsigned long long* __restrict__ fgroup,
                                                         const int32_t* __restrict__ c2r,
-                                                        int txmap_cap,
-                                                        const uint32_t* __restrict__ lk_mask,
-                                                        const uint32_t* __restrict__ lk_hash,
-                                                        int lk_shift) {
+                                                        int txmap_cap) {
   // [band rows][TW], then tx_ptr[64*TW + 1], then (fgroup path) c2r[F], then (txmap_cap > 0)
   // the tile's item-position -> local-transaction map, one byte per item
   extern __shared__ unsigned long long s_bm[];
@@ -468,16 +410,6 @@ __global__ __launch_bounds__(1024) void k_encode_tile(const int64_t* __restrict_
   if (fgroup)
     for (int i = threadIdx.x; i < (int)F; i += blockDim.x) s_c2r[i] = c2r[i];
   uint8_t* s_tx = (uint8_t*)(s_c2r + (fgroup ? F : 0));
-  uint32_t* s_lkm = (uint32_t*)(((uintptr_t)(s_tx + txmap_cap) + 15) & ~(uintptr_t)15);
-  uint32_t* s_lkh = s_lkm + kEncodeLookupMaskBits / 32;
-  if (lk_hash) {
-    const uint4* m4 = reinterpret_cast<const uint4*>(lk_mask);
-    const uint4* h4 = reinterpret_cast<const uint4*>(lk_hash);
-    for (int i = threadIdx.x; i < (int)(kEncodeLookupMaskBits / 128); i += blockDim.x)
-      reinterpret_cast<uint4*>(s_lkm)[i] = m4[i];
-    for (int i = threadIdx.x; i < (int)(kEncodeLookupSlots / 4); i += blockDim.x)
-      reinterpret_cast<uint4*>(s_lkh)[i] = h4[i];
-  }
   __syncthreads();
   const int64_t p0 = s_ptr[0], p1 = s_ptr[nt];
   // item -> transaction without a per-item binary search (8 dependent LDS reads for 256
@@ -510,27 +442,7 @@ __global__ __launch_bounds__(1024) void k_encode_tile(const int64_t* __restrict_
       nx[u] = p < p1 ? items[p] : -1;
     }
     int32_t rk[kEncodeU];
-    if (lk_hash) {
-      // coarse LDS bit test, then (frequent ids and their bucket mates only) a linear probe of
-      // the LDS hash: no global gather per item
-#pragma unroll
-      for (int u = 0; u < kEncodeU; ++u) {
-        rk[u] = -1;
-        if (it[u] < 0) continue;
-        const uint32_t b = (uint32_t)it[u] >> lk_shift;
-        if (!((s_lkm[b >> 5] >> (b & 31)) & 1u)) continue;
-        uint32_t slot = ((uint32_t)it[u] * 0x9E3779B1u) >> 20;
-        for (;;) {
-          const uint32_t e = s_lkh[slot];
-          if (e == 0xFFFFFFFFu) break;
-          if ((e >> 11) == (uint32_t)it[u]) {
-            rk[u] = (int32_t)(e & 2047u) - r0;
-            break;
-          }
-          slot = (slot + 1) & (uint32_t)(kEncodeLookupSlots - 1);
-        }
-      }
-    } else if (fgroup) {
+    if (fgroup) {
       // one 8-byte gather per item: the frequent bits of its 32-id group and the number of
       // frequent ids before the group; the rank comes from the LDS compact-index → rank table
 #pragma unroll
@@ -1009,87 +921,41 @@ void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* 
   KMLS_HIP(hipGetLastError());
 }
 
-// Encode block size: the tile kernel is LDS-bound to 4 blocks per CU (37 KB slab + maps per
-// block) at 40 VGPRs, so more waves per block are more waves per CU on the same LDS: 512
-// threads measured 12.3 ms at 100M against 13.1 (256) and 15.9 (1024).  The multi-band kernel
-// stays at 256 (12.4 ms at config-5 10M vs 13.2 at 1024).  KMLS_ENCODE_BLOCK overrides (A/B)
-static unsigned encode_block(unsigned dflt) {
-  if (const char* e = std::getenv("KMLS_ENCODE_BLOCK")) {
-    const int v = std::atoi(e);
-    if (v == 256 || v == 512 || v == 1024) return (unsigned)v;
-  }
-  return dflt;
-}
-
-int encode_lookup_shift(int64_t n_items) {
-  int sh = 0;
-  while ((std::max<int64_t>(n_items, 1) - 1) >> sh >= kEncodeLookupMaskBits) ++sh;
-  return sh;
-}
-
-void encode_lookup_build(const int32_t* ids, int64_t F, int64_t n_items, uint32_t* mask,
-                         uint32_t* hash, hipStream_t s) {
-  KMLS_HIP(hipMemsetAsync(mask, 0, kEncodeLookupMaskBits / 8, s));
-  KMLS_HIP(hipMemsetAsync(hash, 0xFF, kEncodeLookupSlots * 4, s));
-  if (F <= 0) return;
-  if (F > kEncodeLookupMaxF || n_items > (1 << 21))
-    throw std::runtime_error("encode_lookup_build: F or n_items out of range");
-  hipLaunchKernelGGL(k_encode_lookup_build, dim3((unsigned)((F + kBlock - 1) / kBlock)), dim3(kBlock),
-                     0, s, ids, F, encode_lookup_shift(n_items), mask, hash);
-  KMLS_HIP(hipGetLastError());
-}
-
 bool encode_bitmap_tiled(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                          const int32_t* rank_of, uint64_t* bm, int64_t Wp, int64_t word_off,
                          int64_t F, hipStream_t s, const uint32_t* fmask,
-                         const unsigned long long* fgroup, const int32_t* c2r,
-                         const uint32_t* lk_mask, const uint32_t* lk_hash, int lk_shift) {
+                         const unsigned long long* fgroup, const int32_t* c2r) {
   if (n_tx <= 0 || F <= 0 || F > kEncodeTileMaxF) return false;
   // frequent sets wider than one slab: the multi-band kernel (one block per tile, every band;
-  // KMLS_ENCODE_MULTIBAND=0 keeps one block per (tile, band), A/B)
-  const char* mb = std::getenv("KMLS_ENCODE_MULTIBAND");
-  if (F > 1536 && F < (1 << 24) && !(mb && mb[0] == '0')) {
+  // 22.2 -> 11.7 ms at config-5 10M against one block per (tile, band)), 256 threads (12.4 ms
+  // vs 13.2 at 1024)
+  if (F > 1536 && F < (1 << 24)) {
     const int64_t tiles = (n_tx + 255) / 256;
     if (tiles > INT32_MAX) return false;
-    hipLaunchKernelGGL(k_encode_multiband, dim3((unsigned)tiles), dim3(encode_block(256)), 0, s,
+    hipLaunchKernelGGL(k_encode_multiband, dim3((unsigned)tiles), dim3(256), 0, s,
                        tx_ptr, items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, fmask);
     KMLS_HIP(hipGetLastError());
     return true;
   }
   if (F > kEncodeGroupMaxF) fgroup = nullptr, c2r = nullptr;  // c2r must fit LDS beside the slab
-  if (F > kEncodeLookupMaxF || !lk_mask) lk_hash = nullptr;
-  if (lk_hash) fgroup = nullptr, c2r = nullptr;
-  // words per tile: the slab within 48 KB of LDS.  TW = 4 words (32-byte row segments, the
-  // measured optimum); past 1536 rows, bands of 1536 rows (narrower segments would make the
-  // write-out scattered 8-byte stores).
+  // words per tile: the slab within 48 KB of LDS.  TW = 4 words (32-byte row segments: measured
+  // ahead of 8 and 2 at 100M x 754, 19.5 / 18.3 / 23.2 ms); XCD-aware tile order; the item ->
+  // transaction byte map sized for a tile of 256 transactions of up to 32 items on average
   constexpr int64_t kSlab = 48 * 1024;
-  int tw_log2 = 2;  // TW = 4: measured ahead of 8 and 2 at 100M x 754 (19.5 / 18.3 / 23.2 ms)
-  if (const char* e = std::getenv("KMLS_ENCODE_TW")) tw_log2 = std::max(0, std::min(3, std::atoi(e)));  // A/B
-  const char* xe = std::getenv("KMLS_ENCODE_XCD");  // =0: hardware block order (A/B)
-  const bool xcd = !(xe && xe[0] == '0');
+  const int tw_log2 = 2;
   const int64_t TW = 1ll << tw_log2;
   const int64_t band = std::min<int64_t>(F, kSlab / (8 * TW));
   const int64_t n_bands = (F + band - 1) / band;
-  // item -> transaction byte map (KMLS_ENCODE_TXMAP=0: per-item binary search, A/B): sized for
-  // a tile of 64*TW transactions of up to 32 items each on average
-  const char* me = std::getenv("KMLS_ENCODE_TXMAP");
-  const int txmap_cap = (tw_log2 <= 2 && !(me && me[0] == '0')) ? (int)(64 * TW * 32) : 0;
+  const int txmap_cap = (int)(64 * TW * 32);
   const size_t lds = (size_t)band * TW * 8 + (size_t)(64 * TW + 1) * 8 +
-                     (fgroup ? (size_t)F * 4 : 0) + (size_t)txmap_cap +
-                     (lk_hash ? (size_t)(16 + kEncodeLookupMaskBits / 8 + kEncodeLookupSlots * 4) : 0);
+                     (fgroup ? (size_t)F * 4 : 0) + (size_t)txmap_cap;
   const int64_t blocks = (n_tx + 64 * TW - 1) / (64 * TW) * n_bands;
   if (blocks > INT32_MAX) return false;
-  // items per thread per round (KMLS_ENCODE_U=16: twice the gathers in flight, A/B)
-  const char* ue = std::getenv("KMLS_ENCODE_U");
-  const unsigned eb = encode_block(512);
-  if (ue && std::atoi(ue) == 16)
-    hipLaunchKernelGGL(k_encode_tile<16>, dim3((unsigned)blocks), dim3(eb), lds, s, tx_ptr,
-                       items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2,
-                       (int)band, fmask, xcd, fgroup, c2r, txmap_cap, lk_mask, lk_hash, lk_shift);
-  else
-    hipLaunchKernelGGL(k_encode_tile<8>, dim3((unsigned)blocks), dim3(eb), lds, s, tx_ptr,
-                       items, n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2,
-                       (int)band, fmask, xcd, fgroup, c2r, txmap_cap, lk_mask, lk_hash, lk_shift);
+  // 512 threads: LDS-bound to 4 blocks per CU at 40 VGPRs, so more waves per block are more waves
+  // per CU on the same LDS (12.3 ms at 100M against 13.1 at 256 and 15.9 at 1024)
+  hipLaunchKernelGGL(k_encode_tile, dim3((unsigned)blocks), dim3(512), lds, s, tx_ptr, items,
+                     n_tx, rank_of, (unsigned long long*)bm, Wp, word_off, F, tw_log2, (int)band,
+                     fmask, true, fgroup, c2r, txmap_cap);
   KMLS_HIP(hipGetLastError());
   return true;
 }
@@ -1126,11 +992,8 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
   const int64_t P = ((int64_t)n_items + kPartBins - 1) / kPartBins;
   if (nnz <= 0 || P > kPartMax || scratch_bytes < support_scratch_bytes(nnz, n_items)) return false;
   // blocks of passes 1-2: 1024 = 4 resident blocks per CU (the scatter's 93 VGPRs allow 5);
-  // 1280 / 2048 measured no faster (support 8.73 / 8.62 vs 8.37 ms at 100M). KMLS_SUPPORT_GRID
-  // overrides (A/B)
-  int64_t G = kPartGrid;
-  if (const char* ge = std::getenv("KMLS_SUPPORT_GRID"))
-    G = std::max<int64_t>(64, std::min<int64_t>(kPartGridMax, std::atoll(ge)));
+  // 1280 / 2048 measured no faster (support 8.73 / 8.62 vs 8.37 ms at 100M)
+  const int64_t G = kPartGrid;
   const int64_t n = P * G;
   char* q = (char*)scratch;
   uint16_t* part = (uint16_t*)q;
@@ -1144,15 +1007,9 @@ bool item_support_partitioned(const int32_t* items, int64_t nnz, int32_t n_items
   exclusive_scan_i64(blk, off, n, q, tb, s);
   hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)G), dim3(kBlock), 0, s, items, nnz, (int)P, off,
                      part);
-  // pass 3: equal global slices (default) or KMLS_SUPPORT_COUNT=part, M blocks per partition
-  // (A/B; 8.79 vs 8.70 ms support at 100M x 1M)
-  const char* ce = std::getenv("KMLS_SUPPORT_COUNT");
-  if (ce && std::string(ce) == "part") {
-    const int M = (int)std::max<int64_t>(1, (512 + P - 1) / P);
-    hipLaunchKernelGGL(k_part_count, dim3((unsigned)(P * M)), dim3(1024), 0, s, part, off,
-                       (int)G, M, (int64_t)n_items, counts);
-  } else {
-    // one 128 KB-LDS block per CU: 512 equal slices = 2 rounds over the 256 CUs
+  // pass 3: equal global slices, one 128 KB-LDS block per CU: 512 slices = 2 rounds over the
+  // 256 CUs (per-partition blocks measured 8.79 vs 8.70 ms support at 100M x 1M)
+  {
     const unsigned B = (unsigned)std::min<int64_t>(512, std::max<int64_t>(1, nnz / 65536));
     hipLaunchKernelGGL(k_part_count_bal, dim3(B), dim3(1024), 0, s, part, off, (int)G, (int)P,
                        (int64_t)n_items, counts);
@@ -1349,8 +1206,7 @@ std::atomic<long long> g_split_launches{0};  // extend_count launches that split
 
 static int64_t extend_split(int64_t Wp, int64_t n_cand, int ts) {
   if (ts != 64 || n_cand <= 0) return 1;
-  const char* fe = std::getenv("KMLS_EXTEND_SPLIT");  // test knob: slices per row
-  const int64_t forced = fe ? (int64_t)std::atoll(fe) : 0;
+  const int64_t forced = test_hook("extend_split", 0);  // slices per row
   if (forced > 0) return std::max<int64_t>(1, std::min<int64_t>(forced, (Wp >> 1) / 64));
   const int64_t want = (256 * 8 + n_cand - 1) / n_cand;
   return std::max<int64_t>(1, std::min<int64_t>(want, (Wp >> 1) / 2048));
@@ -1381,10 +1237,8 @@ void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off,
   if (c1 <= c0) return;
   const int ts = team_size(Wp);
   const int64_t teams_per_block = kBlock / ts;
-  // long rows with a known survivor count: survivor-driven grid (KMLS_MATERIALIZE=cand keeps
-  // the candidate-driven one, A/B)
-  const char* me = std::getenv("KMLS_MATERIALIZE");
-  if (o.bm && ts == 64 && n_surv > 0 && surv && !(me && std::string(me) == "cand")) {
+  // long rows with a known survivor count: survivor-driven grid
+  if (o.bm && ts == 64 && n_surv > 0 && surv) {
     hipLaunchKernelGGL(k_surv_index, dim3(grid_for(c1 - c0, kBlock, 2048)), dim3(kBlock), 0, s,
                        cnt, minsup, pos, c0, c1 - c0, surv);
     // >= 8192 teams over the survivors' rows, slices of >= 1024 16-byte chunks

@@ -41,30 +41,12 @@ def _onehot(tx):
     return X
 
 
-# MFMA gram variants (KMLS_GRAM_FP4 / KMLS_GRAM_TILE / KMLS_GRAM_LDS): True = the default
-# (masked-nibble FP4, wide tiles); the others are the A/B kernels kept selectable
-_GRAM_ENV = {
-    True: {},
-    "i8": {"KMLS_GRAM_FP4": "0"},                                   # 128-tile LDS-staged i8
-    "direct": {"KMLS_GRAM_FP4": "0", "KMLS_GRAM_LDS": "0"},         # direct-load i8
-    "fp4": {"KMLS_GRAM_FP4": "1"},                                  # 128-tile LDS, FP4 LUT unpack
-    "fp4direct": {"KMLS_GRAM_FP4": "direct"},                       # direct-load FP4 LUT unpack
-    "wide": {"KMLS_GRAM_FP4": "0", "KMLS_GRAM_TILE": "256"},        # wide tiles, i8
-    "widefp4": {"KMLS_GRAM_FP4": "1", "KMLS_GRAM_TILE": "256"},     # wide tiles, FP4 LUT unpack
-    "mask8": {"KMLS_GRAM_FP4": "mask8"},                            # masked FP4, 2 waves / SIMD
-}
-
-
-@pytest.mark.parametrize("use_mfma", [False] + list(_GRAM_ENV))
+@pytest.mark.parametrize("use_mfma", [False, True])  # popcount bit-GEMM / masked-FP4 MFMA gram
 @pytest.mark.parametrize("shape,ms,n_tx", [("tiny", 0.02, None), ("ds2_weak", 0.03, None),
                                              ("tiny", 0.01, 5000), ("ds2", 0.05, 777),
                                              ("ds2_weak", 0.03, 70000)])
-def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
+def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma):
     import torch
-    if use_mfma is not False:
-        for k, v in _GRAM_ENV[use_mfma].items():
-            monkeypatch.setenv(k, v)
-        use_mfma = True
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     tx = generate(shape, seed=11, n_tx=n_tx)
     # run the miner on torch's current stream so torch allocations/fills are ordered with it
@@ -96,8 +78,7 @@ def test_pair_gram_vs_numpy(gpu_mod, shape, ms, n_tx, use_mfma, monkeypatch):
     np.testing.assert_array_equal(pc.reshape(max(F, 1), Wp).sum(1)[:F], counts)
 
 
-@pytest.mark.parametrize("fp4", ["1", "direct", "wide", "mask", "mask8"])
-def test_pair_gram_fp4_exact_past_2_24_transactions(gpu_mod, fp4, monkeypatch):
+def test_pair_gram_fp4_exact_past_2_24_transactions(gpu_mod):
     """FP4 operands accumulate in f32, exact only below 2^24 per block: with more transactions
     than that the split-K must keep every block's slice under it.  Checked against the popcount
     gram (integer arithmetic) on 17M transactions."""
@@ -115,10 +96,6 @@ def test_pair_gram_fp4_exact_past_2_24_transactions(gpu_mod, fp4, monkeypatch):
     torch.cuda.synchronize()
     g.encode_bitmaps(bm.data_ptr(), Wp, 0)
     g.pair_counts(bm.data_ptr(), Wp, ref.data_ptr(), False)
-    if fp4 == "wide":
-        monkeypatch.setenv("KMLS_GRAM_TILE", "256")
-        fp4 = "1"
-    monkeypatch.setenv("KMLS_GRAM_FP4", fp4)
     g.pair_counts(bm.data_ptr(), Wp, got.data_ptr(), True)
     g.synchronize()
     iu = np.triu_indices(F, 1)
@@ -134,7 +111,7 @@ def test_pair_gram_fp4_exact_past_2_24_transactions(gpu_mod, fp4, monkeypatch):
                                       ("ds_dense", 0.05)])
 def test_gpu_miner_matches_cpu(gpu_mod, shape, ms, use_mfma, fused, monkeypatch):
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    monkeypatch.setenv("KMLS_FUSED_LEVELS", fused)
+    monkeypatch.setenv("KMLS_TEST_HOOKS", f"fused_levels={fused}")
     tx = generate(shape, seed=5)
     g = gpu_mod.GpuMiner(0, 1 << 31, 0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
@@ -186,14 +163,14 @@ def test_gpu_miner_max_len_and_pairs(gpu_mod):
 def test_gpu_miner_chunked_levels(gpu_mod, monkeypatch):
     """Force many candidates per level (multi-chunk path) on a larger synthetic set."""
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    monkeypatch.setenv("KMLS_FUSED_LEVELS", "0")
+    monkeypatch.setenv("KMLS_TEST_HOOKS", "fused_levels=0")
     tx = generate("ds_dense", seed=9)
     g = gpu_mod.GpuMiner(0, 8 << 30, 0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     r = g.mine(0.045)
     c = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, 0.045)
     assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
-    assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
+    assert_same_itemsets(gpu_mod, r, c)
 
 
 def test_fused_levels_repeat_and_small_arena(gpu_mod, monkeypatch):
@@ -209,16 +186,16 @@ def test_fused_levels_repeat_and_small_arena(gpu_mod, monkeypatch):
         r = g.mine(0.05)
         assert r["stats"]["levels_path"] == "fused-resident", r["stats"]
         assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
-        assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
         keep.append(r)  # results stay valid while later calls run (pinned buffers not reused)
     for r in keep:
-        assert np.array_equal(np.sort(r["count"]), np.sort(c["count"]))
-    monkeypatch.setenv("KMLS_FUSED_BUMP_MB", "64")  # device allocations overflow mid-way
+        assert_same_itemsets(gpu_mod, r, c)
+    monkeypatch.setenv("KMLS_TEST_HOOKS", "fused_bump_mb=64")  # device allocations overflow mid-way
     small = gpu_mod.GpuMiner(0, 2 << 30, 0)
     small.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     r = small.mine(0.05)
     assert "fallback: device overflow code 1" in r["stats"]["levels_path"], r["stats"]
     assert r["stats"]["n_itemsets"] == c["stats"]["n_itemsets"]
+    assert_same_itemsets(gpu_mod, r, c)
 
 
 def test_gpu_serve_matches_cpu(gpu_mod):
@@ -331,10 +308,10 @@ def test_dist_protocol_path_on_gpu(gpu_mod):
 
 
 def test_default_arena_grows_on_demand(gpu_mod, monkeypatch):
-    """A default-sized arena starts small (KMLS_ARENA_INIT_MB here; 8 GiB normally) and grows
+    """A default-sized arena starts small (test hook arena_init_mb here; 8 GiB normally) and grows
     when the device-resident path runs out of room, instead of falling back or failing."""
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    monkeypatch.setenv("KMLS_ARENA_INIT_MB", "520")
+    monkeypatch.setenv("KMLS_TEST_HOOKS", "arena_init_mb=520")
     tx = generate("ds_dense", seed=3)
     g = gpu_mod.GpuMiner(0)
     assert g.arena_capacity < (600 << 20)
@@ -362,13 +339,10 @@ def test_support_histograms_large_vocab(gpu_mod, T, I):
                                   np.bincount(items, minlength=I))
 
 
-@pytest.mark.parametrize("mode", ["bal", "part"])
-def test_support_partitioned_count_modes(gpu_mod, monkeypatch, mode):
-    """Pass 3 of the partitioned histogram in each A/B form (equal global slices,
-    M blocks per partition) on a Zipf-headed 1M vocabulary whose hot
-    items repeat inside a thread's 8 ids, against np.bincount."""
+def test_support_partitioned_count(gpu_mod):
+    """The partitioned histogram (pass 3: equal global slices) on a Zipf-headed 1M vocabulary
+    whose hot items repeat inside a thread's 8 ids, against np.bincount."""
     import torch
-    monkeypatch.setenv("KMLS_SUPPORT_COUNT", mode)
     ptr, items = gpu_mod.synth_transactions(400_000, 1_000_003, 30.0, 50, 0.95, 1.1, 11)
     g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(ptr, items, 1_000_003)
@@ -394,13 +368,12 @@ def test_graph_replay_matches_eager(gpu_mod):
         r = g.mine(ms)
         assert r["stats"]["levels_path"] == "fused-resident", r["stats"]
         assert r["stats"]["n_itemsets"] == ref[ms]["stats"]["n_itemsets"]
-        assert np.array_equal(np.sort(r["count"]), np.sort(ref[ms]["count"]))
         phases.append(next(k for k in r["stats"]["phases_ms"] if k.startswith("mine(graph")
                            or k.startswith("prologue")))
         kept.append((ms, r))
     assert "mine(graph replay)" in phases[2:4], phases
     for ms, r in kept:  # pinned results of replayed calls stay valid
-        assert np.array_equal(np.sort(r["count"]), np.sort(ref[ms]["count"]))
+        assert_same_itemsets(gpu_mod, r, ref[ms])
     small = [(ms, r) for ms, r in kept if r["stats"]["n_itemsets"] < 300_000][-1]
     assert _trie_dict(small[1]) == _trie_dict(ref[small[0]])
 
@@ -426,7 +399,7 @@ def test_prefetch_pipeline_matches_sync(gpu_mod):
     assert any("adopted" in p for p in phases), phases
     g.synchronize()
     for ms, r in kept:  # every result buffer stayed intact while later calls ran
-        assert np.array_equal(np.sort(r["count"]), np.sort(ref[ms]["count"]))
+        assert_same_itemsets(gpu_mod, r, ref[ms])
     assert _trie_dict(kept[6][1]) == _trie_dict(ref[0.05])
     # replicated-partition entry point: 2 ranks' pipelined sub-tries cover the full result
     total = 0
@@ -446,11 +419,11 @@ def test_prefetch_pipeline_matches_sync(gpu_mod):
 @pytest.mark.parametrize("tiled", ["1", "0"])
 def test_encode_long_shard_matches_onehot(gpu_mod, tiled, monkeypatch):
     """Bitmap encode of a long shard (>= 65536 transactions: the LDS-slab kernel, or the atomic
-    kernel with KMLS_ENCODE_TILED=0) equals the one-hot matrix of the frequent items bit for bit,
+    kernel with the test hook encode_tiled=0) equals the one-hot matrix of the frequent items bit for bit,
     including a word offset into a wider buffer."""
     import torch
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    monkeypatch.setenv("KMLS_ENCODE_TILED", tiled)
+    monkeypatch.setenv("KMLS_TEST_HOOKS", f"encode_tiled={tiled}")
     tx = generate("tiny", seed=12, n_tx=70001)
     g = gpu_mod.GpuMiner(0, 1 << 28, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
@@ -550,7 +523,7 @@ def test_rule_map_from_gram(gpu_mod, shape, ms, n_tx, mfma):
 def test_rule_index_regrow_and_prefetch(gpu_mod, monkeypatch):
     """A too-small entry capacity regrows and redoes the call; launch-ahead calls adopt their
     own pinned CSR buffers (graph replay)."""
-    monkeypatch.setenv("KMLS_IDX_CAP", "64")
+    monkeypatch.setenv("KMLS_TEST_HOOKS", "idx_cap=64")
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     from kubernetes_machine_learning_server_amd.serve.index import name_tie_rank
     tx = generate("ds1", seed=4)
@@ -568,7 +541,7 @@ def test_max_len_leaf_levels(gpu_mod, fused, monkeypatch):
     """Truncated mining (mlxtend max_len): the last allowed level is written as trie leaves
     without child bitmaps (chunked path) and must equal the CPU miner's truncated result."""
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
-    monkeypatch.setenv("KMLS_FUSED_LEVELS", fused)
+    monkeypatch.setenv("KMLS_TEST_HOOKS", f"fused_levels={fused}")
     tx = generate("ds1", seed=6)
     g = gpu_mod.GpuMiner(0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
@@ -586,8 +559,7 @@ def test_extend_split_k_long_rows(gpu_mod, monkeypatch, split):
     metadata): forced on a long-row chunked run, including an odd chunk remainder, and the trie
     must equal the CPU miner's."""
     from kubernetes_machine_learning_server_amd.data.synthetic import generate_large
-    monkeypatch.setenv("KMLS_FUSED_LEVELS", "0")
-    monkeypatch.setenv("KMLS_EXTEND_SPLIT", split)
+    monkeypatch.setenv("KMLS_TEST_HOOKS", f"fused_levels=0,extend_split={split}")
     tx = generate_large("10Mx1M", seed=11, n_tx=300_000 + 64 * 7, n_items=50_000)
     before = gpu_mod.extend_split_launches()
     g = gpu_mod.GpuMiner(0)
@@ -599,24 +571,17 @@ def test_extend_split_k_long_rows(gpu_mod, monkeypatch, split):
     assert_same_itemsets(gpu_mod, r, c)
 
 
-@pytest.mark.parametrize("lookup", ["lds", "group", "no-multiband"])
 @pytest.mark.parametrize("T,I,ms,min_f", [(300_000 + 37, 60_000, 0.002, 0),
                                             (200_000 + 37, 100_000, 0.002, 100),
                                             (300_000 + 37, 1_000_003, 0.001, 50),
                                             (200_000 + 37, 100_000, 0.0005, 3000)])
-def test_encode_tiled_long_shard(gpu_mod, monkeypatch, T, I, ms, min_f, lookup):
+def test_encode_tiled_long_shard(gpu_mod, T, I, ms, min_f):
     """The LDS-slab encode produces the same tid-bitmaps as the host encoder, on a long shard
     with an odd tail tile; the second case has a million-style vocabulary (frequent-item mask
     in front of the rank gather, or the one-gather group tables when F <= 2048) and more
-    frequent rows than one LDS slab (row bands).  ``lookup``: the 8-byte group gather
-    (default where F <= 2048) or the LDS mask + hash tables (KMLS_ENCODE_LOOKUP=lds, A/B).  The
-    buffer starts as all ones: the tiled encode must write every word of the shard's columns
+    frequent rows than one LDS slab (the multi-band kernel).  The buffer starts as all ones: the tiled encode must write every word of the shard's columns
     (the tx-DP path no longer clears the bitmap first)."""
     import torch
-    if lookup == "lds":
-        monkeypatch.setenv("KMLS_ENCODE_LOOKUP", "lds")
-    if lookup == "no-multiband":  # wide frequent sets: one block per (tile, band), A/B
-        monkeypatch.setenv("KMLS_ENCODE_MULTIBAND", "0")
     ptr, items = gpu_mod.synth_transactions(T, I, 30.0, 500, 0.9, 0.85, 9)
     g = gpu_mod.GpuMiner(0, 1 << 30, torch.cuda.current_stream().cuda_stream or 0)
     g.load_csr(ptr, items, I)
