@@ -551,6 +551,13 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
     const unsigned c = and_count<WT>(bblk, bpad, sa, sb, v);
     const bool surv = act && c >= a.minsup;
     const unsigned long long mask = __ballot(surv);
+    // member groups (frame f, member i) are runs of consecutive lanes (pairs are row-major):
+    // the first lane of each run updates its group once, instead of one LDS atomic per
+    // survivor on the same address
+    const unsigned g = act ? L.G[f] + i : 0xffffffffu;
+    const unsigned gprev = __shfl_up(g, 1u, 64);
+    const bool head = act && (lane == 0 || gprev != g);
+    const unsigned long long hmask = __ballot(head);
     if (surv) {
       const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
       const unsigned long long ih_a = ihp[sa], ih_b = ihp[sb];
@@ -558,11 +565,19 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
       const DigestTerms dt = digest_terms(L.f_hash[f] + ih_a + ih_b, c);
       acc.dsum += dt.sum;
       acc.dxor ^= dt.xr;
-      atomicAdd(&L.depth_cnt[meta_depth(L.f_meta[f]) + 2], 1ull);
-      const unsigned g = L.G[f] + i;
-      atomicAdd(&L.g_cnt[g], 1u);
-      atomicMin(&L.g_start[g], pos);
     }
+    if (head) {
+      const unsigned long long after = hmask & ~((2ull << lane) - 1ull);  // later run heads
+      const unsigned long long below_end = after ? ((1ull << __builtin_ctzll(after)) - 1ull) : ~0ull;
+      const unsigned long long rs = mask & below_end & ~lanelt;  // this run's survivors
+      if (rs) {
+        atomicAdd(&L.g_cnt[g], (unsigned)__popcll(rs));
+        const unsigned first = (unsigned)__builtin_ctzll(rs);
+        atomicMin(&L.g_start[g], S + (unsigned)__popcll(mask & ((1ull << first) - 1ull)));
+      }
+    }
+    // the batch's frames are siblings of one block: one depth
+    if (lane == 0 && mask) L.depth_cnt[meta_depth(top.meta) + 2] += (unsigned long long)__popcll(mask);
     S += (unsigned)__popcll(mask);
     ++acc.chunks;
   }
