@@ -28,7 +28,8 @@ Secondary fields:
                     at N > 1 one relabelled dataset per rank (weak scaling).
 * ``config2``     — ds1 @0.01: deployed rule map, truncated-at-4 trie, full count-only mining
                     with the size cap raised within a time budget (N = 1).
-* ``config3``     — 10M x 1M @0.001 transaction-DP over all ranks.
+* ``config3``     — 10M x 1M @2e-4 (14.8k frequent items) transaction-DP over all ranks,
+                    sampled supports recounted on the host from the CSR shards.
 * ``native_rccl`` — at N > 1 the headline combine once more through the native RCCL
                     communicator (``csrc/host/comm_rccl.cpp``), digest compared.
 

@@ -34,6 +34,8 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--mode", default="tx", choices=["tx", "item", "auto"])
     ap.add_argument("--tiles", type=int, default=4, help="support tiles (all-reduce overlap)")
+    ap.add_argument("--arena-gb", type=float, default=48.0,
+                    help="device arena of the level loop (>10k frequent items need >8 GB)")
     ap.add_argument("--mfma", action="store_true")
     ap.add_argument("--rules", action="store_true", help="also time rules + index + hot reload")
     ap.add_argument("--min-confidence", type=float, default=0.3)
@@ -82,7 +84,7 @@ def main(argv=None) -> int:
     t0 = time.perf_counter()
     dm = DistMiner(ptr, items, shape.n_items, args.min_support, device=local_rank,
                    max_len=args.max_len, mfma=args.mfma, mode=args.mode,
-                   support_tiles=args.tiles, **kw)
+                   support_tiles=args.tiles, arena_bytes=int(args.arena_gb * (1 << 30)), **kw)
     load_s = time.perf_counter() - t0
 
     def barrier():
