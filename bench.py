@@ -28,8 +28,9 @@ Secondary fields:
                     at N > 1 one relabelled dataset per rank (weak scaling).
 * ``config2``     — ds1 @0.01: deployed rule map, truncated-at-4 trie, full count-only mining
                     with the size cap raised within a time budget (N = 1).
-* ``config3``     — 10M x 1M @2e-4 (14.8k frequent items) transaction-DP over all ranks,
-                    sampled supports recounted on the host from the CSR shards.
+* ``config3``     — 10M x 1M @2e-4 (14.8k frequent items) transaction-DP over all ranks
+                    (native RCCL communicator at N > 1 once ``native_rccl`` worked, else the
+                    host one), sampled supports recounted on the host from the CSR shards.
 * ``native_rccl`` — at N > 1 the headline combine once more through the native RCCL
                     communicator (``csrc/host/comm_rccl.cpp``), digest compared.
 
@@ -291,17 +292,6 @@ def main() -> int:
             out.setdefault("errors", {})["config2"] = repr(e)[:300]
         wd.disarm()
 
-    # ---- BASELINE config 3 (all ranks) ----
-    if not args.no_config3:
-        wd.arm("config3", 300)
-        try:
-            c3 = bm.run_config3(N, world, rank, device)
-            if rank == 0:
-                out["config3"] = c3
-        except Exception as e:
-            out.setdefault("errors", {})["config3"] = repr(e)[:300]
-        wd.disarm()
-
     # ---- the headline combine through the native RCCL communicator ----
     if world > 1 and dist_backend == "nccl" and args.comm != "rccl" and not args.cpu:
         os.environ.setdefault("KMLS_COMM_TIMEOUT_S", "60")
@@ -314,6 +304,20 @@ def main() -> int:
                                   "digest_equal": r2["digest"] == h["digest"]}
         except Exception as e:
             out.setdefault("errors", {})["native_rccl"] = repr(e)[:300]
+        wd.disarm()
+
+    # ---- BASELINE config 3 (all ranks) ----
+    if not args.no_config3:
+        wd.arm("config3", 300)
+        try:
+            # over the native RCCL communicator when it came up for the headline combine above
+            c3_comm = "rccl" if (world > 1 and out.get("native_rccl", {}).get("digest_equal")) \
+                else "host"
+            c3 = bm.run_config3(N, world, rank, device, comm=c3_comm)
+            if rank == 0:
+                out["config3"] = c3
+        except Exception as e:
+            out.setdefault("errors", {})["config3"] = repr(e)[:300]
         wd.disarm()
 
     if rank == 0:
