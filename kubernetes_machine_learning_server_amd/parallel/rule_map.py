@@ -96,7 +96,8 @@ class _Gpu:
         self.dev = torch.device("cuda", rm.device)
         # torch fills, the native kernels and the communicator all run on ONE stream
         self.stream = torch.cuda.Stream(device=rm.device)
-        self.g = N.GpuMiner(rm.device, 1 << 30, self.stream.cuda_stream)
+        self.s = self.stream.cuda_stream
+        self.g = N.GpuMiner(rm.device, 1 << 30, self.s)
         self.g.load_csr(tx_ptr, items, rm.n_items)
         self.comm = None
         if rm.world > 1:
@@ -119,21 +120,27 @@ class _Gpu:
     def set_tie_rank(self, tie):
         self.g.set_tie_rank(np.ascontiguousarray(tie, np.int32))
 
-    def step(self, rm: "DistRuleMap", ph: Dict[str, float]):
-        s = self.stream.cuda_stream
-        t0 = time.perf_counter()
+    def supports(self, rm: "DistRuleMap") -> np.ndarray:
+        """Global per-item supports: the shard histogram, all-reduced."""
         with torch.cuda.stream(self.stream):
             cnt = self.buf("cnt", (rm.n_items,), torch.int32)
             cnt.zero_()
             self.g.item_support(cnt.data_ptr())
             if self.comm is not None:
-                self.comm.all_reduce(cnt.data_ptr(), cnt.data_ptr(), rm.n_items, "u32", False, s)
-                self.comm.wait_stream(s)
-            host = cnt.cpu().numpy().view(np.uint32)
-            ph["supports_allreduce"] = time.perf_counter() - t0
-            F = self.g.select(host, rm.n_tx, rm.min_support)
-            ids, fcounts, minsup = self.g.frequent()
-            per, r0, nrows = row_block(F, rm.world, rm.rank)
+                self.comm.all_reduce(cnt.data_ptr(), cnt.data_ptr(), rm.n_items, "u32", False,
+                                     self.s)
+                self.comm.wait_stream(self.s)
+            return cnt.cpu().numpy().view(np.uint32).copy()
+
+    def select(self, rm: "DistRuleMap", counts: np.ndarray):
+        F = self.g.select(np.ascontiguousarray(counts, np.uint32), rm.n_tx, rm.min_support)
+        ids, fcounts, minsup = self.g.frequent()
+        return F, np.asarray(ids), np.asarray(fcounts), int(minsup)
+
+    def gram_rows(self, rm: "DistRuleMap", F: int):
+        """This rank's rows of the summed, mirrored gram (device tensor [per][F])."""
+        per, _, _ = row_block(F, rm.world, rm.rank)
+        with torch.cuda.stream(self.stream):
             bm = self.buf("bm", (max(F, 1), self.Ws), torch.int64)
             if self.Ws > self.used:
                 bm[:, self.used:] = 0
@@ -145,20 +152,27 @@ class _Gpu:
             if F:
                 self.g.pair_counts(bm.data_ptr(), self.Ws, gram.data_ptr(), True)
                 self.g.gram_mirror(gram.data_ptr(), F, F)
-            self.stream.synchronize()
-            ph["encode_gram"] = time.perf_counter() - t0
-            if self.comm is not None:
-                rows = self.buf("rows", (per, max(F, 1)), torch.int32)
-                self.comm.reduce_scatter(gram.data_ptr(), rows.data_ptr(), per * max(F, 1), "u32",
-                                         False, s)
-                self.comm.wait_stream(s)
-            else:
-                rows = gram
-            self.stream.synchronize()
-            ph["reduce_scatter"] = time.perf_counter() - t0
-            loc = self.g.rule_map_rows(rows.data_ptr(), max(F, 1), r0, nrows, int(minsup))
-            ph["rows_csr"] = time.perf_counter() - t0
-        return F, np.asarray(ids), np.asarray(fcounts), int(minsup), loc
+            if self.comm is None:
+                return gram
+            rows = self.buf("rows", (per, max(F, 1)), torch.int32)
+            self.comm.reduce_scatter(gram.data_ptr(), rows.data_ptr(), per * max(F, 1), "u32",
+                                     False, self.s)
+            self.comm.wait_stream(self.s)
+            return rows
+
+    def rows_to_host(self, rows) -> np.ndarray:
+        self.stream.synchronize()
+        return rows.cpu().numpy()
+
+    def rows_from_host(self, rm: "DistRuleMap", a: np.ndarray, F: int):
+        with torch.cuda.stream(self.stream):
+            t = self.buf("rows", tuple(a.shape), torch.int32)
+            t.copy_(torch.from_numpy(np.ascontiguousarray(a)))
+            return t
+
+    def rows_csr(self, rm: "DistRuleMap", rows, F: int, r0: int, nrows: int, minsup: int):
+        self.stream.synchronize()
+        return self.g.rule_map_rows(rows.data_ptr(), max(F, 1), r0, nrows, minsup)
 
     def release(self):
         self.held.clear()
@@ -171,6 +185,7 @@ class _Cpu:
         self.items = np.ascontiguousarray(items, np.int32)
         self.comm = None
         self.tie = None
+        self.rank_of = None
         if rm.world > 1:
             uid = [self.N.host_comm_unique_id() if rm.rank == 0 else b"\0" * 128]
             dist.broadcast_object_list(uid, src=0)
@@ -179,28 +194,38 @@ class _Cpu:
     def set_tie_rank(self, tie):
         self.tie = np.asarray(tie, np.int64)
 
-    def step(self, rm: "DistRuleMap", ph: Dict[str, float]):
-        t0 = time.perf_counter()
+    def supports(self, rm: "DistRuleMap") -> np.ndarray:
         cnt = np.bincount(self.items, minlength=rm.n_items).astype(np.uint32)
         if self.comm is not None:
             self.comm.all_reduce(cnt, False)
-        ph["supports_allreduce"] = time.perf_counter() - t0
-        ids, fcounts, rank_of, minsup = self.N.select_frequent(cnt, rm.n_tx, rm.min_support)
-        F = len(ids)
-        per, r0, nrows = row_block(F, rm.world, rm.rank)
+        return cnt
+
+    def select(self, rm: "DistRuleMap", counts: np.ndarray):
+        ids, fcounts, rank_of, minsup = self.N.select_frequent(counts, rm.n_tx, rm.min_support)
+        self.rank_of = rank_of
+        return len(ids), np.asarray(ids), np.asarray(fcounts), int(minsup)
+
+    def gram_rows(self, rm: "DistRuleMap", F: int):
+        per, _, _ = row_block(F, rm.world, rm.rank)
         W = (len(self.tx_ptr) - 1 + 63) // 64
-        bm = self.N.encode_bitmaps_cpu(self.tx_ptr, self.items, rank_of, F, W)
+        bm = self.N.encode_bitmaps_cpu(self.tx_ptr, self.items, self.rank_of, F, W)
         bits = np.unpackbits(np.ascontiguousarray(bm).view(np.uint8).reshape(F, -1), axis=1,
                              bitorder="little").astype(np.float32)
         gram = np.zeros((per * rm.world, max(F, 1)), np.uint32)
         gram[:F, :F] = np.rint(bits @ bits.T).astype(np.uint32)  # full symmetric
-        ph["encode_gram"] = time.perf_counter() - t0
-        rows = (self.comm.reduce_scatter(gram.reshape(-1), False).reshape(per, -1)
-                if self.comm is not None else gram)
-        ph["reduce_scatter"] = time.perf_counter() - t0
-        loc = rows_csr_host(rows[:nrows, :F], r0, ids, int(minsup), self.tie)
-        ph["rows_csr"] = time.perf_counter() - t0
-        return F, np.asarray(ids), np.asarray(fcounts), int(minsup), loc
+        if self.comm is None:
+            return gram
+        return self.comm.reduce_scatter(gram.reshape(-1), False).reshape(per, -1)
+
+    def rows_to_host(self, rows) -> np.ndarray:
+        return np.asarray(rows)
+
+    def rows_from_host(self, rm: "DistRuleMap", a: np.ndarray, F: int):
+        return np.asarray(a, np.uint32)
+
+    def rows_csr(self, rm: "DistRuleMap", rows, F: int, r0: int, nrows: int, minsup: int):
+        ids = self.ids
+        return rows_csr_host(np.asarray(rows)[:nrows, :F], r0, ids, minsup, self.tie)
 
     def release(self):
         pass
@@ -211,15 +236,23 @@ class DistRuleMap:
 
     ``tx_ptr``/``items``: this rank's shard (global transaction count ``global_n_tx``).
     ``step()`` returns the item-id CSR on rank 0 (``row_ptr``/``cons``/``count``, plus the
-    frequent ids/counts and per-phase times) and ``None`` elsewhere."""
+    frequent ids/counts and per-phase times) and ``None`` elsewhere.
+
+    Phase checkpoints (``ck`` = a ``utils.checkpoint.PhaseCheckpoint``): the global
+    supports (rank 0), every rank's reduce-scattered gram rows (the seconds of MFMA work at HBM
+    scale) and every rank's CSR rows.  A restarted call resumes after the last phase that EVERY
+    rank has (one MIN all-reduce of the ranks' phase levels); the frequent order is a pure
+    function of the supports, so it is recomputed, not stored."""
 
     def __init__(self, tx_ptr, items, n_items: int, global_n_tx: int, min_support: float,
-                 device: int = 0, backend: str = "gpu", comm_backend: Optional[str] = None):
+                 device: int = 0, backend: str = "gpu", comm_backend: Optional[str] = None,
+                 ck=None):
         self.world = dist.get_world_size() if (dist is not None and dist.is_initialized()) else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
         self.n_items, self.n_tx = int(n_items), int(global_n_tx)
         self.min_support = float(min_support)
         self.device = device
+        self.ck = ck
         self.comm_backend = comm_backend or os.environ.get("KMLS_COMM") or (
             "rccl" if self.world > 1 and dist.get_backend() == "nccl" else "host")
         self.ops = (_Gpu if backend == "gpu" else _Cpu)(self, tx_ptr, items)
@@ -227,14 +260,67 @@ class DistRuleMap:
     def set_tie_rank(self, tie: np.ndarray) -> None:
         self.ops.set_tie_rank(tie)
 
+    def _phase(self, name: str) -> str:
+        return f"rulemap_{name}_r{self.rank}of{self.world}"
+
+    def _resume_level(self) -> int:
+        """0 nothing, 1 supports, 2 gram rows, 3 CSR rows — the minimum over the ranks."""
+        ck = self.ck
+        if ck is None or not ck.enabled:
+            return 0
+        lvl = 0
+        if ck.has("rulemap_supports"):
+            lvl = 1
+            if ck.has(self._phase("rows")):
+                lvl = 2
+                if ck.has(self._phase("csr")):
+                    lvl = 3
+        if self.world > 1:
+            t = torch.tensor([lvl], dtype=torch.int64,
+                             device="cuda" if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            lvl = int(t.item())
+        return lvl
+
     def step(self) -> Optional[Dict]:
         from .dist_miner import gather_arrays
         ph: Dict[str, float] = {}
         t0 = time.perf_counter()
-        F, ids, fcounts, minsup, loc = self.ops.step(self, ph)
+        ck, ops = self.ck, self.ops
+        lvl = self._resume_level()
+        if lvl >= 1:
+            counts = ck.load("rulemap_supports")["counts"]
+        else:
+            counts = ops.supports(self)
+            if ck is not None and ck.enabled and self.rank == 0:
+                ck.save("rulemap_supports", counts=counts)
+        ph["supports_allreduce"] = time.perf_counter() - t0
+        F, ids, fcounts, minsup = ops.select(self, counts)
+        ops.ids = ids
+        per, r0, nrows = row_block(F, self.world, self.rank)
+        loc = None
+        if lvl >= 3:
+            z = ck.load(self._phase("csr"))
+            loc = {"row_ptr": z["row_ptr"], "cons": z["cons"], "count": z["count"],
+                   "status": int(z["status"])}
+        else:
+            if lvl >= 2:
+                rows = ops.rows_from_host(self, ck.load(self._phase("rows"))["rows"], F)
+            else:
+                rows = ops.gram_rows(self, F)
+                if ck is not None and ck.enabled:
+                    ck.save(self._phase("rows"), rows=ops.rows_to_host(rows))
+            ph["encode_gram_reduce_scatter"] = time.perf_counter() - t0
+            loc = ops.rows_csr(self, rows, F, r0, nrows, minsup)
+            if ck is not None and ck.enabled:
+                ck.save(self._phase("csr"), row_ptr=np.asarray(loc["row_ptr"]),
+                        cons=np.asarray(loc["cons"]), count=np.asarray(loc["count"]),
+                        status=np.int64(loc.get("status", 0)))
+        ph["rows_csr"] = time.perf_counter() - t0
+        if os.environ.get("KMLS_FAULT") == "rulemap_after_csr":
+            raise RuntimeError("injected fault at rulemap_after_csr")
         lens = np.diff(np.asarray(loc["row_ptr"], np.int64))
-        parts = {"lens": lens.astype(np.int64)}
-        got_l = gather_arrays(parts, self.rank, self.world)
+        got_l = gather_arrays({"lens": lens.astype(np.int64)}, self.rank, self.world)
         got_e = gather_arrays({"cons": np.asarray(loc["cons"], np.int32),
                                "count": np.asarray(loc["count"], np.uint32).view(np.int32)},
                               self.rank, self.world)
@@ -245,7 +331,7 @@ class DistRuleMap:
                              got_e["count"].view(np.uint32), self.n_items)
         ph["assemble"] = time.perf_counter() - t0
         out.update(ids=ids, fcounts=fcounts, minsup=minsup, n_frequent_items=F,
-                   status=int(loc.get("status", 0)),
+                   status=int(loc.get("status", 0)), resumed_from_phase=lvl,
                    phases_ms={k: round(v * 1e3, 3) for k, v in ph.items()})
         return out
 
