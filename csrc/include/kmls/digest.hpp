@@ -25,10 +25,15 @@ struct DigestTerms {
   uint64_t sum, xr;
 };
 
-// the two multiset-hash terms of one itemset (set hash `h`, support count `c`)
+constexpr uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+// the two multiset-hash terms of one itemset (set hash `h`, support count `c`): one mix of the
+// pair, then two different bijections of it for the sum and the xor aggregations.  (Round 3:
+// was four mix64 per itemset; the GPU miner evaluates this once per surviving candidate, so
+// it was ~a quarter of the deep kernel's VALU instructions.)
 constexpr DigestTerms digest_terms(uint64_t h, uint64_t c) {
-  const uint64_t dg = mix64(h ^ mix64(c + 0x51ED270B27ull));
-  return DigestTerms{mix64(dg), mix64(dg ^ 0xA5A5A5A5DEADBEEFull)};
+  const uint64_t dg = mix64(h + c * 0x9E3779B97F4A7C15ull);
+  return DigestTerms{dg, rotl64(dg, 29) * 0xD6E8FEB86659FD93ull};
 }
 
 }  // namespace kmls

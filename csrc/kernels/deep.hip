@@ -240,6 +240,9 @@ struct WaveLds {
   unsigned f_s0[kBatchFrames], f_m[kBatchFrames], f_meta[kBatchFrames];
   unsigned P[kBatchFrames + 1], G[kBatchFrames + 1];
   unsigned g_cnt[kCap], g_start[kCap];
+  unsigned g_pos[kCap];             // first pair of member group g (its run start)
+  unsigned g_fi[kCap];              // frame << 16 | member of group g
+  unsigned long long g_flag[kCap / 64];  // bit p: a group starts at pair p
   unsigned long long b_base[kBStack];
   unsigned b_live[kBStack];
   unsigned long long depth_cnt[64];
@@ -519,44 +522,50 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
   }
   __builtin_amdgcn_wave_barrier();
   const unsigned NG = uni(L.G[k + vzero()]);
+  if (lane < (int)(kCap / 64)) L.g_flag[lane] = 0ull;
+  __builtin_amdgcn_wave_barrier();
+  // member groups once per batch (not per pair): frame, member, first pair, start flag; a pair's
+  // group is then the number of group starts at or before it
   for (unsigned g = lane; g < NG; g += 64) {
     L.g_cnt[g] = 0;
     L.g_start[g] = 0xffffffffu;
+    unsigned f = 0;
+    for (unsigned step = 32; step; step >>= 1)
+      if (f + step < k && L.G[f + step] <= g) f += step;
+    const unsigned i = g - L.G[f], fmm = L.f_m[f];
+    const unsigned pos = L.P[f] + i * fmm - i * (i + 1) / 2;
+    L.g_pos[g] = pos;
+    L.g_fi[g] = (f << 16) | i;
+    atomicOr(&L.g_flag[pos >> 6], 1ull << (pos & 63));
   }
   __builtin_amdgcn_wave_barrier();
   const unsigned long long cpad = roundup16(P);
   const unsigned long long* bblk = (const unsigned long long*)top.blk;
   const unsigned long long bpad = top.pad;
   const unsigned long long* ihp = bblk + (unsigned long long)WT * bpad;
-  unsigned S = 0;
+  unsigned S = 0, gbase = 0;
   for (unsigned c0 = 0; c0 < P; c0 += 64) {
     const unsigned p = c0 + lane;
     const bool act = p < P;
-    // frame of pair p: largest f < k with P[f] <= p
-    unsigned f = 0;
-    for (unsigned step = 32; step; step >>= 1)
-      if (f + step < k && L.P[f + step] <= p) f += step;
-    if (!act) f = 0;
-    const unsigned fmm = L.f_m[f];
-    const unsigned q = act ? p - L.P[f] : 0u;
-    // triangular decode of q into (i, j), i < j < fmm, row-major over i
-    const float twoM = 2.0f * (float)fmm - 1.0f;
-    unsigned i = (unsigned)((twoM - sqrtf(twoM * twoM - 8.0f * (float)q)) * 0.5f);
-    auto row0 = [&](unsigned r) { return r * fmm - r * (r + 1) / 2; };
-    while (i > 0 && row0(i) > q) --i;
-    while (i + 1 < fmm && row0(i + 1) <= q) ++i;
-    const unsigned j = q - row0(i) + i + 1;
+    // group of pair p (row-major pairs: group (f, i) holds (i, j), j > i): starts up to p
+    const unsigned long long gw = uni64(L.g_flag[(c0 >> 6) + vzero()]);
+    const unsigned g = gbase + (unsigned)__popcll(gw & ((2ull << lane) - 1ull)) - 1u;
+    unsigned f = 0, i = 0, j = 0;
+    if (act) {
+      const unsigned fi = L.g_fi[g];
+      f = fi >> 16;
+      i = fi & 0xffffu;
+      j = i + 1 + (p - L.g_pos[g]);
+    }
+    gbase += (unsigned)__popcll(gw);
     const unsigned sa = L.f_s0[f] + i, sb = L.f_s0[f] + (act ? j : i);
     unsigned long long v[WT];
     const unsigned c = and_count<WT>(bblk, bpad, sa, sb, v);
     const bool surv = act && c >= a.minsup;
     const unsigned long long mask = __ballot(surv);
-    // member groups (frame f, member i) are runs of consecutive lanes (pairs are row-major):
-    // the first lane of each run updates its group once, instead of one LDS atomic per
-    // survivor on the same address
-    const unsigned g = act ? L.G[f] + i : 0xffffffffu;
-    const unsigned gprev = __shfl_up(g, 1u, 64);
-    const bool head = act && (lane == 0 || gprev != g);
+    // member groups are runs of consecutive lanes: the first lane of each run updates its
+    // group once, instead of one LDS atomic per survivor on the same address
+    const bool head = act && (lane == 0 || ((gw >> lane) & 1ull));
     const unsigned long long hmask = __ballot(head);
     if (surv) {
       const unsigned pos = S + (unsigned)__popcll(mask & lanelt);

@@ -23,10 +23,10 @@ from typing import Callable, Dict, Optional
 import numpy as np
 
 # Whole-problem references computed on the build host by the native CPU miner
-# (``mine_cpu_count``, 6 threads, 88 s; profiles/r3_config2_cpu_ref.md) on
-# ``generate("ds1", seed=0)``: (digest, n_itemsets, per-level counts from size 1).
+# (``mine_cpu_count``, 8 threads, 143 s) on ``generate("ds1", seed=0)``: (digest, n_itemsets,
+# per-level counts from size 1).  The digest uses the round-3 digest_terms (kmls/digest.hpp).
 CPU_REF = {
-    0.02: ("5645ebcc74e7a31e9f474dfbb0c9e0bb", 1414082373,
+    0.02: ("1d15b1d026fe928d14a65f5b88be8656", 1414082373,
            [2032, 81637, 897824, 5004384, 18407680, 51371444, 114076602, 200624405, 274917544,
             289754387, 232392862, 139994181, 62090008, 19642215, 4215542, 566649, 41695, 1275,
             7]),

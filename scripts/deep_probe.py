@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 # CPU references (mine_cpu_count on the build host, 6 threads; profiles/r3_config2_cpu_ref.md)
 CPU_REF = {
-    0.02: ("5645ebcc74e7a31e9f474dfbb0c9e0bb", 1414082373),
+    0.02: ("1d15b1d026fe928d14a65f5b88be8656", 1414082373),
 }
 
 
