@@ -417,6 +417,7 @@ void register_gpu_bindings(py::module_& m) {
         d["digest"] = std::string(buf);
         d["round_tasks"] = r.round_tasks;
         d["spilled_tasks"] = r.spilled_tasks;
+        d["handoffs"] = r.handoffs;
         d["round_ms"] = r.round_ms;
         py::dict ph;
         ph["prologue"] = r.ms_prologue;

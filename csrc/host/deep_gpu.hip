@@ -103,6 +103,7 @@ DeepResult GpuMiner::mine_deep(double min_support, int max_len, int rank, int wo
   res.level2_tasks = loc.level2_tasks;
   res.round_tasks = loc.round_tasks;
   res.spilled_tasks = loc.spilled_tasks;
+  res.handoffs = loc.handoffs;
   res.round_ms = loc.round_ms;
   res.ms_root = loc.ms_root;
   res.ms_rounds = loc.ms_rounds;

@@ -21,7 +21,7 @@ namespace gpu {
 
 DeepBufs::~DeepBufs() {
   (void)hipSetDevice(device);
-  for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)req, (void*)heap[0],
+  for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)req, (void*)inbox, (void*)inbox_state, (void*)heap[0],
                   (void*)heap[1], (void*)root, (void*)ctl, (void*)d_red, (void*)d_xor,
                   (void*)d_m, (void*)d_off, (void*)d_toff})
     if (p) (void)hipFree(p);
@@ -206,18 +206,23 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   if (opt.steal && n_tasks > 0) {
     // one launch: spilled tasks are queued behind the level-3 tasks and taken by waiting waves
     const auto tr = now();
-    KMLS_HIP(hipMemsetAsync(b.ctl, 0, 4 * sizeof(unsigned long long), s));
+    KMLS_HIP(hipMemsetAsync(b.ctl, 0, 5 * sizeof(unsigned long long), s));
     if (b.req_cap < waves) {
-      if (b.req) KMLS_HIP(hipFree(b.req));
-      KMLS_HIP(hipMalloc((void**)&b.req, (size_t)waves * sizeof(unsigned)));
-      KMLS_HIP(hipMemsetAsync(b.req, 0, (size_t)waves * sizeof(unsigned), s));
+      for (void* p : {(void*)b.req, (void*)b.inbox, (void*)b.inbox_state})
+        if (p) KMLS_HIP(hipFree(p));
+      KMLS_HIP(hipMalloc((void**)&b.req, (size_t)waves * 8));
+      KMLS_HIP(hipMalloc((void**)&b.inbox, (size_t)waves * sizeof(kern::DeepFrame)));
+      KMLS_HIP(hipMalloc((void**)&b.inbox_state, (size_t)waves * 4));
+      KMLS_HIP(hipMemsetAsync(b.req, 0, (size_t)waves * 8, s));
+      KMLS_HIP(hipMemsetAsync(b.inbox_state, 0, (size_t)waves * 4, s));
       b.req_cap = waves;
     }
     b.h_ctl->pending = (unsigned long long)n_tasks;
     KMLS_HIP(hipMemcpyAsync(&b.ctl->pending, &b.h_ctl->pending, 8, hipMemcpyHostToDevice, s));
-    if (++b.epoch >= (1u << 31)) {  // 2^31 launches: restart the stamps
+    if (++b.epoch >= (1u << 30)) {  // 2^30 launches: restart the stamps
       KMLS_HIP(hipMemsetAsync(b.ready, 0, (size_t)b.q_cap * sizeof(unsigned), s));
-      KMLS_HIP(hipMemsetAsync(b.req, 0, (size_t)b.req_cap * sizeof(unsigned), s));
+      KMLS_HIP(hipMemsetAsync(b.req, 0, (size_t)b.req_cap * 8, s));
+      KMLS_HIP(hipMemsetAsync(b.inbox_state, 0, (size_t)b.req_cap * 4, s));
       b.epoch = 1;
     }
     a.in = b.q[0];
@@ -228,8 +233,10 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     a.ready = b.ready;
     a.epoch = b.epoch;
     a.steal = 1;
-    a.steal_eager = opt.steal_idle == 0 ? 1 : 0;
+    a.steal_eager = opt.steal_idle == 0 ? 1 : opt.steal_idle == 2 ? 2 : 0;
     a.req = b.req;
+    a.inbox = b.inbox;
+    a.inbox_state = b.inbox_state;
     a.nwaves = waves;
     kern::deep_count(a, maxt, blocks_per_cu, grid, s);
     KMLS_HIP(hipMemcpyAsync(b.h_ctl, b.ctl, sizeof(kern::DeepCtl), hipMemcpyDeviceToHost, s));
@@ -244,6 +251,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     res.round_tasks.push_back(n_tasks);
     res.round_ms.push_back(ms_since(tr));
     res.spilled_tasks = (int64_t)b.h_ctl->n_out;
+    res.handoffs = (int64_t)b.h_ctl->handoffs;
     n_tasks = 0;  // the rounds below have nothing left
   }
   int cur = 0;

@@ -25,7 +25,9 @@ struct DeepBufs {
   kern::DeepFrame* q[2] = {nullptr, nullptr};
   int64_t q_cap = 0;
   unsigned* ready = nullptr;  // [q_cap] steal-mode publish flags (zeroed once at allocation)
-  unsigned* req = nullptr;    // [req_cap] steal-mode mailboxes (one per wave)
+  unsigned long long* req = nullptr;  // [req_cap] steal-mode mailboxes (one per wave)
+  kern::DeepFrame* inbox = nullptr;   // [req_cap] direct hand-offs
+  unsigned* inbox_state = nullptr;    // [req_cap]
   int64_t req_cap = 0;
   unsigned epoch = 0;         // steal-mode launch stamp of the flags
 
@@ -65,6 +67,7 @@ struct DeepLocal {
   int maxt = 0;  // widest block tier of the count kernel instance
   std::vector<int64_t> round_tasks;
   int64_t spilled_tasks = 0;  // tasks spilled inside the launch(es)
+  int64_t handoffs = 0;       // classes handed straight to a requesting wave (steal mode)
   std::vector<double> round_ms;
   double ms_alloc = 0, ms_root = 0, ms_rounds = 0;
 };

@@ -155,8 +155,8 @@ struct DeepOpts {
   bool steal = true;                  // one launch, spills taken by waiting waves (budget =
                                       // passes between checks for a waiting wave); false =
                                       // spill rounds (budget0/budget = per-task step budgets)
-  unsigned steal_idle = 1;            // steal: 1 = hand over when a waiting wave asks; 0 = at
-                                      // every check (tests)
+  unsigned steal_idle = 1;            // steal: 1 = hand over when a waiting wave asks; tests:
+                                      // 0 = to the queue at every check, 2 = to the partner wave
 };
 struct DeepResult {
   std::vector<uint64_t> per_level;  // [d] = frequent itemsets of size d (index 0 unused)
@@ -165,6 +165,7 @@ struct DeepResult {
   uint64_t digest_sum = 0, digest_xor = 0;
   std::vector<int64_t> round_tasks;
   int64_t spilled_tasks = 0;
+  int64_t handoffs = 0;
   std::vector<double> round_ms;
   double ms_prologue = 0, ms_root = 0, ms_rounds = 0, ms_combine = 0, ms_total = 0;
 };

@@ -277,6 +277,28 @@ __device__ __forceinline__ void free_blocks(WaveLds<MAXT>& L, WaveState& st) {
   }
 }
 
+// drop the bottom `ns` frames (spilled or handed over): their blocks lose a reference, frames
+// ns.. move down by ns (64 at a time, low to high: a chunk's loads happen before its stores, and
+// it only overwrites frames an earlier chunk already moved)
+template <int MAXT>
+__device__ __forceinline__ void drop_bottom(DeepFrame* fst, WaveState& st, WaveLds<MAXT>& L,
+                                            int lane, unsigned ns) {
+  if ((unsigned)lane < ns) {
+    const unsigned b = meta_bidx(fst[lane].meta);
+    if (b) atomicSub(&L.b_live[b - 1], 1u);
+  }
+  const unsigned rest = st.nf - ns;
+  for (unsigned c0 = 0; c0 < rest; c0 += 64) {
+    const bool act = c0 + lane < rest;
+    DeepFrame fr{};
+    if (act) fr = fst[ns + c0 + lane];
+    __builtin_amdgcn_wave_barrier();
+    if (act) store_frame(fst + c0 + lane, fr);
+    __builtin_amdgcn_wave_barrier();
+  }
+  st.nf = rest;
+}
+
 // Copy the bottom `ns` frames of the stack (all of them: ns = nf) to the spill heap and queue
 // them as task(s): frames of more than split_min members become one single-member task each
 // (over one shared copy).  Heap bytes and queue slots are reserved for all of them before
@@ -369,24 +391,58 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
     st.mem_top = 0;
     return 0;
   }
-  // partial: the spilled frames' blocks lose a reference; frames ns.. move down by ns (64 at a
-  // time, low to high: a chunk's loads happen before its stores, and it only overwrites frames
-  // an earlier chunk already moved)
-  if ((unsigned)lane < ns) {
-    const unsigned b = meta_bidx(fst[lane].meta);
-    if (b) atomicSub(&L.b_live[b - 1], 1u);
-  }
-  const unsigned rest = st.nf - ns;
-  for (unsigned c0 = 0; c0 < rest; c0 += 64) {
-    const bool act = c0 + lane < rest;
-    DeepFrame fr{};
-    if (act) fr = fst[ns + c0 + lane];
-    __builtin_amdgcn_wave_barrier();
-    if (act) store_frame(fst + c0 + lane, fr);
-    __builtin_amdgcn_wave_barrier();
-  }
-  st.nf = rest;
+  drop_bottom<MAXT>(fst, st, L, lane, ns);  // partial: the wave keeps the rest
   return 0;
+}
+
+// Direct hand-off of the bottom frame to the inbox of the wave that asked (`req`): claim its
+// inbox (open -> filling), copy the class block to the heap and the frame to the inbox with
+// write-through stores, count the task, mark the inbox full.  False (nothing changed) when the
+// requester is no longer waiting or the heap is full.
+template <int MAXT>
+__device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst, WaveState& st,
+                                              WaveLds<MAXT>& L, int lane, unsigned req,
+                                              unsigned k_open, unsigned k_filling,
+                                              unsigned k_full) {
+  if ((long long)req >= a.nwaves) return false;
+  unsigned ok = 0;
+  if (lane == 0) ok = atomicCAS(&a.inbox_state[req], k_open, k_filling) == k_open;
+  if (!uni(__shfl(ok, 0, 64))) return false;
+  const DeepFrame fr = load_frame(fst, lane);
+  const unsigned m = fr.m, wt = meta_width(fr.meta);
+  const unsigned long long npad = roundup16(m);
+  const unsigned long long bytes = (unsigned long long)(wt + 1) * npad * 8ull;
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(&a.ctl->heap_top, bytes);
+  base = uni64(bcast64(base, 0));
+  if (base + bytes > a.heap_cap) {
+    if (lane == 0) st_agent(&a.inbox_state[req], k_open);
+    return false;
+  }
+  const unsigned long long* src = (const unsigned long long*)fr.blk;
+  unsigned long long* dst = (unsigned long long*)(a.heap + base);
+  const unsigned long long tot = (unsigned long long)(wt + 1) * m;
+  for (unsigned long long e = lane; e < tot; e += 64) {
+    const unsigned long long w = e / m, k = e - w * m;
+    st_agent(dst + w * npad + k, src[w * fr.pad + fr.s0 + k]);
+  }
+  if (lane == 0) {
+    DeepFrame o;
+    o.blk = (unsigned long long)dst;
+    o.hash = fr.hash;
+    o.pad = (unsigned)npad;
+    o.s0 = 0;
+    o.m = m;
+    o.meta = make_meta(meta_depth(fr.meta), (fr.meta & kSingle) != 0, wt, 0);
+    publish_frame(a.inbox + req, o);
+    atomicAdd(&a.ctl->pending, 1ull);
+    atomicAdd(&a.ctl->handoffs, 1ull);
+  }
+  wait_stores();  // block and frame complete before the inbox turns full
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) atomicExch(&a.inbox_state[req], k_full);
+  drop_bottom<MAXT>(fst, st, L, lane, 1);
+  return true;
 }
 
 // ---- row step: member s0 against members s0+1 .. s0+m-1 (lane = candidate) ----
@@ -686,22 +742,34 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
     if (lane == 0) atomicOr(&a.ctl->error, 4u);
     return true;
   };
+  // steal mode: this wave's inbox (direct hand-off from a wave it asked for work)
+  const unsigned kOpen = (a.epoch << 2) | 1u, kFilling = (a.epoch << 2) | 2u,
+                 kFull = (a.epoch << 2) | 3u, kClosed = a.epoch << 2;
+  bool holding = false, inbox_open = false;
+  unsigned long long t = 0;
+  unsigned victim = (unsigned)((gw * 7919ull + 1) % (unsigned long long)(a.nwaves > 0 ? a.nwaves : 1));
   while (!failed) {
-    unsigned long long t = 0;
-    if (lane == 0) t = atomicAdd(&a.ctl->next_task, 1ull);
-    t = uni64(bcast64(t, 0));
+    // ---- the next task: queue ticket t, or (steal mode, while t is not published) a class
+    // another wave handed over on request ----
+    if (!holding) {
+      if (lane == 0) t = atomicAdd(&a.ctl->next_task, 1ull);
+      t = uni64(bcast64(t, 0));
+      holding = true;
+    }
+    DeepFrame tf;
     if (!a.steal) {
       if (t >= (unsigned long long)a.n_in) break;
+      tf = load_frame(a.in + t, lane);
+      holding = false;
     } else {
       // ticket t: wait on its own flag (waiting waves poll distinct addresses: one address
       // polled by thousands of waves serialises every device-scope access to it) until the task
       // is published (epoch) or the launch is over (epoch ^ kDone, written by the wave that
       // finished the last task over every ticket that can still be outstanding).  Meanwhile it
-      // asks busy waves, one mailbox at a time, to hand over their oldest open class.
-      bool done = false;
-      unsigned victim = (unsigned)((gw * 7919ull + 1) % (unsigned long long)a.nwaves);
+      // opens its inbox and asks busy waves, one mailbox at a time, for their oldest open class.
+      bool done = false, from_inbox = false;
       for (unsigned n = 0;; ++n) {
-        unsigned rdy = 0, fin = 0;
+        unsigned rdy = 0, fin = 0, inb = 0;
         if (lane == 0) {
           if (t < (unsigned long long)a.n_in) {
             rdy = 1u;
@@ -712,23 +780,50 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
           } else if ((n & 63) == 63) {  // past the queue's capacity: never published
             fin = ld_agent(&a.ctl->pending) == 0ull;
           }
-          // a failed wave never finishes its task: its error ends the wait of the others
-          if (!rdy && !fin && (n & 255) == 255) fin = ld_agent(&a.ctl->error) != 0u;
-          if (!rdy && !fin && (n & 15) == 15) {
-            if (victim != (unsigned)gw) atomicExch(&a.req[victim], a.epoch);
-            victim = (victim + 97u) % (unsigned)a.nwaves;
+          if (inbox_open) {
+            const unsigned sv = ld_agent(&a.inbox_state[gw]);
+            inb = sv == kFull;
+            // a hand-off in flight: finish receiving it before anything else
+            if (sv == kFilling) rdy = fin = 0;
+            if (rdy && !inb) {  // close the inbox before taking the ticket's task
+              const unsigned old = atomicCAS(&a.inbox_state[gw], kOpen, kClosed);
+              if (old != kOpen) rdy = 0;  // a donor claimed it meanwhile: receive that first
+            }
           }
+          // a failed wave never finishes its task: its error ends the wait of the others
+          if (!rdy && !fin && !inb && (n & 255) == 255) fin = ld_agent(&a.ctl->error) != 0u;
+        }
+        inb = uni(__shfl(inb, 0, 64));
+        if (inb) {
+          from_inbox = true;
+          break;
         }
         if (uni(__shfl(rdy, 0, 64))) break;
         if (uni(__shfl(fin, 0, 64))) { done = true; break; }
+        if (!inbox_open) {  // not published yet: open the inbox, then start asking
+          if (lane == 0) st_agent(&a.inbox_state[gw], kOpen);
+          inbox_open = true;
+        } else if (lane == 0 && (n & 7) == 1) {
+          if (victim != (unsigned)gw)
+            atomicExch(&a.req[victim], ((unsigned long long)a.epoch << 32) | (unsigned long long)(gw + 1));
+          victim = (victim + 97u) % (unsigned)a.nwaves;
+        }
         if (timed_out()) { failed = true; break; }
         wait_short(n);
       }
       if (done || failed) break;
+      if (from_inbox) {
+        tf = load_frame_agent(a.inbox + gw, lane);
+        if (lane == 0) st_agent(&a.inbox_state[gw], kClosed);
+        inbox_open = false;  // ticket t is still held
+      } else {
+        inbox_open = false;
+        holding = false;
+        tf = t >= (unsigned long long)a.n_in ? load_frame_agent(a.in + t, lane)
+                                             : load_frame(a.in + t, lane);
+      }
     }
     {
-      const DeepFrame tf = a.steal && t >= (unsigned long long)a.n_in ? load_frame_agent(a.in + t, lane)
-                                                                       : load_frame(a.in + t, lane);
       if (lane == 0) store_frame(fst, tf);
       // lanes exchange frames through memory: coherent within a wave in program order (one L1);
       // the wave barriers mark those hand-offs (the CPU emulator synchronises its lanes there)
@@ -738,6 +833,7 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
       st.mem_top = 0;
     }
     acc.budget_used = 0;
+    // ---- run the task ----
     while (st.nf > 0) {
       __builtin_amdgcn_wave_barrier();
       // bounded: a launch that runs past its deadline gives up (error bit 2) instead of holding
@@ -759,20 +855,32 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
         break;
       }
       if (a.steal && acc.budget_used >= a.budget) {
-        // a waiting wave asked (this wave's own mailbox): hand over the bottom (oldest,
-        // largest) open class and keep the rest; a lone frame goes whole (a skipped spill keeps
-        // the frames).  steal_eager: at every check (tests)
-        unsigned want = a.steal_eager ? 1u : 0u;
-        if (!want && lane == 0) {
-          want = ld_agent(&a.req[gw]) == a.epoch;
-          if (want) st_agent(&a.req[gw], 0u);
-        }
-        want = uni(__shfl(want, 0, 64));
         acc.budget_used = 0;
-        if (want && spill_frames<MAXT>(a, fst, st, L, lane, true, 1) == 0) {
-          free_blocks(L, st);
-          if (st.nf == 0) break;
-          continue;
+        if (a.steal_eager == 1) {
+          // tests: the bottom frame to the shared queue at every check (a lone frame whole)
+          if (spill_frames<MAXT>(a, fst, st, L, lane, true, 1) == 0) {
+            free_blocks(L, st);
+            if (st.nf == 0) break;
+            continue;
+          }
+        } else if (st.nf >= 2) {
+          // a waiting wave asked (this wave's own mailbox): hand the bottom (oldest, largest)
+          // open class straight to its inbox and keep the rest.  A lone frame stays (handing
+          // the whole stack over just moves the class to a wave that is asked in turn).
+          unsigned long long r = 0;
+          if (a.steal_eager == 2) {  // tests: offer to the partner wave whenever it waits
+            r = (gw ^ 1ull) < (unsigned long long)a.nwaves ? (gw ^ 1ull) + 1ull : 0ull;
+          } else if (lane == 0) {
+            r = ld_agent(&a.req[gw]);
+            if ((r >> 32) == (unsigned long long)a.epoch) st_agent(&a.req[gw], 0ull);
+            else r = 0;
+          }
+          r = uni64(bcast64(r, 0));
+          if (r && donate_bottom<MAXT>(a, fst, st, L, lane, (unsigned)(r & 0xffffffffull) - 1u,
+                                       kOpen, kFilling, kFull)) {
+            free_blocks(L, st);
+            continue;
+          }
         }
       }
       if (wt == 0 || wt > (unsigned)MAXT) {  // never produced by the host or the steps
@@ -784,13 +892,14 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
                                                                stack, lane, acc);
       free_blocks(L, st);
     }
-    if (a.steal && !failed) {  // task t is done
+    if (a.steal && !failed) {  // the task is done
       unsigned long long left = 0;
       if (lane == 0) left = atomicSub(&a.ctl->pending, 1ull);
       left = uni64(bcast64(left, 0));
       if (left == 1) {
-        // the last task: nothing can be spilled any more, so the tail is final and every
-        // ticket at or past it is dead; each wave holds at most one, so nwaves flags cover them
+        // the last task: nothing can be spilled or handed over any more, so the tail is final
+        // and every ticket at or past it is dead; each wave holds at most one, so nwaves flags
+        // cover them
         unsigned long long tail = 0;
         if (lane == 0) tail = (unsigned long long)a.n_in + ld_agent(&a.ctl->n_out);
         tail = uni64(bcast64(tail, 0));

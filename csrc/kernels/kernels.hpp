@@ -24,6 +24,7 @@ struct DeepCtl {  // per-round control + accumulated results (zeroed once per ca
   unsigned long long n_out;       // tasks spilled to the out queue (zeroed per round)
   unsigned long long heap_top;    // bytes of the out heap used (zeroed per round)
   unsigned long long pending;     // steal mode: queued + running tasks (0 = the launch is done)
+  unsigned long long handoffs;    // steal mode: classes handed to a requesting wave's inbox
   unsigned long long digest_sum, digest_xor;
   unsigned long long candidates, chunks;
   unsigned long long per_depth[64];
@@ -53,11 +54,14 @@ struct DeepArgs {
   // and published by ready[k] = epoch; waves that run out of tasks wait for them, and a busy
   // wave spills its frames when it sees a waiting wave (checked every `budget` passes)
   unsigned* ready;
-  unsigned* req;                  // [nwaves] mailboxes: epoch = a waiting wave asks for work
+  unsigned long long* req;        // [nwaves] mailboxes: epoch << 32 | requester + 1
+  DeepFrame* inbox;               // [nwaves] direct hand-offs (one frame per wave)
+  unsigned* inbox_state;          // [nwaves] epoch << 2 | closed 0 / open 1 / filling 2 / full 3
   long long nwaves;
-  unsigned epoch;                 // < 2^31
+  unsigned epoch;                 // < 2^30
   int steal;
-  int steal_eager;                // hand over at every check, asked or not (tests)
+  int steal_eager;                // tests: 1 = bottom frame to the queue at every check,
+                                  // 2 = hand-off to the partner wave (gw ^ 1) whenever it waits
 };
 int deep_max_words();
 int deep_tier(int words);     // smallest instantiated block width >= words

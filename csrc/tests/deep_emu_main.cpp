@@ -22,7 +22,8 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: deep_emu n_tx n_items mean_len genres affinity min_support [...]\n");
     return 2;
   }
-  const int64_t n_tx = std::atoll(argv[1]), n_items = std::atoll(argv[2]);
+  const int64_t n_tx = std::atoll(argv[1]);
+  int64_t n_items = std::atoll(argv[2]);
   const double mean_len = std::atof(argv[3]);
   const int genres = std::atoi(argv[4]);
   const double aff = std::atof(argv[5]), ms = std::atof(argv[6]);
@@ -39,7 +40,20 @@ int main(int argc, char** argv) {
 
   std::vector<int64_t> ptr;
   std::vector<int32_t> items;
-  synth_transactions(n_tx, n_items, mean_len, genres, aff, 0.85, 7, 1, ptr, items);
+  if (n_items < 0) {
+    // clique: every transaction holds items 0..|n_items|-1 (plus, in odd transactions, item
+    // |n_items|): one dense class whose subtree dominates, so waves run dry while one is deep
+    const int64_t k = -n_items;
+    n_items = k + 1;
+    ptr.push_back(0);
+    for (int64_t t = 0; t < n_tx; ++t) {
+      for (int64_t i = 0; i < k; ++i) items.push_back((int32_t)i);
+      if (t & 1) items.push_back((int32_t)k);
+      ptr.push_back((int64_t)items.size());
+    }
+  } else {
+    synth_transactions(n_tx, n_items, mean_len, genres, aff, 0.85, 7, 1, ptr, items);
+  }
   std::vector<uint32_t> cnt((size_t)n_items);
   count_items(ptr.data(), items.data(), n_tx, n_items, cnt.data());
   FrequentItems fi = select_frequent(cnt.data(), n_items, (uint64_t)n_tx, ms);
@@ -59,7 +73,7 @@ int main(int argc, char** argv) {
     dxor ^= t.xr;
   }
   int rounds = 0;
-  long long spilled = 0;
+  long long spilled = 0, handoffs = 0;
   for (int rank = 0; rank < world; ++rank) {
     gpu::DeepBufs b;
     gpu::DeepInput in;
@@ -78,6 +92,7 @@ int main(int argc, char** argv) {
     dxor ^= loc.dxor;
     rounds += (int)loc.round_tasks.size();
     spilled += (long long)loc.spilled_tasks;
+    handoffs += (long long)loc.handoffs;
   }
   CountResult c = mine_cpu_count(ptr.data(), items.data(), n_tx, n_items, ms, max_len, (int64_t)1 << 62, 2);
   bool ok = c.digest_sum == dsum && c.digest_xor == dxor;
@@ -85,9 +100,9 @@ int main(int argc, char** argv) {
     const uint64_t want = d < c.per_level.size() ? (uint64_t)c.per_level[d] : 0;
     if (want != per[d]) ok = false;
   }
-  std::printf("{\"F\": %lld, \"n_cpu\": %lld, \"rounds\": %d, \"spilled\": %lld, \"ok\": %s, "
-              "\"per_level\": [", (long long)F, (long long)c.n_itemsets, rounds, spilled,
-              ok ? "true" : "false");
+  std::printf("{\"F\": %lld, \"n_cpu\": %lld, \"rounds\": %d, \"spilled\": %lld, "
+              "\"handoffs\": %lld, \"ok\": %s, \"per_level\": [", (long long)F,
+              (long long)c.n_itemsets, rounds, spilled, handoffs, ok ? "true" : "false");
   for (size_t d = 1; d < 20; ++d) std::printf("%s%llu", d > 1 ? ", " : "", (unsigned long long)per[d]);
   std::printf("], \"cpu\": [");
   for (size_t d = 1; d < c.per_level.size(); ++d) std::printf("%s%lld", d > 1 ? ", " : "", (long long)c.per_level[d]);

@@ -97,7 +97,7 @@ def main() -> int:
                                   "best_s": round(best, 4), "n": d["n_itemsets"],
                                   "ok": (d["digest"] == ref[0]) if ref and not a.max_len else None,
                                   "chunks": d["chunks"], "n_rounds": len(d["round_tasks"]),
-                                  "spilled": d["spilled_tasks"],
+                                  "spilled": d["spilled_tasks"], "handoffs": d["handoffs"],
                                   "round_ms": [round(x, 1) for x in d["round_ms"][:12]]}),
                       flush=True)
         return 0
@@ -117,7 +117,8 @@ def main() -> int:
                        "level2_tasks": d["level2_tasks"], "phases_ms": d["phases_ms"],
                        "round_tasks": d["round_tasks"][:12],
                        "round_ms": [round(x, 2) for x in d["round_ms"][:12]],
-                       "n_rounds": len(d["round_tasks"]), "spilled": d["spilled_tasks"]}
+                       "n_rounds": len(d["round_tasks"]), "spilled": d["spilled_tasks"],
+                       "handoffs": d["handoffs"]}
                 if ref and a.world == 1 and not a.max_len:
                     out["verified_vs_cpu"] = d["digest"] == ref[0] and d["n_itemsets"] == ref[1]
                 print(json.dumps(out), flush=True)

@@ -70,16 +70,20 @@ def test_deep_spill_rounds(gpu_mod, budget0, budget, split_min):
 
 
 @pytest.mark.parametrize("budget,split_min,steal_idle", [(1, 2, 0), (3, 64, 0), (8, 4, 1),
-                                                         (64, 8, 1)])
+                                                         (64, 8, 1), (2, 8, 2), (256, 8, 1)])
 def test_deep_work_stealing(gpu_mod, budget, split_min, steal_idle):
-    """One launch, spilled stacks taken by waiting waves; steal_idle 0 spills at every check
-    (tens of thousands of in-launch hand-offs through the ready flags)."""
+    """One launch; waves that run dry ask busy waves for work.  steal_idle 1: direct hand-offs
+    to the asking wave's inbox (the default); 0: the bottom frame to the shared queue at every
+    check (tens of thousands of hand-offs through the ready flags); 2: a hand-off to the
+    partner wave whenever it waits."""
     tx = generate("ds1", seed=0)
     d = _gpu_miner(gpu_mod, tx).mine_deep(0.04, budget=budget, split_min=split_min,
                                           steal=True, steal_idle=steal_idle)
     assert len(d["round_tasks"]) == 1
     if steal_idle == 0:
         assert d["spilled_tasks"] > 0
+    else:
+        assert d["handoffs"] > 0, d
     _same(d, _cpu(gpu_mod, tx, 0.04))
 
 
