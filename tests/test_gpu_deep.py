@@ -82,7 +82,7 @@ def test_deep_work_stealing(gpu_mod, budget, split_min, steal_idle):
     assert len(d["round_tasks"]) == 1
     if steal_idle == 0:
         assert d["spilled_tasks"] > 0
-    else:
+    elif budget <= 64:  # (at 256 passes between checks this small problem needs no hand-off)
         assert d["handoffs"] > 0, d
     _same(d, _cpu(gpu_mod, tx, 0.04))
 
