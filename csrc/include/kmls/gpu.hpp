@@ -145,10 +145,10 @@ struct DeepBufsDeleter {
 struct DeepOpts {
   // (defaults: the best of the r3e sweep at ds1 @0.02, profiles/r3_deep_sweep_projected.log)
   unsigned long long budget0 = 1024;  // rounds: 64-lane passes a first-round task may take
-  unsigned long long budget = 256;    // steal: passes between mailbox checks (the r3j sweep:
-                                      // 50.0 ms at ds1 @0.02 vs 59.9 for the best rounds setting,
-                                      // 8-rank split 13.4 vs 18.1 ms); rounds: later-round budget
-                                      // (1024 there)
+  unsigned long long budget = 16;     // steal: passes between mailbox checks (r3s sweep with
+                                      // direct hand-offs: 8 / 16 / 64 / 256 -> 42.7 / 42.7 / 44.3
+                                      // / 51.6 ms at ds1 @0.02, 8-rank split 9.4 / 9.6 / 11.2 /
+                                      // 23.4 ms); rounds: later-round budget (1024 there)
   unsigned split_min = 8;             // spilled frames above this many members split per member
   int blocks_per_cu = 0;              // 0 = the kernel instance's occupancy (deep_waves_per_simd)
   int stack_mb = 0;                   // per-wave stack (0: KMLS_DEEP_STACK_MB or 4)
