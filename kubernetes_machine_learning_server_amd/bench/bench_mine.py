@@ -210,8 +210,9 @@ def run_config2(N, tx, names, tie, steps: int, verify: bool, deep_miner=None,
                 full_budget_s: float = 20.0) -> Dict:
     """BASELINE config 2: ds1 @ min_support 0.01 on 1 GPU."""
     ms = 0.01
-    # a 64 GB arena: the 4-item trie (1e8 nodes) then fits the fused level loop's bump region
-    # (the default 8 GB arena sent it to the chunked fallback: "device overflow code 4")
+    # a 64 GB arena for the 1e8-node 4-item trie.  (The fused level loop still hands level 3
+    # to the chunked path here: its candidate total passes the fused look-back's 2^28 bound,
+    # "device overflow code 4"; the chunked path is exact and digest-verified.)
     g = N.GpuMiner(0, 64 << 30)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     g.set_tie_rank(tie)
