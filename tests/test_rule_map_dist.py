@@ -127,12 +127,14 @@ def test_dist_rule_map_gpu_host_comm_equals_single_gpu(world):
     g = N.GpuMiner(0)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     cnt = torch.zeros(tx.n_items, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # torch's fill ran on its stream, the miner has its own
     g.item_support(cnt.data_ptr())
     torch.cuda.synchronize()
     F = g.select(cnt.cpu().numpy().view(np.uint32), tx.n_tx, MS)
     ids, _, minsup = g.frequent()
     Wp = g.words_local()
     bm = torch.zeros((F, Wp), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
     g.encode_bitmaps(bm.data_ptr(), Wp, 0)
     gram = torch.empty((F, F), dtype=torch.int32, device="cuda")
     g.pair_counts(bm.data_ptr(), Wp, gram.data_ptr(), True)
