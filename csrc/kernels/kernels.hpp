@@ -260,7 +260,7 @@ struct LevelCountArgs {
 // with the tiles' HBM stores, and a saturated PCIe link backs that path up (a level-6 trace showed
 // tile phase 1 at 42 µs with 64 copy blocks vs 19 µs without concurrent copies).  Headline A/B,
 // ms/step by copy blocks per launch: 4: 0.78, 8: 0.68, 12: 0.66, 16: 0.65-0.66, 24: 0.69, 32: 0.70,
-// 64: 0.71, 128: 0.71 (KMLS_COPY_BLOCKS overrides).
+// 64: 0.71, 128: 0.71.
 constexpr int kCopyBlocks = 16;
 // device-resident prologue (single GPU, small vocabularies): selection + root descriptor
 // without a host round trip.  select: items with cnt >= c1, ranked by (count asc, id asc)

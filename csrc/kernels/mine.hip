@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_item_support_hash(const int32_t* __r
 constexpr int kPartBits = 15;
 constexpr int kPartBins = 1 << kPartBits;
 constexpr int kPartMax = 64;     // partitions: n_items <= 2M
-constexpr int kPartGrid = 1024;  // blocks of passes 1 and 2 (KMLS_SUPPORT_GRID: up to kPartGridMax)
+constexpr int kPartGrid = 1024;  // blocks of passes 1 and 2
 constexpr int kPartGridMax = 2048;
 constexpr int kPartTile = 4096;  // items per LDS counting-sort tile (16 per thread)
 
