@@ -307,6 +307,13 @@ void register_gpu_bindings(py::module_& m) {
            py::arg("gram"), py::arg("ld"), py::arg("minsup"))
       .def("gram_mirror", &gpu::GpuMiner::gram_mirror, py::arg("gram"), py::arg("ld"), py::arg("F"),
            py::call_guard<py::gil_scoped_release>())
+      .def("rows_union", &gpu::GpuMiner::rows_union, py::arg("rows"), py::arg("Wp"), py::arg("idx"),
+           py::arg("n"), py::arg("W"), py::arg("mask"), py::call_guard<py::gil_scoped_release>())
+      .def("word_popc", &gpu::GpuMiner::word_popc, py::arg("mask"), py::arg("W"), py::arg("cnt"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("compact_rows", &gpu::GpuMiner::compact_rows, py::arg("rows"), py::arg("R"),
+           py::arg("Wp_in"), py::arg("mask"), py::arg("nzw"), py::arg("off"), py::arg("n_nz"),
+           py::arg("out"), py::arg("Wp_out"), py::call_guard<py::gil_scoped_release>())
       .def("rule_map_rows",
            [](gpu::GpuMiner& g, uintptr_t rows, int64_t ld, int64_t r0, int64_t nrows,
               uint32_t minsup) {

@@ -1096,6 +1096,30 @@ void GpuMiner::gram_mirror(uintptr_t gram_dev, int64_t ld, int64_t F) {
   kern::gram_mirror((uint32_t*)gram_dev, ld, F, (hipStream_t)stream_);
 }
 
+void GpuMiner::rows_union(uintptr_t rows, int64_t Wp, uintptr_t idx, int n, int64_t W,
+                          uintptr_t mask) {
+  KMLS_HIP(hipSetDevice(device_));
+  KMLS_CHECK(n >= 0 && W >= 0 && Wp >= W, "rows_union: Wp >= W, n >= 0");
+  kern::rows_union((const uint64_t*)rows, Wp, (const int32_t*)idx, n, W, (uint64_t*)mask,
+                   (hipStream_t)stream_);
+}
+
+void GpuMiner::word_popc(uintptr_t mask, int64_t W, uintptr_t cnt) {
+  KMLS_HIP(hipSetDevice(device_));
+  kern::word_popc((const uint64_t*)mask, W, (int32_t*)cnt, (hipStream_t)stream_);
+}
+
+void GpuMiner::compact_rows(uintptr_t rows, int64_t R, int64_t Wp_in, uintptr_t mask,
+                            uintptr_t nzw, uintptr_t off, int64_t n_nz, uintptr_t out,
+                            int64_t Wp_out) {
+  KMLS_HIP(hipSetDevice(device_));
+  KMLS_CHECK(R >= 0 && n_nz >= 0 && n_nz <= Wp_in && Wp_out * 64 >= 0,
+             "compact_rows: bad shape");
+  kern::compact_rows((const uint64_t*)rows, R, Wp_in, (const uint64_t*)mask,
+                     (const int64_t*)nzw, (const int64_t*)off, n_nz, (uint64_t*)out, Wp_out,
+                     (hipStream_t)stream_);
+}
+
 GpuMiner::RuleMap GpuMiner::rule_map_rows(uintptr_t rows_dev, int64_t ld, int64_t r0, int64_t nrows,
                                           uint32_t minsup) {
   KMLS_HIP(hipSetDevice(device_));

@@ -253,6 +253,12 @@ class GpuMiner {
   // map: count desc, tie key asc).
   void gram_mirror(uintptr_t gram_dev, int64_t ld, int64_t F);
   RuleMap rule_map_rows(uintptr_t rows_dev, int64_t ld, int64_t r0, int64_t nrows, uint32_t minsup);
+  // Item-sharded mining (parallel/item_shard.py), on this miner's stream: union mask of rows,
+  // per-word popcounts, and rows compressed onto a mask (see kern::compact_rows).
+  void rows_union(uintptr_t rows, int64_t Wp, uintptr_t idx, int n, int64_t W, uintptr_t mask);
+  void word_popc(uintptr_t mask, int64_t W, uintptr_t cnt);
+  void compact_rows(uintptr_t rows, int64_t R, int64_t Wp_in, uintptr_t mask, uintptr_t nzw,
+                    uintptr_t off, int64_t n_nz, uintptr_t out, int64_t Wp_out);
   // C[Fa][ldc] += popcount(A_i & B_j) over Wp words (ring-pass pair counting)
   void bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp, uintptr_t C,
                     int64_t ldc);

@@ -381,6 +381,15 @@ void pairs_enable_big_lds();  // once per process/device before the first pairs_
 // Multi-GPU rule map: the gram's lower triangle from its upper one (full symmetric rows), then
 // the CSR of a row block [r0, r0 + nrows) x F of it (rows by frequent rank, cons = item ids).
 void gram_mirror(uint32_t* gram, int64_t ld, int64_t F, hipStream_t s);
+// Item-sharded mining (kernels/shard.hip): OR of rows idx[0..n) -> mask[W]; per-word popcount;
+// rows [R][Wp_in] compressed onto mask (nzw: the mask's nonzero words, off: their exclusive bit
+// offsets) into a ZEROED out [R][Wp_out].
+void rows_union(const uint64_t* rows, int64_t Wp, const int32_t* idx, int n, int64_t W,
+                uint64_t* mask, hipStream_t s);
+void word_popc(const uint64_t* mask, int64_t W, int32_t* cnt, hipStream_t s);
+void compact_rows(const uint64_t* rows, int64_t R, int64_t Wp_in, const uint64_t* mask,
+                  const int64_t* nzw, const int64_t* off, int64_t n_nz, uint64_t* out,
+                  int64_t Wp_out, hipStream_t s);
 void rows_count(const uint32_t* rows, int64_t ld, int64_t nrows, int64_t F, int64_t r0,
                 uint32_t minsup, uint32_t* len_r, unsigned int* n_long, int32_t* long_rows,
                 hipStream_t s);

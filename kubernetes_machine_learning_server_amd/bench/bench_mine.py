@@ -321,7 +321,8 @@ def sampled_supports_ok(trie, ptr, items, world: int, rank: int, k: int = 64,
 
 
 def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: int = 1,
-                comm: str = "host", min_support: float = C3_MIN_SUPPORT) -> Dict:
+                comm: str = "host", min_support: float = C3_MIN_SUPPORT,
+                mode: str = "tx") -> Dict:
     """BASELINE config 3 (10M transactions x 1M items; min_support 2e-4: 14.8k frequent items)
     on all ranks of the job: transaction-DP mining (each rank generates and encodes only its
     shard; supports, the MFMA gram and per-level candidate counts all-reduced), so support /
@@ -340,7 +341,7 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
         lo, hi, _ = shard_bounds(T, world, rank)
         ptr, items = N.synth_transactions(T, shape.n_items, shape.mean_len, shape.n_genres,
                                           shape.genre_affinity, 0.85, 0, 0, lo, hi)
-        dm = DistMiner(ptr, items, shape.n_items, min_support, device=device, mode="tx",
+        dm = DistMiner(ptr, items, shape.n_items, min_support, device=device, mode=mode,
                        support_tiles=4, global_n_tx=T, arena_bytes=48 << 30)
 
         def bar():
@@ -365,14 +366,23 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
             ms = float(t.item())
         st = r["stats"]
         out = {"model": "fpgrowth-10Mx1M-synthetic", "global_batch": T, "seq_len": shape.n_items,
-               "min_support": min_support, "n_gpus": world, "parallelism": f"tx-dp{world}",
+               "min_support": min_support, "n_gpus": world,
+               "parallelism": f"tx-dp{world}" if mode == "tx" else f"item-shard{world}",
                "comm": comm, "steps": steps, "ms_per_step": round(ms, 3),
                "tx_per_s": round(T / (ms / 1000.0), 1),
                "n_frequent_items": int(st.get("n_frequent_items", 0)),
                "phases_ms": {k: round(v, 3) for k, v in (st.get("phases_ms") or {}).items()}}
-        ok = sampled_supports_ok(r["trie"] if rank == 0 else None, ptr, items, world, rank)
+        trie = r["trie"]
+        if mode == "shard":  # per-rank sub-tries -> the whole trie on rank 0
+            from ..parallel.dist_miner import gather_trie
+            trie = gather_trie(trie, rank, world, int(st["n_frequent_items"]))
+            out["bitmap_bytes_per_rank"] = int(st["own_bitmap_bytes"])
+            out["replicated_bitmap_bytes"] = int(st["replicated_bitmap_bytes"])
+            out["peak_batch_bitmap_bytes"] = int(st["peak_batch_bitmap_bytes"])
+            out["rounds"] = int(st["rounds"])
+        ok = sampled_supports_ok(trie if rank == 0 else None, ptr, items, world, rank)
         if rank == 0:
-            d = digest_of(N, r["trie"])
+            d = digest_of(N, trie)
             n = int(d["n"])
             out["n_itemsets"] = n
             out["per_level"] = d["per_depth"][1:]

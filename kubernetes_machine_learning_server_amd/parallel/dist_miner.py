@@ -139,7 +139,8 @@ class _GpuOps:
             self.comm = N.Comm(dm.rank, dm.world, uid[0], dm.device, backend)
             self.stream = None
             self.g = N.GpuMiner(dm.device, arena_bytes, 0)
-        elif (dm.world > 1 and dm.mode != "local") or dm.force_protocol or dm.mode == "item":
+        elif (dm.world > 1 and dm.mode != "local") or dm.force_protocol \
+                or dm.mode in ("item", "shard"):
             # every torch op of the protocol (allocations, fills, collectives) and every native
             # kernel run on ONE stream, so they are ordered without extra synchronisation
             torch.cuda.set_device(dm.device)
@@ -271,7 +272,7 @@ class DistMiner:
                  global_n_tx: Optional[int] = None, support_tiles: int = 4):
         """``global_n_tx`` given ⇒ (tx_ptr, items) already hold only this rank's shard (tx mode;
         large datasets are generated/loaded per shard).  ``mode``: "item" (replicated bitmaps,
-        item-sharded DFS), "replicate" (full data on every rank, device-side class partition),
+        item-sharded DFS), "shard" (item-sharded bitmaps, 1/N per rank: ``item_shard.py``), "replicate" (full data on every rank, device-side class partition),
         "tx" (transaction-DP, see module doc), "local" (every rank mines its OWN whole dataset
         with no collective: the dataset-parallel job / the weak-scaled bench) or "auto"."""
         self.world = dist.get_world_size() if (dist is not None and dist.is_initialized()) else 1
@@ -286,10 +287,10 @@ class DistMiner:
                 mode = "replicate"
             else:
                 mode = "item"
-        if mode not in ("tx", "item", "replicate", "local"):
+        if mode not in ("tx", "item", "shard", "replicate", "local"):
             raise ValueError(f"unknown mode {mode!r}")
-        if global_n_tx is not None and mode not in ("tx", "item"):
-            raise ValueError("pre-sharded input (global_n_tx) requires mode 'tx' or 'item'")
+        if global_n_tx is not None and mode not in ("tx", "item", "shard"):
+            raise ValueError("pre-sharded input (global_n_tx) requires mode 'tx', 'item' or 'shard'")
         self.mode = mode
         self.support_tiles = int(support_tiles)
         self.min_support = float(min_support)
@@ -340,6 +341,9 @@ class DistMiner:
                 st["global_itemsets"] = self.global_itemsets()
             self.last = r
             return {"stats": st, "trie": r}
+        if self.mode == "shard":
+            from .item_shard import step_shard
+            return step_shard(self, download)
         if self.mode == "tx":
             r = self.ops.mine_txdp(self, download and self.rank == 0)
             st = dict(r["stats"])
