@@ -29,6 +29,7 @@ Secondary fields:
 * ``config2``     — ds1 @0.01: deployed rule map, truncated-at-4 trie, full count-only mining
                     with the size cap raised within a time budget (N = 1).
 * ``config3``     — 10M x 1M @2e-4 (14.8k frequent items) transaction-DP over all ranks
+* ``config3_shard`` — (N > 1) the same problem with item-sharded bitmaps (1/N per rank)
                     (native RCCL communicator at N > 1 once ``native_rccl`` worked, else the
                     host one), sampled supports recounted on the host from the CSR shards.
 * ``native_rccl`` — at N > 1 the headline combine once more through the native RCCL
@@ -318,6 +319,18 @@ def main() -> int:
                 out["config3"] = c3
         except Exception as e:
             out.setdefault("errors", {})["config3"] = repr(e)[:300]
+        wd.disarm()
+
+    # ---- config 3 with item-sharded bitmaps (1/N of the bitmap per rank; N > 1 only) ----
+    if world > 1 and not args.no_config3 and not args.cpu:
+        wd.arm("config3_shard", 300)
+        try:
+            c3s = bm.run_config3(N, world, rank, device, steps=1, warmup=1, mode="shard")
+            if rank == 0:
+                c3s["digest_equal_tx"] = c3s.get("digest") == out.get("config3", {}).get("digest")
+                out["config3_shard"] = c3s
+        except Exception as e:
+            out.setdefault("errors", {})["config3_shard"] = repr(e)[:300]
         wd.disarm()
 
     if rank == 0:
