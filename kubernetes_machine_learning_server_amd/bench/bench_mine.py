@@ -380,6 +380,8 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
             out["replicated_bitmap_bytes"] = int(st["replicated_bitmap_bytes"])
             out["peak_batch_bitmap_bytes"] = int(st["peak_batch_bitmap_bytes"])
             out["rounds"] = int(st["rounds"])
+            out["max_batch_rows"] = int(st["max_batch_rows"])
+            out["shard_phases_ms"] = {k: round(v * 1e3, 1) for k, v in st["host_phases_s"].items()}
         ok = sampled_supports_ok(trie if rank == 0 else None, ptr, items, world, rank)
         if rank == 0:
             d = digest_of(N, trie)

@@ -42,6 +42,12 @@ except Exception:  # pragma: no cover
     dist = None
 
 
+# a batch's transaction budget is T / (N * BATCH_DIV) bits: smaller batches shrink every round's
+# compressed bitmap and its surviving rows (the gram cost is rows^2 x words) at the price of
+# more rounds (profiles/r3_x_item_shard.md)
+BATCH_DIV = 4
+
+
 def plan_batches(own: np.ndarray, supports: np.ndarray, cap_bits: int) -> List[np.ndarray]:
     """Consecutive groups of the owned roots ``own`` whose summed supports stay <= cap_bits (a
     root whose support alone exceeds the cap is a batch of its own)."""
@@ -246,7 +252,7 @@ def step_shard(dm, download: bool = True) -> Dict:
         # projected rounds
         fc = np.asarray(fcounts, np.int64)
         mine_items = np.arange(rank, F, world, dtype=np.int64)
-        cap = max(dm.n_tx // world, 64)
+        cap = max(dm.n_tx // (world * BATCH_DIV), 64)
         batches = plan_batches(mine_items, fc, cap)
         nb = torch.tensor([len(batches)], dtype=torch.int64,
                           device=ops.dev if dm.backend == "gpu" else "cpu")

@@ -15,6 +15,7 @@ def main():
     ap.add_argument("--min-support", type=float, default=None)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch-div", default="", help="comma list: item_shard.BATCH_DIV sweep")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -31,10 +32,14 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     N = native.require_gpu()
     ms = args.min_support if args.min_support is not None else bm.C3_MIN_SUPPORT
-    out = bm.run_config3(N, world, rank, dev, steps=args.steps, warmup=args.warmup,
-                         comm="host", min_support=ms, mode=args.mode)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    from kubernetes_machine_learning_server_amd.parallel import item_shard
+    for div in [int(x) for x in args.batch_div.split(",") if x] or [item_shard.BATCH_DIV]:
+        item_shard.BATCH_DIV = div
+        out = bm.run_config3(N, world, rank, dev, steps=args.steps, warmup=args.warmup,
+                             comm="host", min_support=ms, mode=args.mode)
+        if rank == 0:
+            out["batch_div"] = div
+            print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
