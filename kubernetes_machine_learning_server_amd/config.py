@@ -40,7 +40,7 @@ class JobSettings:
     # RULES_MODE=pairs on several GPUs: how the pair matrix is formed (parallel/pairs.py:
     # allreduce | reduce_scatter | alltoall | ring), or "trie" (mine 2-itemsets, gather sub-tries)
     pairs_strategy: str = "reduce_scatter"
-    dist_mode: str = "auto"      # KMLS_DIST_MODE: auto | tx | item | replicate (multi-GPU mining)
+    dist_mode: str = "auto"      # KMLS_DIST_MODE: auto | tx | item | shard | replicate (multi-GPU mining)
     num_gpus: int = 1
     min_confidence: float = 0.04  # legacy confidence rules (main.py:227)
     checkpoint_dir: Optional[pathlib.Path] = None  # KMLS_CHECKPOINT_DIR: phase resume

@@ -258,7 +258,7 @@ def _run_dist_job(root, world, fault="", extra=None):
     return res
 
 
-@pytest.mark.parametrize("mode", ["auto", "tx"])
+@pytest.mark.parametrize("mode", ["auto", "tx", "shard"])
 def test_distributed_job_phase_checkpoints(tmp_path, mode):
     """torchrun-style job at world size 2 (gloo + the CPU protocol): the per-rank sub-trie
     phase is checkpointed; after a crash between mining and publishing, the restarted job
