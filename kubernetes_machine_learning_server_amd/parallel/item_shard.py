@@ -162,11 +162,8 @@ class _GpuShard:
     def take_rows(self, bm, keep: np.ndarray):
         return bm.index_select(0, torch.from_numpy(keep).to(self.dev)).contiguous()
 
-    def use_subset(self, keep: np.ndarray, want_ids: np.ndarray):
+    def use_subset(self, keep: np.ndarray):
         self.g.use_frequent_subset(keep)
-        ids, _, _ = self.g.frequent()
-        if not np.array_equal(np.asarray(ids), want_ids):
-            raise RuntimeError("item_shard: the miner's frequent subset does not match the batch")
 
     def all_to_all(self, outs, ins):
         if dist.get_backend() == "nccl":
@@ -212,7 +209,7 @@ class _CpuShard:
     def take_rows(self, bm, keep: np.ndarray):
         return bm[torch.from_numpy(keep)].contiguous()
 
-    def use_subset(self, keep: np.ndarray, want_ids: np.ndarray):
+    def use_subset(self, keep: np.ndarray):
         pass  # the host miner takes ids / counts from ops.sel
 
     def all_to_all(self, outs, ins):
@@ -302,8 +299,8 @@ def step_shard(dm, download: bool = True) -> Dict:
             keep = np.flatnonzero(sh.row_counts(bm) >= minsup).astype(np.int64)
             sub = sh.take_rows(bm, keep) if len(keep) < F else bm
             del bm
+            sh.use_subset(keep)
             ops.sel = (np.asarray(ids)[keep], np.asarray(fcounts)[keep], minsup)
-            sh.use_subset(keep, ops.sel[0])
             kept_rows = max(kept_rows, len(keep))
             parts.append((keep, ops.mine(sub, wcs[rank], dm, np.isin(keep, roots).astype(np.uint8),
                                          True, True)))
