@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cctype>
 #include <condition_variable>
 #include <cstring>
 #include <ctime>
@@ -529,8 +530,6 @@ struct HttpFront::Impl {
     std::vector<Outgoing> outbox;
     std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;
     uint64_t next_id = 2;
-    char date[64] = {0};
-    time_t date_t = 0;
   };
   std::vector<std::unique_ptr<Worker>> workers;
   // slow path (FastAPI)
@@ -547,15 +546,19 @@ struct HttpFront::Impl {
       st_gpu_batches{0}, st_gpu_queries{0}, st_conns{0}, st_in{0}, st_out{0};
 
   // ---- response building ----
-  const char* date_hdr(Worker& w) {
+  // Date header cache: per calling thread (I/O threads, the GPU batcher and respond() all build
+  // responses; a per-worker cache written from several of them would race)
+  const char* date_hdr(Worker&) {
+    thread_local time_t date_t = 0;
+    thread_local char date[64] = {0};
     const time_t now = std::time(nullptr);
-    if (now != w.date_t) {
+    if (now != date_t) {
       struct tm g;
       gmtime_r(&now, &g);
-      std::strftime(w.date, sizeof w.date, "%a, %d %b %Y %H:%M:%S GMT", &g);
-      w.date_t = now;
+      std::strftime(date, sizeof date, "%a, %d %b %Y %H:%M:%S GMT", &g);
+      date_t = now;
     }
-    return w.date;
+    return date;
   }
   std::string json_response(Worker& w, const std::string& body, bool keep_alive) {
     std::string r;
@@ -710,7 +713,8 @@ struct HttpFront::Impl {
       r.headers.emplace_back(std::move(name), std::move(val));
       p = e + 2;
     }
-    // body
+    // body (both framings at once is a request-smuggling vector: refuse it)
+    if (chunked && clen >= 0) return -1;
     size_t consumed = hlen;
     if (chunked) {
       size_t pos = hlen;
@@ -719,9 +723,18 @@ struct HttpFront::Impl {
         const char* ce = (const char*)memmem(base + pos, avail - pos, "\r\n", 2);
         if (!ce) goto need_more;
         const std::string hx(base + pos, (size_t)(ce - (base + pos)));
-        char* endp = nullptr;
-        const unsigned long long sz = std::strtoull(hx.c_str(), &endp, 16);
-        if (endp == hx.c_str()) return -1;
+        // chunk-size: 1-16 hex digits, optionally followed by ";ext" (no sign, no blanks, no
+        // overflow), and never more than what is left of the body budget
+        size_t nd = 0;
+        unsigned long long sz = 0;
+        while (nd < hx.size() && std::isxdigit((unsigned char)hx[nd])) {
+          if (nd == 16) return -1;
+          const char ch = hx[nd];
+          sz = (sz << 4) | (unsigned long long)(ch <= '9' ? ch - '0' : (ch | 0x20) - 'a' + 10);
+          ++nd;
+        }
+        if (nd == 0 || (nd < hx.size() && hx[nd] != ';')) return -1;
+        if (sz > kMaxBody - body.size()) return -1;
         pos = (size_t)(ce - base) + 2;
         if (sz == 0) {  // trailers until an empty line
           const char* te = (const char*)memmem(base + pos, avail - pos, "\r\n", 2);
@@ -733,8 +746,8 @@ struct HttpFront::Impl {
           pos += 2;
           break;
         }
-        if (body.size() + sz > kMaxBody) return -1;
-        if (avail - pos < sz + 2) goto need_more;
+        if (avail - pos < sz || avail - pos - sz < 2) goto need_more;
+        if (base[pos + sz] != '\r' || base[pos + sz + 1] != '\n') return -1;
         body.append(base + pos, (size_t)sz);
         pos += (size_t)sz + 2;
       }
@@ -834,14 +847,19 @@ struct HttpFront::Impl {
   bool pump(Worker& w, int wi, Conn& c) {
     while (!c.busy && !c.close_after) {
       Request r;
-      const int st = parse_request(w, c, r);
+      int st = -1;
+      try {  // a malformed request closes its own connection, never the I/O thread
+        st = parse_request(w, c, r);
+        if (st > 0) handle(w, wi, c, r);
+      } catch (const std::exception&) {
+        st = -1;
+      }
       if (st < 0) {
         c.out += "HTTP/1.1 400 Bad Request\r\ncontent-length: 0\r\nconnection: close\r\n\r\n";
         c.close_after = true;
         break;
       }
       if (st == 0) break;
-      handle(w, wi, c, r);
     }
     return flush(w, c);
   }

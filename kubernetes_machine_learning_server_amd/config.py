@@ -47,6 +47,15 @@ class JobSettings:
     dist_timeout_s: float = 600.0      # KMLS_DIST_TIMEOUT_S: process-group init + collectives
     sweep_timeout_s: float = 86400.0   # KMLS_SWEEP_TIMEOUT_S: ranks waiting for rank 0's sweep
 
+    DIST_MODES = ("auto", "tx", "item", "shard", "replicate")
+
+    def __post_init__(self):
+        # 'local' (every rank mines the whole dataset) is a DistMiner test mode: in the job it
+        # would gather N copies of every itemset into the rule map
+        if self.dist_mode not in self.DIST_MODES:
+            raise ValueError(f"KMLS_DIST_MODE={self.dist_mode!r}: expected one of "
+                             f"{', '.join(self.DIST_MODES)}")
+
     @property
     def dataset_list_file(self) -> pathlib.Path:
         return self.base_dir / "datasets_list.txt"

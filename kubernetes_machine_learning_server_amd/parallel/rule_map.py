@@ -320,18 +320,26 @@ class DistRuleMap:
         if os.environ.get("KMLS_FAULT") == "rulemap_after_csr":
             raise RuntimeError("injected fault at rulemap_after_csr")
         lens = np.diff(np.asarray(loc["row_ptr"], np.int64))
+        # every rank's rule_map_rows status rides along (bit 1: fill overflow, bit 2: a row
+        # sorted past kSortBig): a bad row block on ANY rank fails the assembled map
         got_l = gather_arrays({"lens": lens.astype(np.int64)}, self.rank, self.world)
+        got_s = gather_arrays({"status": np.array([int(loc.get("status", 0))], np.int64)},
+                              self.rank, self.world)
         got_e = gather_arrays({"cons": np.asarray(loc["cons"], np.int32),
                                "count": np.asarray(loc["count"], np.uint32).view(np.int32)},
                               self.rank, self.world)
         ph["gather"] = time.perf_counter() - t0
         if self.rank != 0:
             return None
+        status = int(np.bitwise_or.reduce(np.asarray(got_s["status"], np.int64)))
+        if status:
+            raise RuntimeError(f"DistRuleMap: rule_map_rows status {status} on some rank "
+                               "(1: fill overflow, 2: unsorted long row)")
         out = assemble_by_id(ids, got_l["lens"][:F], got_e["cons"],
                              got_e["count"].view(np.uint32), self.n_items)
         ph["assemble"] = time.perf_counter() - t0
         out.update(ids=ids, fcounts=fcounts, minsup=minsup, n_frequent_items=F,
-                   status=int(loc.get("status", 0)), resumed_from_phase=lvl,
+                   status=status, resumed_from_phase=lvl,
                    phases_ms={k: round(v * 1e3, 3) for k, v in ph.items()})
         return out
 

@@ -189,6 +189,27 @@ def test_http_framing(server):
     assert _raw(server.port, b"HELLO\r\n\r\n").startswith(b"HTTP/1.1 400")
 
 
+def test_malformed_chunks_close_only_their_connection(server):
+    """negative / overflowing / oversized chunk sizes, a missing CRLF after the chunk
+    data and TE + CL together are answered 400 on their own connection; the server lives on."""
+    head = (b"POST /api/recommend/ HTTP/1.1\r\nhost: x\r\ncontent-type: application/json\r\n"
+            b"transfer-encoding: chunked\r\n\r\n")
+    bad = [
+        head + b"2\r\nab\r\n-2\r\n" + b"X" * 64,
+        head + b"2\r\nab\r\nfffffffffffffffe\r\n" + b"X" * 64,
+        head + b"10000000000000000\r\n" + b"X" * 64,
+        head + b" 2\r\nab\r\n0\r\n\r\n",
+        head + b"%x\r\n" % (17 << 20) + b"X" * 64,
+        head + b"2\r\nabXY0\r\n\r\n",
+        head.replace(b"\r\n\r\n", b"\r\ncontent-length: 5\r\n\r\n") + b"0\r\n\r\n",
+    ]
+    for req in bad:
+        assert _raw(server.port, req, wait=0.2).startswith(b"HTTP/1.1 400"), req
+    body = json.dumps({"songs": ["x"]}).encode()
+    ok = head + b"%x;ext=1\r\n%s\r\n0\r\n\r\n" % (len(body), body)
+    assert _raw(server.port, ok).startswith(b"HTTP/1.1 200 OK")
+
+
 def test_odd_names_escape_like_json_dumps(tmp_path):
     pk = tmp_path / "api-data" / "pickles"
     pk.mkdir(parents=True)

@@ -99,6 +99,16 @@ def test_no_datasets_raises(tmp_path):
         rot.get_dataset_list(cfg)
 
 
+def test_dist_mode_validated(tmp_path, monkeypatch):
+    """'local' would put every itemset N times into the distributed job's rule map."""
+    from kubernetes_machine_learning_server_amd.config import JobSettings
+    monkeypatch.setenv("KMLS_DIST_MODE", "local")
+    with pytest.raises(ValueError, match="KMLS_DIST_MODE"):
+        JobSettings.from_env(dotenv=False)
+    monkeypatch.setenv("KMLS_DIST_MODE", "Shard")
+    assert JobSettings.from_env(dotenv=False).dist_mode == "shard"
+
+
 def test_artist_validation_raises(tmp_path):
     ds = tmp_path / "datasets"
     ds.mkdir()
