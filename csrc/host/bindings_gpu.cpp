@@ -45,6 +45,8 @@ py::dict result_to_dict(gpu::GpuMineResult&& r) {
   s["seconds"] = r.stats.seconds;
   s["arena_high_water"] = r.arena_high_water;
   s["levels_path"] = r.levels_path;
+  s["level2_method"] = r.level2_method;
+  s["cooc_pairs"] = r.cooc_pairs;
   py::dict ph;
   for (auto& p : r.phases) ph[py::str(p.name)] = p.ms;
   s["phases_ms"] = ph;
@@ -289,6 +291,21 @@ void register_gpu_bindings(py::module_& m) {
       .def("words_local", &gpu::GpuMiner::words_local)
       .def("encode_bitmaps", &gpu::GpuMiner::encode_bitmaps, py::call_guard<py::gil_scoped_release>())
       .def("pair_counts", &gpu::GpuMiner::pair_counts, py::call_guard<py::gil_scoped_release>())
+      .def("pair_counts_csr", &gpu::GpuMiner::pair_counts_csr, py::arg("out"), py::arg("ld"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("cooc_preferred", &gpu::GpuMiner::cooc_preferred,
+           py::call_guard<py::gil_scoped_release>())
+      .def("cooc_stats", [](gpu::GpuMiner& g) {
+        gpu::GpuMiner::CoocStats st;
+        {
+          py::gil_scoped_release nogil;
+          st = g.cooc_stats();
+        }
+        py::dict d;
+        d["pairs"] = st.pairs;
+        d["max_k"] = st.max_k;
+        return d;
+      })
       .def("rule_map_from_gram",
            [](gpu::GpuMiner& g, uintptr_t gram, int64_t ld, uint32_t minsup) {
              gpu::GpuMiner::RuleMap m;

@@ -731,6 +731,7 @@ GpuMiner::~GpuMiner() {
   if (d_tx_ptr_) (void)hipFree(d_tx_ptr_);
   if (d_items_) (void)hipFree(d_items_);
   if (d_rank_of_) (void)hipFree(d_rank_of_);
+  if (d_cooc_) (void)hipFree(d_cooc_);
   if (d_fmask_) (void)hipFree(d_fmask_);
   if (d_fgroup_) (void)hipFree(d_fgroup_);
   if (d_c2r_) (void)hipFree(d_c2r_);
@@ -1016,6 +1017,54 @@ void GpuMiner::pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev
     kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp_total, F, (uint32_t*)out_dev, s);
 }
 
+GpuMiner::CoocStats GpuMiner::cooc_stats() {
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  CoocStats st;
+  if (!d_cooc_) KMLS_HIP(hipMalloc((void**)&d_cooc_, 4 * sizeof(unsigned long long)));
+  KMLS_HIP(hipMemsetAsync(d_cooc_, 0, 4 * sizeof(unsigned long long), s));
+  if (n_tx_ > 0 && !fi_.ids.empty())
+    kern::cooc_stats(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, d_fmask_, d_cooc_, n_cus_, s);
+  unsigned long long h[2] = {0, 0};
+  KMLS_HIP(hipMemcpyAsync(h, d_cooc_, sizeof h, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  st.pairs = h[0];
+  st.max_k = h[1];
+  return st;
+}
+
+bool GpuMiner::pair_counts_csr(uintptr_t out_dev, int64_t ld) {
+  KMLS_HIP(hipSetDevice(device_));
+  const int64_t F = (int64_t)fi_.ids.size();
+  KMLS_CHECK(ld >= F, "pair_counts_csr: ld >= F");
+  hipStream_t s = (hipStream_t)stream_;
+  const CoocStats st = cooc_stats();
+  if (st.max_k > (uint64_t)kern::cooc_max_k()) return false;
+  KMLS_HIP(hipMemsetAsync((void*)out_dev, 0, (size_t)F * ld * sizeof(uint32_t), s));
+  KMLS_HIP(hipMemsetAsync(d_cooc_ + 2, 0, sizeof(unsigned long long), s));
+  kern::cooc_count(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, d_fmask_, F, (uint32_t*)out_dev, ld,
+                   (unsigned*)(d_cooc_ + 2), n_cus_, s);
+  return true;
+}
+
+bool GpuMiner::cooc_cheaper(int64_t F, int64_t Wp, int64_t nnz, const CoocStats& st) {
+  if (st.max_k > (uint64_t)kern::cooc_max_k()) return false;
+  // rates: the bit-GEMM ~2.7e15 bit-ANDs/s (config 5, profiles/r3_n_config5_w1.json.log); the
+  // horizontal count ~1.5e10 pair atomics/s + two CSR passes (rank gathers) at ~5e9 items/s
+  const double gemm_ms = 0.5 * (double)F * (double)F * (double)Wp * 64.0 / 2.7e12;
+  const double cooc_ms = (double)st.pairs / 1.5e7 + 2.0 * (double)nnz / 5e6;
+  return cooc_ms < gemm_ms;
+}
+
+bool GpuMiner::cooc_preferred() {
+  if (words_local() < 1024 || fi_.ids.empty()) return false;
+  const long long h = test_hook("cooc", 1);
+  if (h == 0) return false;
+  const CoocStats st = cooc_stats();
+  if (st.max_k > (uint64_t)kern::cooc_max_k()) return false;
+  return h == 2 || cooc_cheaper((int64_t)fi_.ids.size(), words_local(), nnz_, st);
+}
+
 GpuMiner::RuleMap GpuMiner::rule_map_from_gram(uintptr_t gram_dev, int64_t ld, uint32_t minsup) {
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
@@ -1265,12 +1314,24 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     // level 2 through the bit-GEMM (LDS-tiled, 64x64 tiles) when the dense F x F fits
     if (F <= 32768 && cfg.level2_gram) {
       uint32_t* gram = (uint32_t*)arena_->push((size_t)F * F * sizeof(uint32_t));
-      KMLS_HIP(hipMemsetAsync(gram, 0, (size_t)F * F * sizeof(uint32_t), s));
-      // matrix cores for long rows (large T): the int8 MFMA path moves 8x more MACs per byte
-      if (gram_popcount_forced() ? cfg.level2_mfma : (cfg.level2_mfma || Wp >= 4096))
-        kern::pair_gram_mfma((const uint64_t*)bm_dev, Wp, F, gram, s);
-      else
-        kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);
+      // sparse large data: count the pairs where they occur (cooc.hip) when the cost model says
+      // so (only for bitmaps of this miner's own CSR shard: mine_txdp / the host path of mine)
+      bool sparse = false;
+      if (gram_csr_ok_ && Wp >= 1024 && test_hook("cooc", 1) != 0) {
+        const CoocStats st = cooc_stats();
+        sparse = test_hook("cooc", 1) == 2 || cooc_cheaper(F, Wp, nnz_, st);
+        res.level2_method = sparse ? "cooc" : "gram";
+        res.cooc_pairs = (int64_t)st.pairs;
+      }
+      if (!(sparse && pair_counts_csr((uintptr_t)gram, F))) {
+        if (sparse) res.level2_method = "gram (cooc declined)";
+        KMLS_HIP(hipMemsetAsync(gram, 0, (size_t)F * F * sizeof(uint32_t), s));
+        // matrix cores for long rows (large T): the int8 MFMA path moves 8x more MACs per byte
+        if (gram_popcount_forced() ? cfg.level2_mfma : (cfg.level2_mfma || Wp >= 4096))
+          kern::pair_gram_mfma((const uint64_t*)bm_dev, Wp, F, gram, s);
+        else
+          kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);
+      }
       if (comm_) comm_->all_reduce(gram, gram, (size_t)F * F, CommDtype::U32, false, s);
       run.gram = gram;
     }
@@ -1892,6 +1953,11 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download, bool prefetch
   for (int attempt = 0;; ++attempt) {
     const size_t mark = arena_->mark();
     try {
+      struct CsrFlag {  // the bitmaps are this miner's own CSR (level-2 cooc allowed)
+        bool& f;
+        explicit CsrFlag(bool& x) : f(x) { f = true; }
+        ~CsrFlag() { f = false; }
+      } flag(gram_csr_ok_);
       r = mine_bitmaps((uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
       break;
     } catch (const ArenaExhausted& ex) {
@@ -1981,14 +2047,17 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
   KMLS_HIP(hipEventRecord(e2.e, s));
   // 4. level loop with all-reduced candidate counts
   comm_ = comm;
+  gram_csr_ok_ = true;
   GpuMineResult r;
   try {
     r = mine_bitmaps((uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
   } catch (...) {
     comm_ = nullptr;
+    gram_csr_ok_ = false;
     throw;
   }
   comm_ = nullptr;
+  gram_csr_ok_ = false;
   std::vector<Phase> ph;
   ph.push_back({"support_tiles+allreduce+select", elapsed(e0, e1)});
   ph.push_back({"encode_bitmap", elapsed(e1, e2)});

@@ -82,6 +82,8 @@ struct GpuMineResult {
   std::vector<Phase> phases;  // hipEvent-timed phases
   int64_t arena_high_water = 0;
   std::string levels_path = "none";  // "fused" | "chunked" | "persistent" | "none"
+  std::string level2_method = "gram";  // "gram" (bit-GEMM) | "cooc" (horizontal pair count)
+  int64_t cooc_pairs = -1;             // sum_t k_t(k_t-1)/2 of the shard when it was measured
   // rule map (cfg.rule_index): CSR by item id, rows sorted by (count desc, tie key asc); pinned
   int64_t idx_nnz = -1;  // -1: not built
   int64_t n_items_idx = 0;  // row_ptr has n_items_idx entries (n_items + 1)
@@ -235,6 +237,20 @@ class GpuMiner {
   // count[F][F] (row-major, only i<j valid) via the bit-GEMM kernels. Used by the rule-map
   // fast path and by the multi-GPU pair all-reduce.
   void pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev, bool use_mfma);
+  // The same gram of the RESIDENT CSR shard counted horizontally (kern::cooc_count: every
+  // co-occurring frequent pair once, no bitmaps), out[F][ld] zeroed here.  Sparse data (the
+  // large BASELINE shapes) pays sum_t k_t^2/2 atomics instead of F^2 T/2 bit-ANDs.  False (out
+  // untouched) when a transaction holds more than kern::cooc_max_k() frequent items.
+  struct CoocStats {
+    uint64_t pairs = 0;  // sum_t k_t (k_t - 1) / 2
+    uint64_t max_k = 0;
+  };
+  CoocStats cooc_stats();
+  bool pair_counts_csr(uintptr_t out_dev, int64_t ld);
+  // level-2 cost model: the horizontal count is predicted cheaper than the bit-GEMM over Wp words
+  static bool cooc_cheaper(int64_t F, int64_t Wp, int64_t nnz, const CoocStats& st);
+  // the model applied to this shard and the last select() (one stats pass; false below 64k tx)
+  bool cooc_preferred();
   // Rule map (O10 pairs_to_csr) from a pair-count matrix already on the device (upper triangle,
   // rank order of the last select(), row stride ld): CSR by item id, rows by (count desc, tie
   // key asc).  For callers that own the gram (the large-shape pairs pipeline); the resident
@@ -314,6 +330,8 @@ class GpuMiner {
   std::unique_ptr<DeepBufs, DeepBufsDeleter> deep_;  // count-only deep miner buffers
   std::unique_ptr<GraphCache> graph_;  // steady-state hipGraph of mine_resident
   Comm* comm_ = nullptr;          // set during mine_txdp: level counts are all-reduced
+  bool gram_csr_ok_ = false;      // mine_bitmaps' bitmaps are this miner's own CSR shard
+  unsigned long long* d_cooc_ = nullptr;  // [3]: cooc stats (pairs, max k) + error flag
   std::vector<int64_t> tile_tx_;  // 65 evenly spaced transaction boundaries of the shard
   std::vector<int64_t> tile_nnz_; // and their item offsets
   int64_t last_nodes_ = 0;        // size of the previous trie (pinned download sizing)

@@ -160,6 +160,17 @@ void extend_materialize(const uint64_t* bm, int64_t Wp, const int64_t* cand_off,
 // dense upper-triangular pair counts over a single class of F rows (level 2 bit-GEMM)
 void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
 void pair_gram_mfma(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t s);
+// Horizontal co-occurrence counting (cooc.hip): level-2 supports of sparse data from the
+// transaction CSR.  cooc_stats adds sum_t k_t(k_t-1)/2 to out[0] and max k_t into out[1] (k_t =
+// frequent items of transaction t; out zeroed by the caller).  cooc_count adds every co-occurring
+// frequent pair into gram[lo * ld + hi] (rank order, upper triangle; gram zeroed by the caller);
+// needs max k_t <= cooc_max_k() (err |= 1 otherwise).
+int cooc_max_k();
+void cooc_stats(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, const int32_t* rank_of,
+                const uint32_t* fmask, unsigned long long* out, int n_cus, hipStream_t s);
+void cooc_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, const int32_t* rank_of,
+                const uint32_t* fmask, int64_t F, uint32_t* gram, int64_t ld, unsigned* err,
+                int n_cus, hipStream_t s);
 // same with F read from the device (grid and row stride sized for F_max)
 void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, int64_t F_max,
                             uint32_t* out, hipStream_t s);

@@ -258,27 +258,48 @@ def rule_map_main(args) -> int:
     F = len(ids)
     Ws = rm.ops.Ws
     out.update({"ms_per_step": round(ms, 1), "n_frequent_items": int(F),
-                "bitmap_gb_per_rank": round(F * Ws * 8 / 1e9, 1),
-                "bitmap_gb_total": round(F * Ws * 8 * world / 1e9, 1),
+                "bitmap_gb_per_rank": (round(F * Ws * 8 / 1e9, 1)
+                                       if "bm" in rm.ops.held else 0.0),
+                "bitmap_gb_replicated_equiv": round(F * Ws * 8 * world / 1e9, 1),
                 "gram_gb": round(F * F * 4 / 1e9, 2),
                 "hbm_gb_allocated_rank0": round(torch.cuda.max_memory_allocated() / 1e9, 1)})
     if rank == 0:
         out.update({"rule_map_entries": int(r["nnz"]), "rule_map_status": int(r["status"]),
                     "frequent_pairs": int(r["nnz"]) // 2, "phases_ms_rank0": r["phases_ms"]})
-    # 1. each rank's shard gram rows re-counted by the popcount bit-GEMM (independent kernel)
-    bm, gram = rm.ops.held["bm"], rm.ops.held["gram"]
+    # 1. each rank's shard gram rows re-counted independently: by the popcount bit-GEMM over the
+    # shard's bitmaps when the gram came from them, by the host from the shard's CSR when the
+    # gram was counted horizontally (cooc.hip: no bitmaps exist)
+    out["level2_method"] = getattr(rm.ops, "method", "gram")
+    gram = rm.ops.held["gram"]
+    bm = rm.ops.held.get("bm")
     k = min(args.verify_rows, F)
-    chk = torch.zeros((k, F), dtype=torch.int32, device="cuda")
-    g.bitgemm_rect(bm.data_ptr(), k, bm.data_ptr(), F, Ws, chk.data_ptr(), F)
-    torch.cuda.synchronize()
     gm = gram[:k, :F].cpu().numpy()
-    ck = chk.cpu().numpy()
+    if bm is not None:
+        chk = torch.zeros((k, F), dtype=torch.int32, device="cuda")
+        g.bitgemm_rect(bm.data_ptr(), k, bm.data_ptr(), F, Ws, chk.data_ptr(), F)
+        torch.cuda.synchronize()
+        ck = chk.cpu().numpy()
+        del chk
+    else:
+        rank_of = np.full(I, -1, np.int64)
+        rank_of[ids] = np.arange(F)
+        sel = np.zeros(I, bool)
+        sel[ids[:k]] = True
+        pos_ = np.flatnonzero(sel[items])           # occurrences of the k checked items
+        rows_r = rank_of[items[pos_]]
+        txs = np.searchsorted(ptr, pos_, side="right") - 1
+        lens = (ptr[txs + 1] - ptr[txs]).astype(np.int64)
+        first = np.repeat(ptr[txs] - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)
+        seg = items[first + np.arange(int(lens.sum()))]   # every item of those transactions
+        rk = rank_of[seg]
+        rr = np.repeat(rows_r, lens)
+        keep = rk >= 0
+        ck = np.bincount(rr[keep] * F + rk[keep], minlength=k * F).reshape(k, F)
     # (the gram holds the mirrored shard counts before the reduce-scatter: full rows, so every
     # off-diagonal entry of the k rows is compared — upper entries and their mirror images)
     off = np.ones(gm.shape, bool)
     off[np.arange(k), np.arange(k)] = False
-    ok_rows = bool(np.array_equal(gm[off], ck[off]))
-    del chk
+    ok_rows = bool(np.array_equal(gm[off].astype(np.int64), ck[off].astype(np.int64)))
     # 2. sampled rule-map rows vs host co-occurrence counts, summed over the shards
     rng = np.random.default_rng(1)
     sample = np.sort(rng.choice(ids, size=min(6, F), replace=False)).astype(np.int32)

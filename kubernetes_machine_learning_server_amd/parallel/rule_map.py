@@ -138,19 +138,29 @@ class _Gpu:
         return F, np.asarray(ids), np.asarray(fcounts), int(minsup)
 
     def gram_rows(self, rm: "DistRuleMap", F: int):
-        """This rank's rows of the summed, mirrored gram (device tensor [per][F])."""
+        """This rank's rows of the summed, mirrored gram (device tensor [per][F]).
+
+        The shard's gram is counted horizontally from its CSR (``cooc.hip``: every co-occurring
+        frequent pair once; no bitmaps at all) when the cost model prefers it — at config 5
+        (~7 frequent items per transaction) by orders of magnitude — else through the shard's
+        tid-bitmaps and the MFMA bit-GEMM."""
         per, _, _ = row_block(F, rm.world, rm.rank)
         with torch.cuda.stream(self.stream):
-            bm = self.buf("bm", (max(F, 1), self.Ws), torch.int64)
-            if self.Ws > self.used:
-                bm[:, self.used:] = 0
-            if F:
-                self.g.encode_bitmaps(bm.data_ptr(), self.Ws, 0)
             gram = self.buf("gram", (per * rm.world, max(F, 1)), torch.int32)
             if per * rm.world > F:
                 gram[F:] = 0
+            self.method = "none"
             if F:
-                self.g.pair_counts(bm.data_ptr(), self.Ws, gram.data_ptr(), True)
+                if self.g.cooc_preferred() and self.g.pair_counts_csr(gram.data_ptr(), F):
+                    self.method = "cooc"
+                    self.held.pop("bm", None)
+                else:
+                    self.method = "gram"
+                    bm = self.buf("bm", (max(F, 1), self.Ws), torch.int64)
+                    if self.Ws > self.used:
+                        bm[:, self.used:] = 0
+                    self.g.encode_bitmaps(bm.data_ptr(), self.Ws, 0)
+                    self.g.pair_counts(bm.data_ptr(), self.Ws, gram.data_ptr(), True)
                 self.g.gram_mirror(gram.data_ptr(), F, F)
             if self.comm is None:
                 return gram
@@ -340,6 +350,7 @@ class DistRuleMap:
         ph["assemble"] = time.perf_counter() - t0
         out.update(ids=ids, fcounts=fcounts, minsup=minsup, n_frequent_items=F,
                    status=status, resumed_from_phase=lvl,
+                   level2_method=getattr(ops, "method", "gram"),
                    phases_ms={k: round(v * 1e3, 3) for k, v in ph.items()})
         return out
 
