@@ -175,18 +175,44 @@ def mine_rules_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_su
         merged = sub if rank == 0 else None
     else:
         merged = gather_trie(sub, rank, world, F)
+    del dm  # its device buffers go before the rule map's
+    # the deployed artifact (rules.idx / recommendations.pickle = the pair-support rows,
+    # main.py:282-304) through the distributed rule map: every rank counts its transaction
+    # shard's pairs, row blocks are reduce-scattered, each rank builds the CSR of its rows
+    rmap = rule_map_distributed(cfg, tx, min_support, rank, world, local)
     if rank != 0:
         return None
     trie = ItemsetTrie(merged["parent"], merged["item"], merged["count"], merged["depth"],
                        tx.n_tx, min_support, st, tx.names)
-    idx = build_index_from_trie(trie.parent, trie.item, trie.count, trie.depth, tx.n_tx,
-                                len(tx.names), tx.names)
+    idx = index_from_device_csr(rmap, len(tx.names), rmap["ids"], tx.n_tx, tx.names)
+    trie.stats["rule_map"] = f"distributed-x{world}({rmap.get('level2_method', 'gram')})"
     missing = total_songs - idx.n_keys
     dur = time.perf_counter() - t0
     print("Songs without recommendations:", missing)
     print(f"Time elapsed in rule generation: {format_timedelta(dur)}")
     info = f"min_support: {min_support} \tmissing songs: {missing} \ttime: {format_timedelta(dur)}"
     return idx, trie, info, (missing, dur)
+
+
+def rule_map_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float,
+                         rank: int, world: int, local: int) -> Optional[Dict]:
+    """``parallel.rule_map.DistRuleMap`` over this rank's transaction shard (every rank holds
+    the whole dataset; the shards are the same contiguous ranges the tx-DP miner uses).  The
+    item-id CSR comes back on rank 0 (None elsewhere), rows ordered count desc, name asc: the
+    same bytes as the single-process index."""
+    from ..parallel.dist_miner import shard_bounds
+    from ..parallel.rule_map import DistRuleMap
+    from ..serve.index import name_tie_rank
+    lo, hi, _ = shard_bounds(tx.n_tx, world, rank)
+    ptr = np.asarray(tx.tx_ptr[lo:hi + 1], np.int64)
+    its = np.ascontiguousarray(tx.items[int(ptr[0]):int(ptr[-1])], np.int32)
+    rm = DistRuleMap(ptr - ptr[0], its, len(tx.names), tx.n_tx, min_support, device=local,
+                     backend="cpu" if cfg.miner == "cpu" else "gpu")
+    try:
+        rm.set_tie_rank(name_tie_rank([str(n) for n in tx.names]))
+        return rm.step()
+    finally:
+        rm.release()
 
 
 def resume_from_checkpoint(ck: PhaseCheckpoint, tx: pp.PlaylistTransactions, min_support: float,

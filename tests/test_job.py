@@ -289,6 +289,11 @@ def test_distributed_job_phase_checkpoints(tmp_path, mode):
     ref = job.run(job_settings(single))
     assert summary["n_itemsets"] == ref["n_itemsets"] and summary["n_keys"] == ref["n_keys"]
     assert rec_dict(tmp_path) == rec_dict(single)
+    # the deployed index comes from the distributed rule map, byte-equal to one process's
+    idx_name = job.RULES_INDEX_FILE
+    assert (tmp_path / "api-data" / "pickles" / idx_name).read_bytes() == \
+        (single / "api-data" / "pickles" / idx_name).read_bytes()
+    assert summary["rule_map"].startswith("distributed-x2")
     assert not list((tmp_path / "ck").rglob("*.npz"))  # cleared after success
 
 
