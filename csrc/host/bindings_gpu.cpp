@@ -47,6 +47,7 @@ py::dict result_to_dict(gpu::GpuMineResult&& r) {
   s["levels_path"] = r.levels_path;
   s["level2_method"] = r.level2_method;
   s["cooc_pairs"] = r.cooc_pairs;
+  s["level2_comm"] = r.level2_comm;
   py::dict ph;
   for (auto& p : r.phases) ph[py::str(p.name)] = p.ms;
   s["phases_ms"] = ph;

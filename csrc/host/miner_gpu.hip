@@ -1056,6 +1056,41 @@ bool GpuMiner::cooc_cheaper(int64_t F, int64_t Wp, int64_t nnz, const CoocStats&
   return cooc_ms < gemm_ms;
 }
 
+// tx-DP level 2: the shard grams are summed by a reduce-scatter of row blocks (rank g owns rows
+// [g*per, (g+1)*per), all F columns: (N-1)/N of the gram per rank instead of an all-reduce's
+// 2(N-1)/N), each rank keeps the frequent upper entries of its rows, and one all-gather of those
+// (row, col, count) triples — a few thousand at configs 3/5 — rebuilds on every rank a dense gram
+// holding only the frequent pairs (the level loop reads gram[a][b] >= minsup, nothing else).
+void GpuMiner::txdp_gram_combine(uint32_t* gram, int64_t F, int64_t per, uint32_t minsup) {
+  hipStream_t s = (hipStream_t)stream_;
+  const int W = comm_->world(), R = comm_->rank();
+  if (!d_cooc_) KMLS_HIP(hipMalloc((void**)&d_cooc_, 4 * sizeof(unsigned long long)));
+  const size_t mark = arena_->mark();
+  uint32_t* rows = (uint32_t*)arena_->push((size_t)std::max<int64_t>(per, 1) * F * sizeof(uint32_t));
+  comm_->reduce_scatter(gram, rows, (size_t)per * F, CommDtype::U32, false, s);
+  const int64_t r0 = std::min<int64_t>(F, (int64_t)R * per);
+  const int64_t nrows = std::max<int64_t>(0, std::min<int64_t>(F, r0 + per) - r0);
+  KMLS_HIP(hipMemsetAsync(d_cooc_, 0, sizeof(unsigned long long), s));
+  kern::gram_frequent(rows, F, r0, nrows, F, minsup, d_cooc_, nullptr, s);
+  // every rank's count -> the padded triple block size
+  uint64_t* d_n = (uint64_t*)arena_->push((size_t)W * sizeof(uint64_t));
+  comm_->all_gather(d_cooc_, d_n, 1, CommDtype::U64, s);
+  std::vector<uint64_t> ns((size_t)W);
+  KMLS_HIP(hipMemcpyAsync(ns.data(), d_n, (size_t)W * 8, hipMemcpyDeviceToHost, s));
+  comm_->wait_stream(s);
+  const uint64_t cap = std::max<uint64_t>(1, *std::max_element(ns.begin(), ns.end()));
+  uint32_t* mine = (uint32_t*)arena_->push((size_t)cap * 3 * sizeof(uint32_t));
+  uint32_t* all = (uint32_t*)arena_->push((size_t)cap * 3 * W * sizeof(uint32_t));
+  KMLS_HIP(hipMemsetAsync(mine, 0, (size_t)cap * 3 * sizeof(uint32_t), s));
+  KMLS_HIP(hipMemsetAsync(d_cooc_, 0, sizeof(unsigned long long), s));
+  kern::gram_frequent(rows, F, r0, nrows, F, minsup, d_cooc_, mine, s);
+  comm_->all_gather(mine, all, (size_t)cap * 3, CommDtype::U32, s);
+  KMLS_HIP(hipMemsetAsync(gram, 0, (size_t)F * F * sizeof(uint32_t), s));
+  kern::gram_scatter(all, (int64_t)cap * W, gram, F, s);
+  KMLS_HIP(hipStreamSynchronize(s));  // the arena scratch is released below
+  arena_->pop_to(mark);
+}
+
 bool GpuMiner::cooc_preferred() {
   if (words_local() < 1024 || fi_.ids.empty()) return false;
   const long long h = test_hook("cooc", 1);
@@ -1313,7 +1348,12 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     KMLS_HIP(hipMemcpyAsync(d_len, root_len.data(), (F + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
     // level 2 through the bit-GEMM (LDS-tiled, 64x64 tiles) when the dense F x F fits
     if (F <= 32768 && cfg.level2_gram) {
-      uint32_t* gram = (uint32_t*)arena_->push((size_t)F * F * sizeof(uint32_t));
+      // tx-DP: room for world row blocks of `per` rows (the reduce-scatter's send layout)
+      const int cw = comm_ ? comm_->world() : 1;
+      const int64_t per = (F + cw - 1) / cw;
+      uint32_t* gram = (uint32_t*)arena_->push((size_t)std::max<int64_t>(per * cw, F) * F * sizeof(uint32_t));
+      if (per * cw > F)
+        KMLS_HIP(hipMemsetAsync(gram + (size_t)F * F, 0, (size_t)(per * cw - F) * F * sizeof(uint32_t), s));
       // sparse large data: count the pairs where they occur (cooc.hip) when the cost model says
       // so (only for bitmaps of this miner's own CSR shard: mine_txdp / the host path of mine)
       bool sparse = false;
@@ -1332,7 +1372,12 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
         else
           kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);
       }
-      if (comm_) comm_->all_reduce(gram, gram, (size_t)F * F, CommDtype::U32, false, s);
+      if (comm_ && cw > 1) {
+        txdp_gram_combine(gram, F, per, run.minsup);
+        res.level2_comm = "reduce_scatter+frequent_allgather";
+      } else if (comm_) {
+        comm_->all_reduce(gram, gram, (size_t)F * F, CommDtype::U32, false, s);
+      }
       run.gram = gram;
     }
     KMLS_HIP(hipEventRecord(e1.e, s));

@@ -84,6 +84,7 @@ struct GpuMineResult {
   std::string levels_path = "none";  // "fused" | "chunked" | "persistent" | "none"
   std::string level2_method = "gram";  // "gram" (bit-GEMM) | "cooc" (horizontal pair count)
   int64_t cooc_pairs = -1;             // sum_t k_t(k_t-1)/2 of the shard when it was measured
+  std::string level2_comm = "none";    // tx-DP: how the shard grams were combined
   // rule map (cfg.rule_index): CSR by item id, rows sorted by (count desc, tie key asc); pinned
   int64_t idx_nnz = -1;  // -1: not built
   int64_t n_items_idx = 0;  // row_ptr has n_items_idx entries (n_items + 1)
@@ -331,6 +332,7 @@ class GpuMiner {
   std::unique_ptr<GraphCache> graph_;  // steady-state hipGraph of mine_resident
   Comm* comm_ = nullptr;          // set during mine_txdp: level counts are all-reduced
   bool gram_csr_ok_ = false;      // mine_bitmaps' bitmaps are this miner's own CSR shard
+  void txdp_gram_combine(uint32_t* gram, int64_t F, int64_t per, uint32_t minsup);
   unsigned long long* d_cooc_ = nullptr;  // [3]: cooc stats (pairs, max k) + error flag
   std::vector<int64_t> tile_tx_;  // 65 evenly spaced transaction boundaries of the shard
   std::vector<int64_t> tile_nnz_; // and their item offsets

@@ -181,7 +181,73 @@ __global__ __launch_bounds__(256) void k_cooc_count(const int64_t* __restrict__ 
   }
 }
 
+// ---- tx-DP combine of shard grams: frequent entries of a reduce-scattered row block ----
+// rows [nrows][ld] = global rows r0.. of the summed gram (upper triangle valid): entries (r, c)
+// with c > r and count >= minsup.  emit == nullptr: count them into cnt[0]; else write
+// (row, col, count) triples at slots taken from cnt[0].
+__global__ __launch_bounds__(256) void k_gram_frequent(const uint32_t* __restrict__ rows,
+                                                       int64_t ld, int64_t r0, int64_t nrows,
+                                                       int64_t F, uint32_t minsup,
+                                                       unsigned long long* __restrict__ cnt,
+                                                       uint32_t* __restrict__ emit) {
+  const int64_t n = nrows * F;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x; e0 < n; e0 += stride) {
+    const int64_t e = e0 + threadIdx.x;
+    bool hit = false;
+    int64_t r = 0, c = 0;
+    uint32_t v = 0;
+    if (e < n) {
+      r = e / F;
+      c = e - r * F;
+      v = rows[r * ld + c];
+      hit = c > r0 + r && v >= minsup && v > 0;
+    }
+    const unsigned long long m = __ballot(hit);
+    if (!m) continue;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(cnt, (unsigned long long)__popcll(m));
+    base = bcast64(base, 0);
+    if (hit && emit != nullptr) {
+      const unsigned long long slot = base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+      emit[3 * slot + 0] = (uint32_t)(r0 + r);
+      emit[3 * slot + 1] = (uint32_t)c;
+      emit[3 * slot + 2] = v;
+    }
+  }
+}
+
+// gram[row * ld + col] = count for every triple with count > 0 (padding triples are zero)
+__global__ void k_gram_scatter(const uint32_t* __restrict__ t, int64_t n, uint32_t* __restrict__ gram,
+                               int64_t ld) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = t[3 * i + 2];
+    if (v) gram[(int64_t)t[3 * i] * ld + t[3 * i + 1]] = v;
+  }
+}
+
 }  // namespace
+
+void gram_frequent(const uint32_t* rows, int64_t ld, int64_t r0, int64_t nrows, int64_t F,
+                   uint32_t minsup, unsigned long long* cnt, uint32_t* emit, hipStream_t s) {
+  const int64_t n = nrows * F;
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_gram_frequent, dim3((unsigned)blocks), dim3(256), 0, s, rows, ld, r0, nrows,
+                     F, minsup, cnt, emit);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e));
+}
+
+void gram_scatter(const uint32_t* triples, int64_t n, uint32_t* gram, int64_t ld, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_gram_scatter, dim3((unsigned)blocks), dim3(256), 0, s, triples, n, gram, ld);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e));
+}
 
 int cooc_max_k() { return kEnt; }
 

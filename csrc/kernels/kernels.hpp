@@ -166,6 +166,13 @@ void pair_gram_mfma(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hi
 // frequent pair into gram[lo * ld + hi] (rank order, upper triangle; gram zeroed by the caller);
 // needs max k_t <= cooc_max_k() (err |= 1 otherwise).
 int cooc_max_k();
+// tx-DP gram combine: the frequent upper entries (count >= minsup) of a reduce-scattered row
+// block [nrows][ld] of global rows r0..: counted into cnt[0] (emit == nullptr) or written as
+// (row, col, count) u32 triples at slots taken from cnt[0]; gram_scatter writes triples back
+// into a zeroed dense gram (zero-count padding triples skipped)
+void gram_frequent(const uint32_t* rows, int64_t ld, int64_t r0, int64_t nrows, int64_t F,
+                   uint32_t minsup, unsigned long long* cnt, uint32_t* emit, hipStream_t s);
+void gram_scatter(const uint32_t* triples, int64_t n, uint32_t* gram, int64_t ld, hipStream_t s);
 void cooc_stats(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, const int32_t* rank_of,
                 const uint32_t* fmask, unsigned long long* out, int n_cus, hipStream_t s);
 void cooc_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, const int32_t* rank_of,

@@ -50,7 +50,7 @@ def _worker(rank, world, port, shape, out_q):
             if rank == 0:
                 t = r["trie"]
                 d = native.load().trie_digest(t["parent"], t["item"], t["count"], t["depth"])["digest"]
-            out.append((int(st["n_itemsets"]), d, st.get("levels_path")))
+            out.append((int(st["n_itemsets"]), d, st.get("levels_path"), st.get("level2_comm")))
         out_q.put((rank, out, (dm.lo, dm.hi)))
     finally:
         dist.destroy_process_group()
@@ -74,7 +74,9 @@ def test_txdp_multi_rank_on_one_gpu(world, shape):
     ref = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
     rd = N.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])
     for rank, out, _ in res:
-        for n, d, path in out:
+        for n, d, path, l2comm in out:
+            # the shard grams are combined by a row-block reduce-scatter, not an F^2 all-reduce
+            assert l2comm == "reduce_scatter+frequent_allgather", l2comm
             assert n == rd["n"], (rank, n, rd["n"], path)
             if rank == 0:
                 assert d == rd["digest"], path
