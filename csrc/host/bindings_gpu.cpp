@@ -1,4 +1,5 @@
 // pybind11 bindings of the HIP runtime objects (GpuMiner, GpuRuleIndex).
+#include <cstring>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -413,8 +414,13 @@ void register_gpu_bindings(py::module_& m) {
       .def("mine_deep", [](gpu::GpuMiner& g, double ms, int max_len, int rank, int world,
                            py::object comm, unsigned long long budget0, unsigned long long budget,
                            unsigned split_min, int blocks_per_cu, int stack_mb, bool steal,
-                           unsigned steal_idle) {
+                           unsigned steal_idle, int assign, bool trace, unsigned presplit_cost,
+                           unsigned long long presplit_budget) {
         gpu::DeepOpts o;
+        o.assign = assign;
+        o.trace = trace;
+        o.presplit_cost = presplit_cost;
+        o.presplit_budget = presplit_budget;
         o.steal = steal;
         o.steal_idle = steal_idle;
         o.budget0 = budget0;
@@ -450,12 +456,27 @@ void register_gpu_bindings(py::module_& m) {
         ph["rounds"] = r.ms_rounds;
         ph["combine"] = r.ms_combine;
         ph["total"] = r.ms_total;
+        ph["assign"] = r.ms_assign;
+        ph["presplit"] = r.ms_presplit;
+        d["presplit"] = py::make_tuple(r.presplit_in, r.presplit_out);
         d["phases_ms"] = ph;
+        if (trace) {
+          const size_t nw = r.trace.size() / kern::kDeepTraceWords;
+          py::array_t<uint64_t> tr({(py::ssize_t)nw, (py::ssize_t)kern::kDeepTraceWords});
+          if (!r.trace.empty()) std::memcpy(tr.mutable_data(), r.trace.data(), r.trace.size() * 8);
+          d["trace"] = tr;
+          d["task_ticks"] = py::array_t<uint64_t>((py::ssize_t)r.task_ticks.size(), r.task_ticks.data());
+          d["task_ids"] = py::array_t<int64_t>((py::ssize_t)r.task_ids.size(), r.task_ids.data());
+          d["task_cost"] = py::array_t<uint32_t>((py::ssize_t)r.task_cost.size(), r.task_cost.data());
+          d["clock_khz"] = r.clock_khz;
+        }
         return d;
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("rank") = 0, py::arg("world") = 1,
          py::arg("comm") = py::none(), py::arg("budget0") = 1024ull, py::arg("budget") = 16ull,
          py::arg("split_min") = 8u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0,
-         py::arg("steal") = true, py::arg("steal_idle") = 1u)
+         py::arg("steal") = true, py::arg("steal_idle") = 1u, py::arg("assign") = 1,
+         py::arg("trace") = false, py::arg("presplit_cost") = 16u,
+         py::arg("presplit_budget") = 1ull)
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
   py::class_<gpu::GpuRuleIndex, std::shared_ptr<gpu::GpuRuleIndex>>(m, "GpuRuleIndex")

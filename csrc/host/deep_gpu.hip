@@ -107,6 +107,15 @@ DeepResult GpuMiner::mine_deep(double min_support, int max_len, int rank, int wo
   res.round_ms = loc.round_ms;
   res.ms_root = loc.ms_root;
   res.ms_rounds = loc.ms_rounds;
+  res.ms_assign = loc.ms_assign;
+  res.ms_presplit = loc.ms_presplit;
+  res.presplit_in = loc.presplit_in;
+  res.presplit_out = loc.presplit_out;
+  res.trace = std::move(loc.trace);
+  res.task_ticks = std::move(loc.task_ticks);
+  res.task_ids = std::move(loc.task_ids);
+  res.task_cost = std::move(loc.task_cost);
+  res.clock_khz = loc.clock_khz;
   if (b.xor_cap < world) {
     if (b.d_xor) KMLS_HIP(hipFree(b.d_xor));
     KMLS_HIP(hipMalloc((void**)&b.d_xor, (size_t)world * 8));

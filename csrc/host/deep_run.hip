@@ -23,7 +23,8 @@ DeepBufs::~DeepBufs() {
   (void)hipSetDevice(device);
   for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)req, (void*)inbox, (void*)inbox_state, (void*)heap[0],
                   (void*)heap[1], (void*)root, (void*)ctl, (void*)d_red, (void*)d_xor,
-                  (void*)d_m, (void*)d_off, (void*)d_toff})
+                  (void*)d_m, (void*)d_off, (void*)d_toff, (void*)d_cost, (void*)d_order,
+                  (void*)d_trace, (void*)d_ticks})
     if (p) (void)hipFree(p);
   if (h_ctl) (void)hipHostFree(h_ctl);
 }
@@ -134,6 +135,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   // ---- level 2: root classes (deterministic on every rank) ----
   const auto t1 = now();
   int64_t n_tasks = 0;
+  int64_t n_heavy = 0;  // assign = 1: the queue's prefix of tasks with cost >= presplit_cost
   if (F >= 2 && in.max_len != 1) {
     const size_t root_blk = (size_t)(W + 1) * (size_t)Fpad * 8;
     auto ensure_root = [&](size_t bytes, size_t keep) {  // keep: leading bytes to preserve
@@ -172,11 +174,58 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, b.d_m, b.d_off, b.root,
                     rank == 0 ? b.ctl : nullptr, true, s);
     const int64_t T = toff[(size_t)F];
-    n_tasks = deeper ? (T - rank + world - 1) / world : 0;
-    if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
+    const int64_t* d_order = nullptr;
+    if (deeper && T > 0 && (opt.assign == 1 || opt.trace)) {
+      // every task's class size (its level-3 survivors) on the device; tasks ordered largest
+      // first (counting sort, stable in t) and dealt over the ranks in snake order, so every
+      // rank gets an equal share of each size class and starts its queue with its largest tasks
+      // (the long subtrees begin first instead of last: a shorter tail)
+      const auto ta = now();
+      int64_t c1 = b.t_cap, c2 = b.t_cap;
+      grow(b.d_cost, c1, T);
+      grow(b.d_order, c2, T);
+      b.t_cap = std::max(c1, c2);
+      kern::deep_task_cost(b.d_off, b.d_m, b.d_toff, F, b.root, in.minsup, b.d_cost, s);
+      std::vector<uint32_t> cost((size_t)T);
+      KMLS_HIP(hipMemcpyAsync(cost.data(), b.d_cost, (size_t)T * 4, hipMemcpyDeviceToHost, s));
+      KMLS_HIP(hipStreamSynchronize(s));
+      std::vector<int64_t> mine;
+      mine.reserve((size_t)(T / world + 1));
+      if (opt.assign == 1) {
+        uint32_t cmax = 0;
+        for (uint32_t c : cost) cmax = std::max(cmax, c);
+        std::vector<int64_t> start((size_t)cmax + 2, 0);
+        for (uint32_t c : cost) start[(size_t)(cmax - c) + 1] += 1;  // descending cost buckets
+        for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
+        std::vector<int64_t> sorted((size_t)T);
+        for (int64_t t = 0; t < T; ++t) sorted[(size_t)start[(size_t)(cmax - cost[(size_t)t])]++] = t;
+        for (int64_t q = 0; q < T; ++q) {
+          const int64_t rnd = q / world, pos = q % world;
+          if ((rnd & 1 ? world - 1 - pos : pos) == rank) mine.push_back(sorted[(size_t)q]);
+        }
+      } else {
+        for (int64_t t = rank; t < T; t += world) mine.push_back(t);
+      }
+      n_tasks = (int64_t)mine.size();
+      if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
+      if (opt.assign == 1 && opt.presplit_cost > 0)
+        while (n_heavy < n_tasks && cost[(size_t)mine[(size_t)n_heavy]] >= opt.presplit_cost) ++n_heavy;
+      KMLS_HIP(hipMemcpyAsync(b.d_order, mine.data(), (size_t)n_tasks * 8, hipMemcpyHostToDevice, s));
+      d_order = b.d_order;
+      if (opt.trace) {
+        res.task_ids = mine;
+        res.task_cost.resize(mine.size());
+        for (size_t q = 0; q < mine.size(); ++q) res.task_cost[q] = cost[(size_t)mine[q]];
+      }
+      KMLS_HIP(hipStreamSynchronize(s));  // `mine` dies at scope end
+      res.ms_assign = ms_since(ta);
+    } else {
+      n_tasks = deeper ? (T - rank + world - 1) / world : 0;
+      if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
+    }
     if (n_tasks > 0)
       kern::deep_root_tasks(b.d_off, b.d_m, b.d_toff, F, b.root, (const uint64_t*)b.root, Fpad, W,
-                            rank, world, b.q[0], s);
+                            rank, world, d_order, n_tasks, b.q[0], s);
     KMLS_HIP(hipStreamSynchronize(s));  // pageable off/toff die at scope end
     res.level2_tasks = T;
   }
@@ -196,14 +245,71 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   a.split_min = opt.split_min;
   a.out_cap = b.q_cap;
   a.heap_cap = b.heap_cap;
+  a.trace = nullptr;
+  a.task_ticks = nullptr;
+  if (opt.trace && opt.steal && n_tasks > 0) {
+    int64_t c1 = b.trace_cap, c2 = b.ticks_cap;
+    grow(b.d_trace, c1, waves * kern::kDeepTraceWords);
+    grow(b.d_ticks, c2, n_tasks);
+    b.trace_cap = c1;
+    b.ticks_cap = c2;
+    KMLS_HIP(hipMemsetAsync(b.d_ticks, 0, (size_t)n_tasks * 8, s));
+    a.trace = b.d_trace;
+    a.task_ticks = b.d_ticks;
+  }
   {
     int khz = 0;
     KMLS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, b.device));
+    res.clock_khz = (double)khz;
     double secs = 120.0;
     if (const char* e = std::getenv("KMLS_DEEP_ROUND_TIMEOUT_S")) secs = std::max(1.0, std::atof(e));
     a.timeout_ticks = (unsigned long long)(secs * 1000.0 * (double)std::max(khz, 1));
   }
-  if (opt.steal && n_tasks > 0) {
+  kern::DeepFrame* steal_q = b.q[0];
+  char* steal_heap = b.heap[0];
+  int64_t steal_n = n_tasks;
+  if (opt.steal && n_heavy > 0 && opt.presplit_budget > 0) {
+    // pre-split: the heavy prefix runs presplit_budget passes without stealing and spills its
+    // open classes (one task per member) into q[1] / heap[0]; the light tasks are appended
+    // behind them and the stealing launch takes q[1] (its own spills go to heap[1])
+    const auto tp = now();
+    KMLS_HIP(hipMemsetAsync(b.ctl, 0, 3 * sizeof(unsigned long long), s));  // ticket, n_out, heap
+    kern::DeepArgs p = a;
+    p.in = b.q[0];
+    p.n_in = n_heavy;
+    p.out = b.q[1];
+    p.heap = b.heap[0];
+    p.budget = opt.presplit_budget;
+    p.steal = 0;
+    p.trace = nullptr;
+    p.task_ticks = nullptr;
+    kern::deep_count(p, maxt, blocks_per_cu,
+                     (int)std::min<int64_t>(grid, (n_heavy + kern::deep_waves_per_block() - 1) /
+                                                      kern::deep_waves_per_block()), s);
+    KMLS_HIP(hipMemcpyAsync(b.h_ctl, b.ctl, sizeof(kern::DeepCtl), hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+    if (b.h_ctl->error)
+      throw std::runtime_error("deep_run: the pre-split launch failed (error " +
+                               std::to_string(b.h_ctl->error) +
+                               "); raise KMLS_DEEP_QUEUE_MB / KMLS_DEEP_HEAP_MB");
+    const int64_t n_out = (int64_t)b.h_ctl->n_out;
+    const int64_t n_light = n_tasks - n_heavy;
+    if (n_out + n_light > b.q_cap)
+      throw std::runtime_error("deep_run: pre-split tasks exceed the queue; raise KMLS_DEEP_QUEUE_MB");
+    if (n_light)
+      KMLS_HIP(hipMemcpyAsync(b.q[1] + n_out, b.q[0] + n_heavy, (size_t)n_light * sizeof(kern::DeepFrame),
+                              hipMemcpyDeviceToDevice, s));
+    steal_q = b.q[1];
+    steal_heap = b.heap[1];
+    steal_n = n_out + n_light;
+    a.task_ticks = nullptr;  // the queue no longer holds the level-3 tasks in order
+    res.presplit_in = n_heavy;
+    res.presplit_out = n_out;
+    res.round_tasks.push_back(n_heavy);
+    res.round_ms.push_back(ms_since(tp));
+    res.ms_presplit = ms_since(tp);
+  }
+  if (opt.steal && steal_n > 0) {
     // one launch: spilled tasks are queued behind the level-3 tasks and taken by waiting waves
     const auto tr = now();
     KMLS_HIP(hipMemsetAsync(b.ctl, 0, 5 * sizeof(unsigned long long), s));
@@ -217,7 +323,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       KMLS_HIP(hipMemsetAsync(b.inbox_state, 0, (size_t)waves * 4, s));
       b.req_cap = waves;
     }
-    b.h_ctl->pending = (unsigned long long)n_tasks;
+    b.h_ctl->pending = (unsigned long long)steal_n;
     KMLS_HIP(hipMemcpyAsync(&b.ctl->pending, &b.h_ctl->pending, 8, hipMemcpyHostToDevice, s));
     if (++b.epoch >= (1u << 30)) {  // 2^30 launches: restart the stamps
       KMLS_HIP(hipMemsetAsync(b.ready, 0, (size_t)b.q_cap * sizeof(unsigned), s));
@@ -225,10 +331,10 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       KMLS_HIP(hipMemsetAsync(b.inbox_state, 0, (size_t)b.req_cap * 4, s));
       b.epoch = 1;
     }
-    a.in = b.q[0];
-    a.n_in = n_tasks;
-    a.out = b.q[0];
-    a.heap = b.heap[0];
+    a.in = steal_q;
+    a.n_in = steal_n;
+    a.out = steal_q;
+    a.heap = steal_heap;
     a.budget = std::max<unsigned long long>(opt.budget, 1);
     a.ready = b.ready;
     a.epoch = b.epoch;
@@ -248,10 +354,18 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
                                ((b.h_ctl->error & 8) ? "bad block width" :
                                 (b.h_ctl->error & 1) ? "task queue overflow" : "spill heap overflow") +
                                "); raise KMLS_DEEP_QUEUE_MB / KMLS_DEEP_HEAP_MB");
-    res.round_tasks.push_back(n_tasks);
+    res.round_tasks.push_back(steal_n);
     res.round_ms.push_back(ms_since(tr));
     res.spilled_tasks = (int64_t)b.h_ctl->n_out;
     res.handoffs = (int64_t)b.h_ctl->handoffs;
+    if (a.trace) {
+      res.trace.resize((size_t)waves * kern::kDeepTraceWords);
+      res.task_ticks.resize(a.task_ticks ? (size_t)n_tasks : 0);
+      KMLS_HIP(hipMemcpy(res.trace.data(), b.d_trace, res.trace.size() * 8, hipMemcpyDeviceToHost));
+      if (!res.task_ticks.empty())
+        KMLS_HIP(hipMemcpy(res.task_ticks.data(), b.d_ticks, res.task_ticks.size() * 8,
+                           hipMemcpyDeviceToHost));
+    }
     n_tasks = 0;  // the rounds below have nothing left
   }
   int cur = 0;

@@ -39,6 +39,12 @@ struct DeepBufs {
   int64_t* d_off = nullptr;  // [F + 1] block byte offsets
   int64_t* d_toff = nullptr;  // [F + 1] task offsets
   int64_t f_cap = 0;
+  uint32_t* d_cost = nullptr;   // [T] level-3 task costs (assign = 1)
+  int64_t* d_order = nullptr;   // [T] this rank's task ids in queue order
+  int64_t t_cap = 0;
+  unsigned long long* d_trace = nullptr;  // [waves * kDeepTraceWords] (opts.trace)
+  unsigned long long* d_ticks = nullptr;  // [T] (opts.trace)
+  int64_t trace_cap = 0, ticks_cap = 0;
   kern::DeepCtl* ctl = nullptr;
   kern::DeepCtl* h_ctl = nullptr;  // pinned readback
   uint64_t* d_red = nullptr;       // [66]: per_depth[64], digest_sum, candidates (all-reduce)
@@ -69,7 +75,12 @@ struct DeepLocal {
   int64_t spilled_tasks = 0;  // tasks spilled inside the launch(es)
   int64_t handoffs = 0;       // classes handed straight to a requesting wave (steal mode)
   std::vector<double> round_ms;
-  double ms_alloc = 0, ms_root = 0, ms_rounds = 0;
+  double ms_alloc = 0, ms_root = 0, ms_rounds = 0, ms_assign = 0, ms_presplit = 0;
+  int64_t presplit_in = 0, presplit_out = 0;
+  std::vector<uint64_t> trace, task_ticks;  // opts.trace
+  std::vector<int64_t> task_ids;
+  std::vector<uint32_t> task_cost;
+  double clock_khz = 0;
 };
 
 DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const DeepOpts& opt);

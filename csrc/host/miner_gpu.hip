@@ -833,6 +833,7 @@ void GpuMiner::drain_prefetch() {
 void GpuMiner::load_csr(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx,
                         int64_t n_items) {
   KMLS_HIP(hipSetDevice(device_));
+  ++sel_gen_;
   drain_prefetch();
   hipStream_t s = (hipStream_t)stream_;
   if (d_tx_ptr_) KMLS_HIP(hipFree(d_tx_ptr_));
@@ -881,6 +882,7 @@ void GpuMiner::item_support(uintptr_t counts_dev) {
 int64_t GpuMiner::select_device(const uint32_t* d_counts, int64_t global_n_tx, double min_support,
                                 Comm* comm) {
   hipStream_t s = (hipStream_t)stream_;
+  ++sel_gen_;
   global_n_tx_ = global_n_tx;
   const int64_t I = std::max<int64_t>(n_items_, 1);
   if (d_rank_of_) KMLS_HIP(hipFree(d_rank_of_));
@@ -939,6 +941,7 @@ void GpuMiner::build_encode_tables(int64_t F) {
 int64_t GpuMiner::select(const uint32_t* global_counts, int64_t global_n_tx, double min_support) {
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
+  ++sel_gen_;
   global_n_tx_ = global_n_tx;
   fi_ = select_frequent(global_counts, n_items_, (uint64_t)global_n_tx, min_support);
   if (d_rank_of_) KMLS_HIP(hipFree(d_rank_of_));
@@ -1018,6 +1021,7 @@ void GpuMiner::pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev
 }
 
 GpuMiner::CoocStats GpuMiner::cooc_stats() {
+  if (cooc_gen_ == sel_gen_) return cooc_cache_;  // same CSR and selection: one pass per step
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
   CoocStats st;
@@ -1030,6 +1034,8 @@ GpuMiner::CoocStats GpuMiner::cooc_stats() {
   KMLS_HIP(hipStreamSynchronize(s));
   st.pairs = h[0];
   st.max_k = h[1];
+  cooc_cache_ = st;
+  cooc_gen_ = sel_gen_;
   return st;
 }
 

@@ -160,6 +160,15 @@ struct DeepOpts {
                                       // spill rounds (budget0/budget = per-task step budgets)
   unsigned steal_idle = 1;            // steal: 1 = hand over when a waiting wave asks; tests:
                                       // 0 = to the queue at every check, 2 = to the partner wave
+  int assign = 1;                     // level-3 tasks: 1 = ordered by their measured class size
+                                      // (largest first) and dealt over the ranks in snake order;
+                                      // 0 = task t to rank t % world in index order
+  bool trace = false;                 // per-wave / per-task timing of the launch (DeepResult)
+  // pre-split (assign = 1): the rank's level-3 tasks whose class has >= presplit_cost members
+  // first run `presplit_budget` passes in a non-stealing launch that spills their open classes
+  // as one task per member; the stealing launch then starts from those finer tasks (0 = off)
+  unsigned presplit_cost = 16;
+  unsigned long long presplit_budget = 1;
 };
 struct DeepResult {
   std::vector<uint64_t> per_level;  // [d] = frequent itemsets of size d (index 0 unused)
@@ -171,6 +180,15 @@ struct DeepResult {
   int64_t handoffs = 0;
   std::vector<double> round_ms;
   double ms_prologue = 0, ms_root = 0, ms_rounds = 0, ms_combine = 0, ms_total = 0;
+  double ms_assign = 0;               // task costs + ordering (inside ms_root)
+  int64_t presplit_in = 0, presplit_out = 0;  // heavy tasks pre-split, tasks they became
+  double ms_presplit = 0;
+  // opts.trace: per wave kern::kDeepTraceWords words; per queued task (queue order) its id,
+  // its class-size cost and the ticks its dequeuing wave spent on it; the clock rate
+  std::vector<uint64_t> trace, task_ticks;
+  std::vector<int64_t> task_ids;
+  std::vector<uint32_t> task_cost;
+  double clock_khz = 0;
 };
 struct GraphCache;  // captured launch sequence of the resident path (miner_gpu.hip)
 struct Prefetch;    // a resident call launched ahead of its mine() (miner_gpu.hip)
@@ -334,6 +352,9 @@ class GpuMiner {
   bool gram_csr_ok_ = false;      // mine_bitmaps' bitmaps are this miner's own CSR shard
   void txdp_gram_combine(uint32_t* gram, int64_t F, int64_t per, uint32_t minsup);
   unsigned long long* d_cooc_ = nullptr;  // [3]: cooc stats (pairs, max k) + error flag
+  uint64_t sel_gen_ = 0;          // bumped by load_csr / select*: invalidates cached cooc stats
+  uint64_t cooc_gen_ = ~0ull;
+  CoocStats cooc_cache_;
   std::vector<int64_t> tile_tx_;  // 65 evenly spaced transaction boundaries of the shard
   std::vector<int64_t> tile_nnz_; // and their item offsets
   int64_t last_nodes_ = 0;        // size of the previous trie (pinned download sizing)

@@ -9,11 +9,13 @@
 // once, where it occurs (the reference's own rule map is this pair-support matrix,
 // machine-learning/main.py:282-304).
 //
-// Layout of the work (one 64-lane wave = 64 consecutive transactions, lane = transaction):
-//   1. each lane counts the frequent items of its transaction (frequent-mask bit, then the rank
-//      gather), a wave scan turns the counts into LDS offsets;
-//   2. the lanes write their transactions' frequent ranks into the wave's LDS entry buffer
-//      (sub-chunks of <= kEnt entries when 64 transactions hold more);
+// Layout of the work (one 64-lane wave = a chunk of 64 consecutive transactions):
+//   1. the wave streams the chunk's contiguous CSR span with coalesced loads (frequent-mask bit,
+//      then the rank gather), compacts the frequent ranks in order into its LDS entry buffer and
+//      counts them per transaction (LDS atomics; a binary search of the chunk's offsets gives an
+//      item's transaction);
+//   2. chunks with more frequent entries than the buffer holds (long transactions) fall back to
+//      sub-chunks of lanes whose entries fit, each lane reading its own transaction;
 //   3. the pairs of all those transactions are enumerated FLAT over the wave (pair p -> its
 //      transaction by a binary search of the pair prefix, (i, j) by inverting the row-major
 //      triangle), so a wave64 instruction carries 64 pairs whatever the transaction lengths;
@@ -49,6 +51,53 @@ __device__ __forceinline__ int frequent_rank(int it, const int32_t* __restrict__
   return rank_of[it];
 }
 
+// Per-wave LDS of one 64-transaction chunk.
+struct ChunkLds {
+  int32_t ent[kEnt];          // frequent ranks of the chunk, in CSR (transaction) order
+  uint32_t pt[kTx + 1];       // CSR offsets of the chunk's transactions, relative to pt[0]
+  uint32_t kc[kTx];           // frequent items per transaction
+  uint32_t toff[kTx + 1];     // entry offset of transaction x
+  uint32_t poff[kTx + 1];     // pair offset of transaction x
+};
+
+// Coalesced scan of the chunk's items (the contiguous CSR span of its transactions): frequent
+// ranks compacted in order into L.ent (while they fit: WRITE), per-transaction counts in L.kc.
+// Returns the chunk's frequent entries (may exceed kEnt; then L.ent holds only the first kEnt).
+template <bool WRITE>
+__device__ __forceinline__ unsigned chunk_scan(ChunkLds& L, const int64_t* __restrict__ ptr,
+                                               const int32_t* __restrict__ items,
+                                               const int32_t* __restrict__ rank_of,
+                                               const uint32_t* __restrict__ fmask, int64_t t0,
+                                               unsigned n, int lane) {
+  const int64_t b0 = ptr[t0];
+  const unsigned span = (unsigned)(ptr[t0 + n] - b0);  // (n may be 64: no lane holds it)
+  if ((unsigned)lane < n) L.pt[lane] = (unsigned)(ptr[t0 + lane] - b0);
+  if (lane < kTx) L.kc[lane] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  const unsigned long long lanelt = (1ull << lane) - 1ull;
+  unsigned ne = 0;
+  for (unsigned p0 = 0; p0 < span; p0 += 64) {
+    const unsigned p = p0 + lane;
+    int r = -1;
+    if (p < span) r = frequent_rank(items[b0 + p], rank_of, fmask);
+    const unsigned long long m = __ballot(r >= 0);
+    if (r >= 0) {
+      // transaction: the last x with pt[x] <= p
+      unsigned x = 0;
+      for (unsigned step = 32; step; step >>= 1)
+        if (x + step < n && L.pt[x + step] <= p) x += step;
+      atomicAdd(&L.kc[x], 1u);
+      if (WRITE) {
+        const unsigned e = ne + (unsigned)__popcll(m & lanelt);
+        if (e < (unsigned)kEnt) L.ent[e] = r;
+      }
+    }
+    ne += (unsigned)__popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  return ne;
+}
+
 // per transaction k = its frequent items: sum of k(k-1)/2 and max k (the host's cost model and
 // the entry-buffer bound)
 __global__ __launch_bounds__(256) void k_cooc_stats(const int64_t* __restrict__ ptr,
@@ -56,24 +105,62 @@ __global__ __launch_bounds__(256) void k_cooc_stats(const int64_t* __restrict__ 
                                                     const int32_t* __restrict__ rank_of,
                                                     const uint32_t* __restrict__ fmask,
                                                     unsigned long long* __restrict__ out) {
+  __shared__ ChunkLds lds[kW];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  ChunkLds& L = lds[wid];
   unsigned long long pairs = 0;
   unsigned kmax = 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_tx; t += stride) {
-    unsigned k = 0;
-    for (int64_t p = ptr[t], e = ptr[t + 1]; p < e; ++p) k += frequent_rank(items[p], rank_of, fmask) >= 0;
+  const int64_t nchunks = (n_tx + kTx - 1) / kTx;
+  for (int64_t c = (int64_t)blockIdx.x * kW + wid; c < nchunks; c += (int64_t)gridDim.x * kW) {
+    const int64_t t0 = c * kTx;
+    const unsigned n = (unsigned)(n_tx - t0 < kTx ? n_tx - t0 : kTx);
+    chunk_scan<false>(L, ptr, items, rank_of, fmask, t0, n, lane);
+    const unsigned k = (unsigned)lane < n ? L.kc[lane] : 0u;
     pairs += (unsigned long long)k * (k - (k > 0)) / 2;
     kmax = k > kmax ? k : kmax;
+    __builtin_amdgcn_wave_barrier();
   }
   for (int off = 32; off; off >>= 1) {
     pairs += shfl_xor64(pairs, off);
     const unsigned o = __shfl_xor(kmax, off, 64);
     kmax = o > kmax ? o : kmax;
   }
-  if ((threadIdx.x & 63) == 0) {
+  if (lane == 0) {
     atomicAdd(out, pairs);
     atomicMax(out + 1, (unsigned long long)kmax);
   }
+}
+
+// the pairs of sub-chunk lanes [x0, x0 + nx) whose entries sit at L.ent[L.toff[x]..]: flat over
+// the wave (pair -> transaction by a binary search of L.poff, (i, j) by inverting the triangle)
+__device__ __forceinline__ void chunk_pairs(ChunkLds& L, unsigned nx, unsigned P, int head0,
+                                            uint32_t* head, uint32_t* __restrict__ gram,
+                                            int64_t ld, int lane) {
+  for (unsigned p0 = 0; p0 < P; p0 += 64) {
+    const unsigned p = p0 + lane;
+    if (p < P) {
+      unsigned x = 0;
+      for (unsigned step = 32; step; step >>= 1)
+        if (x + step < nx && L.poff[x + step] <= p) x += step;
+      const unsigned qq = p - L.poff[x];
+      const unsigned e0 = L.toff[x];
+      const unsigned kk = L.toff[x + 1] - e0;
+      // row-major triangle: row i holds (kk-1-i) pairs, S(i) = i(2kk-1-i)/2 before it
+      const float m2 = (float)(2 * kk - 1);
+      int i = (int)((m2 - sqrtf(m2 * m2 - 8.0f * (float)qq)) * 0.5f);
+      if (i < 0) i = 0;
+      while (i > 0 && (unsigned)(i * (2 * (int)kk - 1 - i) / 2) > qq) --i;
+      while ((unsigned)((i + 1) * (2 * (int)kk - 2 - i) / 2) <= qq) ++i;
+      const unsigned j = (unsigned)i + 1u + (qq - (unsigned)(i * (2 * (int)kk - 1 - i) / 2));
+      const int ra = L.ent[e0 + (unsigned)i], rb = L.ent[e0 + j];
+      const int lo = ra < rb ? ra : rb, hi = ra < rb ? rb : ra;
+      if (lo >= head0)
+        atomicAdd(&head[(lo - head0) * kHead + (hi - head0)], 1u);
+      else
+        atomicAdd(&gram[(int64_t)lo * ld + hi], 1u);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
 }
 
 __global__ __launch_bounds__(256) void k_cooc_count(const int64_t* __restrict__ ptr,
@@ -83,23 +170,18 @@ __global__ __launch_bounds__(256) void k_cooc_count(const int64_t* __restrict__ 
                                                     uint32_t* __restrict__ gram, int64_t ld,
                                                     unsigned* __restrict__ err) {
   __shared__ uint32_t head[kHead * kHead];  // [a - head0][b - head0], a < b
-  __shared__ int32_t ent[kW][kEnt];
-  __shared__ uint32_t toff[kW][kTx + 1];    // entry offset of sub-chunk transaction x
-  __shared__ uint32_t poff[kW][kTx + 1];    // pair offset of sub-chunk transaction x
+  __shared__ ChunkLds lds[kW];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  ChunkLds& L = lds[wid];
   const int head0 = F > kHead ? F - kHead : 0;
   for (int e = threadIdx.x; e < kHead * kHead; e += blockDim.x) head[e] = 0u;
   __syncthreads();
-  int32_t* E = ent[wid];
-  uint32_t* TO = toff[wid];
-  uint32_t* PO = poff[wid];
   const int64_t nchunks = (n_tx + kTx - 1) / kTx;
   for (int64_t c = (int64_t)blockIdx.x * kW + wid; c < nchunks; c += (int64_t)gridDim.x * kW) {
-    const int64_t t = c * kTx + lane;
-    const bool act = t < n_tx;
-    const int64_t b = act ? ptr[t] : 0, e = act ? ptr[t + 1] : 0;
-    unsigned k = 0;
-    for (int64_t p = b; p < e; ++p) k += frequent_rank(items[p], rank_of, fmask) >= 0;
+    const int64_t t0 = c * kTx;
+    const unsigned n = (unsigned)(n_tx - t0 < kTx ? n_tx - t0 : kTx);
+    const unsigned ne = chunk_scan<true>(L, ptr, items, rank_of, fmask, t0, n, lane);
+    unsigned k = (unsigned)lane < n ? L.kc[lane] : 0u;
     if (k > (unsigned)kEnt) {  // the host checks max k first; never write past the buffer
       atomicOr(err, 1u);
       k = 0;
@@ -110,9 +192,34 @@ __global__ __launch_bounds__(256) void k_cooc_count(const int64_t* __restrict__ 
       const unsigned o = __shfl_up(incl, off, 64);
       if (lane >= off) incl += o;
     }
+    if (ne <= (unsigned)kEnt) {
+      // the whole chunk's entries are in LDS, in transaction order: one pass of its pairs
+      const unsigned q = k * (k - (k > 0)) / 2;
+      unsigned pin = q;
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned v = __shfl_up(pin, o, 64);
+        if (lane >= o) pin += v;
+      }
+      if ((unsigned)lane < n) {
+        L.toff[lane] = incl - k;
+        L.poff[lane] = pin - q;
+      }
+      const unsigned P = uni(__shfl(pin, 63, 64));
+      if (lane == 0) {
+        L.toff[n] = ne;
+        L.poff[n] = P;
+      }
+      __builtin_amdgcn_wave_barrier();
+      chunk_pairs(L, n, P, head0, head, gram, ld, lane);
+      continue;
+    }
+    // more entries than fit (long transactions): sub-chunks of lanes whose entries fit, each
+    // lane re-reading its own transaction's items
+    const int64_t t = t0 + lane;
+    const bool act = (unsigned)lane < n;
+    const int64_t b = act ? ptr[t] : 0, e = act ? ptr[t + 1] : 0;
     unsigned l0 = 0, base = 0;
     while (l0 < 64u) {
-      // the sub-chunk: lanes l0 .. l1-1 whose entries fit (every single lane fits: k <= kEnt)
       const unsigned long long fit = __ballot((unsigned)lane >= l0 && incl - base <= (unsigned)kEnt);
       const unsigned long long run = fit >> l0;
       const unsigned len = ~run == 0ull ? 64u - l0 : (unsigned)__builtin_ctzll(~run);
@@ -123,11 +230,10 @@ __global__ __launch_bounds__(256) void k_cooc_count(const int64_t* __restrict__ 
         unsigned j = 0;
         for (int64_t p = b; p < e && j < k; ++p) {
           const int r = frequent_rank(items[p], rank_of, fmask);
-          if (r >= 0) E[off + j++] = r;
+          if (r >= 0) L.ent[off + j++] = r;
         }
-        TO[lane - l0] = off;
+        L.toff[lane - l0] = off;
       }
-      // pairs per transaction, inclusive scan over the sub-chunk's lanes
       const unsigned q = in_sub ? k * (k - (k > 0)) / 2 : 0u;
       unsigned pin = q;
       for (int o = 1; o < 64; o <<= 1) {
@@ -135,40 +241,15 @@ __global__ __launch_bounds__(256) void k_cooc_count(const int64_t* __restrict__ 
         if (lane >= o) pin += v;
       }
       const unsigned n_sub = l1 - l0;
-      if (in_sub) PO[lane - l0] = pin - q;
+      if (in_sub) L.poff[lane - l0] = pin - q;
       const unsigned P = uni(__shfl(pin, 63, 64));
       const unsigned last = uni(__shfl(incl, (int)l1 - 1, 64));  // entries up to lane l1-1
       if (lane == 0) {
-        PO[n_sub] = P;
-        TO[n_sub] = last - base;
+        L.poff[n_sub] = P;
+        L.toff[n_sub] = last - base;
       }
       __builtin_amdgcn_wave_barrier();
-      for (unsigned p0 = 0; p0 < P; p0 += 64) {
-        const unsigned p = p0 + lane;
-        if (p < P) {
-          // transaction x: the last with PO[x] <= p
-          unsigned x = 0;
-          for (unsigned step = 32; step; step >>= 1)
-            if (x + step < n_sub && PO[x + step] <= p) x += step;
-          const unsigned qq = p - PO[x];
-          const unsigned e0 = TO[x];
-          const unsigned kk = TO[x + 1] - e0;
-          // row-major triangle: row i holds (kk-1-i) pairs, S(i) = i(2kk-1-i)/2 before it
-          const float m2 = (float)(2 * kk - 1);
-          int i = (int)((m2 - sqrtf(m2 * m2 - 8.0f * (float)qq)) * 0.5f);
-          if (i < 0) i = 0;
-          while (i > 0 && (unsigned)(i * (2 * (int)kk - 1 - i) / 2) > qq) --i;
-          while ((unsigned)((i + 1) * (2 * (int)kk - 2 - i) / 2) <= qq) ++i;
-          const unsigned j = (unsigned)i + 1u + (qq - (unsigned)(i * (2 * (int)kk - 1 - i) / 2));
-          const int ra = E[e0 + (unsigned)i], rb = E[e0 + j];
-          const int lo = ra < rb ? ra : rb, hi = ra < rb ? rb : ra;
-          if (lo >= head0)
-            atomicAdd(&head[(lo - head0) * kHead + (hi - head0)], 1u);
-          else
-            atomicAdd(&gram[(int64_t)lo * ld + hi], 1u);
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
+      chunk_pairs(L, n_sub, P, head0, head, gram, ld, lane);
       base = last;
       l0 = l1;
     }

@@ -747,6 +747,8 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
                  kFull = (a.epoch << 2) | 3u, kClosed = a.epoch << 2;
   bool holding = false, inbox_open = false;
   unsigned long long t = 0;
+  // instrumentation (a.trace != nullptr): first task start, last task end, busy ticks, counts
+  unsigned long long tr_first = 0, tr_last = 0, tr_busy = 0, tr_tasks = 0, tr_inbox = 0;
   unsigned victim = (unsigned)((gw * 7919ull + 1) % (unsigned long long)(a.nwaves > 0 ? a.nwaves : 1));
   while (!failed) {
     // ---- the next task: queue ticket t, or (steal mode, while t is not published) a class
@@ -757,6 +759,8 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
       holding = true;
     }
     DeepFrame tf;
+    bool task_from_inbox = false;
+    unsigned long long task_ticket = t;
     if (!a.steal) {
       if (t >= (unsigned long long)a.n_in) break;
       tf = load_frame(a.in + t, lane);
@@ -812,6 +816,8 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
         wait_short(n);
       }
       if (done || failed) break;
+      task_from_inbox = from_inbox;
+      task_ticket = t;
       if (from_inbox) {
         tf = load_frame_agent(a.inbox + gw, lane);
         if (lane == 0) st_agent(&a.inbox_state[gw], kClosed);
@@ -833,6 +839,8 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
       st.mem_top = 0;
     }
     acc.budget_used = 0;
+    const unsigned long long tr_t0 = a.trace ? wall_clock64() : 0ull;
+    if (a.trace && tr_tasks == 0) tr_first = tr_t0;
     // ---- run the task ----
     while (st.nf > 0) {
       __builtin_amdgcn_wave_barrier();
@@ -892,6 +900,15 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
                                                                stack, lane, acc);
       free_blocks(L, st);
     }
+    if (a.trace && !failed) {
+      const unsigned long long now = wall_clock64();
+      tr_busy += now - tr_t0;
+      tr_last = now;
+      tr_tasks += 1;
+      tr_inbox += task_from_inbox ? 1 : 0;
+      if (a.task_ticks && !task_from_inbox && task_ticket < (unsigned long long)a.n_in && lane == 0)
+        a.task_ticks[task_ticket] = now - tr_t0;
+    }
     if (a.steal && !failed) {  // the task is done
       unsigned long long left = 0;
       if (lane == 0) left = atomicSub(&a.ctl->pending, 1ull);
@@ -923,6 +940,15 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
   }
   for (int d = lane; d < 64; d += 64)
     if (L.depth_cnt[d]) atomicAdd(&a.ctl->per_depth[d], L.depth_cnt[d]);
+  if (a.trace && lane == 0) {
+    unsigned long long* tr = a.trace + gw * (unsigned long long)kDeepTraceWords;
+    tr[0] = t_start;
+    tr[1] = tr_first;
+    tr[2] = tr_last;
+    tr[3] = wall_clock64();
+    tr[4] = tr_busy;
+    tr[5] = (tr_tasks << 32) | tr_inbox;
+  }
 }
 
 // ---- root level: level-2 classes (deterministic, so every rank builds the same task list) ----
@@ -1010,29 +1036,63 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
   }
 }
 
-// this rank's share of the level-3 tasks: task t = (root i, member k), t = task_off[i] + k,
-// taken by rank t % world (interleaved, so each root class is spread over the ranks)
+// this rank's level-3 tasks: out[q] = task order[q] (order == nullptr: task q*world + rank, the
+// interleaved split); task t = (root i, member k), t = task_off[i] + k
 __global__ void k_deep_root_tasks(const long long* blk_off, const int32_t* m, const long long* task_off,
                                   long long F, char* base, const unsigned long long* root,
-                                  long long Fpad, int W, int rank, int world, DeepFrame* out) {
-  const long long i = blockIdx.x;
-  if (i >= F) return;
-  const int mi = m[i];
-  if (mi < 2) return;
-  const unsigned long long h = root[(unsigned long long)W * Fpad + i];
-  const unsigned long long pad = roundup16((unsigned long long)mi);
-  const unsigned wt = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * pad)) - 1u;
-  for (int k = threadIdx.x; k < mi - 1; k += blockDim.x) {
-    const long long t = task_off[i] + k;
-    if (t % world != rank) continue;
+                                  long long Fpad, int W, int rank, int world,
+                                  const long long* order, long long n, DeepFrame* out) {
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n;
+       q += (long long)gridDim.x * blockDim.x) {
+    const long long t = order ? order[q] : q * world + rank;
+    // root i: the last with task_off[i] <= t (empty classes share their offset with the next)
+    long long lo = 0, hi = F - 1;
+    while (lo < hi) {
+      const long long mid = (lo + hi + 1) >> 1;
+      if (task_off[mid] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const long long i = lo;
+    const int mi = m[i];
+    const long long k = t - task_off[i];
+    const unsigned long long pad = roundup16((unsigned long long)mi);
+    const unsigned wt = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * pad)) - 1u;
     DeepFrame f;
     f.blk = (unsigned long long)(base + blk_off[i]);
-    f.hash = h;
+    f.hash = root[(unsigned long long)W * Fpad + i];
     f.pad = (unsigned)pad;
     f.s0 = (unsigned)k;
     f.m = (unsigned)(mi - k);
     f.meta = make_meta(1, true, wt, 0);
-    store_frame(out + t / world, f);
+    store_frame(out + q, f);
+  }
+}
+
+// cost[task_off[i] + k] = members j > k of root class i with |row_k & row_j| >= minsup: the size
+// of the class task (i, k) expands (one wave per task, lanes over j; block widths are runtime)
+__global__ __launch_bounds__(256) void k_deep_task_cost(const long long* blk_off, const int32_t* m,
+                                                        const long long* task_off, long long F,
+                                                        const char* base, unsigned minsup,
+                                                        unsigned* cost) {
+  const long long i = blockIdx.x;
+  if (i >= F) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int mi = m[i];
+  if (mi < 2) return;
+  const unsigned long long pad = roundup16((unsigned long long)mi);
+  const unsigned wt = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * pad)) - 1u;
+  const unsigned long long* blk = (const unsigned long long*)(base + blk_off[i]);
+  for (int k = wid; k < mi - 1; k += (int)(blockDim.x >> 6)) {
+    unsigned c = 0;
+    for (int j0 = k + 1; j0 < mi; j0 += 64) {
+      const int j = j0 + lane;
+      unsigned pc = 0;
+      if (j < mi)
+        for (unsigned w = 0; w < wt; ++w)
+          pc += (unsigned)__popcll(blk[(unsigned long long)w * pad + k] & blk[(unsigned long long)w * pad + j]);
+      c += (unsigned)__popcll(__ballot(j < mi && pc >= minsup));
+    }
+    if (lane == 0) cost[task_off[i] + k] = c;
   }
 }
 
@@ -1095,11 +1155,21 @@ void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t mi
 
 void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
                      char* base, const uint64_t* root, int64_t Fpad, int W, int rank, int world,
-                     DeepFrame* out, hipStream_t s) {
-  if (F <= 0) return;
-  hipLaunchKernelGGL(k_deep_root_tasks, dim3((unsigned)F), dim3(256), 0, s,
+                     const int64_t* order, int64_t n, DeepFrame* out, hipStream_t s) {
+  if (F <= 0 || n <= 0) return;
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_deep_root_tasks, dim3(grid), dim3(256), 0, s,
                      (const long long*)blk_off, m, (const long long*)task_off, (long long)F, base,
-                     (const unsigned long long*)root, (long long)Fpad, W, rank, world, out);
+                     (const unsigned long long*)root, (long long)Fpad, W, rank, world,
+                     (const long long*)order, (long long)n, out);
+}
+
+void deep_task_cost(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
+                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s) {
+  if (F <= 0) return;
+  hipLaunchKernelGGL(k_deep_task_cost, dim3((unsigned)F), dim3(256), 0, s,
+                     (const long long*)blk_off, m, (const long long*)task_off, (long long)F, base,
+                     minsup, cost);
 }
 
 int deep_count_wps(int maxt, int want) {

@@ -62,7 +62,13 @@ struct DeepArgs {
   int steal;
   int steal_eager;                // tests: 1 = bottom frame to the queue at every check,
                                   // 2 = hand-off to the partner wave (gw ^ 1) whenever it waits
+  // optional instrumentation (nullptr = off): per wave [kDeepTraceWords] words (launch start,
+  // first task start, last task end, exit, busy ticks, tasks << 32 | inbox receipts) and per
+  // initial task the ticks its dequeuing wave spent on it (parts handed away excluded)
+  unsigned long long* trace;
+  unsigned long long* task_ticks;
 };
+constexpr int kDeepTraceWords = 6;
 int deep_max_words();
 int deep_tier(int words);     // smallest instantiated block width >= words
 int deep_row_words(int W);    // root block width for W-word rows (a tier)
@@ -77,9 +83,14 @@ void deep_transpose(const uint64_t* bm, int64_t Wp, int64_t F, int W, int W_real
 void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t minsup,
                int32_t* m, const int64_t* blk_off, char* base, DeepCtl* ctl, bool fill,
                hipStream_t s);
+// this rank's level-3 task frames: out[q] = task order[q] (order == nullptr: task q*world+rank),
+// q < n; task t = (root i, member k) with t = task_off[i] + k
 void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
                      char* base, const uint64_t* root, int64_t Fpad, int W, int rank, int world,
-                     DeepFrame* out, hipStream_t s);
+                     const int64_t* order, int64_t n, DeepFrame* out, hipStream_t s);
+// level-3 survivors of every task (the size of the class the task expands): cost[t]
+void deep_task_cost(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
+                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s);
 void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s);
 
 // ---- mining (mine.hip) ----

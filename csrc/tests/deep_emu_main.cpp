@@ -4,7 +4,7 @@
 // content digest must equal mine_cpu_count's.
 //
 //   deep_emu n_tx n_items mean_len genres affinity min_support [budget0 budget split_min stack_mb
-//            world max_len steal steal_idle]
+//            world max_len steal steal_idle presplit_cost]
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -36,6 +36,7 @@ int main(int argc, char** argv) {
   const int max_len = argc > 12 ? std::atoi(argv[12]) : 0;
   opt.steal = argc > 13 ? std::atoi(argv[13]) != 0 : true;
   if (argc > 14) opt.steal_idle = (unsigned)std::atoi(argv[14]);
+  if (argc > 15) opt.presplit_cost = (unsigned)std::atoi(argv[15]);
   opt.blocks_per_cu = 1;
 
   std::vector<int64_t> ptr;

@@ -57,6 +57,11 @@ def main() -> int:
     ap.add_argument("--rounds", action="store_true", help="spill rounds instead of stealing")
     ap.add_argument("--world", type=int, default=1, help="simulate a rank split on one GPU")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--assign", type=int, default=1,
+                    help="level-3 task assignment: 1 = cost-ordered snake deal, 0 = t mod world")
+    ap.add_argument("--trace", action="store_true", help="per-wave / per-task timing summary")
+    ap.add_argument("--presplit-cost", type=int, default=16, help="0 = no pre-split launch")
+    ap.add_argument("--presplit-budget", type=int, default=1)
     a = ap.parse_args()
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     from kubernetes_machine_learning_server_amd.ops import native
@@ -73,6 +78,10 @@ def main() -> int:
         return kw
 
     kw = opts(a.budget0, a.budget, a.split_min, a.blocks_per_cu, 0 if a.rounds else 1)
+    kw["assign"] = a.assign
+    kw["trace"] = a.trace
+    kw["presplit_cost"] = a.presplit_cost
+    kw["presplit_budget"] = a.presplit_budget
     if not a.no_parity:
         t = time.perf_counter()
         d = g.mine_deep(0.03, **kw)
@@ -103,6 +112,7 @@ def main() -> int:
         return 0
     for ms in [float(x) for x in a.supports.split(",")]:
         for rep in range(a.reps):
+            comb = {"sum": 0, "xor": 0, "n": 0, "slowest_ms": 0.0}
             for r in range(a.world):
                 t = time.perf_counter()
                 with Heartbeat(f"min_support {ms} rank {r}"):
@@ -118,11 +128,62 @@ def main() -> int:
                        "round_tasks": d["round_tasks"][:12],
                        "round_ms": [round(x, 2) for x in d["round_ms"][:12]],
                        "n_rounds": len(d["round_tasks"]), "spilled": d["spilled_tasks"],
-                       "handoffs": d["handoffs"]}
+                       "handoffs": d["handoffs"], "presplit": d.get("presplit")}
                 if ref and a.world == 1 and not a.max_len:
                     out["verified_vs_cpu"] = d["digest"] == ref[0] and d["n_itemsets"] == ref[1]
+                if a.trace:
+                    out["trace"] = trace_summary(d)
                 print(json.dumps(out), flush=True)
+                comb["sum"] = (comb["sum"] + int(d["digest"][:16], 16)) % (1 << 64)
+                comb["xor"] ^= int(d["digest"][16:], 16)
+                comb["n"] += d["n_itemsets"]
+                if r > 0 or a.world == 1:  # rank 0's first call also allocates
+                    comb["slowest_ms"] = max(comb["slowest_ms"], d["phases_ms"]["total"])
+            if a.world > 1:
+                dg = f"{comb['sum']:016x}{comb['xor']:016x}"
+                ref = CPU_REF.get(ms)
+                print(json.dumps({"probe": "split", "min_support": ms, "rep": rep,
+                                  "world": a.world, "assign": a.assign,
+                                  "presplit_cost": a.presplit_cost, "n": comb["n"],
+                                  "digest": dg,
+                                  "verified_vs_cpu": (dg == ref[0] and comb["n"] == ref[1])
+                                  if ref and not a.max_len else None,
+                                  "slowest_rank_ms_excl_rank0": round(comb["slowest_ms"], 3)}),
+                      flush=True)
     return 0
+
+
+def trace_summary(d):
+    """Tail analysis of one stealing launch from the per-wave / per-task timing."""
+    import numpy as np
+    tr = np.asarray(d["trace"], np.int64)
+    if tr.size == 0:
+        return None
+    tick_ms = 1.0 / float(d["clock_khz"])
+    t0 = tr[:, 0].min()
+    span = (tr[:, 3].max() - t0) * tick_ms
+    first = (tr[:, 1] - t0) * tick_ms
+    last = (tr[:, 2] - t0) * tick_ms
+    busy = tr[:, 4] * tick_ms
+    tasks = tr[:, 5] >> 32
+    inbox = tr[:, 5] & 0xffffffff
+    pct = lambda x: [round(float(np.percentile(x, q)), 3) for q in (0, 10, 50, 90, 100)]
+    out = {"span_ms": round(span, 3), "busy_frac": round(float(busy.sum() / (len(tr) * span)), 3),
+           "first_task_start_ms_pctl": pct(first), "last_task_end_ms_pctl": pct(last),
+           "tasks_per_wave_pctl": pct(tasks), "inbox_per_wave_pctl": pct(inbox)}
+    tk = np.asarray(d.get("task_ticks", []), np.int64) * tick_ms
+    cost = np.asarray(d.get("task_cost", []), np.int64)
+    if tk.size and cost.size == tk.size:
+        bins = {}
+        for lo, hi in ((0, 1), (1, 4), (4, 16), (16, 64), (64, 256), (256, 1 << 30)):
+            m = (cost >= lo) & (cost < hi)
+            if m.any():
+                bins[f"{lo}-{hi}"] = [int(m.sum()), round(float(tk[m].mean()), 4),
+                                      round(float(tk[m].max()), 3)]
+        out["task_ms_by_cost"] = bins  # [tasks, mean ms, max ms] (own work, hand-offs excluded)
+        top = np.argsort(-tk)[:8]
+        out["top_tasks"] = [[int(q), int(cost[q]), round(float(tk[q]), 3)] for q in top]
+    return out
 
 
 if __name__ == "__main__":
