@@ -93,14 +93,15 @@ class Watchdog:
             self.name, self.deadline = None, None
 
 
-def run_serve_child(qps: str, duration: float, backend: str, timeout: float = 420.0) -> dict:
+def run_serve_child(qps: str, duration: float, backend: str, timeout: float = 420.0,
+                    extra=(), capacity: bool = True) -> dict:
     """Config 4 in a fresh child process (PVC populated by the real job on the CPU miner, the
     native-front server as its own child, the native open-loop load generator)."""
     fd, path = tempfile.mkstemp(prefix="kmls_serve_", suffix=".json")
     os.close(fd)
     cmd = [sys.executable, "-m", "kubernetes_machine_learning_server_amd.bench.bench_serve",
-           "--backend", backend, "--qps", qps, "--duration", str(duration), "--capacity",
-           "--json-out", path]
+           "--backend", backend, "--qps", qps, "--duration", str(duration),
+           "--json-out", path] + (["--capacity"] if capacity else []) + list(extra)
     try:
         p = subprocess.run(cmd, stdout=sys.stderr, stderr=sys.stderr, timeout=timeout)
         if p.returncode != 0:
@@ -136,6 +137,8 @@ def main() -> int:
                     help="offered QPS points for the serving half ('' = skip)")
     ap.add_argument("--serve-duration", type=float, default=4.0)
     ap.add_argument("--serve-backend", default="auto")
+    ap.add_argument("--no-serve-reference", action="store_true",
+                    help="skip the reference-stack serving baseline (uvicorn + Python matcher)")
     ap.add_argument("--no-levelwise", action="store_true")
     ap.add_argument("--no-config2", action="store_true")
     ap.add_argument("--no-config3", action="store_true")
@@ -157,6 +160,22 @@ def main() -> int:
         t = time.time()
         serve = run_serve_child(args.serve_qps, args.serve_duration, args.serve_backend)
         serve["wall_s"] = round(time.time() - t, 1)
+        # the same harness (open-loop native load generator, same PVC build, same queries)
+        # against the reference's serving stack: one uvicorn worker (rest_api/Dockerfile:28)
+        # running the reference-semantics Python matcher (rest_api/app/main.py:224-254)
+        if not args.no_serve_reference:
+            t = time.time()
+            ref = run_serve_child(args.serve_qps, args.serve_duration, "python", timeout=300,
+                                  extra=("--front", "uvicorn", "--workers", "1"),
+                                  capacity=False)
+            ref["wall_s"] = round(time.time() - t, 1)
+            serve["reference_stack"] = ref
+            try:
+                serve["p50_ratio_reference_over_this"] = [
+                    round(r["p50_ms"] / m["p50_ms"], 1)
+                    for r, m in zip(ref["points"], serve["points"]) if m.get("p50_ms")]
+            except Exception:  # noqa: BLE001 — a failed reference run leaves the field out
+                pass
 
     import numpy as np
     import torch
