@@ -140,6 +140,7 @@ def main() -> int:
     ap.add_argument("--no-serve-reference", action="store_true",
                     help="skip the reference-stack serving baseline (uvicorn + Python matcher)")
     ap.add_argument("--no-levelwise", action="store_true")
+    ap.add_argument("--no-emit", action="store_true", help="skip the materialising headline run")
     ap.add_argument("--no-config2", action="store_true")
     ap.add_argument("--no-config3", action="store_true")
     ap.add_argument("--cpu", action="store_true",
@@ -286,6 +287,19 @@ def main() -> int:
     })
     if serve is not None:
         out["serve"] = serve
+
+    # ---- the same problem MATERIALISED: every itemset written to an HBM trie arena ----
+    if not args.cpu and not args.no_emit:
+        wd.arm("emit", 600)
+        try:
+            e = bm.run_deep_emit(deep_miner, args.min_support, world, rank, args.warmup,
+                                 args.steps, barrier_sync, max_over_ranks, gather)
+            e["itemsets_per_s"] = round(h["n_itemsets"] / (e["ms_per_step"] / 1000.0), 1)
+            out["emit"] = e
+            out["value_emitted"] = e["itemsets_per_s"]
+        except Exception as ex:
+            out.setdefault("errors", {})["emit"] = repr(ex)[:300]
+        wd.disarm()
 
     # ---- the round-2 headline form (level-wise, trie + rule map in the step) ----
     if args.cpu:  # the GPU sections below have no CPU tier

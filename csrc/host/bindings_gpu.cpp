@@ -415,8 +415,9 @@ void register_gpu_bindings(py::module_& m) {
                            py::object comm, unsigned long long budget0, unsigned long long budget,
                            unsigned split_min, int blocks_per_cu, int stack_mb, bool steal,
                            unsigned steal_idle, int assign, bool trace, unsigned presplit_cost,
-                           unsigned long long presplit_budget) {
+                           unsigned long long presplit_budget, bool emit) {
         gpu::DeepOpts o;
+        o.emit = emit;
         o.assign = assign;
         o.trace = trace;
         o.presplit_cost = presplit_cost;
@@ -459,6 +460,10 @@ void register_gpu_bindings(py::module_& m) {
         ph["assign"] = r.ms_assign;
         ph["presplit"] = r.ms_presplit;
         d["presplit"] = py::make_tuple(r.presplit_in, r.presplit_out);
+        if (emit) {
+          d["arena_nodes"] = r.arena_nodes;
+          d["arena_cap"] = r.arena_cap;
+        }
         d["phases_ms"] = ph;
         if (trace) {
           const size_t nw = r.trace.size() / kern::kDeepTraceWords;
@@ -476,7 +481,44 @@ void register_gpu_bindings(py::module_& m) {
          py::arg("split_min") = 8u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0,
          py::arg("steal") = true, py::arg("steal_idle") = 1u, py::arg("assign") = 1,
          py::arg("trace") = false, py::arg("presplit_cost") = 16u,
-         py::arg("presplit_budget") = 1ull)
+         py::arg("presplit_budget") = 1ull, py::arg("emit") = false)
+      .def("deep_arena_digest", [](gpu::GpuMiner& g, int min_depth) {
+        gpu::GpuMiner::ArenaDigest r;
+        {
+          py::gil_scoped_release nogil;
+          r = g.deep_arena_digest(min_depth);
+        }
+        char buf[64];
+        std::snprintf(buf, sizeof buf, "%016llx%016llx", (unsigned long long)r.sum,
+                      (unsigned long long)r.xr);
+        py::dict d;
+        d["digest"] = std::string(buf);
+        d["sum"] = r.sum;
+        d["xor"] = r.xr;
+        d["n"] = r.n;
+        d["per_depth"] = r.per_depth;
+        return d;
+      }, py::arg("min_depth") = 1)
+      .def("deep_arena_download", [](gpu::GpuMiner& g, int64_t n) {
+        py::array_t<int64_t> parent((py::ssize_t)n);
+        py::array_t<int32_t> item((py::ssize_t)n);
+        py::array_t<uint32_t> count((py::ssize_t)n);
+        py::array_t<uint8_t> depth((py::ssize_t)n);
+        int64_t* pp = parent.mutable_data();
+        int32_t* pi = item.mutable_data();
+        uint32_t* pc = count.mutable_data();
+        uint8_t* pd = depth.mutable_data();
+        {
+          py::gil_scoped_release nogil;
+          g.deep_arena_download(n, pp, pi, pc, pd);
+        }
+        py::dict d;
+        d["parent"] = parent;
+        d["item"] = item;
+        d["count"] = count;
+        d["depth"] = depth;
+        return d;
+      }, py::arg("n"))
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
   py::class_<gpu::GpuRuleIndex, std::shared_ptr<gpu::GpuRuleIndex>>(m, "GpuRuleIndex")

@@ -93,7 +93,15 @@ DeepResult GpuMiner::mine_deep(double min_support, int max_len, int rank, int wo
   in.n_cus = n_cus_;
   in.stream = s;
   res.ms_prologue = ms_since(t0);
-  DeepLocal loc = deep_run(*deep_, in, rank, world, opt);
+  DeepLocal loc;
+  for (int attempt = 0;; ++attempt) {
+    try {
+      loc = deep_run(*deep_, in, rank, world, opt);
+      break;
+    } catch (const ArenaOverflow& ex) {  // emit: the arena is regrown from the count and rerun
+      if (attempt >= 2) throw;
+    }
+  }
   DeepBufs& b = *deep_;
   for (int d = 2; d < 64; ++d) per[(size_t)d] += loc.per_depth[(size_t)d];
   dsum += loc.dsum;
@@ -109,6 +117,8 @@ DeepResult GpuMiner::mine_deep(double min_support, int max_len, int rank, int wo
   res.ms_rounds = loc.ms_rounds;
   res.ms_assign = loc.ms_assign;
   res.ms_presplit = loc.ms_presplit;
+  res.arena_nodes = loc.arena_nodes;
+  res.arena_cap = deep_->arena_cap;
   res.presplit_in = loc.presplit_in;
   res.presplit_out = loc.presplit_out;
   res.trace = std::move(loc.trace);
@@ -156,6 +166,56 @@ DeepResult GpuMiner::mine_deep(double min_support, int max_len, int rank, int wo
   res.candidates = (int64_t)cands;
   res.ms_total = ms_since(t0);
   return res;
+}
+
+GpuMiner::ArenaDigest GpuMiner::deep_arena_digest(int min_depth) {
+  KMLS_CHECK(deep_ && deep_->arena_used > 0, "deep_arena_digest: no emit-mode mine_deep yet");
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  DeepBufs& b = *deep_;
+  const int64_t n = std::min(b.arena_used, b.arena_cap);
+  uint64_t* hash = nullptr;
+  unsigned long long* out = nullptr;
+  KMLS_HIP(hipMalloc((void**)&hash, (size_t)n * 8));
+  KMLS_HIP(hipMalloc((void**)&out, 66 * 8));
+  ArenaDigest r;
+  try {
+    KMLS_HIP(hipMemsetAsync(out, 0, 66 * 8, s));
+    kern::deep_arena_digest(b.n_parent, b.n_item, b.n_count, b.n_depth, n, d_ids_, b.max_depth,
+                            std::max(min_depth, 1), hash, out, s);
+    std::vector<unsigned long long> h(66);
+    KMLS_HIP(hipMemcpyAsync(h.data(), out, 66 * 8, hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipStreamSynchronize(s));
+    r.per_depth.assign(64, 0);
+    for (int d = 1; d < 62; ++d) r.per_depth[(size_t)d] = h[(size_t)(2 + d)];
+    r.sum = h[0];
+    r.xr = h[1];
+    for (int d = 1; d < 62; ++d) r.n += r.per_depth[(size_t)d];
+  } catch (...) {
+    (void)hipFree(hash);
+    (void)hipFree(out);
+    throw;
+  }
+  (void)hipFree(hash);
+  (void)hipFree(out);
+  return r;
+}
+
+void GpuMiner::deep_arena_download(int64_t n, int64_t* parent, int32_t* item, uint32_t* count,
+                                   uint8_t* depth) {
+  KMLS_CHECK(deep_ && n <= std::min(deep_->arena_used, deep_->arena_cap),
+             "deep_arena_download: n past the arena");
+  KMLS_HIP(hipSetDevice(device_));
+  DeepBufs& b = *deep_;
+  std::vector<uint32_t> p((size_t)n), it((size_t)n);
+  KMLS_HIP(hipMemcpy(p.data(), b.n_parent, (size_t)n * 4, hipMemcpyDeviceToHost));
+  KMLS_HIP(hipMemcpy(it.data(), b.n_item, (size_t)n * 4, hipMemcpyDeviceToHost));
+  KMLS_HIP(hipMemcpy(count, b.n_count, (size_t)n * 4, hipMemcpyDeviceToHost));
+  KMLS_HIP(hipMemcpy(depth, b.n_depth, (size_t)n, hipMemcpyDeviceToHost));
+  for (int64_t v = 0; v < n; ++v) {
+    parent[v] = p[(size_t)v] == 0xffffffffu ? -1 : (int64_t)p[(size_t)v];
+    item[v] = depth[v] ? fi_.ids[(size_t)it[(size_t)v]] : -1;
+  }
 }
 
 }  // namespace gpu

@@ -24,7 +24,8 @@ DeepBufs::~DeepBufs() {
   for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)req, (void*)inbox, (void*)inbox_state, (void*)heap[0],
                   (void*)heap[1], (void*)root, (void*)ctl, (void*)d_red, (void*)d_xor,
                   (void*)d_m, (void*)d_off, (void*)d_toff, (void*)d_cost, (void*)d_order,
-                  (void*)d_trace, (void*)d_ticks})
+                  (void*)d_trace, (void*)d_ticks, (void*)n_parent, (void*)n_item,
+                  (void*)n_count, (void*)n_depth, (void*)d_node_off})
     if (p) (void)hipFree(p);
   if (h_ctl) (void)hipHostFree(h_ctl);
 }
@@ -61,6 +62,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   const int64_t F = in.F;
   const int W = kern::deep_row_words(in.W_real);
   const int64_t Fpad = (F + 15) / 16 * 16;
+  const int E = opt.emit ? 1 : 0;  // emit mode: blocks carry a node-word row
   DeepLocal res;
 
   // width tier of every root class: its rows are projected onto tid(item), |tid(item)| = support
@@ -82,7 +84,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   const int64_t waves = (int64_t)grid * kern::deep_waves_per_block();
   const size_t stack_need = std::max<size_t>(
       opt.stack_mb > 0 ? (size_t)opt.stack_mb << 20 : env_bytes_mb("KMLS_DEEP_STACK_MB", 4),
-      4 * kern::deep_row_block_bytes(W, F));
+      4 * kern::deep_row_block_bytes(W, F, E));
   const int fcap = std::max(4096, kern::deep_min_fcap());
   if (b.waves < waves || b.stack_bytes < stack_need || b.fcap < fcap) {
     if (b.stacks) KMLS_HIP(hipFree(b.stacks));
@@ -163,7 +165,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       const int64_t mi = m[(size_t)i];
       if (mi < 0 || mi > F) throw std::runtime_error("deep_run: bad level-2 class size");
       pairs += mi;
-      off[(size_t)i + 1] = off[(size_t)i] + (int64_t)(wt[(size_t)i] + 1) * ((mi + 15) / 16 * 16) * 8;
+      off[(size_t)i + 1] = off[(size_t)i] + (int64_t)(wt[(size_t)i] + 1 + E) * ((mi + 15) / 16 * 16) * 8;
       toff[(size_t)i + 1] = toff[(size_t)i] + std::max<int64_t>(mi - 1, 0);
     }
     if (rank == 0) res.per_depth[2] = (uint64_t)pairs;
@@ -171,8 +173,52 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     ensure_root((size_t)off[(size_t)F], root_blk);
     KMLS_HIP(hipMemcpyAsync(b.d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, s));
     KMLS_HIP(hipMemcpyAsync(b.d_toff, toff.data(), toff.size() * 8, hipMemcpyHostToDevice, s));
+    kern::DeepNodes nodes{};
+    if (E) {
+      // the arena: level-1 nodes (ids = ranks), level-2 nodes (F + node_off[i] + slot), then
+      // per-wave chunks from node_top; sizes reset to 0 (unused ids) over what the last call used
+      // first guess: the two root levels x 8 and two node chunks per wave; a call that overflows
+      // learns the exact need (node_top) and reruns
+      const int64_t need = std::max<int64_t>({(F + pairs) * 8 + waves * 2 * kern::deep_node_chunk(),
+                                              b.arena_cap, (int64_t)(b.arena_used * 1.1)});
+      if (need >= ((int64_t)1 << 32))
+        throw std::runtime_error("deep_run: emit needs more than 2^32 trie nodes (u32 parent "
+                                 "ids); use the count-only miner at this support");
+      if (b.arena_cap < need) {
+        for (void* p : {(void*)b.n_parent, (void*)b.n_item, (void*)b.n_count, (void*)b.n_depth})
+          if (p) KMLS_HIP(hipFree(p));
+        KMLS_HIP(hipMalloc((void**)&b.n_parent, (size_t)need * 4));
+        KMLS_HIP(hipMalloc((void**)&b.n_item, (size_t)need * 4));
+        KMLS_HIP(hipMalloc((void**)&b.n_count, (size_t)need * 4));
+        KMLS_HIP(hipMalloc((void**)&b.n_depth, (size_t)need));
+        KMLS_HIP(hipMemsetAsync(b.n_depth, 0, (size_t)need, s));
+        b.arena_cap = need;
+        b.arena_used = 0;
+      } else if (b.arena_used > 0) {
+        KMLS_HIP(hipMemsetAsync(b.n_depth, 0, (size_t)std::min(b.arena_used, b.arena_cap), s));
+      }
+      int64_t c1 = b.node_off_cap;
+      grow(b.d_node_off, c1, F + 1);
+      b.node_off_cap = c1;
+      std::vector<int64_t> noff((size_t)F + 1, 0);
+      std::vector<uint32_t> l1p((size_t)F, 0xffffffffu), l1i((size_t)F);
+      std::vector<uint8_t> l1d((size_t)F, 1);
+      for (int64_t i = 0; i < F; ++i) {
+        noff[(size_t)i + 1] = noff[(size_t)i] + m[(size_t)i];
+        l1i[(size_t)i] = (uint32_t)i;
+      }
+      KMLS_HIP(hipMemcpyAsync(b.d_node_off, noff.data(), (size_t)(F + 1) * 8, hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(b.n_parent, l1p.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(b.n_item, l1i.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(b.n_count, in.counts, (size_t)F * 4, hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipMemcpyAsync(b.n_depth, l1d.data(), (size_t)F, hipMemcpyHostToDevice, s));
+      b.h_ctl->node_top = (unsigned long long)(F + pairs);
+      KMLS_HIP(hipMemcpyAsync(&b.ctl->node_top, &b.h_ctl->node_top, 8, hipMemcpyHostToDevice, s));
+      KMLS_HIP(hipStreamSynchronize(s));  // the pageable staging vectors die at scope end
+      nodes = kern::DeepNodes{b.n_parent, b.n_item, b.n_count, b.n_depth, b.d_node_off};
+    }
     kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, b.d_m, b.d_off, b.root,
-                    rank == 0 ? b.ctl : nullptr, true, s);
+                    rank == 0 ? b.ctl : nullptr, true, s, E ? &nodes : nullptr);
     const int64_t T = toff[(size_t)F];
     const int64_t* d_order = nullptr;
     if (deeper && T > 0 && (opt.assign == 1 || opt.trace)) {
@@ -185,7 +231,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       grow(b.d_cost, c1, T);
       grow(b.d_order, c2, T);
       b.t_cap = std::max(c1, c2);
-      kern::deep_task_cost(b.d_off, b.d_m, b.d_toff, F, b.root, in.minsup, b.d_cost, s);
+      kern::deep_task_cost(b.d_off, b.d_m, b.d_toff, F, b.root, in.minsup, b.d_cost, s, E);
       std::vector<uint32_t> cost((size_t)T);
       KMLS_HIP(hipMemcpyAsync(cost.data(), b.d_cost, (size_t)T * 4, hipMemcpyDeviceToHost, s));
       KMLS_HIP(hipStreamSynchronize(s));
@@ -225,7 +271,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     }
     if (n_tasks > 0)
       kern::deep_root_tasks(b.d_off, b.d_m, b.d_toff, F, b.root, (const uint64_t*)b.root, Fpad, W,
-                            rank, world, d_order, n_tasks, b.q[0], s);
+                            rank, world, d_order, n_tasks, b.q[0], s, E);
     KMLS_HIP(hipStreamSynchronize(s));  // pageable off/toff die at scope end
     res.level2_tasks = T;
   }
@@ -247,6 +293,11 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   a.heap_cap = b.heap_cap;
   a.trace = nullptr;
   a.task_ticks = nullptr;
+  a.node_parent = E ? b.n_parent : nullptr;
+  a.node_item = E ? b.n_item : nullptr;
+  a.node_count = E ? b.n_count : nullptr;
+  a.node_depth = E ? b.n_depth : nullptr;
+  a.node_cap = E ? (unsigned long long)b.arena_cap : 0ull;
   if (opt.trace && opt.steal && n_tasks > 0) {
     int64_t c1 = b.trace_cap, c2 = b.ticks_cap;
     grow(b.d_trace, c1, waves * kern::kDeepTraceWords);
@@ -401,6 +452,15 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   KMLS_HIP(hipStreamSynchronize(s));
   res.ms_rounds = ms_since(t2);
   for (int d = 3; d < 64; ++d) res.per_depth[(size_t)d] += b.h_ctl->per_depth[d];
+  if (E) {
+    const int64_t used = (int64_t)b.h_ctl->node_top;
+    b.arena_used = used;  // (past the capacity after an overflow: the next call's size)
+    b.max_depth = 2;
+    for (int d = 3; d < 64; ++d)
+      if (b.h_ctl->per_depth[d]) b.max_depth = d;
+    if (used > b.arena_cap) throw ArenaOverflow(used);
+    res.arena_nodes = used;
+  }
   res.dsum = b.h_ctl->digest_sum;  // level-2 terms (rank 0) + the rounds
   res.dxor = b.h_ctl->digest_xor;
   res.candidates = b.h_ctl->candidates;

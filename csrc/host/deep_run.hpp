@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <stdexcept>
 #include <vector>
 
 #include "../kernels/kernels.hpp"
@@ -42,6 +43,15 @@ struct DeepBufs {
   uint32_t* d_cost = nullptr;   // [T] level-3 task costs (assign = 1)
   int64_t* d_order = nullptr;   // [T] this rank's task ids in queue order
   int64_t t_cap = 0;
+  // emit mode: the node arena (SoA, arena_cap ids) and the level-2 node bases
+  unsigned* n_parent = nullptr;
+  unsigned* n_item = nullptr;
+  unsigned* n_count = nullptr;
+  unsigned char* n_depth = nullptr;
+  int64_t arena_cap = 0, arena_used = 0;
+  int max_depth = 0;
+  int64_t* d_node_off = nullptr;
+  int64_t node_off_cap = 0;
   unsigned long long* d_trace = nullptr;  // [waves * kDeepTraceWords] (opts.trace)
   unsigned long long* d_ticks = nullptr;  // [T] (opts.trace)
   int64_t trace_cap = 0, ticks_cap = 0;
@@ -77,12 +87,19 @@ struct DeepLocal {
   std::vector<double> round_ms;
   double ms_alloc = 0, ms_root = 0, ms_rounds = 0, ms_assign = 0, ms_presplit = 0;
   int64_t presplit_in = 0, presplit_out = 0;
+  int64_t arena_nodes = 0;  // emit: node ids used, holes included
   std::vector<uint64_t> trace, task_ticks;  // opts.trace
   std::vector<int64_t> task_ids;
   std::vector<uint32_t> task_cost;
   double clock_khz = 0;
 };
 
+// emit mode: the arena was too small (node_top counts on past its end); `needed` ids
+struct ArenaOverflow : std::runtime_error {
+  int64_t needed;
+  explicit ArenaOverflow(int64_t n)
+      : std::runtime_error("deep_run: node arena overflow"), needed(n) {}
+};
 DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const DeepOpts& opt);
 
 }  // namespace gpu

@@ -169,6 +169,9 @@ struct DeepOpts {
   // as one task per member; the stealing launch then starts from those finer tasks (0 = off)
   unsigned presplit_cost = 16;
   unsigned long long presplit_budget = 1;
+  // materialise: every frequent itemset becomes a node of an HBM trie arena (parent node id,
+  // item rank, support, size), kept on the device after the call (GpuMiner::deep_arena_*)
+  bool emit = false;
 };
 struct DeepResult {
   std::vector<uint64_t> per_level;  // [d] = frequent itemsets of size d (index 0 unused)
@@ -183,6 +186,8 @@ struct DeepResult {
   double ms_assign = 0;               // task costs + ordering (inside ms_root)
   int64_t presplit_in = 0, presplit_out = 0;  // heavy tasks pre-split, tasks they became
   double ms_presplit = 0;
+  int64_t arena_nodes = 0;            // emit: node ids used (holes included), arena capacity
+  int64_t arena_cap = 0;
   // opts.trace: per wave kern::kDeepTraceWords words; per queued task (queue order) its id,
   // its class-size cost and the ticks its dequeuing wave spent on it; the clock rate
   std::vector<uint64_t> trace, task_ticks;
@@ -249,6 +254,17 @@ class GpuMiner {
   // digests are combined through `comm` (nullptr: world must be 1, or the caller combines).
   DeepResult mine_deep(double min_support, int max_len, int rank, int world, Comm* comm,
                        const DeepOpts& opts);
+  // The trie arena of the last mine_deep(emit) call: its content digest ([min_depth, ...] sizes,
+  // set hashes rebuilt size by size on the device; equal to the count-only digest of the same
+  // share) and, for small results, the arena itself (ids [0, n): parent node id or -1, original
+  // item id, support, size; size 0 = an unused id)
+  struct ArenaDigest {
+    uint64_t sum = 0, xr = 0, n = 0;
+    std::vector<uint64_t> per_depth;
+  };
+  ArenaDigest deep_arena_digest(int min_depth);
+  void deep_arena_download(int64_t n, int64_t* parent, int32_t* item, uint32_t* count,
+                           uint8_t* depth);
 
   // Frequent items of the last select(): ids (ascending support) and counts.
   const FrequentItems& frequent() const { return fi_; }

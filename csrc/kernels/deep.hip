@@ -51,6 +51,7 @@ constexpr int kBatchFrames = 64;     // frames one batch step may take
 constexpr int kBStack = 96;          // blocks on one wave's memory stack
 constexpr unsigned kSingle = 1u << 8;  // frame flag: expand only its first member
 constexpr unsigned kDone = 1u << 31;   // steal mode: ready-flag value epoch ^ kDone = no task
+constexpr unsigned kNodeChunk = 4096;  // emit mode: node ids a wave takes from ctl->node_top
 
 // frame meta: bits 0..7 prefix size, bit 8 single, bits 9..15 block width (words), bits 16..31
 // block-stack index + 1 (0 = external)
@@ -253,7 +254,37 @@ struct WaveState {
   unsigned nf;                 // frames on the stack
   unsigned nb;                 // blocks on the memory stack
   unsigned long long mem_top;  // bytes used in the wave's stack region
+  unsigned long long ncur, nend;  // emit mode: the wave's current chunk of node ids
 };
+
+// emit mode: n consecutive node ids (uniform); a new chunk of the global counter when the
+// wave's current one is used up (the tail of the old chunk stays unused: size 0)
+__device__ __forceinline__ unsigned long long alloc_nodes(const DeepArgs& a, WaveState& st,
+                                                          unsigned n, int lane) {
+  if (st.ncur + n > st.nend) {
+    const unsigned long long chunk = n > kNodeChunk ? n : kNodeChunk;
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(&a.ctl->node_top, chunk);
+    b = uni64(bcast64(b, 0));
+    st.ncur = b;
+    st.nend = b + chunk;
+  }
+  const unsigned long long r = st.ncur;
+  st.ncur += n;
+  return r;
+}
+
+// emit mode: one trie node (ids past the arena are counted by node_top but not written)
+__device__ __forceinline__ void put_node(const DeepArgs& a, unsigned long long id,
+                                         unsigned long long parent, unsigned item, unsigned count,
+                                         unsigned depth) {
+  if (id < a.node_cap) {
+    a.node_parent[id] = (unsigned)parent;
+    a.node_item[id] = item;
+    a.node_count[id] = count;
+    a.node_depth[id] = (unsigned char)depth;
+  }
+}
 
 struct WaveAcc {
   unsigned long long dsum, dxor, cands, chunks, budget_used;
@@ -311,10 +342,11 @@ template <int MAXT>
 __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st,
                                             WaveLds<MAXT>& L, int lane, bool optional,
                                             unsigned ns) {
+  const unsigned E = a.node_parent != nullptr;  // emit mode: the node-word row
   unsigned long long bytes_tot = 0, nt_tot = 0;
   for (unsigned f = 0; f < ns; ++f) {
     const DeepFrame fr = load_frame(fst + f, lane);
-    bytes_tot += (unsigned long long)(meta_width(fr.meta) + 1) * roundup16(fr.m) * 8ull;
+    bytes_tot += (unsigned long long)(meta_width(fr.meta) + 1 + E) * roundup16(fr.m) * 8ull;
     const bool single = (fr.meta & kSingle) != 0;
     nt_tot += (!single && fr.m > a.split_min) ? fr.m - 1 : 1;
   }
@@ -353,7 +385,7 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
     const unsigned long long npad = roundup16(m);
     const unsigned long long* src = (const unsigned long long*)fr.blk;
     unsigned long long* dst = (unsigned long long*)(a.heap + hoff);
-    const unsigned long long tot = (unsigned long long)(wt + 1) * m;
+    const unsigned long long tot = (unsigned long long)(wt + 1 + E) * m;
     for (unsigned long long e = lane; e < tot; e += 64) {
       const unsigned long long w = e / m, k = e - w * m;
       if (a.steal)
@@ -377,7 +409,7 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
       else
         store_frame(out + q + k, o);
     }
-    hoff += (unsigned long long)(wt + 1) * npad * 8ull;
+    hoff += (unsigned long long)(wt + 1 + E) * npad * 8ull;
     q += nt;
   }
   if (a.steal) {
@@ -410,8 +442,9 @@ __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst,
   if (!uni(__shfl(ok, 0, 64))) return false;
   const DeepFrame fr = load_frame(fst, lane);
   const unsigned m = fr.m, wt = meta_width(fr.meta);
+  const unsigned E = a.node_parent != nullptr;
   const unsigned long long npad = roundup16(m);
-  const unsigned long long bytes = (unsigned long long)(wt + 1) * npad * 8ull;
+  const unsigned long long bytes = (unsigned long long)(wt + 1 + E) * npad * 8ull;
   unsigned long long base = 0;
   if (lane == 0) base = atomicAdd(&a.ctl->heap_top, bytes);
   base = uni64(bcast64(base, 0));
@@ -421,7 +454,7 @@ __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst,
   }
   const unsigned long long* src = (const unsigned long long*)fr.blk;
   unsigned long long* dst = (unsigned long long*)(a.heap + base);
-  const unsigned long long tot = (unsigned long long)(wt + 1) * m;
+  const unsigned long long tot = (unsigned long long)(wt + 1 + E) * m;
   for (unsigned long long e = lane; e < tot; e += 64) {
     const unsigned long long w = e / m, k = e - w * m;
     st_agent(dst + w * npad + k, src[w * fr.pad + fr.s0 + k]);
@@ -462,6 +495,9 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
   const unsigned ia = top.s0;
   const unsigned long long ih_a = ihp[ia + vzero()];
   const unsigned long long h_a = top.hash + ih_a;
+  const unsigned E = a.node_parent != nullptr;
+  const unsigned long long* nwp = ihp + top.pad;  // emit mode: node words
+  const unsigned long long node_a = E ? (nwp[ia + vzero()] & kDeepNodeMask) : 0ull;
   unsigned wt_out = WT;
   if (WT > 1 && deeper && nc >= 2) {
     const unsigned s = proj_setup<WT>(L.proj, blk, top.pad, ia, lane);
@@ -490,6 +526,15 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
         write_proj<WT>(cb, cpad, pos, surv, v, L.proj, wt_out, ih_b);
       } else if (surv) {
         write_row<WT>(cb, cpad, pos, v, ih_b);
+      }
+    }
+    if (E && mask) {
+      const unsigned long long nb0 = alloc_nodes(a, st, (unsigned)__popcll(mask), lane);
+      if (surv) {
+        const unsigned long long id = nb0 + (unsigned long long)__popcll(mask & lanelt);
+        const unsigned long long nw_b = nwp[jb];
+        put_node(a, id, node_a, (unsigned)(nw_b >> 40), c, depth + 2);
+        if (deeper) cb[(unsigned long long)(wt_out + 1) * cpad + pos] = ((nw_b >> 40) << 40) | id;
       }
     }
     S += (unsigned)__popcll(mask);
@@ -522,7 +567,7 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
     }
     st.nb += 1;
     st.nf += 1;
-    st.mem_top += (unsigned long long)(wt_out + 1) * cpad * 8ull;
+    st.mem_top += (unsigned long long)(wt_out + 1 + E) * cpad * 8ull;
   }
 }
 
@@ -599,6 +644,8 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
   const unsigned long long* bblk = (const unsigned long long*)top.blk;
   const unsigned long long bpad = top.pad;
   const unsigned long long* ihp = bblk + (unsigned long long)WT * bpad;
+  const unsigned E = a.node_parent != nullptr;
+  const unsigned long long* nwp = ihp + bpad;  // emit mode: node words
   unsigned S = 0, gbase = 0;
   for (unsigned c0 = 0; c0 < P; c0 += 64) {
     const unsigned p = c0 + lane;
@@ -630,6 +677,17 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
       const DigestTerms dt = digest_terms(L.f_hash[f] + ih_a + ih_b, c);
       acc.dsum += dt.sum;
       acc.dxor ^= dt.xr;
+    }
+    if (E && mask) {
+      const unsigned long long nb0 = alloc_nodes(a, st, (unsigned)__popcll(mask), lane);
+      if (surv) {
+        const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
+        const unsigned long long id = nb0 + (unsigned long long)__popcll(mask & lanelt);
+        const unsigned long long nw_b = nwp[sb];
+        put_node(a, id, nwp[sa] & kDeepNodeMask, (unsigned)(nw_b >> 40), c,
+                 meta_depth(top.meta) + 2);
+        cb[(unsigned long long)(WT + 1) * cpad + pos] = ((nw_b >> 40) << 40) | id;
+      }
     }
     if (head) {
       const unsigned long long after = hmask & ~((2ull << lane) - 1ull);  // later run heads
@@ -691,7 +749,7 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
     }
     st.nb += 1;
     st.nf += pushed;
-    st.mem_top += (unsigned long long)(WT + 1) * cpad * 8ull;
+    st.mem_top += (unsigned long long)(WT + 1 + E) * cpad * 8ull;
   }
 }
 
@@ -734,7 +792,8 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
   WaveAcc acc{0, 0, 0, 0, 0};
   __builtin_amdgcn_wave_barrier();
 
-  WaveState st{0, 0, 0};
+  WaveState st{0, 0, 0, 0, 0};
+  const unsigned E = a.node_parent != nullptr;
   bool failed = false;
   const unsigned long long t_start = wall_clock64();
   auto timed_out = [&]() {
@@ -856,7 +915,7 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
       const unsigned long long pairs = (unsigned long long)m * (m - 1) / 2;
       const bool row_mode = (top.meta & kSingle) || pairs > (unsigned long long)kCap;
       const unsigned long long need =
-          (unsigned long long)(wt + 1) * roundup16(row_mode ? m : kCap) * 8ull;
+          (unsigned long long)(wt + 1 + E) * roundup16(row_mode ? m : kCap) * 8ull;
       if (st.mem_top + need > a.stack_bytes || st.nf + kCap + 2 > (unsigned)a.fcap ||
           st.nb + 1 >= (unsigned)kBStack || (!a.steal && acc.budget_used >= a.budget)) {
         if (spill_frames<MAXT>(a, fst, st, L, lane, false, st.nf) < 0) failed = true;
@@ -975,7 +1034,7 @@ template <int WT>
 __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* root, long long Fpad,
                                                    long long F, unsigned minsup, int32_t* m_out,
                                                    const long long* blk_off, char* base,
-                                                   DeepCtl* ctl, int fill) {
+                                                   DeepCtl* ctl, int fill, DeepNodes nodes) {
   __shared__ ProjLds<WT> projs[kWaves];
   const int lane = threadIdx.x & 63;
   const long long i = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -987,11 +1046,12 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
   unsigned long long* cb = nullptr;
   unsigned long long cpad = 0;
   unsigned wt_out = WT;
+  const unsigned E = nodes.parent != nullptr;  // emit mode: node-word row + level-2 nodes
   if (fill) {
     cpad = roundup16((unsigned long long)m_out[i]);
     if (cpad == 0) return;  // wave-uniform: no frequent pair
     cb = (unsigned long long*)(base + blk_off[i]);
-    wt_out = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * cpad)) - 1u;
+    wt_out = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * cpad)) - 1u - E;
     if (wt_out < (unsigned)WT) proj_setup<WT>(PL, root, (unsigned long long)Fpad, (unsigned)i, lane);
   }
   const bool proj = wt_out < (unsigned)WT;
@@ -1017,6 +1077,14 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
         dsum += dt.sum;
         dxor ^= dt.xr;
       }
+      if (E && surv) {  // level-2 node (i, jb): id F + node_off[i] + slot
+        const unsigned long long id = (unsigned long long)(F + nodes.node_off[i] + pos);
+        nodes.parent[id] = (unsigned)i;
+        nodes.item[id] = (unsigned)jb;
+        nodes.count[id] = c;
+        nodes.depth[id] = 2;
+        cb[(unsigned long long)(wt_out + 1) * cpad + pos] = ((unsigned long long)jb << 40) | id;
+      }
     }
     S += (unsigned)__popcll(mask);
   }
@@ -1041,7 +1109,8 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
 __global__ void k_deep_root_tasks(const long long* blk_off, const int32_t* m, const long long* task_off,
                                   long long F, char* base, const unsigned long long* root,
                                   long long Fpad, int W, int rank, int world,
-                                  const long long* order, long long n, DeepFrame* out) {
+                                  const long long* order, long long n, DeepFrame* out,
+                                  unsigned extra) {
   for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n;
        q += (long long)gridDim.x * blockDim.x) {
     const long long t = order ? order[q] : q * world + rank;
@@ -1056,7 +1125,7 @@ __global__ void k_deep_root_tasks(const long long* blk_off, const int32_t* m, co
     const int mi = m[i];
     const long long k = t - task_off[i];
     const unsigned long long pad = roundup16((unsigned long long)mi);
-    const unsigned wt = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * pad)) - 1u;
+    const unsigned wt = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * pad)) - 1u - extra;
     DeepFrame f;
     f.blk = (unsigned long long)(base + blk_off[i]);
     f.hash = root[(unsigned long long)W * Fpad + i];
@@ -1073,14 +1142,14 @@ __global__ void k_deep_root_tasks(const long long* blk_off, const int32_t* m, co
 __global__ __launch_bounds__(256) void k_deep_task_cost(const long long* blk_off, const int32_t* m,
                                                         const long long* task_off, long long F,
                                                         const char* base, unsigned minsup,
-                                                        unsigned* cost) {
+                                                        unsigned* cost, unsigned extra) {
   const long long i = blockIdx.x;
   if (i >= F) return;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int mi = m[i];
   if (mi < 2) return;
   const unsigned long long pad = roundup16((unsigned long long)mi);
-  const unsigned wt = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * pad)) - 1u;
+  const unsigned wt = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * pad)) - 1u - extra;
   const unsigned long long* blk = (const unsigned long long*)(base + blk_off[i]);
   for (int k = wid; k < mi - 1; k += (int)(blockDim.x >> 6)) {
     unsigned c = 0;
@@ -1093,6 +1162,39 @@ __global__ __launch_bounds__(256) void k_deep_task_cost(const long long* blk_off
       c += (unsigned)__popcll(__ballot(j < mi && pc >= minsup));
     }
     if (lane == 0) cost[task_off[i] + k] = c;
+  }
+}
+
+// emit-mode verification, one pass per itemset size d: every node of size d takes its set hash
+// from its parent's (size d-1, hashed in the previous pass) plus its item's mix, then adds its
+// digest terms; out = [sum, xor, per_depth[64]]
+__global__ __launch_bounds__(256) void k_arena_digest(const unsigned* parent, const unsigned* item,
+                                                      const unsigned* count,
+                                                      const unsigned char* depth, long long n,
+                                                      const int32_t* ids, int d, int count_it,
+                                                      unsigned long long* hash,
+                                                      unsigned long long* out) {
+  unsigned long long sum = 0, xr = 0, cnt = 0;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+       v += (long long)gridDim.x * blockDim.x) {
+    if (depth[v] != d) continue;
+    const unsigned long long h = (d == 1 ? 0ull : hash[parent[v]]) + item_mix((unsigned long long)ids[item[v]]);
+    hash[v] = h;
+    if (!count_it) continue;
+    const DigestTerms t = digest_terms(h, count[v]);
+    sum += t.sum;
+    xr ^= t.xr;
+    cnt += 1;
+  }
+  for (int off = 32; off; off >>= 1) {
+    sum += shfl_xor64(sum, off);
+    xr ^= shfl_xor64(xr, off);
+    cnt += shfl_xor64(cnt, off);
+  }
+  if ((threadIdx.x & 63) == 0 && cnt) {
+    atomicAdd(out, sum);
+    atomicXor(out + 1, xr);
+    atomicAdd(out + 2 + d, cnt);
   }
 }
 
@@ -1118,6 +1220,16 @@ void by_tier(int W, Fn&& fn) {
 
 }  // namespace
 
+void deep_arena_digest(const unsigned* parent, const unsigned* item, const unsigned* count,
+                       const unsigned char* depth, int64_t n, const int32_t* ids, int max_depth,
+                       int min_depth, uint64_t* hash, unsigned long long* out, hipStream_t s) {
+  if (n <= 0) return;
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+  for (int d = 1; d <= max_depth && d < 62; ++d)
+    hipLaunchKernelGGL(k_arena_digest, dim3(grid), dim3(256), 0, s, parent, item, count, depth,
+                       (long long)n, ids, d, d >= min_depth ? 1 : 0, (unsigned long long*)hash, out);
+}
+
 int deep_max_words() { return 64; }
 int deep_tier(int words) { return (int)tier_of((unsigned)std::max(words, 1)); }
 int deep_row_words(int W) { return deep_tier(W); }
@@ -1128,9 +1240,10 @@ int deep_waves_per_simd(int maxt) {
 }
 int deep_waves_per_block() { return kWaves; }
 int deep_min_fcap() { return kCap + 64; }
+int deep_node_chunk() { return (int)kNodeChunk; }
 
-size_t deep_row_block_bytes(int W, int64_t m) {
-  return (size_t)(W + 1) * (size_t)roundup16((unsigned long long)std::max<int64_t>(m, kCap)) * 8;
+size_t deep_row_block_bytes(int W, int64_t m, int extra) {
+  return (size_t)(W + 1 + extra) * (size_t)roundup16((unsigned long long)std::max<int64_t>(m, kCap)) * 8;
 }
 
 void deep_transpose(const uint64_t* bm, int64_t Wp, int64_t F, int W, int W_real,
@@ -1143,33 +1256,35 @@ void deep_transpose(const uint64_t* bm, int64_t Wp, int64_t F, int W, int W_real
 
 void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t minsup,
                int32_t* m, const int64_t* blk_off, char* base, DeepCtl* ctl, bool fill,
-               hipStream_t s) {
+               hipStream_t s, const DeepNodes* nodes) {
   const unsigned grid = (unsigned)((F + 3) / 4);
   if (!grid) return;
+  DeepNodes nd{};
+  if (nodes && fill) nd = *nodes;
   by_tier(W, [&](auto wt) {
     hipLaunchKernelGGL(k_deep_root<decltype(wt)::value>, dim3(grid), dim3(256), 0, s,
                        (const unsigned long long*)root, (long long)Fpad, (long long)F, minsup,
-                       m, (const long long*)blk_off, base, ctl, fill ? 1 : 0);
+                       m, (const long long*)blk_off, base, ctl, fill ? 1 : 0, nd);
   });
 }
 
 void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
                      char* base, const uint64_t* root, int64_t Fpad, int W, int rank, int world,
-                     const int64_t* order, int64_t n, DeepFrame* out, hipStream_t s) {
+                     const int64_t* order, int64_t n, DeepFrame* out, hipStream_t s, int extra) {
   if (F <= 0 || n <= 0) return;
   const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(k_deep_root_tasks, dim3(grid), dim3(256), 0, s,
                      (const long long*)blk_off, m, (const long long*)task_off, (long long)F, base,
                      (const unsigned long long*)root, (long long)Fpad, W, rank, world,
-                     (const long long*)order, (long long)n, out);
+                     (const long long*)order, (long long)n, out, (unsigned)extra);
 }
 
 void deep_task_cost(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
-                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s) {
+                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s, int extra) {
   if (F <= 0) return;
   hipLaunchKernelGGL(k_deep_task_cost, dim3((unsigned)F), dim3(256), 0, s,
                      (const long long*)blk_off, m, (const long long*)task_off, (long long)F, base,
-                     minsup, cost);
+                     minsup, cost, (unsigned)extra);
 }
 
 int deep_count_wps(int maxt, int want) {

@@ -25,6 +25,8 @@ struct DeepCtl {  // per-round control + accumulated results (zeroed once per ca
   unsigned long long heap_top;    // bytes of the out heap used (zeroed per round)
   unsigned long long pending;     // steal mode: queued + running tasks (0 = the launch is done)
   unsigned long long handoffs;    // steal mode: classes handed to a requesting wave's inbox
+  unsigned long long node_top;    // emit mode: node ids handed out (chunks; keeps counting past
+                                  // the arena's capacity, so the host learns the size it needs)
   unsigned long long digest_sum, digest_xor;
   unsigned long long candidates, chunks;
   unsigned long long per_depth[64];
@@ -67,8 +69,18 @@ struct DeepArgs {
   // initial task the ticks its dequeuing wave spent on it (parts handed away excluded)
   unsigned long long* trace;
   unsigned long long* task_ticks;
+  // emit mode (node_parent != nullptr): every frequent itemset of size >= 3 found in the launch
+  // becomes a trie node (parent node id, last item's frequency rank, support, size) at an id from
+  // a per-wave chunk of ctl->node_top; unused ids keep size 0.  Blocks then carry one more row
+  // per slot: (rank << 40) | node id of the member itemset.
+  unsigned* node_parent;
+  unsigned* node_item;
+  unsigned* node_count;
+  unsigned char* node_depth;
+  unsigned long long node_cap;
 };
 constexpr int kDeepTraceWords = 6;
+constexpr unsigned long long kDeepNodeMask = (1ull << 40) - 1;  // node id bits of a node word
 int deep_max_words();
 int deep_tier(int words);     // smallest instantiated block width >= words
 int deep_row_words(int W);    // root block width for W-word rows (a tier)
@@ -77,20 +89,37 @@ int deep_waves_per_simd(int maxt);  // its default occupancy (and blocks per CU)
 int deep_count_wps(int maxt, int want);  // instance occupancy: `want` if instantiated
 int deep_waves_per_block();
 int deep_min_fcap();
-size_t deep_row_block_bytes(int W, int64_t m);  // stack room one step over m members may need
+int deep_node_chunk();  // emit mode: node ids a wave takes at a time
+size_t deep_row_block_bytes(int W, int64_t m, int extra = 0);  // stack room of a step over m members
+                                                               // (extra: emit mode's node row)
 void deep_transpose(const uint64_t* bm, int64_t Wp, int64_t F, int W, int W_real,
                     const int32_t* ids, uint64_t* root, int64_t Fpad, hipStream_t s);
+// level-2 classes; emit (nodes != nullptr, fill pass): blocks carry the node-word row, and the
+// level-2 nodes are written at ids F + node_off[i] + slot
+struct DeepNodes {
+  unsigned* parent;
+  unsigned* item;
+  unsigned* count;
+  unsigned char* depth;
+  const int64_t* node_off;  // [F] level-2 node base of root class i
+};
 void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t minsup,
                int32_t* m, const int64_t* blk_off, char* base, DeepCtl* ctl, bool fill,
-               hipStream_t s);
+               hipStream_t s, const DeepNodes* nodes = nullptr);
+// emit-mode verification: digest terms and per-size counts of the node arena (ids [0, n)) for
+// sizes >= min_depth, set hashes built size by size (hash = parent's + item_mix(ids[item]));
+// out = [sum, xor, per_depth[64]] accumulated; hash = scratch [n] u64
+void deep_arena_digest(const unsigned* parent, const unsigned* item, const unsigned* count,
+                       const unsigned char* depth, int64_t n, const int32_t* ids, int max_depth,
+                       int min_depth, uint64_t* hash, unsigned long long* out, hipStream_t s);
 // this rank's level-3 task frames: out[q] = task order[q] (order == nullptr: task q*world+rank),
 // q < n; task t = (root i, member k) with t = task_off[i] + k
 void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
                      char* base, const uint64_t* root, int64_t Fpad, int W, int rank, int world,
-                     const int64_t* order, int64_t n, DeepFrame* out, hipStream_t s);
+                     const int64_t* order, int64_t n, DeepFrame* out, hipStream_t s, int extra = 0);
 // level-3 survivors of every task (the size of the class the task expands): cost[t]
 void deep_task_cost(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
-                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s);
+                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s, int extra = 0);
 void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s);
 
 // ---- mining (mine.hip) ----

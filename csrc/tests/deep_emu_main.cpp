@@ -4,7 +4,7 @@
 // content digest must equal mine_cpu_count's.
 //
 //   deep_emu n_tx n_items mean_len genres affinity min_support [budget0 budget split_min stack_mb
-//            world max_len steal steal_idle presplit_cost]
+//            world max_len steal steal_idle presplit_cost emit]
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -37,6 +37,7 @@ int main(int argc, char** argv) {
   opt.steal = argc > 13 ? std::atoi(argv[13]) != 0 : true;
   if (argc > 14) opt.steal_idle = (unsigned)std::atoi(argv[14]);
   if (argc > 15) opt.presplit_cost = (unsigned)std::atoi(argv[15]);
+  opt.emit = argc > 16 && std::atoi(argv[16]) != 0;
   opt.blocks_per_cu = 1;
 
   std::vector<int64_t> ptr;
@@ -75,6 +76,9 @@ int main(int argc, char** argv) {
   }
   int rounds = 0;
   long long spilled = 0, handoffs = 0;
+  // emit mode: the arenas' own digest (set hashes rebuilt along parent ids, size by size)
+  std::vector<uint64_t> eper(64, 0);
+  uint64_t esum = 0, exor = 0;
   for (int rank = 0; rank < world; ++rank) {
     gpu::DeepBufs b;
     gpu::DeepInput in;
@@ -87,16 +91,43 @@ int main(int argc, char** argv) {
     in.minsup = fi.minsup2;
     in.max_len = max_len;
     in.n_cus = 2;
-    gpu::DeepLocal loc = gpu::deep_run(b, in, rank, world, opt);
+    gpu::DeepLocal loc;
+    for (int attempt = 0;; ++attempt) {
+      try {
+        loc = gpu::deep_run(b, in, rank, world, opt);
+        break;
+      } catch (const gpu::ArenaOverflow&) {  // emit: regrown from the count, rerun (as mine_deep)
+        if (attempt >= 2) throw;
+      }
+    }
     for (int d = 2; d < 64; ++d) per[(size_t)d] += loc.per_depth[(size_t)d];
     dsum += loc.dsum;
     dxor ^= loc.dxor;
     rounds += (int)loc.round_tasks.size();
+    if (opt.emit) {
+      const int64_t n = std::min(b.arena_used, b.arena_cap);
+      std::vector<uint64_t> h((size_t)n, 0);
+      for (int d = 1; d < 64; ++d)
+        for (int64_t v = 0; v < n; ++v) {
+          if (b.n_depth[v] != d) continue;
+          if (d > 1 && (b.n_parent[v] >= (uint64_t)n || b.n_depth[b.n_parent[v]] != d - 1)) {
+            std::printf("{\"ok\": false, \"error\": \"node %lld: bad parent\"}\n", (long long)v);
+            return 1;
+          }
+          h[(size_t)v] = (d == 1 ? 0 : h[b.n_parent[v]]) + item_mix((uint64_t)fi.ids[b.n_item[v]]);
+          if (rank > 0 && d < 3) continue;  // levels 1-2: rank 0's share
+          const DigestTerms t = digest_terms(h[(size_t)v], b.n_count[v]);
+          esum += t.sum;
+          exor ^= t.xr;
+          eper[(size_t)d] += 1;
+        }
+    }
     spilled += (long long)loc.spilled_tasks;
     handoffs += (long long)loc.handoffs;
   }
   CountResult c = mine_cpu_count(ptr.data(), items.data(), n_tx, n_items, ms, max_len, (int64_t)1 << 62, 2);
   bool ok = c.digest_sum == dsum && c.digest_xor == dxor;
+  if (opt.emit) ok = ok && c.digest_sum == esum && c.digest_xor == exor && eper == per;
   for (size_t d = 1; d < 64; ++d) {
     const uint64_t want = d < c.per_level.size() ? (uint64_t)c.per_level[d] : 0;
     if (want != per[d]) ok = false;

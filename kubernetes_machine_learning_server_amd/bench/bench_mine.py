@@ -122,6 +122,48 @@ def run_deep(tx, ms: float, world: int, rank: int, device: int, warmup: int, ste
     return out
 
 
+def run_deep_emit(dm, ms: float, world: int, rank: int, warmup: int, steps: int,
+                  barrier_sync, max_over_ranks, gather) -> Dict:
+    """The headline problem with every itemset MATERIALISED (``mine_deep(emit=True)``): each
+    frequent itemset becomes a node (parent node, item, support, size) of a trie arena in HBM,
+    written inside the timed step.  Verified after the timing: the arena's own content digest
+    (set hashes rebuilt on the device from parent links), combined over the ranks, must equal
+    the CPU miner's digest of the whole problem."""
+    dm.opts["emit"] = True
+    try:
+        r = None
+        for _ in range(max(1, warmup)):  # (the first call sizes the arena)
+            r = dm.mine(ms)
+        dm.synchronize()
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r = dm.mine(ms)
+        dm.synchronize()
+        barrier_sync()
+        ms_step = max_over_ranks((time.perf_counter() - t0) * 1000.0 / max(1, steps))
+        t1 = time.perf_counter()
+        dg = dm.g.deep_arena_digest(1 if rank == 0 else 3)
+        verify_s = time.perf_counter() - t1
+    finally:
+        dm.opts["emit"] = False
+    parts = gather((int(dg["sum"]), int(dg["xor"]), int(dg["n"]), int(r["arena_nodes"])))
+    s = x = n = nodes = 0
+    for ps, px, pn, pa in parts:
+        s, x, n, nodes = (s + ps) % (1 << 64), x ^ px, n + pn, nodes + pa
+    digest = f"{s:016x}{x:016x}"
+    ref = CPU_REF.get(ms)
+    return {"ms_per_step": round(ms_step, 3), "n_itemsets_in_arenas": n,
+            "arena_node_ids_used": nodes,
+            "arena_bytes": int(nodes) * 13,
+            "node_format": "SoA: parent u32, item rank u32, support u32, size u8 (13 B)",
+            "arena_digest": digest,
+            "verified_digest": (digest == ref[0] and n == ref[1]) if ref else None,
+            "digest_equals_count_only": digest == r["digest"],
+            "verify_s_rank0": round(verify_s, 3),
+            "rank0_phases_ms": {k: round(v, 3) for k, v in r["phases_ms"].items()}}
+
+
 def deep_capped(dm, ms: float, budget_s: float, start_len: int = 4, max_cap: int = 64) -> Dict:
     """Full mining at `ms` with the itemset size cap raised one at a time while a call stays
     under `budget_s` (the last completed cap's counts, timed)."""

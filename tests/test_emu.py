@@ -44,7 +44,7 @@ def emu_bin():
 
 @pytest.mark.parametrize("args", [
     # n_tx n_items mean_len genres affinity min_support [budget0 budget split_min stack_mb world
-    #   max_len steal steal_idle presplit_cost]   (n_items < 0: a clique of -n_items items)
+    #   max_len steal steal_idle presplit_cost emit]   (n_items < 0: a clique of -n_items items)
     "400 60 20 3 0.9 0.05",
     "400 60 20 3 0.9 0.05 1 1 2 4 1 0 1 0",          # steal: every check spills, per-member splits
     "300 50 25 2 0.95 0.08 1 1 4 1 3 0 1 0",         # 3 simulated ranks + eager in-launch spills
@@ -56,6 +56,9 @@ def emu_bin():
     "64 -12 1 1 1 0.5 1 1 8 4 3 0 1 1",              # clique, 3 ranks, requested hand-offs
     "400 60 20 3 0.9 0.05 1 4 2 4 2 0 1 1 2",        # 2 ranks, pre-split of every task >= 2
     "64 -12 1 1 1 0.5 1 4 4 4 1 0 1 1 1",            # clique, pre-split, then stealing
+    "400 60 20 3 0.9 0.05 1 1 2 4 1 0 1 1 16 1",     # emit: the node arena's own digest
+    "300 50 25 2 0.95 0.08 1 2 4 1 3 0 1 1 2 1",     # emit, 3 ranks, pre-split + hand-offs
+    "64 -12 1 1 1 0.5 1 4 4 4 1 0 0 0 0 1",          # emit through spill rounds (steal off)
 ])
 def test_deep_kernel_on_emulator(emu_bin, args):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")

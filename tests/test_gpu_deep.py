@@ -116,3 +116,46 @@ def test_deep_small_stack_spills(gpu_mod):
     tx = generate("ds1", seed=0)
     d = _gpu_miner(gpu_mod, tx).mine_deep(0.04, stack_mb=1, blocks_per_cu=1)
     _same(d, _cpu(gpu_mod, tx, 0.04))
+
+
+def _arena_trie(arena):
+    """The downloaded node arena (ids in allocation order, size 0 = unused id) as a trie whose
+    parents come first: nodes sorted by size, parent ids remapped."""
+    dep = np.asarray(arena["depth"])
+    keep = np.flatnonzero(dep > 0)
+    order = keep[np.argsort(dep[keep], kind="stable")]
+    new_id = np.full(len(dep), -1, np.int64)
+    new_id[order] = np.arange(len(order))
+    par = np.asarray(arena["parent"])[order]
+    par = np.where(par >= 0, new_id[np.maximum(par, 0)], -1)
+    return (par, np.asarray(arena["item"])[order], np.asarray(arena["count"])[order],
+            dep[order])
+
+
+@pytest.mark.parametrize("ms,world", [(0.05, 1), (0.04, 1), (0.04, 3)])
+def test_deep_emit_arena_is_the_trie(gpu_mod, ms, world):
+    """Emit mode: every frequent itemset becomes a node of the HBM trie arena.  The downloaded
+    arena, as a trie, has the CPU miner's trie digest (every itemset and support, nothing
+    else), and the device's own arena digest equals it; the count-only digest is unchanged.
+    Rank splits: each rank's arena holds its share (sizes >= 3 past rank 0)."""
+    tx = generate("ds1", seed=0)
+    g = _gpu_miner(gpu_mod, tx)
+    ref = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
+    want = gpu_mod.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])
+    s, x, per = 0, 0, np.zeros(64, np.int64)
+    for rank in range(world):
+        d = g.mine_deep(ms, rank=rank, world=world, emit=True, budget=4)
+        assert d["arena_nodes"] <= d["arena_cap"]
+        dev = g.deep_arena_digest(1 if rank == 0 else 3)
+        a = g.deep_arena_download(d["arena_nodes"])
+        par, item, cnt, dep = _arena_trie(a)
+        # (every rank's arena holds the root levels as parents; sizes 1-2 count on rank 0)
+        host = gpu_mod.trie_digest(par, item, cnt, dep, 1 if rank == 0 else 3)
+        assert host["digest"] == dev["digest"], (rank, host, dev)
+        s = (s + int(dev["sum"])) % (1 << 64)
+        x ^= int(dev["xor"])
+        per[:len(dev["per_depth"])] += np.asarray(dev["per_depth"], np.int64)
+        if world == 1:
+            assert d["digest"] == want["digest"]
+    assert f"{s:016x}{x:016x}" == want["digest"]
+    assert [int(v) for v in per[1:len(want["per_depth"])]] == [int(v) for v in want["per_depth"][1:]]
