@@ -305,6 +305,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     b.trace_cap = c1;
     b.ticks_cap = c2;
     KMLS_HIP(hipMemsetAsync(b.d_ticks, 0, (size_t)n_tasks * 8, s));
+    KMLS_HIP(hipMemsetAsync(b.d_trace, 0, (size_t)waves * kern::kDeepTraceWords * 8, s));
     a.trace = b.d_trace;
     a.task_ticks = b.d_ticks;
   }

@@ -338,11 +338,11 @@ __device__ __forceinline__ void drop_bottom(DeepFrame* fst, WaveState& st, WaveL
 // no room: error set).  Steal mode publishes every task by its ready flag.  A partial spill
 // (ns < nf: the oldest, largest open classes handed to waiting waves) drops the spilled frames'
 // block references and moves the remaining frames down; the wave keeps working on them.
-template <int MAXT>
+template <int MAXT, bool EMIT>
 __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st,
                                             WaveLds<MAXT>& L, int lane, bool optional,
                                             unsigned ns) {
-  const unsigned E = a.node_parent != nullptr;  // emit mode: the node-word row
+  constexpr unsigned E = EMIT ? 1u : 0u;  // emit mode: the node-word row
   unsigned long long bytes_tot = 0, nt_tot = 0;
   for (unsigned f = 0; f < ns; ++f) {
     const DeepFrame fr = load_frame(fst + f, lane);
@@ -431,7 +431,7 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
 // inbox (open -> filling), copy the class block to the heap and the frame to the inbox with
 // write-through stores, count the task, mark the inbox full.  False (nothing changed) when the
 // requester is no longer waiting or the heap is full.
-template <int MAXT>
+template <int MAXT, bool EMIT>
 __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst, WaveState& st,
                                               WaveLds<MAXT>& L, int lane, unsigned req,
                                               unsigned k_open, unsigned k_filling,
@@ -442,7 +442,7 @@ __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst,
   if (!uni(__shfl(ok, 0, 64))) return false;
   const DeepFrame fr = load_frame(fst, lane);
   const unsigned m = fr.m, wt = meta_width(fr.meta);
-  const unsigned E = a.node_parent != nullptr;
+  constexpr unsigned E = EMIT ? 1u : 0u;
   const unsigned long long npad = roundup16(m);
   const unsigned long long bytes = (unsigned long long)(wt + 1 + E) * npad * 8ull;
   unsigned long long base = 0;
@@ -480,7 +480,7 @@ __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst,
 
 // ---- row step: member s0 against members s0+1 .. s0+m-1 (lane = candidate) ----
 // The child class (prefix P ∪ {a}) is projected onto row a when that narrows its tier.
-template <int WT, int MAXT>
+template <int WT, int MAXT, bool EMIT>
 __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, WaveState& st,
                                          WaveLds<MAXT>& L, DeepFrame top, char* stack, int lane,
                                          WaveAcc& acc) {
@@ -495,9 +495,9 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
   const unsigned ia = top.s0;
   const unsigned long long ih_a = ihp[ia + vzero()];
   const unsigned long long h_a = top.hash + ih_a;
-  const unsigned E = a.node_parent != nullptr;
+  constexpr unsigned E = EMIT ? 1u : 0u;
   const unsigned long long* nwp = ihp + top.pad;  // emit mode: node words
-  const unsigned long long node_a = E ? (nwp[ia + vzero()] & kDeepNodeMask) : 0ull;
+  const unsigned long long node_a = E ? uni64(nwp[ia + vzero()] & kDeepNodeMask) : 0ull;
   unsigned wt_out = WT;
   if (WT > 1 && deeper && nc >= 2) {
     const unsigned s = proj_setup<WT>(L.proj, blk, top.pad, ia, lane);
@@ -574,7 +574,7 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
 // ---- batch step: the top frames' member pairs, up to kCap lanes ----
 // (frames of the top frame's block only: sibling classes, so the block base and width stay
 // uniform)
-template <int WT, int MAXT>
+template <int WT, int MAXT, bool EMIT>
 __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, WaveState& st,
                                            WaveLds<MAXT>& L, DeepFrame top, char* stack,
                                            int lane, WaveAcc& acc) {
@@ -644,7 +644,7 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
   const unsigned long long* bblk = (const unsigned long long*)top.blk;
   const unsigned long long bpad = top.pad;
   const unsigned long long* ihp = bblk + (unsigned long long)WT * bpad;
-  const unsigned E = a.node_parent != nullptr;
+  constexpr unsigned E = EMIT ? 1u : 0u;
   const unsigned long long* nwp = ihp + bpad;  // emit mode: node words
   unsigned S = 0, gbase = 0;
   for (unsigned c0 = 0; c0 < P; c0 += 64) {
@@ -754,7 +754,7 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
 }
 
 // one step of the top frame, dispatched on its block width (wave-uniform)
-template <int MAXT, int T0, int... Ts>
+template <int MAXT, bool EMIT, int T0, int... Ts>
 __device__ __forceinline__ void step_tier(unsigned wt, bool row_mode, const DeepArgs& a,
                                           DeepFrame* fst, WaveState& st, WaveLds<MAXT>& L,
                                           const DeepFrame& top, char* stack, int lane,
@@ -762,13 +762,13 @@ __device__ __forceinline__ void step_tier(unsigned wt, bool row_mode, const Deep
   if constexpr (T0 <= MAXT) {
     if (wt == (unsigned)T0) {
       if (row_mode)
-        row_step<T0, MAXT>(a, fst, st, L, top, stack, lane, acc);
+        row_step<T0, MAXT, EMIT>(a, fst, st, L, top, stack, lane, acc);
       else
-        batch_step<T0, MAXT>(a, fst, st, L, top, stack, lane, acc);
+        batch_step<T0, MAXT, EMIT>(a, fst, st, L, top, stack, lane, acc);
       return;
     }
   }
-  if constexpr (sizeof...(Ts) > 0) step_tier<MAXT, Ts...>(wt, row_mode, a, fst, st, L, top, stack,
+  if constexpr (sizeof...(Ts) > 0) step_tier<MAXT, EMIT, Ts...>(wt, row_mode, a, fst, st, L, top, stack,
                                                           lane, acc);
 }
 
@@ -778,7 +778,7 @@ __device__ __forceinline__ void step_tier(unsigned wt, bool row_mode, const Deep
 template <int MAXT>
 constexpr int deep_waves_per_simd() { return MAXT <= 8 ? 4 : (MAXT <= 16 ? 3 : 2); }
 
-template <int MAXT, int WPS>
+template <int MAXT, int WPS, bool EMIT>
 __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
   __shared__ WaveLds<MAXT> lds[kWaves];
   const int lane = threadIdx.x & 63;
@@ -793,7 +793,7 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
   __builtin_amdgcn_wave_barrier();
 
   WaveState st{0, 0, 0, 0, 0};
-  const unsigned E = a.node_parent != nullptr;
+  constexpr unsigned E = EMIT ? 1u : 0u;
   bool failed = false;
   const unsigned long long t_start = wall_clock64();
   auto timed_out = [&]() {
@@ -806,8 +806,9 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
                  kFull = (a.epoch << 2) | 3u, kClosed = a.epoch << 2;
   bool holding = false, inbox_open = false;
   unsigned long long t = 0;
-  // instrumentation (a.trace != nullptr): first task start, last task end, busy ticks, counts
-  unsigned long long tr_first = 0, tr_last = 0, tr_busy = 0, tr_tasks = 0, tr_inbox = 0;
+  // instrumentation (a.trace != nullptr, zeroed by the host): kept in the wave's trace record,
+  // not in registers held across the whole loop
+  unsigned long long* tr = a.trace ? a.trace + gw * (unsigned long long)kDeepTraceWords : nullptr;
   unsigned victim = (unsigned)((gw * 7919ull + 1) % (unsigned long long)(a.nwaves > 0 ? a.nwaves : 1));
   while (!failed) {
     // ---- the next task: queue ticket t, or (steal mode, while t is not published) a class
@@ -898,8 +899,8 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
       st.mem_top = 0;
     }
     acc.budget_used = 0;
-    const unsigned long long tr_t0 = a.trace ? wall_clock64() : 0ull;
-    if (a.trace && tr_tasks == 0) tr_first = tr_t0;
+    const unsigned long long tr_t0 = tr ? wall_clock64() : 0ull;
+    if (tr && lane == 0 && tr[1] == 0) tr[1] = tr_t0;
     // ---- run the task ----
     while (st.nf > 0) {
       __builtin_amdgcn_wave_barrier();
@@ -918,14 +919,14 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
           (unsigned long long)(wt + 1 + E) * roundup16(row_mode ? m : kCap) * 8ull;
       if (st.mem_top + need > a.stack_bytes || st.nf + kCap + 2 > (unsigned)a.fcap ||
           st.nb + 1 >= (unsigned)kBStack || (!a.steal && acc.budget_used >= a.budget)) {
-        if (spill_frames<MAXT>(a, fst, st, L, lane, false, st.nf) < 0) failed = true;
+        if (spill_frames<MAXT, EMIT>(a, fst, st, L, lane, false, st.nf) < 0) failed = true;
         break;
       }
       if (a.steal && acc.budget_used >= a.budget) {
         acc.budget_used = 0;
         if (a.steal_eager == 1) {
           // tests: the bottom frame to the shared queue at every check (a lone frame whole)
-          if (spill_frames<MAXT>(a, fst, st, L, lane, true, 1) == 0) {
+          if (spill_frames<MAXT, EMIT>(a, fst, st, L, lane, true, 1) == 0) {
             free_blocks(L, st);
             if (st.nf == 0) break;
             continue;
@@ -943,7 +944,7 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
             else r = 0;
           }
           r = uni64(bcast64(r, 0));
-          if (r && donate_bottom<MAXT>(a, fst, st, L, lane, (unsigned)(r & 0xffffffffull) - 1u,
+          if (r && donate_bottom<MAXT, EMIT>(a, fst, st, L, lane, (unsigned)(r & 0xffffffffull) - 1u,
                                        kOpen, kFilling, kFull)) {
             free_blocks(L, st);
             continue;
@@ -955,17 +956,16 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
         failed = true;
         break;
       }
-      step_tier<MAXT, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64>(wt, row_mode, a, fst, st, L, top,
+      step_tier<MAXT, EMIT, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64>(wt, row_mode, a, fst, st, L, top,
                                                                stack, lane, acc);
       free_blocks(L, st);
     }
-    if (a.trace && !failed) {
+    if (tr && !failed && lane == 0) {
       const unsigned long long now = wall_clock64();
-      tr_busy += now - tr_t0;
-      tr_last = now;
-      tr_tasks += 1;
-      tr_inbox += task_from_inbox ? 1 : 0;
-      if (a.task_ticks && !task_from_inbox && task_ticket < (unsigned long long)a.n_in && lane == 0)
+      tr[4] += now - tr_t0;
+      tr[2] = now;
+      tr[5] += (1ull << 32) | (task_from_inbox ? 1ull : 0ull);
+      if (a.task_ticks && !task_from_inbox && task_ticket < (unsigned long long)a.n_in)
         a.task_ticks[task_ticket] = now - tr_t0;
     }
     if (a.steal && !failed) {  // the task is done
@@ -999,14 +999,9 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
   }
   for (int d = lane; d < 64; d += 64)
     if (L.depth_cnt[d]) atomicAdd(&a.ctl->per_depth[d], L.depth_cnt[d]);
-  if (a.trace && lane == 0) {
-    unsigned long long* tr = a.trace + gw * (unsigned long long)kDeepTraceWords;
+  if (tr && lane == 0) {
     tr[0] = t_start;
-    tr[1] = tr_first;
-    tr[2] = tr_last;
     tr[3] = wall_clock64();
-    tr[4] = tr_busy;
-    tr[5] = (tr_tasks << 32) | tr_inbox;
   }
 }
 
@@ -1299,13 +1294,20 @@ void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s) {
   const int mt = deep_count_maxt(maxt);
   const int w = deep_count_wps(mt, wps);
   const dim3 g((unsigned)grid), b(64 * kWaves);
-  if (mt == 8 && w == 5) hipLaunchKernelGGL((k_deep_count<8, 5>), g, b, 0, s, a);
-  else if (mt == 8) hipLaunchKernelGGL((k_deep_count<8, 4>), g, b, 0, s, a);
-  else if (mt == 16 && w == 4) hipLaunchKernelGGL((k_deep_count<16, 4>), g, b, 0, s, a);
-  else if (mt == 16) hipLaunchKernelGGL((k_deep_count<16, 3>), g, b, 0, s, a);
-  else if (mt == 32 && w == 3) hipLaunchKernelGGL((k_deep_count<32, 3>), g, b, 0, s, a);
-  else if (mt == 32) hipLaunchKernelGGL((k_deep_count<32, 2>), g, b, 0, s, a);
-  else hipLaunchKernelGGL((k_deep_count<64, 2>), g, b, 0, s, a);
+  if (a.node_parent != nullptr) {  // emit mode: the default occupancy of each width class
+    if (mt == 8) hipLaunchKernelGGL((k_deep_count<8, 4, true>), g, b, 0, s, a);
+    else if (mt == 16) hipLaunchKernelGGL((k_deep_count<16, 3, true>), g, b, 0, s, a);
+    else if (mt == 32) hipLaunchKernelGGL((k_deep_count<32, 2, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_deep_count<64, 2, true>), g, b, 0, s, a);
+    return;
+  }
+  if (mt == 8 && w == 5) hipLaunchKernelGGL((k_deep_count<8, 5, false>), g, b, 0, s, a);
+  else if (mt == 8) hipLaunchKernelGGL((k_deep_count<8, 4, false>), g, b, 0, s, a);
+  else if (mt == 16 && w == 4) hipLaunchKernelGGL((k_deep_count<16, 4, false>), g, b, 0, s, a);
+  else if (mt == 16) hipLaunchKernelGGL((k_deep_count<16, 3, false>), g, b, 0, s, a);
+  else if (mt == 32 && w == 3) hipLaunchKernelGGL((k_deep_count<32, 3, false>), g, b, 0, s, a);
+  else if (mt == 32) hipLaunchKernelGGL((k_deep_count<32, 2, false>), g, b, 0, s, a);
+  else hipLaunchKernelGGL((k_deep_count<64, 2, false>), g, b, 0, s, a);
 }
 
 }  // namespace kern
