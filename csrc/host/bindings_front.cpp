@@ -82,6 +82,7 @@ void register_front_bindings(py::module_& m) {
     py::dict d;
     d["lat_ns"] = py::array_t<int64_t>((py::ssize_t)res.lat_ns.size(), res.lat_ns.data());
     d["lag_ns"] = py::array_t<int64_t>((py::ssize_t)res.lag_ns.size(), res.lag_ns.data());
+    d["at_ns"] = py::array_t<int64_t>((py::ssize_t)res.at_ns.size(), res.at_ns.data());
     d["offered"] = res.offered;
     d["sent"] = res.sent;
     d["completed"] = res.completed;

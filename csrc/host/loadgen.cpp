@@ -96,7 +96,7 @@ LoadResult run_loadgen(const std::string& host, int port, const std::vector<std:
   const double period_ns = 1e9 / qps;
   LoadResult res;
   res.offered = n_total;
-  std::vector<std::vector<int64_t>> lat((size_t)T), lag((size_t)T);
+  std::vector<std::vector<int64_t>> lat((size_t)T), lag((size_t)T), at((size_t)T);
   std::vector<int64_t> errors((size_t)T, 0), done((size_t)T, 0), sent((size_t)T, 0);
   // connect everything first, then start the clock
   std::vector<LConn> conns((size_t)C);
@@ -127,6 +127,7 @@ LoadResult run_loadgen(const std::string& host, int port, const std::vector<std:
     }
     auto& L = lat[(size_t)t];
     auto& G = lag[(size_t)t];
+    auto& A = at[(size_t)t];
     L.reserve((size_t)(n_total / T + 16));
     char buf[65536];
     epoll_event evs[64];
@@ -181,6 +182,7 @@ LoadResult run_loadgen(const std::string& host, int port, const std::vector<std:
           x->in.erase(0, len);
           L.push_back(tr - x->sched);
           G.push_back(x->sent_at - x->sched);
+          A.push_back(x->sched - t0);
           if (st != 200) ++errors[(size_t)t];
           ++done[(size_t)t];
           x->busy = false;
@@ -209,6 +211,7 @@ LoadResult run_loadgen(const std::string& host, int port, const std::vector<std:
   for (int t = 0; t < T; ++t) {
     res.lat_ns.insert(res.lat_ns.end(), lat[(size_t)t].begin(), lat[(size_t)t].end());
     res.lag_ns.insert(res.lag_ns.end(), lag[(size_t)t].begin(), lag[(size_t)t].end());
+    res.at_ns.insert(res.at_ns.end(), at[(size_t)t].begin(), at[(size_t)t].end());
     res.errors += errors[(size_t)t];
     res.completed += done[(size_t)t];
     res.sent += sent[(size_t)t];

@@ -10,6 +10,7 @@ namespace kmls {
 struct LoadResult {
   std::vector<int64_t> lat_ns;  // completion - scheduled send time, per answered request
   std::vector<int64_t> lag_ns;  // actual - scheduled send time (client/connection backlog)
+  std::vector<int64_t> at_ns;   // scheduled send time of each answered request, from the start
   int64_t offered = 0, sent = 0, completed = 0, errors = 0;  // errors: non-200 answers
   double duration_s = 0;
 };

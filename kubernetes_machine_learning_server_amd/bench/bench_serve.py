@@ -81,10 +81,10 @@ def _free_port() -> int:
 
 
 def start_server(base: pathlib.Path, backend: str, workers: int, port: int,
-                 front: str = "native", threads: int = 4):
+                 front: str = "native", threads: int = 4, poll_minutes: float = 60.0):
     env = dict(os.environ)
     env.update(BASE_DIR=str(base) + "/", PICKLE_DIR="pickles/", SERVE_BACKEND=backend,
-               KMLS_LOG_LEVEL="ERROR", POLLING_WAIT_IN_MINUTES="60",
+               KMLS_LOG_LEVEL="ERROR", POLLING_WAIT_IN_MINUTES=str(poll_minutes),
                PYTHONPATH=str(ROOT) + os.pathsep + env.get("PYTHONPATH", ""))
     cmd = [sys.executable, "-m", "kubernetes_machine_learning_server_amd.serve", "--host",
            "127.0.0.1", "--port", str(port), "--front", front, "--threads", str(threads),
@@ -183,6 +183,68 @@ def measure_native(port: int, qps: float, duration: float, queries, connections:
             "max_ms": round(float(a.max()), 3), "mean_ms": round(float(a.mean()), 3),
             "send_lag_p99_ms": round(float(np.percentile(lag, 99)), 3),
             "latency_from": "scheduled send time", "connections": connections}
+
+
+def _window(a: np.ndarray) -> dict:
+    if len(a) == 0:
+        return {"n": 0}
+    return {"n": int(len(a)), "p50_ms": round(float(np.percentile(a, 50)), 3),
+            "p99_ms": round(float(np.percentile(a, 99)), 3),
+            "max_ms": round(float(a.max()), 3)}
+
+
+def reload_under_load(port: int, base: pathlib.Path, alt_index: pathlib.Path, qps: float,
+                      duration: float, reload_at: float, queries, connections: int = 64,
+                      settle_s: float = 2.0) -> dict:
+    """Open-loop load at `qps` for `duration` s; at `reload_at` s the job's publish step is
+    replayed on the PVC (the alternate rules.idx renamed over the served one, then a new marker,
+    written last), so the server's poller hot-reloads mid-run.  Latency percentiles (from the
+    scheduled send time) before the flip, in the `settle_s` window after it, and after that."""
+    import threading
+    from ..ops import native
+    from ..utils.atomic_io import atomic_write_bytes
+    N = native.load()
+    pk = base / "pickles"
+    marker = base / "last_execution.txt"
+    flip = {}
+
+    def publisher():
+        time.sleep(reload_at + 0.02)  # the load generator's clock starts 20 ms after connect
+        t = time.time()
+        atomic_write_bytes(pk / "rules.idx", alt_index.read_bytes())
+        atomic_write_bytes(marker, f"reload-under-load {t:.3f}".encode())
+        flip["t"] = time.time()
+
+    th = threading.Thread(target=publisher, daemon=True)
+    reloads0 = _metric(port, "kmls_reload_count")
+    th.start()
+    r = N.loadgen("127.0.0.1", port, request_bytes(queries, port), float(qps), float(duration),
+                  connections, 2, 5.0)
+    th.join()
+    lat = np.asarray(r["lat_ns"], np.float64) / 1e6
+    at = np.asarray(r["at_ns"], np.float64) / 1e9
+    t1 = reload_at
+    out = {"offered_qps": qps, "duration_s": duration, "reload_at_s": reload_at,
+           "completed": int(r["completed"]), "errors": int(r["errors"]),
+           "unanswered": int(r["offered"] - r["completed"]),
+           "before": _window(lat[at < t1]),
+           "during": _window(lat[(at >= t1) & (at < t1 + settle_s)]),
+           "after": _window(lat[at >= t1 + settle_s]),
+           "reloads": (_metric(port, "kmls_reload_count") or 0) - (reloads0 or 0),
+           "latency_from": "scheduled send time (open loop)"}
+    return out
+
+
+def _metric(port: int, name: str) -> Optional[float]:
+    import urllib.request
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+            for ln in r.read().decode().splitlines():
+                if ln.startswith(name + " ") or ln.startswith(name + "{"):
+                    return float(ln.split()[-1])
+    except Exception:
+        return None
+    return None
 
 
 def capacity(port: int, queries, start_qps: float = 10000.0, duration: float = 2.0,
@@ -326,6 +388,13 @@ def main(argv=None) -> int:
     ap.add_argument("--json-out", default=None, help="also write the summary JSON here")
     ap.add_argument("--matcher-only", action="store_true")
     ap.add_argument("--pvc", default=None, help="reuse a populated PVC dir")
+    ap.add_argument("--reload-index", default=None,
+                    help="rules.idx to hot-swap in mid-run (reload under load)")
+    ap.add_argument("--reload-at", type=float, default=4.0)
+    ap.add_argument("--reload-qps", type=float, default=10000.0)
+    ap.add_argument("--reload-duration", type=float, default=10.0)
+    ap.add_argument("--poll-minutes", type=float, default=0.01,
+                    help="server marker poll interval for --reload-index (POLLING_WAIT_IN_MINUTES)")
     a = ap.parse_args(argv)
     tmp = tempfile.mkdtemp(prefix="kmls_serve_") if a.pvc is None else a.pvc
     root = pathlib.Path(tmp)
@@ -335,9 +404,13 @@ def main(argv=None) -> int:
     if a.matcher_only:
         print(json.dumps({"bench": "matcher", **matcher_bench(base)}), flush=True)
         return 0
+    reload = None
+    if a.reload_index:
+        reload = {"alt_index": a.reload_index, "at": a.reload_at, "qps": a.reload_qps,
+                  "duration": a.reload_duration, "poll_minutes": a.poll_minutes}
     summary = run_serve_bench(base, a.backend, [float(x) for x in a.qps.split(",") if x],
                               a.duration, a.front, a.threads, a.workers, a.client, a.clients,
-                              a.connections, a.capacity, verbose=True)
+                              a.connections, a.capacity, verbose=True, reload=reload)
     print(json.dumps({"bench": "serve_summary", **summary}), flush=True)
     if a.json_out:
         pathlib.Path(a.json_out).write_text(json.dumps(summary))
@@ -347,13 +420,15 @@ def main(argv=None) -> int:
 def run_serve_bench(base: pathlib.Path, backend: str, qps_list, duration: float,
                     front: str = "native", threads: int = 4, workers: int = 4,
                     client: str = "native", clients: int = 8, connections: int = 64,
-                    with_capacity: bool = True, verbose: bool = False) -> dict:
+                    with_capacity: bool = True, verbose: bool = False,
+                    reload: Optional[dict] = None) -> dict:
     """Start the server (a fresh child process), run the fixed-QPS points and the capacity
     search, stop the server.  Returns the summary dict (bench.py's ``serve`` block)."""
     queries = make_queries(base, 50000)
     port = _free_port()
     t_start = time.time()
-    proc = start_server(base, backend, workers, port, front=front, threads=threads)
+    proc = start_server(base, backend, workers, port, front=front, threads=threads,
+                        poll_minutes=(reload or {}).get("poll_minutes", 60.0))
     res = {"backend": backend, "front": front,
            "threads" if front == "native" else "workers": threads if front == "native" else workers,
            "client": client, "duration_s": duration, "points": []}
@@ -381,6 +456,13 @@ def run_serve_bench(base: pathlib.Path, backend: str, qps_list, duration: float,
             res["points"].append(r)
             if verbose:
                 print(json.dumps({"bench": "serve", **r}), flush=True)
+        if reload:
+            res["reload_under_load"] = reload_under_load(
+                port, base, pathlib.Path(reload["alt_index"]), reload["qps"], reload["duration"],
+                reload["at"], queries, connections)
+            if verbose:
+                print(json.dumps({"bench": "reload_under_load", **res["reload_under_load"]}),
+                      flush=True)
         if with_capacity and client == "native":
             res["capacity"] = capacity(port, queries, start_qps=max(qps_list or [10000.0]) * 2)
             if verbose:
