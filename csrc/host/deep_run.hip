@@ -25,7 +25,8 @@ DeepBufs::~DeepBufs() {
                   (void*)heap[1], (void*)root, (void*)ctl, (void*)d_red, (void*)d_xor,
                   (void*)d_m, (void*)d_off, (void*)d_toff, (void*)d_cost, (void*)d_order,
                   (void*)d_trace, (void*)d_ticks, (void*)n_parent, (void*)n_item,
-                  (void*)n_count, (void*)n_depth, (void*)d_node_off})
+                  (void*)n_count, (void*)n_depth, (void*)d_node_off, (void*)d_split_q,
+                  (void*)d_split_heap})
     if (p) (void)hipFree(p);
   if (h_ctl) (void)hipHostFree(h_ctl);
 }
@@ -138,6 +139,8 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   const auto t1 = now();
   int64_t n_tasks = 0;
   int64_t n_heavy = 0;  // assign = 1: the queue's prefix of tasks with cost >= presplit_cost
+  std::vector<int64_t> split_q, split_heap;  // pre-split layout of the heavy prefix (host)
+  int64_t split_tasks = 0, split_bytes = 0;
   if (F >= 2 && in.max_len != 1) {
     const size_t root_blk = (size_t)(W + 1) * (size_t)Fpad * 8;
     auto ensure_root = [&](size_t bytes, size_t keep) {  // keep: leading bytes to preserve
@@ -254,8 +257,32 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       }
       n_tasks = (int64_t)mine.size();
       if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
-      if (opt.assign == 1 && opt.presplit_cost > 0)
-        while (n_heavy < n_tasks && cost[(size_t)mine[(size_t)n_heavy]] >= opt.presplit_cost) ++n_heavy;
+      const bool deeper4 = in.max_len == 0 || in.max_len >= 4;  // the split classes expand
+      if (opt.assign == 1 && opt.presplit_cost > 0 && opt.presplit_budget > 0 && opt.steal && deeper4)
+        while (n_heavy < n_tasks && cost[(size_t)mine[(size_t)n_heavy]] >= std::max(opt.presplit_cost, 2u) &&
+               cost[(size_t)mine[(size_t)n_heavy]] > opt.split_min)
+          ++n_heavy;
+      if (n_heavy > 0) {
+        // every heavy task (i, k) becomes its class of c = cost members after one row step,
+        // spilled as c - 1 single-member tasks over one heap copy of at most the root class
+        // width: exact queue slots and heap offsets, no shared counter in the launch
+        std::vector<int32_t> root_of((size_t)T);
+        for (int64_t i = 0; i < F; ++i)
+          for (int64_t t = toff[(size_t)i]; t < toff[(size_t)i + 1]; ++t) root_of[(size_t)t] = (int32_t)i;
+        split_q.resize((size_t)n_heavy);
+        split_heap.resize((size_t)n_heavy);
+        for (int64_t q = 0; q < n_heavy; ++q) {
+          const int64_t t = mine[(size_t)q];
+          const int64_t i = root_of[(size_t)t];
+          const int64_t c = cost[(size_t)t];
+          const int64_t pad_i = (m[(size_t)i] + 15) / 16 * 16;
+          const int64_t wt_i = (off[(size_t)i + 1] - off[(size_t)i]) / (8 * pad_i) - 1 - E;
+          split_q[(size_t)q] = split_tasks;
+          split_heap[(size_t)q] = split_bytes;
+          split_tasks += c - 1;
+          split_bytes += (wt_i + 1 + E) * ((c + 15) / 16 * 16) * 8;
+        }
+      }
       KMLS_HIP(hipMemcpyAsync(b.d_order, mine.data(), (size_t)n_tasks * 8, hipMemcpyHostToDevice, s));
       d_order = b.d_order;
       if (opt.trace) {
@@ -298,6 +325,8 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   a.node_count = E ? b.n_count : nullptr;
   a.node_depth = E ? b.n_depth : nullptr;
   a.node_cap = E ? (unsigned long long)b.arena_cap : 0ull;
+  a.split_q = nullptr;
+  a.split_heap = nullptr;
   if (opt.trace && opt.steal && n_tasks > 0) {
     int64_t c1 = b.trace_cap, c2 = b.ticks_cap;
     grow(b.d_trace, c1, waves * kern::kDeepTraceWords);
@@ -320,43 +349,51 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   kern::DeepFrame* steal_q = b.q[0];
   char* steal_heap = b.heap[0];
   int64_t steal_n = n_tasks;
-  if (opt.steal && n_heavy > 0 && opt.presplit_budget > 0) {
-    // pre-split: the heavy prefix runs presplit_budget passes without stealing and spills its
-    // open classes (one task per member) into q[1] / heap[0]; the light tasks are appended
-    // behind them and the stealing launch takes q[1] (its own spills go to heap[1])
+  if (opt.steal && n_heavy > 0) {
+    // pre-split: the heavy prefix runs one row step each without stealing and spills its class
+    // at the host's offsets into q[1] / heap[0]; the light tasks are appended behind them and
+    // the stealing launch takes q[1] (its own spills go to heap[1])
     const auto tp = now();
+    const int64_t n_light = n_tasks - n_heavy;
+    if (split_tasks + n_light > b.q_cap || (size_t)split_bytes > b.heap_cap)
+      throw std::runtime_error("deep_run: pre-split tasks exceed the queue / heap; raise "
+                               "KMLS_DEEP_QUEUE_MB / KMLS_DEEP_HEAP_MB");
+    int64_t c1 = b.split_cap, c2 = b.split_cap;
+    grow(b.d_split_q, c1, n_heavy);
+    grow(b.d_split_heap, c2, n_heavy);
+    b.split_cap = std::max(c1, c2);
+    KMLS_HIP(hipMemcpyAsync(b.d_split_q, split_q.data(), (size_t)n_heavy * 8, hipMemcpyHostToDevice, s));
+    KMLS_HIP(hipMemcpyAsync(b.d_split_heap, split_heap.data(), (size_t)n_heavy * 8,
+                            hipMemcpyHostToDevice, s));
     KMLS_HIP(hipMemsetAsync(b.ctl, 0, 3 * sizeof(unsigned long long), s));  // ticket, n_out, heap
     kern::DeepArgs p = a;
     p.in = b.q[0];
     p.n_in = n_heavy;
     p.out = b.q[1];
     p.heap = b.heap[0];
-    p.budget = opt.presplit_budget;
+    p.budget = 1;
     p.steal = 0;
     p.trace = nullptr;
     p.task_ticks = nullptr;
+    p.split_q = (const long long*)b.d_split_q;
+    p.split_heap = (const unsigned long long*)b.d_split_heap;
     kern::deep_count(p, maxt, blocks_per_cu,
                      (int)std::min<int64_t>(grid, (n_heavy + kern::deep_waves_per_block() - 1) /
                                                       kern::deep_waves_per_block()), s);
+    if (n_light)
+      KMLS_HIP(hipMemcpyAsync(b.q[1] + split_tasks, b.q[0] + n_heavy,
+                              (size_t)n_light * sizeof(kern::DeepFrame), hipMemcpyDeviceToDevice, s));
     KMLS_HIP(hipMemcpyAsync(b.h_ctl, b.ctl, sizeof(kern::DeepCtl), hipMemcpyDeviceToHost, s));
-    KMLS_HIP(hipStreamSynchronize(s));
+    KMLS_HIP(hipStreamSynchronize(s));  // (also: split_q / split_heap die at scope end)
     if (b.h_ctl->error)
       throw std::runtime_error("deep_run: the pre-split launch failed (error " +
-                               std::to_string(b.h_ctl->error) +
-                               "); raise KMLS_DEEP_QUEUE_MB / KMLS_DEEP_HEAP_MB");
-    const int64_t n_out = (int64_t)b.h_ctl->n_out;
-    const int64_t n_light = n_tasks - n_heavy;
-    if (n_out + n_light > b.q_cap)
-      throw std::runtime_error("deep_run: pre-split tasks exceed the queue; raise KMLS_DEEP_QUEUE_MB");
-    if (n_light)
-      KMLS_HIP(hipMemcpyAsync(b.q[1] + n_out, b.q[0] + n_heavy, (size_t)n_light * sizeof(kern::DeepFrame),
-                              hipMemcpyDeviceToDevice, s));
+                               std::to_string(b.h_ctl->error) + ")");
     steal_q = b.q[1];
     steal_heap = b.heap[1];
-    steal_n = n_out + n_light;
+    steal_n = split_tasks + n_light;
     a.task_ticks = nullptr;  // the queue no longer holds the level-3 tasks in order
     res.presplit_in = n_heavy;
-    res.presplit_out = n_out;
+    res.presplit_out = split_tasks;
     res.round_tasks.push_back(n_heavy);
     res.round_ms.push_back(ms_since(tp));
     res.ms_presplit = ms_since(tp);

@@ -51,6 +51,9 @@ struct DeepBufs {
   int64_t arena_cap = 0, arena_used = 0;
   int max_depth = 0;
   int64_t* d_node_off = nullptr;
+  int64_t* d_split_q = nullptr;   // pre-split layout: queue slot and heap offset per heavy task
+  int64_t* d_split_heap = nullptr;
+  int64_t split_cap = 0;
   int64_t node_off_cap = 0;
   unsigned long long* d_trace = nullptr;  // [waves * kDeepTraceWords] (opts.trace)
   unsigned long long* d_ticks = nullptr;  // [T] (opts.trace)

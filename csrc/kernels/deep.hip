@@ -341,7 +341,7 @@ __device__ __forceinline__ void drop_bottom(DeepFrame* fst, WaveState& st, WaveL
 template <int MAXT, bool EMIT>
 __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, WaveState& st,
                                             WaveLds<MAXT>& L, int lane, bool optional,
-                                            unsigned ns) {
+                                            unsigned ns, long long fixed = -1) {
   constexpr unsigned E = EMIT ? 1u : 0u;  // emit mode: the node-word row
   unsigned long long bytes_tot = 0, nt_tot = 0;
   for (unsigned f = 0; f < ns; ++f) {
@@ -351,8 +351,12 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
     nt_tot += (!single && fr.m > a.split_min) ? fr.m - 1 : 1;
   }
   unsigned long long hbase = 0;
-  if (lane == 0) hbase = atomicAdd(&a.ctl->heap_top, bytes_tot);  // overshoot is harmless
-  hbase = uni64(bcast64(hbase, 0));
+  if (fixed >= 0) {  // pre-split: the host laid out every task's heap bytes and queue slots
+    hbase = a.split_heap[fixed];
+  } else {
+    if (lane == 0) hbase = atomicAdd(&a.ctl->heap_top, bytes_tot);  // overshoot is harmless
+    hbase = uni64(bcast64(hbase, 0));
+  }
   if (hbase + bytes_tot > a.heap_cap) {
     if (!optional && lane == 0) atomicOr(&a.ctl->error, 2u);
     return optional ? 1 : -1;
@@ -360,7 +364,10 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
   // queue slots: never reserved past the capacity (steal-mode readers wait on reserved slots)
   const unsigned long long qcap = (unsigned long long)a.out_cap - (a.steal ? (unsigned long long)a.n_in : 0ull);
   unsigned long long t0 = 0;
-  if (lane == 0) {
+  if (fixed >= 0) {
+    t0 = (unsigned long long)a.split_q[fixed];
+    if (t0 + nt_tot > qcap) t0 = ~0ull;
+  } else if (lane == 0) {
     unsigned long long old = ld_agent(&a.ctl->n_out);
     for (;;) {
       if (old + nt_tot > qcap) { old = ~0ull; break; }
@@ -919,7 +926,9 @@ __global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
           (unsigned long long)(wt + 1 + E) * roundup16(row_mode ? m : kCap) * 8ull;
       if (st.mem_top + need > a.stack_bytes || st.nf + kCap + 2 > (unsigned)a.fcap ||
           st.nb + 1 >= (unsigned)kBStack || (!a.steal && acc.budget_used >= a.budget)) {
-        if (spill_frames<MAXT, EMIT>(a, fst, st, L, lane, false, st.nf) < 0) failed = true;
+        if (spill_frames<MAXT, EMIT>(a, fst, st, L, lane, false, st.nf,
+                                     a.split_q ? (long long)task_ticket : -1ll) < 0)
+          failed = true;
         break;
       }
       if (a.steal && acc.budget_used >= a.budget) {

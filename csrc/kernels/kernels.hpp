@@ -78,6 +78,10 @@ struct DeepArgs {
   unsigned* node_count;
   unsigned char* node_depth;
   unsigned long long node_cap;
+  // pre-split launch (non-stealing, budget 1; nullptr otherwise): queued task q spills its one
+  // child class at heap byte offset split_heap[q] as tasks out[split_q[q] ...] (host layout)
+  const long long* split_q;
+  const unsigned long long* split_heap;
 };
 constexpr int kDeepTraceWords = 6;
 constexpr unsigned long long kDeepNodeMask = (1ull << 40) - 1;  // node id bits of a node word

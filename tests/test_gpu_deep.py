@@ -79,7 +79,8 @@ def test_deep_work_stealing(gpu_mod, budget, split_min, steal_idle):
     tx = generate("ds1", seed=0)
     d = _gpu_miner(gpu_mod, tx).mine_deep(0.04, budget=budget, split_min=split_min,
                                           steal=True, steal_idle=steal_idle)
-    assert len(d["round_tasks"]) == 1
+    # one stealing launch (after the pre-split launch of the heaviest tasks, when any)
+    assert len(d["round_tasks"]) == 1 + (d["presplit"][0] > 0)
     if steal_idle == 0:
         assert d["spilled_tasks"] > 0
     elif budget <= 64:  # (at 256 passes between checks this small problem needs no hand-off)
