@@ -258,7 +258,10 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       n_tasks = (int64_t)mine.size();
       if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
       const bool deeper4 = in.max_len == 0 || in.max_len >= 4;  // the split classes expand
-      if (opt.assign == 1 && opt.presplit_cost > 0 && opt.presplit_budget > 0 && opt.steal && deeper4)
+      // (a rank split only: on one GPU the extra launch costs more than the shorter tail gains,
+      // profiles/r4i_*)
+      if (opt.assign == 1 && opt.presplit_cost > 0 && opt.presplit_budget > 0 && opt.steal &&
+          deeper4 && world > 1)
         while (n_heavy < n_tasks && cost[(size_t)mine[(size_t)n_heavy]] >= std::max(opt.presplit_cost, 2u) &&
                cost[(size_t)mine[(size_t)n_heavy]] > opt.split_min)
           ++n_heavy;

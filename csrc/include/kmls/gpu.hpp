@@ -148,10 +148,11 @@ struct DeepBufsDeleter {
 struct DeepOpts {
   // (defaults: the best of the r3e sweep at ds1 @0.02, profiles/r3_deep_sweep_projected.log)
   unsigned long long budget0 = 1024;  // rounds: 64-lane passes a first-round task may take
-  unsigned long long budget = 16;     // steal: passes between mailbox checks (r3s sweep with
+  unsigned long long budget = 8;      // steal: passes between mailbox checks (r3s sweep with
                                       // direct hand-offs: 8 / 16 / 64 / 256 -> 42.7 / 42.7 / 44.3
                                       // / 51.6 ms at ds1 @0.02, 8-rank split 9.4 / 9.6 / 11.2 /
-                                      // 23.4 ms); rounds: later-round budget (1024 there)
+                                      // 23.4 ms; r4i: 8 beats 16 by 1-3 % at 1 and 8 ranks);
+                                      // rounds: later-round budget (1024 there)
   unsigned split_min = 8;             // spilled frames above this many members split per member
   int blocks_per_cu = 0;              // 0 = the kernel instance's occupancy (deep_waves_per_simd)
   int stack_mb = 0;                   // per-wave stack (0: KMLS_DEEP_STACK_MB or 4)
@@ -164,7 +165,8 @@ struct DeepOpts {
                                       // (largest first) and dealt over the ranks in snake order;
                                       // 0 = task t to rank t % world in index order
   bool trace = false;                 // per-wave / per-task timing of the launch (DeepResult)
-  // pre-split (assign = 1): the rank's level-3 tasks whose class has >= presplit_cost members
+  // pre-split (assign = 1, rank splits only): the rank's level-3 tasks whose class has >=
+  // presplit_cost members
   // first run `presplit_budget` passes in a non-stealing launch that spills their open classes
   // as one task per member; the stealing launch then starts from those finer tasks (0 = off)
   unsigned presplit_cost = 16;

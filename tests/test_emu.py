@@ -55,7 +55,7 @@ def emu_bin():
     "64 -13 1 1 1 0.5 1 2 8 4 1 0 1 2",              # clique of 13 items, partner hand-offs
     "64 -12 1 1 1 0.5 1 1 8 4 3 0 1 1",              # clique, 3 ranks, requested hand-offs
     "400 60 20 3 0.9 0.05 1 4 2 4 2 0 1 1 2",        # 2 ranks, pre-split of every task >= 2
-    "64 -12 1 1 1 0.5 1 4 4 4 1 0 1 1 1",            # clique, pre-split, then stealing
+    "64 -12 1 1 1 0.5 1 4 4 4 2 0 1 1 1",            # clique, 2 ranks: pre-split, then stealing
     "400 60 20 3 0.9 0.05 1 1 2 4 1 0 1 1 16 1",     # emit: the node arena's own digest
     "300 50 25 2 0.95 0.08 1 2 4 1 3 0 1 1 2 1",     # emit, 3 ranks, pre-split + hand-offs
     "64 -12 1 1 1 0.5 1 4 4 4 1 0 0 0 0 1",          # emit through spill rounds (steal off)
