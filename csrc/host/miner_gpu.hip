@@ -146,7 +146,8 @@ struct OutBufs {
   unsigned long long* status = nullptr;  // [2 * status_cap]: two words per tile (SegAgg)
   int32_t* tile_row = nullptr;   // [2][status_cap] count tile → first row, by level parity
   unsigned long long* trace = nullptr;  // KMLS_LEVEL_TRACE diagnostics ([status_cap][8])
-  int64_t status_cap = 1 << 20;  // tiles per launch (256M candidates / 2G rows)
+  // tiles per launch: 2^22 x 256 = 1G candidates (KMLS_TEST_HOOKS status_cap=<tiles> shrinks it)
+  int64_t status_cap = std::max<long long>(64, test_hook("status_cap", 1ll << 22));
   // look-back tags: tag = epoch_base (per call, in FCtl) + launch index (kernel argument)
   unsigned epoch_base = 0;
   unsigned launch_idx = 0;
@@ -161,11 +162,11 @@ struct OutBufs {
     KMLS_HIP(hipMalloc((void**)&tile_row, (size_t)status_cap * 2 * sizeof(int32_t)));
   }
   static constexpr unsigned kLaunchesPerCall = 64;  // level launches per call (<= 61 levels)
-  // start a fused call: a fresh 64-tag window (the 16-bit tag wraps after 1024 calls: then the
+  // start a fused call: a fresh 64-tag window (the 12-bit tag wraps after 63 calls: then the
   // status words are zeroed so no stale word can match)
   unsigned begin_call(hipStream_t s) {
     epoch_base += kLaunchesPerCall;
-    if (epoch_base + kLaunchesPerCall >= (1u << 16)) {
+    if (epoch_base + kLaunchesPerCall >= (1u << 12)) {  // 12-bit tags (levels.hip)
       KMLS_HIP(hipMemsetAsync(status, 0, (size_t)status_cap * 2 * sizeof(unsigned long long), s));
       epoch_base = kLaunchesPerCall;
     }
@@ -467,6 +468,7 @@ struct MineRun {
       t_postsync = std::chrono::steady_clock::now();
       if (b_ctl->overflow) {
         ok = false;
+        need_nodes = std::max<int64_t>(need_nodes, (int64_t)b_ctl->need_out_m << 20);
         fallback_reason = "device overflow code " + std::to_string(b_ctl->overflow) +
                           " at level " + std::to_string(last) + " (bump " +
                           std::to_string(b_ctl->bump_top >> 20) + "/" +
@@ -515,6 +517,7 @@ struct MineRun {
   std::chrono::steady_clock::time_point t_presync, t_postsync;  // host-side profile
 
   int64_t fast_hint = 0;
+  int64_t need_nodes = 0;  // trie nodes a failed fused call needed (overflow 4 on out_cap)
   std::string fallback_reason;
 
   int64_t read_i64(const int64_t* dptr) {
@@ -1412,8 +1415,9 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       froot.rank = d_rrank;
       froot.gid = d_rgid;
       run.pinned = pinned_;
-      run.fast_hint = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 16ll << 20);
+      run.fast_hint = std::max<int64_t>({last_nodes_ + (last_nodes_ >> 2), 16ll << 20, fused_need_});
       done = run.run_fast(froot, off, off[(size_t)F]);
+      fused_need_ = std::max(fused_need_, run.need_nodes);
       KMLS_HIP(hipStreamSynchronize(s));  // the pageable staging vectors die at scope end
     }
     if (!done) run.process(root, 1, d_len, root_total);
@@ -1547,7 +1551,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   run.pinned = pinned_;
   run.n_cus = n_cus_;
   run.h_scalar = h_scalar_;
-  const int64_t cap_nodes = std::max<int64_t>(last_nodes_ + (last_nodes_ >> 2), 16ll << 20);
+  const int64_t cap_nodes = std::max<int64_t>({last_nodes_ + (last_nodes_ >> 2), 16ll << 20, fused_need_});
   run.ensure_out(cap_nodes);
   const int64_t out_cap = std::min<int64_t>({run.out_parent.cap, run.out_item.cap, run.out_count.cap, run.out_depth.cap});
   bool adopt_bufs = adopt && !download && !adopt->download;  // the host trie it writes is ours
@@ -1834,6 +1838,7 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
     trace::Range rg("kmls.levels");
     try {
       ok = run.levels_loop(d_desc, d_ctl, out_cap);
+      fused_need_ = std::max(fused_need_, run.need_nodes);
     } catch (...) {
       if (run.graph_capture) {
         hipStreamCaptureStatus st = hipStreamCaptureStatusNone;

@@ -376,6 +376,7 @@ class GpuMiner {
   std::vector<int64_t> tile_tx_;  // 65 evenly spaced transaction boundaries of the shard
   std::vector<int64_t> tile_nnz_; // and their item offsets
   int64_t last_nodes_ = 0;        // size of the previous trie (pinned download sizing)
+  int64_t fused_need_ = 0;        // trie nodes a fused call ran out of (output sizing hint)
   int32_t* d_tie_ = nullptr;      // rule-map tie key (item id -> rank) and its inverse
   int32_t* d_inv_tie_ = nullptr;
   int64_t idx_cap_ = 1 << 20;     // rule-map entry capacity (grown after an overflow)

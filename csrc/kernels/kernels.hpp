@@ -284,8 +284,8 @@ struct FCtl {
   unsigned long long candidates;   // Σ n_cand over the counted levels
   unsigned int overflow;           // 1 bump, 2 spin, 3/4 capacity → host falls back
   unsigned int dl_overflow;        // pinned host arrays too small → host copies at the end
-  unsigned int epoch_base;         // look-back tag of launch i = epoch_base + i (24 bits)
-  unsigned int pad0;
+  unsigned int epoch_base;         // look-back tag of launch i = epoch_base + i (12 bits)
+  unsigned int need_out_m;         // overflow 4 on the trie capacity: nodes needed, MiB units
   HostTrie h;                      // streamed download destination (pinned)
   int32_t* host_tab;               // frequent-item tables ids | counts | rank_of (pinned)
   int64_t tab_stride;

@@ -26,7 +26,7 @@
 // pinned host memory (coalesced PCIe writes), so finished levels reach the host while deeper
 // levels run, with no copy kernel or cross-stream event.
 //
-// Status words pack (epoch:24 | flag:2 | value:38), so publishing needs no fence, and the per-call
+// Status words pack (epoch:12 | flag:2 | value:50), so publishing needs no fence, and the per-call
 // epoch makes re-zeroing the status array unnecessary.  Every spin is bounded: a bug sets
 // FCtl::overflow and the host falls back to the chunked path instead of hanging the GPU.
 #include <hip/hip_runtime.h>
@@ -54,7 +54,9 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kTile = 256;              // candidates per count tile
 constexpr int kWin = 1024;              // LDS cand_off window (rows) per count tile
-constexpr unsigned long long kValMask = (1ull << 46) - 1;  // status word payload
+constexpr unsigned long long kValMask = (1ull << 50) - 1;  // status word payload
+constexpr unsigned kEpochMask = 0xFFFu;                     // 12-bit look-back tags
+constexpr long long kRowLimit = 1ll << 31;                  // level rows are int32-indexed
 constexpr long long kSpinLimit = 1ll << 26;
 
 __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
@@ -63,14 +65,14 @@ __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long lon
 __device__ __forceinline__ void st_relaxed(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// status word: epoch:16 | flag:2 (1 aggregate, 2 inclusive prefix) | payload:46
+// status word: epoch:12 | flag:2 (1 aggregate, 2 inclusive prefix) | payload:50
 __device__ __forceinline__ unsigned long long pack(unsigned epoch, unsigned flag,
                                                    unsigned long long v) {
-  return ((unsigned long long)(epoch & 0xFFFFu) << 48) | ((unsigned long long)flag << 46) |
+  return ((unsigned long long)(epoch & kEpochMask) << 52) | ((unsigned long long)flag << 50) |
          (v & kValMask);
 }
-__device__ __forceinline__ unsigned w_epoch(unsigned long long w) { return (unsigned)(w >> 48); }
-__device__ __forceinline__ unsigned w_flag(unsigned long long w) { return (unsigned)(w >> 46) & 3u; }
+__device__ __forceinline__ unsigned w_epoch(unsigned long long w) { return (unsigned)(w >> 52); }
+__device__ __forceinline__ unsigned w_flag(unsigned long long w) { return (unsigned)(w >> 50) & 3u; }
 
 // Tile aggregate of the segmented scan that lays out the next level (a segment = the survivors
 // of one owner row b; segments start at the owner's first candidate, a "head"):
@@ -105,10 +107,11 @@ __device__ __forceinline__ SegAgg seg_shfl_xor(const SegAgg& v, int off) {
 // Two words per tile.  An aggregate fits ONE word (S, O, F <= 256 and C <= 256*255/2: 9+9+9+1+15
 // bits), so the common case of the look-back reads one word per predecessor; an inclusive prefix
 // spans both, w1 written before w0 and accepted only when both carry the flag.  S and O count
-// this level's rows (< 2^28: a level has at most status_cap * 256 = 2^28 candidates) but C, the
-// NEXT level's candidate total, is quadratic in the survivors per class: it gets 36 bits and
-// saturates there, so a prefix past the limit reads as >= 2^28 and the last tile's capacity
-// guard (Ct >= 2^28 -> overflow 4 -> chunked path) fires instead of accepting wrapped offsets.
+// this level's rows (< 2^31: rows are int32-indexed; 31 bits each) but C, the NEXT level's
+// candidate total, is quadratic in the survivors per class: it gets 38 bits and saturates
+// there, so a prefix past the limit reads as >= 2^31 and the last tile's capacity guard
+// (Ct >= 2^31 -> overflow 4 -> chunked path) fires instead of accepting wrapped offsets.
+// (Round 3 packed S / O in 28 bits with 16-bit tags: config 2 at max_len 4 overflowed.)
 __device__ __forceinline__ void seg_publish(unsigned long long* my, unsigned e, unsigned flag,
                                             const SegAgg& v) {
   if (flag == 1) {
@@ -117,9 +120,9 @@ __device__ __forceinline__ void seg_publish(unsigned long long* my, unsigned e, 
                                   ((unsigned long long)v.C << 28)));
   } else {
     const unsigned long long o = (unsigned long long)v.O;
-    const unsigned long long c = v.C >= (1ll << 36) ? (1ull << 36) - 1 : (unsigned long long)v.C;
-    st_relaxed(my + 1, pack(e, 2, c | ((o >> 18) << 36)));
-    st_relaxed(my, pack(e, 2, (unsigned long long)v.S | ((o & 0x3FFFFull) << 28)));
+    const unsigned long long c = v.C >= (1ll << 38) ? (1ull << 38) - 1 : (unsigned long long)v.C;
+    st_relaxed(my + 1, pack(e, 2, c | ((o >> 19) << 38)));
+    st_relaxed(my, pack(e, 2, (unsigned long long)v.S | ((o & 0x7FFFFull) << 31)));
   }
 }
 __device__ __forceinline__ bool seg_valid(unsigned long long w0, unsigned long long w1, unsigned e) {
@@ -137,11 +140,11 @@ __device__ __forceinline__ SegAgg seg_decode(unsigned long long w0, unsigned lon
     v.C = (int64_t)(x >> 28);
   } else {
     const unsigned long long y = w1 & kValMask;
-    v.S = (int32_t)(x & 0xFFFFFFFull);
-    v.O = (int32_t)((x >> 28) | ((y >> 36) << 18));
+    v.S = (int32_t)(x & 0x7FFFFFFFull);
+    v.O = (int32_t)((x >> 31) | ((y >> 38) << 19));
     v.F = 0;
     v.H = true;
-    v.C = (int64_t)(y & 0xFFFFFFFFFull);
+    v.C = (int64_t)(y & 0x3FFFFFFFFFull);
   }
   return v;
 }
@@ -163,7 +166,7 @@ __device__ __forceinline__ SegAgg wave_fold(SegAgg v) {
 // exclusive prefix (every lane).
 __device__ SegAgg lookback_seg(unsigned long long* st, int64_t t, unsigned epoch, const SegAgg& agg,
                                FCtl* ctl) {
-  const unsigned e = epoch & 0xFFFFu;
+  const unsigned e = epoch & kEpochMask;
   const int lane = threadIdx.x & 63;
   unsigned long long* my = st + 2 * t;
   const SegAgg zero{0, 0, 0, false, 0};
@@ -427,6 +430,13 @@ __device__ __forceinline__ int64_t wave_incl_sum64(int64_t x) {
 // look-back and writes the next level's candidate offsets and tile→row entries, so the block
 // meets only twice.  Returns the survivor's row index in the next level (-1: failed); the last
 // tile sets the next level's sizes and allocates its children's buffers (not at a leaf level).
+// capacity guard (overflow 4): when the trie arrays are what ran out, record the node count the
+// level needs (MiB units) so the host sizes the next call's arrays for it
+__device__ inline void fail_capacity(FCtl* ctl, int64_t need, int64_t out_cap) {
+  if (need > out_cap) atomicMax(&ctl->need_out_m, (unsigned)((need + (1ll << 20) - 1) >> 20));
+  atomicExch(&ctl->overflow, 4u);
+}
+
 __device__ int64_t tile_epilogue(EpiSmem& sm, int64_t t, int64_t n_tiles, bool live, int flag,
                                  bool head, unsigned long long* status, unsigned epoch, FCtl* ctl,
                                  FLevel* nx, int64_t* co_nx, int32_t* tile_row_nx, int64_t scap,
@@ -528,8 +538,8 @@ __device__ int64_t tile_epilogue(EpiSmem& sm, int64_t t, int64_t n_tiles, bool l
       if (!leaf) {
         co_nx[St] = Ct;
         if (child_base + St + Ct > out_cap || (Ct + kTile - 1) / kTile > scap ||
-            Ct >= (1ll << 28))
-          atomicExch(&ctl->overflow, 4u);
+            Ct >= kRowLimit)
+          fail_capacity(ctl, child_base + St + Ct, out_cap);
         else
           alloc_level(ctl, nx + 1, Ct, Wp);
       }
@@ -567,7 +577,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(FLevel* __restrict__ lv,
   __shared__ int64_t s_ticket;
   __shared__ EpiSmem epi;
   if (ctl->overflow) return;
-  epoch = (ctl->epoch_base + epoch) & 0xFFFFu;  // per-call base (FCtl) + launch index
+  epoch = (ctl->epoch_base + epoch) & kEpochMask;  // per-call base (FCtl) + launch index
   const int cbk = A.deferred_dl ? A.copy_blocks : 0;  // copy blocks (lead the grid by default)
   const int64_t tgrid = (int64_t)gridDim.x - cbk;     // tile blocks
   const int64_t cb0 = A.copy_last ? tgrid : 0;
@@ -795,7 +805,7 @@ __global__ __launch_bounds__(kBlock, KB <= 6 ? 4 : 1) void k_level_count_small(F
                "s"(rank), "s"(gid));
   asm volatile("" ::"s"(cbm2), "s"(crank), "s"(cgid), "s"(cslot), "s"(r0_spec), "s"(ebase));
   if (ovf) return;
-  epoch = (ebase + epoch) & 0xFFFFu;  // per-call base (FCtl) + launch index
+  epoch = (ebase + epoch) & kEpochMask;  // per-call base (FCtl) + launch index
   if (copy_role) {
     copy_prev_level(lv, ctl, A, (int)(blockIdx.x - cb0));
     return;
@@ -1249,8 +1259,8 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
     ok = 1;
     if (!a.m) {
       if (F + n_cand > a.out_cap || (n_cand + kTile - 1) / kTile > (int64_t)ctl->status_cap ||
-          n_cand >= (1ll << 28)) {
-        atomicExch(&ctl->overflow, 4u);
+          n_cand >= kRowLimit) {
+        fail_capacity(ctl, F + n_cand, a.out_cap);
         ok = 0;
       } else {
         alloc_level(ctl, &desc[2], n_cand, a.Wp);
@@ -1262,8 +1272,8 @@ __global__ __launch_bounds__(1024) void k_level_root_setup(FLevel* desc, FCtl* c
       atomicAdd(&ctl->candidates, (unsigned long long)n_cand);
       if (a.leaf) C2 = 0;  // level 2 is the last: no candidates below it
       if (F + S2 + C2 > a.out_cap || (C2 + kTile - 1) / kTile > (int64_t)ctl->status_cap ||
-          C2 >= (1ll << 28) || S2 >= (1ll << 28)) {
-        atomicExch(&ctl->overflow, 4u);
+          C2 >= kRowLimit || S2 >= kRowLimit) {
+        fail_capacity(ctl, F + S2 + C2, a.out_cap);
         ok = 0;
       } else {
         alloc_level(ctl, &l2, S2, a.Wp);

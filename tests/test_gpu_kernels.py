@@ -601,21 +601,29 @@ def test_encode_tiled_long_shard(gpu_mod, T, I, ms, min_f):
                                   ref.reshape(F, Wp)[:, :used])
 
 
-def test_level_candidate_total_past_2_28_falls_back(gpu_mod):
+def test_level_candidate_total_past_the_status_capacity(gpu_mod, monkeypatch):
     """64 transactions holding the same 1200 items: every itemset is frequent, and the level-3
-    candidate total C(1200, 3) = 287,280,400 passes 2^28.  The fused path's look-back prefix
-    saturates instead of wrapping, its capacity guard fires (overflow 4) and the chunked path
-    produces the exact binomial counts; the deep count-only miner agrees."""
+    candidate total C(1200, 3) = 287,280,400 passes 2^28 (round 3's look-back limit).  With the
+    look-back window shrunk (status_cap hook) past it, the capacity guard fires (overflow 4) and
+    the chunked path produces the exact binomial counts; with the default window the level is
+    counted (fused, or chunked when the device arena declines) with the same counts; the deep
+    count-only miner agrees."""
     from math import comb
     T, I = 64, 1200
     tx_ptr = np.arange(T + 1, dtype=np.int64) * I
     items = np.tile(np.arange(I, dtype=np.int32), T)
+    want = I + comb(I, 2) + comb(I, 3)
+    monkeypatch.setenv("KMLS_TEST_HOOKS", "status_cap=65536")
     g = gpu_mod.GpuMiner(0)
     g.load_csr(tx_ptr, items, I)
     r = g.mine(0.5, 3, download=False)
-    want = I + comb(I, 2) + comb(I, 3)
     assert r["stats"]["n_itemsets"] == want
     assert "overflow code 4" in r["stats"].get("levels_path", "") or \
         "fallback" in r["stats"].get("levels_path", ""), r["stats"].get("levels_path")
+    monkeypatch.delenv("KMLS_TEST_HOOKS")
+    g2 = gpu_mod.GpuMiner(0)
+    g2.load_csr(tx_ptr, items, I)
+    r2 = g2.mine(0.5, 3, download=False)
+    assert r2["stats"]["n_itemsets"] == want, r2["stats"].get("levels_path")
     d = g.mine_deep(0.5, 3)
     assert d["per_level"][1:4] == [I, comb(I, 2), comb(I, 3)]
