@@ -240,11 +240,14 @@ struct WaveLds {
   unsigned long long f_hash[kBatchFrames];
   unsigned f_s0[kBatchFrames], f_m[kBatchFrames], f_meta[kBatchFrames];
   unsigned P[kBatchFrames + 1], G[kBatchFrames + 1];
-  unsigned g_cnt[kCap], g_start[kCap];
-  unsigned g_pos[kCap];             // first pair of member group g (its run start)
-  unsigned g_fi[kCap];              // frame << 16 | member of group g
+  // member-group tables in 16 bits (every value < kCap; frames of a batch have <= 32 members):
+  // with the u32 block bases, 8 KB of LDS per wave instead of 12.5, so four 4-wave workgroups
+  // fit a CU's 160 KB
+  unsigned short g_cnt[kCap], g_start[kCap];
+  unsigned short g_pos[kCap];       // first pair of member group g (its run start)
+  unsigned short g_fi[kCap];        // frame << 8 | member of group g
   unsigned long long g_flag[kCap / 64];  // bit p: a group starts at pair p
-  unsigned long long b_base[kBStack];
+  unsigned b_base[kBStack];         // byte offset in the wave's stack region (< 4 GB)
   unsigned b_live[kBStack];
   unsigned long long depth_cnt[64];
   ProjLds<MAXT> proj;
@@ -303,7 +306,7 @@ __device__ __forceinline__ void free_blocks(WaveLds<MAXT>& L, WaveState& st) {
   while (st.nb > 0) {
     const unsigned live = uni(L.b_live[st.nb - 1 + vzero()]);
     if (live) break;
-    st.mem_top = uni64(L.b_base[st.nb - 1 + vzero()]);
+    st.mem_top = (unsigned long long)uni(L.b_base[st.nb - 1 + vzero()]);
     st.nb -= 1;
   }
 }
@@ -561,7 +564,7 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
   }
   if (S >= 2 && deeper) {
     if (lane == 0) {
-      L.b_base[st.nb] = st.mem_top;
+      L.b_base[st.nb] = (unsigned)st.mem_top;
       L.b_live[st.nb] = 1;
       DeepFrame c;
       c.blk = (unsigned long long)cb;
@@ -636,14 +639,14 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
   // group is then the number of group starts at or before it
   for (unsigned g = lane; g < NG; g += 64) {
     L.g_cnt[g] = 0;
-    L.g_start[g] = 0xffffffffu;
+    L.g_start[g] = 0xffffu;
     unsigned f = 0;
     for (unsigned step = 32; step; step >>= 1)
       if (f + step < k && L.G[f + step] <= g) f += step;
     const unsigned i = g - L.G[f], fmm = L.f_m[f];
     const unsigned pos = L.P[f] + i * fmm - i * (i + 1) / 2;
-    L.g_pos[g] = pos;
-    L.g_fi[g] = (f << 16) | i;
+    L.g_pos[g] = (unsigned short)pos;
+    L.g_fi[g] = (unsigned short)((f << 8) | i);
     atomicOr(&L.g_flag[pos >> 6], 1ull << (pos & 63));
   }
   __builtin_amdgcn_wave_barrier();
@@ -663,8 +666,8 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
     unsigned f = 0, i = 0, j = 0;
     if (act) {
       const unsigned fi = L.g_fi[g];
-      f = fi >> 16;
-      i = fi & 0xffffu;
+      f = fi >> 8;
+      i = fi & 0xffu;
       j = i + 1 + (p - L.g_pos[g]);
     }
     gbase += (unsigned)__popcll(gw);
@@ -701,9 +704,13 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
       const unsigned long long below_end = after ? ((1ull << __builtin_ctzll(after)) - 1ull) : ~0ull;
       const unsigned long long rs = mask & below_end & ~lanelt;  // this run's survivors
       if (rs) {
-        atomicAdd(&L.g_cnt[g], (unsigned)__popcll(rs));
-        const unsigned first = (unsigned)__builtin_ctzll(rs);
-        atomicMin(&L.g_start[g], S + (unsigned)__popcll(mask & ((1ull << first) - 1ull)));
+        // one head per group in a chunk (its run of lanes), chunks in program order: plain
+        // read-modify-writes, no two lanes on one group
+        L.g_cnt[g] = (unsigned short)(L.g_cnt[g] + (unsigned)__popcll(rs));
+        if (L.g_start[g] == 0xffffu) {
+          const unsigned first = (unsigned)__builtin_ctzll(rs);
+          L.g_start[g] = (unsigned short)(S + (unsigned)__popcll(mask & ((1ull << first) - 1ull)));
+        }
       }
     }
     // the batch's frames are siblings of one block: one depth
@@ -751,7 +758,7 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
   pushed = uni(pushed);
   if (pushed) {
     if (lane == 0) {
-      L.b_base[st.nb] = st.mem_top;
+      L.b_base[st.nb] = (unsigned)st.mem_top;
       L.b_live[st.nb] = pushed;
     }
     st.nb += 1;
@@ -779,14 +786,15 @@ __device__ __forceinline__ void step_tier(unsigned wt, bool row_mode, const Deep
                                                           lane, acc);
 }
 
-// waves per SIMD the count kernel is compiled for by default: the register budget that keeps
-// the widest tier of the launch free of scratch spills (blocks_per_cu may select the other
-// instance of a width class)
+// waves per SIMD the count kernel is compiled for by default (blocks_per_cu may select the other
+// instance of a width class).  4 up to MAXT 16: 128 VGPRs with ~20 spilled to scratch, and 8 KB
+// of LDS tables per wave so four workgroups fit the CU — 33.2 vs 36.1 ms at ds1 @0.02 against
+// 3 waves/SIMD at 162 VGPRs (profiles/r4p_*); the wider tiers keep their registers.
 template <int MAXT>
-constexpr int deep_waves_per_simd() { return MAXT <= 8 ? 4 : (MAXT <= 16 ? 3 : 2); }
+constexpr int deep_waves_per_simd() { return MAXT <= 16 ? 4 : 2; }
 
 template <int MAXT, int WPS, bool EMIT>
-__global__ __launch_bounds__(256, WPS) void k_deep_count(DeepArgs a) {
+__global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS))) void k_deep_count(DeepArgs a) {
   __shared__ WaveLds<MAXT> lds[kWaves];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -1305,6 +1313,7 @@ void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s) {
   const dim3 g((unsigned)grid), b(64 * kWaves);
   if (a.node_parent != nullptr) {  // emit mode: the default occupancy of each width class
     if (mt == 8) hipLaunchKernelGGL((k_deep_count<8, 4, true>), g, b, 0, s, a);
+    else if (mt == 16 && w == 4) hipLaunchKernelGGL((k_deep_count<16, 4, true>), g, b, 0, s, a);
     else if (mt == 16) hipLaunchKernelGGL((k_deep_count<16, 3, true>), g, b, 0, s, a);
     else if (mt == 32) hipLaunchKernelGGL((k_deep_count<32, 2, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_deep_count<64, 2, true>), g, b, 0, s, a);

@@ -7,9 +7,10 @@ per-size counts and the content digest (``kmls/digest.hpp``, equal to the digest
 trie) are kept, nothing is materialised (``GpuMiner.mine_deep``, ``csrc/kernels/deep.hip``).
 
 Split over ranks (strong scaling): every rank builds the same level-2 classes on its own GPU
-(deterministic), rank r mines the level-3 tasks t with t % world == r, and the per-size counts
-and digest sums are all-reduced (the digest xors all-gathered), so every rank ends with the
-result of the whole problem.  The combine runs through one of:
+(deterministic), the level-3 tasks are ordered by an estimated cost and dealt to the ranks in a
+snake order (``csrc/host/deep_run.hip``), and the per-size counts and digest sums are all-reduced
+(the digest xors all-gathered), so every rank ends with the result of the whole problem.  The
+combine runs through one of:
 
 * ``"rccl"``  — the native communicator (``csrc/host/comm_rccl.cpp``: RCCL over xGMI, issued on
   the miner's stream inside ``mine_deep``);
@@ -21,7 +22,10 @@ result of the whole problem.  The combine runs through one of:
 from __future__ import annotations
 
 import os
-from typing import Dict, List, Optional
+import math
+import random
+import time
+from typing import Dict, List, Optional, Sequence
 
 from ..ops import native
 
@@ -122,3 +126,54 @@ class DeepMiner:
 
     def synchronize(self) -> None:
         self.g.synchronize()
+
+
+def estimate_total(g, min_support: float, world: int, samples: int, seed: int = 0,
+                   max_len: int = 0, budget_s: float = 0.0, ranks: Optional[Sequence[int]] = None,
+                   **opts) -> Dict:
+    """Estimate of a full mining result too large to count whole on one GPU in a bench step
+    (BASELINE config 2, ds1 @ 0.01: > 4.7e11 itemsets up to size 9 alone).
+
+    The level-3 tasks are dealt to `world` virtual ranks exactly as a real split deals them
+    (cost-ordered snake deal, so every rank's share is a stratified slice of the task costs);
+    `samples` ranks drawn uniformly without replacement are mined EXACTLY (``mine_deep`` with
+    that rank/world, no communicator), and the total is ``world x mean`` of their counts: an
+    unbiased estimator, with the standard error from the sample variance and the
+    finite-population correction.  Per-size counts are estimated the same way.  Sampling stops
+    early once `budget_s` seconds have been spent (at least two samples).  Reference: the
+    reference mines every size (``machine-learning/main.py:272``)."""
+    rng = random.Random(seed)
+    pick = list(ranks) if ranks is not None else rng.sample(range(world), min(samples, world))
+    xs, per, secs, done = [], [], [], []
+    t_all = time.perf_counter()
+    for r in pick:
+        t = time.perf_counter()
+        d = g.mine_deep(min_support, max_len, int(r), int(world), None, **opts)
+        secs.append(time.perf_counter() - t)
+        xs.append(int(d["n_itemsets"]))
+        per.append([int(v) for v in d["per_level"]])
+        done.append(int(r))
+        if budget_s and len(xs) >= 2 and time.perf_counter() - t_all > budget_s:
+            break
+    k = len(xs)
+    fpc = 1.0 - k / world
+
+    def est(vals):
+        m = sum(vals) / k
+        var = sum((v - m) ** 2 for v in vals) / (k - 1) if k > 1 else float("nan")
+        return world * m, world * math.sqrt(max(var, 0.0) * fpc / k) if k > 1 else float("nan")
+
+    n_est, n_se = est(xs)
+    depth = max(len(p) for p in per)
+    per_est = []
+    for dd in range(1, depth):
+        e, s = est([p[dd] if dd < len(p) else 0 for p in per])
+        per_est.append({"size": dd, "estimate": round(e), "se": round(s)})
+    t_est, t_se = est(secs)
+    return {"method": "snake-dealt virtual ranks, simple random sample, world x mean",
+            "world": world, "samples": k, "ranks": done, "min_support": min_support,
+            "max_len": max_len, "n_itemsets_estimate": round(n_est),
+            "n_itemsets_se": round(n_se), "rel_se": round(n_se / n_est, 4) if n_est else None,
+            "per_size": per_est, "one_gpu_s_estimate": round(t_est, 1),
+            "one_gpu_s_se": round(t_se, 1), "sample_s": [round(x, 3) for x in secs],
+            "sample_n": xs}
