@@ -26,7 +26,7 @@ DeepBufs::~DeepBufs() {
                   (void*)d_m, (void*)d_off, (void*)d_toff, (void*)d_cost, (void*)d_order,
                   (void*)d_trace, (void*)d_ticks, (void*)n_parent, (void*)n_item,
                   (void*)n_count, (void*)n_depth, (void*)d_node_off, (void*)d_split_q,
-                  (void*)d_split_heap})
+                  (void*)d_split_heap, (void*)d_ocost, (void*)d_otmp})
     if (p) (void)hipFree(p);
   if (h_ctl) (void)hipHostFree(h_ctl);
 }
@@ -226,45 +226,56 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     const int64_t* d_order = nullptr;
     if (deeper && T > 0 && (opt.assign == 1 || opt.trace)) {
       // every task's class size (its level-3 survivors) on the device; tasks ordered largest
-      // first (counting sort, stable in t) and dealt over the ranks in snake order, so every
+      // first (device radix sort, stable in t) and dealt over the ranks in snake order, so every
       // rank gets an equal share of each size class and starts its queue with its largest tasks
       // (the long subtrees begin first instead of last: a shorter tail)
       const auto ta = now();
-      int64_t c1 = b.t_cap, c2 = b.t_cap;
+      int64_t c1 = b.t_cap, c2 = b.t_cap, c3 = b.t_cap;
       grow(b.d_cost, c1, T);
       grow(b.d_order, c2, T);
-      b.t_cap = std::max(c1, c2);
+      grow(b.d_ocost, c3, T);
+      b.t_cap = std::min({c1, c2, c3});
       kern::deep_task_cost(b.d_off, b.d_m, b.d_toff, F, b.root, in.minsup, b.d_cost, s, E);
-      std::vector<uint32_t> cost((size_t)T);
-      KMLS_HIP(hipMemcpyAsync(cost.data(), b.d_cost, (size_t)T * 4, hipMemcpyDeviceToHost, s));
-      KMLS_HIP(hipStreamSynchronize(s));
       std::vector<int64_t> mine;
-      mine.reserve((size_t)(T / world + 1));
+      std::vector<uint32_t> cost;  // cost[q] of the rank's q-th task (host copies: pre-split, trace)
       if (opt.assign == 1) {
-        uint32_t cmax = 0;
-        for (uint32_t c : cost) cmax = std::max(cmax, c);
-        std::vector<int64_t> start((size_t)cmax + 2, 0);
-        for (uint32_t c : cost) start[(size_t)(cmax - c) + 1] += 1;  // descending cost buckets
-        for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
-        std::vector<int64_t> sorted((size_t)T);
-        for (int64_t t = 0; t < T; ++t) sorted[(size_t)start[(size_t)(cmax - cost[(size_t)t])]++] = t;
-        for (int64_t q = 0; q < T; ++q) {
-          const int64_t rnd = q / world, pos = q % world;
-          if ((rnd & 1 ? world - 1 - pos : pos) == rank) mine.push_back(sorted[(size_t)q]);
+        // sorted and dealt on the device (deep_order.hip): no copy of the costs, no sync here
+        if (b.otmp_bytes < kern::deep_task_order_bytes(T)) {
+          if (b.d_otmp) KMLS_HIP(hipFree(b.d_otmp));
+          b.otmp_bytes = kern::deep_task_order_bytes(T);
+          KMLS_HIP(hipMalloc((void**)&b.d_otmp, b.otmp_bytes));
         }
+        n_tasks = kern::deep_task_order(b.d_cost, T, rank, world, b.d_otmp, b.otmp_bytes,
+                                        b.d_order, b.d_ocost, s);
+        if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
+        const bool deeper4 = in.max_len == 0 || in.max_len >= 4;  // the split classes expand
+        const bool presplit = opt.presplit_cost > 0 && opt.presplit_budget > 0 && opt.steal &&
+                              deeper4 && world > 1;
+        if (presplit || opt.trace) {
+          mine.resize((size_t)n_tasks);
+          cost.resize((size_t)n_tasks);
+          KMLS_HIP(hipMemcpyAsync(mine.data(), b.d_order, (size_t)n_tasks * 8, hipMemcpyDeviceToHost, s));
+          KMLS_HIP(hipMemcpyAsync(cost.data(), b.d_ocost, (size_t)n_tasks * 4, hipMemcpyDeviceToHost, s));
+          KMLS_HIP(hipStreamSynchronize(s));
+        }
+        // (a rank split only: on one GPU the extra launch costs more than the shorter tail gains,
+        // profiles/r4i_*)
+        if (presplit)
+          while (n_heavy < n_tasks && cost[(size_t)n_heavy] >= std::max(opt.presplit_cost, 2u) &&
+                 cost[(size_t)n_heavy] > opt.split_min)
+            ++n_heavy;
       } else {
-        for (int64_t t = rank; t < T; t += world) mine.push_back(t);
+        std::vector<uint32_t> all((size_t)T);
+        KMLS_HIP(hipMemcpyAsync(all.data(), b.d_cost, (size_t)T * 4, hipMemcpyDeviceToHost, s));
+        KMLS_HIP(hipStreamSynchronize(s));
+        for (int64_t t = rank; t < T; t += world) {
+          mine.push_back(t);
+          cost.push_back(all[(size_t)t]);
+        }
+        n_tasks = (int64_t)mine.size();
+        if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
+        KMLS_HIP(hipMemcpyAsync(b.d_order, mine.data(), (size_t)n_tasks * 8, hipMemcpyHostToDevice, s));
       }
-      n_tasks = (int64_t)mine.size();
-      if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
-      const bool deeper4 = in.max_len == 0 || in.max_len >= 4;  // the split classes expand
-      // (a rank split only: on one GPU the extra launch costs more than the shorter tail gains,
-      // profiles/r4i_*)
-      if (opt.assign == 1 && opt.presplit_cost > 0 && opt.presplit_budget > 0 && opt.steal &&
-          deeper4 && world > 1)
-        while (n_heavy < n_tasks && cost[(size_t)mine[(size_t)n_heavy]] >= std::max(opt.presplit_cost, 2u) &&
-               cost[(size_t)mine[(size_t)n_heavy]] > opt.split_min)
-          ++n_heavy;
       if (n_heavy > 0) {
         // every heavy task (i, k) becomes its class of c = cost members after one row step,
         // spilled as c - 1 single-member tasks over one heap copy of at most the root class
@@ -277,7 +288,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
         for (int64_t q = 0; q < n_heavy; ++q) {
           const int64_t t = mine[(size_t)q];
           const int64_t i = root_of[(size_t)t];
-          const int64_t c = cost[(size_t)t];
+          const int64_t c = cost[(size_t)q];
           const int64_t pad_i = (m[(size_t)i] + 15) / 16 * 16;
           const int64_t wt_i = (off[(size_t)i + 1] - off[(size_t)i]) / (8 * pad_i) - 1 - E;
           split_q[(size_t)q] = split_tasks;
@@ -286,14 +297,12 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
           split_bytes += (wt_i + 1 + E) * ((c + 15) / 16 * 16) * 8;
         }
       }
-      KMLS_HIP(hipMemcpyAsync(b.d_order, mine.data(), (size_t)n_tasks * 8, hipMemcpyHostToDevice, s));
       d_order = b.d_order;
       if (opt.trace) {
         res.task_ids = mine;
-        res.task_cost.resize(mine.size());
-        for (size_t q = 0; q < mine.size(); ++q) res.task_cost[q] = cost[(size_t)mine[q]];
+        res.task_cost = cost;
       }
-      KMLS_HIP(hipStreamSynchronize(s));  // `mine` dies at scope end
+      if (opt.assign != 1) KMLS_HIP(hipStreamSynchronize(s));  // `mine` dies at scope end
       res.ms_assign = ms_since(ta);
     } else {
       n_tasks = deeper ? (T - rank + world - 1) / world : 0;

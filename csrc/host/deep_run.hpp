@@ -42,7 +42,10 @@ struct DeepBufs {
   int64_t f_cap = 0;
   uint32_t* d_cost = nullptr;   // [T] level-3 task costs (assign = 1)
   int64_t* d_order = nullptr;   // [T] this rank's task ids in queue order
+  uint32_t* d_ocost = nullptr;  // [T] their costs
   int64_t t_cap = 0;
+  char* d_otmp = nullptr;       // kern::deep_task_order scratch
+  size_t otmp_bytes = 0;
   // emit mode: the node arena (SoA, arena_cap ids) and the level-2 node bases
   unsigned* n_parent = nullptr;
   unsigned* n_item = nullptr;

@@ -44,6 +44,7 @@ constexpr int kW = 4;       // waves per workgroup
 constexpr int kTx = 64;     // transactions per wave chunk (lane = transaction)
 constexpr int kEnt = 2048;  // frequent entries of one sub-chunk (LDS, per wave)
 constexpr int kHead = 64;   // most frequent ranks whose pairs are counted in LDS
+constexpr int kScanU = 4;   // 64-item rows of the CSR scan in flight per wave
 
 __device__ __forceinline__ int frequent_rank(int it, const int32_t* __restrict__ rank_of,
                                              const uint32_t* __restrict__ fmask) {
@@ -60,11 +61,18 @@ struct ChunkLds {
   uint32_t poff[kTx + 1];     // pair offset of transaction x
 };
 
+// the stats pass only counts: offsets and per-transaction counts (0.5 KB per wave, so its
+// occupancy is set by registers, not by an unused entry buffer)
+struct ScanLds {
+  uint32_t pt[kTx + 1];
+  uint32_t kc[kTx];
+};
+
 // Coalesced scan of the chunk's items (the contiguous CSR span of its transactions): frequent
 // ranks compacted in order into L.ent (while they fit: WRITE), per-transaction counts in L.kc.
 // Returns the chunk's frequent entries (may exceed kEnt; then L.ent holds only the first kEnt).
-template <bool WRITE>
-__device__ __forceinline__ unsigned chunk_scan(ChunkLds& L, const int64_t* __restrict__ ptr,
+template <bool WRITE, typename Lds>
+__device__ __forceinline__ unsigned chunk_scan(Lds& L, const int64_t* __restrict__ ptr,
                                                const int32_t* __restrict__ items,
                                                const int32_t* __restrict__ rank_of,
                                                const uint32_t* __restrict__ fmask, int64_t t0,
@@ -76,23 +84,40 @@ __device__ __forceinline__ unsigned chunk_scan(ChunkLds& L, const int64_t* __res
   __builtin_amdgcn_wave_barrier();
   const unsigned long long lanelt = (1ull << lane) - 1ull;
   unsigned ne = 0;
-  for (unsigned p0 = 0; p0 < span; p0 += 64) {
-    const unsigned p = p0 + lane;
-    int r = -1;
-    if (p < span) r = frequent_rank(items[b0 + p], rank_of, fmask);
-    const unsigned long long m = __ballot(r >= 0);
-    if (r >= 0) {
-      // transaction: the last x with pt[x] <= p
-      unsigned x = 0;
-      for (unsigned step = 32; step; step >>= 1)
-        if (x + step < n && L.pt[x + step] <= p) x += step;
-      atomicAdd(&L.kc[x], 1u);
-      if (WRITE) {
-        const unsigned e = ne + (unsigned)__popcll(m & lanelt);
-        if (e < (unsigned)kEnt) L.ent[e] = r;
-      }
+  // kScanU rows of 64 items per iteration: their item loads, then their mask-word and rank
+  // gathers, are all in flight before the first is used (one row at a time left the scan
+  // latency-bound: ~280 GB/s of items at 100M x 1M)
+  for (unsigned p0 = 0; p0 < span; p0 += 64u * kScanU) {
+    int it[kScanU], r[kScanU];
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) {
+      const unsigned p = p0 + 64u * (unsigned)u + (unsigned)lane;
+      it[u] = p < span ? items[b0 + p] : -1;
     }
-    ne += (unsigned)__popcll(m);
+    uint32_t fw[kScanU];
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u)
+      fw[u] = (fmask != nullptr && it[u] >= 0) ? fmask[it[u] >> 5] : ~0u;
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u)
+      r[u] = (it[u] >= 0 && ((fw[u] >> (it[u] & 31)) & 1u)) ? rank_of[it[u]] : -1;
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) {
+      const unsigned p = p0 + 64u * (unsigned)u + (unsigned)lane;
+      const unsigned long long m = __ballot(r[u] >= 0);
+      if (r[u] >= 0) {
+        // transaction: the last x with pt[x] <= p
+        unsigned x = 0;
+        for (unsigned step = 32; step; step >>= 1)
+          if (x + step < n && L.pt[x + step] <= p) x += step;
+        atomicAdd(&L.kc[x], 1u);
+        if constexpr (WRITE) {
+          const unsigned e = ne + (unsigned)__popcll(m & lanelt);
+          if (e < (unsigned)kEnt) L.ent[e] = r[u];
+        }
+      }
+      ne += (unsigned)__popcll(m);
+    }
   }
   __builtin_amdgcn_wave_barrier();
   return ne;
@@ -105,9 +130,9 @@ __global__ __launch_bounds__(256) void k_cooc_stats(const int64_t* __restrict__ 
                                                     const int32_t* __restrict__ rank_of,
                                                     const uint32_t* __restrict__ fmask,
                                                     unsigned long long* __restrict__ out) {
-  __shared__ ChunkLds lds[kW];
+  __shared__ ScanLds lds[kW];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  ChunkLds& L = lds[wid];
+  ScanLds& L = lds[wid];
   unsigned long long pairs = 0;
   unsigned kmax = 0;
   const int64_t nchunks = (n_tx + kTx - 1) / kTx;

@@ -125,6 +125,13 @@ void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* ta
 void deep_task_cost(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
                     const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s, int extra = 0);
 void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s);
+// (deep_order.hip) tasks by cost, largest first and stable in t, dealt over `world` ranks in
+// snake order: order[j] / order_cost[j] = this rank's j-th task and its cost, j < the returned
+// count (= deep_task_share); tmp = deep_task_order_bytes(T) bytes of device scratch
+int64_t deep_task_share(int64_t T, int rank, int world);
+size_t deep_task_order_bytes(int64_t T);
+int64_t deep_task_order(const uint32_t* cost, int64_t T, int rank, int world, void* tmp,
+                        size_t tmp_bytes, int64_t* order, uint32_t* order_cost, hipStream_t s);
 
 // ---- mining (mine.hip) ----
 void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* counts,

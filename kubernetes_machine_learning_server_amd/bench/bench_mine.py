@@ -16,6 +16,7 @@ all sizes mined (``main.py:272``), support sweep downwards (``main.py:450-473``)
 """
 from __future__ import annotations
 
+import json
 import os
 import time
 from typing import Callable, Dict, Optional
@@ -164,6 +165,19 @@ def run_deep_emit(dm, ms: float, world: int, rank: int, warmup: int, steps: int,
             "rank0_phases_ms": {k: round(v, 3) for k, v in r["phases_ms"].items()}}
 
 
+OFFLINE_SOURCE = ("scripts/full_count.py --world 256 on one MI355X (every virtual rank mined "
+                  "exactly, partials combined; profiles/config2_full/)")
+
+
+def offline_full_count() -> Optional[Dict]:
+    """The complete config-2 count (ds1 @ 0.01, every size) measured by scripts/full_count.py."""
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "config2_full_count.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as fh:
+        return json.load(fh)
+
+
 def deep_capped(dm, ms: float, budget_s: float, start_len: int = 4, max_cap: int = 64) -> Dict:
     """Full mining at `ms` with the itemset size cap raised one at a time while a call stays
     under `budget_s` (the last completed cap's counts, timed)."""
@@ -252,9 +266,8 @@ def run_config2(N, tx, names, tie, steps: int, verify: bool, deep_miner=None,
                 full_budget_s: float = 20.0) -> Dict:
     """BASELINE config 2: ds1 @ min_support 0.01 on 1 GPU."""
     ms = 0.01
-    # a 64 GB arena for the 1e8-node 4-item trie.  (The fused level loop still hands level 3
-    # to the chunked path here: its candidate total passes the fused look-back's 2^28 bound,
-    # "device overflow code 4"; the chunked path is exact and digest-verified.)
+    # a 64 GB arena for the 1e8-node 4-item trie: the fused level loop (1G-candidate look-back
+    # window) runs it from the second call on, once the first has sized the trie arrays
     g = N.GpuMiner(0, 64 << 30)
     g.load_csr(tx.tx_ptr, tx.items, tx.n_items)
     g.set_tie_rank(tie)
@@ -307,6 +320,17 @@ def run_config2(N, tx, names, tie, steps: int, verify: bool, deep_miner=None,
         if f["trail"] and f["trail"][0]["max_len"] == 4:
             r4 = deep_miner.mine(ms, 4)
             f["verified_max_len4_vs_trie"] = r4["digest"] == d4["digest"]
+        off = offline_full_count()
+        if off is not None:
+            # the complete result, counted once in 256 virtual-rank calls (55 GPU-minutes: too
+            # long for a bench step); this step's size-capped per-size counts must equal its prefix
+            L = f["max_len"]
+            f["complete_count_offline"] = {
+                k: off[k] for k in ("n_itemsets", "max_depth", "digest", "one_gpu_s",
+                                    "itemsets_per_s", "world_virtual")}
+            f["complete_count_offline"]["source"] = OFFLINE_SOURCE
+            f["capped_counts_match_offline_prefix"] = (
+                f["per_level"] == [int(x) for x in off["per_level"][1:L + 1]])
         out["full_mining"] = f
     return out
 

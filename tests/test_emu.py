@@ -21,6 +21,7 @@ def _build():
     srcs = [ROOT / "csrc/kernels/deep.hip", ROOT / "csrc/host/deep_run.hip"]
     host = [ROOT / f"csrc/host/{f}" for f in ("miner_cpu.cpp", "synth.cpp", "digest.cpp")]
     main = ROOT / "csrc/tests/deep_emu_main.cpp"
+    host.append(ROOT / "csrc/tests/deep_order_emu.cpp")  # stand-in for the hipCUB task sort
     deps = srcs + host + [main] + list((ROOT / "csrc/emu").rglob("*")) + \
         list((ROOT / "csrc/include").rglob("*.hpp")) + [ROOT / "csrc/kernels/kernels.hpp",
                                                         ROOT / "csrc/host/deep_run.hpp"]
