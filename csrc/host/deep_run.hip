@@ -80,7 +80,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   // ---- buffers (kept across calls) ----
   const auto t0 = now();
   // one 4-wave block per SIMD slot of the kernel instance (blocks_per_cu picks the instance)
-  const int blocks_per_cu = kern::deep_count_wps(maxt, opt.blocks_per_cu);
+  const int blocks_per_cu = kern::deep_count_wps(maxt, opt.blocks_per_cu, E != 0);
   const int grid = std::max(1, in.n_cus * blocks_per_cu);
   const int64_t waves = (int64_t)grid * kern::deep_waves_per_block();
   const size_t stack_need = std::max<size_t>(

@@ -1299,8 +1299,9 @@ void deep_task_cost(const int64_t* blk_off, const int32_t* m, const int64_t* tas
                      minsup, cost, (unsigned)extra);
 }
 
-int deep_count_wps(int maxt, int want) {
+int deep_count_wps(int maxt, int want, bool emit) {
   const int mt = deep_count_maxt(maxt);
+  if (emit) return mt == 8 ? 4 : mt == 16 ? 3 : 2;  // the instances deep_count launches
   if (mt == 8 && (want == 4 || want == 5)) return want;
   if (mt == 16 && (want == 3 || want == 4)) return want;
   if (mt == 32 && (want == 2 || want == 3)) return want;
@@ -1309,11 +1310,12 @@ int deep_count_wps(int maxt, int want) {
 
 void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s) {
   const int mt = deep_count_maxt(maxt);
-  const int w = deep_count_wps(mt, wps);
+  const int w = deep_count_wps(mt, wps, a.node_parent != nullptr);
   const dim3 g((unsigned)grid), b(64 * kWaves);
   if (a.node_parent != nullptr) {  // emit mode: the default occupancy of each width class
+    // (emit keeps 3 waves/SIMD at MAXT 16: its node-id bookkeeping pushes a 128-VGPR build into
+    // heavy spills, 56.7 vs 51.5 ms at ds1 @0.02, profiles/r4r_*)
     if (mt == 8) hipLaunchKernelGGL((k_deep_count<8, 4, true>), g, b, 0, s, a);
-    else if (mt == 16 && w == 4) hipLaunchKernelGGL((k_deep_count<16, 4, true>), g, b, 0, s, a);
     else if (mt == 16) hipLaunchKernelGGL((k_deep_count<16, 3, true>), g, b, 0, s, a);
     else if (mt == 32) hipLaunchKernelGGL((k_deep_count<32, 2, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_deep_count<64, 2, true>), g, b, 0, s, a);

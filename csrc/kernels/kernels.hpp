@@ -90,7 +90,7 @@ int deep_tier(int words);     // smallest instantiated block width >= words
 int deep_row_words(int W);    // root block width for W-word rows (a tier)
 int deep_count_maxt(int widest);    // count kernel instance covering block widths <= widest
 int deep_waves_per_simd(int maxt);  // its default occupancy (and blocks per CU)
-int deep_count_wps(int maxt, int want);  // instance occupancy: `want` if instantiated
+int deep_count_wps(int maxt, int want, bool emit = false);  // instance occupancy: `want` if instantiated
 int deep_waves_per_block();
 int deep_min_fcap();
 int deep_node_chunk();  // emit mode: node ids a wave takes at a time
