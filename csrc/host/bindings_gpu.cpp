@@ -351,6 +351,9 @@ void register_gpu_bindings(py::module_& m) {
            },
            py::arg("rows"), py::arg("ld"), py::arg("r0"), py::arg("nrows"), py::arg("minsup"))
       .def("bitgemm_rect", &gpu::GpuMiner::bitgemm_rect, py::call_guard<py::gil_scoped_release>())
+      .def("ring_pair_rows", &gpu::GpuMiner::ring_pair_rows, py::arg("comm"), py::arg("X"),
+           py::arg("F"), py::arg("Ws"), py::arg("out"), py::arg("ldo"),
+           py::call_guard<py::gil_scoped_release>())
       .def("mine_bitmaps", [](gpu::GpuMiner& g, uintptr_t bm, int64_t Wp, double ms, int max_len,
                               bool pairs_only, py::object owned, bool emit_level1, bool download,
                               bool gram, bool mfma) {

@@ -1276,6 +1276,50 @@ GpuMiner::RuleMap GpuMiner::rule_map_rows(uintptr_t rows_dev, int64_t ld, int64_
   return out;
 }
 
+void GpuMiner::ring_pair_rows(Comm* comm, uintptr_t X, int64_t F, int64_t Ws, uintptr_t out,
+                              int64_t ldo) {
+  KMLS_HIP(hipSetDevice(device_));
+  KMLS_CHECK(comm != nullptr && F >= 0 && Ws >= 0 && ldo >= F, "ring_pair_rows: comm, ldo >= F");
+  hipStream_t s = (hipStream_t)stream_;
+  const int W = comm->world(), R = comm->rank();
+  const int64_t fb = (F + W - 1) / std::max(W, 1);
+  const int64_t r0 = std::min<int64_t>(F, (int64_t)R * fb), r1 = std::min<int64_t>(F, r0 + fb);
+  KMLS_HIP(hipMemsetAsync((void*)out, 0, (size_t)std::max<int64_t>(r1 - r0, 0) * ldo * 4, s));
+  const uint64_t* x = (const uint64_t*)X;
+  if (W == 1) {
+    kern::bitgemm_rect(x + r0 * Ws, r1 - r0, x, F, Ws, (uint32_t*)out, ldo, s);
+    return;
+  }
+  if (!comm_s_) KMLS_HIP(hipStreamCreateWithFlags((hipStream_t*)&comm_s_, hipStreamNonBlocking));
+  hipStream_t cs = (hipStream_t)comm_s_;
+  const size_t blk = (size_t)F * (size_t)Ws;
+  const size_t mark = arena_->mark();
+  uint64_t* buf[2] = {(uint64_t*)arena_->push(std::max<size_t>(blk, 1) * 8),
+                      (uint64_t*)arena_->push(std::max<size_t>(blk, 1) * 8)};
+  Event ready, comp, recv;  // shard X written (encode on s) / count k done / shard k+1 landed
+  KMLS_HIP(hipEventRecord(ready.e, s));
+  KMLS_HIP(hipStreamWaitEvent(cs, ready.e, 0));
+  const uint64_t* cur = x;
+  for (int k = 0; k < W; ++k) {
+    uint64_t* nxt = buf[k & 1];
+    if (k + 1 < W) {
+      // nxt was the block counted at step k - 1: its count must be done before it is overwritten
+      if (k > 0) KMLS_HIP(hipStreamWaitEvent(cs, comp.e, 0));
+      comm->sendrecv(cur, (R + 1) % W, nxt, (R + W - 1) % W, blk, CommDtype::U64, cs);
+      KMLS_HIP(hipEventRecord(recv.e, cs));
+    }
+    kern::bitgemm_rect(cur + r0 * Ws, r1 - r0, cur, F, Ws, (uint32_t*)out, ldo, s);
+    KMLS_HIP(hipEventRecord(comp.e, s));
+    if (k + 1 < W) {
+      KMLS_HIP(hipStreamWaitEvent(s, recv.e, 0));
+      cur = nxt;
+    }
+  }
+  KMLS_HIP(hipStreamSynchronize(s));  // the scratch shards are released below
+  comm->wait_stream(cs);
+  arena_->pop_to(mark);
+}
+
 void GpuMiner::bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp,
                             uintptr_t C, int64_t ldc) {
   KMLS_HIP(hipSetDevice(device_));

@@ -312,6 +312,12 @@ class GpuMiner {
   void word_popc(uintptr_t mask, int64_t W, uintptr_t cnt);
   void compact_rows(uintptr_t rows, int64_t R, int64_t Wp_in, uintptr_t mask, uintptr_t nzw,
                     uintptr_t off, int64_t n_nz, uintptr_t out, int64_t Wp_out);
+  // Context-parallel pair rows (parallel/pairs.py "ring"), native: X = this rank's [F][Ws]
+  // transaction-shard bitmaps; rank r keeps its owned rows [r0, r1) of the pair-support matrix
+  // (row_block) while the shards rotate around the ring through comm.sendrecv on a side stream,
+  // block k counted on the miner's stream while block k+1 travels.  out[r1 - r0][ldo] (zeroed
+  // here) = the owned rows summed over every shard.  Two shard copies of arena scratch.
+  void ring_pair_rows(Comm* comm, uintptr_t X, int64_t F, int64_t Ws, uintptr_t out, int64_t ldo);
   // C[Fa][ldc] += popcount(A_i & B_j) over Wp words (ring-pass pair counting)
   void bitgemm_rect(uintptr_t A, int64_t Fa, uintptr_t B, int64_t Fb, int64_t Wp, uintptr_t C,
                     int64_t ldc);

@@ -379,6 +379,18 @@ class DistMiner:
             return int(tot.item())
         return int(self._last_global)
 
+    def _native_comm(self):
+        """This rank's native communicator for the pair ring (created once; RCCL on an nccl
+        process group, the host shared-memory backend otherwise)."""
+        if getattr(self, "_ncomm", None) is None:
+            N = native.require_gpu()
+            backend = comm_backend()
+            make_uid = N.host_comm_unique_id if backend == "host" else N.comm_unique_id
+            uid = [make_uid() if self.rank == 0 else b"\0" * 128]
+            dist.broadcast_object_list(uid, src=0)
+            self._ncomm = N.Comm(self.rank, self.world, uid[0], self.device, backend)
+        return self._ncomm
+
     def pair_rows(self, mode: str = "reduce_scatter"):
         """Pairs-only step (``RULES_MODE=pairs``: the reference's rule map is the pair-support
         matrix): tx-sharded supports + all-reduce, selection, shard bitmaps, then one of the
@@ -396,7 +408,10 @@ class DistMiner:
             F, ids, fcounts, minsup = ops.select(host_counts, self.n_tx, self.min_support)
             ops.sel = (ids, fcounts, minsup)
             X = ops.encode(F, self.ts // 64)
-            r0, r1, rows = PairCounter(getattr(ops, "g", None)).count(X, mode)
+            comm = None
+            if mode == "ring" and self.backend == "gpu" and self.world > 1:
+                comm = self._native_comm()
+            r0, r1, rows = PairCounter(getattr(ops, "g", None), comm).count(X, mode)
             if hasattr(rows, "cpu"):
                 rows = rows.cpu()
         return ids, r0, r1, np.asarray(rows)

@@ -14,7 +14,9 @@ words of its shard for every frequent item), four strategies produce G:
 * ``ring``           — context-parallel / ring-attention analog: rank r keeps its owned rows
   resident ("Q stays") while the transaction blocks X_j rotate around the ring ("KV rotates")
   with send/recv; step k computes G[S_r, :] += X_j[S_r]·X_jᵀ on the matrix engine of rank r
-  while X_j travels on to the next rank.  Peak memory is two blocks instead of N.
+  while X_j travels on to the next rank.  Peak memory is two blocks instead of N.  With a native
+  communicator the whole pass runs in C++ (``GpuMiner.ring_pair_rows``: RCCL / host sendrecv on
+  a side stream, events ordering it against the bit-GEMM on the miner's stream).
 
 Every strategy returns the same thing: ``(row0, row1, rows)`` with ``rows[i][j]`` = support of
 items (row0+i, j) — the symmetric count matrix, diagonal = item supports.  GPU ranks use the
@@ -56,8 +58,9 @@ class PairCounter:
     """Runs one strategy on a rank.  ``miner``: the rank's ``_native.GpuMiner`` (its stream must
     be torch's current stream — see DistMiner's protocol ops) or None for the CPU backend."""
 
-    def __init__(self, miner=None):
+    def __init__(self, miner=None, comm=None):
         self.g = miner
+        self.comm = comm  # native Comm (RCCL / host): the ring runs in C++ on a side stream
 
     def _rect(self, a, b, out=None):
         """out[i][j] += popcount(a_i & b_j); returns out."""
@@ -100,6 +103,12 @@ class PairCounter:
         # ring: owned rows stay, transaction blocks rotate
         acc = torch.zeros((fb, F), dtype=torch.int32 if self.g is not None else torch.int64,
                           device=X.device)
+        if self.g is not None and self.comm is not None:
+            # native (GpuMiner::ring_pair_rows): sendrecv of block k+1 on the communicator's
+            # stream overlapped with block k's bit-GEMM on the miner's stream
+            X = X.contiguous()
+            self.g.ring_pair_rows(self.comm, X.data_ptr(), F, X.shape[1], acc.data_ptr(), F)
+            return r0, r1, acc[: r1 - r0]
         cur = X.contiguous()
         nxt = torch.empty_like(cur)
         for k in range(world):

@@ -113,3 +113,45 @@ def test_txdp_through_a_one_rank_rccl_communicator(shape):
     N = native.load()
     ref = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
     assert d == N.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])["digest"]
+
+
+def _pair_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), KMLS_COMM="host", KMLS_COMM_TIMEOUT_S="120")
+    import torch.distributed as dist
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tx, ms = _data("ds1")
+        dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, ms, device=0, mode="item")
+        got = {}
+        for mode in ("reduce_scatter", "ring", "ring"):  # the second ring reuses stream/events
+            ids, r0, r1, rows = dm.pair_rows(mode)
+            got.setdefault(mode, []).append((r0, r1, np.asarray(rows, np.int64)))
+        out_q.put((rank, got, dm._ncomm.backend if getattr(dm, "_ncomm", None) else None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_ring_pair_rows_on_one_gpu(world):
+    """The context-parallel pair ring in C++ (GpuMiner.ring_pair_rows: shards rotating through
+    the native communicator's sendrecv on a side stream) equals the reduce-scatter strategy row
+    block for row block, on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pair_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got, backend in res:
+        assert backend == "host"
+        r0, r1, ref = got["reduce_scatter"][0]
+        assert ref.sum() > 0
+        for a0, a1, rows in got["ring"]:
+            assert (a0, a1) == (r0, r1)
+            np.testing.assert_array_equal(rows, ref)
