@@ -285,6 +285,10 @@ void register_gpu_bindings(py::module_& m) {
         py::gil_scoped_release nogil;
         return g.select(counts.data(), n_tx, ms);
       })
+      .def("use_frequent_subset", [](gpu::GpuMiner& g, I64 keep) {
+        py::gil_scoped_release nogil;
+        g.use_frequent_subset(keep.data(), (int64_t)keep.size());
+      }, py::arg("keep"))
       .def("frequent", [](const gpu::GpuMiner& g) {
         auto& f = g.frequent();
         return py::make_tuple(to_array(std::vector<int32_t>(f.ids)),

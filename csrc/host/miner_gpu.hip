@@ -918,6 +918,8 @@ int64_t GpuMiner::select_device(const uint32_t* d_counts, int64_t global_n_tx, d
   for (int64_t r = 0; r < F; ++r) fi_.rank_of[(size_t)fi_.ids[(size_t)r]] = (int32_t)r;
   fi_.minsup2 = level2_threshold((uint64_t)global_n_tx, min_support);
   build_encode_tables(F);
+  sel_ids_ = fi_.ids;
+  sel_counts_ = fi_.counts;
   return F;
 }
 
@@ -967,7 +969,30 @@ int64_t GpuMiner::select(const uint32_t* global_counts, int64_t global_n_tx, dou
                             hipMemcpyHostToDevice, s));
   KMLS_HIP(hipStreamSynchronize(s));
   build_encode_tables((int64_t)fi_.ids.size());
+  sel_ids_ = fi_.ids;
+  sel_counts_ = fi_.counts;
   return (int64_t)fi_.ids.size();
+}
+
+void GpuMiner::use_frequent_subset(const int64_t* keep, int64_t n) {
+  KMLS_HIP(hipSetDevice(device_));
+  const int64_t F = (int64_t)sel_ids_.size();
+  KMLS_CHECK(n >= 0 && n <= F, "use_frequent_subset: more positions than frequent items");
+  std::vector<int32_t> ids((size_t)n);
+  std::vector<uint32_t> cnt((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    KMLS_CHECK(keep[i] >= 0 && keep[i] < F && (i == 0 || keep[i] > keep[i - 1]),
+               "use_frequent_subset: positions must be ascending and < F");
+    ids[(size_t)i] = sel_ids_[(size_t)keep[i]];
+    cnt[(size_t)i] = sel_counts_[(size_t)keep[i]];
+  }
+  hipStream_t s = (hipStream_t)stream_;
+  KMLS_HIP(hipStreamSynchronize(s));  // a queued kernel may still read d_ids_
+  fi_.ids.swap(ids);
+  fi_.counts.swap(cnt);
+  ++sel_gen_;  // cached per-selection state (cooc stats) no longer applies
+  if (n) KMLS_HIP(hipMemcpyAsync(d_ids_, fi_.ids.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
+  KMLS_HIP(hipStreamSynchronize(s));
 }
 
 int64_t GpuMiner::words_local() const {

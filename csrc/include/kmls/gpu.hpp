@@ -223,6 +223,11 @@ class GpuMiner {
   int64_t select(const uint32_t* global_counts, int64_t global_n_tx, double min_support);
   int64_t select_device(const uint32_t* d_counts, int64_t global_n_tx, double min_support,
                         Comm* comm = nullptr);
+  // Item-sharded rounds (parallel/item_shard.py): make the frequent items at positions keep[]
+  // (ascending, into the last select()'s order) the current set, for mine_bitmaps only — the
+  // encode tables keep the full selection, and the next select() starts over.  Host work is O(n)
+  // against select()'s O(n_items) table rebuild.
+  void use_frequent_subset(const int64_t* keep, int64_t n);
   // Phase C: tid-bitmaps of frequent items for the resident shard, into an external buffer
   // (uint64[F][Wp]) at word offset `word_off` of rows of stride `Wp_total` words.
   int64_t words_local() const;  // padded words for the local shard
@@ -340,6 +345,8 @@ class GpuMiner {
   int64_t* d_tx_ptr_ = nullptr;
   int32_t* d_items_ = nullptr;
   FrequentItems fi_;
+  std::vector<int32_t> sel_ids_;    // the last select()'s ids / counts (use_frequent_subset)
+  std::vector<uint32_t> sel_counts_;
   int64_t global_n_tx_ = 0;
   int32_t* d_rank_of_ = nullptr;
   uint32_t* d_fmask_ = nullptr;  // frequent-item bit mask (large vocabularies, select())

@@ -162,6 +162,12 @@ class _GpuShard:
     def take_rows(self, bm, keep: np.ndarray):
         return bm.index_select(0, torch.from_numpy(keep).to(self.dev)).contiguous()
 
+    def use_subset(self, keep: np.ndarray, want_ids: np.ndarray):
+        self.g.use_frequent_subset(keep)
+        ids, _, _ = self.g.frequent()
+        if not np.array_equal(np.asarray(ids), want_ids):
+            raise RuntimeError("item_shard: the miner's frequent subset does not match the batch")
+
     def all_to_all(self, outs, ins):
         if dist.get_backend() == "nccl":
             dist.all_to_all(outs, ins)
@@ -205,6 +211,9 @@ class _CpuShard:
 
     def take_rows(self, bm, keep: np.ndarray):
         return bm[torch.from_numpy(keep)].contiguous()
+
+    def use_subset(self, keep: np.ndarray, want_ids: np.ndarray):
+        pass  # the host miner takes ids / counts from ops.sel
 
     def all_to_all(self, outs, ins):
         _p2p_all_to_all(outs, ins)
@@ -272,30 +281,29 @@ def step_shard(dm, download: bool = True) -> Dict:
             plans = [sh.plan(m) for m in masks]
             wcs = [_wc(p[2]) for p in plans]
             sends = [sh.compress(own, masks[h], plans[h], wcs[h]) for h in range(world)]
-            recvs = [sh.zeros_rows(len(range(g, F, world)), wcs[rank]) for g in range(world)]
             if world > 1:
+                recvs = [sh.zeros_rows(len(range(g, F, world)), wcs[rank]) for g in range(world)]
                 sh.all_to_all(recvs, sends)
-            else:
+            else:  # one rank: its own compressed rows (no zero-filled receive buffer per round)
                 recvs = sends
             if len(roots) == 0:
                 continue
-            bm = sh.zeros_rows(F, wcs[rank])
-            for g in range(world):
-                bm[g::world] = recvs[g]
+            if world > 1:
+                bm = sh.zeros_rows(F, wcs[rank])
+                for g in range(world):
+                    bm[g::world] = recvs[g]
+            else:
+                bm = recvs[0]
             del sends, recvs
             peak_batch_bytes = max(peak_batch_bytes, sh.nbytes(bm))
             # an item with fewer than minsup transactions inside U is in no frequent itemset of
-            # the batch's classes: mine on the surviving rows only (selected again, so the
-            # miner's frequent order is the global order restricted to them)
+            # the batch's classes: mine on the surviving rows only (the miner's frequent order is
+            # the global order restricted to them)
             keep = np.flatnonzero(sh.row_counts(bm) >= minsup).astype(np.int64)
             sub = sh.take_rows(bm, keep) if len(keep) < F else bm
             del bm
-            hc = np.zeros(dm.n_items, np.uint32)
-            hc[np.asarray(ids)[keep]] = np.asarray(fcounts, np.uint32)[keep]
-            Fk, kids, kcounts, kms = ops.select(hc, dm.n_tx, dm.min_support)
-            if Fk != len(keep) or not np.array_equal(np.asarray(kids), np.asarray(ids)[keep]):
-                raise RuntimeError("item_shard: batch selection does not preserve the order")
-            ops.sel = (kids, kcounts, kms)
+            ops.sel = (np.asarray(ids)[keep], np.asarray(fcounts)[keep], minsup)
+            sh.use_subset(keep, ops.sel[0])
             kept_rows = max(kept_rows, len(keep))
             parts.append((keep, ops.mine(sub, wcs[rank], dm, np.isin(keep, roots).astype(np.uint8),
                                          True, True)))

@@ -132,7 +132,10 @@ def test_shard_mode_equals_single_process(world, shape, ms, max_len):
 
 
 @pytest.mark.gpu
-def test_gpu_compact_rows_kernel():
+@pytest.mark.parametrize("density", ["dense", "sparse", "empty"])
+def test_gpu_compact_rows_kernel(density):
+    """Masks of ~16 bits per word, of a few bits per many words (one output word gathers many
+    input words), and empty."""
     import torch
     from kubernetes_machine_learning_server_amd.ops import native
     from kubernetes_machine_learning_server_amd.parallel.item_shard import compress_np
@@ -144,6 +147,11 @@ def test_gpu_compact_rows_kernel():
     mask = rng.integers(-2**63, 2**63 - 1, size=W, dtype=np.int64)
     mask &= rng.integers(-2**63, 2**63 - 1, size=W, dtype=np.int64)
     mask[::7] = 0
+    if density == "sparse":
+        mask = np.where(rng.random(W) < 0.3, np.int64(1) << rng.integers(0, 63, size=W), 0)
+        mask = mask.astype(np.int64)
+    elif density == "empty":
+        mask[:] = 0
     d_rows = torch.from_numpy(rows).cuda()
     d_mask = torch.from_numpy(mask).cuda()
     cnt = torch.empty(W, dtype=torch.int32, device="cuda")
@@ -154,7 +162,7 @@ def test_gpu_compact_rows_kernel():
     nz = torch.nonzero(c64).flatten()
     off = (torch.cumsum(c64, 0) - c64)[nz].contiguous()
     bits = int(c64.sum())
-    wc = (-(-bits // 64) + 7) // 8 * 8
+    wc = max(8, (-(-bits // 64) + 7) // 8 * 8)
     out = torch.zeros((R, wc), dtype=torch.int64, device="cuda")
     idx = torch.tensor([3, 5, 30], dtype=torch.int32, device="cuda")
     um = torch.empty(W, dtype=torch.int64, device="cuda")
