@@ -12,8 +12,9 @@ the digest of the full trie, ``kmls/digest.hpp``).  Verified: per-size counts an
 the native CPU miner's whole-problem count (``bench/bench_mine.CPU_REF``).
 
 Multi-GPU (``torchrun --nproc-per-node N``, one rank per GPU): **strong scaling** — the SAME
-problem is split over the ranks (rank r mines level-3 tasks t ≡ r mod N; every rank builds the
-deterministic level-2 classes itself), and the per-size counts + digest sums are all-reduced,
+problem is split over the ranks (every rank builds the deterministic level-2 classes itself,
+measures every level-3 task's cost on the device, and takes its share of the cost-ordered snake
+deal), and the per-size counts + digest sums are all-reduced,
 digest xors all-gathered, over RCCL (torch.distributed on the nccl group); every rank ends with
 the whole-problem result and verifies it.  ``value`` = itemsets of the problem ÷ the slowest
 rank's step.
@@ -23,6 +24,11 @@ Secondary fields:
                     the GPU yet): native HTTP front + open-loop native load generator, latency
                     from the scheduled send time, fixed QPS points and the capacity (max QPS with
                     p99 < 5 ms).
+* ``job_full``    — the product path at the headline support (N = 1): ``job.main.run`` end to
+                    end on a reference-schema CSV of the same data (artifacts, the deep engine's
+                    trie of all 1.4e9 itemsets written to ``frequent_itemsets.npz``, rule map,
+                    marker last); wall time, and the written trie's digest (relabelled to the
+                    dataset's ids) equal to the headline digest.
 * ``levelwise_0.05`` — the round-2 headline form (ds1 @0.05 through the level-wise graph path,
                     trie download + device rule map in the step, verified against the CPU miner);
                     at N > 1 one relabelled dataset per rank (weak scaling).
@@ -142,6 +148,7 @@ def main() -> int:
     ap.add_argument("--no-levelwise", action="store_true")
     ap.add_argument("--no-emit", action="store_true", help="skip the materialising headline run")
     ap.add_argument("--no-config2", action="store_true")
+    ap.add_argument("--no-job", action="store_true", help="skip the job at the headline support")
     ap.add_argument("--no-config3", action="store_true")
     ap.add_argument("--cpu", action="store_true",
                     help="CPU tier of the headline (native CPU count miner, gloo): no GPU")
@@ -299,6 +306,15 @@ def main() -> int:
             out["value_emitted"] = e["itemsets_per_s"]
         except Exception as ex:
             out.setdefault("errors", {})["emit"] = repr(ex)[:300]
+        wd.disarm()
+
+    # ---- the product path at the headline support: the job end to end (1 GPU) ----
+    if world == 1 and not args.cpu and not args.no_job:
+        wd.arm("job_full", 420)
+        try:
+            out["job_full"] = bm.run_job_full(tx, args.min_support, h["digest"], h["per_level"])
+        except Exception as ex:
+            out.setdefault("errors", {})["job_full"] = repr(ex)[:300]
         wd.disarm()
 
     # ---- the round-2 headline form (level-wise, trie + rule map in the step) ----

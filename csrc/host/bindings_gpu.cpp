@@ -299,6 +299,8 @@ void register_gpu_bindings(py::module_& m) {
       .def("pair_counts", &gpu::GpuMiner::pair_counts, py::call_guard<py::gil_scoped_release>())
       .def("pair_counts_csr", &gpu::GpuMiner::pair_counts_csr, py::arg("out"), py::arg("ld"),
            py::call_guard<py::gil_scoped_release>())
+      .def("cooc_check", &gpu::GpuMiner::cooc_check, py::call_guard<py::gil_scoped_release>())
+      .def("subset_active", &gpu::GpuMiner::subset_active)
       .def("cooc_preferred", &gpu::GpuMiner::cooc_preferred,
            py::call_guard<py::gil_scoped_release>())
       .def("cooc_stats", [](gpu::GpuMiner& g) {
@@ -526,6 +528,34 @@ void register_gpu_bindings(py::module_& m) {
         d["depth"] = depth;
         return d;
       }, py::arg("n"))
+      .def("deep_arena_trie", [](gpu::GpuMiner& g, int min_depth, int64_t base) {
+        bool item16 = true;
+        int64_t n = 0;
+        {
+          py::gil_scoped_release nogil;
+          n = g.deep_arena_trie(min_depth, base, &item16);
+        }
+        py::array_t<int32_t> parent((py::ssize_t)n);
+        py::array item = item16 ? (py::array)py::array_t<uint16_t>((py::ssize_t)n)
+                                : (py::array)py::array_t<int32_t>((py::ssize_t)n);
+        py::array_t<uint16_t> count((py::ssize_t)n);
+        py::array_t<uint8_t> depth((py::ssize_t)n);
+        int32_t* pp = parent.mutable_data();
+        void* pi = item.mutable_data();
+        uint16_t* pc = count.mutable_data();
+        uint8_t* pd = depth.mutable_data();
+        {
+          py::gil_scoped_release nogil;
+          g.deep_trie_download(pp, pi, pc, pd);
+        }
+        py::dict d;
+        d["parent"] = parent;
+        d["item"] = item;
+        d["count"] = count;
+        d["depth"] = depth;
+        d["n"] = n;
+        return d;
+      }, py::arg("min_depth") = 1, py::arg("base") = 0)
       .def("synchronize", &gpu::GpuMiner::synchronize, py::call_guard<py::gil_scoped_release>());
 
   py::class_<gpu::GpuRuleIndex, std::shared_ptr<gpu::GpuRuleIndex>>(m, "GpuRuleIndex")

@@ -218,5 +218,60 @@ void GpuMiner::deep_arena_download(int64_t n, int64_t* parent, int32_t* item, ui
   }
 }
 
+int64_t GpuMiner::deep_arena_trie(int min_depth, int64_t base, bool* item16) {
+  KMLS_CHECK(deep_ && deep_->arena_used > 0 && deep_->arena_used <= deep_->arena_cap,
+             "deep_arena_trie: no emit-mode mine_deep yet");
+  KMLS_CHECK(n_tx_ < 65536, "deep_arena_trie: supports must fit 16 bits");
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  DeepBufs& b = *deep_;
+  const int64_t n = b.arena_used;
+  const int nd = std::min(b.max_depth + 1, 64);
+  auto dgrow = [&](auto*& p, size_t bytes) {
+    if (p) KMLS_HIP(hipFree(p));
+    p = nullptr;
+    KMLS_HIP(hipMalloc((void**)&p, std::max<size_t>(bytes, 256)));
+  };
+  if (b.t_ids_cap < n) {
+    dgrow(b.t_new_id, (size_t)n * 4);
+    b.t_ids_cap = n;
+  }
+  const size_t tb = kern::deep_trie_scratch_bytes(n, nd);
+  if (b.t_tmp_bytes < tb) {
+    dgrow(b.t_tmp, tb);
+    b.t_tmp_bytes = tb;
+  }
+  const int64_t m = kern::deep_trie_layout(b.n_depth, n, std::max(min_depth, 1), nd, b.t_new_id,
+                                           b.t_tmp, b.t_tmp_bytes, s);
+  KMLS_CHECK(base >= 0 && base + m < ((int64_t)1 << 31),
+             "deep_arena_trie: 2^31 trie nodes (i32 parent ids)");
+  if (b.tr_cap < m) {
+    dgrow(b.t_parent, (size_t)m * 4);
+    dgrow(b.t_item, (size_t)m * 4);
+    dgrow(b.t_count, (size_t)m * 2);
+    dgrow(b.t_depth, (size_t)m);
+    b.tr_cap = m;
+  }
+  b.t_item16 = n_items_ <= 65536;
+  kern::deep_trie_scatter(b.n_parent, b.n_item, b.n_count, b.n_depth, n, b.t_new_id, d_ids_, base,
+                          b.t_parent, b.t_item, b.t_item16, b.t_count, b.t_depth, s);
+  b.t_n = m;
+  if (item16) *item16 = b.t_item16;
+  return m;
+}
+
+void GpuMiner::deep_trie_download(int32_t* parent, void* item, uint16_t* count, uint8_t* depth) {
+  KMLS_CHECK(deep_ && deep_->t_n >= 0, "deep_trie_download: deep_arena_trie first");
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  DeepBufs& b = *deep_;
+  const size_t m = (size_t)b.t_n;
+  KMLS_HIP(hipMemcpyAsync(parent, b.t_parent, m * 4, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipMemcpyAsync(item, b.t_item, m * (b.t_item16 ? 2 : 4), hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipMemcpyAsync(count, b.t_count, m * 2, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipMemcpyAsync(depth, b.t_depth, m, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+}
+
 }  // namespace gpu
 }  // namespace kmls

@@ -26,9 +26,12 @@ DeepBufs::~DeepBufs() {
                   (void*)d_m, (void*)d_off, (void*)d_toff, (void*)d_cost, (void*)d_order,
                   (void*)d_trace, (void*)d_ticks, (void*)n_parent, (void*)n_item,
                   (void*)n_count, (void*)n_depth, (void*)d_node_off, (void*)d_split_q,
-                  (void*)d_split_heap, (void*)d_ocost, (void*)d_otmp})
+                  (void*)d_split_heap, (void*)d_ocost, (void*)d_otmp, (void*)t_new_id,
+                  (void*)t_tmp, (void*)t_parent, (void*)t_item, (void*)t_count, (void*)t_depth,
+                  (void*)d_part, (void*)d_wt})
     if (p) (void)hipFree(p);
   if (h_ctl) (void)hipHostFree(h_ctl);
+  if (h_tot) (void)hipHostFree(h_tot);
 }
 
 void DeepBufsDeleter::operator()(DeepBufs* p) const { delete p; }
@@ -123,14 +126,24 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   if (!b.ctl) {
     KMLS_HIP(hipMalloc((void**)&b.ctl, sizeof(kern::DeepCtl)));
     KMLS_HIP(hipHostMalloc((void**)&b.h_ctl, sizeof(kern::DeepCtl)));
+    KMLS_HIP(hipHostMalloc((void**)&b.h_tot, 4 * sizeof(int64_t)));
     KMLS_HIP(hipMalloc((void**)&b.d_red, 66 * 8));
   }
   if (b.f_cap < F + 1) {
-    int64_t c1 = b.f_cap, c2 = b.f_cap, c3 = b.f_cap;
+    int64_t c1 = b.f_cap, c2 = b.f_cap, c3 = b.f_cap, c4 = b.f_cap, c5 = b.f_cap;
     grow(b.d_m, c1, F + 1);
     grow(b.d_off, c2, F + 1);
     grow(b.d_toff, c3, F + 1);
+    grow(b.d_node_off, c4, F + 1);
+    grow(b.d_wt, c5, F + 1);
+    b.node_off_cap = c4;
     b.f_cap = F + 1;
+  }
+  {
+    const int64_t np = F * kern::deep_root_chunks(F);
+    int64_t c = b.part_cap;
+    grow(b.d_part, c, np);
+    b.part_cap = c;
   }
   KMLS_HIP(hipMemsetAsync(b.ctl, 0, sizeof(kern::DeepCtl), s));
   res.ms_alloc = ms_since(t0);
@@ -140,6 +153,8 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   int64_t n_tasks = 0;
   int64_t n_heavy = 0;  // assign = 1: the queue's prefix of tasks with cost >= presplit_cost
   std::vector<int64_t> split_q, split_heap;  // pre-split layout of the heavy prefix (host)
+  std::vector<int32_t> m;                     // (pre-split only) class sizes and offsets
+  std::vector<int64_t> off, toff;
   int64_t split_tasks = 0, split_bytes = 0;
   if (F >= 2 && in.max_len != 1) {
     const size_t root_blk = (size_t)(W + 1) * (size_t)Fpad * 8;
@@ -156,26 +171,23 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     };
     ensure_root(root_blk, 0);
     kern::deep_transpose(in.bm, in.Wp, F, W, in.W_real, in.d_ids, (uint64_t*)b.root, Fpad, s);
-    kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, b.d_m, nullptr, nullptr,
-                    nullptr, false, s);
-    std::vector<int32_t> m((size_t)F, 0);
-    KMLS_HIP(hipMemcpyAsync(m.data(), b.d_m, (size_t)F * 4, hipMemcpyDeviceToHost, s));
+    // level-2 classes laid out on the device: chunk counts -> class sizes, block / task / node
+    // offsets (prefix sums); one readback of the three totals (T is needed for the task order)
+    KMLS_HIP(hipMemcpyAsync(b.d_wt, wt.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
+    kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, nullptr, b.d_part, nullptr,
+                    nullptr, nullptr, false, s);
+    kern::deep_root_scan(b.d_part, F, b.d_wt, E, (int64_t)root_blk, b.d_m, b.d_off, b.d_toff,
+                         b.d_node_off, s);
+    KMLS_HIP(hipMemcpyAsync(&b.h_tot[0], b.d_off + F, 8, hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipMemcpyAsync(&b.h_tot[1], b.d_toff + F, 8, hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipMemcpyAsync(&b.h_tot[2], b.d_node_off + F, 8, hipMemcpyDeviceToHost, s));
     KMLS_HIP(hipStreamSynchronize(s));
-    std::vector<int64_t> off((size_t)F + 1, 0), toff((size_t)F + 1, 0);
-    int64_t pairs = 0;
-    off[0] = (int64_t)root_blk;
-    for (int64_t i = 0; i < F; ++i) {
-      const int64_t mi = m[(size_t)i];
-      if (mi < 0 || mi > F) throw std::runtime_error("deep_run: bad level-2 class size");
-      pairs += mi;
-      off[(size_t)i + 1] = off[(size_t)i] + (int64_t)(wt[(size_t)i] + 1 + E) * ((mi + 15) / 16 * 16) * 8;
-      toff[(size_t)i + 1] = toff[(size_t)i] + std::max<int64_t>(mi - 1, 0);
-    }
+    const int64_t blk_end = b.h_tot[0], T = b.h_tot[1], pairs = b.h_tot[2];
+    if (pairs < 0 || pairs > F * (F - 1) / 2 || T < 0 || blk_end < (int64_t)root_blk)
+      throw std::runtime_error("deep_run: bad level-2 layout");
     if (rank == 0) res.per_depth[2] = (uint64_t)pairs;
     const bool deeper = in.max_len == 0 || in.max_len >= 3;
-    ensure_root((size_t)off[(size_t)F], root_blk);
-    KMLS_HIP(hipMemcpyAsync(b.d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, s));
-    KMLS_HIP(hipMemcpyAsync(b.d_toff, toff.data(), toff.size() * 8, hipMemcpyHostToDevice, s));
+    ensure_root((size_t)blk_end, root_blk);
     kern::DeepNodes nodes{};
     if (E) {
       // the arena: level-1 nodes (ids = ranks), level-2 nodes (F + node_off[i] + slot), then
@@ -200,17 +212,9 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       } else if (b.arena_used > 0) {
         KMLS_HIP(hipMemsetAsync(b.n_depth, 0, (size_t)std::min(b.arena_used, b.arena_cap), s));
       }
-      int64_t c1 = b.node_off_cap;
-      grow(b.d_node_off, c1, F + 1);
-      b.node_off_cap = c1;
-      std::vector<int64_t> noff((size_t)F + 1, 0);
       std::vector<uint32_t> l1p((size_t)F, 0xffffffffu), l1i((size_t)F);
       std::vector<uint8_t> l1d((size_t)F, 1);
-      for (int64_t i = 0; i < F; ++i) {
-        noff[(size_t)i + 1] = noff[(size_t)i] + m[(size_t)i];
-        l1i[(size_t)i] = (uint32_t)i;
-      }
-      KMLS_HIP(hipMemcpyAsync(b.d_node_off, noff.data(), (size_t)(F + 1) * 8, hipMemcpyHostToDevice, s));
+      for (int64_t i = 0; i < F; ++i) l1i[(size_t)i] = (uint32_t)i;
       KMLS_HIP(hipMemcpyAsync(b.n_parent, l1p.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
       KMLS_HIP(hipMemcpyAsync(b.n_item, l1i.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
       KMLS_HIP(hipMemcpyAsync(b.n_count, in.counts, (size_t)F * 4, hipMemcpyHostToDevice, s));
@@ -220,9 +224,8 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       KMLS_HIP(hipStreamSynchronize(s));  // the pageable staging vectors die at scope end
       nodes = kern::DeepNodes{b.n_parent, b.n_item, b.n_count, b.n_depth, b.d_node_off};
     }
-    kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, b.d_m, b.d_off, b.root,
-                    rank == 0 ? b.ctl : nullptr, true, s, E ? &nodes : nullptr);
-    const int64_t T = toff[(size_t)F];
+    kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, b.d_m, b.d_part, b.d_off,
+                    b.root, rank == 0 ? b.ctl : nullptr, true, s, E ? &nodes : nullptr);
     const int64_t* d_order = nullptr;
     if (deeper && T > 0 && (opt.assign == 1 || opt.trace)) {
       // every task's class size (its level-3 survivors) on the device; tasks ordered largest
@@ -256,6 +259,14 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
           cost.resize((size_t)n_tasks);
           KMLS_HIP(hipMemcpyAsync(mine.data(), b.d_order, (size_t)n_tasks * 8, hipMemcpyDeviceToHost, s));
           KMLS_HIP(hipMemcpyAsync(cost.data(), b.d_ocost, (size_t)n_tasks * 4, hipMemcpyDeviceToHost, s));
+          if (presplit) {  // the heavy tasks' class layout (host pre-split plan below)
+            m.resize((size_t)F);
+            off.resize((size_t)F + 1);
+            toff.resize((size_t)F + 1);
+            KMLS_HIP(hipMemcpyAsync(m.data(), b.d_m, (size_t)F * 4, hipMemcpyDeviceToHost, s));
+            KMLS_HIP(hipMemcpyAsync(off.data(), b.d_off, (size_t)(F + 1) * 8, hipMemcpyDeviceToHost, s));
+            KMLS_HIP(hipMemcpyAsync(toff.data(), b.d_toff, (size_t)(F + 1) * 8, hipMemcpyDeviceToHost, s));
+          }
           KMLS_HIP(hipStreamSynchronize(s));
         }
         // (a rank split only: on one GPU the extra launch costs more than the shorter tail gains,

@@ -37,6 +37,10 @@ struct DeepBufs {
   char* root = nullptr;  // root block + level-2 blocks
   size_t root_bytes = 0;
   int32_t* d_m = nullptr;  // [F] level-2 class sizes
+  int32_t* d_part = nullptr;  // [F][deep_root_chunks(F)] level-2 chunk counts / bases
+  int64_t part_cap = 0;
+  int32_t* d_wt = nullptr;    // [F] projected width tier of each root class
+  int64_t* h_tot = nullptr;   // pinned [4]: layout totals read back once per call
   int64_t* d_off = nullptr;  // [F + 1] block byte offsets
   int64_t* d_toff = nullptr;  // [F + 1] task offsets
   int64_t f_cap = 0;
@@ -54,6 +58,17 @@ struct DeepBufs {
   int64_t arena_cap = 0, arena_used = 0;
   int max_depth = 0;
   int64_t* d_node_off = nullptr;
+  // the arena as a dense trie (GpuMiner::deep_arena_trie): new ids, scratch, narrow outputs
+  uint32_t* t_new_id = nullptr;
+  char* t_tmp = nullptr;
+  size_t t_tmp_bytes = 0;
+  int32_t* t_parent = nullptr;
+  int32_t* t_item = nullptr;     // u16 or i32 items
+  uint16_t* t_count = nullptr;
+  unsigned char* t_depth = nullptr;
+  int64_t tr_cap = 0, t_ids_cap = 0;
+  int64_t t_n = 0;               // nodes of the last layout
+  bool t_item16 = true;
   int64_t* d_split_q = nullptr;   // pre-split layout: queue slot and heap offset per heavy task
   int64_t* d_split_heap = nullptr;
   int64_t split_cap = 0;

@@ -850,9 +850,22 @@ struct HttpFront::Impl {
       int st = -1;
       try {  // a malformed request closes its own connection, never the I/O thread
         st = parse_request(w, c, r);
-        if (st > 0) handle(w, wi, c, r);
       } catch (const std::exception&) {
         st = -1;
+      }
+      if (st > 0) {
+        const size_t out0 = c.out.size();
+        try {
+          handle(w, wi, c, r);
+        } catch (const std::exception&) {
+          // handle() failed after the parse: if it already queued the request (busy) or wrote
+          // its answer, that path owns the connection's response — close without a second one
+          if (c.busy || c.out.size() != out0) {
+            c.close_after = true;
+            break;
+          }
+          st = -1;
+        }
       }
       if (st < 0) {
         c.out += "HTTP/1.1 400 Bad Request\r\ncontent-length: 0\r\nconnection: close\r\n\r\n";

@@ -1049,6 +1049,8 @@ void GpuMiner::pair_counts(uintptr_t bm_dev, int64_t Wp_total, uintptr_t out_dev
 }
 
 GpuMiner::CoocStats GpuMiner::cooc_stats() {
+  KMLS_CHECK(!subset_active(), "cooc_stats: a use_frequent_subset() set is active (rank tables "
+                               "describe the full selection); select() again first");
   if (cooc_gen_ == sel_gen_) return cooc_cache_;  // same CSR and selection: one pass per step
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;
@@ -1071,6 +1073,8 @@ bool GpuMiner::pair_counts_csr(uintptr_t out_dev, int64_t ld) {
   KMLS_HIP(hipSetDevice(device_));
   const int64_t F = (int64_t)fi_.ids.size();
   KMLS_CHECK(ld >= F, "pair_counts_csr: ld >= F");
+  KMLS_CHECK(!subset_active(), "pair_counts_csr: a use_frequent_subset() set is active; "
+                               "select() again first");
   hipStream_t s = (hipStream_t)stream_;
   const CoocStats st = cooc_stats();
   if (st.max_k > (uint64_t)kern::cooc_max_k()) return false;
@@ -1079,6 +1083,18 @@ bool GpuMiner::pair_counts_csr(uintptr_t out_dev, int64_t ld) {
   kern::cooc_count(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, d_fmask_, F, (uint32_t*)out_dev, ld,
                    (unsigned*)(d_cooc_ + 2), n_cus_, s);
   return true;
+}
+
+void GpuMiner::cooc_check() {
+  KMLS_CHECK(d_cooc_ != nullptr, "cooc_check: no horizontal count ran");
+  hipStream_t s = (hipStream_t)stream_;
+  unsigned long long f = 0;
+  KMLS_HIP(hipMemcpyAsync(&f, d_cooc_ + 2, sizeof f, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  KMLS_CHECK(!(f & 1ull), "cooc_count: a transaction held more frequent items than the entry "
+                          "buffer (its pairs were not counted)");
+  KMLS_CHECK(!(f & 2ull), "cooc_count: a transaction holds the same frequent item twice "
+                          "(load_csr requires duplicate-free rows)");
 }
 
 bool GpuMiner::cooc_cheaper(int64_t F, int64_t Wp, int64_t nnz, const CoocStats& st) {
@@ -1126,7 +1142,7 @@ void GpuMiner::txdp_gram_combine(uint32_t* gram, int64_t F, int64_t per, uint32_
 }
 
 bool GpuMiner::cooc_preferred() {
-  if (words_local() < 1024 || fi_.ids.empty()) return false;
+  if (words_local() < 1024 || fi_.ids.empty() || subset_active()) return false;
   const long long h = test_hook("cooc", 1);
   if (h == 0) return false;
   const CoocStats st = cooc_stats();
@@ -1139,6 +1155,8 @@ GpuMiner::RuleMap GpuMiner::rule_map_from_gram(uintptr_t gram_dev, int64_t ld, u
   hipStream_t s = (hipStream_t)stream_;
   const int64_t F = (int64_t)fi_.ids.size();
   KMLS_CHECK(F > 0 && ld >= F, "rule_map_from_gram: select() first, ld >= F");
+  KMLS_CHECK(!subset_active(), "rule_map_from_gram: a use_frequent_subset() set is active; "
+                               "select() again first");
   if (!big_lds_) {
     kern::pairs_enable_big_lds();
     big_lds_ = true;
@@ -1493,6 +1511,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     res.levels_path = done ? "fused" : (comm_ ? "chunked-txdp" : "chunked");
     if (!done && !run.fallback_reason.empty()) res.levels_path += " (fused fallback: " + run.fallback_reason + ")";
     KMLS_HIP(hipStreamSynchronize(s));  // host staging vectors die at scope end
+    if (res.level2_method == "cooc") cooc_check();
   } else {
     KMLS_HIP(hipEventRecord(e1.e, s));
   }
@@ -1503,6 +1522,9 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
   const int64_t N = run.out_size;
   res.n_nodes = N;
   last_nodes_ = N;
+  // the overflow hint is a high-water mark of one (earlier, larger) problem: a call that fit
+  // with 8x room to spare releases it, so later small calls stop sizing for that one
+  if (run.need_nodes == 0 && N < (fused_need_ >> 3)) fused_need_ = 0;
   if (download && run.stream_dl) {
     run.stream_out();  // tail (normally empty: every chunk streamed itself)
   } else if (download) {  // the trie outgrew the pinned arrays: one full copy
@@ -1949,6 +1971,9 @@ bool GpuMiner::mine_resident(const MineConfig& cfg, bool download, GpuMineResult
   const int64_t N = run.out_size;
   res.n_nodes = N;
   last_nodes_ = N;
+  // the overflow hint is a high-water mark of one (earlier, larger) problem: a call that fit
+  // with 8x room to spare releases it, so later small calls stop sizing for that one
+  if (run.need_nodes == 0 && N < (fused_need_ >> 3)) fused_need_ = 0;
   if (download && !run.stream_dl) {
     KMLS_HIP(hipStreamSynchronize(out_->copy_s));
     res.par_w = 8;

@@ -228,6 +228,10 @@ class GpuMiner {
   // encode tables keep the full selection, and the next select() starts over.  Host work is O(n)
   // against select()'s O(n_items) table rebuild.
   void use_frequent_subset(const int64_t* keep, int64_t n);
+  // a use_frequent_subset() set is current: d_rank_of_ / d_fmask_ / the encode tables still
+  // describe the full selection, so the CSR-driven methods (cooc_*, pair_counts_csr,
+  // rule_map_from_gram) would index past an F-row gram; they refuse while this holds
+  bool subset_active() const { return fi_.ids.size() != sel_ids_.size(); }
   // Phase C: tid-bitmaps of frequent items for the resident shard, into an external buffer
   // (uint64[F][Wp]) at word offset `word_off` of rows of stride `Wp_total` words.
   int64_t words_local() const;  // padded words for the local shard
@@ -272,6 +276,14 @@ class GpuMiner {
   ArenaDigest deep_arena_digest(int min_depth);
   void deep_arena_download(int64_t n, int64_t* parent, int32_t* item, uint32_t* count,
                            uint8_t* depth);
+  // The arena of the last mine_deep(emit) as a dense trie whose parents come first (the product
+  // output: kern::deep_trie_*), built on the device.  Nodes of size >= min_depth (a rank > 0 of
+  // a split: 3, its share); their parents are new ids + `base` when exported, else their arena
+  // id (levels 1-2: the same on every rank, and their ids in rank 0's export).  Returns the node
+  // count; deep_trie_download copies the narrow arrays (parent i32, item u16 when item16 else
+  // i32, support u16, size u8) to host memory.
+  int64_t deep_arena_trie(int min_depth, int64_t base, bool* item16);
+  void deep_trie_download(int32_t* parent, void* item, uint16_t* count, uint8_t* depth);
 
   // Frequent items of the last select(): ids (ascending support) and counts.
   const FrequentItems& frequent() const { return fi_; }
@@ -289,6 +301,10 @@ class GpuMiner {
   };
   CoocStats cooc_stats();
   bool pair_counts_csr(uintptr_t out_dev, int64_t ld);
+  // after a pair_counts_csr on the stream: synchronises and throws if the count kernel met a
+  // transaction with more frequent items than its entry buffer (pairs would be missing) or a
+  // row holding one frequent item twice (load_csr's duplicate-free precondition broken)
+  void cooc_check();
   // level-2 cost model: the horizontal count is predicted cheaper than the bit-GEMM over Wp words
   static bool cooc_cheaper(int64_t F, int64_t Wp, int64_t nnz, const CoocStats& st);
   // the model applied to this shard and the last select() (one stats pass; false below 64k tx)

@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void k_cooc_stats(const int64_t* __restrict__ 
 // the wave (pair -> transaction by a binary search of L.poff, (i, j) by inverting the triangle)
 __device__ __forceinline__ void chunk_pairs(ChunkLds& L, unsigned nx, unsigned P, int head0,
                                             uint32_t* head, uint32_t* __restrict__ gram,
-                                            int64_t ld, int lane) {
+                                            int64_t ld, unsigned* __restrict__ err, int lane) {
   for (unsigned p0 = 0; p0 < P; p0 += 64) {
     const unsigned p = p0 + lane;
     if (p < P) {
@@ -179,7 +179,9 @@ __device__ __forceinline__ void chunk_pairs(ChunkLds& L, unsigned nx, unsigned P
       const unsigned j = (unsigned)i + 1u + (qq - (unsigned)(i * (2 * (int)kk - 1 - i) / 2));
       const int ra = L.ent[e0 + (unsigned)i], rb = L.ent[e0 + j];
       const int lo = ra < rb ? ra : rb, hi = ra < rb ? rb : ra;
-      if (lo >= head0)
+      if (lo == hi)  // a duplicated item (rows must be duplicate-free): flag, count nothing
+        atomicOr(err, 2u);
+      else if (lo >= head0)
         atomicAdd(&head[(lo - head0) * kHead + (hi - head0)], 1u);
       else
         atomicAdd(&gram[(int64_t)lo * ld + hi], 1u);
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256) void k_cooc_count(const int64_t* __restrict__ 
         L.poff[n] = P;
       }
       __builtin_amdgcn_wave_barrier();
-      chunk_pairs(L, n, P, head0, head, gram, ld, lane);
+      chunk_pairs(L, n, P, head0, head, gram, ld, err, lane);
       continue;
     }
     // more entries than fit (long transactions): sub-chunks of lanes whose entries fit, each
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(256) void k_cooc_count(const int64_t* __restrict__ 
         L.toff[n_sub] = last - base;
       }
       __builtin_amdgcn_wave_barrier();
-      chunk_pairs(L, n_sub, P, head0, head, gram, ld, lane);
+      chunk_pairs(L, n_sub, P, head0, head, gram, ld, err, lane);
       base = last;
       l0 = l1;
     }

@@ -46,6 +46,7 @@ namespace kern {
 namespace {
 
 constexpr int kWaves = 4;            // independent waves per workgroup
+constexpr int kRootChunk = 256;      // level-2 candidates per wave of k_deep_root
 constexpr int kCap = 512;            // candidate pairs per batch step (256: 42.7 ms, 512: 39.6, 1024 with 16-bit group fields: 43.9 at ds1 @0.02)
 constexpr int kBatchFrames = 64;     // frames one batch step may take
 constexpr int kBStack = 96;          // blocks on one wave's memory stack
@@ -1038,40 +1039,55 @@ __global__ void k_deep_transpose(const unsigned long long* bm, long long Wp, lon
   root[e] = v;
 }
 
-// one wave per root item i: its frequent pairs with every later item j (lane = candidate);
-// fill == false: count only (m[i]); fill == true: write block i (slots in j order), projected
-// onto row i (the block's width comes from its byte size: blk_off[i+1] - blk_off[i]) and, when
-// ctl != nullptr, add the level-2 digest terms
+// one wave per (root item i, chunk c of kRootChunk later items j) (lane = candidate): the
+// level-2 class of i is counted / filled by ceil((F-1-i) / kRootChunk) waves instead of one, so
+// the first classes (F-1 candidates) no longer set the launch's length (one wave per class:
+// 144 + 339 us for the two passes at F = 2032, profiles/r4r_ktrace_headline.md).
+// fill == false: count only, part[i * maxch + c] = the chunk's survivors;
+// fill == true: part holds the chunk's exclusive base inside the class (k_deep_root_scan), block i
+// (slots in j order) is written, projected onto row i (the block's width comes from its byte
+// size: blk_off[i+1] - blk_off[i]) and, when ctl != nullptr, the level-2 digest terms added
 template <int WT>
 __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* root, long long Fpad,
-                                                   long long F, unsigned minsup, int32_t* m_out,
+                                                   long long F, int maxch, unsigned minsup,
+                                                   const int32_t* m_in, int32_t* part,
                                                    const long long* blk_off, char* base,
                                                    DeepCtl* ctl, int fill, DeepNodes nodes) {
   __shared__ ProjLds<WT> projs[kWaves];
   const int lane = threadIdx.x & 63;
-  const long long i = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const long long gw = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const long long i = gw / maxch;
+  const long long ch = gw - i * maxch;
   if (i >= F) return;  // wave-uniform
+  const long long nc = F - 1 - i;
+  const long long cbeg = ch * kRootChunk;
+  if (cbeg >= nc) {  // wave-uniform: past the class's candidates (an empty chunk)
+    if (!fill && lane == 0) part[gw] = 0;
+    return;
+  }
+  const long long cend = cbeg + kRootChunk < nc ? cbeg + kRootChunk : nc;
   ProjLds<WT>& PL = projs[threadIdx.x >> 6];
   const unsigned long long* ihp = root + (unsigned long long)WT * Fpad;
   const unsigned long long h_a = ihp[i];
-  const long long nc = F - 1 - i;
   unsigned long long* cb = nullptr;
   unsigned long long cpad = 0;
   unsigned wt_out = WT;
+  unsigned S = 0;
   const unsigned E = nodes.parent != nullptr;  // emit mode: node-word row + level-2 nodes
   if (fill) {
-    cpad = roundup16((unsigned long long)m_out[i]);
+    cpad = roundup16((unsigned long long)m_in[i]);
     if (cpad == 0) return;  // wave-uniform: no frequent pair
+    S = (unsigned)part[gw];  // this chunk's first slot
     cb = (unsigned long long*)(base + blk_off[i]);
     wt_out = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * cpad)) - 1u - E;
     if (wt_out < (unsigned)WT) proj_setup<WT>(PL, root, (unsigned long long)Fpad, (unsigned)i, lane);
   }
   const bool proj = wt_out < (unsigned)WT;
-  unsigned S = 0;
+  const unsigned S0 = S;
   unsigned long long dsum = 0, dxor = 0;
   const unsigned long long lanelt = (1ull << lane) - 1ull;
-  for (long long c0 = 0; c0 < nc; c0 += 64) {
-    const bool act = c0 + lane < nc;
+  for (long long c0 = cbeg; c0 < cend; c0 += 64) {
+    const bool act = c0 + lane < cend;
     const long long jb = act ? i + 1 + c0 + lane : i;
     unsigned long long v[WT];
     const unsigned c = and_count<WT>(root, (unsigned long long)Fpad, (unsigned)i + vzero(), (unsigned)jb, v);
@@ -1101,7 +1117,7 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
     S += (unsigned)__popcll(mask);
   }
   if (!fill) {
-    if (lane == 0) m_out[i] = (int32_t)S;
+    if (lane == 0) part[gw] = (int32_t)S;
     return;
   }
   if (ctl) {
@@ -1109,11 +1125,76 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
       dsum += shfl_xor64(dsum, off);
       dxor ^= shfl_xor64(dxor, off);
     }
-    if (lane == 0 && S) {
+    if (lane == 0 && S > S0) {
       atomicAdd(&ctl->digest_sum, dsum);
       atomicXor(&ctl->digest_xor, dxor);
     }
   }
+}
+
+// one wave: inclusive prefix sums of three int64 arrays of n entries, in place (the level-2
+// layout: block byte offsets, task offsets, node ids; n = F + 1, a few thousand)
+__global__ __launch_bounds__(64) void k_deep_prefix3(long long* a, long long* b, long long* c,
+                                                     long long n) {
+  __shared__ long long sh[3][64];
+  const int t = threadIdx.x & 63;
+  const long long per = (n + 63) / 64;
+  const long long lo = (long long)t * per;
+  const long long hi = lo + per < n ? lo + per : n;
+  long long sa = 0, sb = 0, sc = 0;
+  for (long long k = lo; k < hi; ++k) {
+    sa += a[k];
+    sb += b[k];
+    sc += c[k];
+  }
+  sh[0][t] = sa;
+  sh[1][t] = sb;
+  sh[2][t] = sc;
+  __builtin_amdgcn_wave_barrier();
+  if (t < 3) {  // exclusive scan of the 64 partials of one array
+    long long run = 0;
+    for (int q = 0; q < 64; ++q) {
+      const long long v = sh[t][q];
+      sh[t][q] = run;
+      run += v;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  long long ra = sh[0][t], rb = sh[1][t], rc = sh[2][t];
+  for (long long k = lo; k < hi; ++k) {
+    ra += a[k];
+    a[k] = ra;
+    rb += b[k];
+    b[k] = rb;
+    rc += c[k];
+    c[k] = rc;
+  }
+}
+
+// per root class i (thread): the chunk counts of the count pass -> exclusive chunk bases (in
+// place), m[i], and the three per-class sizes whose prefix sums lay out the level-2 blocks (byte
+// offsets from the class's projected width tier wt[i]), the level-3 tasks and (emit) the level-2
+// node ids: sz[k][i + 1] (sz[k][0] = the first offset: root block bytes / 0 / 0)
+__global__ void k_deep_root_scan(int32_t* part, int maxch, long long F, const int32_t* wt,
+                                 unsigned extra, long long root_blk, int32_t* m,
+                                 long long* sz_blk, long long* sz_task, long long* sz_node) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    sz_blk[0] = root_blk;
+    sz_task[0] = 0;
+    sz_node[0] = 0;
+  }
+  if (i >= F) return;
+  int32_t tot = 0;
+  for (int c = 0; c < maxch; ++c) {
+    const int32_t v = part[i * maxch + c];
+    part[i * maxch + c] = tot;
+    tot += v;
+  }
+  m[i] = tot;
+  sz_blk[i + 1] = (long long)(wt[i] + 1 + (int)extra) * (long long)roundup16((unsigned long long)tot) * 8;
+  sz_task[i + 1] = tot > 1 ? tot - 1 : 0;
+  sz_node[i + 1] = tot;
 }
 
 // this rank's level-3 tasks: out[q] = task order[q] (order == nullptr: task q*world + rank, the
@@ -1266,18 +1347,31 @@ void deep_transpose(const uint64_t* bm, int64_t Wp, int64_t F, int W, int W_real
                      (unsigned long long*)root, (long long)Fpad);
 }
 
+int deep_root_chunks(int64_t F) { return (int)std::max<int64_t>(1, (F - 1 + kRootChunk - 1) / kRootChunk); }
+
 void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t minsup,
-               int32_t* m, const int64_t* blk_off, char* base, DeepCtl* ctl, bool fill,
-               hipStream_t s, const DeepNodes* nodes) {
-  const unsigned grid = (unsigned)((F + 3) / 4);
-  if (!grid) return;
+               const int32_t* m, int32_t* part, const int64_t* blk_off, char* base, DeepCtl* ctl,
+               bool fill, hipStream_t s, const DeepNodes* nodes) {
+  if (F <= 0) return;
+  const int maxch = deep_root_chunks(F);
+  const unsigned grid = (unsigned)((F * maxch + kWaves - 1) / kWaves);
   DeepNodes nd{};
   if (nodes && fill) nd = *nodes;
   by_tier(W, [&](auto wt) {
-    hipLaunchKernelGGL(k_deep_root<decltype(wt)::value>, dim3(grid), dim3(256), 0, s,
-                       (const unsigned long long*)root, (long long)Fpad, (long long)F, minsup,
-                       m, (const long long*)blk_off, base, ctl, fill ? 1 : 0, nd);
+    hipLaunchKernelGGL(k_deep_root<decltype(wt)::value>, dim3(grid), dim3(64 * kWaves), 0, s,
+                       (const unsigned long long*)root, (long long)Fpad, (long long)F, maxch,
+                       minsup, m, part, (const long long*)blk_off, base, ctl, fill ? 1 : 0, nd);
   });
+}
+
+void deep_root_scan(int32_t* part, int64_t F, const int32_t* wt, int extra, int64_t root_blk,
+                    int32_t* m, int64_t* off, int64_t* task_off, int64_t* node_off, hipStream_t s) {
+  if (F <= 0) return;
+  hipLaunchKernelGGL(k_deep_root_scan, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, s, part,
+                     deep_root_chunks(F), (long long)F, wt, (unsigned)extra, (long long)root_blk,
+                     m, (long long*)off, (long long*)task_off, (long long*)node_off);
+  hipLaunchKernelGGL(k_deep_prefix3, dim3(1), dim3(64), 0, s, (long long*)off,
+                     (long long*)task_off, (long long*)node_off, (long long)(F + 1));
 }
 
 void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,

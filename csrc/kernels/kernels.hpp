@@ -107,9 +107,17 @@ struct DeepNodes {
   unsigned char* depth;
   const int64_t* node_off;  // [F] level-2 node base of root class i
 };
+// (chunked: one wave per (class, 256 candidates); part = [F][deep_root_chunks(F)] int32)
+// count pass (fill = false): part = per-chunk survivors; deep_root_scan turns them into chunk
+// bases and lays the classes out on the device: m[i], off[0..F] (block byte offsets, off[0] =
+// root_blk), task_off[0..F], node_off[0..F] (prefix sums, no host round trip); the fill pass
+// then writes every block at off[i] (m = the scanned sizes)
+int deep_root_chunks(int64_t F);
 void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t minsup,
-               int32_t* m, const int64_t* blk_off, char* base, DeepCtl* ctl, bool fill,
-               hipStream_t s, const DeepNodes* nodes = nullptr);
+               const int32_t* m, int32_t* part, const int64_t* blk_off, char* base, DeepCtl* ctl,
+               bool fill, hipStream_t s, const DeepNodes* nodes = nullptr);
+void deep_root_scan(int32_t* part, int64_t F, const int32_t* wt, int extra, int64_t root_blk,
+                    int32_t* m, int64_t* off, int64_t* task_off, int64_t* node_off, hipStream_t s);
 // emit-mode verification: digest terms and per-size counts of the node arena (ids [0, n)) for
 // sizes >= min_depth, set hashes built size by size (hash = parent's + item_mix(ids[item]));
 // out = [sum, xor, per_depth[64]] accumulated; hash = scratch [n] u64
@@ -132,6 +140,17 @@ int64_t deep_task_share(int64_t T, int rank, int world);
 size_t deep_task_order_bytes(int64_t T);
 int64_t deep_task_order(const uint32_t* cost, int64_t T, int rank, int world, void* tmp,
                         size_t tmp_bytes, int64_t* order, uint32_t* order_cost, hipStream_t s);
+// (deep_trie.hip) emit arena -> dense trie, parents first: new_id[i] for every arena id of size
+// in [min_depth, nd) (size-major, arena order inside a size; others kNone), returns the node
+// count (synchronises); then the scatter writes the trie at new_id (parent remapped, + base for
+// exported parents, arena id kept for parents below min_depth; item rank -> ids[rank])
+size_t deep_trie_scratch_bytes(int64_t n, int nd);
+int64_t deep_trie_layout(const unsigned char* depth, int64_t n, int min_depth, int nd,
+                         uint32_t* new_id, void* tmp, size_t tmp_bytes, hipStream_t s);
+void deep_trie_scatter(const unsigned* parent, const unsigned* item, const unsigned* count,
+                       const unsigned char* depth, int64_t n, const uint32_t* new_id,
+                       const int32_t* ids, int64_t base, int32_t* o_parent, void* o_item,
+                       bool item16, uint16_t* o_count, unsigned char* o_depth, hipStream_t s);
 
 // ---- mining (mine.hip) ----
 void item_support(const int32_t* items, int64_t nnz, int32_t n_items, uint32_t* counts,

@@ -464,3 +464,73 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
             os.environ.pop("KMLS_COMM", None)
         else:
             os.environ["KMLS_COMM"] = prev
+
+
+def run_job_full(tx, ms: float, want_digest: Optional[str] = None,
+                 want_per_level=None) -> Dict:
+    """The PRODUCT path at the headline support: the job (``job.main.run``, MINER=gpu,
+    RULES_MODE=full) on a reference-schema CSV of this dataset — CSV ingest, pre-processing
+    artifacts, every frequent itemset through the deep engine (emit -> device trie compaction
+    -> host), the device rule map, ``recommendations.pickle`` / ``rules.idx`` and the
+    1.4e9-itemset ``frequent_itemsets.npz``, marker last (machine-learning/main.py:421-484).
+    Track names are made unique (``name #id``) so the job's name codes map back to this
+    dataset's item ids: the written trie, relabelled, must carry the headline's digest."""
+    import dataclasses
+    import shutil
+    import tempfile
+    from ..config import JobSettings
+    from ..data.synthetic import to_reference_csv
+    from ..job import main as job
+    from ..ops import native
+    N = native.load()
+    root = tempfile.mkdtemp(prefix="kmls_job_full_")
+    try:
+        names = [f"{n} #{i:05d}" for i, n in enumerate(tx.names or [f"t{i}" for i in range(tx.n_items)])]
+        ds = os.path.join(root, "datasets")
+        os.makedirs(ds)
+        to_reference_csv(dataclasses.replace(tx, names=names), os.path.join(ds, "2023_spotify_ds1.csv"))
+        import pathlib
+        base = pathlib.Path(root) / "api-data"
+        cfg = JobSettings(min_support=ms, base_dir=base, datasets_dir=pathlib.Path(ds),
+                          pickles_folder=base / "pickles",
+                          recommendations_file="recommendations.pickle",
+                          best_tracks_file="best_tracks.pickle",
+                          data_invalidation_file="last_execution.txt",
+                          regex_filename="2023_spotify_ds*.csv", top_tracks_save_percentile=0.03,
+                          miner="gpu", rules_mode="full")
+        t0 = time.perf_counter()
+        st = job.run(cfg)
+        wall = time.perf_counter() - t0
+        npz = base / "pickles" / "frequent_itemsets.npz"
+        out = {"min_support": ms, "wall_s": round(wall, 2), "rule_seconds": round(st["rule_seconds"], 3),
+               "n_itemsets": int(st["n_itemsets"]), "backend": st.get("backend"),
+               "rule_map": st.get("rule_map"), "n_keys": int(st["n_keys"]),
+               "npz_bytes": npz.stat().st_size,
+               "what": "job.main.run end to end: CSV -> artifacts -> deep-engine trie -> npz, "
+                       "marker last"}
+        t1 = time.perf_counter()
+        z = np.load(npz)
+        par, item, cnt, dep = z["parent"], z["item"], z["count"], z["depth"]
+        # job name code -> dataset item id (the "#id" suffix), then the content digest
+        code_names = job_names(cfg)
+        back = np.array([int(n.rsplit("#", 1)[1]) for n in code_names], dtype=np.int32)
+        d = N.trie_digest(par, back[item.astype(np.int64)], cnt, dep)
+        out["verify_s"] = round(time.perf_counter() - t1, 2)
+        out["digest"] = d["digest"]
+        out["per_level"] = [int(v) for v in d["per_depth"][1:]]
+        if want_digest is not None:
+            out["verified_digest"] = d["digest"] == want_digest
+        if want_per_level is not None:
+            out["per_level_equal_headline"] = out["per_level"] == [int(v) for v in want_per_level[1:]]
+        return out
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
+def job_names(cfg) -> list:
+    """The job's item-code -> track-name table for its (single) dataset: the same CSV read,
+    cleaning and group-by as the job."""
+    from ..job import preprocess as pp
+    path = sorted(cfg.datasets_dir.glob(cfg.regex_filename))[0]
+    t = pp.clean_df(pp.read_tracks(str(path), 1.0, verbose=False))
+    return list(pp.group_tracks_by_playlist(t).names)

@@ -40,14 +40,16 @@ class JobSettings:
     # RULES_MODE=pairs on several GPUs: how the pair matrix is formed (parallel/pairs.py:
     # allreduce | reduce_scatter | alltoall | ring), or "trie" (mine 2-itemsets, gather sub-tries)
     pairs_strategy: str = "reduce_scatter"
-    dist_mode: str = "auto"      # KMLS_DIST_MODE: auto | tx | item | shard | replicate (multi-GPU mining)
+    # KMLS_DIST_MODE: auto | deep | tx | item | shard | replicate (multi-GPU mining); auto = deep
+    # (the headline DFS split, parallel/deep.py) for GPU full mining of <= 4096 transactions
+    dist_mode: str = "auto"
     num_gpus: int = 1
     min_confidence: float = 0.04  # legacy confidence rules (main.py:227)
     checkpoint_dir: Optional[pathlib.Path] = None  # KMLS_CHECKPOINT_DIR: phase resume
     dist_timeout_s: float = 600.0      # KMLS_DIST_TIMEOUT_S: process-group init + collectives
     sweep_timeout_s: float = 86400.0   # KMLS_SWEEP_TIMEOUT_S: ranks waiting for rank 0's sweep
 
-    DIST_MODES = ("auto", "tx", "item", "shard", "replicate")
+    DIST_MODES = ("auto", "deep", "tx", "item", "shard", "replicate")
 
     def __post_init__(self):
         # 'local' (every rank mines the whole dataset) is a DistMiner test mode: in the job it

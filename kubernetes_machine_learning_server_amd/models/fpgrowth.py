@@ -7,7 +7,8 @@
 :class:`ItemsetTrie` — the compact form every miner emits (node = parent itemset + one item,
 with its support count) — and materialised to the mlxtend DataFrame only on request.
 
-Backends: ``"gpu"`` (HIP kernels, csrc/kernels/mine.hip), ``"cpu"`` (C++ bitmap Eclat,
+Backends: ``"gpu"`` (HIP kernels: the deep DFS miner, csrc/kernels/deep.hip, for short
+transaction sets; the level-wise miner, csrc/kernels/levels.hip, otherwise), ``"cpu"`` (C++ bitmap Eclat,
 csrc/host/miner_cpu.cpp), ``"oracle"`` (pure-Python mlxtend-faithful FP-tree, models/oracle.py).
 ``"auto"`` = gpu if a HIP device is visible, else cpu.
 """
@@ -23,7 +24,7 @@ from ..ops import native
 from . import oracle as _oracle
 
 __all__ = ["TransactionEncoder", "ItemsetTrie", "fpgrowth", "mine_csr", "csr_from_lists",
-           "default_backend"]
+           "default_backend", "full_miner"]
 
 
 # --------------------------------------------------------------------------------------------
@@ -143,11 +144,51 @@ def _gpu_miner():
     return _GPU_MINER
 
 
+DEEP_MAX_TX = 4096  # the deep miner's tid rows: at most 64 words (kern::deep_max_words)
+
+
+def full_miner(n_tx: int, pairs_only: bool = False) -> str:
+    """Which GPU engine mines every itemset: ``"deep"`` (the headline's persistent wave-per-task
+    DFS, kernels/deep.hip, emitting its trie into an HBM arena) whenever the transactions fit its
+    tid rows, else ``"levels"`` (the level-wise fused / chunked miner, kernels/levels.hip).
+    ``KMLS_FULL_MINER=deep|levels`` overrides (deep still needs n_tx <= 4096)."""
+    want = os.environ.get("KMLS_FULL_MINER", "auto").lower()
+    if want not in ("auto", "deep", "levels"):
+        raise ValueError(f"KMLS_FULL_MINER={want!r}: expected auto, deep or levels")
+    fits = 0 < n_tx <= DEEP_MAX_TX and not pairs_only
+    if want == "levels" or not fits:
+        return "levels"
+    return "deep"
+
+
+def _mine_deep_trie(g, min_support: float, ml: int) -> Dict:
+    """Every frequent itemset through the deep miner: emit mode writes each one as a node of an
+    HBM arena inside the search, the arena is compacted into a parent-first trie on the device
+    (kernels/deep_trie.hip) and copied out in narrow widths (9 B per itemset)."""
+    import time
+    t0 = time.perf_counter()
+    d = g.mine_deep(float(min_support), ml, emit=True)
+    t1 = time.perf_counter()
+    t = g.deep_arena_trie(1, 0)
+    t2 = time.perf_counter()
+    if int(t["n"]) != int(d["n_itemsets"]):
+        raise RuntimeError(f"deep trie holds {t['n']} nodes for {d['n_itemsets']} itemsets")
+    st = {"n_itemsets": int(d["n_itemsets"]), "n_frequent_items": int(d["n_frequent_items"]),
+          "max_depth": int(d["max_depth"]), "per_level": list(d["per_level"]),
+          "digest": d["digest"], "miner": "deep", "levels_path": "deep-emit",
+          "deep_ms": round((t1 - t0) * 1e3, 3), "trie_ms": round((t2 - t1) * 1e3, 3)}
+    return {"parent": t["parent"], "item": t["item"], "count": t["count"], "depth": t["depth"],
+            "stats": st}
+
+
 def mine_csr(tx_ptr: np.ndarray, items: np.ndarray, n_items: int, min_support: float,
              max_len: Optional[int] = None, backend: str = "auto", pairs_only: bool = False,
              columns: Optional[Sequence] = None, mfma: bool = False,
              rule_index: bool = False) -> ItemsetTrie:
     """Mine CSR transactions (rows duplicate-free, item ids in [0, n_items)).
+
+    GPU backend: short-transaction data (n_tx <= 4096, the reference's datasets) is mined by the
+    deep miner in emit mode (``full_miner``); everything else by the level-wise miner.
 
     ``rule_index`` (GPU backend): the mining call also builds the rule map on the device
     (``pairs_to_csr``, rows ordered by score desc then consequent name when ``columns`` are
@@ -184,8 +225,18 @@ def mine_csr(tx_ptr: np.ndarray, items: np.ndarray, n_items: int, min_support: f
         # path, which is the one that builds the rule map
         if pairs_only:
             ml = 2 if ml == 0 else min(ml, 2)
-        r = g.mine(float(min_support), ml, False, True, True, bool(mfma), False,
-                   bool(rule_index))
+        if full_miner(n_tx, pairs_only) == "deep" and not mfma:
+            idx = None
+            if rule_index:  # the deployed rule map = the pair supports: the level-wise call
+                # truncated at 2 items builds it on the device (its trie is not downloaded)
+                rm = g.mine(float(min_support), 2, False, False, True, False, False, True)
+                idx = rm.get("index")
+            r = _mine_deep_trie(g, min_support, ml)
+            if idx is not None:
+                r["index"] = idx
+        else:
+            r = g.mine(float(min_support), ml, False, True, True, bool(mfma), False,
+                       bool(rule_index))
     else:
         raise ValueError(f"unknown backend {backend!r}")
     st = dict(r["stats"])

@@ -25,7 +25,9 @@ import os
 import math
 import random
 import time
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
 
 from ..ops import native
 
@@ -42,6 +44,15 @@ _U64 = 1 << 64
 def _s64(v: int) -> int:
     v %= _U64
     return v - _U64 if v >= (1 << 63) else v
+
+
+def _all_gather_int(v: int, world: int, device: int = 0) -> List[int]:
+    dev = (torch.device("cuda", device) if dist.get_backend() == "nccl"
+           else torch.device("cpu"))
+    x = torch.tensor([v], dtype=torch.int64, device=dev)
+    xs = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(xs, x)
+    return [int(a) for a in xs.cpu().tolist()]
 
 
 def combine_partials(parts: List[Dict]) -> Dict:
@@ -120,6 +131,49 @@ class DeepMiner:
         if self.comm_backend == "torch":
             d = self._combine_torch(d)
         return d
+
+    def mine_trie(self, min_support: float, max_len: int = 0) -> Tuple[Dict, Optional[Dict]]:
+        """Every frequent itemset as a trie, mined by the split (emit mode) and gathered on rank
+        0: ``(whole-problem result, trie arrays on rank 0 / None elsewhere)``.
+
+        Each rank's arena is compacted on its GPU (``deep_arena_trie``): rank 0 exports every
+        size (levels 1-2 are the dense ids [0, P12), P12 = F + frequent pairs, the same arena ids
+        on every rank), a rank r > 0 exports its share (sizes >= 3) with its own node ids shifted
+        past P12 and its size-2 parents kept as arena ids.  Rank 0 concatenates the shares in
+        rank order and moves each share's ids to its offset; parents stay before children (a
+        share's parents are in the share or in rank 0's levels 1-2)."""
+        d = self.g.mine_deep(min_support, max_len, self.rank, self.world, self.comm, emit=True,
+                             **self.opts)
+        if self.comm_backend == "torch":
+            d = self._combine_torch(d)
+        per = list(d["per_level"]) + [0, 0, 0]
+        p12 = int(per[1]) + int(per[2])
+        t = self.g.deep_arena_trie(1 if self.rank == 0 else 3, 0 if self.rank == 0 else p12)
+        fields = ("parent", "item", "count", "depth")
+        if self.world == 1:
+            return d, {k: t[k] for k in fields}
+        from .dist_miner import gather_arrays
+        dtypes = {k: np.asarray(t[k]).dtype for k in fields}
+        # uint8 views: every collective backend carries bytes (RCCL has no 16-bit integers)
+        # (one field per call: gather_arrays sizes every field by the first one's length)
+        raw = {k: gather_arrays({k: np.ascontiguousarray(t[k]).view(np.uint8)}, self.rank,
+                                self.world) for k in fields}
+        raw = {k: (v[k] if v is not None else None) for k, v in raw.items()}
+        sizes = [int(x) for x in _all_gather_int(int(t["n"]), self.world, self.device)]
+        if self.rank != 0:
+            return d, None
+        out = {k: raw[k].view(dtypes[k]).copy() for k in fields}
+        par = out["parent"]
+        if sum(sizes) >= (1 << 31):
+            raise RuntimeError("deep trie: 2^31 nodes (i32 parents)")
+        off = sizes[0]
+        for r in range(1, self.world):
+            blk = par[off:off + sizes[r]]
+            blk[blk >= p12] += off - p12
+            off += sizes[r]
+        if off != int(d["n_itemsets"]):
+            raise RuntimeError(f"deep trie: gathered {off} nodes for {d['n_itemsets']} itemsets")
+        return d, out
 
     def _combine_torch(self, d: Dict) -> Dict:
         return allreduce_partial(d, self.world, self.device)

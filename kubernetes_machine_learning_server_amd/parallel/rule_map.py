@@ -152,6 +152,7 @@ class _Gpu:
             self.method = "none"
             if F:
                 if self.g.cooc_preferred() and self.g.pair_counts_csr(gram.data_ptr(), F):
+                    self.g.cooc_check()  # entry overflow / duplicate rows: fail, not drop pairs
                     self.method = "cooc"
                     self.held.pop("bm", None)
                 else:

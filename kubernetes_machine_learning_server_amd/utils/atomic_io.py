@@ -52,6 +52,28 @@ def atomic_write_bytes(path: PathLike, data: bytes, mode: int = 0o644) -> None:
     _fsync_dir(p.parent)
 
 
+def atomic_write_with(path: PathLike, write, mode: int = 0o644) -> None:
+    """``atomic_write_bytes`` for large artifacts: ``write(file)`` streams into the temp file
+    (no in-memory copy of the whole artifact), then fsync + rename as above."""
+    p = pathlib.Path(path)
+    p.parent.mkdir(parents=True, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(prefix=f".{p.name}.", suffix=".tmp", dir=str(p.parent))
+    try:
+        with os.fdopen(fd, "wb") as f:
+            write(f)
+            f.flush()
+            os.fsync(f.fileno())
+        os.chmod(tmp, mode)
+        os.replace(tmp, p)
+    except BaseException:
+        try:
+            os.unlink(tmp)
+        except OSError:
+            pass
+        raise
+    _fsync_dir(p.parent)
+
+
 def atomic_write_text(path: PathLike, text: str, encoding: str = "utf-8") -> None:
     atomic_write_bytes(path, text.encode(encoding))
 

@@ -111,8 +111,11 @@ def main() -> int:
                       flush=True)
         return 0
     for ms in [float(x) for x in a.supports.split(",")]:
+        # one untimed call first: the first call allocates the miner's buffers (the cold call is
+        # what is dropped, not a rank)
+        g.mine_deep(ms, a.max_len, rank=0, world=a.world, **kw)
         for rep in range(a.reps):
-            comb = {"sum": 0, "xor": 0, "n": 0, "slowest_ms": 0.0}
+            comb = {"sum": 0, "xor": 0, "n": 0, "slowest_ms": 0.0, "ranks_ms": []}
             for r in range(a.world):
                 t = time.perf_counter()
                 with Heartbeat(f"min_support {ms} rank {r}"):
@@ -137,8 +140,8 @@ def main() -> int:
                 comb["sum"] = (comb["sum"] + int(d["digest"][:16], 16)) % (1 << 64)
                 comb["xor"] ^= int(d["digest"][16:], 16)
                 comb["n"] += d["n_itemsets"]
-                if r > 0 or a.world == 1:  # rank 0's first call also allocates
-                    comb["slowest_ms"] = max(comb["slowest_ms"], d["phases_ms"]["total"])
+                comb["slowest_ms"] = max(comb["slowest_ms"], d["phases_ms"]["total"])
+                comb["ranks_ms"].append(round(d["phases_ms"]["total"], 3))
             if a.world > 1:
                 dg = f"{comb['sum']:016x}{comb['xor']:016x}"
                 ref = CPU_REF.get(ms)
@@ -148,7 +151,8 @@ def main() -> int:
                                   "digest": dg,
                                   "verified_vs_cpu": (dg == ref[0] and comb["n"] == ref[1])
                                   if ref and not a.max_len else None,
-                                  "slowest_rank_ms_excl_rank0": round(comb["slowest_ms"], 3)}),
+                                  "slowest_rank_ms": round(comb["slowest_ms"], 3),
+                                  "ranks_ms": comb["ranks_ms"]}),
                       flush=True)
     return 0
 

@@ -108,3 +108,45 @@ def test_txdp_level2_method_same_trie(gpu_mod, monkeypatch):
     da = gpu_mod.trie_digest(a["parent"], a["item"], a["count"], a["depth"])
     db = gpu_mod.trie_digest(b["parent"], b["item"], b["count"], b["depth"])
     assert da["digest"] == db["digest"] and da["per_depth"] == db["per_depth"]
+
+
+def test_cooc_refuses_after_frequent_subset(gpu_mod):
+    """use_frequent_subset leaves the rank tables on the full selection: the CSR-driven pair
+    count and the rule map refuse (an F-row gram would be written past its end otherwise), the
+    cost model declines, and a fresh select() restores them."""
+    import torch
+    from kubernetes_machine_learning_server_amd.data.synthetic import generate
+    tx = generate("ds2", seed=7, n_tx=1500)
+    g = _miner(gpu_mod, tx.tx_ptr, tx.items, tx.n_items)
+    counts = np.bincount(tx.items, minlength=tx.n_items).astype(np.uint32)
+    F = g.select(counts, tx.n_tx, 0.05)
+    assert F > 4 and not g.subset_active()
+    g.use_frequent_subset(np.arange(0, F, 2, dtype=np.int64))
+    assert g.subset_active()
+    gram = torch.zeros((F, F), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    for call in (lambda: g.pair_counts_csr(gram.data_ptr(), F), lambda: g.cooc_stats(),
+                 lambda: g.rule_map_from_gram(gram.data_ptr(), F, 1)):
+        with pytest.raises(Exception, match="use_frequent_subset"):
+            call()
+    assert not g.cooc_preferred()
+    assert g.select(counts, tx.n_tx, 0.05) == F and not g.subset_active()
+    assert g.pair_counts_csr(gram.data_ptr(), F)
+    g.cooc_check()
+
+
+def test_cooc_flags_duplicate_rows(gpu_mod):
+    """A row holding one frequent item twice breaks load_csr's precondition: the horizontal
+    count flags it (cooc_check raises) instead of silently double-counting its pairs."""
+    import torch
+    rows = [np.array([1, 2, 2, 3], np.int32)] + [np.array([1, 2, 3], np.int32)] * 20
+    ptr = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+    items = np.concatenate(rows).astype(np.int32)
+    g = _miner(gpu_mod, ptr, items, 8)
+    counts = np.bincount(items, minlength=8).astype(np.uint32)
+    F = g.select(counts, len(rows), 0.5)
+    gram = torch.zeros((F, F), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert g.pair_counts_csr(gram.data_ptr(), F)
+    with pytest.raises(Exception, match="duplicate"):
+        g.cooc_check()
