@@ -483,6 +483,8 @@ void register_gpu_bindings(py::module_& m) {
           d["task_ids"] = py::array_t<int64_t>((py::ssize_t)r.task_ids.size(), r.task_ids.data());
           d["task_cost"] = py::array_t<uint32_t>((py::ssize_t)r.task_cost.size(), r.task_cost.data());
           d["clock_khz"] = r.clock_khz;
+          d["t_drain"] = r.t_drain;
+          d["trace_bucket"] = r.trace_bucket;
         }
         return d;
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("rank") = 0, py::arg("world") = 1,

@@ -126,6 +126,8 @@ DeepResult GpuMiner::mine_deep(double min_support, int max_len, int rank, int wo
   res.task_ids = std::move(loc.task_ids);
   res.task_cost = std::move(loc.task_cost);
   res.clock_khz = loc.clock_khz;
+  res.t_drain = loc.t_drain;
+  res.trace_bucket = loc.trace_bucket;
   if (b.xor_cap < world) {
     if (b.d_xor) KMLS_HIP(hipFree(b.d_xor));
     KMLS_HIP(hipMalloc((void**)&b.d_xor, (size_t)world * 8));

@@ -28,7 +28,7 @@ DeepBufs::~DeepBufs() {
                   (void*)n_count, (void*)n_depth, (void*)d_node_off, (void*)d_split_q,
                   (void*)d_split_heap, (void*)d_ocost, (void*)d_otmp, (void*)t_new_id,
                   (void*)t_tmp, (void*)t_parent, (void*)t_item, (void*)t_count, (void*)t_depth,
-                  (void*)d_part, (void*)d_wt})
+                  (void*)d_part, (void*)d_wt, (void*)d_gram})
     if (p) (void)hipFree(p);
   if (h_ctl) (void)hipHostFree(h_ctl);
   if (h_tot) (void)hipHostFree(h_tot);
@@ -174,8 +174,19 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     // level-2 classes laid out on the device: chunk counts -> class sizes, block / task / node
     // offsets (prefix sums); one readback of the three totals (T is needed for the task order)
     KMLS_HIP(hipMemcpyAsync(b.d_wt, wt.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
+    // the level-2 supports through the LDS-tiled popcount bit-GEMM (each row read once per tile)
+    // instead of one AND + popcount per candidate pair in the class kernel (k_deep_root at
+    // 140 + 277 us for F = 2032, gpurun_out/r5d_prof)
+    {
+      int64_t c = b.gram_cap;
+      grow(b.d_gram, c, F * F);
+      b.gram_cap = c;
+      if (kern::pair_gram_dev_needs_zero(in.Wp, F))
+        KMLS_HIP(hipMemsetAsync(b.d_gram, 0, (size_t)F * F * 4, s));
+      kern::pair_gram_popcount(in.bm, in.Wp, F, b.d_gram, s);
+    }
     kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, nullptr, b.d_part, nullptr,
-                    nullptr, nullptr, false, s);
+                    nullptr, nullptr, false, s, nullptr, b.d_gram);
     kern::deep_root_scan(b.d_part, F, b.d_wt, E, (int64_t)root_blk, b.d_m, b.d_off, b.d_toff,
                          b.d_node_off, s);
     KMLS_HIP(hipMemcpyAsync(&b.h_tot[0], b.d_off + F, 8, hipMemcpyDeviceToHost, s));
@@ -225,7 +236,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       nodes = kern::DeepNodes{b.n_parent, b.n_item, b.n_count, b.n_depth, b.d_node_off};
     }
     kern::deep_root((const uint64_t*)b.root, Fpad, F, W, in.minsup, b.d_m, b.d_part, b.d_off,
-                    b.root, rank == 0 ? b.ctl : nullptr, true, s, E ? &nodes : nullptr);
+                    b.root, rank == 0 ? b.ctl : nullptr, true, s, E ? &nodes : nullptr, b.d_gram);
     const int64_t* d_order = nullptr;
     if (deeper && T > 0 && (opt.assign == 1 || opt.trace)) {
       // every task's class size (its level-3 survivors) on the device; tasks ordered largest
@@ -360,6 +371,10 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     KMLS_HIP(hipMemsetAsync(b.d_trace, 0, (size_t)waves * kern::kDeepTraceWords * 8, s));
     a.trace = b.d_trace;
     a.task_ticks = b.d_ticks;
+    int khz = 0;
+    KMLS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, b.device));
+    // 200 us buckets for a rank split, 1 ms for a whole problem
+    a.trace_bucket = (unsigned long long)std::max(1, khz) * (world > 1 ? 1ull : 5ull) / 5ull;
   }
   {
     int khz = 0;
@@ -471,6 +486,8 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
     res.spilled_tasks = (int64_t)b.h_ctl->n_out;
     res.handoffs = (int64_t)b.h_ctl->handoffs;
     if (a.trace) {
+      res.t_drain = b.h_ctl->t_drain;
+      res.trace_bucket = a.trace_bucket;
       res.trace.resize((size_t)waves * kern::kDeepTraceWords);
       res.task_ticks.resize(a.task_ticks ? (size_t)n_tasks : 0);
       KMLS_HIP(hipMemcpy(res.trace.data(), b.d_trace, res.trace.size() * 8, hipMemcpyDeviceToHost));

@@ -40,6 +40,8 @@ struct DeepBufs {
   int32_t* d_part = nullptr;  // [F][deep_root_chunks(F)] level-2 chunk counts / bases
   int64_t part_cap = 0;
   int32_t* d_wt = nullptr;    // [F] projected width tier of each root class
+  uint32_t* d_gram = nullptr; // [F][F] level-2 pair gram (upper triangle)
+  int64_t gram_cap = 0;
   int64_t* h_tot = nullptr;   // pinned [4]: layout totals read back once per call
   int64_t* d_off = nullptr;  // [F + 1] block byte offsets
   int64_t* d_toff = nullptr;  // [F + 1] task offsets
@@ -113,6 +115,7 @@ struct DeepLocal {
   std::vector<int64_t> task_ids;
   std::vector<uint32_t> task_cost;
   double clock_khz = 0;
+  uint64_t t_drain = 0, trace_bucket = 0;  // (trace) queue drained at; bucket width (ticks)
 };
 
 // emit mode: the arena was too small (node_top counts on past its end); `needed` ids

@@ -196,6 +196,7 @@ struct DeepResult {
   std::vector<int64_t> task_ids;
   std::vector<uint32_t> task_cost;
   double clock_khz = 0;
+  uint64_t t_drain = 0, trace_bucket = 0;  // (trace) queue drained at; busy bucket width (ticks)
 };
 struct GraphCache;  // captured launch sequence of the resident path (miner_gpu.hip)
 struct Prefetch;    // a resident call launched ahead of its mine() (miner_gpu.hip)

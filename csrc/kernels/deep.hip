@@ -842,6 +842,7 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
       tf = load_frame(a.in + t, lane);
       holding = false;
     } else {
+      if (tr && lane == 0 && t + 1 == (unsigned long long)a.n_in) a.ctl->t_drain = wall_clock64();
       // ticket t: wait on its own flag (waiting waves poll distinct addresses: one address
       // polled by thousands of waves serialises every device-scope access to it) until the task
       // is published (epoch) or the launch is over (epoch ^ kDone, written by the wave that
@@ -883,10 +884,12 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
         if (!inbox_open) {  // not published yet: open the inbox, then start asking
           if (lane == 0) st_agent(&a.inbox_state[gw], kOpen);
           inbox_open = true;
-        } else if (lane == 0 && (n & 7) == 1) {
-          if (victim != (unsigned)gw)
-            atomicExch(&a.req[victim], ((unsigned long long)a.epoch << 32) | (unsigned long long)(gw + 1));
-          victim = (victim + 97u) % (unsigned)a.nwaves;
+        } else if ((n & 7) == 1) {
+          if (lane == 0) {
+            if (victim != (unsigned)gw)
+              atomicExch(&a.req[victim], ((unsigned long long)a.epoch << 32) | (unsigned long long)(gw + 1));
+            victim = (victim + 97u) % (unsigned)a.nwaves;
+          }
         }
         if (timed_out()) { failed = true; break; }
         wait_short(n);
@@ -980,6 +983,19 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
     }
     if (tr && !failed && lane == 0) {
       const unsigned long long now = wall_clock64();
+      if (a.trace_bucket) {  // the busy interval spread over the time buckets
+        constexpr unsigned long long kLast = (unsigned long long)(kDeepTraceBuckets - 1);
+        unsigned long long x0 = tr_t0 - t_start;
+        const unsigned long long x1 = now - t_start;
+        while (x0 < x1) {
+          const unsigned long long b0 = x0 / a.trace_bucket;
+          const unsigned long long bk = b0 < kLast ? b0 : kLast;
+          const unsigned long long e =
+              bk == kLast ? x1 : ((bk + 1) * a.trace_bucket < x1 ? (bk + 1) * a.trace_bucket : x1);
+          tr[6 + bk] += e - x0;
+          x0 = e;
+        }
+      }
       tr[4] += now - tr_t0;
       tr[2] = now;
       tr[5] += (1ull << 32) | (task_from_inbox ? 1ull : 0ull);
@@ -1052,7 +1068,8 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
                                                    long long F, int maxch, unsigned minsup,
                                                    const int32_t* m_in, int32_t* part,
                                                    const long long* blk_off, char* base,
-                                                   DeepCtl* ctl, int fill, DeepNodes nodes) {
+                                                   DeepCtl* ctl, int fill, DeepNodes nodes,
+                                                   const uint32_t* gram) {
   __shared__ ProjLds<WT> projs[kWaves];
   const int lane = threadIdx.x & 63;
   const long long gw = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -1078,6 +1095,9 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
     cpad = roundup16((unsigned long long)m_in[i]);
     if (cpad == 0) return;  // wave-uniform: no frequent pair
     S = (unsigned)part[gw];  // this chunk's first slot
+    // the chunk's survivors = the next chunk's first slot (or the class size) - S
+    const long long nx = (ch + 1) * kRootChunk < nc ? (long long)part[gw + 1] : (long long)m_in[i];
+    if (nx == (long long)S) return;  // wave-uniform: nothing to write
     cb = (unsigned long long*)(base + blk_off[i]);
     wt_out = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * cpad)) - 1u - E;
     if (wt_out < (unsigned)WT) proj_setup<WT>(PL, root, (unsigned long long)Fpad, (unsigned)i, lane);
@@ -1089,8 +1109,13 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
   for (long long c0 = cbeg; c0 < cend; c0 += 64) {
     const bool act = c0 + lane < cend;
     const long long jb = act ? i + 1 + c0 + lane : i;
+    // with the pair gram (fill pass): 64 candidates without a survivor cost one coalesced read,
+    // and only the survivors' lanes load their rows
+    const bool pre = gram == nullptr || (act && gram[i * F + jb] >= minsup);
+    if (gram != nullptr && __ballot(pre) == 0ull) continue;
     unsigned long long v[WT];
-    const unsigned c = and_count<WT>(root, (unsigned long long)Fpad, (unsigned)i + vzero(), (unsigned)jb, v);
+    unsigned c = 0;
+    if (pre) c = and_count<WT>(root, (unsigned long long)Fpad, (unsigned)i + vzero(), (unsigned)jb, v);
     const bool surv = act && c >= minsup;
     const unsigned long long mask = __ballot(surv);
     if (fill) {
@@ -1132,6 +1157,28 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
   }
 }
 
+// the count pass from the level-2 pair gram (upper triangle, row-major F x F, rank order): one
+// wave per (class i, chunk of kRootChunk candidates), part[i * maxch + c] = the chunk's pairs
+// with support >= minsup (one coalesced read per 64 candidates instead of their AND rows)
+__global__ __launch_bounds__(256) void k_deep_root_gcount(const uint32_t* gram, long long F,
+                                                          int maxch, unsigned minsup,
+                                                          int32_t* part) {
+  const int lane = threadIdx.x & 63;
+  const long long gw = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const long long i = gw / maxch;
+  const long long ch = gw - i * maxch;
+  if (i >= F) return;  // wave-uniform
+  const long long nc = F - 1 - i;
+  const long long cbeg = ch * kRootChunk;
+  const long long cend = cbeg + kRootChunk < nc ? cbeg + kRootChunk : nc;
+  unsigned S = 0;
+  for (long long c0 = cbeg; c0 < cend; c0 += 64) {
+    const bool act = c0 + lane < cend;
+    S += (unsigned)__popcll(__ballot(act && gram[i * F + i + 1 + c0 + lane] >= minsup));
+  }
+  if (lane == 0) part[gw] = (int32_t)S;  // (0 for a chunk past the class's candidates)
+}
+
 // one wave: inclusive prefix sums of three int64 arrays of n entries, in place (the level-2
 // layout: block byte offsets, task offsets, node ids; n = F + 1, a few thousand)
 __global__ __launch_bounds__(64) void k_deep_prefix3(long long* a, long long* b, long long* c,
@@ -1142,7 +1189,25 @@ __global__ __launch_bounds__(64) void k_deep_prefix3(long long* a, long long* b,
   const long long lo = (long long)t * per;
   const long long hi = lo + per < n ? lo + per : n;
   long long sa = 0, sb = 0, sc = 0;
-  for (long long k = lo; k < hi; ++k) {
+  // 8 independent loads of each array in flight per lane (a serial chain of dependent loads
+  // took 27 us at n = 2033)
+  long long k = lo;
+  for (; k + 8 <= hi; k += 8) {
+    long long va[8], vb[8], vc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      va[u] = a[k + u];
+      vb[u] = b[k + u];
+      vc[u] = c[k + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      sa += va[u];
+      sb += vb[u];
+      sc += vc[u];
+    }
+  }
+  for (; k < hi; ++k) {
     sa += a[k];
     sb += b[k];
     sc += c[k];
@@ -1161,13 +1226,26 @@ __global__ __launch_bounds__(64) void k_deep_prefix3(long long* a, long long* b,
   }
   __builtin_amdgcn_wave_barrier();
   long long ra = sh[0][t], rb = sh[1][t], rc = sh[2][t];
-  for (long long k = lo; k < hi; ++k) {
-    ra += a[k];
-    a[k] = ra;
-    rb += b[k];
-    b[k] = rb;
-    rc += c[k];
-    c[k] = rc;
+  for (long long q = lo; q < hi; q += 8) {
+    const int cnt = hi - q < 8 ? (int)(hi - q) : 8;
+    long long va[8], vb[8], vc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < cnt) {
+        va[u] = a[q + u];
+        vb[u] = b[q + u];
+        vc[u] = c[q + u];
+      }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < cnt) {
+        ra += va[u];
+        a[q + u] = ra;
+        rb += vb[u];
+        b[q + u] = rb;
+        rc += vc[u];
+        c[q + u] = rc;
+      }
   }
 }
 
@@ -1351,16 +1429,22 @@ int deep_root_chunks(int64_t F) { return (int)std::max<int64_t>(1, (F - 1 + kRoo
 
 void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t minsup,
                const int32_t* m, int32_t* part, const int64_t* blk_off, char* base, DeepCtl* ctl,
-               bool fill, hipStream_t s, const DeepNodes* nodes) {
+               bool fill, hipStream_t s, const DeepNodes* nodes, const uint32_t* gram) {
   if (F <= 0) return;
   const int maxch = deep_root_chunks(F);
   const unsigned grid = (unsigned)((F * maxch + kWaves - 1) / kWaves);
+  if (gram != nullptr && !fill) {
+    hipLaunchKernelGGL(k_deep_root_gcount, dim3(grid), dim3(64 * kWaves), 0, s, gram,
+                       (long long)F, maxch, minsup, part);
+    return;
+  }
   DeepNodes nd{};
   if (nodes && fill) nd = *nodes;
   by_tier(W, [&](auto wt) {
     hipLaunchKernelGGL(k_deep_root<decltype(wt)::value>, dim3(grid), dim3(64 * kWaves), 0, s,
                        (const unsigned long long*)root, (long long)Fpad, (long long)F, maxch,
-                       minsup, m, part, (const long long*)blk_off, base, ctl, fill ? 1 : 0, nd);
+                       minsup, m, part, (const long long*)blk_off, base, ctl, fill ? 1 : 0, nd,
+                       gram);
   });
 }
 

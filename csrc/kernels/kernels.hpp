@@ -33,6 +33,7 @@ struct DeepCtl {  // per-round control + accumulated results (zeroed once per ca
   unsigned error;                 // bit 0 out queue full, bit 1 heap full, bit 2 timeout,
                                   // bit 3 a frame of an uninstantiated width
   unsigned pad_[3];
+  unsigned long long t_drain;     // (trace) wall clock when the last queued task was dequeued
 };
 struct DeepArgs {
   const DeepFrame* in;
@@ -69,6 +70,7 @@ struct DeepArgs {
   // initial task the ticks its dequeuing wave spent on it (parts handed away excluded)
   unsigned long long* trace;
   unsigned long long* task_ticks;
+  unsigned long long trace_bucket;  // ticks per busy-time bucket of the trace record
   // emit mode (node_parent != nullptr): every frequent itemset of size >= 3 found in the launch
   // becomes a trie node (parent node id, last item's frequency rank, support, size) at an id from
   // a per-wave chunk of ctl->node_top; unused ids keep size 0.  Blocks then carry one more row
@@ -83,7 +85,11 @@ struct DeepArgs {
   const long long* split_q;
   const unsigned long long* split_heap;
 };
-constexpr int kDeepTraceWords = 6;
+// trace record per wave: [0] launch start, [1] first task start, [2] last task end, [3] exit,
+// [4] busy ticks, [5] tasks << 32 | inbox receipts, [6 ..) busy ticks per time bucket of
+// DeepArgs::trace_bucket ticks from the wave's launch start (the last bucket takes the rest)
+constexpr int kDeepTraceBuckets = 58;
+constexpr int kDeepTraceWords = 6 + kDeepTraceBuckets;
 constexpr unsigned long long kDeepNodeMask = (1ull << 40) - 1;  // node id bits of a node word
 int deep_max_words();
 int deep_tier(int words);     // smallest instantiated block width >= words
@@ -113,9 +119,13 @@ struct DeepNodes {
 // root_blk), task_off[0..F], node_off[0..F] (prefix sums, no host round trip); the fill pass
 // then writes every block at off[i] (m = the scanned sizes)
 int deep_root_chunks(int64_t F);
+// gram (optional): the level-2 pair gram (kern::pair_gram_popcount of the root bitmaps, F x F
+// upper triangle): the count pass reads it instead of ANDing every candidate pair, and the fill
+// pass ANDs only the 64-candidate groups holding a survivor
 void deep_root(const uint64_t* root, int64_t Fpad, int64_t F, int W, uint32_t minsup,
                const int32_t* m, int32_t* part, const int64_t* blk_off, char* base, DeepCtl* ctl,
-               bool fill, hipStream_t s, const DeepNodes* nodes = nullptr);
+               bool fill, hipStream_t s, const DeepNodes* nodes = nullptr,
+               const uint32_t* gram = nullptr);
 void deep_root_scan(int32_t* part, int64_t F, const int32_t* wt, int extra, int64_t root_blk,
                     int32_t* m, int64_t* off, int64_t* task_off, int64_t* node_off, hipStream_t s);
 // emit-mode verification: digest terms and per-size counts of the node arena (ids [0, n)) for

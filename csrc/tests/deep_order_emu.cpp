@@ -15,6 +15,18 @@
 namespace kmls {
 namespace kern {
 
+// stand-in for the popcount bit-GEMM (mine.hip): out[i][j] = |row i & row j| for i < j
+void pair_gram_popcount(const uint64_t* bm, int64_t Wp, int64_t F, uint32_t* out, hipStream_t) {
+  for (int64_t i = 0; i < F; ++i)
+    for (int64_t j = i + 1; j < F; ++j) {
+      uint32_t c = 0;
+      for (int64_t w = 0; w < Wp; ++w) c += (uint32_t)__builtin_popcountll(bm[i * Wp + w] & bm[j * Wp + w]);
+      out[i * F + j] = c;
+    }
+}
+
+bool pair_gram_dev_needs_zero(int64_t, int64_t) { return false; }
+
 int64_t deep_task_share(int64_t T, int rank, int world) {
   int64_t n = 0;
   while (n * world + ((n & 1) ? world - 1 - rank : rank) < T) ++n;

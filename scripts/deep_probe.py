@@ -172,7 +172,16 @@ def trace_summary(d):
     tasks = tr[:, 5] >> 32
     inbox = tr[:, 5] & 0xffffffff
     pct = lambda x: [round(float(np.percentile(x, q)), 3) for q in (0, 10, 50, 90, 100)]
+    bw = float(d.get("trace_bucket", 0) or 0)
+    curve = None
+    if bw and tr.shape[1] > 6:
+        # fraction of the waves busy in each time bucket (the launch's activity profile)
+        nb = int(np.ceil(span / (bw * tick_ms)))
+        curve = [round(float(x), 3) for x in (tr[:, 6:6 + nb].sum(0) / (bw * len(tr)))]
+    drain = (float(d["t_drain"]) - t0) * tick_ms if d.get("t_drain") else None
     out = {"span_ms": round(span, 3), "busy_frac": round(float(busy.sum() / (len(tr) * span)), 3),
+           "bucket_ms": round(bw * tick_ms, 3) if bw else None, "busy_curve": curve,
+           "queue_drained_ms": round(drain, 3) if drain is not None else None,
            "first_task_start_ms_pctl": pct(first), "last_task_end_ms_pctl": pct(last),
            "tasks_per_wave_pctl": pct(tasks), "inbox_per_wave_pctl": pct(inbox)}
     tk = np.asarray(d.get("task_ticks", []), np.int64) * tick_ms
