@@ -35,6 +35,11 @@ Secondary fields:
 * ``config2``     — ds1 @0.01: deployed rule map, truncated-at-4 trie, full count-only mining
                     with the size cap raised within a time budget (N = 1).
 * ``config3``     — 10M x 1M @2e-4 (14.8k frequent items) transaction-DP over all ranks
+* ``config5``     — 100M transactions x 1M items @2e-4 (BASELINE config 5) on all ranks: each
+                    rank generates its transaction shard; the deployed rule map (pair supports
+                    counted from the CSR, row blocks reduce-scattered, per-rank CSR, gather),
+                    then rules.idx + hot reload + batched queries; gram rows and sampled
+                    rule-map rows re-counted on the host.
 * ``config3_shard`` — (N > 1) the same problem with item-sharded bitmaps (1/N per rank)
                     (native RCCL communicator at N > 1 once ``native_rccl`` worked, else the
                     host one), sampled supports recounted on the host from the CSR shards.
@@ -149,6 +154,8 @@ def main() -> int:
     ap.add_argument("--no-emit", action="store_true", help="skip the materialising headline run")
     ap.add_argument("--no-config2", action="store_true")
     ap.add_argument("--no-job", action="store_true", help="skip the job at the headline support")
+    ap.add_argument("--no-config5", action="store_true", help="skip the 100M-transaction rule map")
+    ap.add_argument("--config5-steps", type=int, default=3)
     ap.add_argument("--no-config3", action="store_true")
     ap.add_argument("--cpu", action="store_true",
                     help="CPU tier of the headline (native CPU count miner, gloo): no GPU")
@@ -375,6 +382,25 @@ def main() -> int:
                 out["config3"] = c3
         except Exception as e:
             out.setdefault("errors", {})["config3"] = repr(e)[:300]
+        wd.disarm()
+
+    # ---- BASELINE config 5 (all ranks): 100M transactions x 1M items, the deployed rule map ----
+    if not args.no_config5 and not args.cpu:
+        wd.arm("config5", 600)
+        try:
+            from kubernetes_machine_learning_server_amd.bench.bench_large import run_rule_map
+            t_c5 = time.time()
+            c5 = run_rule_map("100Mx1M", min_support=2e-4, steps=args.config5_steps, warmup=1)
+            c5["section_wall_s"] = round(time.time() - t_c5, 1)
+            if rank == 0:
+                c5["model"] = "rule-map-100Mx1M-synthetic"
+                c5["what"] = ("BASELINE config 5: 100M transactions x 1M items @2e-4 -> the "
+                              "deployed artifact (rule map = pair supports, main.py:282-304), "
+                              "timed step = supports + selection + pair counts + CSR per rank, "
+                              "then rules.idx write + hot reload into the C++ and HBM indexes")
+                out["config5"] = c5
+        except Exception as e:
+            out.setdefault("errors", {})["config5"] = repr(e)[:300]
         wd.disarm()
 
     # ---- config 3 with item-sharded bitmaps (1/N of the bitmap per rank; N > 1 only) ----

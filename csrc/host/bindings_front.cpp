@@ -24,7 +24,8 @@ void register_front_bindings(py::module_& m) {
       .def("set_model", [](HttpFront& f, std::shared_ptr<RuleIndex> index,
                            const std::vector<std::string>& names,
                            const std::vector<std::string>& best, py::object marker,
-                           std::shared_ptr<gpu::GpuRuleIndex> gpu, int gpu_min_batch) {
+                           std::shared_ptr<gpu::GpuRuleIndex> gpu, int gpu_min_batch,
+                           int gpu_min_merge) {
         std::string mk;
         const std::string* mp = nullptr;
         if (!marker.is_none()) {
@@ -32,9 +33,10 @@ void register_front_bindings(py::module_& m) {
           mp = &mk;
         }
         py::gil_scoped_release nogil;
-        f.set_model(std::move(index), names, best, mp, std::move(gpu), gpu_min_batch);
+        f.set_model(std::move(index), names, best, mp, std::move(gpu), gpu_min_batch,
+                    gpu_min_merge);
       }, py::arg("index"), py::arg("names"), py::arg("best_names"), py::arg("marker"),
-         py::arg("gpu") = nullptr, py::arg("gpu_min_batch") = 0)
+         py::arg("gpu") = nullptr, py::arg("gpu_min_batch") = 0, py::arg("gpu_min_merge") = -1)
       .def("clear_model", &HttpFront::clear_model)
       .def("next_slow", [](HttpFront& f) -> py::object {
         SlowRequest r;
@@ -65,6 +67,8 @@ void register_front_bindings(py::module_& m) {
         d["slow"] = s.slow;
         d["gpu_batches"] = s.gpu_batches;
         d["gpu_queries"] = s.gpu_queries;
+        d["gpu_loop_batches"] = s.gpu_loop_batches;
+        d["gpu_loop_refused"] = s.gpu_loop_refused;
         d["connections"] = s.connections;
         d["bytes_in"] = s.bytes_in;
         d["bytes_out"] = s.bytes_out;

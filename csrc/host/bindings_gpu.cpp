@@ -300,6 +300,9 @@ void register_gpu_bindings(py::module_& m) {
       .def("pair_counts_csr", &gpu::GpuMiner::pair_counts_csr, py::arg("out"), py::arg("ld"),
            py::call_guard<py::gil_scoped_release>())
       .def("cooc_check", &gpu::GpuMiner::cooc_check, py::call_guard<py::gil_scoped_release>())
+      .def("cooc_likely", &gpu::GpuMiner::cooc_likely)
+      .def("pair_counts_csr_direct", &gpu::GpuMiner::pair_counts_csr_direct, py::arg("out"),
+           py::arg("ld"), py::call_guard<py::gil_scoped_release>())
       .def("subset_active", &gpu::GpuMiner::subset_active)
       .def("cooc_preferred", &gpu::GpuMiner::cooc_preferred,
            py::call_guard<py::gil_scoped_release>())
@@ -576,7 +579,39 @@ void register_gpu_bindings(py::module_& m) {
           ix.query_batch(q_ptr.data(), B, seeds.data(), k, po, pn);
         }
         return py::make_tuple(ids, ns);
+      })
+      .def("query_loop", [](gpu::GpuRuleIndex& ix, I64 q_ptr, I32 seeds, int k) {
+        const int64_t B = q_ptr.size() - 1;
+        py::array_t<int32_t> ids({(py::ssize_t)B, (py::ssize_t)k});
+        py::array_t<int32_t> ns({(py::ssize_t)B});
+        int32_t* po = ids.mutable_data();
+        int32_t* pn = ns.mutable_data();
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = ix.query_loop(q_ptr.data(), B, seeds.data(), k, po, pn);
+        }
+        return py::make_tuple(ids, ns, ok);
+      })
+      .def("merged_size", [](const gpu::GpuRuleIndex& ix, I32 seeds) {
+        return ix.merged_size(seeds.data(), (int64_t)seeds.size());
       });
+  m.def("serve_loop_stats", [](int device) {
+    const gpu::ServeLoopStats st = gpu::GpuServeLoop::for_device(device).stats();
+    py::dict d;
+    d["requests"] = st.requests;
+    d["queries"] = st.queries;
+    d["launches"] = st.launches;
+    d["refused"] = st.refused;
+    d["last_us"] = st.last_us;
+    d["mean_us"] = st.requests ? st.sum_us / (double)st.requests : 0.0;
+    d["kernel_mean_us"] = st.requests ? st.kernel_us / (double)st.requests : 0.0;
+    return d;
+  }, py::arg("device") = 0);
+  m.def("serve_loop_pause", [](int device, bool pause) {
+    if (pause) gpu::GpuServeLoop::for_device(device).pause();
+    else gpu::GpuServeLoop::for_device(device).resume();
+  }, py::arg("device") = 0, py::arg("pause") = true, py::call_guard<py::gil_scoped_release>());
 }
 
 }  // namespace kmls

@@ -7,6 +7,7 @@
 //   JSONResponse (json.dumps(ensure_ascii=False, separators=(",", ":"))).
 // Anything the native route does not answer goes to the FastAPI app unchanged.
 #include "kmls/http_front.hpp"
+#include "../kernels/kernels.hpp"  // kServeMaxSeeds / kServeWaveMerge (the loop router)
 
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -543,7 +544,8 @@ struct HttpFront::Impl {
   std::atomic<int> gpu_pending{0};
   // stats
   std::atomic<uint64_t> st_requests{0}, st_native{0}, st_fallback{0}, st_slow{0},
-      st_gpu_batches{0}, st_gpu_queries{0}, st_conns{0}, st_in{0}, st_out{0};
+      st_gpu_batches{0}, st_gpu_queries{0}, st_conns{0}, st_in{0}, st_out{0}, st_gpu_loop{0},
+      st_gpu_loop_refused{0};
 
   // ---- response building ----
   // Date header cache: per calling thread (I/O threads, the GPU batcher and respond() all build
@@ -816,8 +818,17 @@ struct HttpFront::Impl {
       auto it = m->name_to_id.find(seeds[i]);
       ids[i] = it == m->name_to_id.end() ? -1 : it->second;
     }
-    if (m->gpu && m->gpu_min_batch > 0 &&
-        (m->gpu_min_batch == 1 || gpu_pending.load(std::memory_order_relaxed) + 1 >= m->gpu_min_batch)) {
+    bool to_gpu = false;
+    if (m->gpu && m->gpu_min_merge >= 0) {  // the serving loop: by the query's merged size
+      if ((int)ids.size() <= kern::kServeMaxSeeds) {
+        const int64_t merged = m->gpu->merged_size(ids.data(), (int64_t)ids.size());
+        to_gpu = merged >= m->gpu_min_merge && merged <= kern::kServeWaveMerge && merged > 0;
+      }
+    } else if (m->gpu && m->gpu_min_batch > 0) {
+      to_gpu = m->gpu_min_batch == 1 ||
+               gpu_pending.load(std::memory_order_relaxed) + 1 >= m->gpu_min_batch;
+    }
+    if (to_gpu) {
       c.busy = true;
       c.close_after = c.close_after || !r.keep_alive;
       ++gpu_pending;
@@ -995,7 +1006,11 @@ struct HttpFront::Impl {
         std::unique_lock<std::mutex> lk(gpu_mu);
         gpu_cv.wait(lk, [&] { return !gpu_q.empty() || !running.load(); });
         if (gpu_q.empty() && !running.load()) return;
-        if ((int)gpu_q.size() < batch_max && batch_wait_us > 0) {
+        // the serving loop answers a request in one round trip whatever the batch: no
+        // micro-batching wait for it (that wait is for the per-batch launch path)
+        const std::shared_ptr<const FrontModel> cur = std::atomic_load(&model);
+        const bool loop_mode = cur && cur->gpu_min_merge >= 0;
+        if ((int)gpu_q.size() < batch_max && batch_wait_us > 0 && !loop_mode) {
           gpu_cv.wait_for(lk, std::chrono::microseconds(batch_wait_us),
                           [&] { return (int)gpu_q.size() >= batch_max || !running.load(); });
         }
@@ -1023,19 +1038,27 @@ struct HttpFront::Impl {
         out_n.assign((size_t)B, 0);
         bool ok = true;
         try {
-          m.gpu->query_batch(q_ptr.data(), B, seeds.data(), k, out_ids.data(), out_n.data());
+          if (m.gpu_min_merge >= 0) {  // the persistent serving kernel (false: paused)
+            ok = m.gpu->query_loop(q_ptr.data(), B, seeds.data(), k, out_ids.data(), out_n.data());
+            if (ok) ++st_gpu_loop;
+            else ++st_gpu_loop_refused;
+          } else {
+            m.gpu->query_batch(q_ptr.data(), B, seeds.data(), k, out_ids.data(), out_n.data());
+          }
         } catch (...) {
           ok = false;
         }
-        ++st_gpu_batches;
-        st_gpu_queries += (uint64_t)B;
+        if (ok) {
+          ++st_gpu_batches;
+          st_gpu_queries += (uint64_t)B;
+        }
         for (size_t i = a; i < b; ++i) {
           GpuJob& j = batch[i];
           const int64_t row = (int64_t)(i - a);
           int n = ok ? out_n[(size_t)row] : 0;
           std::vector<int32_t> cpu(256);
           const int32_t* ids = out_ids.data() + row * k;
-          if (!ok) {  // HIP error: answer from the C++ matcher
+          if (!ok || n == -2) {  // HIP error / paused loop / long merge: the C++ matcher
             n = m.index->query(j.ids.data(), (int)j.ids.size(), std::min(k, 256), cpu.data(), nullptr);
             ids = cpu.data();
           }
@@ -1159,7 +1182,8 @@ void HttpFront::stop() {
 void HttpFront::set_model(std::shared_ptr<const RuleIndex> index,
                           const std::vector<std::string>& names,
                           const std::vector<std::string>& best_names, const std::string* marker,
-                          std::shared_ptr<gpu::GpuRuleIndex> gpu, int gpu_min_batch) {
+                          std::shared_ptr<gpu::GpuRuleIndex> gpu, int gpu_min_batch,
+                          int gpu_min_merge) {
   KMLS_CHECK(index != nullptr, "set_model: no index");
   KMLS_CHECK((int64_t)names.size() == index->n_items(), "set_model: names != index items");
   auto m = std::make_shared<FrontModel>();
@@ -1184,6 +1208,7 @@ void HttpFront::set_model(std::shared_ptr<const RuleIndex> index,
   else m->marker_json = "null";
   m->gpu = std::move(gpu);
   m->gpu_min_batch = m->gpu ? std::max(0, gpu_min_batch) : 0;
+  m->gpu_min_merge = m->gpu ? gpu_min_merge : -1;
   std::shared_ptr<const FrontModel> cm = m;
   std::atomic_store(&impl_->model, cm);
 }
@@ -1248,6 +1273,8 @@ FrontStats HttpFront::stats() const {
   s.slow = impl_->st_slow;
   s.gpu_batches = impl_->st_gpu_batches;
   s.gpu_queries = impl_->st_gpu_queries;
+  s.gpu_loop_batches = impl_->st_gpu_loop;
+  s.gpu_loop_refused = impl_->st_gpu_loop_refused;
   s.connections = impl_->st_conns;
   s.bytes_in = impl_->st_in;
   s.bytes_out = impl_->st_out;

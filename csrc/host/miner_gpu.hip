@@ -1150,6 +1150,41 @@ bool GpuMiner::cooc_preferred() {
   return h == 2 || cooc_cheaper((int64_t)fi_.ids.size(), words_local(), nnz_, st);
 }
 
+bool GpuMiner::cooc_likely() {
+  if (words_local() < 1024 || fi_.ids.empty() || subset_active()) return false;
+  const long long h = test_hook("cooc", 1);
+  if (h == 0) return false;
+  if (h == 2) return true;
+  double sum = 0;
+  for (uint32_t c : fi_.counts) sum += (double)c;
+  const double kbar = sum / (double)std::max<int64_t>(global_n_tx_, 1);
+  CoocStats st;
+  // sum_t k_t(k_t-1)/2 ~ T kbar^2 / 2 (x1.5 for the spread of k_t: the model's margin)
+  st.pairs = (uint64_t)(1.5 * (double)n_tx_ * kbar * kbar / 2.0);
+  st.max_k = 0;
+  return cooc_cheaper((int64_t)fi_.ids.size(), words_local(), nnz_, st);
+}
+
+bool GpuMiner::pair_counts_csr_direct(uintptr_t out_dev, int64_t ld) {
+  KMLS_HIP(hipSetDevice(device_));
+  const int64_t F = (int64_t)fi_.ids.size();
+  KMLS_CHECK(ld >= F, "pair_counts_csr_direct: ld >= F");
+  KMLS_CHECK(!subset_active(), "pair_counts_csr_direct: a use_frequent_subset() set is active; "
+                               "select() again first");
+  hipStream_t s = (hipStream_t)stream_;
+  if (!d_cooc_) KMLS_HIP(hipMalloc((void**)&d_cooc_, 4 * sizeof(unsigned long long)));
+  KMLS_HIP(hipMemsetAsync((void*)out_dev, 0, (size_t)F * ld * sizeof(uint32_t), s));
+  KMLS_HIP(hipMemsetAsync(d_cooc_ + 2, 0, sizeof(unsigned long long), s));
+  kern::cooc_count(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, d_fmask_, F, (uint32_t*)out_dev, ld,
+                   (unsigned*)(d_cooc_ + 2), n_cus_, s);
+  unsigned long long f = 0;
+  KMLS_HIP(hipMemcpyAsync(&f, d_cooc_ + 2, sizeof f, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  KMLS_CHECK(!(f & 2ull), "cooc_count: a transaction holds the same frequent item twice "
+                          "(load_csr requires duplicate-free rows)");
+  return !(f & 1ull);
+}
+
 GpuMiner::RuleMap GpuMiner::rule_map_from_gram(uintptr_t gram_dev, int64_t ld, uint32_t minsup) {
   KMLS_HIP(hipSetDevice(device_));
   hipStream_t s = (hipStream_t)stream_;

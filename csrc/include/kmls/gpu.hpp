@@ -310,6 +310,12 @@ class GpuMiner {
   static bool cooc_cheaper(int64_t F, int64_t Wp, int64_t nnz, const CoocStats& st);
   // the model applied to this shard and the last select() (one stats pass; false below 64k tx)
   bool cooc_preferred();
+  // the same decision from the supports alone (mean frequent items per transaction from the
+  // selected counts; no CSR pass), and the count without the stats pass: 1 = done, 0 = a
+  // transaction held more frequent items than the entry buffer (out is invalid: use the
+  // bit-GEMM); synchronises; throws on a duplicated item.  Config 5 drops its 17 ms stats pass.
+  bool cooc_likely();
+  bool pair_counts_csr_direct(uintptr_t out_dev, int64_t ld);
   // Rule map (O10 pairs_to_csr) from a pair-count matrix already on the device (upper triangle,
   // rank order of the last select(), row stride ld): CSR by item id, rows by (count desc, tie
   // key asc).  For callers that own the gram (the large-shape pairs pipeline); the resident
@@ -440,6 +446,15 @@ class GpuRuleIndex {
   // first-insertion order).
   void query_batch(const int64_t* q_ptr, int64_t B, const int32_t* seeds, int k, int32_t* out_ids,
                    int32_t* out_n);
+  // The same answers through the device's persistent serving kernel (GpuServeLoop): no launch
+  // and no stream synchronisation per batch.  Only queries with <= kServeMaxSeeds seeds whose
+  // merged rows fit the wave matcher (<= kServeWaveMerge entries) are answered there; others get
+  // out_n = -2 (the caller answers them).  False: the loop is paused (an index is being built
+  // or freed) or failed — nothing was answered.
+  bool query_loop(const int64_t* q_ptr, int64_t B, const int32_t* seeds, int k,
+                  int32_t* out_ids, int32_t* out_n);
+  // merged entries of one query (sum of its key seeds' row lengths; the router's size)
+  int64_t merged_size(const int32_t* seeds, int64_t n) const;
   int64_t nnz() const { return nnz_; }
   int64_t n_items() const { return n_items_; }
   int max_row() const { return max_row_; }
@@ -461,6 +476,57 @@ class GpuRuleIndex {
   // mapped pinned staging (queries in, results out; grown on demand)
   int32_t* h_pinned_ = nullptr;
   int64_t cap_pinned_ = 0;
+};
+
+// The device's persistent serving kernel: one 256-thread workgroup that polls a request word
+// in mapped, coherent host memory, answers the batch with the wave matcher (4 queries at a
+// time), publishes the results and a done word, and polls again — a round trip is two PCIe
+// crossings instead of a kernel launch plus a stream synchronisation (~14.5 us per batch).  It
+// exits after idle_ms without a request, after life_ms in all, or when stopped; the next
+// request relaunches it.  While any index of the device is being built or freed the loops are
+// paused (allocation calls must not wait behind a running kernel) and refuse requests.
+struct ServeLoopStats {
+  uint64_t requests = 0, queries = 0, launches = 0, refused = 0;
+  double last_us = 0, sum_us = 0;
+  double kernel_us = 0;  // sum over requests of the kernel's own time (request seen -> done)
+};
+class GpuServeLoop {
+ public:
+  static GpuServeLoop& for_device(int device);
+  // one batch; false when paused / failed (nothing answered)
+  bool run(const int64_t* d_row_ptr, const int32_t* d_cons, const uint32_t* d_score,
+           const uint8_t* d_is_key, int64_t n_items, const int64_t* q_ptr, int64_t B,
+           const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n);
+  void pause();   // stop the kernel, wait for it to exit; run() refuses until resume()
+  void resume();
+  ServeLoopStats stats();
+  ~GpuServeLoop();
+
+ private:
+  explicit GpuServeLoop(int device);
+  bool run_one(const int64_t* d_row_ptr, const int32_t* d_cons, const uint32_t* d_score,
+               const uint8_t* d_is_key, int64_t n_items, const int64_t* q_ptr, int64_t B,
+               const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n);
+  bool ensure_running();
+  void stop_and_wait();
+  int device_;
+  void* stream_ = nullptr;
+  void* mail_ = nullptr;          // mapped coherent host: kern::ServeMail
+  int32_t* buf_ = nullptr;        // mapped coherent host: queries and results
+  int64_t cap_ = 0;               // int32 words of buf_
+  unsigned seq_ = 0;
+  int paused_ = 0;
+  bool launched_ = false;
+  unsigned long long idle_ticks_ = 0, life_ticks_ = 0;
+  double ticks_per_us_ = 100.0;
+  ServeLoopStats st_;
+  std::mutex mu_;
+};
+// pauses every serving loop of `device` for the guard's lifetime (index builds / frees)
+struct ServeLoopPause {
+  explicit ServeLoopPause(int device);
+  ~ServeLoopPause();
+  int device;
 };
 
 }  // namespace gpu

@@ -37,11 +37,16 @@ struct FrontModel {
   std::string marker_json;              // model_date: JSON string literal or null
   std::shared_ptr<gpu::GpuRuleIndex> gpu;  // HBM index (optional)
   int gpu_min_batch = 0;                // batches >= this go to the GPU (0: never)
+  // persistent serving kernel (gpu::GpuServeLoop): a query whose merged rows hold at least this
+  // many entries (and fit the wave matcher) is answered by the loop, whatever the batch;
+  // -1 = off (batch routing by gpu_min_batch)
+  int gpu_min_merge = -1;
 };
 
 struct FrontStats {
   uint64_t requests = 0, native_ok = 0, fallback = 0, slow = 0, gpu_batches = 0,
            gpu_queries = 0, connections = 0, bytes_in = 0, bytes_out = 0;
+  uint64_t gpu_loop_batches = 0, gpu_loop_refused = 0;  // (of gpu_batches) via the serving loop
 };
 
 struct SlowRequest {  // a request handed to the Python (FastAPI) side
@@ -70,7 +75,8 @@ class HttpFront {
   // last request that holds it finishes)
   void set_model(std::shared_ptr<const RuleIndex> index, const std::vector<std::string>& names,
                  const std::vector<std::string>& best_names, const std::string* marker,
-                 std::shared_ptr<gpu::GpuRuleIndex> gpu, int gpu_min_batch);
+                 std::shared_ptr<gpu::GpuRuleIndex> gpu, int gpu_min_batch,
+                 int gpu_min_merge = -1);
   void clear_model();
 
   // Python side of the slow path: the eventfd becomes readable when requests are queued

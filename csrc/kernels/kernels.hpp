@@ -554,6 +554,37 @@ void serve_topk_big(const int64_t* row_ptr, const int32_t* cons, const uint32_t*
                     const int32_t* id_pos, const int64_t* q_ptr, const int32_t* seeds,
                     const int32_t* qlist, int64_t nq, int k, int32_t* out, hipStream_t s);
 constexpr int kServeWaveMerge = 512;  // merged entries the wave kernel takes (its table / 2)
+constexpr int kServeLoopStage = 2048;  // int32 words of one loop request staged in LDS
+constexpr int kServeLoopOut = 1536;    // int32 words of one loop request's results in LDS
+// persistent serving loop (serve.hip k_serve_loop, gpu::GpuServeLoop): mapped coherent host
+// memory, every word the two sides poll on a 64-byte line of its own
+struct ServeReq {
+  const int64_t* row_ptr;
+  const int32_t* cons;
+  const uint32_t* srank;
+  const uint8_t* is_key;
+  long long n_items;
+  const long long* q_ptr;   // [B + 1] (device view of mapped host memory)
+  const int32_t* seeds;
+  int32_t* out;             // [B][k + 1]
+  long long B;
+  long long k;
+  long long n_seeds;        // seeds follow q_ptr in the payload: [q_ptr | seeds] contiguous
+};
+struct ServeMail {
+  unsigned req_seq;   // host -> device, written after the descriptor
+  unsigned pad0[15];
+  unsigned done_seq;  // device -> host, written after the results
+  unsigned pad1[15];
+  unsigned alive;     // device: 1 while the kernel runs
+  unsigned pad2[15];
+  unsigned stop;      // host -> device
+  unsigned pad3[15];
+  ServeReq req;
+  unsigned long long t_seen, t_done;  // device wall clock: request seen, done word written
+};
+void serve_loop_launch(ServeMail* mail, unsigned long long idle_ticks,
+                       unsigned long long life_ticks, hipStream_t s);
 constexpr int kServeMaxSeeds = 256;
 
 }  // namespace kern

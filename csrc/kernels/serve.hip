@@ -32,6 +32,11 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -251,26 +256,13 @@ __global__ __launch_bounds__(kBigThreads) void k_serve_topk_big(
   if (tid == 0) o[0] = n_out;
 }
 
-__global__ __launch_bounds__(64 * kWaves) void k_serve_match_topk(
+// one query (seeds[q0, q1), request order) answered by the calling wave into o[0 .. k]: o[0] =
+// the number of ids (-1 no seed is a key, -2 host path), o[1 ..] = ids; per-wave LDS tables
+__device__ __forceinline__ void serve_query_wave(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ cons,
     const uint32_t* __restrict__ srank, const uint8_t* __restrict__ is_key, int64_t n_items,
-    const int64_t* __restrict__ q_ptr, const int32_t* __restrict__ seeds, int64_t B, int k,
-    int32_t* __restrict__ out) {
-  __shared__ int32_t s_key[kWaves][kSlots];
-  __shared__ uint32_t s_val[kWaves][kSlots];
-  __shared__ uint32_t s_pos[kWaves][kSlots];
-  __shared__ int64_t s_seg[kWaves][kMaxSeeds + 1];  // concatenation offsets of present seeds
-  __shared__ int64_t s_row[kWaves][kMaxSeeds];      // row start of each present seed
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * kWaves + w;
-  if (b >= B) return;  // wave-uniform: no block barrier below
-  int32_t* key = s_key[w];
-  uint32_t* val = s_val[w];
-  uint32_t* pos = s_pos[w];
-  int64_t* seg = s_seg[w];
-  int64_t* rowp = s_row[w];
-  const int64_t q0 = q_ptr[b], q1 = q_ptr[b + 1];
-  int32_t* o = out + b * (int64_t)(k + 1);
+    const int32_t* __restrict__ seeds, int64_t q0, int64_t q1, int k, int32_t* __restrict__ o,
+    int32_t* key, uint32_t* val, uint32_t* pos, int64_t* seg, int64_t* rowp, int lane) {
   for (int i = lane; i < kSlots; i += 64) {
     key[i] = -1;
     val[i] = 0;
@@ -381,6 +373,138 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_match_topk(
   if (lane == 0) o[0] = n_out;
 }
 
+__global__ __launch_bounds__(64 * kWaves) void k_serve_match_topk(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ cons,
+    const uint32_t* __restrict__ srank, const uint8_t* __restrict__ is_key, int64_t n_items,
+    const int64_t* __restrict__ q_ptr, const int32_t* __restrict__ seeds, int64_t B, int k,
+    int32_t* __restrict__ out) {
+  __shared__ int32_t s_key[kWaves][kSlots];
+  __shared__ uint32_t s_val[kWaves][kSlots];
+  __shared__ uint32_t s_pos[kWaves][kSlots];
+  __shared__ int64_t s_seg[kWaves][kMaxSeeds + 1];  // concatenation offsets of present seeds
+  __shared__ int64_t s_row[kWaves][kMaxSeeds];      // row start of each present seed
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * kWaves + w;
+  if (b >= B) return;  // wave-uniform: no block barrier below
+  int32_t* key = s_key[w];
+  uint32_t* val = s_val[w];
+  uint32_t* pos = s_pos[w];
+  int64_t* seg = s_seg[w];
+  int64_t* rowp = s_row[w];
+  const int64_t q0 = q_ptr[b], q1 = q_ptr[b + 1];
+  serve_query_wave(row_ptr, cons, srank, is_key, n_items, seeds, q0, q1, k,
+                   out + b * (int64_t)(k + 1), key, val, pos, seg, rowp, lane);
+}
+
+// ---- the persistent serving loop (gpu::GpuServeLoop) ----
+// The mailbox and the payload live in fine-grained (coherent, uncached) host memory: relaxed
+// system-scope accesses go to the host every time, so no acquire/release fences are used — a
+// system-scope acquire invalidates, and a release writes back, the XCD's whole L2 on every poll
+// and every answer (measured: ~33 us per round trip with them).  Ordering instead: the host
+// writes payload and descriptor before the request word (x86 store order); the kernel's result
+// stores drain (vmcnt 0) before the done word is written, and PCIe keeps posted writes in order.
+__device__ __forceinline__ unsigned ld_sys(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+constexpr int kLoopStage = kServeLoopStage;
+constexpr int kLoopOut = kServeLoopOut;
+
+// One workgroup: lane 0 of wave 0 polls the request word (a short sleep between polls); a new
+// sequence number is broadcast through LDS, the request is staged into LDS by every thread in
+// one round of loads, every wave answers queries w, w + 4, ... with the wave matcher (results
+// written straight to mapped host memory), and after the barrier lane 0 publishes the done
+// word.  Exit (every wave, same iteration): stop word set, or no request for idle_ticks, or
+// life_ticks since the launch (wall_clock64 ticks) — the host relaunches on demand.
+__global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
+                                                            unsigned long long idle_ticks,
+                                                            unsigned long long life_ticks) {
+  __shared__ int32_t s_key[kWaves][kSlots];
+  __shared__ uint32_t s_val[kWaves][kSlots];
+  __shared__ uint32_t s_pos[kWaves][kSlots];
+  __shared__ int64_t s_seg[kWaves][kMaxSeeds + 1];
+  __shared__ int64_t s_row[kWaves][kMaxSeeds];
+  __shared__ long long s_stage64[kLoopStage / 2];  // (8-byte aligned: q_ptr is int64)
+  __shared__ int32_t s_out[kLoopOut];
+  int32_t* s_stage = (int32_t*)s_stage64;
+  __shared__ unsigned s_cmd, s_seq;
+  __shared__ ServeReq s_req;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  unsigned last = 0;
+  const unsigned long long t0 = wall_clock64();
+  unsigned long long t_last = t0;
+  if (tid == 0) {
+    last = ld_sys(&mail->done_seq);
+    st_sys(&mail->alive, 1u);
+  }
+  while (true) {
+    if (tid == 0) {
+      unsigned cmd = 0;
+      for (unsigned n = 0;; ++n) {
+        const unsigned r = ld_sys(&mail->req_seq);
+        if (r != last) {
+          cmd = 1;
+          s_seq = r;
+          break;
+        }
+        if ((n & 15u) == 15u) {
+          if (ld_sys(&mail->stop) != 0u) break;
+          const unsigned long long now = wall_clock64();
+          if (now - t_last > idle_ticks || now - t0 > life_ticks) break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (cmd) {
+        __hip_atomic_store(&mail->t_seen, wall_clock64(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);  // (instrumentation: device clock)
+        const unsigned long long* src = (const unsigned long long*)&mail->req;
+        unsigned long long* dst = (unsigned long long*)&s_req;
+        for (int i = 0; i < (int)(sizeof(ServeReq) / 8); ++i)
+          dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      s_cmd = cmd;
+    }
+    __syncthreads();
+    if (s_cmd == 0u) break;
+    const ServeReq rq = s_req;
+    // stage [q_ptr (B + 1 int64) | seeds] (contiguous in the payload; the host keeps every
+    // request within the stage) in LDS: one round of system-scope loads, which bypass the
+    // caches (the payload buffer is rewritten by the host for every request)
+    const long long words = 2 * (rq.B + 1) + rq.n_seeds;
+    {
+      const int32_t* src = (const int32_t*)rq.q_ptr;
+      for (long long i = tid; i < words && i < kLoopStage; i += 64 * kWaves)
+        s_stage[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    const long long* qp = (const long long*)s_stage;
+    const int32_t* sd = s_stage + 2 * (rq.B + 1);
+    const long long ow = rq.B * (rq.k + 1);
+    for (long long b = w; b < rq.B; b += kWaves) {
+      const long long q0 = qp[b], q1 = qp[b + 1];
+      serve_query_wave(rq.row_ptr, rq.cons, rq.srank, rq.is_key, rq.n_items, sd, q0, q1, rq.k,
+                       s_out + b * (long long)(rq.k + 1), s_key[w], s_val[w], s_pos[w],
+                       s_seg[w], s_row[w], lane);
+    }
+    __syncthreads();
+    // results out with system-scope (write-through) stores, drained before the done word
+    for (long long i = tid; i < ow && i < kLoopOut; i += 64 * kWaves)
+      __hip_atomic_store(rq.out + i, s_out[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      last = s_seq;
+      t_last = wall_clock64();
+      __hip_atomic_store(&mail->t_done, t_last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      st_sys(&mail->done_seq, last);
+    }
+  }
+  if (tid == 0) st_sys(&mail->alive, 0u);
+}
+
 }  // namespace
 
 void serve_topk_big(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,
@@ -390,6 +514,12 @@ void serve_topk_big(const int64_t* row_ptr, const int32_t* cons, const uint32_t*
   if (nq <= 0) return;
   hipLaunchKernelGGL(k_serve_topk_big, dim3((unsigned)nq), dim3(kBigThreads), 0, s, row_ptr, cons,
                      srank, is_key, n_items, id_cons, id_pos, q_ptr, seeds, qlist, k, out);
+  KMLS_HIP(hipGetLastError());
+}
+
+void serve_loop_launch(ServeMail* mail, unsigned long long idle_ticks,
+                       unsigned long long life_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(k_serve_loop, dim3(1), dim3(64 * kWaves), 0, s, mail, idle_ticks, life_ticks);
   KMLS_HIP(hipGetLastError());
 }
 
@@ -407,9 +537,248 @@ void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_
 
 namespace gpu {
 
+// ---- the persistent serving loop ----
+namespace {
+std::mutex g_loops_mu;
+std::vector<std::unique_ptr<GpuServeLoop>> g_loops;  // by device (never destroyed before exit)
+std::vector<int> g_pending_pause;                     // pauses requested before a loop existed
+}  // namespace
+
+GpuServeLoop& GpuServeLoop::for_device(int device) {
+  std::lock_guard<std::mutex> lk(g_loops_mu);
+  if ((int)g_loops.size() <= device) g_loops.resize((size_t)device + 1);
+  if (!g_loops[(size_t)device]) {
+    g_loops[(size_t)device].reset(new GpuServeLoop(device));
+    if ((int)g_pending_pause.size() > device) g_loops[(size_t)device]->paused_ = g_pending_pause[(size_t)device];
+  }
+  return *g_loops[(size_t)device];
+}
+
+ServeLoopPause::ServeLoopPause(int dev) : device(dev) {
+  GpuServeLoop* l = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_loops_mu);
+    if ((int)g_loops.size() > dev && g_loops[(size_t)dev]) l = g_loops[(size_t)dev].get();
+    else {
+      if ((int)g_pending_pause.size() <= dev) g_pending_pause.resize((size_t)dev + 1, 0);
+      ++g_pending_pause[(size_t)dev];
+    }
+  }
+  if (l) l->pause();
+}
+
+ServeLoopPause::~ServeLoopPause() {
+  GpuServeLoop* l = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_loops_mu);
+    if ((int)g_loops.size() > device && g_loops[(size_t)device]) l = g_loops[(size_t)device].get();
+    else if ((int)g_pending_pause.size() > device) --g_pending_pause[(size_t)device];
+  }
+  if (l) l->resume();
+}
+
+GpuServeLoop::GpuServeLoop(int device) : device_(device) {
+  KMLS_HIP(hipSetDevice(device));
+  hipStream_t st;
+  KMLS_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  stream_ = (void*)st;
+  KMLS_HIP(hipHostMalloc(&mail_, sizeof(kern::ServeMail), hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(mail_, 0, sizeof(kern::ServeMail));
+  int khz = 0;
+  KMLS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+  const unsigned long long per_ms = (unsigned long long)std::max(khz, 1);
+  ticks_per_us_ = (double)per_ms / 1000.0;
+  idle_ticks_ = per_ms * 20;     // 20 ms without a request: exit (relaunched on demand)
+  life_ticks_ = per_ms * 2000;   // and at most 2 s per launch
+}
+
+GpuServeLoop::~GpuServeLoop() {
+  try {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_and_wait();
+  } catch (...) {
+  }
+  if (buf_) (void)hipHostFree(buf_);
+  if (mail_) (void)hipHostFree(mail_);
+  if (stream_) (void)hipStreamDestroy((hipStream_t)stream_);
+}
+
+void GpuServeLoop::stop_and_wait() {
+  if (!launched_) return;
+  volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
+  m->stop = 1u;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_));  // the kernel exits within one poll
+  launched_ = false;
+}
+
+bool GpuServeLoop::ensure_running() {
+  volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
+  if (launched_ && m->alive != 0u) return true;
+  if (launched_) {  // exited (idle / lifetime) or about to: let it finish, then relaunch
+    KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_));
+    launched_ = false;
+  }
+  m->stop = 0u;
+  m->alive = 0u;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  kmls::kern::ServeMail* dm = nullptr;
+  KMLS_HIP(hipHostGetDevicePointer((void**)&dm, mail_, 0));
+  kern::serve_loop_launch(dm, idle_ticks_, life_ticks_, (hipStream_t)stream_);
+  launched_ = true;
+  ++st_.launches;
+  return true;
+}
+
+void GpuServeLoop::pause() {
+  std::lock_guard<std::mutex> lk(mu_);
+  ++paused_;
+  stop_and_wait();
+}
+
+void GpuServeLoop::resume() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (paused_ > 0) --paused_;
+}
+
+ServeLoopStats GpuServeLoop::stats() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return st_;
+}
+
+bool GpuServeLoop::run(const int64_t* d_row_ptr, const int32_t* d_cons, const uint32_t* d_score,
+                       const uint8_t* d_is_key, int64_t n_items, const int64_t* q_ptr, int64_t B,
+                       const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n) {
+  // one round trip holds what the kernel stages in LDS: split longer batches
+  int64_t b0 = 0;
+  while (b0 < B) {
+    int64_t b1 = b0;
+    while (b1 < B) {
+      const int64_t nb = b1 + 1 - b0;
+      if (2 * (nb + 1) + (q_ptr[b1 + 1] - q_ptr[b0]) > kern::kServeLoopStage ||
+          nb * (k + 1) > kern::kServeLoopOut)
+        break;
+      ++b1;
+    }
+    if (b1 == b0) {  // one query past the stage (hundreds of seeds): not the loop's
+      out_n[b0] = -2;
+      for (int j = 0; j < k; ++j) out_ids[b0 * k + j] = -1;
+      ++b0;
+      continue;
+    }
+    if (!run_one(d_row_ptr, d_cons, d_score, d_is_key, n_items, q_ptr + b0, b1 - b0, seeds, k,
+                 out_ids + b0 * k, out_n + b0))
+      return false;
+    b0 = b1;
+  }
+  return true;
+}
+
+bool GpuServeLoop::run_one(const int64_t* d_row_ptr, const int32_t* d_cons,
+                           const uint32_t* d_score, const uint8_t* d_is_key, int64_t n_items,
+                           const int64_t* q_ptr, int64_t B, const int32_t* seeds, int k,
+                           int32_t* out_ids, int32_t* out_n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (paused_ > 0 || B <= 0) {
+    ++st_.refused;
+    return false;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  KMLS_HIP(hipSetDevice(device_));
+  const int64_t ns = q_ptr[B] - q_ptr[0];
+  const int64_t no = B * (int64_t)(k + 1);
+  const int64_t words = 2 * (B + 1) + ns + no;
+  if (words > cap_) {  // grow: the kernel must not hold the old buffer
+    stop_and_wait();
+    if (buf_) KMLS_HIP(hipHostFree(buf_));
+    buf_ = nullptr;
+    cap_ = std::max<int64_t>(words, std::max<int64_t>(cap_ * 2, 1 << 16));
+    KMLS_HIP(hipHostMalloc((void**)&buf_, (size_t)cap_ * sizeof(int32_t),
+                           hipHostMallocMapped | hipHostMallocCoherent));
+  }
+  int64_t* hq = reinterpret_cast<int64_t*>(buf_);
+  int32_t* hs = buf_ + 2 * (B + 1);
+  int32_t* ho = hs + ns;
+  for (int64_t i = 0; i <= B; ++i) hq[i] = q_ptr[i] - q_ptr[0];
+  std::copy(seeds + q_ptr[0], seeds + q_ptr[B], hs);
+  int32_t* dev = nullptr;
+  KMLS_HIP(hipHostGetDevicePointer((void**)&dev, buf_, 0));
+  volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
+  kern::ServeReq rq;
+  rq.row_ptr = d_row_ptr;
+  rq.cons = d_cons;
+  rq.srank = d_score;
+  rq.is_key = d_is_key;
+  rq.n_items = n_items;
+  rq.q_ptr = reinterpret_cast<const long long*>(dev);
+  rq.seeds = dev + 2 * (B + 1);
+  rq.out = dev + 2 * (B + 1) + ns;
+  rq.B = B;
+  rq.k = k;
+  rq.n_seeds = ns;
+  std::memcpy((void*)&m->req, &rq, sizeof rq);
+  for (int64_t i = 0; i < B; ++i) ho[i * (k + 1)] = -3;  // (never a real answer)
+  ensure_running();
+  const unsigned seq = ++seq_;
+  std::atomic_thread_fence(std::memory_order_seq_cst);  // descriptor and payload before the word
+  m->req_seq = seq;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  // wait for the done word; a kernel that exited meanwhile (idle race) is relaunched once
+  const auto t_start = std::chrono::steady_clock::now();
+  bool relaunched = false;
+  for (unsigned n = 0;; ++n) {
+    if (m->done_seq == seq) break;
+    if ((n & 1023u) == 1023u) {
+      if (m->alive == 0u && !relaunched && m->done_seq != seq) {
+        KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_));  // it has exited
+        launched_ = false;
+        ensure_running();
+        relaunched = true;
+      }
+      if (std::chrono::steady_clock::now() - t_start > std::chrono::milliseconds(500)) {
+        stop_and_wait();  // lost: the next batch relaunches; this one is answered elsewhere
+        ++st_.refused;
+        return false;
+      }
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  for (int64_t b = 0; b < B; ++b) {
+    const int32_t n = ho[b * (k + 1)];
+    out_n[b] = n;
+    for (int j = 0; j < k; ++j) out_ids[b * k + j] = (j < n) ? ho[b * (k + 1) + 1 + j] : -1;
+  }
+  const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  st_.kernel_us += (double)(m->t_done - m->t_seen) / ticks_per_us_;
+  ++st_.requests;
+  st_.queries += (uint64_t)B;
+  st_.last_us = us;
+  st_.sum_us += us;
+  return true;
+}
+
+int64_t GpuRuleIndex::merged_size(const int32_t* seeds, int64_t n) const {
+  int64_t acc = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t sd = seeds[i];
+    if (sd >= 0 && sd < n_items_ && h_is_key_[(size_t)sd])
+      acc += h_row_ptr_[(size_t)sd + 1] - h_row_ptr_[(size_t)sd];
+  }
+  return acc;
+}
+
+bool GpuRuleIndex::query_loop(const int64_t* q_ptr, int64_t B, const int32_t* seeds, int k,
+                              int32_t* out_ids, int32_t* out_n) {
+  KMLS_CHECK(k >= 0 && k <= 256, "query_loop: 0 <= k <= 256");
+  return GpuServeLoop::for_device(device_).run(d_row_ptr_, d_cons_, d_score_, d_is_key_, n_items_,
+                                               q_ptr, B, seeds, k, out_ids, out_n);
+}
+
 GpuRuleIndex::GpuRuleIndex(int device, const RuleIndex& host, uintptr_t stream)
     : device_(device), n_items_(host.n_items()), nnz_(host.nnz()) {
   KMLS_HIP(hipSetDevice(device));
+  ServeLoopPause pause(device);  // allocation calls must not wait behind the serving kernel
   if (stream) {
     stream_ = (void*)stream;
   } else {
@@ -482,6 +851,7 @@ GpuRuleIndex::GpuRuleIndex(int device, const RuleIndex& host, uintptr_t stream)
 
 GpuRuleIndex::~GpuRuleIndex() {
   (void)hipSetDevice(device_);
+  ServeLoopPause pause(device_);  // (frees must not wait behind the serving kernel)
   for (void* p : {(void*)d_row_ptr_, (void*)d_cons_, (void*)d_score_, (void*)d_is_key_,
                   (void*)d_id_cons_, (void*)d_id_pos_})
     if (p) (void)hipFree(p);

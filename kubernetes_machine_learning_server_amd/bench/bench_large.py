@@ -209,8 +209,10 @@ def rule_map_main(args) -> int:
     N = native.require_gpu()
     dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    if world > 1:
+    own_group = False
+    if world > 1 and not dist.is_initialized():  # (bench.py calls in with its group up)
         import datetime
+        own_group = True
         backend = os.environ.get("KMLS_BENCH_DIST", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev),
@@ -373,10 +375,23 @@ def rule_map_main(args) -> int:
                 out[f"query_batch{B}_us"] = {"cpp": round(res["cpp"][0], 1),
                                              "hip": round(res["hip"][0], 1), "same": same}
             del gidx
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        if not getattr(args, "quiet", False):
+            print(json.dumps(out), flush=True)
+    if world > 1 and own_group:
         dist.destroy_process_group()
+    args.result = out
     return 0
+
+
+def run_rule_map(shape: str = "100Mx1M", min_support: float = 2e-4, steps: int = 3,
+                 warmup: int = 1, n_tx: int = 0, seed: int = 0, verify_rows: int = 64) -> dict:
+    """``rule_map_main`` as a function (bench.py's config-5 section): every rank of the caller's
+    process group (or one process) generates its shard and times ``DistRuleMap.step``; the
+    result dict (complete on rank 0) is returned instead of printed."""
+    ns = argparse.Namespace(shape=shape, n_tx=n_tx, min_support=min_support, steps=steps,
+                            warmup=warmup, seed=seed, verify_rows=verify_rows, quiet=True)
+    rule_map_main(ns)
+    return ns.result
 
 
 if __name__ == "__main__":

@@ -440,9 +440,12 @@ def run_serve_bench(base: pathlib.Path, backend: str, qps_list, duration: float,
         res["gpu_index"] = ready.get("gpu_index")
         res["gpu_min_batch"] = ready.get("gpu_min_batch")
         res["crossover_us"] = ready.get("crossover_us")
+        res["gpu_min_merge"] = ready.get("gpu_min_merge")
+        res["loop_crossover_us"] = ready.get("loop_crossover_us")
         if verbose:
             print(json.dumps({"bench": "serve_ready", **{k: res[k] for k in
-                  ("backend", "gpu_index", "gpu_min_batch", "crossover_us")}}), flush=True)
+                  ("backend", "gpu_index", "gpu_min_batch", "crossover_us", "gpu_min_merge",
+                   "loop_crossover_us")}}), flush=True)
         # warm-up
         if client == "native":
             measure_native(port, 500, 1.0, queries, connections)

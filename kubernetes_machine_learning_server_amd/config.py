@@ -3,7 +3,7 @@
 Every variable name and default of the reference is kept, including the API's ``PICKLE_DIR``
 vs the job's ``PICKLES_FOLDER`` (``machine-learning/main.py:17-47``,
 ``rest_api/app/main.py:31-47``).  New knobs: ``MINER`` (gpu|cpu|oracle), ``RULES_MODE``
-(full|pairs), ``NUM_GPUS``, ``SERVE_BACKEND`` (auto|hip|cpu), ``BATCH_MAX``, ``BATCH_WAIT_US``,
+(full|pairs), ``NUM_GPUS``, ``SERVE_BACKEND`` (auto|hip|loop|cpu), ``BATCH_MAX``, ``BATCH_WAIT_US``,
 ``MIN_CONFIDENCE``, ``KMLS_FAULT`` (fault injection, tests only).
 """
 from __future__ import annotations
@@ -111,7 +111,9 @@ class ApiSettings:
     best_tracks_file: str
     data_invalidation_file: str
     app_path_from_root: Optional[pathlib.Path]
-    serve_backend: str = "auto"   # auto | hip | cpu
+    # auto | hip (every batch through the batch kernels) | loop (queries up to the wave matcher's
+    # merge size through the persistent serving kernel) | cpu | python
+    serve_backend: str = "auto"
     batch_max: int = 256
     batch_wait_us: int = 200
     gpu_min_batch: int = 16       # below this a batch is answered by the C++ CPU matcher

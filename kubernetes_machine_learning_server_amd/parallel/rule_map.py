@@ -151,8 +151,9 @@ class _Gpu:
                 gram[F:] = 0
             self.method = "none"
             if F:
-                if self.g.cooc_preferred() and self.g.pair_counts_csr(gram.data_ptr(), F):
-                    self.g.cooc_check()  # entry overflow / duplicate rows: fail, not drop pairs
+                # the cost model from the supports (no statistics pass over the CSR); a
+                # transaction past the count's entry buffer sends the call to the bit-GEMM
+                if self.g.cooc_likely() and self.g.pair_counts_csr_direct(gram.data_ptr(), F):
                     self.method = "cooc"
                     self.held.pop("bm", None)
                 else:

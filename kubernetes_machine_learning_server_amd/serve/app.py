@@ -87,8 +87,8 @@ def _gpu_factory(cfg: ApiSettings):
         return None
     from ..ops import native
     if not native.gpu_available():
-        if cfg.serve_backend == "hip":
-            raise RuntimeError("SERVE_BACKEND=hip but no HIP device is visible")
+        if cfg.serve_backend in ("hip", "loop"):
+            raise RuntimeError(f"SERVE_BACKEND={cfg.serve_backend} but no HIP device is visible")
         return None
     N = native.load()
     dev = int(os.environ.get("KMLS_DEVICE", "0"))
@@ -237,7 +237,9 @@ def create_app(cfg: Optional[ApiSettings] = None, native_front: bool = False) ->
         return {"ready": True, "model_date": snap.marker, "keys": snap.index.n_keys,
                 "source": snap.source, "gpu_index": snap.gpu_index is not None,
                 "gpu_min_batch": snap.gpu_min_batch,
-                "crossover_us": {str(b): v for b, v in (snap.crossover or {}).items()}}
+                "crossover_us": {str(b): v for b, v in (snap.crossover or {}).items()},
+                "gpu_min_merge": snap.gpu_min_merge,
+                "loop_crossover_us": dict(snap.loop_crossover or {})}
 
     @app.get("/metrics", include_in_schema=False)
     def prometheus_metrics():

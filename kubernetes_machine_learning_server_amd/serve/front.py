@@ -52,8 +52,10 @@ class NativeFront:
         names = list(idx.names) if idx.names is not None else [str(i) for i in range(idx.n_items)]
         gpu = snap.gpu_index if (snap.gpu_index is not None and
                                  isinstance(snap.gpu_index, self.N.GpuRuleIndex)) else None
+        gmm = getattr(snap, "gpu_min_merge", None)
         self.front.set_model(idx.native(), names, snap.best_track_names, snap.marker, gpu,
-                             int(snap.gpu_min_batch or 0) if gpu is not None else 0)
+                             int(snap.gpu_min_batch or 0) if gpu is not None else 0,
+                             int(gmm) if (gpu is not None and gmm is not None) else -1)
 
     # -- ASGI bridge for the slow path ----------------------------------------------------------
     def _drain(self) -> None:

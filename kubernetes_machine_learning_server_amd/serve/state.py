@@ -43,6 +43,10 @@ class ModelSnapshot:  # immutable; _py_rec (python backend cache) is set once vi
     # when the snapshot is built; None = the GPU never wins, every batch stays on the CPU)
     gpu_min_batch: Optional[int] = None
     crossover: Any = None  # the measurement behind gpu_min_batch
+    # persistent serving kernel: queries whose merged rows hold >= this many entries (up to the
+    # wave matcher's 512) go to it one by one (None = off); and the measurement behind it
+    gpu_min_merge: Optional[int] = None
+    loop_crossover: Any = None
 
     @property
     def best_track_names(self) -> List[str]:
@@ -121,6 +125,60 @@ def measure_crossover(index, gpu_index, k: int = 10, reps: int = 5, seed: int = 
     return best, res
 
 
+MERGE_BINS = ((1, 32), (32, 64), (64, 128), (128, 256), (256, 513))
+
+
+def measure_loop(index, gpu_index, k: int = 10, per_bin: int = 24, seed: int = 0):
+    """Per-query latency of the C++ matcher against the persistent serving kernel
+    (``GpuRuleIndex.query_loop``: one request, one round trip) by merged-row size: returns (the
+    smallest merged size from which the loop answers every larger bin at least as fast, or None;
+    {bin: (cpu_us, loop_us, queries)}).  The native front then sends a query to the loop when
+    its merged rows reach that size (SERVE_BACKEND=auto)."""
+    import numpy as np
+    keys = np.nonzero(index.is_key)[0].astype(np.int32)
+    if len(keys) == 0:
+        return None, {}
+    rp = np.asarray(index.row_ptr)
+    rl = rp[keys + 1] - rp[keys]
+    rng = np.random.default_rng(seed)
+    host = index.native()
+    res = {}
+    for lo, hi in MERGE_BINS:
+        qs = []
+        for _ in range(4000):
+            n = int(rng.integers(1, 6))
+            pick = rng.integers(0, len(keys), n)
+            if lo <= int(rl[pick].sum()) < hi:
+                qs.append(keys[pick])
+            if len(qs) >= per_bin:
+                break
+        if not qs:
+            continue
+        tc, tg = [], []
+        for q in qs:
+            q_ptr = np.array([0, len(q)], np.int64)
+            if not gpu_index.query_loop(q_ptr, q, k)[2]:
+                return None, {}
+            t0 = time.perf_counter()
+            host.query_batch(q_ptr, q, k)
+            tc.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            gpu_index.query_loop(q_ptr, q, k)
+            tg.append(time.perf_counter() - t0)
+        res[f"{lo}-{hi - 1}"] = (round(float(np.median(tc)) * 1e6, 2),
+                                 round(float(np.median(tg)) * 1e6, 2), len(qs))
+    best = None
+    for (lo, hi) in reversed(MERGE_BINS):  # the suffix of bins where the loop is no slower
+        r = res.get(f"{lo}-{hi - 1}")
+        if r is None:
+            continue
+        if r[1] <= r[0]:
+            best = lo
+        else:
+            break
+    return best, res
+
+
 class ReloadManager:
     """Owns the current snapshot; thread-safe reload with single-assignment swap."""
 
@@ -178,12 +236,15 @@ class ReloadManager:
         try:
             best, index, source = read_pickle_dict(self.cfg)
             gpu_index = self._gpu_factory(index) if self._gpu_factory else None
-            gmb, cross = None, None
+            gmb, cross, gmm, lcross = None, None, None, None
             if gpu_index is not None:
                 if self.cfg.serve_backend == "hip":  # forced: every batch on the GPU
                     gmb = 1
+                elif self.cfg.serve_backend == "loop":  # forced: the serving kernel
+                    gmm = 0
                 else:
                     gmb, cross = measure_crossover(index, gpu_index)
+                    gmm, lcross = measure_loop(index, gpu_index)
         except Exception as e:  # keep serving the previous snapshot; retry next tick
             self.failed_reloads += 1
             self.last_error = f"{type(e).__name__}: {e}"
@@ -192,10 +253,12 @@ class ReloadManager:
         # the marker may have moved while we were reading: re-read, and only commit the value
         # we read BEFORE loading (a later change triggers another reload next tick)
         snap = ModelSnapshot(best, index, marker, time.time(), index.n_keys, source, gpu_index,
-                             gmb, cross)
+                             gmb, cross, gmm, lcross)
         if gpu_index is not None:
             logger.info(f"HIP matcher crossover: batches >= {gmb} go to the GPU" if gmb else
                         "HIP matcher never beats the C++ matcher on this index: CPU only")
+            if gmm is not None:
+                logger.info(f"HIP serving loop: queries merging >= {gmm} entries go to the GPU")
         self.snapshot = snap  # single reference assignment = atomic swap
         for fn in list(self.listeners):
             try:

@@ -1,0 +1,110 @@
+"""The persistent serving kernel (csrc/kernels/serve.hip k_serve_loop, gpu::GpuServeLoop): every
+answer equals the C++ matcher's (the reference matcher semantics, rest_api/app/main.py:224-254),
+across idle exits and relaunches, pauses for index builds, and a reload that swaps the index
+while the loop keeps serving."""
+import time
+
+import numpy as np
+import pytest
+
+from kubernetes_machine_learning_server_amd.data.synthetic import generate
+
+pytestmark = pytest.mark.gpu
+
+
+def _index(gpu_mod, shape="ds1", ms=0.03, seed=0):
+    from kubernetes_machine_learning_server_amd.serve.index import build_index_from_trie
+    tx = generate(shape, seed=seed)
+    r = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms, 2)
+    idx = build_index_from_trie(r["parent"], r["item"], r["count"], r["depth"], tx.n_tx,
+                                tx.n_items)
+    return idx
+
+
+def _queries(rng, keys, B, n_items, lo=1, hi=6):
+    lens = rng.integers(lo, hi, size=B)
+    q_ptr = np.zeros(B + 1, np.int64)
+    np.cumsum(lens, out=q_ptr[1:])
+    seeds = keys[rng.integers(0, len(keys), int(q_ptr[-1]))].astype(np.int32)
+    # some unknown ids and non-keys too
+    bad = rng.random(len(seeds)) < 0.05
+    seeds[bad] = rng.integers(-1, n_items, int(bad.sum()))
+    return q_ptr, seeds
+
+
+def _check(host, gidx, q_ptr, seeds, k=10):
+    ids, n, ok = gidx.query_loop(q_ptr, seeds, k)
+    assert ok
+    cids, cn = host.query_batch(q_ptr, seeds, k)
+    ids, n, cids, cn = map(np.asarray, (ids, n, cids, cn))
+    small = n != -2  # merged rows past the wave table: the caller answers those
+    assert (n[small] == cn[small]).all()
+    for b in np.flatnonzero(small):
+        assert (ids[b, :max(n[b], 0)] == cids[b, :max(cn[b], 0)]).all()
+    return int(small.sum())
+
+
+def test_serve_loop_matches_cpp_matcher(gpu_mod):
+    idx = _index(gpu_mod)
+    host = idx.native()
+    gidx = gpu_mod.GpuRuleIndex(0, host)
+    keys = np.flatnonzero(idx.is_key).astype(np.int32)
+    rng = np.random.default_rng(0)
+    answered = 0
+    for B in (1, 3, 17, 64, 300):
+        for _ in range(5):
+            q_ptr, seeds = _queries(rng, keys, B, idx.n_items)
+            answered += _check(host, gidx, q_ptr, seeds)
+    assert answered > 1000
+    st = gpu_mod.serve_loop_stats(0)
+    assert st["requests"] >= 25 and st["launches"] >= 1
+    # many back-to-back single-query requests: one kernel serves them all (no launch each)
+    l0 = gpu_mod.serve_loop_stats(0)["launches"]
+    t0 = time.perf_counter()
+    for i in range(400):
+        q_ptr, seeds = _queries(rng, keys, 1, idx.n_items)
+        _check(host, gidx, q_ptr, seeds)
+    dt = (time.perf_counter() - t0) / 400
+    st = gpu_mod.serve_loop_stats(0)
+    assert st["launches"] - l0 <= 2, st
+    print(f"\n[serve_loop] single-query round trip incl. host checks: {dt * 1e6:.1f} us, "
+          f"loop mean {st['mean_us']:.1f} us, kernel {st['kernel_mean_us']:.1f} us")
+
+
+def test_serve_loop_idle_exit_relaunch_and_pause(gpu_mod):
+    idx = _index(gpu_mod, seed=1)
+    host = idx.native()
+    gidx = gpu_mod.GpuRuleIndex(0, host)
+    keys = np.flatnonzero(idx.is_key).astype(np.int32)
+    rng = np.random.default_rng(1)
+    q_ptr, seeds = _queries(rng, keys, 8, idx.n_items)
+    _check(host, gidx, q_ptr, seeds)
+    l0 = gpu_mod.serve_loop_stats(0)["launches"]
+    time.sleep(0.1)  # past the loop's idle limit: the kernel has exited
+    _check(host, gidx, q_ptr, seeds)
+    assert gpu_mod.serve_loop_stats(0)["launches"] == l0 + 1
+    gpu_mod.serve_loop_pause(0, True)
+    _, _, ok = gidx.query_loop(q_ptr, seeds, 10)
+    assert not ok  # paused: nothing answered, the caller uses the C++ matcher
+    gpu_mod.serve_loop_pause(0, False)
+    _check(host, gidx, q_ptr, seeds)
+
+
+def test_serve_loop_across_an_index_reload(gpu_mod):
+    """A second index built while the first is being served (its construction pauses the
+    loop), both answered correctly afterwards, and the first one freed while the loop runs."""
+    a = _index(gpu_mod, seed=2)
+    b = _index(gpu_mod, "ds2_weak", 0.05, seed=3)
+    ha, hb = a.native(), b.native()
+    ga = gpu_mod.GpuRuleIndex(0, ha)
+    rng = np.random.default_rng(2)
+    ka = np.flatnonzero(a.is_key).astype(np.int32)
+    kb = np.flatnonzero(b.is_key).astype(np.int32)
+    q, s = _queries(rng, ka, 32, a.n_items)
+    _check(ha, ga, q, s)
+    gb = gpu_mod.GpuRuleIndex(0, hb)
+    q2, s2 = _queries(rng, kb, 32, b.n_items)
+    _check(hb, gb, q2, s2)
+    _check(ha, ga, q, s)
+    del ga
+    _check(hb, gb, q2, s2)
