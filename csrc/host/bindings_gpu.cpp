@@ -49,6 +49,14 @@ py::dict result_to_dict(gpu::GpuMineResult&& r) {
   s["level2_method"] = r.level2_method;
   s["cooc_pairs"] = r.cooc_pairs;
   s["level2_comm"] = r.level2_comm;
+  if (r.hl_tx_kept >= 0) {
+    py::dict h;
+    h["tx_kept"] = r.hl_tx_kept;
+    h["nnz_kept"] = r.hl_nnz_kept;
+    h["per_level"] = r.hl_per_level;
+    h["hits"] = r.hl_hits;
+    s["horizontal"] = h;
+  }
   py::dict ph;
   for (auto& p : r.phases) ph[py::str(p.name)] = p.ms;
   s["phases_ms"] = ph;

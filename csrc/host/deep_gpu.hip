@@ -5,10 +5,12 @@
 //
 // Call sequence (one rank = one GPU; every rank runs the same prologue on the full data):
 //   supports -> selection -> bitmaps [F][Wp] -> transposed root block ->
-//   level-2 classes (deterministic: count pass, host scan, fill pass) -> this rank's share of the
-//   level-3 tasks (task t = (root i, member k) goes to rank t % world) ->
-//   rounds of k_deep_count (ticket dequeue, per-task step budget, spills become the next round's
-//   tasks) until no task is left -> per-size counts + digest, all-reduced over the ranks.
+//   level-2 classes (the popcount gram read by a count pass, a device prefix scan, a fill pass
+//   over the surviving groups only) -> every level-3 task's cost probed on the device, the tasks
+//   cost-ordered and dealt to the ranks in a snake (deep_order.hip) -> one stealing launch of
+//   k_deep_count over this rank's share (idle waves take open classes from busy ones) ->
+//   per-size counts + digest, all-reduced over the ranks.  Emit mode writes a node arena instead,
+//   compacted into a parent-first trie on the device (deep_trie.hip).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -1111,6 +1111,37 @@ bool GpuMiner::cooc_cheaper(int64_t F, int64_t Wp, int64_t nnz, const CoocStats&
 // 2(N-1)/N), each rank keeps the frequent upper entries of its rows, and one all-gather of those
 // (row, col, count) triples — a few thousand at configs 3/5 — rebuilds on every rank a dense gram
 // holding only the frequent pairs (the level loop reads gram[a][b] >= minsup, nothing else).
+// Horizontal levels instead of bitmaps: the shard is long (>= 1024 bitmap words, as for the
+// level-2 cooc choice) and the cost model picks the horizontal pair count.  Every tx-DP rank must
+// take the same path (the two run different collectives): the shard votes are all-reduced.
+// KMLS_HLEVELS=0 (or test hook hlevels=0) keeps the bitmap levels.
+bool GpuMiner::hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* comm) {
+  static const long long env_dflt = [] {
+    const char* e = std::getenv("KMLS_HLEVELS");
+    return e ? std::atoll(e) : 1ll;
+  }();
+  bool want = test_hook("hlevels", env_dflt) != 0 && cfg.level2_gram && F >= 2 &&
+              F <= 32768 && Wp >= 1024 && test_hook("cooc", 1) != 0 && !subset_active();
+  if (want) {
+    const CoocStats st = cooc_stats();
+    want = st.max_k <= (uint64_t)kern::cooc_max_k() &&
+           (test_hook("cooc", 1) == 2 || cooc_cheaper(F, Wp, nnz_, st));
+  }
+  if (comm && comm->world() > 1) {
+    hipStream_t s = (hipStream_t)stream_;
+    const size_t mark = arena_->mark();
+    uint32_t* d = (uint32_t*)arena_->push(256);
+    const uint32_t v = want ? 1u : 0u;
+    KMLS_HIP(hipMemcpyAsync(d, &v, 4, hipMemcpyHostToDevice, s));
+    comm->all_reduce(d, d, 1, CommDtype::U32, false, s);
+    KMLS_HIP(hipMemcpyAsync(h_scalar_, d, 4, hipMemcpyDeviceToHost, s));
+    comm->wait_stream(s);
+    arena_->pop_to(mark);
+    want = (int)((uint32_t*)h_scalar_)[0] == comm->world();
+  }
+  return want;
+}
+
 void GpuMiner::txdp_gram_combine(uint32_t* gram, int64_t F, int64_t per, uint32_t minsup) {
   hipStream_t s = (hipStream_t)stream_;
   const int W = comm_->world(), R = comm_->rank();
@@ -1488,16 +1519,24 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       // sparse large data: count the pairs where they occur (cooc.hip) when the cost model says
       // so (only for bitmaps of this miner's own CSR shard: mine_txdp / the host path of mine)
       bool sparse = false;
-      if (gram_csr_ok_ && Wp >= 1024 && test_hook("cooc", 1) != 0) {
+      if (hl_plan_) {  // decided (globally) before the encode: there is no bitmap
+        sparse = true;
+        res.level2_method = "cooc";
+        res.cooc_pairs = (int64_t)cooc_stats().pairs;
+      } else if (gram_csr_ok_ && Wp >= 1024 && test_hook("cooc", 1) != 0) {
         const CoocStats st = cooc_stats();
         sparse = test_hook("cooc", 1) == 2 || cooc_cheaper(F, Wp, nnz_, st);
         res.level2_method = sparse ? "cooc" : "gram";
         res.cooc_pairs = (int64_t)st.pairs;
       }
       if (!(sparse && pair_counts_csr((uintptr_t)gram, F))) {
+        if (hl_plan_) throw std::logic_error("kmls: horizontal plan but cooc declined");
         if (sparse) res.level2_method = "gram (cooc declined)";
         KMLS_HIP(hipMemsetAsync(gram, 0, (size_t)F * F * sizeof(uint32_t), s));
-        // matrix cores for long rows (large T): the int8 MFMA path moves 8x more MACs per byte
+        // matrix cores for long rows (large T): the masked-nibble FP4 MFMA gram
+        // (v_mfma_scale_f32_32x32x64_f8f6f4, gram_mfma.hip) beats the VALU popcount gram there.
+        // No BASELINE config reaches this branch today: ds1 rows are short (popcount gram),
+        // configs 3 and 5 count pairs horizontally (cooc.hip)
         if (gram_popcount_forced() ? cfg.level2_mfma : (cfg.level2_mfma || Wp >= 4096))
           kern::pair_gram_mfma((const uint64_t*)bm_dev, Wp, F, gram, s);
         else
@@ -1519,7 +1558,40 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     root.gid = d_gid;
     root.row_end = d_end;
     bool done = false;
-    if (comm_ == nullptr && fused_levels_enabled()) {
+    if (hl_plan_) {
+      // levels >= 2 from the gram and a filtered CSR (hlevels.hip): no bitmap anywhere
+      if (!hl_) hl_ = std::make_shared<kern::HLevels>();
+      auto* H = static_cast<kern::HLevels*>(hl_.get());
+      kern::HlInput in{d_tx_ptr_, d_items_, n_tx_, d_rank_of_, d_fmask_, d_ids_, run.gram, F, F,
+                       run.minsup, run.max_len, n_cus_};
+      kern::HlHooks hk;
+      hk.reserve = [&](int64_t n) {
+        run.ensure_out(run.out_size + n);
+        return kern::HlTrieOut{run.out_parent.p, run.out_item.p, run.out_count.p,
+                               run.out_depth.p, run.out_size, nullptr};
+      };
+      hk.commit = [&](int64_t n) {
+        run.out_size += n;
+        run.stream_out();
+      };
+      if (comm_)
+        hk.allreduce = [&](uint32_t* c, int64_t n) {
+          comm_->all_reduce(c, c, (size_t)n, CommDtype::U32, false, s);
+        };
+      hk.wait = [&]() {
+        if (comm_) comm_->wait_stream(s);
+        else KMLS_HIP(hipStreamSynchronize(s));
+      };
+      kern::HlStats hs;
+      H->run(in, hk, s, hs);
+      run.max_depth = hs.max_depth;
+      run.n_candidates = hs.candidates;
+      res.hl_tx_kept = hs.n_tx_kept;
+      res.hl_nnz_kept = hs.nnz_kept;
+      res.hl_per_level = hs.per_level;
+      res.hl_hits = hs.hits;
+      done = true;
+    } else if (comm_ == nullptr && fused_levels_enabled()) {
       // the fused levels take the root rows in descending rank, each owning its pairs with
       // the rows before it (levels.hip header): row r = rank F-1-r, root class of rank F-1-r
       std::vector<int32_t> rrank((size_t)F);
@@ -1543,7 +1615,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       KMLS_HIP(hipStreamSynchronize(s));  // the pageable staging vectors die at scope end
     }
     if (!done) run.process(root, 1, d_len, root_total);
-    res.levels_path = done ? "fused" : (comm_ ? "chunked-txdp" : "chunked");
+    res.levels_path = hl_plan_ ? "horizontal" : done ? "fused" : (comm_ ? "chunked-txdp" : "chunked");
     if (!done && !run.fallback_reason.empty()) res.levels_path += " (fused fallback: " + run.fallback_reason + ")";
     KMLS_HIP(hipStreamSynchronize(s));  // host staging vectors die at scope end
     if (res.level2_method == "cooc") cooc_check();
@@ -2126,13 +2198,16 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download, bool prefetch
   const int64_t F = select(cnt.data(), n_tx_, cfg.min_support);
   KMLS_HIP(hipEventRecord(e1.e, s));
   const int64_t Wp = words_local();
-  const size_t need = (size_t)std::max<int64_t>(F, 1) * Wp * sizeof(uint64_t);
-  if (need > own_bm_bytes_) {
-    if (d_own_bm_) KMLS_HIP(hipFree(d_own_bm_));
-    KMLS_HIP(hipMalloc((void**)&d_own_bm_, need));
-    own_bm_bytes_ = need;
+  const bool hl = hlevels_plan(cfg, F, Wp, nullptr);
+  if (!hl) {
+    const size_t need = (size_t)std::max<int64_t>(F, 1) * Wp * sizeof(uint64_t);
+    if (need > own_bm_bytes_) {
+      if (d_own_bm_) KMLS_HIP(hipFree(d_own_bm_));
+      KMLS_HIP(hipMalloc((void**)&d_own_bm_, need));
+      own_bm_bytes_ = need;
+    }
+    encode_bitmaps_fresh(d_own_bm_, F, Wp);
   }
-  encode_bitmaps_fresh(d_own_bm_, F, Wp);
   KMLS_HIP(hipEventRecord(e2.e, s));
   GpuMineResult r;
   for (int attempt = 0;; ++attempt) {
@@ -2140,10 +2215,10 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download, bool prefetch
     try {
       struct CsrFlag {  // the bitmaps are this miner's own CSR (level-2 cooc allowed)
         bool& f;
-        explicit CsrFlag(bool& x) : f(x) { f = true; }
+        explicit CsrFlag(bool& x, bool v = true) : f(x) { f = v; }
         ~CsrFlag() { f = false; }
-      } flag(gram_csr_ok_);
-      r = mine_bitmaps((uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
+      } flag(gram_csr_ok_), plan(hl_plan_, hl);
+      r = mine_bitmaps(hl ? 0 : (uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
       break;
     } catch (const ArenaExhausted& ex) {
       // a default-sized arena grows (up to its maximum) and the chunked search reruns
@@ -2156,7 +2231,7 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download, bool prefetch
     r.levels_path += " (resident fallback: " + fused_fallback_ + ")";
   std::vector<Phase> ph;
   ph.push_back({"support+select", elapsed(e0, e1)});
-  ph.push_back({"encode_bitmap", elapsed(e1, e2)});
+  ph.push_back({hl ? "cooc_stats" : "encode_bitmap", elapsed(e1, e2)});
   for (auto& p : r.phases) ph.push_back(p);
   r.phases = ph;
   r.stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -2220,32 +2295,38 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
     F = select(cnt.data(), global_n_tx, cfg.min_support);
   }
   KMLS_HIP(hipEventRecord(e1.e, s));
-  // 3. shard-local bitmaps
+  // 3. shard-local bitmaps (none when every level is counted horizontally from the CSR)
   const int64_t Wp = words_local();
-  const size_t need = (size_t)std::max<int64_t>(F, 1) * Wp * sizeof(uint64_t);
-  if (need > own_bm_bytes_) {
-    if (d_own_bm_) KMLS_HIP(hipFree(d_own_bm_));
-    KMLS_HIP(hipMalloc((void**)&d_own_bm_, need));
-    own_bm_bytes_ = need;
+  const bool hl = hlevels_plan(cfg, F, Wp, comm);
+  if (!hl) {
+    const size_t need = (size_t)std::max<int64_t>(F, 1) * Wp * sizeof(uint64_t);
+    if (need > own_bm_bytes_) {
+      if (d_own_bm_) KMLS_HIP(hipFree(d_own_bm_));
+      KMLS_HIP(hipMalloc((void**)&d_own_bm_, need));
+      own_bm_bytes_ = need;
+    }
+    encode_bitmaps_fresh(d_own_bm_, F, Wp);
   }
-  encode_bitmaps_fresh(d_own_bm_, F, Wp);
   KMLS_HIP(hipEventRecord(e2.e, s));
   // 4. level loop with all-reduced candidate counts
   comm_ = comm;
   gram_csr_ok_ = true;
+  hl_plan_ = hl;
   GpuMineResult r;
   try {
-    r = mine_bitmaps((uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
+    r = mine_bitmaps(hl ? 0 : (uintptr_t)d_own_bm_, Wp, cfg, nullptr, true, download);
   } catch (...) {
     comm_ = nullptr;
     gram_csr_ok_ = false;
+    hl_plan_ = false;
     throw;
   }
   comm_ = nullptr;
   gram_csr_ok_ = false;
+  hl_plan_ = false;
   std::vector<Phase> ph;
   ph.push_back({"support_tiles+allreduce+select", elapsed(e0, e1)});
-  ph.push_back({"encode_bitmap", elapsed(e1, e2)});
+  ph.push_back({hl ? "cooc_stats" : "encode_bitmap", elapsed(e1, e2)});
   for (auto& p : r.phases) ph.push_back(p);
   r.phases = ph;
   r.stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -84,6 +84,9 @@ struct GpuMineResult {
   std::string levels_path = "none";  // "fused" | "chunked" | "persistent" | "none"
   std::string level2_method = "gram";  // "gram" (bit-GEMM) | "cooc" (horizontal pair count)
   int64_t cooc_pairs = -1;             // sum_t k_t(k_t-1)/2 of the shard when it was measured
+  // horizontal levels: filtered transactions / items, itemsets and containing-hit totals per size
+  int64_t hl_tx_kept = -1, hl_nnz_kept = -1;
+  std::vector<int64_t> hl_per_level, hl_hits;
   std::string level2_comm = "none";    // tx-DP: how the shard grams were combined
   // rule map (cfg.rule_index): CSR by item id, rows sorted by (count desc, tie key asc); pinned
   int64_t idx_nnz = -1;  // -1: not built
@@ -404,6 +407,12 @@ class GpuMiner {
   std::unique_ptr<GraphCache> graph_;  // steady-state hipGraph of mine_resident
   Comm* comm_ = nullptr;          // set during mine_txdp: level counts are all-reduced
   bool gram_csr_ok_ = false;      // mine_bitmaps' bitmaps are this miner's own CSR shard
+  // horizontal levels (kern::HLevels, hlevels.hip): sparse long shards skip the bitmap encode;
+  // level 2 from the CSR (cooc), levels >= 3 from a filtered CSR
+  std::shared_ptr<void> hl_;
+  bool hl_plan_ = false;          // the current mine_bitmaps call runs without bitmaps
+  bool hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* comm);
+  std::string hl_stats_;          // last horizontal run (JSON-ish summary for the phases)
   void txdp_gram_combine(uint32_t* gram, int64_t F, int64_t per, uint32_t minsup);
   unsigned long long* d_cooc_ = nullptr;  // [3]: cooc stats (pairs, max k) + error flag
   uint64_t sel_gen_ = 0;          // bumped by load_csr / select*: invalidates cached cooc stats

@@ -4,7 +4,7 @@
 // transactions, T <= 4096, i.e. <= 64 bitmap words) at supports where the output has 1e9-1e10
 // itemsets (BASELINE config 2, ds1 @ 0.01-0.02), a level-wise miner cannot hold one level in HBM.
 //
-// Design (one wave = one independent depth-first worker, no inter-wave hand-off inside a launch):
+// Design (one wave = one depth-first worker; idle waves take work from busy ones inside the launch):
 // * A class (prefix P, members P∪{x_k}) lives in a BLOCK: WT bitmap words x `pad` slots stored
 //   word-major ([w][slot]), then one item-hash word per slot.  Lanes that read consecutive
 //   member slots of one word row read contiguous memory, so every bitmap load is coalesced.
@@ -26,9 +26,12 @@
 //   member PAIRS fill up to kCap lanes, so a wave64 instruction still carries 64 candidates when
 //   classes have 5-20 members.  Survivors of one (frame, member) group stay contiguous in the
 //   child block (lane order = pair order), so each group becomes a child frame.
-// * Load balance: tasks are dequeued by ticket.  A wave that exceeds its step budget on one task
-//   SPILLS its remaining frames to a heap as new tasks (big frames split into one task per
-//   member) and the host runs another round; heavy dense subtrees are thus cut into many tasks.
+// * Load balance: tasks are dequeued by ticket, heaviest first (deep_order.hip's cost order).
+//   Steal mode (the default): a wave whose ticket finds the queue drained opens its inbox and
+//   asks busy waves, one mailbox at a time; a busy wave past its step budget that finds a request
+//   in its mailbox hands its bottom (oldest, largest) open class straight to that inbox.  Without
+//   steal mode a wave past its budget SPILLS its frames to a heap as new tasks and the host runs
+//   another round.
 // Counts are exact (popcount of at most 4096 bits per row, u32).
 #include <hip/hip_runtime.h>
 

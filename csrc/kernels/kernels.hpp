@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
+#include <vector>
 
 namespace kmls {
 namespace kern {
@@ -258,6 +260,53 @@ void cooc_stats(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, const
 void cooc_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, const int32_t* rank_of,
                 const uint32_t* fmask, int64_t F, uint32_t* gram, int64_t ld, unsigned* err,
                 int n_cus, hipStream_t s);
+// ---- horizontal levels >= 3 from a filtered CSR (hlevels.hip) ----
+struct HlTrieOut {  // device trie arrays (whole arrays; new nodes go to [base, base + n))
+  int64_t* parent;
+  int32_t* item;
+  uint32_t* count;
+  uint8_t* depth;
+  int64_t base;
+  const int32_t* ids;  // rank -> item id (set by HLevels)
+};
+struct HlInput {
+  const int64_t* tx_ptr;   // this rank's CSR (rebased)
+  const int32_t* items;
+  int64_t n_tx;
+  const int32_t* rank_of;  // item -> frequent rank (-1 otherwise)
+  const uint32_t* fmask;   // optional frequent-item bit mask
+  const int32_t* ids;      // rank -> item
+  const uint32_t* gram;    // level-2 counts, upper triangle, global (all-reduced) counts
+  int64_t ld, F;
+  uint32_t minsup;
+  int max_len;             // 0 = no cap
+  int n_cus;
+};
+struct HlHooks {
+  std::function<HlTrieOut(int64_t n)> reserve;   // room for n more trie nodes (base = first id)
+  std::function<void(int64_t n)> commit;         // n nodes written after the last reserve
+  std::function<void(uint32_t* cnt, int64_t n)> allreduce;  // tx-DP candidate counts (or empty)
+  std::function<void()> wait;                    // host wait for the stream (bounded with comm)
+};
+struct HlStats {
+  int64_t n_tx_kept = 0, nnz_kept = 0, candidates = 0;
+  int max_depth = 1;
+  std::vector<int64_t> per_level;  // itemsets of size 2, 3, ...
+  std::vector<int64_t> hits;       // containing (transaction, itemset) pairs of size 2, 3, ...
+};
+class HLevels {  // grow-only device buffers kept across calls
+ public:
+  HLevels();
+  ~HLevels();
+  HLevels(const HLevels&) = delete;
+  HLevels& operator=(const HLevels&) = delete;
+  bool run(const HlInput& in, const HlHooks& hooks, hipStream_t s, HlStats& st);
+
+ private:
+  struct Impl;
+  Impl* p_;
+};
+
 // same with F read from the device (grid and row stride sized for F_max)
 void pair_gram_popcount_dev(const uint64_t* bm, int64_t Wp, const int64_t* dF, int64_t F_max,
                             uint32_t* out, hipStream_t s);

@@ -282,10 +282,15 @@ __device__ __forceinline__ void serve_query_wave(
     int64_t rs = 0;
     if (i < q1) {
       const int32_t sd = seeds[i];
-      if (sd >= 0 && sd < n_items && is_key[sd]) {
-        present = true;
-        rs = row_ptr[sd];
-        len = row_ptr[sd + 1] - rs;
+      if (sd >= 0 && sd < n_items) {
+        // the three loads in flight together (is_key gated a dependent second round trip)
+        const uint8_t kk = is_key[sd];
+        const int64_t r0 = row_ptr[sd], r1 = row_ptr[sd + 1];
+        if (kk) {
+          present = true;
+          rs = r0;
+          len = r1 - r0;
+        }
       }
     }
     const unsigned long long bal = __ballot(present);
@@ -315,15 +320,34 @@ __device__ __forceinline__ void serve_query_wave(
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   // ---- max-merge into the wave's table ----
-  for (int64_t e = lane; e < acc; e += 64) {
-    int lo = 0, hi = np;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (seg[mid] <= e) lo = mid; else hi = mid;
+  // every entry of this lane (<= kSlots / 2 / 64) is loaded first, all loads in flight at once;
+  // then inserted (the LDS atomics kept each iteration's HBM loads from overlapping the next:
+  // ~1 us of latency per 64 entries)
+  constexpr int kPer = kSlots / 2 / 64;
+  int32_t ec[kPer];
+  uint32_t ev[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t e = lane + 64 * u;
+    ec[u] = -1;
+    ev[u] = 0;
+    if (e < acc) {
+      int lo = 0, hi = np;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (seg[mid] <= e) lo = mid; else hi = mid;
+      }
+      const int64_t p = rowp[lo] + (e - seg[lo]);
+      ec[u] = cons[p];
+      ev[u] = srank[p];
     }
-    const int64_t p = rowp[lo] + (e - seg[lo]);
-    const int32_t c = cons[p];
-    const uint32_t v = srank[p];
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t e = lane + 64 * u;
+    if (e >= acc) continue;
+    const int32_t c = ec[u];
+    const uint32_t v = ev[u];
     uint32_t h = ((uint32_t)c * 2654435761u) & (kSlots - 1);
     while (true) {
       const int32_t prev = atomicCAS(&key[h], -1, c);

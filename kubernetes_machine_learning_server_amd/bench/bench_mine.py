@@ -437,7 +437,10 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
                "comm": comm, "steps": steps, "ms_per_step": round(ms, 3),
                "tx_per_s": round(T / (ms / 1000.0), 1),
                "n_frequent_items": int(st.get("n_frequent_items", 0)),
-               "phases_ms": {k: round(v, 3) for k, v in (st.get("phases_ms") or {}).items()}}
+               "phases_ms": {k: round(v, 3) for k, v in (st.get("phases_ms") or {}).items()},
+               "levels_path": st.get("levels_path"), "level2_method": st.get("level2_method")}
+        if "horizontal" in st:
+            out["horizontal"] = st["horizontal"]
         trie = r["trie"]
         if mode == "shard":  # per-rank sub-tries -> the whole trie on rank 0
             from ..parallel.dist_miner import gather_trie
