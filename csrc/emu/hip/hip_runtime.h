@@ -28,6 +28,11 @@
 #define __launch_bounds__(...)
 #define __shared__ static
 
+struct uint2 {  // HIP's vector type, as far as the shared headers name it
+  unsigned int x, y;
+};
+inline uint2 make_uint2(unsigned int x, unsigned int y) { return uint2{x, y}; }
+
 struct dim3 {
   unsigned x, y, z;
   constexpr dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}

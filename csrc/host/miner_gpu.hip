@@ -1069,6 +1069,29 @@ GpuMiner::CoocStats GpuMiner::cooc_stats() {
   return st;
 }
 
+// The row form of the horizontal count (kern::PairRows) on long shards: every increment an LDS
+// atomic.  KMLS_PAIR_ROWS=0 / test hook pair_rows=0 keeps the scattered-atomic count (cooc.hip).
+bool GpuMiner::pair_rows_ok(int64_t F) const {
+  static const long long env_dflt = [] {
+    const char* e = std::getenv("KMLS_PAIR_ROWS");
+    return e ? std::atoll(e) : 1ll;
+  }();
+  return test_hook("pair_rows", env_dflt) != 0 && F >= 2 && F <= 32768 && !subset_active();
+}
+
+bool GpuMiner::pair_rows_count(uint32_t* gram, int64_t ld) {
+  hipStream_t s = (hipStream_t)stream_;
+  if (!prows_) prows_ = std::make_shared<kern::PairRows>();
+  auto* P = static_cast<kern::PairRows*>(prows_.get());
+  const int64_t F = (int64_t)fi_.ids.size();
+  kern::PrInput in{d_tx_ptr_, d_items_, n_tx_, n_items_, d_ids_, F, n_cus_};
+  Comm* c = comm_;
+  return P->count(in, gram, ld, s, [&] {
+    if (c) c->wait_stream(s);
+    else KMLS_HIP(hipStreamSynchronize(s));
+  });
+}
+
 bool GpuMiner::pair_counts_csr(uintptr_t out_dev, int64_t ld) {
   KMLS_HIP(hipSetDevice(device_));
   const int64_t F = (int64_t)fi_.ids.size();
@@ -1076,6 +1099,12 @@ bool GpuMiner::pair_counts_csr(uintptr_t out_dev, int64_t ld) {
   KMLS_CHECK(!subset_active(), "pair_counts_csr: a use_frequent_subset() set is active; "
                                "select() again first");
   hipStream_t s = (hipStream_t)stream_;
+  prows_fresh_ = false;
+  if (pair_rows_ok(F)) {
+    if (!d_cooc_) KMLS_HIP(hipMalloc((void**)&d_cooc_, 4 * sizeof(unsigned long long)));
+    KMLS_HIP(hipMemsetAsync(d_cooc_ + 2, 0, sizeof(unsigned long long), s));  // cooc_check: clean
+    if (pair_rows_count((uint32_t*)out_dev, ld)) return prows_fresh_ = true;
+  }
   const CoocStats st = cooc_stats();
   if (st.max_k > (uint64_t)kern::cooc_max_k()) return false;
   KMLS_HIP(hipMemsetAsync((void*)out_dev, 0, (size_t)F * ld * sizeof(uint32_t), s));
@@ -1204,6 +1233,8 @@ bool GpuMiner::pair_counts_csr_direct(uintptr_t out_dev, int64_t ld) {
                                "select() again first");
   hipStream_t s = (hipStream_t)stream_;
   if (!d_cooc_) KMLS_HIP(hipMalloc((void**)&d_cooc_, 4 * sizeof(unsigned long long)));
+  prows_fresh_ = false;
+  if (pair_rows_ok(F) && pair_rows_count((uint32_t*)out_dev, ld)) return prows_fresh_ = true;
   KMLS_HIP(hipMemsetAsync((void*)out_dev, 0, (size_t)F * ld * sizeof(uint32_t), s));
   KMLS_HIP(hipMemsetAsync(d_cooc_ + 2, 0, sizeof(unsigned long long), s));
   kern::cooc_count(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, d_fmask_, F, (uint32_t*)out_dev, ld,
@@ -1562,7 +1593,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       // levels >= 2 from the gram and a filtered CSR (hlevels.hip): no bitmap anywhere
       if (!hl_) hl_ = std::make_shared<kern::HLevels>();
       auto* H = static_cast<kern::HLevels*>(hl_.get());
-      kern::HlInput in{d_tx_ptr_, d_items_, n_tx_, d_rank_of_, d_fmask_, d_ids_, run.gram, F, F,
+      kern::HlInput in{d_tx_ptr_, d_items_, n_tx_, n_items_, d_rank_of_, d_fmask_, d_ids_, run.gram, F, F,
                        run.minsup, run.max_len, n_cus_};
       kern::HlHooks hk;
       hk.reserve = [&](int64_t n) {
@@ -1582,6 +1613,12 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
         if (comm_) comm_->wait_stream(s);
         else KMLS_HIP(hipStreamSynchronize(s));
       };
+      if (prows_ && prows_fresh_) {  // level 2 came from the row count: reuse its rank CSR
+        auto* P = static_cast<kern::PairRows*>(prows_.get());
+        in.f_txrec = P->txrec();
+        in.f_fit = P->fit();
+        in.f_rows = P->n_rows();
+      }
       kern::HlStats hs;
       H->run(in, hk, s, hs);
       run.max_depth = hs.max_depth;

@@ -410,6 +410,10 @@ class GpuMiner {
   // horizontal levels (kern::HLevels, hlevels.hip): sparse long shards skip the bitmap encode;
   // level 2 from the CSR (cooc), levels >= 3 from a filtered CSR
   std::shared_ptr<void> hl_;
+  std::shared_ptr<void> prows_;   // kern::PairRows: level-2 pair counts row by row in LDS
+  bool pair_rows_ok(int64_t F) const;
+  bool prows_fresh_ = false;      // the last pair_counts_csr used the row count (its CSR is valid)
+  bool pair_rows_count(uint32_t* gram, int64_t ld);
   bool hl_plan_ = false;          // the current mine_bitmaps call runs without bitmaps
   bool hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* comm);
   std::string hl_stats_;          // last horizontal run (JSON-ish summary for the phases)

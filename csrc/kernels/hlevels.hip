@@ -32,6 +32,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "devbuf.hpp"
 #include "kernels.hpp"
 #include "kmls/common.hpp"
 #include "kmls/hooks.hpp"
@@ -87,19 +88,6 @@ __device__ __forceinline__ int32_t ht_find(const HSlot* __restrict__ t, uint32_t
     h = (h + 1) & mask;
   }
   return -1;
-}
-
-// Wave-aggregated slot allocation: one atomic per wave (and per call) for the active lanes that
-// want a slot.  Every active lane must call it (it contains a ballot).
-__device__ __forceinline__ unsigned long long wave_alloc(bool want, unsigned long long* ctr) {
-  const unsigned long long m = __ballot(want);
-  if (m == 0ull) return 0ull;
-  const int lane = (int)(threadIdx.x & 63);
-  const int leader = __builtin_ctzll(m);
-  unsigned long long base = 0ull;
-  if (lane == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
-  base = __shfl(base, leader, 64);
-  return base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
 }
 
 __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* red) {
@@ -175,87 +163,6 @@ __global__ __launch_bounds__(256) void k_hl_row_fill(
 }
 
 // ---- filtered CSR ------------------------------------------------------------------------
-
-// Thread per transaction: its pair items as ranks, ascending (a 16-entry register insertion
-// network; longer rows are sorted in place in their output slot).  Transactions with >= 3 of
-// them get a slot (off, len) and their items; the counters count past the capacities, so the
-// caller can re-run with the exact sizes.
-__global__ __launch_bounds__(256) void k_hl_filter(
-    const int64_t* __restrict__ tx_ptr, const int32_t* __restrict__ items, int64_t n_tx,
-    const int32_t* __restrict__ rank_of, const uint32_t* __restrict__ fmask,
-    const uint8_t* __restrict__ inpair, uint2* __restrict__ txrec, uint16_t* __restrict__ fit,
-    unsigned long long* ctr, unsigned long long tx_cap, unsigned long long nnz_cap,
-    unsigned* err) {
-  const int lane = threadIdx.x & 63;
-  for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < n_tx; t0 += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = t0 + threadIdx.x;
-    uint32_t v[kSortRegs];
-#pragma unroll
-    for (int q = 0; q < kSortRegs; ++q) v[q] = 0xFFFFFFFFu;
-    uint32_t kept = 0;
-    int64_t s = 0, e = 0;
-    if (t < n_tx) {
-      s = tx_ptr[t];
-      e = tx_ptr[t + 1];
-      for (int64_t p = s; p < e; ++p) {
-        const int32_t it = items[p];
-        if (fmask && !((fmask[it >> 5] >> (it & 31)) & 1u)) continue;
-        const int32_t r = rank_of[it];
-        if (r < 0 || !inpair[r]) continue;
-        uint32_t x = (uint32_t)r;
-#pragma unroll
-        for (int q = 0; q < kSortRegs; ++q) {
-          const uint32_t lo = min(v[q], x), hi = max(v[q], x);
-          v[q] = lo;
-          x = hi;
-        }
-        ++kept;
-      }
-    }
-    const bool want = kept >= 3u;
-    if (kept > 65535u) atomicOr(err, 1u);
-    // slots: transactions by a ballot, items by a wave prefix sum (one atomic each per wave)
-    const unsigned long long ti = wave_alloc(want, &ctr[0]);
-    uint32_t incl = want ? kept : 0u;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += u;
-    }
-    const uint32_t tot = __shfl(incl, 63, 64);
-    unsigned long long ib = 0;
-    if (lane == 63 && tot) ib = atomicAdd(&ctr[1], (unsigned long long)tot);
-    ib = __shfl(ib, 63, 64);
-    if (want) {
-      const unsigned long long off = ib + incl - kept;
-      if (ti < tx_cap && off + kept <= nnz_cap) {
-        txrec[ti] = make_uint2((uint32_t)off, kept);
-        uint16_t* dst = fit + off;
-        if (kept <= (uint32_t)kSortRegs) {
-#pragma unroll
-          for (int q = 0; q < kSortRegs; ++q)
-            if ((uint32_t)q < kept) dst[q] = (uint16_t)v[q];
-        } else {  // long row: write, then insertion-sort in place (rare)
-          uint32_t n = 0;
-          for (int64_t p = s; p < e; ++p) {
-            const int32_t it = items[p];
-            if (fmask && !((fmask[it >> 5] >> (it & 31)) & 1u)) continue;
-            const int32_t r = rank_of[it];
-            if (r < 0 || !inpair[r]) continue;
-            uint16_t x = (uint16_t)r;
-            uint32_t j = n++;
-            while (j > 0 && dst[j - 1] > x) {
-              dst[j] = dst[j - 1];
-              --j;
-            }
-            dst[j] = x;
-          }
-        }
-      }
-    }
-  }
-}
-
-// ---- hits ----------------------------------------------------------------------------------
 
 // Hit lists are appended through per-wave blocks of kHitBlk slots (one global atomic per block,
 // not per hit: a single counter taking an atomic per wave iteration serialised the first version
@@ -547,6 +454,7 @@ unsigned grid_for(int64_t n, int n_cus) {
 
 struct HLevels::Impl {
   Buf<uint8_t> inpair;
+  Buf<int16_t> pr;  // item -> pair-item rank
   Buf<uint32_t> row_cnt, row_off;
   Buf<uint32_t> lv_par[2], lv_item[2], lv_end[2];
   Buf<uint32_t> c_par, c_item, c_cnt, c_n, c_off, flag, sidx;
@@ -584,7 +492,7 @@ bool HLevels::run(const HlInput& in, const HlHooks& hk, hipStream_t s, HlStats& 
   const int64_t F = in.F;
   st = HlStats{};
   if (F < 2 || in.max_len == 1) return true;
-  KMLS_CHECK(F <= 65536, "hlevels: item ranks are 16-bit");
+  KMLS_CHECK(F <= 32768, "hlevels: item ranks are 16-bit (signed)");
   // ---- level 2: frequent pairs from the gram ----
   I.row_cnt.need((size_t)F + 1);
   I.row_off.need((size_t)F + 1);
@@ -625,25 +533,46 @@ bool HLevels::run(const HlInput& in, const HlHooks& hk, hipStream_t s, HlStats& 
   const unsigned long long cap0 = (unsigned long long)test_hook("hl_cap", 1ll << 20);
   unsigned long long tx_cap = std::max<unsigned long long>(I.txrec.cap, cap0);
   unsigned long long nnz_cap = std::max<unsigned long long>(I.fit.cap, cap0);
+  if (in.f_txrec == nullptr) {  // no rank CSR given: map the items straight to pair-item ranks
+    I.pr.need((size_t)std::max<int64_t>(in.n_items, 1));
+    KMLS_HIP(hipMemsetAsync(I.pr.p, 0xFF, (size_t)std::max<int64_t>(in.n_items, 1) * 2, s));
+    hipLaunchKernelGGL(devbuf::k_rank_map, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, s,
+                       in.ids, F, (const uint8_t*)I.inpair.p, I.pr.p);
+    KMLS_HIP(hipGetLastError());
+  }
   for (int attempt = 0;; ++attempt) {
     I.txrec.need(tx_cap);
     I.fit.need(nnz_cap);
     tx_cap = I.txrec.cap;
     nnz_cap = I.fit.cap;
-    KMLS_HIP(hipMemsetAsync(I.ctr.p, 0, 2 * sizeof(unsigned long long), s));
-    if (in.n_tx > 0)
-      hipLaunchKernelGGL(k_hl_filter, dim3(grid_for(in.n_tx, in.n_cus)), dim3(256), 0, s,
-                         in.tx_ptr, in.items, in.n_tx, in.rank_of, in.fmask, I.inpair.p,
-                         I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p);
+    KMLS_HIP(hipMemsetAsync(I.ctr.p, 0, sizeof(unsigned long long), s));
+    KMLS_HIP(hipMemsetAsync(I.err.p, 0, sizeof(unsigned), s));
+    if (in.f_txrec != nullptr) {
+      if (in.f_rows > 0)
+        hipLaunchKernelGGL(devbuf::k_csr_refilter, dim3(grid_for(in.f_rows, in.n_cus)), dim3(256),
+                           0, s, in.f_txrec, in.f_rows, in.f_fit, (const uint8_t*)I.inpair.p, 3u,
+                           I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap);
+    } else if (in.n_tx > 0) {
+      hipLaunchKernelGGL(devbuf::k_map_filter, dim3(grid_for(in.n_tx, in.n_cus)), dim3(256), 0, s,
+                         in.tx_ptr, in.items, in.n_tx, I.pr.p, 3u, I.txrec.p, I.fit.p, I.ctr.p,
+                         tx_cap, nnz_cap, I.err.p);
+    }
     KMLS_HIP(hipGetLastError());
-    KMLS_HIP(hipMemcpyAsync(I.h, I.ctr.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    KMLS_HIP(hipMemcpyAsync(I.h, I.ctr.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     KMLS_HIP(hipMemcpyAsync(I.h + 2, I.err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     hk.wait();
-    KMLS_CHECK(((unsigned*)(I.h + 2))[0] == 0u, "hlevels: a transaction kept > 65535 items");
-    if (I.h[0] <= tx_cap && I.h[1] <= nnz_cap) break;
+    const unsigned e = ((unsigned*)(I.h + 2))[0];
+    KMLS_CHECK(!(e & 1u), "hlevels: a transaction kept > 65535 items");
+    KMLS_CHECK(!(e & 2u), "hlevels: a transaction holds the same frequent item twice");
+    const unsigned long long nt = I.h[0] >> devbuf::kPackShift, nn = I.h[0] & devbuf::kPackMask;
+    if (nt <= tx_cap && nn <= nnz_cap) {
+      I.h[0] = nt;
+      I.h[1] = nn;
+      break;
+    }
     KMLS_CHECK(attempt == 0, "hlevels: filtered CSR sizes grew between passes");
-    tx_cap = I.h[0];
-    nnz_cap = I.h[1];
+    tx_cap = nt;
+    nnz_cap = nn;
   }
   const int64_t n_ftx = (int64_t)I.h[0];
   st.n_tx_kept = n_ftx;

@@ -260,6 +260,38 @@ void cooc_stats(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, const
 void cooc_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, const int32_t* rank_of,
                 const uint32_t* fmask, int64_t F, uint32_t* gram, int64_t ld, unsigned* err,
                 int n_cus, hipStream_t s);
+// ---- level-2 pair counts row by row in LDS (pairrows.hip) ----
+struct PrInput {
+  const int64_t* tx_ptr;  // this rank's CSR (rebased)
+  const int32_t* items;
+  int64_t n_tx, n_items;
+  const int32_t* ids;     // rank -> item
+  int64_t F;
+  int n_cus;
+};
+class PairRows {  // grow-only device buffers kept across calls
+ public:
+  PairRows();
+  ~PairRows();
+  PairRows(const PairRows&) = delete;
+  PairRows& operator=(const PairRows&) = delete;
+  // gram[a * ld + b] (ranks a < b) = co-occurrences in the shard; the rest of the F x ld block
+  // zero.  False (gram zeroed, nothing counted): a transaction holds > 65535 frequent items.
+  // `wait` is the host wait for s (bounded under a communicator).
+  bool count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t s,
+             const std::function<void()>& wait);
+  // the frequent-rank CSR of the last count: rows (off, len) of >= 2 ranks, ascending
+  const uint2* txrec() const;
+  const uint16_t* fit() const;
+  int64_t n_rows() const;
+  int64_t nnz() const;
+  static size_t lds_bytes(int64_t F);
+
+ private:
+  struct Impl;
+  Impl* p_;
+};
+
 // ---- horizontal levels >= 3 from a filtered CSR (hlevels.hip) ----
 struct HlTrieOut {  // device trie arrays (whole arrays; new nodes go to [base, base + n))
   int64_t* parent;
@@ -272,7 +304,7 @@ struct HlTrieOut {  // device trie arrays (whole arrays; new nodes go to [base, 
 struct HlInput {
   const int64_t* tx_ptr;   // this rank's CSR (rebased)
   const int32_t* items;
-  int64_t n_tx;
+  int64_t n_tx, n_items;
   const int32_t* rank_of;  // item -> frequent rank (-1 otherwise)
   const uint32_t* fmask;   // optional frequent-item bit mask
   const int32_t* ids;      // rank -> item
@@ -281,6 +313,10 @@ struct HlInput {
   uint32_t minsup;
   int max_len;             // 0 = no cap
   int n_cus;
+  // optional: the frequent-rank CSR of this shard (PairRows) — re-filtered instead of the items
+  const uint2* f_txrec = nullptr;
+  const uint16_t* f_fit = nullptr;
+  int64_t f_rows = 0;
 };
 struct HlHooks {
   std::function<HlTrieOut(int64_t n)> reserve;   // room for n more trie nodes (base = first id)

@@ -244,7 +244,11 @@ class ReloadManager:
                     gmm = 0
                 else:
                     gmb, cross = measure_crossover(index, gpu_index)
-                    gmm, lcross = measure_loop(index, gpu_index)
+                    if hasattr(gpu_index, "query_loop"):  # the serving kernel is optional
+                        try:
+                            gmm, lcross = measure_loop(index, gpu_index)
+                        except Exception as e:  # the loop stays off; batches still measured
+                            logger.warning(f"serving-loop measurement failed ({e}); loop off")
         except Exception as e:  # keep serving the previous snapshot; retry next tick
             self.failed_reloads += 1
             self.last_error = f"{type(e).__name__}: {e}"

@@ -1,7 +1,8 @@
-"""GPU parity of the horizontal co-occurrence count (csrc/kernels/cooc.hip): the level-2 pair
-gram counted from the transaction CSR, checked against a numpy one-hot Gram (float64 BLAS,
-exact) and against the bitmap bit-GEMM of the same shard; and the miner with the level-2 method
-forced each way producing the same trie (content digest)."""
+"""GPU parity of the horizontal co-occurrence counts: the level-2 pair gram counted from the
+transaction CSR — row by row in LDS (csrc/kernels/pairrows.hip, the default) and by scattered
+atomics (csrc/kernels/cooc.hip, test hook pair_rows=0) — checked against a numpy one-hot Gram
+(float64 BLAS, exact) and against the bitmap bit-GEMM of the same shard; and the miner with the
+level-2 method forced each way producing the same trie (content digest)."""
 import numpy as np
 import pytest
 
@@ -22,10 +23,16 @@ def _miner(gpu_mod, ptr, items, n_items):
     return g
 
 
+@pytest.fixture(params=["rows", "atomic"])
+def method(request, monkeypatch):
+    monkeypatch.setenv("KMLS_TEST_HOOKS", "pair_rows=1" if request.param == "rows" else "pair_rows=0")
+    return request.param
+
+
 @pytest.mark.parametrize("shape,ms,n_tx,ld_pad", [("tiny", 0.02, None, 0), ("ds2", 0.05, 1500, 3),
                                                   ("ds_dense", 0.05, None, 0),
                                                   ("ds2_weak", 0.01, 4000, 1)])
-def test_cooc_vs_numpy(gpu_mod, shape, ms, n_tx, ld_pad):
+def test_cooc_vs_numpy(gpu_mod, method, shape, ms, n_tx, ld_pad):
     import torch
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     tx = generate(shape, seed=7, n_tx=n_tx)
@@ -47,7 +54,7 @@ def test_cooc_vs_numpy(gpu_mod, shape, ms, n_tx, ld_pad):
     np.testing.assert_array_equal(got, ref)
 
 
-def test_cooc_large_vocab_matches_bit_gemm(gpu_mod):
+def test_cooc_large_vocab_matches_bit_gemm(gpu_mod, method):
     """1M-item vocabulary (the frequent bit-mask filter) and > 2^16 transactions: equal to the
     popcount bit-GEMM over the shard's bitmaps."""
     import torch
@@ -72,8 +79,9 @@ def test_cooc_large_vocab_matches_bit_gemm(gpu_mod):
     np.testing.assert_array_equal(o, r)
 
 
-def test_cooc_declines_long_transactions(gpu_mod):
-    """A transaction with more frequent items than the LDS entry buffer: declined, gram untouched."""
+def test_cooc_declines_long_transactions(gpu_mod, method):
+    """A transaction with more frequent items than the LDS entry buffer: the atomic count
+    declines (gram untouched); the row count takes it (its row is sorted in place)."""
     import torch
     n_items = 2100
     rows = [np.arange(n_items, dtype=np.int32)] + [np.array([1, 2, 3], np.int32)] * 50
@@ -85,9 +93,17 @@ def test_cooc_declines_long_transactions(gpu_mod):
     assert F == n_items and g.cooc_stats()["max_k"] == n_items
     gram = torch.full((F, F), 5, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
-    assert not g.pair_counts_csr(gram.data_ptr(), F)
+    if method == "atomic":
+        assert not g.pair_counts_csr(gram.data_ptr(), F)
+        g.synchronize()
+        assert int(gram[0, 1].item()) == 5
+        return
+    assert g.pair_counts_csr(gram.data_ptr(), F)
     g.synchronize()
-    assert int(gram[0, 1].item()) == 5
+    ids = np.asarray(g.frequent()[0])
+    X = _onehot(ptr, items, len(rows), n_items)[:, ids]
+    got = np.triu(gram.cpu().numpy().astype(np.int64), 1)
+    np.testing.assert_array_equal(got, np.triu(np.rint(X.T @ X).astype(np.int64), 1))
 
 
 def test_txdp_level2_method_same_trie(gpu_mod, monkeypatch):
@@ -135,9 +151,9 @@ def test_cooc_refuses_after_frequent_subset(gpu_mod):
     g.cooc_check()
 
 
-def test_cooc_flags_duplicate_rows(gpu_mod):
+def test_cooc_flags_duplicate_rows(gpu_mod, method):
     """A row holding one frequent item twice breaks load_csr's precondition: the horizontal
-    count flags it (cooc_check raises) instead of silently double-counting its pairs."""
+    counts flag it (cooc_check / the row count raise) instead of silently double-counting."""
     import torch
     rows = [np.array([1, 2, 2, 3], np.int32)] + [np.array([1, 2, 3], np.int32)] * 20
     ptr = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
@@ -147,6 +163,10 @@ def test_cooc_flags_duplicate_rows(gpu_mod):
     F = g.select(counts, len(rows), 0.5)
     gram = torch.zeros((F, F), dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
+    if method == "rows":
+        with pytest.raises(Exception, match="twice"):
+            g.pair_counts_csr(gram.data_ptr(), F)
+        return
     assert g.pair_counts_csr(gram.data_ptr(), F)
     with pytest.raises(Exception, match="duplicate"):
         g.cooc_check()

@@ -79,7 +79,7 @@ def test_horizontal_long_rows_and_regrown_buffers(gpu_mod, monkeypatch):
     ms = 200 / 70_000
     want = _cpu(gpu_mod, ptr, items, n_items, ms)
     assert want["per_depth"][3] > 0  # triples of hot items are frequent
-    for hooks in ("cooc=2", "cooc=2,hl_cap=64"):
+    for hooks in ("cooc=2", "cooc=2,hl_cap=64", "cooc=2,pair_rows=0"):
         monkeypatch.setenv("KMLS_TEST_HOOKS", hooks)
         r, d = _mine(gpu_mod, ptr, items, n_items, ms)
         assert r["stats"]["levels_path"] == "horizontal"
