@@ -1103,7 +1103,10 @@ bool GpuMiner::pair_counts_csr(uintptr_t out_dev, int64_t ld) {
   if (pair_rows_ok(F)) {
     if (!d_cooc_) KMLS_HIP(hipMalloc((void**)&d_cooc_, 4 * sizeof(unsigned long long)));
     KMLS_HIP(hipMemsetAsync(d_cooc_ + 2, 0, sizeof(unsigned long long), s));  // cooc_check: clean
-    if (pair_rows_count((uint32_t*)out_dev, ld)) return prows_fresh_ = true;
+    if (pair_rows_count((uint32_t*)out_dev, ld)) {
+      hl_pairs_est_ = static_cast<kern::PairRows*>(prows_.get())->pairs();  // exact now
+      return prows_fresh_ = true;
+    }
   }
   const CoocStats st = cooc_stats();
   if (st.max_k > (uint64_t)kern::cooc_max_k()) return false;
@@ -1140,6 +1143,19 @@ bool GpuMiner::cooc_cheaper(int64_t F, int64_t Wp, int64_t nnz, const CoocStats&
 // 2(N-1)/N), each rank keeps the frequent upper entries of its rows, and one all-gather of those
 // (row, col, count) triples — a few thousand at configs 3/5 — rebuilds on every rank a dense gram
 // holding only the frequent pairs (the level loop reads gram[a][b] >= minsup, nothing else).
+// sum_t k_t(k_t-1)/2 estimated from the first 1/16 of the shard's transactions (>= 65536)
+int64_t GpuMiner::cooc_pairs_sampled() {
+  hipStream_t s = (hipStream_t)stream_;
+  if (n_tx_ <= 0 || fi_.ids.empty()) return 0;
+  const int64_t ns = std::min<int64_t>(n_tx_, std::max<int64_t>(65536, n_tx_ / 16));
+  if (!d_cooc_) KMLS_HIP(hipMalloc((void**)&d_cooc_, 4 * sizeof(unsigned long long)));
+  KMLS_HIP(hipMemsetAsync(d_cooc_, 0, 2 * sizeof(unsigned long long), s));
+  kern::cooc_stats(d_tx_ptr_, d_items_, ns, d_rank_of_, d_fmask_, d_cooc_, n_cus_, s);
+  KMLS_HIP(hipMemcpyAsync(h_scalar_, d_cooc_, 8, hipMemcpyDeviceToHost, s));
+  KMLS_HIP(hipStreamSynchronize(s));
+  return (int64_t)((double)h_scalar_[0] * (double)n_tx_ / (double)ns);
+}
+
 // Horizontal levels instead of bitmaps: the shard is long (>= 1024 bitmap words, as for the
 // level-2 cooc choice) and the cost model picks the horizontal pair count.  Every tx-DP rank must
 // take the same path (the two run different collectives): the shard votes are all-reduced.
@@ -1151,8 +1167,17 @@ bool GpuMiner::hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* 
   }();
   bool want = test_hook("hlevels", env_dflt) != 0 && cfg.level2_gram && F >= 2 &&
               F <= 32768 && Wp >= 1024 && test_hook("cooc", 1) != 0 && !subset_active();
-  if (want) {
+  if (want && pair_rows_ok(F)) {
+    // the row count has no per-transaction bound: a sampled pair estimate feeds the cost model
+    // (a full statistics pass cost as much as a tenth of the config-3 step)
+    hl_pairs_est_ = cooc_pairs_sampled();
+    CoocStats st;
+    st.pairs = (uint64_t)hl_pairs_est_;
+    st.max_k = 0;
+    want = test_hook("cooc", 1) == 2 || cooc_cheaper(F, Wp, nnz_, st);
+  } else if (want) {
     const CoocStats st = cooc_stats();
+    hl_pairs_est_ = (int64_t)st.pairs;
     want = st.max_k <= (uint64_t)kern::cooc_max_k() &&
            (test_hook("cooc", 1) == 2 || cooc_cheaper(F, Wp, nnz_, st));
   }
@@ -1553,7 +1578,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       if (hl_plan_) {  // decided (globally) before the encode: there is no bitmap
         sparse = true;
         res.level2_method = "cooc";
-        res.cooc_pairs = (int64_t)cooc_stats().pairs;
+        res.cooc_pairs = hl_pairs_est_;
       } else if (gram_csr_ok_ && Wp >= 1024 && test_hook("cooc", 1) != 0) {
         const CoocStats st = cooc_stats();
         sparse = test_hook("cooc", 1) == 2 || cooc_cheaper(F, Wp, nnz_, st);
@@ -1573,6 +1598,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
         else
           kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);
       }
+      if (hl_plan_) res.cooc_pairs = hl_pairs_est_;  // exact after the row count
       if (comm_ && cw > 1) {
         txdp_gram_combine(gram, F, per, run.minsup);
         res.level2_comm = "reduce_scatter+frequent_allgather";

@@ -412,6 +412,8 @@ class GpuMiner {
   std::shared_ptr<void> hl_;
   std::shared_ptr<void> prows_;   // kern::PairRows: level-2 pair counts row by row in LDS
   bool pair_rows_ok(int64_t F) const;
+  int64_t cooc_pairs_sampled();
+  int64_t hl_pairs_est_ = -1;
   bool prows_fresh_ = false;      // the last pair_counts_csr used the row count (its CSR is valid)
   bool pair_rows_count(uint32_t* gram, int64_t ld);
   bool hl_plan_ = false;          // the current mine_bitmaps call runs without bitmaps

@@ -51,6 +51,15 @@ inline void scan_u32(const uint32_t* in, uint32_t* out, int64_t m, Buf<uint8_t>&
   hip_ok(hipcub::DeviceScan::ExclusiveSum(tmp.p, b, in, out, (int)m, s), "scan");
 }
 
+inline void scan_u64(const unsigned long long* in, unsigned long long* out, int64_t m,
+                     Buf<uint8_t>& tmp, hipStream_t s) {
+  KMLS_CHECK(m < (1ll << 31), "scan past 2^31 elements");
+  size_t b = 0;
+  hip_ok(hipcub::DeviceScan::ExclusiveSum(nullptr, b, in, out, (int)m), "scan size");
+  tmp.need(b + 256);
+  hip_ok(hipcub::DeviceScan::ExclusiveSum(tmp.p, b, in, out, (int)m, s), "scan");
+}
+
 namespace {  // kernels and device helpers: one copy per translation unit
 
 // Wave-aggregated slot allocation: one atomic per wave (and per call) for the active lanes that

@@ -285,6 +285,7 @@ class PairRows {  // grow-only device buffers kept across calls
   const uint16_t* fit() const;
   int64_t n_rows() const;
   int64_t nnz() const;
+  int64_t pairs() const;  // co-occurring pairs counted (sum k(k-1)/2)
   static size_t lds_bytes(int64_t F);
 
  private:

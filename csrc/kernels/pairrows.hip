@@ -6,14 +6,17 @@
 //
 //   1. frequent-rank CSR: each transaction's frequent items as ranks, ascending, 16-bit
 //      (devbuf::k_map_filter; rows with < 2 of them dropped — they hold no pair);
-//   2. its transpose (CSC: for each rank a, the rows containing a): per-workgroup LDS histograms
-//      of a contiguous row block, written rank-major, one exclusive scan = every (rank,
-//      workgroup) output base; the fill pass scatters with LDS cursors (no global atomics,
-//      deterministic);
-//   3. row a = one or more 1024-thread workgroups (slices of kSlice rows of its column), each
-//      with an F-counter LDS accumulator: for every transaction containing a, +1 at each later
-//      (higher-ranked) item; a one-slice row stores its counters straight into gram row a
-//      (coalesced, no zero fill needed), slices of a split row add their non-zero counters.
+//   2. the PAIR LISTS: row a's list holds, for every transaction containing a, the items after
+//      a — i.e. every co-occurring pair (a, b > a) once, 16 bits each.  Per-workgroup LDS
+//      histograms of a contiguous block of transactions (pairs each rank heads), written
+//      rank-major; one exclusive scan gives every (rank, block) segment; the fill pass appends
+//      each transaction's runs at LDS cursors (no global atomics, deterministic layout);
+//   3. row a = one or more 1024-thread workgroups (slices of kSlice list entries), each streaming
+//      its slice with coalesced loads into an F-counter LDS accumulator; a one-slice row stores
+//      its counters straight into gram row a, slices of a split row add their non-zero counters
+//      (the gram is zeroed first).  (A first version walked a transposed CSR instead, re-reading
+//      every transaction's record and items at random for each of its items: 40 ms of the 100 ms
+//      config-5 step, HBM-latency bound.)
 // The CSR built in step 1 is kept for the horizontal levels (hlevels.hip re-filters it to the
 // pair items instead of re-reading the 32-bit item CSR).
 #include <hip/hip_runtime.h>
@@ -35,74 +38,173 @@ namespace {
 using devbuf::Buf;
 
 constexpr int kRowThreads = 1024;
-constexpr uint32_t kSlice = 8192;   // column entries per row workgroup
-constexpr int64_t kBlockTx = 4096;  // CSR rows per histogram / fill workgroup
+constexpr uint64_t kSlice = 65536;  // pair-list entries per row workgroup
+constexpr int64_t kBlockTx = 32768;  // CSR rows per histogram workgroup
+constexpr int64_t kPartTx = 1024;    // CSR rows per partition workgroup (one per thread)
+constexpr int kNG = 64;              // coarse row groups of the first partition pass
+constexpr uint32_t kChunk = 65536;   // group-list entries per split workgroup
 
 void ok(hipError_t e, const char* what) { devbuf::hip_ok(e, what); }
 
-// rows [t0, t1) of the workgroup's block; their items are fit[e0, e1) (row order = item order)
-__device__ __forceinline__ void block_rows(const uint2* __restrict__ txrec, int64_t n_tx,
-                                           int64_t& t0, int64_t& t1) {
+__device__ __forceinline__ void block_rows(int64_t n_tx, int64_t& t0, int64_t& t1) {
   t0 = (int64_t)blockIdx.x * kBlockTx;
   t1 = t0 + kBlockTx < n_tx ? t0 + kBlockTx : n_tx;
 }
 
-__global__ __launch_bounds__(kRowThreads) void k_pr_hist(const uint2* __restrict__ txrec,
+// pairs each rank heads (the later items of its rows) in this block of rows, rank-major
+__global__ __launch_bounds__(kRowThreads) void k_pl_hist(const uint2* __restrict__ txrec,
                                                          int64_t n_tx,
                                                          const uint16_t* __restrict__ fit, int64_t F,
-                                                         int64_t n_wg, uint32_t* __restrict__ hist) {
+                                                         int64_t n_wg,
+                                                         unsigned long long* __restrict__ hist) {
   extern __shared__ uint32_t h[];
   for (int64_t i = threadIdx.x; i < F; i += kRowThreads) h[i] = 0u;
   __syncthreads();
   int64_t t0, t1;
-  block_rows(txrec, n_tx, t0, t1);
-  if (t0 < t1) {
-    const uint2 last = txrec[t1 - 1];
-    const uint32_t e0 = txrec[t0].x, e1 = last.x + last.y;
-    for (uint32_t p = e0 + threadIdx.x; p < e1; p += kRowThreads) atomicAdd(&h[fit[p]], 1u);
+  block_rows(n_tx, t0, t1);
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += kRowThreads) {
+    const uint2 rec = txrec[t];
+    const uint16_t* it = fit + rec.x;
+    for (uint32_t i = 0; i + 1 < rec.y; ++i) atomicAdd(&h[it[i]], rec.y - 1u - i);
   }
   __syncthreads();
   for (int64_t r = threadIdx.x; r < F; r += kRowThreads) hist[r * n_wg + blockIdx.x] = h[r];
 }
 
-// the CSC: csc[base(r, wg) ...] = the rows of this block containing rank r
-__global__ __launch_bounds__(kRowThreads) void k_pr_fill(const uint2* __restrict__ txrec,
-                                                         int64_t n_tx,
-                                                         const uint16_t* __restrict__ fit, int64_t F,
-                                                         int64_t n_wg, const uint32_t* __restrict__ off,
-                                                         uint32_t* __restrict__ csc) {
-  extern __shared__ uint32_t cur[];
-  for (int64_t r = threadIdx.x; r < F; r += kRowThreads) cur[r] = off[r * n_wg + blockIdx.x];
+// Group table and split chunks from the scanned row bases (one block): row r's group =
+// floor(base[r] * kNG / total) (groups of ~equal pair mass, rows contiguous); gcur[g] = the
+// first list position of group g; per group its row range and chunks of kChunk entries;
+// meta[0] = total chunks.
+__global__ __launch_bounds__(1024) void k_pl_groups(const unsigned long long* __restrict__ base,
+                                                   int64_t F, uint8_t* __restrict__ grp,
+                                                   unsigned long long* __restrict__ gcur,
+                                                   uint32_t* __restrict__ grow,  // [kNG][2]
+                                                   uint32_t* __restrict__ gch,   // [kNG + 1]
+                                                   uint32_t* __restrict__ meta) {
+  __shared__ uint32_t lo[kNG], hi[kNG];
+  const unsigned long long total = base[F];
+  if (threadIdx.x < kNG) {
+    lo[threadIdx.x] = 0xFFFFFFFFu;
+    hi[threadIdx.x] = 0u;
+  }
   __syncthreads();
-  int64_t t0, t1;
-  block_rows(txrec, n_tx, t0, t1);
-  for (int64_t t = t0 + threadIdx.x; t < t1; t += kRowThreads) {
-    const uint2 rec = txrec[t];
-    for (uint32_t j = 0; j < rec.y; ++j) {
-      const uint32_t slot = atomicAdd(&cur[fit[rec.x + j]], 1u);
-      csc[slot] = (uint32_t)t;
+  for (int64_t r = threadIdx.x; r < F; r += blockDim.x) {
+    const unsigned g = total ? (unsigned)(base[r] * (unsigned long long)kNG / total) : 0u;
+    const unsigned gg = g < (unsigned)kNG ? g : (unsigned)kNG - 1u;
+    grp[r] = (uint8_t)gg;
+    atomicMin(&lo[gg], (uint32_t)r);
+    atomicMax(&hi[gg], (uint32_t)r + 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int g = 0; g < kNG; ++g) {
+      gch[g] = c;
+      if (lo[g] < hi[g]) {
+        const unsigned long long b0 = base[lo[g]], b1 = base[hi[g]];
+        gcur[g] = b0;
+        grow[2 * g] = lo[g];
+        grow[2 * g + 1] = hi[g];
+        c += (uint32_t)((b1 - b0 + kChunk - 1) / kChunk);
+      } else {
+        gcur[g] = 0;
+        grow[2 * g] = grow[2 * g + 1] = 0;
+      }
     }
+    gch[kNG] = c;
+    meta[0] = c;
   }
 }
 
-// slices per rank (0 for a rank that occurs in no kept row); cnt[F] = 0 for the scan's total
-__global__ void k_pr_slices(const uint32_t* __restrict__ off, int64_t F, int64_t n_wg,
-                            uint32_t* __restrict__ col, uint32_t* __restrict__ nsl) {
+// Pass A: every pair (a, b) of a block of rows appended to a's GROUP list as (a << 16 | b):
+// per-group LDS counts, one global reservation per (block, group), then LDS cursors.  A block's
+// 64 segments stay in L2 while they fill (the per-row version wrote 7-byte runs to 14.8k places).
+__global__ __launch_bounds__(kPartTx) void k_pl_part(const uint2* __restrict__ txrec, int64_t n_tx,
+                                                     const uint16_t* __restrict__ fit, int64_t F,
+                                                     const uint8_t* __restrict__ grp_g,
+                                                     unsigned long long* __restrict__ gcur,
+                                                     uint32_t* __restrict__ gl) {
+  extern __shared__ uint8_t grp[];  // [F]
+  __shared__ uint32_t cnt[kNG];
+  __shared__ unsigned long long gb[kNG];
+  for (int64_t r = threadIdx.x; r < F; r += kPartTx) grp[r] = grp_g[r];
+  if (threadIdx.x < kNG) cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  const int64_t t = (int64_t)blockIdx.x * kPartTx + threadIdx.x;
+  uint2 rec = make_uint2(0u, 0u);
+  if (t < n_tx) rec = txrec[t];
+  const uint16_t* it = fit + rec.x;
+  for (uint32_t i = 0; i + 1 < rec.y; ++i) atomicAdd(&cnt[grp[it[i]]], rec.y - 1u - i);
+  __syncthreads();
+  if (threadIdx.x < kNG) {
+    const uint32_t c = cnt[threadIdx.x];
+    gb[threadIdx.x] = c ? atomicAdd(&gcur[threadIdx.x], (unsigned long long)c) : 0ull;
+    cnt[threadIdx.x] = 0u;
+  }
+  __syncthreads();
+  for (uint32_t i = 0; i + 1 < rec.y; ++i) {
+    const uint32_t a = it[i], n = rec.y - 1u - i;
+    const uint32_t g = grp[a];
+    uint32_t* dst = gl + gb[g] + atomicAdd(&cnt[g], n);
+    for (uint32_t j = 0; j < n; ++j) dst[j] = (a << 16) | (uint32_t)it[i + 1u + j];
+  }
+}
+
+// Pass B: a chunk of one group's list split into its rows' lists (the b halves): per-row LDS
+// counts over the group's row range, one global reservation per (chunk, row) through a relative
+// row cursor, then LDS cursors.
+__global__ __launch_bounds__(kRowThreads) void k_pl_split(
+    const uint32_t* __restrict__ gl, const unsigned long long* __restrict__ gbeg_all,
+    const unsigned long long* __restrict__ base, const uint32_t* __restrict__ grow,
+    const uint32_t* __restrict__ gch, uint32_t* __restrict__ rcur, uint16_t* __restrict__ pl) {
+  extern __shared__ uint32_t rc[];  // [rows of the group]
+  __shared__ int32_t s_g;
+  if (threadIdx.x == 0) {
+    int g = 0;
+    while (g + 1 < kNG && gch[g + 1] <= blockIdx.x) ++g;
+    s_g = g;
+  }
+  __syncthreads();
+  const int g = s_g;
+  const uint32_t r0 = grow[2 * g], r1 = grow[2 * g + 1];
+  const unsigned long long g0 = base[r0], g1 = base[r1];
+  const unsigned long long c0 = g0 + (unsigned long long)(blockIdx.x - gch[g]) * kChunk;
+  const unsigned long long c1 = c0 + kChunk < g1 ? c0 + kChunk : g1;
+  for (uint32_t r = threadIdx.x; r < r1 - r0; r += kRowThreads) rc[r] = 0u;
+  __syncthreads();
+  for (unsigned long long i = c0 + threadIdx.x; i < c1; i += kRowThreads)
+    atomicAdd(&rc[(gl[i] >> 16) - r0], 1u);
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < r1 - r0; r += kRowThreads) {
+    const uint32_t c = rc[r];
+    rc[r] = c ? atomicAdd(&rcur[r0 + r], c) : 0u;  // relative position in the row's list
+  }
+  __syncthreads();
+  for (unsigned long long i = c0 + threadIdx.x; i < c1; i += kRowThreads) {
+    const uint32_t v = gl[i];
+    const uint32_t a = v >> 16;
+    pl[base[a] + atomicAdd(&rc[a - r0], 1u)] = (uint16_t)(v & 0xFFFFu);
+  }
+  (void)gbeg_all;
+}
+
+// row bases / slices per rank (0 slices for a rank heading no pair); nsl[F] = 0 for the total
+__global__ void k_pl_slices(const unsigned long long* __restrict__ off, int64_t F, int64_t n_wg,
+                            unsigned long long* __restrict__ base, uint32_t* __restrict__ nsl) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r < F) {
-    const uint32_t a = off[r * n_wg], b = off[(r + 1) * n_wg];
-    col[r] = a;
-    nsl[r] = (b - a + kSlice - 1) / kSlice;
+    const unsigned long long a = off[r * n_wg], b = off[(r + 1) * n_wg];
+    base[r] = a;
+    nsl[r] = (uint32_t)((b - a + kSlice - 1) / kSlice);
   } else if (r == F) {
-    col[F] = off[F * n_wg];
+    base[F] = off[F * n_wg];
     nsl[F] = 0u;
   }
 }
 
-__global__ __launch_bounds__(kRowThreads) void k_pr_rows(
-    const uint32_t* __restrict__ slice_off, int64_t F, const uint32_t* __restrict__ col,
-    const uint32_t* __restrict__ csc, const uint2* __restrict__ txrec,
-    const uint16_t* __restrict__ fit, uint32_t* __restrict__ gram, int64_t ld) {
+__global__ __launch_bounds__(kRowThreads) void k_pl_rows(
+    const uint32_t* __restrict__ slice_off, int64_t F, const unsigned long long* __restrict__ base,
+    const uint16_t* __restrict__ pl, uint32_t* __restrict__ gram, int64_t ld) {
   extern __shared__ uint32_t acc[];
   __shared__ int32_t s_r;
   if (threadIdx.x == 0) {  // the rank whose slices hold this block: last r with slice_off[r] <= b
@@ -119,17 +221,9 @@ __global__ __launch_bounds__(kRowThreads) void k_pr_rows(
   const uint32_t r = (uint32_t)s_r;
   const uint32_t k = blockIdx.x - slice_off[r];
   const uint32_t nsl = slice_off[r + 1] - slice_off[r];
-  const uint32_t b0 = col[r] + k * kSlice;
-  const uint32_t b1 = min(b0 + kSlice, col[r + 1]);
-  for (uint32_t i = b0 + threadIdx.x; i < b1; i += kRowThreads) {
-    const uint2 rec = txrec[csc[i]];
-    const uint16_t* it = fit + rec.x;
-    for (int j = (int)rec.y - 1; j >= 0; --j) {
-      const uint32_t y = it[j];
-      if (y <= r) break;
-      atomicAdd(&acc[y], 1u);
-    }
-  }
+  const unsigned long long b0 = base[r] + (unsigned long long)k * kSlice;
+  const unsigned long long b1 = min(b0 + kSlice, base[r + 1]);
+  for (unsigned long long i = b0 + threadIdx.x; i < b1; i += kRowThreads) atomicAdd(&acc[pl[i]], 1u);
   __syncthreads();
   uint32_t* row = gram + (int64_t)r * ld;
   if (nsl == 1) {
@@ -146,7 +240,14 @@ struct PairRows::Impl {
   Buf<int16_t> pr;
   Buf<uint2> txrec;
   Buf<uint16_t> fit;
-  Buf<uint32_t> hist, hoff, col, nsl, soff, csc;
+  Buf<unsigned long long> hist, hoff, base;
+  Buf<uint32_t> nsl, soff;
+  Buf<uint16_t> pl;  // the pair lists, row after row
+  Buf<uint32_t> gl;  // the group lists (a << 16 | b)
+  Buf<uint8_t> grp;
+  Buf<unsigned long long> gcur;
+  Buf<uint32_t> grow, gch, meta, rcur;
+  int64_t pairs = 0;
   Buf<unsigned long long> ctr;
   Buf<unsigned> err;
   Buf<uint8_t> tmp;
@@ -164,6 +265,7 @@ const uint2* PairRows::txrec() const { return p_->txrec.p; }
 const uint16_t* PairRows::fit() const { return p_->fit.p; }
 int64_t PairRows::n_rows() const { return p_->n_tx; }
 int64_t PairRows::nnz() const { return p_->nnz; }
+int64_t PairRows::pairs() const { return p_->pairs; }
 
 size_t PairRows::lds_bytes(int64_t F) { return (size_t)std::max<int64_t>(F, 1) * 4; }
 
@@ -172,7 +274,7 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   Impl& I = *p_;
   const int64_t F = in.F;
   KMLS_CHECK(F >= 0 && F <= 32768 && ld >= F, "pair rows: F <= 32768 ranks, ld >= F");
-  I.n_tx = I.nnz = 0;
+  I.n_tx = I.nnz = I.pairs = 0;
   if (F > 0) ok(hipMemsetAsync(gram, 0, (size_t)F * ld * 4, s), "gram zero");
   if (F < 2 || in.n_tx <= 0) return true;
   // 1. frequent-rank CSR
@@ -217,41 +319,64 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   }
   KMLS_CHECK(I.nnz < (1ll << 32), "pair rows: the rank CSR passed 2^32 entries");
   if (I.n_tx == 0) return true;
-  // 2. CSC by per-block histograms, rank-major scan, LDS-cursor fill
+  // 2. pair lists by per-block histograms, a rank-major scan, LDS-cursor fill
   const int64_t n_wg = (I.n_tx + kBlockTx - 1) / kBlockTx;
   const int64_t H = F * n_wg;
   KMLS_CHECK(H + 1 < (1ll << 31), "pair rows: histogram too large");
   I.hist.need((size_t)H + 1);
   I.hoff.need((size_t)H + 1);
-  ok(hipMemsetAsync(I.hist.p + H, 0, 4, s), "hist tail");
+  ok(hipMemsetAsync(I.hist.p + H, 0, 8, s), "hist tail");
   const size_t lds = lds_bytes(F);
   if (lds > 65536) {  // past the default dynamic-LDS limit (F > 16384): up to 160 KB per block
-    ok(hipFuncSetAttribute((const void*)k_pr_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
-    ok(hipFuncSetAttribute((const void*)k_pr_fill, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
-    ok(hipFuncSetAttribute((const void*)k_pr_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
+    ok(hipFuncSetAttribute((const void*)k_pl_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
+    ok(hipFuncSetAttribute((const void*)k_pl_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
+    ok(hipFuncSetAttribute((const void*)k_pl_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
   }
-  hipLaunchKernelGGL(k_pr_hist, dim3((unsigned)n_wg), dim3(kRowThreads), lds, s, I.txrec.p, I.n_tx,
+  hipLaunchKernelGGL(k_pl_hist, dim3((unsigned)n_wg), dim3(kRowThreads), lds, s, I.txrec.p, I.n_tx,
                      I.fit.p, F, n_wg, I.hist.p);
   ok(hipGetLastError(), "hist");
-  devbuf::scan_u32(I.hist.p, I.hoff.p, H + 1, I.tmp, s);
-  I.csc.need((size_t)I.nnz);
-  hipLaunchKernelGGL(k_pr_fill, dim3((unsigned)n_wg), dim3(kRowThreads), lds, s, I.txrec.p, I.n_tx,
-                     I.fit.p, F, n_wg, I.hoff.p, I.csc.p);
-  ok(hipGetLastError(), "fill");
-  // 3. row slices, then the rows
-  I.col.need((size_t)F + 1);
+  devbuf::scan_u64(I.hist.p, I.hoff.p, H + 1, I.tmp, s);
+  I.base.need((size_t)F + 1);
   I.nsl.need((size_t)F + 1);
   I.soff.need((size_t)F + 1);
-  hipLaunchKernelGGL(k_pr_slices, dim3((unsigned)((F + 1 + 255) / 256)), dim3(256), 0, s, I.hoff.p,
-                     F, n_wg, I.col.p, I.nsl.p);
+  hipLaunchKernelGGL(k_pl_slices, dim3((unsigned)((F + 1 + 255) / 256)), dim3(256), 0, s, I.hoff.p,
+                     F, n_wg, I.base.p, I.nsl.p);
   ok(hipGetLastError(), "slices");
   devbuf::scan_u32(I.nsl.p, I.soff.p, F + 1, I.tmp, s);
-  ok(hipMemcpyAsync(I.h, I.soff.p + F, 4, hipMemcpyDeviceToHost, s), "rb");
+  I.grp.need((size_t)F);
+  I.gcur.need(kNG);
+  I.grow.need(2 * kNG);
+  I.gch.need(kNG + 1);
+  I.meta.need(4);
+  hipLaunchKernelGGL(k_pl_groups, dim3(1), dim3(1024), 0, s, I.base.p, F, I.grp.p, I.gcur.p,
+                     I.grow.p, I.gch.p, I.meta.p);
+  ok(hipGetLastError(), "groups");
+  ok(hipMemcpyAsync(I.h, I.base.p + F, 8, hipMemcpyDeviceToHost, s), "rb");
+  ok(hipMemcpyAsync(I.h + 1, I.soff.p + F, 4, hipMemcpyDeviceToHost, s), "rb");
+  ok(hipMemcpyAsync(I.h + 2, I.meta.p, 4, hipMemcpyDeviceToHost, s), "rb");
   wait();
-  const uint32_t n_sl = (uint32_t)(I.h[0] & 0xFFFFFFFFull);
+  I.pairs = (int64_t)I.h[0];
+  const uint32_t n_sl = (uint32_t)(I.h[1] & 0xFFFFFFFFull);
+  const uint32_t n_ch = (uint32_t)(I.h[2] & 0xFFFFFFFFull);
+  if (I.pairs == 0) return true;
+  // pass A: group lists; pass B: row lists
+  I.gl.need((size_t)I.pairs);
+  I.pl.need((size_t)I.pairs);
+  I.rcur.need((size_t)F);
+  ok(hipMemsetAsync(I.rcur.p, 0, (size_t)F * 4, s), "rcur");
+  const int64_t n_pb = (I.n_tx + kPartTx - 1) / kPartTx;
+  hipLaunchKernelGGL(k_pl_part, dim3((unsigned)n_pb), dim3(kPartTx), (size_t)F, s, I.txrec.p,
+                     I.n_tx, I.fit.p, F, I.grp.p, I.gcur.p, I.gl.p);
+  ok(hipGetLastError(), "part");
+  if (n_ch > 0)
+    hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds, s, I.gl.p,
+                       (const unsigned long long*)nullptr, I.base.p, I.grow.p, I.gch.p, I.rcur.p,
+                       I.pl.p);
+  ok(hipGetLastError(), "split");
+  // 3. the rows
   if (n_sl > 0)
-    hipLaunchKernelGGL(k_pr_rows, dim3(n_sl), dim3(kRowThreads), lds, s, I.soff.p, F, I.col.p,
-                       I.csc.p, I.txrec.p, I.fit.p, gram, ld);
+    hipLaunchKernelGGL(k_pl_rows, dim3(n_sl), dim3(kRowThreads), lds, s, I.soff.p, F, I.base.p,
+                       I.pl.p, gram, ld);
   ok(hipGetLastError(), "rows");
   return true;
 }
