@@ -864,7 +864,8 @@ void GpuMiner::load_csr(const int64_t* tx_ptr, const int32_t* items, int64_t n_t
     KMLS_CHECK(it >= 0 && it < n_items, "item id out of range in CSR");
   }
   KMLS_HIP(hipMalloc((void**)&d_tx_ptr_, rebased.size() * sizeof(int64_t)));
-  KMLS_HIP(hipMalloc((void**)&d_items_, (size_t)std::max<int64_t>(nnz_, 4) * sizeof(int32_t)));
+  // (+16 items of padding: the filter kernels read 16-byte vectors that may run past the end)
+  KMLS_HIP(hipMalloc((void**)&d_items_, (size_t)(std::max<int64_t>(nnz_, 4) + 16) * sizeof(int32_t)));
   KMLS_HIP(hipMemcpyAsync(d_tx_ptr_, rebased.data(), rebased.size() * sizeof(int64_t),
                           hipMemcpyHostToDevice, s));
   if (nnz_)
@@ -1084,7 +1085,7 @@ bool GpuMiner::pair_rows_count(uint32_t* gram, int64_t ld) {
   if (!prows_) prows_ = std::make_shared<kern::PairRows>();
   auto* P = static_cast<kern::PairRows*>(prows_.get());
   const int64_t F = (int64_t)fi_.ids.size();
-  kern::PrInput in{d_tx_ptr_, d_items_, n_tx_, n_items_, d_ids_, F, n_cus_};
+  kern::PrInput in{d_tx_ptr_, d_items_, n_tx_, n_items_, d_ids_, F, n_cus_, d_fmask_};
   Comm* c = comm_;
   return P->count(in, gram, ld, s, [&] {
     if (c) c->wait_stream(s);

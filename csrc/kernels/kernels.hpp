@@ -268,6 +268,7 @@ struct PrInput {
   const int32_t* ids;     // rank -> item
   int64_t F;
   int n_cus;
+  const uint32_t* fmask = nullptr;  // frequent-item bit mask (large vocabularies), or null
 };
 class PairRows {  // grow-only device buffers kept across calls
  public:

@@ -290,6 +290,12 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   unsigned long long nnz_cap = std::max<unsigned long long>(I.fit.cap, 1ull << 20);
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((in.n_tx + 255) / 256,
                                                                       (int64_t)in.n_cus * 32));
+  // the LDS-mask filter when the frequent-item mask fits next to the wave buffers
+  const int64_t mask_words = (in.n_items + 31) / 32;
+  const bool lds_mask = in.fmask != nullptr && mask_words * 4 <= (128 << 10);
+  if (lds_mask && mask_words * 4 > 65536)
+    ok(hipFuncSetAttribute((const void*)devbuf::k_map_filter_lds,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(mask_words * 4)), "attr");
   for (int attempt = 0;; ++attempt) {
     I.txrec.need(tx_cap);
     I.fit.need(nnz_cap);
@@ -297,8 +303,18 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
     nnz_cap = I.fit.cap;
     ok(hipMemsetAsync(I.ctr.p, 0, sizeof(unsigned long long), s), "ctr");
     ok(hipMemsetAsync(I.err.p, 0, sizeof(unsigned), s), "err");
-    hipLaunchKernelGGL(devbuf::k_map_filter, dim3(g), dim3(256), 0, s, in.tx_ptr, in.items, in.n_tx,
-                       I.pr.p, 2u, I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p);
+    if (lds_mask) {
+      const int64_t chunks = (in.n_tx + 63) / 64;
+      const unsigned gm = (unsigned)std::max<int64_t>(
+          1, std::min<int64_t>((chunks + devbuf::kMW - 1) / devbuf::kMW, (int64_t)in.n_cus * 2));
+      hipLaunchKernelGGL(devbuf::k_map_filter_lds, dim3(gm), dim3(64 * devbuf::kMW),
+                         (size_t)mask_words * 4, s, in.tx_ptr, in.items, in.n_tx, in.fmask,
+                         mask_words, I.pr.p, 2u, I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap,
+                         I.err.p);
+    } else {
+      hipLaunchKernelGGL(devbuf::k_map_filter, dim3(g), dim3(256), 0, s, in.tx_ptr, in.items,
+                         in.n_tx, I.pr.p, 2u, I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p);
+    }
     ok(hipGetLastError(), "filter");
     ok(hipMemcpyAsync(I.h, I.ctr.p, 8, hipMemcpyDeviceToHost, s), "rb");
     ok(hipMemcpyAsync(I.h + 1, I.err.p, 4, hipMemcpyDeviceToHost, s), "rb");

@@ -170,3 +170,37 @@ def test_cooc_flags_duplicate_rows(gpu_mod, method):
     assert g.pair_counts_csr(gram.data_ptr(), F)
     with pytest.raises(Exception, match="duplicate"):
         g.cooc_check()
+
+
+def test_pair_rows_long_rows_large_vocab(gpu_mod):
+    """A >= 64k-item vocabulary (the LDS-mask filter) whose rows hold more frequent items than
+    the 16-entry register sort (in-place path): the row count equals the numpy Gram."""
+    import torch
+    rng = np.random.default_rng(3)
+    T, I, hot = 70_000, 100_000, 48
+    rows = []
+    for t in range(T):
+        r = rng.choice(I - hot, 6, replace=False)
+        if t % 20 == 0:
+            r = np.concatenate([r, I - hot + rng.choice(hot, 24, replace=False)])
+        rows.append(np.sort(r))
+    ptr = np.zeros(T + 1, np.int64)
+    ptr[1:] = np.cumsum([len(r) for r in rows])
+    items = np.concatenate(rows).astype(np.int32)
+    g = _miner(gpu_mod, ptr, items, I)
+    counts = np.bincount(items, minlength=I).astype(np.uint32)
+    F = g.select(counts, T, 500 / T)
+    assert F >= hot
+    gram = torch.zeros((F, F), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert g.pair_counts_csr(gram.data_ptr(), F)
+    g.synchronize()
+    ids = np.asarray(g.frequent()[0])
+    col = np.full(I, -1, np.int64)
+    col[ids] = np.arange(F)
+    X = np.zeros((T, F), dtype=np.float64)  # one-hot over the frequent items only
+    rix = np.repeat(np.arange(T), np.diff(ptr))
+    keep = col[items] >= 0
+    X[rix[keep], col[items][keep]] = 1.0
+    got = np.triu(gram.cpu().numpy().astype(np.int64), 1)
+    np.testing.assert_array_equal(got, np.triu(np.rint(X.T @ X).astype(np.int64), 1))
