@@ -40,9 +40,11 @@ Secondary fields:
                     counted from the CSR, row blocks reduce-scattered, per-rank CSR, gather),
                     then rules.idx + hot reload + batched queries; gram rows and sampled
                     rule-map rows re-counted on the host.
-* ``config3_shard`` — (N > 1) the same problem with item-sharded bitmaps (1/N per rank)
-                    (native RCCL communicator at N > 1 once ``native_rccl`` worked, else the
-                    host one), sampled supports recounted on the host from the CSR shards.
+* ``config3_shard`` — the same problem item-sharded (every N): the ranks all-gather their
+                    frequent-rank CSRs, then each counts the pair rows and the horizontal
+                    levels of its own items (``GpuMiner.mine_shard``, no bitmap, no count
+                    reduction); sub-tries gathered on rank 0, digest compared with tx mode,
+                    sampled supports recounted on the host from the CSR shards.
 * ``native_rccl`` — at N > 1 the headline combine once more through the native RCCL
                     communicator (``csrc/host/comm_rccl.cpp``), digest compared.
 
@@ -403,11 +405,12 @@ def main() -> int:
             out.setdefault("errors", {})["config5"] = repr(e)[:300]
         wd.disarm()
 
-    # ---- config 3 with item-sharded bitmaps (1/N of the bitmap per rank; N > 1 only) ----
-    if world > 1 and not args.no_config3 and not args.cpu:
+    # ---- config 3 item-sharded (every N: each rank counts the pair rows and horizontal
+    #      levels of its own items over the all-gathered frequent-rank CSRs) ----
+    if not args.no_config3 and not args.cpu:
         wd.arm("config3_shard", 300)
         try:
-            c3s = bm.run_config3(N, world, rank, device, steps=1, warmup=1, mode="shard")
+            c3s = bm.run_config3(N, world, rank, device, steps=3, warmup=1, mode="shard")
             if rank == 0:
                 c3s["digest_equal_tx"] = c3s.get("digest") == out.get("config3", {}).get("digest")
                 out["config3_shard"] = c3s

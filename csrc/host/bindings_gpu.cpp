@@ -431,6 +431,19 @@ void register_gpu_bindings(py::module_& m) {
         return result_to_dict(std::move(r));
       }, py::arg("comm"), py::arg("global_n_tx"), py::arg("min_support"), py::arg("max_len") = 0,
          py::arg("download") = true, py::arg("mfma") = false, py::arg("support_tiles") = 4)
+      .def("mine_shard", [](gpu::GpuMiner& g, gpu::Comm* comm, int64_t global_n_tx, double ms,
+                            int max_len, bool download, int support_tiles) -> py::object {
+        gpu::GpuMineResult r;
+        bool declined = false;
+        {
+          py::gil_scoped_release nogil;
+          r = g.mine_shard(comm, global_n_tx, make_cfg(ms, max_len, false, true, false), download,
+                           support_tiles, &declined);
+        }
+        if (declined) return py::none();
+        return result_to_dict(std::move(r));
+      }, py::arg("comm"), py::arg("global_n_tx"), py::arg("min_support"), py::arg("max_len") = 0,
+         py::arg("download") = true, py::arg("support_tiles") = 4)
       .def("mine_deep", [](gpu::GpuMiner& g, double ms, int max_len, int rank, int world,
                            py::object comm, unsigned long long budget0, unsigned long long budget,
                            unsigned split_min, int blocks_per_cu, int stack_mb, bool steal,

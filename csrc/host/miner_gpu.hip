@@ -1086,11 +1086,19 @@ bool GpuMiner::pair_rows_count(uint32_t* gram, int64_t ld) {
   auto* P = static_cast<kern::PairRows*>(prows_.get());
   const int64_t F = (int64_t)fi_.ids.size();
   kern::PrInput in{d_tx_ptr_, d_items_, n_tx_, n_items_, d_ids_, F, n_cus_, d_fmask_};
-  Comm* c = comm_;
-  return P->count(in, gram, ld, s, [&] {
+  Comm* c = comm_ ? comm_ : shard_comm_;
+  auto wait = [&] {
     if (c) c->wait_stream(s);
     else KMLS_HIP(hipStreamSynchronize(s));
-  });
+  };
+  if (shard_comm_ && shard_comm_->world() > 1) {
+    kern::PrShard sh{shard_comm_->rank(), shard_comm_->world(),
+                     [&](const void* send, void* recv, size_t words) {
+                       shard_comm_->all_gather(send, recv, words, CommDtype::U32, s);
+                     }};
+    return P->count(in, gram, ld, s, wait, &sh);
+  }
+  return P->count(in, gram, ld, s, wait);
 }
 
 bool GpuMiner::pair_counts_csr(uintptr_t out_dev, int64_t ld) {
@@ -2303,14 +2311,12 @@ GpuMineResult GpuMiner::mine(const MineConfig& cfg, bool download, bool prefetch
 }
 
 
-GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineConfig& cfg,
-                                  bool download, int support_tiles) {
-  drain_prefetch();  // a launched-ahead resident call shares the device buffers
-  KMLS_HIP(hipSetDevice(device_));
+// Steps 1-2 of the tx-DP call (and of the item-sharded one): supports of the shard in K tiles,
+// all-reduced over the ranks (tile k's all-reduce on the comm stream overlaps tile k+1's
+// histogram), then the frequent-item selection on the device.  Returns F.
+int64_t GpuMiner::txdp_select(Comm* comm, int64_t global_n_tx, const MineConfig& cfg,
+                              int support_tiles) {
   hipStream_t s = (hipStream_t)stream_;
-  auto t0 = std::chrono::steady_clock::now();
-  Event e0, e1, e2;
-  KMLS_HIP(hipEventRecord(e0.e, s));
   const size_t mark = arena_->mark();
   // 1. supports in K tiles; tile k's all-reduce (comm stream) overlaps tile k+1's histogram.
   //    The comm stream and the tile events live as long as the miner (no per-call creation).
@@ -2358,6 +2364,18 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
     arena_->pop_to(mark);
     F = select(cnt.data(), global_n_tx, cfg.min_support);
   }
+  return F;
+}
+
+GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineConfig& cfg,
+                                  bool download, int support_tiles) {
+  drain_prefetch();  // a launched-ahead resident call shares the device buffers
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  auto t0 = std::chrono::steady_clock::now();
+  Event e0, e1, e2;
+  KMLS_HIP(hipEventRecord(e0.e, s));
+  const int64_t F = txdp_select(comm, global_n_tx, cfg, support_tiles);
   KMLS_HIP(hipEventRecord(e1.e, s));
   // 3. shard-local bitmaps (none when every level is counted horizontally from the CSR)
   const int64_t Wp = words_local();
@@ -2393,6 +2411,49 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
   ph.push_back({hl ? "cooc_stats" : "encode_bitmap", elapsed(e1, e2)});
   for (auto& p : r.phases) ph.push_back(p);
   r.phases = ph;
+  r.stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return r;
+}
+
+// Item-sharded mining without bitmaps (the horizontal plan): supports/selection as in tx-DP,
+// then every rank all-gathers the frequent-rank CSR (PairRows, PrShard) and counts the pair rows
+// of its own items (rank a % world == r) and the horizontal levels of their subtrees — complete
+// counts from every transaction, so nothing else is reduced.  The result is this rank's
+// sub-trie (level 1 + its roots' subtrees); the caller gathers them (dist_miner.gather_trie).
+// declined = true (nothing mined) when the shard is not long and sparse enough for the plan.
+GpuMineResult GpuMiner::mine_shard(Comm* comm, int64_t global_n_tx, const MineConfig& cfg,
+                                   bool download, int support_tiles, bool* declined) {
+  drain_prefetch();
+  KMLS_HIP(hipSetDevice(device_));
+  hipStream_t s = (hipStream_t)stream_;
+  auto t0 = std::chrono::steady_clock::now();
+  Event e0, e1;
+  KMLS_HIP(hipEventRecord(e0.e, s));
+  const int64_t F = txdp_select(comm, global_n_tx, cfg, support_tiles);
+  const int64_t Wp = words_local();
+  *declined = !hlevels_plan(cfg, F, Wp, comm);
+  KMLS_HIP(hipEventRecord(e1.e, s));
+  if (*declined) return GpuMineResult{};
+  shard_comm_ = comm;
+  gram_csr_ok_ = true;
+  hl_plan_ = true;
+  GpuMineResult r;
+  try {
+    r = mine_bitmaps(0, Wp, cfg, nullptr, true, download);
+  } catch (...) {
+    shard_comm_ = nullptr;
+    gram_csr_ok_ = false;
+    hl_plan_ = false;
+    throw;
+  }
+  shard_comm_ = nullptr;
+  gram_csr_ok_ = false;
+  hl_plan_ = false;
+  std::vector<Phase> ph;
+  ph.push_back({"support_tiles+allreduce+select", elapsed(e0, e1)});
+  for (auto& p : r.phases) ph.push_back(p);
+  r.phases = ph;
+  r.levels_path = "horizontal-item-shard";
   r.stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return r;
 }

@@ -264,6 +264,11 @@ class GpuMiner {
   // ever replicating bitmaps.  comm == nullptr behaves as world size 1.
   GpuMineResult mine_txdp(Comm* comm, int64_t global_n_tx, const MineConfig& cfg, bool download,
                           int support_tiles);
+  // Item-sharded mining of sparse long shards without bitmaps (miner_gpu.hip): this rank's
+  // sub-trie (level 1 + the subtrees of ranks r with r % world == rank); *declined when the
+  // horizontal plan does not apply (nothing mined: the caller takes the bitmap protocol)
+  GpuMineResult mine_shard(Comm* comm, int64_t global_n_tx, const MineConfig& cfg, bool download,
+                           int support_tiles, bool* declined);
   // Count-only full mining (short transactions, T <= 4096): every rank holds the full CSR and
   // builds the level-2 classes; rank r mines level-3 tasks t with t % world == r; counts and
   // digests are combined through `comm` (nullptr: world must be 1, or the caller combines).
@@ -413,6 +418,8 @@ class GpuMiner {
   std::shared_ptr<void> prows_;   // kern::PairRows: level-2 pair counts row by row in LDS
   bool pair_rows_ok(int64_t F) const;
   int64_t cooc_pairs_sampled();
+  int64_t txdp_select(Comm* comm, int64_t global_n_tx, const MineConfig& cfg, int support_tiles);
+  Comm* shard_comm_ = nullptr;    // mine_shard: the CSR all-gather's communicator
   int64_t hl_pairs_est_ = -1;
   bool prows_fresh_ = false;      // the last pair_counts_csr used the row count (its CSR is valid)
   bool pair_rows_count(uint32_t* gram, int64_t ld);

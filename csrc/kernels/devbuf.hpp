@@ -34,6 +34,19 @@ struct Buf {  // grow-only (25 % headroom), kept across calls
     hip_ok(hipMalloc((void**)&p, c * sizeof(T)), "Buf alloc");
     cap = c;
   }
+  // grow keeping the first `used` elements (stream-ordered copy)
+  void need_keep(size_t n, size_t used, hipStream_t s) {
+    if (n <= cap) return;
+    T* old = p;
+    const size_t c = std::max<size_t>(n + (n >> 2), 1024);
+    hip_ok(hipMalloc((void**)&p, c * sizeof(T)), "Buf alloc");
+    if (old && used) hip_ok(hipMemcpyAsync(p, old, used * sizeof(T), hipMemcpyDeviceToDevice, s), "Buf copy");
+    if (old) {
+      hip_ok(hipStreamSynchronize(s), "Buf sync");
+      hip_ok(hipFree(old), "Buf free");
+    }
+    cap = c;
+  }
   Buf() = default;
   Buf(const Buf&) = delete;
   Buf& operator=(const Buf&) = delete;

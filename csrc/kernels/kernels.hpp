@@ -270,6 +270,14 @@ struct PrInput {
   int n_cus;
   const uint32_t* fmask = nullptr;  // frequent-item bit mask (large vocabularies), or null
 };
+// Item-sharded counting: the ranks' frequent-rank CSRs are all-gathered (every rank then holds
+// every transaction's frequent ranks) and this rank counts only the rows a with a % world == rank
+// (the other gram rows stay zero), so every owned row is complete without a gram reduction.
+struct PrShard {
+  int rank, world;
+  // all-gather of `words` u32 per rank from send into recv (world * words), on the stream
+  std::function<void(const void* send, void* recv, size_t words)> all_gather;
+};
 class PairRows {  // grow-only device buffers kept across calls
  public:
   PairRows();
@@ -280,7 +288,7 @@ class PairRows {  // grow-only device buffers kept across calls
   // zero.  False (gram zeroed, nothing counted): a transaction holds > 65535 frequent items.
   // `wait` is the host wait for s (bounded under a communicator).
   bool count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t s,
-             const std::function<void()>& wait);
+             const std::function<void()>& wait, const struct PrShard* shard = nullptr);
   // the frequent-rank CSR of the last count: rows (off, len) of >= 2 ranks, ascending
   const uint2* txrec() const;
   const uint16_t* fit() const;

@@ -56,7 +56,8 @@ __global__ __launch_bounds__(kRowThreads) void k_pl_hist(const uint2* __restrict
                                                          int64_t n_tx,
                                                          const uint16_t* __restrict__ fit, int64_t F,
                                                          int64_t n_wg,
-                                                         unsigned long long* __restrict__ hist) {
+                                                         unsigned long long* __restrict__ hist,
+                                                         int own_rank, int own_world) {
   extern __shared__ uint32_t h[];
   for (int64_t i = threadIdx.x; i < F; i += kRowThreads) h[i] = 0u;
   __syncthreads();
@@ -65,7 +66,8 @@ __global__ __launch_bounds__(kRowThreads) void k_pl_hist(const uint2* __restrict
   for (int64_t t = t0 + threadIdx.x; t < t1; t += kRowThreads) {
     const uint2 rec = txrec[t];
     const uint16_t* it = fit + rec.x;
-    for (uint32_t i = 0; i + 1 < rec.y; ++i) atomicAdd(&h[it[i]], rec.y - 1u - i);
+    for (uint32_t i = 0; i + 1 < rec.y; ++i)
+      if ((int)(it[i] % (uint32_t)own_world) == own_rank) atomicAdd(&h[it[i]], rec.y - 1u - i);
   }
   __syncthreads();
   for (int64_t r = threadIdx.x; r < F; r += kRowThreads) hist[r * n_wg + blockIdx.x] = h[r];
@@ -123,7 +125,8 @@ __global__ __launch_bounds__(kPartTx) void k_pl_part(const uint2* __restrict__ t
                                                      const uint16_t* __restrict__ fit, int64_t F,
                                                      const uint8_t* __restrict__ grp_g,
                                                      unsigned long long* __restrict__ gcur,
-                                                     uint32_t* __restrict__ gl) {
+                                                     uint32_t* __restrict__ gl, int own_rank,
+                                                     int own_world) {
   extern __shared__ uint8_t grp[];  // [F]
   __shared__ uint32_t cnt[kNG];
   __shared__ unsigned long long gb[kNG];
@@ -134,7 +137,8 @@ __global__ __launch_bounds__(kPartTx) void k_pl_part(const uint2* __restrict__ t
   uint2 rec = make_uint2(0u, 0u);
   if (t < n_tx) rec = txrec[t];
   const uint16_t* it = fit + rec.x;
-  for (uint32_t i = 0; i + 1 < rec.y; ++i) atomicAdd(&cnt[grp[it[i]]], rec.y - 1u - i);
+  for (uint32_t i = 0; i + 1 < rec.y; ++i)
+    if ((int)(it[i] % (uint32_t)own_world) == own_rank) atomicAdd(&cnt[grp[it[i]]], rec.y - 1u - i);
   __syncthreads();
   if (threadIdx.x < kNG) {
     const uint32_t c = cnt[threadIdx.x];
@@ -144,6 +148,7 @@ __global__ __launch_bounds__(kPartTx) void k_pl_part(const uint2* __restrict__ t
   __syncthreads();
   for (uint32_t i = 0; i + 1 < rec.y; ++i) {
     const uint32_t a = it[i], n = rec.y - 1u - i;
+    if ((int)(a % (uint32_t)own_world) != own_rank) continue;
     const uint32_t g = grp[a];
     uint32_t* dst = gl + gb[g] + atomicAdd(&cnt[g], n);
     for (uint32_t j = 0; j < n; ++j) dst[j] = (a << 16) | (uint32_t)it[i + 1u + j];
@@ -186,6 +191,36 @@ __global__ __launch_bounds__(kRowThreads) void k_pl_split(
     pl[base[a] + atomicAdd(&rc[a - r0], 1u)] = (uint16_t)(v & 0xFFFFu);
   }
   (void)gbeg_all;
+}
+
+// all-gathered CSRs (world blocks of cap_tx records / cap_nnz items) -> one CSR: rank q's rows
+// at tbase[q], its items at nbase[q] (record offsets rebased)
+__global__ void k_pr_gather_rows(const uint2* __restrict__ rec_all, int64_t cap_tx,
+                                 const unsigned long long* __restrict__ sz, int world,
+                                 uint2* __restrict__ out) {
+  const int q = blockIdx.y;
+  unsigned long long tb = 0, nb = 0;
+  for (int i = 0; i < q; ++i) {
+    tb += sz[2 * i];
+    nb += sz[2 * i + 1];
+  }
+  const unsigned long long n = sz[2 * q];
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    const uint2 r = rec_all[(unsigned long long)q * cap_tx + i];
+    out[tb + i] = make_uint2((uint32_t)(r.x + nb), r.y);
+  }
+}
+__global__ void k_pr_gather_items(const uint16_t* __restrict__ fit_all, int64_t cap_nnz,
+                                  const unsigned long long* __restrict__ sz, int world,
+                                  uint16_t* __restrict__ out) {
+  const int q = blockIdx.y;
+  unsigned long long nb = 0;
+  for (int i = 0; i < q; ++i) nb += sz[2 * i + 1];
+  const unsigned long long n = sz[2 * q + 1];
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (unsigned long long)gridDim.x * blockDim.x)
+    out[nb + i] = fit_all[(unsigned long long)q * cap_nnz + i];
 }
 
 // row bases / slices per rank (0 slices for a rank heading no pair); nsl[F] = 0 for the total
@@ -247,6 +282,10 @@ struct PairRows::Impl {
   Buf<uint8_t> grp;
   Buf<unsigned long long> gcur;
   Buf<uint32_t> grow, gch, meta, rcur;
+  Buf<uint2> gtxrec, txrec_all;     // item-sharded: the all-gathered CSR (and the raw blocks)
+  Buf<uint16_t> gfit, fit_all;
+  Buf<unsigned long long> gsz;
+  bool gathered = false;
   int64_t pairs = 0;
   Buf<unsigned long long> ctr;
   Buf<unsigned> err;
@@ -261,8 +300,8 @@ struct PairRows::Impl {
 
 PairRows::PairRows() : p_(new Impl) {}
 PairRows::~PairRows() { delete p_; }
-const uint2* PairRows::txrec() const { return p_->txrec.p; }
-const uint16_t* PairRows::fit() const { return p_->fit.p; }
+const uint2* PairRows::txrec() const { return p_->gathered ? p_->gtxrec.p : p_->txrec.p; }
+const uint16_t* PairRows::fit() const { return p_->gathered ? p_->gfit.p : p_->fit.p; }
 int64_t PairRows::n_rows() const { return p_->n_tx; }
 int64_t PairRows::nnz() const { return p_->nnz; }
 int64_t PairRows::pairs() const { return p_->pairs; }
@@ -270,11 +309,13 @@ int64_t PairRows::pairs() const { return p_->pairs; }
 size_t PairRows::lds_bytes(int64_t F) { return (size_t)std::max<int64_t>(F, 1) * 4; }
 
 bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t s,
-                     const std::function<void()>& wait) {
+                     const std::function<void()>& wait, const PrShard* shard) {
   Impl& I = *p_;
   const int64_t F = in.F;
   KMLS_CHECK(F >= 0 && F <= 32768 && ld >= F, "pair rows: F <= 32768 ranks, ld >= F");
   I.n_tx = I.nnz = I.pairs = 0;
+  I.gathered = false;
+  const int own_rank = shard ? shard->rank : 0, own_world = shard ? std::max(shard->world, 1) : 1;
   if (F > 0) ok(hipMemsetAsync(gram, 0, (size_t)F * ld * 4, s), "gram zero");
   if (F < 2 || in.n_tx <= 0) return true;
   // 1. frequent-rank CSR
@@ -333,8 +374,44 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
     tx_cap = nt;
     nnz_cap = nn;
   }
+  if (own_world > 1) {  // item-sharded: every rank's CSR on every rank
+    I.gsz.need((size_t)2 * own_world + 2);
+    unsigned long long mine[2] = {(unsigned long long)I.n_tx, (unsigned long long)I.nnz};
+    ok(hipMemcpyAsync(I.gsz.p + 2 * own_world, mine, 16, hipMemcpyHostToDevice, s), "sz");
+    shard->all_gather(I.gsz.p + 2 * own_world, I.gsz.p, 4);
+    std::vector<unsigned long long> sz((size_t)2 * own_world);
+    ok(hipMemcpyAsync(sz.data(), I.gsz.p, sz.size() * 8, hipMemcpyDeviceToHost, s), "sz");
+    wait();
+    unsigned long long cap_tx = 1, cap_nnz = 2, tot_tx = 0, tot_nnz = 0;
+    for (int q = 0; q < own_world; ++q) {
+      cap_tx = std::max(cap_tx, sz[2 * q]);
+      cap_nnz = std::max(cap_nnz, sz[2 * q + 1]);
+      tot_tx += sz[2 * q];
+      tot_nnz += sz[2 * q + 1];
+    }
+    cap_nnz = (cap_nnz + 1) & ~1ull;  // whole u32 words
+    KMLS_CHECK(tot_nnz < (1ull << 32) && tot_tx < (1ull << 32), "pair rows: gathered CSR too large");
+    I.txrec.need_keep(cap_tx, (size_t)I.n_tx, s);  // send blocks are read up to the cap
+    I.fit.need_keep(cap_nnz, (size_t)I.nnz, s);
+    I.txrec_all.need(cap_tx * own_world);
+    I.fit_all.need(cap_nnz * own_world);
+    shard->all_gather(I.txrec.p, I.txrec_all.p, cap_tx * 2);
+    shard->all_gather(I.fit.p, I.fit_all.p, cap_nnz / 2);
+    I.gtxrec.need(std::max<unsigned long long>(tot_tx, 1));
+    I.gfit.need(std::max<unsigned long long>(tot_nnz, 1));
+    hipLaunchKernelGGL(k_pr_gather_rows, dim3(1024, own_world), dim3(256), 0, s, I.txrec_all.p,
+                       (int64_t)cap_tx, I.gsz.p, own_world, I.gtxrec.p);
+    hipLaunchKernelGGL(k_pr_gather_items, dim3(1024, own_world), dim3(256), 0, s, I.fit_all.p,
+                       (int64_t)cap_nnz, I.gsz.p, own_world, I.gfit.p);
+    ok(hipGetLastError(), "gather");
+    I.gathered = true;
+    I.n_tx = (int64_t)tot_tx;
+    I.nnz = (int64_t)tot_nnz;
+  }
   KMLS_CHECK(I.nnz < (1ll << 32), "pair rows: the rank CSR passed 2^32 entries");
   if (I.n_tx == 0) return true;
+  const uint2* txrec = I.gathered ? I.gtxrec.p : I.txrec.p;
+  const uint16_t* fit = I.gathered ? I.gfit.p : I.fit.p;
   // 2. pair lists by per-block histograms, a rank-major scan, LDS-cursor fill
   const int64_t n_wg = (I.n_tx + kBlockTx - 1) / kBlockTx;
   const int64_t H = F * n_wg;
@@ -348,8 +425,8 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
     ok(hipFuncSetAttribute((const void*)k_pl_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
     ok(hipFuncSetAttribute((const void*)k_pl_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
   }
-  hipLaunchKernelGGL(k_pl_hist, dim3((unsigned)n_wg), dim3(kRowThreads), lds, s, I.txrec.p, I.n_tx,
-                     I.fit.p, F, n_wg, I.hist.p);
+  hipLaunchKernelGGL(k_pl_hist, dim3((unsigned)n_wg), dim3(kRowThreads), lds, s, txrec, I.n_tx,
+                     fit, F, n_wg, I.hist.p, own_rank, own_world);
   ok(hipGetLastError(), "hist");
   devbuf::scan_u64(I.hist.p, I.hoff.p, H + 1, I.tmp, s);
   I.base.need((size_t)F + 1);
@@ -381,8 +458,8 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   I.rcur.need((size_t)F);
   ok(hipMemsetAsync(I.rcur.p, 0, (size_t)F * 4, s), "rcur");
   const int64_t n_pb = (I.n_tx + kPartTx - 1) / kPartTx;
-  hipLaunchKernelGGL(k_pl_part, dim3((unsigned)n_pb), dim3(kPartTx), (size_t)F, s, I.txrec.p,
-                     I.n_tx, I.fit.p, F, I.grp.p, I.gcur.p, I.gl.p);
+  hipLaunchKernelGGL(k_pl_part, dim3((unsigned)n_pb), dim3(kPartTx), (size_t)F, s, txrec,
+                     I.n_tx, fit, F, I.grp.p, I.gcur.p, I.gl.p, own_rank, own_world);
   ok(hipGetLastError(), "part");
   if (n_ch > 0)
     hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds, s, I.gl.p,

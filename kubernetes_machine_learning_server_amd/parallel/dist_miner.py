@@ -146,6 +146,14 @@ class _GpuOps:
             torch.cuda.set_device(dm.device)
             self.stream = torch.cuda.Stream(device=dm.device)
             self.g = N.GpuMiner(dm.device, arena_bytes, self.stream.cuda_stream)
+            if dm.mode == "shard" and os.environ.get("KMLS_SHARD_NATIVE", "1") != "0":
+                # the native item-sharded path (GpuMiner.mine_shard) all-gathers rank CSRs
+                backend = comm_backend()
+                make_uid = N.host_comm_unique_id if backend == "host" else N.comm_unique_id
+                uid = [make_uid() if dm.rank == 0 and dm.world > 1 else b"\0" * 128]
+                if dm.world > 1:
+                    dist.broadcast_object_list(uid, src=0)
+                self.comm = N.Comm(dm.rank, dm.world, uid[0], dm.device, backend)
         else:
             self.stream = None  # native-only single-GPU path: the miner owns its stream
             self.g = N.GpuMiner(dm.device, arena_bytes, 0)
@@ -164,6 +172,15 @@ class _GpuOps:
     def mine_txdp(self, dm: "DistMiner", download: bool):
         return self.g.mine_txdp(self.comm, dm.n_tx, dm.min_support, dm.max_len, download,
                                 dm.mfma, dm.support_tiles)
+
+    def mine_shard(self, dm: "DistMiner", download: bool):
+        """Native item-sharded call (None: the horizontal plan declined this data)."""
+        if self.comm is None:
+            return None
+        if self.stream is not None:
+            self.stream.synchronize()
+        return self.g.mine_shard(self.comm, dm.n_tx, dm.min_support, dm.max_len, download,
+                                 dm.support_tiles)
 
     def supports(self):
         c = torch.empty(self.n_items, dtype=torch.int32, device=self.dev)
@@ -342,6 +359,26 @@ class DistMiner:
             self.last = r
             return {"stats": st, "trie": r}
         if self.mode == "shard":
+            native_shard = getattr(self.ops, "mine_shard", None)
+            r = native_shard(self, download) if native_shard is not None else None
+            if r is not None:  # sub-trie of this rank's items (gather_trie merges them)
+                st = dict(r["stats"])
+                st["rounds"] = 0
+                st["own_bitmap_bytes"] = st["replicated_bitmap_bytes"] = 0
+                st["peak_batch_bitmap_bytes"] = st["max_batch_rows"] = 0
+                st["host_phases_s"] = {k: v / 1e3 for k, v in (st.get("phases_ms") or {}).items()}
+                F = int(st["n_frequent_items"])
+                n_local = int(st["n_itemsets"]) - F + (F if self.rank == 0 else 0)
+                tot = torch.tensor([n_local], dtype=torch.int64,
+                                   device=self.ops.dev if dist.get_backend() == "nccl" else "cpu") \
+                    if self.world > 1 else None
+                if tot is not None:
+                    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+                st["n_itemsets"] = n_local
+                st["global_itemsets"] = int(tot.item()) if tot is not None else n_local
+                self._last_global = st["global_itemsets"]
+                self.last = r
+                return {"stats": st, "trie": r}
             from .item_shard import step_shard
             return step_shard(self, download)
         if self.mode == "tx":

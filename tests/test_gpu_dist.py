@@ -155,3 +155,67 @@ def test_native_ring_pair_rows_on_one_gpu(world):
         for a0, a1, rows in got["ring"]:
             assert (a0, a1) == (r0, r1)
             np.testing.assert_array_equal(rows, ref)
+
+
+def _shard_worker(rank, world, port, out_q):
+    # cooc=2: the horizontal plan even where the cost model prefers the GEMM (small F here)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), KMLS_COMM="host", KMLS_COMM_TIMEOUT_S="120",
+                      KMLS_TEST_HOOKS="cooc=2")
+    import torch.distributed as dist
+    from kubernetes_machine_learning_server_amd.ops import native
+    from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner, gather_trie
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        try:
+            tx, ms = _data("large")
+            dm = DistMiner(tx.tx_ptr, tx.items, tx.n_items, ms, device=0, mode="shard")
+            out = []
+            for _ in range(2):
+                r = dm.step(download=True)
+                st = r["stats"]
+                t = gather_trie(r["trie"], rank, world, int(st["n_frequent_items"]))
+                d = None
+                if rank == 0:
+                    d = native.load().trie_digest(t["parent"], t["item"], t["count"], t["depth"])
+                    d = (d["digest"], d["n"])
+                out.append((st.get("levels_path"), int(st["global_itemsets"]), d))
+            out_q.put((rank, out))
+        except BaseException as e:
+            import traceback
+            out_q.put((rank, "error", repr(e), traceback.format_exc()))
+            raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_native_item_shard_on_one_gpu(world):
+    """Item-sharded mining without bitmaps (GpuMiner.mine_shard): each rank all-gathers the
+    frequent-rank CSRs, counts the pair rows and horizontal levels of its own items; the
+    gathered sub-tries are the whole trie (content digest of the CPU miner)."""
+    from kubernetes_machine_learning_server_amd.ops import native
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    for _ in range(world):
+        res.append(q.get(timeout=240))
+        assert res[-1][1] != "error", res[-1]
+    res.sort(key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    tx, ms = _data("large")
+    N = native.load()
+    ref = N.mine_cpu(tx.tx_ptr, tx.items, tx.n_items, ms)
+    rd = N.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])
+    for rank, out in res:
+        for path, glob, d in out:
+            assert path == "horizontal-item-shard", path
+            assert glob == rd["n"]
+            if rank == 0:
+                assert d == (rd["digest"], rd["n"])
