@@ -627,6 +627,11 @@ void register_gpu_bindings(py::module_& m) {
     d["last_us"] = st.last_us;
     d["mean_us"] = st.requests ? st.sum_us / (double)st.requests : 0.0;
     d["kernel_mean_us"] = st.requests ? st.kernel_us / (double)st.requests : 0.0;
+    d["stage_mean_us"] = st.requests ? st.stage_us / (double)st.requests : 0.0;
+    d["compute_mean_us"] = st.requests ? st.compute_us / (double)st.requests : 0.0;
+    py::list ph;
+    for (int i = 0; i < 4; ++i) ph.append(st.requests ? st.phase_us[i] / (double)st.requests : 0.0);
+    d["phase_mean_us"] = ph;
     return d;
   }, py::arg("device") = 0);
   m.def("serve_loop_pause", [](int device, bool pause) {

@@ -490,6 +490,7 @@ class GpuRuleIndex {
   int64_t* d_row_ptr_ = nullptr;
   int32_t* d_cons_ = nullptr;
   uint32_t* d_score_ = nullptr;  // dense rank of the score (exact order key), see serve.hip
+  bool narrow_ = false;          // score ranks < 2^23: the matcher's 32-bit order keys
   uint8_t* d_is_key_ = nullptr;
   int32_t* d_id_cons_ = nullptr;  // per row: consequents sorted by id (long-merge kernel)
   int32_t* d_id_pos_ = nullptr;   // ... and their index in the score-ordered row
@@ -511,6 +512,8 @@ struct ServeLoopStats {
   uint64_t requests = 0, queries = 0, launches = 0, refused = 0;
   double last_us = 0, sum_us = 0;
   double kernel_us = 0;  // sum over requests of the kernel's own time (request seen -> done)
+  double stage_us = 0, compute_us = 0;  // ... of which: staging the request, answering it
+  double phase_us[4] = {0, 0, 0, 0};  // first query: table init + seeds, row loads, inserts, top-k
 };
 class GpuServeLoop {
  public:
@@ -518,7 +521,7 @@ class GpuServeLoop {
   // one batch; false when paused / failed (nothing answered)
   bool run(const int64_t* d_row_ptr, const int32_t* d_cons, const uint32_t* d_score,
            const uint8_t* d_is_key, int64_t n_items, const int64_t* q_ptr, int64_t B,
-           const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n);
+           const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n, bool narrow = false);
   void pause();   // stop the kernel, wait for it to exit; run() refuses until resume()
   void resume();
   ServeLoopStats stats();
@@ -528,7 +531,7 @@ class GpuServeLoop {
   explicit GpuServeLoop(int device);
   bool run_one(const int64_t* d_row_ptr, const int32_t* d_cons, const uint32_t* d_score,
                const uint8_t* d_is_key, int64_t n_items, const int64_t* q_ptr, int64_t B,
-               const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n);
+               const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n, bool narrow);
   bool ensure_running();
   void stop_and_wait();
   int device_;

@@ -640,7 +640,8 @@ int64_t groupby_csr(const int32_t* d_keys, const int32_t* d_vals, int64_t n, int
 // ---- serving (serve.hip) ----
 void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,
                       const uint8_t* is_key, int64_t n_items, const int64_t* q_ptr,
-                      const int32_t* seeds, int64_t B, int k, int32_t* out, hipStream_t s);
+                      const int32_t* seeds, int64_t B, int k, int32_t* out, hipStream_t s,
+                      bool narrow = false);
 // long-row queries (qlist: indices into the batch, each with <= 256 seeds): one workgroup
 // each, threshold-pruned exact merge; id_cons/id_pos = each row's consequents sorted by id and
 // their index in the score-ordered row
@@ -665,18 +666,26 @@ struct ServeReq {
   long long B;
   long long k;
   long long n_seeds;        // seeds follow q_ptr in the payload: [q_ptr | seeds] contiguous
+  long long narrow;         // 1: score ranks < 2^23, 32-bit order keys in the top-k
 };
 struct ServeMail {
-  unsigned req_seq;   // host -> device, written after the descriptor
-  unsigned pad0[15];
+  unsigned long long req;  // host -> device: (inline words << 32) | seq, written after the
+                           // descriptor and the inline payload
+  unsigned pad0[14];
   unsigned done_seq;  // device -> host, written after the results
   unsigned pad1[15];
   unsigned alive;     // device: 1 while the kernel runs
   unsigned pad2[15];
   unsigned stop;      // host -> device
   unsigned pad3[15];
-  ServeReq req;
-  unsigned long long t_seen, t_done;  // device wall clock: request seen, done word written
+  // device wall clock (instrumentation): request seen, descriptor + payload staged, answers in
+  // LDS, done word written
+  unsigned long long t_seen, t_staged, t_computed, t_done;
+  unsigned long long t_phase[6];  // the first query's matcher phases (wall clock)
+  // [descriptor | q_ptr (B + 1 int64) | seeds]: read by the kernel in ONE round of parallel
+  // system-scope loads (the inline word count travels in `req`)
+  ServeReq req_desc;
+  int32_t payload[kServeLoopStage];
 };
 void serve_loop_launch(ServeMail* mail, unsigned long long idle_ticks,
                        unsigned long long life_ticks, hipStream_t s);

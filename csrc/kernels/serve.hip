@@ -43,6 +43,7 @@
 
 #include "../include/kmls/gpu.hpp"
 #include "kernels.hpp"
+#include "kmls/hooks.hpp"
 
 #define KMLS_HIP(expr)                                                                  \
   do {                                                                                  \
@@ -256,13 +257,39 @@ __global__ __launch_bounds__(kBigThreads) void k_serve_topk_big(
   if (tid == 0) o[0] = n_out;
 }
 
+// Wave-wide max of a u32 through DPP row shifts and row broadcasts (an inclusive max-scan
+// whose lane 63 holds the total), then a lane-63 read: ~8 short-latency DPP steps instead of
+// six 64-lane permutes through the LDS crossbar.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x113, 0xf, 0xf, false));  // row_shr:3
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xf, 0xe, false));  // row_shr:4
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xf, 0xc, false));  // row_shr:8
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// 64-bit wave max as two u32 passes (high words, then the low words of the lanes that hold it)
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+  const uint32_t hi = wave_max_u32((uint32_t)(v >> 32));
+  const uint32_t lo = wave_max_u32((uint32_t)(v >> 32) == hi ? (uint32_t)v : 0u);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 // one query (seeds[q0, q1), request order) answered by the calling wave into o[0 .. k]: o[0] =
 // the number of ids (-1 no seed is a key, -2 host path), o[1 ..] = ids; per-wave LDS tables
 __device__ __forceinline__ void serve_query_wave(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ cons,
     const uint32_t* __restrict__ srank, const uint8_t* __restrict__ is_key, int64_t n_items,
     const int32_t* __restrict__ seeds, int64_t q0, int64_t q1, int k, int32_t* __restrict__ o,
-    int32_t* key, uint32_t* val, uint32_t* pos, int64_t* seg, int64_t* rowp, int lane) {
+    int32_t* key, uint32_t* val, uint32_t* pos, int64_t* seg, int64_t* rowp, int lane,
+    unsigned long long* stamps = nullptr, bool narrow = false) {
+  // (stamps: instrumentation, the serving loop's first query; lane 0 writes wall clock ticks)
+  auto stamp = [&](int i) {
+    if (stamps && lane == 0) stamps[i] = wall_clock64();
+  };
+  stamp(0);
   for (int i = lane; i < kSlots; i += 64) {
     key[i] = -1;
     val[i] = 0;
@@ -308,6 +335,7 @@ __device__ __forceinline__ void serve_query_wave(
     np += __popcll(bal);
     acc += __shfl(inc, 63, 64);
   }
+  stamp(1);
   if (np == 0) {
     if (lane == 0) o[0] = -1;  // no seed is a key: static fallback on the host
     return;
@@ -342,6 +370,7 @@ __device__ __forceinline__ void serve_query_wave(
       ev[u] = srank[p];
     }
   }
+  stamp(2);
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
     const int64_t e = lane + 64 * u;
@@ -359,49 +388,90 @@ __device__ __forceinline__ void serve_query_wave(
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __builtin_amdgcn_wave_barrier();
-  // ---- top-k: per-lane best over its own slots, k rounds of a wave max ----
-  auto lane_best = [&](int& slot) {
-    unsigned long long best = 0;
-    slot = -1;
-#pragma unroll 4
+  stamp(3);
+  // ---- top-k: each lane's own slots held in registers (one pipelined round of LDS loads),
+  // k rounds of a wave max; the winning lane clears its entry and re-takes its register max.
+  // (Rescanning the winner's slots from LDS every round cost ~1 us per round: 12 of the 14 us
+  // of a one-query request in the serving loop.)
+  int n_out = 0;
+  if (narrow) {
+    // score ranks < 2^23 (checked at index load) and first positions < 512: the order key fits
+    // 32 bits, so a round is one 32-bit DPP max
+    uint32_t kk[kPerLane];
+    int32_t kc[kPerLane];
+#pragma unroll
     for (int j = 0; j < kPerLane; ++j) {
       const int i = j * 64 + lane;
-      if (key[i] >= 0) {
-        const unsigned long long kk =
-            ((unsigned long long)val[i] << 32) | (unsigned long long)(0xFFFFFFFFu - pos[i]);
-        if (kk > best) {
-          best = kk;
-          slot = i;
-        }
+      const int32_t c = key[i];
+      const uint32_t v = val[i], ps = pos[i];
+      kc[j] = c;
+      kk[j] = c >= 0 ? ((v << 9) | (511u - ps)) : 0u;
+    }
+    auto reg_best = [&]() {
+      uint32_t b = 0;
+#pragma unroll
+      for (int j = 0; j < kPerLane; ++j) b = max(b, kk[j]);
+      return b;
+    };
+    uint32_t mine = reg_best();
+    for (; n_out < k; ++n_out) {
+      const uint32_t bb = wave_max_u32(mine);
+      if (bb == 0) break;
+      if (mine == bb) {
+        int32_t id = -1;
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j)
+          if (kk[j] == bb) {
+            id = kc[j];
+            kk[j] = 0u;
+          }
+        o[1 + n_out] = id;
+        mine = reg_best();
       }
     }
-    return best;
-  };
-  int my_slot;
-  unsigned long long mine = lane_best(my_slot);
-  int n_out = 0;
-  for (; n_out < k; ++n_out) {
-    unsigned long long bb = mine;
+  } else {
+    unsigned long long kk[kPerLane];
+    int32_t kc[kPerLane];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const unsigned long long t = __shfl_xor(bb, off, 64);
-      bb = t > bb ? t : bb;
+    for (int j = 0; j < kPerLane; ++j) {
+      const int i = j * 64 + lane;
+      const int32_t c = key[i];
+      const uint32_t v = val[i], ps = pos[i];
+      kc[j] = c;
+      kk[j] = c >= 0 ? (((unsigned long long)v << 32) | (unsigned long long)(0xFFFFFFFFu - ps)) : 0ull;
     }
-    if (bb == 0) break;
-    if (mine == bb) {  // unique: positions are distinct per consequent
-      o[1 + n_out] = key[my_slot];
-      key[my_slot] = -1;
-      mine = lane_best(my_slot);
+    auto reg_best = [&]() {
+      unsigned long long b = 0;
+#pragma unroll
+      for (int j = 0; j < kPerLane; ++j) b = kk[j] > b ? kk[j] : b;
+      return b;
+    };
+    unsigned long long mine = reg_best();
+    for (; n_out < k; ++n_out) {
+      const unsigned long long bb = wave_max_u64(mine);
+      if (bb == 0) break;
+      if (mine == bb) {  // unique: positions are distinct per consequent
+        int32_t id = -1;
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j)
+          if (kk[j] == bb) {
+            id = kc[j];
+            kk[j] = 0ull;
+          }
+        o[1 + n_out] = id;
+        mine = reg_best();
+      }
     }
   }
   if (lane == 0) o[0] = n_out;
+  stamp(4);
 }
 
 __global__ __launch_bounds__(64 * kWaves) void k_serve_match_topk(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ cons,
     const uint32_t* __restrict__ srank, const uint8_t* __restrict__ is_key, int64_t n_items,
     const int64_t* __restrict__ q_ptr, const int32_t* __restrict__ seeds, int64_t B, int k,
-    int32_t* __restrict__ out) {
+    int32_t* __restrict__ out, int narrow) {
   __shared__ int32_t s_key[kWaves][kSlots];
   __shared__ uint32_t s_val[kWaves][kSlots];
   __shared__ uint32_t s_pos[kWaves][kSlots];
@@ -417,7 +487,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_match_topk(
   int64_t* rowp = s_row[w];
   const int64_t q0 = q_ptr[b], q1 = q_ptr[b + 1];
   serve_query_wave(row_ptr, cons, srank, is_key, n_items, seeds, q0, q1, k,
-                   out + b * (int64_t)(k + 1), key, val, pos, seg, rowp, lane);
+                   out + b * (int64_t)(k + 1), key, val, pos, seg, rowp, lane, nullptr,
+                   narrow != 0);
 }
 
 // ---- the persistent serving loop (gpu::GpuServeLoop) ----
@@ -454,7 +525,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
   __shared__ long long s_stage64[kLoopStage / 2];  // (8-byte aligned: q_ptr is int64)
   __shared__ int32_t s_out[kLoopOut];
   int32_t* s_stage = (int32_t*)s_stage64;
-  __shared__ unsigned s_cmd, s_seq;
+  __shared__ unsigned s_cmd, s_seq, s_words;
+  __shared__ unsigned long long s_stamps[6];
   __shared__ ServeReq s_req;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   unsigned last = 0;
@@ -468,10 +540,12 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
     if (tid == 0) {
       unsigned cmd = 0;
       for (unsigned n = 0;; ++n) {
-        const unsigned r = ld_sys(&mail->req_seq);
-        if (r != last) {
+        const unsigned long long r =
+            __hip_atomic_load(&mail->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((unsigned)r != last) {
           cmd = 1;
-          s_seq = r;
+          s_seq = (unsigned)r;
+          s_words = (unsigned)(r >> 32);
           break;
         }
         if ((n & 15u) == 15u) {
@@ -481,29 +555,32 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (cmd) {
+      if (cmd)
         __hip_atomic_store(&mail->t_seen, wall_clock64(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);  // (instrumentation: device clock)
-        const unsigned long long* src = (const unsigned long long*)&mail->req;
-        unsigned long long* dst = (unsigned long long*)&s_req;
-        for (int i = 0; i < (int)(sizeof(ServeReq) / 8); ++i)
-          dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
       s_cmd = cmd;
     }
     __syncthreads();
     if (s_cmd == 0u) break;
-    const ServeReq rq = s_req;
-    // stage [q_ptr (B + 1 int64) | seeds] (contiguous in the payload; the host keeps every
-    // request within the stage) in LDS: one round of system-scope loads, which bypass the
-    // caches (the payload buffer is rewritten by the host for every request)
-    const long long words = 2 * (rq.B + 1) + rq.n_seeds;
+    // stage [descriptor | q_ptr | seeds] in ONE round of parallel system-scope loads, which
+    // bypass the caches (the mailbox is rewritten by the host for every request)
     {
-      const int32_t* src = (const int32_t*)rq.q_ptr;
-      for (long long i = tid; i < words && i < kLoopStage; i += 64 * kWaves)
-        s_stage[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      constexpr int kDesc = (int)(sizeof(ServeReq) / 4);
+      const int total = kDesc + (int)min(s_words, (unsigned)kLoopStage);
+      const unsigned* src = (const unsigned*)&mail->req_desc;
+      unsigned* dreq = (unsigned*)&s_req;
+      unsigned* dst = (unsigned*)s_stage;
+      for (int i = tid; i < total; i += 64 * kWaves) {
+        const unsigned v = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (i < kDesc) dreq[i] = v;
+        else dst[i - kDesc] = v;
+      }
     }
     __syncthreads();
+    const ServeReq rq = s_req;
+    if (tid == 0)
+      __hip_atomic_store(&mail->t_staged, wall_clock64(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     const long long* qp = (const long long*)s_stage;
     const int32_t* sd = s_stage + 2 * (rq.B + 1);
     const long long ow = rq.B * (rq.k + 1);
@@ -511,9 +588,17 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
       const long long q0 = qp[b], q1 = qp[b + 1];
       serve_query_wave(rq.row_ptr, rq.cons, rq.srank, rq.is_key, rq.n_items, sd, q0, q1, rq.k,
                        s_out + b * (long long)(rq.k + 1), s_key[w], s_val[w], s_pos[w],
-                       s_seg[w], s_row[w], lane);
+                       s_seg[w], s_row[w], lane, b == 0 ? s_stamps : nullptr,
+                       rq.narrow != 0);
     }
     __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_store(&mail->t_computed, wall_clock64(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int i = 0; i < 5; ++i)
+        __hip_atomic_store(&mail->t_phase[i], s_stamps[i], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     // results out with system-scope (write-through) stores, drained before the done word
     for (long long i = tid; i < ow && i < kLoopOut; i += 64 * kWaves)
       __hip_atomic_store(rq.out + i, s_out[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -549,11 +634,12 @@ void serve_loop_launch(ServeMail* mail, unsigned long long idle_ticks,
 
 void serve_match_topk(const int64_t* row_ptr, const int32_t* cons, const uint32_t* srank,
                       const uint8_t* is_key, int64_t n_items, const int64_t* q_ptr,
-                      const int32_t* seeds, int64_t B, int k, int32_t* out, hipStream_t s) {
+                      const int32_t* seeds, int64_t B, int k, int32_t* out, hipStream_t s,
+                      bool narrow) {
   if (B <= 0) return;
   const unsigned blocks = (unsigned)((B + kWaves - 1) / kWaves);
   hipLaunchKernelGGL(k_serve_match_topk, dim3(blocks), dim3(64 * kWaves), 0, s, row_ptr, cons,
-                     srank, is_key, n_items, q_ptr, seeds, B, k, out);
+                     srank, is_key, n_items, q_ptr, seeds, B, k, out, narrow ? 1 : 0);
   KMLS_HIP(hipGetLastError());
 }
 
@@ -672,7 +758,8 @@ ServeLoopStats GpuServeLoop::stats() {
 
 bool GpuServeLoop::run(const int64_t* d_row_ptr, const int32_t* d_cons, const uint32_t* d_score,
                        const uint8_t* d_is_key, int64_t n_items, const int64_t* q_ptr, int64_t B,
-                       const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n) {
+                       const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n,
+                       bool narrow) {
   // one round trip holds what the kernel stages in LDS: split longer batches
   int64_t b0 = 0;
   while (b0 < B) {
@@ -691,7 +778,7 @@ bool GpuServeLoop::run(const int64_t* d_row_ptr, const int32_t* d_cons, const ui
       continue;
     }
     if (!run_one(d_row_ptr, d_cons, d_score, d_is_key, n_items, q_ptr + b0, b1 - b0, seeds, k,
-                 out_ids + b0 * k, out_n + b0))
+                 out_ids + b0 * k, out_n + b0, narrow))
       return false;
     b0 = b1;
   }
@@ -701,7 +788,7 @@ bool GpuServeLoop::run(const int64_t* d_row_ptr, const int32_t* d_cons, const ui
 bool GpuServeLoop::run_one(const int64_t* d_row_ptr, const int32_t* d_cons,
                            const uint32_t* d_score, const uint8_t* d_is_key, int64_t n_items,
                            const int64_t* q_ptr, int64_t B, const int32_t* seeds, int k,
-                           int32_t* out_ids, int32_t* out_n) {
+                           int32_t* out_ids, int32_t* out_n, bool narrow) {
   std::lock_guard<std::mutex> lk(mu_);
   if (paused_ > 0 || B <= 0) {
     ++st_.refused;
@@ -711,7 +798,8 @@ bool GpuServeLoop::run_one(const int64_t* d_row_ptr, const int32_t* d_cons,
   KMLS_HIP(hipSetDevice(device_));
   const int64_t ns = q_ptr[B] - q_ptr[0];
   const int64_t no = B * (int64_t)(k + 1);
-  const int64_t words = 2 * (B + 1) + ns + no;
+  const int64_t words = no;  // the host buffer holds only the answers (payload is inline)
+  KMLS_CHECK(2 * (B + 1) + ns <= kern::kServeLoopStage, "serve loop: request past the stage");
   if (words > cap_) {  // grow: the kernel must not hold the old buffer
     stop_and_wait();
     if (buf_) KMLS_HIP(hipHostFree(buf_));
@@ -720,32 +808,34 @@ bool GpuServeLoop::run_one(const int64_t* d_row_ptr, const int32_t* d_cons,
     KMLS_HIP(hipHostMalloc((void**)&buf_, (size_t)cap_ * sizeof(int32_t),
                            hipHostMallocMapped | hipHostMallocCoherent));
   }
-  int64_t* hq = reinterpret_cast<int64_t*>(buf_);
-  int32_t* hs = buf_ + 2 * (B + 1);
-  int32_t* ho = hs + ns;
+  volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
+  kern::ServeMail* mw = (kern::ServeMail*)mail_;
+  int64_t* hq = reinterpret_cast<int64_t*>(mw->payload);
+  int32_t* hs = mw->payload + 2 * (B + 1);
+  int32_t* ho = buf_;
   for (int64_t i = 0; i <= B; ++i) hq[i] = q_ptr[i] - q_ptr[0];
   std::copy(seeds + q_ptr[0], seeds + q_ptr[B], hs);
   int32_t* dev = nullptr;
   KMLS_HIP(hipHostGetDevicePointer((void**)&dev, buf_, 0));
-  volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
   kern::ServeReq rq;
   rq.row_ptr = d_row_ptr;
   rq.cons = d_cons;
   rq.srank = d_score;
   rq.is_key = d_is_key;
   rq.n_items = n_items;
-  rq.q_ptr = reinterpret_cast<const long long*>(dev);
-  rq.seeds = dev + 2 * (B + 1);
-  rq.out = dev + 2 * (B + 1) + ns;
+  rq.q_ptr = nullptr;  // inline: staged from the mailbox
+  rq.seeds = nullptr;
+  rq.out = dev;
   rq.B = B;
   rq.k = k;
   rq.n_seeds = ns;
-  std::memcpy((void*)&m->req, &rq, sizeof rq);
+  rq.narrow = narrow ? 1 : 0;
+  std::memcpy((void*)&m->req_desc, &rq, sizeof rq);
   for (int64_t i = 0; i < B; ++i) ho[i * (k + 1)] = -3;  // (never a real answer)
   ensure_running();
   const unsigned seq = ++seq_;
   std::atomic_thread_fence(std::memory_order_seq_cst);  // descriptor and payload before the word
-  m->req_seq = seq;
+  m->req = ((unsigned long long)(2 * (B + 1) + ns) << 32) | (unsigned long long)seq;
   std::atomic_thread_fence(std::memory_order_seq_cst);
   // wait for the done word; a kernel that exited meanwhile (idle race) is relaunched once
   const auto t_start = std::chrono::steady_clock::now();
@@ -775,6 +865,10 @@ bool GpuServeLoop::run_one(const int64_t* d_row_ptr, const int32_t* d_cons,
   }
   const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
   st_.kernel_us += (double)(m->t_done - m->t_seen) / ticks_per_us_;
+  st_.stage_us += (double)(m->t_staged - m->t_seen) / ticks_per_us_;
+  st_.compute_us += (double)(m->t_computed - m->t_staged) / ticks_per_us_;
+  for (int i = 0; i < 4; ++i)
+    st_.phase_us[i] += (double)(m->t_phase[i + 1] - m->t_phase[i]) / ticks_per_us_;
   ++st_.requests;
   st_.queries += (uint64_t)B;
   st_.last_us = us;
@@ -796,7 +890,7 @@ bool GpuRuleIndex::query_loop(const int64_t* q_ptr, int64_t B, const int32_t* se
                               int32_t* out_ids, int32_t* out_n) {
   KMLS_CHECK(k >= 0 && k <= 256, "query_loop: 0 <= k <= 256");
   return GpuServeLoop::for_device(device_).run(d_row_ptr_, d_cons_, d_score_, d_is_key_, n_items_,
-                                               q_ptr, B, seeds, k, out_ids, out_n);
+                                               q_ptr, B, seeds, k, out_ids, out_n, narrow_);
 }
 
 GpuRuleIndex::GpuRuleIndex(int device, const RuleIndex& host, uintptr_t stream)
@@ -821,6 +915,8 @@ GpuRuleIndex::GpuRuleIndex(int device, const RuleIndex& host, uintptr_t stream)
     sr[i] = (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), sc[i]) - uniq.begin()) + 1;
   const auto& rp = host.row_ptr();
   for (int64_t i = 0; i < n_items_; ++i) max_row_ = std::max<int>(max_row_, (int)(rp[i + 1] - rp[i]));
+  // merged order keys fit 32 bits (serve_query_wave); test hook serve_wide=1 keeps 64-bit keys
+  narrow_ = uniq.size() + 2 < (1u << 23) && test_hook("serve_wide", 0) == 0;
   h_row_ptr_.assign(rp.begin(), rp.end());
   h_is_key_.assign(host.is_key().begin(), host.is_key().end());
   hipStream_t s = (hipStream_t)stream_;
@@ -926,7 +1022,7 @@ void GpuRuleIndex::query_batch(const int64_t* q_ptr, int64_t B, const int32_t* s
   const int64_t* dq = reinterpret_cast<const int64_t*>(dev);
   int32_t* dout = dev + 2 * (B + 1) + ns;
   kern::serve_match_topk(d_row_ptr_, d_cons_, d_score_, d_is_key_, n_items_, dq,
-                         dev + 2 * (B + 1), B, k, dout, s);
+                         dev + 2 * (B + 1), B, k, dout, s, narrow_);
   // same stream: overwrites the wave kernel's -2 for the long merges
   kern::serve_topk_big(d_row_ptr_, d_cons_, d_score_, d_is_key_, n_items_, d_id_cons_,
                        d_id_pos_, dq, dev + 2 * (B + 1), dout + no, nb, k, dout, s);

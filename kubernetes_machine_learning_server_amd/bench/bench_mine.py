@@ -524,7 +524,7 @@ def run_job_full(tx, ms: float, want_digest: Optional[str] = None,
         if want_digest is not None:
             out["verified_digest"] = d["digest"] == want_digest
         if want_per_level is not None:
-            out["per_level_equal_headline"] = out["per_level"] == [int(v) for v in want_per_level[1:]]
+            out["per_level_equal_headline"] = out["per_level"] == [int(v) for v in want_per_level]
         return out
     finally:
         shutil.rmtree(root, ignore_errors=True)

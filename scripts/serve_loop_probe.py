@@ -48,6 +48,9 @@ def main():
                          "p99_us": round(float(np.percentile(ts, 99)), 2)}
         st = N.serve_loop_stats(0)
         out["loop_kernel_mean_us"] = round(st["kernel_mean_us"], 2)
+        out["loop_stage_mean_us"] = round(st.get("stage_mean_us", 0.0), 2)
+        out["loop_compute_mean_us"] = round(st.get("compute_mean_us", 0.0), 2)
+        out["loop_phase_us"] = [round(x, 2) for x in st.get("phase_mean_us", [])]
         out["loop_launches"] = st["launches"]
         print(json.dumps(out), flush=True)
 

@@ -44,10 +44,18 @@ def _check(host, gidx, q_ptr, seeds, k=10):
     return int(small.sum())
 
 
-def test_serve_loop_matches_cpp_matcher(gpu_mod):
+@pytest.mark.parametrize("keys", ["narrow", "wide"])
+def test_serve_loop_matches_cpp_matcher(gpu_mod, monkeypatch, keys):
+    """narrow: 32-bit top-k order keys (score ranks < 2^23, the common case); wide: the 64-bit
+    keys of very large score vocabularies (test hook serve_wide=1)."""
+    if keys == "wide":
+        monkeypatch.setenv("KMLS_TEST_HOOKS", "serve_wide=1")
     idx = _index(gpu_mod)
     host = idx.native()
     gidx = gpu_mod.GpuRuleIndex(0, host)
+    ids, n = gidx.query_batch(np.array([0, 1], np.int64), np.flatnonzero(idx.is_key)[:1].astype(np.int32), 10)
+    cids, cn = host.query_batch(np.array([0, 1], np.int64), np.flatnonzero(idx.is_key)[:1].astype(np.int32), 10)
+    assert (np.asarray(n) == np.asarray(cn)).all() and (np.asarray(ids) == np.asarray(cids)).all()
     keys = np.flatnonzero(idx.is_key).astype(np.int32)
     rng = np.random.default_rng(0)
     answered = 0
