@@ -29,6 +29,7 @@
 #include "devbuf.hpp"
 #include "kernels.hpp"
 #include "kmls/common.hpp"
+#include "kmls/hooks.hpp"
 
 namespace kmls {
 namespace kern {
@@ -334,8 +335,10 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   // the LDS-mask filter when the frequent-item mask fits next to the wave buffers
   const int64_t mask_words = (in.n_items + 31) / 32;
   const bool lds_mask = in.fmask != nullptr && mask_words * 4 <= (128 << 10);
-  if (lds_mask && mask_words * 4 > 65536)
-    ok(hipFuncSetAttribute((const void*)devbuf::k_map_filter_lds,
+  // (test hook filter_lds=0: the L2-mask instance of the same kernel, at full occupancy)
+  const bool mask_in_lds = lds_mask && test_hook("filter_lds", 1) != 0;
+  if (mask_in_lds && mask_words * 4 > 65536)
+    ok(hipFuncSetAttribute((const void*)devbuf::k_map_filter_lds<true>,
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(mask_words * 4)), "attr");
   for (int attempt = 0;; ++attempt) {
     I.txrec.need(tx_cap);
@@ -348,10 +351,15 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
       const int64_t chunks = (in.n_tx + 63) / 64;
       const unsigned gm = (unsigned)std::max<int64_t>(
           1, std::min<int64_t>((chunks + devbuf::kMW - 1) / devbuf::kMW, (int64_t)in.n_cus * 2));
-      hipLaunchKernelGGL(devbuf::k_map_filter_lds, dim3(gm), dim3(64 * devbuf::kMW),
-                         (size_t)mask_words * 4, s, in.tx_ptr, in.items, in.n_tx, in.fmask,
-                         mask_words, I.pr.p, 2u, I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap,
-                         I.err.p);
+      if (mask_in_lds)
+        hipLaunchKernelGGL(devbuf::k_map_filter_lds<true>, dim3(gm), dim3(64 * devbuf::kMW),
+                           (size_t)mask_words * 4, s, in.tx_ptr, in.items, in.n_tx, in.fmask,
+                           mask_words, I.pr.p, 2u, I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap,
+                           I.err.p);
+      else
+        hipLaunchKernelGGL(devbuf::k_map_filter_lds<false>, dim3(gm * 4), dim3(64 * devbuf::kMW),
+                           0, s, in.tx_ptr, in.items, in.n_tx, in.fmask, mask_words, I.pr.p, 2u,
+                           I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p);
     } else {
       hipLaunchKernelGGL(devbuf::k_map_filter, dim3(g), dim3(256), 0, s, in.tx_ptr, in.items,
                          in.n_tx, I.pr.p, 2u, I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p);
