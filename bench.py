@@ -20,6 +20,8 @@ the whole-problem result and verifies it.  ``value`` = itemsets of the problem Ã
 rank's step.
 
 Secondary fields:
+* ``serve.hip_loop`` â€” the same harness with the persistent HIP serving kernel forced
+                    (``SERVE_BACKEND=loop``): every request answered by the polling kernel.
 * ``serve``       â€” config 4, run FIRST in a fresh child process (this process has not touched
                     the GPU yet): native HTTP front + open-loop native load generator, latency
                     from the scheduled send time, fixed QPS points and the capacity (max QPS with
@@ -152,6 +154,8 @@ def main() -> int:
     ap.add_argument("--serve-backend", default="auto")
     ap.add_argument("--no-serve-reference", action="store_true",
                     help="skip the reference-stack serving baseline (uvicorn + Python matcher)")
+    ap.add_argument("--serve-loop-qps", default="2000,5000",
+                    help="QPS points with the persistent HIP serving kernel forced ('' = skip)")
     ap.add_argument("--no-levelwise", action="store_true")
     ap.add_argument("--no-emit", action="store_true", help="skip the materialising headline run")
     ap.add_argument("--no-config2", action="store_true")
@@ -193,6 +197,13 @@ def main() -> int:
                     for r, m in zip(ref["points"], serve["points"]) if m.get("p50_ms")]
             except Exception:  # noqa: BLE001 â€” a failed reference run leaves the field out
                 pass
+        # the persistent HIP serving kernel forced on (SERVE_BACKEND=loop): every request the
+        # native front receives is answered by the polling kernel (front_stats.gpu_loop_batches)
+        if args.serve_loop_qps:
+            t = time.time()
+            loop = run_serve_child(args.serve_loop_qps, 3.0, "loop", timeout=300, capacity=False)
+            loop["wall_s"] = round(time.time() - t, 1)
+            serve["hip_loop"] = loop
 
     import numpy as np
     import torch

@@ -375,7 +375,7 @@ def matcher_bench(base: pathlib.Path, n_queries: int = 20000) -> dict:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--backend", default="auto", help="hip | cpu | python | auto")
+    ap.add_argument("--backend", default="auto", help="hip | loop | cpu | python | auto")
     ap.add_argument("--qps", default="2000,5000,10000")
     ap.add_argument("--duration", type=float, default=5.0)
     ap.add_argument("--front", choices=("native", "uvicorn"), default="native")
