@@ -1581,7 +1581,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
       uint32_t* gram = (uint32_t*)arena_->push((size_t)std::max<int64_t>(per * cw, F) * F * sizeof(uint32_t));
       if (per * cw > F)
         KMLS_HIP(hipMemsetAsync(gram + (size_t)F * F, 0, (size_t)(per * cw - F) * F * sizeof(uint32_t), s));
-      // sparse large data: count the pairs where they occur (cooc.hip) when the cost model says
+      // sparse large data: count the pairs where they occur (pairrows.hip, cooc.hip fallback) when the cost model says
       // so (only for bitmaps of this miner's own CSR shard: mine_txdp / the host path of mine)
       bool sparse = false;
       if (hl_plan_) {  // decided (globally) before the encode: there is no bitmap
@@ -1601,7 +1601,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
         // matrix cores for long rows (large T): the masked-nibble FP4 MFMA gram
         // (v_mfma_scale_f32_32x32x64_f8f6f4, gram_mfma.hip) beats the VALU popcount gram there.
         // No BASELINE config reaches this branch today: ds1 rows are short (popcount gram),
-        // configs 3 and 5 count pairs horizontally (cooc.hip)
+        // configs 3 and 5 count pairs horizontally (pairrows.hip)
         if (gram_popcount_forced() ? cfg.level2_mfma : (cfg.level2_mfma || Wp >= 4096))
           kern::pair_gram_mfma((const uint64_t*)bm_dev, Wp, F, gram, s);
         else
