@@ -78,6 +78,7 @@ class HttpFront {
                  std::shared_ptr<gpu::GpuRuleIndex> gpu, int gpu_min_batch,
                  int gpu_min_merge = -1);
   void clear_model();
+  void retire(std::shared_ptr<const FrontModel> prev);  // (internal: deferred release)
 
   // Python side of the slow path: the eventfd becomes readable when requests are queued
   int slow_fd() const { return slow_efd_; }
