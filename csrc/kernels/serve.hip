@@ -394,7 +394,49 @@ __device__ __forceinline__ void serve_query_wave(
   // (Rescanning the winner's slots from LDS every round cost ~1 us per round: 12 of the 14 us
   // of a one-query request in the serving loop.)
   int n_out = 0;
+  bool done_small = false;
   if (narrow) {
+    // small merges (<= 128 distinct consequents, the common request): compact the occupied
+    // slots into LDS, then every lane ranks its (one or two) entries against all of them
+    // (broadcast reads) and writes each at its rank if it is in the top k — no serial rounds
+    uint32_t* cv = reinterpret_cast<uint32_t*>(seg);  // (free after the merge)
+    int32_t* ck = reinterpret_cast<int32_t*>(rowp);
+    uint32_t nocc = 0;
+    const unsigned long long lanelt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < kPerLane; ++j) {
+      const int i = j * 64 + lane;
+      const int32_t c = key[i];
+      const bool occ = c >= 0;
+      const unsigned long long m = __ballot(occ);
+      if (occ) {
+        const uint32_t q = nocc + (uint32_t)__popcll(m & lanelt);
+        if (q < 128u) {
+          cv[q] = (val[i] << 9) | (511u - pos[i]);
+          ck[q] = c;
+        }
+      }
+      nocc += (uint32_t)__popcll(m);
+    }
+    if (nocc <= 128u) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t a_idx = (uint32_t)lane, b_idx = (uint32_t)lane + 64u;
+      const uint32_t va = a_idx < nocc ? cv[a_idx] : 0u;
+      const uint32_t vb = b_idx < nocc ? cv[b_idx] : 0u;
+      uint32_t ra = 0, rb = 0;
+      for (uint32_t t = 0; t < nocc; ++t) {
+        const uint32_t x = cv[t];
+        ra += x > va ? 1u : 0u;
+        rb += x > vb ? 1u : 0u;
+      }
+      if (a_idx < nocc && ra < (uint32_t)k) o[1 + ra] = ck[a_idx];
+      if (b_idx < nocc && rb < (uint32_t)k) o[1 + rb] = ck[b_idx];
+      n_out = (int)min(nocc, (uint32_t)k);
+      done_small = true;
+    }
+  }
+  if (narrow && !done_small) {
     // score ranks < 2^23 (checked at index load) and first positions < 512: the order key fits
     // 32 bits, so a round is one 32-bit DPP max
     uint32_t kk[kPerLane];
@@ -429,7 +471,7 @@ __device__ __forceinline__ void serve_query_wave(
         mine = reg_best();
       }
     }
-  } else {
+  } else if (!narrow) {
     unsigned long long kk[kPerLane];
     int32_t kc[kPerLane];
 #pragma unroll
