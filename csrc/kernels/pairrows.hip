@@ -42,8 +42,8 @@ constexpr int kRowThreads = 1024;
 constexpr uint64_t kSlice = 65536;  // pair-list entries per row workgroup
 constexpr int64_t kBlockTx = 32768;  // CSR rows per histogram workgroup
 constexpr int64_t kPartTx = 1024;    // CSR rows per partition workgroup (one per thread)
-constexpr int kNG = 64;              // coarse row groups of the first partition pass
-constexpr uint32_t kChunk = 65536;   // group-list entries per split workgroup
+constexpr int kNGMax = 256;          // coarse row groups of the first partition pass (max; 64 default)
+constexpr uint32_t kChunkDflt = 65536;  // group-list entries per split workgroup (default)
 
 void ok(hipError_t e, const char* what) { devbuf::hip_ok(e, what); }
 
@@ -81,19 +81,20 @@ __global__ __launch_bounds__(kRowThreads) void k_pl_hist(const uint2* __restrict
 __global__ __launch_bounds__(1024) void k_pl_groups(const unsigned long long* __restrict__ base,
                                                    int64_t F, uint8_t* __restrict__ grp,
                                                    unsigned long long* __restrict__ gcur,
-                                                   uint32_t* __restrict__ grow,  // [kNG][2]
-                                                   uint32_t* __restrict__ gch,   // [kNG + 1]
-                                                   uint32_t* __restrict__ meta) {
-  __shared__ uint32_t lo[kNG], hi[kNG];
+                                                   uint32_t* __restrict__ grow,  // [ng][2]
+                                                   uint32_t* __restrict__ gch,   // [ng + 1]
+                                                   uint32_t* __restrict__ meta, int ng,
+                                                   uint32_t chunk) {
+  __shared__ uint32_t lo[kNGMax], hi[kNGMax];
   const unsigned long long total = base[F];
-  if (threadIdx.x < kNG) {
+  if ((int)threadIdx.x < ng) {
     lo[threadIdx.x] = 0xFFFFFFFFu;
     hi[threadIdx.x] = 0u;
   }
   __syncthreads();
   for (int64_t r = threadIdx.x; r < F; r += blockDim.x) {
-    const unsigned g = total ? (unsigned)(base[r] * (unsigned long long)kNG / total) : 0u;
-    const unsigned gg = g < (unsigned)kNG ? g : (unsigned)kNG - 1u;
+    const unsigned g = total ? (unsigned)(base[r] * (unsigned long long)ng / total) : 0u;
+    const unsigned gg = g < (unsigned)ng ? g : (unsigned)ng - 1u;
     grp[r] = (uint8_t)gg;
     atomicMin(&lo[gg], (uint32_t)r);
     atomicMax(&hi[gg], (uint32_t)r + 1u);
@@ -101,20 +102,20 @@ __global__ __launch_bounds__(1024) void k_pl_groups(const unsigned long long* __
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t c = 0;
-    for (int g = 0; g < kNG; ++g) {
+    for (int g = 0; g < ng; ++g) {
       gch[g] = c;
       if (lo[g] < hi[g]) {
         const unsigned long long b0 = base[lo[g]], b1 = base[hi[g]];
         gcur[g] = b0;
         grow[2 * g] = lo[g];
         grow[2 * g + 1] = hi[g];
-        c += (uint32_t)((b1 - b0 + kChunk - 1) / kChunk);
+        c += (uint32_t)((b1 - b0 + chunk - 1) / chunk);
       } else {
         gcur[g] = 0;
         grow[2 * g] = grow[2 * g + 1] = 0;
       }
     }
-    gch[kNG] = c;
+    gch[ng] = c;
     meta[0] = c;
   }
 }
@@ -127,12 +128,12 @@ __global__ __launch_bounds__(kPartTx) void k_pl_part(const uint2* __restrict__ t
                                                      const uint8_t* __restrict__ grp_g,
                                                      unsigned long long* __restrict__ gcur,
                                                      uint32_t* __restrict__ gl, int own_rank,
-                                                     int own_world) {
+                                                     int own_world, int ng) {
   extern __shared__ uint8_t grp[];  // [F]
-  __shared__ uint32_t cnt[kNG];
-  __shared__ unsigned long long gb[kNG];
+  __shared__ uint32_t cnt[kNGMax];
+  __shared__ unsigned long long gb[kNGMax];
   for (int64_t r = threadIdx.x; r < F; r += kPartTx) grp[r] = grp_g[r];
-  if (threadIdx.x < kNG) cnt[threadIdx.x] = 0u;
+  if ((int)threadIdx.x < ng) cnt[threadIdx.x] = 0u;
   __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * kPartTx + threadIdx.x;
   uint2 rec = make_uint2(0u, 0u);
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(kPartTx) void k_pl_part(const uint2* __restrict__ t
   for (uint32_t i = 0; i + 1 < rec.y; ++i)
     if ((int)(it[i] % (uint32_t)own_world) == own_rank) atomicAdd(&cnt[grp[it[i]]], rec.y - 1u - i);
   __syncthreads();
-  if (threadIdx.x < kNG) {
+  if ((int)threadIdx.x < ng) {
     const uint32_t c = cnt[threadIdx.x];
     gb[threadIdx.x] = c ? atomicAdd(&gcur[threadIdx.x], (unsigned long long)c) : 0ull;
     cnt[threadIdx.x] = 0u;
@@ -162,20 +163,21 @@ __global__ __launch_bounds__(kPartTx) void k_pl_part(const uint2* __restrict__ t
 __global__ __launch_bounds__(kRowThreads) void k_pl_split(
     const uint32_t* __restrict__ gl, const unsigned long long* __restrict__ gbeg_all,
     const unsigned long long* __restrict__ base, const uint32_t* __restrict__ grow,
-    const uint32_t* __restrict__ gch, uint32_t* __restrict__ rcur, uint16_t* __restrict__ pl) {
+    const uint32_t* __restrict__ gch, uint32_t* __restrict__ rcur, uint16_t* __restrict__ pl,
+    int ng, uint32_t chunk) {
   extern __shared__ uint32_t rc[];  // [rows of the group]
   __shared__ int32_t s_g;
   if (threadIdx.x == 0) {
     int g = 0;
-    while (g + 1 < kNG && gch[g + 1] <= blockIdx.x) ++g;
+    while (g + 1 < ng && gch[g + 1] <= blockIdx.x) ++g;
     s_g = g;
   }
   __syncthreads();
   const int g = s_g;
   const uint32_t r0 = grow[2 * g], r1 = grow[2 * g + 1];
   const unsigned long long g0 = base[r0], g1 = base[r1];
-  const unsigned long long c0 = g0 + (unsigned long long)(blockIdx.x - gch[g]) * kChunk;
-  const unsigned long long c1 = c0 + kChunk < g1 ? c0 + kChunk : g1;
+  const unsigned long long c0 = g0 + (unsigned long long)(blockIdx.x - gch[g]) * chunk;
+  const unsigned long long c1 = c0 + chunk < g1 ? c0 + chunk : g1;
   for (uint32_t r = threadIdx.x; r < r1 - r0; r += kRowThreads) rc[r] = 0u;
   __syncthreads();
   for (unsigned long long i = c0 + threadIdx.x; i < c1; i += kRowThreads)
@@ -445,12 +447,15 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   ok(hipGetLastError(), "slices");
   devbuf::scan_u32(I.nsl.p, I.soff.p, F + 1, I.tmp, s);
   I.grp.need((size_t)F);
-  I.gcur.need(kNG);
-  I.grow.need(2 * kNG);
-  I.gch.need(kNG + 1);
+  // (test hooks pl_groups / pl_chunk: the partition's group count and split chunk)
+  const int ng = (int)std::max<long long>(1, std::min<long long>(kNGMax, test_hook("pl_groups", 64)));
+  const uint32_t chunk = (uint32_t)std::max<long long>(1024, test_hook("pl_chunk", kChunkDflt));
+  I.gcur.need(ng);
+  I.grow.need(2 * ng);
+  I.gch.need(ng + 1);
   I.meta.need(4);
   hipLaunchKernelGGL(k_pl_groups, dim3(1), dim3(1024), 0, s, I.base.p, F, I.grp.p, I.gcur.p,
-                     I.grow.p, I.gch.p, I.meta.p);
+                     I.grow.p, I.gch.p, I.meta.p, ng, chunk);
   ok(hipGetLastError(), "groups");
   ok(hipMemcpyAsync(I.h, I.base.p + F, 8, hipMemcpyDeviceToHost, s), "rb");
   ok(hipMemcpyAsync(I.h + 1, I.soff.p + F, 4, hipMemcpyDeviceToHost, s), "rb");
@@ -467,12 +472,12 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   ok(hipMemsetAsync(I.rcur.p, 0, (size_t)F * 4, s), "rcur");
   const int64_t n_pb = (I.n_tx + kPartTx - 1) / kPartTx;
   hipLaunchKernelGGL(k_pl_part, dim3((unsigned)n_pb), dim3(kPartTx), (size_t)F, s, txrec,
-                     I.n_tx, fit, F, I.grp.p, I.gcur.p, I.gl.p, own_rank, own_world);
+                     I.n_tx, fit, F, I.grp.p, I.gcur.p, I.gl.p, own_rank, own_world, ng);
   ok(hipGetLastError(), "part");
   if (n_ch > 0)
     hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds, s, I.gl.p,
                        (const unsigned long long*)nullptr, I.base.p, I.grow.p, I.gch.p, I.rcur.p,
-                       I.pl.p);
+                       I.pl.p, ng, chunk);
   ok(hipGetLastError(), "split");
   // 3. the rows
   if (n_sl > 0)
