@@ -25,14 +25,24 @@ def _build():
     deps = srcs + host + [main] + list((ROOT / "csrc/emu").rglob("*")) + \
         list((ROOT / "csrc/include").rglob("*.hpp")) + [ROOT / "csrc/kernels/kernels.hpp",
                                                         ROOT / "csrc/host/deep_run.hpp"]
-    if BIN.exists() and BIN.stat().st_mtime >= max(p.stat().st_mtime for p in deps if p.is_file()):
+    newest = max(p.stat().st_mtime for p in deps if p.is_file())
+    if BIN.exists() and BIN.stat().st_mtime >= newest:
         return
     BIN.parent.mkdir(parents=True, exist_ok=True)
-    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
-           "-fno-omit-frame-pointer", f"-I{ROOT / 'csrc/emu'}", f"-I{ROOT / 'csrc/include'}",
-           "-x", "c++"] + [str(s) for s in srcs] + ["-x", "none"] + [str(h) for h in host] + \
-          [str(main), "-lpthread", "-o", str(BIN)]
-    subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+    # parallel test workers (pytest -n): one builds under an exclusive lock, into a temp file
+    # renamed over the binary, so no worker executes a half-written file
+    import fcntl
+    with open(BIN.parent / ".build.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if BIN.exists() and BIN.stat().st_mtime >= newest:
+            return
+        tmp = BIN.with_name(f"{BIN.name}.{os.getpid()}.tmp")
+        cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+               "-fno-omit-frame-pointer", f"-I{ROOT / 'csrc/emu'}", f"-I{ROOT / 'csrc/include'}",
+               "-x", "c++"] + [str(s) for s in srcs] + ["-x", "none"] + [str(h) for h in host] + \
+              [str(main), "-lpthread", "-o", str(tmp)]
+        subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+        os.replace(tmp, BIN)
 
 
 @pytest.fixture(scope="module")
