@@ -137,6 +137,8 @@ def run_serve_child(qps: str, duration: float, backend: str, timeout: float = 42
     out["capacity"] = {k: cap.get(k) for k in ("capacity_qps", "max_qps_p99_under_ms",
                                                "at_capacity", "limit_hit")}
     out["front_stats"] = s.get("front_stats")
+    if s.get("reload_under_load"):
+        out["reload_under_load"] = s["reload_under_load"]
     return out
 
 
@@ -154,8 +156,10 @@ def main() -> int:
     ap.add_argument("--serve-backend", default="auto")
     ap.add_argument("--no-serve-reference", action="store_true",
                     help="skip the reference-stack serving baseline (uvicorn + Python matcher)")
-    ap.add_argument("--serve-loop-qps", default="2000,5000",
+    ap.add_argument("--serve-loop-qps", default="2000,5000,10000",
                     help="QPS points with the persistent HIP serving kernel forced ('' = skip)")
+    ap.add_argument("--no-config5-serve", action="store_true",
+                    help="skip serving the config-5 index across a hot reload (10k QPS)")
     ap.add_argument("--no-levelwise", action="store_true")
     ap.add_argument("--no-emit", action="store_true", help="skip the materialising headline run")
     ap.add_argument("--no-config2", action="store_true")
@@ -201,7 +205,7 @@ def main() -> int:
         # native front receives is answered by the polling kernel (front_stats.gpu_loop_batches)
         if args.serve_loop_qps:
             t = time.time()
-            loop = run_serve_child(args.serve_loop_qps, 3.0, "loop", timeout=300, capacity=False)
+            loop = run_serve_child(args.serve_loop_qps, 3.0, "loop", timeout=360, capacity=True)
             loop["wall_s"] = round(time.time() - t, 1)
             serve["hip_loop"] = loop
 
@@ -360,7 +364,7 @@ def main() -> int:
     # ---- BASELINE config 2 (1 GPU) ----
     if world == 1 and not args.no_config2:
         from kubernetes_machine_learning_server_amd.serve.index import name_tie_rank
-        wd.arm("config2", 400)
+        wd.arm("config2", 520)
         try:
             tie = name_tie_rank(tx.names) if tx.names else np.arange(tx.n_items, dtype=np.int32)
             out["config2"] = bm.run_config2(N, tx, tx.names, tie, steps=10,
@@ -403,7 +407,10 @@ def main() -> int:
         try:
             from kubernetes_machine_learning_server_amd.bench.bench_large import run_rule_map
             t_c5 = time.time()
-            c5 = run_rule_map("100Mx1M", min_support=2e-4, steps=args.config5_steps, warmup=1)
+            serve_c5 = world == 1 and not args.no_config5_serve and bool(args.serve_qps)
+            pvc_c5 = tempfile.mkdtemp(prefix="kmls_pvc_c5_") if serve_c5 and rank == 0 else ""
+            c5 = run_rule_map("100Mx1M", min_support=2e-4, steps=args.config5_steps, warmup=1,
+                              pvc_dir=pvc_c5)
             c5["section_wall_s"] = round(time.time() - t_c5, 1)
             if rank == 0:
                 c5["model"] = "rule-map-100Mx1M-synthetic"
@@ -415,6 +422,37 @@ def main() -> int:
         except Exception as e:
             out.setdefault("errors", {})["config5"] = repr(e)[:300]
         wd.disarm()
+        # the config-5 index served at 10k QPS while the next job's index is hot-reloaded
+        # under load (the marker-last publish, rest_api/app/main.py:106-122): the default
+        # router and the persistent HIP serving kernel forced, each in a fresh server process
+        if serve_c5 and rank == 0 and (out.get("config5") or {}).get("pvc"):
+            wd.arm("config5_serve", 420)
+            try:
+                alt = os.path.join(pvc_c5, "rules_alt.idx")
+                c5s = {}
+                for be in ("auto", "loop"):
+                    t = time.time()
+                    c5s[be] = run_serve_child("10000", 3.0, be, timeout=200, capacity=False,
+                                              extra=("--pvc", pvc_c5, "--reload-index", alt,
+                                                     "--reload-at", "3", "--reload-duration",
+                                                     "8"))
+                    c5s[be]["wall_s"] = round(time.time() - t, 1)
+                    # (the PVC's marker and index are now the alt ones: restore for the next)
+                    if be == "auto":
+                        from kubernetes_machine_learning_server_amd.utils.atomic_io import \
+                            atomic_write_bytes
+                        pk = os.path.join(pvc_c5, "api-data", "pickles")
+                        with open(os.path.join(pvc_c5, "rules_main.idx"), "rb") as fh:
+                            atomic_write_bytes(os.path.join(pk, "rules.idx"), fh.read())
+                        atomic_write_bytes(os.path.join(pvc_c5, "api-data", "last_execution.txt"),
+                                           b"initial")
+                out["config5"]["serve_reload"] = c5s
+            except Exception as e:
+                out.setdefault("errors", {})["config5_serve"] = repr(e)[:300]
+            wd.disarm()
+        if pvc_c5:
+            import shutil
+            shutil.rmtree(pvc_c5, ignore_errors=True)
 
     # ---- config 3 item-sharded (every N: each rank counts the pair rows and horizontal
     #      levels of its own items over the all-gathered frequent-rank CSRs) ----

@@ -834,6 +834,40 @@ struct HttpFront::Impl {
       to_gpu = m->gpu_min_batch == 1 ||
                gpu_pending.load(std::memory_order_relaxed) + 1 >= m->gpu_min_batch;
     }
+    int32_t out[256];
+    const int kk = std::min(k, 256);
+    if (to_gpu && m->gpu_min_merge >= 0) {
+      // the persistent serving kernel answers on THIS I/O thread (each caller gets its own
+      // request slot, answered by its own workgroup): no hop to the GPU thread and back
+      const int64_t qp[2] = {0, (int64_t)ids.size()};
+      int32_t on = -3;
+      bool ok = false;
+      try {
+        ok = m->gpu->query_loop(qp, 1, ids.data(), kk, out, &on);
+      } catch (...) {
+        ok = false;
+      }
+      int n = on;
+      if (ok) {
+        ++st_gpu_loop;
+        ++st_gpu_batches;
+        ++st_gpu_queries;
+      } else {
+        ++st_gpu_loop_refused;
+      }
+      if (!ok || n == -2) n = m->index->query(ids.data(), (int)ids.size(), kk, out, nullptr);
+      std::string body;
+      if (n < 0) {
+        body = fallback_body(*m, seeds);
+        ++st_fallback;
+      } else {
+        body = songs_body(*m, out, n);
+      }
+      ++st_native;
+      c.out += json_response(w, body, r.keep_alive);
+      if (!r.keep_alive) c.close_after = true;
+      return;
+    }
     if (to_gpu) {
       c.busy = true;
       c.close_after = c.close_after || !r.keep_alive;
@@ -845,8 +879,6 @@ struct HttpFront::Impl {
       gpu_cv.notify_one();
       return;
     }
-    int32_t out[256];
-    const int kk = std::min(k, 256);
     const int n = m->index->query(ids.data(), (int)ids.size(), kk, out, nullptr);
     std::string body;
     if (n < 0) {

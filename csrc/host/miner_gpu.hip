@@ -1169,7 +1169,8 @@ int64_t GpuMiner::cooc_pairs_sampled() {
 // level-2 cooc choice) and the cost model picks the horizontal pair count.  Every tx-DP rank must
 // take the same path (the two run different collectives): the shard votes are all-reduced.
 // KMLS_HLEVELS=0 (or test hook hlevels=0) keeps the bitmap levels.
-bool GpuMiner::hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* comm) {
+bool GpuMiner::hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* comm,
+                            bool need_rows) {
   static const long long env_dflt = [] {
     const char* e = std::getenv("KMLS_HLEVELS");
     return e ? std::atoll(e) : 1ll;
@@ -1184,6 +1185,8 @@ bool GpuMiner::hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* 
     st.pairs = (uint64_t)hl_pairs_est_;
     st.max_k = 0;
     want = test_hook("cooc", 1) == 2 || cooc_cheaper(F, Wp, nnz_, st);
+  } else if (want && need_rows) {
+    want = false;  // folded into the vote below, so every rank declines together
   } else if (want) {
     const CoocStats st = cooc_stats();
     hl_pairs_est_ = (int64_t)st.pairs;
@@ -2431,7 +2434,9 @@ GpuMineResult GpuMiner::mine_shard(Comm* comm, int64_t global_n_tx, const MineCo
   KMLS_HIP(hipEventRecord(e0.e, s));
   const int64_t F = txdp_select(comm, global_n_tx, cfg, support_tiles);
   const int64_t Wp = words_local();
-  *declined = !hlevels_plan(cfg, F, Wp, comm);
+  // only the row form counts complete pairs from the all-gathered CSR (pair_rows_count's PrShard);
+  // without it (KMLS_PAIR_ROWS=0, F > 32768) every rank declines and the caller falls back
+  *declined = !hlevels_plan(cfg, F, Wp, comm, /*need_rows=*/true);
   KMLS_HIP(hipEventRecord(e1.e, s));
   if (*declined) return GpuMineResult{};
   shard_comm_ = comm;

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -424,7 +425,10 @@ class GpuMiner {
   bool prows_fresh_ = false;      // the last pair_counts_csr used the row count (its CSR is valid)
   bool pair_rows_count(uint32_t* gram, int64_t ld);
   bool hl_plan_ = false;          // the current mine_bitmaps call runs without bitmaps
-  bool hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* comm);
+  // need_rows: the plan also requires the row form of the pair count (item sharding: the
+  // scattered-atomic fallback counts only this rank's CSR and nothing would reduce it)
+  bool hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* comm,
+                    bool need_rows = false);
   std::string hl_stats_;          // last horizontal run (JSON-ish summary for the phases)
   void txdp_gram_combine(uint32_t* gram, int64_t F, int64_t per, uint32_t minsup);
   unsigned long long* d_cooc_ = nullptr;  // [3]: cooc stats (pairs, max k) + error flag
@@ -518,7 +522,9 @@ struct ServeLoopStats {
 class GpuServeLoop {
  public:
   static GpuServeLoop& for_device(int device);
-  // one batch; false when paused / failed (nothing answered)
+  // one batch; false when paused / failed / every slot busy (nothing answered: the caller uses
+  // the C++ matcher).  Thread-safe: callers on different threads use different request slots
+  // and are answered concurrently.
   bool run(const int64_t* d_row_ptr, const int32_t* d_cons, const uint32_t* d_score,
            const uint8_t* d_is_key, int64_t n_items, const int64_t* q_ptr, int64_t B,
            const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n, bool narrow = false);
@@ -529,23 +535,33 @@ class GpuServeLoop {
 
  private:
   explicit GpuServeLoop(int device);
-  bool run_one(const int64_t* d_row_ptr, const int32_t* d_cons, const uint32_t* d_score,
-               const uint8_t* d_is_key, int64_t n_items, const int64_t* q_ptr, int64_t B,
-               const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n, bool narrow);
-  bool ensure_running();
-  void stop_and_wait();
+  bool run_one(int slot, const int64_t* d_row_ptr, const int32_t* d_cons,
+               const uint32_t* d_score, const uint8_t* d_is_key, int64_t n_items,
+               const int64_t* q_ptr, int64_t B, const int32_t* seeds, int k, int32_t* out_ids,
+               int32_t* out_n, bool narrow);
+  int claim_slot();
+  void release_slot(int slot);
+  // under launch_mu_: the generation of a running launch (launching one if none runs); 0 when
+  // paused
+  unsigned ensure_running_locked();
+  bool exited_locked(unsigned gen) const;  // every workgroup of launch `gen` has left
+  void stop_and_wait_locked();
+  void consume_locked(int slot, unsigned seq);  // no kernel runs: mark a request given up
   int device_;
+  int nslots_ = 1;
   void* stream_ = nullptr;
   void* mail_ = nullptr;          // mapped coherent host: kern::ServeMail
-  int32_t* buf_ = nullptr;        // mapped coherent host: queries and results
-  int64_t cap_ = 0;               // int32 words of buf_
-  unsigned seq_ = 0;
+  void* ctl_ = nullptr;           // device: kern::ServeLoopCtl
+  int32_t* buf_ = nullptr;        // mapped coherent host: each slot's results
+  unsigned seq_[16] = {0};        // per slot (owned by the slot's holder)
+  std::atomic<uint32_t> free_mask_{0};
   int paused_ = 0;
   bool launched_ = false;
+  unsigned gen_ = 0;              // generation of the newest launch
   unsigned long long idle_ticks_ = 0, life_ticks_ = 0;
   double ticks_per_us_ = 100.0;
   ServeLoopStats st_;
-  std::mutex mu_;
+  std::mutex launch_mu_, stats_mu_;
 };
 // pauses every serving loop of `device` for the guard's lifetime (index builds / frees)
 struct ServeLoopPause {

@@ -668,27 +668,43 @@ struct ServeReq {
   long long n_seeds;        // seeds follow q_ptr in the payload: [q_ptr | seeds] contiguous
   long long narrow;         // 1: score ranks < 2^23, 32-bit order keys in the top-k
 };
-struct ServeMail {
+// One request slot of the serving loop: polled by ITS workgroup of the kernel, owned by one host
+// thread at a time (a front I/O thread calls the loop directly, no hop to a GPU thread).
+struct ServeSlot {
   unsigned long long req;  // host -> device: (inline words << 32) | seq, written after the
                            // descriptor and the inline payload
   unsigned pad0[14];
-  unsigned done_seq;  // device -> host, written after the results
+  unsigned done_seq;    // device -> host, written after the results (the host writes it too,
+                        // only while no kernel runs: a request given up is marked consumed)
   unsigned pad1[15];
-  unsigned alive;     // device: 1 while the kernel runs
+  unsigned exited_gen;  // device -> host: the launch generation whose workgroup left this slot
   unsigned pad2[15];
-  unsigned stop;      // host -> device
-  unsigned pad3[15];
   // device wall clock (instrumentation): request seen, descriptor + payload staged, answers in
   // LDS, done word written
   unsigned long long t_seen, t_staged, t_computed, t_done;
   unsigned long long t_phase[6];  // the first query's matcher phases (wall clock)
+  unsigned pad3[12];
   // [descriptor | q_ptr (B + 1 int64) | seeds]: read by the kernel in ONE round of parallel
   // system-scope loads (the inline word count travels in `req`)
   ServeReq req_desc;
   int32_t payload[kServeLoopStage];
 };
-void serve_loop_launch(ServeMail* mail, unsigned long long idle_ticks,
-                       unsigned long long life_ticks, hipStream_t s);
+constexpr int kServeLoopSlots = 8;  // request slots = polling workgroups of one launch
+struct ServeMail {
+  unsigned stop;  // host -> device: every workgroup exits
+  unsigned pad0[31];
+  ServeSlot slot[kServeLoopSlots];
+};
+// device-memory coordination of one launch's workgroups (agent-scope atomics): the newest
+// request's clock (idle exit is decided once, by workgroup 0, for all) and the quit word
+struct ServeLoopCtl {
+  unsigned long long last_activity;
+  unsigned quit;  // == the launch's generation: every workgroup of that launch leaves
+  unsigned pad;
+};
+void serve_loop_launch(ServeMail* mail, ServeLoopCtl* ctl, unsigned gen, int nslots,
+                       unsigned long long idle_ticks, unsigned long long life_ticks,
+                       hipStream_t s);
 constexpr int kServeMaxSeeds = 256;
 
 }  // namespace kern

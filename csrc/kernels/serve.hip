@@ -550,13 +550,20 @@ __device__ __forceinline__ void st_sys(unsigned* p, unsigned v) {
 constexpr int kLoopStage = kServeLoopStage;
 constexpr int kLoopOut = kServeLoopOut;
 
-// One workgroup: lane 0 of wave 0 polls the request word (a short sleep between polls); a new
-// sequence number is broadcast through LDS, the request is staged into LDS by every thread in
-// one round of loads, every wave answers queries w, w + 4, ... with the wave matcher (results
-// written straight to mapped host memory), and after the barrier lane 0 publishes the done
-// word.  Exit (every wave, same iteration): stop word set, or no request for idle_ticks, or
-// life_ticks since the launch (wall_clock64 ticks) — the host relaunches on demand.
-__global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
+// One workgroup per request slot (blockIdx.x = slot): lane 0 of wave 0 polls the slot's request
+// word (a short sleep between polls); a new sequence number is broadcast through LDS, the request
+// is staged into LDS by every thread in one round of loads, every wave answers queries w, w + 4,
+// ... with the wave matcher (results written straight to mapped host memory), and after the
+// barrier lane 0 publishes the slot's done word.  The slots are independent: host threads with
+// requests in different slots are answered concurrently by different workgroups (one mailbox
+// serialised every front thread behind one request in flight).
+// Exit: the stop word, or (decided by workgroup 0 for the whole launch, from the newest request
+// clock any workgroup recorded) no request for idle_ticks or life_ticks since the launch: it
+// sets ctl->quit = gen, which every workgroup sees within one poll round.  A leaving workgroup
+// writes its slot's exited_gen = gen: the host tells "this launch exited" from "not started
+// yet" by that word alone (an alive flag set by the kernel once it ran could not).
+__global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail, ServeLoopCtl* ctl,
+                                                            unsigned gen,
                                                             unsigned long long idle_ticks,
                                                             unsigned long long life_ticks) {
   __shared__ int32_t s_key[kWaves][kSlots];
@@ -571,19 +578,21 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
   __shared__ unsigned long long s_stamps[6];
   __shared__ ServeReq s_req;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  ServeSlot* slot = &mail->slot[blockIdx.x];
   unsigned last = 0;
   const unsigned long long t0 = wall_clock64();
-  unsigned long long t_last = t0;
   if (tid == 0) {
-    last = ld_sys(&mail->done_seq);
-    st_sys(&mail->alive, 1u);
+    // a request the host gave up on was marked consumed (done_seq = its seq) before this
+    // launch, so only requests still pending are served
+    last = ld_sys(&slot->done_seq);
+    if (blockIdx.x == 0) atomicMax(&ctl->last_activity, t0);
   }
   while (true) {
     if (tid == 0) {
       unsigned cmd = 0;
       for (unsigned n = 0;; ++n) {
         const unsigned long long r =
-            __hip_atomic_load(&mail->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_load(&slot->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if ((unsigned)r != last) {
           cmd = 1;
           s_seq = (unsigned)r;
@@ -592,13 +601,22 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
         }
         if ((n & 15u) == 15u) {
           if (ld_sys(&mail->stop) != 0u) break;
-          const unsigned long long now = wall_clock64();
-          if (now - t_last > idle_ticks || now - t0 > life_ticks) break;
+          if (__hip_atomic_load(&ctl->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen)
+            break;
+          if (blockIdx.x == 0) {
+            const unsigned long long now = wall_clock64();
+            const unsigned long long la =
+                __hip_atomic_load(&ctl->last_activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((now > la && now - la > idle_ticks) || now - t0 > life_ticks) {
+              __hip_atomic_store(&ctl->quit, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
         }
         __builtin_amdgcn_s_sleep(1);
       }
       if (cmd)
-        __hip_atomic_store(&mail->t_seen, wall_clock64(), __ATOMIC_RELAXED,
+        __hip_atomic_store(&slot->t_seen, wall_clock64(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);  // (instrumentation: device clock)
       s_cmd = cmd;
     }
@@ -609,7 +627,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
     {
       constexpr int kDesc = (int)(sizeof(ServeReq) / 4);
       const int total = kDesc + (int)min(s_words, (unsigned)kLoopStage);
-      const unsigned* src = (const unsigned*)&mail->req_desc;
+      const unsigned* src = (const unsigned*)&slot->req_desc;
       unsigned* dreq = (unsigned*)&s_req;
       unsigned* dst = (unsigned*)s_stage;
       for (int i = tid; i < total; i += 64 * kWaves) {
@@ -621,7 +639,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
     __syncthreads();
     const ServeReq rq = s_req;
     if (tid == 0)
-      __hip_atomic_store(&mail->t_staged, wall_clock64(), __ATOMIC_RELAXED,
+      __hip_atomic_store(&slot->t_staged, wall_clock64(), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
     const long long* qp = (const long long*)s_stage;
     const int32_t* sd = s_stage + 2 * (rq.B + 1);
@@ -635,10 +653,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
     }
     __syncthreads();
     if (tid == 0) {
-      __hip_atomic_store(&mail->t_computed, wall_clock64(), __ATOMIC_RELAXED,
+      __hip_atomic_store(&slot->t_computed, wall_clock64(), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
       for (int i = 0; i < 5; ++i)
-        __hip_atomic_store(&mail->t_phase[i], s_stamps[i], __ATOMIC_RELAXED,
+        __hip_atomic_store(&slot->t_phase[i], s_stamps[i], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
     // results out with system-scope (write-through) stores, drained before the done word
@@ -648,12 +666,13 @@ __global__ __launch_bounds__(64 * kWaves) void k_serve_loop(ServeMail* mail,
     __syncthreads();
     if (tid == 0) {
       last = s_seq;
-      t_last = wall_clock64();
-      __hip_atomic_store(&mail->t_done, t_last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      st_sys(&mail->done_seq, last);
+      const unsigned long long now = wall_clock64();
+      atomicMax(&ctl->last_activity, now);
+      __hip_atomic_store(&slot->t_done, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      st_sys(&slot->done_seq, last);
     }
   }
-  if (tid == 0) st_sys(&mail->alive, 0u);
+  if (tid == 0) st_sys(&slot->exited_gen, gen);
 }
 
 }  // namespace
@@ -668,9 +687,13 @@ void serve_topk_big(const int64_t* row_ptr, const int32_t* cons, const uint32_t*
   KMLS_HIP(hipGetLastError());
 }
 
-void serve_loop_launch(ServeMail* mail, unsigned long long idle_ticks,
-                       unsigned long long life_ticks, hipStream_t s) {
-  hipLaunchKernelGGL(k_serve_loop, dim3(1), dim3(64 * kWaves), 0, s, mail, idle_ticks, life_ticks);
+void serve_loop_launch(ServeMail* mail, ServeLoopCtl* ctl, unsigned gen, int nslots,
+                       unsigned long long idle_ticks, unsigned long long life_ticks,
+                       hipStream_t s) {
+  if (nslots < 1 || nslots > kServeLoopSlots)
+    throw std::runtime_error("serve_loop_launch: 1 <= nslots <= kServeLoopSlots");
+  hipLaunchKernelGGL(k_serve_loop, dim3((unsigned)nslots), dim3(64 * kWaves), 0, s, mail, ctl,
+                     gen, idle_ticks, life_ticks);
   KMLS_HIP(hipGetLastError());
 }
 
@@ -736,6 +759,17 @@ GpuServeLoop::GpuServeLoop(int device) : device_(device) {
   stream_ = (void*)st;
   KMLS_HIP(hipHostMalloc(&mail_, sizeof(kern::ServeMail), hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(mail_, 0, sizeof(kern::ServeMail));
+  KMLS_HIP(hipMalloc(&ctl_, sizeof(kern::ServeLoopCtl)));
+  KMLS_HIP(hipMemset(ctl_, 0, sizeof(kern::ServeLoopCtl)));
+  // slots (polling workgroups): KMLS_SERVE_SLOTS, default 4 = the native front's I/O threads
+  nslots_ = (int)std::max<long long>(1, std::min<long long>(kern::kServeLoopSlots,
+                                                            test_hook("serve_slots", [] {
+    const char* e = std::getenv("KMLS_SERVE_SLOTS");
+    return e ? std::atoll(e) : 4ll;
+  }())));
+  free_mask_.store((uint32_t)((1ull << nslots_) - 1ull));
+  KMLS_HIP(hipHostMalloc((void**)&buf_, (size_t)nslots_ * kern::kServeLoopOut * sizeof(int32_t),
+                         hipHostMallocMapped | hipHostMallocCoherent));
   int khz = 0;
   KMLS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
   const unsigned long long per_ms = (unsigned long long)std::max(khz, 1);
@@ -746,16 +780,24 @@ GpuServeLoop::GpuServeLoop(int device) : device_(device) {
 
 GpuServeLoop::~GpuServeLoop() {
   try {
-    std::lock_guard<std::mutex> lk(mu_);
-    stop_and_wait();
+    std::lock_guard<std::mutex> lk(launch_mu_);
+    stop_and_wait_locked();
   } catch (...) {
   }
   if (buf_) (void)hipHostFree(buf_);
   if (mail_) (void)hipHostFree(mail_);
+  if (ctl_) (void)hipFree(ctl_);
   if (stream_) (void)hipStreamDestroy((hipStream_t)stream_);
 }
 
-void GpuServeLoop::stop_and_wait() {
+bool GpuServeLoop::exited_locked(unsigned gen) const {
+  volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
+  for (int s = 0; s < nslots_; ++s)
+    if (m->slot[s].exited_gen != gen) return false;
+  return true;
+}
+
+void GpuServeLoop::stop_and_wait_locked() {
   if (!launched_) return;
   volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
   m->stop = 1u;
@@ -764,44 +806,81 @@ void GpuServeLoop::stop_and_wait() {
   launched_ = false;
 }
 
-bool GpuServeLoop::ensure_running() {
+void GpuServeLoop::consume_locked(int slot, unsigned seq) {
+  // only while no kernel runs: the next launch starts from done_seq and never serves it
   volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
-  if (launched_ && m->alive != 0u) return true;
-  if (launched_) {  // exited (idle / lifetime) or about to: let it finish, then relaunch
+  m->slot[slot].done_seq = seq;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+}
+
+unsigned GpuServeLoop::ensure_running_locked() {
+  if (paused_ > 0) return 0;
+  if (launched_ && !exited_locked(gen_)) return gen_;
+  if (launched_) {  // every workgroup of it has left (idle / lifetime): it is finishing
     KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_));
     launched_ = false;
   }
+  volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
   m->stop = 0u;
-  m->alive = 0u;
+  const unsigned gen = ++gen_;
   std::atomic_thread_fence(std::memory_order_seq_cst);
   kmls::kern::ServeMail* dm = nullptr;
   KMLS_HIP(hipHostGetDevicePointer((void**)&dm, mail_, 0));
-  kern::serve_loop_launch(dm, idle_ticks_, life_ticks_, (hipStream_t)stream_);
+  kern::serve_loop_launch(dm, (kern::ServeLoopCtl*)ctl_, gen, nslots_, idle_ticks_, life_ticks_,
+                          (hipStream_t)stream_);
   launched_ = true;
-  ++st_.launches;
-  return true;
+  {
+    std::lock_guard<std::mutex> sl(stats_mu_);
+    ++st_.launches;
+  }
+  return gen;
 }
 
 void GpuServeLoop::pause() {
-  std::lock_guard<std::mutex> lk(mu_);
+  std::lock_guard<std::mutex> lk(launch_mu_);
   ++paused_;
-  stop_and_wait();
+  stop_and_wait_locked();
 }
 
 void GpuServeLoop::resume() {
-  std::lock_guard<std::mutex> lk(mu_);
+  std::lock_guard<std::mutex> lk(launch_mu_);
   if (paused_ > 0) --paused_;
 }
 
 ServeLoopStats GpuServeLoop::stats() {
-  std::lock_guard<std::mutex> lk(mu_);
+  std::lock_guard<std::mutex> lk(stats_mu_);
   return st_;
+}
+
+int GpuServeLoop::claim_slot() {
+  uint32_t m = free_mask_.load(std::memory_order_acquire);
+  while (m) {
+    const int s = __builtin_ctz(m);
+    if (free_mask_.compare_exchange_weak(m, m & ~(1u << s), std::memory_order_acq_rel))
+      return s;
+  }
+  return -1;
+}
+
+void GpuServeLoop::release_slot(int slot) {
+  free_mask_.fetch_or(1u << slot, std::memory_order_acq_rel);
 }
 
 bool GpuServeLoop::run(const int64_t* d_row_ptr, const int32_t* d_cons, const uint32_t* d_score,
                        const uint8_t* d_is_key, int64_t n_items, const int64_t* q_ptr, int64_t B,
                        const int32_t* seeds, int k, int32_t* out_ids, int32_t* out_n,
                        bool narrow) {
+  const int slot = claim_slot();
+  if (slot < 0) {  // every slot holds a request in flight: the caller answers on the host
+    std::lock_guard<std::mutex> sl(stats_mu_);
+    ++st_.refused;
+    return false;
+  }
+  struct Release {
+    GpuServeLoop* l;
+    int s;
+    ~Release() { l->release_slot(s); }
+  } rel{this, slot};
   // one round trip holds what the kernel stages in LDS: split longer batches
   int64_t b0 = 0;
   while (b0 < B) {
@@ -819,42 +898,28 @@ bool GpuServeLoop::run(const int64_t* d_row_ptr, const int32_t* d_cons, const ui
       ++b0;
       continue;
     }
-    if (!run_one(d_row_ptr, d_cons, d_score, d_is_key, n_items, q_ptr + b0, b1 - b0, seeds, k,
-                 out_ids + b0 * k, out_n + b0, narrow))
+    if (!run_one(slot, d_row_ptr, d_cons, d_score, d_is_key, n_items, q_ptr + b0, b1 - b0,
+                 seeds, k, out_ids + b0 * k, out_n + b0, narrow))
       return false;
     b0 = b1;
   }
   return true;
 }
 
-bool GpuServeLoop::run_one(const int64_t* d_row_ptr, const int32_t* d_cons,
+bool GpuServeLoop::run_one(int slot, const int64_t* d_row_ptr, const int32_t* d_cons,
                            const uint32_t* d_score, const uint8_t* d_is_key, int64_t n_items,
                            const int64_t* q_ptr, int64_t B, const int32_t* seeds, int k,
                            int32_t* out_ids, int32_t* out_n, bool narrow) {
-  std::lock_guard<std::mutex> lk(mu_);
-  if (paused_ > 0 || B <= 0) {
-    ++st_.refused;
-    return false;
-  }
+  if (B <= 0) return false;
   const auto t0 = std::chrono::steady_clock::now();
-  KMLS_HIP(hipSetDevice(device_));
   const int64_t ns = q_ptr[B] - q_ptr[0];
-  const int64_t no = B * (int64_t)(k + 1);
-  const int64_t words = no;  // the host buffer holds only the answers (payload is inline)
   KMLS_CHECK(2 * (B + 1) + ns <= kern::kServeLoopStage, "serve loop: request past the stage");
-  if (words > cap_) {  // grow: the kernel must not hold the old buffer
-    stop_and_wait();
-    if (buf_) KMLS_HIP(hipHostFree(buf_));
-    buf_ = nullptr;
-    cap_ = std::max<int64_t>(words, std::max<int64_t>(cap_ * 2, 1 << 16));
-    KMLS_HIP(hipHostMalloc((void**)&buf_, (size_t)cap_ * sizeof(int32_t),
-                           hipHostMallocMapped | hipHostMallocCoherent));
-  }
-  volatile kern::ServeMail* m = (volatile kern::ServeMail*)mail_;
-  kern::ServeMail* mw = (kern::ServeMail*)mail_;
+  KMLS_CHECK(B * (int64_t)(k + 1) <= kern::kServeLoopOut, "serve loop: answers past the slot");
+  volatile kern::ServeSlot* m = &((volatile kern::ServeMail*)mail_)->slot[slot];
+  kern::ServeSlot* mw = &((kern::ServeMail*)mail_)->slot[slot];
   int64_t* hq = reinterpret_cast<int64_t*>(mw->payload);
   int32_t* hs = mw->payload + 2 * (B + 1);
-  int32_t* ho = buf_;
+  int32_t* ho = buf_ + (size_t)slot * kern::kServeLoopOut;
   for (int64_t i = 0; i <= B; ++i) hq[i] = q_ptr[i] - q_ptr[0];
   std::copy(seeds + q_ptr[0], seeds + q_ptr[B], hs);
   int32_t* dev = nullptr;
@@ -867,34 +932,60 @@ bool GpuServeLoop::run_one(const int64_t* d_row_ptr, const int32_t* d_cons,
   rq.n_items = n_items;
   rq.q_ptr = nullptr;  // inline: staged from the mailbox
   rq.seeds = nullptr;
-  rq.out = dev;
+  rq.out = dev + (size_t)slot * kern::kServeLoopOut;
   rq.B = B;
   rq.k = k;
   rq.n_seeds = ns;
   rq.narrow = narrow ? 1 : 0;
   std::memcpy((void*)&m->req_desc, &rq, sizeof rq);
   for (int64_t i = 0; i < B; ++i) ho[i * (k + 1)] = -3;  // (never a real answer)
-  ensure_running();
-  const unsigned seq = ++seq_;
+  unsigned gen;
+  {
+    std::lock_guard<std::mutex> lk(launch_mu_);
+    gen = ensure_running_locked();
+  }
+  if (gen == 0) {  // paused
+    std::lock_guard<std::mutex> sl(stats_mu_);
+    ++st_.refused;
+    return false;
+  }
+  const unsigned seq = ++seq_[slot];
   std::atomic_thread_fence(std::memory_order_seq_cst);  // descriptor and payload before the word
   m->req = ((unsigned long long)(2 * (B + 1) + ns) << 32) | (unsigned long long)seq;
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  // wait for the done word; a kernel that exited meanwhile (idle race) is relaunched once
+  // wait for the done word.  The launch can leave without serving it (its idle exit raced the
+  // request, or a pause stopped it): then relaunch (the new launch serves the pending word) or,
+  // paused, mark it consumed and refuse.
   const auto t_start = std::chrono::steady_clock::now();
-  bool relaunched = false;
   for (unsigned n = 0;; ++n) {
     if (m->done_seq == seq) break;
-    if ((n & 1023u) == 1023u) {
-      if (m->alive == 0u && !relaunched && m->done_seq != seq) {
-        KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_));  // it has exited
-        launched_ = false;
-        ensure_running();
-        relaunched = true;
+    if ((n & 255u) == 255u) {
+      if (m->exited_gen == gen) {
+        std::lock_guard<std::mutex> lk(launch_mu_);
+        if (m->done_seq != seq) {
+          if (gen_ == gen) {
+            gen = ensure_running_locked();  // 0: paused (the kernel is stopped)
+          } else {
+            gen = (launched_ && paused_ == 0) ? gen_ : 0u;
+          }
+          if (gen == 0) {
+            if (launched_) stop_and_wait_locked();
+            consume_locked(slot, seq);
+            std::lock_guard<std::mutex> sl(stats_mu_);
+            ++st_.refused;
+            return false;
+          }
+        }
       }
       if (std::chrono::steady_clock::now() - t_start > std::chrono::milliseconds(500)) {
-        stop_and_wait();  // lost: the next batch relaunches; this one is answered elsewhere
-        ++st_.refused;
-        return false;
+        std::lock_guard<std::mutex> lk(launch_mu_);
+        if (m->done_seq != seq) {
+          stop_and_wait_locked();  // lost: no kernel runs now; the next request relaunches
+          if (m->done_seq != seq) consume_locked(slot, seq);
+          std::lock_guard<std::mutex> sl(stats_mu_);
+          ++st_.refused;
+          return false;
+        }
       }
     }
     __builtin_ia32_pause();
@@ -906,6 +997,7 @@ bool GpuServeLoop::run_one(const int64_t* d_row_ptr, const int32_t* d_cons,
     for (int j = 0; j < k; ++j) out_ids[b * k + j] = (j < n) ? ho[b * (k + 1) + 1 + j] : -1;
   }
   const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  std::lock_guard<std::mutex> sl(stats_mu_);
   st_.kernel_us += (double)(m->t_done - m->t_seen) / ticks_per_us_;
   st_.stage_us += (double)(m->t_staged - m->t_seen) / ticks_per_us_;
   st_.compute_us += (double)(m->t_computed - m->t_staged) / ticks_per_us_;

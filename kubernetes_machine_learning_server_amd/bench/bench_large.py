@@ -375,6 +375,9 @@ def rule_map_main(args) -> int:
                 out[f"query_batch{B}_us"] = {"cpp": round(res["cpp"][0], 1),
                                              "hip": round(res["hip"][0], 1), "same": same}
             del gidx
+            pvc = getattr(args, "pvc_dir", None)
+            if pvc:
+                out["pvc"] = write_config5_pvc(pvc, r, I, ids, fcounts, T, minsup)
         if not getattr(args, "quiet", False):
             print(json.dumps(out), flush=True)
     if world > 1 and own_group:
@@ -383,13 +386,58 @@ def rule_map_main(args) -> int:
     return 0
 
 
+def write_config5_pvc(pvc_dir: str, r: dict, I: int, ids, fcounts, T: int, minsup: int,
+                      alt_factor: float = 1.5, top: float = 0.03) -> dict:
+    """A serving PVC of the config-5 artifact (``<pvc>/api-data/{pickles/rules.idx,
+    pickles/best_tracks.pickle, last_execution.txt}``) plus ``<pvc>/rules_alt.idx``, the rule
+    map of the same data at alt_factor x the support (the pair rows filtered to counts >= the
+    higher threshold, keys = items frequent at it): what the next job run would publish, for the
+    reload-under-load run (``bench_serve --reload-index``)."""
+    import pathlib
+    import pickle
+    import numpy as np
+    from ..serve.index import index_from_device_csr
+    base = pathlib.Path(pvc_dir) / "api-data"
+    pk = base / "pickles"
+    pk.mkdir(parents=True, exist_ok=True)
+    names = [f"track_{i}" for i in range(I)]  # random-init vocabulary (make_large_pvc.py)
+    ix = index_from_device_csr({k: r[k] for k in ("row_ptr", "cons", "count")}, I, ids, T, names)
+    ix.save(pk / "rules.idx")
+    ix.save(pathlib.Path(pvc_dir) / "rules_main.idx")  # to restore between reload runs
+    fc = np.asarray(fcounts, np.int64)
+    order = np.argsort(-fc, kind="stable")[:max(10, int(len(ids) * top))]
+    best = [{"track_name": f"track_{int(ids[o])}", "count": int(fc[o])} for o in order]
+    with open(pk / "best_tracks.pickle", "wb") as f:
+        pickle.dump(best, f)
+    (base / "last_execution.txt").write_text("initial")
+    ms2 = int(np.ceil(minsup * alt_factor))
+    row_ptr = np.asarray(r["row_ptr"], np.int64)
+    cons, cnt = np.asarray(r["cons"]), np.asarray(r["count"])
+    keep = cnt >= ms2
+    csum = np.zeros(len(cnt) + 1, np.int64)
+    np.cumsum(keep, out=csum[1:])
+    per_row = csum[row_ptr[1:]] - csum[row_ptr[:-1]]
+    rp2 = np.zeros(I + 1, np.int64)
+    np.cumsum(per_row, out=rp2[1:])
+    ids2 = np.asarray(ids)[fc >= ms2]
+    alt = index_from_device_csr({"row_ptr": rp2, "cons": cons[keep], "count": cnt[keep]}, I,
+                                ids2, T, names)
+    alt_path = pathlib.Path(pvc_dir) / "rules_alt.idx"
+    alt.save(alt_path)
+    return {"dir": str(pvc_dir), "keys": int(ix.n_keys), "alt_keys": int(alt.n_keys),
+            "alt_min_count": ms2, "alt_entries": int(keep.sum())}
+
+
 def run_rule_map(shape: str = "100Mx1M", min_support: float = 2e-4, steps: int = 3,
-                 warmup: int = 1, n_tx: int = 0, seed: int = 0, verify_rows: int = 64) -> dict:
+                 warmup: int = 1, n_tx: int = 0, seed: int = 0, verify_rows: int = 64,
+                 pvc_dir: str = "") -> dict:
     """``rule_map_main`` as a function (bench.py's config-5 section): every rank of the caller's
     process group (or one process) generates its shard and times ``DistRuleMap.step``; the
-    result dict (complete on rank 0) is returned instead of printed."""
+    result dict (complete on rank 0) is returned instead of printed.  ``pvc_dir``: rank 0 also
+    writes the serving PVC of the artifact (``write_config5_pvc``)."""
     ns = argparse.Namespace(shape=shape, n_tx=n_tx, min_support=min_support, steps=steps,
-                            warmup=warmup, seed=seed, verify_rows=verify_rows, quiet=True)
+                            warmup=warmup, seed=seed, verify_rows=verify_rows, quiet=True,
+                            pvc_dir=pvc_dir)
     rule_map_main(ns)
     return ns.result
 

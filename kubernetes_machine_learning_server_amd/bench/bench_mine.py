@@ -19,7 +19,7 @@ from __future__ import annotations
 import json
 import os
 import time
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, List, Optional
 
 import numpy as np
 
@@ -178,6 +178,77 @@ def offline_full_count() -> Optional[Dict]:
         return json.load(fh)
 
 
+# BASELINE config 2 complete, on a pre-declared subset of the offline run's 256 virtual ranks:
+# the ranks at the 0 / 25 / 50 / 75 / 90 % quantiles of the offline per-rank time (1.3-23 s
+# each, ~57 s in all), fixed before any bench run, so light and heavy shares are both timed.
+CONFIG2_SUBSET_RANKS = (38, 250, 156, 92, 192)
+CONFIG2_WORLD = 256
+
+
+def config2_partials() -> Optional[Dict[int, Dict]]:
+    """Per-virtual-rank partials of the complete config-2 count (scripts/full_count.py --world
+    256: per-size counts, digest, seconds), as committed under profiles/config2_full/."""
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data",
+                     "config2_world256_partials.jsonl")
+    if not os.path.exists(p):
+        return None
+    out = {}
+    with open(p) as fh:
+        for line in fh:
+            if line.strip():
+                d = json.loads(line)
+                out[int(d["rank"])] = d
+    return out if len(out) == CONFIG2_WORLD else None
+
+
+def _trim(per) -> List[int]:
+    per = [int(x) for x in per]
+    while per and per[-1] == 0:
+        per.pop()
+    return per
+
+
+def config2_complete_subset(g, ms: float = 0.01, ranks=CONFIG2_SUBSET_RANKS) -> Dict:
+    """Complete full mining of BASELINE config 2 (ds1 @ 0.01, every size: 1.64e14 itemsets)
+    timed by the bench on `ranks` of the 256 snake-dealt virtual ranks: each rank's share (its
+    level-3 tasks' whole subtrees) is mined exactly (``mine_deep`` with that rank / world, no
+    communicator) and its per-size counts and digest must equal the offline run's partial of
+    the same rank.  Reports the itemsets/s of config 2 proper and the whole-problem time
+    projected from the offline per-rank times scaled by this run's measured/offline ratio."""
+    parts = config2_partials()
+    if parts is None:
+        return {"error": "config2_world256_partials.jsonl missing"}
+    recs, n_tot, s_tot, off_tot = [], 0, 0.0, 0.0
+    for r in ranks:
+        t = time.perf_counter()
+        d = g.mine_deep(ms, 0, int(r), CONFIG2_WORLD, None)
+        s = time.perf_counter() - t
+        ref = parts[int(r)]
+        ok = (d["digest"] == ref["digest"] and int(d["n_itemsets"]) == int(ref["n_itemsets"])
+              and _trim(d["per_level"]) == _trim(ref["per_level"]))
+        recs.append({"rank": int(r), "s": round(s, 3), "offline_s": ref["s"],
+                     "n_itemsets": int(d["n_itemsets"]), "max_depth": int(d["max_depth"]),
+                     "verified": bool(ok)})
+        n_tot += int(d["n_itemsets"])
+        s_tot += s
+        off_tot += float(ref["s"])
+    all_off = sum(float(p["s"]) for p in parts.values())
+    off = offline_full_count() or {}
+    proj = all_off * s_tot / off_tot if off_tot else None
+    return {"what": "BASELINE config 2 complete (ds1 @0.01, every itemset of every size), "
+                    "mined exactly on pre-declared virtual ranks of the 256-way snake deal",
+            "world_virtual": CONFIG2_WORLD, "ranks": recs,
+            "verified": all(x["verified"] for x in recs),
+            "n_itemsets": n_tot, "s": round(s_tot, 3),
+            "itemsets_per_s": round(n_tot / s_tot, 1) if s_tot else None,
+            "share_of_problem": round(n_tot / int(off["n_itemsets"]), 5) if off else None,
+            "measured_over_offline": round(s_tot / off_tot, 4) if off_tot else None,
+            "projected_whole_problem_s_1gpu": round(proj, 1) if proj else None,
+            "projected_itemsets_per_s_1gpu": (round(int(off["n_itemsets"]) / proj, 1)
+                                              if proj and off else None),
+            "whole_problem_n_itemsets": off.get("n_itemsets")}
+
+
 def deep_capped(dm, ms: float, budget_s: float, start_len: int = 4, max_cap: int = 64) -> Dict:
     """Full mining at `ms` with the itemset size cap raised one at a time while a call stays
     under `budget_s` (the last completed cap's counts, timed)."""
@@ -332,6 +403,7 @@ def run_config2(N, tx, names, tie, steps: int, verify: bool, deep_miner=None,
             f["capped_counts_match_offline_prefix"] = (
                 f["per_level"] == [int(x) for x in off["per_level"][1:L + 1]])
         out["full_mining"] = f
+        out["complete_subset"] = config2_complete_subset(deep_miner.g, ms)
     return out
 
 

@@ -147,7 +147,8 @@ def mine_rules_distributed(cfg: JobSettings, tx: pp.PlaylistTransactions, min_su
     rank, world = dist.get_rank(), dist.get_world_size()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if use_deep_split(cfg, tx.n_tx):
-        return mine_rules_deep_split(cfg, tx, min_support, total_songs, rank, world, local, t0)
+        return mine_rules_deep_split(cfg, tx, min_support, total_songs, rank, world, local, t0,
+                                     ck)
     dm = DistMiner(tx.tx_ptr, tx.items, len(tx.names), min_support, device=local,
                    max_len=2 if cfg.rules_mode == "pairs" else 0,
                    backend="cpu" if cfg.miner == "cpu" else "gpu", mode=cfg.dist_mode)
@@ -209,17 +210,43 @@ def use_deep_split(cfg: JobSettings, n_tx: int) -> bool:
 
 
 def mine_rules_deep_split(cfg: JobSettings, tx: pp.PlaylistTransactions, min_support: float,
-                          total_songs: int, rank: int, world: int, local: int, t0: float):
+                          total_songs: int, rank: int, world: int, local: int, t0: float,
+                          ck: Optional[PhaseCheckpoint] = None):
     """Full mining split over the ranks (the headline engine, ``parallel/deep.py``): level-3
     tasks dealt by measured cost, every rank's itemsets emitted into its HBM arena, compacted on
-    its GPU and gathered on rank 0 as one trie; the rule map through ``DistRuleMap``."""
+    its GPU and gathered on rank 0 as one trie; the rule map through ``DistRuleMap``.
+
+    Phase checkpoint: rank 0 (the only holder of the gathered trie) saves it; a restarted job
+    whose rank 0 finds it skips the mining on every rank (the vote is all-reduced, so all ranks
+    take the same branch and the rule map's collectives still line up)."""
+    import torch
+    import torch.distributed as dist
     from ..parallel.deep import DeepMiner
-    dm = DeepMiner(tx.tx_ptr, tx.items, len(tx.names), device=local, rank=rank, world=world)
-    d, arrs = dm.mine_trie(min_support)
-    st = {"n_frequent_items": int(d["n_frequent_items"]), "n_itemsets": int(d["n_itemsets"]),
-          "digest": d["digest"], "miner": "deep", "dist_mode": f"deep-x{world}",
-          "backend": "gpu"}
-    del dm  # its device buffers go before the rule map's
+    phase = f"deeptrie_x{world}"
+    have = 1 if (rank != 0 or (ck is not None and ck.has(phase))) else 0
+    flag = torch.tensor([have], dtype=torch.int64,
+                        device=torch.device("cuda", local) if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    keys = ("parent", "item", "count", "depth")
+    if int(flag.item()) == 1:
+        arrs, st = None, {"backend": "checkpoint", "miner": "deep", "dist_mode": f"deep-x{world}"}
+        if rank == 0:
+            z = ck.load(phase)
+            arrs = {k: z[k] for k in keys}
+            st.update(n_frequent_items=int(z["n_frequent"]), n_itemsets=int(z["n_itemsets"]),
+                      digest=str(z["digest"]))
+            print("Resumed the gathered deep trie from checkpoint", ck.dir)
+    else:
+        dm = DeepMiner(tx.tx_ptr, tx.items, len(tx.names), device=local, rank=rank, world=world)
+        d, arrs = dm.mine_trie(min_support)
+        st = {"n_frequent_items": int(d["n_frequent_items"]), "n_itemsets": int(d["n_itemsets"]),
+              "digest": d["digest"], "miner": "deep", "dist_mode": f"deep-x{world}",
+              "backend": "gpu"}
+        del dm  # its device buffers go before the rule map's
+        if rank == 0 and ck is not None and ck.enabled:
+            ck.save(phase, n_frequent=np.int64(st["n_frequent_items"]),
+                    n_itemsets=np.int64(st["n_itemsets"]), digest=np.array(st["digest"]),
+                    **{k: np.asarray(arrs[k]) for k in keys})
     _fault("after_mining_phase")
     rmap = rule_map_distributed(cfg, tx, min_support, rank, world, local)
     if rank != 0:
@@ -334,7 +361,9 @@ def run(cfg: Optional[JobSettings] = None) -> Dict:
         # fails the job within KMLS_DIST_TIMEOUT_S instead of hanging it; K8s then re-runs it.
         # MINER=cpu runs the same protocol over gloo (the CPU test tier)
         timeout = datetime.timedelta(seconds=cfg.dist_timeout_s)
-        if cfg.miner == "cpu":
+        # KMLS_DIST_BACKEND=gloo: GPU miners under a gloo group (tests: ranks sharing one GPU,
+        # with KMLS_COMM=host for the native collectives; RCCL refuses two ranks on one device)
+        if cfg.miner == "cpu" or os.environ.get("KMLS_DIST_BACKEND") == "gloo":
             dist.init_process_group("gloo", timeout=timeout)
         else:
             torch.cuda.set_device(local)

@@ -170,3 +170,63 @@ def test_job_full_mining_through_the_deep_engine(tmp_path, gpu_mod):
     want = gpu_mod.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])
     assert got["digest"] == want["digest"] and st["n_itemsets"] == want["n"]
     _check_trie(z["parent"], z["depth"])
+
+
+def _deep_job_worker(rank, world, port, root, fault, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", KMLS_COMM="host",
+                      KMLS_COMM_TIMEOUT_S="120", KMLS_DIST_BACKEND="gloo")
+    if fault:
+        os.environ["KMLS_FAULT"] = fault
+    else:
+        os.environ.pop("KMLS_FAULT", None)
+    import pathlib
+    os.chdir(root)
+    from kubernetes_machine_learning_server_amd.job import main as job
+    from tests.helpers import job_settings
+    cfg = job_settings(pathlib.Path(root), miner="gpu", rules_mode="full", min_support=0.04,
+                       num_gpus=world, checkpoint_dir=pathlib.Path(root) / "ck",
+                       dist_timeout_s=120.0, dist_mode="deep")
+    try:
+        out_q.put((rank, job.run(cfg), None))
+    except Exception as e:  # noqa: BLE001 — the injected fault
+        out_q.put((rank, None, repr(e)))
+
+
+def _run_deep_job(root, world, fault=""):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_deep_job_worker, args=(r, world, port, str(root), fault, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=200) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+def test_deep_split_job_resumes_from_the_trie_checkpoint(tmp_path, gpu_mod):
+    """The multi-GPU job's deep split (world 2, ranks sharing the GPU): rank 0 checkpoints the
+    gathered trie; after a crash between mining and publishing the restarted job resumes from
+    it on every rank (no re-mining) and publishes the CPU trie's content."""
+    from tests.helpers import make_datasets
+    make_datasets(tmp_path, shapes=("ds1", "tiny"), seeds=(0, 4))
+    res = _run_deep_job(tmp_path, 2, fault="after_mining_phase")
+    assert all("injected fault" in (r[2] or "") for r in res), res
+    assert len(list((tmp_path / "ck").rglob("deeptrie_x2.npz"))) == 1
+    res = _run_deep_job(tmp_path, 2)
+    assert all(r[2] is None for r in res), res
+    summary = res[0][1]
+    assert summary["backend"] == "checkpoint" and summary["dataset_index"] == 1
+    z = np.load(tmp_path / "api-data" / "pickles" / "frequent_itemsets.npz")
+    got = gpu_mod.trie_digest(z["parent"], z["item"], z["count"], z["depth"])
+    from kubernetes_machine_learning_server_amd.job import preprocess as pp
+    t = pp.clean_df(pp.read_tracks(str(tmp_path / "datasets" / "2023_spotify_ds1.csv"), 1.0,
+                                   verbose=False))
+    tx = pp.group_tracks_by_playlist(t)
+    ref = gpu_mod.mine_cpu(tx.tx_ptr, tx.items, len(tx.names), 0.04)
+    want = gpu_mod.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])
+    assert got["digest"] == want["digest"] and summary["n_itemsets"] == want["n"]
+    assert not list((tmp_path / "ck").rglob("*.npz"))  # cleared after success

@@ -157,11 +157,11 @@ def test_native_ring_pair_rows_on_one_gpu(world):
             np.testing.assert_array_equal(rows, ref)
 
 
-def _shard_worker(rank, world, port, out_q):
+def _shard_worker(rank, world, port, out_q, hooks="cooc=2"):
     # cooc=2: the horizontal plan even where the cost model prefers the GEMM (small F here)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), KMLS_COMM="host", KMLS_COMM_TIMEOUT_S="120",
-                      KMLS_TEST_HOOKS="cooc=2")
+                      KMLS_TEST_HOOKS=hooks)
     import torch.distributed as dist
     from kubernetes_machine_learning_server_amd.ops import native
     from kubernetes_machine_learning_server_amd.parallel.dist_miner import DistMiner, gather_trie
@@ -189,16 +189,21 @@ def _shard_worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_native_item_shard_on_one_gpu(world):
+@pytest.mark.parametrize("world,hooks", [(1, "cooc=2"), (2, "cooc=2"), (3, "cooc=2"),
+                                         (2, "cooc=2,pair_rows=0")])
+def test_native_item_shard_on_one_gpu(world, hooks):
     """Item-sharded mining without bitmaps (GpuMiner.mine_shard): each rank all-gathers the
     frequent-rank CSRs, counts the pair rows and horizontal levels of its own items; the
-    gathered sub-tries are the whole trie (content digest of the CPU miner)."""
+    gathered sub-tries are the whole trie (content digest of the CPU miner).  With the row
+    count disabled (pair_rows=0) every rank must decline the native plan together (the
+    scattered-atomic fallback would count only the rank's own CSR) and the bitmap shard
+    protocol mines instead: the same digest."""
     from kubernetes_machine_learning_server_amd.ops import native
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q, hooks))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = []
@@ -215,7 +220,10 @@ def test_native_item_shard_on_one_gpu(world):
     rd = N.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])
     for rank, out in res:
         for path, glob, d in out:
-            assert path == "horizontal-item-shard", path
+            if "pair_rows=0" in hooks:
+                assert path != "horizontal-item-shard", path
+            else:
+                assert path == "horizontal-item-shard", path
             assert glob == rd["n"]
             if rank == 0:
                 assert d == (rd["digest"], rd["n"])

@@ -116,3 +116,54 @@ def test_serve_loop_across_an_index_reload(gpu_mod):
     _check(ha, ga, q, s)
     del ga
     _check(hb, gb, q2, s2)
+
+
+def test_serve_loop_concurrent_callers_and_low_qps(gpu_mod):
+    """Several host threads in flight at once (each takes its own request slot, answered by its
+    own workgroup: the native front's I/O threads call the loop directly), every answer equal to
+    the C++ matcher's; then requests spaced past the kernel's 20 ms idle exit: each is answered
+    by a relaunch without waiting out a stale launch (no 20 ms stall per request)."""
+    import threading
+    idx = _index(gpu_mod, seed=4)
+    host = idx.native()
+    gidx = gpu_mod.GpuRuleIndex(0, host)
+    keys = np.flatnonzero(idx.is_key).astype(np.int32)
+    errors, answered = [], [0]
+    lock = threading.Lock()
+
+    def worker(t):
+        rng = np.random.default_rng(100 + t)
+        try:
+            for _ in range(150):
+                q_ptr, seeds = _queries(rng, keys, 1 + (t % 3), idx.n_items)
+                ids, n, ok = gidx.query_loop(q_ptr, seeds, 10)
+                cids, cn = host.query_batch(q_ptr, seeds, 10)
+                ids, n, cids, cn = map(np.asarray, (ids, n, cids, cn))
+                if not ok:  # every slot busy: the caller's C++ path (allowed, counted)
+                    continue
+                small = n != -2
+                assert (n[small] == cn[small]).all()
+                for b in np.flatnonzero(small):
+                    assert (ids[b, :max(n[b], 0)] == cids[b, :max(cn[b], 0)]).all()
+                with lock:
+                    answered[0] += 1
+        except BaseException as e:  # noqa: BLE001 — reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert answered[0] >= 400, answered[0]
+    # low QPS: requests 30 ms apart, past the idle exit each time
+    rng = np.random.default_rng(7)
+    slow = []
+    for _ in range(6):
+        time.sleep(0.03)
+        q_ptr, seeds = _queries(rng, keys, 1, idx.n_items)
+        t0 = time.perf_counter()
+        _check(host, gidx, q_ptr, seeds)
+        slow.append(time.perf_counter() - t0)
+    assert max(slow) < 0.015, slow  # a relaunch costs a launch, never an idle period
