@@ -8,6 +8,13 @@ namespace kern {
 
 inline unsigned vzero() { return 0u; }
 
+template <typename T>
+using gptr = T*;
+template <typename T>
+inline gptr<T> as_global(T* p) { return p; }
+template <typename T>
+inline gptr<T> as_global_addr(unsigned long long a) { return (T*)a; }
+
 inline unsigned long long bcast64(unsigned long long v, int src) {
   return emu::xchg(v, src);
 }
@@ -15,6 +22,8 @@ inline unsigned long long shfl_xor64(unsigned long long v, int m) {
   return emu::xchg(v, emu::tl->lane ^ m);
 }
 inline unsigned uni(unsigned v) { return (unsigned)__builtin_amdgcn_readfirstlane((int)v); }
+inline unsigned lane0(unsigned v) { return (unsigned)emu::xchg((unsigned long long)v, 0); }
+inline unsigned long long lane0_64(unsigned long long v) { return emu::xchg(v, 0); }
 inline unsigned long long uni64(unsigned long long v) {
   return ((unsigned long long)uni((unsigned)(v >> 32)) << 32) | uni((unsigned)v);
 }

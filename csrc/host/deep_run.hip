@@ -86,10 +86,15 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   const int blocks_per_cu = kern::deep_count_wps(maxt, opt.blocks_per_cu, E != 0);
   const int grid = std::max(1, in.n_cus * blocks_per_cu);
   const int64_t waves = (int64_t)grid * kern::deep_waves_per_block();
+  // Per-wave strides that are NOT powers of two: every wave works near the bottom of its own
+  // stack, so 4 MiB-aligned stacks (and 128 KiB-aligned frame stacks) put the hot lines of all
+  // 512 waves of an XCD into the same L2 sets (index bits 7-17), a few hundred of its 2048.
+  // An odd number of 128-byte lines past the power of two spreads wave g's base over every set
+  // (g x odd mod 2048 has full period).
   const size_t stack_need = std::max<size_t>(
       opt.stack_mb > 0 ? (size_t)opt.stack_mb << 20 : env_bytes_mb("KMLS_DEEP_STACK_MB", 4),
-      4 * kern::deep_row_block_bytes(W, F, E));
-  const int fcap = std::max(4096, kern::deep_min_fcap());
+      4 * kern::deep_row_block_bytes(W, F, E)) + 69 * 128;
+  const int fcap = std::max(4096, kern::deep_min_fcap()) + 36;  // 4132 x 32 B = 1033 lines
   if (b.waves < waves || b.stack_bytes < stack_need || b.fcap < fcap) {
     if (b.stacks) KMLS_HIP(hipFree(b.stacks));
     if (b.fstacks) KMLS_HIP(hipFree(b.fstacks));

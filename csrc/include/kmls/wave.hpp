@@ -16,6 +16,21 @@ __device__ __forceinline__ unsigned vzero() {
   return z;
 }
 
+// A pointer the compiler must treat as GLOBAL memory (address space 1).  A row pointer rebuilt
+// from an integer (a frame's block address) is otherwise generic, so its loads become flat_load:
+// those count in lgkmcnt as well as vmcnt and may return out of order, so every later wait for
+// an LDS result also waits for the row loads in flight.  Through a gptr they are global_load.
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ gptr<T> as_global(T* p) {
+  return (gptr<T>)p;
+}
+template <typename T>
+__device__ __forceinline__ gptr<T> as_global_addr(unsigned long long a) {
+  return (gptr<T>)a;
+}
+
 __device__ __forceinline__ unsigned long long bcast64(unsigned long long v, int src) {
   const unsigned lo = __shfl((unsigned)v, src, 64);
   const unsigned hi = __shfl((unsigned)(v >> 32), src, 64);
@@ -26,6 +41,14 @@ __device__ __forceinline__ unsigned long long shfl_xor64(unsigned long long v, i
   const unsigned lo = __shfl_xor((unsigned)v, m, 64);
   const unsigned hi = __shfl_xor((unsigned)(v >> 32), m, 64);
   return ((unsigned long long)hi << 32) | lo;
+}
+
+// lane 0's value (uniform) whichever lanes are active
+__device__ __forceinline__ unsigned lane0(unsigned v) {
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 0);
+}
+__device__ __forceinline__ unsigned long long lane0_64(unsigned long long v) {
+  return ((unsigned long long)lane0((unsigned)(v >> 32)) << 32) | lane0((unsigned)v);
 }
 
 // (the builtin returns int: both halves go through unsigned, or the low half sign-extends)

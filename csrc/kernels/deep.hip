@@ -139,7 +139,7 @@ struct ProjLds {
 
 // lanes w < WT: word w of the uniform row R = blk[w][ia]; returns |R| (uniform)
 template <int WT, int NW>
-__device__ __forceinline__ unsigned proj_setup(ProjLds<NW>& P, const unsigned long long* blk,
+__device__ __forceinline__ unsigned proj_setup(ProjLds<NW>& P, gptr<const unsigned long long> blk,
                                                unsigned long long pad, unsigned ia, int lane) {
   static_assert(WT <= NW && NW <= 64, "projection words");
   unsigned n = 0;
@@ -173,13 +173,13 @@ __device__ __forceinline__ unsigned proj_setup(ProjLds<NW>& P, const unsigned lo
 // (rows are padded with zero words up to their tier), so the loads are unrolled without guards
 // and all 2*WT of them can be in flight.
 template <int WT>
-__device__ __forceinline__ unsigned and_count(const unsigned long long* blk, unsigned long long pad,
-                                              unsigned sa, unsigned sb,
+__device__ __forceinline__ unsigned and_count(gptr<const unsigned long long> blk,
+                                              unsigned long long pad, unsigned sa, unsigned sb,
                                               unsigned long long (&v)[WT]) {
   unsigned c = 0;
 #pragma unroll
   for (int w = 0; w < WT; ++w) {
-    const unsigned long long* row = blk + (unsigned long long)w * pad;
+    const gptr<const unsigned long long> row = blk + (unsigned long long)w * pad;
     v[w] = row[sa] & row[sb];
   }
 #pragma unroll
@@ -504,13 +504,13 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
   const bool deeper = a.max_len == 0 || (int)depth + 3 <= a.max_len;  // children expandable
   const unsigned nc = m - 1;
   const unsigned long long cpad = roundup16(nc);
-  const unsigned long long* blk = (const unsigned long long*)top.blk;
-  const unsigned long long* ihp = blk + (unsigned long long)WT * top.pad;
+  const gptr<const unsigned long long> blk = as_global_addr<const unsigned long long>(top.blk);
+  const gptr<const unsigned long long> ihp = blk + (unsigned long long)WT * top.pad;
   const unsigned ia = top.s0;
   const unsigned long long ih_a = ihp[ia + vzero()];
   const unsigned long long h_a = top.hash + ih_a;
   constexpr unsigned E = EMIT ? 1u : 0u;
-  const unsigned long long* nwp = ihp + top.pad;  // emit mode: node words
+  const gptr<const unsigned long long> nwp = ihp + top.pad;  // emit mode: node words
   const unsigned long long node_a = E ? uni64(nwp[ia + vzero()] & kDeepNodeMask) : 0ull;
   unsigned wt_out = WT;
   if (WT > 1 && deeper && nc >= 2) {
@@ -524,13 +524,16 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
     const bool act = c0 + lane < nc;
     const unsigned jb = act ? ia + 1 + c0 + lane : ia;
     unsigned long long v[WT];
+    // the candidate's item hash is loaded with its row words (96 % of the candidates survive
+    // at the headline): one round trip per chunk instead of a second one after the count
+    const unsigned long long ih_ld = ihp[jb];
     const unsigned c = and_count<WT>(blk, top.pad, ia + vzero(), jb, v);
     const bool surv = act && c >= a.minsup;
     const unsigned long long mask = __ballot(surv);
     const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
     unsigned long long ih_b = 0;
     if (surv) {
-      ih_b = ihp[jb];
+      ih_b = ih_ld;
       const DigestTerms dt = digest_terms(h_a + ih_b, c);
       acc.dsum += dt.sum;
       acc.dxor ^= dt.xr;
@@ -590,21 +593,22 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
 // uniform)
 template <int WT, int MAXT, bool EMIT>
 __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, WaveState& st,
-                                           WaveLds<MAXT>& L, DeepFrame top, char* stack,
-                                           int lane, WaveAcc& acc) {
+                                           WaveLds<MAXT>& L, DeepFrame top, const DeepFrame& lf,
+                                           char* stack, int lane, WaveAcc& acc) {
   const unsigned long long lanelt = (1ull << lane) - 1ull;
   unsigned long long* cb = (unsigned long long*)(stack + st.mem_top);
   unsigned k = 0, P = 0;
   {
-    // frame f (from the top) is read by lane f: vector loads, then two wave scans
+    // frame f (from the top) came with lane f's registers (the step's one round of frame
+    // loads, k_deep_count), then two wave scans
+    static_assert(kBatchFrames == 64, "one batch frame per lane");
     unsigned fm = 0, fmeta = kSingle;
-    if (lane < kBatchFrames && (unsigned)lane < st.nf) {
-      const DeepFrame* p = fst + (st.nf - 1 - lane);
-      fm = p->m;
-      fmeta = p->meta;
-      if (p->blk != top.blk) fmeta |= kSingle;  // another block: ends the batch
-      L.f_hash[lane] = p->hash;
-      L.f_s0[lane] = p->s0;
+    if ((unsigned)lane < st.nf) {
+      fm = lf.m;
+      fmeta = lf.meta;
+      if (lf.blk != top.blk) fmeta |= kSingle;  // another block: ends the batch
+      L.f_hash[lane] = lf.hash;
+      L.f_s0[lane] = lf.s0;
       L.f_m[lane] = fm;
       L.f_meta[lane] = fmeta;
     }
@@ -655,11 +659,11 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
   }
   __builtin_amdgcn_wave_barrier();
   const unsigned long long cpad = roundup16(P);
-  const unsigned long long* bblk = (const unsigned long long*)top.blk;
+  const gptr<const unsigned long long> bblk = as_global_addr<const unsigned long long>(top.blk);
   const unsigned long long bpad = top.pad;
-  const unsigned long long* ihp = bblk + (unsigned long long)WT * bpad;
+  const gptr<const unsigned long long> ihp = bblk + (unsigned long long)WT * bpad;
   constexpr unsigned E = EMIT ? 1u : 0u;
-  const unsigned long long* nwp = ihp + bpad;  // emit mode: node words
+  const gptr<const unsigned long long> nwp = ihp + bpad;  // emit mode: node words
   unsigned S = 0, gbase = 0;
   for (unsigned c0 = 0; c0 < P; c0 += 64) {
     const unsigned p = c0 + lane;
@@ -677,6 +681,8 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
     gbase += (unsigned)__popcll(gw);
     const unsigned sa = L.f_s0[f] + i, sb = L.f_s0[f] + (act ? j : i);
     unsigned long long v[WT];
+    // item hashes in flight with the row words (see row_step)
+    const unsigned long long ih_la = ihp[sa], ih_lb = ihp[sb];
     const unsigned c = and_count<WT>(bblk, bpad, sa, sb, v);
     const bool surv = act && c >= a.minsup;
     const unsigned long long mask = __ballot(surv);
@@ -686,7 +692,7 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
     const unsigned long long hmask = __ballot(head);
     if (surv) {
       const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
-      const unsigned long long ih_a = ihp[sa], ih_b = ihp[sb];
+      const unsigned long long ih_a = ih_la, ih_b = ih_lb;
       write_row<WT>(cb, cpad, pos, v, ih_b);
       const DigestTerms dt = digest_terms(L.f_hash[f] + ih_a + ih_b, c);
       acc.dsum += dt.sum;
@@ -775,19 +781,19 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
 template <int MAXT, bool EMIT, int T0, int... Ts>
 __device__ __forceinline__ void step_tier(unsigned wt, bool row_mode, const DeepArgs& a,
                                           DeepFrame* fst, WaveState& st, WaveLds<MAXT>& L,
-                                          const DeepFrame& top, char* stack, int lane,
-                                          WaveAcc& acc) {
+                                          const DeepFrame& top, const DeepFrame& lf, char* stack,
+                                          int lane, WaveAcc& acc) {
   if constexpr (T0 <= MAXT) {
     if (wt == (unsigned)T0) {
       if (row_mode)
         row_step<T0, MAXT, EMIT>(a, fst, st, L, top, stack, lane, acc);
       else
-        batch_step<T0, MAXT, EMIT>(a, fst, st, L, top, stack, lane, acc);
+        batch_step<T0, MAXT, EMIT>(a, fst, st, L, top, lf, stack, lane, acc);
       return;
     }
   }
-  if constexpr (sizeof...(Ts) > 0) step_tier<MAXT, EMIT, Ts...>(wt, row_mode, a, fst, st, L, top, stack,
-                                                          lane, acc);
+  if constexpr (sizeof...(Ts) > 0)
+    step_tier<MAXT, EMIT, Ts...>(wt, row_mode, a, fst, st, L, top, lf, stack, lane, acc);
 }
 
 // waves per SIMD the count kernel is compiled for by default (blocks_per_cu may select the other
@@ -924,15 +930,42 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
     const unsigned long long tr_t0 = tr ? wall_clock64() : 0ull;
     if (tr && lane == 0 && tr[1] == 0) tr[1] = tr_t0;
     // ---- run the task ----
+    unsigned steps = 0;
     while (st.nf > 0) {
       __builtin_amdgcn_wave_barrier();
       // bounded: a launch that runs past its deadline gives up (error bit 2) instead of holding
-      // the GPU; the host reports it
-      if (timed_out()) {
+      // the GPU; the host reports it (the clock is read every 32 steps: s_memrealtime is a
+      // scalar-memory round trip the step would otherwise wait for)
+      if ((++steps & 31u) == 0u && timed_out()) {
         failed = true;
         break;
       }
-      const DeepFrame top = load_frame(fst + st.nf - 1, lane);
+      // the top min(nf, 64) frames, lane f holding frame nf-1-f, in ONE round of vector loads:
+      // lane 0's is the top frame, and a batch step takes its frames from these registers (a
+      // separate top-frame load was a dependent round trip of its own every step)
+      DeepFrame lf;
+      lf.blk = 0;
+      lf.hash = 0;
+      lf.pad = 0;
+      lf.s0 = 0;
+      lf.m = 0;
+      lf.meta = kSingle;
+      if ((unsigned)lane < st.nf) {
+        const gptr<const DeepFrame> fp = as_global((const DeepFrame*)fst) + (st.nf - 1 - lane);
+        lf.blk = fp->blk;
+        lf.hash = fp->hash;
+        lf.pad = fp->pad;
+        lf.s0 = fp->s0;
+        lf.m = fp->m;
+        lf.meta = fp->meta;
+      }
+      DeepFrame top;
+      top.blk = lane0_64(lf.blk);
+      top.hash = lane0_64(lf.hash);
+      top.pad = lane0(lf.pad);
+      top.s0 = lane0(lf.s0);
+      top.m = lane0(lf.m);
+      top.meta = lane0(lf.meta);
       const unsigned m = top.m;
       const unsigned wt = meta_width(top.meta);
       const unsigned long long pairs = (unsigned long long)m * (m - 1) / 2;
@@ -981,7 +1014,7 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
         break;
       }
       step_tier<MAXT, EMIT, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64>(wt, row_mode, a, fst, st, L, top,
-                                                               stack, lane, acc);
+                                                               lf, stack, lane, acc);
       free_blocks(L, st);
     }
     if (tr && !failed && lane == 0) {
@@ -1103,7 +1136,7 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
     if (nx == (long long)S) return;  // wave-uniform: nothing to write
     cb = (unsigned long long*)(base + blk_off[i]);
     wt_out = (unsigned)((blk_off[i + 1] - blk_off[i]) / (long long)(8 * cpad)) - 1u - E;
-    if (wt_out < (unsigned)WT) proj_setup<WT>(PL, root, (unsigned long long)Fpad, (unsigned)i, lane);
+    if (wt_out < (unsigned)WT) proj_setup<WT>(PL, as_global(root), (unsigned long long)Fpad, (unsigned)i, lane);
   }
   const bool proj = wt_out < (unsigned)WT;
   const unsigned S0 = S;
@@ -1118,7 +1151,7 @@ __global__ __launch_bounds__(256) void k_deep_root(const unsigned long long* roo
     if (gram != nullptr && __ballot(pre) == 0ull) continue;
     unsigned long long v[WT];
     unsigned c = 0;
-    if (pre) c = and_count<WT>(root, (unsigned long long)Fpad, (unsigned)i + vzero(), (unsigned)jb, v);
+    if (pre) c = and_count<WT>(as_global(root), (unsigned long long)Fpad, (unsigned)i + vzero(), (unsigned)jb, v);
     const bool surv = act && c >= minsup;
     const unsigned long long mask = __ballot(surv);
     if (fill) {
