@@ -1086,6 +1086,11 @@ bool GpuMiner::pair_rows_count(uint32_t* gram, int64_t ld) {
   auto* P = static_cast<kern::PairRows*>(prows_.get());
   const int64_t F = (int64_t)fi_.ids.size();
   kern::PrInput in{d_tx_ptr_, d_items_, n_tx_, n_items_, d_ids_, F, n_cus_, d_fmask_};
+  {  // the frequent items' share of the global supports -> mean kept per transaction
+    double sum = 0;
+    for (uint32_t c : fi_.counts) sum += (double)c;
+    in.kept_per_tx = sum / (double)std::max<int64_t>(global_n_tx_, 1);
+  }
   Comm* c = comm_ ? comm_ : shard_comm_;
   auto wait = [&] {
     if (c) c->wait_stream(s);

@@ -117,6 +117,59 @@ __device__ __forceinline__ void packed_alloc(bool want, uint32_t n, unsigned lon
   *item = (old & kPackMask) + incl - n;
 }
 
+// The same slots from a PER-WAVE pool: a wave reserves rows_res rows and items_res items of the
+// packed counter at a time and hands them out chunk by chunk.  One atomic per 64-transaction chunk
+// on the single counter serialised the 100M-transaction filter: one address takes ~88 atomics per
+// microsecond, 1.56M chunks ~18 ms of its 20.  A chunk that does not fit the rest of the wave's
+// range abandons that tail (rows left zero: the caller zeroes txrec, so they read as empty
+// (0, 0) rows; items never referenced) and reserves a new range; the counter therefore ends past
+// the rows/items actually written, and consumers size by it.
+struct WavePool {
+  unsigned long long r0, r1, i0, i1;
+};
+// reservation sizes: ~16 chunks' rows per atomic, fewer when a wave gets few chunks (so the
+// abandoned tails stay a few % of the output); items from the mean kept per transaction
+struct PoolRes {
+  uint32_t rows, items;
+};
+inline PoolRes pool_res(int64_t n_tx, double kept_per_tx, int64_t waves) {
+  const int64_t chunks = (n_tx + 63) / 64;
+  const int64_t per_wave = std::max<int64_t>(1, chunks / std::max<int64_t>(waves, 1));
+  const int64_t k = std::max<int64_t>(1, std::min<int64_t>(16, per_wave / 4));
+  const double kept = std::max(kept_per_tx, 2.0);
+  PoolRes r;
+  r.rows = (uint32_t)(64 * k);
+  r.items = (uint32_t)std::min<double>(1u << 30, 64.0 * (double)k * kept * 1.25 + 64.0);
+  return r;
+}
+__device__ __forceinline__ void pool_alloc(bool want, uint32_t n, unsigned long long* ctr, int lane,
+                                           WavePool& P, uint32_t rows_res, uint32_t items_res,
+                                           unsigned long long* row, unsigned long long* item) {
+  const unsigned long long m = __ballot(want);
+  uint32_t incl = n;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  const uint32_t tot = __shfl(incl, 63, 64);
+  const uint32_t nr = (uint32_t)__popcll(m);
+  if (m && (P.r0 + nr > P.r1 || P.i0 + tot > P.i1)) {  // wave-uniform
+    const unsigned long long rr = nr > rows_res ? nr : rows_res;
+    const unsigned long long ii = tot > items_res ? tot : items_res;
+    unsigned long long old = 0;
+    if (lane == 0) old = atomicAdd(ctr, (rr << kPackShift) + ii);
+    old = __shfl(old, 0, 64);
+    P.r0 = old >> kPackShift;
+    P.r1 = P.r0 + rr;
+    P.i0 = old & kPackMask;
+    P.i1 = P.i0 + ii;
+  }
+  *row = P.r0 + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+  *item = P.i0 + incl - n;
+  P.r0 += nr;
+  P.i0 += tot;
+}
+
 // Thread per row of a rank CSR (txrec, fit): the ranks r with keep[r], order kept; rows with >=
 // min_keep of them compacted through the packed counter (counts past the capacities as above).
 // A wave takes kRG blocks of 64 rows per reservation (count pass, one atomic, write pass): one
@@ -196,8 +249,9 @@ __global__ __launch_bounds__(256) void k_map_filter(
     const int64_t* __restrict__ tx_ptr, const int32_t* __restrict__ items, int64_t n_tx,
     const int16_t* __restrict__ pr, uint32_t min_keep, uint2* __restrict__ txrec,
     uint16_t* __restrict__ fit, unsigned long long* ctr, unsigned long long tx_cap,
-    unsigned long long nnz_cap, unsigned* err) {
+    unsigned long long nnz_cap, unsigned* err, uint32_t rows_res, uint32_t items_res) {
   const int lane = threadIdx.x & 63;
+  WavePool pool{0, 0, 0, 0};
   for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < n_tx; t0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = t0 + threadIdx.x;
     uint32_t v[kSortRegs];
@@ -236,7 +290,7 @@ __global__ __launch_bounds__(256) void k_map_filter(
     if (dup) atomicOr(err, 2u);
     const bool want = kept >= min_keep && kept <= 65535u;
     unsigned long long ti, off;
-    packed_alloc(want, want ? kept : 0u, ctr, lane, &ti, &off);
+    pool_alloc(want, want ? kept : 0u, ctr, lane, pool, rows_res, items_res, &ti, &off);
     if (want) {
       if (ti < tx_cap && off + kept <= nnz_cap) {
         txrec[ti] = make_uint2((uint32_t)off, kept);
@@ -271,40 +325,63 @@ __global__ __launch_bounds__(256) void k_map_filter(
 // (kMU rows of 64 items in flight).  The chunk's ranks are compacted into a per-wave LDS buffer
 // in CSR order; each lane then sorts its own transaction's run.  Chunks with more frequent
 // entries than the buffer holds take the per-lane path of k_map_filter.
-constexpr int kMW = 8;       // waves per workgroup
+constexpr int kMW = 8;       // waves per workgroup (mask in L2)
+constexpr int kMW16 = 16;    // waves per workgroup (mask in LDS: one workgroup per CU, 4 waves/SIMD)
 constexpr int kMEnt = 1024;  // per-wave entry buffer
+constexpr int kMEnt16 = 768; // (16 waves: the buffers fit next to a 125 KB mask)
 constexpr int kMU = 4;       // 64-item rows of the span scan in flight
-struct MapLds {
-  uint16_t ent[kMEnt];
+template <int ENT>
+struct MapLdsT {
+  uint16_t ent[ENT];
   uint32_t pt[65];
   uint32_t kc[64];
 };
-template <bool LDS_MASK>
-__global__ __launch_bounds__(64 * kMW) void k_map_filter_lds(
+// next chunk's CSR bounds, loaded before the current chunk is scanned (a dependent round trip
+// less per chunk): lane l holds tx_ptr[t0 + l] (l < n), every lane tx_ptr[t0 + n]
+struct ChunkPtr {
+  int64_t p, e;
+  unsigned n;
+};
+__device__ __forceinline__ ChunkPtr load_chunk_ptr(const int64_t* __restrict__ tx_ptr, int64_t c,
+                                                   int64_t nchunks, int64_t n_tx, int lane) {
+  ChunkPtr r{0, 0, 0u};
+  if (c < nchunks) {
+    const int64_t t0 = c * 64;
+    r.n = (unsigned)(n_tx - t0 < 64 ? n_tx - t0 : 64);
+    r.p = tx_ptr[t0 + ((unsigned)lane < r.n ? lane : 0)];
+    r.e = tx_ptr[t0 + r.n];
+  }
+  return r;
+}
+template <bool LDS_MASK, int NW, int ENT>
+__global__ __launch_bounds__(64 * NW) void k_map_filter_lds(
     const int64_t* __restrict__ tx_ptr, const int32_t* __restrict__ items, int64_t n_tx,
     const uint32_t* __restrict__ fmask, int64_t mask_words, const int16_t* __restrict__ pr,
     uint32_t min_keep, uint2* __restrict__ txrec, uint16_t* __restrict__ fit,
     unsigned long long* ctr, unsigned long long tx_cap, unsigned long long nnz_cap,
-    unsigned* err) {
+    unsigned* err, uint32_t rows_res, uint32_t items_res) {
   // LDS_MASK: the mask copied into LDS (one workgroup per CU); else read from L2 (more waves)
+  WavePool pool{0, 0, 0, 0};
   extern __shared__ uint32_t smask_lds[];
-  __shared__ MapLds lds[kMW];
+  __shared__ MapLdsT<ENT> lds[NW];
   if constexpr (LDS_MASK) {
-    for (int64_t i = threadIdx.x; i < mask_words; i += 64 * kMW) smask_lds[i] = fmask[i];
+    for (int64_t i = threadIdx.x; i < mask_words; i += 64 * NW) smask_lds[i] = fmask[i];
     __syncthreads();
   }
   const uint32_t* smask = LDS_MASK ? smask_lds : fmask;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  MapLds& L = lds[w];
+  MapLdsT<ENT>& L = lds[w];
   const unsigned long long lanelt = (1ull << lane) - 1ull;
   const int64_t nchunks = (n_tx + 63) / 64;
-  for (int64_t c = (int64_t)blockIdx.x * kMW + w; c < nchunks; c += (int64_t)gridDim.x * kMW) {
-    const int64_t t0 = c * 64;
-    const unsigned n = (unsigned)(n_tx - t0 < 64 ? n_tx - t0 : 64);
-    const int64_t b0 = tx_ptr[t0];
-    const unsigned span = (unsigned)(tx_ptr[t0 + n] - b0);
-    if ((unsigned)lane < n) L.pt[lane] = (unsigned)(tx_ptr[t0 + lane] - b0);
-    if ((unsigned)lane >= n) L.pt[lane] = span;
+  const int64_t stride = (int64_t)gridDim.x * NW;
+  ChunkPtr nx = load_chunk_ptr(tx_ptr, (int64_t)blockIdx.x * NW + w, nchunks, n_tx, lane);
+  for (int64_t c = (int64_t)blockIdx.x * NW + w; c < nchunks; c += stride) {
+    const ChunkPtr cp = nx;
+    nx = load_chunk_ptr(tx_ptr, c + stride, nchunks, n_tx, lane);
+    const unsigned n = cp.n;
+    const int64_t b0 = (int64_t)__shfl((long long)cp.p, 0, 64);
+    const unsigned span = (unsigned)(cp.e - b0);
+    L.pt[lane] = (unsigned)lane < n ? (unsigned)(cp.p - b0) : span;
     if (lane == 0) L.pt[64] = span;
     L.kc[lane] = 0u;
     __builtin_amdgcn_wave_barrier();
@@ -340,16 +417,25 @@ __global__ __launch_bounds__(64 * kMW) void k_map_filter_lds(
           if (lane >= o) incl += t;
         }
         unsigned e0 = ne + incl - cnt;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (r[e] < 0) continue;
-          const unsigned q = qb + (unsigned)e - lead;  // position in the span
-          unsigned x = 0;  // transaction: the last x with pt[x] <= q
+        if (cnt) {
+          // transaction of the lane's first kept item by ONE binary search (the last x with
+          // pt[x] <= q), the later ones by stepping forward: 4 consecutive items rarely cross
+          // a boundary (a search per kept item was 6 dependent LDS reads each)
+          int ef = 0;
+          while (r[ef] < 0) ++ef;
+          const unsigned qf = qb + (unsigned)ef - lead;
+          unsigned x = 0;
           for (unsigned step = 32; step; step >>= 1)
-            if (L.pt[x + step] <= q) x += step;
-          atomicAdd(&L.kc[x], 1u);
-          if (e0 < (unsigned)kMEnt) L.ent[e0] = (uint16_t)r[e];
-          ++e0;
+            if (L.pt[x + step] <= qf) x += step;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (r[e] < 0) continue;
+            const unsigned q = qb + (unsigned)e - lead;  // position in the span
+            while (x < 63u && L.pt[x + 1] <= q) ++x;
+            atomicAdd(&L.kc[x], 1u);
+            if (e0 < (unsigned)ENT) L.ent[e0] = (uint16_t)r[e];
+            ++e0;
+          }
         }
         ne += __shfl(incl, 63, 64);
       }
@@ -362,7 +448,7 @@ __global__ __launch_bounds__(64 * kMW) void k_map_filter_lds(
       if (lane >= o) incl += u;
     }
     const uint32_t toff = incl - kept;
-    const bool buffered = ne <= (unsigned)kMEnt;
+    const bool buffered = ne <= (unsigned)ENT;
     uint32_t v[kSortRegs];
 #pragma unroll
     for (int q = 0; q < kSortRegs; ++q) v[q] = 0xFFFFFFFFu;
@@ -401,7 +487,7 @@ __global__ __launch_bounds__(64 * kMW) void k_map_filter_lds(
     if (dup) atomicOr(err, 2u);
     const bool want = kept >= min_keep && kept <= 65535u;
     unsigned long long ti, off;
-    packed_alloc(want, want ? kept : 0u, ctr, lane, &ti, &off);
+    pool_alloc(want, want ? kept : 0u, ctr, lane, pool, rows_res, items_res, &ti, &off);
     if (want && ti < tx_cap && off + kept <= nnz_cap) {
       txrec[ti] = make_uint2((uint32_t)off, kept);
       uint16_t* dst = fit + off;

@@ -540,6 +540,8 @@ bool HLevels::run(const HlInput& in, const HlHooks& hk, hipStream_t s, HlStats& 
                        in.ids, F, (const uint8_t*)I.inpair.p, I.pr.p);
     KMLS_HIP(hipGetLastError());
   }
+  const int64_t f_waves = (int64_t)grid_for(in.n_tx, in.n_cus) * 4;
+  const devbuf::PoolRes pres = devbuf::pool_res(in.n_tx, 4.0, f_waves);
   for (int attempt = 0;; ++attempt) {
     I.txrec.need(tx_cap);
     I.fit.need(nnz_cap);
@@ -547,6 +549,8 @@ bool HLevels::run(const HlInput& in, const HlHooks& hk, hipStream_t s, HlStats& 
     nnz_cap = I.fit.cap;
     KMLS_HIP(hipMemsetAsync(I.ctr.p, 0, sizeof(unsigned long long), s));
     KMLS_HIP(hipMemsetAsync(I.err.p, 0, sizeof(unsigned), s));
+    if (in.f_txrec == nullptr)  // (the filter pools' abandoned rows must read as empty)
+      KMLS_HIP(hipMemsetAsync(I.txrec.p, 0, (size_t)tx_cap * sizeof(uint2), s));
     if (in.f_txrec != nullptr) {
       if (in.f_rows > 0)
         hipLaunchKernelGGL(devbuf::k_csr_refilter, dim3(grid_for(in.f_rows, in.n_cus)), dim3(256),
@@ -555,7 +559,7 @@ bool HLevels::run(const HlInput& in, const HlHooks& hk, hipStream_t s, HlStats& 
     } else if (in.n_tx > 0) {
       hipLaunchKernelGGL(devbuf::k_map_filter, dim3(grid_for(in.n_tx, in.n_cus)), dim3(256), 0, s,
                          in.tx_ptr, in.items, in.n_tx, I.pr.p, 3u, I.txrec.p, I.fit.p, I.ctr.p,
-                         tx_cap, nnz_cap, I.err.p);
+                         tx_cap, nnz_cap, I.err.p, pres.rows, pres.items);
     }
     KMLS_HIP(hipGetLastError());
     KMLS_HIP(hipMemcpyAsync(I.h, I.ctr.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -570,9 +574,10 @@ bool HLevels::run(const HlInput& in, const HlHooks& hk, hipStream_t s, HlStats& 
       I.h[1] = nn;
       break;
     }
-    KMLS_CHECK(attempt == 0, "hlevels: filtered CSR sizes grew between passes");
-    tx_cap = nt;
-    nnz_cap = nn;
+    KMLS_CHECK(attempt < 3, "hlevels: filtered CSR sizes grew between passes");
+    const bool pooled = in.f_txrec == nullptr;  // the map filter's tails vary run to run
+    tx_cap = nt + (pooled ? (unsigned long long)f_waves * pres.rows : 0ull);
+    nnz_cap = nn + (pooled ? (unsigned long long)f_waves * pres.items : 0ull);
   }
   const int64_t n_ftx = (int64_t)I.h[0];
   st.n_tx_kept = n_ftx;

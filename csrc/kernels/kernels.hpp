@@ -269,6 +269,7 @@ struct PrInput {
   int64_t F;
   int n_cus;
   const uint32_t* fmask = nullptr;  // frequent-item bit mask (large vocabularies), or null
+  double kept_per_tx = 0.0;  // mean frequent items per transaction (sizes the filter's pools)
 };
 // Item-sharded counting: the ranks' frequent-rank CSRs are all-gathered (every rank then holds
 // every transaction's frequent ranks) and this rank counts only the rows a with a % world == rank

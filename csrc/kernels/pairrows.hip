@@ -196,6 +196,155 @@ __global__ __launch_bounds__(kRowThreads) void k_pl_split(
   (void)gbeg_all;
 }
 
+// ---- staged forms of passes A and B: the same lists, written as contiguous runs ----
+// Pass A and pass B above write every entry to its own scattered address (a thread's pairs one
+// by one; a chunk's entries to the cursors of ~230 rows), ~0.9-1.4 TB/s of partial-line writes
+// at config 5.  The staged forms collect a tile's entries in LDS grouped by destination first,
+// then copy each destination's run out with consecutive threads on consecutive addresses.
+constexpr int kStA = 256;        // pass A: rows (= threads) per tile
+constexpr int kStAEnt = 12288;   // pass A: staged pairs per tile (u32), 48 KB (~37 pairs a row
+                                 // at config 5: two blocks per CU)
+constexpr int kStBThreads = 1024;
+constexpr int kStBEnt = 16384;   // pass B: entries per chunk (u32 staged), 64 KB
+constexpr int kStBRows = 4096;   // pass B: group rows the staged form takes (else the direct form)
+
+__global__ __launch_bounds__(kStA) void k_pl_part_staged(const uint2* __restrict__ txrec,
+                                                          int64_t n_tx,
+                                                          const uint16_t* __restrict__ fit,
+                                                          int64_t F,
+                                                          const uint8_t* __restrict__ grp_g,
+                                                          unsigned long long* __restrict__ gcur,
+                                                          uint32_t* __restrict__ gl, int own_rank,
+                                                          int own_world, int ng) {
+  extern __shared__ uint8_t grp[];  // [F]
+  __shared__ uint32_t cnt[kNGMax], loff[kNGMax + 1], cur[kNGMax];
+  __shared__ unsigned long long gb[kNGMax];
+  __shared__ uint32_t stage[kStAEnt];
+  for (int64_t r = threadIdx.x; r < F; r += kStA) grp[r] = grp_g[r];
+  const int64_t ntiles = (n_tx + kStA - 1) / kStA;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    if ((int)threadIdx.x < ng) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    const int64_t t = tile * kStA + threadIdx.x;
+    uint2 rec = make_uint2(0u, 0u);
+    if (t < n_tx) rec = txrec[t];
+    const uint16_t* it = fit + rec.x;
+    for (uint32_t i = 0; i + 1 < rec.y; ++i)
+      if ((int)(it[i] % (uint32_t)own_world) == own_rank)
+        atomicAdd(&cnt[grp[it[i]]], rec.y - 1u - i);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // one wave: the group reservations and the exclusive scan
+      uint32_t run = 0;
+      for (int g0 = 0; g0 < ng; g0 += 64) {
+        const int g = g0 + (int)threadIdx.x;
+        const uint32_t c = g < ng ? cnt[g] : 0u;
+        if (g < ng) gb[g] = c ? atomicAdd(&gcur[g], (unsigned long long)c) : 0ull;
+        uint32_t incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t u = __shfl_up(incl, o, 64);
+          if ((int)threadIdx.x >= o) incl += u;
+        }
+        if (g < ng) {
+          loff[g] = run + incl - c;
+          cur[g] = run + incl - c;
+        }
+        run += __shfl(incl, 63, 64);
+      }
+      if (threadIdx.x == 0) loff[ng] = run;
+    }
+    __syncthreads();
+    const uint32_t total = loff[ng];
+    const bool staged = total <= (uint32_t)kStAEnt;
+    for (uint32_t i = 0; i + 1 < rec.y; ++i) {
+      const uint32_t a = it[i], n = rec.y - 1u - i;
+      if ((int)(a % (uint32_t)own_world) != own_rank) continue;
+      const uint32_t g = grp[a];
+      const uint32_t p = atomicAdd(&cur[g], n);
+      if (staged) {
+        for (uint32_t j = 0; j < n; ++j) stage[p + j] = (a << 16) | (uint32_t)it[i + 1u + j];
+      } else {  // a tile of very long rows: the direct form for this tile
+        uint32_t* dst = gl + gb[g] + (p - loff[g]);
+        for (uint32_t j = 0; j < n; ++j) dst[j] = (a << 16) | (uint32_t)it[i + 1u + j];
+      }
+    }
+    __syncthreads();
+    if (staged)
+      for (uint32_t k = threadIdx.x; k < total; k += kStA) {
+        const uint32_t v = stage[k];
+        const uint32_t g = grp[v >> 16];
+        gl[gb[g] + (k - loff[g])] = v;
+      }
+    __syncthreads();
+  }
+}
+
+// pass B staged: one chunk of kStBEnt entries of one group's list; the group's rows (<= kStBRows)
+// get LDS counts, an exclusive scan, one global reservation each, and the chunk is staged in row
+// order, then copied out row run by row run.  Dynamic LDS: 3 x rows u32.
+__global__ __launch_bounds__(kStBThreads) void k_pl_split_staged(
+    const uint32_t* __restrict__ gl, const unsigned long long* __restrict__ base,
+    const uint32_t* __restrict__ grow, const uint32_t* __restrict__ gch,
+    uint32_t* __restrict__ rcur, uint16_t* __restrict__ pl, int ng) {
+  extern __shared__ uint32_t rw[];  // loff [rows + 1] | cur [rows] | gpos [rows]
+  __shared__ uint32_t stage[kStBEnt];
+  __shared__ uint32_t wsum[kStBThreads / 64];
+  __shared__ int32_t s_g;
+  if (threadIdx.x == 0) {
+    int g = 0;
+    while (g + 1 < ng && gch[g + 1] <= blockIdx.x) ++g;
+    s_g = g;
+  }
+  __syncthreads();
+  const int g = s_g;
+  const uint32_t r0 = grow[2 * g], r1 = grow[2 * g + 1], nr = r1 - r0;
+  uint32_t* loff = rw;
+  uint32_t* cur = rw + nr + 1;
+  uint32_t* gpos = rw + 2 * nr + 1;
+  const unsigned long long g0 = base[r0], g1 = base[r1];
+  const unsigned long long c0 = g0 + (unsigned long long)(blockIdx.x - gch[g]) * kStBEnt;
+  const unsigned long long c1 = c0 + kStBEnt < g1 ? c0 + kStBEnt : g1;
+  const uint32_t n = (uint32_t)(c1 - c0);
+  for (uint32_t r = threadIdx.x; r < nr; r += kStBThreads) cur[r] = 0u;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += kStBThreads) atomicAdd(&cur[(gl[c0 + i] >> 16) - r0], 1u);
+  __syncthreads();
+  // exclusive scan of the row counts: thread t takes rows [t*per, (t+1)*per)
+  const uint32_t per = (nr + kStBThreads - 1) / kStBThreads;
+  const uint32_t lo = threadIdx.x * per, hi = lo + per < nr ? lo + per : nr;
+  uint32_t sum = 0;
+  for (uint32_t r = lo; r < hi; ++r) sum += cur[r];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t wb = 0;
+  for (int q = 0; q < w; ++q) wb += wsum[q];
+  uint32_t run = wb + incl - sum;
+  for (uint32_t r = lo; r < hi; ++r) {
+    const uint32_t c = cur[r];
+    loff[r] = run;
+    gpos[r] = c ? atomicAdd(&rcur[r0 + r], c) : 0u;  // the row's relative position
+    cur[r] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) loff[nr] = n;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += kStBThreads) {
+    const uint32_t v = gl[c0 + i];
+    stage[atomicAdd(&cur[(v >> 16) - r0], 1u)] = v;
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < n; k += kStBThreads) {
+    const uint32_t v = stage[k];
+    const uint32_t a = v >> 16, r = a - r0;
+    pl[base[a] + gpos[r] + (k - loff[r])] = (uint16_t)(v & 0xFFFFu);
+  }
+}
+
 // all-gathered CSRs (world blocks of cap_tx records / cap_nnz items) -> one CSR: rank q's rows
 // at tbase[q], its items at nbase[q] (record offsets rebased)
 __global__ void k_pr_gather_rows(const uint2* __restrict__ rec_all, int64_t cap_tx,
@@ -339,9 +488,21 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   const bool lds_mask = in.fmask != nullptr && mask_words * 4 <= (128 << 10);
   // (test hook filter_lds=0: the L2-mask instance of the same kernel, at full occupancy)
   const bool mask_in_lds = lds_mask && test_hook("filter_lds", 1) != 0;
+  // (the mask-in-LDS instance: one 16-wave workgroup per CU)
+  auto* const k_lds = devbuf::k_map_filter_lds<true, devbuf::kMW16, devbuf::kMEnt16>;
+  auto* const k_l2 = devbuf::k_map_filter_lds<false, devbuf::kMW, devbuf::kMEnt>;
   if (mask_in_lds && mask_words * 4 > 65536)
-    ok(hipFuncSetAttribute((const void*)devbuf::k_map_filter_lds<true>,
-                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(mask_words * 4)), "attr");
+    ok(hipFuncSetAttribute((const void*)k_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)(mask_words * 4)), "attr");
+  const int64_t chunks = (in.n_tx + 63) / 64;
+  const unsigned gm = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>((chunks + devbuf::kMW - 1) / devbuf::kMW, (int64_t)in.n_cus * 2));
+  const unsigned gm16 = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>((chunks + devbuf::kMW16 - 1) / devbuf::kMW16, (int64_t)in.n_cus));
+  const int64_t waves = lds_mask ? (mask_in_lds ? (int64_t)gm16 * devbuf::kMW16
+                                                : (int64_t)gm * 4 * devbuf::kMW)
+                                 : (int64_t)g * 4;
+  const devbuf::PoolRes pres = devbuf::pool_res(in.n_tx, in.kept_per_tx, waves);
   for (int attempt = 0;; ++attempt) {
     I.txrec.need(tx_cap);
     I.fit.need(nnz_cap);
@@ -349,22 +510,22 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
     nnz_cap = I.fit.cap;
     ok(hipMemsetAsync(I.ctr.p, 0, sizeof(unsigned long long), s), "ctr");
     ok(hipMemsetAsync(I.err.p, 0, sizeof(unsigned), s), "err");
+    // (the pools' abandoned rows must read as empty)
+    ok(hipMemsetAsync(I.txrec.p, 0, (size_t)tx_cap * sizeof(uint2), s), "txrec zero");
     if (lds_mask) {
-      const int64_t chunks = (in.n_tx + 63) / 64;
-      const unsigned gm = (unsigned)std::max<int64_t>(
-          1, std::min<int64_t>((chunks + devbuf::kMW - 1) / devbuf::kMW, (int64_t)in.n_cus * 2));
       if (mask_in_lds)
-        hipLaunchKernelGGL(devbuf::k_map_filter_lds<true>, dim3(gm), dim3(64 * devbuf::kMW),
-                           (size_t)mask_words * 4, s, in.tx_ptr, in.items, in.n_tx, in.fmask,
-                           mask_words, I.pr.p, 2u, I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap,
-                           I.err.p);
+        hipLaunchKernelGGL(k_lds, dim3(gm16), dim3(64 * devbuf::kMW16), (size_t)mask_words * 4,
+                           s, in.tx_ptr, in.items, in.n_tx, in.fmask, mask_words, I.pr.p, 2u,
+                           I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p, pres.rows,
+                           pres.items);
       else
-        hipLaunchKernelGGL(devbuf::k_map_filter_lds<false>, dim3(gm * 4), dim3(64 * devbuf::kMW),
-                           0, s, in.tx_ptr, in.items, in.n_tx, in.fmask, mask_words, I.pr.p, 2u,
-                           I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p);
+        hipLaunchKernelGGL(k_l2, dim3(gm * 4), dim3(64 * devbuf::kMW), 0, s, in.tx_ptr,
+                           in.items, in.n_tx, in.fmask, mask_words, I.pr.p, 2u, I.txrec.p,
+                           I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p, pres.rows, pres.items);
     } else {
       hipLaunchKernelGGL(devbuf::k_map_filter, dim3(g), dim3(256), 0, s, in.tx_ptr, in.items,
-                         in.n_tx, I.pr.p, 2u, I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p);
+                         in.n_tx, I.pr.p, 2u, I.txrec.p, I.fit.p, I.ctr.p, tx_cap, nnz_cap, I.err.p,
+                         pres.rows, pres.items);
     }
     ok(hipGetLastError(), "filter");
     ok(hipMemcpyAsync(I.h, I.ctr.p, 8, hipMemcpyDeviceToHost, s), "rb");
@@ -380,9 +541,10 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
       I.nnz = (int64_t)nn;
       break;
     }
-    KMLS_CHECK(attempt == 0, "pair rows: CSR sizes grew between passes");
-    tx_cap = nt;
-    nnz_cap = nn;
+    // (the pools' tails differ from run to run: leave room for every wave to abandon more)
+    KMLS_CHECK(attempt < 3, "pair rows: CSR sizes grew between passes");
+    tx_cap = nt + (unsigned long long)waves * pres.rows;
+    nnz_cap = nn + (unsigned long long)waves * pres.items;
   }
   if (own_world > 1) {  // item-sharded: every rank's CSR on every rank
     I.gsz.need((size_t)2 * own_world + 2);
@@ -450,34 +612,59 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   // (test hooks pl_groups / pl_chunk: the partition's group count and split chunk)
   const int ng = (int)std::max<long long>(1, std::min<long long>(kNGMax, test_hook("pl_groups", 64)));
   const uint32_t chunk = (uint32_t)std::max<long long>(1024, test_hook("pl_chunk", kChunkDflt));
+  // (test hook pl_staged=0: the direct (unstaged) passes A and B)
+  const bool staged = test_hook("pl_staged", 1) != 0;
+  const uint32_t chunk_b = staged ? (uint32_t)kStBEnt : chunk;
   I.gcur.need(ng);
   I.grow.need(2 * ng);
   I.gch.need(ng + 1);
   I.meta.need(4);
   hipLaunchKernelGGL(k_pl_groups, dim3(1), dim3(1024), 0, s, I.base.p, F, I.grp.p, I.gcur.p,
-                     I.grow.p, I.gch.p, I.meta.p, ng, chunk);
+                     I.grow.p, I.gch.p, I.meta.p, ng, chunk_b);
   ok(hipGetLastError(), "groups");
+  std::vector<uint32_t> grow_h((size_t)2 * ng);
   ok(hipMemcpyAsync(I.h, I.base.p + F, 8, hipMemcpyDeviceToHost, s), "rb");
   ok(hipMemcpyAsync(I.h + 1, I.soff.p + F, 4, hipMemcpyDeviceToHost, s), "rb");
   ok(hipMemcpyAsync(I.h + 2, I.meta.p, 4, hipMemcpyDeviceToHost, s), "rb");
+  ok(hipMemcpyAsync(grow_h.data(), I.grow.p, grow_h.size() * 4, hipMemcpyDeviceToHost, s), "rb");
   wait();
   I.pairs = (int64_t)I.h[0];
   const uint32_t n_sl = (uint32_t)(I.h[1] & 0xFFFFFFFFull);
   const uint32_t n_ch = (uint32_t)(I.h[2] & 0xFFFFFFFFull);
   if (I.pairs == 0) return true;
+  uint32_t max_rows = 0;
+  for (int q = 0; q < ng; ++q) max_rows = std::max(max_rows, grow_h[2 * q + 1] - grow_h[2 * q]);
   // pass A: group lists; pass B: row lists
   I.gl.need((size_t)I.pairs);
   I.pl.need((size_t)I.pairs);
   I.rcur.need((size_t)F);
   ok(hipMemsetAsync(I.rcur.p, 0, (size_t)F * 4, s), "rcur");
-  const int64_t n_pb = (I.n_tx + kPartTx - 1) / kPartTx;
-  hipLaunchKernelGGL(k_pl_part, dim3((unsigned)n_pb), dim3(kPartTx), (size_t)F, s, txrec,
-                     I.n_tx, fit, F, I.grp.p, I.gcur.p, I.gl.p, own_rank, own_world, ng);
+  if (staged && test_hook("pl_staged_a", 0) != 0) {  // (measured slower than the direct pass A
+                                                      // at config 5: 14.8 vs 11.3 ms)
+    const int64_t ntiles = (I.n_tx + kStA - 1) / kStA;
+    const unsigned gA = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)in.n_cus * 2));
+    hipLaunchKernelGGL(k_pl_part_staged, dim3(gA), dim3(kStA), (size_t)F, s, txrec, I.n_tx, fit,
+                       F, I.grp.p, I.gcur.p, I.gl.p, own_rank, own_world, ng);
+  } else {
+    const int64_t n_pb = (I.n_tx + kPartTx - 1) / kPartTx;
+    hipLaunchKernelGGL(k_pl_part, dim3((unsigned)n_pb), dim3(kPartTx), (size_t)F, s, txrec,
+                       I.n_tx, fit, F, I.grp.p, I.gcur.p, I.gl.p, own_rank, own_world, ng);
+  }
   ok(hipGetLastError(), "part");
-  if (n_ch > 0)
-    hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds, s, I.gl.p,
-                       (const unsigned long long*)nullptr, I.base.p, I.grow.p, I.gch.p, I.rcur.p,
-                       I.pl.p, ng, chunk);
+  if (n_ch > 0) {
+    if (staged && max_rows <= (uint32_t)kStBRows)
+      hipLaunchKernelGGL(k_pl_split_staged, dim3(n_ch), dim3(kStBThreads),
+                         (size_t)(3 * max_rows + 1) * 4, s, I.gl.p, I.base.p, I.grow.p, I.gch.p,
+                         I.rcur.p, I.pl.p, ng);
+    else if (staged)  // a group of more rows than the staged form holds: direct, same chunks
+      hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds, s, I.gl.p,
+                         (const unsigned long long*)nullptr, I.base.p, I.grow.p, I.gch.p,
+                         I.rcur.p, I.pl.p, ng, chunk_b);
+    else
+      hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds, s, I.gl.p,
+                         (const unsigned long long*)nullptr, I.base.p, I.grow.p, I.gch.p,
+                         I.rcur.p, I.pl.p, ng, chunk);
+  }
   ok(hipGetLastError(), "split");
   // 3. the rows
   if (n_sl > 0)
