@@ -28,10 +28,17 @@
 #define __launch_bounds__(...)
 #define __shared__ static
 
-struct uint2 {  // HIP's vector type, as far as the shared headers name it
+struct uint2 {  // HIP's vector types, as far as the shared headers name them
   unsigned int x, y;
 };
 inline uint2 make_uint2(unsigned int x, unsigned int y) { return uint2{x, y}; }
+struct alignas(16) ulonglong2 {
+  unsigned long long x, y;
+};
+struct alignas(16) int4 {
+  int x, y, z, w;
+};
+inline int4 make_int4(int x, int y, int z, int w) { return int4{x, y, z, w}; }
 
 struct dim3 {
   unsigned x, y, z;
@@ -63,9 +70,44 @@ struct Wave {
   }
 };
 
+// the workgroup's barrier (__syncthreads): every live thread of the block; a finished thread
+// leaves the count, so the others are not left waiting for it
+struct Block {
+  std::mutex mu;
+  std::condition_variable cv;
+  int alive = 0;
+  int arrived = 0;
+  uint64_t gen = 0;
+  std::vector<unsigned char> dyn;  // the launch's dynamic LDS (extern __shared__)
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const uint64_t g = gen;
+    if (++arrived >= alive) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return gen != g; })) {
+      std::fprintf(stderr, "emu: block deadlock (a __syncthreads not reached by every thread)\n");
+      std::abort();
+    }
+  }
+  void leave() {
+    std::unique_lock<std::mutex> lk(mu);
+    alive -= 1;
+    if (arrived > 0 && arrived >= alive) {
+      arrived = 0;
+      ++gen;
+    }
+    cv.notify_all();
+  }
+};
+
 struct Lane {
   int lane = 0;
   Wave* wave = nullptr;
+  Block* block = nullptr;
   dim3 tidx;
 };
 
@@ -101,6 +143,16 @@ inline void wave_barrier() { tl->wave->barrier(); }
 
 inline unsigned __shfl(unsigned v, int src, int = 64) { return (unsigned)emu::xchg(v, src); }
 inline int __shfl(int v, int src, int = 64) { return (int)emu::xchg((uint32_t)v, src); }
+inline long long __shfl(long long v, int src, int = 64) {
+  return (long long)emu::xchg((uint64_t)v, src);
+}
+inline unsigned long long __shfl(unsigned long long v, int src, int = 64) {
+  return emu::xchg(v, src);
+}
+inline void __syncthreads() { emu::tl->block->barrier(); }
+namespace emu {
+inline void* dyn_lds() { return tl->block->dyn.data(); }
+}  // namespace emu
 inline unsigned __shfl_up(unsigned v, unsigned delta, int = 64) {
   const int l = emu::tl->lane;
   const int src = l - (int)delta;
@@ -119,6 +171,11 @@ inline unsigned long long __ballot(int pred) {
   w->barrier();
   return m;
 }
+// HIP's device min/max (the kernels call them unqualified)
+template <typename A, typename B>
+inline auto min(A a, B b) -> decltype(a < b ? a : b) { return a < b ? a : b; }
+template <typename A, typename B>
+inline auto max(A a, B b) -> decltype(a > b ? a : b) { return a > b ? a : b; }
 inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
 inline int __popc(unsigned x) { return __builtin_popcount(x); }
 inline unsigned long long wall_clock64() {
@@ -134,6 +191,12 @@ template <typename T> inline T atomicExch(T* p, T v) { return __atomic_exchange_
 template <typename T> inline T atomicCAS(T* p, T cmp, T v) {
   __atomic_compare_exchange_n(p, &cmp, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
   return cmp;  // the old value (== the expected one on success)
+}
+template <typename T> inline T atomicMax(T* p, T v) {
+  T old = __atomic_load_n(p, __ATOMIC_SEQ_CST);
+  while (v > old && !__atomic_compare_exchange_n(p, &old, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
+  }
+  return old;
 }
 template <typename T> inline T atomicMin(T* p, T v) {
   T old = __atomic_load_n(p, __ATOMIC_SEQ_CST);
@@ -170,6 +233,10 @@ inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t = nullptr
   return hipSuccess;
 }
 inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+constexpr unsigned hipHostMallocDefault = 0, hipHostMallocMapped = 2, hipHostMallocCoherent = 4;
+enum hipFuncAttribute { hipFuncAttributeMaxDynamicSharedMemorySize = 8 };
+inline hipError_t hipFuncSetAttribute(const void*, hipFuncAttribute, int) { return hipSuccess; }
+inline hipError_t hipGetLastError() { return hipSuccess; }
 inline hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) {
   *v = 100000;  // kHz of wall_clock64 above
   return hipSuccess;
@@ -177,15 +244,20 @@ inline hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) {
 
 // one workgroup at a time, every thread a host thread, grouped into waves of 64
 template <typename K, typename... Args>
-inline void hipLaunchKernelGGL(K kernel, dim3 grid, dim3 block, size_t, hipStream_t, Args... args) {
+inline void hipLaunchKernelGGL(K kernel, dim3 grid, dim3 block, size_t shared, hipStream_t,
+                               Args... args) {
   emu::g_grid_dim = grid;
   emu::g_block_dim = block;
   const unsigned nt = block.x;
   const unsigned nw = (nt + 63) / 64;
+  for (unsigned by = 0; by < grid.y; ++by)
   for (unsigned bx = 0; bx < grid.x; ++bx) {
-    emu::g_block_idx = dim3(bx);
+    emu::g_block_idx = dim3(bx, by);
     std::vector<emu::Wave> waves(nw);
     for (unsigned w = 0; w < nw; ++w) waves[w].nlanes = (int)std::min(64u, nt - 64 * w);
+    emu::Block blk;
+    blk.alive = (int)nt;
+    blk.dyn.assign(std::max<size_t>(shared, 16), (unsigned char)0xCD);  // LDS starts as garbage
     std::vector<std::thread> th;
     th.reserve(nt);
     for (unsigned t = 0; t < nt; ++t) {
@@ -193,18 +265,22 @@ inline void hipLaunchKernelGGL(K kernel, dim3 grid, dim3 block, size_t, hipStrea
         emu::Lane me;
         me.lane = (int)(t & 63);
         me.wave = &waves[t / 64];
+        me.block = &blk;
         me.tidx = dim3(t);
         emu::tl = &me;
         kernel(args...);
         // a finished lane keeps answering its wave's barriers until every lane is done
         emu::Wave* w = me.wave;
-        std::unique_lock<std::mutex> lk(w->mu);
-        w->nlanes -= 1;
-        if (w->arrived >= w->nlanes && w->arrived > 0) {
-          w->arrived = 0;
-          ++w->gen;
+        {
+          std::unique_lock<std::mutex> lk(w->mu);
+          w->nlanes -= 1;
+          if (w->arrived >= w->nlanes && w->arrived > 0) {
+            w->arrived = 0;
+            ++w->gen;
+          }
+          w->cv.notify_all();
         }
-        w->cv.notify_all();
+        blk.leave();
       });
     }
     for (auto& x : th) x.join();

@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#define KMLS_DYN_LDS(T, name) T* name = (T*)emu::dyn_lds()
+
 namespace kmls {
 namespace kern {
 

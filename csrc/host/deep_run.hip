@@ -1,5 +1,6 @@
 // Device orchestration of the count-only deep miner (see deep_run.hpp and kernels/deep.hip).
 #include "deep_run.hpp"
+#include "kmls/hooks.hpp"
 
 #include <algorithm>
 #include <chrono>
@@ -21,7 +22,7 @@ namespace gpu {
 
 DeepBufs::~DeepBufs() {
   (void)hipSetDevice(device);
-  for (void* p : {(void*)stacks, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)req, (void*)inbox, (void*)inbox_state, (void*)heap[0],
+  for (void* p : {(void*)stacks, (void*)stacks0, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)req, (void*)inbox, (void*)inbox_state, (void*)heap[0],
                   (void*)heap[1], (void*)root, (void*)ctl, (void*)d_red, (void*)d_xor,
                   (void*)d_m, (void*)d_off, (void*)d_toff, (void*)d_cost, (void*)d_order,
                   (void*)d_trace, (void*)d_ticks, (void*)n_parent, (void*)n_item,
@@ -95,15 +96,23 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       opt.stack_mb > 0 ? (size_t)opt.stack_mb << 20 : env_bytes_mb("KMLS_DEEP_STACK_MB", 4),
       4 * kern::deep_row_block_bytes(W, F, E)) + 69 * 128;
   const int fcap = std::max(4096, kern::deep_min_fcap()) + 36;  // 4132 x 32 B = 1033 lines
-  if (b.waves < waves || b.stack_bytes < stack_need || b.fcap < fcap) {
+  // the dense first stack segment (KMLS_TEST_HOOKS deep_seg0_kb=0: none), its stride skewed
+  // off a power of two like the others
+  const long long seg0_kb = test_hook("deep_seg0_kb", 256);
+  const size_t seg0 = seg0_kb > 0 ? ((size_t)seg0_kb << 10) + 69 * 128 : 0;
+  if (b.waves < waves || b.stack_bytes < stack_need || b.fcap < fcap || b.seg0 != seg0) {
     if (b.stacks) KMLS_HIP(hipFree(b.stacks));
+    if (b.stacks0) KMLS_HIP(hipFree(b.stacks0));
     if (b.fstacks) KMLS_HIP(hipFree(b.fstacks));
     b.stacks = nullptr;
+    b.stacks0 = nullptr;
     b.fstacks = nullptr;
     KMLS_HIP(hipMalloc((void**)&b.stacks, (size_t)waves * stack_need));
+    if (seg0) KMLS_HIP(hipMalloc((void**)&b.stacks0, (size_t)waves * seg0));
     KMLS_HIP(hipMalloc((void**)&b.fstacks, (size_t)waves * fcap * sizeof(kern::DeepFrame)));
     b.waves = waves;
     b.stack_bytes = stack_need;
+    b.seg0 = seg0;
     b.fcap = fcap;
   }
   const int64_t q_cap = (int64_t)(env_bytes_mb("KMLS_DEEP_QUEUE_MB", 512) / sizeof(kern::DeepFrame));
@@ -348,6 +357,8 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   kern::DeepArgs a{};
   a.stacks = b.stacks;
   a.stack_bytes = b.stack_bytes;
+  a.stacks0 = b.stacks0;
+  a.seg0 = b.seg0;
   a.fstacks = b.fstacks;
   a.fcap = b.fcap;
   a.ctl = b.ctl;

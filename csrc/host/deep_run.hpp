@@ -20,6 +20,8 @@ struct DeepBufs {
   int device = 0;
   char* stacks = nullptr;
   size_t stack_bytes = 0;  // per wave
+  char* stacks0 = nullptr;  // per wave: the dense first segment of its stack (kern::DeepArgs)
+  size_t seg0 = 0;
   int64_t waves = 0;
   kern::DeepFrame* fstacks = nullptr;
   int fcap = 0;

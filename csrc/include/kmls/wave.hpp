@@ -4,6 +4,10 @@
 
 #include <hip/hip_runtime.h>
 
+// Dynamic LDS of a kernel (`extern __shared__ T name[]`); the CPU wave emulator maps it to the
+// launch's dynamic-LDS buffer.
+#define KMLS_DYN_LDS(T, name) extern __shared__ T name[]
+
 namespace kmls {
 namespace kern {
 

@@ -293,6 +293,24 @@ __device__ __forceinline__ void put_node(const DeepArgs& a, unsigned long long i
   }
 }
 
+// A wave's block stack in two parts: the first seg0 bytes in a region where the waves' segments
+// are packed next to each other, the rest in a 4 MiB-scale region of its own.  A wave works near
+// the bottom of its stack almost all the time, so the hot blocks of all waves sit in a few hundred
+// 2 MiB pages instead of one page per wave (4096 waves: more pages than the TLBs map).
+struct WaveStack {
+  char* s0;  // this wave's dense segment (n0 bytes)
+  char* s1;  // the rest of its stack
+  unsigned long long n0;
+};
+// the block of `bytes` at the stack top; no block straddles the two parts (one that would goes to
+// the start of the second part: the skipped tail returns when the block below it is freed)
+__device__ __forceinline__ unsigned long long* stack_block(const WaveStack& ws,
+                                                           unsigned long long& mem_top,
+                                                           unsigned long long bytes) {
+  if (mem_top < ws.n0 && mem_top + bytes > ws.n0) mem_top = ws.n0;
+  return (unsigned long long*)(mem_top < ws.n0 ? ws.s0 + mem_top : ws.s1 + (mem_top - ws.n0));
+}
+
 struct WaveAcc {
   unsigned long long dsum, dxor, cands, chunks, budget_used;
 };
@@ -496,8 +514,8 @@ __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst,
 // The child class (prefix P ∪ {a}) is projected onto row a when that narrows its tier.
 template <int WT, int MAXT, bool EMIT>
 __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, WaveState& st,
-                                         WaveLds<MAXT>& L, DeepFrame top, char* stack, int lane,
-                                         WaveAcc& acc) {
+                                         WaveLds<MAXT>& L, DeepFrame top, const WaveStack& stack,
+                                         int lane, WaveAcc& acc) {
   const unsigned long long lanelt = (1ull << lane) - 1ull;
   const unsigned m = top.m;
   const unsigned depth = meta_depth(top.meta);  // prefix size: members are depth+1 itemsets
@@ -518,7 +536,8 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
     wt_out = tier_of((s + 63) / 64);
   }
   const bool proj = wt_out < (unsigned)WT;
-  unsigned long long* cb = (unsigned long long*)(stack + st.mem_top);
+  unsigned long long* cb =
+      stack_block(stack, st.mem_top, (unsigned long long)(wt_out + 1 + E) * cpad * 8ull);
   unsigned S = 0;
   for (unsigned c0 = 0; c0 < nc; c0 += 64) {
     const bool act = c0 + lane < nc;
@@ -594,9 +613,9 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
 template <int WT, int MAXT, bool EMIT>
 __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, WaveState& st,
                                            WaveLds<MAXT>& L, DeepFrame top, const DeepFrame& lf,
-                                           char* stack, int lane, WaveAcc& acc) {
+                                           const WaveStack& stack, int lane, WaveAcc& acc) {
   const unsigned long long lanelt = (1ull << lane) - 1ull;
-  unsigned long long* cb = (unsigned long long*)(stack + st.mem_top);
+  unsigned long long* cb = nullptr;  // (the child block: placed once P is known, below)
   unsigned k = 0, P = 0;
   {
     // frame f (from the top) came with lane f's registers (the step's one round of frame
@@ -659,6 +678,7 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
   }
   __builtin_amdgcn_wave_barrier();
   const unsigned long long cpad = roundup16(P);
+  cb = stack_block(stack, st.mem_top, (unsigned long long)(WT + 1 + (EMIT ? 1u : 0u)) * cpad * 8ull);
   const gptr<const unsigned long long> bblk = as_global_addr<const unsigned long long>(top.blk);
   const unsigned long long bpad = top.pad;
   const gptr<const unsigned long long> ihp = bblk + (unsigned long long)WT * bpad;
@@ -781,8 +801,8 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
 template <int MAXT, bool EMIT, int T0, int... Ts>
 __device__ __forceinline__ void step_tier(unsigned wt, bool row_mode, const DeepArgs& a,
                                           DeepFrame* fst, WaveState& st, WaveLds<MAXT>& L,
-                                          const DeepFrame& top, const DeepFrame& lf, char* stack,
-                                          int lane, WaveAcc& acc) {
+                                          const DeepFrame& top, const DeepFrame& lf,
+                                          const WaveStack& stack, int lane, WaveAcc& acc) {
   if constexpr (T0 <= MAXT) {
     if (wt == (unsigned)T0) {
       if (row_mode)
@@ -811,7 +831,8 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
   WaveLds<MAXT>& L = lds[wid];
   const unsigned long long gw = (unsigned long long)blockIdx.x * kWaves + wid;
   DeepFrame* fst = a.fstacks + gw * (unsigned long long)a.fcap;
-  char* stack = a.stacks + gw * a.stack_bytes;
+  const WaveStack stack{a.stacks0 ? a.stacks0 + gw * a.seg0 : nullptr,
+                        a.stacks + gw * a.stack_bytes, a.stacks0 ? a.seg0 : 0ull};
 
   for (int d = lane; d < 64; d += 64) L.depth_cnt[d] = 0;
   WaveAcc acc{0, 0, 0, 0, 0};
@@ -972,7 +993,9 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
       const bool row_mode = (top.meta & kSingle) || pairs > (unsigned long long)kCap;
       const unsigned long long need =
           (unsigned long long)(wt + 1 + E) * roundup16(row_mode ? m : kCap) * 8ull;
-      if (st.mem_top + need > a.stack_bytes || st.nf + kCap + 2 > (unsigned)a.fcap ||
+      const unsigned long long top_at =  // (a block never straddles the two stack parts)
+          (st.mem_top < stack.n0 && st.mem_top + need > stack.n0) ? stack.n0 : st.mem_top;
+      if (top_at + need > stack.n0 + a.stack_bytes || st.nf + kCap + 2 > (unsigned)a.fcap ||
           st.nb + 1 >= (unsigned)kBStack || (!a.steal && acc.budget_used >= a.budget)) {
         if (spill_frames<MAXT, EMIT>(a, fst, st, L, lane, false, st.nf,
                                      a.split_q ? (long long)task_ticket : -1ll) < 0)

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <kmls/wave.hpp>
 
 #include <algorithm>
 #include <cstdint>
@@ -329,7 +330,7 @@ constexpr int kMW = 8;       // waves per workgroup (mask in L2)
 constexpr int kMW16 = 16;    // waves per workgroup (mask in LDS: one workgroup per CU, 4 waves/SIMD)
 constexpr int kMEnt = 1024;  // per-wave entry buffer
 constexpr int kMEnt16 = 768; // (16 waves: the buffers fit next to a 125 KB mask)
-constexpr int kMU = 4;       // 64-item rows of the span scan in flight
+constexpr int kMU = 8;       // 64-item rows of the span scan in flight (a whole chunk, mostly)
 template <int ENT>
 struct MapLdsT {
   uint16_t ent[ENT];
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(64 * NW) void k_map_filter_lds(
     unsigned* err, uint32_t rows_res, uint32_t items_res) {
   // LDS_MASK: the mask copied into LDS (one workgroup per CU); else read from L2 (more waves)
   WavePool pool{0, 0, 0, 0};
-  extern __shared__ uint32_t smask_lds[];
+  KMLS_DYN_LDS(uint32_t, smask_lds);
   __shared__ MapLdsT<ENT> lds[NW];
   if constexpr (LDS_MASK) {
     for (int64_t i = threadIdx.x; i < mask_words; i += 64 * NW) smask_lds[i] = fmask[i];

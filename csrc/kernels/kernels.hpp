@@ -46,6 +46,8 @@ struct DeepArgs {
   unsigned long long heap_cap;
   char* stacks;                   // per wave: stack_bytes of blocks
   unsigned long long stack_bytes;
+  char* stacks0;                  // per wave: the first seg0 bytes of its stack, densely packed
+  unsigned long long seg0;        // (0: none; see deep.hip WaveStack)
   DeepFrame* fstacks;             // per wave: fcap frames
   int fcap;
   DeepCtl* ctl;

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kRowThreads) void k_pl_hist(const uint2* __restrict
                                                          int64_t n_wg,
                                                          unsigned long long* __restrict__ hist,
                                                          int own_rank, int own_world) {
-  extern __shared__ uint32_t h[];
+  KMLS_DYN_LDS(uint32_t, h);
   for (int64_t i = threadIdx.x; i < F; i += kRowThreads) h[i] = 0u;
   __syncthreads();
   int64_t t0, t1;
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(kPartTx) void k_pl_part(const uint2* __restrict__ t
                                                      unsigned long long* __restrict__ gcur,
                                                      uint32_t* __restrict__ gl, int own_rank,
                                                      int own_world, int ng) {
-  extern __shared__ uint8_t grp[];  // [F]
+  KMLS_DYN_LDS(uint8_t, grp);  // [F]
   __shared__ uint32_t cnt[kNGMax];
   __shared__ unsigned long long gb[kNGMax];
   for (int64_t r = threadIdx.x; r < F; r += kPartTx) grp[r] = grp_g[r];
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kRowThreads) void k_pl_split(
     const unsigned long long* __restrict__ base, const uint32_t* __restrict__ grow,
     const uint32_t* __restrict__ gch, uint32_t* __restrict__ rcur, uint16_t* __restrict__ pl,
     int ng, uint32_t chunk) {
-  extern __shared__ uint32_t rc[];  // [rows of the group]
+  KMLS_DYN_LDS(uint32_t, rc);  // [rows of the group]
   __shared__ int32_t s_g;
   if (threadIdx.x == 0) {
     int g = 0;
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kStA) void k_pl_part_staged(const uint2* __restrict
                                                           unsigned long long* __restrict__ gcur,
                                                           uint32_t* __restrict__ gl, int own_rank,
                                                           int own_world, int ng) {
-  extern __shared__ uint8_t grp[];  // [F]
+  KMLS_DYN_LDS(uint8_t, grp);  // [F]
   __shared__ uint32_t cnt[kNGMax], loff[kNGMax + 1], cur[kNGMax];
   __shared__ unsigned long long gb[kNGMax];
   __shared__ uint32_t stage[kStAEnt];
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kStBThreads) void k_pl_split_staged(
     const uint32_t* __restrict__ gl, const unsigned long long* __restrict__ base,
     const uint32_t* __restrict__ grow, const uint32_t* __restrict__ gch,
     uint32_t* __restrict__ rcur, uint16_t* __restrict__ pl, int ng) {
-  extern __shared__ uint32_t rw[];  // loff [rows + 1] | cur [rows] | gpos [rows]
+  KMLS_DYN_LDS(uint32_t, rw);  // loff [rows + 1] | cur [rows] | gpos [rows]
   __shared__ uint32_t stage[kStBEnt];
   __shared__ uint32_t wsum[kStBThreads / 64];
   __shared__ int32_t s_g;
@@ -392,7 +392,7 @@ __global__ void k_pl_slices(const unsigned long long* __restrict__ off, int64_t 
 __global__ __launch_bounds__(kRowThreads) void k_pl_rows(
     const uint32_t* __restrict__ slice_off, int64_t F, const unsigned long long* __restrict__ base,
     const uint16_t* __restrict__ pl, uint32_t* __restrict__ gram, int64_t ld) {
-  extern __shared__ uint32_t acc[];
+  KMLS_DYN_LDS(uint32_t, acc);
   __shared__ int32_t s_r;
   if (threadIdx.x == 0) {  // the rank whose slices hold this block: last r with slice_off[r] <= b
     const uint32_t b = blockIdx.x;

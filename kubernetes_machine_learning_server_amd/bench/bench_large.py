@@ -226,6 +226,8 @@ def rule_map_main(args) -> int:
     ptr, items = N.synth_transactions(T, I, shape.mean_len, shape.n_genres, shape.genre_affinity,
                                       0.85, args.seed, 0, lo, hi)
     gen_s = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(dev)[0]  # every allocation (native hipMalloc included)
     t0 = time.perf_counter()
     rm = DistRuleMap(ptr, items, I, T, args.min_support, device=dev)
     load_s = time.perf_counter() - t0
@@ -264,10 +266,16 @@ def rule_map_main(args) -> int:
                                        if "bm" in rm.ops.held else 0.0),
                 "bitmap_gb_replicated_equiv": round(F * Ws * 8 * world / 1e9, 1),
                 "gram_gb": round(F * F * 4 / 1e9, 2),
-                "hbm_gb_allocated_rank0": round(torch.cuda.max_memory_allocated() / 1e9, 1)})
+                # device memory the rule map holds after its steps (its buffers are grow-only and
+                # kept across calls, so this is the high-water mark): hipMemGetInfo before the
+                # miner existed minus now — native hipMalloc buffers included, unlike torch's
+                # allocator statistics
+                "hbm_gb_used_rank0": round((free0 - torch.cuda.mem_get_info(dev)[0]) / 1e9, 2),
+                "hbm_gb_torch_allocator_rank0": round(torch.cuda.max_memory_allocated() / 1e9, 2)})
     if rank == 0:
         out.update({"rule_map_entries": int(r["nnz"]), "rule_map_status": int(r["status"]),
-                    "frequent_pairs": int(r["nnz"]) // 2, "phases_ms_rank0": r["phases_ms"]})
+                    "frequent_pairs": int(r["nnz"]) // 2,
+                    "phase_wall_ms_rank0": r["phases_ms"]})
     # 1. each rank's shard gram rows re-counted independently: by the popcount bit-GEMM over the
     # shard's bitmaps when the gram came from them, by the host from the shard's CSR when the
     # gram was counted horizontally (cooc.hip: no bitmaps exist)

@@ -190,6 +190,15 @@ class _Gpu:
         self.held.clear()
 
 
+def _deltas_ms(ph: Dict[str, float]) -> Dict[str, float]:
+    """Cumulative phase-end marks (s) -> each phase's own duration (ms)."""
+    out, prev = {}, 0.0
+    for k, v in ph.items():
+        out[k] = round((v - prev) * 1e3, 3)
+        prev = v
+    return out
+
+
 class _Cpu:
     def __init__(self, rm: "DistRuleMap", tx_ptr, items):
         self.N = native.load()
@@ -322,6 +331,8 @@ class DistRuleMap:
                 rows = ops.gram_rows(self, F)
                 if ck is not None and ck.enabled:
                     ck.save(self._phase("rows"), rows=ops.rows_to_host(rows))
+            if hasattr(ops, "stream"):  # the phase's device work ends inside the phase
+                ops.stream.synchronize()
             ph["encode_gram_reduce_scatter"] = time.perf_counter() - t0
             loc = ops.rows_csr(self, rows, F, r0, nrows, minsup)
             if ck is not None and ck.enabled:
@@ -353,7 +364,8 @@ class DistRuleMap:
         out.update(ids=ids, fcounts=fcounts, minsup=minsup, n_frequent_items=F,
                    status=status, resumed_from_phase=lvl,
                    level2_method=getattr(ops, "method", "gram"),
-                   phases_ms={k: round(v * 1e3, 3) for k, v in ph.items()})
+                   # wall time of each phase (device work of a phase waited for at its end)
+                   phases_ms=_deltas_ms(ph))
         return out
 
     def release(self) -> None:
