@@ -96,9 +96,9 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       opt.stack_mb > 0 ? (size_t)opt.stack_mb << 20 : env_bytes_mb("KMLS_DEEP_STACK_MB", 4),
       4 * kern::deep_row_block_bytes(W, F, E)) + 69 * 128;
   const int fcap = std::max(4096, kern::deep_min_fcap()) + 36;  // 4132 x 32 B = 1033 lines
-  // the dense first stack segment (KMLS_TEST_HOOKS deep_seg0_kb=0: none), its stride skewed
+  // the dense first stack segment (off by default; KMLS_TEST_HOOKS deep_seg0_kb=<KB> turns it on), its stride skewed
   // off a power of two like the others
-  const long long seg0_kb = test_hook("deep_seg0_kb", 256);
+  const long long seg0_kb = test_hook("deep_seg0_kb", 0);  // (measured: 256 KB segments 29.4-30.2 ms vs 28.9-29.4 without, profiles/r6i_*)
   const size_t seg0 = seg0_kb > 0 ? ((size_t)seg0_kb << 10) + 69 * 128 : 0;
   if (b.waves < waves || b.stack_bytes < stack_need || b.fcap < fcap || b.seg0 != seg0) {
     if (b.stacks) KMLS_HIP(hipFree(b.stacks));

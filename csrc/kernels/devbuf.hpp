@@ -330,7 +330,7 @@ constexpr int kMW = 8;       // waves per workgroup (mask in L2)
 constexpr int kMW16 = 16;    // waves per workgroup (mask in LDS: one workgroup per CU, 4 waves/SIMD)
 constexpr int kMEnt = 1024;  // per-wave entry buffer
 constexpr int kMEnt16 = 768; // (16 waves: the buffers fit next to a 125 KB mask)
-constexpr int kMU = 8;       // 64-item rows of the span scan in flight (a whole chunk, mostly)
+constexpr int kMU = 4;       // 64-item rows of the span scan in flight (8: no faster at config 5)
 template <int ENT>
 struct MapLdsT {
   uint16_t ent[ENT];
