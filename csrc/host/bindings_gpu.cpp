@@ -293,6 +293,12 @@ void register_gpu_bindings(py::module_& m) {
         py::gil_scoped_release nogil;
         return g.select(counts.data(), n_tx, ms);
       })
+      .def("select_device", [](gpu::GpuMiner& g, uintptr_t d_counts, int64_t n_tx, double ms) {
+        // the selection from supports already on the device (an all-reduced histogram): no
+        // copies of the vocabulary's counts either way
+        py::gil_scoped_release nogil;
+        return g.select_device((const uint32_t*)d_counts, n_tx, ms, nullptr);
+      }, py::arg("counts"), py::arg("n_tx"), py::arg("min_support"))
       .def("use_frequent_subset", [](gpu::GpuMiner& g, I64 keep) {
         py::gil_scoped_release nogil;
         g.use_frequent_subset(keep.data(), (int64_t)keep.size());

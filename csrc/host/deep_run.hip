@@ -366,6 +366,8 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   a.minsup = in.minsup;
   a.max_len = in.max_len;
   a.split_min = opt.split_min;
+  a.ask_mask = (unsigned)test_hook("deep_ask_mask", 7);
+  a.sleep_n = (unsigned)test_hook("deep_sleep_n", 1u << 30);
   a.out_cap = b.q_cap;
   a.heap_cap = b.heap_cap;
   a.trace = nullptr;

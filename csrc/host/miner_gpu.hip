@@ -883,19 +883,30 @@ void GpuMiner::item_support(uintptr_t counts_dev) {
 
 // Device-side selection from device-resident (all-reduced) supports: only the F frequent ids
 // and counts cross PCIe (kern::select_large), not the n_items support vector.
+// The selection's device tables (rank_of / ids over the whole vocabulary, the frequent bit mask of
+// a large one), allocated once per vocabulary size: a reselection (every rule-map step) frees and
+// allocates nothing — each hipFree waits for the whole device.
+void GpuMiner::ensure_select_bufs() {
+  const int64_t I = std::max<int64_t>(n_items_, 1);
+  if (sel_cap_ == I) return;
+  for (void* p : {(void*)d_rank_of_, (void*)d_ids_, (void*)d_fmask_, (void*)d_fgroup_, (void*)d_c2r_})
+    if (p) KMLS_HIP(hipFree(p));
+  d_fmask_ = nullptr;
+  d_fgroup_ = nullptr;
+  d_c2r_ = nullptr;
+  KMLS_HIP(hipMalloc((void**)&d_rank_of_, (size_t)I * sizeof(int32_t)));
+  KMLS_HIP(hipMalloc((void**)&d_ids_, (size_t)I * sizeof(int32_t)));
+  if (n_items_ >= (1 << 16)) KMLS_HIP(hipMalloc((void**)&d_fmask_, (size_t)(I + 31) / 32 * 4));
+  sel_cap_ = I;
+}
+
 int64_t GpuMiner::select_device(const uint32_t* d_counts, int64_t global_n_tx, double min_support,
                                 Comm* comm) {
   hipStream_t s = (hipStream_t)stream_;
   ++sel_gen_;
   global_n_tx_ = global_n_tx;
   const int64_t I = std::max<int64_t>(n_items_, 1);
-  if (d_rank_of_) KMLS_HIP(hipFree(d_rank_of_));
-  if (d_ids_) KMLS_HIP(hipFree(d_ids_));
-  if (d_fmask_) KMLS_HIP(hipFree(d_fmask_));
-  d_fmask_ = nullptr;
-  KMLS_HIP(hipMalloc((void**)&d_rank_of_, (size_t)I * sizeof(int32_t)));
-  KMLS_HIP(hipMalloc((void**)&d_ids_, (size_t)I * sizeof(int32_t)));
-  if (n_items_ >= (1 << 16)) KMLS_HIP(hipMalloc((void**)&d_fmask_, (size_t)(I + 31) / 32 * 4));
+  ensure_select_bufs();
   const size_t mark = arena_->mark();
   const size_t tb = kern::select_large_temp_bytes(I);
   void* tmp = arena_->push(tb);
@@ -913,12 +924,11 @@ int64_t GpuMiner::select_device(const uint32_t* d_counts, int64_t global_n_tx, d
     KMLS_HIP(hipMemcpyAsync(fi_.ids.data(), d_ids_, (size_t)F * 4, hipMemcpyDeviceToHost, s));
     KMLS_HIP(hipMemcpyAsync(fi_.counts.data(), d_fc, (size_t)F * 4, hipMemcpyDeviceToHost, s));
   }
-  KMLS_HIP(hipStreamSynchronize(s));
-  arena_->pop_to(mark);
-  fi_.rank_of.assign((size_t)n_items_, -1);
-  for (int64_t r = 0; r < F; ++r) fi_.rank_of[(size_t)fi_.ids[(size_t)r]] = (int32_t)r;
+  // (the encode tables below run on this stream after the copies; one sync at their end)
+  fi_.rank_of.clear();  // the device holds it (d_rank_of_); no host reader of a device selection
   fi_.minsup2 = level2_threshold((uint64_t)global_n_tx, min_support);
-  build_encode_tables(F);
+  build_encode_tables(F);  // syncs the stream: the copies above are complete
+  arena_->pop_to(mark);
   sel_ids_ = fi_.ids;
   sel_counts_ = fi_.counts;
   return F;
@@ -927,15 +937,16 @@ int64_t GpuMiner::select_device(const uint32_t* d_counts, int64_t global_n_tx, d
 // Encode lookup tables (kern::frequent_groups) for the selection just made; small vocabularies
 // or wide frequent sets keep the mask + rank gathers.
 void GpuMiner::build_encode_tables(int64_t F) {
-  if (d_fgroup_) KMLS_HIP(hipFree(d_fgroup_));
-  if (d_c2r_) KMLS_HIP(hipFree(d_c2r_));
-  d_fgroup_ = nullptr;
-  d_c2r_ = nullptr;
-  if (!d_fmask_ || F <= 0 || F > kern::kEncodeGroupMaxF) return;
+  encode_tables_ = false;
+  if (!d_fmask_ || F <= 0 || F > kern::kEncodeGroupMaxF) {
+    KMLS_HIP(hipStreamSynchronize((hipStream_t)stream_));
+    return;
+  }
   hipStream_t s = (hipStream_t)stream_;
   const int64_t G = (n_items_ + 31) / 32;
-  KMLS_HIP(hipMalloc((void**)&d_fgroup_, (size_t)G * 8));
-  KMLS_HIP(hipMalloc((void**)&d_c2r_, (size_t)F * 4));
+  if (!d_fgroup_) KMLS_HIP(hipMalloc((void**)&d_fgroup_, (size_t)G * 8));  // (freed with d_fmask_)
+  if (!d_c2r_) KMLS_HIP(hipMalloc((void**)&d_c2r_, (size_t)kern::kEncodeGroupMaxF * 4));
+  encode_tables_ = true;
   const size_t mark = arena_->mark();
   const size_t tb = kern::frequent_groups_temp_bytes(n_items_);
   void* tmp = arena_->push(tb);
@@ -950,19 +961,14 @@ int64_t GpuMiner::select(const uint32_t* global_counts, int64_t global_n_tx, dou
   ++sel_gen_;
   global_n_tx_ = global_n_tx;
   fi_ = select_frequent(global_counts, n_items_, (uint64_t)global_n_tx, min_support);
-  if (d_rank_of_) KMLS_HIP(hipFree(d_rank_of_));
-  if (d_ids_) KMLS_HIP(hipFree(d_ids_));
-  if (d_fmask_) KMLS_HIP(hipFree(d_fmask_));
-  d_fmask_ = nullptr;
-  if (n_items_ >= (1 << 16)) {  // frequent-item bit mask for the encode gather (kernels.hpp)
-    std::vector<uint32_t> mask((size_t)(n_items_ + 31) / 32, 0u);
+  ensure_select_bufs();
+  std::vector<uint32_t> mask;
+  if (d_fmask_) {  // frequent-item bit mask for the encode gather (kernels.hpp)
+    mask.assign((size_t)(n_items_ + 31) / 32, 0u);
     for (int32_t id : fi_.ids) mask[(size_t)id >> 5] |= 1u << (id & 31);
-    KMLS_HIP(hipMalloc((void**)&d_fmask_, mask.size() * sizeof(uint32_t)));
     KMLS_HIP(hipMemcpyAsync(d_fmask_, mask.data(), mask.size() * sizeof(uint32_t),
                             hipMemcpyHostToDevice, s));
   }
-  KMLS_HIP(hipMalloc((void**)&d_rank_of_, (size_t)std::max<int64_t>(n_items_, 1) * sizeof(int32_t)));
-  KMLS_HIP(hipMalloc((void**)&d_ids_, std::max<size_t>(fi_.ids.size(), 1) * sizeof(int32_t)));
   KMLS_HIP(hipMemcpyAsync(d_rank_of_, fi_.rank_of.data(), (size_t)n_items_ * sizeof(int32_t),
                           hipMemcpyHostToDevice, s));
   if (!fi_.ids.empty())
@@ -1011,8 +1017,9 @@ bool GpuMiner::encode_bitmaps(uintptr_t bm_dev, int64_t Wp_total, int64_t word_o
   const uint32_t* fmask = d_fmask_;
   if (tiled && n_tx_ >= (1 << 16) &&
       kern::encode_bitmap_tiled(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev,
-                                Wp_total, word_off, F, (hipStream_t)stream_, fmask, d_fgroup_,
-                                d_c2r_))
+                                Wp_total, word_off, F, (hipStream_t)stream_, fmask,
+                                encode_tables_ ? d_fgroup_ : nullptr,
+                                encode_tables_ ? d_c2r_ : nullptr))
     return true;
   kern::encode_bitmap(d_tx_ptr_, d_items_, n_tx_, d_rank_of_, (uint64_t*)bm_dev, Wp_total,
                       word_off, (hipStream_t)stream_, fmask);

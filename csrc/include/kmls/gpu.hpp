@@ -384,7 +384,10 @@ class GpuMiner {
   uint32_t* d_fmask_ = nullptr;  // frequent-item bit mask (large vocabularies, select())
   unsigned long long* d_fgroup_ = nullptr;  // encode tables (kern::frequent_groups)
   int32_t* d_c2r_ = nullptr;
-  void build_encode_tables(int64_t F);
+  void build_encode_tables(int64_t F);  // syncs the stream
+  void ensure_select_bufs();
+  int64_t sel_cap_ = 0;           // vocabulary size the selection tables above are allocated for
+  bool encode_tables_ = false;    // d_fgroup_ / d_c2r_ hold the current selection's tables
   int32_t* d_ids_ = nullptr;
   uint64_t* d_own_bm_ = nullptr;  // single-GPU bitmap buffer
   size_t own_bm_bytes_ = 0;

@@ -557,7 +557,7 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
       acc.dsum += dt.sum;
       acc.dxor ^= dt.xr;
     }
-    if (deeper && nc >= 2) {  // (one candidate: never a child class of >= 2 members)
+    if (deeper) {
       if (proj) {
         write_proj<WT>(cb, cpad, pos, surv, v, L.proj, wt_out, ih_b);
       } else if (surv) {
@@ -570,7 +570,7 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
         const unsigned long long id = nb0 + (unsigned long long)__popcll(mask & lanelt);
         const unsigned long long nw_b = nwp[jb];
         put_node(a, id, node_a, (unsigned)(nw_b >> 40), c, depth + 2);
-        if (deeper && nc >= 2) cb[(unsigned long long)(wt_out + 1) * cpad + pos] = ((nw_b >> 40) << 40) | id;
+        if (deeper) cb[(unsigned long long)(wt_out + 1) * cpad + pos] = ((nw_b >> 40) << 40) | id;
       }
     }
     S += (unsigned)__popcll(mask);
@@ -684,8 +684,6 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
   const gptr<const unsigned long long> ihp = bblk + (unsigned long long)WT * bpad;
   constexpr unsigned E = EMIT ? 1u : 0u;
   const gptr<const unsigned long long> nwp = ihp + bpad;  // emit mode: node words
-  // the batch's frames are siblings of one block: one depth, one max_len decision
-  const bool deeper_b = a.max_len == 0 || (int)meta_depth(top.meta) + 3 <= a.max_len;
   unsigned S = 0, gbase = 0;
   for (unsigned c0 = 0; c0 < P; c0 += 64) {
     const unsigned p = c0 + lane;
@@ -693,13 +691,12 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
     // group of pair p (row-major pairs: group (f, i) holds (i, j), j > i): starts up to p
     const unsigned long long gw = uni64(L.g_flag[(c0 >> 6) + vzero()]);
     const unsigned g = gbase + (unsigned)__popcll(gw & ((2ull << lane) - 1ull)) - 1u;
-    unsigned f = 0, i = 0, j = 0, gsz = 0;
+    unsigned f = 0, i = 0, j = 0;
     if (act) {
       const unsigned fi = L.g_fi[g];
       f = fi >> 8;
       i = fi & 0xffu;
       j = i + 1 + (p - L.g_pos[g]);
-      gsz = L.f_m[f] - 1u - i;  // pairs of member group (f, i)
     }
     gbase += (unsigned)__popcll(gw);
     const unsigned sa = L.f_s0[f] + i, sb = L.f_s0[f] + (act ? j : i);
@@ -713,14 +710,10 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
     // group once, instead of one LDS atomic per survivor on the same address
     const bool head = act && (lane == 0 || ((gw >> lane) & 1ull));
     const unsigned long long hmask = __ballot(head);
-    // a group of ONE pair never becomes a child frame (< 2 members), nor does any group past
-    // max_len: its survivor is counted but its row is never read, so it is not written (one
-    // such group per frame: ~10 % of the rows at the headline)
-    const bool row_needed = gsz >= 2u && deeper_b;
     if (surv) {
       const unsigned pos = S + (unsigned)__popcll(mask & lanelt);
       const unsigned long long ih_a = ih_la, ih_b = ih_lb;
-      if (row_needed) write_row<WT>(cb, cpad, pos, v, ih_b);
+      write_row<WT>(cb, cpad, pos, v, ih_b);
       const DigestTerms dt = digest_terms(L.f_hash[f] + ih_a + ih_b, c);
       acc.dsum += dt.sum;
       acc.dxor ^= dt.xr;
@@ -733,7 +726,7 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
         const unsigned long long nw_b = nwp[sb];
         put_node(a, id, nwp[sa] & kDeepNodeMask, (unsigned)(nw_b >> 40), c,
                  meta_depth(top.meta) + 2);
-        if (row_needed) cb[(unsigned long long)(WT + 1) * cpad + pos] = ((nw_b >> 40) << 40) | id;
+        cb[(unsigned long long)(WT + 1) * cpad + pos] = ((nw_b >> 40) << 40) | id;
       }
     }
     if (head) {
@@ -921,7 +914,7 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
         if (!inbox_open) {  // not published yet: open the inbox, then start asking
           if (lane == 0) st_agent(&a.inbox_state[gw], kOpen);
           inbox_open = true;
-        } else if ((n & 7) == 1) {
+        } else if ((n & a.ask_mask) == 1) {
           if (lane == 0) {
             if (victim != (unsigned)gw)
               atomicExch(&a.req[victim], ((unsigned long long)a.epoch << 32) | (unsigned long long)(gw + 1));
@@ -929,7 +922,7 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
           }
         }
         if (timed_out()) { failed = true; break; }
-        wait_short(n);
+        wait_short(n < a.sleep_n ? n : a.sleep_n);
       }
       if (done || failed) break;
       task_from_inbox = from_inbox;

@@ -67,6 +67,9 @@ struct DeepArgs {
   long long nwaves;
   unsigned epoch;                 // < 2^30
   int steal;
+  unsigned ask_mask;              // a waiting wave asks a victim every (ask_mask + 1) polls
+  unsigned sleep_n;               // poll backoff: s_sleep 2 / 16 / 127 from poll 0 / 4 / 16 on,
+                                  // the poll count capped at sleep_n
   int steal_eager;                // tests: 1 = bottom frame to the queue at every check,
                                   // 2 = hand-off to the partner wave (gw ^ 1) whenever it waits
   // optional instrumentation (nullptr = off): per wave [kDeepTraceWords] words (launch start,

@@ -120,8 +120,9 @@ class _Gpu:
     def set_tie_rank(self, tie):
         self.g.set_tie_rank(np.ascontiguousarray(tie, np.int32))
 
-    def supports(self, rm: "DistRuleMap") -> np.ndarray:
-        """Global per-item supports: the shard histogram, all-reduced."""
+    def supports(self, rm: "DistRuleMap"):
+        """Global per-item supports: the shard histogram, all-reduced — left on the device (the
+        selection reads them there; a checkpoint copies them out)."""
         with torch.cuda.stream(self.stream):
             cnt = self.buf("cnt", (rm.n_items,), torch.int32)
             cnt.zero_()
@@ -130,10 +131,23 @@ class _Gpu:
                 self.comm.all_reduce(cnt.data_ptr(), cnt.data_ptr(), rm.n_items, "u32", False,
                                      self.s)
                 self.comm.wait_stream(self.s)
-            return cnt.cpu().numpy().view(np.uint32).copy()
+            return cnt
 
-    def select(self, rm: "DistRuleMap", counts: np.ndarray):
-        F = self.g.select(np.ascontiguousarray(counts, np.uint32), rm.n_tx, rm.min_support)
+    def counts_to_host(self, counts) -> np.ndarray:
+        self.stream.synchronize()
+        return counts.cpu().numpy().view(np.uint32).copy()
+
+    def select(self, rm: "DistRuleMap", counts):
+        """The selection on the device (``select_device``): no 4 MB count / rank-table copies and
+        no host scan of the 1M-item vocabulary per step.  Counts restored from a checkpoint are
+        uploaded and take the same path, so a resumed step ranks the items identically."""
+        if isinstance(counts, np.ndarray):
+            with torch.cuda.stream(self.stream):
+                cnt = self.buf("cnt", (rm.n_items,), torch.int32)
+                cnt.copy_(torch.from_numpy(np.ascontiguousarray(counts, np.uint32).view(np.int32)))
+            counts = cnt
+        with torch.cuda.stream(self.stream):
+            F = self.g.select_device(counts.data_ptr(), rm.n_tx, rm.min_support)
         ids, fcounts, minsup = self.g.frequent()
         return F, np.asarray(ids), np.asarray(fcounts), int(minsup)
 
@@ -214,6 +228,9 @@ class _Cpu:
 
     def set_tie_rank(self, tie):
         self.tie = np.asarray(tie, np.int64)
+
+    def counts_to_host(self, counts) -> np.ndarray:
+        return np.asarray(counts, np.uint32)
 
     def supports(self, rm: "DistRuleMap") -> np.ndarray:
         cnt = np.bincount(self.items, minlength=rm.n_items).astype(np.uint32)
@@ -314,7 +331,7 @@ class DistRuleMap:
         else:
             counts = ops.supports(self)
             if ck is not None and ck.enabled and self.rank == 0:
-                ck.save("rulemap_supports", counts=counts)
+                ck.save("rulemap_supports", counts=ops.counts_to_host(counts))
         ph["supports_allreduce"] = time.perf_counter() - t0
         F, ids, fcounts, minsup = ops.select(self, counts)
         ops.ids = ids
