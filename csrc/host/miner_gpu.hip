@@ -1084,7 +1084,8 @@ bool GpuMiner::pair_rows_ok(int64_t F) const {
     const char* e = std::getenv("KMLS_PAIR_ROWS");
     return e ? std::atoll(e) : 1ll;
   }();
-  return test_hook("pair_rows", env_dflt) != 0 && F >= 2 && F <= 32768 && !subset_active();
+  return test_hook("pair_rows", env_dflt) != 0 && F >= 2 && F <= kern::kSparseMaxF &&
+         !subset_active();
 }
 
 bool GpuMiner::pair_rows_count(uint32_t* gram, int64_t ld) {
@@ -1188,7 +1189,7 @@ bool GpuMiner::hlevels_plan(const MineConfig& cfg, int64_t F, int64_t Wp, Comm* 
     return e ? std::atoll(e) : 1ll;
   }();
   bool want = test_hook("hlevels", env_dflt) != 0 && cfg.level2_gram && F >= 2 &&
-              F <= 32768 && Wp >= 1024 && test_hook("cooc", 1) != 0 && !subset_active();
+              F <= kern::kSparseMaxF && Wp >= 1024 && test_hook("cooc", 1) != 0 && !subset_active();
   if (want && pair_rows_ok(F)) {
     // the row count has no per-transaction bound: a sampled pair estimate feeds the cost model
     // (a full statistics pass cost as much as a tenth of the config-3 step)
@@ -1589,7 +1590,7 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
     int64_t* d_len = (int64_t*)arena_->push((F + 1) * sizeof(int64_t));
     KMLS_HIP(hipMemcpyAsync(d_len, root_len.data(), (F + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
     // level 2 through the bit-GEMM (LDS-tiled, 64x64 tiles) when the dense F x F fits
-    if (F <= 32768 && cfg.level2_gram) {
+    if (F <= kern::kSparseMaxF && cfg.level2_gram) {
       // tx-DP: room for world row blocks of `per` rows (the reduce-scatter's send layout)
       const int cw = comm_ ? comm_->world() : 1;
       const int64_t per = (F + cw - 1) / cw;
@@ -2405,6 +2406,15 @@ GpuMineResult GpuMiner::mine_txdp(Comm* comm, int64_t global_n_tx, const MineCon
     encode_bitmaps_fresh(d_own_bm_, F, Wp);
   }
   KMLS_HIP(hipEventRecord(e2.e, s));
+  // the dense level-2 gram (mine_bitmaps) lives in the arena: a default-sized arena grows ahead
+  // of it — every rank computes the same F, so no rank re-runs alone inside a collective (at
+  // 60k frequent items the gram alone is 14.4 GB, past the 8 GB first guess)
+  if (cfg.level2_gram && F >= 2 && F <= kern::kSparseMaxF) {
+    const int cw = comm ? comm->world() : 1;
+    const size_t gram = (size_t)((F + cw - 1) / cw * cw) * (size_t)F * sizeof(uint32_t);
+    const size_t want = gram + gram / 4 + ((size_t)256 << 20);
+    if (arena_->capacity() < want) grow_arena(want);
+  }
   // 4. level loop with all-reduced candidate counts
   comm_ = comm;
   gram_csr_ok_ = true;
@@ -2447,7 +2457,7 @@ GpuMineResult GpuMiner::mine_shard(Comm* comm, int64_t global_n_tx, const MineCo
   const int64_t F = txdp_select(comm, global_n_tx, cfg, support_tiles);
   const int64_t Wp = words_local();
   // only the row form counts complete pairs from the all-gathered CSR (pair_rows_count's PrShard);
-  // without it (KMLS_PAIR_ROWS=0, F > 32768) every rank declines and the caller falls back
+  // without it (KMLS_PAIR_ROWS=0, F > 65535) every rank declines and the caller falls back
   *declined = !hlevels_plan(cfg, F, Wp, comm, /*need_rows=*/true);
   KMLS_HIP(hipEventRecord(e1.e, s));
   if (*declined) return GpuMineResult{};

@@ -89,12 +89,15 @@ __device__ __forceinline__ unsigned long long wave_alloc(bool want, unsigned lon
   return base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-// item id -> rank (16-bit, F <= 32768) for the ranks with keep[r] != 0 (keep == nullptr: all);
-// the map starts at -1 (memset 0xFF)
+// item id -> rank (unsigned 16-bit, F <= kMaxRank16 + 1) for the ranks with keep[r] != 0
+// (keep == nullptr: all); the map starts at kNoRank16 (memset 0xFF)
+constexpr uint32_t kNoRank16 = 0xFFFFu;
+constexpr int64_t kMaxF16 = 65535;  // ranks 0 .. 65534; 0xFFFF marks an item without one
+__device__ __forceinline__ int rank16(uint16_t v) { return v == kNoRank16 ? -1 : (int)v; }
 __global__ void k_rank_map(const int32_t* __restrict__ ids, int64_t F, const uint8_t* __restrict__ keep,
-                           int16_t* __restrict__ pr) {
+                           uint16_t* __restrict__ pr) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < F && (keep == nullptr || keep[r])) pr[ids[r]] = (int16_t)r;
+  if (r < F && (keep == nullptr || keep[r])) pr[ids[r]] = (uint16_t)r;
 }
 
 // Slots of a compacted CSR from ONE packed counter (transactions << 36 | items): a wave's rows
@@ -248,7 +251,7 @@ constexpr int kFU = 4;         // items read per step, their gathers in flight t
 // re-run with the exact sizes.  err |= 1: a row kept > 65535 items; |= 2: a row holds an item twice.
 __global__ __launch_bounds__(256) void k_map_filter(
     const int64_t* __restrict__ tx_ptr, const int32_t* __restrict__ items, int64_t n_tx,
-    const int16_t* __restrict__ pr, uint32_t min_keep, uint2* __restrict__ txrec,
+    const uint16_t* __restrict__ pr, uint32_t min_keep, uint2* __restrict__ txrec,
     uint16_t* __restrict__ fit, unsigned long long* ctr, unsigned long long tx_cap,
     unsigned long long nnz_cap, unsigned* err, uint32_t rows_res, uint32_t items_res) {
   const int lane = threadIdx.x & 63;
@@ -269,7 +272,7 @@ __global__ __launch_bounds__(256) void k_map_filter(
         for (int u = 0; u < kFU; ++u) it[u] = p0 + u < e ? items[p0 + u] : -1;
         int32_t r[kFU];
 #pragma unroll
-        for (int u = 0; u < kFU; ++u) r[u] = it[u] >= 0 ? (int32_t)pr[it[u]] : -1;
+        for (int u = 0; u < kFU; ++u) r[u] = it[u] >= 0 ? rank16(pr[it[u]]) : -1;
 #pragma unroll
         for (int u = 0; u < kFU; ++u) {
           if (r[u] < 0) continue;
@@ -303,7 +306,7 @@ __global__ __launch_bounds__(256) void k_map_filter(
         } else {  // long row: write, then insertion-sort in place (rare)
           uint32_t n = 0;
           for (int64_t p = s; p < e; ++p) {
-            const int32_t r = pr[items[p]];
+            const int32_t r = rank16(pr[items[p]]);
             if (r < 0) continue;
             const uint16_t x = (uint16_t)r;
             uint32_t j = n++;
@@ -357,7 +360,7 @@ __device__ __forceinline__ ChunkPtr load_chunk_ptr(const int64_t* __restrict__ t
 template <bool LDS_MASK, int NW, int ENT>
 __global__ __launch_bounds__(64 * NW) void k_map_filter_lds(
     const int64_t* __restrict__ tx_ptr, const int32_t* __restrict__ items, int64_t n_tx,
-    const uint32_t* __restrict__ fmask, int64_t mask_words, const int16_t* __restrict__ pr,
+    const uint32_t* __restrict__ fmask, int64_t mask_words, const uint16_t* __restrict__ pr,
     uint32_t min_keep, uint2* __restrict__ txrec, uint16_t* __restrict__ fit,
     unsigned long long* ctr, unsigned long long tx_cap, unsigned long long nnz_cap,
     unsigned* err, uint32_t rows_res, uint32_t items_res) {
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(64 * NW) void k_map_filter_lds(
         for (int e = 0; e < 4; ++e) {
           const unsigned q = qb + (unsigned)e;
           const int x = iv[e];
-          r[e] = (q >= lead && q < end && x >= 0 && ((smask[x >> 5] >> (x & 31)) & 1u)) ? (int)pr[x] : -1;
+          r[e] = (q >= lead && q < end && x >= 0 && ((smask[x >> 5] >> (x & 31)) & 1u)) ? rank16(pr[x]) : -1;
         }
         // the 4 items of a lane are consecutive: ranks in CSR order = lane-major, item-minor
         const unsigned cnt = (r[0] >= 0) + (r[1] >= 0) + (r[2] >= 0) + (r[3] >= 0);

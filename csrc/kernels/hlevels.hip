@@ -454,7 +454,7 @@ unsigned grid_for(int64_t n, int n_cus) {
 
 struct HLevels::Impl {
   Buf<uint8_t> inpair;
-  Buf<int16_t> pr;  // item -> pair-item rank
+  Buf<uint16_t> pr;  // item -> pair-item rank
   Buf<uint32_t> row_cnt, row_off;
   Buf<uint32_t> lv_par[2], lv_item[2], lv_end[2];
   Buf<uint32_t> c_par, c_item, c_cnt, c_n, c_off, flag, sidx;
@@ -492,7 +492,7 @@ bool HLevels::run(const HlInput& in, const HlHooks& hk, hipStream_t s, HlStats& 
   const int64_t F = in.F;
   st = HlStats{};
   if (F < 2 || in.max_len == 1) return true;
-  KMLS_CHECK(F <= 32768, "hlevels: item ranks are 16-bit (signed)");
+  KMLS_CHECK(F <= kSparseMaxF, "hlevels: item ranks are 16-bit (0xFFFF: none)");
   // ---- level 2: frequent pairs from the gram ----
   I.row_cnt.need((size_t)F + 1);
   I.row_off.need((size_t)F + 1);

@@ -266,6 +266,9 @@ void cooc_count(const int64_t* tx_ptr, const int32_t* items, int64_t n_tx, const
                 const uint32_t* fmask, int64_t F, uint32_t* gram, int64_t ld, unsigned* err,
                 int n_cus, hipStream_t s);
 // ---- level-2 pair counts row by row in LDS (pairrows.hip) ----
+// The sparse (horizontal) path keeps item ranks in 16 bits: ranks 0 .. 65534, 0xFFFF = none
+// (devbuf::rank16), pair entries packed as (a << 16 | b)
+constexpr int64_t kSparseMaxF = 65535;
 struct PrInput {
   const int64_t* tx_ptr;  // this rank's CSR (rebased)
   const int32_t* items;

@@ -58,20 +58,28 @@ __global__ __launch_bounds__(kRowThreads) void k_pl_hist(const uint2* __restrict
                                                          const uint16_t* __restrict__ fit, int64_t F,
                                                          int64_t n_wg,
                                                          unsigned long long* __restrict__ hist,
-                                                         int own_rank, int own_world) {
+                                                         int own_rank, int own_world,
+                                                         uint32_t r_lo, uint32_t r_hi) {
+  // ranks [r_lo, r_hi) only: the LDS counters of a window (past ~40k ranks a full table no
+  // longer fits the 160 KB of LDS; the caller launches one window after another)
   KMLS_DYN_LDS(uint32_t, h);
-  for (int64_t i = threadIdx.x; i < F; i += kRowThreads) h[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < r_hi - r_lo; i += kRowThreads) h[i] = 0u;
   __syncthreads();
   int64_t t0, t1;
   block_rows(n_tx, t0, t1);
   for (int64_t t = t0 + threadIdx.x; t < t1; t += kRowThreads) {
     const uint2 rec = txrec[t];
     const uint16_t* it = fit + rec.x;
-    for (uint32_t i = 0; i + 1 < rec.y; ++i)
-      if ((int)(it[i] % (uint32_t)own_world) == own_rank) atomicAdd(&h[it[i]], rec.y - 1u - i);
+    for (uint32_t i = 0; i + 1 < rec.y; ++i) {
+      const uint32_t a = it[i];
+      if (a >= r_lo && a < r_hi && (int)(a % (uint32_t)own_world) == own_rank)
+        atomicAdd(&h[a - r_lo], rec.y - 1u - i);
+    }
   }
   __syncthreads();
-  for (int64_t r = threadIdx.x; r < F; r += kRowThreads) hist[r * n_wg + blockIdx.x] = h[r];
+  for (uint32_t r = threadIdx.x; r < r_hi - r_lo; r += kRowThreads)
+    hist[(int64_t)(r_lo + r) * n_wg + blockIdx.x] = h[r];
+  (void)F;
 }
 
 // Group table and split chunks from the scanned row bases (one block): row r's group =
@@ -205,6 +213,8 @@ constexpr int kStA = 256;        // pass A: rows (= threads) per tile
 constexpr int kStAEnt = 12288;   // pass A: staged pairs per tile (u32), 48 KB (~37 pairs a row
                                  // at config 5: two blocks per CU)
 constexpr int kStBThreads = 1024;
+constexpr int64_t kRankWindow = 32768;  // LDS counters of one hist / row window (128 KB)
+constexpr int64_t kMaxDynLds = 160 * 1024;  // a workgroup's LDS on gfx950
 constexpr int kStBEnt = 16384;   // pass B: entries per chunk (u32 staged), 64 KB
 constexpr int kStBRows = 4096;   // pass B: group rows the staged form takes (else the direct form)
 
@@ -391,7 +401,9 @@ __global__ void k_pl_slices(const unsigned long long* __restrict__ off, int64_t 
 
 __global__ __launch_bounds__(kRowThreads) void k_pl_rows(
     const uint32_t* __restrict__ slice_off, int64_t F, const unsigned long long* __restrict__ base,
-    const uint16_t* __restrict__ pl, uint32_t* __restrict__ gram, int64_t ld) {
+    const uint16_t* __restrict__ pl, uint32_t* __restrict__ gram, int64_t ld, uint32_t c_lo,
+    uint32_t c_hi) {
+  // columns [c_lo, c_hi) of every row (one LDS window per launch when F x 4 bytes pass the LDS)
   KMLS_DYN_LDS(uint32_t, acc);
   __shared__ int32_t s_r;
   if (threadIdx.x == 0) {  // the rank whose slices hold this block: last r with slice_off[r] <= b
@@ -403,28 +415,38 @@ __global__ __launch_bounds__(kRowThreads) void k_pl_rows(
     }
     s_r = (int32_t)lo;
   }
-  for (int64_t i = threadIdx.x; i < F; i += kRowThreads) acc[i] = 0u;
   __syncthreads();
   const uint32_t r = (uint32_t)s_r;
+  const uint32_t y0 = r + 1 > c_lo ? r + 1 : c_lo;  // this row's columns in the window
+  if (y0 >= c_hi) return;                             // (uniform: the whole block leaves)
+  for (uint32_t i = threadIdx.x; i < c_hi - c_lo; i += kRowThreads) acc[i] = 0u;
+  __syncthreads();
   const uint32_t k = blockIdx.x - slice_off[r];
   const uint32_t nsl = slice_off[r + 1] - slice_off[r];
   const unsigned long long b0 = base[r] + (unsigned long long)k * kSlice;
   const unsigned long long b1 = min(b0 + kSlice, base[r + 1]);
-  for (unsigned long long i = b0 + threadIdx.x; i < b1; i += kRowThreads) atomicAdd(&acc[pl[i]], 1u);
+  if (c_lo == 0 && c_hi >= (uint32_t)F) {
+    for (unsigned long long i = b0 + threadIdx.x; i < b1; i += kRowThreads) atomicAdd(&acc[pl[i]], 1u);
+  } else {
+    for (unsigned long long i = b0 + threadIdx.x; i < b1; i += kRowThreads) {
+      const uint32_t b = pl[i];
+      if (b >= c_lo && b < c_hi) atomicAdd(&acc[b - c_lo], 1u);
+    }
+  }
   __syncthreads();
   uint32_t* row = gram + (int64_t)r * ld;
   if (nsl == 1) {
-    for (int64_t y = r + 1 + threadIdx.x; y < F; y += kRowThreads) row[y] = acc[y];
+    for (uint32_t y = y0 + threadIdx.x; y < c_hi; y += kRowThreads) row[y] = acc[y - c_lo];
   } else {
-    for (int64_t y = r + 1 + threadIdx.x; y < F; y += kRowThreads)
-      if (acc[y]) atomicAdd(&row[y], acc[y]);
+    for (uint32_t y = y0 + threadIdx.x; y < c_hi; y += kRowThreads)
+      if (acc[y - c_lo]) atomicAdd(&row[y], acc[y - c_lo]);
   }
 }
 
 }  // namespace
 
 struct PairRows::Impl {
-  Buf<int16_t> pr;
+  Buf<uint16_t> pr;
   Buf<uint2> txrec;
   Buf<uint16_t> fit;
   Buf<unsigned long long> hist, hoff, base;
@@ -458,13 +480,15 @@ int64_t PairRows::n_rows() const { return p_->n_tx; }
 int64_t PairRows::nnz() const { return p_->nnz; }
 int64_t PairRows::pairs() const { return p_->pairs; }
 
-size_t PairRows::lds_bytes(int64_t F) { return (size_t)std::max<int64_t>(F, 1) * 4; }
+size_t PairRows::lds_bytes(int64_t F) {
+  return (size_t)std::min<int64_t>(std::max<int64_t>(F, 1), kRankWindow) * 4;
+}
 
 bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t s,
                      const std::function<void()>& wait, const PrShard* shard) {
   Impl& I = *p_;
   const int64_t F = in.F;
-  KMLS_CHECK(F >= 0 && F <= 32768 && ld >= F, "pair rows: F <= 32768 ranks, ld >= F");
+  KMLS_CHECK(F >= 0 && F <= kSparseMaxF && ld >= F, "pair rows: F <= 65535 ranks, ld >= F");
   I.n_tx = I.nnz = I.pairs = 0;
   I.gathered = false;
   const int own_rank = shard ? shard->rank : 0, own_world = shard ? std::max(shard->world, 1) : 1;
@@ -591,14 +615,16 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
   I.hist.need((size_t)H + 1);
   I.hoff.need((size_t)H + 1);
   ok(hipMemsetAsync(I.hist.p + H, 0, 8, s), "hist tail");
+  // rank windows of kRankWindow LDS counters (one window up to F = 32768)
   const size_t lds = lds_bytes(F);
-  if (lds > 65536) {  // past the default dynamic-LDS limit (F > 16384): up to 160 KB per block
+  if (lds > 65536) {  // past the default dynamic-LDS limit (F > 16384): up to 128 KB per block
     ok(hipFuncSetAttribute((const void*)k_pl_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
-    ok(hipFuncSetAttribute((const void*)k_pl_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
     ok(hipFuncSetAttribute((const void*)k_pl_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "attr");
   }
-  hipLaunchKernelGGL(k_pl_hist, dim3((unsigned)n_wg), dim3(kRowThreads), lds, s, txrec, I.n_tx,
-                     fit, F, n_wg, I.hist.p, own_rank, own_world);
+  for (int64_t lo = 0; lo < F; lo += kRankWindow)
+    hipLaunchKernelGGL(k_pl_hist, dim3((unsigned)n_wg), dim3(kRowThreads), lds, s, txrec, I.n_tx,
+                       fit, F, n_wg, I.hist.p, own_rank, own_world, (uint32_t)lo,
+                       (uint32_t)std::min<int64_t>(F, lo + kRankWindow));
   ok(hipGetLastError(), "hist");
   devbuf::scan_u64(I.hist.p, I.hoff.p, H + 1, I.tmp, s);
   I.base.need((size_t)F + 1);
@@ -651,25 +677,36 @@ bool PairRows::count(const PrInput& in, uint32_t* gram, int64_t ld, hipStream_t 
                        I.n_tx, fit, F, I.grp.p, I.gcur.p, I.gl.p, own_rank, own_world, ng);
   }
   ok(hipGetLastError(), "part");
+  // the direct split keeps a counter per row of the group in LDS
+  const size_t lds_split = (size_t)std::max<uint32_t>(max_rows, 1u) * 4;
+  if (!(staged && max_rows <= (uint32_t)kStBRows) && n_ch > 0) {
+    if (lds_split > (size_t)kMaxDynLds) return false;  // (a group of > 40k rows: the caller's
+                                                       // scattered-atomic count takes it)
+    if (lds_split > 65536)
+      ok(hipFuncSetAttribute((const void*)k_pl_split, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_split), "attr");
+  }
   if (n_ch > 0) {
     if (staged && max_rows <= (uint32_t)kStBRows)
       hipLaunchKernelGGL(k_pl_split_staged, dim3(n_ch), dim3(kStBThreads),
                          (size_t)(3 * max_rows + 1) * 4, s, I.gl.p, I.base.p, I.grow.p, I.gch.p,
                          I.rcur.p, I.pl.p, ng);
     else if (staged)  // a group of more rows than the staged form holds: direct, same chunks
-      hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds, s, I.gl.p,
+      hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds_split, s, I.gl.p,
                          (const unsigned long long*)nullptr, I.base.p, I.grow.p, I.gch.p,
                          I.rcur.p, I.pl.p, ng, chunk_b);
     else
-      hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds, s, I.gl.p,
+      hipLaunchKernelGGL(k_pl_split, dim3(n_ch), dim3(kRowThreads), lds_split, s, I.gl.p,
                          (const unsigned long long*)nullptr, I.base.p, I.grow.p, I.gch.p,
                          I.rcur.p, I.pl.p, ng, chunk);
   }
   ok(hipGetLastError(), "split");
   // 3. the rows
   if (n_sl > 0)
-    hipLaunchKernelGGL(k_pl_rows, dim3(n_sl), dim3(kRowThreads), lds, s, I.soff.p, F, I.base.p,
-                       I.pl.p, gram, ld);
+    for (int64_t lo = 0; lo < F; lo += kRankWindow)
+      hipLaunchKernelGGL(k_pl_rows, dim3(n_sl), dim3(kRowThreads), lds, s, I.soff.p, F, I.base.p,
+                         I.pl.p, gram, ld, (uint32_t)lo,
+                         (uint32_t)std::min<int64_t>(F, lo + kRankWindow));
   ok(hipGetLastError(), "rows");
   return true;
 }
