@@ -47,6 +47,8 @@ Secondary fields:
                     levels of its own items (``GpuMiner.mine_shard``, no bitmap, no count
                     reduction); sub-tries gathered on rank 0, digest compared with tx mode,
                     sampled supports recounted on the host from the CSR shards.
+* ``config3_wide`` — config 3's data at 7e-5 (59,664 frequent items; N = 1): the sparse path
+                    past 32,768 ranks, sampled supports recounted on the host.
 * ``native_rccl`` — at N > 1 the headline combine once more through the native RCCL
                     communicator (``csrc/host/comm_rccl.cpp``), digest compared.
 
@@ -465,6 +467,17 @@ def main() -> int:
                 out["config3_shard"] = c3s
         except Exception as e:
             out.setdefault("errors", {})["config3_shard"] = repr(e)[:300]
+        wd.disarm()
+
+    # ---- config 3's data at 7e-5 (59,664 frequent items, N = 1): the sparse path past 32,768
+    #      ranks (16-bit rank windows), reference min_support sweep downwards ----
+    if not args.no_config3 and not args.cpu and world == 1:
+        wd.arm("config3_wide", 300)
+        try:
+            out["config3_wide"] = bm.run_config3(N, world, rank, device, steps=2, warmup=1,
+                                                 min_support=7e-5)
+        except Exception as e:
+            out.setdefault("errors", {})["config3_wide"] = repr(e)[:300]
         wd.disarm()
 
     if rank == 0:
