@@ -22,7 +22,7 @@ namespace gpu {
 
 DeepBufs::~DeepBufs() {
   (void)hipSetDevice(device);
-  for (void* p : {(void*)stacks, (void*)stacks0, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)req, (void*)inbox, (void*)inbox_state, (void*)heap[0],
+  for (void* p : {(void*)stacks, (void*)stacks0, (void*)fstacks, (void*)q[0], (void*)q[1], (void*)ready, (void*)req, (void*)inbox, (void*)inbox_state, (void*)d_key, (void*)heap[0],
                   (void*)heap[1], (void*)root, (void*)ctl, (void*)d_red, (void*)d_xor,
                   (void*)d_m, (void*)d_off, (void*)d_toff, (void*)d_cost, (void*)d_order,
                   (void*)d_trace, (void*)d_ticks, (void*)n_parent, (void*)n_item,
@@ -263,7 +263,18 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       grow(b.d_order, c2, T);
       grow(b.d_ocost, c3, T);
       b.t_cap = std::min({c1, c2, c3});
-      kern::deep_task_cost(b.d_off, b.d_m, b.d_toff, F, b.root, in.minsup, b.d_cost, s, E);
+      // the deal's sort key (test hook deep_cost_key): 0 the class size (cost), 1 the class's
+      // support mass (default: per-rank itemset shares 0.88-1.16 of the mean on 8 ranks, against
+      // 0.77-1.18 by class size; profiles/r6s_*), 2 its square; a rank split only (one GPU takes
+      // every task anyway)
+      const int key_mode = world > 1 ? (int)test_hook("deep_cost_key", 1) : 0;
+      if (key_mode) {
+        int64_t c4 = b.key_cap;
+        grow(b.d_key, c4, T);
+        b.key_cap = c4;
+      }
+      kern::deep_task_cost(b.d_off, b.d_m, b.d_toff, F, b.root, in.minsup, b.d_cost, s, E,
+                           key_mode ? b.d_key : nullptr, key_mode);
       std::vector<int64_t> mine;
       std::vector<uint32_t> cost;  // cost[q] of the rank's q-th task (host copies: pre-split, trace)
       if (opt.assign == 1) {
@@ -274,7 +285,7 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
           KMLS_HIP(hipMalloc((void**)&b.d_otmp, b.otmp_bytes));
         }
         n_tasks = kern::deep_task_order(b.d_cost, T, rank, world, b.d_otmp, b.otmp_bytes,
-                                        b.d_order, b.d_ocost, s);
+                                        b.d_order, b.d_ocost, s, key_mode ? b.d_key : nullptr);
         if (n_tasks > b.q_cap) throw std::runtime_error("deep_run: level-3 task list exceeds the queue");
         const bool deeper4 = in.max_len == 0 || in.max_len >= 4;  // the split classes expand
         const bool presplit = opt.presplit_cost > 0 && opt.presplit_budget > 0 && opt.steal &&
@@ -366,6 +377,10 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   a.minsup = in.minsup;
   a.max_len = in.max_len;
   a.split_min = opt.split_min;
+  // hand-offs split classes of >= 32 first members, keeping 5/16 of them (1 GPU: 29.3-29.9 ms
+  // against 30.0-31.1 unsplit; 8 ranks: 8.1-8.3 vs 7.9-8.2 unsplit, 8.5-9.1 at >= 8 members)
+  a.split_firsts = (unsigned)std::max<long long>(2, test_hook("deep_split_firsts", 32));
+  a.split_keep16 = (unsigned)std::min<long long>(15, test_hook("deep_split_keep16", 5));
   a.ask_mask = (unsigned)test_hook("deep_ask_mask", 7);
   a.sleep_n = (unsigned)test_hook("deep_sleep_n", 1u << 30);
   a.out_cap = b.q_cap;

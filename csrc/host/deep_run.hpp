@@ -49,6 +49,8 @@ struct DeepBufs {
   int64_t* d_toff = nullptr;  // [F + 1] task offsets
   int64_t f_cap = 0;
   uint32_t* d_cost = nullptr;   // [T] level-3 task costs (assign = 1)
+  uint32_t* d_key = nullptr;    // [key_cap] the deal's sort key (test hook deep_cost_key)
+  int64_t key_cap = 0;
   int64_t* d_order = nullptr;   // [T] this rank's task ids in queue order
   uint32_t* d_ocost = nullptr;  // [T] their costs
   int64_t t_cap = 0;

@@ -29,7 +29,8 @@
 // * Load balance: tasks are dequeued by ticket, heaviest first (deep_order.hip's cost order).
 //   Steal mode (the default): a wave whose ticket finds the queue drained opens its inbox and
 //   asks busy waves, one mailbox at a time; a busy wave past its step budget that finds a request
-//   in its mailbox hands its bottom (oldest, largest) open class straight to that inbox.  Without
+//   in its mailbox hands its bottom (oldest, largest) open class straight to that inbox — a
+//   large one split: the upper members go, the lower first members stay (frame lead).  Without
 //   steal mode a wave past its budget SPILLS its frames to a heap as new tasks and the host runs
 //   another round.
 // Counts are exact (popcount of at most 4096 bits per row, u32).
@@ -53,18 +54,33 @@ constexpr int kRootChunk = 256;      // level-2 candidates per wave of k_deep_ro
 constexpr int kCap = 512;            // candidate pairs per batch step (256: 42.7 ms, 512: 39.6, 1024 with 16-bit group fields: 43.9 at ds1 @0.02)
 constexpr int kBatchFrames = 64;     // frames one batch step may take
 constexpr int kBStack = 96;          // blocks on one wave's memory stack
-constexpr unsigned kSingle = 1u << 8;  // frame flag: expand only its first member
+static_assert(kBStack < 127, "block-stack index + 1 must fit the 7 meta bits");
+constexpr unsigned kSingle = 1u << 6;  // frame flag: expand only its first member
+constexpr unsigned kMaxLead = 2047;    // frame lead field (11 bits)
+// (hand-offs split a class of >= DeepArgs::split_firsts first members, keeping split_keep16/16)
 constexpr unsigned kDone = 1u << 31;   // steal mode: ready-flag value epoch ^ kDone = no task
 constexpr unsigned kNodeChunk = 4096;  // emit mode: node ids a wave takes from ctl->node_top
 
-// frame meta: bits 0..7 prefix size, bit 8 single, bits 9..15 block width (words), bits 16..31
-// block-stack index + 1 (0 = external)
-__device__ __forceinline__ unsigned meta_depth(unsigned m) { return m & 0xffu; }
-__device__ __forceinline__ unsigned meta_width(unsigned m) { return (m >> 9) & 0x7fu; }
-__device__ __forceinline__ unsigned meta_bidx(unsigned m) { return m >> 16; }
+// frame meta: bits 0..5 prefix size, bit 6 single, bits 7..13 block width (words), bits 14..20
+// block-stack index + 1 (0 = external), bits 21..31 lead: how many of the class's members, from
+// s0 on, are still to be expanded as first members (0 = all; every member stays a candidate).  A
+// hand-off of a large class gives away its upper members as a class of their own and keeps
+// the first `lead` (halving instead of one member per hop: the tail of a split launch).
+__device__ __forceinline__ unsigned meta_depth(unsigned m) { return m & 0x3fu; }
+__device__ __forceinline__ unsigned meta_width(unsigned m) { return (m >> 7) & 0x7fu; }
+__device__ __forceinline__ unsigned meta_bidx(unsigned m) { return (m >> 14) & 0x7fu; }
+__device__ __forceinline__ unsigned meta_lead(unsigned m) { return m >> 21; }
+__device__ __forceinline__ unsigned meta_with_lead(unsigned m, unsigned lead) {
+  return (m & 0x1fffffu) | (lead << 21);
+}
 __host__ __device__ constexpr unsigned make_meta(unsigned depth, bool single, unsigned width,
-                                                 unsigned bidx) {
-  return depth | (single ? kSingle : 0u) | (width << 9) | (bidx << 16);
+                                                 unsigned bidx, unsigned lead = 0) {
+  return depth | (single ? kSingle : 0u) | (width << 7) | (bidx << 14) | (lead << 21);
+}
+// the first members a frame still expands (single: 1; lead: lead; else all but the last)
+__device__ __forceinline__ unsigned frame_firsts(unsigned meta, unsigned m) {
+  const unsigned lead = meta_lead(meta);
+  return (meta & kSingle) ? 1u : lead ? lead : m - 1u;
 }
 
 // block widths the kernels are instantiated for (words); tier(n) = smallest >= n
@@ -373,7 +389,7 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
     const DeepFrame fr = load_frame(fst + f, lane);
     bytes_tot += (unsigned long long)(meta_width(fr.meta) + 1 + E) * roundup16(fr.m) * 8ull;
     const bool single = (fr.meta & kSingle) != 0;
-    nt_tot += (!single && fr.m > a.split_min) ? fr.m - 1 : 1;
+    nt_tot += (!single && fr.m > a.split_min) ? frame_firsts(fr.meta, fr.m) : 1;
   }
   unsigned long long hbase = 0;
   if (fixed >= 0) {  // pre-split: the host laid out every task's heap bytes and queue slots
@@ -427,7 +443,7 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
     }
     const bool single = (fr.meta & kSingle) != 0;
     const bool split = !single && m > a.split_min;
-    const unsigned nt = split ? m - 1 : 1;
+    const unsigned nt = split ? frame_firsts(fr.meta, m) : 1;
     for (unsigned k = lane; k < nt; k += 64) {
       DeepFrame o;
       o.blk = (unsigned long long)dst;
@@ -435,7 +451,8 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
       o.pad = (unsigned)npad;
       o.s0 = split ? k : 0u;
       o.m = split ? m - k : m;
-      o.meta = make_meta(meta_depth(fr.meta), split || single, wt, 0);
+      o.meta = make_meta(meta_depth(fr.meta), split || single, wt, 0,
+                         (split || single) ? 0u : meta_lead(fr.meta));
       if (a.steal)
         publish_frame(out + q + k, o);
       else
@@ -459,23 +476,38 @@ __device__ __forceinline__ int spill_frames(const DeepArgs& a, DeepFrame* fst, W
   return 0;
 }
 
-// Direct hand-off of the bottom frame to the inbox of the wave that asked (`req`): claim its
-// inbox (open -> filling), copy the class block to the heap and the frame to the inbox with
-// write-through stores, count the task, mark the inbox full.  False (nothing changed) when the
-// requester is no longer waiting or the heap is full.
+// Direct hand-off to the inbox of the wave that asked (`req`): claim its inbox (open ->
+// filling), copy a class block to the heap and the frame to the inbox with write-through stores,
+// count the task, mark the inbox full.  The bottom frame (the oldest, largest open class) goes
+// whole when it is small; a class of >= split_firsts first members is split instead: its upper
+// members become the handed-off class (with the first members past the kept ones) and the wave
+// keeps expanding the lower split_keep16/16 of the first members (lead), which pair with more candidates
+// each — a large class spreads over the waves in a logarithmic number of hand-offs, not one
+// member per hop.  False (nothing changed) when the requester is no longer waiting or the heap
+// is full.
 template <int MAXT, bool EMIT>
 __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst, WaveState& st,
                                               WaveLds<MAXT>& L, int lane, unsigned req,
                                               unsigned k_open, unsigned k_filling,
                                               unsigned k_full) {
   if ((long long)req >= a.nwaves) return false;
+  const DeepFrame fr = load_frame(fst, lane);
+  const unsigned m = fr.m, wt = meta_width(fr.meta);
+  const bool single = (fr.meta & kSingle) != 0;
+  const unsigned lead = meta_lead(fr.meta);
+  const unsigned firsts = frame_firsts(fr.meta, m);
+  unsigned h = 0;  // first members kept (0: the whole frame goes)
+  if (!single && a.split_keep16 && firsts >= a.split_firsts) {
+    h = firsts * a.split_keep16 / 16u;
+    h = h < 1u ? 1u : h > kMaxLead ? kMaxLead : h;
+  }
+  if (h == 0 && st.nf < 2) return false;  // a lone small frame stays
   unsigned ok = 0;
   if (lane == 0) ok = atomicCAS(&a.inbox_state[req], k_open, k_filling) == k_open;
   if (!uni(__shfl(ok, 0, 64))) return false;
-  const DeepFrame fr = load_frame(fst, lane);
-  const unsigned m = fr.m, wt = meta_width(fr.meta);
+  const unsigned mo = m - h;  // members [s0 + h, s0 + m) go
   constexpr unsigned E = EMIT ? 1u : 0u;
-  const unsigned long long npad = roundup16(m);
+  const unsigned long long npad = roundup16(mo);
   const unsigned long long bytes = (unsigned long long)(wt + 1 + E) * npad * 8ull;
   unsigned long long base = 0;
   if (lane == 0) base = atomicAdd(&a.ctl->heap_top, bytes);
@@ -486,10 +518,10 @@ __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst,
   }
   const unsigned long long* src = (const unsigned long long*)fr.blk;
   unsigned long long* dst = (unsigned long long*)(a.heap + base);
-  const unsigned long long tot = (unsigned long long)(wt + 1 + E) * m;
+  const unsigned long long tot = (unsigned long long)(wt + 1 + E) * mo;
   for (unsigned long long e = lane; e < tot; e += 64) {
-    const unsigned long long w = e / m, k = e - w * m;
-    st_agent(dst + w * npad + k, src[w * fr.pad + fr.s0 + k]);
+    const unsigned long long w = e / mo, k = e - w * mo;
+    st_agent(dst + w * npad + k, src[w * fr.pad + fr.s0 + h + k]);
   }
   if (lane == 0) {
     DeepFrame o;
@@ -497,8 +529,10 @@ __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst,
     o.hash = fr.hash;
     o.pad = (unsigned)npad;
     o.s0 = 0;
-    o.m = m;
-    o.meta = make_meta(meta_depth(fr.meta), (fr.meta & kSingle) != 0, wt, 0);
+    o.m = mo;
+    // the given class expands its own first members: all of them, or (a frame with a lead:
+    // also when it goes whole) those up to the old lead
+    o.meta = make_meta(meta_depth(fr.meta), single, wt, 0, lead ? lead - h : 0u);
     publish_frame(a.inbox + req, o);
     atomicAdd(&a.ctl->pending, 1ull);
     atomicAdd(&a.ctl->handoffs, 1ull);
@@ -506,7 +540,16 @@ __device__ __forceinline__ bool donate_bottom(const DeepArgs& a, DeepFrame* fst,
   wait_stores();  // block and frame complete before the inbox turns full
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) atomicExch(&a.inbox_state[req], k_full);
-  drop_bottom<MAXT>(fst, st, L, lane, 1);
+  if (h) {  // the wave keeps the bottom class's first h members (still paired with all of them)
+    if (lane == 0) {
+      DeepFrame kf = fr;
+      kf.meta = meta_with_lead(fr.meta, h);
+      store_frame(fst, kf);
+    }
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    drop_bottom<MAXT>(fst, st, L, lane, 1);
+  }
   return true;
 }
 
@@ -579,13 +622,15 @@ __device__ __forceinline__ void row_step(const DeepArgs& a, DeepFrame* fst, Wave
   acc.cands += nc;
   if (lane == 0 && S) L.depth_cnt[depth + 2] += S;
   acc.budget_used += (nc + 63) / 64;
-  // parent: done with member s0
-  if ((top.meta & kSingle) || m <= 2) {
+  // parent: done with member s0 (a frame with a lead: with its last first member)
+  const unsigned lead = meta_lead(top.meta);
+  if ((top.meta & kSingle) || m <= 2 || lead == 1u) {
     release_frame(L, top.meta, lane);
     st.nf -= 1;
   } else {
     top.s0 += 1;
     top.m -= 1;
+    if (lead) top.meta = meta_with_lead(top.meta, lead - 1u);
     if (lane == 0) store_frame(fst + st.nf - 1, top);
   }
   if (S >= 2 && deeper) {
@@ -625,7 +670,8 @@ __device__ __forceinline__ void batch_step(const DeepArgs& a, DeepFrame* fst, Wa
     if ((unsigned)lane < st.nf) {
       fm = lf.m;
       fmeta = lf.meta;
-      if (lf.blk != top.blk) fmeta |= kSingle;  // another block: ends the batch
+      // another block, or a frame with a lead (expanded row by row): ends the batch
+      if (lf.blk != top.blk || meta_lead(lf.meta)) fmeta |= kSingle;
       L.f_hash[lane] = lf.hash;
       L.f_s0[lane] = lf.s0;
       L.f_m[lane] = fm;
@@ -990,7 +1036,8 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
       const unsigned m = top.m;
       const unsigned wt = meta_width(top.meta);
       const unsigned long long pairs = (unsigned long long)m * (m - 1) / 2;
-      const bool row_mode = (top.meta & kSingle) || pairs > (unsigned long long)kCap;
+      const bool row_mode = (top.meta & kSingle) || meta_lead(top.meta) ||
+                            pairs > (unsigned long long)kCap;
       const unsigned long long need =
           (unsigned long long)(wt + 1 + E) * roundup16(row_mode ? m : kCap) * 8ull;
       const unsigned long long top_at =  // (a block never straddles the two stack parts)
@@ -1011,10 +1058,12 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
             if (st.nf == 0) break;
             continue;
           }
-        } else if (st.nf >= 2) {
+        } else if (st.nf >= 2 ||
+                   (a.split_keep16 && frame_firsts(top.meta, top.m) >= a.split_firsts)) {
           // a waiting wave asked (this wave's own mailbox): hand the bottom (oldest, largest)
-          // open class straight to its inbox and keep the rest.  A lone frame stays (handing
-          // the whole stack over just moves the class to a wave that is asked in turn).
+          // open class straight to its inbox — split when large (donate_bottom) — and keep the
+          // rest.  A lone small frame stays (handing the whole stack over just moves the class
+          // to a wave that is asked in turn).
           unsigned long long r = 0;
           if (a.steal_eager == 2) {  // tests: offer to the partner wave whenever it waits
             r = (gw ^ 1ull) < (unsigned long long)a.nwaves ? (gw ^ 1ull) + 1ull : 0ull;
@@ -1372,7 +1421,8 @@ __global__ void k_deep_root_tasks(const long long* blk_off, const int32_t* m, co
 __global__ __launch_bounds__(256) void k_deep_task_cost(const long long* blk_off, const int32_t* m,
                                                         const long long* task_off, long long F,
                                                         const char* base, unsigned minsup,
-                                                        unsigned* cost, unsigned extra) {
+                                                        unsigned* cost, unsigned extra,
+                                                        unsigned* key, int key_mode) {
   const long long i = blockIdx.x;
   if (i >= F) return;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1383,15 +1433,29 @@ __global__ __launch_bounds__(256) void k_deep_task_cost(const long long* blk_off
   const unsigned long long* blk = (const unsigned long long*)(base + blk_off[i]);
   for (int k = wid; k < mi - 1; k += (int)(blockDim.x >> 6)) {
     unsigned c = 0;
+    unsigned long long mass = 0;  // (key_mode 1) the survivors' supports above minsup - 1
     for (int j0 = k + 1; j0 < mi; j0 += 64) {
       const int j = j0 + lane;
       unsigned pc = 0;
       if (j < mi)
         for (unsigned w = 0; w < wt; ++w)
           pc += (unsigned)__popcll(blk[(unsigned long long)w * pad + k] & blk[(unsigned long long)w * pad + j]);
-      c += (unsigned)__popcll(__ballot(j < mi && pc >= minsup));
+      const bool surv = j < mi && pc >= minsup;
+      c += (unsigned)__popcll(__ballot(surv));
+      if (key_mode == 1) {
+        unsigned long long x = surv ? (unsigned long long)(pc - minsup + 1u) : 0ull;
+        for (int o = 32; o; o >>= 1) x += __shfl_xor(x, o, 64);
+        mass += x;
+      }
     }
-    if (lane == 0) cost[task_off[i] + k] = c;
+    if (lane == 0) {
+      cost[task_off[i] + k] = c;
+      // the deal's sort key: the class size (0), its support mass (1) or its square (2)
+      if (key)
+        key[task_off[i] + k] =
+            key_mode == 1 ? (unsigned)(mass < 0xFFFFFFFFull ? mass : 0xFFFFFFFFull)
+            : key_mode == 2 ? (c < 65535u ? c * c : 0xFFFFFFFFu) : c;
+    }
   }
 }
 
@@ -1529,11 +1593,12 @@ void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* ta
 }
 
 void deep_task_cost(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
-                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s, int extra) {
+                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s, int extra,
+                    uint32_t* key, int key_mode) {
   if (F <= 0) return;
   hipLaunchKernelGGL(k_deep_task_cost, dim3((unsigned)F), dim3(256), 0, s,
                      (const long long*)blk_off, m, (const long long*)task_off, (long long)F, base,
-                     minsup, cost, (unsigned)extra);
+                     minsup, cost, (unsigned)extra, key, key_mode);
 }
 
 int deep_count_wps(int maxt, int want, bool emit) {

@@ -29,31 +29,32 @@ namespace {
 
 constexpr uint64_t kCostMask = 0xFFFFull;  // costs saturate at 65535 (class sizes are smaller)
 
-// key = (65535 - cost) << 32 | t: ascending keys = descending cost, ascending t
-__global__ void k_order_keys(const uint32_t* __restrict__ cost, int64_t T, uint64_t* __restrict__ key) {
+// key = (kKeyMax - min(c, kKeyMax)) << 32 | t, c = by[t] (the cost, or a separate deal key):
+// ascending keys = descending c, ascending t
+constexpr uint64_t kKeyMax = 0xFFFFFFFFull;
+__global__ void k_order_keys(const uint32_t* __restrict__ by, int64_t T, uint64_t* __restrict__ key) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < T;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t c = std::min<uint64_t>(cost[t], kCostMask);
-    key[t] = ((kCostMask - c) << 32) | (uint64_t)t;
-  }
+       t += (int64_t)gridDim.x * blockDim.x)
+    key[t] = ((kKeyMax - (uint64_t)by[t]) << 32) | (uint64_t)t;
 }
 
 // this rank's j-th task: sorted position q(j) = j * world + (j odd ? world - 1 - rank : rank)
-__global__ void k_order_deal(const uint64_t* __restrict__ sorted, int64_t T, int rank, int world,
-                             int64_t n, int64_t* __restrict__ order, uint32_t* __restrict__ ocost) {
+__global__ void k_order_deal(const uint64_t* __restrict__ sorted, const uint32_t* __restrict__ cost,
+                             int64_t T, int rank, int world, int64_t n,
+                             int64_t* __restrict__ order, uint32_t* __restrict__ ocost) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
        j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t q = j * world + ((j & 1) ? world - 1 - rank : rank);
-    const uint64_t k = sorted[q];
-    order[j] = (int64_t)(k & 0xFFFFFFFFull);
-    ocost[j] = (uint32_t)(kCostMask - (k >> 32));
+    const uint64_t t = sorted[q] & 0xFFFFFFFFull;
+    order[j] = (int64_t)t;
+    ocost[j] = std::min<uint32_t>(cost[t], (uint32_t)kCostMask);
   }
 }
 
 size_t cub_bytes(int64_t T) {
   size_t b = 0;
   KMLS_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b, (const uint64_t*)nullptr,
-                                             (uint64_t*)nullptr, (int)T, 0, 48));
+                                             (uint64_t*)nullptr, (int)T, 0, 64));
   return b;
 }
 
@@ -71,7 +72,8 @@ size_t deep_task_order_bytes(int64_t T) {
 }
 
 int64_t deep_task_order(const uint32_t* cost, int64_t T, int rank, int world, void* tmp,
-                        size_t tmp_bytes, int64_t* order, uint32_t* order_cost, hipStream_t s) {
+                        size_t tmp_bytes, int64_t* order, uint32_t* order_cost, hipStream_t s,
+                        const uint32_t* key) {
   if (T <= 0) return 0;
   KMLS_CHECK(T < ((int64_t)1 << 32), "deep_task_order: task ids must fit 32 bits");
   KMLS_CHECK(tmp_bytes >= deep_task_order_bytes(T), "deep_task_order: scratch too small");
@@ -80,15 +82,15 @@ int64_t deep_task_order(const uint32_t* cost, int64_t T, int rank, int world, vo
   void* cub = (void*)(((uintptr_t)(sorted + T) + 255) & ~(uintptr_t)255);
   size_t cb = cub_bytes(T);
   const unsigned g = (unsigned)std::min<int64_t>((T + 255) / 256, 2048);
-  hipLaunchKernelGGL(k_order_keys, dim3(g), dim3(256), 0, s, cost, T, keys);
+  hipLaunchKernelGGL(k_order_keys, dim3(g), dim3(256), 0, s, key ? key : cost, T, keys);
   KMLS_HIP(hipGetLastError());
-  // 48 key bits: the 32-bit task id and the 16-bit inverted cost
-  KMLS_HIP(hipcub::DeviceRadixSort::SortKeys(cub, cb, keys, sorted, (int)T, 0, 48, s));
+  // 64 key bits: the 32-bit task id and the 32-bit inverted cost / deal key
+  KMLS_HIP(hipcub::DeviceRadixSort::SortKeys(cub, cb, keys, sorted, (int)T, 0, 64, s));
   const int64_t n = deep_task_share(T, rank, world);
   if (n > 0) {
     const unsigned g2 = (unsigned)std::min<int64_t>((n + 255) / 256, 2048);
-    hipLaunchKernelGGL(k_order_deal, dim3(g2), dim3(256), 0, s, sorted, T, rank, world, n, order,
-                       order_cost);
+    hipLaunchKernelGGL(k_order_deal, dim3(g2), dim3(256), 0, s, sorted, cost, T, rank, world, n,
+                       order, order_cost);
     KMLS_HIP(hipGetLastError());
   }
   return n;

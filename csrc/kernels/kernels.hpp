@@ -67,6 +67,8 @@ struct DeepArgs {
   long long nwaves;
   unsigned epoch;                 // < 2^30
   int steal;
+  unsigned split_firsts;          // a hand-off splits a class of >= this many first members
+  unsigned split_keep16;          // ... keeping split_keep16 / 16 of them (0: never split)
   unsigned ask_mask;              // a waiting wave asks a victim every (ask_mask + 1) polls
   unsigned sleep_n;               // poll backoff: s_sleep 2 / 16 / 127 from poll 0 / 4 / 16 on,
                                   // the poll count capped at sleep_n
@@ -146,17 +148,22 @@ void deep_arena_digest(const unsigned* parent, const unsigned* item, const unsig
 void deep_root_tasks(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
                      char* base, const uint64_t* root, int64_t Fpad, int W, int rank, int world,
                      const int64_t* order, int64_t n, DeepFrame* out, hipStream_t s, int extra = 0);
-// level-3 survivors of every task (the size of the class the task expands): cost[t]
+// level-3 survivors of every task (the size of the class the task expands): cost[t]; with key
+// != nullptr also the deal's sort key: key_mode 0 the class size, 1 its support mass
+// (sum of survivor supports - minsup + 1), 2 its square
 void deep_task_cost(const int64_t* blk_off, const int32_t* m, const int64_t* task_off, int64_t F,
-                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s, int extra = 0);
+                    const char* base, uint32_t minsup, uint32_t* cost, hipStream_t s, int extra = 0,
+                    uint32_t* key = nullptr, int key_mode = 0);
 void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s);
 // (deep_order.hip) tasks by cost, largest first and stable in t, dealt over `world` ranks in
 // snake order: order[j] / order_cost[j] = this rank's j-th task and its cost, j < the returned
 // count (= deep_task_share); tmp = deep_task_order_bytes(T) bytes of device scratch
 int64_t deep_task_share(int64_t T, int rank, int world);
 size_t deep_task_order_bytes(int64_t T);
+// key (optional): sort by key[t] (32 bits) instead of cost[t]; order_cost still = cost
 int64_t deep_task_order(const uint32_t* cost, int64_t T, int rank, int world, void* tmp,
-                        size_t tmp_bytes, int64_t* order, uint32_t* order_cost, hipStream_t s);
+                        size_t tmp_bytes, int64_t* order, uint32_t* order_cost, hipStream_t s,
+                        const uint32_t* key = nullptr);
 // (deep_trie.hip) emit arena -> dense trie, parents first: new_id[i] for every arena id of size
 // in [min_depth, nd) (size-major, arena order inside a size; others kNone), returns the node
 // count (synchronises); then the scatter writes the trie at new_id (parent remapped, + base for

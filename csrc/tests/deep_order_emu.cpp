@@ -36,17 +36,17 @@ int64_t deep_task_share(int64_t T, int rank, int world) {
 size_t deep_task_order_bytes(int64_t T) { return (size_t)std::max<int64_t>(T, 1) * 8; }
 
 int64_t deep_task_order(const uint32_t* cost, int64_t T, int rank, int world, void*, size_t,
-                        int64_t* order, uint32_t* order_cost, hipStream_t) {
+                        int64_t* order, uint32_t* order_cost, hipStream_t, const uint32_t* by) {
   if (T <= 0) return 0;
   std::vector<int64_t> idx((size_t)T);
   std::iota(idx.begin(), idx.end(), 0);
-  auto key = [&](int64_t t) { return std::min<uint32_t>(cost[t], 0xFFFFu); };
-  std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return key(a) > key(b); });
+  const uint32_t* k = by ? by : cost;  // the deal key (or the cost)
+  std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return k[a] > k[b]; });
   const int64_t n = deep_task_share(T, rank, world);
   for (int64_t j = 0; j < n; ++j) {
     const int64_t q = j * world + ((j & 1) ? world - 1 - rank : rank);
     order[j] = idx[(size_t)q];
-    order_cost[j] = key(idx[(size_t)q]);
+    order_cost[j] = std::min<uint32_t>(cost[idx[(size_t)q]], 0xFFFFu);
   }
   return n;
 }

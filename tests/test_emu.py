@@ -77,3 +77,20 @@ def test_deep_kernel_on_emulator(emu_bin, args):
                        timeout=900, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     assert '"ok": true' in r.stdout
+
+
+@pytest.mark.parametrize("args", [
+    "64 -13 1 1 1 0.5 1 2 8 4 1 0 1 2",              # clique of 13, partner hand-offs
+    "64 -12 1 1 1 0.5 1 1 8 4 3 0 1 1",              # clique, 3 ranks, requested hand-offs
+    "300 50 25 2 0.95 0.08 1 2 4 1 3 0 1 1 2 1",     # emit, 3 ranks, pre-split + hand-offs
+])
+def test_deep_split_handoffs_on_emulator(emu_bin, args):
+    """Hand-offs that split classes (donate_bottom: the upper members go, the frame keeps a lead
+    of first members) at every size from 2 first members, so the small emulator problems split
+    and re-split frames that already carry a lead — counts and digests still exact."""
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0",
+               KMLS_TEST_HOOKS="deep_split_firsts=2,deep_split_keep16=8")
+    r = subprocess.run([str(emu_bin)] + args.split(), capture_output=True, text=True,
+                       timeout=900, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert '"ok": true' in r.stdout
