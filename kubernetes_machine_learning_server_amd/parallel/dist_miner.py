@@ -506,42 +506,54 @@ class DistMiner:
         return {"stats": st, "trie": r}
 
 
-def gather_arrays(arrs: Dict[str, np.ndarray], rank: int, world: int
-                  ) -> Optional[Dict[str, np.ndarray]]:
-    """Concatenate equally-keyed 1-D arrays of every rank on rank 0 (rank order), by tensor
-    collectives: one all-gather of the lengths, one per field of buffers padded to the longest."""
-    if world == 1:
-        return {k: np.asarray(v) for k, v in arrs.items()}
+def _to_root(parts: Dict[str, np.ndarray], rank: int, world: int):
+    """Every rank's 1-D arrays (same keys, same dtypes, any lengths) to rank 0 only, exactly:
+    one all-gather of the lengths, then per field one ``all_to_all_single`` whose only non-empty
+    splits go to rank 0 — no padding to the longest share, nothing delivered to the other ranks,
+    and no extra point-to-point communicators (the collective's own group carries it).  Returns
+    (lengths, {key: list of per-rank arrays}) on rank 0, (lengths, None) elsewhere."""
     dev = (torch.device("cuda", torch.cuda.current_device())
            if dist.get_backend() == "nccl" else torch.device("cpu"))
-    n = len(next(iter(arrs.values()))) if arrs else 0
+    n = len(next(iter(parts.values()))) if parts else 0
     n_local = torch.tensor([n], dtype=torch.int64, device=dev)
-    sizes = torch.empty(world, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(sizes, n_local)
-    sizes = sizes.cpu().numpy()
-    cap = max(int(sizes.max()), 1)
-    out: Dict[str, np.ndarray] = {}
-    for k, a in arrs.items():
+    sizes_t = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(sizes_t, n_local)
+    sizes = [int(x) for x in sizes_t.cpu().numpy()]
+    out: Dict[str, List[np.ndarray]] = {}
+    for key, a in parts.items():
         a = np.ascontiguousarray(a)
-        buf = torch.zeros(cap, dtype=getattr(torch, str(a.dtype)), device=dev)
-        if len(a):
-            buf[:len(a)] = torch.from_numpy(a).to(dev)
-        allb = torch.empty(world * cap, dtype=buf.dtype, device=dev)
-        dist.all_gather_into_tensor(allb, buf)
+        dt = getattr(torch, str(a.dtype))
+        send = torch.from_numpy(a).to(dev) if n else torch.empty(0, dtype=dt, device=dev)
+        recv = torch.empty(sum(sizes) if rank == 0 else 0, dtype=dt, device=dev)
+        dist.all_to_all_single(recv, send,
+                               output_split_sizes=sizes if rank == 0 else [0] * world,
+                               input_split_sizes=[n] + [0] * (world - 1))
         if rank == 0:
-            h = allb.cpu().numpy()
-            out[k] = np.concatenate([h[q * cap:q * cap + int(sizes[q])] for q in range(world)])
-    return out if rank == 0 else None
+            h = recv.cpu().numpy()
+            offs = np.concatenate([[0], np.cumsum(sizes)])
+            out[key] = [h[offs[q]:offs[q + 1]] for q in range(world)]
+    return sizes, (out if rank == 0 else None)
+
+
+def gather_arrays(arrs: Dict[str, np.ndarray], rank: int, world: int
+                  ) -> Optional[Dict[str, np.ndarray]]:
+    """Concatenate equally-keyed 1-D arrays of every rank on rank 0 (rank order): exact-size
+    transfers to rank 0 only (``_to_root``)."""
+    if world == 1:
+        return {k: np.asarray(v) for k, v in arrs.items()}
+    _, got = _to_root(arrs, rank, world)
+    if rank != 0:
+        return None
+    return {k: np.concatenate(v) for k, v in got.items()}
 
 
 def gather_trie(r: Dict, rank: int, world: int, n_frequent: int) -> Optional[Dict[str, np.ndarray]]:
     """Concatenate per-rank sub-tries on rank 0 (level-1 nodes 0..F-1 are shared; every rank's
     local ids >= F are rebased).
 
-    Transport: tensor collectives on the process group's device (HBM for RCCL, host for gloo)
-    — one all-gather of the sizes, then one all-gather per field of buffers padded to the
-    largest sub-trie — instead of pickling numpy arrays through the group: 10^8-node sub-tries
-    move as 4 flat collectives."""
+    Transport: tensor collectives on the process group's device (HBM for RCCL, host for gloo),
+    exact sizes to rank 0 only (``_to_root``: one all-gather of the sizes, one all_to_all_single
+    per field) — the other ranks receive nothing, and no share is padded to the largest."""
     fields = ("parent", "item", "count", "depth")
     if world == 1:
         return {k: np.asarray(r[k]) for k in fields}
@@ -549,40 +561,23 @@ def gather_trie(r: Dict, rank: int, world: int, n_frequent: int) -> Optional[Dic
     mine = {"parent": np.asarray(r["parent"], np.int64)[F:], "item": np.asarray(r["item"], np.int32)[F:],
             "count": np.asarray(r["count"]).astype(np.uint32).view(np.int32)[F:],
             "depth": np.asarray(r["depth"], np.uint8)[F:]}
-    dev = (torch.device("cuda", torch.cuda.current_device())
-           if dist.get_backend() == "nccl" else torch.device("cpu"))
-    n_local = torch.tensor([len(mine["item"])], dtype=torch.int64, device=dev)
-    sizes = torch.empty(world, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(sizes, n_local)
-    sizes = sizes.cpu().numpy()
-    cap = int(sizes.max()) if len(sizes) else 0
-    parts: Dict[str, np.ndarray] = {}
-    for k in fields:
-        a = mine[k]
-        buf = torch.zeros(max(cap, 1), dtype=getattr(torch, str(a.dtype)), device=dev)
-        if len(a):
-            buf[:len(a)] = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-        out = torch.empty(world * max(cap, 1), dtype=buf.dtype, device=dev)
-        dist.all_gather_into_tensor(out, buf)
-        parts[k] = out.cpu().numpy() if rank == 0 else None
+    sizes, parts = _to_root(mine, rank, world)
     if rank != 0:
         return None
     head = {k: np.asarray(r[k])[:F] for k in fields}
     out = {"parent": [head["parent"].astype(np.int64)], "item": [head["item"].astype(np.int32)],
            "count": [head["count"].astype(np.uint32)], "depth": [head["depth"].astype(np.uint8)]}
     base = F
-    stride = max(cap, 1)
     for q in range(world):
         n = int(sizes[q])
         if n == 0:
             continue
-        sl = slice(q * stride, q * stride + n)
-        par = parts["parent"][sl].copy()
+        par = parts["parent"][q].copy()
         loc = par >= F
         par[loc] += base - F
         out["parent"].append(par)
-        out["item"].append(parts["item"][sl])
-        out["count"].append(parts["count"][sl].view(np.uint32))
-        out["depth"].append(parts["depth"][sl])
+        out["item"].append(parts["item"][q])
+        out["count"].append(parts["count"][q].view(np.uint32))
+        out["depth"].append(parts["depth"][q])
         base += n
     return {k: np.concatenate(v) for k, v in out.items()}
