@@ -47,6 +47,9 @@ Secondary fields:
                     levels of its own items (``GpuMiner.mine_shard``, no bitmap, no count
                     reduction); sub-tries gathered on rank 0, digest compared with tx mode,
                     sampled supports recounted on the host from the CSR shards.
+* ``config5_mine`` — config 5's data (100M x 1M @2e-4) mined completely at every N (tx-DP, every
+                    frequent itemset of every size), sampled supports recounted on the host,
+                    plus confidence rules (HIP rule_score) on rank 0, compared with the C++ rules.
 * ``config3_wide`` — config 3's data at 7e-5 (59,664 frequent items; N = 1): the sparse path
                     past 32,768 ranks, sampled supports recounted on the host.
 * ``native_rccl`` — at N > 1 the headline combine once more through the native RCCL
@@ -467,6 +470,21 @@ def main() -> int:
                 out["config3_shard"] = c3s
         except Exception as e:
             out.setdefault("errors", {})["config3_shard"] = repr(e)[:300]
+        wd.disarm()
+
+    # ---- config 5's data mined completely (all ranks: every frequent itemset of every size
+    #      of 100M x 1M @2e-4, tx-DP like config 3) + confidence rules on rank 0 ----
+    if not args.no_config5 and not args.cpu:
+        wd.arm("config5_mine", 420)
+        try:
+            c5m = bm.run_config3(N, world, rank, device, steps=2, warmup=1,
+                                 comm=("rccl" if (world > 1 and out.get("native_rccl", {})
+                                                  .get("digest_equal")) else "host"),
+                                 shape_name="100Mx1M", rules_min_confidence=0.1)
+            if rank == 0:
+                out["config5_mine"] = c5m
+        except Exception as e:
+            out.setdefault("errors", {})["config5_mine"] = repr(e)[:300]
         wd.disarm()
 
     # ---- config 3's data at 7e-5 (59,664 frequent items, N = 1): the sparse path past 32,768

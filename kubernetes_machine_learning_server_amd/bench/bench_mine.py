@@ -460,7 +460,8 @@ def sampled_supports_ok(trie, ptr, items, world: int, rank: int, k: int = 64,
 
 def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: int = 1,
                 comm: str = "host", min_support: float = C3_MIN_SUPPORT,
-                mode: str = "tx") -> Dict:
+                mode: str = "tx", shape_name: str = "10Mx1M",
+                rules_min_confidence: float = 0.0) -> Dict:
     """BASELINE config 3 (10M transactions x 1M items; min_support 2e-4: 14.8k frequent items)
     on all ranks of the job: transaction-DP mining (each rank generates and encodes only its
     shard; supports, the MFMA gram and per-level candidate counts all-reduced), so support /
@@ -474,7 +475,7 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
     prev = os.environ.get("KMLS_COMM")
     os.environ["KMLS_COMM"] = comm
     try:
-        shape = SHAPES["10Mx1M"]
+        shape = SHAPES[shape_name]
         T = shape.n_tx
         lo, hi, _ = shard_bounds(T, world, rank)
         ptr, items = N.synth_transactions(T, shape.n_items, shape.mean_len, shape.n_genres,
@@ -503,7 +504,7 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             ms = float(t.item())
         st = r["stats"]
-        out = {"model": "fpgrowth-10Mx1M-synthetic", "global_batch": T, "seq_len": shape.n_items,
+        out = {"model": f"fpgrowth-{shape_name}-synthetic", "global_batch": T, "seq_len": shape.n_items,
                "min_support": min_support, "n_gpus": world,
                "parallelism": f"tx-dp{world}" if mode == "tx" else f"item-shard{world}",
                "comm": comm, "steps": steps, "ms_per_step": round(ms, 3),
@@ -532,6 +533,28 @@ def run_config3(N, world: int, rank: int, device: int, steps: int = 5, warmup: i
             out["itemsets_per_s"] = round(n / (ms / 1000.0), 1)
             out["digest"] = d["digest"]
             out["verified_sampled_supports"] = ok
+            if rules_min_confidence > 0:
+                # rule generation on the mined trie (machine-learning/main.py:224-260's
+                # association_rules(metric="confidence")), the HIP rule_score kernels
+                from ..models.fpgrowth import ItemsetTrie
+                from ..models.rules import rules_from_trie
+                tr = ItemsetTrie(np.asarray(trie["parent"]), np.asarray(trie["item"]),
+                                 np.asarray(trie["count"]), np.asarray(trie["depth"]), T,
+                                 min_support)
+                best = None
+                for _ in range(3):
+                    t1 = time.perf_counter()
+                    rules = rules_from_trie(tr, "confidence", rules_min_confidence,
+                                            backend="gpu", device=device)
+                    dt = (time.perf_counter() - t1) * 1000.0
+                    best = dt if best is None else min(best, dt)
+                cpu = rules_from_trie(tr, "confidence", rules_min_confidence, backend="cpu")
+                out["rules"] = {"metric": "confidence", "min_confidence": rules_min_confidence,
+                                "n_rules": len(rules), "ms": round(best, 3),
+                                "backend": "gpu (rule_score)",
+                                "equal_cpu": len(rules) == len(cpu) and all(
+                                    np.array_equal(getattr(rules, f), getattr(cpu, f))
+                                    for f in ("itemset", "antecedent", "consequent"))}
         del dm
         return out
     finally:

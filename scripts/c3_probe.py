@@ -15,6 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--hooks", default="")
+    ap.add_argument("--shape", default="10Mx1M", help="100Mx1M: config 5's data, every size")
     ap.add_argument("--min-support", type=float, default=0.0,
                     help="0 = the config's 2e-4; 7e-5 gives ~59.7k frequent items")
     a = ap.parse_args()
@@ -24,6 +25,7 @@ def main():
     from kubernetes_machine_learning_server_amd.ops import native
     N = native.require_gpu()
     kw = {"min_support": a.min_support} if a.min_support else {}
+    kw["shape_name"] = a.shape
     out = bm.run_config3(N, 1, 0, 0, steps=a.steps, warmup=1, **kw)
     print(json.dumps(out), flush=True)
 
