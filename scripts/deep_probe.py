@@ -62,6 +62,8 @@ def main() -> int:
     ap.add_argument("--trace", action="store_true", help="per-wave / per-task timing summary")
     ap.add_argument("--presplit-cost", type=int, default=16, help="0 = no pre-split launch")
     ap.add_argument("--presplit-budget", type=int, default=1)
+    ap.add_argument("--emit", action="store_true",
+                    help="materialise every itemset (the bench's emit block; digest = arena's)")
     a = ap.parse_args()
     from kubernetes_machine_learning_server_amd.data.synthetic import generate
     from kubernetes_machine_learning_server_amd.ops import native
@@ -82,6 +84,7 @@ def main() -> int:
     kw["trace"] = a.trace
     kw["presplit_cost"] = a.presplit_cost
     kw["presplit_budget"] = a.presplit_budget
+    kw["emit"] = a.emit
     if not a.no_parity:
         t = time.perf_counter()
         d = g.mine_deep(0.03, **kw)
