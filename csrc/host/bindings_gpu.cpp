@@ -454,9 +454,10 @@ void register_gpu_bindings(py::module_& m) {
                            py::object comm, unsigned long long budget0, unsigned long long budget,
                            unsigned split_min, int blocks_per_cu, int stack_mb, bool steal,
                            unsigned steal_idle, int assign, bool trace, unsigned presplit_cost,
-                           unsigned long long presplit_budget, bool emit) {
+                           unsigned long long presplit_budget, bool emit, int deal_key) {
         gpu::DeepOpts o;
         o.emit = emit;
+        o.deal_key = deal_key;
         o.assign = assign;
         o.trace = trace;
         o.presplit_cost = presplit_cost;
@@ -522,7 +523,7 @@ void register_gpu_bindings(py::module_& m) {
          py::arg("split_min") = 8u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0,
          py::arg("steal") = true, py::arg("steal_idle") = 1u, py::arg("assign") = 1,
          py::arg("trace") = false, py::arg("presplit_cost") = 16u,
-         py::arg("presplit_budget") = 1ull, py::arg("emit") = false)
+         py::arg("presplit_budget") = 1ull, py::arg("emit") = false, py::arg("deal_key") = -1)
       .def("deep_arena_digest", [](gpu::GpuMiner& g, int min_depth) {
         gpu::GpuMiner::ArenaDigest r;
         {

@@ -267,7 +267,8 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       // support mass (default: per-rank itemset shares 0.88-1.16 of the mean on 8 ranks, against
       // 0.77-1.18 by class size; profiles/r6s_*), 2 its square; a rank split only (one GPU takes
       // every task anyway)
-      const int key_mode = world > 1 ? (int)test_hook("deep_cost_key", 1) : 0;
+      const int key_mode =
+          world > 1 ? (opt.deal_key >= 0 ? opt.deal_key : (int)test_hook("deep_cost_key", 1)) : 0;
       if (key_mode) {
         int64_t c4 = b.key_cap;
         grow(b.d_key, c4, T);

@@ -169,6 +169,10 @@ struct DeepOpts {
                                       // (largest first) and dealt over the ranks in snake order;
                                       // 0 = task t to rank t % world in index order
   bool trace = false;                 // per-wave / per-task timing of the launch (DeepResult)
+  int deal_key = -1;                  // the snake deal's sort key at world > 1: 0 the class size,
+                                      // 1 the class's support mass, -1 the default (1; test hook
+                                      // deep_cost_key).  A partition recorded under one key (the
+                                      // config-2 virtual ranks, profiles/config2_full) needs it.
   // pre-split (assign = 1, rank splits only): the rank's level-3 tasks whose class has >=
   // presplit_cost members
   // first run `presplit_budget` passes in a non-stealing launch that spills their open classes

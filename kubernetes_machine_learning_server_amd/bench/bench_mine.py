@@ -221,7 +221,8 @@ def config2_complete_subset(g, ms: float = 0.01, ranks=CONFIG2_SUBSET_RANKS) -> 
     recs, n_tot, s_tot, off_tot = [], 0, 0.0, 0.0
     for r in ranks:
         t = time.perf_counter()
-        d = g.mine_deep(ms, 0, int(r), CONFIG2_WORLD, None)
+        # the deal the offline partials were counted under: level-3 tasks by class size
+        d = g.mine_deep(ms, 0, int(r), CONFIG2_WORLD, None, deal_key=0)
         s = time.perf_counter() - t
         ref = parts[int(r)]
         ok = (d["digest"] == ref["digest"] and int(d["n_itemsets"]) == int(ref["n_itemsets"])

@@ -81,7 +81,7 @@ def main() -> int:
                 break
             cur[0] = r
             t = time.perf_counter()
-            d = g.mine_deep(a.support, 0, r, a.world, None)
+            d = g.mine_deep(a.support, 0, r, a.world, None, deal_key=0)  # (profiles/config2_full)
             s = time.perf_counter() - t
             rec = {"world": a.world, "rank": r, "min_support": a.support, "s": round(s, 4),
                    "n_itemsets": int(d["n_itemsets"]),
