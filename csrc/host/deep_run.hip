@@ -218,13 +218,16 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
       // the arena: level-1 nodes (ids = ranks), level-2 nodes (F + node_off[i] + slot), then
       // per-wave chunks from node_top; sizes reset to 0 (unused ids) over what the last call used
       // first guess: the two root levels x 8 and two node chunks per wave; a call that overflows
-      // learns the exact need (node_top) and reruns
-      const int64_t need = std::max<int64_t>({(F + pairs) * 8 + waves * 2 * kern::deep_node_chunk(),
-                                              b.arena_cap, (int64_t)(b.arena_used * 1.1)});
+      // learns the exact need (node_top) and reruns.  The arena is regrown only when the last
+      // call's ids come within 3 % of it, then to 10 % past them: node_top varies a little from
+      // call to call (partly used per-wave chunks), and regrowing on every such wobble re-allocates
+      // ~20 GB inside a timed step (164 vs 46 ms in one bench run)
+      const int64_t guess = (F + pairs) * 8 + waves * 2 * kern::deep_node_chunk();
+      const int64_t need = std::max<int64_t>({guess, b.arena_cap, (int64_t)(b.arena_used * 1.1)});
       if (need >= ((int64_t)1 << 32))
         throw std::runtime_error("deep_run: emit needs more than 2^32 trie nodes (u32 parent "
                                  "ids); use the count-only miner at this support");
-      if (b.arena_cap < need) {
+      if (b.arena_cap < std::max<int64_t>(guess, (int64_t)(b.arena_used * 1.03))) {
         for (void* p : {(void*)b.n_parent, (void*)b.n_item, (void*)b.n_count, (void*)b.n_depth})
           if (p) KMLS_HIP(hipFree(p));
         KMLS_HIP(hipMalloc((void**)&b.n_parent, (size_t)need * 4));
