@@ -519,7 +519,7 @@ void register_gpu_bindings(py::module_& m) {
         }
         return d;
       }, py::arg("min_support"), py::arg("max_len") = 0, py::arg("rank") = 0, py::arg("world") = 1,
-         py::arg("comm") = py::none(), py::arg("budget0") = 1024ull, py::arg("budget") = 8ull,
+         py::arg("comm") = py::none(), py::arg("budget0") = 1024ull, py::arg("budget") = 16ull,
          py::arg("split_min") = 8u, py::arg("blocks_per_cu") = 0, py::arg("stack_mb") = 0,
          py::arg("steal") = true, py::arg("steal_idle") = 1u, py::arg("assign") = 1,
          py::arg("trace") = false, py::arg("presplit_cost") = 16u,

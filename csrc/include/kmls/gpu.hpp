@@ -152,10 +152,13 @@ struct DeepBufsDeleter {
 struct DeepOpts {
   // (defaults: the best of the r3e sweep at ds1 @0.02, profiles/r3_deep_sweep_projected.log)
   unsigned long long budget0 = 1024;  // rounds: 64-lane passes a first-round task may take
-  unsigned long long budget = 8;      // steal: passes between mailbox checks (r3s sweep with
+  unsigned long long budget = 16;     // steal: passes between mailbox checks (r3s sweep with
                                       // direct hand-offs: 8 / 16 / 64 / 256 -> 42.7 / 42.7 / 44.3
                                       // / 51.6 ms at ds1 @0.02, 8-rank split 9.4 / 9.6 / 11.2 /
-                                      // 23.4 ms; r4i: 8 beats 16 by 1-3 % at 1 and 8 ranks);
+                                      // 23.4 ms; r4i: 8 beat 16 by 1-3 %; with splitting
+                                      // hand-offs (r7e/r7f) 2 / 4 / 8 / 16 / 32 / 64 -> 8-rank
+                                      // 8.9-9.1 / 8.1-8.3 / 7.6-8.3 / 7.5-7.8 / 8.3 / 9.7-9.9 ms,
+                                      // 1 GPU 28.3 at 16 vs 28.3-29.0 at 8);
                                       // rounds: later-round budget (1024 there)
   unsigned split_min = 8;             // spilled frames above this many members split per member
   int blocks_per_cu = 0;              // 0 = the kernel instance's occupancy (deep_waves_per_simd)
