@@ -1618,10 +1618,13 @@ GpuMineResult GpuMiner::mine_bitmaps(uintptr_t bm_dev, int64_t Wp, const MineCon
         // (v_mfma_scale_f32_32x32x64_f8f6f4, gram_mfma.hip) beats the VALU popcount gram there.
         // No BASELINE config reaches this branch today: ds1 rows are short (popcount gram),
         // configs 3 and 5 count pairs horizontally (pairrows.hip)
-        if (gram_popcount_forced() ? cfg.level2_mfma : (cfg.level2_mfma || Wp >= 4096))
+        const bool mfma = gram_popcount_forced() ? cfg.level2_mfma : (cfg.level2_mfma || Wp >= 4096);
+        if (mfma)
           kern::pair_gram_mfma((const uint64_t*)bm_dev, Wp, F, gram, s);
         else
           kern::pair_gram_popcount((const uint64_t*)bm_dev, Wp, F, gram, s);
+        if (res.level2_method.empty() || res.level2_method == "gram")
+          res.level2_method = mfma ? "gram_mfma" : "gram_popcount";
       }
       if (hl_plan_) res.cooc_pairs = hl_pairs_est_;  // exact after the row count
       if (comm_ && cw > 1) {

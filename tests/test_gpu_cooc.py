@@ -118,7 +118,7 @@ def test_txdp_level2_method_same_trie(gpu_mod, monkeypatch):
         g.load_csr(ptr, items, I)
         r = g.mine_txdp(None, T, 1e-3)
         out[hook] = r
-        assert r["stats"]["level2_method"] == ("cooc" if hook == "cooc=2" else "gram")
+        assert r["stats"]["level2_method"] == ("cooc" if hook == "cooc=2" else "gram_popcount")
     a, b = out["cooc=2"], out["cooc=0"]
     assert a["stats"]["n_itemsets"] == b["stats"]["n_itemsets"] > 0
     da = gpu_mod.trie_digest(a["parent"], a["item"], a["count"], a["depth"])
@@ -204,3 +204,21 @@ def test_pair_rows_long_rows_large_vocab(gpu_mod):
     X[rix[keep], col[items][keep]] = 1.0
     got = np.triu(gram.cpu().numpy().astype(np.int64), 1)
     np.testing.assert_array_equal(got, np.triu(np.rint(X.T @ X).astype(np.int64), 1))
+
+
+def test_txdp_long_rows_take_the_mfma_gram(gpu_mod, monkeypatch):
+    """Long bitmap rows (>= 4,096 words: 300k transactions) with level 2 on the bit-GEMM: the
+    miner picks the masked-FP4 MFMA gram by itself (gram_mfma.hip, not forced by an option) and
+    the trie equals the C++ miner's by content digest."""
+    T, I = 300_000, 400
+    ptr, items = gpu_mod.synth_transactions(T, I, 12.0, 20, 0.9, 0.85, 3)
+    ms = 0.01
+    monkeypatch.setenv("KMLS_TEST_HOOKS", "cooc=0")
+    g = gpu_mod.GpuMiner(0, 1 << 30, 0)
+    g.load_csr(ptr, items, I)
+    r = g.mine_txdp(None, T, ms)
+    assert r["stats"]["level2_method"] == "gram_mfma"
+    d = gpu_mod.trie_digest(r["parent"], r["item"], r["count"], r["depth"])
+    ref = gpu_mod.mine_cpu(ptr, items, I, ms, 0)
+    want = gpu_mod.trie_digest(ref["parent"], ref["item"], ref["count"], ref["depth"])
+    assert d["per_depth"][2] > 0 and d["digest"] == want["digest"]
