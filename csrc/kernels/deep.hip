@@ -873,7 +873,7 @@ template <int MAXT, int WPS, bool EMIT>
 __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS))) void k_deep_count(DeepArgs a) {
   __shared__ WaveLds<MAXT> lds[kWaves];
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int wid = (int)uni(threadIdx.x >> 6);  // (uniform: the wave's pointers live in SGPRs)
   WaveLds<MAXT>& L = lds[wid];
   const unsigned long long gw = (unsigned long long)blockIdx.x * kWaves + wid;
   DeepFrame* fst = a.fstacks + gw * (unsigned long long)a.fcap;
@@ -1603,7 +1603,9 @@ void deep_task_cost(const int64_t* blk_off, const int32_t* m, const int64_t* tas
 
 int deep_count_wps(int maxt, int want, bool emit) {
   const int mt = deep_count_maxt(maxt);
-  if (emit) return mt == 8 ? 4 : mt == 16 ? 3 : 2;  // the instances deep_count launches
+  // emit at MAXT 16: 4 waves/SIMD since the wave id is uniform (the wave's pointers in SGPRs:
+  // 44.0-44.8 vs 45.6-46.0 ms at 3 waves, profiles/r6s_*); 3 on request
+  if (emit) return mt == 8 ? 4 : mt == 16 ? (want == 3 ? 3 : 4) : 2;  // (launched instances)
   if (mt == 8 && (want == 4 || want == 5)) return want;
   if (mt == 16 && (want == 3 || want == 4)) return want;
   if (mt == 32 && (want == 2 || want == 3)) return want;
@@ -1615,9 +1617,11 @@ void deep_count(const DeepArgs& a, int maxt, int wps, int grid, hipStream_t s) {
   const int w = deep_count_wps(mt, wps, a.node_parent != nullptr);
   const dim3 g((unsigned)grid), b(64 * kWaves);
   if (a.node_parent != nullptr) {  // emit mode: the default occupancy of each width class
-    // (emit keeps 3 waves/SIMD at MAXT 16: its node-id bookkeeping pushes a 128-VGPR build into
-    // heavy spills, 56.7 vs 51.5 ms at ds1 @0.02, profiles/r4r_*)
+    // (round 4 kept emit at 3 waves/SIMD for MAXT 16: its node-id bookkeeping pushed a 128-VGPR
+    // build into heavy spills, 56.7 vs 51.5 ms, profiles/r4r_*; with the wave id uniform the
+    // 4-wave build spills little and wins)
     if (mt == 8) hipLaunchKernelGGL((k_deep_count<8, 4, true>), g, b, 0, s, a);
+    else if (mt == 16 && w == 4) hipLaunchKernelGGL((k_deep_count<16, 4, true>), g, b, 0, s, a);
     else if (mt == 16) hipLaunchKernelGGL((k_deep_count<16, 3, true>), g, b, 0, s, a);
     else if (mt == 32) hipLaunchKernelGGL((k_deep_count<32, 2, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_deep_count<64, 2, true>), g, b, 0, s, a);
