@@ -386,6 +386,9 @@ DeepLocal deep_run(DeepBufs& b, const DeepInput& in, int rank, int world, const 
   a.split_firsts = (unsigned)std::max<long long>(2, test_hook("deep_split_firsts", 32));
   a.split_keep16 = (unsigned)std::min<long long>(15, test_hook("deep_split_keep16", 5));
   a.ask_mask = (unsigned)test_hook("deep_ask_mask", 7);
+  // a waiting wave asks 4 victims at once (the first donor fills its inbox): 1 GPU rounds
+  // 27.8-27.9 vs 28.3-29.1 ms with one, 8 ranks 7.3-7.4 vs 7.6-8.0 ms (profiles/r6s_*)
+  a.ask_fanout = (unsigned)std::max<long long>(1, std::min<long long>(64, test_hook("deep_ask_fanout", 4)));
   a.sleep_n = (unsigned)test_hook("deep_sleep_n", 1u << 30);
   a.out_cap = b.q_cap;
   a.heap_cap = b.heap_cap;

@@ -961,11 +961,14 @@ __global__ __launch_bounds__(256, WPS) __attribute__((amdgpu_waves_per_eu(WPS)))
           if (lane == 0) st_agent(&a.inbox_state[gw], kOpen);
           inbox_open = true;
         } else if ((n & a.ask_mask) == 1) {
-          if (lane == 0) {
-            if (victim != (unsigned)gw)
-              atomicExch(&a.req[victim], ((unsigned long long)a.epoch << 32) | (unsigned long long)(gw + 1));
-            victim = (victim + 97u) % (unsigned)a.nwaves;
+          // (ask_fanout victims per ask: the first donor fills the inbox, the others find it
+          // taken and keep their frames)
+          if ((unsigned)lane < a.ask_fanout) {
+            const unsigned v = (unsigned)((victim + 97ull * (unsigned)lane) % (unsigned long long)a.nwaves);
+            if (v != (unsigned)gw)
+              atomicExch(&a.req[v], ((unsigned long long)a.epoch << 32) | (unsigned long long)(gw + 1));
           }
+          victim = (unsigned)((victim + 97ull * a.ask_fanout) % (unsigned long long)a.nwaves);
         }
         if (timed_out()) { failed = true; break; }
         wait_short(n < a.sleep_n ? n : a.sleep_n);

@@ -70,6 +70,7 @@ struct DeepArgs {
   unsigned split_firsts;          // a hand-off splits a class of >= this many first members
   unsigned split_keep16;          // ... keeping split_keep16 / 16 of them (0: never split)
   unsigned ask_mask;              // a waiting wave asks a victim every (ask_mask + 1) polls
+  unsigned ask_fanout;            // ... and that many victims at once (>= 1)
   unsigned sleep_n;               // poll backoff: s_sleep 2 / 16 / 127 from poll 0 / 4 / 16 on,
                                   // the poll count capped at sleep_n
   int steal_eager;                // tests: 1 = bottom frame to the queue at every check,
